@@ -1,0 +1,147 @@
+"""``DenseMatrix`` (row-level API of ``A/common/linalg/DenseMatrix.java``).
+
+Backed by a 2-D float64 numpy array.  Gson form follows the Java class: ``{"m":..,"n":..,"data":[...]}``
+with ``data`` in column-major order.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .vector import DenseVector
+
+__all__ = ["DenseMatrix"]
+
+
+class DenseMatrix:
+    __gson_fields__ = ("m", "n", "data")
+
+    def __init__(self, *args):
+        if len(args) == 1:
+            a = np.asarray(args[0], dtype=np.float64)
+            if a.ndim == 1:
+                a = a.reshape(-1, 1)
+            self.a = a.copy()
+        elif len(args) == 2:
+            self.a = np.zeros((int(args[0]), int(args[1])), dtype=np.float64)
+        elif len(args) == 3:  # (m, n, column-major data)
+            m, n, data = args
+            self.a = np.asarray(data, dtype=np.float64).reshape(n, m).T.copy()
+        else:
+            self.a = np.zeros((0, 0))
+
+    # gson view
+    @property
+    def m(self):
+        return self.a.shape[0]
+
+    @property
+    def n(self):
+        return self.a.shape[1]
+
+    @property
+    def data(self):
+        return self.a.T.reshape(-1)
+
+    @staticmethod
+    def eye(n):
+        return DenseMatrix(np.eye(n))
+
+    @staticmethod
+    def zeros(m, n):
+        return DenseMatrix(m, n)
+
+    @staticmethod
+    def rand(m, n, seed=None):
+        return DenseMatrix(np.random.default_rng(seed).random((m, n)))
+
+    def numRows(self):
+        return self.a.shape[0]
+
+    def numCols(self):
+        return self.a.shape[1]
+
+    def get(self, i, j):
+        return float(self.a[i, j])
+
+    def set(self, i, j, v):
+        self.a[i, j] = v
+
+    def add(self, i, j, v):
+        self.a[i, j] += v
+
+    def getArrayCopy2D(self):
+        return self.a.copy()
+
+    def getData(self):
+        return self.data
+
+    def getRow(self, i):
+        return self.a[i].copy()
+
+    def getColumn(self, j):
+        return self.a[:, j].copy()
+
+    def transpose(self):
+        return DenseMatrix(self.a.T)
+
+    def multiplies(self, o):
+        if isinstance(o, DenseMatrix):
+            return DenseMatrix(self.a @ o.a)
+        if isinstance(o, DenseVector):
+            return DenseVector(self.a @ o.data)
+        return DenseMatrix(self.a @ np.asarray(o))
+
+    def plus(self, o):
+        return DenseMatrix(self.a + (o.a if isinstance(o, DenseMatrix) else o))
+
+    def minus(self, o):
+        return DenseMatrix(self.a - o.a)
+
+    def scale(self, v):
+        return DenseMatrix(self.a * v)
+
+    def scaleEqual(self, v):
+        self.a *= v
+
+    def solve(self, b):
+        bb = b.a if isinstance(b, DenseMatrix) else (b.data if isinstance(b, DenseVector) else np.asarray(b))
+        x = np.linalg.lstsq(self.a, bb, rcond=None)[0] if self.a.shape[0] != self.a.shape[1] else np.linalg.solve(self.a, bb)
+        return DenseMatrix(x) if isinstance(b, DenseMatrix) else DenseVector(x)
+
+    def solveLS(self, b):
+        bb = b.a if isinstance(b, DenseMatrix) else b.data
+        x = np.linalg.lstsq(self.a, bb, rcond=None)[0]
+        return DenseMatrix(x) if isinstance(b, DenseMatrix) else DenseVector(x)
+
+    def inverse(self):
+        return DenseMatrix(np.linalg.inv(self.a))
+
+    def pseudoInverse(self):
+        return DenseMatrix(np.linalg.pinv(self.a))
+
+    def det(self):
+        return float(np.linalg.det(self.a))
+
+    def rank(self):
+        return int(np.linalg.matrix_rank(self.a))
+
+    def norm2(self):
+        return float(np.linalg.norm(self.a, 2))
+
+    def normF(self):
+        return float(np.linalg.norm(self.a))
+
+    def isSymmetric(self):
+        return self.a.shape[0] == self.a.shape[1] and np.allclose(self.a, self.a.T)
+
+    def isSquare(self):
+        return self.a.shape[0] == self.a.shape[1]
+
+    def clone(self):
+        return DenseMatrix(self.a.copy())
+
+    def __eq__(self, o):
+        return isinstance(o, DenseMatrix) and np.array_equal(o.a, self.a)
+
+    def __repr__(self):
+        return f"DenseMatrix({self.a.tolist()})"

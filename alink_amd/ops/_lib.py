@@ -1,0 +1,82 @@
+"""Loader for the in-tree HIP kernel library (``libalink_hip.so``, built for gfx950 by ``build_native.py``).
+
+The library exposes a plain C ABI (raw device pointers + the caller's HIP stream), called through
+``ctypes``: no torch C++ ABI coupling, and every launch goes on torch's current stream so kernels
+compose with RCCL collectives and hipGraph capture.
+
+On a GPU box a missing/unloadable library is an error (``require()`` raises) — ops never silently fall
+back to PyTorch when a GPU is present, unless ``ALINK_ALLOW_TORCH_FALLBACK=1`` is set explicitly.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional
+
+import torch  # noqa: F401  (loads torch's HIP runtime first; our .so resolves libamdhip64.so.7 to it)
+
+__all__ = ["lib", "require", "available", "LIB_PATH", "stream_ptr"]
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libalink_hip.so")
+_lib: Optional[ctypes.CDLL] = None
+_err: Optional[str] = None
+
+
+def _load():
+    global _lib, _err
+    if _lib is not None or _err is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        _err = f"{LIB_PATH} not built (run python build_native.py)"
+        return None
+    try:
+        L = ctypes.CDLL(LIB_PATH)
+    except OSError as e:  # pragma: no cover - depends on box
+        _err = f"cannot load {LIB_PATH}: {e}"
+        return None
+    c_i64, c_int, c_vp = ctypes.c_int64, ctypes.c_int, ctypes.c_void_p
+    L.alink_kmeans_assign_accum_bf16.argtypes = [c_vp, c_i64, c_vp, c_vp, c_int, c_vp, c_vp, c_int, c_vp]
+    L.alink_kmeans_assign_accum_bf16.restype = c_int
+    L.alink_kmeans_reduce_slabs.argtypes = [c_vp, c_vp, c_int, c_int, c_vp, c_vp]
+    L.alink_kmeans_reduce_slabs.restype = c_int
+    for name, argtypes in _EXTRA_SIGNATURES.items():
+        if hasattr(L, name):
+            getattr(L, name).argtypes = argtypes
+            getattr(L, name).restype = c_int
+    _lib = L
+    return _lib
+
+
+_c_i64, _c_int, _c_vp, _c_f = ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.c_float
+_c_d = ctypes.c_double
+# signatures of further kernels (registered when present in the library)
+_EXTRA_SIGNATURES = {
+    "alink_gbdt_hist_u8": [_c_vp, _c_i64, _c_int, _c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_vp, _c_vp],
+    "alink_logistic_grad": [_c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_int, _c_vp, _c_vp, _c_vp],
+    "alink_vector_assemble": [_c_vp, _c_vp, _c_int, _c_i64, _c_vp, _c_int, _c_vp],
+    "alink_feature_hash": [_c_vp, _c_vp, _c_i64, _c_int, _c_vp, _c_vp],
+    "alink_als_normal_eq_solve": [_c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_int, _c_f, _c_vp, _c_vp],
+}
+
+
+def lib() -> Optional[ctypes.CDLL]:
+    return _load()
+
+
+def available() -> bool:
+    return _load() is not None
+
+
+def require() -> ctypes.CDLL:
+    L = _load()
+    if L is None:
+        raise RuntimeError(f"alink_amd HIP kernels unavailable: {_err}")
+    return L
+
+
+def torch_fallback_allowed() -> bool:
+    return os.environ.get("ALINK_ALLOW_TORCH_FALLBACK", "0") == "1"
+
+
+def stream_ptr(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream

@@ -1,0 +1,314 @@
+// Fused KMeans assign + accumulate for CDNA4 (gfx950 / MI355X).
+//
+// Replaces the reference's per-sample Java loop (KMeansAssignCluster.calc -> KMeansUtil.updateSumMatrix,
+// A/operator/common/clustering/kmeans/KMeansUtil.java:60-85, distance via EuclideanDistance gemv
+// A/operator/common/distance/EuclideanDistance.java:109-141) with ONE persistent kernel per superstep:
+//
+//   per 128-row tile (staged HBM -> LDS by global_load_lds, 3-deep ring, swizzled image):
+//     1. distance GEMM on MFMA (v_mfma_f32_32x32x16_bf16):  S[c][r] = x_r . c  -  |c|^2 / 2
+//        (the -|c|^2/2 term is the accumulator's initial value, so argmax S == argmin ||x - c||^2);
+//        wave w owns rows 32w..32w+31, centroid fragments live in registers for the whole kernel;
+//     2. argmax over centroids in registers (index packed into the 7 low mantissa bits, v_max_f32);
+//     3. one-hot accumulate on MFMA:  Sum[c][d] += Onehot[c][r] . X[r][d]
+//        one-hot A fragments come from a 256-entry byte->8xbf16 LUT in LDS indexed by per-centroid row
+//        bitmasks (built with ds_or_b32), X^T B fragments from ds_read_b64_tr_b16 on the same LDS image;
+//        wave w owns centroid block w (32 centroids x 128 dims, 64 accumulators).
+//   end: each workgroup writes its fp32 partial sums + counts (slab); a second kernel reduces slabs in a
+//   fixed order in fp64 -> deterministic [k][d+1] buffer that the BSP AllReduce then sums across GPUs.
+//
+// Contract (checked on the host by the Python wrapper before launch):
+//   D == 128, 1 <= k <= 128, X row-major bf16 [N][128] (16-byte aligned), C padded [128][128] bf16
+//   (zero rows beyond k), ninit[128] (-|c|^2/2 for c < k, -3e38 for padding).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+#define LDS_PTR(p) ((__attribute__((address_space(3))) void*)(p))
+
+constexpr int D = 128;               // feature dims (fast path)
+constexpr int TR = 128;              // rows per tile
+constexpr int ROWB = D * 2;          // 256 B per row
+constexpr int TILE_BYTES = TR * ROWB;  // 32 KiB
+constexpr int NSTAGE = 3;            // LDS ring depth (tiles in flight = NSTAGE - 1)
+constexpr int GLDS_PER_THREAD = TILE_BYTES / (256 * 16);  // 8
+
+// LDS carve (one __shared__ array: avoids hipcc's extra vmcnt(0) on a second LDS object)
+constexpr int OFF_X = 0;
+constexpr int OFF_LUT = NSTAGE * TILE_BYTES;          // 256 x 16 B
+constexpr int OFF_MASK = OFF_LUT + 256 * 16;          // [2][128 c][4 words]
+constexpr int OFF_NINIT = OFF_MASK + 2 * 128 * 4 * 4; // [128] f32
+constexpr int LDS_BYTES = OFF_NINIT + 128 * 4;
+
+// swizzled image of a [rows][16 chunks of 16 B] tile (conflict-free for 32x32x16 row reads and
+// for ds_read_b64_tr_b16 transposed reads)
+__device__ __forceinline__ int xoff(int row, int ch) {
+    return row * ROWB + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
+}
+
+__device__ __forceinline__ void wait_vmcnt_n(int n) {
+    // n is one of {0, 8, 16}; immediates must be literal
+    if (n >= 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+__device__ __forceinline__ void barrier_lds() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+// stage one 128-row tile (rows >= N are clamped to N-1; their mask bits are never set)
+__device__ __forceinline__ void stage_tile(char* lds, int buf, const char* X, int64_t row0, int64_t N,
+                                           int tid, int wave) {
+    char* dst_base = lds + OFF_X + buf * TILE_BYTES;
+#pragma unroll
+    for (int i = 0; i < GLDS_PER_THREAD; ++i) {
+        const int p = i * 4096 + tid * 16;       // linear LDS byte this lane fills
+        const int row = p >> 8;
+        const int chp = (p >> 4) & 15;           // physical chunk
+        const int chl = chp ^ (((row & 3) << 2) | ((row >> 2) & 3));  // logical chunk stored there
+        int64_t grow = row0 + row;
+        grow = grow < N ? grow : (N - 1);
+        const char* src = X + grow * ROWB + chl * 16;
+        // LDS-DMA issued from inline asm: hipcc does not track it, so it does not drain the ring with
+        // vmcnt(0) before unrelated LDS accesses; completion is counted by hand (wait_vmcnt_n).
+        const uint32_t m0v = __builtin_amdgcn_readfirstlane(
+            (uint32_t)(uintptr_t)LDS_PTR(dst_base + i * 4096 + wave * 1024));
+        uint32_t keep;
+        asm volatile(
+            "s_mov_b32 %0, m0\n\t"
+            "s_mov_b32 m0, %2\n\t"
+            "s_nop 0\n\t"
+            "global_load_lds_dwordx4 %1, off\n\t"
+            "s_mov_b32 m0, %0"
+            : "=&s"(keep)
+            : "v"(src), "s"(m0v)
+            : "memory");
+    }
+}
+
+template <int KB>
+__global__ __launch_bounds__(256, 1) void kmeans_assign_accum_kernel(
+    const __bf16* __restrict__ Xp, int64_t N, const __bf16* __restrict__ Cp, const float* __restrict__ ninit,
+    float* __restrict__ slab, float* __restrict__ slab_cnt, int64_t ntiles) {
+    __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int h = lane >> 5;
+    const int l32 = lane & 31;
+    const char* X = reinterpret_cast<const char*>(Xp);
+
+    const int64_t G = gridDim.x;
+    const int64_t my_ntiles = (ntiles > (int64_t)blockIdx.x) ? (ntiles - 1 - blockIdx.x) / G + 1 : 0;
+
+    // ---- prologue: start the tile ring before any other setup ----
+    for (int s = 0; s < NSTAGE - 1; ++s)
+        if (s < my_ntiles) stage_tile(lds, s, X, ((int64_t)blockIdx.x + s * G) * TR, N, tid, wave);
+
+    // LUT: byte -> 8 x bf16 {0, 1.0}; masks cleared; ninit
+    {
+        uint32_t* lut = reinterpret_cast<uint32_t*>(lds + OFF_LUT);
+        for (int e = tid; e < 256 * 4; e += 256) {
+            const int ent = e >> 2, pair = e & 3;
+            const uint32_t b0 = (ent >> (2 * pair)) & 1, b1 = (ent >> (2 * pair + 1)) & 1;
+            lut[e] = (b0 ? 0x3F80u : 0u) | (b1 ? 0x3F800000u : 0u);
+        }
+        uint32_t* m = reinterpret_cast<uint32_t*>(lds + OFF_MASK);
+        for (int e = tid; e < 2 * 128 * 4; e += 256) m[e] = 0u;
+        float* ni = reinterpret_cast<float*>(lds + OFF_NINIT);
+        if (tid < 128) ni[tid] = ninit[tid];
+    }
+    // centroid A fragments in registers: cf[b][s] = C[32b + l32][16s + 8h .. +7]
+    bf16x8 cf[KB][8];
+#pragma unroll
+    for (int b = 0; b < KB; ++b)
+#pragma unroll
+        for (int s = 0; s < 8; ++s)
+            cf[b][s] = *reinterpret_cast<const bf16x8*>(Cp + (32 * b + l32) * D + 16 * s + 8 * h);
+    // consume the fragments here so hipcc places its load waits before the loop, not at their first
+    // (in-loop) use where a per-iteration vmcnt(N<16) would drain the LDS-DMA ring
+#pragma unroll
+    for (int b = 0; b < KB; ++b)
+#pragma unroll
+        for (int s = 0; s < 8; ++s) asm volatile("" ::"v"(cf[b][s]));
+
+    f32x16 sacc[4];
+#pragma unroll
+    for (int db = 0; db < 4; ++db)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sacc[db][r] = 0.f;
+    float cnt = 0.f;
+
+    // make the prologue's non-DMA LDS writes and the centroid loads visible; the ring stays in flight
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+
+    for (int64_t it = 0; it < my_ntiles; ++it) {
+        const int buf = (int)(it % NSTAGE);
+        const int64_t tile = (int64_t)blockIdx.x + it * G;
+        // prefetch tile it + NSTAGE - 1
+        int ahead = 0;
+        if (it + NSTAGE - 1 < my_ntiles) {
+            stage_tile(lds, (int)((it + NSTAGE - 1) % NSTAGE), X, (tile + (NSTAGE - 1) * G) * TR, N, tid, wave);
+            ahead = NSTAGE - 1;
+        } else {
+            ahead = (int)(my_ntiles - 1 - it);
+        }
+        wait_vmcnt_n(ahead * GLDS_PER_THREAD);
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+
+        const char* xb = lds + OFF_X + buf * TILE_BYTES;
+        uint32_t* mcur = reinterpret_cast<uint32_t*>(lds + OFF_MASK + (int)(it & 1) * 128 * 16);
+        uint32_t* mnext = reinterpret_cast<uint32_t*>(lds + OFF_MASK + (int)((it + 1) & 1) * 128 * 16);
+        // clear next parity's masks (last read in iteration it-1, next written in it+1)
+        mnext[tid] = 0u;
+        mnext[tid + 256] = 0u;
+
+        // ---- 1. distance GEMM: rows 32*wave + l32 ----
+        const float* ni = reinterpret_cast<const float*>(lds + OFF_NINIT);
+        f32x16 acc[KB];
+#pragma unroll
+        for (int b = 0; b < KB; ++b) {
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const f32x4 v = *reinterpret_cast<const f32x4*>(ni + 32 * b + 8 * g + 4 * h);
+                acc[b][4 * g + 0] = v[0];
+                acc[b][4 * g + 1] = v[1];
+                acc[b][4 * g + 2] = v[2];
+                acc[b][4 * g + 3] = v[3];
+            }
+        }
+        const int myrow = 32 * wave + l32;
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+            const bf16x8 xv = *reinterpret_cast<const bf16x8*>(xb + xoff(myrow, 2 * s + h));
+#pragma unroll
+            for (int b = 0; b < KB; ++b)
+                acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cf[b][s], xv, acc[b], 0, 0, 0);
+        }
+        // ---- 2. argmax over centroids (index in low 7 mantissa bits) ----
+        float best = -3.0e38f;
+#pragma unroll
+        for (int b = 0; b < KB; ++b) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const uint32_t c = 32 * b + (r & 3) + 8 * (r >> 2) + 4 * h;
+                const float v = __uint_as_float((__float_as_uint(acc[b][r]) & 0xFFFFFF80u) | c);
+                best = fmaxf(best, v);
+            }
+        }
+        best = fmaxf(best, __shfl_xor(best, 32));
+        const int64_t grow = tile * TR + myrow;
+        if (h == 0 && grow < N) {
+            const uint32_t c = __float_as_uint(best) & 127u;
+            __hip_atomic_fetch_or(mcur + c * 4 + (myrow >> 5), 1u << (myrow & 31), __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        barrier_lds();
+
+        // ---- 3. one-hot accumulate: centroid block = wave ----
+        if (wave < KB) {
+            const u32x4 mw = *reinterpret_cast<const u32x4*>(mcur + (32 * wave + l32) * 4);
+            if (h == 0) cnt += (float)(__popc(mw[0]) + __popc(mw[1]) + __popc(mw[2]) + __popc(mw[3]));
+            const int g = lane >> 4, i16 = lane & 15, q = i16 >> 2, p = i16 & 3;
+#pragma unroll
+            for (int s = 0; s < 8; ++s) {
+                const uint32_t word = mw[s >> 1];
+                const uint32_t byte = (word >> (16 * (s & 1) + 8 * h)) & 255u;
+                const bf16x8 a = *reinterpret_cast<const bf16x8*>(lds + OFF_LUT + byte * 16);
+#pragma unroll
+                for (int db = 0; db < 4; ++db) {
+                    const int ch = 4 * db + 2 * (g & 1) + (p >> 1);
+                    const int r0 = 16 * s + 8 * (g >> 1) + q;
+                    const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+                        (__attribute__((address_space(3))) bf16x4*)(xb + xoff(r0, ch) + 8 * (p & 1)));
+                    const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+                        (__attribute__((address_space(3))) bf16x4*)(xb + xoff(r0 + 4, ch) + 8 * (p & 1)));
+                    const bf16x8 bv = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                    sacc[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bv, sacc[db], 0, 0, 0);
+                }
+            }
+        }
+        barrier_lds();
+    }
+
+    // ---- epilogue: partial sums (fp32) of centroid block `wave` ----
+    if (wave < KB) {
+        float* S = slab + (int64_t)blockIdx.x * 128 * D;
+#pragma unroll
+        for (int db = 0; db < 4; ++db)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int c = 32 * wave + (r & 3) + 8 * (r >> 2) + 4 * h;
+                S[c * D + 32 * db + l32] = sacc[db][r];
+            }
+        if (h == 0) slab_cnt[(int64_t)blockIdx.x * 128 + 32 * wave + l32] = cnt;
+    } else {
+        float* S = slab + (int64_t)blockIdx.x * 128 * D;
+        for (int e = lane; e < 32 * D; e += 64) S[(32 * wave) * D + e] = 0.f;
+        if (h == 0) slab_cnt[(int64_t)blockIdx.x * 128 + 32 * wave + l32] = 0.f;
+    }
+}
+
+// fixed-order fp64 reduction of the per-workgroup slabs -> out[k][D+1] (last column = count)
+__global__ void kmeans_reduce_slabs_kernel(const float* __restrict__ slab, const float* __restrict__ slab_cnt,
+                                           int nslab, int k, double* __restrict__ out) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    const int total = k * (D + 1);
+    if (e >= total) return;
+    const int c = e / (D + 1), d = e % (D + 1);
+    double s = 0.0;
+    if (d < D) {
+        for (int w = 0; w < nslab; ++w) s += (double)slab[((int64_t)w * 128 + c) * D + d];
+    } else {
+        for (int w = 0; w < nslab; ++w) s += (double)slab_cnt[(int64_t)w * 128 + c];
+    }
+    out[e] = s;
+}
+
+}  // namespace
+
+extern "C" {
+
+int alink_kmeans_lds_bytes() { return LDS_BYTES; }
+
+// returns 0 on success, hipError_t otherwise
+int alink_kmeans_assign_accum_bf16(const void* X, int64_t N, const void* C, const float* ninit, int k,
+                                   float* slab, float* slab_cnt, int grid, void* stream) {
+    if (N <= 0 || k < 1 || k > 128 || grid <= 0) return -1;
+    const int KB = (k + 31) / 32;
+    const int64_t ntiles = (N + TR - 1) / TR;
+    if (grid > ntiles) grid = (int)ntiles;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    switch (KB) {
+        case 1: hipLaunchKernelGGL(kmeans_assign_accum_kernel<1>, dim3(grid), dim3(256), 0, st,
+                                   (const __bf16*)X, N, (const __bf16*)C, ninit, slab, slab_cnt, ntiles); break;
+        case 2: hipLaunchKernelGGL(kmeans_assign_accum_kernel<2>, dim3(grid), dim3(256), 0, st,
+                                   (const __bf16*)X, N, (const __bf16*)C, ninit, slab, slab_cnt, ntiles); break;
+        case 3: hipLaunchKernelGGL(kmeans_assign_accum_kernel<3>, dim3(grid), dim3(256), 0, st,
+                                   (const __bf16*)X, N, (const __bf16*)C, ninit, slab, slab_cnt, ntiles); break;
+        default: hipLaunchKernelGGL(kmeans_assign_accum_kernel<4>, dim3(grid), dim3(256), 0, st,
+                                    (const __bf16*)X, N, (const __bf16*)C, ninit, slab, slab_cnt, ntiles); break;
+    }
+    return (int)hipGetLastError();
+}
+
+int alink_kmeans_reduce_slabs(const float* slab, const float* slab_cnt, int nslab, int k, double* out,
+                              void* stream) {
+    const int total = k * (D + 1);
+    hipLaunchKernelGGL(kmeans_reduce_slabs_kernel, dim3((total + 255) / 256), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), slab, slab_cnt, nslab, k, out);
+    return (int)hipGetLastError();
+}
+
+}  // extern "C"

@@ -1,0 +1,129 @@
+"""KMeans hot path: fused distance + argmin + per-cluster accumulation (kernels K1+K2).
+
+``assign_accumulate(X, C)`` returns the ``[k, d+1]`` float64 buffer ``[sum_x | count]`` per centroid — the
+``centroidAllReduce`` buffer of the reference (``KMeansAssignCluster.java:48-63``,
+``KMeansUtil.updateSumMatrix`` ``KMeansUtil.java:60-85``) — for this rank's rows, ready for the BSP
+all-reduce.
+
+* GPU, bf16 rows, d == 128, k <= 128: one persistent MFMA kernel (``csrc/kmeans.hip``) + an fp64
+  fixed-order slab reduction (deterministic).
+* anything else: chunked PyTorch path (fp64 on CPU; on GPU fp32 GEMM of the same bf16-rounded centroids).
+"""
+from __future__ import annotations
+
+from typing import Dict, Optional, Tuple
+
+import torch
+
+from . import _lib
+
+__all__ = ["assign_accumulate", "assign", "assign_accumulate_torch", "hip_supported", "prepare_centroids"]
+
+_BUF: Dict[Tuple, Tuple[torch.Tensor, torch.Tensor]] = {}
+HIP_D = 128
+HIP_KMAX = 128
+
+
+def hip_supported(X: torch.Tensor, k: int) -> bool:
+    return (X.is_cuda and X.dtype == torch.bfloat16 and X.dim() == 2 and X.shape[1] == HIP_D
+            and 1 <= k <= HIP_KMAX and X.shape[0] > 0 and X.is_contiguous() and X.data_ptr() % 16 == 0)
+
+
+def prepare_centroids(C: torch.Tensor, device) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Padded bf16 centroid block [128,128] and accumulator init -|c|^2/2 (of the bf16-rounded centroids)."""
+    k = C.shape[0]
+    cb = C.to(device=device, dtype=torch.bfloat16)
+    cpad = torch.zeros((HIP_KMAX, HIP_D), dtype=torch.bfloat16, device=device)
+    cpad[:k] = cb
+    ninit = torch.full((HIP_KMAX,), -3.0e38, dtype=torch.float32, device=device)
+    ninit[:k] = -0.5 * (cb.float() ** 2).sum(1)
+    return cpad, ninit
+
+
+def _num_cus(device) -> int:
+    return torch.cuda.get_device_properties(device).multi_processor_count
+
+
+def assign_accumulate_hip(X: torch.Tensor, C: torch.Tensor, grid: Optional[int] = None) -> torch.Tensor:
+    L = _lib.require()
+    dev = X.device
+    k = C.shape[0]
+    if not hip_supported(X, k):
+        raise ValueError("HIP KMeans path needs contiguous bf16 [N,128] on GPU and k <= 128")
+    cpad, ninit = prepare_centroids(C, dev)
+    n = X.shape[0]
+    if grid is None:
+        grid = _num_cus(dev)
+    ntiles = (n + 127) // 128
+    grid = max(1, min(grid, ntiles))
+    key = (dev.index, grid)
+    if key not in _BUF:
+        _BUF[key] = (torch.empty((grid, HIP_KMAX, HIP_D), dtype=torch.float32, device=dev),
+                     torch.empty((grid, HIP_KMAX), dtype=torch.float32, device=dev))
+    slab, slab_cnt = _BUF[key]
+    out = torch.empty((k, HIP_D + 1), dtype=torch.float64, device=dev)
+    st = _lib.stream_ptr(dev)
+    rc = L.alink_kmeans_assign_accum_bf16(X.data_ptr(), n, cpad.data_ptr(), ninit.data_ptr(), k,
+                                          slab.data_ptr(), slab_cnt.data_ptr(), grid, st)
+    if rc != 0:
+        raise RuntimeError(f"alink_kmeans_assign_accum_bf16 failed: {rc}")
+    rc = L.alink_kmeans_reduce_slabs(slab.data_ptr(), slab_cnt.data_ptr(), grid, k, out.data_ptr(), st)
+    if rc != 0:
+        raise RuntimeError(f"alink_kmeans_reduce_slabs failed: {rc}")
+    return out
+
+
+def _scores(Xc: torch.Tensor, C: torch.Tensor, emulate_bf16: bool) -> torch.Tensor:
+    """x.c - |c|^2/2 (argmax == argmin of squared euclidean distance)."""
+    if emulate_bf16:
+        cb = C.to(torch.bfloat16).float()
+        return Xc.float() @ cb.T - 0.5 * (cb ** 2).sum(1)
+    Cd = C.to(Xc.dtype)
+    return Xc @ Cd.T - 0.5 * (Cd ** 2).sum(1)
+
+
+def assign_accumulate_torch(X: torch.Tensor, C: torch.Tensor, weights: Optional[torch.Tensor] = None,
+                            chunk: int = 1 << 20) -> torch.Tensor:
+    """Reference implementation: [k, d+1] float64 sums/counts of the nearest-centroid assignment."""
+    k, d = C.shape
+    out = torch.zeros((k, d + 1), dtype=torch.float64, device=X.device)
+    low = X.dtype in (torch.bfloat16, torch.float16)
+    for s in range(0, X.shape[0], chunk):
+        xc = X[s:s + chunk]
+        if not low:
+            xc = xc.to(torch.float64)
+        idx = _scores(xc, C, low).argmax(1)
+        w = None if weights is None else weights[s:s + chunk].to(torch.float64)
+        xs = xc.to(torch.float64)
+        if w is not None:
+            xs = xs * w[:, None]
+        out[:, :d].index_add_(0, idx, xs)
+        out[:, d].index_add_(0, idx, torch.ones_like(idx, dtype=torch.float64) if w is None else w)
+    return out
+
+
+def assign_accumulate(X: torch.Tensor, C: torch.Tensor, weights: Optional[torch.Tensor] = None) -> torch.Tensor:
+    if weights is None and hip_supported(X, C.shape[0]):
+        if _lib.available() or not _lib.torch_fallback_allowed():
+            return assign_accumulate_hip(X, C)
+    return assign_accumulate_torch(X, C, weights)
+
+
+def assign(X: torch.Tensor, C: torch.Tensor, chunk: int = 1 << 20) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Nearest centroid index and squared euclidean distance for every row."""
+    low = X.dtype in (torch.bfloat16, torch.float16)
+    idx_all, d2_all = [], []
+    for s in range(0, X.shape[0], chunk):
+        xc = X[s:s + chunk]
+        if not low:
+            xc = xc.to(torch.float64)
+        sc = _scores(xc, C, low)
+        best, idx = sc.max(1)
+        xn = (xc.to(torch.float64) ** 2).sum(1)
+        d2 = (xn - 2.0 * best.to(torch.float64)).clamp_min(0.0)
+        idx_all.append(idx)
+        d2_all.append(d2)
+    if not idx_all:
+        return (torch.zeros(0, dtype=torch.int64, device=X.device),
+                torch.zeros(0, dtype=torch.float64, device=X.device))
+    return torch.cat(idx_all), torch.cat(d2_all)

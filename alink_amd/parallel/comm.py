@@ -1,0 +1,223 @@
+"""Collective communication for the SPMD runtime.
+
+Reference: Alink's only collective is a shuffle-based ``AllReduce`` over Flink's network stack
+(``A/common/comqueue/communication/AllReduce.java:42-360``) plus broadcast variables, keyed shuffles and
+accumulator-based collect.  Here every partition is one process (one MI355X), and
+collectives go through ``torch.distributed``:
+
+* backend ``nccl`` (= RCCL over xGMI on ROCm) for device tensors — one process per GPU;
+* a companion ``gloo`` group for host objects (row lists, model rows, small Python state), so object
+  traffic never serialises through GPU memory;
+* ``gloo`` alone for CPU-only runs / tests (the analogue of Flink's LocalEnvironment).
+
+With world size 1 every call is a local no-op.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+import pickle
+from typing import Any, List, Optional
+
+import torch
+import torch.distributed as dist
+
+__all__ = ["init_distributed", "get_rank", "get_world_size", "is_distributed", "all_reduce", "all_gather_object",
+           "broadcast_object", "barrier", "all_gather_tensor", "all_to_all_objects", "reduce_scatter",
+           "object_group", "device_for_rank", "CommStats", "STATS", "shutdown", "all_reduce_coalesced"]
+
+_OBJ_GROUP = None
+
+
+class CommStats:
+    """Per-process counters: number of collectives and bytes reduced (observability)."""
+
+    def __init__(self):
+        self.calls = 0
+        self.bytes = 0
+        self.time_s = 0.0
+
+    def reset(self):
+        self.calls = 0
+        self.bytes = 0
+        self.time_s = 0.0
+
+    def as_dict(self):
+        return {"collectives": self.calls, "bytes": self.bytes}
+
+
+STATS = CommStats()
+
+
+def is_distributed() -> bool:
+    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+
+
+def get_rank() -> int:
+    return dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
+
+
+def get_world_size() -> int:
+    return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+
+
+def device_for_rank() -> torch.device:
+    if torch.cuda.is_available():
+        lr = int(os.environ.get("LOCAL_RANK", "0"))
+        return torch.device("cuda", lr % max(1, torch.cuda.device_count()))
+    return torch.device("cpu")
+
+
+def init_distributed(backend: Optional[str] = None, timeout_s: float = 1800.0) -> bool:
+    """Initialise the default process group from torchrun env vars (RANK/WORLD_SIZE/MASTER_*).
+
+    Returns True if a multi-process group is active.  Safe to call repeatedly.
+    """
+    global _OBJ_GROUP
+    if not dist.is_available():
+        return False
+    if dist.is_initialized():
+        return dist.get_world_size() > 1
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    if ws <= 1:
+        return False
+    if backend is None:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    kw = {}
+    if backend == "nccl":
+        dev = device_for_rank()
+        torch.cuda.set_device(dev)
+        kw["device_id"] = dev
+    dist.init_process_group(backend=backend, timeout=datetime.timedelta(seconds=timeout_s), **kw)
+    if backend != "gloo":
+        _OBJ_GROUP = dist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=timeout_s))
+    else:
+        _OBJ_GROUP = None
+    return True
+
+
+def shutdown():
+    global _OBJ_GROUP
+    if dist.is_available() and dist.is_initialized():
+        dist.destroy_process_group()
+    _OBJ_GROUP = None
+
+
+def object_group():
+    return _OBJ_GROUP
+
+
+def _backend() -> str:
+    return dist.get_backend() if dist.is_initialized() else "none"
+
+
+_OPS = {"sum": "SUM", "max": "MAX", "min": "MIN", "prod": "PRODUCT"}
+
+
+def all_reduce(t: torch.Tensor, op: str = "sum") -> torch.Tensor:
+    """In-place all-reduce of a tensor (SUM/MAX/MIN, reference ``AllReduce.java:125-159``).
+
+    Device tensors use RCCL; on a gloo job, device tensors are staged through host memory.
+    """
+    if not is_distributed():
+        return t
+    rop = getattr(dist.ReduceOp, _OPS[op.lower()])
+    STATS.calls += 1
+    STATS.bytes += t.numel() * t.element_size()
+    if t.is_cuda and _backend() != "nccl":
+        h = t.cpu()
+        dist.all_reduce(h, op=rop)
+        t.copy_(h)
+        return t
+    if (not t.is_cuda) and _backend() == "nccl":
+        d = t.to(device_for_rank())
+        dist.all_reduce(d, op=rop)
+        t.copy_(d.cpu())
+        return t
+    dist.all_reduce(t, op=rop)
+    return t
+
+
+def all_reduce_coalesced(ts: List[torch.Tensor], op: str = "sum") -> List[torch.Tensor]:
+    """Fuse several small same-dtype buffers into one collective (latency-bound regime)."""
+    if not is_distributed() or not ts:
+        return ts
+    flat = torch.cat([t.reshape(-1) for t in ts])
+    all_reduce(flat, op)
+    off = 0
+    for t in ts:
+        n = t.numel()
+        t.copy_(flat[off:off + n].view_as(t))
+        off += n
+    return ts
+
+
+def reduce_scatter(t: torch.Tensor, op: str = "sum") -> torch.Tensor:
+    """Reduce-scatter along dim 0 (t.shape[0] must divide world size); returns this rank's block."""
+    ws = get_world_size()
+    if ws == 1:
+        return t
+    rop = getattr(dist.ReduceOp, _OPS[op.lower()])
+    out = torch.empty((t.shape[0] // ws,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+    STATS.calls += 1
+    STATS.bytes += t.numel() * t.element_size()
+    if _backend() == "nccl" and t.is_cuda:
+        dist.reduce_scatter_tensor(out, t.contiguous(), op=rop)
+        return out
+    full = t.clone()
+    all_reduce(full, op)
+    r = get_rank()
+    return full[r * out.shape[0]:(r + 1) * out.shape[0]].clone()
+
+
+def all_gather_tensor(t: torch.Tensor) -> torch.Tensor:
+    """Concatenate equally-shaped tensors from all ranks along dim 0."""
+    ws = get_world_size()
+    if ws == 1:
+        return t
+    STATS.calls += 1
+    if _backend() == "nccl" and t.is_cuda:
+        out = torch.empty((ws * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(out, t.contiguous())
+        return out
+    parts = [torch.empty_like(t.cpu()) for _ in range(ws)]
+    dist.all_gather(parts, t.cpu().contiguous())
+    return torch.cat(parts).to(t.device)
+
+
+def all_gather_object(obj: Any) -> List[Any]:
+    ws = get_world_size()
+    if ws == 1:
+        return [obj]
+    out: List[Any] = [None] * ws
+    STATS.calls += 1
+    dist.all_gather_object(out, obj, group=_OBJ_GROUP)
+    return out
+
+
+def broadcast_object(obj: Any, src: int = 0) -> Any:
+    if get_world_size() == 1:
+        return obj
+    box = [obj]
+    STATS.calls += 1
+    dist.broadcast_object_list(box, src=src, group=_OBJ_GROUP)
+    return box[0]
+
+
+def all_to_all_objects(send: List[Any]) -> List[Any]:
+    """Object all-to-all: ``send[j]`` goes to rank j; returns the list received from every rank."""
+    ws = get_world_size()
+    if ws == 1:
+        return list(send)
+    gathered = all_gather_object(send)
+    r = get_rank()
+    return [gathered[src][r] for src in range(ws)]
+
+
+def barrier():
+    if is_distributed():
+        if _backend() == "nccl":
+            dist.barrier(device_ids=[torch.cuda.current_device()])
+        else:
+            dist.barrier()

@@ -1,0 +1,348 @@
+"""BSP iteration engine: ``IterativeComQueue`` / ``ComContext`` / queue items.
+
+Reference: ``A/common/comqueue/BaseComQueue.java:39-549`` (declarative superstep queue over a Flink bulk
+iteration; per-task state in a JVM-static map, ``SessionSharedObjs``/``IterTaskObjKeeper``),
+``ComContext.java``, ``ComputeFunction/CommunicateFunction/CompareCriterionFunction/
+CompleteResultFunction`` and ``communication/AllReduce.java``.
+
+MI355X design: the queue is plain SPMD.  Each process owns ``local_tasks`` BSP tasks (1 per GPU in
+production) whose state lives in ``ComContext`` dictionaries (device tensors stay on the device between
+supersteps — no serialisation, no barrier edges).  A superstep is: run every item in order for every
+local task; ``CommunicateFunction`` items first combine the local tasks, then issue one collective over
+RCCL (GPU) / gloo (CPU).  The criterion of task 0 decides termination; when the queue state is
+bit-identical on every rank after an all-reduce (``criterion_replicated=True``) each rank evaluates it
+locally and no broadcast is needed.
+
+Observability: per-superstep wall time and collective bytes are recorded in ``queue.stats``; optional
+``on_step`` callbacks and a ``roctx`` range per superstep when running on ROCm.
+"""
+from __future__ import annotations
+
+import time
+from typing import Any, Callable, Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import comm
+
+__all__ = ["ComContext", "ComputeFunction", "CommunicateFunction", "CompareCriterionFunction",
+           "CompleteResultFunction", "AllReduce", "BaseComQueue", "IterativeComQueue", "ComQueue",
+           "ChainedComputation", "AllGather", "Broadcast", "SUM", "MAX", "MIN"]
+
+SUM, MAX, MIN = "sum", "max", "min"
+
+
+class ComContext:
+    def __init__(self, store: Dict[str, Any], task_id: int, num_task: int, queue: "BaseComQueue"):
+        self._store = store
+        self._task_id = task_id
+        self._num_task = num_task
+        self._queue = queue
+
+    def getTaskId(self) -> int:
+        return self._task_id
+
+    def getNumTask(self) -> int:
+        return self._num_task
+
+    def getStepNo(self) -> int:
+        return self._queue.step_no
+
+    def getObj(self, name: str):
+        return self._store.get(name)
+
+    def putObj(self, name: str, obj):
+        self._store[name] = obj
+
+    def removeObj(self, name: str):
+        self._store.pop(name, None)
+
+    def containsObj(self, name: str) -> bool:
+        return name in self._store
+
+    @property
+    def device(self):
+        return self._queue.device
+
+
+class ComputeFunction:
+    def calc(self, context: ComContext):
+        raise NotImplementedError
+
+    def name(self):
+        return type(self).__name__
+
+
+class ChainedComputation(ComputeFunction):
+    """Adjacent compute items fused into one (reference ``ChainedComputation.java:10-39``)."""
+
+    def __init__(self, fns: Sequence[ComputeFunction]):
+        self.fns = list(fns)
+
+    def calc(self, context):
+        for f in self.fns:
+            f.calc(context)
+
+    def name(self):
+        return "chained computation@" + "->".join(f.name() for f in self.fns)
+
+
+class CommunicateFunction:
+    def communicate(self, contexts: List[ComContext], queue: "BaseComQueue"):
+        raise NotImplementedError
+
+    def name(self):
+        return type(self).__name__
+
+
+class CompareCriterionFunction:
+    def calc(self, context: ComContext) -> bool:
+        raise NotImplementedError
+
+
+class CompleteResultFunction:
+    def calc(self, context: ComContext) -> Optional[List]:
+        raise NotImplementedError
+
+
+def _as_tensor(buf):
+    if isinstance(buf, torch.Tensor):
+        return buf, "torch"
+    if isinstance(buf, np.ndarray):
+        return torch.from_numpy(buf), "numpy"
+    if isinstance(buf, list):
+        return torch.tensor(buf, dtype=torch.float64), "list"
+    raise TypeError(f"AllReduce buffer must be tensor/ndarray/list, got {type(buf)}")
+
+
+class AllReduce(CommunicateFunction):
+    """Element-wise SUM/MAX/MIN of buffer ``bufferName`` across all tasks; optionally only the prefix
+    ``[0, ctx.getObj(lengthName))``.  Local tasks are folded on-device before one collective."""
+
+    def __init__(self, bufferName: str, lengthName: Optional[str] = None, op: str = SUM):
+        self.buffer = bufferName
+        self.length = lengthName
+        self.op = op if isinstance(op, str) else str(op)
+
+    def name(self):
+        return f"AllReduce({self.buffer})"
+
+    def communicate(self, contexts, queue):
+        bufs = [c.getObj(self.buffer) for c in contexts]
+        present = [b for b in bufs if b is not None]
+        if not present:
+            raise RuntimeError(f"AllReduce buffer {self.buffer} missing")
+        n = None
+        if self.length is not None:
+            n = int(contexts[0].getObj(self.length))
+        t0, kind = _as_tensor(present[0])
+        view = (lambda t: t.reshape(-1)[:n]) if n is not None else (lambda t: t.reshape(-1))
+        acc = view(t0).clone()
+        for b in present[1:]:
+            tb, _ = _as_tensor(b)
+            tb = view(tb).to(acc.device)
+            if self.op == SUM:
+                acc += tb
+            elif self.op == MAX:
+                torch.maximum(acc, tb, out=acc)
+            else:
+                torch.minimum(acc, tb, out=acc)
+        comm.all_reduce(acc, self.op)
+        for c, b in zip(contexts, bufs):
+            if b is None:
+                continue
+            tb, kind = _as_tensor(b)
+            view(tb).copy_(acc.to(tb.device))
+            if kind == "list":
+                c.putObj(self.buffer, tb.tolist())
+
+
+class AllGather(CommunicateFunction):
+    """Every task ends with the list of all tasks' ``bufferName`` objects (in task order)."""
+
+    def __init__(self, bufferName: str, outName: Optional[str] = None):
+        self.buffer, self.out = bufferName, outName or bufferName + "_all"
+
+    def communicate(self, contexts, queue):
+        local = [c.getObj(self.buffer) for c in contexts]
+        allv = [x for part in comm.all_gather_object(local) for x in part]
+        for c in contexts:
+            c.putObj(self.out, list(allv))
+
+
+class Broadcast(CommunicateFunction):
+    """Object in task 0's ``bufferName`` copied to every task."""
+
+    def __init__(self, bufferName: str):
+        self.buffer = bufferName
+
+    def communicate(self, contexts, queue):
+        v = contexts[0].getObj(self.buffer) if comm.get_rank() == 0 else None
+        v = comm.broadcast_object(v, 0)
+        for c in contexts:
+            c.putObj(self.buffer, v)
+
+
+def _split(data, parts: int) -> List[Any]:
+    """Split a partition into ``parts`` contiguous sub-partitions."""
+    if parts == 1:
+        return [data]
+    from ..common.table import MTable
+    n = len(data) if not isinstance(data, torch.Tensor) else data.shape[0]
+    bounds = [(i * n) // parts for i in range(parts + 1)]
+    out = []
+    for i in range(parts):
+        lo, hi = bounds[i], bounds[i + 1]
+        if isinstance(data, MTable):
+            out.append(data.slice(lo, hi))
+        else:
+            out.append(data[lo:hi])
+    return out
+
+
+class BaseComQueue:
+    def __init__(self):
+        self.items: List[Any] = []
+        self.criterion: Optional[CompareCriterionFunction] = None
+        self.criterion_replicated = False
+        self.complete: Optional[CompleteResultFunction] = None
+        self.max_iter = 2 ** 31 - 1
+        self.partitioned: List = []
+        self.broadcast: List = []
+        self.step_no = 0
+        self.stats: List[Dict[str, float]] = []
+        self.on_step: List[Callable[[int, "BaseComQueue"], None]] = []
+        self.env = None
+        self.device = None
+        self.sync_device_per_step = False
+
+    # ---- builder API (names as in the reference) ----
+    def initWithPartitionedData(self, name: str, data):
+        self.partitioned.append((name, data))
+        return self
+
+    def initWithBroadcastData(self, name: str, data):
+        self.broadcast.append((name, data))
+        return self
+
+    def add(self, item):
+        self.items.append(item)
+        return self
+
+    def setCompareCriterionOfNode0(self, criterion: CompareCriterionFunction, replicated: bool = False):
+        self.criterion = criterion
+        self.criterion_replicated = replicated
+        return self
+
+    def closeWith(self, complete: CompleteResultFunction):
+        self.complete = complete
+        return self
+
+    def setMaxIter(self, n: int):
+        self.max_iter = int(n)
+        return self
+
+    def setMLEnvironment(self, env):
+        self.env = env
+        return self
+
+    def addStepCallback(self, fn: Callable[[int, "BaseComQueue"], None]):
+        self.on_step.append(fn)
+        return self
+
+    def optimize(self) -> List[Any]:
+        """Fuse runs of adjacent compute items (reference ``BaseComQueue.optimize`` :470-495)."""
+        out: List[Any] = []
+        run: List[ComputeFunction] = []
+        for it in self.items:
+            if isinstance(it, ComputeFunction):
+                run.append(it)
+                continue
+            if run:
+                out.append(run[0] if len(run) == 1 else ChainedComputation(run))
+                run = []
+            out.append(it)
+        if run:
+            out.append(run[0] if len(run) == 1 else ChainedComputation(run))
+        return out
+
+    def __str__(self):
+        return "->".join(it.name() for it in self.optimize())
+
+    # ---- execution ----
+    def exec(self) -> List:
+        from ..common.mlenv import MLEnvironmentFactory
+        from ..common.table import MTable
+        from ..operator.base import gather_table
+        env = self.env or MLEnvironmentFactory.getDefault()
+        self.device = env.device
+        lt = env.local_tasks
+        ws = env.world_size
+        num_task = ws * lt
+        first_task = env.rank * lt
+        stores: List[Dict[str, Any]] = [dict() for _ in range(lt)]
+        ctxs = [ComContext(stores[i], first_task + i, num_task, self) for i in range(lt)]
+        for name, data in self.partitioned:
+            for s, part in zip(stores, _split(data, lt)):
+                s[name] = part
+        for name, data in self.broadcast:
+            full = gather_table(data) if isinstance(data, MTable) else data
+            for s in stores:
+                s[name] = full
+        items = self.optimize()
+        use_roctx = self.device is not None and self.device.type == "cuda" and hasattr(torch.cuda, "nvtx")
+        self.step_no = 0
+        stop = False
+        while not stop and self.step_no < self.max_iter:
+            self.step_no += 1
+            t0 = time.perf_counter()
+            b0 = comm.STATS.bytes
+            if use_roctx:
+                try:
+                    torch.cuda.nvtx.range_push(f"superstep {self.step_no}")
+                except Exception:
+                    use_roctx = False
+            for it in items:
+                if isinstance(it, CommunicateFunction):
+                    it.communicate(ctxs, self)
+                else:
+                    for c in ctxs:
+                        it.calc(c)
+            if self.criterion is not None:
+                if self.criterion_replicated or ws == 1:
+                    dec = bool(self.criterion.calc(ctxs[0]))
+                else:
+                    dec = bool(self.criterion.calc(ctxs[0])) if env.rank == 0 else None
+                    dec = comm.broadcast_object(dec, 0)
+                stop = dec
+            if use_roctx:
+                torch.cuda.nvtx.range_pop()
+            if self.sync_device_per_step and self.device is not None and self.device.type == "cuda":
+                torch.cuda.synchronize(self.device)
+            self.stats.append({"step": self.step_no, "wall_s": time.perf_counter() - t0,
+                               "comm_bytes": comm.STATS.bytes - b0})
+            for fn in self.on_step:
+                fn(self.step_no, self)
+        result: List = []
+        if self.complete is not None:
+            local = []
+            for c in ctxs:
+                r = self.complete.calc(c)
+                if r is not None:
+                    local.extend(r)
+            parts = comm.all_gather_object(local) if ws > 1 else [local]
+            for p in parts:
+                result.extend(p)
+        self.final_contexts = ctxs
+        return result
+
+
+class IterativeComQueue(BaseComQueue):
+    pass
+
+
+class ComQueue(BaseComQueue):
+    def __init__(self):
+        super().__init__()
+        self.max_iter = 1

@@ -1,0 +1,39 @@
+"""Numerics of the fused HIP KMeans assign+accumulate kernel vs a PyTorch fp32/fp64 reference."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _data(n, k, seed=0, dev="cuda"):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    centers = torch.randn(k, 128, generator=g) * 4
+    lab = torch.randint(0, k, (n,), generator=g)
+    X = (centers[lab] + torch.randn(n, 128, generator=g)).to(dev, torch.bfloat16)
+    C = (centers + 0.3 * torch.randn(k, 128, generator=g)).to(dev, torch.float64)
+    return X, C
+
+
+@pytest.mark.parametrize("n,k", [(1, 1), (127, 3), (128, 32), (1000, 33), (4097, 100), (50000, 128), (300001, 100)])
+def test_assign_accumulate_matches_reference(n, k):
+    from alink_amd.ops import kmeans as K
+    from alink_amd.ops import _lib
+    assert _lib.available(), "HIP library must be built and loadable on the GPU box"
+    X, C = _data(n, k)
+    got = K.assign_accumulate_hip(X, C)
+    ref = K.assign_accumulate_torch(X, C)
+    torch.cuda.synchronize()
+    # counts: assignments may differ only for near-ties (relative 2^-16 packing); allow a tiny fraction
+    dc = (got[:, -1] - ref[:, -1]).abs().sum().item()
+    assert dc <= max(2, 1e-4 * n), f"count mismatch {dc}"
+    assert abs(got[:, -1].sum().item() - n) < 0.5
+    if dc == 0:
+        torch.testing.assert_close(got[:, :-1], ref[:, :-1], rtol=1e-5, atol=1e-3 * max(1.0, n / 1000))
+
+
+def test_kernel_deterministic():
+    from alink_amd.ops import kmeans as K
+    X, C = _data(200000, 100, seed=3)
+    a = K.assign_accumulate_hip(X, C)
+    b = K.assign_accumulate_hip(X, C)
+    assert torch.equal(a, b)
