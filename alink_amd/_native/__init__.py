@@ -1,0 +1,119 @@
+"""ctypes binding of the host C++ runtime (``csrc/runtime.cpp`` -> ``libalink_native.so``).
+
+Provides bulk CSV parsing, Guava-compatible murmur3 (UTF-16) hashing and dense vector-string parsing.
+Every function has a pure-Python fallback in its caller; ``lib`` is ``None`` when the library is not built.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+__all__ = ["lib", "parse_csv_lines", "murmur3_utf16", "parse_dense_vectors"]
+
+_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libalink_native.so")
+lib = None
+if os.path.exists(_PATH):
+    try:
+        lib = ctypes.CDLL(_PATH)
+        lib.alink_csv_parse.restype = ctypes.c_int
+        lib.alink_murmur3_utf16_batch.restype = None
+        lib.alink_parse_dense_vectors.restype = ctypes.c_int
+    except OSError:
+        lib = None
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def parse_csv_lines(lines: Sequence[str], codes: List[int], delim: str, quote: str, skip_blank: bool):
+    """Returns per column (values, nulls): numpy arrays for numeric, python lists for strings; or None."""
+    if lib is None:
+        return None
+    if not skip_blank:
+        lines = list(lines)
+    else:
+        lines = [l for l in lines if l]
+    enc = [l.encode("utf-8") for l in lines]
+    n = len(enc)
+    off = np.zeros(n + 1, dtype=np.int64)
+    if n:
+        np.cumsum([len(b) for b in enc], out=off[1:])
+    buf = b"".join(enc)
+    ncol = len(codes)
+    nums, nulls, soffs, sescs = [], [], [], []
+    num_ptrs = (ctypes.c_void_p * ncol)()
+    null_ptrs = (ctypes.c_void_p * ncol)()
+    soff_ptrs = (ctypes.c_void_p * ncol)()
+    sesc_ptrs = (ctypes.c_void_p * ncol)()
+    for c, t in enumerate(codes):
+        a = np.zeros(n, dtype=np.float64 if t == 1 else np.int64) if t != 0 else np.zeros(1, dtype=np.int64)
+        nl = np.ones(max(n, 1), dtype=np.uint8)
+        so = np.full(2 * max(n, 1), -1, dtype=np.int64)
+        se = np.zeros(max(n, 1), dtype=np.uint8)
+        nums.append(a), nulls.append(nl), soffs.append(so), sescs.append(se)
+        num_ptrs[c] = a.ctypes.data
+        null_ptrs[c] = nl.ctypes.data
+        soff_ptrs[c] = so.ctypes.data
+        sesc_ptrs[c] = se.ctypes.data
+    ct = np.asarray(codes, dtype=np.int32)
+    q = ord(quote) if quote else -1
+    rc = lib.alink_csv_parse(ctypes.c_char_p(buf), _ptr(off), ctypes.c_int64(n), ctypes.c_int(ncol), _ptr(ct),
+                             ctypes.c_char(delim.encode()), ctypes.c_int(q), num_ptrs, null_ptrs, soff_ptrs,
+                             sesc_ptrs)
+    if rc != 0:
+        raise RuntimeError(f'Fail to parse line "{lines[-1 - rc]}"')
+    out = []
+    for c, t in enumerate(codes):
+        nl = nulls[c][:n].astype(bool)
+        if t == 0:
+            so = soffs[c]
+            vals = []
+            for i in range(n):
+                a, b = so[2 * i], so[2 * i + 1]
+                if a < 0:
+                    vals.append(None)
+                else:
+                    s = buf[a:b].decode("utf-8")
+                    if sescs[c][i]:
+                        s = s.replace(quote * 2, quote)
+                    vals.append(s)
+            out.append((vals, None))
+        elif t == 3:
+            out.append((nums[c].astype(bool), nl))
+        else:
+            out.append((nums[c], nl))
+    return out
+
+
+def murmur3_utf16(strings: Sequence[str], seed: int = 0) -> Optional[np.ndarray]:
+    if lib is None:
+        return None
+    units = [np.frombuffer(s.encode("utf-16-le"), dtype=np.uint16) for s in strings]
+    off = np.zeros(len(units) + 1, dtype=np.int64)
+    if units:
+        np.cumsum([len(u) for u in units], out=off[1:])
+    chars = np.concatenate(units) if units else np.zeros(1, dtype=np.uint16)
+    out = np.zeros(len(units), dtype=np.int32)
+    lib.alink_murmur3_utf16_batch(_ptr(chars), _ptr(off), ctypes.c_int64(len(units)), ctypes.c_uint32(seed),
+                                  _ptr(out))
+    return out
+
+
+def parse_dense_vectors(strings: Sequence[str], d: int) -> Optional[np.ndarray]:
+    if lib is None:
+        return None
+    enc = [s.encode("ascii") for s in strings]
+    off = np.zeros(len(enc) + 1, dtype=np.int64)
+    if enc:
+        np.cumsum([len(b) for b in enc], out=off[1:])
+    buf = b"".join(enc)
+    out = np.zeros((len(enc), d), dtype=np.float64)
+    rc = lib.alink_parse_dense_vectors(ctypes.c_char_p(buf), _ptr(off), ctypes.c_int64(len(enc)),
+                                       ctypes.c_int64(d), _ptr(out))
+    if rc != 0:
+        return None
+    return out

@@ -1,0 +1,204 @@
+// Host-side native runtime for alink_amd (C ABI, loaded with ctypes).
+//
+//  * CSV line parsing with Alink CsvParser semantics (A/operator/common/io/csv/CsvParser.java): quoting only
+//    for string columns, doubled quote = literal quote, blank non-string token = NULL.  Numeric columns are
+//    parsed straight into typed arrays in parallel (OpenMP) — the reference parses row-by-row in Java.
+//  * Guava-compatible murmur3_32(seed 0) over UTF-16 code units ("hashUnencodedChars"), used by
+//    FeatureHasher (A/operator/common/feature/FeatureHasherMapper.java:37,63-106).
+//  * dense vector string parsing ("1 2 3" / "1,2,3") into a row-major double matrix.
+#include <cmath>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+
+extern "C" {
+
+// types: 0 = string, 1 = double, 2 = int64, 3 = bool
+// out_num[c]: double* (type 1) or int64_t* (types 2, 3) with nlines entries (may be null for string cols)
+// out_null[c]: uint8_t* nlines (1 = NULL)
+// out_soff[c]: int64_t* 2*nlines (start, end byte offsets into buf; -1 = NULL), for string columns
+// out_sesc[c]: uint8_t* nlines (1 = contains escaped quotes to collapse)
+// returns -1 - line on parse error, else 0
+int alink_csv_parse(const char* buf, const int64_t* line_off, int64_t nlines, int ncols, const int* types,
+                    char delim, int quote, void** out_num, uint8_t** out_null, int64_t** out_soff,
+                    uint8_t** out_sesc) {
+    int64_t err = -1;
+#pragma omp parallel for schedule(static)
+    for (int64_t li = 0; li < nlines; ++li) {
+        const char* s = buf + line_off[li];
+        const int64_t n = line_off[li + 1] - line_off[li];
+        int64_t pos = 0;
+        bool ok = true;
+        for (int c = 0; c < ncols; ++c) {
+            out_null[c][li] = 1;
+            if (types[c] == 0) {
+                out_soff[c][2 * li] = -1;
+                out_soff[c][2 * li + 1] = -1;
+                out_sesc[c][li] = 0;
+            }
+            if (pos > n) {
+                ok = false;
+                continue;
+            }
+            // find the end of this field
+            int64_t end;
+            if (types[c] == 0 && quote >= 0 && pos < n && s[pos] == (char)quote) {
+                int64_t p = pos + 1;
+                bool esc = false;
+                while (p < n) {
+                    if (s[p] == (char)quote) {
+                        if (!esc) {
+                            if (p + 1 < n && s[p + 1] == (char)quote) esc = true;
+                            else break;
+                        } else {
+                            esc = false;
+                        }
+                    }
+                    ++p;
+                }
+                if (p >= n) end = n;
+                else {
+                    const char* d = (const char*)memchr(s + p + 1, delim, n - p - 1);
+                    end = d ? (d - s) : n;
+                }
+            } else {
+                const char* d = (pos < n) ? (const char*)memchr(s + pos, delim, n - pos) : nullptr;
+                end = d ? (d - s) : n;
+            }
+            const int64_t tl = end - pos;
+            if (tl > 0) {
+                const char* tok = s + pos;
+                if (types[c] == 0) {
+                    int64_t a = line_off[li] + pos, b = line_off[li] + end;
+                    if (quote >= 0 && tok[0] == (char)quote) {
+                        a += 1;
+                        if (tl > 1 && tok[tl - 1] == (char)quote) b -= 1;
+                        for (int64_t q = 1; q + 1 < tl; ++q)
+                            if (tok[q] == (char)quote && tok[q + 1] == (char)quote) { out_sesc[c][li] = 1; break; }
+                    }
+                    out_soff[c][2 * li] = a;
+                    out_soff[c][2 * li + 1] = b;
+                    out_null[c][li] = 0;
+                } else {
+                    int64_t a = 0, b = tl;
+                    while (a < b && (tok[a] == ' ' || tok[a] == '\t' || tok[a] == '\r')) ++a;
+                    while (b > a && (tok[b - 1] == ' ' || tok[b - 1] == '\t' || tok[b - 1] == '\r')) --b;
+                    if (b > a) {
+                        std::string t(tok + a, b - a);
+                        char* ep = nullptr;
+                        if (types[c] == 1) {
+                            double v = strtod(t.c_str(), &ep);
+                            if (*ep != 0) ok = false;
+                            ((double*)out_num[c])[li] = v;
+                        } else if (types[c] == 2) {
+                            long long v = strtoll(t.c_str(), &ep, 10);
+                            if (*ep != 0) {  // allow "3.0"-style integers like Long.parseLong would not; reject
+                                ok = false;
+                            }
+                            ((int64_t*)out_num[c])[li] = (int64_t)v;
+                        } else {
+                            bool v;
+                            if (t == "true" || t == "TRUE" || t == "True" || t == "1") v = true;
+                            else if (t == "false" || t == "FALSE" || t == "False" || t == "0") v = false;
+                            else { ok = false; v = false; }
+                            ((int64_t*)out_num[c])[li] = v ? 1 : 0;
+                        }
+                        out_null[c][li] = 0;
+                    }
+                }
+            }
+            pos = end + 1;
+        }
+        if (!ok) {
+#pragma omp critical
+            { if (err < 0 || li < err) err = li; }
+        }
+    }
+    return err >= 0 ? (int)(-1 - err) : 0;
+}
+
+static inline uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+
+static inline uint32_t mix_k1(uint32_t k1) {
+    k1 *= 0xcc9e2d51u;
+    k1 = rotl32(k1, 15);
+    k1 *= 0x1b873593u;
+    return k1;
+}
+
+static inline uint32_t mix_h1(uint32_t h1, uint32_t k1) {
+    h1 ^= k1;
+    h1 = rotl32(h1, 13);
+    h1 = h1 * 5 + 0xe6546b64u;
+    return h1;
+}
+
+static inline uint32_t fmix(uint32_t h1, uint32_t length) {
+    h1 ^= length;
+    h1 ^= h1 >> 16;
+    h1 *= 0x85ebca6bu;
+    h1 ^= h1 >> 13;
+    h1 *= 0xc2b2ae35u;
+    h1 ^= h1 >> 16;
+    return h1;
+}
+
+// Guava Murmur3_32HashFunction.hashUnencodedChars(seed) over UTF-16 code units
+static int32_t murmur3_utf16(const uint16_t* chars, int64_t len, uint32_t seed) {
+    uint32_t h1 = seed;
+    int64_t i = 1;
+    for (; i < len; i += 2) {
+        uint32_t k1 = (uint32_t)chars[i - 1] | ((uint32_t)chars[i] << 16);
+        k1 = mix_k1(k1);
+        h1 = mix_h1(h1, k1);
+    }
+    if ((len & 1) == 1) {
+        uint32_t k1 = chars[len - 1];
+        k1 = mix_k1(k1);
+        h1 ^= k1;
+    }
+    return (int32_t)fmix(h1, (uint32_t)(2 * len));
+}
+
+// batch: strings given as UTF-16 code units concatenated, offsets (in code units) n+1
+void alink_murmur3_utf16_batch(const uint16_t* chars, const int64_t* off, int64_t n, uint32_t seed,
+                               int32_t* out) {
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; ++i) out[i] = murmur3_utf16(chars + off[i], off[i + 1] - off[i], seed);
+}
+
+// dense vector strings -> row-major [n][d] doubles (missing tail = 0); returns -1 - row on error
+int alink_parse_dense_vectors(const char* buf, const int64_t* off, int64_t n, int64_t d, double* out) {
+    int64_t err = -1;
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; ++i) {
+        const char* p = buf + off[i];
+        const char* e = buf + off[i + 1];
+        double* row = out + i * d;
+        for (int64_t j = 0; j < d; ++j) row[j] = 0.0;
+        int64_t j = 0;
+        std::string tmp;
+        while (p < e) {
+            while (p < e && (*p == ' ' || *p == ',' || *p == '\t')) ++p;
+            if (p >= e) break;
+            const char* q = p;
+            while (q < e && *q != ' ' && *q != ',' && *q != '\t') ++q;
+            tmp.assign(p, q - p);
+            char* ep = nullptr;
+            double v = strtod(tmp.c_str(), &ep);
+            if (*ep != 0 || j >= d) {
+#pragma omp critical
+                { if (err < 0 || i < err) err = i; }
+                break;
+            }
+            row[j++] = v;
+            p = q;
+        }
+    }
+    return err >= 0 ? (int)(-1 - err) : 0;
+}
+
+int alink_native_version() { return 1; }
+
+}  // extern "C"

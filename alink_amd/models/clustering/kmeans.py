@@ -1,0 +1,481 @@
+"""KMeans: model data, converter, BSP training (Lloyd with k-means|| init) and batched prediction.
+
+Reference behaviour (cited per piece):
+* model format — ``KMeansModelDataConverter.java:16-33``: meta = ``ParamSummary.toParams``
+  (distanceType, k, vectorSize, vectorCol, latitudeCol, longitudeCol), one JSON ``ClusterSummary``
+  ``{"clusterId","weight","vec":{"data":[..]}}`` per centroid;
+* superstep — ``KMeansTrainBatchOp.java:58-81``: preallocate -> assign+accumulate -> AllReduce ->
+  update (drops empty clusters, ``KMeansUpdateCentroids.java:52-69``) -> task-0 criterion
+  (max per-centroid shift < epsilon, ``KMeansIterTermination.java:28-44``) -> output;
+  the two centroid buffers alternate by step parity;
+* init — ``KMeansInitCentroids.java``: RANDOM (sample k rows) or K_MEANS_PARALLEL (k-means||: one random
+  center, ``initSteps-1`` rounds sampling each point with probability ``2k*cost/sum(cost)``, weights =
+  nearest-candidate counts, then weighted local k-means++ + Lloyd (``LocalKmeansFunc.java``, 30 iters));
+  the k-means|| oversampling cost is the FastDistance value as in the reference; deliberate deviation: the
+  final weighted k-means++ over the candidates uses the *squared* Euclidean distance (Arthur & Vassilvitskii)
+  — with the plain distance it regularly puts two seeds in one well-separated cluster;
+* predict — ``KMeansModelMapper.java:61-97``: prediction (cluster id), optional detail
+  (``KMeansUtil.getProbArrayFromDistanceArray``) and distance columns.
+
+MI355X path: rows stay on the GPU; the assign/accumulate step is the fused HIP kernel
+(``ops/csrc/kmeans.hip``) for bf16 d=128 data, the all-reduce is RCCL, and the update/criterion are a
+handful of device ops — no per-sample host work.
+"""
+from __future__ import annotations
+
+import json
+import math
+from typing import List, Optional
+
+import numpy as np
+import torch
+
+from ...common.linalg import DenseVector, VectorUtil
+from ...common.mapper import RichModelMapper, ModelMapper, OutputColsHelper
+from ...common.model import SimpleModelDataConverter
+from ...common.params import Params
+from ...common.table import Column, MTable
+from ...common.types import TableSchema, Types
+from ...params import get_enum, param
+from ...parallel import comm
+from ...parallel.comqueue import (AllReduce, CompareCriterionFunction, CompleteResultFunction, ComputeFunction,
+                                  IterativeComQueue)
+from ...ops import kmeans as kops
+
+__all__ = ["ClusterSummary", "KMeansTrainModelData", "KMeansModelDataConverter", "KMeansPredictModelData",
+           "KMeansModelMapper", "train_kmeans", "kmeans_init", "pairwise_distance"]
+
+TRAIN_DATA = "trainData"
+INIT_CENTROID = "initCentroid"
+CENTROID1 = "centroid1"
+CENTROID2 = "centroid2"
+CENTROID_ALL_REDUCE = "centroidAllReduce"
+VECTOR_SIZE = "vectorSize"
+K = "k"
+
+
+class ClusterSummary:
+    __gson_fields__ = ("clusterId", "weight", "vec")
+
+    def __init__(self, vec: DenseVector, clusterId: int, weight: float):
+        self.vec, self.clusterId, self.weight = vec, int(clusterId), float(weight)
+
+
+class KMeansTrainModelData:
+    def __init__(self, centroids: List[ClusterSummary], k: int, vectorSize: int, distanceType: str,
+                 vectorColName: Optional[str], latitudeColName=None, longitudeColName=None):
+        self.centroids = centroids
+        self.k = k
+        self.vectorSize = vectorSize
+        self.distanceType = distanceType
+        self.vectorColName = vectorColName
+        self.latitudeColName = latitudeColName
+        self.longitudeColName = longitudeColName
+
+    def to_params(self) -> Params:
+        dt = get_enum("DistanceType", "HasKMeansWithHaversineDistanceType")[self.distanceType]
+        p = Params()
+        p.set("distanceType", dt)
+        p.set("k", self.k)
+        p.set("vectorSize", self.vectorSize)
+        p.set("vectorCol", self.vectorColName)
+        p.set("latitudeCol", self.latitudeColName)
+        p.set("longitudeCol", self.longitudeColName)
+        return p
+
+
+class KMeansPredictModelData:
+    def __init__(self, centroids: np.ndarray, ids: np.ndarray, weights: np.ndarray, params: Params):
+        self.centroids = centroids  # [k, d] float64
+        self.ids = ids
+        self.weights = weights
+        self.params = params
+        self.k = int(params.get("k", int))
+        self.distanceType = params.get("distanceType", str)
+        self.vectorColName = params.get("vectorCol", str) if params.contains("vectorCol") else None
+        self.latitudeColName = params.get("latitudeCol", str) if params.contains("latitudeCol") else None
+        self.longitudeColName = params.get("longitudeCol", str) if params.contains("longitudeCol") else None
+
+
+class KMeansModelDataConverter(SimpleModelDataConverter):
+    def serializeModel(self, model: KMeansTrainModelData):
+        from ...common.javafmt import gson_dumps
+        return model.to_params(), [gson_dumps(c) for c in model.centroids]
+
+    def deserializeModel(self, meta: Params, data: List[str]) -> KMeansPredictModelData:
+        vecs, ids, ws = [], [], []
+        for s in data:
+            o = json.loads(s)
+            if "vec" in o and o["vec"] is not None:
+                v = o["vec"]["data"] if isinstance(o["vec"], dict) else o["vec"]
+            else:  # legacy OldClusterSummary with "center" string (KMeansUtil.java:278-310)
+                c = o.get("center")
+                v = json.loads(c)["data"] if "data" in c else json.loads(c)
+            vecs.append(np.asarray(v, dtype=np.float64))
+            ids.append(int(o["clusterId"]))
+            ws.append(float(o.get("weight", 0.0)))
+        C = np.stack(vecs) if vecs else np.zeros((0, 0))
+        if str(meta.get("distanceType", str)).upper() == "COSINE":
+            n = np.linalg.norm(C, axis=1, keepdims=True)
+            C = np.where(n > 0, C / np.where(n > 0, n, 1), C)
+        return KMeansPredictModelData(C, np.asarray(ids), np.asarray(ws), meta)
+
+
+# ---------------------------------------------------------------------------------------------------
+# distances
+# ---------------------------------------------------------------------------------------------------
+def pairwise_distance(X: torch.Tensor, C: torch.Tensor, distance_type: str) -> torch.Tensor:
+    """[n, k] FastDistance values (EUCLIDEAN: sqrt|x-c|^2, COSINE: 1 - x.c on normalised inputs,
+    HAVERSINE: great-circle km on (lat, lon) degrees)."""
+    dt = distance_type.upper()
+    if dt == "COSINE":
+        return 1.0 - X @ C.T
+    if dt == "HAVERSINE":
+        lat1 = torch.deg2rad(X[:, 0:1])
+        lon1 = torch.deg2rad(X[:, 1:2])
+        lat2 = torch.deg2rad(C[:, 0])[None, :]
+        lon2 = torch.deg2rad(C[:, 1])[None, :]
+        a = torch.sin((lat2 - lat1) / 2) ** 2 + torch.cos(lat1) * torch.cos(lat2) * torch.sin((lon2 - lon1) / 2) ** 2
+        return 2 * 6371.0 * torch.asin(torch.sqrt(a.clamp(0, 1)))
+    xn = (X * X).sum(1, keepdim=True)
+    cn = (C * C).sum(1)[None, :]
+    return torch.sqrt((xn + cn - 2.0 * (X @ C.T)).abs())
+
+
+def _normalize_rows(X: torch.Tensor) -> torch.Tensor:
+    n = X.norm(dim=1, keepdim=True)
+    return torch.where(n > 0, X / torch.where(n > 0, n, torch.ones_like(n)), X)
+
+
+# ---------------------------------------------------------------------------------------------------
+# initialisation
+# ---------------------------------------------------------------------------------------------------
+def _seed_cost(d: torch.Tensor, dist_type: str) -> torch.Tensor:
+    return d * d if dist_type.upper() == "EUCLIDEAN" else d
+
+
+def _min_dist_to(X: torch.Tensor, C: torch.Tensor, dist_type: str, chunk=1 << 20) -> torch.Tensor:
+    out = []
+    Cf = C.to(torch.float32 if X.dtype in (torch.bfloat16, torch.float16) else X.dtype)
+    for s in range(0, X.shape[0], chunk):
+        xc = X[s:s + chunk].to(Cf.dtype)
+        out.append(pairwise_distance(xc, Cf, dist_type).min(1).values.to(torch.float64))
+    return torch.cat(out) if out else torch.zeros(0, dtype=torch.float64, device=X.device)
+
+
+def _nearest(X: torch.Tensor, C: torch.Tensor, dist_type: str, chunk=1 << 20) -> torch.Tensor:
+    out = []
+    Cf = C.to(torch.float32 if X.dtype in (torch.bfloat16, torch.float16) else X.dtype)
+    for s in range(0, X.shape[0], chunk):
+        xc = X[s:s + chunk].to(Cf.dtype)
+        out.append(pairwise_distance(xc, Cf, dist_type).argmin(1))
+    return torch.cat(out) if out else torch.zeros(0, dtype=torch.int64, device=X.device)
+
+
+def _global_count(n_local: int) -> List[int]:
+    return comm.all_gather_object(int(n_local))
+
+
+def _fetch_global_rows(X: torch.Tensor, global_idx: List[int], counts: List[int]) -> torch.Tensor:
+    """Rows by global index (rank-order concatenation), replicated on every rank."""
+    rank = comm.get_rank()
+    offs = np.concatenate([[0], np.cumsum(counts)])
+    mine = [(j, g - offs[rank]) for j, g in enumerate(global_idx) if offs[rank] <= g < offs[rank + 1]]
+    local = [(j, X[i].to(torch.float64).cpu().numpy()) for j, i in mine]
+    parts = comm.all_gather_object(local)
+    rows = [None] * len(global_idx)
+    for p in parts:
+        for j, v in p:
+            rows[j] = v
+    return torch.from_numpy(np.stack(rows)).to(X.device)
+
+
+def _local_kmeans(samples: torch.Tensor, weights: torch.Tensor, k: int, dist_type: str,
+                  max_iter: int = 30, seed: int = 0) -> torch.Tensor:
+    """Weighted k-means++ seeding + Lloyd on the candidate set (LocalKmeansFunc.java)."""
+    rng = np.random.default_rng(seed)
+    n = samples.shape[0]
+    w = weights.to(torch.float64)
+    costs = torch.ones(n, dtype=torch.float64, device=samples.device)
+    idx = 0
+    chosen = []
+    for i in range(k):
+        if i > 0:
+            d = _seed_cost(pairwise_distance(samples, samples[idx:idx + 1], dist_type)[:, 0], dist_type)
+            costs = torch.minimum(d, costs) if i > 1 else d
+        cum = torch.cumsum(w * costs, 0).cpu().numpy()
+        r = rng.random() * cum[-1]
+        j = int(np.searchsorted(cum, r, side="left"))
+        idx = min(max(j, 0), n - 1)
+        chosen.append(idx)
+    C = samples[chosen].clone()
+    assign = torch.full((n,), -1, dtype=torch.int64, device=samples.device)
+    for _ in range(max_iter):
+        a = pairwise_distance(samples, C, dist_type).argmin(1)
+        converged = bool(torch.equal(a, assign))
+        assign = a
+        S = torch.zeros_like(C)
+        S.index_add_(0, a, samples * w[:, None])
+        cnt = torch.zeros(k, dtype=torch.float64, device=samples.device).index_add_(0, a, w)
+        for c in range(k):
+            if cnt[c] > 0:
+                C[c] = S[c] / cnt[c]
+            else:
+                C[c] = samples[int(rng.integers(n))]
+        if dist_type.upper() == "COSINE":
+            C = _normalize_rows(C)
+        if converged:
+            break
+    return C
+
+
+def kmeans_init(X: torch.Tensor, k: int, init_mode: str, init_steps: int, dist_type: str,
+                seed: int = 0) -> torch.Tensor:
+    """Initial centroids [k', d] float64 (identical on every rank)."""
+    counts = _global_count(X.shape[0])
+    n = int(sum(counts))
+    if n == 0:
+        raise ValueError("The train dataset is empty!")
+    rng = np.random.default_rng(seed)
+    if init_mode.upper() == "RANDOM" or n <= k:
+        gidx = sorted(rng.choice(n, size=min(k, n), replace=False).tolist())
+        return _fetch_global_rows(X, gidx, counts)
+    # k-means||
+    centers = _fetch_global_rows(X, [int(rng.integers(n))], counts)
+    cost = _min_dist_to(X, centers, dist_type)
+    lrng = torch.Generator(device="cpu").manual_seed(seed * 7919 + comm.get_rank() + 1)
+    for _ in range(max(0, init_steps - 1)):
+        tot = torch.tensor([float(cost.sum().item())], dtype=torch.float64)
+        comm.all_reduce(tot)
+        thre = 2.0 * k / max(float(tot.item()), 1e-300)
+        u = torch.rand(X.shape[0], generator=lrng, dtype=torch.float64).to(X.device)
+        pick = torch.nonzero(u < cost * thre).reshape(-1)
+        local_new = X[pick].to(torch.float64).cpu()
+        parts = comm.all_gather_object(local_new)
+        new = torch.cat([p for p in parts if p.shape[0] > 0]) if any(p.shape[0] > 0 for p in parts) else None
+        if new is None:
+            continue
+        new = new.to(X.device)
+        centers = torch.cat([centers, new])
+        cost = torch.minimum(cost, _min_dist_to(X, new, dist_type))
+    if centers.shape[0] <= k:
+        return centers
+    near = _nearest(X, centers, dist_type)
+    w = torch.bincount(near, minlength=centers.shape[0]).to(torch.float64)
+    comm.all_reduce(w)
+    return _local_kmeans(centers, w, k, dist_type, seed=seed)
+
+
+# ---------------------------------------------------------------------------------------------------
+# BSP queue items
+# ---------------------------------------------------------------------------------------------------
+class KMeansPreallocateCentroid(ComputeFunction):
+    def calc(self, ctx):
+        if ctx.getStepNo() == 1:
+            C = ctx.getObj(INIT_CENTROID)
+            ctx.putObj(CENTROID1, [0, C.clone()])
+            ctx.putObj(CENTROID2, [0, C.clone()])
+            ctx.putObj(K, C.shape[0])
+
+
+class KMeansAssignCluster(ComputeFunction):
+    def calc(self, ctx):
+        cur = ctx.getObj(CENTROID1) if ctx.getStepNo() % 2 == 0 else ctx.getObj(CENTROID2)
+        k = ctx.getObj(K)
+        X = ctx.getObj(TRAIN_DATA)
+        C = cur[1][:k]
+        if X is None or X.shape[0] == 0:
+            buf = torch.zeros((k, C.shape[1] + 1), dtype=torch.float64, device=C.device)
+        else:
+            buf = kops.assign_accumulate(X, C)
+        ctx.putObj(CENTROID_ALL_REDUCE, buf)
+
+
+class KMeansUpdateCentroids(ComputeFunction):
+    def __init__(self, dist_type: str):
+        self.dist_type = dist_type
+
+    def calc(self, ctx):
+        tgt = ctx.getObj(CENTROID2) if ctx.getStepNo() % 2 == 0 else ctx.getObj(CENTROID1)
+        buf = ctx.getObj(CENTROID_ALL_REDUCE)
+        d = buf.shape[1] - 1
+        cnt = buf[:, d]
+        keep = cnt > 0
+        C = buf[keep, :d] / cnt[keep, None]
+        if self.dist_type == "COSINE":
+            C = _normalize_rows(C)
+        tgt[0] = ctx.getStepNo()
+        tgt[1] = C
+        ctx.putObj("lastWeights", cnt[keep])
+        ctx.putObj(K, int(C.shape[0]))
+
+
+class KMeansIterTermination(CompareCriterionFunction):
+    def __init__(self, dist_type: str, tol: float):
+        self.dist_type, self.tol = dist_type, tol
+
+    def calc(self, ctx) -> bool:
+        k = ctx.getObj(K)
+        a = ctx.getObj(CENTROID1)[1][:k]
+        b = ctx.getObj(CENTROID2)[1][:k]
+        if a.shape != b.shape:
+            return False
+        if self.dist_type == "COSINE":
+            d = 1.0 - (a * b).sum(1)
+        elif self.dist_type == "HAVERSINE":
+            d = torch.diagonal(pairwise_distance(a, b, "HAVERSINE"))
+        else:
+            d = (a - b).norm(dim=1)
+        return bool((d < self.tol).all().item())
+
+
+class KMeansOutputModel(CompleteResultFunction):
+    def __init__(self, dist_type, vector_col, lat_col=None, lon_col=None):
+        self.dist_type, self.vector_col, self.lat_col, self.lon_col = dist_type, vector_col, lat_col, lon_col
+
+    def calc(self, ctx):
+        if ctx.getTaskId() != 0:
+            return None
+        c1, c2 = ctx.getObj(CENTROID1), ctx.getObj(CENTROID2)
+        cur = c1 if c1[0] > c2[0] else c2
+        k = ctx.getObj(K)
+        C = cur[1][:k].to(torch.float64).cpu().numpy()
+        w = ctx.getObj("lastWeights")
+        w = w.cpu().numpy() if w is not None else np.zeros(k)
+        cents = [ClusterSummary(DenseVector(C[i]), i, float(w[i]) if i < len(w) else 0.0) for i in range(k)]
+        md = KMeansTrainModelData(cents, k, int(ctx.getObj(VECTOR_SIZE)), self.dist_type, self.vector_col,
+                                  self.lat_col, self.lon_col)
+        return KMeansModelDataConverter().save(md)
+
+
+def train_kmeans(X: torch.Tensor, k: int, max_iter: int, tol: float, dist_type: str, init_mode: str,
+                 init_steps: int, vector_col: Optional[str], env, lat_col=None, lon_col=None,
+                 init_centroids: Optional[torch.Tensor] = None, on_step=None, seed: int = 0):
+    """Run the KMeans BSP queue on this rank's rows ``X`` ([n, d] on the env device); returns
+    (model rows, queue)."""
+    dist_type = dist_type.upper()
+    if dist_type == "COSINE":
+        X = _normalize_rows(X.to(torch.float64)) if X.dtype == torch.float64 else \
+            _normalize_rows(X.float()).to(X.dtype)
+    vector_size = max(comm.all_gather_object(int(X.shape[1]) if X.shape[0] else 0))
+    init = init_centroids if init_centroids is not None else kmeans_init(X, k, init_mode, init_steps, dist_type,
+                                                                         seed=seed)
+    init = init.to(device=X.device, dtype=torch.float64)
+    q = (IterativeComQueue()
+         .setMLEnvironment(env)
+         .initWithPartitionedData(TRAIN_DATA, X)
+         .initWithBroadcastData(INIT_CENTROID, init)
+         .add(KMeansPreallocateCentroid())
+         .add(KMeansAssignCluster())
+         .add(AllReduce(CENTROID_ALL_REDUCE))
+         .add(KMeansUpdateCentroids(dist_type))
+         .setCompareCriterionOfNode0(KMeansIterTermination(dist_type, tol), replicated=True)
+         .closeWith(KMeansOutputModel(dist_type, vector_col, lat_col, lon_col))
+         .setMaxIter(max_iter))
+    q.initWithBroadcastData(VECTOR_SIZE, vector_size)
+    # VECTOR_SIZE is consumed by the output function; mirror the reference's KMEANS_STATISTICS broadcast
+    if on_step is not None:
+        q.addStepCallback(on_step)
+    rows = q.exec()
+    return rows, q
+
+
+# ---------------------------------------------------------------------------------------------------
+# prediction
+# ---------------------------------------------------------------------------------------------------
+def prob_from_distances(d: torch.Tensor) -> torch.Tensor:
+    """Row-wise ``getProbArrayFromDistanceArray`` (KMeansUtil.java)."""
+    k = d.shape[1]
+    s = d.sum(1, keepdim=True)
+    return 1.0 / (k - 1) - d / s / (k - 1)
+
+
+class KMeansModelMapper(ModelMapper):
+    def __init__(self, modelSchema, dataSchema, params=None):
+        super().__init__(modelSchema, dataSchema, params)
+        p = self.params
+        reserved = p.get("reservedCols") if p.contains("reservedCols") else None
+        self.pred_col = p.get("predictionCol")
+        self.detail_col = p.get("predictionDetailCol") if p.contains("predictionDetailCol") else None
+        self.dist_col = p.get("predictionDistanceCol") if p.contains("predictionDistanceCol") else None
+        names, types = [self.pred_col], [Types.LONG]
+        if self.detail_col:
+            names.append(self.detail_col)
+            types.append(Types.STRING)
+        if self.dist_col:
+            names.append(self.dist_col)
+            types.append(Types.DOUBLE)
+        self.helper = OutputColsHelper(dataSchema, names, types, reserved)
+
+    def loadModel(self, modelRows):
+        self.model = KMeansModelDataConverter().load(modelRows)
+        self.C = torch.from_numpy(self.model.centroids)
+
+    def _input_block(self, mt: MTable):
+        m = self.model
+        if m.vectorColName is not None:
+            c = mt.col(m.vectorColName)
+            v = c.values
+            if isinstance(v, torch.Tensor) and v.dim() == 2:
+                return v, None
+            vecs = [VectorUtil.getVector(x) for x in v]
+            nulls = [x is None for x in vecs]
+            d = self.C.shape[1]
+            arr = np.zeros((len(vecs), d))
+            for i, x in enumerate(vecs):
+                if x is None:
+                    continue
+                if hasattr(x, "indices"):
+                    sel = x.indices < d
+                    arr[i, x.indices[sel]] = x.values[sel]
+                else:
+                    arr[i, :min(d, x.size())] = x.data[:d]
+            return torch.from_numpy(arr), nulls
+        lat = mt.col(m.latitudeColName).to_list()
+        lon = mt.col(m.longitudeColName).to_list()
+        return torch.tensor(np.stack([np.asarray(lat, float), np.asarray(lon, float)], 1)), None
+
+    def _map_columns(self, mt: MTable):
+        X, nulls = self._input_block(mt)
+        dev = X.device
+        dt = self.model.distanceType.upper()
+        if X.dtype in (torch.bfloat16, torch.float16) and dt == "EUCLIDEAN" and X.is_cuda:
+            C = self.C.to(dev)
+            idx, d2 = kops.assign(X, C)
+            dist_all = None
+            if self.detail_col:
+                dist_all = torch.cat([pairwise_distance(X[s:s + (1 << 20)].float(), C.float(), dt).double()
+                                      for s in range(0, X.shape[0], 1 << 20)])
+            best = d2.sqrt()
+        else:
+            Xf = X.to(torch.float64)
+            if dt == "COSINE":
+                Xf = _normalize_rows(Xf)
+            C = self.C.to(Xf.device)
+            dist_all = pairwise_distance(Xf, C, dt)
+            best, idx = dist_all.min(1)
+        ids = torch.as_tensor(self.model.ids, device=idx.device)[idx]
+        outs = [Column(ids.to(torch.int64).cpu())]
+        if nulls is not None and any(nulls):
+            outs[0] = Column.from_values([None if nl else int(v) for v, nl in zip(outs[0].to_list(), nulls)],
+                                         Types.LONG)
+        if self.detail_col:
+            probs = prob_from_distances(dist_all).cpu().numpy()
+            order = self.model.ids
+            det = []
+            for r in range(probs.shape[0]):
+                if nulls is not None and nulls[r]:
+                    det.append(None)
+                    continue
+                v = np.zeros(probs.shape[1])
+                v[order] = probs[r]
+                det.append(VectorUtil.toString(DenseVector(v)))
+            outs.append(Column(det))
+        if self.dist_col:
+            bd = best.to(torch.float64).cpu()
+            if nulls is not None and any(nulls):
+                outs.append(Column.from_values([None if nl else float(v) for v, nl in zip(bd.tolist(), nulls)],
+                                               Types.DOUBLE))
+            else:
+                outs.append(Column(bd))
+        return outs

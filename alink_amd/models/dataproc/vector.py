@@ -1,0 +1,205 @@
+"""Vector mappers: VectorAssembler, VectorNormalize, VectorSlice, VectorElementwiseProduct, VectorInteraction,
+VectorPolynomialExpand, VectorSizeHint, VectorToColumns, VectorSerialize.
+
+Reference: ``A/operator/common/dataproc/vector/*Mapper.java``.  ``VectorAssemblerMapper.java:50-106``
+assembles numbers/vectors/vector strings into a SparseVector that is densified when ``nnz * 1.5 > size``;
+null inputs follow ``handleInvalid`` (ERROR raises, SKIP -> null output, otherwise ignored).
+The batched path concatenates numeric / dense-block columns directly on the device (K24).
+"""
+from __future__ import annotations
+
+import itertools
+from typing import List
+
+import numpy as np
+import torch
+
+from ...common.linalg import DenseVector, SparseVector, Vector, VectorUtil
+from ...common.mapper import Mapper, MISOMapper, OutputColsHelper, SISOMapper, find_col_index, find_col_indices
+from ...common.table import Column, MTable
+from ...common.types import Types, is_numeric
+
+RATIO = 1.5
+
+
+def _append(vec: Vector, items: dict, pos: int) -> int:
+    if isinstance(vec, SparseVector):
+        for i, v in zip(vec.indices, vec.values):
+            items[pos + int(i)] = float(v)
+        return pos + vec.size()
+    for j in range(vec.size()):
+        items[pos + j] = float(vec.data[j])
+    return pos + vec.size()
+
+
+class VectorAssemblerMapper(MISOMapper):
+    def outputType(self):
+        return Types.VECTOR
+
+    def __init__(self, dataSchema, params=None):
+        super().__init__(dataSchema, params)
+        hi = self.params.get("handleInvalid") if self.params.contains("handleInvalid") else \
+            (self.params.get("handleInvalidMethod") if self.params.contains("handleInvalidMethod") else "ERROR")
+        self.handle = str(hi).upper().split(".")[-1]
+
+    def mapColumns(self, vals):
+        pos = 0
+        items = {}
+        for col in vals:
+            if col is None:
+                if self.handle == "ERROR":
+                    raise ValueError("null value is found in vector assembler inputs.")
+                if self.handle == "SKIP":
+                    return None
+                continue
+            if isinstance(col, bool):
+                items[pos] = float(col)
+                pos += 1
+            elif isinstance(col, (int, float, np.integer, np.floating)):
+                items[pos] = float(col)
+                pos += 1
+            elif isinstance(col, str):
+                pos = _append(VectorUtil.getVector(col), items, pos)
+            elif isinstance(col, Vector):
+                pos = _append(col, items, pos)
+            else:
+                raise TypeError("not support type of object.")
+        sv = SparseVector(pos, items)
+        if len(items) * RATIO > pos:
+            return sv.toDenseVector()
+        return sv
+
+    def _map_columns(self, mt: MTable):
+        cols = [mt.cols[i] for i in self.col_idx]
+        fast = all(isinstance(c.values, torch.Tensor) and c.nulls is None for c in cols)
+        if fast and cols:
+            dev = cols[0].values.device
+            parts = [(c.values.to(dev).reshape(c.values.shape[0], -1)) for c in cols]
+            dt = torch.float64
+            if all(p.dtype in (torch.bfloat16,) for p in parts):
+                dt = torch.bfloat16
+            elif all(p.dtype in (torch.bfloat16, torch.float32, torch.float16) for p in parts):
+                dt = torch.float32
+            return [Column(torch.cat([p.to(dt) for p in parts], 1))]
+        return super()._map_columns(mt)
+
+
+class VectorNormalizeMapper(SISOMapper):
+    def outputType(self):
+        return Types.VECTOR
+
+    def mapColumn(self, v):
+        if v is None:
+            return None
+        vec = VectorUtil.getVector(v).clone()
+        vec.normalizeEqual(float(self.params.get("p")) if self.params.contains("p") else 2.0)
+        return vec
+
+
+class VectorSliceMapper(SISOMapper):
+    def outputType(self):
+        return Types.VECTOR
+
+    def mapColumn(self, v):
+        if v is None:
+            return None
+        return VectorUtil.getVector(v).slice(self.params.get("indices"))
+
+
+class VectorElementwiseProductMapper(SISOMapper):
+    def outputType(self):
+        return Types.VECTOR
+
+    def __init__(self, dataSchema, params=None):
+        super().__init__(dataSchema, params)
+        self.scale = VectorUtil.getVector(self.params.get("scalingVector"))
+
+    def mapColumn(self, v):
+        if v is None:
+            return None
+        vec = VectorUtil.getVector(v)
+        s = self.scale.toDense().data
+        if isinstance(vec, SparseVector):
+            return SparseVector(vec.n, vec.indices.copy(), vec.values * s[vec.indices])
+        return DenseVector(vec.data * s[:vec.size()])
+
+
+class VectorInteractionMapper(MISOMapper):
+    def outputType(self):
+        return Types.VECTOR
+
+    def mapColumns(self, vals):
+        if any(v is None for v in vals):
+            return None
+        a, b = [VectorUtil.getVector(x).toDense().data for x in vals[:2]]
+        return DenseVector(np.outer(b, a).reshape(-1))
+
+
+class VectorPolynomialExpandMapper(SISOMapper):
+    def outputType(self):
+        return Types.VECTOR
+
+    def mapColumn(self, v):
+        if v is None:
+            return None
+        x = VectorUtil.getVector(v).toDense().data
+        degree = int(self.params.get("degree")) if self.params.contains("degree") else 2
+        out = []
+        n = len(x)
+        # Spark/Alink ordering: for degree expansion generate monomials in lexicographic order of exponents
+        for deg in range(1, degree + 1):
+            for comb in itertools.combinations_with_replacement(range(n), deg):
+                out.append(float(np.prod([x[i] for i in comb])))
+        return DenseVector(out)
+
+
+class VectorSizeHintMapper(SISOMapper):
+    def outputType(self):
+        return Types.VECTOR
+
+    def mapColumn(self, v):
+        if v is None:
+            hi = str(self.params.get("handleInvalid")).upper() if self.params.contains("handleInvalid") else "ERROR"
+            if "ERROR" in hi:
+                raise ValueError("Got null vector in VectorSizeHint")
+            return None
+        vec = VectorUtil.getVector(v)
+        size = self.params.get("size")
+        if vec.size() != size:
+            hi = str(self.params.get("handleInvalid")).upper() if self.params.contains("handleInvalid") else "ERROR"
+            if "ERROR" in hi:
+                raise ValueError(f"VectorSizeHint: expect size {size}, got {vec.size()}")
+            return None
+        return vec
+
+
+class VectorSerializeMapper(Mapper):
+    """Vector columns -> their string form (used before CSV/model export)."""
+
+    def __init__(self, dataSchema, params=None):
+        super().__init__(dataSchema, params)
+        from ...common.types import is_vector, TableSchema
+        self.vidx = [i for i, t in enumerate(dataSchema.types) if is_vector(t)]
+        names = [dataSchema.names[i] for i in self.vidx]
+        self.helper = OutputColsHelper(dataSchema, names, [Types.STRING] * len(names))
+
+    def _map_row_values(self, row):
+        return [None if row[i] is None else (VectorUtil.toString(row[i]) if isinstance(row[i], Vector)
+                                             else str(row[i])) for i in self.vidx]
+
+
+class VectorToColumnsMapper(Mapper):
+    def __init__(self, dataSchema, params=None):
+        super().__init__(dataSchema, params)
+        p = self.params
+        self.idx = find_col_index(dataSchema.names, p.get("selectedCol"))
+        self.outs = p.get("outputCols")
+        reserved = p.get("reservedCols") if p.contains("reservedCols") else None
+        self.helper = OutputColsHelper(dataSchema, self.outs, [Types.DOUBLE] * len(self.outs), reserved)
+
+    def _map_row_values(self, row):
+        v = row[self.idx]
+        if v is None:
+            return [None] * len(self.outs)
+        vec = VectorUtil.getVector(v)
+        return [vec.get(i) for i in range(len(self.outs))]

@@ -1,0 +1,1 @@
+from .base import AlgoOperator, BatchOperator  # noqa: F401

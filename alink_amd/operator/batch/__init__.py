@@ -1,0 +1,7 @@
+"""Batch operators."""
+from .source import *  # noqa: F401,F403
+from .sink import *  # noqa: F401,F403
+from .utils import *  # noqa: F401,F403
+from .dataproc import *  # noqa: F401,F403
+from .clustering import *  # noqa: F401,F403
+from .sql import *  # noqa: F401,F403

@@ -1,0 +1,278 @@
+"""Relational operations on (full) ``MTable``s used by the SQL-sugar operators.
+
+Reference: ``A/operator/common/sql/BatchSqlOperators.java:51-388`` (select, as, where/filter, distinct,
+orderBy with limit/offset/fetch, groupBy, inner/left/right/full joins over aliases ``a``/``b``, union(All),
+intersect(All), minus(All)).
+"""
+from __future__ import annotations
+
+from collections import Counter, OrderedDict
+from typing import Any, List, Optional, Sequence, Tuple
+
+from ....common.table import MTable, Row, infer_type
+from ....common.types import AlinkType, TableSchema, Types
+from .expr import Expr, compile_expr, parse_expr, parse_select_list, split_top_level
+
+__all__ = ["sql_select", "sql_where", "sql_as", "sql_distinct", "sql_order_by", "sql_group_by", "sql_join",
+           "sql_union", "sql_intersect", "sql_minus"]
+
+
+def _resolver(names: Sequence[str], qualifiers: Optional[dict] = None):
+    names = list(names)
+    lower = [n.lower() for n in names]
+
+    def resolve(n: str) -> int:
+        if qualifiers and "." in n:
+            q, c = n.split(".", 1)
+            if q in qualifiers:
+                off, sub = qualifiers[q]
+                if c in sub:
+                    return off + sub.index(c)
+                sl = [x.lower() for x in sub]
+                if c.lower() in sl:
+                    return off + sl.index(c.lower())
+                raise ValueError(f"Column {n} not found")
+        if n in names:
+            return names.index(n)
+        if n.lower() in lower:
+            return lower.index(n.lower())
+        if "." in n:
+            return resolve(n.split(".", 1)[1])
+        raise ValueError(f"Column '{n}' not found in table, all columns: {names}")
+    return resolve
+
+
+def _out_type(e: Expr, schema: TableSchema, vals: List[Any], resolve) -> AlinkType:
+    if e.kind == "col":
+        return schema.types[resolve(e.args[0])]
+    if e.kind == "agg" and e.args[0] == "COUNT":
+        return Types.LONG
+    if e.kind == "agg" and e.args[0] in ("MIN", "MAX", "SUM") and e.args[1] and e.args[1][0].kind == "col":
+        return schema.types[resolve(e.args[1][0].args[0])]
+    if e.kind == "cast":
+        from ....common.types import type_from_str
+        try:
+            return type_from_str(e.args[1])
+        except ValueError:
+            pass
+    if e.kind in ("cmp", "and", "or", "not", "isnull", "like", "in", "between"):
+        return Types.BOOLEAN
+    for v in vals:
+        if v is not None:
+            return infer_type(v)
+    return Types.STRING
+
+
+def _expand_star(items, schema):
+    out = []
+    for it in items:
+        if it.expr.kind == "star":
+            for n in schema.names:
+                from .expr import SelectItem
+                out.append(SelectItem(Expr("col", n), None, n))
+        else:
+            out.append(it)
+    return out
+
+
+def _names_for(items):
+    names = []
+    for i, it in enumerate(items):
+        if it.alias:
+            names.append(it.alias)
+        elif it.expr.kind == "col":
+            names.append(it.expr.args[0].split(".")[-1])
+        else:
+            names.append(f"EXPR${i}")
+    return names
+
+
+def _select_rows(rows: List[Row], schema: TableSchema, clause: str, qualifiers=None) -> Tuple[List[Row], TableSchema]:
+    items = _expand_star(parse_select_list(clause), schema)
+    resolve = _resolver(schema.names, qualifiers)
+    fns = [compile_expr(it.expr, resolve) for it in items]
+    out = [Row(tuple(f(r) for f in fns)) for r in rows]
+    names = _names_for(items)
+    types = [_out_type(it.expr, schema, [o[j] for o in out[:100]], resolve) for j, it in enumerate(items)]
+    return out, TableSchema(names, types)
+
+
+def sql_select(mt: MTable, clause: str) -> MTable:
+    items = _expand_star(parse_select_list(clause), mt.schema)
+    # pure column projection: keep native column storage (tensors stay on device)
+    if all(it.expr.kind == "col" for it in items):
+        resolve = _resolver(mt.schema.names)
+        idx = [resolve(it.expr.args[0]) for it in items]
+        names = _names_for(items)
+        return MTable(TableSchema(names, [mt.schema.types[i] for i in idx]), [mt.cols[i] for i in idx],
+                      mt.replicated)
+    rows, schema = _select_rows(mt.rows(), mt.schema, clause)
+    return MTable.from_rows(rows, schema, mt.replicated)
+
+
+def sql_as(mt: MTable, clause: str) -> MTable:
+    names = [x.strip() for x in split_top_level(clause)]
+    if len(names) != len(mt.schema.names):
+        raise ValueError("The number of alias names must equal the number of columns")
+    return mt.rename(names)
+
+
+def sql_where(mt: MTable, clause: str) -> MTable:
+    f = compile_expr(parse_expr(clause), _resolver(mt.schema.names))
+    keep = [i for i, r in enumerate(mt.rows()) if f(r) is True]
+    return mt.take(keep)
+
+
+def _key(v):
+    from ....common.linalg import Vector, VectorUtil
+    return VectorUtil.toString(v) if isinstance(v, Vector) else v
+
+
+def sql_distinct(mt: MTable) -> MTable:
+    seen = set()
+    keep = []
+    for i, r in enumerate(mt.rows()):
+        k = tuple(_key(v) for v in r)
+        if k not in seen:
+            seen.add(k)
+            keep.append(i)
+    return mt.take(keep)
+
+
+def sql_order_by(mt: MTable, clause: str, order: str = "asc", limit=None, offset=None, fetch=None) -> MTable:
+    keys = []
+    for part in split_top_level(clause):
+        toks = part.split()
+        asc = order.lower() != "desc"
+        if len(toks) > 1 and toks[-1].lower() in ("asc", "desc"):
+            asc = toks[-1].lower() == "asc"
+            part = " ".join(toks[:-1])
+        keys.append((compile_expr(parse_expr(part), _resolver(mt.schema.names)), asc))
+    rows = mt.rows()
+    idx = list(range(len(rows)))
+    for f, asc in reversed(keys):
+        vals = [f(rows[i]) for i in range(len(rows))]
+        # NULLs first in ascending order (Flink default), last in descending
+        idx.sort(key=lambda i: (vals[i] is not None, vals[i] if vals[i] is not None else 0), reverse=not asc)
+    if offset is not None and offset > 0:
+        idx = idx[offset:]
+    if fetch is not None and fetch >= 0:
+        idx = idx[:fetch]
+    if limit is not None and limit >= 0:
+        idx = idx[:limit]
+    return mt.take(idx)
+
+
+def sql_group_by(mt: MTable, by: str, select: str) -> MTable:
+    resolve = _resolver(mt.schema.names)
+    kfs = [compile_expr(parse_expr(p), resolve) for p in split_top_level(by)]
+    groups: "OrderedDict[tuple, List[Row]]" = OrderedDict()
+    for r in mt.rows():
+        k = tuple(_key(f(r)) for f in kfs)
+        groups.setdefault(k, []).append(r)
+    items = _expand_star(parse_select_list(select), mt.schema)
+    fns = [compile_expr(it.expr, resolve) for it in items]
+    out = [Row(tuple(f(g[0], g) for f in fns)) for g in groups.values()]
+    names = _names_for(items)
+    types = [_out_type(it.expr, mt.schema, [o[j] for o in out[:100]], resolve) for j, it in enumerate(items)]
+    return MTable.from_rows(out, TableSchema(names, types))
+
+
+def _split_and(e: Expr) -> List[Expr]:
+    if e.kind == "and":
+        return _split_and(e.args[0]) + _split_and(e.args[1])
+    return [e]
+
+
+def sql_join(left: MTable, right: MTable, predicate: str, select: str = "*", how: str = "inner") -> MTable:
+    ln, rn = left.schema.names, right.schema.names
+    qual = {"a": (0, ln), "b": (len(ln), rn)}
+    names = list(ln) + list(rn)
+    schema = TableSchema(names, list(left.schema.types) + list(right.schema.types))
+    resolve = _resolver(names, qual)
+    pred = parse_expr(predicate)
+    # hash join on equality conjuncts between the two sides
+    eq_l, eq_r = [], []
+    for c in _split_and(pred):
+        if c.kind == "cmp" and c.args[0] == "=" and c.args[1].kind == "col" and c.args[2].kind == "col":
+            i, j = resolve(c.args[1].args[0]), resolve(c.args[2].args[0])
+            if i < len(ln) <= j:
+                eq_l.append(i)
+                eq_r.append(j - len(ln))
+            elif j < len(ln) <= i:
+                eq_l.append(j)
+                eq_r.append(i - len(ln))
+    pf = compile_expr(pred, resolve)
+    lrows, rrows = left.rows(), right.rows()
+    nl, nr = (None,) * len(ln), (None,) * len(rn)
+    out = []
+    r_matched = [False] * len(rrows)
+    if eq_l:
+        index = {}
+        for j, r in enumerate(rrows):
+            index.setdefault(tuple(_key(r[x]) for x in eq_r), []).append(j)
+        for l in lrows:
+            cands = index.get(tuple(_key(l[x]) for x in eq_l), [])
+            hit = False
+            for j in cands:
+                row = tuple(l) + tuple(rrows[j])
+                if pf(row) is True:
+                    out.append(row)
+                    r_matched[j] = True
+                    hit = True
+            if not hit and how in ("left", "full"):
+                out.append(tuple(l) + nr)
+    else:
+        for l in lrows:
+            hit = False
+            for j, r in enumerate(rrows):
+                row = tuple(l) + tuple(r)
+                if pf(row) is True:
+                    out.append(row)
+                    r_matched[j] = True
+                    hit = True
+            if not hit and how in ("left", "full"):
+                out.append(tuple(l) + nr)
+    if how in ("right", "full"):
+        for j, r in enumerate(rrows):
+            if not r_matched[j]:
+                out.append(nl + tuple(r))
+    rows, sch = _select_rows([Row(r) for r in out], schema, select, qual)
+    return MTable.from_rows(rows, sch)
+
+
+def sql_union(a: MTable, b: MTable, all_: bool) -> MTable:
+    b2 = MTable(a.schema, b.cols, a.replicated)
+    u = MTable.concat([a, b2])
+    return u if all_ else sql_distinct(u)
+
+
+def sql_intersect(a: MTable, b: MTable, all_: bool) -> MTable:
+    cb = Counter(tuple(_key(v) for v in r) for r in b.rows())
+    keep, seen = [], set()
+    for i, r in enumerate(a.rows()):
+        k = tuple(_key(v) for v in r)
+        if cb.get(k, 0) > 0:
+            if all_:
+                cb[k] -= 1
+                keep.append(i)
+            elif k not in seen:
+                seen.add(k)
+                keep.append(i)
+    return a.take(keep)
+
+
+def sql_minus(a: MTable, b: MTable, all_: bool) -> MTable:
+    cb = Counter(tuple(_key(v) for v in r) for r in b.rows())
+    keep, seen = [], set()
+    for i, r in enumerate(a.rows()):
+        k = tuple(_key(v) for v in r)
+        if all_:
+            if cb.get(k, 0) > 0:
+                cb[k] -= 1
+            else:
+                keep.append(i)
+        elif k not in cb and k not in seen:
+            seen.add(k)
+            keep.append(i)
+    return a.take(keep)

@@ -1,0 +1,281 @@
+"""Micro-batch streaming engine: ``StreamOperator`` and the generic Map/ModelMap/FlatMap stream ops.
+
+Reference: ``A/operator/stream/StreamOperator.java:37-389`` (Flink ``DataStream<Row>`` wrapper; ``link``,
+``print``, ``execute``) and ``A/operator/stream/utils/{MapStreamOp,ModelMapStreamOp,FlatMapStreamOp}.java``.
+
+Design: Flink's record-at-a-time dataflow becomes a *push-based DAG of micro-batches*.
+Each operator receives ``MTable`` micro-batches on an input port and emits micro-batches to its
+subscribers; ``StreamOperator.execute()`` drives every source of the environment to exhaustion, interleaving
+sources round-robin (a deterministic stand-in for Flink's asynchronous arrival order).  Model streams
+(FTRL snapshots) are just another input port, so predictors hot-swap models between micro-batches.
+Micro-batches keep tensors on the rank's device, so the per-batch math runs on the GPU.
+"""
+from __future__ import annotations
+
+import sys
+from typing import Callable, Dict, Iterator, List, Optional
+
+from ...common.mapper import FlatMapper, Mapper, ModelMapper
+from ...common.mlenv import MLEnvironmentFactory
+from ...common.params import ParamInfo, Params
+from ...common.table import MTable, Row
+from ...common.types import TableSchema
+from ..base import AlgoOperator, format_rows, format_title, _fmt_val
+
+__all__ = ["StreamOperator", "StreamSourceOp", "MapStreamOp", "ModelMapStreamOp", "FlatMapStreamOp",
+           "StreamEngine"]
+
+
+class StreamEngine:
+    """Per-environment registry of stream sources and sinks."""
+
+    def __init__(self):
+        self.sources: List["StreamSourceOp"] = []
+        self.sinks: List["StreamOperator"] = []
+
+    def register_source(self, src):
+        if src not in self.sources:
+            self.sources.append(src)
+
+    def register_sink(self, op):
+        if op not in self.sinks:
+            self.sinks.append(op)
+
+    def run(self):
+        its = [(s, s.batches()) for s in self.sources if s._subscribers]
+        active = list(its)
+        while active:
+            nxt = []
+            for src, it in active:
+                try:
+                    mt = next(it)
+                except StopIteration:
+                    src._finish()
+                    continue
+                src._emit(mt)
+                nxt.append((src, it))
+            active = nxt
+        for s in self.sinks:
+            s._close()
+        self.sources.clear()
+        self.sinks.clear()
+
+
+def _engine(env) -> StreamEngine:
+    e = getattr(env, "_stream_engine", None)
+    if e is None:
+        e = StreamEngine()
+        env._stream_engine = e
+    return e
+
+
+class StreamOperator(AlgoOperator):
+    """A node of the micro-batch DAG.  Subclasses implement ``on_batch(port, mt)`` (and optionally
+    ``on_finish(port)``) and call ``self._emit(mt)``; ``linkFrom`` wires ports and sets the output schema."""
+
+    def __init__(self, params: Optional[Params] = None, **kw):
+        super().__init__(params, **kw)
+        self._subscribers: List[tuple] = []  # (op, port)
+        self._schema: Optional[TableSchema] = None
+        self._n_inputs = 0
+        self._finished_ports = set()
+        self._side: List["StreamOperator"] = []
+
+    # ---- wiring ----
+    def link(self, nxt: "StreamOperator"):
+        nxt.linkFrom(self)
+        return nxt
+
+    linkTo = link
+
+    def linkFrom(self, *inputs):
+        raise NotImplementedError
+
+    def _connect(self, *inputs: "StreamOperator"):
+        if len(inputs) == 1 and isinstance(inputs[0], (list, tuple)):
+            inputs = inputs[0]
+        self._n_inputs = len(inputs)
+        self._upstreams = list(inputs)
+        for port, inp in enumerate(inputs):
+            inp._subscribers.append((self, port))
+            _register_upstream_sources(inp)
+        return inputs
+
+    def getSchema(self) -> TableSchema:
+        return self._schema
+
+    def getColNames(self):
+        return list(self._schema.names)
+
+    def getColTypes(self):
+        return list(self._schema.types)
+
+    def getOutputTable(self):
+        raise RuntimeError("stream operators have no materialised output table; use print/collect sinks")
+
+    # ---- data flow ----
+    def _emit(self, mt: MTable):
+        for op, port in self._subscribers:
+            op.on_batch(port, mt)
+
+    def on_batch(self, port: int, mt: MTable):
+        raise NotImplementedError
+
+    def on_finish(self, port: int):
+        pass
+
+    def _finish(self, port: int = 0):
+        self._finished_ports.add(port)
+        self.on_finish(port)
+        if len(self._finished_ports) >= max(1, self._n_inputs):
+            for op, p in self._subscribers:
+                op._finish(p)
+            for s in self._side:
+                for op, p in s._subscribers:
+                    op._finish(p)
+
+    def _close(self):
+        pass
+
+    def getSideOutput(self, i: int) -> "StreamOperator":
+        return self._side[i]
+
+    # ---- sinks / execution ----
+    def print(self, key: Optional[str] = None, refreshInterval: int = 0, maxLimit: int = 100):
+        from .utils import PrintStreamOp
+        self.link(PrintStreamOp().setMLEnvironmentId(self.getMLEnvironmentId()))
+        return self
+
+    def collect_to(self, box: List[Row]):
+        from .utils import CollectStreamOp
+        self.link(CollectStreamOp(box).setMLEnvironmentId(self.getMLEnvironmentId()))
+        return self
+
+    @staticmethod
+    def execute(env=None):
+        env = env or MLEnvironmentFactory.getDefault()
+        _engine(env).run()
+
+    def select(self, fields):
+        from .sql import SelectStreamOp
+        if isinstance(fields, (list, tuple)):
+            fields = ",".join(fields)
+        return self.link(SelectStreamOp().setClause(fields))
+
+    def where(self, predicate: str):
+        from .sql import WhereStreamOp
+        return self.link(WhereStreamOp().setClause(predicate))
+
+    filter = where
+
+    def alias(self, fields):
+        from .sql import AsStreamOp
+        if isinstance(fields, (list, tuple)):
+            fields = ",".join(fields)
+        return self.link(AsStreamOp().setClause(fields))
+
+    def unionAll(self, other):
+        from .sql import UnionAllStreamOp
+        return UnionAllStreamOp().linkFrom(self, other)
+
+    def sample(self, ratio: float):
+        from .dataproc import SampleStreamOp
+        return self.link(SampleStreamOp().setRatio(ratio))
+
+
+class StreamSourceOp(StreamOperator):
+    """Base of stream sources: ``batches()`` yields micro-batches for this rank."""
+    _NO_AUTO_PARAMS = False
+    BATCH_SIZE = 1024
+
+    def linkFrom(self, *inputs):
+        raise RuntimeError("Source operator does not support linkFrom()")
+
+    def batches(self) -> Iterator[MTable]:
+        raise NotImplementedError
+
+    def _emit(self, mt):
+        super()._emit(mt)
+
+    def link(self, nxt):
+        _engine(self.env).register_source(self)
+        return super().link(nxt)
+
+    def _ensure_registered(self):
+        _engine(self.env).register_source(self)
+
+
+class MapStreamOp(StreamOperator):
+    MAPPER: Callable[..., Mapper] = None
+
+    def __init__(self, params: Optional[Params] = None, mapper=None, **kw):
+        super().__init__(params, **kw)
+        if mapper is not None:
+            self.MAPPER = mapper
+
+    def linkFrom(self, *inputs):
+        (inp,) = self._connect(*inputs)
+        self._mapper = self.MAPPER(inp.getSchema(), self.getParams())
+        self._mapper.open()
+        self._schema = self._mapper.getOutputSchema()
+        _register_upstream_sources(inp)
+        return self
+
+    def on_batch(self, port, mt):
+        self._emit(self._mapper.map_table(mt))
+
+
+class ModelMapStreamOp(StreamOperator):
+    """Stream predict with a static model (reference ``ModelMapStreamOp.java:39-56``)."""
+    MAPPER: Callable[..., ModelMapper] = None
+
+    def __init__(self, model=None, params: Optional[Params] = None, mapper=None, **kw):
+        if isinstance(model, Params):
+            model, params = None, model
+        super().__init__(params, **kw)
+        self._model_op = model
+        if mapper is not None:
+            self.MAPPER = mapper
+
+    def linkFrom(self, *inputs):
+        (inp,) = self._connect(*inputs)
+        from ..batch.utils import load_model_mapper
+        self._mapper = load_model_mapper(self.MAPPER, self._model_op.getOutputTable(), inp.getSchema(),
+                                         self.getParams())
+        self._schema = self._mapper.getOutputSchema()
+        _register_upstream_sources(inp)
+        return self
+
+    def on_batch(self, port, mt):
+        self._emit(self._mapper.map_table(mt))
+
+
+class FlatMapStreamOp(StreamOperator):
+    MAPPER: Callable[..., FlatMapper] = None
+
+    def __init__(self, params: Optional[Params] = None, mapper=None, **kw):
+        super().__init__(params, **kw)
+        if mapper is not None:
+            self.MAPPER = mapper
+
+    def linkFrom(self, *inputs):
+        (inp,) = self._connect(*inputs)
+        self._mapper = self.MAPPER(inp.getSchema(), self.getParams())
+        self._schema = self._mapper.getOutputSchema()
+        _register_upstream_sources(inp)
+        return self
+
+    def on_batch(self, port, mt):
+        self._emit(self._mapper.flat_map_table(mt))
+
+
+def _register_upstream_sources(op: StreamOperator, seen=None):
+    """Make sure every source feeding ``op`` is registered with the engine."""
+    seen = seen if seen is not None else set()
+    if id(op) in seen:
+        return
+    seen.add(id(op))
+    if isinstance(op, StreamSourceOp):
+        op._ensure_registered()
+    for up in getattr(op, "_upstreams", []):
+        _register_upstream_sources(up, seen)

@@ -37,6 +37,8 @@ def _load():
     c_i64, c_int, c_vp = ctypes.c_int64, ctypes.c_int, ctypes.c_void_p
     L.alink_kmeans_assign_accum_bf16.argtypes = [c_vp, c_i64, c_vp, c_vp, c_int, c_vp, c_vp, c_int, c_vp]
     L.alink_kmeans_assign_accum_bf16.restype = c_int
+    L.alink_kmeans_assign_accum_bf16_v2.argtypes = [c_vp, c_i64, c_vp, c_vp, c_int, c_vp, c_vp, c_int, c_vp]
+    L.alink_kmeans_assign_accum_bf16_v2.restype = c_int
     L.alink_kmeans_reduce_slabs.argtypes = [c_vp, c_vp, c_int, c_int, c_vp, c_vp]
     L.alink_kmeans_reduce_slabs.restype = c_int
     for name, argtypes in _EXTRA_SIGNATURES.items():

@@ -260,6 +260,219 @@ __global__ __launch_bounds__(256, 1) void kmeans_assign_accum_kernel(
     }
 }
 
+// ---------------------------------------------------------------------------------------------------
+// v2: role-split producer/consumer pipeline, 8 waves (2 per SIMD), ONE barrier per tile.
+//   waves 0-3 ("D"): distance GEMM + argmax + mask build for tile i (rows 32w..32w+31)
+//   waves 4-7 ("A"): one-hot accumulation of tile i-1 (centroid block w-4)
+// so each SIMD co-schedules one matrix-heavy distance wave with one accumulation wave, and VALU
+// (argmax), LDS reads and MFMA of the two roles overlap.  X ring: 4 x 32 KiB (tile i-1 still read by
+// the A-waves while tiles i+1, i+2 land); masks: 3 rotating buffers.
+// ---------------------------------------------------------------------------------------------------
+constexpr int V2_NBUF = 4;
+constexpr int V2_AHEAD = 2;                              // tiles in flight beyond the current one
+constexpr int V2_GLDS = TILE_BYTES / (512 * 16);         // 4 per thread per tile
+constexpr int V2_OFF_X = 0;
+constexpr int V2_OFF_LUT = V2_NBUF * TILE_BYTES;
+constexpr int V2_OFF_MASK = V2_OFF_LUT + 256 * 16;       // [3][128][4] u32
+constexpr int V2_OFF_NINIT = V2_OFF_MASK + 3 * 128 * 16;
+constexpr int V2_LDS_BYTES = V2_OFF_NINIT + 128 * 4;
+
+__device__ __forceinline__ void v2_stage_tile(char* lds, int buf, const char* X, int64_t row0, int64_t N,
+                                              int tid, int wave) {
+    char* dst_base = lds + V2_OFF_X + buf * TILE_BYTES;
+#pragma unroll
+    for (int i = 0; i < V2_GLDS; ++i) {
+        const int p = i * 8192 + tid * 16;
+        const int row = p >> 8;
+        const int chp = (p >> 4) & 15;
+        const int chl = chp ^ (((row & 3) << 2) | ((row >> 2) & 3));
+        int64_t grow = row0 + row;
+        grow = grow < N ? grow : (N - 1);
+        const char* src = X + grow * ROWB + chl * 16;
+        const uint32_t m0v = __builtin_amdgcn_readfirstlane(
+            (uint32_t)(uintptr_t)LDS_PTR(dst_base + i * 8192 + wave * 1024));
+        uint32_t keep;
+        asm volatile(
+            "s_mov_b32 %0, m0\n\t"
+            "s_mov_b32 m0, %2\n\t"
+            "s_nop 0\n\t"
+            "global_load_lds_dwordx4 %1, off\n\t"
+            "s_mov_b32 m0, %0"
+            : "=&s"(keep)
+            : "v"(src), "s"(m0v)
+            : "memory");
+    }
+}
+
+__device__ __forceinline__ void v2_wait(int ahead) {
+    if (ahead >= 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <int KB>
+__global__ __launch_bounds__(512, 2) void kmeans_assign_accum_v2_kernel(
+    const __bf16* __restrict__ Xp, int64_t N, const __bf16* __restrict__ Cp, const float* __restrict__ ninit,
+    float* __restrict__ slab, float* __restrict__ slab_cnt, int64_t ntiles) {
+    __shared__ __attribute__((aligned(16))) char lds[V2_LDS_BYTES];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int h = lane >> 5;
+    const int l32 = lane & 31;
+    const bool is_d = wave < 4;
+    const int wr = wave & 3;                     // row group (D) / centroid block (A)
+    const char* X = reinterpret_cast<const char*>(Xp);
+    const int64_t G = gridDim.x;
+    const int64_t my_ntiles = (ntiles > (int64_t)blockIdx.x) ? (ntiles - 1 - blockIdx.x) / G + 1 : 0;
+
+    for (int s = 0; s < V2_AHEAD; ++s)
+        if (s < my_ntiles) v2_stage_tile(lds, s, X, ((int64_t)blockIdx.x + s * G) * TR, N, tid, wave);
+    {
+        uint32_t* lut = reinterpret_cast<uint32_t*>(lds + V2_OFF_LUT);
+        for (int e = tid; e < 256 * 4; e += 512) {
+            const int ent = e >> 2, pair = e & 3;
+            const uint32_t b0 = (ent >> (2 * pair)) & 1, b1 = (ent >> (2 * pair + 1)) & 1;
+            lut[e] = (b0 ? 0x3F80u : 0u) | (b1 ? 0x3F800000u : 0u);
+        }
+        uint32_t* m = reinterpret_cast<uint32_t*>(lds + V2_OFF_MASK);
+        for (int e = tid; e < 3 * 128 * 4; e += 512) m[e] = 0u;
+        float* ni = reinterpret_cast<float*>(lds + V2_OFF_NINIT);
+        if (tid < 128) ni[tid] = ninit[tid];
+    }
+    bf16x8 cf[KB][8];
+    if (is_d) {
+#pragma unroll
+        for (int b = 0; b < KB; ++b)
+#pragma unroll
+            for (int s = 0; s < 8; ++s)
+                cf[b][s] = *reinterpret_cast<const bf16x8*>(Cp + (32 * b + l32) * D + 16 * s + 8 * h);
+#pragma unroll
+        for (int b = 0; b < KB; ++b)
+#pragma unroll
+            for (int s = 0; s < 8; ++s) asm volatile("" ::"v"(cf[b][s]));
+    }
+    // one accumulator set per wave, role-dependent: D-waves re-initialise it per tile (distance scores),
+    // A-waves keep it for the whole kernel (per-centroid-block sums) -> no duplicated register budget
+    f32x16 acc[4];
+#pragma unroll
+    for (int db = 0; db < 4; ++db)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[db][r] = 0.f;
+    float cnt = 0.f;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+
+    // iteration i: D-waves on tile i (if i < my_ntiles), A-waves on tile i-1 (if i >= 1)
+    for (int64_t i = 0; i <= my_ntiles; ++i) {
+        // X(i) was issued two iterations ago; X(i+1) (if any) may stay in flight
+        v2_wait((i + 1 < my_ntiles) ? 1 : 0);
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        // every wave has left iteration i-1, so buffer (i+2)%4 (tile i-2) is free: refill it
+        if (i + V2_AHEAD < my_ntiles)
+            v2_stage_tile(lds, (int)((i + V2_AHEAD) % V2_NBUF), X,
+                          ((int64_t)blockIdx.x + (i + V2_AHEAD) * G) * TR, N, tid, wave);
+
+        if (is_d) {
+            if (i < my_ntiles) {
+                const char* xb = lds + V2_OFF_X + (int)(i % V2_NBUF) * TILE_BYTES;
+                uint32_t* mcur = reinterpret_cast<uint32_t*>(lds + V2_OFF_MASK + (int)(i % 3) * 128 * 16);
+                const float* ni = reinterpret_cast<const float*>(lds + V2_OFF_NINIT);
+#pragma unroll
+                for (int b = 0; b < KB; ++b)
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) {
+                        const f32x4 v = *reinterpret_cast<const f32x4*>(ni + 32 * b + 8 * g + 4 * h);
+                        acc[b][4 * g + 0] = v[0];
+                        acc[b][4 * g + 1] = v[1];
+                        acc[b][4 * g + 2] = v[2];
+                        acc[b][4 * g + 3] = v[3];
+                    }
+                const int myrow = 32 * wr + l32;
+#pragma unroll
+                for (int s = 0; s < 8; ++s) {
+                    const bf16x8 xv = *reinterpret_cast<const bf16x8*>(xb + xoff(myrow, 2 * s + h));
+#pragma unroll
+                    for (int b = 0; b < KB; ++b)
+                        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cf[b][s], xv, acc[b], 0, 0, 0);
+                }
+                float best = -3.0e38f;
+#pragma unroll
+                for (int b = 0; b < KB; ++b)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const uint32_t c = 32 * b + (r & 3) + 8 * (r >> 2) + 4 * h;
+                        best = fmaxf(best, __uint_as_float((__float_as_uint(acc[b][r]) & 0xFFFFFF80u) | c));
+                    }
+                best = fmaxf(best, __shfl_xor(best, 32));
+                const int64_t grow = ((int64_t)blockIdx.x + i * G) * TR + myrow;
+                if (h == 0 && grow < N) {
+                    const uint32_t c = __float_as_uint(best) & 127u;
+                    __hip_atomic_fetch_or(mcur + c * 4 + (myrow >> 5), 1u << (myrow & 31), __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+            }
+        } else {
+            // clear masks of tile i-2 (read by the A-waves in iteration i-1) for tile i+1
+            uint32_t* mclr = reinterpret_cast<uint32_t*>(lds + V2_OFF_MASK + (int)((i + 1) % 3) * 128 * 16);
+            mclr[tid - 256] = 0u;
+            mclr[tid] = 0u;  // tid in [256,512): covers words 256..511
+            if (i >= 1 && wr < KB) {
+                const int64_t j = i - 1;
+                const char* xb = lds + V2_OFF_X + (int)(j % V2_NBUF) * TILE_BYTES;
+                const uint32_t* mprev =
+                    reinterpret_cast<const uint32_t*>(lds + V2_OFF_MASK + (int)(j % 3) * 128 * 16);
+                const u32x4 mw = *reinterpret_cast<const u32x4*>(mprev + (32 * wr + l32) * 4);
+                if (h == 0) cnt += (float)(__popc(mw[0]) + __popc(mw[1]) + __popc(mw[2]) + __popc(mw[3]));
+                // per-lane tr-read bases: rows 8(g>>1)+q (+4 for the upper half) of k-step 0, chunk group db;
+                // k-step s adds s*4096 B (16 rows; the swizzle depends on row & 15 only) -> immediate offsets
+                const int g = lane >> 4, i16 = lane & 15, q = i16 >> 2, p = i16 & 3;
+                int tb_lo[4], tb_hi[4];
+#pragma unroll
+                for (int db = 0; db < 4; ++db) {
+                    const int ch = 4 * db + 2 * (g & 1) + (p >> 1);
+                    tb_lo[db] = (int)(uintptr_t)LDS_PTR(xb) + xoff(8 * (g >> 1) + q, ch) + 8 * (p & 1);
+                    tb_hi[db] = (int)(uintptr_t)LDS_PTR(xb) + xoff(8 * (g >> 1) + q + 4, ch) + 8 * (p & 1);
+                }
+#pragma unroll
+                for (int s = 0; s < 8; ++s) {
+                    const uint32_t word = mw[s >> 1];
+                    const uint32_t byte = (word >> (16 * (s & 1) + 8 * h)) & 255u;
+                    const bf16x8 a = *reinterpret_cast<const bf16x8*>(lds + V2_OFF_LUT + byte * 16);
+#pragma unroll
+                    for (int db = 0; db < 4; ++db) {
+                        const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+                            (__attribute__((address_space(3))) bf16x4*)(uintptr_t)(tb_lo[db] + s * 4096));
+                        const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+                            (__attribute__((address_space(3))) bf16x4*)(uintptr_t)(tb_hi[db] + s * 4096));
+                        const bf16x8 bv = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                        acc[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bv, acc[db], 0, 0, 0);
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+
+    float* S = slab + (int64_t)blockIdx.x * 128 * D;
+    if (!is_d) {
+        if (wr < KB) {
+#pragma unroll
+            for (int db = 0; db < 4; ++db)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int c = 32 * wr + (r & 3) + 8 * (r >> 2) + 4 * h;
+                    S[c * D + 32 * db + l32] = acc[db][r];
+                }
+            if (h == 0) slab_cnt[(int64_t)blockIdx.x * 128 + 32 * wr + l32] = cnt;
+        } else {
+            for (int e = lane; e < 32 * D; e += 64) S[(32 * wr) * D + e] = 0.f;
+            if (h == 0) slab_cnt[(int64_t)blockIdx.x * 128 + 32 * wr + l32] = 0.f;
+        }
+    }
+}
+
 // fixed-order fp64 reduction of the per-workgroup slabs -> out[k][D+1] (last column = count)
 __global__ void kmeans_reduce_slabs_kernel(const float* __restrict__ slab, const float* __restrict__ slab_cnt,
                                            int nslab, int k, double* __restrict__ out) {
@@ -300,6 +513,26 @@ int alink_kmeans_assign_accum_bf16(const void* X, int64_t N, const void* C, cons
         default: hipLaunchKernelGGL(kmeans_assign_accum_kernel<4>, dim3(grid), dim3(256), 0, st,
                                     (const __bf16*)X, N, (const __bf16*)C, ninit, slab, slab_cnt, ntiles); break;
     }
+    return (int)hipGetLastError();
+}
+
+int alink_kmeans_assign_accum_bf16_v2(const void* X, int64_t N, const void* C, const float* ninit, int k,
+                                      float* slab, float* slab_cnt, int grid, void* stream) {
+    if (N <= 0 || k < 1 || k > 128 || grid <= 0) return -1;
+    const int KB = (k + 31) / 32;
+    const int64_t ntiles = (N + TR - 1) / TR;
+    if (grid > ntiles) grid = (int)ntiles;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+#define V2_LAUNCH(KBV)                                                                                   \
+    hipLaunchKernelGGL(kmeans_assign_accum_v2_kernel<KBV>, dim3(grid), dim3(512), 0, st, (const __bf16*)X, N, \
+                       (const __bf16*)C, ninit, slab, slab_cnt, ntiles)
+    switch (KB) {
+        case 1: V2_LAUNCH(1); break;
+        case 2: V2_LAUNCH(2); break;
+        case 3: V2_LAUNCH(3); break;
+        default: V2_LAUNCH(4); break;
+    }
+#undef V2_LAUNCH
     return (int)hipGetLastError();
 }
 

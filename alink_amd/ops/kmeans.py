@@ -44,7 +44,8 @@ def _num_cus(device) -> int:
     return torch.cuda.get_device_properties(device).multi_processor_count
 
 
-def assign_accumulate_hip(X: torch.Tensor, C: torch.Tensor, grid: Optional[int] = None) -> torch.Tensor:
+def assign_accumulate_hip(X: torch.Tensor, C: torch.Tensor, grid: Optional[int] = None,
+                          variant: int = 1) -> torch.Tensor:
     L = _lib.require()
     dev = X.device
     k = C.shape[0]
@@ -63,8 +64,8 @@ def assign_accumulate_hip(X: torch.Tensor, C: torch.Tensor, grid: Optional[int] 
     slab, slab_cnt = _BUF[key]
     out = torch.empty((k, HIP_D + 1), dtype=torch.float64, device=dev)
     st = _lib.stream_ptr(dev)
-    rc = L.alink_kmeans_assign_accum_bf16(X.data_ptr(), n, cpad.data_ptr(), ninit.data_ptr(), k,
-                                          slab.data_ptr(), slab_cnt.data_ptr(), grid, st)
+    fn = L.alink_kmeans_assign_accum_bf16 if variant == 1 else L.alink_kmeans_assign_accum_bf16_v2
+    rc = fn(X.data_ptr(), n, cpad.data_ptr(), ninit.data_ptr(), k, slab.data_ptr(), slab_cnt.data_ptr(), grid, st)
     if rc != 0:
         raise RuntimeError(f"alink_kmeans_assign_accum_bf16 failed: {rc}")
     rc = L.alink_kmeans_reduce_slabs(slab.data_ptr(), slab_cnt.data_ptr(), grid, k, out.data_ptr(), st)

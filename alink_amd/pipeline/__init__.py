@@ -1,0 +1,4 @@
+"""Pipeline API and stages."""
+from .base import *  # noqa: F401,F403
+from .clustering import *  # noqa: F401,F403
+from .dataproc import *  # noqa: F401,F403

@@ -1,0 +1,125 @@
+#!/usr/bin/env python3
+"""Headline benchmark: KMeans k=100 on 1e8 synthetic rows x 128 dims (bf16), data-parallel over N MI355X.
+
+Metric (BASELINE.json): rows/sec/node + iterations-to-converge.  One *step* = one Lloyd superstep of the
+framework's ``KMeansTrainBatchOp`` BSP queue: fused HIP assign+accumulate over this rank's rows, RCCL
+all-reduce of the [k, d+1] sums, centroid update and the convergence criterion.  The 1e8-row table is fixed
+(strong scaling: each of N ranks holds 1e8/N rows, generated on its own GPU).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--rows R] [--k 100] [--dims 128]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+
+Prints ONE JSON line on rank 0.  ``value`` = total rows processed per second by the whole job
+(rows x K / max-over-ranks elapsed).  Also reports ``iters_to_converge`` from a separate untimed run with
+the reference defaults (epsilon 1e-4, k-means|| init with initSteps 2).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+import torch  # noqa: E402
+
+METRIC = "rows/sec/node + iters-to-converge, KMeans k=100 1e8-row×128-dim at 1/2/4/8 MI355X"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--rows", type=int, default=100_000_000)
+    ap.add_argument("--k", type=int, default=100)
+    ap.add_argument("--dims", type=int, default=128)
+    ap.add_argument("--converge-iters", type=int, default=100, help="maxIter of the convergence run (0 = skip)")
+    a = ap.parse_args()
+
+    from alink_amd import useLocalEnv, KMeansTrainBatchOp, RandomVectorSourceBatchOp
+    from alink_amd.parallel import comm
+    from alink_amd.ops import _lib
+
+    env = useLocalEnv(1)
+    if env.world_size != a.gpus and env.rank == 0:
+        print(f"[bench] warning: --gpus {a.gpus} but WORLD_SIZE={env.world_size}", file=sys.stderr)
+    dev = env.device
+    if dev.type == "cuda":
+        _lib.require()
+
+    src = RandomVectorSourceBatchOp().setNumRows(a.rows).setSize(a.dims).setNumClusters(a.k) \
+        .setClusterStd(1.0).setCenterScale(4.0).setDtype("bf16").setSeed(2024).setOutputCol("vec")
+    t_gen = time.perf_counter()
+    data = src.getOutputTable()
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    t_gen = time.perf_counter() - t_gen
+
+    # ---- timed run: W warmup supersteps + exactly K timed supersteps (no early convergence) ----
+    marks = {}
+
+    def on_step(step, q):
+        if step == a.warmup or step == a.warmup + a.steps:
+            if dev.type == "cuda":
+                torch.cuda.synchronize(dev)
+            comm.barrier()
+            if dev.type == "cuda":
+                torch.cuda.synchronize(dev)
+            marks[step] = time.perf_counter()
+
+    op = KMeansTrainBatchOp().setVectorCol("vec").setK(a.k).setMaxIter(a.warmup + a.steps).setEpsilon(-1.0)
+    op._on_step = on_step
+    from alink_amd.operator.batch.source import TableSourceBatchOp
+    t_tot = time.perf_counter()
+    op.linkFrom(TableSourceBatchOp(data))
+    t_tot = time.perf_counter() - t_tot
+    if a.warmup == 0:
+        raise SystemExit("--warmup must be >= 1 (the first superstep includes one-time setup)")
+    elapsed = marks[a.warmup + a.steps] - marks[a.warmup]
+    el = torch.tensor([elapsed], dtype=torch.float64)
+    comm.all_reduce(el, "max")
+    elapsed = float(el.item())
+    stats = op._queue.stats[a.warmup:a.warmup + a.steps]
+    comm_bytes = sum(s["comm_bytes"] for s in stats) / max(1, len(stats))
+
+    # ---- convergence run (reference defaults: epsilon 1e-4, k-means|| initSteps 2) ----
+    iters = None
+    if a.converge_iters > 0:
+        op2 = KMeansTrainBatchOp().setVectorCol("vec").setK(a.k).setMaxIter(a.converge_iters)
+        op2.linkFrom(TableSourceBatchOp(data))
+        iters = op2.getTrainInfo()["iterations"]
+
+    rows_per_s = a.rows * a.steps / elapsed
+    res = {
+        "metric": METRIC,
+        "value": rows_per_s,
+        "unit": "rows/s",
+        "n_gpus": env.world_size,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": elapsed / a.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "bf16",
+        "data": "synthetic (Gaussian mixture, 100 components, generated on-device)",
+        "config": {"model": "KMeans k=100 (Lloyd, EUCLIDEAN, k-means|| init)", "global_batch": a.rows,
+                   "seq_len": a.dims, "rows": a.rows, "dims": a.dims, "k": a.k,
+                   "parallelism": f"dp{env.world_size}"},
+        "rows_per_s_per_gpu": rows_per_s / env.world_size,
+        "iters_to_converge": iters,
+        "allreduce_bytes_per_step": comm_bytes,
+        "hip_kernels": _lib.available(),
+        "datagen_s": t_gen,
+        "train_wall_s": t_tot,
+    }
+    if env.rank == 0:
+        print(json.dumps(res), flush=True)
+    comm.shutdown()
+
+
+if __name__ == "__main__":
+    main()
