@@ -21,6 +21,7 @@
 //   (zero rows beyond k), ninit[128] (-|c|^2/2 for c < k, -3e38 for padding).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <type_traits>
 
 namespace {
 
@@ -473,6 +474,730 @@ __global__ __launch_bounds__(512, 2) void kmeans_assign_accum_v2_kernel(
     }
 }
 
+// ---------------------------------------------------------------------------------------------------
+// v3: register-lean 3-stage pipeline for any k <= 128, 8 waves (2 per SIMD), 64-row tiles, one barrier
+// per tile.  Iteration i:
+//   D-waves (0-3): wave w -> rows 32*(w&1)..+31 of tile i vs centroid blocks {2(w>>1), 2(w>>1)+1}
+//                  (64 centroids, 64 VGPRs of fragments); per-row partial argmax -> pbest[i&1][w>>1][row]
+//   A-waves (4-7): (a) combine the two partials of tile i-1 -> per-centroid row masks (ds_or_b32)
+//                  (b) one-hot MFMA accumulation of tile i-2 for centroid block (w-4)
+// LDS: 6 x 16 KiB X ring (3 tiles in flight), 3 mask sets, 2 pbest sets, LUT, -|c|^2/2.
+// ---------------------------------------------------------------------------------------------------
+constexpr int V3_TR = 64;
+constexpr int V3_TILE = V3_TR * ROWB;                      // 16 KiB
+constexpr int V3_NBUF = 6;
+constexpr int V3_AHEAD = 3;
+constexpr int V3_GLDS = V3_TILE / (512 * 16);             // 2 per thread per tile
+constexpr int V3_OFF_LUT = V3_NBUF * V3_TILE;
+constexpr int V3_OFF_MASK = V3_OFF_LUT + 256 * 16;        // [3][128 c][2 words]
+constexpr int V3_OFF_PBEST = V3_OFF_MASK + 3 * 128 * 8;   // [2][2 halves][64 rows] f32
+constexpr int V3_OFF_NINIT = V3_OFF_PBEST + 2 * 2 * 64 * 4;
+constexpr int V3_OFF_C = V3_OFF_NINIT + 128 * 4;         // [128 c][128 d] bf16, swizzled like X
+constexpr int V3_LDS_BYTES = V3_OFF_C + 128 * ROWB;
+
+__device__ __forceinline__ void v3_stage_tile(char* lds, int buf, const char* X, int64_t row0, int64_t N,
+                                              int tid, int wave) {
+    char* dst_base = lds + buf * V3_TILE;
+#pragma unroll
+    for (int i = 0; i < V3_GLDS; ++i) {
+        const int p = i * 8192 + tid * 16;
+        const int row = p >> 8;
+        const int chp = (p >> 4) & 15;
+        const int chl = chp ^ (((row & 3) << 2) | ((row >> 2) & 3));
+        int64_t grow = row0 + row;
+        grow = grow < N ? grow : (N - 1);
+        const char* src = X + grow * ROWB + chl * 16;
+        const uint32_t m0v = __builtin_amdgcn_readfirstlane(
+            (uint32_t)(uintptr_t)LDS_PTR(dst_base + i * 8192 + wave * 1024));
+        uint32_t keep;
+        asm volatile(
+            "s_mov_b32 %0, m0\n\t"
+            "s_mov_b32 m0, %2\n\t"
+            "s_nop 0\n\t"
+            "global_load_lds_dwordx4 %1, off\n\t"
+            "s_mov_b32 m0, %0"
+            : "=&s"(keep)
+            : "v"(src), "s"(m0v)
+            : "memory");
+    }
+}
+
+__device__ __forceinline__ void v3_wait(int pending_after) {
+    // pending_after = number of tiles issued after the one we need (0..2), 2 glds each
+    if (pending_after >= 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if (pending_after == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <int KB>
+__global__ __launch_bounds__(512, 2) void kmeans_assign_accum_v3_kernel(
+    const __bf16* __restrict__ Xp, int64_t N, const __bf16* __restrict__ Cp, const float* __restrict__ ninit,
+    float* __restrict__ slab, float* __restrict__ slab_cnt, int64_t ntiles) {
+    __shared__ __attribute__((aligned(16))) char lds[V3_LDS_BYTES];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int h = lane >> 5;
+    const int l32 = lane & 31;
+    const bool is_d = wave < 4;
+    const int wr = wave & 3;
+    const char* X = reinterpret_cast<const char*>(Xp);
+    const int64_t G = gridDim.x;
+    const int64_t my_ntiles = (ntiles > (int64_t)blockIdx.x) ? (ntiles - 1 - blockIdx.x) / G + 1 : 0;
+
+    for (int s = 0; s < V3_AHEAD; ++s)
+        if (s < my_ntiles) v3_stage_tile(lds, s, X, ((int64_t)blockIdx.x + s * G) * V3_TR, N, tid, wave);
+    {
+        uint32_t* lut = reinterpret_cast<uint32_t*>(lds + V3_OFF_LUT);
+        for (int e = tid; e < 256 * 4; e += 512) {
+            const int ent = e >> 2, pair = e & 3;
+            const uint32_t b0 = (ent >> (2 * pair)) & 1, b1 = (ent >> (2 * pair + 1)) & 1;
+            lut[e] = (b0 ? 0x3F80u : 0u) | (b1 ? 0x3F800000u : 0u);
+        }
+        uint32_t* m = reinterpret_cast<uint32_t*>(lds + V3_OFF_MASK);
+        for (int e = tid; e < 3 * 128 * 2; e += 512) m[e] = 0u;
+        float* ni = reinterpret_cast<float*>(lds + V3_OFF_NINIT);
+        if (tid < 128) ni[tid] = ninit[tid];
+    }
+    // centroids -> LDS (swizzled [c][d] image read by the D-waves as MFMA A operand)
+    {
+        bf16x8 cv[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int e = r * 512 + tid;  // 16-byte chunk index: row e>>4, chunk e&15
+            cv[r] = *reinterpret_cast<const bf16x8*>(Cp + (e >> 4) * D + (e & 15) * 8);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int e = r * 512 + tid;
+            *reinterpret_cast<bf16x8*>(lds + V3_OFF_C + xoff(e >> 4, e & 15)) = cv[r];
+        }
+    }
+    const int cb0 = 2 * (wr >> 1);
+    f32x16 acc[4];
+#pragma unroll
+    for (int db = 0; db < 4; ++db)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[db][r] = 0.f;
+    float cnt = 0.f;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+
+    for (int64_t i = 0; i < my_ntiles + 2; ++i) {
+        {
+            int64_t after = my_ntiles - 1 - i;  // tiles issued after tile i (at most AHEAD-1 = 2 outstanding)
+            after = after < 0 ? 0 : (after > 2 ? 2 : after);
+            v3_wait((int)after);
+        }
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (i + V3_AHEAD < my_ntiles)
+            v3_stage_tile(lds, (int)((i + V3_AHEAD) % V3_NBUF), X,
+                          ((int64_t)blockIdx.x + (i + V3_AHEAD) * G) * V3_TR, N, tid, wave);
+
+        if (is_d) {
+            if (i < my_ntiles && cb0 < KB) {
+                const char* xb = lds + (int)(i % V3_NBUF) * V3_TILE;
+                const float* ni = reinterpret_cast<const float*>(lds + V3_OFF_NINIT);
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) {
+                        const f32x4 v = *reinterpret_cast<const f32x4*>(ni + 32 * (cb0 + j) + 8 * g + 4 * h);
+                        acc[j][4 * g + 0] = v[0];
+                        acc[j][4 * g + 1] = v[1];
+                        acc[j][4 * g + 2] = v[2];
+                        acc[j][4 * g + 3] = v[3];
+                    }
+                const int myrow = 32 * (wr & 1) + l32;
+                const char* cbase = lds + V3_OFF_C;
+#pragma unroll
+                for (int s = 0; s < 8; ++s) {
+                    const bf16x8 xv = *reinterpret_cast<const bf16x8*>(xb + xoff(myrow, 2 * s + h));
+                    const bf16x8 c0 = *reinterpret_cast<const bf16x8*>(cbase + xoff(32 * cb0 + l32, 2 * s + h));
+                    acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(c0, xv, acc[0], 0, 0, 0);
+                    if (cb0 + 1 < KB) {
+                        const bf16x8 c1 =
+                            *reinterpret_cast<const bf16x8*>(cbase + xoff(32 * (cb0 + 1) + l32, 2 * s + h));
+                        acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(c1, xv, acc[1], 0, 0, 0);
+                    }
+                }
+                float best = -3.0e38f;
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    if (cb0 + j < KB) {
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) {
+                            const uint32_t c = 32 * (cb0 + j) + (r & 3) + 8 * (r >> 2) + 4 * h;
+                            best = fmaxf(best, __uint_as_float((__float_as_uint(acc[j][r]) & 0xFFFFFF80u) | c));
+                        }
+                    }
+                }
+                best = fmaxf(best, __shfl_xor(best, 32));
+                if (h == 0) {
+                    float* pb = reinterpret_cast<float*>(lds + V3_OFF_PBEST) + (int)(i & 1) * 128 + (wr >> 1) * 64;
+                    pb[myrow] = best;
+                }
+            } else if (i < my_ntiles && h == 0) {
+                float* pb = reinterpret_cast<float*>(lds + V3_OFF_PBEST) + (int)(i & 1) * 128 + (wr >> 1) * 64;
+                pb[32 * (wr & 1) + l32] = -3.0e38f;
+            }
+        } else {
+            // clear the mask set of tile i-3 (consumed in iteration i-1, rebuilt in iteration i+1)
+            {
+                uint32_t* mclr = reinterpret_cast<uint32_t*>(lds + V3_OFF_MASK + (int)(i % 3) * 128 * 8);
+                mclr[tid - 256] = 0u;
+            }
+            // (a) combine partials of tile i-1 into its masks
+            if (i >= 1 && i <= my_ntiles && wr == 0) {
+                const int64_t t = i - 1;
+                const float* pb = reinterpret_cast<const float*>(lds + V3_OFF_PBEST) + (int)(t & 1) * 128;
+                const float best = fmaxf(pb[lane], pb[64 + lane]);
+                const int64_t grow = ((int64_t)blockIdx.x + t * G) * V3_TR + lane;
+                if (grow < N) {
+                    const uint32_t c = __float_as_uint(best) & 127u;
+                    uint32_t* mt = reinterpret_cast<uint32_t*>(lds + V3_OFF_MASK + (int)(t % 3) * 128 * 8);
+                    __hip_atomic_fetch_or(mt + c * 2 + (lane >> 5), 1u << (lane & 31), __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+            }
+            // (b) accumulate tile i-2
+            if (i >= 2 && wr < KB) {
+                const int64_t t = i - 2;
+                const char* xb = lds + (int)(t % V3_NBUF) * V3_TILE;
+                const uint32_t* mprev = reinterpret_cast<const uint32_t*>(lds + V3_OFF_MASK + (int)(t % 3) * 128 * 8);
+                const uint32_t mw0 = mprev[(32 * wr + l32) * 2 + 0];
+                const uint32_t mw1 = mprev[(32 * wr + l32) * 2 + 1];
+                if (h == 0) cnt += (float)(__popc(mw0) + __popc(mw1));
+                const int g = lane >> 4, i16 = lane & 15, q = i16 >> 2, p = i16 & 3;
+                int tb_lo[4], tb_hi[4];
+#pragma unroll
+                for (int db = 0; db < 4; ++db) {
+                    const int ch = 4 * db + 2 * (g & 1) + (p >> 1);
+                    tb_lo[db] = (int)(uintptr_t)LDS_PTR(xb) + xoff(8 * (g >> 1) + q, ch) + 8 * (p & 1);
+                    tb_hi[db] = (int)(uintptr_t)LDS_PTR(xb) + xoff(8 * (g >> 1) + q + 4, ch) + 8 * (p & 1);
+                }
+#pragma unroll
+                for (int s = 0; s < 4; ++s) {
+                    const uint32_t word = (s >> 1) ? mw1 : mw0;
+                    const uint32_t byte = (word >> (16 * (s & 1) + 8 * h)) & 255u;
+                    const bf16x8 a = *reinterpret_cast<const bf16x8*>(lds + V3_OFF_LUT + byte * 16);
+#pragma unroll
+                    for (int db = 0; db < 4; ++db) {
+                        const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+                            (__attribute__((address_space(3))) bf16x4*)(uintptr_t)(tb_lo[db] + s * 4096));
+                        const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+                            (__attribute__((address_space(3))) bf16x4*)(uintptr_t)(tb_hi[db] + s * 4096));
+                        const bf16x8 bv = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                        acc[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bv, acc[db], 0, 0, 0);
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+
+    float* S = slab + (int64_t)blockIdx.x * 128 * D;
+    if (!is_d) {
+        if (wr < KB) {
+#pragma unroll
+            for (int db = 0; db < 4; ++db)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int c = 32 * wr + (r & 3) + 8 * (r >> 2) + 4 * h;
+                    S[c * D + 32 * db + l32] = acc[db][r];
+                }
+            if (h == 0) slab_cnt[(int64_t)blockIdx.x * 128 + 32 * wr + l32] = cnt;
+        } else {
+            for (int e = lane; e < 32 * D; e += 64) S[(32 * wr) * D + e] = 0.f;
+            if (h == 0) slab_cnt[(int64_t)blockIdx.x * 128 + 32 * wr + l32] = 0.f;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------------
+// v4: VALU-lean, one wave per SIMD (4 waves, up to 512 registers each), 128-row tiles, one barrier per
+// tile, software-pipelined so the argmax VALU work of tile i is issued between the one-hot MFMAs of
+// tile i-1 (profiling v1 showed 12 VALU per MFMA and VALU issue, not MFMA or HBM, bounding it):
+//   * LDS-DMA through a per-tile buffer descriptor (buffer_load ... lds): no per-lane 64-bit address math,
+//     out-of-range rows read as zero by the hardware bounds check (no clamping);
+//   * the -|c|^2/2 init lives in registers and is the C operand of the first distance MFMA (no moves);
+//   * all LDS addresses are loop-invariant VGPRs + a per-tile scalar offset;
+//   * each wave clears the mask words it consumed, so the mask ring needs no extra phase.
+// ---------------------------------------------------------------------------------------------------
+constexpr int V4_NBUF = 4;
+constexpr int V4_OFF_LUT = V4_NBUF * TILE_BYTES;          // 128 KiB of X ring
+constexpr int V4_OFF_MASK = V4_OFF_LUT + 256 * 16;        // [2][128 c][4 words]
+constexpr int V4_LDS_BYTES = V4_OFF_MASK + 2 * 128 * 16;
+
+__device__ __forceinline__ void v4_stage(char* lds, int buf, const char* X, int64_t row0, int64_t N,
+                                         const uint32_t (&voff)[8], int wave) {
+    const int64_t rem = (N - row0) * ROWB;
+    const int nbytes = rem < TILE_BYTES ? (int)rem : TILE_BYTES;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(X + row0 * ROWB), (short)0, nbytes, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const uint32_t m0v = __builtin_amdgcn_readfirstlane(
+            (uint32_t)(uintptr_t)LDS_PTR(lds + buf * TILE_BYTES + i * 4096 + wave * 1024));
+        uint32_t keep;
+        asm volatile(
+            "s_mov_b32 %0, m0\n\t"
+            "s_mov_b32 m0, %3\n\t"
+            "s_nop 0\n\t"
+            "buffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
+            "s_mov_b32 m0, %0"
+            : "=&s"(keep)
+            : "v"(voff[i]), "s"(rs), "s"(m0v)
+            : "memory");
+    }
+}
+
+template <int KB, bool DIST, bool ACC>
+__device__ __forceinline__ void v4_body(char* lds, int cur_off, int prev_off, uint32_t* mcur, uint32_t* mprev,
+                                        const bf16x8 (&cf)[KB][8], const bf16x8 (&cn)[KB], const bf16x8& ones,
+                                        const int (&xr)[8],
+                                        const int (&tbl)[4], const int (&tbh)[4], f32x16 (&sacc)[4], float& cnt,
+                                        int wave, int h, int l32, int lane, int64_t grow) {
+    f32x16 acc[KB];
+    if constexpr (DIST) {
+        // k-step "-1": the accumulator starts at -|c|^2/2 = hi + mid + lo (three bf16 parts) x ones
+#pragma unroll
+        for (int b = 0; b < KB; ++b) {
+            const f32x16 z = {};
+            acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cn[b], ones, z, 0, 0, 0);
+        }
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+            const bf16x8 xv = *reinterpret_cast<const bf16x8*>(lds + cur_off + xr[s]);
+#pragma unroll
+            for (int b = 0; b < KB; ++b)
+                acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cf[b][s], xv, acc[b], 0, 0, 0);
+        }
+    }
+    float best = -3.0e38f;
+    if constexpr (ACC) {
+        int tl[4], th[4];
+#pragma unroll
+        for (int db = 0; db < 4; ++db) {
+            tl[db] = tbl[db] + prev_off;
+            th[db] = tbh[db] + prev_off;
+        }
+        const u32x4 mw = *reinterpret_cast<const u32x4*>(mprev + (32 * wave + l32) * 4);
+        if (h == 0) {
+            cnt += (float)(__popc(mw[0]) + __popc(mw[1]) + __popc(mw[2]) + __popc(mw[3]));
+            *reinterpret_cast<u32x4*>(mprev + (32 * wave + l32) * 4) = u32x4{0u, 0u, 0u, 0u};
+        }
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+            const uint32_t byte = (mw[s >> 1] >> (16 * (s & 1) + 8 * h)) & 255u;
+            const bf16x8 a = *reinterpret_cast<const bf16x8*>(lds + V4_OFF_LUT + byte * 16);
+#pragma unroll
+            for (int db = 0; db < 4; ++db) {
+                const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+                    (__attribute__((address_space(3))) bf16x4*)(uintptr_t)(tl[db] + s * 4096));
+                const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+                    (__attribute__((address_space(3))) bf16x4*)(uintptr_t)(th[db] + s * 4096));
+                const bf16x8 bv = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                sacc[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bv, sacc[db], 0, 0, 0);
+            }
+            if constexpr (DIST) {
+                // argmax slice of the current tile, interleaved with the one-hot MFMAs of the previous one
+                constexpr int PER = (KB * 16 + 7) / 8;
+#pragma unroll
+                for (int t = 0; t < PER; ++t) {
+                    const int v = s * PER + t;
+                    if (v < KB * 16) {
+                        const int b = v >> 4, r = v & 15;
+                        const uint32_t c = 32 * b + (r & 3) + 8 * (r >> 2) + 4 * h;
+                        best = fmaxf(best, __uint_as_float((__float_as_uint(acc[b][r]) & 0xFFFFFF80u) | c));
+                    }
+                }
+            }
+        }
+    } else if constexpr (DIST) {
+#pragma unroll
+        for (int b = 0; b < KB; ++b)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const uint32_t c = 32 * b + (r & 3) + 8 * (r >> 2) + 4 * h;
+                best = fmaxf(best, __uint_as_float((__float_as_uint(acc[b][r]) & 0xFFFFFF80u) | c));
+            }
+    }
+    if constexpr (DIST) {
+        best = fmaxf(best, __shfl_xor(best, 32));
+        if (h == 0 && grow >= 0) {
+            const uint32_t c = __float_as_uint(best) & 127u;
+            const int myrow = 32 * wave + l32;
+            __hip_atomic_fetch_or(mcur + c * 4 + (myrow >> 5), 1u << (myrow & 31), __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    }
+}
+
+template <int KB>
+__global__ __launch_bounds__(256, 1) void kmeans_assign_accum_v4_kernel(
+    const __bf16* __restrict__ Xp, int64_t N, const __bf16* __restrict__ Cp, const float* __restrict__ ninit,
+    float* __restrict__ slab, float* __restrict__ slab_cnt, int64_t ntiles) {
+    __shared__ __attribute__((aligned(16))) char lds[V4_LDS_BYTES];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int h = lane >> 5;
+    const int l32 = lane & 31;
+    const char* X = reinterpret_cast<const char*>(Xp);
+    const int64_t G = gridDim.x;
+    const int64_t my_ntiles = (ntiles > (int64_t)blockIdx.x) ? (ntiles - 1 - blockIdx.x) / G + 1 : 0;
+
+    uint32_t voff[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int p = i * 4096 + tid * 16;
+        const int row = p >> 8;
+        const int chp = (p >> 4) & 15;
+        voff[i] = (uint32_t)(row * ROWB + 16 * (chp ^ (((row & 3) << 2) | ((row >> 2) & 3))));
+    }
+    for (int s = 0; s < 2; ++s)
+        if (s < my_ntiles) v4_stage(lds, s, X, ((int64_t)blockIdx.x + s * G) * TR, N, voff, wave);
+    {
+        uint32_t* lut = reinterpret_cast<uint32_t*>(lds + V4_OFF_LUT);
+        for (int e = tid; e < 256 * 4; e += 256) {
+            const int ent = e >> 2, pair = e & 3;
+            const uint32_t b0 = (ent >> (2 * pair)) & 1, b1 = (ent >> (2 * pair + 1)) & 1;
+            lut[e] = (b0 ? 0x3F80u : 0u) | (b1 ? 0x3F800000u : 0u);
+        }
+        uint32_t* m = reinterpret_cast<uint32_t*>(lds + V4_OFF_MASK);
+        for (int e = tid; e < 2 * 128 * 4; e += 256) m[e] = 0u;
+    }
+    bf16x8 cf[KB][8];
+    bf16x8 cn[KB];
+    // A operand of the norm k-step: row c = 32b + l32, k = 8h + j: three bf16 parts of -|c|^2/2 (h == 0)
+#pragma unroll
+    for (int b = 0; b < KB; ++b) {
+#pragma unroll
+        for (int s = 0; s < 8; ++s)
+            cf[b][s] = *reinterpret_cast<const bf16x8*>(Cp + (32 * b + l32) * D + 16 * s + 8 * h);
+        const float v = ninit[32 * b + l32];
+        const __bf16 p0 = (__bf16)v;
+        const float r1 = v - (float)p0;
+        const __bf16 p1 = (__bf16)r1;
+        const __bf16 p2 = (__bf16)(r1 - (float)p1);
+        const __bf16 zb = (__bf16)0.0f;
+        cn[b] = (h == 0) ? bf16x8{p0, p1, p2, zb, zb, zb, zb, zb} : bf16x8{zb, zb, zb, zb, zb, zb, zb, zb};
+    }
+    const __bf16 one = (__bf16)1.0f, zb = (__bf16)0.0f;
+    const bf16x8 ones = (h == 0) ? bf16x8{one, one, one, zb, zb, zb, zb, zb} : bf16x8{zb, zb, zb, zb, zb, zb, zb, zb};
+#pragma unroll
+    for (int b = 0; b < KB; ++b) {
+#pragma unroll
+        for (int s = 0; s < 8; ++s) asm volatile("" ::"v"(cf[b][s]));
+        asm volatile("" ::"v"(cn[b]));
+    }
+    int xr[8];
+    const int myrow = 32 * wave + l32;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) xr[s] = (int)(uintptr_t)LDS_PTR(lds) + xoff(myrow, 2 * s + h) -
+                                        (int)(uintptr_t)LDS_PTR(lds);
+    int tbl[4], tbh[4];
+    {
+        const int g = lane >> 4, i16 = lane & 15, q = i16 >> 2, p = i16 & 3;
+#pragma unroll
+        for (int db = 0; db < 4; ++db) {
+            const int ch = 4 * db + 2 * (g & 1) + (p >> 1);
+            tbl[db] = (int)(uintptr_t)LDS_PTR(lds) + xoff(8 * (g >> 1) + q, ch) + 8 * (p & 1);
+            tbh[db] = (int)(uintptr_t)LDS_PTR(lds) + xoff(8 * (g >> 1) + q + 4, ch) + 8 * (p & 1);
+        }
+    }
+    f32x16 sacc[4];
+#pragma unroll
+    for (int db = 0; db < 4; ++db)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sacc[db][r] = 0.f;
+    float cnt = 0.f;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+
+    uint32_t* mbase = reinterpret_cast<uint32_t*>(lds + V4_OFF_MASK);
+    // iteration i: distance/argmax of tile i and one-hot accumulation of tile i-1.  The first and the last
+    // iteration are peeled so the steady-state loop is one straight-line body (no phi copies of the
+    // persistent accumulators between VGPRs and AGPRs).
+    auto iter = [&](int64_t i, auto dist_tag, auto acc_tag) {
+        constexpr bool DIST = decltype(dist_tag)::value;
+        constexpr bool ACC = decltype(acc_tag)::value;
+        if (DIST) {
+            if (i + 1 < my_ntiles) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (i + 2 < my_ntiles)
+            v4_stage(lds, (int)((i + 2) % V4_NBUF), X, ((int64_t)blockIdx.x + (i + 2) * G) * TR, N, voff, wave);
+        const int cur_off = (int)(i % V4_NBUF) * TILE_BYTES;
+        const int prev_off = (int)((i + V4_NBUF - 1) % V4_NBUF) * TILE_BYTES;
+        uint32_t* mcur = mbase + (int)(i & 1) * 128 * 4;
+        uint32_t* mprev = mbase + (int)((i + 1) & 1) * 128 * 4;
+        const int64_t grow = ((int64_t)blockIdx.x + i * G) * TR + myrow;
+        const int64_t gr = (grow < N) ? grow : -1;
+        v4_body<KB, DIST, ACC>(lds, cur_off, prev_off, mcur, mprev, cf, cn, ones, xr, tbl, tbh, sacc, cnt, wave,
+                               h, l32, lane, gr);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    };
+    using T_ = std::true_type;
+    using F_ = std::false_type;
+    if (my_ntiles > 0) {
+        iter(0, T_{}, F_{});
+        for (int64_t i = 1; i < my_ntiles; ++i) iter(i, T_{}, T_{});
+        iter(my_ntiles, F_{}, T_{});
+    }
+
+    float* S = slab + (int64_t)blockIdx.x * 128 * D;
+#pragma unroll
+    for (int db = 0; db < 4; ++db)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int c = 32 * wave + (r & 3) + 8 * (r >> 2) + 4 * h;
+            S[c * D + 32 * db + l32] = sacc[db][r];
+        }
+    if (h == 0) slab_cnt[(int64_t)blockIdx.x * 128 + 32 * wave + l32] = cnt;
+}
+
+// ---------------------------------------------------------------------------------------------------
+// v5: block-owning waves.  Wave w owns centroid block w for BOTH GEMMs (32 centroids: 32 VGPRs of
+// fragments instead of 128), so registers stay well under 256 and out of the AGPR shuffle that bounded v4
+// at k > 64.  64-row tiles, 6-deep LDS ring (3 tiles in flight), one barrier per tile, 3-stage skew:
+//   iteration i:  distance(tile i, block w) -> per-block row partial argmax pbest[i&1][w][row]
+//                 combine(tile i-1): rows 16w..16w+15 take the max over the 4 block partials -> row masks
+//                 accumulate(tile i-2, block w) with the one-hot LUT + ds_read_b64_tr_b16 B fragments
+// ---------------------------------------------------------------------------------------------------
+constexpr int V5_TR = 64;
+constexpr int V5_TILE = V5_TR * ROWB;                      // 16 KiB
+constexpr int V5_NBUF = 6;
+constexpr int V5_AHEAD = 3;
+constexpr int V5_OFF_LUT = V5_NBUF * V5_TILE;             // 96 KiB ring
+constexpr int V5_OFF_MASK = V5_OFF_LUT + 256 * 16;        // [3][128 c][2 words]
+constexpr int V5_OFF_PBEST = V5_OFF_MASK + 3 * 128 * 8;   // [2][4 blocks][64 rows] f32
+constexpr int V5_LDS_BYTES = V5_OFF_PBEST + 2 * 4 * 64 * 4;
+
+__device__ __forceinline__ void v5_stage(char* lds, int buf, const char* X, int64_t row0, int64_t N,
+                                         const uint32_t (&voff)[4], int wave) {
+    const int64_t rem = (N - row0) * ROWB;
+    const int nbytes = rem < V5_TILE ? (int)rem : V5_TILE;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(X + row0 * ROWB), (short)0, nbytes, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t m0v = __builtin_amdgcn_readfirstlane(
+            (uint32_t)(uintptr_t)LDS_PTR(lds + buf * V5_TILE + i * 4096 + wave * 1024));
+        uint32_t keep;
+        asm volatile(
+            "s_mov_b32 %0, m0\n\t"
+            "s_mov_b32 m0, %3\n\t"
+            "s_nop 0\n\t"
+            "buffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
+            "s_mov_b32 m0, %0"
+            : "=&s"(keep)
+            : "v"(voff[i]), "s"(rs), "s"(m0v)
+            : "memory");
+    }
+}
+
+template <int KB>
+__global__ __launch_bounds__(256, 1) void kmeans_assign_accum_v5_kernel(
+    const __bf16* __restrict__ Xp, int64_t N, const __bf16* __restrict__ Cp, const float* __restrict__ ninit,
+    float* __restrict__ slab, float* __restrict__ slab_cnt, int64_t ntiles) {
+    __shared__ __attribute__((aligned(16))) char lds[V5_LDS_BYTES];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int h = lane >> 5;
+    const int l32 = lane & 31;
+    const char* X = reinterpret_cast<const char*>(Xp);
+    const int64_t G = gridDim.x;
+    const int64_t my_ntiles = (ntiles > (int64_t)blockIdx.x) ? (ntiles - 1 - blockIdx.x) / G + 1 : 0;
+    const bool active = wave < KB;
+
+    uint32_t voff[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int p = i * 4096 + tid * 16;
+        const int row = p >> 8;
+        const int chp = (p >> 4) & 15;
+        voff[i] = (uint32_t)(row * ROWB + 16 * (chp ^ (((row & 3) << 2) | ((row >> 2) & 3))));
+    }
+    {
+        uint4* ring = reinterpret_cast<uint4*>(lds);
+        for (int e = tid; e < V5_NBUF * V5_TILE / 16; e += 256) ring[e] = uint4{0u, 0u, 0u, 0u};
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+    }
+    for (int s = 0; s < V5_AHEAD; ++s)
+        if (s < my_ntiles) v5_stage(lds, s, X, ((int64_t)blockIdx.x + s * G) * V5_TR, N, voff, wave);
+    {
+        uint32_t* lut = reinterpret_cast<uint32_t*>(lds + V5_OFF_LUT);
+        for (int e = tid; e < 256 * 4; e += 256) {
+            const int ent = e >> 2, pair = e & 3;
+            const uint32_t b0 = (ent >> (2 * pair)) & 1, b1 = (ent >> (2 * pair + 1)) & 1;
+            lut[e] = (b0 ? 0x3F80u : 0u) | (b1 ? 0x3F800000u : 0u);
+        }
+        uint32_t* m = reinterpret_cast<uint32_t*>(lds + V5_OFF_MASK);
+        for (int e = tid; e < 3 * 128 * 2; e += 256) m[e] = 0u;
+        float* pb = reinterpret_cast<float*>(lds + V5_OFF_PBEST);
+        for (int e = tid; e < 2 * 4 * 64; e += 256) pb[e] = -3.0e38f;
+    }
+    // own centroid block: fragments + the norm k-step operand (-|c|^2/2 as three bf16 parts)
+    const int cb = wave;
+    bf16x8 cf[8];
+    bf16x8 cn;
+    {
+        const __bf16 zb = (__bf16)0.0f;
+#pragma unroll
+        for (int s = 0; s < 8; ++s)
+            cf[s] = active ? *reinterpret_cast<const bf16x8*>(Cp + (32 * cb + l32) * D + 16 * s + 8 * h)
+                           : bf16x8{zb, zb, zb, zb, zb, zb, zb, zb};
+        const float v = active ? ninit[32 * cb + l32] : -3.0e38f;
+        const __bf16 p0 = (__bf16)v;
+        const float r1 = v - (float)p0;
+        const __bf16 p1 = (__bf16)r1;
+        const __bf16 p2 = (__bf16)(r1 - (float)p1);
+        cn = (h == 0) ? bf16x8{p0, p1, p2, zb, zb, zb, zb, zb} : bf16x8{zb, zb, zb, zb, zb, zb, zb, zb};
+#pragma unroll
+        for (int s = 0; s < 8; ++s) asm volatile("" ::"v"(cf[s]));
+        asm volatile("" ::"v"(cn));
+    }
+    const __bf16 one = (__bf16)1.0f, zb = (__bf16)0.0f;
+    const bf16x8 ones = (h == 0) ? bf16x8{one, one, one, zb, zb, zb, zb, zb} : bf16x8{zb, zb, zb, zb, zb, zb, zb, zb};
+    int xr[2][8];
+#pragma unroll
+    for (int rg = 0; rg < 2; ++rg)
+#pragma unroll
+        for (int s = 0; s < 8; ++s) xr[rg][s] = xoff(32 * rg + l32, 2 * s + h);
+    int tbl[4], tbh[4];
+    {
+        const int g = lane >> 4, i16 = lane & 15, q = i16 >> 2, p = i16 & 3;
+#pragma unroll
+        for (int db = 0; db < 4; ++db) {
+            const int ch = 4 * db + 2 * (g & 1) + (p >> 1);
+            tbl[db] = (int)(uintptr_t)LDS_PTR(lds) + xoff(8 * (g >> 1) + q, ch) + 8 * (p & 1);
+            tbh[db] = (int)(uintptr_t)LDS_PTR(lds) + xoff(8 * (g >> 1) + q + 4, ch) + 8 * (p & 1);
+        }
+    }
+    f32x16 sacc[4];
+#pragma unroll
+    for (int db = 0; db < 4; ++db)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sacc[db][r] = 0.f;
+    float cnt = 0.f;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+
+    float* pbest = reinterpret_cast<float*>(lds + V5_OFF_PBEST);
+    uint32_t* masks = reinterpret_cast<uint32_t*>(lds + V5_OFF_MASK);
+
+    // Every iteration runs the same straight-line MFMA code (no divergent paths -> no register-file
+    // copies at control-flow joins): warm-up/drain iterations operate on zero/stale-but-finite LDS tiles
+    // with all-zero row masks, and the combine step (scalar/lane work only) skips tiles that do not exist.
+    for (int64_t i = 0; i < my_ntiles + 2; ++i) {
+        if (i < my_ntiles) {
+            const int64_t after = my_ntiles - 1 - i;  // tiles issued after tile i and still outstanding
+            if (after >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            else if (after == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (i + V5_AHEAD < my_ntiles)
+            v5_stage(lds, (int)((i + V5_AHEAD) % V5_NBUF), X, ((int64_t)blockIdx.x + (i + V5_AHEAD) * G) * V5_TR,
+                     N, voff, wave);
+
+        // ---- distance of tile i against the own centroid block ----
+        f32x16 acc[2];
+        {
+            const int cur = (int)(i % V5_NBUF) * V5_TILE;
+            const f32x16 z = {};
+#pragma unroll
+            for (int rg = 0; rg < 2; ++rg) acc[rg] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cn, ones, z, 0, 0, 0);
+#pragma unroll
+            for (int s = 0; s < 8; ++s) {
+#pragma unroll
+                for (int rg = 0; rg < 2; ++rg) {
+                    const bf16x8 xv = *reinterpret_cast<const bf16x8*>(lds + cur + xr[rg][s]);
+                    acc[rg] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cf[s], xv, acc[rg], 0, 0, 0);
+                }
+            }
+        }
+        // ---- combine tile i-1 (rows 16w..16w+15): max over the 4 block partials -> row masks ----
+        {
+            const int64_t t = i - 1;
+            const int row = 16 * wave + (lane & 15);
+            const int64_t grow = ((int64_t)blockIdx.x + t * G) * V5_TR + row;
+            if (lane < 16 && t >= 0 && t < my_ntiles && grow < N) {
+                const float* pb = pbest + (int)((i + 1) & 1) * 256;
+                const float best = fmaxf(fmaxf(pb[row], pb[64 + row]), fmaxf(pb[128 + row], pb[192 + row]));
+                const uint32_t c = __float_as_uint(best) & 127u;
+                __hip_atomic_fetch_or(masks + (int)((i + 2) % 3) * 256 + c * 2 + (row >> 5), 1u << (row & 31),
+                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+        }
+        // ---- accumulate tile i-2 for the own block; argmax of tile i interleaved ----
+        float best0 = -3.0e38f, best1 = -3.0e38f;
+        {
+            const int po = (int)((i + 4) % V5_NBUF) * V5_TILE;
+            uint32_t* mp = masks + (int)((i + 1) % 3) * 256 + (32 * wave + l32) * 2;
+            const uint32_t mw0 = mp[0], mw1 = mp[1];
+            cnt += (h == 0) ? (float)(__popc(mw0) + __popc(mw1)) : 0.f;
+            mp[h] = 0u;  // both halves read the same pair; lane h clears word h
+            int tl[4], th[4];
+#pragma unroll
+            for (int db = 0; db < 4; ++db) {
+                tl[db] = tbl[db] + po;
+                th[db] = tbh[db] + po;
+            }
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const uint32_t word = (s >> 1) ? mw1 : mw0;
+                const uint32_t byte = (word >> (16 * (s & 1) + 8 * h)) & 255u;
+                const bf16x8 a = *reinterpret_cast<const bf16x8*>(lds + V5_OFF_LUT + byte * 16);
+#pragma unroll
+                for (int db = 0; db < 4; ++db) {
+                    const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+                        (__attribute__((address_space(3))) bf16x4*)(uintptr_t)(tl[db] + s * 4096));
+                    const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+                        (__attribute__((address_space(3))) bf16x4*)(uintptr_t)(th[db] + s * 4096));
+                    const bf16x8 bv = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                    sacc[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bv, sacc[db], 0, 0, 0);
+                }
+#pragma unroll
+                for (int t2 = 0; t2 < 8; ++t2) {
+                    const int v = s * 8 + t2;  // 32 values: rg = v >> 4, r = v & 15
+                    const int rg = v >> 4, r = v & 15;
+                    const uint32_t c = 32 * cb + (r & 3) + 8 * (r >> 2) + 4 * h;
+                    const float pk = __uint_as_float((__float_as_uint(acc[rg][r]) & 0xFFFFFF80u) | c);
+                    if (rg == 0) best0 = fmaxf(best0, pk);
+                    else best1 = fmaxf(best1, pk);
+                }
+            }
+        }
+        best0 = fmaxf(best0, __shfl_xor(best0, 32));
+        best1 = fmaxf(best1, __shfl_xor(best1, 32));
+        {
+            float* pb = pbest + (int)(i & 1) * 256 + wave * 64 + 32 * h;
+            pb[l32] = h ? best1 : best0;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+
+    float* S = slab + (int64_t)blockIdx.x * 128 * D;
+#pragma unroll
+    for (int db = 0; db < 4; ++db)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int c = 32 * wave + (r & 3) + 8 * (r >> 2) + 4 * h;
+            S[c * D + 32 * db + l32] = sacc[db][r];
+        }
+    if (h == 0) slab_cnt[(int64_t)blockIdx.x * 128 + 32 * wave + l32] = cnt;
+}
+
 // fixed-order fp64 reduction of the per-workgroup slabs -> out[k][D+1] (last column = count)
 __global__ void kmeans_reduce_slabs_kernel(const float* __restrict__ slab, const float* __restrict__ slab_cnt,
                                            int nslab, int k, double* __restrict__ out) {
@@ -533,6 +1258,66 @@ int alink_kmeans_assign_accum_bf16_v2(const void* X, int64_t N, const void* C, c
         default: V2_LAUNCH(4); break;
     }
 #undef V2_LAUNCH
+    return (int)hipGetLastError();
+}
+
+int alink_kmeans_assign_accum_bf16_v3(const void* X, int64_t N, const void* C, const float* ninit, int k,
+                                      float* slab, float* slab_cnt, int grid, void* stream) {
+    if (N <= 0 || k < 1 || k > 128 || grid <= 0) return -1;
+    const int KB = (k + 31) / 32;
+    const int64_t ntiles = (N + V3_TR - 1) / V3_TR;
+    if (grid > ntiles) grid = (int)ntiles;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+#define V3_LAUNCH(KBV)                                                                                   \
+    hipLaunchKernelGGL(kmeans_assign_accum_v3_kernel<KBV>, dim3(grid), dim3(512), 0, st, (const __bf16*)X, N, \
+                       (const __bf16*)C, ninit, slab, slab_cnt, ntiles)
+    switch (KB) {
+        case 1: V3_LAUNCH(1); break;
+        case 2: V3_LAUNCH(2); break;
+        case 3: V3_LAUNCH(3); break;
+        default: V3_LAUNCH(4); break;
+    }
+#undef V3_LAUNCH
+    return (int)hipGetLastError();
+}
+
+int alink_kmeans_assign_accum_bf16_v4(const void* X, int64_t N, const void* C, const float* ninit, int k,
+                                      float* slab, float* slab_cnt, int grid, void* stream) {
+    if (N <= 0 || k < 1 || k > 128 || grid <= 0) return -1;
+    const int KB = (k + 31) / 32;
+    const int64_t ntiles = (N + TR - 1) / TR;
+    if (grid > ntiles) grid = (int)ntiles;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+#define V4_LAUNCH(KBV)                                                                                   \
+    hipLaunchKernelGGL(kmeans_assign_accum_v4_kernel<KBV>, dim3(grid), dim3(256), 0, st, (const __bf16*)X, N, \
+                       (const __bf16*)C, ninit, slab, slab_cnt, ntiles)
+    switch (KB) {
+        case 1: V4_LAUNCH(1); break;
+        case 2: V4_LAUNCH(2); break;
+        case 3: V4_LAUNCH(3); break;
+        default: V4_LAUNCH(4); break;
+    }
+#undef V4_LAUNCH
+    return (int)hipGetLastError();
+}
+
+int alink_kmeans_assign_accum_bf16_v5(const void* X, int64_t N, const void* C, const float* ninit, int k,
+                                      float* slab, float* slab_cnt, int grid, void* stream) {
+    if (N <= 0 || k < 1 || k > 128 || grid <= 0) return -1;
+    const int KB = (k + 31) / 32;
+    const int64_t ntiles = (N + V5_TR - 1) / V5_TR;
+    if (grid > ntiles) grid = (int)ntiles;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+#define V5_LAUNCH(KBV)                                                                                   \
+    hipLaunchKernelGGL(kmeans_assign_accum_v5_kernel<KBV>, dim3(grid), dim3(256), 0, st, (const __bf16*)X, N, \
+                       (const __bf16*)C, ninit, slab, slab_cnt, ntiles)
+    switch (KB) {
+        case 1: V5_LAUNCH(1); break;
+        case 2: V5_LAUNCH(2); break;
+        case 3: V5_LAUNCH(3); break;
+        default: V5_LAUNCH(4); break;
+    }
+#undef V5_LAUNCH
     return (int)hipGetLastError();
 }
 

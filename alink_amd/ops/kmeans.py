@@ -20,6 +20,7 @@ from . import _lib
 __all__ = ["assign_accumulate", "assign", "assign_accumulate_torch", "hip_supported", "prepare_centroids"]
 
 _BUF: Dict[Tuple, Tuple[torch.Tensor, torch.Tensor]] = {}
+DEFAULT_VARIANT = 1
 HIP_D = 128
 HIP_KMAX = 128
 
@@ -45,8 +46,9 @@ def _num_cus(device) -> int:
 
 
 def assign_accumulate_hip(X: torch.Tensor, C: torch.Tensor, grid: Optional[int] = None,
-                          variant: int = 1) -> torch.Tensor:
+                          variant: Optional[int] = None) -> torch.Tensor:
     L = _lib.require()
+    variant = DEFAULT_VARIANT if variant is None else variant
     dev = X.device
     k = C.shape[0]
     if not hip_supported(X, k):
@@ -55,7 +57,7 @@ def assign_accumulate_hip(X: torch.Tensor, C: torch.Tensor, grid: Optional[int] 
     n = X.shape[0]
     if grid is None:
         grid = _num_cus(dev)
-    ntiles = (n + 127) // 128
+    ntiles = (n + 127) // 128 if variant not in (3, 5) else (n + 63) // 64
     grid = max(1, min(grid, ntiles))
     key = (dev.index, grid)
     if key not in _BUF:
@@ -64,7 +66,11 @@ def assign_accumulate_hip(X: torch.Tensor, C: torch.Tensor, grid: Optional[int] 
     slab, slab_cnt = _BUF[key]
     out = torch.empty((k, HIP_D + 1), dtype=torch.float64, device=dev)
     st = _lib.stream_ptr(dev)
-    fn = L.alink_kmeans_assign_accum_bf16 if variant == 1 else L.alink_kmeans_assign_accum_bf16_v2
+    fn = {1: L.alink_kmeans_assign_accum_bf16, 2: L.alink_kmeans_assign_accum_bf16_v2,
+          3: L.alink_kmeans_assign_accum_bf16_v3, 4: L.alink_kmeans_assign_accum_bf16_v4,
+          5: L.alink_kmeans_assign_accum_bf16_v5}[variant]
+    if variant == 2 and k > 64:
+        raise ValueError("variant 2 spills registers for k > 64")
     rc = fn(X.data_ptr(), n, cpad.data_ptr(), ninit.data_ptr(), k, slab.data_ptr(), slab_cnt.data_ptr(), grid, st)
     if rc != 0:
         raise RuntimeError(f"alink_kmeans_assign_accum_bf16 failed: {rc}")
