@@ -192,22 +192,43 @@ def _fetch_global_rows(X: torch.Tensor, global_idx: List[int], counts: List[int]
 
 def _local_kmeans(samples: torch.Tensor, weights: torch.Tensor, k: int, dist_type: str,
                   max_iter: int = 30, seed: int = 0) -> torch.Tensor:
-    """Weighted k-means++ seeding + Lloyd on the candidate set (LocalKmeansFunc.java)."""
+    """Weighted k-means++ seeding + Lloyd on the k-means|| candidate set (LocalKmeansFunc.java:36-141).
+
+    Seeding is *greedy* k-means++: every pick takes the candidate that lowers the weighted potential most —
+    over ALL candidates when the set is small (<= 4096, the usual k-means|| output, O(k m^2) on the device),
+    else over 2 + ln k sampled trials.  The reference samples one candidate per pick with plain distance
+    weights, which in high dimension (within-cluster spread comparable to cluster separation) regularly
+    seeds two centroids in one true cluster and then needs tens of Lloyd steps to creep apart."""
     rng = np.random.default_rng(seed)
     n = samples.shape[0]
     w = weights.to(torch.float64)
-    costs = torch.ones(n, dtype=torch.float64, device=samples.device)
-    idx = 0
-    chosen = []
-    for i in range(k):
-        if i > 0:
-            d = _seed_cost(pairwise_distance(samples, samples[idx:idx + 1], dist_type)[:, 0], dist_type)
-            costs = torch.minimum(d, costs) if i > 1 else d
-        cum = torch.cumsum(w * costs, 0).cpu().numpy()
-        r = rng.random() * cum[-1]
-        j = int(np.searchsorted(cum, r, side="left"))
-        idx = min(max(j, 0), n - 1)
-        chosen.append(idx)
+    D = _seed_cost(pairwise_distance(samples, samples, dist_type), dist_type)  # [n, n]
+    exhaustive = n <= 4096
+    trials = 2 + int(np.log(max(k, 2)))
+    cum = torch.cumsum(w, 0).cpu().numpy()
+    idx = int(min(np.searchsorted(cum, rng.random() * cum[-1], side="left"), n - 1))
+    chosen = [idx]
+    costs = D[idx].clone()
+    for _ in range(1, k):
+        if exhaustive:
+            pot = (torch.minimum(costs[None, :], D) * w[None, :]).sum(1)
+            pot[chosen] = float("inf")
+            b = int(pot.argmin().item())
+            chosen.append(b)
+            costs = torch.minimum(costs, D[b])
+            continue
+        cw = torch.cumsum(w * costs, 0).cpu().numpy()
+        tot = cw[-1]
+        if tot <= 0:
+            cand = rng.integers(n, size=trials)
+        else:
+            cand = np.minimum(np.searchsorted(cw, rng.random(trials) * tot, side="left"), n - 1)
+        cand_t = torch.as_tensor(cand, device=samples.device)
+        newc = torch.minimum(costs[None, :], D[cand_t])  # [trials, n]
+        pot = (newc * w[None, :]).sum(1)
+        b = int(pot.argmin().item())
+        chosen.append(int(cand[b]))
+        costs = newc[b]
     C = samples[chosen].clone()
     assign = torch.full((n,), -1, dtype=torch.int64, device=samples.device)
     for _ in range(max_iter):
@@ -313,6 +334,7 @@ class KMeansUpdateCentroids(ComputeFunction):
 class KMeansIterTermination(CompareCriterionFunction):
     def __init__(self, dist_type: str, tol: float):
         self.dist_type, self.tol = dist_type, tol
+        self.history = []  # max centroid movement per superstep (diagnostics / train info)
 
     def calc(self, ctx) -> bool:
         k = ctx.getObj(K)
@@ -326,7 +348,9 @@ class KMeansIterTermination(CompareCriterionFunction):
             d = torch.diagonal(pairwise_distance(a, b, "HAVERSINE"))
         else:
             d = (a - b).norm(dim=1)
-        return bool((d < self.tol).all().item())
+        mx = float(d.max().item())
+        self.history.append(mx)
+        return mx < self.tol
 
 
 class KMeansOutputModel(CompleteResultFunction):

@@ -52,7 +52,9 @@ class KMeansTrainBatchOp(BatchOperator):
 
     def getTrainInfo(self):
         q = getattr(self, "_queue", None)
-        return {"iterations": q.step_no if q else None, "steps": q.stats if q else None}
+        crit = getattr(q, "criterion", None) if q else None
+        return {"iterations": q.step_no if q else None, "steps": q.stats if q else None,
+                "max_shift": list(getattr(crit, "history", []))}
 
 
 class KMeansPredictBatchOp(ModelMapBatchOp):

@@ -41,10 +41,12 @@ def _load():
     L.alink_kmeans_assign_accum_bf16_v2.restype = c_int
     L.alink_kmeans_assign_accum_bf16_v3.argtypes = [c_vp, c_i64, c_vp, c_vp, c_int, c_vp, c_vp, c_int, c_vp]
     L.alink_kmeans_assign_accum_bf16_v3.restype = c_int
-    L.alink_kmeans_assign_accum_bf16_v4.argtypes = [c_vp, c_i64, c_vp, c_vp, c_int, c_vp, c_vp, c_int, c_vp]
+    L.alink_kmeans_assign_accum_bf16_v4.argtypes = [c_vp, c_i64, c_vp, c_vp, c_int, c_vp, c_vp, c_int, c_vp, c_int]
     L.alink_kmeans_assign_accum_bf16_v4.restype = c_int
-    L.alink_kmeans_assign_accum_bf16_v5.argtypes = [c_vp, c_i64, c_vp, c_vp, c_int, c_vp, c_vp, c_int, c_vp]
+    L.alink_kmeans_assign_accum_bf16_v5.argtypes = [c_vp, c_i64, c_vp, c_vp, c_int, c_vp, c_vp, c_int, c_vp, c_int]
     L.alink_kmeans_assign_accum_bf16_v5.restype = c_int
+    L.alink_kmeans_assign_accum_bf16_v6.argtypes = [c_vp, c_i64, c_vp, c_vp, c_int, c_vp, c_vp, c_int, c_vp, c_int]
+    L.alink_kmeans_assign_accum_bf16_v6.restype = c_int
     L.alink_kmeans_reduce_slabs.argtypes = [c_vp, c_vp, c_int, c_int, c_vp, c_vp]
     L.alink_kmeans_reduce_slabs.restype = c_int
     for name, argtypes in _EXTRA_SIGNATURES.items():

@@ -839,7 +839,7 @@ __device__ __forceinline__ void v4_body(char* lds, int cur_off, int prev_off, ui
 template <int KB>
 __global__ __launch_bounds__(256, 1) void kmeans_assign_accum_v4_kernel(
     const __bf16* __restrict__ Xp, int64_t N, const __bf16* __restrict__ Cp, const float* __restrict__ ninit,
-    float* __restrict__ slab, float* __restrict__ slab_cnt, int64_t ntiles) {
+    float* __restrict__ slab, float* __restrict__ slab_cnt, int64_t ntiles, int64_t per) {
     __shared__ __attribute__((aligned(16))) char lds[V4_LDS_BYTES];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -848,7 +848,12 @@ __global__ __launch_bounds__(256, 1) void kmeans_assign_accum_v4_kernel(
     const int l32 = lane & 31;
     const char* X = reinterpret_cast<const char*>(Xp);
     const int64_t G = gridDim.x;
-    const int64_t my_ntiles = (ntiles > (int64_t)blockIdx.x) ? (ntiles - 1 - blockIdx.x) / G + 1 : 0;
+    // tile schedule: per > 0 -> contiguous run of `per` tiles per workgroup (sequential pages/TLB reach),
+    //                per == 0 -> tiles strided by the grid
+    const int64_t tbase = per > 0 ? (int64_t)blockIdx.x * per : (int64_t)blockIdx.x;
+    const int64_t tstride = per > 0 ? 1 : G;
+    const int64_t my_ntiles = per > 0 ? (ntiles > tbase ? (ntiles - tbase < per ? ntiles - tbase : per) : 0)
+                                      : ((ntiles > (int64_t)blockIdx.x) ? (ntiles - 1 - blockIdx.x) / G + 1 : 0);
 
     uint32_t voff[8];
 #pragma unroll
@@ -859,7 +864,7 @@ __global__ __launch_bounds__(256, 1) void kmeans_assign_accum_v4_kernel(
         voff[i] = (uint32_t)(row * ROWB + 16 * (chp ^ (((row & 3) << 2) | ((row >> 2) & 3))));
     }
     for (int s = 0; s < 2; ++s)
-        if (s < my_ntiles) v4_stage(lds, s, X, ((int64_t)blockIdx.x + s * G) * TR, N, voff, wave);
+        if (s < my_ntiles) v4_stage(lds, s, X, (tbase + (int64_t)(s) * tstride) * TR, N, voff, wave);
     {
         uint32_t* lut = reinterpret_cast<uint32_t*>(lds + V4_OFF_LUT);
         for (int e = tid; e < 256 * 4; e += 256) {
@@ -932,12 +937,12 @@ __global__ __launch_bounds__(256, 1) void kmeans_assign_accum_v4_kernel(
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         if (i + 2 < my_ntiles)
-            v4_stage(lds, (int)((i + 2) % V4_NBUF), X, ((int64_t)blockIdx.x + (i + 2) * G) * TR, N, voff, wave);
+            v4_stage(lds, (int)((i + 2) % V4_NBUF), X, (tbase + (int64_t)((i + 2)) * tstride) * TR, N, voff, wave);
         const int cur_off = (int)(i % V4_NBUF) * TILE_BYTES;
         const int prev_off = (int)((i + V4_NBUF - 1) % V4_NBUF) * TILE_BYTES;
         uint32_t* mcur = mbase + (int)(i & 1) * 128 * 4;
         uint32_t* mprev = mbase + (int)((i + 1) & 1) * 128 * 4;
-        const int64_t grow = ((int64_t)blockIdx.x + i * G) * TR + myrow;
+        const int64_t grow = (tbase + (int64_t)(i) * tstride) * TR + myrow;
         const int64_t gr = (grow < N) ? grow : -1;
         v4_body<KB, DIST, ACC>(lds, cur_off, prev_off, mcur, mprev, cf, cn, ones, xr, tbl, tbh, sacc, cnt, wave,
                                h, l32, lane, gr);
@@ -972,9 +977,9 @@ __global__ __launch_bounds__(256, 1) void kmeans_assign_accum_v4_kernel(
 // ---------------------------------------------------------------------------------------------------
 constexpr int V5_TR = 64;
 constexpr int V5_TILE = V5_TR * ROWB;                      // 16 KiB
-constexpr int V5_NBUF = 6;
-constexpr int V5_AHEAD = 3;
-constexpr int V5_OFF_LUT = V5_NBUF * V5_TILE;             // 96 KiB ring
+constexpr uint32_t V5_NBUF = 8;
+constexpr int V5_AHEAD = 4;
+constexpr int V5_OFF_LUT = V5_NBUF * V5_TILE;             // 128 KiB ring (4 tiles = 64 KiB in flight)
 constexpr int V5_OFF_MASK = V5_OFF_LUT + 256 * 16;        // [3][128 c][2 words]
 constexpr int V5_OFF_PBEST = V5_OFF_MASK + 3 * 128 * 8;   // [2][4 blocks][64 rows] f32
 constexpr int V5_LDS_BYTES = V5_OFF_PBEST + 2 * 4 * 64 * 4;
@@ -1005,7 +1010,7 @@ __device__ __forceinline__ void v5_stage(char* lds, int buf, const char* X, int6
 template <int KB>
 __global__ __launch_bounds__(256, 1) void kmeans_assign_accum_v5_kernel(
     const __bf16* __restrict__ Xp, int64_t N, const __bf16* __restrict__ Cp, const float* __restrict__ ninit,
-    float* __restrict__ slab, float* __restrict__ slab_cnt, int64_t ntiles) {
+    float* __restrict__ slab, float* __restrict__ slab_cnt, int64_t ntiles, int64_t per) {
     __shared__ __attribute__((aligned(16))) char lds[V5_LDS_BYTES];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -1014,7 +1019,12 @@ __global__ __launch_bounds__(256, 1) void kmeans_assign_accum_v5_kernel(
     const int l32 = lane & 31;
     const char* X = reinterpret_cast<const char*>(Xp);
     const int64_t G = gridDim.x;
-    const int64_t my_ntiles = (ntiles > (int64_t)blockIdx.x) ? (ntiles - 1 - blockIdx.x) / G + 1 : 0;
+    // tile schedule: per > 0 -> contiguous run of `per` tiles per workgroup (sequential pages/TLB reach),
+    //                per == 0 -> tiles strided by the grid
+    const int64_t tbase = per > 0 ? (int64_t)blockIdx.x * per : (int64_t)blockIdx.x;
+    const int64_t tstride = per > 0 ? 1 : G;
+    const int64_t my_ntiles = per > 0 ? (ntiles > tbase ? (ntiles - tbase < per ? ntiles - tbase : per) : 0)
+                                      : ((ntiles > (int64_t)blockIdx.x) ? (ntiles - 1 - blockIdx.x) / G + 1 : 0);
     const bool active = wave < KB;
 
     uint32_t voff[4];
@@ -1032,7 +1042,7 @@ __global__ __launch_bounds__(256, 1) void kmeans_assign_accum_v5_kernel(
         __builtin_amdgcn_s_barrier();
     }
     for (int s = 0; s < V5_AHEAD; ++s)
-        if (s < my_ntiles) v5_stage(lds, s, X, ((int64_t)blockIdx.x + s * G) * V5_TR, N, voff, wave);
+        if (s < my_ntiles) v5_stage(lds, s, X, (tbase + (int64_t)(s) * tstride) * V5_TR, N, voff, wave);
     {
         uint32_t* lut = reinterpret_cast<uint32_t*>(lds + V5_OFF_LUT);
         for (int e = tid; e < 256 * 4; e += 256) {
@@ -1097,23 +1107,45 @@ __global__ __launch_bounds__(256, 1) void kmeans_assign_accum_v5_kernel(
     // Every iteration runs the same straight-line MFMA code (no divergent paths -> no register-file
     // copies at control-flow joins): warm-up/drain iterations operate on zero/stale-but-finite LDS tiles
     // with all-zero row masks, and the combine step (scalar/lane work only) skips tiles that do not exist.
-    for (int64_t i = 0; i < my_ntiles + 2; ++i) {
-        if (i < my_ntiles) {
-            const int64_t after = my_ntiles - 1 - i;  // tiles issued after tile i and still outstanding
-            if (after >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    // 4-stage skew so no step waits on a result produced in the same iteration:
+    //   iteration i: distance(tile i) MFMAs, argmax(tile i-1) VALU in their gaps, combine(tile i-2),
+    //                one-hot accumulate(tile i-3) with masks/LUT fragments loaded right after the barrier.
+    const int nt = (int)my_ntiles;
+    const int total = (nt + 3 + 1) & ~1;  // even: the loop body is unrolled twice (acc ping-pong)
+    f32x16 accA[2], accB[2];
+#pragma unroll
+    for (int rg = 0; rg < 2; ++rg)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) accA[rg][r] = accB[rg][r] = -3.0e38f;
+
+    auto body = [&](const int i, f32x16 (&acc)[2], const f32x16 (&accp)[2]) {
+        const uint32_t ui = (uint32_t)i;
+        if (i < nt) {
+            const int after = nt - 1 - i;  // tiles issued after tile i and still outstanding
+            if (after >= 3) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+            else if (after == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
             else if (after == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
             else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        if (i + V5_AHEAD < my_ntiles)
-            v5_stage(lds, (int)((i + V5_AHEAD) % V5_NBUF), X, ((int64_t)blockIdx.x + (i + V5_AHEAD) * G) * V5_TR,
-                     N, voff, wave);
-
-        // ---- distance of tile i against the own centroid block ----
-        f32x16 acc[2];
+        if (i + V5_AHEAD < nt)
+            v5_stage(lds, (int)((ui + V5_AHEAD) % V5_NBUF), X,
+                     (tbase + (int64_t)((int64_t)(i + V5_AHEAD)) * tstride) * V5_TR, N, voff, wave);
+        // accumulation operands of tile i-3 (masks written by last iteration's combine)
+        uint32_t* mp = masks + (int)(ui % 3u) * 256 + (32 * wave + l32) * 2;
+        const uint32_t mw0 = mp[0], mw1 = mp[1];
+        bf16x8 af[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const uint32_t word = (s >> 1) ? mw1 : mw0;
+            const uint32_t byte = (word >> (16 * (s & 1) + 8 * h)) & 255u;
+            af[s] = *reinterpret_cast<const bf16x8*>(lds + V5_OFF_LUT + byte * 16);
+        }
+        // ---- distance of tile i against the own centroid block; argmax of tile i-1 in the gaps ----
+        float best0 = -3.0e38f, best1 = -3.0e38f;
         {
-            const int cur = (int)(i % V5_NBUF) * V5_TILE;
+            const int cur = (int)(ui % V5_NBUF) * V5_TILE;
             const f32x16 z = {};
 #pragma unroll
             for (int rg = 0; rg < 2; ++rg) acc[rg] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cn, ones, z, 0, 0, 0);
@@ -1123,68 +1155,59 @@ __global__ __launch_bounds__(256, 1) void kmeans_assign_accum_v5_kernel(
                 for (int rg = 0; rg < 2; ++rg) {
                     const bf16x8 xv = *reinterpret_cast<const bf16x8*>(lds + cur + xr[rg][s]);
                     acc[rg] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cf[s], xv, acc[rg], 0, 0, 0);
-                }
-            }
-        }
-        // ---- combine tile i-1 (rows 16w..16w+15): max over the 4 block partials -> row masks ----
-        {
-            const int64_t t = i - 1;
-            const int row = 16 * wave + (lane & 15);
-            const int64_t grow = ((int64_t)blockIdx.x + t * G) * V5_TR + row;
-            if (lane < 16 && t >= 0 && t < my_ntiles && grow < N) {
-                const float* pb = pbest + (int)((i + 1) & 1) * 256;
-                const float best = fmaxf(fmaxf(pb[row], pb[64 + row]), fmaxf(pb[128 + row], pb[192 + row]));
-                const uint32_t c = __float_as_uint(best) & 127u;
-                __hip_atomic_fetch_or(masks + (int)((i + 2) % 3) * 256 + c * 2 + (row >> 5), 1u << (row & 31),
-                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            }
-        }
-        // ---- accumulate tile i-2 for the own block; argmax of tile i interleaved ----
-        float best0 = -3.0e38f, best1 = -3.0e38f;
-        {
-            const int po = (int)((i + 4) % V5_NBUF) * V5_TILE;
-            uint32_t* mp = masks + (int)((i + 1) % 3) * 256 + (32 * wave + l32) * 2;
-            const uint32_t mw0 = mp[0], mw1 = mp[1];
-            cnt += (h == 0) ? (float)(__popc(mw0) + __popc(mw1)) : 0.f;
-            mp[h] = 0u;  // both halves read the same pair; lane h clears word h
-            int tl[4], th[4];
 #pragma unroll
-            for (int db = 0; db < 4; ++db) {
-                tl[db] = tbl[db] + po;
-                th[db] = tbh[db] + po;
-            }
-#pragma unroll
-            for (int s = 0; s < 4; ++s) {
-                const uint32_t word = (s >> 1) ? mw1 : mw0;
-                const uint32_t byte = (word >> (16 * (s & 1) + 8 * h)) & 255u;
-                const bf16x8 a = *reinterpret_cast<const bf16x8*>(lds + V5_OFF_LUT + byte * 16);
-#pragma unroll
-                for (int db = 0; db < 4; ++db) {
-                    const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
-                        (__attribute__((address_space(3))) bf16x4*)(uintptr_t)(tl[db] + s * 4096));
-                    const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
-                        (__attribute__((address_space(3))) bf16x4*)(uintptr_t)(th[db] + s * 4096));
-                    const bf16x8 bv = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-                    sacc[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bv, sacc[db], 0, 0, 0);
-                }
-#pragma unroll
-                for (int t2 = 0; t2 < 8; ++t2) {
-                    const int v = s * 8 + t2;  // 32 values: rg = v >> 4, r = v & 15
-                    const int rg = v >> 4, r = v & 15;
-                    const uint32_t c = 32 * cb + (r & 3) + 8 * (r >> 2) + 4 * h;
-                    const float pk = __uint_as_float((__float_as_uint(acc[rg][r]) & 0xFFFFFF80u) | c);
-                    if (rg == 0) best0 = fmaxf(best0, pk);
-                    else best1 = fmaxf(best1, pk);
+                    for (int t2 = 0; t2 < 2; ++t2) {
+                        const int r = 2 * s + t2;
+                        const uint32_t c = 32 * cb + (r & 3) + 8 * (r >> 2) + 4 * h;
+                        const float pk = __uint_as_float((__float_as_uint(accp[rg][r]) & 0xFFFFFF80u) | c);
+                        if (rg == 0) best0 = fmaxf(best0, pk);
+                        else best1 = fmaxf(best1, pk);
+                    }
                 }
             }
         }
         best0 = fmaxf(best0, __shfl_xor(best0, 32));
         best1 = fmaxf(best1, __shfl_xor(best1, 32));
         {
-            float* pb = pbest + (int)(i & 1) * 256 + wave * 64 + 32 * h;
+            float* pb = pbest + (int)((ui + 1) & 1u) * 256 + wave * 64 + 32 * h;
             pb[l32] = h ? best1 : best0;
         }
+        // ---- combine tile i-2 (rows 16w..16w+15): max over the 4 block partials -> row masks ----
+        {
+            const int t = i - 2;
+            const int row = 16 * wave + (lane & 15);
+            const int64_t grow = (tbase + (int64_t)((int64_t)t) * tstride) * V5_TR + row;
+            if (lane < 16 && t >= 0 && t < nt && grow < N) {
+                const float* pb = pbest + (int)(ui & 1u) * 256;
+                const float best = fmaxf(fmaxf(pb[row], pb[64 + row]), fmaxf(pb[128 + row], pb[192 + row]));
+                const uint32_t c = __float_as_uint(best) & 127u;
+                __hip_atomic_fetch_or(masks + (int)((ui + 1) % 3u) * 256 + c * 2 + (row >> 5), 1u << (row & 31),
+                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+        }
+        // ---- accumulate tile i-3 for the own block ----
+        {
+            const int po = (int)((ui + V5_NBUF - 3) % V5_NBUF) * V5_TILE;
+            cnt += (h == 0) ? (float)(__popc(mw0) + __popc(mw1)) : 0.f;
+            mp[h] = 0u;  // both halves read the same pair; lane h clears word h
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+#pragma unroll
+                for (int db = 0; db < 4; ++db) {
+                    const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+                        (__attribute__((address_space(3))) bf16x4*)(uintptr_t)(tbl[db] + po + s * 4096));
+                    const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+                        (__attribute__((address_space(3))) bf16x4*)(uintptr_t)(tbh[db] + po + s * 4096));
+                    const bf16x8 bv = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                    sacc[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[s], bv, sacc[db], 0, 0, 0);
+                }
+            }
+        }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    };
+    for (int i = 0; i < total; i += 2) {
+        body(i, accA, accB);
+        body(i + 1, accB, accA);
     }
 
     float* S = slab + (int64_t)blockIdx.x * 128 * D;
@@ -1196,6 +1219,229 @@ __global__ __launch_bounds__(256, 1) void kmeans_assign_accum_v5_kernel(
             S[c * D + 32 * db + l32] = sacc[db][r];
         }
     if (h == 0) slab_cnt[(int64_t)blockIdx.x * 128 + 32 * wave + l32] = cnt;
+}
+
+// ---------------------------------------------------------------------------------------------------
+// v6: v5's block-owning schedule on 8 waves (512 threads, two waves per SIMD) so one wave's LDS/MFMA
+// latency stalls are covered by its SIMD partner.  Wave w: centroid block cb = w & 3, half = w >> 2.
+//   distance: rows 32*half..+31 of the tile vs block cb (9 MFMAs); combine: rows 8w..8w+7;
+//   accumulate: block cb x d-blocks {2*half, 2*half+1} (8 MFMAs).  <= 256 registers per wave.
+// Same 64-row tiles / 8-deep ring / 4-stage skew as v5; mask words of tile t are cleared one iteration
+// after they are consumed (both halves read them).
+// ---------------------------------------------------------------------------------------------------
+__device__ __forceinline__ void v6_stage(char* lds, int buf, const char* X, int64_t row0, int64_t N,
+                                         const uint32_t (&voff)[2], int wave) {
+    const int64_t rem = (N - row0) * ROWB;
+    const int nbytes = rem < V5_TILE ? (int)rem : V5_TILE;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(X + row0 * ROWB), (short)0, nbytes, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const uint32_t m0v = __builtin_amdgcn_readfirstlane(
+            (uint32_t)(uintptr_t)LDS_PTR(lds + buf * V5_TILE + i * 8192 + wave * 1024));
+        uint32_t keep;
+        asm volatile(
+            "s_mov_b32 %0, m0\n\t"
+            "s_mov_b32 m0, %3\n\t"
+            "s_nop 0\n\t"
+            "buffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
+            "s_mov_b32 m0, %0"
+            : "=&s"(keep)
+            : "v"(voff[i]), "s"(rs), "s"(m0v)
+            : "memory");
+    }
+}
+
+template <int KB, bool LOAD_ONLY = false, bool COMPUTE_ONLY = false>
+__global__ __launch_bounds__(512, 1) void kmeans_assign_accum_v6_kernel(
+    const __bf16* __restrict__ Xp, int64_t N, const __bf16* __restrict__ Cp, const float* __restrict__ ninit,
+    float* __restrict__ slab, float* __restrict__ slab_cnt, int64_t ntiles, int64_t per) {
+    __shared__ __attribute__((aligned(16))) char lds[V5_LDS_BYTES];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int cb = wave & 3;
+    const int half = wave >> 2;
+    const int h = lane >> 5;
+    const int l32 = lane & 31;
+    const char* X = reinterpret_cast<const char*>(Xp);
+    const int64_t G = gridDim.x;
+    const int64_t tbase = per > 0 ? (int64_t)blockIdx.x * per : (int64_t)blockIdx.x;
+    const int64_t tstride = per > 0 ? 1 : G;
+    const int64_t my_ntiles = per > 0 ? (ntiles > tbase ? (ntiles - tbase < per ? ntiles - tbase : per) : 0)
+                                      : ((ntiles > (int64_t)blockIdx.x) ? (ntiles - 1 - blockIdx.x) / G + 1 : 0);
+    const bool active = cb < KB;
+
+    uint32_t voff[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int p = i * 8192 + tid * 16;
+        const int row = p >> 8;
+        const int chp = (p >> 4) & 15;
+        voff[i] = (uint32_t)(row * ROWB + 16 * (chp ^ (((row & 3) << 2) | ((row >> 2) & 3))));
+    }
+    {
+        uint4* ring = reinterpret_cast<uint4*>(lds);
+        for (int e = tid; e < (int)(V5_NBUF * V5_TILE / 16); e += 512) ring[e] = uint4{0u, 0u, 0u, 0u};
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+    for (int s = 0; s < V5_AHEAD; ++s)
+        if (s < my_ntiles && !COMPUTE_ONLY) v6_stage(lds, s, X, (tbase + (int64_t)s * tstride) * V5_TR, N, voff, wave);
+    {
+        uint32_t* lut = reinterpret_cast<uint32_t*>(lds + V5_OFF_LUT);
+        for (int e = tid; e < 256 * 4; e += 512) {
+            const int ent = e >> 2, pair = e & 3;
+            const uint32_t b0 = (ent >> (2 * pair)) & 1, b1 = (ent >> (2 * pair + 1)) & 1;
+            lut[e] = (b0 ? 0x3F80u : 0u) | (b1 ? 0x3F800000u : 0u);
+        }
+        uint32_t* m = reinterpret_cast<uint32_t*>(lds + V5_OFF_MASK);
+        for (int e = tid; e < 3 * 128 * 2; e += 512) m[e] = 0u;
+        float* pb = reinterpret_cast<float*>(lds + V5_OFF_PBEST);
+        for (int e = tid; e < 2 * 4 * 64; e += 512) pb[e] = -3.0e38f;
+    }
+    bf16x8 cf[8];
+    bf16x8 cn;
+    const __bf16 one = (__bf16)1.0f, zb = (__bf16)0.0f;
+    {
+#pragma unroll
+        for (int s = 0; s < 8; ++s)
+            cf[s] = active ? *reinterpret_cast<const bf16x8*>(Cp + (32 * cb + l32) * D + 16 * s + 8 * h)
+                           : bf16x8{zb, zb, zb, zb, zb, zb, zb, zb};
+        const float v = active ? ninit[32 * cb + l32] : -3.0e38f;
+        const __bf16 p0 = (__bf16)v;
+        const float r1 = v - (float)p0;
+        const __bf16 p1 = (__bf16)r1;
+        const __bf16 p2 = (__bf16)(r1 - (float)p1);
+        cn = (h == 0) ? bf16x8{p0, p1, p2, zb, zb, zb, zb, zb} : bf16x8{zb, zb, zb, zb, zb, zb, zb, zb};
+#pragma unroll
+        for (int s = 0; s < 8; ++s) asm volatile("" ::"v"(cf[s]));
+        asm volatile("" ::"v"(cn));
+    }
+    const bf16x8 ones = (h == 0) ? bf16x8{one, one, one, zb, zb, zb, zb, zb} : bf16x8{zb, zb, zb, zb, zb, zb, zb, zb};
+    int xr[8];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) xr[s] = xoff(32 * half + l32, 2 * s + h);
+    int tbl[2], tbh[2];
+    {
+        const int g = lane >> 4, i16 = lane & 15, q = i16 >> 2, p = i16 & 3;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int db = 2 * half + j;
+            const int ch = 4 * db + 2 * (g & 1) + (p >> 1);
+            tbl[j] = (int)(uintptr_t)LDS_PTR(lds) + xoff(8 * (g >> 1) + q, ch) + 8 * (p & 1);
+            tbh[j] = (int)(uintptr_t)LDS_PTR(lds) + xoff(8 * (g >> 1) + q + 4, ch) + 8 * (p & 1);
+        }
+    }
+    f32x16 sacc[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sacc[j][r] = 0.f;
+    float cnt = 0.f;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    float* pbest = reinterpret_cast<float*>(lds + V5_OFF_PBEST);
+    uint32_t* masks = reinterpret_cast<uint32_t*>(lds + V5_OFF_MASK);
+    const int nt = (int)my_ntiles;
+    const int total = (nt + 3 + 1) & ~1;
+    f32x16 accA, accB;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) accA[r] = accB[r] = -3.0e38f;
+
+    auto body = [&](const int i, f32x16& acc, const f32x16& accp) {
+        const uint32_t ui = (uint32_t)i;
+        if (i < nt && !COMPUTE_ONLY) {
+            const int after = nt - 1 - i;
+            if (after >= 3) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+            else if (after == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            else if (after == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (i + V5_AHEAD < nt && !COMPUTE_ONLY)
+            v6_stage(lds, (int)((ui + V5_AHEAD) % V5_NBUF), X,
+                     (tbase + (int64_t)(i + V5_AHEAD) * tstride) * V5_TR, N, voff, wave);
+        if constexpr (LOAD_ONLY) return;
+        // masks of tile i-3 (set i%3); the set consumed last iteration ((i+2)%3) is cleared by half 0
+        uint32_t* mp = masks + (int)(ui % 3u) * 256 + (32 * cb + l32) * 2;
+        const uint32_t mw0 = mp[0], mw1 = mp[1];
+        if (half == 0) masks[(int)((ui + 2) % 3u) * 256 + (32 * cb + l32) * 2 + h] = 0u;
+        bf16x8 af[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const uint32_t word = (s >> 1) ? mw1 : mw0;
+            const uint32_t byte = (word >> (16 * (s & 1) + 8 * h)) & 255u;
+            af[s] = *reinterpret_cast<const bf16x8*>(lds + V5_OFF_LUT + byte * 16);
+        }
+        // ---- distance of tile i (own rows, own block); argmax of tile i-1 in the gaps ----
+        float best = -3.0e38f;
+        {
+            const int cur = (int)(ui % V5_NBUF) * V5_TILE;
+            const f32x16 z = {};
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cn, ones, z, 0, 0, 0);
+#pragma unroll
+            for (int s = 0; s < 8; ++s) {
+                const bf16x8 xv = *reinterpret_cast<const bf16x8*>(lds + cur + xr[s]);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cf[s], xv, acc, 0, 0, 0);
+#pragma unroll
+                for (int t2 = 0; t2 < 2; ++t2) {
+                    const int r = 2 * s + t2;
+                    const uint32_t c = 32 * cb + (r & 3) + 8 * (r >> 2) + 4 * h;
+                    best = fmaxf(best, __uint_as_float((__float_as_uint(accp[r]) & 0xFFFFFF80u) | c));
+                }
+            }
+        }
+        best = fmaxf(best, __shfl_xor(best, 32));
+        if (h == 0) pbest[(int)((ui + 1) & 1u) * 256 + cb * 64 + 32 * half + l32] = best;
+        // ---- combine tile i-2 (rows 8w..8w+7) ----
+        {
+            const int t = i - 2;
+            const int row = 8 * wave + (lane & 7);
+            const int64_t grow = (tbase + (int64_t)t * tstride) * V5_TR + row;
+            if (lane < 8 && t >= 0 && t < nt && grow < N) {
+                const float* pb = pbest + (int)(ui & 1u) * 256;
+                const float bb = fmaxf(fmaxf(pb[row], pb[64 + row]), fmaxf(pb[128 + row], pb[192 + row]));
+                const uint32_t c = __float_as_uint(bb) & 127u;
+                __hip_atomic_fetch_or(masks + (int)((ui + 1) % 3u) * 256 + c * 2 + (row >> 5), 1u << (row & 31),
+                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+        }
+        // ---- accumulate tile i-3: block cb x d-blocks 2*half, 2*half+1 ----
+        {
+            const int po = (int)((ui + V5_NBUF - 3) % V5_NBUF) * V5_TILE;
+            cnt += (h == 0 && half == 0) ? (float)(__popc(mw0) + __popc(mw1)) : 0.f;
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+                        (__attribute__((address_space(3))) bf16x4*)(uintptr_t)(tbl[j] + po + s * 4096));
+                    const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+                        (__attribute__((address_space(3))) bf16x4*)(uintptr_t)(tbh[j] + po + s * 4096));
+                    const bf16x8 bv = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                    sacc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[s], bv, sacc[j], 0, 0, 0);
+                }
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    };
+    for (int i = 0; i < total; i += 2) {
+        body(i, accA, accB);
+        body(i + 1, accB, accA);
+    }
+
+    float* S = slab + (int64_t)blockIdx.x * 128 * D;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int c = 32 * cb + (r & 3) + 8 * (r >> 2) + 4 * h;
+            S[c * D + 32 * (2 * half + j) + l32] = sacc[j][r];
+        }
+    if (h == 0 && half == 0) slab_cnt[(int64_t)blockIdx.x * 128 + 32 * cb + l32] = cnt;
 }
 
 // fixed-order fp64 reduction of the per-workgroup slabs -> out[k][D+1] (last column = count)
@@ -1282,15 +1528,16 @@ int alink_kmeans_assign_accum_bf16_v3(const void* X, int64_t N, const void* C, c
 }
 
 int alink_kmeans_assign_accum_bf16_v4(const void* X, int64_t N, const void* C, const float* ninit, int k,
-                                      float* slab, float* slab_cnt, int grid, void* stream) {
+                                      float* slab, float* slab_cnt, int grid, void* stream, int contiguous) {
     if (N <= 0 || k < 1 || k > 128 || grid <= 0) return -1;
     const int KB = (k + 31) / 32;
     const int64_t ntiles = (N + TR - 1) / TR;
     if (grid > ntiles) grid = (int)ntiles;
+    const int64_t per = contiguous ? (ntiles + grid - 1) / grid : 0;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
 #define V4_LAUNCH(KBV)                                                                                   \
     hipLaunchKernelGGL(kmeans_assign_accum_v4_kernel<KBV>, dim3(grid), dim3(256), 0, st, (const __bf16*)X, N, \
-                       (const __bf16*)C, ninit, slab, slab_cnt, ntiles)
+                       (const __bf16*)C, ninit, slab, slab_cnt, ntiles, per)
     switch (KB) {
         case 1: V4_LAUNCH(1); break;
         case 2: V4_LAUNCH(2); break;
@@ -1302,15 +1549,16 @@ int alink_kmeans_assign_accum_bf16_v4(const void* X, int64_t N, const void* C, c
 }
 
 int alink_kmeans_assign_accum_bf16_v5(const void* X, int64_t N, const void* C, const float* ninit, int k,
-                                      float* slab, float* slab_cnt, int grid, void* stream) {
+                                      float* slab, float* slab_cnt, int grid, void* stream, int contiguous) {
     if (N <= 0 || k < 1 || k > 128 || grid <= 0) return -1;
     const int KB = (k + 31) / 32;
     const int64_t ntiles = (N + V5_TR - 1) / V5_TR;
     if (grid > ntiles) grid = (int)ntiles;
+    const int64_t per = contiguous ? (ntiles + grid - 1) / grid : 0;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
 #define V5_LAUNCH(KBV)                                                                                   \
     hipLaunchKernelGGL(kmeans_assign_accum_v5_kernel<KBV>, dim3(grid), dim3(256), 0, st, (const __bf16*)X, N, \
-                       (const __bf16*)C, ninit, slab, slab_cnt, ntiles)
+                       (const __bf16*)C, ninit, slab, slab_cnt, ntiles, per)
     switch (KB) {
         case 1: V5_LAUNCH(1); break;
         case 2: V5_LAUNCH(2); break;
@@ -1318,6 +1566,37 @@ int alink_kmeans_assign_accum_bf16_v5(const void* X, int64_t N, const void* C, c
         default: V5_LAUNCH(4); break;
     }
 #undef V5_LAUNCH
+    return (int)hipGetLastError();
+}
+
+int alink_kmeans_assign_accum_bf16_v6(const void* X, int64_t N, const void* C, const float* ninit, int k,
+                                      float* slab, float* slab_cnt, int grid, void* stream, int contiguous) {
+    if (N <= 0 || k < 1 || k > 128 || grid <= 0) return -1;
+    const int KB = (k + 31) / 32;
+    const int64_t ntiles = (N + V5_TR - 1) / V5_TR;
+    if (grid > ntiles) grid = (int)ntiles;
+    const int64_t per = contiguous ? (ntiles + grid - 1) / grid : 0;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (contiguous == 4) {  // diagnostics: the compute alone (tiles never loaded; results meaningless)
+        hipLaunchKernelGGL((kmeans_assign_accum_v6_kernel<4, false, true>), dim3(grid), dim3(512), 0, st,
+                           (const __bf16*)X, N, (const __bf16*)C, ninit, slab, slab_cnt, ntiles, per);
+        return (int)hipGetLastError();
+    }
+    if (contiguous >= 2) {  // diagnostics: the load pipeline alone (no compute; slabs not written)
+        hipLaunchKernelGGL((kmeans_assign_accum_v6_kernel<4, true>), dim3(grid), dim3(512), 0, st, (const __bf16*)X,
+                           N, (const __bf16*)C, ninit, slab, slab_cnt, ntiles, contiguous == 2 ? per : 0);
+        return (int)hipGetLastError();
+    }
+#define V6_LAUNCH(KBV)                                                                                   \
+    hipLaunchKernelGGL(kmeans_assign_accum_v6_kernel<KBV>, dim3(grid), dim3(512), 0, st, (const __bf16*)X, N, \
+                       (const __bf16*)C, ninit, slab, slab_cnt, ntiles, per)
+    switch (KB) {
+        case 1: V6_LAUNCH(1); break;
+        case 2: V6_LAUNCH(2); break;
+        case 3: V6_LAUNCH(3); break;
+        default: V6_LAUNCH(4); break;
+    }
+#undef V6_LAUNCH
     return (int)hipGetLastError();
 }
 

@@ -20,7 +20,8 @@ from . import _lib
 __all__ = ["assign_accumulate", "assign", "assign_accumulate_torch", "hip_supported", "prepare_centroids"]
 
 _BUF: Dict[Tuple, Tuple[torch.Tensor, torch.Tensor]] = {}
-DEFAULT_VARIANT = 1
+DEFAULT_VARIANT = None  # None -> per-k choice below (measured on MI355X, profiles/kmeans_variants.txt)
+DEFAULT_CONTIGUOUS = True  # v4/v5: contiguous tile run per workgroup (vs grid-strided tiles)
 HIP_D = 128
 HIP_KMAX = 128
 
@@ -41,14 +42,21 @@ def prepare_centroids(C: torch.Tensor, device) -> Tuple[torch.Tensor, torch.Tens
     return cpad, ninit
 
 
+def pick_variant(k: int) -> int:
+    """v4 (row-owning waves, 128-row tiles) wins while k <= 64 (two centroid blocks); beyond that the
+    block-owning 8-wave v6 is fastest (1e8 x 128, MI355X: k=32 5.1 ms, k=64 5.5 ms (v4); k=100 8.2 ms (v6))."""
+    return 4 if k <= 64 else 6
+
+
 def _num_cus(device) -> int:
     return torch.cuda.get_device_properties(device).multi_processor_count
 
 
 def assign_accumulate_hip(X: torch.Tensor, C: torch.Tensor, grid: Optional[int] = None,
-                          variant: Optional[int] = None) -> torch.Tensor:
+                          variant: Optional[int] = None, contiguous: Optional[bool] = None) -> torch.Tensor:
     L = _lib.require()
-    variant = DEFAULT_VARIANT if variant is None else variant
+    if variant is None:
+        variant = DEFAULT_VARIANT if DEFAULT_VARIANT is not None else pick_variant(C.shape[0])
     dev = X.device
     k = C.shape[0]
     if not hip_supported(X, k):
@@ -57,7 +65,7 @@ def assign_accumulate_hip(X: torch.Tensor, C: torch.Tensor, grid: Optional[int] 
     n = X.shape[0]
     if grid is None:
         grid = _num_cus(dev)
-    ntiles = (n + 127) // 128 if variant not in (3, 5) else (n + 63) // 64
+    ntiles = (n + 127) // 128 if variant not in (3, 5, 6) else (n + 63) // 64
     grid = max(1, min(grid, ntiles))
     key = (dev.index, grid)
     if key not in _BUF:
@@ -68,10 +76,13 @@ def assign_accumulate_hip(X: torch.Tensor, C: torch.Tensor, grid: Optional[int] 
     st = _lib.stream_ptr(dev)
     fn = {1: L.alink_kmeans_assign_accum_bf16, 2: L.alink_kmeans_assign_accum_bf16_v2,
           3: L.alink_kmeans_assign_accum_bf16_v3, 4: L.alink_kmeans_assign_accum_bf16_v4,
-          5: L.alink_kmeans_assign_accum_bf16_v5}[variant]
+          5: L.alink_kmeans_assign_accum_bf16_v5, 6: L.alink_kmeans_assign_accum_bf16_v6}[variant]
     if variant == 2 and k > 64:
         raise ValueError("variant 2 spills registers for k > 64")
-    rc = fn(X.data_ptr(), n, cpad.data_ptr(), ninit.data_ptr(), k, slab.data_ptr(), slab_cnt.data_ptr(), grid, st)
+    args = [X.data_ptr(), n, cpad.data_ptr(), ninit.data_ptr(), k, slab.data_ptr(), slab_cnt.data_ptr(), grid, st]
+    if variant in (4, 5, 6):
+        args.append(int(DEFAULT_CONTIGUOUS if contiguous is None else contiguous))
+    rc = fn(*args)
     if rc != 0:
         raise RuntimeError(f"alink_kmeans_assign_accum_bf16 failed: {rc}")
     rc = L.alink_kmeans_reduce_slabs(slab.data_ptr(), slab_cnt.data_ptr(), grid, k, out.data_ptr(), st)

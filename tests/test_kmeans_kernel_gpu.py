@@ -14,7 +14,7 @@ def _data(n, k, seed=0, dev="cuda"):
     return X, C
 
 
-@pytest.mark.parametrize("variant", [1, 3, 4, 5])
+@pytest.mark.parametrize("variant", [1, 3, 4, 5, 6])
 @pytest.mark.parametrize("n,k", [(1, 1), (127, 3), (128, 32), (1000, 33), (4097, 100), (50000, 128), (300001, 100)])
 def test_assign_accumulate_matches_reference(n, k, variant):
     from alink_amd.ops import kmeans as K
@@ -30,6 +30,19 @@ def test_assign_accumulate_matches_reference(n, k, variant):
     assert abs(got[:, -1].sum().item() - n) < 0.5
     if dc == 0:
         torch.testing.assert_close(got[:, :-1], ref[:, :-1], rtol=1e-5, atol=1e-3 * max(1.0, n / 1000))
+
+
+@pytest.mark.parametrize("variant,contig", [(1, None), (4, True), (4, False), (5, True), (5, False), (6, True), (6, False)])
+@pytest.mark.parametrize("n,k,grid", [(200, 7, 1), (49157, 100, 3), (33333, 64, 7), (640, 100, 2), (70000, 100, 256)])
+def test_assign_accumulate_small_grid(n, k, grid, variant, contig):
+    """Few workgroups -> long per-workgroup tile loops (pipeline warm-up, steady state and drain)."""
+    from alink_amd.ops import kmeans as K
+    X, C = _data(n, k, seed=11)
+    got = K.assign_accumulate_hip(X, C, grid=grid, variant=variant, contiguous=contig)
+    ref = K.assign_accumulate_torch(X, C)
+    torch.cuda.synchronize()
+    assert (got[:, -1] - ref[:, -1]).abs().sum().item() <= 2
+    assert abs(got[:, -1].sum().item() - n) < 0.5
 
 
 def test_kernel_deterministic():
