@@ -140,9 +140,15 @@ def gson_dumps(v: Any, java_map_order: bool = True) -> str:
     if isinstance(v, str):
         return _gson_escape(v)
     if hasattr(v, "__gson_fields__"):
+        # POJO fields in declaration order; null fields are written as null (what the reference's model
+        # tables show, e.g. docs/en/aftsurvivalregression.md) unless the class sets __gson_skip_nulls__
+        keep_nulls = not getattr(v, "__gson_skip_nulls__", False)
         parts = []
         for f in v.__gson_fields__:
-            parts.append(_gson_escape(f) + ":" + gson_dumps(getattr(v, f), java_map_order))
+            fv = getattr(v, f, None)
+            if fv is None and not keep_nulls:
+                continue
+            parts.append(_gson_escape(f) + ":" + gson_dumps(fv, java_map_order))
         return "{" + ",".join(parts) + "}"
     if isinstance(v, dict):
         keys = java_hashmap_order(list(v.keys())) if java_map_order else list(v.keys())

@@ -1,0 +1,443 @@
+"""Distributed optimizers on the BSP queue: L-BFGS, OWL-QN, GD, SGD, Newton.
+
+Each optimizer is an ``IterativeComQueue`` with the same items, buffers and update rules as the reference:
+
+* ``Lbfgs.java:55-175``  — CalcGradient -> AllReduce(grad) -> two-loop direction (m = 10 corrections,
+  no initial Hessian scaling) -> CalcLosses at ``numSearchStep + 1`` step sizes -> AllReduce(losses) ->
+  ``UpdateModel`` (adaptive learning rate, ``subfunc/UpdateModel.java:68-176``);
+* ``Owlqn.java`` — the same with the L1 pseudo-gradient, direction sign projection and orthant-wise
+  coefficient clipping;
+* ``Gd.java`` — steepest descent with the same search;
+* ``Sgd.java:82-200`` — sampled mini-batch gradient, ``eta = lr / (|g|_inf + sqrt(step))``;
+* ``Newton.java`` — gradient + Hessian all-reduce, ``H x = g`` solve, full step.
+
+MI355X design: all state (coefficients, the L-BFGS ``s_k / y_k`` history, directions) is a device tensor;
+the gradient of a partition is one GEMV pair (or CSR segment-sum) and the line search evaluates all step
+sizes from ONE pass over the samples (``X @ [coef, dir]``).  The only host synchronisations per superstep
+are the scalar decisions of ``UpdateModel`` (which step won, convergence), exactly the values the reference
+computes on every task.  All tasks hold bit-identical state after each all-reduce, so the termination
+criterion is evaluated locally (no broadcast).
+"""
+from __future__ import annotations
+
+import math
+from typing import List, Optional, Tuple
+
+import numpy as np
+import torch
+
+from ...common.params import Params
+from ...parallel.comqueue import (AllReduce, ComputeFunction, CompareCriterionFunction, CompleteResultFunction,
+                                  IterativeComQueue)
+from .objfunc import LabeledData, OptimObjFunc
+
+__all__ = ["optimize", "OptimMethodName", "NUM_CORRECTIONS", "LEARNING_RATE"]
+
+NUM_CORRECTIONS = 10        # OptimVariable.numCorrections
+LEARNING_RATE = 0.1         # OptimVariable.learningRate
+EPS = 1.0e-18               # UpdateModel.EPS
+
+TRAIN, MODEL, OBJ = "trainData", "model", "objFunc"
+CUR, MIN, CURVE = "currentCoef", "minCoef", "lossCurve"
+DIR, GRAD, PSE = "direction", "gradient", "pseGradient"
+GRAD_AR, LOSS_AR, SKYK, GH_AR = "gradAllReduce", "lossAllReduce", "sKyK", "gradHessAllReduce"
+
+
+class OptimMethodName:
+    LBFGS, OWLQN, GD, SGD, NEWTON = "LBFGS", "OWLQN", "GD", "SGD", "Newton"
+
+
+class _State:
+    """(vector, scalars) pair — the reference's ``Tuple2<DenseVector, double[]>`` / ``Tuple2<DenseVector,Double>``."""
+    __slots__ = ("v", "f")
+
+    def __init__(self, v, f):
+        self.v, self.f = v, f
+
+
+# ---------------------------------------------------------------------------------------------------
+# preallocation
+# ---------------------------------------------------------------------------------------------------
+class _Preallocate(ComputeFunction):
+    def __init__(self, max_iter: int, method: str):
+        self.max_iter, self.method = max_iter, method
+
+    def calc(self, ctx):
+        if ctx.getStepNo() != 1:
+            return
+        coef = ctx.getObj(MODEL)
+        coef = coef.to(device=ctx.device or coef.device, dtype=torch.float64).clone()
+        ctx.putObj(CUR, _State(coef.clone(), 1.7976931348623157e308))
+        ctx.putObj(MIN, _State(coef.clone(), 1.7976931348623157e308))
+        ctx.putObj(CURVE, np.full(self.max_iter, np.inf))
+        ctx.putObj(DIR, _State(torch.zeros_like(coef), [0.0, LEARNING_RATE if self.method != OptimMethodName.SGD
+                                                          else 0.0]))
+        ctx.putObj(GRAD, _State(torch.zeros_like(coef), [0.0]))
+        ctx.putObj(PSE, _State(torch.zeros_like(coef), [0.0]))
+        if self.method in (OptimMethodName.LBFGS, OptimMethodName.OWLQN):
+            d = coef.shape[0]
+            ctx.putObj(SKYK, (torch.zeros((NUM_CORRECTIONS, d), dtype=torch.float64, device=coef.device),
+                              torch.zeros((NUM_CORRECTIONS, d), dtype=torch.float64, device=coef.device)))
+            ctx.putObj("oldGradient", None)
+
+
+# ---------------------------------------------------------------------------------------------------
+# gradient / losses
+# ---------------------------------------------------------------------------------------------------
+class CalcGradient(ComputeFunction):
+    def calc(self, ctx):
+        data: LabeledData = ctx.getObj(TRAIN)
+        obj: OptimObjFunc = ctx.getObj(OBJ)
+        coef = ctx.getObj(CUR).v
+        g, ws = obj.calc_gradient(data, coef)
+        ctx.getObj(DIR).v = g
+        buf = torch.empty(coef.shape[0] + 1, dtype=torch.float64, device=coef.device)
+        buf[:-1] = g * ws
+        buf[-1] = ws
+        ctx.putObj(GRAD_AR, buf)
+
+
+class CalcLosses(ComputeFunction):
+    def __init__(self, method: str, num_search_step: int):
+        self.method, self.ns = method, num_search_step
+
+    def calc(self, ctx):
+        data = ctx.getObj(TRAIN)
+        obj = ctx.getObj(OBJ)
+        d = ctx.getObj(DIR)
+        coef = ctx.getObj(CUR).v
+        beta = d.f[1] / self.ns
+        if self.method == OptimMethodName.OWLQN:
+            vec = obj.constraint_calc_search_values(data, coef, d.v, beta, self.ns)
+        else:
+            vec = obj.calc_search_values(data, coef, d.v, beta, self.ns)
+        ctx.putObj(LOSS_AR, vec.to(torch.float64).clone())
+
+
+def _two_loop(ctx, grad_vec, start_dir, k):
+    """L-BFGS two-loop recursion over the stored corrections (``Lbfgs.CalDirection`` :109-175).
+
+    Kept entirely on the device: a correction pair with ``s.y == 0`` is skipped in the reference; here its
+    ``rho`` is 0, which makes the same update a no-op without a host round trip."""
+    sK, yK = ctx.getObj(SKYK)
+    m = NUM_CORRECTIONS
+    dirv = start_dir.clone()
+    delta = k - m if k > m else 0
+    l = k if k <= m else m
+    if l == 0:
+        return dirv
+    order = [(i + delta) % m for i in range(l)]
+    S, Y = sK[order], yK[order]                      # [l, d]
+    dots = (S * Y).sum(1)
+    rho = torch.where(dots.abs() > 0, 1.0 / torch.where(dots == 0, torch.ones_like(dots), dots),
+                      torch.zeros_like(dots))
+    alpha = torch.zeros(l, dtype=dirv.dtype, device=dirv.device)
+    for i in range(l - 1, -1, -1):
+        alpha[i] = rho[i] * torch.dot(S[i], dirv)
+        dirv = dirv - alpha[i] * Y[i]
+    for i in range(l):
+        beta_i = rho[i] * torch.dot(Y[i], dirv)
+        dirv = dirv + (alpha[i] - beta_i) * S[i]
+    return dirv
+
+
+def _update_history(ctx, grad_vec, k):
+    sK, yK = ctx.getObj(SKYK)
+    old = ctx.getObj("oldGradient")
+    if k > 0:
+        yK[(k - 1) % NUM_CORRECTIONS] = grad_vec - old
+    ctx.putObj("oldGradient", grad_vec.clone())
+
+
+class LbfgsDirection(ComputeFunction):
+    def calc(self, ctx):
+        arr = ctx.getObj(GRAD_AR)
+        size = arr.shape[0] - 1
+        ws = float(arr[size].item())
+        g = arr[:size] / ws
+        ctx.getObj(GRAD).v = g
+        d = ctx.getObj(DIR)
+        d.f[0] = ws
+        k = ctx.getStepNo() - 1
+        _update_history(ctx, g, k)
+        d.v = _two_loop(ctx, g, g, k)
+
+
+class OwlqnDirection(ComputeFunction):
+    def __init__(self, l1: float):
+        self.l1 = float(l1)
+
+    def calc(self, ctx):
+        arr = ctx.getObj(GRAD_AR)
+        size = arr.shape[0] - 1
+        ws = float(arr[size].item())
+        g = arr[:size] / ws
+        ctx.getObj(GRAD).v = g
+        d = ctx.getObj(DIR)
+        d.f[0] = ws
+        coef = ctx.getObj(CUR).v
+        if abs(self.l1) > 0.0:
+            pse = torch.where(coef == 0.0,
+                              torch.where(g - self.l1 > 0, g - self.l1,
+                                          torch.where(g + self.l1 < 0, g + self.l1, torch.zeros_like(g))), g)
+        else:
+            pse = g.clone()
+        ctx.getObj(PSE).v = pse
+        k = ctx.getStepNo() - 1
+        _update_history(ctx, g, k)
+        dirv = _two_loop(ctx, g, pse, k)
+        if abs(self.l1) > 0.0:
+            dirv = torch.where(dirv * pse < 0, torch.zeros_like(dirv), dirv)
+        d.v = dirv
+
+
+class GdDirection(ComputeFunction):
+    def calc(self, ctx):
+        arr = ctx.getObj(GRAD_AR)
+        size = arr.shape[0] - 1
+        d = ctx.getObj(DIR)
+        d.v = arr[:size] / arr[size]
+        d.f[0] = float(arr[size].item())
+
+
+class UpdateModel(ComputeFunction):
+    """Adaptive-step line search result + stopping rules (``subfunc/UpdateModel.java:47-176``)."""
+
+    def __init__(self, method: str, grad_name: str, num_search_step: int, epsilon: float, max_iter: int):
+        self.method, self.grad_name, self.ns = method, grad_name, num_search_step
+        self.epsilon, self.max_iter = epsilon, max_iter
+
+    def calc(self, ctx):
+        losses = (ctx.getObj(LOSS_AR) / ctx.getObj(DIR).f[0]).cpu().tolist()
+        d = ctx.getObj(DIR)
+        cur, mn = ctx.getObj(CUR), ctx.getObj(MIN)
+        curve = ctx.getObj(CURVE)
+        ratio = 1.0
+        pos = -1
+        for j in range(len(losses)):
+            if losses[j] < losses[0]:
+                losses[0] = losses[j]
+                pos = j
+        beta = d.f[1] / self.ns
+        if pos == -1:
+            eta = 0.0
+            d.f[1] *= 1.0 / (self.ns * self.ns)
+            cur.f = losses[0]
+        elif pos == self.ns:
+            eta = beta * pos
+            d.f[1] *= self.ns
+            d.f[1] = min(d.f[1], float(self.ns))
+            ratio = abs((cur.f - losses[pos]) / cur.f)
+            cur.f = losses[self.ns]
+        else:
+            eta = beta * pos
+            ratio = abs((cur.f - losses[pos]) / cur.f)
+            cur.f = losses[pos]
+        step = ctx.getStepNo()
+        curve[step - 1] = cur.f
+        k = step - 1
+        if self.method == OptimMethodName.OWLQN:
+            sK, _ = ctx.getObj(SKYK)
+            val = cur.v
+            new = val - d.v * eta
+            pse = ctx.getObj(PSE).v
+            new = torch.where(val.abs() > 0.0, torch.where(new * val < 0, torch.zeros_like(new), new),
+                              torch.where(new * pse > 0, torch.zeros_like(new), new))
+            sK[k % NUM_CORRECTIONS] = new - val
+            cur.v = new
+        elif self.method == OptimMethodName.LBFGS:
+            sK, _ = ctx.getObj(SKYK)
+            sK[k % NUM_CORRECTIONS] = d.v * (-eta)
+            cur.v = cur.v - eta * d.v
+        else:
+            cur.v = cur.v - eta * d.v
+        if cur.f < mn.f:
+            mn.f = cur.f
+            mn.v = cur.v.clone()
+        # stopping rules
+        gnorm = float(ctx.getObj(self.grad_name).v.norm().item())
+        if cur.f < self.epsilon or gnorm < self.epsilon:
+            d.f[0] = -1.0
+        elif step > self.max_iter - 1:
+            d.f[0] = -1.0
+        elif d.f[1] < EPS:
+            d.f[0] = -1.0
+        elif ratio < self.epsilon and gnorm < math.sqrt(self.epsilon):
+            d.f[0] = -1.0
+        hist = ctx.getObj("history")
+        if hist is not None:
+            hist.append({"step": step, "loss": cur.f, "gradNorm": gnorm, "learningRate": d.f[1]})
+
+
+class SgdSubGradient(ComputeFunction):
+    def __init__(self, fraction: float, seed: int = 0):
+        self.fraction, self.seed = fraction, seed
+
+    def calc(self, ctx):
+        data: LabeledData = ctx.getObj(TRAIN)
+        obj: OptimObjFunc = ctx.getObj(OBJ)
+        n = len(data)
+        bs = int(n * self.fraction)
+        gen = ctx.getObj("sgdGen")
+        if gen is None:
+            gen = torch.Generator(device="cpu").manual_seed(self.seed * 1000003 + ctx.getTaskId())
+            ctx.putObj("sgdGen", gen)
+        coef = ctx.getObj(MIN).v
+        if bs > 0:
+            idx = torch.randint(0, n, (bs,), generator=gen).to(data.device)
+            mb = data[idx]
+            g, ws = obj.calc_gradient(mb, coef)
+            loss, _ = obj.calc_obj_value(mb, coef)
+        else:
+            g, ws, loss = torch.zeros_like(coef), 0.0, 0.0
+        buf = torch.empty(coef.shape[0] + 2, dtype=torch.float64, device=coef.device)
+        buf[:-2] = g * ws
+        buf[-2] = ws
+        buf[-1] = loss
+        ctx.putObj(GRAD_AR, buf)
+
+
+class SgdUpdate(ComputeFunction):
+    def __init__(self, max_iter: int, epsilon: float, lr: float):
+        self.max_iter, self.epsilon, self.lr = max_iter, epsilon, lr
+
+    def calc(self, ctx):
+        arr = ctx.getObj(GRAD_AR)
+        size = arr.shape[0] - 2
+        d = ctx.getObj(DIR)
+        ws = float(arr[size].item())
+        d.v = arr[:size] / ws if ws != 0 else torch.zeros_like(arr[:size])
+        d.f = [ws, float(arr[size + 1].item())]
+        m = ctx.getObj(MIN)
+        step = ctx.getStepNo()
+        eta = self.lr / (float(d.v.abs().max().item()) + math.sqrt(step))
+        m.v = m.v - eta * d.v
+        gnorm = float(d.v.norm().item())
+        if gnorm < self.epsilon or step > self.max_iter - 1:
+            d.f[0] = -1.0
+
+
+class NewtonGradHess(ComputeFunction):
+    def calc(self, ctx):
+        data = ctx.getObj(TRAIN)
+        obj = ctx.getObj(OBJ)
+        coef = ctx.getObj(CUR).v
+        H, g, ws, loss = obj.calc_hessian_gradient_loss(data, coef)
+        size = coef.shape[0]
+        buf = torch.empty(size + size * size + 2, dtype=torch.float64, device=coef.device)
+        buf[:size] = g
+        buf[size:size + size * size] = H.reshape(-1)
+        buf[-2] = ws
+        buf[-1] = loss
+        ctx.putObj(GH_AR, buf)
+
+
+class NewtonUpdate(ComputeFunction):
+    def __init__(self, max_iter: int, epsilon: float):
+        self.max_iter, self.epsilon = max_iter, epsilon
+
+    def calc(self, ctx):
+        arr = ctx.getObj(GH_AR)
+        cur, mn, d = ctx.getObj(CUR), ctx.getObj(MIN), ctx.getObj(DIR)
+        size = cur.v.shape[0]
+        ws = float(arr[-2].item())
+        g = arr[:size] / ws
+        H = arr[size:size + size * size].reshape(size, size) / ws
+        loss = float(arr[-1].item()) / ws
+        gnorm = float(g.norm().item())
+        norm = 1.0 / float(g.abs().sum().item()) if float(g.abs().sum().item()) > 0 else 1.0
+        H = H * norm
+        g = g * norm
+        x = torch.linalg.lstsq(H.cpu(), g.cpu()[:, None]).solution[:, 0].to(g.device)
+        cur.v = cur.v - x
+        cur.f = loss
+        d.v = x
+        d.f = [ws, loss]
+        curve = ctx.getObj(CURVE)
+        step = ctx.getStepNo()
+        curve[step - 1] = loss
+        if cur.f < mn.f:
+            mn.f = cur.f
+            mn.v = cur.v.clone()
+        if cur.f < self.epsilon or gnorm < self.epsilon or step > self.max_iter - 1:
+            d.f[0] = -1.0
+
+
+class IterTermination(CompareCriterionFunction):
+    def calc(self, ctx) -> bool:
+        return ctx.getObj(DIR).f[0] < 0.0
+
+
+class OutputModel(CompleteResultFunction):
+    def calc(self, ctx):
+        if ctx.getTaskId() != 0:
+            return None
+        mn = ctx.getObj(MIN)
+        curve = ctx.getObj(CURVE)
+        eff = len(curve)
+        for i, v in enumerate(curve):
+            if np.isinf(v):
+                eff = i
+                break
+        coef = mn.v.detach().cpu().numpy().astype(np.float64)
+        if not np.all(np.isfinite(coef)):
+            raise RuntimeError("Optimization result has NAN or infinite value, coefficient is invalid")
+        return [(coef, np.asarray(curve[:eff], dtype=np.float64))]
+
+
+def optimize(obj: OptimObjFunc, data: LabeledData, dim: int, params: Params, method: Optional[str] = None,
+             env=None, init_coef: Optional[torch.Tensor] = None, history: Optional[list] = None
+             ) -> Tuple[np.ndarray, np.ndarray]:
+    """Run the selected optimizer over this rank's partition; returns (coef, lossCurve) on every rank.
+
+    Method selection mirrors ``BaseLinearModelTrainBatchOp.optimize`` :229-269: explicit ``optimMethod``,
+    else OWL-QN when ``l1 > 0``, else L-BFGS."""
+    from ...common.mlenv import MLEnvironmentFactory
+
+    def pget(name, default):
+        return params.get(name) if params.contains(name) and params.get(name) is not None else default
+
+    if method is None:
+        om = pget("optimMethod", None)
+        method = (om.name if hasattr(om, "name") else str(om)) if om is not None else \
+            (OptimMethodName.OWLQN if obj.l1 > 0 else OptimMethodName.LBFGS)
+    method = {"LBFGS": "LBFGS", "OWLQN": "OWLQN", "GD": "GD", "SGD": "SGD", "NEWTON": "Newton"}[method.upper()]
+    max_iter = int(pget("maxIter", 100))
+    epsilon = float(pget("epsilon", 1.0e-6))
+    ns = int(pget("numSearchStep", 4))
+    env = env or MLEnvironmentFactory.getDefault()
+    dev = data.device
+    if init_coef is None:
+        init_coef = torch.zeros(dim, dtype=torch.float64, device=dev)
+        init_coef[0] = 1.0e-3   # Optimizer.initCoefZeros
+    q = IterativeComQueue().setMLEnvironment(env)
+    q.initWithPartitionedData(TRAIN, data)
+    q.initWithBroadcastData(MODEL, init_coef.to(dev))
+    q.initWithBroadcastData(OBJ, obj)
+    q.add(_Preallocate(max_iter, method))
+    if method == OptimMethodName.SGD:
+        lr = float(pget("learningRate", 0.1))
+        frac = float(pget("miniBatchFraction", 0.1))
+        q.add(SgdSubGradient(frac, int(pget("randomSeed", 0)))).add(AllReduce(GRAD_AR)) \
+            .add(SgdUpdate(max_iter, epsilon, lr))
+    elif method == OptimMethodName.NEWTON:
+        q.add(NewtonGradHess()).add(AllReduce(GH_AR)).add(NewtonUpdate(max_iter, epsilon))
+    else:
+        q.add(CalcGradient()).add(AllReduce(GRAD_AR))
+        if method == OptimMethodName.LBFGS:
+            q.add(LbfgsDirection())
+            gname = GRAD
+        elif method == OptimMethodName.OWLQN:
+            q.add(OwlqnDirection(obj.l1))
+            gname = GRAD
+        else:
+            q.add(GdDirection())
+            gname = DIR
+        q.add(CalcLosses(method, ns)).add(AllReduce(LOSS_AR)) \
+            .add(UpdateModel(method, gname, ns, epsilon, max_iter))
+    if history is not None:
+        q.initWithBroadcastData("history", history)
+    q.setCompareCriterionOfNode0(IterTermination(), replicated=True).closeWith(OutputModel()).setMaxIter(max_iter)
+    rows = q.exec()
+    coef, curve = rows[0]
+    return coef, curve

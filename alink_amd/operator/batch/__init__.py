@@ -5,3 +5,4 @@ from .utils import *  # noqa: F401,F403
 from .dataproc import *  # noqa: F401,F403
 from .clustering import *  # noqa: F401,F403
 from .sql import *  # noqa: F401,F403
+from .linear import *  # noqa: F401,F403

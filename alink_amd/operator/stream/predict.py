@@ -1,0 +1,37 @@
+"""Stream predict operators: a batch-trained model applied to every micro-batch.
+
+Reference: ``A/operator/stream/{classification,regression,clustering,...}/*PredictStreamOp.java`` — each is a
+``ModelMapStreamOp`` bound to the same ``ModelMapper`` as its batch twin (model pre-collected through
+DirectReader, ``ModelMapStreamOp.java:39-56``).
+"""
+from __future__ import annotations
+
+from ...models.clustering.kmeans import KMeansModelMapper
+from ...models.linear.model import AFTModelMapper, LinearModelMapper, SoftmaxModelMapper
+from .base import ModelMapStreamOp
+
+_PREDICTORS = {
+    "KMeansPredictStreamOp": KMeansModelMapper,
+    "LogisticRegressionPredictStreamOp": LinearModelMapper,
+    "LinearSvmPredictStreamOp": LinearModelMapper,
+    "LinearRegPredictStreamOp": LinearModelMapper,
+    "RidgeRegPredictStreamOp": LinearModelMapper,
+    "LassoRegPredictStreamOp": LinearModelMapper,
+    "SoftmaxPredictStreamOp": SoftmaxModelMapper,
+    "AftSurvivalRegPredictStreamOp": AFTModelMapper,
+}
+
+__all__ = []
+
+
+def register_stream_predictor(name: str, mapper):
+    cls = type(name, (ModelMapStreamOp,), {"MAPPER": mapper, "__module__": __name__,
+                                          "__doc__": f"Stream predict with ``{mapper.__name__}``."})
+    globals()[name] = cls
+    if name not in __all__:
+        __all__.append(name)
+    return cls
+
+
+for _n, _m in _PREDICTORS.items():
+    register_stream_predictor(_n, _m)

@@ -2,3 +2,4 @@
 from .base import *  # noqa: F401,F403
 from .clustering import *  # noqa: F401,F403
 from .dataproc import *  # noqa: F401,F403
+from .linear import *  # noqa: F401,F403

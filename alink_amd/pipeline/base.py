@@ -321,6 +321,12 @@ class PipelineModel(ModelBase):
             transformers = transformers[0]
         self.transformers: List[TransformerBase] = list(transformers)
 
+    def getTransformers(self) -> List[TransformerBase]:
+        return list(self.transformers)
+
+    def getTransformer(self, i: int) -> TransformerBase:
+        return self.transformers[i]
+
     def transformBatch(self, input):
         for t in self.transformers:
             input = t.transform(input)

@@ -1,0 +1,90 @@
+"""Multi-process (gloo, CPU) scenarios for tests/test_distributed.py — each rank is one process, exactly
+like one-process-per-GPU on MI355X but with the gloo backend (the analogue of Flink's LocalEnvironment)."""
+import json
+import os
+import sys
+import traceback
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def _data_frame():
+    import numpy as np
+    import pandas as pd
+    rng = np.random.default_rng(7)
+    X = rng.normal(size=(600, 4))
+    y = (X @ np.array([1.0, -2.0, 0.5, 0.0]) + 0.2 > 0).astype(int)
+    df = pd.DataFrame({f"x{i}": X[:, i] for i in range(4)})
+    df["y"] = y
+    return df
+
+
+def scenario_pi(out):
+    import torch
+    from alink_amd.parallel.comqueue import (AllReduce, ComputeFunction, CompleteResultFunction,
+                                             IterativeComQueue)
+    from alink_amd import useLocalEnv
+
+    env = useLocalEnv(4)   # 2 processes x 2 local tasks
+
+    class Sample(ComputeFunction):
+        def calc(self, ctx):
+            g = torch.Generator().manual_seed(1000 + ctx.getTaskId() * 31 + ctx.getStepNo())
+            pts = torch.rand((20000, 2), generator=g, dtype=torch.float64)
+            inside = float(((pts ** 2).sum(1) <= 1.0).sum())
+            acc = ctx.getObj("acc")
+            if acc is None:
+                acc = torch.zeros(2, dtype=torch.float64)
+            acc = acc + torch.tensor([inside, 20000.0], dtype=torch.float64)
+            ctx.putObj("acc", acc)
+            ctx.putObj("buf", torch.tensor([inside, 20000.0], dtype=torch.float64))
+
+    class Out(CompleteResultFunction):
+        def calc(self, ctx):
+            b = ctx.getObj("buf")
+            return [(ctx.getTaskId(), ctx.getNumTask(), float(4.0 * b[0] / b[1]))]
+
+    rows = IterativeComQueue().setMLEnvironment(env).add(Sample()).add(AllReduce("buf")).closeWith(Out()) \
+        .setMaxIter(3).exec()
+    out["rows"] = rows
+
+
+def scenario_kmeans(out):
+    from alink_amd import useLocalEnv, BatchOperator, KMeansTrainBatchOp, VectorAssemblerBatchOp
+    from alink_amd.operator.batch.source import MemSourceBatchOp
+    df = _data_frame()
+    useLocalEnv(1)
+    src = BatchOperator.fromDataframe(df, schemaStr="x0 double, x1 double, x2 double, x3 double, y int")
+    va = VectorAssemblerBatchOp().setSelectedCols(["x0", "x1", "x2", "x3"]).setOutputCol("v").linkFrom(src)
+    m = KMeansTrainBatchOp().setVectorCol("v").setK(4).setInitMode("RANDOM").setMaxIter(15).linkFrom(va)
+    out["model"] = [list(r) for r in m.collect()]
+
+
+def scenario_lr(out):
+    from alink_amd import useLocalEnv, BatchOperator, LogisticRegressionTrainBatchOp
+    df = _data_frame()
+    useLocalEnv(1)
+    src = BatchOperator.fromDataframe(df, schemaStr="x0 double, x1 double, x2 double, x3 double, y int")
+    m = LogisticRegressionTrainBatchOp().setFeatureCols(["x0", "x1", "x2", "x3"]).setLabelCol("y").linkFrom(src)
+    rows = m.collect()
+    out["coef"] = json.loads(rows[1][1])["coefVector"]["data"]
+
+
+def run(rank, world, port, scenario, outdir):
+    os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
+                       "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "ALINK_DEVICE": "cpu"})
+    out = {}
+    try:
+        globals()["scenario_" + scenario](out)
+    except Exception:
+        out["error"] = traceback.format_exc()
+    with open(os.path.join(outdir, f"{scenario}_{world}_{rank}.json"), "w") as f:
+        json.dump(out, f)
+    from alink_amd.parallel import comm
+    comm.shutdown()
+
+
+if __name__ == "__main__":
+    run(int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), sys.argv[4], sys.argv[5])

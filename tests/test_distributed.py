@@ -1,0 +1,68 @@
+"""Multi-process SPMD runs on CPU (gloo, world_size 2) must agree with the single-process run.
+
+Each rank is a separate Python process started exactly like ``torchrun`` would (RANK/WORLD_SIZE/MASTER_*
+with 127.0.0.1) — the CPU stand-in for one process per MI355X over RCCL."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run(scenario, world, tmp_path):
+    port = _free_port()
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    env.pop("RANK", None)
+    procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "dist_helpers.py"), str(r), str(world), str(port),
+                               scenario, str(tmp_path)], env=env) for r in range(world)]
+    for p in procs:
+        p.wait(timeout=300)
+    outs = []
+    for r in range(world):
+        with open(os.path.join(str(tmp_path), f"{scenario}_{world}_{r}.json")) as f:
+            o = json.load(f)
+        assert "error" not in o, o.get("error")
+        outs.append(o)
+    return outs
+
+
+def test_comqueue_pi_two_processes(tmp_path):
+    outs = _run("pi", 2, tmp_path)
+    rows = outs[0]["rows"]
+    assert outs[1]["rows"] == rows                 # closeWith results gathered on every rank
+    assert sorted(r[0] for r in rows) == [0, 1, 2, 3] and all(r[1] == 4 for r in rows)
+    assert len({r[2] for r in rows}) == 1          # every task sees the all-reduced buffer
+    assert abs(rows[0][2] - np.pi) < 0.05
+
+
+def test_kmeans_two_processes_equal_single(tmp_path):
+    one = _run("kmeans", 1, tmp_path)[0]["model"]
+    two = _run("kmeans", 2, tmp_path)
+    assert two[0]["model"] == two[1]["model"]
+    c1 = [json.loads(r[1]) for r in one[1:]]
+    c2 = [json.loads(r[1]) for r in two[0]["model"][1:]]
+    assert len(c1) == len(c2)
+    for a, b in zip(c1, c2):
+        np.testing.assert_allclose(a["vec"]["data"], b["vec"]["data"], atol=1e-9)
+        assert a["weight"] == b["weight"]
+
+
+def test_logistic_regression_two_processes_equal_single(tmp_path):
+    one = _run("lr", 1, tmp_path)[0]["coef"]
+    two = _run("lr", 2, tmp_path)
+    np.testing.assert_allclose(two[0]["coef"], two[1]["coef"], rtol=0, atol=0)
+    np.testing.assert_allclose(one, two[0]["coef"], rtol=1e-6, atol=1e-8)

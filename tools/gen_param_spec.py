@@ -174,7 +174,7 @@ def main():
         # operator / stage classes
         cm = re.search(r"public\s+(?:final\s+)?(?:abstract\s+)?class\s+(\w+)\s*(?:<[^{]*?>)?\s*"
                        r"(?:extends\s+([\w\.]+)\s*(?:<[^{]*?>)?)?\s*(?:implements\s+([^{]*))?\{", src)
-        if cm and ("/operator/batch/" in path or "/operator/stream/" in path or "/pipeline/" in path):
+        if cm and ("/operator/" in path or "/pipeline/" in path):
             impl = []
             if cm.group(3):
                 s = re.sub(r"<[^<>]*(<[^<>]*>[^<>]*)*>", "", cm.group(3))
