@@ -1,0 +1,473 @@
+"""Evaluation metrics: binary / multi-class / regression summaries and their Params-backed metric objects.
+
+Reference: ``A/operator/common/evaluation/{EvaluationUtil,ClassificationEvaluationUtil,BinaryMetricsSummary,
+MultiMetricsSummary,RegressionMetricsSummary,ConfusionMatrix,ClassificationMetricComputers,EvaluationCurve,
+BaseMetrics,BinaryClassMetrics,MultiClassMetrics,RegressionMetrics}.java``.
+
+MI355X design: a partition's sufficient statistics are built with device kernels — the binary summary is a
+100000-bin probability histogram per class (``bincount`` on the device), the multi-class summary a
+confusion matrix (``bincount`` of ``pred * K + label``), regression a handful of sums — then ONE all-reduce
+merges them across ranks (the reference's ``ReduceBaseMetrics``).  Curves, thresholds and the ~60 derived
+metrics are computed on the host from the merged histograms, with the reference's bin, sampling and
+threshold rules, and stored as a ``Params`` JSON row (``BaseMetrics.serialize``).
+"""
+from __future__ import annotations
+
+import json
+import math
+from typing import Any, Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from ...common.javafmt import gson_dumps
+from ...common.params import Params
+from ...parallel import comm
+
+__all__ = ["DETAIL_BIN_NUMBER", "BaseMetrics", "BinaryClassMetrics", "MultiClassMetrics", "RegressionMetrics",
+           "ClusterMetrics", "build_label_index", "binary_summary", "multi_summary_from_detail",
+           "multi_summary_from_pred", "regression_summary", "binary_metrics", "multi_metrics",
+           "regression_metrics", "parse_detail"]
+
+DETAIL_BIN_NUMBER = 100000
+PROBABILITY_INTERVAL = 0.001
+PROBABILITY_ERROR = 0.00001
+LOG_LOSS_EPS = 1e-15
+PROB_SUM_EPS = 0.01
+
+
+# ---------------------------------------------------------------------------------------------------
+# metric objects
+# ---------------------------------------------------------------------------------------------------
+def _camel(name: str) -> str:
+    return name[0].upper() + name[1:]
+
+
+class BaseMetrics:
+    """Params holder; ``getXxx()`` returns the param named ``Xxx`` (or an alias below)."""
+    _ALIASES: Dict[str, str] = {}
+
+    def __init__(self, params: Optional[Params] = None):
+        self.params = params if params is not None else Params()
+
+    @classmethod
+    def fromRow(cls, row):
+        return cls(Params.fromJson(row[0]))
+
+    def serialize(self):
+        return (self.params.toJson(),)
+
+    def getParams(self) -> Params:
+        return self.params
+
+    def _get(self, name):
+        if not self.params.contains(name):
+            raise KeyError(name)
+        return json.loads(self.params._m[name]) if self.params._m[name] is not None else None
+
+    def __getattr__(self, item):
+        if item.startswith("get") and len(item) > 3:
+            key = self._ALIASES.get(item[3:], item[3:])
+            return lambda *a: self._get_metric(key, *a)
+        raise AttributeError(item)
+
+    def _get_metric(self, key, *args):
+        return self._get(key)
+
+    def __str__(self):
+        return self.params.toJson()
+
+
+class _ClassifierMetrics(BaseMetrics):
+    _ALIASES = {"LabelArray": "LabelArray", "Ks": "K-S", "Auc": "AUC", "Prc": "PRC"}
+
+    def _label_index(self, label):
+        labels = self._get("LabelArray")
+        return labels.index(str(label))
+
+    def _get_metric(self, key, *args):
+        if args:   # per-label value from the *Array param
+            arr = self._get(key + "Array")
+            return arr[self._label_index(args[0])]
+        return self._get(key)
+
+    def getConfusionMatrix(self):
+        return np.asarray(self._get("ConfusionMatrix"), dtype=np.int64)
+
+
+class BinaryClassMetrics(_ClassifierMetrics):
+    def getRocCurve(self):
+        return self._get("RocCurve")
+
+    def getRecallPrecisionCurve(self):
+        return self._get("RecallPrecisionCurve")
+
+    def getLiftChart(self):
+        return self._get("LiftChart")
+
+    def getThresholdArray(self):
+        return self._get("ThresholdArray")
+
+
+class MultiClassMetrics(_ClassifierMetrics):
+    pass
+
+
+class RegressionMetrics(BaseMetrics):
+    _ALIASES = {"Sse": "SSE", "Sst": "SST", "Ssr": "SSR", "Sae": "SAE", "Mse": "MSE", "Rmse": "RMSE", "Mae": "MAE",
+                "Mape": "MAPE", "Count": "count", "YMean": "yMean", "PredictionMean": "predictionMean",
+                "ExplainedVariance": "Explained Variance"}
+
+
+class ClusterMetrics(BaseMetrics):
+    _ALIASES = {"K": "k", "Count": "count", "Ssw": "SSW", "Ssb": "SSB", "ClusterArray": "clusterArray",
+                "CountArray": "countArray", "Nmi": "NMI", "Purity": "purity", "Ri": "ri", "Ari": "ari",
+                "SilhouetteCoefficient": "silhouetteCoefficient", "CalinskiHarabaz": "calinskiHarabaz",
+                "Compactness": "compactness", "Seperation": "seperation", "DaviesBouldin": "daviesBouldin"}
+
+
+# ---------------------------------------------------------------------------------------------------
+# label handling
+# ---------------------------------------------------------------------------------------------------
+def build_label_index(labels, binary: bool, positive: Optional[str] = None):
+    """Distinct labels sorted in reverse string order; binary + positiveValue puts it first
+    (``ClassificationEvaluationUtil.buildLabelIndexLabelArray``)."""
+    labels = sorted({str(l) for l in labels}, reverse=True)
+    if len(labels) < 2:
+        raise ValueError("The distinct label number less than 2!")
+    if binary and len(labels) != 2:
+        raise ValueError("The number of labels must be equal to 2!")
+    if binary and positive is not None:
+        if labels[1] == positive:
+            labels[1] = labels[0]
+            labels[0] = positive
+        elif labels[0] != positive:
+            raise ValueError("Not contain positiveValue")
+    return labels
+
+
+def parse_detail(s: str) -> Dict[str, float]:
+    try:
+        m = json.loads(s)
+    except Exception:
+        raise RuntimeError(f"Fail to deserialize detail column {s}!")
+    m = {str(k): float(v) for k, v in m.items()}
+    for v in m.values():
+        if not (0.0 <= v <= 1.0):
+            raise ValueError(f"Probibality in {s} not in range [0, 1]!")
+    if abs(sum(m.values()) - 1.0) >= PROB_SUM_EPS:
+        raise ValueError(f"Probability sum in {s} not equal to 1.0!")
+    return m
+
+
+# ---------------------------------------------------------------------------------------------------
+# summaries (device histograms + one all-reduce)
+# ---------------------------------------------------------------------------------------------------
+def binary_summary(labels_col: Sequence[Any], details: Sequence[str], label_array: List[str], device=None):
+    """(positiveBin, negativeBin, logLoss, total) over all ranks."""
+    dev = device or torch.device("cpu")
+    pos_p, is_pos, ll, keep = [], [], 0.0, 0
+    for lab, det in zip(labels_col, details):
+        if lab is None or det is None:
+            continue
+        m = parse_detail(det)
+        if len(m) != 2:
+            raise ValueError("The number of labels must be equal to 2!")
+        lab = str(lab)
+        if lab not in label_array:
+            continue
+        p = m.get(label_array[0])
+        pl = m.get(lab, 0.0)
+        ll += -math.log(max(min(pl, 1 - LOG_LOSS_EPS), LOG_LOSS_EPS))
+        pos_p.append(p)
+        is_pos.append(lab == label_array[0])
+        keep += 1
+    p = torch.tensor(pos_p, dtype=torch.float64, device=dev)
+    idx = torch.where(p == 1.0, torch.full_like(p, DETAIL_BIN_NUMBER - 1), torch.floor(p * DETAIL_BIN_NUMBER)).long()
+    lbl = torch.tensor(is_pos, dtype=torch.bool, device=dev)
+    ok = (idx >= 0) & (idx < DETAIL_BIN_NUMBER)
+    posb = torch.bincount(idx[ok & lbl], minlength=DETAIL_BIN_NUMBER).double()
+    negb = torch.bincount(idx[ok & ~lbl], minlength=DETAIL_BIN_NUMBER).double()
+    buf = torch.cat([posb, negb, torch.tensor([ll, float(keep)], dtype=torch.float64, device=dev)])
+    comm.all_reduce(buf, "sum")
+    b = buf.cpu().numpy()
+    return (b[:DETAIL_BIN_NUMBER].astype(np.int64), b[DETAIL_BIN_NUMBER:2 * DETAIL_BIN_NUMBER].astype(np.int64),
+            float(b[-2]), int(b[-1]))
+
+
+def multi_summary_from_detail(labels_col, details, label_array: List[str], device=None):
+    dev = device or torch.device("cpu")
+    K = len(label_array)
+    index = {l: i for i, l in enumerate(label_array)}
+    pi, li, ll, n = [], [], 0.0, 0
+    for lab, det in zip(labels_col, details):
+        if lab is None or det is None:
+            continue
+        m = parse_detail(det)
+        lab = str(lab)
+        if lab not in index:
+            continue
+        best, pred = -math.inf, None
+        for k in sorted(m):           # TreeMap iteration order, first max wins
+            if m[k] > best:
+                best, pred = m[k], k
+        pl = m.get(lab, 0.0)
+        ll += -math.log(max(min(pl, 1 - LOG_LOSS_EPS), LOG_LOSS_EPS))
+        pi.append(index[pred])
+        li.append(index[lab])
+        n += 1
+    return _confusion(pi, li, K, ll, n, dev)
+
+
+def multi_summary_from_pred(labels_col, preds, label_array: List[str], device=None):
+    dev = device or torch.device("cpu")
+    index = {l: i for i, l in enumerate(label_array)}
+    pi, li = [], []
+    for lab, pr in zip(labels_col, preds):
+        if lab is None or pr is None:
+            continue
+        pi.append(index[str(pr)])
+        li.append(index[str(lab)])
+    return _confusion(pi, li, len(label_array), -1.0, len(pi), dev)
+
+
+def _confusion(pi, li, K, ll, n, dev):
+    p = torch.tensor(pi, dtype=torch.long, device=dev)
+    l = torch.tensor(li, dtype=torch.long, device=dev)
+    mat = torch.bincount(p * K + l, minlength=K * K).double()
+    buf = torch.cat([mat, torch.tensor([max(ll, 0.0), float(n)], dtype=torch.float64, device=dev)])
+    comm.all_reduce(buf, "sum")
+    b = buf.cpu().numpy()
+    return b[:K * K].reshape(K, K).astype(np.int64), (float(b[-2]) if ll >= 0 else -1.0), int(b[-1])
+
+
+def regression_summary(y, pred, device=None):
+    dev = device or torch.device("cpu")
+    yv = torch.as_tensor(np.asarray(y, dtype=np.float64), device=dev)
+    pv = torch.as_tensor(np.asarray(pred, dtype=np.float64), device=dev)
+    diff = (yv - pv).abs()
+    buf = torch.stack([yv.sum(), (yv * yv).sum(), pv.sum(), (pv * pv).sum(), diff.sum(), (diff * diff).sum(),
+                       (diff / yv).abs().sum(), torch.tensor(float(yv.shape[0]), dtype=torch.float64, device=dev)])
+    comm.all_reduce(buf, "sum")
+    return buf.cpu().numpy()
+
+
+# ---------------------------------------------------------------------------------------------------
+# confusion-matrix metrics (ConfusionMatrix.java + ClassificationMetricComputers.java)
+# ---------------------------------------------------------------------------------------------------
+class _CM:
+    def __init__(self, m: np.ndarray):
+        self.m = np.asarray(m, dtype=np.float64)
+        self.k = self.m.shape[0]
+        self.actual = self.m.sum(0)
+        self.pred = self.m.sum(1)
+        self.total = float(self.m.sum())
+        d = np.diag(self.m)
+        self.tp_i = d
+        self.fp_i = self.pred - d
+        self.fn_i = self.actual - d
+        self.tn_i = d + self.total - self.pred - self.actual
+        self.tp, self.fp, self.fn, self.tn = self.tp_i.sum(), self.fp_i.sum(), self.fn_i.sum(), self.tn_i.sum()
+
+    def counts(self, i):
+        if i is None:
+            return self.tp, self.fp, self.fn, self.tn
+        return self.tp_i[i], self.fp_i[i], self.fn_i[i], self.tn_i[i]
+
+    def proportion(self):
+        return self.actual / self.total if self.total else np.zeros(self.k)
+
+    def accuracy(self):
+        return float(np.trace(self.m) / self.total) if self.total else float("nan")
+
+    def kappa(self):
+        pe = float((self.pred * self.actual).sum()) / (self.total * self.total)
+        pa = float(np.trace(self.m)) / self.total
+        return (pa - pe) / (1 - pe) if pe < 1 else 1.0
+
+
+def _div(a, b):
+    return 0.0 if b == 0 else a / b
+
+
+def _tpr(c, i):
+    tp, fp, fn, tn = c.counts(i)
+    return _div(tp, tp + fn)
+
+
+def _tnr(c, i):
+    tp, fp, fn, tn = c.counts(i)
+    return _div(tn, fp + tn)
+
+
+def _fpr(c, i):
+    tp, fp, fn, tn = c.counts(i)
+    return _div(fp, fp + tn)
+
+
+def _fnr(c, i):
+    tp, fp, fn, tn = c.counts(i)
+    return _div(fn, tp + fn)
+
+
+def _precision(c, i):
+    tp, fp, fn, tn = c.counts(i)
+    return _div(tp, tp + fp)
+
+
+def _f1(c, i):
+    tp, fp, fn, tn = c.counts(i)
+    return _div(2 * tp, 2 * tp + fp + fn)
+
+
+def _acc(c, i):
+    tp, fp, fn, tn = c.counts(i)
+    return (tp + tn) / (tp + fp + fn + tn)
+
+
+def _kappa(c, i):
+    tp, fp, fn, tn = c.counts(i)
+    total = tp + fp + fn + tn
+    pa = (tp + tn) / total
+    pe = ((tp + fn) * (tp + fp) + (tn + fp) * (tn + fn)) / (total * total)
+    return (pa - pe) / (1 - pe) if pe < 1 else 1.0
+
+
+# (array param, weighted, macro, micro, computer) in ClassificationEvaluationUtil.Computations order
+_COMPUTATIONS = [
+    ("TrueNegativeRate", _tnr), ("TruePositiveRate", _tpr), ("FalseNegativeRate", _fnr),
+    ("FalsePositiveRate", _fpr), ("Precision", _precision), ("Specificity", _tnr), ("Sensitivity", _tpr),
+    ("Recall", _tpr), ("F1", _f1), ("Accuracy", _acc), ("Kappa", _kappa)]
+
+
+def _weighted(fn, c):
+    prop = c.proportion()
+    return float(sum(fn(c, i) * prop[i] for i in range(c.k)))
+
+
+def _macro(fn, c):
+    return float(sum(fn(c, i) for i in range(c.k)) / c.k)
+
+
+def _set(params: Params, name, value):
+    params.set(name, value)
+
+
+def _common(params: Params, c: _CM, labels: List[str]):
+    _set(params, "LabelArray", list(labels))
+    _set(params, "ActualLabelFrequency", [int(x) for x in c.actual])
+    _set(params, "ActualLabelProportion", [float(x) for x in c.proportion()])
+    _set(params, "ConfusionMatrix", [[int(x) for x in row] for row in c.m])
+    _set(params, "TotalSamples", int(c.total))
+    for name, fn in _COMPUTATIONS:
+        _set(params, "Weighted" + name, _weighted(fn, c))
+        _set(params, "Macro" + name, _macro(fn, c))
+        _set(params, "Micro" + name, float(fn(c, None)))
+    _set(params, "Accuracy", c.accuracy())
+    _set(params, "Kappa", c.kappa())
+
+
+def multi_metrics(matrix: np.ndarray, labels: List[str], logloss: float, total: int) -> MultiClassMetrics:
+    params = Params()
+    c = _CM(matrix)
+    _set(params, "PredictLabelFrequency", [int(x) for x in c.pred])
+    _set(params, "PredictLabelProportion", [float(x) for x in (c.pred / c.total if c.total else c.pred)])
+    for name, fn in _COMPUTATIONS:
+        vals = [float(fn(c, i)) for i in range(c.k)] + [_weighted(fn, c), _macro(fn, c), float(fn(c, None))]
+        _set(params, name + "Array", vals)
+    _common(params, c, labels)
+    if logloss >= 0:
+        _set(params, "LogLoss", logloss / total)
+    return MultiClassMetrics(params)
+
+
+def _area(x, y):
+    return float(np.sum((x[1:] - x[:-1]) * (y[1:] + y[:-1]) / 2)) if len(x) > 1 else 0.0
+
+
+def binary_metrics(posb: np.ndarray, negb: np.ndarray, labels: List[str], logloss: float, total: int
+                   ) -> BinaryClassMetrics:
+    """``BinaryMetricsSummary.toMetrics`` :72-...: full curves for AUC/PRC/KS, 0.001-sampled curves and
+    threshold arrays, confusion matrix at the threshold nearest 0.5."""
+    eff = np.nonzero((posb != 0) | (negb != 0))[0]
+    mid = DETAIL_BIN_NUMBER // 2
+    if mid not in set(eff.tolist()):
+        eff = np.sort(np.append(eff, mid))
+    total_true, total_false = int(posb[eff].sum()), int(negb[eff].sum())
+    if total_true + total_false != total:
+        raise ValueError("The effective number in bins must be equal to total!")
+    rev = eff[::-1]
+    cur_t = np.cumsum(posb[rev]).astype(np.float64)
+    cur_f = np.cumsum(negb[rev]).astype(np.float64)
+    n1 = len(rev) + 1
+    thr = np.empty(n1)
+    thr[0] = 1.0
+    thr[1:] = rev * (1.0 / DETAIL_BIN_NUMBER)
+    tp = np.concatenate([[0.0], cur_t])
+    fp = np.concatenate([[0.0], cur_f])
+    tpr = tp / total_true if total_true else np.ones(n1)
+    fpr = fp / total_false if total_false else np.ones(n1)
+    roc_x, roc_y = fpr.copy(), tpr.copy()
+    roc_x[0], roc_y[0] = 0.0, 0.0
+    prec = np.where(tp == 0, 1.0, tp / np.where(tp + fp == 0, 1.0, tp + fp))
+    pr_x, pr_y = tpr.copy(), prec.copy()
+    pr_x[0], pr_y[0] = 0.0, prec[1] if n1 > 1 else 1.0
+    lift_x = (tp + fp) / total
+    lift_y = tp.copy()
+    lift_x[0], lift_y[0] = 0.0, 0.0
+    params = Params()
+    _set(params, "AUC", _area(roc_x, roc_y))
+    _set(params, "PRC", _area(pr_x, pr_y))
+    _set(params, "K-S", float(np.max(np.abs(roc_x - roc_y))))
+    # sampling of thresholds at 0.001 resolution (plus the 0.5 point)
+    keep = [0]
+    pre = thr[0]
+    for i in range(n1):
+        if abs(pre - thr[i]) >= PROBABILITY_INTERVAL - PROBABILITY_ERROR or abs(thr[i] - 0.5) < PROBABILITY_ERROR:
+            keep.append(i)
+            pre = thr[i]
+    keep = np.asarray(keep)
+    _set(params, "RocCurve", [roc_x[keep].tolist(), roc_y[keep].tolist()])
+    _set(params, "RecallPrecisionCurve", [pr_x[keep].tolist(), pr_y[keep].tolist()])
+    _set(params, "LiftChart", [lift_x[keep].tolist(), lift_y[keep].tolist()])
+    sk = keep[1:]
+    s_thr = thr[sk]
+    mats = []
+    for i in sk:
+        mats.append(np.array([[tp[i], fp[i]], [total_true - tp[i], total_false - fp[i]]]))
+    _set(params, "ThresholdArray", s_thr.tolist())
+    cms = [_CM(m) for m in mats]
+    for name, fn in _COMPUTATIONS:
+        _set(params, name + "Array", [float(fn(c, 0)) for c in cms])
+    if logloss >= 0:
+        _set(params, "LogLoss", logloss / total)
+    mid_i = int(np.argmin(np.abs(s_thr - 0.5)))
+    c = cms[mid_i]
+    _set(params, "Precision", float(_precision(c, 0)))
+    _set(params, "Recall", float(_tpr(c, 0)))
+    _set(params, "F1", float(_f1(c, 0)))
+    _common(params, c, labels)
+    return BinaryClassMetrics(params)
+
+
+def regression_metrics(s: np.ndarray) -> RegressionMetrics:
+    y_sum, y_sum2, p_sum, p_sum2, mae, sse, mape, total = [float(v) for v in s]
+    params = Params()
+    sst = y_sum2 - y_sum * y_sum / total
+    ssr = p_sum2 - 2 * y_sum * p_sum / total + y_sum * y_sum / total
+    r2 = 1 - sse / sst if sst != 0 else float("nan")
+    _set(params, "SST", sst)
+    _set(params, "SSE", sse)
+    _set(params, "SSR", ssr)
+    _set(params, "R2", r2)
+    _set(params, "R", math.sqrt(r2) if r2 >= 0 else float("nan"))
+    _set(params, "MSE", sse / total)
+    _set(params, "RMSE", math.sqrt(sse / total))
+    _set(params, "SAE", mae)
+    _set(params, "MAE", mae / total)
+    _set(params, "count", total)
+    _set(params, "MAPE", mape * 100 / total)
+    _set(params, "yMean", y_sum / total)
+    _set(params, "predictionMean", p_sum / total)
+    _set(params, "Explained Variance", ssr / total)
+    return RegressionMetrics(params)

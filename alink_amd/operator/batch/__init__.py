@@ -6,3 +6,4 @@ from .dataproc import *  # noqa: F401,F403
 from .clustering import *  # noqa: F401,F403
 from .sql import *  # noqa: F401,F403
 from .linear import *  # noqa: F401,F403
+from .evaluation import *  # noqa: F401,F403

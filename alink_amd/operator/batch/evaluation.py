@@ -1,0 +1,128 @@
+"""Evaluation batch operators (reference ``A/operator/batch/evaluation/*``, ``BaseEvalClassBatchOp.java``):
+each outputs ONE row ``Data`` = the metrics ``Params`` JSON; ``collectMetrics()`` returns the metric object."""
+from __future__ import annotations
+
+import numpy as np
+
+from ...common.table import MTable
+from ...common.types import TableSchema, Types
+from ...models.evaluation import metrics as M
+from ...parallel import comm
+from ..base import BatchOperator
+
+__all__ = ["EvalBinaryClassBatchOp", "EvalMultiClassBatchOp", "EvalRegressionBatchOp", "EvalClusterBatchOp"]
+
+_SCHEMA = TableSchema(["Data"], [Types.STRING])
+
+
+def _global_labels(vals):
+    seen = set()
+    for part in comm.all_gather_object(sorted({str(v) for v in vals if v is not None})):
+        seen.update(part)
+    return seen
+
+
+def _pget(p, name):
+    try:
+        return p.get(name) if p.contains(name) else None
+    except KeyError:
+        return None
+
+
+class _EvalBase(BatchOperator):
+    METRICS = M.BaseMetrics
+
+    def _out(self, metrics):
+        self._metrics = metrics
+        self.setOutputTable(MTable.from_rows([metrics.serialize()], _SCHEMA, replicated=True))
+        return self
+
+    def collectMetrics(self):
+        rows = self.collect()
+        return self.METRICS.fromRow(rows[0])
+
+    def lazyCollectMetrics(self, *callbacks):
+        def cb(rows):
+            m = self.METRICS.fromRow(rows[0])
+            for c in callbacks:
+                c(m)
+        return self.lazyCollect(cb)
+
+    def lazyPrintMetrics(self, title=None):
+        def cb(rows):
+            if title:
+                print(title)
+            print(self.METRICS.fromRow(rows[0]))
+        return self.lazyCollect(cb)
+
+
+class _EvalClass(_EvalBase):
+    BINARY = False
+
+    def linkFrom(self, *inputs):
+        mt = self.checkAndGetFirst(inputs).getOutputTable()
+        p = self.getParams()
+        label_col = p.get("labelCol")
+        detail_col = _pget(p, "predictionDetailCol")
+        pred_col = _pget(p, "predictionCol")
+        pos = _pget(p, "positiveLabelValueString")
+        labels = mt.column_values(label_col)
+        dev = self.env.device
+        if detail_col:
+            details = mt.column_values(detail_col)
+            keys = set()
+            for l, d in zip(labels, details):
+                if l is not None and d is not None:
+                    keys.update(M.parse_detail(d).keys())
+                    keys.add(str(l))
+            label_set = set()
+            for part in comm.all_gather_object(sorted(keys)):
+                label_set.update(part)
+            arr = M.build_label_index(label_set, self.BINARY, pos)
+            if self.BINARY:
+                pb, nb, ll, n = M.binary_summary(labels, details, arr, dev)
+                if n == 0:
+                    raise ValueError("Please check the evaluation input! there is no effective row!")
+                return self._out(M.binary_metrics(pb, nb, arr, ll, n))
+            mat, ll, n = M.multi_summary_from_detail(labels, details, arr, dev)
+        elif pred_col:
+            preds = mt.column_values(pred_col)
+            arr = M.build_label_index(_global_labels(labels) | _global_labels(preds), self.BINARY, pos)
+            mat, ll, n = M.multi_summary_from_pred(labels, preds, arr, dev)
+        else:
+            raise ValueError("Error Input, must give either predictionCol or predictionDetailCol!")
+        if n == 0:
+            raise ValueError("Please check the evaluation input! there is no effective row!")
+        return self._out(M.multi_metrics(mat, arr, ll, n))
+
+
+class EvalBinaryClassBatchOp(_EvalClass):
+    BINARY = True
+    METRICS = M.BinaryClassMetrics
+
+
+class EvalMultiClassBatchOp(_EvalClass):
+    METRICS = M.MultiClassMetrics
+
+
+class EvalRegressionBatchOp(_EvalBase):
+    METRICS = M.RegressionMetrics
+
+    def linkFrom(self, *inputs):
+        mt = self.checkAndGetFirst(inputs).getOutputTable()
+        y = mt.column_values(self.getLabelCol())
+        pr = mt.column_values(self.getPredictionCol())
+        keep = [(a, b) for a, b in zip(y, pr) if a is not None and b is not None]
+        s = M.regression_summary([a for a, _ in keep], [b for _, b in keep], self.env.device)
+        if s[-1] == 0:
+            raise ValueError("Please check the evaluation input! there is no effective row!")
+        return self._out(M.regression_metrics(s))
+
+
+class EvalClusterBatchOp(_EvalBase):
+    METRICS = M.ClusterMetrics
+
+    def linkFrom(self, *inputs):
+        from ...models.evaluation.cluster import cluster_metrics
+        mt = self.checkAndGetFirst(inputs).getOutputTable()
+        return self._out(cluster_metrics(mt, self.getParams(), self.env))

@@ -178,6 +178,11 @@ class StreamOperator(AlgoOperator):
         from .sql import UnionAllStreamOp
         return UnionAllStreamOp().linkFrom(self, other)
 
+    @staticmethod
+    def fromDataframe(df, schemaStr: Optional[str] = None):
+        from .source import MemSourceStreamOp
+        return MemSourceStreamOp.fromDataframe(df, schemaStr)
+
     def sample(self, ratio: float):
         from .dataproc import SampleStreamOp
         return self.link(SampleStreamOp().setRatio(ratio))

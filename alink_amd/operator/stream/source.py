@@ -1,0 +1,117 @@
+"""Stream sources: a bounded table replayed as micro-batches.
+
+Reference: ``A/operator/stream/source/{CsvSourceStreamOp,MemSourceStreamOp,NumSeqSourceStreamOp,
+TableSourceStreamOp,TextSourceStreamOp,LibSvmSourceStreamOp,RandomTableSourceStreamOp}.java`` (Flink
+``DataStream`` sources).  Each source reads/generates its rank's row block with the batch reader of the same
+name (same Params) and yields it in fixed-size micro-batches (``ALINK_STREAM_BATCH`` rows, default 1024), so
+a GPU-resident pipeline processes one device block per micro-batch.
+"""
+from __future__ import annotations
+
+import os
+from typing import Iterator, Optional
+
+from ...common.params import Params
+from ...common.table import MTable
+from ..batch import source as B
+from .base import StreamSourceOp
+
+__all__ = ["TableSourceStreamOp", "MemSourceStreamOp", "CsvSourceStreamOp", "TextSourceStreamOp",
+           "LibSvmSourceStreamOp", "NumSeqSourceStreamOp", "RandomTableSourceStreamOp",
+           "RandomVectorSourceStreamOp"]
+
+
+def _batch_rows() -> int:
+    return int(os.environ.get("ALINK_STREAM_BATCH", "1024"))
+
+
+class _TableReplaySource(StreamSourceOp):
+    BATCH_OP = None
+
+    def _table(self) -> MTable:
+        op = self.BATCH_OP(self.getParams().clone())
+        op.setMLEnvironmentId(self.getMLEnvironmentId())
+        return op.getOutputTable()
+
+    def _ensure_schema(self):
+        if self._schema is None:
+            self._mt = self._table()
+            self._schema = self._mt.schema
+        return self._schema
+
+    def getSchema(self):
+        return self._ensure_schema()
+
+    def batches(self) -> Iterator[MTable]:
+        self._ensure_schema()
+        mt = self._mt
+        bs = max(1, _batch_rows())
+        for s in range(0, mt.num_rows, bs):
+            yield mt.slice(s, min(mt.num_rows, s + bs))
+
+
+class TableSourceStreamOp(_TableReplaySource):
+    _NO_AUTO_PARAMS = True
+
+    def __init__(self, table=None, params: Optional[Params] = None):
+        super().__init__(params)
+        self._src = table
+
+    def _table(self):
+        t = self._src
+        return t.getOutputTable() if hasattr(t, "getOutputTable") else t
+
+
+class MemSourceStreamOp(_TableReplaySource):
+    def __init__(self, vals=None, schema=None, params: Optional[Params] = None):
+        super().__init__(params)
+        self._vals, self._sch = vals, schema
+
+    def _table(self):
+        return B.MemSourceBatchOp(self._vals, self._sch).setMLEnvironmentId(self.getMLEnvironmentId()) \
+            .getOutputTable()
+
+    @staticmethod
+    def fromDataframe(df, schemaStr: Optional[str] = None):
+        op = MemSourceStreamOp()
+        op._table = lambda: B.MemSourceBatchOp.fromDataframe(df, schemaStr).getOutputTable()
+        return op
+
+
+class CsvSourceStreamOp(_TableReplaySource):
+    BATCH_OP = B.CsvSourceBatchOp
+
+    def __init__(self, filePath: Optional[str] = None, schemaStr: Optional[str] = None,
+                 params: Optional[Params] = None):
+        super().__init__(params)
+        if filePath is not None:
+            self.setFilePath(filePath)
+        if schemaStr is not None:
+            self.setSchemaStr(schemaStr)
+
+
+class TextSourceStreamOp(_TableReplaySource):
+    BATCH_OP = B.TextSourceBatchOp
+
+
+class LibSvmSourceStreamOp(_TableReplaySource):
+    BATCH_OP = B.LibSvmSourceBatchOp
+
+
+class NumSeqSourceStreamOp(_TableReplaySource):
+    def __init__(self, start: int = 1, end: Optional[int] = None, colName: str = "num",
+                 params: Optional[Params] = None):
+        super().__init__(params)
+        self._args = (start, end, colName)
+
+    def _table(self):
+        s, e, c = self._args
+        return B.NumSeqSourceBatchOp(s, e, c).setMLEnvironmentId(self.getMLEnvironmentId()).getOutputTable()
+
+
+class RandomTableSourceStreamOp(_TableReplaySource):
+    BATCH_OP = B.RandomTableSourceBatchOp
+
+
+class RandomVectorSourceStreamOp(_TableReplaySource):
+    BATCH_OP = B.RandomVectorSourceBatchOp

@@ -1,0 +1,83 @@
+"""Evaluation ops vs the reference docs (docs/en/eval*.md script examples)."""
+import json
+
+import numpy as np
+import pandas as pd
+import pytest
+
+from alink_amd import (BatchOperator, EvalBinaryClassBatchOp, EvalClusterBatchOp, EvalMultiClassBatchOp,
+                       EvalRegressionBatchOp, EvalBinaryClassStreamOp, StreamOperator, CollectStreamOp)
+
+DATA = [["prefix1", '{"prefix1": 0.9, "prefix0": 0.1}'], ["prefix1", '{"prefix1": 0.8, "prefix0": 0.2}'],
+        ["prefix1", '{"prefix1": 0.7, "prefix0": 0.3}'], ["prefix0", '{"prefix1": 0.75, "prefix0": 0.25}'],
+        ["prefix0", '{"prefix1": 0.6, "prefix0": 0.4}']]
+
+
+def _in():
+    df = pd.DataFrame({"label": [r[0] for r in DATA], "detailInput": [r[1] for r in DATA]})
+    return BatchOperator.fromDataframe(df, schemaStr="label string, detailInput string"), df
+
+
+def test_eval_binary_doc():
+    op, _ = _in()
+    m = EvalBinaryClassBatchOp().setLabelCol("label").setPredictionDetailCol("detailInput").linkFrom(op) \
+        .collectMetrics()
+    assert m.getAuc() == pytest.approx(0.8333333333333333, abs=1e-15)
+    assert m.getKs() == pytest.approx(0.6666666666666666, abs=1e-15)
+    assert m.getPrc() == pytest.approx(0.9027777777777777, abs=1e-15)
+    assert m.getAccuracy() == pytest.approx(0.6)
+    assert m.getMacroPrecision() == pytest.approx(0.3)
+    assert m.getMicroRecall() == pytest.approx(0.6)
+    assert m.getWeightedSensitivity() == pytest.approx(0.6)
+    assert m.getLabelArray() == ["prefix1", "prefix0"]
+    assert len(m.getThresholdArray()) == len(m.getPrecisionArray())
+
+
+def test_eval_multi_doc():
+    op, _ = _in()
+    m = EvalMultiClassBatchOp().setLabelCol("label").setPredictionDetailCol("detailInput").linkFrom(op) \
+        .collectMetrics()
+    assert m.getAccuracy("prefix0") == pytest.approx(0.6)
+    assert m.getRecall("prefix1") == pytest.approx(1.0)
+    assert m.getMacroPrecision() == pytest.approx(0.3)
+    assert m.getMicroRecall() == pytest.approx(0.6)
+    assert m.getWeightedSensitivity() == pytest.approx(0.6)
+    assert m.getConfusionMatrix().tolist() == [[3, 2], [0, 0]]
+
+
+def test_eval_regression_doc():
+    d = np.array([[0, 0], [8, 8], [1, 2], [9, 10], [3, 1], [10, 7]])
+    op = BatchOperator.fromDataframe(pd.DataFrame({"pred": d[:, 0], "label": d[:, 1]}),
+                                     schemaStr="pred int, label int")
+    m = EvalRegressionBatchOp().setPredictionCol("pred").setLabelCol("label").linkFrom(op).collectMetrics()
+    assert m.getCount() == 6.0 and m.getSse() == 15.0 and m.getSae() == 7.0
+    assert m.getRmse() == pytest.approx(1.5811388300841898, abs=1e-15)
+    assert m.getR2() == pytest.approx(0.8282442748091603, abs=1e-15)
+
+
+def test_eval_cluster_doc():
+    df = pd.DataFrame({"id": [0, 0, 0, 1, 1, 1],
+                       "vec": ["0 0 0", "0.1,0.1,0.1", "0.2,0.2,0.2", "9 9 9", "9.1 9.1 9.1", "9.2 9.2 9.2"]})
+    op = BatchOperator.fromDataframe(df, schemaStr="id int, vec string")
+    m = EvalClusterBatchOp().setVectorCol("vec").setPredictionCol("id").linkFrom(op).collectMetrics()
+    assert m.getCount() == 6 and m.getK() == 2
+    assert m.getClusterArray() == ["0", "1"] and m.getCountArray() == [3.0, 3.0]
+    assert m.getCompactness() == pytest.approx(0.11547005383792497, rel=1e-12)
+    assert m.getDaviesBouldin() == pytest.approx(0.014814814814814791, rel=1e-10)
+    assert m.getSeperation() == pytest.approx(15.588457268119896, rel=1e-12)
+    assert m.getSsb() == pytest.approx(364.5, rel=1e-12)
+    assert m.getSsw() == pytest.approx(0.12, rel=1e-9)
+    assert m.getCalinskiHarabaz() == pytest.approx(12150.0, rel=1e-9)
+    assert 0.9 < m.getSilhouetteCoefficient() <= 1.0
+
+
+def test_eval_binary_stream_window_and_all():
+    _, df = _in()
+    box = []
+    src = StreamOperator.fromDataframe(df, schemaStr="label string, detailInput string")
+    EvalBinaryClassStreamOp().setLabelCol("label").setPredictionDetailCol("detailInput").linkFrom(src) \
+        .link(CollectStreamOp(box))
+    StreamOperator.execute()
+    assert [r[0] for r in box] == ["window", "all"]
+    auc = json.loads(json.loads(box[1][1])["AUC"])
+    assert auc == pytest.approx(0.8333333333333333)
