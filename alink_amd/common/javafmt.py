@@ -11,7 +11,7 @@ import math
 from typing import Any, Dict, Iterable, List
 
 __all__ = [
-    "java_double_str", "java_float_str", "gson_dumps", "java_string_hash", "java_hashmap_order",
+    "java_double_str", "java_float_str", "gson_dumps", "java_str", "java_string_hash", "java_hashmap_order",
 ]
 
 
@@ -187,3 +187,18 @@ def java_hashmap_order(keys: Iterable[str]) -> List[str]:
     indexed = [(_spread(java_string_hash(k)) & (cap - 1), i, k) for i, k in enumerate(keys)]
     indexed.sort(key=lambda t: (t[0], t[1]))
     return [k for _, _, k in indexed]
+
+
+def java_str(v) -> str:
+    """``String.valueOf(obj)`` of a Java-typed cell: booleans lower-case, doubles via ``Double.toString``,
+    vectors in Alink's string format."""
+    import numpy as np
+    if v is None:
+        return "null"
+    if isinstance(v, (bool, np.bool_)):
+        return "true" if v else "false"
+    if isinstance(v, (float, np.floating)):
+        return java_double_str(float(v))
+    if hasattr(v, "toString") and not isinstance(v, str):
+        return v.toString()
+    return str(v)

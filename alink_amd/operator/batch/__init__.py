@@ -7,3 +7,4 @@ from .clustering import *  # noqa: F401,F403
 from .sql import *  # noqa: F401,F403
 from .linear import *  # noqa: F401,F403
 from .evaluation import *  # noqa: F401,F403
+from .feature import *  # noqa: F401,F403

@@ -8,7 +8,9 @@ from __future__ import annotations
 
 from ...models.clustering.kmeans import KMeansModelMapper
 from ...models.linear.model import AFTModelMapper, LinearModelMapper, SoftmaxModelMapper
-from .base import ModelMapStreamOp
+from ...models.feature import encoders as _E
+from ...models.feature import scalers as _S
+from .base import MapStreamOp, ModelMapStreamOp
 
 _PREDICTORS = {
     "KMeansPredictStreamOp": KMeansModelMapper,
@@ -19,6 +21,26 @@ _PREDICTORS = {
     "LassoRegPredictStreamOp": LinearModelMapper,
     "SoftmaxPredictStreamOp": SoftmaxModelMapper,
     "AftSurvivalRegPredictStreamOp": AFTModelMapper,
+    "StandardScalerPredictStreamOp": _S.StandardScalerModelMapper,
+    "MinMaxScalerPredictStreamOp": _S.MinMaxScalerModelMapper,
+    "MaxAbsScalerPredictStreamOp": _S.MaxAbsScalerModelMapper,
+    "ImputerPredictStreamOp": _S.ImputerModelMapper,
+    "VectorStandardScalerPredictStreamOp": _S.VectorScalerModelMapper,
+    "VectorMinMaxScalerPredictStreamOp": _S.VectorScalerModelMapper,
+    "VectorMaxAbsScalerPredictStreamOp": _S.VectorScalerModelMapper,
+    "VectorImputerPredictStreamOp": _S.VectorImputerModelMapper,
+    "StringIndexerPredictStreamOp": _E.StringIndexerModelMapper,
+    "MultiStringIndexerPredictStreamOp": _E.MultiStringIndexerModelMapper,
+    "IndexToStringPredictStreamOp": _E.IndexToStringModelMapper,
+    "OneHotPredictStreamOp": _E.OneHotModelMapper,
+    "QuantileDiscretizerPredictStreamOp": _E.QuantileDiscretizerModelMapper,
+}
+
+_MAPPERS = {
+    "BinarizerStreamOp": _E.BinarizerMapper,
+    "BucketizerStreamOp": _E.BucketizerMapper,
+    "FeatureHasherStreamOp": _E.FeatureHasherMapper,
+    "DCTStreamOp": _E.DCTMapper,
 }
 
 __all__ = []
@@ -33,5 +55,16 @@ def register_stream_predictor(name: str, mapper):
     return cls
 
 
+def register_stream_mapper(name: str, mapper):
+    cls = type(name, (MapStreamOp,), {"MAPPER": mapper, "__module__": __name__,
+                                     "__doc__": f"Stream transform with ``{mapper.__name__}``."})
+    globals()[name] = cls
+    if name not in __all__:
+        __all__.append(name)
+    return cls
+
+
 for _n, _m in _PREDICTORS.items():
     register_stream_predictor(_n, _m)
+for _n, _m in _MAPPERS.items():
+    register_stream_mapper(_n, _m)

@@ -82,7 +82,10 @@ def init_distributed(backend: Optional[str] = None, timeout_s: float = 1800.0) -
     if ws <= 1:
         return False
     if backend is None:
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        backend = os.environ.get("ALINK_DIST_BACKEND")
+    if backend is None:
+        cpu_only = os.environ.get("ALINK_DEVICE", "").startswith("cpu")
+        backend = "nccl" if torch.cuda.is_available() and not cpu_only else "gloo"
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     kw = {}
     if backend == "nccl":

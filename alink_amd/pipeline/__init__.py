@@ -3,3 +3,4 @@ from .base import *  # noqa: F401,F403
 from .clustering import *  # noqa: F401,F403
 from .dataproc import *  # noqa: F401,F403
 from .linear import *  # noqa: F401,F403
+from .feature import *  # noqa: F401,F403

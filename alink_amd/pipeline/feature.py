@@ -1,0 +1,35 @@
+"""Feature / data-processing pipeline stages (reference ``A/pipeline/{dataproc,feature}/*``)."""
+from ..models.feature import encoders as E
+from ..models.feature import scalers as S
+from ..operator.batch import feature as F
+from .base import MapModel, MapTransformer, Trainer
+
+__all__ = []
+
+
+def _stage(name, base, **attrs):
+    cls = type(name, (base,), dict(attrs, __module__=__name__))
+    globals()[name] = cls
+    __all__.append(name)
+    return cls
+
+
+for _n, _mapper in (("StandardScaler", S.StandardScalerModelMapper), ("MinMaxScaler", S.MinMaxScalerModelMapper),
+                    ("MaxAbsScaler", S.MaxAbsScalerModelMapper), ("Imputer", S.ImputerModelMapper),
+                    ("VectorStandardScaler", S.VectorScalerModelMapper),
+                    ("VectorMinMaxScaler", S.VectorScalerModelMapper),
+                    ("VectorMaxAbsScaler", S.VectorScalerModelMapper),
+                    ("VectorImputer", S.VectorImputerModelMapper),
+                    ("StringIndexer", E.StringIndexerModelMapper),
+                    ("MultiStringIndexer", E.MultiStringIndexerModelMapper),
+                    ("QuantileDiscretizer", E.QuantileDiscretizerModelMapper)):
+    _stage(_n + "Model", MapModel, MAPPER=_mapper)
+    _stage(_n, Trainer, TRAIN_OP=getattr(F, _n + "TrainBatchOp"), MODEL=_n + "Model")
+
+_stage("OneHotEncoderModel", MapModel, MAPPER=E.OneHotModelMapper)
+_stage("OneHotEncoder", Trainer, TRAIN_OP=F.OneHotTrainBatchOp, MODEL="OneHotEncoderModel")
+_stage("IndexToString", MapModel, MAPPER=E.IndexToStringModelMapper)
+_stage("Binarizer", MapTransformer, MAPPER=E.BinarizerMapper)
+_stage("Bucketizer", MapTransformer, MAPPER=E.BucketizerMapper)
+_stage("FeatureHasher", MapTransformer, MAPPER=E.FeatureHasherMapper)
+_stage("DCT", MapTransformer, MAPPER=E.DCTMapper)

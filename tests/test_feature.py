@@ -1,0 +1,107 @@
+"""Feature engineering / statistics vs the reference docs (docs/en/*.md script examples)."""
+import numpy as np
+import pandas as pd
+import pytest
+
+from alink_amd import *  # noqa: F401,F403
+from alink_amd.common.linalg import VectorUtil
+
+SC = [["a", 10.0, 100], ["b", -2.5, 9], ["c", 100.2, 1], ["d", -99.9, 100], ["a", 1.4, 1], ["b", -2.2, 9],
+      ["c", 100.9, 1]]
+
+
+def _scaler_in(extra_null=False):
+    rows = SC + ([[None, None, None]] if extra_null else [])
+    df = pd.DataFrame({"col1": [r[0] for r in rows], "col2": [r[1] for r in rows], "col3": [r[2] for r in rows]})
+    return BatchOperator.fromDataframe(df, schemaStr="col1 string, col2 double, col3 long"), df
+
+
+@pytest.mark.parametrize("stage,ref2,ref3", [
+    (StandardScaler, [-0.078352, -0.259243, 1.226961, -1.668749, -0.202805, -0.254902, 1.237091],
+     [1.459581, -0.481449, -0.652089, 1.459581, -0.652089, -0.481449, -0.652089]),
+    (MinMaxScaler, [0.547311, 0.485060, 0.996514, 0.0, 0.504482, 0.486554, 1.0],
+     [1.0, 0.080808, 0.0, 1.0, 0.0, 0.080808, 0.0]),
+    (MaxAbsScaler, [0.099108, -0.024777, 0.993062, -0.990089, 0.013875, -0.021804, 1.0],
+     [1.0, 0.09, 0.01, 1.0, 0.01, 0.09, 0.01])])
+def test_scalers_doc(stage, ref2, ref3):
+    op, df = _scaler_in()
+    out = stage().setSelectedCols(["col2", "col3"]).fit(op).transform(op).collectToDataframe()
+    np.testing.assert_allclose(out["col2"].values, ref2, atol=1e-6)
+    np.testing.assert_allclose(out["col3"].values, ref3, atol=1e-6)
+    # stream path with the same model
+    box = []
+    m = stage().setSelectedCols(["col2", "col3"]).fit(op)
+    m.transform(StreamOperator.fromDataframe(df, schemaStr="col1 string, col2 double, col3 long")) \
+        .link(CollectStreamOp(box))
+    StreamOperator.execute()
+    np.testing.assert_allclose([r[1] for r in box], ref2, atol=1e-6)
+
+
+def test_imputer_doc():
+    op, _ = _scaler_in(extra_null=True)
+    out = Imputer().setSelectedCols(["col2", "col3"]).fit(op).transform(op).collect()
+    assert out[-1][1] == pytest.approx(15.414286, abs=1e-6) and out[-1][2] == 31
+
+
+def test_string_indexer_doc():
+    df = pd.DataFrame({"f0": ["football"] * 3 + ["basketball"] * 2 + ["tennis"]})
+    op = BatchOperator.fromDataframe(df, schemaStr="f0 string")
+    out = StringIndexer().setSelectedCol("f0").setOutputCol("f0_indexed").setStringOrderType("frequency_asc") \
+        .fit(op).transform(op).collectToDataframe()
+    assert list(out["f0_indexed"]) == [2, 2, 2, 1, 1, 0]
+
+
+D4 = [[1.1, True, 2, "A"], [1.1, False, 2, "B"], [1.1, True, 1, "B"], [2.2, True, 1, "A"]]
+
+
+def _d4():
+    df = pd.DataFrame({"double": [r[0] for r in D4], "bool": [r[1] for r in D4], "number": [r[2] for r in D4],
+                       "str": [r[3] for r in D4]})
+    return BatchOperator.fromDataframe(df, schemaStr="double double, bool boolean, number int, str string")
+
+
+def test_feature_hasher_doc_bitexact():
+    out = FeatureHasher().setSelectedCols(["double", "bool", "number", "str"]).setOutputCol("output") \
+        .setNumFeatures(200).transform(_d4()).collect()
+    got = [VectorUtil.toString(r[4]) for r in out]
+    assert got == ["$200$13:2.0 38:1.1 45:1.0 195:1.0", "$200$13:2.0 30:1.0 38:1.1 76:1.0",
+                   "$200$13:1.0 38:1.1 76:1.0 195:1.0", "$200$13:1.0 38:2.2 45:1.0 195:1.0"]
+
+
+def test_one_hot_doc():
+    src = _d4()
+    onehot = OneHotTrainBatchOp().setSelectedCols(["double", "bool", "number", "str"]).setDiscreteThresholds(2)
+    pred = OneHotPredictBatchOp().setSelectedCols(["double", "bool"]).setEncode("ASSEMBLED_VECTOR") \
+        .setOutputCols(["pred"]).setDropLast(False)
+    onehot.linkFrom(src)
+    out = pred.linkFrom(onehot, src).collect()
+    assert [VectorUtil.toString(r[4]) for r in out] == ["$6$0:1.0 3:1.0", "$6$0:1.0 5:1.0", "$6$0:1.0 3:1.0",
+                                                         "$6$2:1.0 3:1.0"]
+
+
+def test_bucketizer_binarizer_doc():
+    out = Bucketizer().setSelectedCols(["double"]).setCutsArray([[2.0]]).transform(_d4()).collect()
+    assert [r[0] for r in out] == [0, 0, 0, 1]
+    out = Binarizer().setSelectedCol("double").setThreshold(2.0).transform(_d4()).collect()
+    assert [r[0] for r in out] == [0.0, 0.0, 0.0, 1.0]
+
+
+def test_dct_doc():
+    df = pd.DataFrame({"features": ["-0.6264538 0.1836433", "11.1249309 9.9550664"]})
+    out = DCT().setSelectedCol("features").setOutputCol("result").transform(
+        BatchOperator.fromDataframe(df, schemaStr="features string")).collect()
+    np.testing.assert_allclose(out[0][1].data, [-0.31311430733060563, -0.5728251528295567], rtol=1e-12)
+    np.testing.assert_allclose(out[1][1].data, [14.905809038224113, 0.8272191210194105], rtol=1e-12)
+
+
+def test_quantile_discretizer_and_summarizer():
+    rng = np.random.default_rng(0)
+    df = pd.DataFrame({"x": rng.normal(size=1000), "y": rng.integers(0, 10, 1000)})
+    op = BatchOperator.fromDataframe(df, schemaStr="x double, y long")
+    out = QuantileDiscretizer().setSelectedCols(["x"]).setNumBuckets(4).fit(op).transform(op).collectToDataframe()
+    counts = np.bincount(out["x"].values.astype(int))
+    assert len(counts) == 4 and counts.min() > 200
+    s = SummarizerBatchOp().setSelectedCols(["x", "y"]).linkFrom(op).collectSummary()
+    assert s.mean("x") == pytest.approx(df["x"].mean()) and s.standardDeviation("y") == pytest.approx(df["y"].std())
+    c = CorrelationBatchOp().setSelectedCols(["x", "y"]).linkFrom(op).collectCorrelation().getCorrelation()
+    assert c[0, 1] == pytest.approx(np.corrcoef(df["x"], df["y"])[0, 1])
