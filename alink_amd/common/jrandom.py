@@ -1,0 +1,56 @@
+"""``java.util.Random`` (48-bit LCG) — reproduces the reference's seeded draws where they shape results
+(e.g. the per-node feature shuffles of ``seriestree/DecisionTree.bagging``)."""
+from __future__ import annotations
+
+__all__ = ["JavaRandom"]
+
+_MULT = 0x5DEECE66D
+_ADD = 0xB
+_MASK = (1 << 48) - 1
+
+
+def _to_int32(x: int) -> int:
+    x &= 0xFFFFFFFF
+    return x - (1 << 32) if x >= (1 << 31) else x
+
+
+class JavaRandom:
+    def __init__(self, seed: int):
+        self._seed = (int(seed) ^ _MULT) & _MASK
+
+    def _next(self, bits: int) -> int:
+        self._seed = (self._seed * _MULT + _ADD) & _MASK
+        return _to_int32(self._seed >> (48 - bits))
+
+    def nextInt(self, bound: int = None) -> int:
+        if bound is None:
+            return self._next(32)
+        if bound <= 0:
+            raise ValueError("bound must be positive")
+        if (bound & -bound) == bound:
+            return _to_int32((bound * self._next(31)) >> 31)
+        while True:
+            bits = self._next(31)
+            val = bits % bound
+            if _to_int32(bits - val + (bound - 1)) >= 0:
+                return val
+
+    def nextLong(self) -> int:
+        v = (self._next(32) << 32) + self._next(32)
+        v &= (1 << 64) - 1
+        return v - (1 << 64) if v >= (1 << 63) else v
+
+    def nextDouble(self) -> float:
+        return ((self._next(26) << 27) + self._next(27)) * (1.0 / (1 << 53))
+
+    def nextBoolean(self) -> bool:
+        return self._next(1) != 0
+
+    def shuffle(self, arr: list) -> list:
+        """In-place shuffle as ``DecisionTree.shuffle`` (Fisher-Yates from the end, ``nextInt(i + 1)``)."""
+        for i in range(len(arr) - 1, 0, -1):
+            idx = self.nextInt(i + 1)
+            if idx == i:
+                continue
+            arr[idx], arr[i] = arr[i], arr[idx]
+        return arr

@@ -1,0 +1,473 @@
+"""Level-wise histogram tree builder shared by GBDT, random forests and decision trees.
+
+Reference algorithms (behaviour, not structure):
+
+* GBDT — ``parallelcart/{ConstructLocalBin,CalBestSplit,Split,UpdateTreeData,SaveModel}.java``: per level one
+  ``[node][feature][bin](g^2, g, h, 1)`` histogram all-reduce, best split per node with
+  ``gain = |GL^2/HL + GR^2/HR - G^2/H|`` (``CalBestSplit.java:178-218``), categorical bins ordered by ``g/h``
+  (``:98-120``), child counters ``sum = -lr * G`` (``:296-297``), rows routed ``2id / 2id+1``.
+* RF / decision tree — ``seriestree/{DecisionTree,ContinuousSplitter,CategoricalSplitter,FeatureSplitter}.java``
+  and ``Criteria.java``: Gini / InfoGain / InfoGainRatio / MSE impurities, per-node feature bagging, C4.5
+  multi-way categorical splits for the information-gain criteria, BFS node order.
+
+MI355X design: the training rows never leave HBM.  Each level does ONE histogram launch over the uint8 bin
+matrix (``ops/tree.py`` — LDS-privatised HIP kernel) for only the smaller children (the larger sibling is the
+parent minus its siblings), ONE all-reduce of that histogram (RCCL), a fully vectorised split search over
+``[nodes, features, bins]`` on the device, and ONE routing launch.  Only the chosen splits (a few numbers per
+node) cross to the host to build the model objects.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import List, Optional, Tuple
+
+import numpy as np
+import torch
+
+from ...ops import tree as tops
+from ...parallel import comm
+from .data import BinnedData
+from .model import LabelCounter, Node
+
+__all__ = ["SplitConfig", "TreeBuilder", "EPS"]
+
+EPS = 1e-15
+NEG = float("-inf")
+
+
+@dataclass
+class SplitConfig:
+    kind: str                              # gbdt | gini | infogain | infogainratio | mse
+    max_depth: int                         # root has depth 1; nodes at depth >= max_depth are leaves
+    min_samples_per_leaf: int = 1
+    n_classes: int = 0
+    min_sample_ratio_per_child: float = 0.0
+    min_info_gain: float = 0.0
+    max_leaves: int = 2 ** 31 - 1
+    min_sum_hessian_per_leaf: float = 0.0
+    learning_rate: float = 1.0
+    node_feature_count: Optional[int] = None  # RF bagging: features tried per node (shuffled order)
+
+    @property
+    def classification(self) -> bool:
+        return self.kind in ("gini", "infogain", "infogainratio")
+
+    @property
+    def n_stats(self) -> int:
+        return self.n_classes + 1 if self.classification else 4
+
+
+# ---------------------------------------------------------------------------------------------------
+# criteria on stacked statistics [..., S]
+# ---------------------------------------------------------------------------------------------------
+def _weight(cfg: SplitConfig, X: torch.Tensor) -> torch.Tensor:
+    if cfg.classification:
+        return X[..., :cfg.n_classes].sum(-1)
+    if cfg.kind == "mse":
+        return X[..., 0]
+    return X[..., 2]  # gbdt: hessian
+
+
+def _count(cfg: SplitConfig, X: torch.Tensor) -> torch.Tensor:
+    return X[..., -1]
+
+
+def _impurity(cfg: SplitConfig, X: torch.Tensor) -> torch.Tensor:
+    w = _weight(cfg, X)
+    safe = torch.where(w < EPS, torch.ones_like(w), w)
+    if cfg.kind == "mse":
+        mean = X[..., 1] / safe
+        imp = X[..., 2] / safe - mean * mean
+    else:
+        p = X[..., :cfg.n_classes] / safe[..., None]
+        if cfg.kind == "gini":
+            imp = 1.0 - (p * p).sum(-1)
+        else:
+            lg = torch.where(p > 0, torch.log(torch.where(p > 0, p, torch.ones_like(p))) / math.log(2.0),
+                             torch.zeros_like(p))
+            imp = -(p * lg).sum(-1)
+    return torch.where(w < EPS, torch.zeros_like(imp), imp)
+
+
+def _binary_gain(cfg: SplitConfig, T: torch.Tensor, L: torch.Tensor, R: torch.Tensor) -> torch.Tensor:
+    if cfg.kind == "gbdt":
+        G, H = T[..., 1], T[..., 2]
+        GL, HL = L[..., 1], L[..., 2]
+        GR, HR = G - GL, H - HL
+        ok = (HL != 0) & (HR != 0)
+        sHL = torch.where(HL == 0, torch.ones_like(HL), HL)
+        sHR = torch.where(HR == 0, torch.ones_like(HR), HR)
+        sH = torch.where(H == 0, torch.ones_like(H), H)
+        g = torch.abs(GL * GL / sHL + GR * GR / sHR - G * G / sH)
+        return torch.where(ok, g, torch.zeros_like(g))
+    wT = _weight(cfg, T)
+    safe = torch.where(wT < EPS, torch.ones_like(wT), wT)
+    pl, pr = _weight(cfg, L) / safe, _weight(cfg, R) / safe
+    g = _impurity(cfg, T) - pl * _impurity(cfg, L) - pr * _impurity(cfg, R)
+    if cfg.kind == "infogainratio":
+        def lg2(p):
+            return torch.where(p > 0, torch.log(torch.where(p > 0, p, torch.ones_like(p))) / math.log(2.0),
+                               torch.zeros_like(p))
+        iv = -(pl * lg2(pl) + pr * lg2(pr))
+        g = torch.where(iv < EPS, torch.zeros_like(g), g / torch.where(iv < EPS, torch.ones_like(iv), iv))
+    return torch.where(wT < EPS, torch.zeros_like(g), g)
+
+
+# ---------------------------------------------------------------------------------------------------
+@dataclass
+class _Pending:
+    node: Node
+    depth: int
+    total: np.ndarray          # [S] float64 node statistics (incl. missing)
+    parent: int = -1           # index of the parent in the previous level
+    splittable: bool = True
+    order: Optional[list] = None  # RF: inherited (shuffled) feature order of this node's splitters
+
+
+@dataclass
+class _Split:
+    feature: int
+    gain: float
+    route: np.ndarray          # [256] child index per bin
+    n_children: int
+    child_totals: np.ndarray   # [k, S]
+    categorical: Optional[list]
+    threshold: float
+
+
+class TreeBuilder:
+    """Grows trees over one ``BinnedData`` (rows stay on the device between trees)."""
+
+    def __init__(self, data: BinnedData, cfg: SplitConfig):
+        self.d = data
+        self.cfg = cfg
+        self.dev = data.bins.device
+        self.F = len(data.feature_cols)
+        self.B = data.B
+        self.is_cat = torch.tensor(data.is_cat, dtype=torch.bool, device=self.dev)
+        self.nbins = torch.tensor(data.nbins, dtype=torch.long, device=self.dev)
+        self.hist_dtype = torch.float32 if data.bins.is_cuda else torch.float64
+
+    # -------------------------------------------------------------------------------------------
+    def _histograms(self, node_of_row, sample, slot_of_node: torch.Tensor, nslots: int, stats) -> torch.Tensor:
+        slot = torch.full_like(node_of_row, -1)
+        act = sample & (node_of_row >= 0) & (node_of_row < slot_of_node.numel())
+        slot[act] = slot_of_node[node_of_row[act].long()].to(slot.dtype)
+        H = tops.histogram(self.d.bins, slot, stats, nslots, self.B)
+        comm.all_reduce(H, "sum")
+        return H
+
+    # -------------------------------------------------------------------------------------------
+    def _search(self, Hn: torch.Tensor, feat_order: torch.Tensor, feat_ok: torch.Tensor):
+        """Best split per node.  Hn [m, F, B, S] (float64); feat_order [m, F] (scan order of features);
+        feat_ok [m, F] allowed.  Returns per node (gain, feature, j, multiway flag, perm [m,F,B-1])."""
+        cfg = self.cfg
+        m, F, B, S = Hn.shape
+        Hv = Hn[:, :, :B - 1, :]
+        Hmiss = Hn[:, :, B - 1, :]
+        cnt = _count(cfg, Hv)
+        # ordering key for categorical bins (continuous: identity)
+        binpos = torch.arange(B - 1, device=Hn.device, dtype=Hn.dtype).expand(m, F, B - 1)
+        if cfg.kind == "gbdt":
+            g, h = Hv[..., 1], Hv[..., 2]
+            key = torch.where(h < 1e-6, torch.full_like(g, -1.0), g / torch.where(h < 1e-6, torch.ones_like(h), h))
+        elif cfg.kind == "mse":
+            w = Hv[..., 0]
+            key = torch.where(cnt > 0, Hv[..., 1] / torch.where(w == 0, torch.ones_like(w), w),
+                              torch.full_like(w, float("inf")))
+        else:
+            w = _weight(cfg, Hv)
+            key = torch.where(cnt > 0, Hv[..., 0] / torch.where(w == 0, torch.ones_like(w), w),
+                              torch.full_like(w, float("inf")))
+        iscat = self.is_cat[None, :, None].expand(m, F, B - 1)
+        key = torch.where(iscat, key, binpos)
+        key, perm = torch.sort(key, dim=2, stable=True)
+        Hs = torch.gather(Hv, 2, perm[..., None].expand(m, F, B - 1, S))
+        L = torch.cumsum(Hs, dim=2)
+        Tv = L[:, :, -1, :]
+        if cfg.kind == "gbdt":
+            T = Tv + Hmiss
+            R = T[:, :, None, :] - L
+            gain = _binary_gain(cfg, T[:, :, None, :].expand_as(L), L, R)
+            HT = T[..., 2][:, :, None]
+            HL, HR = L[..., 2], T[..., 2][:, :, None] - L[..., 2]
+            cT = _count(cfg, T)[:, :, None]
+            cL = _count(cfg, L)
+            ratio = HL / torch.where(HT < 1e-6, torch.ones_like(HT), HT)
+            ok = (HT >= 1e-6) & (ratio >= 1e-7) & (ratio <= 1.0 - 1e-7)
+            ok &= (cL >= cfg.min_samples_per_leaf) & (cT - cL >= cfg.min_samples_per_leaf)
+            ok &= (HL >= cfg.min_sum_hessian_per_leaf) & (HR >= cfg.min_sum_hessian_per_leaf)
+        else:
+            R = Tv[:, :, None, :] - L
+            gain = _binary_gain(cfg, Tv[:, :, None, :].expand_as(L), L, R)
+            cM = _count(cfg, Hmiss)[:, :, None]
+            cL, cR = _count(cfg, L), _count(cfg, R)
+            cT = cL + cR
+            ok = (cL > 0) & (cR > 0)
+            ok &= (cfg.min_samples_per_leaf <= cL + cM) & (cfg.min_samples_per_leaf <= cR + cM)
+            den = cT + cM
+            den = torch.where(den == 0, torch.ones_like(den), den)
+            ok &= (cfg.min_sample_ratio_per_child <= (cL + cM) / den)
+            ok &= (cfg.min_sample_ratio_per_child <= (cR + cM) / den)
+            # a categorical candidate is evaluated only right after a non-empty category joins the left side
+            sorted_cnt = torch.gather(cnt, 2, perm)
+            ok &= ~iscat | (sorted_cnt > 0)
+            ok &= (gain > 0) & (gain >= cfg.min_info_gain)
+        gain = torch.where(ok, gain, torch.full_like(gain, NEG))
+        best_j_gain, best_j = gain.max(dim=2)       # first max along bins
+        multi = torch.zeros((m, F), dtype=torch.bool, device=Hn.device)
+        if cfg.kind in ("infogain", "infogainratio") and bool(self.is_cat.any()):
+            mg = self._multiway_gain(Hv, Hmiss, Tv)
+            catf = self.is_cat[None, :].expand(m, F)
+            best_j_gain = torch.where(catf, mg, best_j_gain)
+            multi = catf.clone()
+        best_j_gain = torch.where(feat_ok, best_j_gain, torch.full_like(best_j_gain, NEG))
+        ordered = torch.gather(best_j_gain, 1, feat_order)
+        gbest, pos = ordered.max(dim=1)
+        fbest = torch.gather(feat_order, 1, pos[:, None])[:, 0]
+        jbest = torch.gather(best_j, 1, fbest[:, None])[:, 0]
+        mbest = torch.gather(multi, 1, fbest[:, None])[:, 0]
+        if cfg.kind == "gbdt":
+            accept = gbest > cfg.min_info_gain + 1e-6
+        else:
+            accept = gbest > 0
+        return gbest, fbest, jbest, mbest, accept, perm
+
+    def _multiway_gain(self, Hv, Hmiss, Tv):
+        """C4.5 split on every non-empty category (``CategoricalSplitter.bestSplitInfo``)."""
+        cfg = self.cfg
+        cnt = _count(cfg, Hv)
+        w = _weight(cfg, Hv)
+        nonempty = (cnt > 0) & (w != 0)
+        wT = _weight(cfg, Tv)
+        safe = torch.where(wT < EPS, torch.ones_like(wT), wT)
+        p = w / safe[..., None]
+        g = _impurity(cfg, Tv) - (torch.where(nonempty, p * _impurity(cfg, Hv), torch.zeros_like(p))).sum(-1)
+        if cfg.kind == "infogainratio":
+            lg = torch.where(p > 0, torch.log(torch.where(p > 0, p, torch.ones_like(p))) / math.log(2.0),
+                             torch.zeros_like(p))
+            iv = -(torch.where(nonempty, p * lg, torch.zeros_like(p))).sum(-1)
+            g = torch.where(iv < EPS, torch.zeros_like(g), g / torch.where(iv < EPS, torch.ones_like(iv), iv))
+        cM = _count(cfg, Hmiss)
+        cT = cnt.sum(-1)
+        bad = nonempty & ((cfg.min_samples_per_leaf > cnt + cM[..., None])
+                          | (cfg.min_sample_ratio_per_child > (cnt + cM[..., None])
+                             / torch.where(cT + cM == 0, torch.ones_like(cT), cT + cM)[..., None]))
+        nchild = nonempty.sum(-1)
+        ok = (~bad.any(-1)) & (nchild >= 2) & (wT >= EPS) & (g > 0) & (g >= cfg.min_info_gain)
+        return torch.where(ok, g, torch.full_like(g, NEG))
+
+    # -------------------------------------------------------------------------------------------
+    def _materialise(self, Hn_np_feat: np.ndarray, f: int, j: int, multi: bool, perm_row: np.ndarray,
+                     gain: float) -> _Split:
+        """Host-side split description from the chosen feature's [B, S] histogram row."""
+        cfg, B = self.cfg, self.B
+        h = Hn_np_feat                      # [B, S]
+        cnt = h[:, -1]
+        nb = self.d.nbins[f]
+        route = np.zeros(256, dtype=np.int64)
+        categorical, threshold = None, 0.0
+        if multi:
+            cats = [c for c in range(nb) if cnt[c] > 0 and self._w_np(h[c]) != 0]
+            k = len(cats)
+            child = {c: i for i, c in enumerate(cats)}
+            categorical = [child.get(c, -1) for c in range(nb)]
+            totals = np.stack([h[c] for c in cats])
+            big = int(np.argmax(totals[:, -1]))
+            for b in range(256):
+                route[b] = child.get(b, big)
+        else:
+            k = 2
+            if self.d.is_cat[f]:
+                left = set(int(x) for x in perm_row[:j + 1])
+                if cfg.kind == "gbdt":
+                    categorical = [0 if c in left else 1 for c in range(nb)]
+                else:
+                    categorical = [(-1 if cnt[c] <= 0 else (0 if c in left else 1)) for c in range(nb)]
+                inl = np.array([b in left for b in range(B - 1)])
+            else:
+                inl = np.arange(B - 1) <= j
+                vals = self.d.bin_values[f] if self.d.bin_values else None
+                if cfg.kind != "gbdt" and vals is not None:
+                    nz = np.nonzero(cnt[:B - 1] > 0)[0]
+                    nxt = nz[nz > j]
+                    hi = vals[nxt[0]] if nxt.size else vals[min(j + 1, len(vals) - 1)]
+                    threshold = float((vals[j] + hi) / 2.0)
+                else:
+                    threshold = float(self.d.thresholds[f][j]) if j < len(self.d.thresholds[f]) else float("inf")
+            lt = h[:B - 1][inl].sum(0)
+            rt = h[:B - 1][~inl].sum(0)
+            totals = np.stack([lt, rt])
+            route[:B - 1] = np.where(inl, 0, 1)
+            route[B - 1:] = 1
+        # missing bin (and bins no training row used): GBDT right; otherwise the heavier child
+        miss = h[B - 1]
+        if cfg.kind == "gbdt":
+            mchild = 1 if not multi else int(np.argmax(totals[:, -1]))
+        else:
+            mchild = int(np.argmax(totals[:, -1]))
+            if not multi and self.d.is_cat[f]:
+                for c in range(nb):
+                    if cnt[c] <= 0:
+                        route[c] = mchild
+        route[B - 1] = mchild
+        totals = totals.copy()
+        totals[mchild] += miss
+        return _Split(f, gain, route, k, totals, categorical, threshold)
+
+    def _w_np(self, x):
+        cfg = self.cfg
+        if cfg.classification:
+            return float(x[:cfg.n_classes].sum())
+        return float(x[0] if cfg.kind == "mse" else x[2])
+
+    # -------------------------------------------------------------------------------------------
+    def _counter(self, total: np.ndarray) -> LabelCounter:
+        cfg = self.cfg
+        if cfg.kind == "gbdt":
+            return LabelCounter(total[2], int(round(total[3])), [-total[1] * cfg.learning_rate, total[0]])
+        if cfg.kind == "mse":
+            return LabelCounter(total[0], int(round(total[3])), [total[1], total[2]])
+        return LabelCounter(float(total[:cfg.n_classes].sum()), int(round(total[-1])),
+                            [float(x) for x in total[:cfg.n_classes]])
+
+    def _node_splittable(self, p: _Pending) -> bool:
+        cfg = self.cfg
+        if p.depth >= cfg.max_depth:
+            return False
+        if cfg.kind != "gbdt" and p.total[-1] <= cfg.min_samples_per_leaf:
+            return False
+        return p.total[-1] > 0
+
+    def build(self, stats: torch.Tensor, sample: torch.Tensor, feature_mask: Optional[np.ndarray] = None,
+              rng=None) -> Tuple[Node, torch.Tensor, List[Node]]:
+        """Grow one tree.  ``stats`` [n, S] per-row statistics, ``sample`` [n] rows that count.
+        ``rng`` (a ``JavaRandom``) enables RF per-node feature bagging.
+        Returns (root, leaf code per row (-1-k for leaf k; rows outside the tree keep their code), leaves)."""
+        cfg, F, B = self.cfg, self.F, self.B
+        n = self.d.bins.shape[0]
+        dev = self.dev
+        stats = stats.to(self.hist_dtype if stats.is_cuda else torch.float64).contiguous()
+        node_of_row = torch.zeros(n, dtype=torch.int32, device=dev)
+        if cfg.kind != "gbdt":
+            node_of_row = torch.where(sample, node_of_row, torch.full_like(node_of_row, -(1 << 30)))
+        fmask = torch.ones(F, dtype=torch.bool, device=dev) if feature_mask is None else \
+            torch.as_tensor(feature_mask, dtype=torch.bool, device=dev)
+        leaves: List[Node] = []
+        # root statistics from a 1-slot histogram
+        Hroot = self._histograms(node_of_row, sample, torch.zeros(1, dtype=torch.int32, device=dev), 1, stats)
+        root_total = Hroot[0, 0].to(torch.float64).sum(0).cpu().numpy()
+        root = Node(counter=self._counter(root_total))
+        bagging = cfg.kind != "gbdt" and rng is not None
+        level = [_Pending(root, 1, root_total, order=list(range(F)))]
+        level_hist = {0: Hroot[0]}
+        while level:
+            nl = len(level)
+            for p in level:
+                p.splittable = self._node_splittable(p)
+            # which nodes need a histogram built vs derived from the parent
+            build_ids, derive = [], {}
+            if all(k in level_hist for k in range(nl)):
+                pass
+            else:
+                groups = {}
+                for i, p in enumerate(level):
+                    groups.setdefault(p.parent, []).append(i)
+                for par, ids in groups.items():
+                    need = [i for i in ids if level[i].splittable]
+                    if not need:
+                        continue
+                    big = max(ids, key=lambda i: (level[i].total[-1], -i))
+                    if big in need and len(ids) >= 2 and par in self._prev_hist:
+                        derive[big] = (par, [i for i in ids if i != big])
+                        build_ids.extend(i for i in ids if i != big)
+                    else:
+                        build_ids.extend(need)
+                build_ids = sorted(set(build_ids))
+                if build_ids:
+                    som = torch.full((nl,), -1, dtype=torch.int32)
+                    for s, i in enumerate(build_ids):
+                        som[i] = s
+                    H = self._histograms(node_of_row, sample, som.to(dev), len(build_ids), stats)
+                    for s, i in enumerate(build_ids):
+                        level_hist[i] = H[s]
+                for big, (par, others) in derive.items():
+                    h = self._prev_hist[par].clone()
+                    for o in others:
+                        h -= level_hist[o]
+                    level_hist[big] = h
+            if bagging:
+                # every polled node shuffles its inherited splitter order (DecisionTree.bagging), in BFS order
+                for p in level:
+                    p.order = rng.shuffle(list(p.order))
+            cand = [i for i in range(nl) if level[i].splittable]
+            splits = {}
+            if cand:
+                Hn = torch.stack([level_hist[i] for i in cand]).to(torch.float32).to(torch.float64)
+                m = len(cand)
+                order = torch.arange(F, device=dev).expand(m, F).clone()
+                ok = fmask[None, :].expand(m, F).clone()
+                if bagging:
+                    ok[:] = False
+                    k = cfg.node_feature_count or F
+                    for r_, i in enumerate(cand):
+                        pf = level[i].order
+                        order[r_] = torch.as_tensor(pf, device=dev)
+                        ok[r_, torch.as_tensor(pf[:k], device=dev)] = True
+                gbest, fbest, jbest, mbest, accept, perm = self._search(Hn, order, ok)
+                acc = accept.cpu().numpy()
+                fb, jb, mb, gb = (fbest.cpu().numpy(), jbest.cpu().numpy(), mbest.cpu().numpy(),
+                                  gbest.cpu().numpy())
+                rows_host = Hn[torch.arange(m, device=dev), fbest].cpu().numpy()      # [m, B, S]
+                perm_host = perm[torch.arange(m, device=dev), fbest].cpu().numpy()    # [m, B-1]
+                for r_, i in enumerate(cand):
+                    if acc[r_]:
+                        splits[i] = self._materialise(rows_host[r_], int(fb[r_]), int(jb[r_]), bool(mb[r_]),
+                                                      perm_host[r_], float(gb[r_]))
+            # finalize nodes in BFS order; children form the next level
+            nxt: List[_Pending] = []
+            feat = np.full(nl, -1, dtype=np.int32)
+            base = np.zeros(nl, dtype=np.int32)
+            route = np.zeros((nl, 256), dtype=np.int16)
+            for i, p in enumerate(level):
+                sp = splits.get(i)
+                if sp is not None and cfg.kind != "gbdt":
+                    queue_size = (nl - i - 1) + len(nxt)
+                    if queue_size + sp.n_children >= cfg.max_leaves:
+                        sp = None
+                if sp is None:
+                    code = len(leaves)
+                    leaves.append(p.node)
+                    feat[i] = -1
+                    base[i] = -1 - code
+                    continue
+                nd = p.node
+                nd.featureIndex = sp.feature
+                if cfg.kind != "gbdt":
+                    nd.gain = sp.gain
+                if sp.categorical is not None:
+                    nd.categoricalSplit = [int(x) for x in sp.categorical]
+                else:
+                    nd.continuousSplit = sp.threshold
+                feat[i] = sp.feature
+                base[i] = len(nxt)
+                route[i] = sp.route
+                for c in range(sp.n_children):
+                    child = Node(counter=self._counter(sp.child_totals[c]))
+                    nd.nextNodes.append(child)
+                    nxt.append(_Pending(child, p.depth + 1, sp.child_totals[c], parent=i, order=p.order))
+            node_of_row = tops.route(self.d.bins, node_of_row, torch.as_tensor(feat, device=dev),
+                                     torch.as_tensor(base, device=dev), torch.as_tensor(route, device=dev))
+            self._prev_hist = level_hist
+            level_hist = {}
+            level = nxt
+        self._prev_hist = {}
+        # leaf probabilities (split nodes keep raw counters)
+        for lf in leaves:
+            lf.make_leaf_prob()
+        if cfg.kind == "gbdt" and root.featureIndex >= 0:
+            root.counter = LabelCounter(0.0, 0, [0.0, 0.0])
+        return root, node_of_row, leaves
+
+    _prev_hist: dict = {}

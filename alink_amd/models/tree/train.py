@@ -1,0 +1,265 @@
+"""GBDT / random forest / decision tree training drivers on top of ``engine.TreeBuilder``.
+
+Reference: ``A/operator/common/tree/BaseGbdtTrainBatchOp.java`` (params, depth from ``maxLeaves``
+``:255-263``, label handling, model meta ``:265-300``, feature-importance side output ``:230-236``),
+``parallelcart/ConstructLocalBin.java`` (gradients: least squares ``g = pred - (y - mean)``, ``h = 1``
+``:105-131``; logistic ``g = p - y``, ``h = p(1-p)`` with float32 storage ``:170-205``),
+``parallelcart/Split.java`` (row / feature subsampling after every tree ``:100-160``) and
+``BaseRandomForestTrainBatchOp.java`` (per-tree row sampling ``SampleData`` ``:470-503``, gain type per tree
+for ``treeType`` AVG/PARTITION ``:420-460``, model meta = the op params).
+
+Random-forest trees are independent: each one re-uses the device-resident bin matrix with its own row
+sample, so the whole forest is trained without re-reading or re-binning the table.
+"""
+from __future__ import annotations
+
+import math
+from typing import Any, List, Optional, Tuple
+
+import numpy as np
+import torch
+
+from ...common.jrandom import JavaRandom
+from ...common.params import Params
+from ...common.table import MTable
+from ...common.types import TableSchema, Types
+from ...parallel import comm
+from .data import build_bins, categorical_cols, distinct_labels, numeric_column
+from .engine import SplitConfig, TreeBuilder
+from .model import TreeModel, TreeModelDataConverter, feature_importance
+
+__all__ = ["train_gbdt", "train_forest", "IMPORTANCE_SCHEMA"]
+
+IMPORTANCE_SCHEMA = TableSchema(["feature", "importance"], [Types.STRING, Types.LONG])
+
+
+def _pget(p: Params, name, default=None):
+    try:
+        if p.contains(name):
+            v = p.get(name)
+            return default if v is None else v
+    except KeyError:
+        pass
+    return default
+
+
+def _ename(v, default):
+    if v is None:
+        return default
+    return str(getattr(v, "name", v)).upper()
+
+
+def _label_indices(mt: MTable, label_col: str, labels: List[Any], device) -> torch.Tensor:
+    from ...common.javafmt import java_str
+    col = mt.col(label_col)
+    if isinstance(col.values, torch.Tensor) and col.values.dim() == 1 and col.nulls is None and \
+            all(isinstance(l, (int, float)) and not isinstance(l, bool) for l in labels):
+        v = col.values.to(device=device, dtype=torch.float64)
+        lab = torch.tensor([float(l) for l in labels], dtype=torch.float64, device=device)
+        idx = torch.searchsorted(lab, v).clamp(max=len(labels) - 1)
+        if not bool((lab[idx] == v).all()):
+            raise RuntimeError("Can not find a label value in the label set")
+        return idx
+    pos = {java_str(l): i for i, l in enumerate(labels)}
+    idx = []
+    for v in mt.column_values(label_col):
+        if v is None or java_str(v) not in pos:
+            raise RuntimeError(f"Can not find {v}")
+        idx.append(pos[java_str(v)])
+    return torch.tensor(idx, dtype=torch.long, device=device)
+
+
+def _weights(mt: MTable, params: Params, device) -> torch.Tensor:
+    wc = _pget(params, "weightCol")
+    if wc is None:
+        return torch.ones(mt.num_rows, dtype=torch.float64, device=device)
+    w, null = numeric_column(mt, wc, device)
+    return torch.where(null, torch.zeros_like(w), w)
+
+
+def _type_string(t) -> str:
+    return t.sql if t.sql != "VARCHAR" else "VARCHAR"
+
+
+# ---------------------------------------------------------------------------------------------------
+# GBDT
+# ---------------------------------------------------------------------------------------------------
+def train_gbdt(mt: MTable, params: Params, env, algo_type: int) -> Tuple[List[tuple], TreeModelDataConverter,
+                                                                         List[tuple], dict]:
+    """Returns (model rows, converter, importance rows, train info)."""
+    dev = env.device
+    feature_cols = list(params.get("featureCols"))
+    label_col = params.get("labelCol")
+    cat = categorical_cols(mt.schema, feature_cols, _pget(params, "categoricalCols"))
+    params.set("categoricalCols", cat)
+    depth = int(_pget(params, "maxDepth", 6))
+    max_leaves = int(_pget(params, "maxLeaves", 2 ** 31 - 1))
+    if max_leaves > 0:
+        depth_leaf = int(math.log(max_leaves + 0.01) / math.log(2.0)) + 1
+        depth = min(depth, depth_leaf)
+    num_trees = int(_pget(params, "numTrees", 100))
+    max_bins = int(_pget(params, "maxBins", 128))
+    lr = float(_pget(params, "learningRate", 0.3))
+    sub_ratio = float(_pget(params, "subsamplingRatio", 1.0))
+    feat_ratio = float(_pget(params, "featureSubsamplingRatio", 1.0))
+    seed = int(_pget(params, "seed", 0))
+    label_type = mt.col_type(label_col)
+    labels = None
+    if algo_type == 1:
+        labels = distinct_labels(mt, label_col)
+        if len(labels) != 2:
+            raise ValueError(f"Binary classification requires exactly 2 labels, found {len(labels)}")
+        y = _label_indices(mt, label_col, labels, dev).to(torch.float32)
+        period = 0.0
+    else:
+        yd, null = numeric_column(mt, label_col, dev)
+        tot = torch.stack([yd.sum(), torch.tensor(float(yd.numel()), dtype=torch.float64, device=dev)])
+        comm.all_reduce(tot, "sum")
+        period = float(tot[0] / tot[1]) if float(tot[1]) > 0 else 0.0
+        y = (yd - period).to(torch.float32)
+    w = _weights(mt, params, dev).to(torch.float32)
+    data = build_bins(mt, feature_cols, cat, max_bins, dev, exact_midpoints=False, seed=seed)
+    cfg = SplitConfig("gbdt", max_depth=depth, min_samples_per_leaf=int(_pget(params, "minSamplesPerLeaf", 100)),
+                      min_info_gain=float(_pget(params, "minInfoGain", 0.0)),
+                      min_sum_hessian_per_leaf=float(_pget(params, "minSumHessianPerLeaf", 0.0)),
+                      learning_rate=lr)
+    builder = TreeBuilder(data, cfg)
+    n = mt.num_rows
+    F = len(feature_cols)
+    row_rng = np.random.default_rng(seed + 7919 * comm.get_rank())
+    feat_rng = np.random.default_rng(seed + 104729)       # identical on every rank
+    pred = torch.zeros(n, dtype=torch.float32, device=dev)
+    roots = []
+    fmask = np.ones(F, dtype=bool)
+    for t in range(num_trees):
+        sample = torch.as_tensor(row_rng.random(n) < sub_ratio, device=dev) if sub_ratio < 1.0 else \
+            torch.ones(n, dtype=torch.bool, device=dev)
+        if feat_ratio < 1.0:   # InitialTrainningBuffer / Split draw a feature subset for every tree
+            fmask = feat_rng.random(F) < feat_ratio
+        if algo_type == 1:
+            p = torch.sigmoid(pred.double())
+            g = (p - y.double()).float()
+            h = (p * (1.0 - p)).float()
+        else:
+            g = pred - y
+            h = torch.ones_like(g)
+        g, h = g * w, h * w
+        stats = torch.stack([g * g, g, h, torch.ones_like(g)], dim=1)
+        root, codes, leaves = builder.build(stats, sample, fmask)
+        roots.append(root)
+        # Split.java: predBuf = (float) (curPred + leftCounter.sum / leftCounter.weightSum)
+        vals = torch.tensor([lf.counter.distributions[0] if lf.counter and lf.counter.distributions else 0.0
+                             for lf in leaves] or [0.0], dtype=torch.float64, device=dev)
+        leaf = (-1 - codes.long()).clamp(min=0, max=vals.numel() - 1)
+        inc = torch.where(codes < 0, vals[leaf], torch.zeros_like(vals[leaf]))
+        pred = (pred.double() + inc).float()
+    meta = params.clone()
+    meta.set("featureCols", feature_cols).set("labelCol", label_col).set("categoricalCols", cat)
+    meta.set("numTrees", num_trees).set("maxDepth", depth).set("algoType", algo_type)
+    lt = label_type if algo_type == 1 else Types.DOUBLE
+    meta.set("labelTypeName", _type_string(lt))
+    meta.set("gbdt.y.period", float(period))
+    conv = TreeModelDataConverter(lt)
+    model = TreeModel(meta, roots, labels, data.indexer_rows or None)
+    rows = conv.save(model)
+    imp = feature_importance(roots, feature_cols)
+    info = {"numTrees": num_trees, "depth": depth, "bins": data.B}
+    return rows, conv, imp, info
+
+
+# ---------------------------------------------------------------------------------------------------
+# random forest / decision tree
+# ---------------------------------------------------------------------------------------------------
+def _avg_gain(num_trees: int, tid: int) -> str:
+    div, mod = num_trees // 3, num_trees % 3
+    start_gini = div if mod < 1 else div + 1
+    start_ratio = start_gini + div if mod < 2 else start_gini + div + 1
+    return _interval_gain(start_gini, start_ratio, tid)
+
+
+def _interval_gain(start_gini: int, start_ratio: int, tid: int) -> str:
+    if tid < start_gini:
+        return "infogain"
+    if tid < start_ratio:
+        return "gini"
+    return "infogainratio"
+
+
+def _gain_for_tree(tree_type: str, params: Params, num_trees: int, tid: int) -> str:
+    if tree_type == "AVG":
+        return _avg_gain(num_trees, tid)
+    if tree_type == "PARTITION":
+        a, b = str(_pget(params, "treePartition", "")).split(",")
+        return _interval_gain(int(a), int(b), tid)
+    return {"MSE": "mse", "GINI": "gini", "INFOGAIN": "infogain", "INFOGAINRATIO": "infogainratio"}[tree_type]
+
+
+def train_forest(mt: MTable, params: Params, env, regression: bool) -> Tuple[List[tuple], TreeModelDataConverter,
+                                                                             dict]:
+    dev = env.device
+    feature_cols = list(params.get("featureCols"))
+    label_col = params.get("labelCol")
+    tree_type = _ename(_pget(params, "treeType"), "AVG")
+    if regression:
+        tree_type = "MSE"
+    params.set("treeType", tree_type)
+    cat = categorical_cols(mt.schema, feature_cols, _pget(params, "categoricalCols"))
+    params.set("categoricalCols", cat)
+    params.set("featureTypes", [_type_string(mt.col_type(c)) for c in feature_cols])
+    num_trees = int(_pget(params, "numTrees", 10))
+    max_bins = int(_pget(params, "maxBins", 128))
+    seed = int(_pget(params, "seed", 0))
+    max_depth = int(_pget(params, "maxDepth", 2 ** 31 - 1))
+    msl = int(_pget(params, "minSamplesPerLeaf", 2))
+    F = len(feature_cols)
+    ratio = float(_pget(params, "featureSubsamplingRatio", 0.2))
+    nsub = int(_pget(params, "numSubsetFeatures", 2 ** 31 - 1))
+    node_feats = max(1, min(int(ratio * F), min(F, nsub)))
+    factor = float(_pget(params, "subsamplingRatio", 100000.0))
+    n = mt.num_rows
+    if factor > 1.0:
+        total = float(sum(comm.all_gather_object(int(n))))
+        factor = min(factor / total, 1.0) if total > 0 else 1.0
+    label_type = mt.col_type(label_col)
+    labels = None
+    w = _weights(mt, params, dev)
+    if regression:
+        y, _ = numeric_column(mt, label_col, dev)
+        lt = Types.DOUBLE
+    else:
+        labels = distinct_labels(mt, label_col)
+        y = _label_indices(mt, label_col, labels, dev)
+        lt = label_type
+    params.set("labelTypeName", _type_string(lt))
+    data = build_bins(mt, feature_cols, cat, max_bins, dev, exact_midpoints=True, seed=seed)
+    hdt = torch.float32 if dev.type == "cuda" else torch.float64
+    if regression:
+        wy = (w * y)
+        stats = torch.stack([w, wy, wy * wy, torch.ones_like(w)], dim=1).to(hdt)
+    else:
+        C = len(labels)
+        stats = torch.zeros((n, C + 1), dtype=hdt, device=dev)
+        stats[torch.arange(n, device=dev), y] = w.to(hdt)
+        stats[:, C] = 1.0
+    rng = np.random.default_rng(seed + 7919 * comm.get_rank())
+    # all trees' row samples up front: rand < factor per (row, tree), rows in row-major order
+    draws = rng.random((n, num_trees)) < factor if factor < 1.0 else None
+    roots = []
+    for t in range(num_trees):
+        kind = _gain_for_tree(tree_type, params, num_trees, t)
+        cfg = SplitConfig(kind, max_depth=max_depth, min_samples_per_leaf=msl,
+                          n_classes=0 if regression else len(labels),
+                          min_sample_ratio_per_child=float(_pget(params, "minSampleRatioPerChild", 0.0)),
+                          min_info_gain=float(_pget(params, "minInfoGain", 0.0)),
+                          max_leaves=int(_pget(params, "maxLeaves", 2 ** 31 - 1)),
+                          node_feature_count=node_feats)
+        builder = TreeBuilder(data, cfg)
+        sample = torch.as_tensor(draws[:, t], device=dev) if draws is not None else \
+            torch.ones(n, dtype=torch.bool, device=dev)
+        # DecisionTree seeds java.util.Random with the same `seed` for every tree
+        root, _, _ = builder.build(stats, sample, None, JavaRandom(seed))
+        roots.append(root)
+    meta = params.clone()
+    conv = TreeModelDataConverter(lt)
+    model = TreeModel(meta, roots, labels, data.indexer_rows or None)
+    return conv.save(model), conv, {"numTrees": num_trees, "bins": data.B}

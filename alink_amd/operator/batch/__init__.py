@@ -8,3 +8,4 @@ from .sql import *  # noqa: F401,F403
 from .linear import *  # noqa: F401,F403
 from .evaluation import *  # noqa: F401,F403
 from .feature import *  # noqa: F401,F403
+from .tree import *  # noqa: F401,F403

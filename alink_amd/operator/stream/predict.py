@@ -10,6 +10,7 @@ from ...models.clustering.kmeans import KMeansModelMapper
 from ...models.linear.model import AFTModelMapper, LinearModelMapper, SoftmaxModelMapper
 from ...models.feature import encoders as _E
 from ...models.feature import scalers as _S
+from ...models.tree.model import GbdtModelMapper, RandomForestModelMapper
 from .base import MapStreamOp, ModelMapStreamOp
 
 _PREDICTORS = {
@@ -34,6 +35,12 @@ _PREDICTORS = {
     "IndexToStringPredictStreamOp": _E.IndexToStringModelMapper,
     "OneHotPredictStreamOp": _E.OneHotModelMapper,
     "QuantileDiscretizerPredictStreamOp": _E.QuantileDiscretizerModelMapper,
+    "GbdtPredictStreamOp": GbdtModelMapper,
+    "GbdtRegPredictStreamOp": GbdtModelMapper,
+    "RandomForestPredictStreamOp": RandomForestModelMapper,
+    "RandomForestRegPredictStreamOp": RandomForestModelMapper,
+    "DecisionTreePredictStreamOp": RandomForestModelMapper,
+    "DecisionTreeRegPredictStreamOp": RandomForestModelMapper,
 }
 
 _MAPPERS = {

@@ -1,0 +1,176 @@
+// Tree histogram kernels: hist[slot][feature][bin][stat] += stats[row][stat].
+//
+// Reference hot loops: ConstructLocalBin.java:135-166,209-240 (GBDT: per (node, feature, bin) sums of
+// (g^2, g, h, 1) over fp64 arrays, one feature at a time on one CPU task) and TreeObj.stat
+// (paralleltree/TreeObj.java:321-390; class-count / moment histograms for RF).
+//
+// CDNA4 design:
+//  * bins are a row-major uint8 matrix [n, F] (one byte per (row, feature), <= 255 bins + a missing bin),
+//    so consecutive lanes read consecutive feature bytes of a row: fully coalesced 256-byte wave loads.
+//  * each workgroup owns a contiguous row range and a feature group; it privatises the
+//    [slots x features x bins x stats] histogram in LDS (ds_add_f32 atomics — native, no CAS loop) and
+//    flushes non-zero entries once with global fp32 atomics.  Per-(slot, feature) rows are padded by one
+//    float so lanes working on neighbouring features land in different LDS banks.
+//  * when even one feature of all slots does not fit the LDS budget the slots are split into groups
+//    (grid.z); past 8 groups (very deep / wide levels, few rows per node) the kernel accumulates straight
+//    into global memory instead, where contention is negligible.
+//  * the host side builds only the smaller child of every split (histogram subtraction), so slot counts
+//    stay at half the level width.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kLdsBudget = 64 * 1024;  // bytes per workgroup -> 2 workgroups per CU (160 KB LDS)
+
+__global__ __launch_bounds__(kThreads) void tree_hist_lds(
+    const uint8_t* __restrict__ bins, int64_t n, int F, const int32_t* __restrict__ slot,
+    const float* __restrict__ stats, int S, int B, int slots_per_group, int FG, int64_t rows_per_block,
+    float* __restrict__ hist) {
+  extern __shared__ float sh[];
+  const int fstride = B * S + 1;
+  const int f0 = blockIdx.y * FG;
+  const int fg = min(FG, F - f0);
+  const int slot0 = blockIdx.z * slots_per_group;
+  const int lds_n = slots_per_group * FG * fstride;
+  for (int i = threadIdx.x; i < lds_n; i += kThreads) sh[i] = 0.f;
+  __syncthreads();
+
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t r1 = min(n, r0 + rows_per_block);
+  if (r0 < r1) {
+    const int npairs = (int)(r1 - r0) * fg;  // host guarantees < 2^31
+    for (int p = threadIdx.x; p < npairs; p += kThreads) {
+      const int rl = p / fg;
+      const int f = p - rl * fg;
+      const int64_t r = r0 + rl;
+      const int s = slot[r] - slot0;
+      if ((unsigned)s >= (unsigned)slots_per_group) continue;
+      const int b = bins[r * F + f0 + f];
+      float* h = sh + (s * FG + f) * fstride + b * S;
+      const float* st = stats + r * S;
+      for (int k = 0; k < S; ++k) {
+        const float v = st[k];
+        if (v != 0.f) atomicAdd(h + k, v);
+      }
+    }
+  }
+  __syncthreads();
+
+  // flush: LDS index i -> (slot s, local feature f, bin*S + k)
+  const int bs = B * S;
+  for (int i = threadIdx.x; i < lds_n; i += kThreads) {
+    const float v = sh[i];
+    if (v == 0.f) continue;
+    const int sf = i / fstride;
+    const int rem = i - sf * fstride;
+    if (rem >= bs) continue;  // padding column
+    const int s = sf / FG;
+    const int f = sf - s * FG;
+    if (f >= fg || slot0 + s < 0) continue;
+    const int64_t g = ((int64_t)(slot0 + s) * F + (f0 + f)) * bs + rem;
+    unsafeAtomicAdd(hist + g, v);
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void tree_hist_global(
+    const uint8_t* __restrict__ bins, int64_t n, int F, const int32_t* __restrict__ slot,
+    const float* __restrict__ stats, int S, int B, int nslots, float* __restrict__ hist) {
+  const int64_t total = n * (int64_t)F;
+  const int bs = B * S;
+  for (int64_t p = (int64_t)blockIdx.x * kThreads + threadIdx.x; p < total;
+       p += (int64_t)gridDim.x * kThreads) {
+    const int64_t r = p / F;
+    const int f = (int)(p - r * F);
+    const int s = slot[r];
+    if ((unsigned)s >= (unsigned)nslots) continue;
+    const int b = bins[p];
+    float* h = hist + ((int64_t)s * F + f) * bs + b * S;
+    const float* st = stats + r * S;
+    for (int k = 0; k < S; ++k) {
+      const float v = st[k];
+      if (v != 0.f) unsafeAtomicAdd(h + k, v);
+    }
+  }
+}
+
+// route rows one level down: child = base[node] + route[node][bin(row, feat[node])]
+__global__ __launch_bounds__(kThreads) void tree_route(
+    const uint8_t* __restrict__ bins, int64_t n, int F, int32_t* __restrict__ node,
+    const int32_t* __restrict__ feat, const int32_t* __restrict__ base, const int16_t* __restrict__ route,
+    int nnodes) {
+  for (int64_t r = (int64_t)blockIdx.x * kThreads + threadIdx.x; r < n; r += (int64_t)gridDim.x * kThreads) {
+    const int v = node[r];
+    if ((unsigned)v >= (unsigned)nnodes) continue;
+    const int f = feat[v];
+    if (f < 0) {
+      node[r] = base[v];  // leaf: host passes its final (negative) code
+      continue;
+    }
+    const int b = bins[r * F + f];
+    node[r] = base[v] + route[v * 256 + b];
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+// hist must be zeroed by the caller: [nslots, F, B, S] fp32.
+int alink_tree_hist_f32(const uint8_t* bins, int64_t n, int F, const int32_t* slot, const float* stats,
+                        int S, int B, int nslots, float* hist, int num_cus, hipStream_t stream) {
+  if (n <= 0 || nslots <= 0) return 0;
+  if (F <= 0 || S <= 0 || B <= 0 || B > 256) return 1;
+  const int unit = (B * S + 1) * (int)sizeof(float);  // one (slot, feature) row in LDS
+  const int max_units = kLdsBudget / unit;
+  int FG, spg, groups;
+  if (max_units >= nslots) {
+    spg = nslots;
+    groups = 1;
+    FG = max_units / nslots;
+    if (FG > F) FG = F;
+  } else {
+    FG = 1;
+    spg = max_units > 0 ? max_units : 1;
+    groups = (nslots + spg - 1) / spg;
+  }
+  if (max_units == 0 || groups > 8) {
+    int64_t total = n * (int64_t)F;
+    int64_t blocks = (total + kThreads - 1) / kThreads;
+    int grid = (int)(blocks < (int64_t)num_cus * 16 ? blocks : (int64_t)num_cus * 16);
+    hipLaunchKernelGGL(tree_hist_global, dim3(grid), dim3(kThreads), 0, stream, bins, n, F, slot, stats, S, B,
+                       nslots, hist);
+    return hipGetLastError() == hipSuccess ? 0 : 2;
+  }
+  const int gy = (F + FG - 1) / FG;
+  // ~4 workgroups per CU overall; each needs enough rows to amortise its LDS clear + flush
+  int64_t target = (int64_t)num_cus * 4 / ((int64_t)gy * groups);
+  if (target < 1) target = 1;
+  int64_t rows_per_block = (n + target - 1) / target;
+  const int64_t min_rows = 2048;
+  if (rows_per_block < min_rows) rows_per_block = min_rows;
+  const int64_t max_rows = ((int64_t)1 << 30) / (FG > 0 ? FG : 1);
+  if (rows_per_block > max_rows) rows_per_block = max_rows;
+  const int64_t gx = (n + rows_per_block - 1) / rows_per_block;
+  const size_t lds = (size_t)spg * FG * unit;
+  hipLaunchKernelGGL(tree_hist_lds, dim3((unsigned)gx, gy, groups), dim3(kThreads), lds, stream, bins, n, F,
+                     slot, stats, S, B, spg, FG, rows_per_block, hist);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+// node: int32 [n] current node index within the level (>= nnodes or < 0: already finished, untouched).
+// feat: [nnodes] split feature (-1 = leaf); base: [nnodes] first child index in the next level (for a leaf:
+// the negative code the row keeps from now on);
+// route: [nnodes, 256] child offset per bin.
+int alink_tree_route(const uint8_t* bins, int64_t n, int F, int32_t* node, const int32_t* feat,
+                     const int32_t* base, const int16_t* route, int nnodes, int num_cus, hipStream_t stream) {
+  if (n <= 0) return 0;
+  int64_t blocks = (n + kThreads - 1) / kThreads;
+  int grid = (int)(blocks < (int64_t)num_cus * 8 ? blocks : (int64_t)num_cus * 8);
+  hipLaunchKernelGGL(tree_route, dim3(grid), dim3(kThreads), 0, stream, bins, n, F, node, feat, base, route,
+                     nnodes);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+}  // extern "C"

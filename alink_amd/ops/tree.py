@@ -1,0 +1,112 @@
+"""Tree-training hot path: binned histograms (K7/K10) and level routing (K9), SURVEY §2.13.
+
+``histogram(bins, slot, stats, nslots, B)`` returns ``hist[nslots, F, B, S]`` with
+``hist[slot[r], f, bins[r, f], :] += stats[r, :]`` for every row whose slot is in ``[0, nslots)``.
+Reference: ``ConstructLocalBin.java:135-166`` (GBDT ``(g^2, g, h, 1)``) and ``paralleltree/TreeObj.java:321-390``
+(RF class counts / moments).
+
+``route(bins, node, feat, base, route_tab)`` moves every row one level down
+(``Split.java:64-195``): ``node[r] = base[v] + route_tab[v, bins[r, feat[v]]]`` for an internal node ``v``
+and ``node[r] = base[v]`` (a negative leaf code) for a leaf.
+
+On a GPU the HIP kernels in ``csrc/tree_hist.hip`` run (fp32 LDS-privatised atomics); on the CPU the
+fp64 ``index_add_`` reference below is used.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+
+__all__ = ["histogram", "histogram_torch", "route", "route_torch"]
+
+
+def _num_cus(device) -> int:
+    return torch.cuda.get_device_properties(device).multi_processor_count
+
+
+def histogram_torch(bins: torch.Tensor, slot: torch.Tensor, stats: torch.Tensor, nslots: int, B: int,
+                    dtype=torch.float64) -> torch.Tensor:
+    n, F = bins.shape
+    S = stats.shape[1]
+    out = torch.zeros((nslots * F * B, S), dtype=dtype, device=bins.device)
+    keep = (slot >= 0) & (slot < nslots)
+    if nslots == 0 or not bool(keep.any()):
+        return out.view(nslots, F, B, S)
+    rows = keep.nonzero().view(-1)
+    chunk = max(1, (1 << 22) // max(F, 1))
+    farange = torch.arange(F, device=bins.device, dtype=torch.long) * B
+    for s in range(0, rows.numel(), chunk):
+        r = rows[s:s + chunk]
+        idx = (slot[r].long() * (F * B))[:, None] + farange[None, :] + bins[r].long()
+        vals = stats[r].to(dtype)
+        out.index_add_(0, idx.reshape(-1), vals[:, None, :].expand(-1, F, -1).reshape(-1, S))
+    return out.view(nslots, F, B, S)
+
+
+def histogram(bins: torch.Tensor, slot: torch.Tensor, stats: torch.Tensor, nslots: int, B: int) -> torch.Tensor:
+    """[nslots, F, B, S] histogram (fp32 on GPU via HIP, fp64 on CPU)."""
+    if not bins.is_cuda:
+        return histogram_torch(bins, slot, stats, nslots, B)
+    if not _lib.available() and _lib.torch_fallback_allowed():
+        return histogram_torch(bins, slot, stats, nslots, B, dtype=torch.float32)
+    L = _lib.require()
+    n, F = bins.shape
+    S = stats.shape[1]
+    if bins.dtype != torch.uint8 or not bins.is_contiguous():
+        raise ValueError("bins must be a contiguous uint8 [n, F] matrix")
+    if B > 256:
+        raise ValueError("at most 256 bins per feature")
+    slot = slot.to(torch.int32).contiguous()
+    stats = stats.to(torch.float32).contiguous()
+    if slot.shape[0] != n or stats.shape[0] != n:
+        raise ValueError("slot/stats row count mismatch")
+    hist = torch.zeros((nslots, F, B, S), dtype=torch.float32, device=bins.device)
+    if n == 0 or nslots == 0:
+        return hist
+    rc = L.alink_tree_hist_f32(bins.data_ptr(), n, F, slot.data_ptr(), stats.data_ptr(), S, B, nslots,
+                               hist.data_ptr(), _num_cus(bins.device), _lib.stream_ptr(bins.device))
+    if rc != 0:
+        raise RuntimeError(f"alink_tree_hist_f32 failed: {rc}")
+    return hist
+
+
+def route_torch(bins, node, feat, base, route_tab):
+    nn = feat.shape[0]
+    act = (node >= 0) & (node < nn)
+    if not bool(act.any()):
+        return node
+    r = act.nonzero().view(-1)
+    v = node[r].long()
+    f = feat[v].long()
+    leaf = f < 0
+    b = bins[r, f.clamp(min=0)].long()
+    child = base[v].long() + torch.where(leaf, torch.zeros_like(b), route_tab[v, b].long())
+    node = node.clone()
+    node[r] = child.to(node.dtype)
+    return node
+
+
+def route(bins: torch.Tensor, node: torch.Tensor, feat: torch.Tensor, base: torch.Tensor,
+          route_tab: torch.Tensor) -> torch.Tensor:
+    """New int32 node ids (in place on GPU)."""
+    if not bins.is_cuda:
+        return route_torch(bins, node, feat, base, route_tab)
+    if not _lib.available() and _lib.torch_fallback_allowed():
+        return route_torch(bins, node, feat, base, route_tab)
+    L = _lib.require()
+    n, F = bins.shape
+    nn = feat.shape[0]
+    if route_tab.shape != (nn, 256):
+        raise ValueError("route table must be [nnodes, 256]")
+    feat = feat.to(torch.int32).contiguous()
+    if bool((feat >= F).any()):
+        raise ValueError("split feature out of range")
+    base = base.to(torch.int32).contiguous()
+    route_tab = route_tab.to(torch.int16).contiguous()
+    assert node.dtype == torch.int32 and node.is_contiguous() and node.shape[0] == n
+    rc = L.alink_tree_route(bins.data_ptr(), n, F, node.data_ptr(), feat.data_ptr(), base.data_ptr(),
+                            route_tab.data_ptr(), nn, _num_cus(bins.device), _lib.stream_ptr(bins.device))
+    if rc != 0:
+        raise RuntimeError(f"alink_tree_route failed: {rc}")
+    return node

@@ -4,3 +4,4 @@ from .clustering import *  # noqa: F401,F403
 from .dataproc import *  # noqa: F401,F403
 from .linear import *  # noqa: F401,F403
 from .feature import *  # noqa: F401,F403
+from .tree import *  # noqa: F401,F403

@@ -72,6 +72,26 @@ def scenario_lr(out):
     out["coef"] = json.loads(rows[1][1])["coefVector"]["data"]
 
 
+def scenario_gbdt(out):
+    from alink_amd import useLocalEnv, BatchOperator, GbdtTrainBatchOp, GbdtPredictBatchOp
+    df = _data_frame()
+    useLocalEnv(1)
+    src = BatchOperator.fromDataframe(df, schemaStr="x0 double, x1 double, x2 double, x3 double, y int")
+    m = GbdtTrainBatchOp().setFeatureCols(["x0", "x1", "x2", "x3"]).setLabelCol("y").setNumTrees(5) \
+        .setMinSamplesPerLeaf(5).setMaxDepth(4).linkFrom(src)
+    out["model"] = [list(r) for r in m.collect()]
+
+
+def scenario_rf(out):
+    from alink_amd import useLocalEnv, BatchOperator, RandomForestTrainBatchOp
+    df = _data_frame()
+    useLocalEnv(1)
+    src = BatchOperator.fromDataframe(df, schemaStr="x0 double, x1 double, x2 double, x3 double, y int")
+    m = RandomForestTrainBatchOp().setFeatureCols(["x0", "x1", "x2", "x3"]).setLabelCol("y").setNumTrees(3) \
+        .setMaxDepth(5).linkFrom(src)
+    out["model"] = [list(r) for r in m.collect()]
+
+
 def run(rank, world, port, scenario, outdir):
     os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
                        "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "ALINK_DEVICE": "cpu"})

@@ -66,3 +66,28 @@ def test_logistic_regression_two_processes_equal_single(tmp_path):
     two = _run("lr", 2, tmp_path)
     np.testing.assert_allclose(two[0]["coef"], two[1]["coef"], rtol=0, atol=0)
     np.testing.assert_allclose(one, two[0]["coef"], rtol=1e-6, atol=1e-8)
+
+
+def _tree_nodes(model_rows):
+    out = []
+    for r in model_rows[1:]:
+        if r[1] is None or not r[1].startswith('{"node"'):
+            continue
+        out.append(json.loads(r[1]))
+    return out
+
+
+@pytest.mark.parametrize("scenario", ["gbdt", "rf"])
+def test_trees_two_processes_equal_single(tmp_path, scenario):
+    """Histogram all-reduce over 2 ranks grows the same trees as one rank (same splits, same leaves)."""
+    one = _tree_nodes(_run(scenario, 1, tmp_path)[0]["model"])
+    two = _run(scenario, 2, tmp_path)
+    assert two[0]["model"] == two[1]["model"]
+    t2 = _tree_nodes(two[0]["model"])
+    assert len(one) == len(t2)
+    for a, b in zip(one, t2):
+        assert a["id"] == b["id"] and a.get("nextIds") == b.get("nextIds")
+        assert a["node"]["featureIndex"] == b["node"]["featureIndex"]
+        assert a["node"].get("continuousSplit") == pytest.approx(b["node"].get("continuousSplit"))
+        np.testing.assert_allclose(a["node"]["counter"]["distributions"], b["node"]["counter"]["distributions"],
+                                   rtol=1e-5, atol=1e-7)

@@ -1,0 +1,57 @@
+"""GBDT training throughput on a synthetic HIGGS-shaped table (n rows x F float features, binary label).
+
+    python tools/gbdt_bench.py --rows 10000000 --features 28 --trees 20 --depth 6
+Prints one JSON line: rows, features, trees, seconds, ms/tree, rows*trees/s.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", type=int, default=1000000)
+    ap.add_argument("--features", type=int, default=28)
+    ap.add_argument("--trees", type=int, default=20)
+    ap.add_argument("--depth", type=int, default=6)
+    ap.add_argument("--bins", type=int, default=128)
+    a = ap.parse_args()
+    from alink_amd import useLocalEnv, GbdtTrainBatchOp
+    from alink_amd.common.table import MTable, Column
+    from alink_amd.common.types import TableSchema, Types
+    env = useLocalEnv(1)
+    dev = env.device
+    g = torch.Generator(device=dev).manual_seed(0)
+    X = torch.randn((a.rows, a.features), generator=g, device=dev, dtype=torch.float64)
+    w = torch.linspace(-1, 1, a.features, device=dev, dtype=torch.float64)
+    y = ((X @ w + 0.5 * torch.sin(3 * X[:, 0]) + 0.3 * torch.randn(a.rows, generator=g, device=dev,
+                                                                  dtype=torch.float64)) > 0).to(torch.int32)
+    names = [f"f{i}" for i in range(a.features)] + ["label"]
+    cols = [Column(X[:, i].contiguous()) for i in range(a.features)] + [Column(y)]
+    mt = MTable(TableSchema(names, [Types.DOUBLE] * a.features + [Types.INT]), cols)
+    from alink_amd.operator.batch.source import TableSourceBatchOp
+    src = TableSourceBatchOp(mt)
+    op = GbdtTrainBatchOp().setFeatureCols(names[:-1]).setLabelCol("label").setNumTrees(a.trees) \
+        .setMaxDepth(a.depth).setMaxBins(a.bins).setMinSamplesPerLeaf(100)
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    t0 = time.time()
+    op.linkFrom(src)
+    op.getOutputTable()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    dt = time.time() - t0
+    print(json.dumps({"rows": a.rows, "features": a.features, "trees": a.trees, "depth": a.depth,
+                      "seconds": round(dt, 3), "ms_per_tree": round(1000 * dt / a.trees, 2),
+                      "row_trees_per_s": a.rows * a.trees / dt, "device": str(dev)}))
+
+
+if __name__ == "__main__":
+    main()
