@@ -150,13 +150,30 @@ class TreeBuilder:
         self.hist_dtype = torch.float32 if data.bins.is_cuda else torch.float64
 
     # -------------------------------------------------------------------------------------------
+    def _hist_cols(self, S: int) -> List[int]:
+        """Statistics the split search reads: GBDT needs (g, h, count) — the g^2 column only feeds node
+        counters, which come from per-node row sums instead — so the kernel moves 3 floats, not 4."""
+        return [1, 2, 3] if self.cfg.kind == "gbdt" else list(range(S))
+
     def _histograms(self, node_of_row, sample, slot_of_node: torch.Tensor, nslots: int, stats) -> torch.Tensor:
         slot = torch.full_like(node_of_row, -1)
         act = sample & (node_of_row >= 0) & (node_of_row < slot_of_node.numel())
         slot[act] = slot_of_node[node_of_row[act].long()].to(slot.dtype)
-        H = tops.histogram(self.d.bins, slot, stats, nslots, self.B)
+        cols = self._hist_cols(stats.shape[1])
+        sub = stats if len(cols) == stats.shape[1] else stats[:, cols].contiguous()
+        H = tops.histogram(self.d.bins, slot, sub, nslots, self.B)
         comm.all_reduce(H, "sum")
+        if len(cols) != stats.shape[1]:
+            full = torch.zeros(H.shape[:-1] + (stats.shape[1],), dtype=H.dtype, device=H.device)
+            full[..., cols] = H
+            H = full
         return H
+
+    def _node_totals(self, node_of_row, sample, nnodes: int, stats) -> np.ndarray:
+        """[nnodes, S] float64 per-node sums over the sampled rows (one pass over rows, then all-reduce)."""
+        out = tops.node_sums(node_of_row, sample, stats, nnodes)
+        comm.all_reduce(out, "sum")
+        return out[:nnodes].cpu().numpy()
 
     # -------------------------------------------------------------------------------------------
     def _search(self, Hn: torch.Tensor, feat_order: torch.Tensor, feat_ok: torch.Tensor):
@@ -357,7 +374,7 @@ class TreeBuilder:
         leaves: List[Node] = []
         # root statistics from a 1-slot histogram
         Hroot = self._histograms(node_of_row, sample, torch.zeros(1, dtype=torch.int32, device=dev), 1, stats)
-        root_total = Hroot[0, 0].to(torch.float64).sum(0).cpu().numpy()
+        root_total = self._node_totals(node_of_row, sample, 1, stats)[0]
         root = Node(counter=self._counter(root_total))
         bagging = cfg.kind != "gbdt" and rng is not None
         level = [_Pending(root, 1, root_total, order=list(range(F)))]
@@ -459,6 +476,12 @@ class TreeBuilder:
                     nxt.append(_Pending(child, p.depth + 1, sp.child_totals[c], parent=i, order=p.order))
             node_of_row = tops.route(self.d.bins, node_of_row, torch.as_tensor(feat, device=dev),
                                      torch.as_tensor(base, device=dev), torch.as_tensor(route, device=dev))
+            if nxt:
+                # exact child statistics (all S columns, missing rows where they were routed)
+                tot = self._node_totals(node_of_row, sample, len(nxt), stats)
+                for c, q in enumerate(nxt):
+                    q.total = tot[c]
+                    q.node.counter = self._counter(tot[c])
             self._prev_hist = level_hist
             level_hist = {}
             level = nxt

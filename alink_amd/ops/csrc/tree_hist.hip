@@ -74,6 +74,53 @@ __global__ __launch_bounds__(kThreads) void tree_hist_lds(
   }
 }
 
+// Row-per-lane variant: a lane owns one row, keeps its S statistics in registers and walks the row's
+// feature bytes; lanes of a wave hit the same feature at random bins (random LDS banks) and every row's
+// stats/slot are loaded once instead of once per feature.
+template <int S>
+__global__ __launch_bounds__(kThreads) void tree_hist_rows(
+    const uint8_t* __restrict__ bins, int64_t n, int F, const int32_t* __restrict__ slot,
+    const float* __restrict__ stats, int B, int slots_per_group, int FG, int64_t rows_per_block,
+    float* __restrict__ hist) {
+  extern __shared__ float sh[];
+  const int fstride = B * S + 1;
+  const int f0 = blockIdx.y * FG;
+  const int fg = min(FG, F - f0);
+  const int slot0 = blockIdx.z * slots_per_group;
+  const int lds_n = slots_per_group * FG * fstride;
+  for (int i = threadIdx.x; i < lds_n; i += kThreads) sh[i] = 0.f;
+  __syncthreads();
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t r1 = min(n, r0 + rows_per_block);
+  for (int64_t r = r0 + threadIdx.x; r < r1; r += kThreads) {
+    const int s = slot[r] - slot0;
+    if ((unsigned)s >= (unsigned)slots_per_group) continue;
+    float v[S];
+#pragma unroll
+    for (int k = 0; k < S; ++k) v[k] = stats[r * S + k];
+    const uint8_t* br = bins + r * F + f0;
+    float* base = sh + s * FG * fstride;
+    for (int f = 0; f < fg; ++f) {
+      float* h = base + f * fstride + (int)br[f] * S;
+#pragma unroll
+      for (int k = 0; k < S; ++k) atomicAdd(h + k, v[k]);
+    }
+  }
+  __syncthreads();
+  const int bs = B * S;
+  for (int i = threadIdx.x; i < lds_n; i += kThreads) {
+    const float val = sh[i];
+    if (val == 0.f) continue;
+    const int sf = i / fstride;
+    const int rem = i - sf * fstride;
+    if (rem >= bs) continue;
+    const int s = sf / FG;
+    const int f = sf - s * FG;
+    if (f >= fg) continue;
+    unsafeAtomicAdd(hist + ((int64_t)(slot0 + s) * F + (f0 + f)) * bs + rem, val);
+  }
+}
+
 __global__ __launch_bounds__(kThreads) void tree_hist_global(
     const uint8_t* __restrict__ bins, int64_t n, int F, const int32_t* __restrict__ slot,
     const float* __restrict__ stats, int S, int B, int nslots, float* __restrict__ hist) {
@@ -113,13 +160,73 @@ __global__ __launch_bounds__(kThreads) void tree_route(
   }
 }
 
+// Per-node statistic sums in fp64 (node counters: weight sum, count, g^2 ...): LDS-privatised ds_add_f64
+// per workgroup, one global f64 atomic per (node, stat) per workgroup.  Rows with node outside [0, nnodes)
+// or sample == 0 are skipped.
+__global__ __launch_bounds__(kThreads) void tree_node_sums(const int32_t* __restrict__ node,
+                                                           const uint8_t* __restrict__ sample,
+                                                           const float* __restrict__ stats, int64_t n, int S,
+                                                           int nnodes, int64_t rows_per_block,
+                                                           double* __restrict__ out) {
+  extern __shared__ double shd[];
+  const int m = nnodes * S;
+  for (int i = threadIdx.x; i < m; i += kThreads) shd[i] = 0.0;
+  __syncthreads();
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t r1 = min(n, r0 + rows_per_block);
+  for (int64_t r = r0 + threadIdx.x; r < r1; r += kThreads) {
+    const int v = node[r];
+    if ((unsigned)v >= (unsigned)nnodes || !sample[r]) continue;
+    for (int k = 0; k < S; ++k) atomicAdd(shd + v * S + k, (double)stats[r * S + k]);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < m; i += kThreads) {
+    const double x = shd[i];
+    if (x != 0.0) unsafeAtomicAdd(out + i, x);
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void tree_node_sums_global(const int32_t* __restrict__ node,
+                                                                  const uint8_t* __restrict__ sample,
+                                                                  const float* __restrict__ stats, int64_t n,
+                                                                  int S, int nnodes, double* __restrict__ out) {
+  for (int64_t r = (int64_t)blockIdx.x * kThreads + threadIdx.x; r < n; r += (int64_t)gridDim.x * kThreads) {
+    const int v = node[r];
+    if ((unsigned)v >= (unsigned)nnodes || !sample[r]) continue;
+    for (int k = 0; k < S; ++k) unsafeAtomicAdd(out + (int64_t)v * S + k, (double)stats[r * S + k]);
+  }
+}
+
 }  // namespace
 
 extern "C" {
 
+// out: [nnodes, S] fp64, zeroed by the caller.
+int alink_tree_node_sums(const int32_t* node, const uint8_t* sample, const float* stats, int64_t n, int S,
+                         int nnodes, double* out, int num_cus, hipStream_t stream) {
+  if (n <= 0 || nnodes <= 0) return 0;
+  const size_t lds = (size_t)nnodes * S * sizeof(double);
+  if (lds <= 64 * 1024) {
+    int64_t target = (int64_t)num_cus * 4;
+    int64_t rpb = (n + target - 1) / target;
+    if (rpb < 4096) rpb = 4096;
+    const int64_t gx = (n + rpb - 1) / rpb;
+    hipLaunchKernelGGL(tree_node_sums, dim3((unsigned)gx), dim3(kThreads), lds, stream, node, sample, stats, n, S,
+                       nnodes, rpb, out);
+  } else {
+    int64_t blocks = (n + kThreads - 1) / kThreads;
+    int grid = (int)(blocks < (int64_t)num_cus * 8 ? blocks : (int64_t)num_cus * 8);
+    hipLaunchKernelGGL(tree_node_sums_global, dim3(grid), dim3(kThreads), 0, stream, node, sample, stats, n, S,
+                       nnodes, out);
+  }
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+
 // hist must be zeroed by the caller: [nslots, F, B, S] fp32.
+// variant bit 0: use the (row, feature)-pair kernel instead of the row-per-lane kernel.
 int alink_tree_hist_f32(const uint8_t* bins, int64_t n, int F, const int32_t* slot, const float* stats,
-                        int S, int B, int nslots, float* hist, int num_cus, hipStream_t stream) {
+                        int S, int B, int nslots, float* hist, int num_cus, int variant, hipStream_t stream) {
   if (n <= 0 || nslots <= 0) return 0;
   if (F <= 0 || S <= 0 || B <= 0 || B > 256) return 1;
   const int unit = (B * S + 1) * (int)sizeof(float);  // one (slot, feature) row in LDS
@@ -154,8 +261,21 @@ int alink_tree_hist_f32(const uint8_t* bins, int64_t n, int F, const int32_t* sl
   if (rows_per_block > max_rows) rows_per_block = max_rows;
   const int64_t gx = (n + rows_per_block - 1) / rows_per_block;
   const size_t lds = (size_t)spg * FG * unit;
-  hipLaunchKernelGGL(tree_hist_lds, dim3((unsigned)gx, gy, groups), dim3(kThreads), lds, stream, bins, n, F,
-                     slot, stats, S, B, spg, FG, rows_per_block, hist);
+  const dim3 grid((unsigned)gx, gy, groups);
+  if (S >= 2 && S <= 4 && !(variant & 1)) {
+    if (S == 2)
+      hipLaunchKernelGGL(tree_hist_rows<2>, grid, dim3(kThreads), lds, stream, bins, n, F, slot, stats, B, spg, FG,
+                         rows_per_block, hist);
+    else if (S == 3)
+      hipLaunchKernelGGL(tree_hist_rows<3>, grid, dim3(kThreads), lds, stream, bins, n, F, slot, stats, B, spg, FG,
+                         rows_per_block, hist);
+    else
+      hipLaunchKernelGGL(tree_hist_rows<4>, grid, dim3(kThreads), lds, stream, bins, n, F, slot, stats, B, spg, FG,
+                         rows_per_block, hist);
+  } else {
+    hipLaunchKernelGGL(tree_hist_lds, grid, dim3(kThreads), lds, stream, bins, n, F, slot, stats, S, B, spg, FG,
+                       rows_per_block, hist);
+  }
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 

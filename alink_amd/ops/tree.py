@@ -18,7 +18,7 @@ import torch
 
 from . import _lib
 
-__all__ = ["histogram", "histogram_torch", "route", "route_torch"]
+__all__ = ["histogram", "histogram_torch", "route", "route_torch", "node_sums", "node_sums_torch"]
 
 
 def _num_cus(device) -> int:
@@ -44,7 +44,14 @@ def histogram_torch(bins: torch.Tensor, slot: torch.Tensor, stats: torch.Tensor,
     return out.view(nslots, F, B, S)
 
 
-def histogram(bins: torch.Tensor, slot: torch.Tensor, stats: torch.Tensor, nslots: int, B: int) -> torch.Tensor:
+import os
+
+# 0: row-per-lane kernel (S in 2..4), 1: (row, feature)-pair kernel
+HIST_VARIANT = int(os.environ.get("ALINK_TREE_HIST_VARIANT", "0"))
+
+
+def histogram(bins: torch.Tensor, slot: torch.Tensor, stats: torch.Tensor, nslots: int, B: int,
+              variant: int = None) -> torch.Tensor:
     """[nslots, F, B, S] histogram (fp32 on GPU via HIP, fp64 on CPU)."""
     if not bins.is_cuda:
         return histogram_torch(bins, slot, stats, nslots, B)
@@ -65,7 +72,8 @@ def histogram(bins: torch.Tensor, slot: torch.Tensor, stats: torch.Tensor, nslot
     if n == 0 or nslots == 0:
         return hist
     rc = L.alink_tree_hist_f32(bins.data_ptr(), n, F, slot.data_ptr(), stats.data_ptr(), S, B, nslots,
-                               hist.data_ptr(), _num_cus(bins.device), _lib.stream_ptr(bins.device))
+                               hist.data_ptr(), _num_cus(bins.device),
+                               HIST_VARIANT if variant is None else int(variant), _lib.stream_ptr(bins.device))
     if rc != 0:
         raise RuntimeError(f"alink_tree_hist_f32 failed: {rc}")
     return hist
@@ -110,3 +118,32 @@ def route(bins: torch.Tensor, node: torch.Tensor, feat: torch.Tensor, base: torc
     if rc != 0:
         raise RuntimeError(f"alink_tree_route failed: {rc}")
     return node
+
+
+def node_sums_torch(node: torch.Tensor, sample: torch.Tensor, stats: torch.Tensor, nnodes: int) -> torch.Tensor:
+    S = stats.shape[1]
+    out = torch.zeros((nnodes + 1, S), dtype=torch.float64, device=stats.device)
+    chunk = 1 << 22
+    for s0 in range(0, node.shape[0], chunk):
+        nd = node[s0:s0 + chunk]
+        ok = sample[s0:s0 + chunk] & (nd >= 0) & (nd < nnodes)
+        idx = torch.where(ok, nd.long(), torch.full_like(nd, nnodes, dtype=torch.long))
+        out.index_add_(0, idx, stats[s0:s0 + chunk].to(torch.float64))
+    return out[:nnodes]
+
+
+def node_sums(node: torch.Tensor, sample: torch.Tensor, stats: torch.Tensor, nnodes: int) -> torch.Tensor:
+    """[nnodes, S] fp64 sums of ``stats`` rows per node id (sampled rows only) — node counters."""
+    if not stats.is_cuda or (not _lib.available() and _lib.torch_fallback_allowed()):
+        return node_sums_torch(node, sample, stats, nnodes)
+    L = _lib.require()
+    n, S = stats.shape
+    node = node.to(torch.int32).contiguous()
+    samp = sample.to(torch.uint8).contiguous()
+    st = stats.to(torch.float32).contiguous()
+    out = torch.zeros((max(nnodes, 1), S), dtype=torch.float64, device=stats.device)
+    rc = L.alink_tree_node_sums(node.data_ptr(), samp.data_ptr(), st.data_ptr(), n, S, nnodes, out.data_ptr(),
+                                _num_cus(stats.device), _lib.stream_ptr(stats.device))
+    if rc != 0:
+        raise RuntimeError(f"alink_tree_node_sums failed: {rc}")
+    return out[:nnodes]

@@ -208,8 +208,9 @@ def test_hip_histogram_and_route_match_torch():
         slot = torch.as_tensor(rng.integers(-1, nslots, size=n), dtype=torch.int32)
         stats = torch.as_tensor(rng.normal(size=(n, S)), dtype=torch.float32)
         ref = tops.histogram_torch(bins, slot, stats.double(), nslots, B)
-        got = tops.histogram(bins.cuda(), slot.cuda(), stats.cuda(), nslots, B).cpu().double()
-        np.testing.assert_allclose(got.numpy(), ref.numpy(), rtol=1e-4, atol=2e-3)
+        for variant in (0, 1):
+            got = tops.histogram(bins.cuda(), slot.cuda(), stats.cuda(), nslots, B, variant=variant).cpu().double()
+            np.testing.assert_allclose(got.numpy(), ref.numpy(), rtol=1e-4, atol=2e-3)
     n, F = 70001, 5
     bins = torch.as_tensor(rng.integers(0, 200, size=(n, F)), dtype=torch.uint8)
     node = torch.as_tensor(rng.integers(-3, 4, size=n), dtype=torch.int32)
