@@ -1,0 +1,253 @@
+"""Alternating least squares (reference ``A/operator/common/recommendation/{AlsTrain,AlsPredict,
+AlsModelDataConverter,AlsModelMapper}.java``, ``A/operator/batch/recommendation/*``).
+
+Semantics kept from the reference: the rating graph is split into user and item "nodes"; every iteration
+updates all user factors (in ``numBlocks`` mini-batches, ``|id| % numBlocks``) and then all item factors;
+explicit feedback solves ``(Y_u^T Y_u + lambda n_u I) x = Y_u^T r_u`` (``AlsTrain.java:510-520``), implicit
+feedback ``(Y^T Y + Y_u^T C_u Y_u + lambda n_u^+ I) x = Y_u^T (1 + C_u) p_u`` with ``c = alpha r``
+(``:521-540``); non-negative solves use NNLS.
+
+MI355X design (SURVEY §2.3 P5 -> RCCL): instead of the reference's per-superstep request/response coGroups,
+the ratings are shuffled ONCE into two owner-partitioned CSR copies (by user and by item; one
+``all_to_all_single`` each), the small factor tables are replicated in HBM on every rank, each rank builds
+and solves the normal equations of the nodes it owns (HIP kernel ``ops/csrc/als.hip`` + batched Cholesky)
+and the updated rows are all-gathered.  Model table: ``(userCol LONG, itemCol LONG, factors STRING)`` with
+``Float.toString`` factors joined by spaces, user rows have a null item and vice versa.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from ...common.javafmt import java_float_str
+from ...common.mapper import ModelMapper, OutputColsHelper, find_col_index
+from ...common.params import Params
+from ...common.table import Column, MTable
+from ...common.types import TableSchema, Types
+from ...ops import als as aops
+from ...parallel import comm
+
+__all__ = ["AlsModelData", "AlsModelDataConverter", "AlsModelMapper", "train_als", "als_topk"]
+
+
+class AlsModelData:
+    def __init__(self, user_ids, user_factors, item_ids, item_factors):
+        self.user_ids = np.asarray(user_ids, dtype=np.int64)
+        self.user_factors = np.asarray(user_factors, dtype=np.float32)
+        self.item_ids = np.asarray(item_ids, dtype=np.int64)
+        self.item_factors = np.asarray(item_factors, dtype=np.float32)
+        self.user_map = {int(u): i for i, u in enumerate(self.user_ids)}
+        self.item_map = {int(u): i for i, u in enumerate(self.item_ids)}
+
+
+def _factor_str(f: np.ndarray) -> str:
+    return " ".join(java_float_str(float(x)) for x in f)
+
+
+class AlsModelDataConverter:
+    def __init__(self, user_col: str, item_col: str):
+        self.user_col, self.item_col = user_col, item_col
+
+    def getModelSchema(self) -> TableSchema:
+        return TableSchema([self.user_col, self.item_col, "factors"], [Types.LONG, Types.LONG, Types.STRING])
+
+    def save(self, m: AlsModelData) -> List[tuple]:
+        rows = [(int(u), None, _factor_str(f)) for u, f in zip(m.user_ids, m.user_factors)]
+        rows += [(None, int(i), _factor_str(f)) for i, f in zip(m.item_ids, m.item_factors)]
+        return rows
+
+    @staticmethod
+    def load(rows) -> AlsModelData:
+        us, uf, its, itf = [], [], [], []
+        for r in rows:
+            f = np.asarray([float(x) for x in str(r[2]).split(" ")], dtype=np.float32)
+            if r[0] is not None:
+                us.append(int(r[0]))
+                uf.append(f)
+            else:
+                its.append(int(r[1]))
+                itf.append(f)
+        rk = len(uf[0]) if uf else (len(itf[0]) if itf else 0)
+        return AlsModelData(us, np.stack(uf) if uf else np.zeros((0, rk)), its,
+                            np.stack(itf) if itf else np.zeros((0, rk)))
+
+
+# ---------------------------------------------------------------------------------------------------
+def _ids(mt: MTable, c: str, device) -> torch.Tensor:
+    col = mt.col(c)
+    if isinstance(col.values, torch.Tensor):
+        v = col.values.to(device)
+        if v.is_floating_point():
+            v = v.to(torch.float64).trunc()
+        return v.to(torch.int64)
+    return torch.tensor([int(float(v)) for v in col.to_list()], dtype=torch.int64, device=device)
+
+
+def _vals(mt: MTable, c: str, device) -> torch.Tensor:
+    col = mt.col(c)
+    if isinstance(col.values, torch.Tensor):
+        return col.values.to(device).to(torch.float32)
+    return torch.tensor([float(v) for v in col.to_list()], dtype=torch.float32, device=device)
+
+
+class _Side:
+    """Owner-partitioned CSR of one side (rows = owned nodes of this rank, ascending global index)."""
+
+    def __init__(self, rows_idx: torch.Tensor, nbr_idx: torch.Tensor, rating: torch.Tensor, raw_ids: torch.Tensor):
+        order = torch.argsort(rows_idx * (int(nbr_idx.max()) + 1 if nbr_idx.numel() else 1) + nbr_idx)
+        rows_idx, nbr_idx, rating = rows_idx[order], nbr_idx[order], rating[order]
+        self.nodes, counts = torch.unique_consecutive(rows_idx, return_counts=True)   # global node indices
+        self.indptr = torch.zeros(self.nodes.numel() + 1, dtype=torch.int64, device=rows_idx.device)
+        self.indptr[1:] = torch.cumsum(counts, 0)
+        self.nbr = nbr_idx.to(torch.int32)
+        self.rating = rating
+        self.raw = raw_ids[self.nodes]            # original ids of the owned nodes
+        self.n_pos = torch.zeros(self.nodes.numel(), dtype=torch.float64, device=rows_idx.device)
+        rows_local = torch.repeat_interleave(torch.arange(self.nodes.numel(), device=rows_idx.device), counts)
+        self.n_pos.index_add_(0, rows_local, (rating > 0).to(torch.float64))
+        self.n_all = counts.to(torch.float64)
+
+    def subset(self, mask: torch.Tensor):
+        sel = mask.nonzero().view(-1)
+        starts, ends = self.indptr[:-1][sel], self.indptr[1:][sel]
+        cnt = ends - starts
+        indptr = torch.zeros(sel.numel() + 1, dtype=torch.int64, device=sel.device)
+        indptr[1:] = torch.cumsum(cnt, 0)
+        if sel.numel():
+            pos = torch.repeat_interleave(starts - indptr[:-1], cnt) + torch.arange(int(indptr[-1]), device=sel.device)
+        else:
+            pos = torch.zeros(0, dtype=torch.int64, device=sel.device)
+        return sel, indptr, self.nbr[pos], self.rating[pos]
+
+
+def _update(side: _Side, mask: torch.Tensor, Y: torch.Tensor, X: torch.Tensor, lam: float, implicit: bool,
+            alpha: float, nonneg: bool, YtY: Optional[torch.Tensor]):
+    sel, indptr, nbr, rating = side.subset(mask)
+    if sel.numel():
+        A, b = aops.normal_equations(indptr, nbr, rating, Y, implicit, alpha)
+        A = A.to(torch.float64)
+        reg = (side.n_pos[sel] if implicit else side.n_all[sel]) * lam
+        if implicit:
+            A = A + YtY[None, :, :]
+        A = A + reg[:, None, None] * torch.eye(A.shape[1], dtype=A.dtype, device=A.device)[None]
+        x = aops.solve(A, b.to(torch.float64), nonneg)
+        rows = side.nodes[sel]
+    else:
+        x = torch.zeros((0, X.shape[1]), dtype=torch.float32, device=X.device)
+        rows = torch.zeros(0, dtype=torch.int64, device=X.device)
+    rows_all = comm.all_gather_varlen(rows)
+    x_all = comm.all_gather_varlen(x)
+    X[rows_all] = x_all.to(X.dtype)
+
+
+def train_als(mt: MTable, params: Params, env) -> AlsModelData:
+    dev = env.device
+    g = lambda k, d: params.get(k) if params.contains(k) and params.get(k) is not None else d  # noqa: E731
+    user_col, item_col, rate_col = params.get("userCol"), params.get("itemCol"), params.get("rateCol")
+    rank = int(g("rank", 10))
+    lam = float(g("lambda", 0.1))
+    num_iter = int(g("numIter", 10))
+    implicit = bool(g("implicitPrefs", False))
+    alpha = float(g("alpha", 40.0))
+    nonneg = bool(g("nonnegative", False))
+    nblocks = max(1, int(g("numBlocks", 1)))
+    seed = int(g("seed", 0)) if params.contains("seed") else 0
+    u = _ids(mt, user_col, dev)
+    it = _ids(mt, item_col, dev)
+    r = _vals(mt, rate_col, dev)
+    users = torch.unique(comm.all_gather_varlen(torch.unique(u)))
+    items = torch.unique(comm.all_gather_varlen(torch.unique(it)))
+    ui = torch.searchsorted(users, u)
+    ii = torch.searchsorted(items, it)
+    ws, me = comm.get_world_size(), comm.get_rank()
+
+    def shuffle(owner_idx):
+        if ws == 1:
+            return ui, ii, r
+        dest = owner_idx % ws
+        order = torch.argsort(dest)
+        counts = torch.bincount(dest, minlength=ws).tolist()
+        pairs = torch.stack([ui, ii], 1)[order]
+        rr = r[order]
+        got_p = comm.all_to_all_tensors(list(torch.split(pairs, counts)))
+        got_r = comm.all_to_all_tensors([x[:, None] for x in torch.split(rr, counts)])
+        p = torch.cat(got_p)
+        return p[:, 0], p[:, 1], torch.cat(got_r)[:, 0]
+
+    su, si, sr = shuffle(ui)
+    by_user = _Side(su, si, sr, users)
+    tu, ti, tr = shuffle(ii)
+    by_item = _Side(ti, tu, tr, items)
+    gen = torch.Generator().manual_seed(seed)
+    U = torch.rand((users.numel(), rank), generator=gen, dtype=torch.float32).to(dev)
+    V = torch.rand((items.numel(), rank), generator=gen, dtype=torch.float32).to(dev)
+    for _ in range(num_iter):
+        for side, Y, X in ((by_user, V, U), (by_item, U, V)):
+            YtY = (Y.to(torch.float64).T @ Y.to(torch.float64)) if implicit else None
+            for bb in range(nblocks):
+                mask = (side.raw.abs() % nblocks) == bb
+                _update(side, mask, Y, X, lam, implicit, alpha, nonneg, YtY)
+    return AlsModelData(users.cpu().numpy(), U.cpu().numpy(), items.cpu().numpy(), V.cpu().numpy())
+
+
+# ---------------------------------------------------------------------------------------------------
+class AlsModelMapper(ModelMapper):
+    """Predicted rating = sum_i (float) u_i * v_i accumulated in double (``AlsModelMapper.predictRating``);
+    unknown user or item -> null."""
+
+    def __init__(self, modelSchema, dataSchema, params=None):
+        super().__init__(modelSchema, dataSchema, params)
+        p = self.params
+        self.ucol = find_col_index(dataSchema.names, p.get("userCol"))
+        self.icol = find_col_index(dataSchema.names, p.get("itemCol"))
+        reserved = p.get("reservedCols") if p.contains("reservedCols") else None
+        self.helper = OutputColsHelper(dataSchema, [p.get("predictionCol")], [Types.DOUBLE], reserved)
+
+    def loadModel(self, rows):
+        self.model = AlsModelDataConverter.load(rows)
+
+    def _map_columns(self, mt):
+        m = self.model
+        us = mt.col(self.dataSchema.names[self.ucol]).to_list()
+        its = mt.col(self.dataSchema.names[self.icol]).to_list()
+        out = []
+        for a, b in zip(us, its):
+            ui = m.user_map.get(int(a)) if a is not None else None
+            ii = m.item_map.get(int(b)) if b is not None else None
+            if ui is None or ii is None:
+                out.append(None)
+            else:
+                prod = (m.user_factors[ui] * m.item_factors[ii]).astype(np.float32).astype(np.float64)
+                s = 0.0
+                for x in prod:
+                    s += float(x)
+                out.append(s)
+        return [Column.from_values(out, Types.DOUBLE)]
+
+
+def als_topk(model: AlsModelData, users: Sequence[int], k: int, device) -> List[tuple]:
+    """Top-``k`` items per requested user by ``u . v`` (one fp32 GEMM + ``topk`` on the device; reference
+    ``AlsPredict.recommendForUsers`` -> ``BlockwiseCross.findTopK``).  Output ``"item:score,..."``."""
+    want = [int(x) for x in users if x is not None and int(x) in model.user_map]
+    if not want:
+        return []
+    seen, uniq = set(), []
+    for x in want:
+        if x not in seen:
+            seen.add(x)
+            uniq.append(x)
+    U = torch.as_tensor(model.user_factors[[model.user_map[x] for x in uniq]], device=device)
+    V = torch.as_tensor(model.item_factors, device=device)
+    kk = min(k, V.shape[0])
+    out = []
+    chunk = 1 << 14
+    for s in range(0, len(uniq), chunk):
+        sc = U[s:s + chunk] @ V.T
+        val, idx = torch.topk(sc, kk, dim=1)
+        val, idx = val.cpu().numpy(), idx.cpu().numpy()
+        for j, uid in enumerate(uniq[s:s + chunk]):
+            items = model.item_ids[idx[j]]
+            out.append((uid, ",".join(f"{int(a)}:{java_float_str(float(b))}" for a, b in zip(items, val[j]))))
+    return out

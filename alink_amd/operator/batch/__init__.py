@@ -9,3 +9,4 @@ from .linear import *  # noqa: F401,F403
 from .evaluation import *  # noqa: F401,F403
 from .feature import *  # noqa: F401,F403
 from .tree import *  # noqa: F401,F403
+from .recommendation import *  # noqa: F401,F403

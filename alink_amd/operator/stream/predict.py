@@ -10,6 +10,7 @@ from ...models.clustering.kmeans import KMeansModelMapper
 from ...models.linear.model import AFTModelMapper, LinearModelMapper, SoftmaxModelMapper
 from ...models.feature import encoders as _E
 from ...models.feature import scalers as _S
+from ...models.recommendation.als import AlsModelMapper
 from ...models.tree.model import GbdtModelMapper, RandomForestModelMapper
 from .base import MapStreamOp, ModelMapStreamOp
 
@@ -41,6 +42,7 @@ _PREDICTORS = {
     "RandomForestRegPredictStreamOp": RandomForestModelMapper,
     "DecisionTreePredictStreamOp": RandomForestModelMapper,
     "DecisionTreeRegPredictStreamOp": RandomForestModelMapper,
+    "AlsPredictStreamOp": AlsModelMapper,
 }
 
 _MAPPERS = {

@@ -19,6 +19,7 @@ import os
 import pickle
 from typing import Any, List, Optional
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -187,6 +188,46 @@ def all_gather_tensor(t: torch.Tensor) -> torch.Tensor:
     parts = [torch.empty_like(t.cpu()) for _ in range(ws)]
     dist.all_gather(parts, t.cpu().contiguous())
     return torch.cat(parts).to(t.device)
+
+
+def all_gather_varlen(t: torch.Tensor) -> torch.Tensor:
+    """Concatenate tensors whose dim-0 length differs per rank (pads to the max length, one collective)."""
+    ws = get_world_size()
+    if ws == 1:
+        return t
+    n = torch.tensor([t.shape[0]], dtype=torch.int64, device=t.device if _backend() == "nccl" else "cpu")
+    lens = all_gather_tensor(n).cpu().tolist()
+    mx = max(lens)
+    pad = torch.zeros((mx,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+    pad[:t.shape[0]] = t
+    full = all_gather_tensor(pad)
+    return torch.cat([full[i * mx:i * mx + lens[i]] for i in range(ws)])
+
+
+def all_to_all_tensors(send: List[torch.Tensor]) -> List[torch.Tensor]:
+    """Tensor all-to-all (``send[j]`` -> rank j; same trailing shape/dtype): one ``all_to_all_single`` after a
+    count exchange.  This is the request/response shuffle of the reference's ALS (``AlsTrain.java:283-389``)
+    done as a single RCCL all-to-all(v)."""
+    ws = get_world_size()
+    if ws == 1:
+        return [send[0]]
+    dev = send[0].device
+    tail = tuple(send[0].shape[1:])
+    counts = torch.tensor([x.shape[0] for x in send], dtype=torch.int64)
+    all_counts = all_gather_tensor(counts.to(dev) if _backend() == "nccl" else counts).cpu().view(ws, ws)
+    recv_counts = all_counts[:, get_rank()].tolist()
+    flat = torch.cat([x.reshape(x.shape[0], -1) for x in send]) if send else torch.empty(0)
+    width = int(np.prod(tail)) if tail else 1
+    STATS.calls += 1
+    if _backend() == "nccl" and dev.type == "cuda":
+        out = torch.empty((sum(recv_counts), width), dtype=flat.dtype, device=dev)
+        dist.all_to_all_single(out, flat.reshape(-1, width).contiguous(), recv_counts, counts.tolist())
+    else:
+        out = torch.empty((sum(recv_counts), width), dtype=flat.dtype)
+        dist.all_to_all_single(out, flat.reshape(-1, width).cpu().contiguous(), recv_counts, counts.tolist())
+        out = out.to(dev)
+    res = list(torch.split(out, recv_counts))
+    return [x.reshape((x.shape[0],) + tail) for x in res]
 
 
 def all_gather_object(obj: Any) -> List[Any]:

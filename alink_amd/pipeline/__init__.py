@@ -5,3 +5,4 @@ from .dataproc import *  # noqa: F401,F403
 from .linear import *  # noqa: F401,F403
 from .feature import *  # noqa: F401,F403
 from .tree import *  # noqa: F401,F403
+from .recommendation import *  # noqa: F401,F403

@@ -92,6 +92,20 @@ def scenario_rf(out):
     out["model"] = [list(r) for r in m.collect()]
 
 
+def scenario_als(out):
+    import numpy as np
+    import pandas as pd
+    from alink_amd import useLocalEnv, BatchOperator, AlsTrainBatchOp
+    rng = np.random.default_rng(5)
+    uu, ii = np.nonzero(rng.random((40, 30)) < 0.4)
+    df = pd.DataFrame({"u": uu * 3 + 1, "i": ii * 7 + 2, "r": rng.normal(size=uu.size)})
+    useLocalEnv(1)
+    src = BatchOperator.fromDataframe(df, schemaStr="u bigint, i bigint, r double")
+    m = AlsTrainBatchOp().setUserCol("u").setItemCol("i").setRateCol("r").setRank(6).setNumIter(5) \
+        .setNumBlocks(2).linkFrom(src)
+    out["model"] = [list(r) for r in m.collect()]
+
+
 def run(rank, world, port, scenario, outdir):
     os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
                        "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "ALINK_DEVICE": "cpu"})

@@ -1,0 +1,125 @@
+"""ALS vs the reference docs (docs/en/als*.md) + format / mode / kernel checks."""
+import numpy as np
+import pandas as pd
+import pytest
+import torch
+
+from alink_amd import *  # noqa: F401,F403
+from alink_amd.models.recommendation.als import AlsModelDataConverter
+from alink_amd.ops import als as aops
+
+DATA = np.array([[1, 1, 0.6], [2, 2, 0.8], [2, 3, 0.6], [4, 1, 0.6], [4, 2, 0.3], [4, 3, 0.4]])
+REF = [0.579622, 0.766851, 0.581079, 0.574481, 0.298500, 0.382157]
+
+
+def _src():
+    df = pd.DataFrame({"user": DATA[:, 0].astype(int), "item": DATA[:, 1].astype(int), "rating": DATA[:, 2]})
+    return BatchOperator.fromDataframe(df, schemaStr="user bigint, item bigint, rating double"), df
+
+
+def _train(**kw):
+    op = AlsTrainBatchOp().setUserCol("user").setItemCol("item").setRateCol("rating").setNumIter(10) \
+        .setRank(10).setLambda(0.01)
+    for k, v in kw.items():
+        getattr(op, "set" + k[0].upper() + k[1:])(v)
+    return op
+
+
+def test_als_doc_example_predictions():
+    src, df = _src()
+    model = _train().linkFrom(src)
+    rows = model.collect()
+    assert [(r[0], r[1]) for r in rows] == [(1, None), (2, None), (4, None), (None, 1), (None, 2), (None, 3)]
+    assert len(rows[0][2].split(" ")) == 10
+    out = AlsPredictBatchOp().setUserCol("user").setItemCol("item").setPredictionCol("p") \
+        .linkFrom(model, src).collect()
+    # factor initialisation is random in the reference too; the fitted ratings agree to ~1e-2
+    np.testing.assert_allclose([r[3] for r in out], REF, atol=1e-2)
+    # unseen user -> null
+    df2 = pd.DataFrame({"user": [99], "item": [1], "rating": [0.0]})
+    miss = AlsPredictBatchOp().setUserCol("user").setItemCol("item").setPredictionCol("p").linkFrom(
+        model, BatchOperator.fromDataframe(df2, schemaStr="user bigint, item bigint, rating double")).collect()
+    assert miss[0][3] is None
+
+
+def test_als_topk_stream_and_pipeline():
+    src, df = _src()
+    model = _train().linkFrom(src)
+    top = AlsTopKPredictBatchOp().setUserCol("user").setPredictionCol("rec").setTopK(2).linkFrom(model, src).collect()
+    assert [r[0] for r in top] == [1, 2, 4]
+    for _, rec in top:
+        parts = [p.split(":") for p in rec.split(",")]
+        assert len(parts) == 2 and float(parts[0][1]) >= float(parts[1][1])
+    box = []
+    AlsPredictStreamOp(model).setUserCol("user").setItemCol("item").setPredictionCol("p") \
+        .linkFrom(StreamOperator.fromDataframe(df, schemaStr="user bigint, item bigint, rating double")) \
+        .link(CollectStreamOp(box))
+    StreamOperator.execute()
+    np.testing.assert_allclose(sorted(r[3] for r in box), sorted(REF), atol=1e-2)
+    m = ALS().setUserCol("user").setItemCol("item").setRateCol("rating").setRank(10).setLambda(0.01) \
+        .setPredictionCol("p").fit(src)
+    np.testing.assert_allclose([r[3] for r in m.transform(src).collect()], REF, atol=1e-2)
+
+
+def test_als_modes_and_roundtrip():
+    src, _ = _src()
+    nn = AlsModelDataConverter.load(_train(nonnegative=True, numBlocks=2).linkFrom(src).collect())
+    assert (nn.user_factors >= 0).all() and (nn.item_factors >= 0).all()
+    imp = AlsModelDataConverter.load(_train(implicitPrefs=True, alpha=10.0).linkFrom(src).collect())
+    # implicit preference: observed pairs score higher than unobserved ones for user 1 (rated only item 1)
+    s = imp.user_factors[imp.user_map[1]] @ imp.item_factors.T
+    assert s[imp.item_map[1]] > max(s[imp.item_map[2]], s[imp.item_map[3]])
+
+
+def test_als_recovers_low_rank_matrix():
+    rng = np.random.default_rng(0)
+    nu, ni, k = 60, 40, 4
+    U, V = rng.normal(size=(nu, k)), rng.normal(size=(ni, k))
+    R = U @ V.T
+    mask = rng.random((nu, ni)) < 0.5
+    uu, ii = np.nonzero(mask)
+    df = pd.DataFrame({"u": uu, "i": ii, "r": R[uu, ii]})
+    src = BatchOperator.fromDataframe(df, schemaStr="u bigint, i bigint, r double")
+    model = AlsTrainBatchOp().setUserCol("u").setItemCol("i").setRateCol("r").setRank(k).setLambda(1e-4) \
+        .setNumIter(30).linkFrom(src)
+    m = AlsModelDataConverter.load(model.collect())
+    pred = m.user_factors @ m.item_factors.T
+    held = ~mask
+    rmse = np.sqrt(((pred[np.ix_(m.user_ids, m.item_ids)] - R)[held] ** 2).mean())
+    assert rmse < 0.05 * R.std()
+
+
+def test_normal_equations_torch_matches_dense():
+    rng = np.random.default_rng(1)
+    Y = torch.as_tensor(rng.normal(size=(7, 5)), dtype=torch.float32)
+    indptr = torch.tensor([0, 3, 3, 6])
+    nbr = torch.tensor([0, 2, 6, 1, 2, 3], dtype=torch.int32)
+    rt = torch.tensor([1.0, -2.0, 0.5, 0.0, 3.0, 1.5])
+    A, b = aops.normal_equations(indptr, nbr, rt, Y, implicit=False)
+    Yd = Y.double()
+    np.testing.assert_allclose(A[0].numpy(), (Yd[[0, 2, 6]].T @ Yd[[0, 2, 6]]).numpy(), atol=1e-12)
+    np.testing.assert_allclose(b[2].numpy(), (Yd[[1, 2, 3]].T @ rt[3:].double()).numpy(), atol=1e-12)
+    assert float(A[1].abs().sum()) == 0.0
+    x = aops.nnls(torch.eye(2, dtype=torch.float64)[None] * 2, torch.tensor([[2.0, -4.0]], dtype=torch.float64))
+    np.testing.assert_allclose(x.numpy(), [[1.0, 0.0]])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("r", [3, 10, 16, 40, 64])
+@pytest.mark.parametrize("implicit", [False, True])
+def test_hip_als_normal_equations(r, implicit):
+    import alink_amd.ops._lib as L
+    assert L.available()
+    rng = np.random.default_rng(r)
+    m, n = 300, 500
+    counts = rng.integers(0, 90, size=m)
+    indptr = torch.zeros(m + 1, dtype=torch.int64)
+    indptr[1:] = torch.as_tensor(np.cumsum(counts))
+    nnz = int(indptr[-1])
+    nbr = torch.as_tensor(rng.integers(0, n, size=nnz), dtype=torch.int32)
+    rt = torch.as_tensor(rng.normal(size=nnz), dtype=torch.float32)
+    Y = torch.as_tensor(rng.normal(size=(n, r)), dtype=torch.float32)
+    A0, b0 = aops.normal_equations_torch(indptr, nbr, rt, Y, implicit, 3.0)
+    A1, b1 = aops.normal_equations(indptr.cuda(), nbr.cuda(), rt.cuda(), Y.cuda(), implicit, 3.0)
+    np.testing.assert_allclose(A1.cpu().double().numpy(), A0.numpy(), rtol=1e-4, atol=1e-3)
+    np.testing.assert_allclose(b1.cpu().double().numpy(), b0.numpy(), rtol=1e-4, atol=1e-3)

@@ -91,3 +91,14 @@ def test_trees_two_processes_equal_single(tmp_path, scenario):
         assert a["node"].get("continuousSplit") == pytest.approx(b["node"].get("continuousSplit"))
         np.testing.assert_allclose(a["node"]["counter"]["distributions"], b["node"]["counter"]["distributions"],
                                    rtol=1e-5, atol=1e-7)
+
+
+def test_als_two_processes_equal_single(tmp_path):
+    """Owner-partitioned CSR + all-to-all shuffle + all-gathered factor rows == single-process ALS."""
+    one = _run("als", 1, tmp_path)[0]["model"]
+    two = _run("als", 2, tmp_path)
+    assert two[0]["model"] == two[1]["model"]
+    assert [r[:2] for r in one] == [r[:2] for r in two[0]["model"]]
+    a = np.array([[float(x) for x in r[2].split()] for r in one])
+    b = np.array([[float(x) for x in r[2].split()] for r in two[0]["model"]])
+    np.testing.assert_allclose(a, b, rtol=1e-4, atol=1e-5)
