@@ -141,6 +141,18 @@ class SimpleModelDataConverter(ModelDataConverter):
     def getModelSchema(self):
         return TableSchema(["model_id", "model_info"], [Types.LONG, Types.STRING])
 
+    @staticmethod
+    def rows_from(meta: Params, data: Iterable[str]) -> List[Row]:
+        """Model rows of the default ``(model_id, model_info)`` schema from a meta + data strings."""
+        out: List[Row] = []
+        append_meta_rows(meta, out, 2)
+        append_data_rows(data, out, 2)
+        return out
+
+    @staticmethod
+    def split_rows(rows) -> Tuple[Params, List[str]]:
+        return extract_meta_and_data(rows)
+
     def save(self, model):
         meta, data = self.serializeModel(model)
         out: List[Row] = []

@@ -10,3 +10,4 @@ from .evaluation import *  # noqa: F401,F403
 from .feature import *  # noqa: F401,F403
 from .tree import *  # noqa: F401,F403
 from .recommendation import *  # noqa: F401,F403
+from .nlp import *  # noqa: F401,F403

@@ -1,0 +1,56 @@
+"""NLP batch operators (reference ``A/operator/batch/nlp/*``); mappers in ``models/nlp/text.py``."""
+from __future__ import annotations
+
+from ...common.model.converter import SimpleModelDataConverter
+from ...common.table import MTable
+from ...models.nlp import text as T
+from ..base import BatchOperator
+from .utils import MapBatchOp, ModelMapBatchOp
+
+__all__ = ["TokenizerBatchOp", "RegexTokenizerBatchOp", "StopWordsRemoverBatchOp", "NGramBatchOp", "SegmentBatchOp",
+           "DocCountVectorizerTrainBatchOp", "DocCountVectorizerPredictBatchOp",
+           "DocHashCountVectorizerTrainBatchOp", "DocHashCountVectorizerPredictBatchOp"]
+
+
+class TokenizerBatchOp(MapBatchOp):
+    MAPPER = T.TokenizerMapper
+
+
+class RegexTokenizerBatchOp(MapBatchOp):
+    MAPPER = T.RegexTokenizerMapper
+
+
+class StopWordsRemoverBatchOp(MapBatchOp):
+    MAPPER = T.StopWordsRemoverMapper
+
+
+class NGramBatchOp(MapBatchOp):
+    MAPPER = T.NGramMapper
+
+
+class SegmentBatchOp(MapBatchOp):
+    MAPPER = T.SegmentMapper
+
+
+class DocCountVectorizerTrainBatchOp(BatchOperator):
+    def linkFrom(self, *inputs):
+        mt = self.checkAndGetFirst(inputs).getOutputTable()
+        rows = T.train_doc_count_vectorizer(mt, self.getParams())
+        self.setOutputTable(MTable.from_rows(rows, SimpleModelDataConverter().getModelSchema(), replicated=True))
+        return self
+
+
+class DocHashCountVectorizerTrainBatchOp(BatchOperator):
+    def linkFrom(self, *inputs):
+        mt = self.checkAndGetFirst(inputs).getOutputTable()
+        rows = T.train_doc_hash_count_vectorizer(mt, self.getParams())
+        self.setOutputTable(MTable.from_rows(rows, SimpleModelDataConverter().getModelSchema(), replicated=True))
+        return self
+
+
+class DocCountVectorizerPredictBatchOp(ModelMapBatchOp):
+    MAPPER = T.DocCountVectorizerModelMapper
+
+
+class DocHashCountVectorizerPredictBatchOp(ModelMapBatchOp):
+    MAPPER = T.DocHashCountVectorizerModelMapper

@@ -10,6 +10,7 @@ from ...models.clustering.kmeans import KMeansModelMapper
 from ...models.linear.model import AFTModelMapper, LinearModelMapper, SoftmaxModelMapper
 from ...models.feature import encoders as _E
 from ...models.feature import scalers as _S
+from ...models.nlp import text as _T
 from ...models.recommendation.als import AlsModelMapper
 from ...models.tree.model import GbdtModelMapper, RandomForestModelMapper
 from .base import MapStreamOp, ModelMapStreamOp
@@ -43,6 +44,8 @@ _PREDICTORS = {
     "DecisionTreePredictStreamOp": RandomForestModelMapper,
     "DecisionTreeRegPredictStreamOp": RandomForestModelMapper,
     "AlsPredictStreamOp": AlsModelMapper,
+    "DocCountVectorizerPredictStreamOp": _T.DocCountVectorizerModelMapper,
+    "DocHashCountVectorizerPredictStreamOp": _T.DocHashCountVectorizerModelMapper,
 }
 
 _MAPPERS = {
@@ -50,6 +53,11 @@ _MAPPERS = {
     "BucketizerStreamOp": _E.BucketizerMapper,
     "FeatureHasherStreamOp": _E.FeatureHasherMapper,
     "DCTStreamOp": _E.DCTMapper,
+    "TokenizerStreamOp": _T.TokenizerMapper,
+    "RegexTokenizerStreamOp": _T.RegexTokenizerMapper,
+    "StopWordsRemoverStreamOp": _T.StopWordsRemoverMapper,
+    "NGramStreamOp": _T.NGramMapper,
+    "SegmentStreamOp": _T.SegmentMapper,
 }
 
 __all__ = []

@@ -1,0 +1,45 @@
+"""NLP pipeline stages (reference ``A/pipeline/nlp/*``)."""
+from ..models.nlp import text as T
+from ..operator.batch import nlp as N
+from .base import MapModel, MapTransformer, Trainer
+
+__all__ = ["Tokenizer", "RegexTokenizer", "StopWordsRemover", "NGram", "Segment", "DocCountVectorizer",
+           "DocCountVectorizerModel", "DocHashCountVectorizer", "DocHashCountVectorizerModel"]
+
+
+class Tokenizer(MapTransformer):
+    MAPPER = T.TokenizerMapper
+
+
+class RegexTokenizer(MapTransformer):
+    MAPPER = T.RegexTokenizerMapper
+
+
+class StopWordsRemover(MapTransformer):
+    MAPPER = T.StopWordsRemoverMapper
+
+
+class NGram(MapTransformer):
+    MAPPER = T.NGramMapper
+
+
+class Segment(MapTransformer):
+    MAPPER = T.SegmentMapper
+
+
+class DocCountVectorizer(Trainer):
+    TRAIN_OP = N.DocCountVectorizerTrainBatchOp
+    MODEL = "DocCountVectorizerModel"
+
+
+class DocCountVectorizerModel(MapModel):
+    MAPPER = T.DocCountVectorizerModelMapper
+
+
+class DocHashCountVectorizer(Trainer):
+    TRAIN_OP = N.DocHashCountVectorizerTrainBatchOp
+    MODEL = "DocHashCountVectorizerModel"
+
+
+class DocHashCountVectorizerModel(MapModel):
+    MAPPER = T.DocHashCountVectorizerModelMapper

@@ -1,0 +1,81 @@
+"""NLP operators vs the reference docs (docs/en/{tokenizer,regextokenizer,ngram,stopwordsremover,
+doccountvectorizer,dochashcountvectorizer}*.md)."""
+import json
+
+import pandas as pd
+
+from alink_amd import *  # noqa: F401,F403
+from alink_amd.models.nlp.text import JiebaSegmenter, java_split
+
+EN = pd.DataFrame({"id": [0, 1, 2], "text": ["That is an English Book!", "Do you like math?", "Have a good day!"]})
+ZH = pd.DataFrame({"id": [0, 1, 2, 3, 4], "text": [
+    "二手旧书:医学电磁成像", "二手美国文学选读（ 下册 ）李宜燮南开大学出版社 9787310003969",
+    "二手正版图解象棋入门/谢恩思主编/华龄出版社", "二手中国糖尿病文献索引", "二手郁达夫文集（ 国内版 ）全十二册馆藏书"]})
+
+
+def _en():
+    return BatchOperator.fromDataframe(EN, schemaStr="id long, text string")
+
+
+def _zh():
+    return BatchOperator.fromDataframe(ZH, schemaStr="id int, text string")
+
+
+def test_java_split_semantics():
+    assert java_split("  a b", r"\s+") == ["", "a", "b"]
+    assert java_split("a b  ", r"\s+") == ["a", "b"]
+    assert java_split("", " ") == [""]
+    assert java_split("a  b", " ") == ["a", "", "b"]
+
+
+def test_tokenizers_and_ngram_doc():
+    assert [r[1] for r in TokenizerBatchOp().setSelectedCol("text").linkFrom(_en()).collect()] == \
+        ["that is an english book!", "do you like math?", "have a good day!"]
+    out = RegexTokenizerBatchOp().setSelectedCol("text").setGaps(False).setToLowerCase(True) \
+        .setOutputCol("token").setPattern("\\w+").linkFrom(_en()).collect()
+    assert [r[2] for r in out] == ["that is an english book", "do you like math", "have a good day"]
+    assert [r[1] for r in NGramBatchOp().setSelectedCol("text").linkFrom(_en()).collect()] == \
+        ["That_is is_an an_English English_Book!", "Do_you you_like like_math?", "Have_a a_good good_day!"]
+    box = []
+    TokenizerStreamOp().setSelectedCol("text").linkFrom(
+        StreamOperator.fromDataframe(EN, schemaStr="id long, text string")).link(CollectStreamOp(box))
+    StreamOperator.execute()
+    assert sorted(r[1] for r in box) == ["do you like math?", "have a good day!", "that is an english book!"]
+
+
+def test_segment_stopwords_and_user_dict():
+    seg = SegmentBatchOp().setSelectedCol("text").setOutputCol("segment").linkFrom(_zh())
+    rem = StopWordsRemoverBatchOp().setSelectedCol("segment").setOutputCol("remover").linkFrom(seg).collect()
+    # punctuation is in the default stop list; "二手" starts every document
+    assert all(r[3].split(" ")[0] == "二手" for r in rem)
+    assert ":" not in rem[0][3] and "/" not in rem[2][3]
+    s = JiebaSegmenter(["电磁成像"])
+    assert "电磁成像" in s.cut("医学电磁成像")
+
+
+def test_doc_count_vectorizer_doc_model():
+    segt = SegmentBatchOp().setSelectedCol("text").linkFrom(_zh())
+    train = DocCountVectorizerTrainBatchOp().setSelectedCol("text").linkFrom(segt)
+    rows = train.collect()
+    assert rows[0][1] == '{"minTF":"1.0","featureType":"\\"WORD_COUNT\\""}'
+    # reference model head (docs/en/doccountvectorizerpredictbatchop.md)
+    assert [rows[i][1] for i in range(1, 6)] == [
+        '{"f0":"二手","f1":0.0,"f2":0}', '{"f0":"/","f1":1.0986122886681098,"f2":1}',
+        '{"f0":"出版社","f1":0.6931471805599453,"f2":2}', '{"f0":"（","f1":0.6931471805599453,"f2":3}',
+        '{"f0":"）","f1":0.6931471805599453,"f2":4}']
+    pred = DocCountVectorizerPredictBatchOp().setSelectedCol("text").linkFrom(train, segt).collect()
+    v = pred[0][1]
+    assert v.size() == len(rows) - 1 and v.get(0) == 1.0
+
+
+def test_doc_hash_count_vectorizer_doc_indices():
+    segt = SegmentBatchOp().setSelectedCol("text").linkFrom(_zh())
+    train = DocHashCountVectorizerTrainBatchOp().setSelectedCol("text").linkFrom(segt)
+    meta = json.loads(train.collect()[0][1])
+    assert meta["numFeatures"] == "262144"
+    pred = DocHashCountVectorizerPredictBatchOp().setSelectedCol("text").linkFrom(train, segt).collect()
+    v1 = pred[1][1]
+    # murmur3(word) indices of the reference output: "$262144$0:6.0 37505:1.0 46743:1.0 93228:1.0 ..."
+    idx = set(v1.getIndices().tolist())
+    assert {0, 37505, 93228} <= idx and v1.get(0) == 6.0
+    assert {64444, 206232} <= set(pred[0][1].getIndices().tolist())
