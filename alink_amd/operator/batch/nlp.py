@@ -4,12 +4,14 @@ from __future__ import annotations
 from ...common.model.converter import SimpleModelDataConverter
 from ...common.table import MTable
 from ...models.nlp import text as T
+from ...models.nlp import word2vec as W
 from ..base import BatchOperator
 from .utils import MapBatchOp, ModelMapBatchOp
 
 __all__ = ["TokenizerBatchOp", "RegexTokenizerBatchOp", "StopWordsRemoverBatchOp", "NGramBatchOp", "SegmentBatchOp",
            "DocCountVectorizerTrainBatchOp", "DocCountVectorizerPredictBatchOp",
-           "DocHashCountVectorizerTrainBatchOp", "DocHashCountVectorizerPredictBatchOp"]
+           "DocHashCountVectorizerTrainBatchOp", "DocHashCountVectorizerPredictBatchOp", "Word2VecTrainBatchOp",
+           "Word2VecPredictBatchOp"]
 
 
 class TokenizerBatchOp(MapBatchOp):
@@ -54,3 +56,15 @@ class DocCountVectorizerPredictBatchOp(ModelMapBatchOp):
 
 class DocHashCountVectorizerPredictBatchOp(ModelMapBatchOp):
     MAPPER = T.DocHashCountVectorizerModelMapper
+
+
+class Word2VecTrainBatchOp(BatchOperator):
+    def linkFrom(self, *inputs):
+        mt = self.checkAndGetFirst(inputs).getOutputTable()
+        rows = W.train_word2vec(mt, self.getParams(), self.env)
+        self.setOutputTable(MTable.from_rows(rows, W.MODEL_SCHEMA, replicated=True))
+        return self
+
+
+class Word2VecPredictBatchOp(ModelMapBatchOp):
+    MAPPER = W.Word2VecModelMapper

@@ -11,6 +11,7 @@ from ...models.linear.model import AFTModelMapper, LinearModelMapper, SoftmaxMod
 from ...models.feature import encoders as _E
 from ...models.feature import scalers as _S
 from ...models.nlp import text as _T
+from ...models.nlp import word2vec as _W
 from ...models.recommendation.als import AlsModelMapper
 from ...models.tree.model import GbdtModelMapper, RandomForestModelMapper
 from .base import MapStreamOp, ModelMapStreamOp
@@ -46,6 +47,7 @@ _PREDICTORS = {
     "AlsPredictStreamOp": AlsModelMapper,
     "DocCountVectorizerPredictStreamOp": _T.DocCountVectorizerModelMapper,
     "DocHashCountVectorizerPredictStreamOp": _T.DocHashCountVectorizerModelMapper,
+    "Word2VecPredictStreamOp": _W.Word2VecModelMapper,
 }
 
 _MAPPERS = {

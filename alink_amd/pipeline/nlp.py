@@ -1,10 +1,11 @@
 """NLP pipeline stages (reference ``A/pipeline/nlp/*``)."""
 from ..models.nlp import text as T
+from ..models.nlp import word2vec as W
 from ..operator.batch import nlp as N
 from .base import MapModel, MapTransformer, Trainer
 
 __all__ = ["Tokenizer", "RegexTokenizer", "StopWordsRemover", "NGram", "Segment", "DocCountVectorizer",
-           "DocCountVectorizerModel", "DocHashCountVectorizer", "DocHashCountVectorizerModel"]
+           "DocCountVectorizerModel", "DocHashCountVectorizer", "DocHashCountVectorizerModel", "Word2Vec", "Word2VecModel"]
 
 
 class Tokenizer(MapTransformer):
@@ -43,3 +44,12 @@ class DocHashCountVectorizer(Trainer):
 
 class DocHashCountVectorizerModel(MapModel):
     MAPPER = T.DocHashCountVectorizerModelMapper
+
+
+class Word2Vec(Trainer):
+    TRAIN_OP = N.Word2VecTrainBatchOp
+    MODEL = "Word2VecModel"
+
+
+class Word2VecModel(MapModel):
+    MAPPER = W.Word2VecModelMapper

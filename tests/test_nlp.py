@@ -79,3 +79,29 @@ def test_doc_hash_count_vectorizer_doc_indices():
     idx = set(v1.getIndices().tolist())
     assert {0, 37505, 93228} <= idx and v1.get(0) == 6.0
     assert {64444, 206232} <= set(pred[0][1].getIndices().tolist())
+
+
+def test_word2vec_doc_and_semantics():
+    import numpy as np
+    from alink_amd.models.nlp.word2vec import huffman
+    df = pd.DataFrame({"tokens": ["A B C"]})
+    src = BatchOperator.fromDataframe(df, schemaStr="tokens string")
+    train = Word2VecTrainBatchOp().setSelectedCol("tokens").setMinCount(1).setVectorSize(4).linkFrom(src)
+    rows = train.collect()
+    assert sorted(r[0] for r in rows) == ["A", "B", "C"] and rows[0][1].size() == 4
+    pred = Word2VecPredictBatchOp().setSelectedCol("tokens").linkFrom(train, src).collect()
+    vecs = np.stack([r[1].data for r in rows])
+    got = np.array([float(x) for x in pred[0][0].split(" ")])
+    np.testing.assert_allclose(got, vecs.mean(0), rtol=1e-12)
+    # Huffman: frequent words get short codes, codes are prefix-free
+    C, P, L = huffman(np.array([50, 20, 10, 5, 5]))
+    assert L[0] <= L[-1] and len({tuple(C[i, :L[i]]) for i in range(5)}) == 5
+    # co-occurring words end up closer than unrelated ones
+    rng = np.random.default_rng(0)
+    docs = [" ".join(rng.permutation(["x1", "x2", "x3"]).tolist()) for _ in range(150)] + \
+           [" ".join(rng.permutation(["y1", "y2", "y3"]).tolist()) for _ in range(150)]
+    src2 = BatchOperator.fromDataframe(pd.DataFrame({"t": docs}), schemaStr="t string")
+    m = Word2VecTrainBatchOp().setSelectedCol("t").setMinCount(1).setVectorSize(8).setNumIter(5) \
+        .setWindow(2).linkFrom(src2).collect()
+    E = {r[0]: r[1].data / np.linalg.norm(r[1].data) for r in m}
+    assert E["x1"] @ E["x2"] > E["x1"] @ E["y1"]
