@@ -11,7 +11,7 @@ from typing import List, Optional, Sequence
 
 import numpy as np
 
-__all__ = ["lib", "parse_csv_lines", "murmur3_utf16", "parse_dense_vectors"]
+__all__ = ["lib", "parse_csv_lines", "murmur3_utf16", "parse_dense_vectors", "ftrl_update_csr"]
 
 _PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libalink_native.so")
 lib = None
@@ -21,6 +21,7 @@ if os.path.exists(_PATH):
         lib.alink_csv_parse.restype = ctypes.c_int
         lib.alink_murmur3_utf16_batch.restype = None
         lib.alink_parse_dense_vectors.restype = ctypes.c_int
+        lib.alink_ftrl_update_csr.restype = ctypes.c_int
     except OSError:
         lib = None
 
@@ -117,3 +118,22 @@ def parse_dense_vectors(strings: Sequence[str], d: int) -> Optional[np.ndarray]:
     if rc != 0:
         return None
     return out
+
+
+def ftrl_update_csr(indptr, indices, values, label, w, n, z, alpha, beta, l1, l2, scale=1.0) -> bool:
+    """Sequential FTRL-proximal over CSR rows (in place on ``w, n, z``); False when the library is missing."""
+    if lib is None:
+        return False
+    indptr = np.ascontiguousarray(indptr, dtype=np.int64)
+    indices = np.ascontiguousarray(indices, dtype=np.int32)
+    values = np.ascontiguousarray(values, dtype=np.float64)
+    label = np.ascontiguousarray(label, dtype=np.float64)
+    for a in (w, n, z):
+        assert a.dtype == np.float64 and a.flags["C_CONTIGUOUS"]
+    rc = lib.alink_ftrl_update_csr(_ptr(indptr), _ptr(indices), _ptr(values), _ptr(label),
+                                   ctypes.c_int64(len(indptr) - 1), _ptr(w), _ptr(n), _ptr(z),
+                                   ctypes.c_int64(len(w)), ctypes.c_double(alpha), ctypes.c_double(beta),
+                                   ctypes.c_double(l1), ctypes.c_double(l2), ctypes.c_double(scale))
+    if rc != 0:
+        raise ValueError("feature index out of range in FTRL update")
+    return True

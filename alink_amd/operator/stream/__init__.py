@@ -7,3 +7,4 @@ from .sink import *  # noqa: F401,F403
 from .sql import *  # noqa: F401,F403
 from .dataproc import *  # noqa: F401,F403
 from .evaluation import *  # noqa: F401,F403
+from .onlinelearning import *  # noqa: F401,F403
