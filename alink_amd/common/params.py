@@ -147,7 +147,10 @@ def search_enum(enum_cls, value: str, param_name: str = ""):
 def _decode(json_str: Optional[str], info: Optional[ParamInfo]):
     if json_str is None:
         return None
-    v = json.loads(json_str)
+    try:
+        v = json.loads(json_str)
+    except ValueError:
+        v = json_str    # legacy models store some string params unquoted (e.g. "vectorCol":"vec")
     if info is None:
         return v
     t = info.value_type

@@ -10,6 +10,7 @@ from ...models.clustering.kmeans import KMeansModelMapper
 from ...models.linear.model import AFTModelMapper, LinearModelMapper, SoftmaxModelMapper
 from ...models.feature import encoders as _E
 from ...models.feature import scalers as _S
+from ...models.classification.naive_bayes import NaiveBayesTextModelMapper
 from ...models.nlp import text as _T
 from ...models.nlp import word2vec as _W
 from ...models.recommendation.als import AlsModelMapper
@@ -48,6 +49,7 @@ _PREDICTORS = {
     "DocCountVectorizerPredictStreamOp": _T.DocCountVectorizerModelMapper,
     "DocHashCountVectorizerPredictStreamOp": _T.DocHashCountVectorizerModelMapper,
     "Word2VecPredictStreamOp": _W.Word2VecModelMapper,
+    "NaiveBayesTextPredictStreamOp": NaiveBayesTextModelMapper,
 }
 
 _MAPPERS = {
