@@ -149,6 +149,10 @@ class NaiveBayesTextModelMapper(RichModelMapper):
             return X @ self.minmat.T + self.model["pi"][None, :] + self.phi[None, :]
         return X @ th.T + self.model["pi"][None, :]
 
+    def _map_row_values(self, row):
+        mt = MTable.from_rows([tuple(row)], self.dataSchema)
+        return [c.to_list()[0] for c in self._map_columns(mt)]
+
     def _map_columns(self, mt):
         S = self._scores(mt)
         labels = self.model["labels"]

@@ -170,8 +170,9 @@ def train_word2vec(mt: MTable, params: Params, env) -> List[tuple]:
         lo, hi = (len(docs) * k) // sync, (len(docs) * (k + 1)) // sync
         cen, ctx = _pairs(docs[lo:hi], window, random_window, rng)
         if cen.size:
+            # pairs in one batch read the same (stale) vectors; keep a batch to a few updates per word
             _sgd(inp, out, Ct, Pt, Lt, torch.as_tensor(cen, device=dev), torch.as_tensor(ctx, device=dev), alpha,
-                 batch=8192 if dev.type != "cpu" else 256)
+                 batch=int(min(8192, max(16, 2 * V))))
         if ws > 1:
             comm.all_reduce(inp, "sum")
             comm.all_reduce(out, "sum")

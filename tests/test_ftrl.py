@@ -1,4 +1,6 @@
 """FTRL online learning vs the reference docs (docs/en/ftrltrainstreamop.md) + update-rule checks."""
+import json
+
 import numpy as np
 import pandas as pd
 import pytest
@@ -33,7 +35,9 @@ def _run(interval=1):
 def test_ftrl_doc_example():
     preds, snaps = _run()
     assert [r[1] for r in preds] == [r[0] for r in preds] == [1, 1, 2, 1, 1, 2, 1, 2]
-    assert [r[2] for r in preds[:3]] == DETAILS
+    for r, ref in zip(preds[:3], DETAILS):   # the warm-start LR model is trained on the device: ~1e-12 apart
+        got, exp = json.loads(r[2]), json.loads(ref)
+        assert got.keys() == exp.keys() and all(abs(float(got[k]) - float(exp[k])) < 1e-9 for k in exp)
     # snapshot framing: bid, ntab, then the linear-model table rows
     bids = sorted({r[0] for r in snaps})
     assert bids[0] == 0 and all(r[1] == 4 for r in snaps)
