@@ -10,6 +10,7 @@ from ...common.params import Params
 from ...common.table import MTable
 from ...common.types import TableSchema, Types
 from ...models.feature import encoders as E
+from ...models.feature import pca as PCA_
 from ...models.feature import scalers as S
 from ...models.statistics import summary as ST
 from ..base import BatchOperator
@@ -264,3 +265,96 @@ class VectorChiSquareTestBatchOp(ChiSquareTestBatchOp):
 
 _export("SummarizerBatchOp", "VectorSummarizerBatchOp", "CorrelationBatchOp", "VectorCorrelationBatchOp",
         "ChiSquareTestBatchOp", "VectorChiSquareTestBatchOp")
+
+
+# ---------------------------------------------------------------------------------------------------
+# PCA and chi-square feature selection
+# ---------------------------------------------------------------------------------------------------
+class PcaTrainBatchOp(_FnTrainBatchOp):
+    def train(self, mt):
+        from ...common.model.converter import SimpleModelDataConverter
+        rows = PCA_.train_pca(mt, self.getParams(), self.env)
+        return MTable.from_rows(rows, SimpleModelDataConverter().getModelSchema(), replicated=True)
+
+
+_export("PcaTrainBatchOp")
+_model_map("PcaPredictBatchOp", PCA_.PcaModelMapper)
+
+
+def _chisq_select(results, p: Params):
+    """``ChiSquareTest.selector``: rows (index, p-value) -> selected indices."""
+    st = str(getattr(p.get("selectorType"), "name", p.get("selectorType"))).upper() \
+        if p.contains("selectorType") and p.get("selectorType") is not None else "NUMTOPFEATURES"
+    g = lambda k, d: p.get(k) if p.contains(k) and p.get(k) is not None else d  # noqa: E731
+    rows = [(i, r.p) for i, r in enumerate(results)]
+    n = len(rows)
+    asc = sorted(rows, key=lambda t: (t[1], t[0]))
+    if st == "NUMTOPFEATURES":
+        sel = [i for i, _ in asc[:int(g("numTopFeatures", 50))]]
+    elif st == "PERCENTILE":
+        size = max(1, int(n * float(g("percentile", 0.1))))
+        sel = [i for i, _ in asc[:size]]
+    elif st == "FPR":
+        sel = [i for i, pv in rows if pv < float(g("fpr", 0.05))]
+    elif st == "FDR":
+        fdr = float(g("fdr", 0.05))
+        mx = 0
+        for k, (_, pv) in enumerate(asc):
+            if pv <= fdr * (k + 1) / n:
+                mx = k
+        sel = sorted(i for i, _ in asc[:mx + 1])
+    elif st == "FWE":
+        sel = [i for i, pv in rows if pv <= float(g("fwe", 0.05)) / n]
+    else:
+        raise ValueError(f"Selector Type not support. {st}")
+    return sel
+
+
+class ChiSqSelectorBatchOp(BatchOperator):
+    """Chi-square feature selection over ``selectedCols`` (reference ``ChiSqSelectorBatchOp`` ->
+    ``ChiSquareTestUtil.selector``); output = model table with the selected column indices (JSON int[])."""
+
+    def linkFrom(self, *inputs):
+        from ...common.model.converter import SimpleModelDataConverter
+        inp = self.checkAndGetFirst(inputs)
+        p = self.getParams()
+        test = ChiSquareTestBatchOp(p.clone()).linkFrom(inp)
+        import json as _json
+        res = [ST.ChiSquareTestResult(_json.loads(r[1])["df"], _json.loads(r[1])["p"], _json.loads(r[1])["value"],
+                                      col=r[0]) for r in test.collect()]
+        sel = _chisq_select(res, p)
+        rows = SimpleModelDataConverter.rows_from(Params(), [_json.dumps(sel, separators=(",", ":"))])
+        self.setOutputTable(MTable.from_rows(rows, SimpleModelDataConverter().getModelSchema(), replicated=True))
+        return self
+
+    def collectResult(self):
+        """As the reference (``ChiSqSelectorBatchOp.collectResult``): the first ``len(selected)`` names of
+        ``selectedCols`` — the docs example output depends on it; ``selectedIndices()`` gives the indices."""
+        cols = list(self.getParams().get("selectedCols"))
+        return [cols[i] for i in range(len(self.selectedIndices()))]
+
+    def selectedIndices(self):
+        import json as _json
+        return _json.loads(self.collect()[1][1])
+
+
+class VectorChiSqSelectorBatchOp(ChiSqSelectorBatchOp):
+    def linkFrom(self, *inputs):
+        from ...common.model.converter import SimpleModelDataConverter
+        import json as _json
+        inp = self.checkAndGetFirst(inputs)
+        p = self.getParams()
+        test = VectorChiSquareTestBatchOp(p.clone()).linkFrom(inp)
+        res = [ST.ChiSquareTestResult(_json.loads(r[1])["df"], _json.loads(r[1])["p"], _json.loads(r[1])["value"],
+                                      col=r[0]) for r in test.collect()]
+        sel = _chisq_select(res, p)
+        rows = SimpleModelDataConverter.rows_from(Params(), [_json.dumps(sel, separators=(",", ":"))])
+        self.setOutputTable(MTable.from_rows(rows, SimpleModelDataConverter().getModelSchema(), replicated=True))
+        return self
+
+    def collectResult(self):
+        import json as _json
+        return _json.loads(self.collect()[1][1])
+
+
+_export("ChiSqSelectorBatchOp", "VectorChiSqSelectorBatchOp")

@@ -9,6 +9,7 @@ from __future__ import annotations
 from ...models.clustering.kmeans import KMeansModelMapper
 from ...models.linear.model import AFTModelMapper, LinearModelMapper, SoftmaxModelMapper
 from ...models.feature import encoders as _E
+from ...models.feature import pca as _PCA
 from ...models.feature import scalers as _S
 from ...models.classification.naive_bayes import NaiveBayesTextModelMapper
 from ...models.nlp import text as _T
@@ -50,6 +51,7 @@ _PREDICTORS = {
     "DocHashCountVectorizerPredictStreamOp": _T.DocHashCountVectorizerModelMapper,
     "Word2VecPredictStreamOp": _W.Word2VecModelMapper,
     "NaiveBayesTextPredictStreamOp": NaiveBayesTextModelMapper,
+    "PcaPredictStreamOp": _PCA.PcaModelMapper,
 }
 
 _MAPPERS = {

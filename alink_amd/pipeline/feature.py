@@ -33,3 +33,7 @@ _stage("Binarizer", MapTransformer, MAPPER=E.BinarizerMapper)
 _stage("Bucketizer", MapTransformer, MAPPER=E.BucketizerMapper)
 _stage("FeatureHasher", MapTransformer, MAPPER=E.FeatureHasherMapper)
 _stage("DCT", MapTransformer, MAPPER=E.DCTMapper)
+
+from ..models.feature import pca as _PCA  # noqa: E402
+_stage("PCAModel", MapModel, MAPPER=_PCA.PcaModelMapper)
+_stage("PCA", Trainer, TRAIN_OP=F.PcaTrainBatchOp, MODEL="PCAModel")
