@@ -11,7 +11,8 @@ from ...models.clustering.kmeans import KMeansModelDataConverter, KMeansModelMap
 from ..base import BatchOperator
 from .utils import ModelMapBatchOp
 
-__all__ = ["KMeansTrainBatchOp", "KMeansPredictBatchOp", "vector_tensor"]
+__all__ = ["KMeansTrainBatchOp", "KMeansPredictBatchOp", "vector_tensor", "GmmTrainBatchOp", "GmmPredictBatchOp",
+           "BisectingKMeansTrainBatchOp", "BisectingKMeansPredictBatchOp"]
 
 
 def vector_tensor(mt: MTable, col: str, device) -> torch.Tensor:
@@ -59,3 +60,39 @@ class KMeansTrainBatchOp(BatchOperator):
 
 class KMeansPredictBatchOp(ModelMapBatchOp):
     MAPPER = KMeansModelMapper
+
+
+class GmmTrainBatchOp(BatchOperator):
+    """EM for a Gaussian mixture (``models/clustering/gmm.py``)."""
+
+    def linkFrom(self, *inputs):
+        from ...common.model.converter import SimpleModelDataConverter
+        from ...models.clustering.gmm import train_gmm
+        mt = self.checkAndGetFirst(inputs).getOutputTable()
+        rows = train_gmm(mt, self.getParams(), self.env)
+        self.setOutputTable(MTable.from_rows(rows, SimpleModelDataConverter().getModelSchema(), replicated=True))
+        return self
+
+
+class BisectingKMeansTrainBatchOp(BatchOperator):
+    """Bisecting k-means (``models/clustering/bisecting.py``)."""
+
+    def linkFrom(self, *inputs):
+        from ...common.model.converter import SimpleModelDataConverter
+        from ...models.clustering.bisecting import train_bisecting_kmeans
+        mt = self.checkAndGetFirst(inputs).getOutputTable()
+        rows = train_bisecting_kmeans(mt, self.getParams(), self.env)
+        self.setOutputTable(MTable.from_rows(rows, SimpleModelDataConverter().getModelSchema(), replicated=True))
+        return self
+
+
+from ...models.clustering.bisecting import BisectingKMeansModelMapper  # noqa: E402
+from ...models.clustering.gmm import GmmModelMapper  # noqa: E402
+
+
+class GmmPredictBatchOp(ModelMapBatchOp):
+    MAPPER = GmmModelMapper
+
+
+class BisectingKMeansPredictBatchOp(ModelMapBatchOp):
+    MAPPER = BisectingKMeansModelMapper

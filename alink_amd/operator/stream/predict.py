@@ -6,6 +6,8 @@ DirectReader, ``ModelMapStreamOp.java:39-56``).
 """
 from __future__ import annotations
 
+from ...models.clustering import bisecting as _BKM
+from ...models.clustering import gmm as _GMM
 from ...models.clustering.kmeans import KMeansModelMapper
 from ...models.linear.model import AFTModelMapper, LinearModelMapper, SoftmaxModelMapper
 from ...models.feature import encoders as _E
@@ -52,6 +54,8 @@ _PREDICTORS = {
     "Word2VecPredictStreamOp": _W.Word2VecModelMapper,
     "NaiveBayesTextPredictStreamOp": NaiveBayesTextModelMapper,
     "PcaPredictStreamOp": _PCA.PcaModelMapper,
+    "GmmPredictStreamOp": _GMM.GmmModelMapper,
+    "BisectingKMeansPredictStreamOp": _BKM.BisectingKMeansModelMapper,
 }
 
 _MAPPERS = {

@@ -3,7 +3,8 @@ from ..models.clustering.kmeans import KMeansModelMapper
 from ..operator.batch.clustering import KMeansTrainBatchOp
 from .base import MapModel, Trainer
 
-__all__ = ["KMeans", "KMeansModel"]
+__all__ = ["KMeans", "KMeansModel", "GaussianMixture", "GaussianMixtureModel", "BisectingKMeans",
+           "BisectingKMeansModel"]
 
 
 class KMeans(Trainer):
@@ -13,3 +14,26 @@ class KMeans(Trainer):
 
 class KMeansModel(MapModel):
     MAPPER = KMeansModelMapper
+
+
+from ..models.clustering.bisecting import BisectingKMeansModelMapper  # noqa: E402
+from ..models.clustering.gmm import GmmModelMapper  # noqa: E402
+from ..operator.batch.clustering import BisectingKMeansTrainBatchOp, GmmTrainBatchOp  # noqa: E402
+
+
+class GaussianMixture(Trainer):
+    TRAIN_OP = GmmTrainBatchOp
+    MODEL = "GaussianMixtureModel"
+
+
+class GaussianMixtureModel(MapModel):
+    MAPPER = GmmModelMapper
+
+
+class BisectingKMeans(Trainer):
+    TRAIN_OP = BisectingKMeansTrainBatchOp
+    MODEL = "BisectingKMeansModel"
+
+
+class BisectingKMeansModel(MapModel):
+    MAPPER = BisectingKMeansModelMapper

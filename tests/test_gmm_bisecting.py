@@ -1,0 +1,74 @@
+"""GMM and bisecting k-means vs the reference docs (docs/en/gmm*.md, bisectingkmeans*.md)."""
+import json
+
+import numpy as np
+import pandas as pd
+
+from alink_amd import *  # noqa: F401,F403
+from alink_amd.models.clustering.gmm import pack_cov, unpack_cov
+
+GMM_DATA = ["-0.6264538 0.1836433", "-0.8356286 1.5952808", "0.3295078 -0.8204684", "0.4874291 0.7383247",
+            "0.5757814 -0.3053884", "1.5117812 0.3898432", "-0.6212406 -2.2146999", "11.1249309 9.9550664",
+            "9.9838097 10.9438362", "10.8212212 10.5939013", "10.9189774 10.7821363", "10.0745650 8.0106483",
+            "10.6198257 9.9438713", "9.8442045 8.5292476", "9.5218499 10.4179416"]
+
+
+def test_gmm_doc_example():
+    src = BatchOperator.fromDataframe(pd.DataFrame({"features": GMM_DATA}), schemaStr="features string")
+    model = GmmTrainBatchOp().setVectorCol("features").setTol(0.).linkFrom(src)
+    rows = model.collect()
+    meta = json.loads(rows[0][1])
+    assert meta["numFeatures"] == "2" and meta["k"] == "2"
+    c0 = json.loads(rows[1][1])
+    assert set(c0) == {"clusterId", "weight", "mean", "cov"} and len(c0["cov"]["data"]) == 3
+    out = GmmPredictBatchOp().setVectorCol("features").setPredictionCol("cluster_id") \
+        .setPredictionDetailCol("cluster_detail").linkFrom(model, src).collect()
+    # EM reaches the same local optimum as the reference's documented model (component order differs)
+    weights = sorted(json.loads(r[1])["weight"] for r in rows[1:])
+    np.testing.assert_allclose(weights, [0.26455102514508383, 0.7354489748549162], atol=1e-9)
+    for r in out:
+        p = [float(x) for x in r[2].split(" ")]
+        assert abs(sum(p) - 1) < 1e-9
+    m = GaussianMixture().setVectorCol("features").setPredictionCol("c").fit(src)
+    assert len(m.transform(src).collect()) == 15
+
+
+def test_gmm_cov_packing():
+    S = np.array([[1.0, 2.0, 3.0], [2.0, 5.0, 6.0], [3.0, 6.0, 9.0]])
+    v = pack_cov(S)
+    assert v.tolist() == [1.0, 2.0, 5.0, 3.0, 6.0, 9.0]
+    np.testing.assert_array_equal(unpack_cov(v, 3), S)
+
+
+def test_bisecting_kmeans_doc_example():
+    df = pd.DataFrame({"id": [0, 1, 2, 3, 4, 5],
+                       "vec": ["0 0 0", "0.1,0.1,0.1", "0.2,0.2,0.2", "9 9 9", "9.1 9.1 9.1", "9.2 9.2 9.2"]})
+    src = BatchOperator.fromDataframe(df, schemaStr="id int, vec string")
+    model = BisectingKMeansTrainBatchOp().setVectorCol("vec").setK(2).linkFrom(src)
+    rows = model.collect()
+    nodes = [json.loads(r[1]) for r in rows[1:]]
+    assert [(n["clusterId"], n["size"]) for n in nodes] == [(1, 6), (2, 3), (3, 3)]
+    np.testing.assert_allclose(nodes[0]["center"]["data"], [4.6] * 3)
+    np.testing.assert_allclose(nodes[1]["center"]["data"], [0.1] * 3)
+    np.testing.assert_allclose(nodes[2]["center"]["data"], [9.1] * 3)
+    pred = BisectingKMeansPredictBatchOp().setPredictionCol("pred").linkFrom(model, src).collect()
+    assert [r[2] for r in pred] == [0, 0, 0, 1, 1, 1]
+    box = []
+    BisectingKMeansPredictStreamOp(model).setPredictionCol("pred").linkFrom(
+        StreamOperator.fromDataframe(df, schemaStr="id int, vec string")).link(CollectStreamOp(box))
+    StreamOperator.execute()
+    assert sorted((r[0], r[2]) for r in box) == [(0, 0), (1, 0), (2, 0), (3, 1), (4, 1), (5, 1)]
+
+
+def test_bisecting_kmeans_k4():
+    rng = np.random.default_rng(0)
+    centers = np.array([[0, 0], [10, 0], [0, 10], [10, 10]], dtype=float)
+    X = np.concatenate([c + rng.normal(scale=0.5, size=(30, 2)) for c in centers])
+    df = pd.DataFrame({"v": [f"{a} {b}" for a, b in X]})
+    src = BatchOperator.fromDataframe(df, schemaStr="v string")
+    m = BisectingKMeans().setVectorCol("v").setK(4).setPredictionCol("p").setPredictionDetailCol("d").fit(src)
+    out = m.transform(src).collect()
+    labels = np.array([r[1] for r in out]).reshape(4, 30)
+    assert all(len(set(row)) == 1 for row in labels) and len({row[0] for row in labels}) == 4
+    p = [float(x) for x in out[0][2].split(" ")]
+    assert abs(sum(p) - 1.0) < 1e-12
