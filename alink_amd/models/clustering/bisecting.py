@@ -11,8 +11,8 @@ tree; leaves are numbered in BFS order and the detail vector turns tree distance
 (``KMeansUtil.getProbArrayFromDistanceArray``).
 
 MI355X design: the samples stay on the device with an int64 tree-node id per row; an inner iteration is one
-fused projection (``X @ V`` for all dividing clusters at once), a ``where`` and two ``index_add_`` segment
-sums, then one all-reduce of ``[#children, d + 2]`` statistics.
+fused projection (``X @ V`` for all dividing clusters at once), a ``where`` and one one-hot GEMM for the
+per-child segment sums, then one all-reduce of ``[#children, d + 2]`` statistics.
 """
 from __future__ import annotations
 
@@ -68,9 +68,9 @@ def _summaries(X, node, ids: List[int], cosine: bool):
         Xs, ps = X[ok], p[ok]
         norm2 = (Xs * Xs).sum(1)
         vec = Xs / torch.sqrt(norm2)[:, None] if cosine else Xs
-        stats[:, :d].index_add_(0, ps, vec)
-        stats[:, d].index_add_(0, ps, torch.ones_like(norm2))
-        stats[:, d + 1].index_add_(0, ps, norm2)
+        # segment sums as one [m, n] x [n, d + 2] GEMM (few segments: atomics would serialise)
+        onehot = torch.nn.functional.one_hot(ps, m).to(X.dtype)
+        stats += onehot.T @ torch.cat([vec, torch.ones_like(norm2)[:, None], norm2[:, None]], 1)
     comm.all_reduce(stats, "sum")
     out = {}
     S = stats.cpu().numpy()

@@ -12,7 +12,7 @@ from ..base import BatchOperator
 from .utils import ModelMapBatchOp
 
 __all__ = ["KMeansTrainBatchOp", "KMeansPredictBatchOp", "vector_tensor", "GmmTrainBatchOp", "GmmPredictBatchOp",
-           "BisectingKMeansTrainBatchOp", "BisectingKMeansPredictBatchOp"]
+           "BisectingKMeansTrainBatchOp", "BisectingKMeansPredictBatchOp", "LdaTrainBatchOp", "LdaPredictBatchOp"]
 
 
 def vector_tensor(mt: MTable, col: str, device) -> torch.Tensor:
@@ -96,3 +96,22 @@ class GmmPredictBatchOp(ModelMapBatchOp):
 
 class BisectingKMeansPredictBatchOp(ModelMapBatchOp):
     MAPPER = BisectingKMeansModelMapper
+
+
+class LdaTrainBatchOp(BatchOperator):
+    """LDA, collapsed Gibbs ("em") or online variational Bayes (``models/clustering/lda.py``)."""
+
+    def linkFrom(self, *inputs):
+        from ...common.model.converter import SimpleModelDataConverter
+        from ...models.clustering.lda import train_lda
+        mt = self.checkAndGetFirst(inputs).getOutputTable()
+        rows = train_lda(mt, self.getParams(), self.env)
+        self.setOutputTable(MTable.from_rows(rows, SimpleModelDataConverter().getModelSchema(), replicated=True))
+        return self
+
+
+from ...models.clustering.lda import LdaModelMapper  # noqa: E402
+
+
+class LdaPredictBatchOp(ModelMapBatchOp):
+    MAPPER = LdaModelMapper

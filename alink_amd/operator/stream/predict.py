@@ -8,6 +8,7 @@ from __future__ import annotations
 
 from ...models.clustering import bisecting as _BKM
 from ...models.clustering import gmm as _GMM
+from ...models.clustering import lda as _LDA
 from ...models.clustering.kmeans import KMeansModelMapper
 from ...models.linear.model import AFTModelMapper, LinearModelMapper, SoftmaxModelMapper
 from ...models.feature import encoders as _E
@@ -56,6 +57,7 @@ _PREDICTORS = {
     "PcaPredictStreamOp": _PCA.PcaModelMapper,
     "GmmPredictStreamOp": _GMM.GmmModelMapper,
     "BisectingKMeansPredictStreamOp": _BKM.BisectingKMeansModelMapper,
+    "LdaPredictStreamOp": _LDA.LdaModelMapper,
 }
 
 _MAPPERS = {

@@ -4,7 +4,7 @@ from ..operator.batch.clustering import KMeansTrainBatchOp
 from .base import MapModel, Trainer
 
 __all__ = ["KMeans", "KMeansModel", "GaussianMixture", "GaussianMixtureModel", "BisectingKMeans",
-           "BisectingKMeansModel"]
+           "BisectingKMeansModel", "Lda", "LdaModel"]
 
 
 class KMeans(Trainer):
@@ -37,3 +37,16 @@ class BisectingKMeans(Trainer):
 
 class BisectingKMeansModel(MapModel):
     MAPPER = BisectingKMeansModelMapper
+
+
+from ..models.clustering.lda import LdaModelMapper  # noqa: E402
+from ..operator.batch.clustering import LdaTrainBatchOp  # noqa: E402
+
+
+class Lda(Trainer):
+    TRAIN_OP = LdaTrainBatchOp
+    MODEL = "LdaModel"
+
+
+class LdaModel(MapModel):
+    MAPPER = LdaModelMapper
