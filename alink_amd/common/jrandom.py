@@ -17,6 +17,7 @@ def _to_int32(x: int) -> int:
 class JavaRandom:
     def __init__(self, seed: int):
         self._seed = (int(seed) ^ _MULT) & _MASK
+        self._next_gaussian = None
 
     def _next(self, bits: int) -> int:
         self._seed = (self._seed * _MULT + _ADD) & _MASK
@@ -42,6 +43,25 @@ class JavaRandom:
 
     def nextDouble(self) -> float:
         return ((self._next(26) << 27) + self._next(27)) * (1.0 / (1 << 53))
+
+    def nextFloat(self) -> float:
+        return self._next(24) / float(1 << 24)
+
+    def nextGaussian(self) -> float:
+        """Marsaglia polar method with the cached second value, as ``Random.nextGaussian``."""
+        import math
+        if self._next_gaussian is not None:
+            v, self._next_gaussian = self._next_gaussian, None
+            return v
+        while True:
+            v1 = 2 * self.nextDouble() - 1
+            v2 = 2 * self.nextDouble() - 1
+            s = v1 * v1 + v2 * v2
+            if 0 < s < 1:
+                break
+        mul = math.sqrt(-2 * math.log(s) / s)
+        self._next_gaussian = v2 * mul
+        return v1 * mul
 
     def nextBoolean(self) -> bool:
         return self._next(1) != 0

@@ -118,7 +118,9 @@ def _two_loop(ctx, grad_vec, start_dir, k):
     """L-BFGS two-loop recursion over the stored corrections (``Lbfgs.CalDirection`` :109-175).
 
     Kept entirely on the device: a correction pair with ``s.y == 0`` is skipped in the reference; here its
-    ``rho`` is 0, which makes the same update a no-op without a host round trip."""
+    ``rho`` is 0, which makes the same update a no-op without a host round trip.  Pairs with ``s.y < 0``
+    (impossible for the convex linear losses, common for the MLP objective) are skipped the same way so
+    the direction stays a descent direction."""
     sK, yK = ctx.getObj(SKYK)
     m = NUM_CORRECTIONS
     dirv = start_dir.clone()
@@ -129,7 +131,7 @@ def _two_loop(ctx, grad_vec, start_dir, k):
     order = [(i + delta) % m for i in range(l)]
     S, Y = sK[order], yK[order]                      # [l, d]
     dots = (S * Y).sum(1)
-    rho = torch.where(dots.abs() > 0, 1.0 / torch.where(dots == 0, torch.ones_like(dots), dots),
+    rho = torch.where(dots > 0, 1.0 / torch.where(dots <= 0, torch.ones_like(dots), dots),
                       torch.zeros_like(dots))
     alpha = torch.zeros(l, dtype=dirv.dtype, device=dirv.device)
     for i in range(l - 1, -1, -1):

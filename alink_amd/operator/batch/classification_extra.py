@@ -7,7 +7,8 @@ from ...models.classification.naive_bayes import (NaiveBayesTextModelDataConvert
 from ..base import BatchOperator
 from .utils import ModelMapBatchOp
 
-__all__ = ["NaiveBayesTextTrainBatchOp", "NaiveBayesTextPredictBatchOp"]
+__all__ = ["NaiveBayesTextTrainBatchOp", "NaiveBayesTextPredictBatchOp", "MultilayerPerceptronTrainBatchOp",
+           "MultilayerPerceptronPredictBatchOp"]
 
 
 class NaiveBayesTextTrainBatchOp(BatchOperator):
@@ -22,3 +23,20 @@ class NaiveBayesTextTrainBatchOp(BatchOperator):
 
 class NaiveBayesTextPredictBatchOp(ModelMapBatchOp):
     MAPPER = NaiveBayesTextModelMapper
+
+
+class MultilayerPerceptronTrainBatchOp(BatchOperator):
+    def linkFrom(self, *inputs):
+        from ...models.classification.mlp import MlpcModelDataConverter, train_mlp
+        mt = self.checkAndGetFirst(inputs).getOutputTable()
+        meta, w, labels, lt = train_mlp(mt, self.getParams(), self.env)
+        conv = MlpcModelDataConverter(lt)
+        self.setOutputTable(MTable.from_rows(conv.save((meta, w, labels)), conv.getModelSchema(), replicated=True))
+        return self
+
+
+from ...models.classification.mlp import MlpcModelMapper  # noqa: E402
+
+
+class MultilayerPerceptronPredictBatchOp(ModelMapBatchOp):
+    MAPPER = MlpcModelMapper

@@ -14,6 +14,7 @@ from ...models.linear.model import AFTModelMapper, LinearModelMapper, SoftmaxMod
 from ...models.feature import encoders as _E
 from ...models.feature import pca as _PCA
 from ...models.feature import scalers as _S
+from ...models.classification import mlp as _MLP
 from ...models.classification.naive_bayes import NaiveBayesTextModelMapper
 from ...models.nlp import text as _T
 from ...models.nlp import word2vec as _W
@@ -58,6 +59,7 @@ _PREDICTORS = {
     "GmmPredictStreamOp": _GMM.GmmModelMapper,
     "BisectingKMeansPredictStreamOp": _BKM.BisectingKMeansModelMapper,
     "LdaPredictStreamOp": _LDA.LdaModelMapper,
+    "MultilayerPerceptronPredictStreamOp": _MLP.MlpcModelMapper,
 }
 
 _MAPPERS = {

@@ -3,7 +3,8 @@ from ..models.classification.naive_bayes import NaiveBayesTextModelMapper
 from ..operator.batch import classification_extra as C
 from .base import MapModel, Trainer
 
-__all__ = ["NaiveBayesTextClassifier", "NaiveBayesTextModel"]
+__all__ = ["NaiveBayesTextClassifier", "NaiveBayesTextModel", "MultilayerPerceptronClassifier",
+           "MultilayerPerceptronClassificationModel"]
 
 
 class NaiveBayesTextClassifier(Trainer):
@@ -13,3 +14,15 @@ class NaiveBayesTextClassifier(Trainer):
 
 class NaiveBayesTextModel(MapModel):
     MAPPER = NaiveBayesTextModelMapper
+
+
+from ..models.classification.mlp import MlpcModelMapper  # noqa: E402
+
+
+class MultilayerPerceptronClassifier(Trainer):
+    TRAIN_OP = C.MultilayerPerceptronTrainBatchOp
+    MODEL = "MultilayerPerceptronClassificationModel"
+
+
+class MultilayerPerceptronClassificationModel(MapModel):
+    MAPPER = MlpcModelMapper
