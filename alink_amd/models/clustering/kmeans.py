@@ -321,13 +321,20 @@ class KMeansUpdateCentroids(ComputeFunction):
         buf = ctx.getObj(CENTROID_ALL_REDUCE)
         d = buf.shape[1] - 1
         cnt = buf[:, d]
-        keep = cnt > 0
-        C = buf[keep, :d] / cnt[keep, None]
+        # one small D2H read decides the (rare) empty-cluster compaction on the host; the common
+        # all-non-empty step stays a single device division (no mask indexing / nonzero syncs)
+        empty = (cnt <= 0).nonzero().reshape(-1).tolist() if bool((cnt <= 0).any().item()) else []
+        if empty:
+            keep = torch.as_tensor([i for i in range(buf.shape[0]) if i not in set(empty)], dtype=torch.long,
+                                   device=buf.device)
+            buf = buf.index_select(0, keep)
+            cnt = buf[:, d]
+        C = buf[:, :d] / cnt[:, None]
         if self.dist_type == "COSINE":
             C = _normalize_rows(C)
         tgt[0] = ctx.getStepNo()
         tgt[1] = C
-        ctx.putObj("lastWeights", cnt[keep])
+        ctx.putObj("lastWeights", cnt)
         ctx.putObj(K, int(C.shape[0]))
 
 

@@ -17,7 +17,7 @@ import torch  # noqa: F401  (loads torch's HIP runtime first; our .so resolves l
 
 __all__ = ["lib", "require", "available", "LIB_PATH", "stream_ptr"]
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libalink_hip.so")
+LIB_PATH = os.environ.get("ALINK_HIP_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libalink_hip.so")
 _lib: Optional[ctypes.CDLL] = None
 _err: Optional[str] = None
 
@@ -49,6 +49,8 @@ def _load():
     L.alink_kmeans_assign_accum_bf16_v6.restype = c_int
     L.alink_kmeans_reduce_slabs.argtypes = [c_vp, c_vp, c_int, c_int, c_vp, c_vp]
     L.alink_kmeans_reduce_slabs.restype = c_int
+    L.alink_kmeans_prep_centroids.argtypes = [c_vp, c_int, c_vp, c_vp, c_vp]
+    L.alink_kmeans_prep_centroids.restype = c_int
     for name, argtypes in _EXTRA_SIGNATURES.items():
         if hasattr(L, name):
             getattr(L, name).argtypes = argtypes

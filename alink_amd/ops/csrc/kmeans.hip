@@ -1229,6 +1229,7 @@ __global__ __launch_bounds__(256, 1) void kmeans_assign_accum_v5_kernel(
 // Same 64-row tiles / 8-deep ring / 4-stage skew as v5; mask words of tile t are cleared one iteration
 // after they are consumed (both halves read them).
 // ---------------------------------------------------------------------------------------------------
+template <int P0 = 0, int P1 = 2>
 __device__ __forceinline__ void v6_stage(char* lds, int buf, const char* X, int64_t row0, int64_t N,
                                          const uint32_t (&voff)[2], int wave) {
     const int64_t rem = (N - row0) * ROWB;
@@ -1236,7 +1237,7 @@ __device__ __forceinline__ void v6_stage(char* lds, int buf, const char* X, int6
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc((void*)(X + row0 * ROWB), (short)0, nbytes, 0x00020000);
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = P0; i < P1; ++i) {
         const uint32_t m0v = __builtin_amdgcn_readfirstlane(
             (uint32_t)(uintptr_t)LDS_PTR(lds + buf * V5_TILE + i * 8192 + wave * 1024));
         uint32_t keep;
@@ -1252,6 +1253,9 @@ __device__ __forceinline__ void v6_stage(char* lds, int buf, const char* X, int6
     }
 }
 
+#ifndef ALINK_V6_LATE_STAGE
+#define ALINK_V6_LATE_STAGE 1
+#endif
 template <int KB, bool LOAD_ONLY = false, bool COMPUTE_ONLY = false>
 __global__ __launch_bounds__(512, 1) void kmeans_assign_accum_v6_kernel(
     const __bf16* __restrict__ Xp, int64_t N, const __bf16* __restrict__ Cp, const float* __restrict__ ninit,
@@ -1301,24 +1305,22 @@ __global__ __launch_bounds__(512, 1) void kmeans_assign_accum_v6_kernel(
         for (int e = tid; e < 2 * 4 * 64; e += 512) pb[e] = -3.0e38f;
     }
     bf16x8 cf[8];
-    bf16x8 cn;
-    const __bf16 one = (__bf16)1.0f, zb = (__bf16)0.0f;
+    // -|c|^2/2 of the 16 centroids this lane's accumulator registers hold (row r of the 32x32 C block is
+    // centroid 32cb + (r&3) + 8(r>>2) + 4h for every sample column): the distance GEMM starts from it as its
+    // fp32 C operand, so the norm costs no MFMA k-step and no bf16 splitting
+    f32x16 nv;
+    const __bf16 zb = (__bf16)0.0f;
     {
 #pragma unroll
         for (int s = 0; s < 8; ++s)
             cf[s] = active ? *reinterpret_cast<const bf16x8*>(Cp + (32 * cb + l32) * D + 16 * s + 8 * h)
                            : bf16x8{zb, zb, zb, zb, zb, zb, zb, zb};
-        const float v = active ? ninit[32 * cb + l32] : -3.0e38f;
-        const __bf16 p0 = (__bf16)v;
-        const float r1 = v - (float)p0;
-        const __bf16 p1 = (__bf16)r1;
-        const __bf16 p2 = (__bf16)(r1 - (float)p1);
-        cn = (h == 0) ? bf16x8{p0, p1, p2, zb, zb, zb, zb, zb} : bf16x8{zb, zb, zb, zb, zb, zb, zb, zb};
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+            nv[r] = active ? ninit[32 * cb + (r & 3) + 8 * (r >> 2) + 4 * h] : -3.0e38f;
 #pragma unroll
         for (int s = 0; s < 8; ++s) asm volatile("" ::"v"(cf[s]));
-        asm volatile("" ::"v"(cn));
     }
-    const bf16x8 ones = (h == 0) ? bf16x8{one, one, one, zb, zb, zb, zb, zb} : bf16x8{zb, zb, zb, zb, zb, zb, zb, zb};
     int xr[8];
 #pragma unroll
     for (int s = 0; s < 8; ++s) xr[s] = xoff(32 * half + l32, 2 * s + h);
@@ -1361,9 +1363,15 @@ __global__ __launch_bounds__(512, 1) void kmeans_assign_accum_v6_kernel(
         }
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        if (i + V5_AHEAD < nt && !COMPUTE_ONLY)
-            v6_stage(lds, (int)((ui + V5_AHEAD) % V5_NBUF), X,
-                     (tbase + (int64_t)(i + V5_AHEAD) * tstride) * V5_TR, N, voff, wave);
+        // ring slot (i+4)%8 held tile i-4, last read by the accumulate of iteration i-1: free anywhere after
+        // the barrier.  The LDS-DMA pieces are cheapest to issue outside the MFMA/ds_read phases, so by
+        // default they go out in the combine section after the distance GEMM (ALINK_V6_LATE_STAGE).
+        const bool stage_now = i + V5_AHEAD < nt && !COMPUTE_ONLY;
+        if (!ALINK_V6_LATE_STAGE || LOAD_ONLY) {
+            if (stage_now)
+                v6_stage(lds, (int)((ui + V5_AHEAD) % V5_NBUF), X,
+                         (tbase + (int64_t)(i + V5_AHEAD) * tstride) * V5_TR, N, voff, wave);
+        }
         if constexpr (LOAD_ONLY) return;
         // masks of tile i-3 (set i%3); the set consumed last iteration ((i+2)%3) is cleared by half 0
         uint32_t* mp = masks + (int)(ui % 3u) * 256 + (32 * cb + l32) * 2;
@@ -1380,12 +1388,10 @@ __global__ __launch_bounds__(512, 1) void kmeans_assign_accum_v6_kernel(
         float best = -3.0e38f;
         {
             const int cur = (int)(ui % V5_NBUF) * V5_TILE;
-            const f32x16 z = {};
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cn, ones, z, 0, 0, 0);
 #pragma unroll
             for (int s = 0; s < 8; ++s) {
                 const bf16x8 xv = *reinterpret_cast<const bf16x8*>(lds + cur + xr[s]);
-                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cf[s], xv, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cf[s], xv, s == 0 ? nv : acc, 0, 0, 0);
 #pragma unroll
                 for (int t2 = 0; t2 < 2; ++t2) {
                     const int r = 2 * s + t2;
@@ -1396,6 +1402,11 @@ __global__ __launch_bounds__(512, 1) void kmeans_assign_accum_v6_kernel(
         }
         best = fmaxf(best, __shfl_xor(best, 32));
         if (h == 0) pbest[(int)((ui + 1) & 1u) * 256 + cb * 64 + 32 * half + l32] = best;
+        if (ALINK_V6_LATE_STAGE == 1 || ALINK_V6_LATE_STAGE == 3) {
+            if (stage_now)
+                v6_stage<0, (ALINK_V6_LATE_STAGE == 1 ? 2 : 1)>(lds, (int)((ui + V5_AHEAD) % V5_NBUF), X,
+                         (tbase + (int64_t)(i + V5_AHEAD) * tstride) * V5_TR, N, voff, wave);
+        }
         // ---- combine tile i-2 (rows 8w..8w+7) ----
         {
             const int t = i - 2;
@@ -1426,6 +1437,11 @@ __global__ __launch_bounds__(512, 1) void kmeans_assign_accum_v6_kernel(
                 }
             }
         }
+        if (ALINK_V6_LATE_STAGE == 2 || ALINK_V6_LATE_STAGE == 3) {
+            if (stage_now)
+                v6_stage<(ALINK_V6_LATE_STAGE == 2 ? 0 : 1), 2>(lds, (int)((ui + V5_AHEAD) % V5_NBUF), X,
+                         (tbase + (int64_t)(i + V5_AHEAD) * tstride) * V5_TR, N, voff, wave);
+        }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     };
     for (int i = 0; i < total; i += 2) {
@@ -1444,20 +1460,50 @@ __global__ __launch_bounds__(512, 1) void kmeans_assign_accum_v6_kernel(
     if (h == 0 && half == 0) slab_cnt[(int64_t)blockIdx.x * 128 + 32 * cb + l32] = cnt;
 }
 
-// fixed-order fp64 reduction of the per-workgroup slabs -> out[k][D+1] (last column = count)
-__global__ void kmeans_reduce_slabs_kernel(const float* __restrict__ slab, const float* __restrict__ slab_cnt,
-                                           int nslab, int k, double* __restrict__ out) {
-    const int e = blockIdx.x * blockDim.x + threadIdx.x;
-    const int total = k * (D + 1);
-    if (e >= total) return;
-    const int c = e / (D + 1), d = e % (D + 1);
+// fixed-order fp64 reduction of the per-workgroup slabs -> out[k][D+1] (last column = count).
+// Block (c, y): y < 4 -> dims 32y..32y+31, y == 4 -> the count; 8 lane groups stride the slabs (coalesced
+// 128-B rows), then group partials are added in group order, so the result is run-to-run deterministic.
+__global__ __launch_bounds__(256) void kmeans_reduce_slabs_kernel(const float* __restrict__ slab,
+                                                                  const float* __restrict__ slab_cnt, int nslab,
+                                                                  int k, double* __restrict__ out) {
+    __shared__ double part[8][32];
+    const int c = blockIdx.x, y = blockIdx.y;
+    const int d = threadIdx.x & 31, g = threadIdx.x >> 5;
     double s = 0.0;
-    if (d < D) {
-        for (int w = 0; w < nslab; ++w) s += (double)slab[((int64_t)w * 128 + c) * D + d];
-    } else {
-        for (int w = 0; w < nslab; ++w) s += (double)slab_cnt[(int64_t)w * 128 + c];
+    if (y < 4) {
+        const float* p = slab + (int64_t)c * D + 32 * y + d;
+        for (int w = g; w < nslab; w += 8) s += (double)p[(int64_t)w * 128 * D];
+    } else if (d == 0) {
+        for (int w = g; w < nslab; w += 8) s += (double)slab_cnt[(int64_t)w * 128 + c];
     }
-    out[e] = s;
+    part[g][d] = s;
+    __syncthreads();
+    if (g == 0) {
+        double t = 0.0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) t += part[j][d];
+        if (y < 4) out[(int64_t)c * (D + 1) + 32 * y + d] = t;
+        else if (d == 0) out[(int64_t)c * (D + 1) + D] = t;
+    }
+}
+
+// next-step centroid operands from fp64 centroids C [k][D]: bf16 block [128][D] (zero rows past k) and the
+// accumulator init -|bf16(c)|^2/2 (-3e38 past k), one launch instead of a chain of small torch ops.
+__global__ __launch_bounds__(128) void kmeans_prep_centroids_kernel(const double* __restrict__ C, int k,
+                                                                    __bf16* __restrict__ cpad,
+                                                                    float* __restrict__ ninit) {
+    __shared__ float red[128];
+    const int c = blockIdx.x, d = threadIdx.x;
+    const __bf16 b = c < k ? (__bf16)(float)C[(int64_t)c * D + d] : (__bf16)0.0f;
+    cpad[c * D + d] = b;
+    const float f = (float)b;
+    red[d] = f * f;
+    __syncthreads();
+    for (int off = 64; off > 0; off >>= 1) {
+        if (d < off) red[d] += red[d + off];
+        __syncthreads();
+    }
+    if (d == 0) ninit[c] = c < k ? -0.5f * red[0] : -3.0e38f;
 }
 
 }  // namespace
@@ -1602,9 +1648,16 @@ int alink_kmeans_assign_accum_bf16_v6(const void* X, int64_t N, const void* C, c
 
 int alink_kmeans_reduce_slabs(const float* slab, const float* slab_cnt, int nslab, int k, double* out,
                               void* stream) {
-    const int total = k * (D + 1);
-    hipLaunchKernelGGL(kmeans_reduce_slabs_kernel, dim3((total + 255) / 256), dim3(256), 0,
-                       reinterpret_cast<hipStream_t>(stream), slab, slab_cnt, nslab, k, out);
+    if (k < 1 || k > 128 || nslab < 1) return -1;
+    hipLaunchKernelGGL(kmeans_reduce_slabs_kernel, dim3(k, 5), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                       slab, slab_cnt, nslab, k, out);
+    return (int)hipGetLastError();
+}
+
+int alink_kmeans_prep_centroids(const double* C, int k, void* cpad, float* ninit, void* stream) {
+    if (k < 0 || k > 128) return -1;
+    hipLaunchKernelGGL(kmeans_prep_centroids_kernel, dim3(128), dim3(128), 0, reinterpret_cast<hipStream_t>(stream),
+                       C, k, (__bf16*)cpad, ninit);
     return (int)hipGetLastError();
 }
 

@@ -31,9 +31,25 @@ def hip_supported(X: torch.Tensor, k: int) -> bool:
             and 1 <= k <= HIP_KMAX and X.shape[0] > 0 and X.is_contiguous() and X.data_ptr() % 16 == 0)
 
 
+_PREP = {}
+
+
 def prepare_centroids(C: torch.Tensor, device) -> Tuple[torch.Tensor, torch.Tensor]:
-    """Padded bf16 centroid block [128,128] and accumulator init -|c|^2/2 (of the bf16-rounded centroids)."""
+    """Padded bf16 centroid block [128,128] and accumulator init -|c|^2/2 (of the bf16-rounded centroids).
+    fp64 centroids on the GPU go through one HIP launch into per-device buffers (stream-ordered reuse)."""
     k = C.shape[0]
+    if C.is_cuda and C.dtype == torch.float64 and C.shape[1] == HIP_D and k <= HIP_KMAX:
+        L = _lib.require()
+        key = C.device.index
+        if key not in _PREP:
+            _PREP[key] = (torch.empty((HIP_KMAX, HIP_D), dtype=torch.bfloat16, device=C.device),
+                          torch.empty((HIP_KMAX,), dtype=torch.float32, device=C.device))
+        cpad, ninit = _PREP[key]
+        Cc = C.contiguous()
+        rc = L.alink_kmeans_prep_centroids(Cc.data_ptr(), k, cpad.data_ptr(), ninit.data_ptr(), _lib.stream_ptr(C.device))
+        if rc != 0:
+            raise RuntimeError(f"alink_kmeans_prep_centroids failed: {rc}")
+        return cpad, ninit
     cb = C.to(device=device, dtype=torch.bfloat16)
     cpad = torch.zeros((HIP_KMAX, HIP_D), dtype=torch.bfloat16, device=device)
     cpad[:k] = cb
