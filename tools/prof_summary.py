@@ -28,6 +28,13 @@ def main(root, out):
             lines.append(k)
             for c, v in sorted(d.items()):
                 lines.append(f"   {c:32s} {v:.4g}")
+    for f in sorted(glob.glob(os.path.join(root, "**", "*.db"), recursive=True)):
+        import sqlite3
+        c = sqlite3.connect(f)
+        lines.append(f"== kernel stats (rocpd db) {os.path.relpath(f, root)}")
+        for name, calls, tot, avg, pct in c.execute(
+                "select name, total_calls, total_duration, average, percentage from top_kernels limit 25"):
+            lines.append(f"{name[:90]:90s} calls={calls} total_ms={tot/1e3:.3f} avg_us={avg:.1f} pct={pct:.1f}")
     txt = "\n".join(lines)
     open(out, "w").write(txt + "\n")
     print(txt)
