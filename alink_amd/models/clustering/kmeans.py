@@ -40,7 +40,7 @@ from ...params import get_enum, param
 from ...parallel import comm
 from ...parallel.comqueue import (AllReduce, CompareCriterionFunction, CompleteResultFunction, ComputeFunction,
                                   IterativeComQueue)
-from ...ops import kmeans as kops
+from ...ops import _lib, kmeans as kops
 
 __all__ = ["ClusterSummary", "KMeansTrainModelData", "KMeansModelDataConverter", "KMeansPredictModelData",
            "KMeansModelMapper", "train_kmeans", "kmeans_init", "pairwise_distance"]
@@ -154,7 +154,13 @@ def _seed_cost(d: torch.Tensor, dist_type: str) -> torch.Tensor:
     return d * d if dist_type.upper() == "EUCLIDEAN" else d
 
 
+def _hip_nearest_ok(X: torch.Tensor, dist_type: str) -> bool:
+    return dist_type.upper() == "EUCLIDEAN" and kops.nearest_supported(X) and _lib.available()
+
+
 def _min_dist_to(X: torch.Tensor, C: torch.Tensor, dist_type: str, chunk=1 << 20) -> torch.Tensor:
+    if _hip_nearest_ok(X, dist_type):
+        return kops.nearest_hip(X, C)[1].to(torch.float64).sqrt_()
     out = []
     Cf = C.to(torch.float32 if X.dtype in (torch.bfloat16, torch.float16) else X.dtype)
     for s in range(0, X.shape[0], chunk):
@@ -164,6 +170,8 @@ def _min_dist_to(X: torch.Tensor, C: torch.Tensor, dist_type: str, chunk=1 << 20
 
 
 def _nearest(X: torch.Tensor, C: torch.Tensor, dist_type: str, chunk=1 << 20) -> torch.Tensor:
+    if _hip_nearest_ok(X, dist_type):
+        return kops.nearest_hip(X, C)[0].to(torch.int64)
     out = []
     Cf = C.to(torch.float32 if X.dtype in (torch.bfloat16, torch.float16) else X.dtype)
     for s in range(0, X.shape[0], chunk):
@@ -264,12 +272,12 @@ def kmeans_init(X: torch.Tensor, k: int, init_mode: str, init_steps: int, dist_t
     # k-means||
     centers = _fetch_global_rows(X, [int(rng.integers(n))], counts)
     cost = _min_dist_to(X, centers, dist_type)
-    lrng = torch.Generator(device="cpu").manual_seed(seed * 7919 + comm.get_rank() + 1)
+    lrng = torch.Generator(device=X.device).manual_seed(seed * 7919 + comm.get_rank() + 1)
     for _ in range(max(0, init_steps - 1)):
         tot = torch.tensor([float(cost.sum().item())], dtype=torch.float64)
         comm.all_reduce(tot)
         thre = 2.0 * k / max(float(tot.item()), 1e-300)
-        u = torch.rand(X.shape[0], generator=lrng, dtype=torch.float64).to(X.device)
+        u = torch.rand(X.shape[0], generator=lrng, dtype=torch.float64, device=X.device)
         pick = torch.nonzero(u < cost * thre).reshape(-1)
         local_new = X[pick].to(torch.float64).cpu()
         parts = comm.all_gather_object(local_new)

@@ -70,6 +70,8 @@ _EXTRA_SIGNATURES = {
     "alink_logistic_grad": [_c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_int, _c_vp, _c_vp, _c_vp],
     "alink_vector_assemble": [_c_vp, _c_vp, _c_int, _c_i64, _c_vp, _c_int, _c_vp],
     "alink_feature_hash": [_c_vp, _c_vp, _c_i64, _c_int, _c_vp, _c_vp],
+    "alink_kmeans_nearest_bf16": [_c_vp, _c_i64, _c_int, _c_vp, _c_vp, _c_int, _c_int, _c_vp, _c_vp, _c_int,
+                                  _c_int, _c_vp],
     "alink_als_gram_f32": [_c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_int, _c_int, _c_f, _c_vp, _c_vp, _c_vp],
 }
 

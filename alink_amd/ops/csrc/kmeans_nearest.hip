@@ -1,0 +1,179 @@
+// Nearest-centroid search for k-means|| initialisation and KMeans predict on CDNA4 (gfx950 / MI355X).
+//
+// Replaces the reference's per-sample distance loop used while seeding (KMeansInitCentroids.java:40-165:
+// the cost of every row to the candidate set, then the nearest candidate of every row for the candidate
+// weights) and KMeansModelMapper's per-row argmin (KMeansModelMapper.java:25-106).  In PyTorch the same
+// work is ~6 elementwise launches over an [N, m] fp32 matrix; here it is ONE pass over X per chunk of
+// up to 256 candidates:
+//
+//   S[r][c] = x_r . c - |c|^2 / 2        (v_mfma_f32_32x32x16_bf16, fp32 accumulate; -|c|^2/2 is the
+//                                          accumulator's initial value)
+//   best_r  = argmax_c S[r][c]  (== argmin |x_r - c|^2; ties -> lowest index, like torch.argmin)
+//   d2_r    = max(|x_r|^2 - 2 best_r, 0)
+//
+// * one workgroup = 4 waves; a wave owns 32 rows whose bf16 B fragments stay in 4*KS VGPRs while it
+//   sweeps every centroid block of the chunk (C chunk staged once per workgroup in LDS, XOR-swizzled so
+//   the 32 rows a fragment read touches fall in distinct 16-byte bank groups);
+// * the next 32-row group's fragments are loaded while the current group runs its MFMAs;
+// * chunks of > 256 candidates are processed by successive launches that merge into (idx, d2) in place
+//   (``merge`` = 1), so X is read once per 256 candidates.
+//
+// Contract (checked by the Python wrapper): D in {64, 128, 256} (KS = D/16 k-steps), X row-major bf16
+// [N][D] 16-byte aligned, C row-major bf16 [m][D], cnorm_half[m] = |c|^2/2 in fp32, 1 <= m.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int NB_MAX = 8;    // centroid blocks of 32 per chunk -> 256 candidates
+constexpr int WAVES = 4;
+
+template <int KS>
+__device__ __forceinline__ int cswz(int row, int ch) {
+    // ch: 16-byte chunk index within a row (2*KS chunks); XOR with low row bits
+    constexpr int NCH = 2 * KS;
+    constexpr int MASK = NCH - 1 < 15 ? NCH - 1 : 15;
+    return row * (NCH * 16) + 16 * (ch ^ (row & MASK));
+}
+
+template <int KS>
+__global__ __launch_bounds__(256, 2) void kmeans_nearest_kernel(
+    const __bf16* __restrict__ X, int64_t N, const __bf16* __restrict__ C, const float* __restrict__ chalf,
+    int m, int c0, int* __restrict__ out_idx, float* __restrict__ out_d2, int merge) {
+    constexpr int D = 16 * KS;
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    const int nb = (m + 31) >> 5;
+    float* lneg = reinterpret_cast<float*>(lds + nb * 32 * D * 2);  // after the staged chunk
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int h = lane >> 5;
+    const int l32 = lane & 31;
+
+    // ---- stage the chunk (zero rows beyond m, padding score -inf) ----
+    for (int e = tid; e < nb * 32 * 2 * KS; e += 256) {
+        const int row = e / (2 * KS), ch = e % (2 * KS);
+        uint4 v = {0u, 0u, 0u, 0u};
+        if (row < m) v = *reinterpret_cast<const uint4*>(C + (int64_t)row * D + 8 * ch);
+        *reinterpret_cast<uint4*>(lds + cswz<KS>(row, ch)) = v;
+    }
+    for (int e = tid; e < nb * 32; e += 256) lneg[e] = e < m ? -chalf[e] : -3.0e38f;
+    __syncthreads();
+
+    const int64_t ngroups = (N + 31) >> 5;
+    const int64_t gstride = (int64_t)gridDim.x * WAVES;
+    int64_t g = (int64_t)blockIdx.x * WAVES + wave;
+
+    auto load_frags = [&](int64_t grp, bf16x8* xf) {
+        int64_t r = grp * 32 + l32;
+        r = r < N ? r : N - 1;
+        const bf16x8* p = reinterpret_cast<const bf16x8*>(X + r * D + 8 * h);
+#pragma unroll
+        for (int s = 0; s < KS; ++s) xf[s] = p[2 * s];
+    };
+
+    bf16x8 xf[KS], xn[KS];
+    if (g < ngroups) load_frags(g, xf);
+    for (; g < ngroups; g += gstride) {
+        const int64_t gn = g + gstride;
+        if (gn < ngroups) load_frags(gn, xn);
+
+        float xx = 0.f;
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float v = (float)xf[s][j];
+                xx = fmaf(v, v, xx);
+            }
+        xx += __shfl_xor(xx, 32);
+
+        float best = -3.4e38f;
+        int bidx = 0x7fffffff;
+        for (int b = 0; b < nb; ++b) {
+            f32x16 acc;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[r] = lneg[32 * b + (r & 3) + 8 * (r >> 2) + 4 * h];
+            const int crow = 32 * b + l32;
+#pragma unroll
+            for (int s = 0; s < KS; ++s) {
+                const bf16x8 cf = *reinterpret_cast<const bf16x8*>(lds + cswz<KS>(crow, 2 * s + h));
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cf, xf[s], acc, 0, 0, 0);
+            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int c = 32 * b + (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (acc[r] > best) {   // c increases with r inside a lane -> strict > keeps the lowest index
+                    best = acc[r];
+                    bidx = c;
+                }
+            }
+        }
+        const float ob = __shfl_xor(best, 32);
+        const int oi = __shfl_xor(bidx, 32);
+        if (ob > best || (ob == best && oi < bidx)) {
+            best = ob;
+            bidx = oi;
+        }
+        const int64_t row = g * 32 + l32;
+        if (h == 0 && row < N) {
+            const float d2 = fmaxf(xx - 2.f * best, 0.f);
+            const int gi = bidx + c0;
+            if (merge) {
+                const float prev = out_d2[row];
+                if (d2 < prev) {
+                    out_d2[row] = d2;
+                    out_idx[row] = gi;
+                }
+            } else {
+                out_d2[row] = d2;
+                out_idx[row] = gi;
+            }
+        }
+        if (gn < ngroups) {
+#pragma unroll
+            for (int s = 0; s < KS; ++s) xf[s] = xn[s];
+        }
+    }
+}
+
+template <int KS>
+int launch(const void* X, int64_t N, const void* C, const float* chalf, int m, int c0, int* idx, float* d2,
+           int merge, int grid, hipStream_t st) {
+    const int nb = (m + 31) / 32;
+    const size_t lds = (size_t)nb * 32 * (16 * KS) * 2 + (size_t)nb * 32 * 4;
+    static bool attr_set = false;  // > 64 KiB of dynamic LDS must be opted into once per kernel
+    if (!attr_set) {
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(kmeans_nearest_kernel<KS>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                NB_MAX * 32 * 16 * KS * 2 + NB_MAX * 32 * 4) != hipSuccess)
+            return 3;
+        attr_set = true;
+    }
+    hipLaunchKernelGGL(kmeans_nearest_kernel<KS>, dim3(grid), dim3(256), lds, st,
+                       reinterpret_cast<const __bf16*>(X), N, reinterpret_cast<const __bf16*>(C), chalf, m, c0,
+                       idx, d2, merge);
+    return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+}  // namespace
+
+extern "C" {
+
+// one chunk (m <= 256) of nearest-centroid search; grid = persistent workgroups
+int alink_kmeans_nearest_bf16(const void* X, int64_t N, int D, const void* C, const float* chalf, int m, int c0,
+                              int* out_idx, float* out_d2, int merge, int grid, void* stream) {
+    if (N <= 0 || m <= 0 || m > NB_MAX * 32 || grid <= 0) return 1;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    switch (D) {
+        case 64: return launch<4>(X, N, C, chalf, m, c0, out_idx, out_d2, merge, grid, st);
+        case 128: return launch<8>(X, N, C, chalf, m, c0, out_idx, out_d2, merge, grid, st);
+        case 256: return launch<16>(X, N, C, chalf, m, c0, out_idx, out_d2, merge, grid, st);
+        default: return 1;
+    }
+}
+
+}  // extern "C"

@@ -145,6 +145,9 @@ def assign_accumulate(X: torch.Tensor, C: torch.Tensor, weights: Optional[torch.
 
 def assign(X: torch.Tensor, C: torch.Tensor, chunk: int = 1 << 20) -> Tuple[torch.Tensor, torch.Tensor]:
     """Nearest centroid index and squared euclidean distance for every row."""
+    if nearest_supported(X) and (_lib.available() or not _lib.torch_fallback_allowed()):
+        idx, d2 = nearest_hip(X, C)
+        return idx.to(torch.int64), d2.to(torch.float64)
     low = X.dtype in (torch.bfloat16, torch.float16)
     idx_all, d2_all = [], []
     for s in range(0, X.shape[0], chunk):
@@ -161,3 +164,37 @@ def assign(X: torch.Tensor, C: torch.Tensor, chunk: int = 1 << 20) -> Tuple[torc
         return (torch.zeros(0, dtype=torch.int64, device=X.device),
                 torch.zeros(0, dtype=torch.float64, device=X.device))
     return torch.cat(idx_all), torch.cat(d2_all)
+
+
+NEAREST_DIMS = (64, 128, 256)
+NEAREST_CHUNK = 256
+
+
+def nearest_supported(X: torch.Tensor) -> bool:
+    return (X.is_cuda and X.dtype == torch.bfloat16 and X.dim() == 2 and X.shape[1] in NEAREST_DIMS
+            and X.shape[0] > 0 and X.is_contiguous() and X.data_ptr() % 16 == 0)
+
+
+def nearest_hip(X: torch.Tensor, C: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """(index int32 [N], squared Euclidean distance float32 [N]) of every row's nearest centroid —
+    ``csrc/kmeans_nearest.hip``: one MFMA pass over X per 256 centroids (k-means|| seeding, predict).
+    Centroids are rounded to bf16 (k-means|| candidates are rows of X, so exactly representable)."""
+    L = _lib.require()
+    if not nearest_supported(X):
+        raise ValueError("nearest_hip needs contiguous bf16 [N, D] on GPU with D in (64, 128, 256)")
+    n, d = X.shape
+    Cb = C.to(device=X.device, dtype=torch.bfloat16).contiguous()
+    if Cb.shape[1] != d or Cb.shape[0] == 0:
+        raise ValueError("centroid shape mismatch")
+    chalf = (0.5 * (Cb.float() ** 2).sum(1)).contiguous()
+    idx = torch.empty(n, dtype=torch.int32, device=X.device)
+    d2 = torch.empty(n, dtype=torch.float32, device=X.device)
+    grid = 2 * _num_cus(X.device)
+    st = _lib.stream_ptr(X.device)
+    for c0 in range(0, Cb.shape[0], NEAREST_CHUNK):
+        m = min(NEAREST_CHUNK, Cb.shape[0] - c0)
+        rc = L.alink_kmeans_nearest_bf16(X.data_ptr(), n, d, Cb[c0].data_ptr(), chalf[c0].data_ptr(), m, c0,
+                                         idx.data_ptr(), d2.data_ptr(), int(c0 > 0), grid, st)
+        if rc != 0:
+            raise RuntimeError(f"alink_kmeans_nearest_bf16 failed: {rc}")
+    return idx, d2

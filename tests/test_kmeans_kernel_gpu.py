@@ -60,3 +60,36 @@ def test_v2_kernel_small_k(n, k):
     got = K.assign_accumulate_hip(X, C, variant=2)
     ref = K.assign_accumulate_torch(X, C)
     assert (got[:, -1] - ref[:, -1]).abs().sum().item() <= 2
+
+
+@pytest.mark.parametrize("d", [64, 128, 256])
+@pytest.mark.parametrize("n,m", [(1, 1), (31, 5), (1000, 33), (4097, 256), (20001, 300), (70000, 700)])
+def test_nearest_kernel_matches_fp32_reference(n, m, d):
+    """csrc/kmeans_nearest.hip vs a plain fp32 PyTorch argmin of |x - c|^2 (bf16-rounded centroids)."""
+    from alink_amd.ops import kmeans as K
+    g = torch.Generator(device="cpu").manual_seed(n + m + d)
+    X = (torch.randn(n, d, generator=g) * 2).to("cuda", torch.bfloat16)
+    C = (torch.randn(m, d, generator=g) * 2).to("cuda", torch.float64)
+    idx, d2 = K.nearest_hip(X, C)
+    Cb = C.to(torch.bfloat16).float()
+    ref = ((X.float()[:, None, :] - Cb[None, :, :]) ** 2).sum(-1) if n * m <= 4_000_000 else torch.cdist(X.float(), Cb) ** 2
+    rbest, ridx = ref.min(1)
+    torch.cuda.synchronize()
+    assert idx.shape == (n,) and d2.shape == (n,)
+    assert int(idx.min()) >= 0 and int(idx.max()) < m
+    # chosen centroid's true distance equals the optimum up to fp32 rounding of the expanded form
+    chosen = ref.gather(1, idx.long()[:, None])[:, 0]
+    tol = 1e-4 * (X.float() ** 2).sum(1) + 1e-3
+    assert bool(((chosen - rbest) <= tol).all())
+    assert bool(((d2 - rbest).abs() <= tol + 1e-3 * rbest).all())
+    assert (idx.long() != ridx).float().mean().item() < 0.01
+
+
+def test_nearest_kernel_exact_candidates():
+    """k-means|| candidates are rows of X: distance to itself must come out 0 and the index its own."""
+    from alink_amd.ops import kmeans as K
+    X = torch.randn(5000, 128, device="cuda").to(torch.bfloat16)
+    sel = torch.arange(0, 5000, 17, device="cuda")
+    idx, d2 = K.nearest_hip(X, X[sel].double())
+    assert torch.equal(idx[sel].long(), torch.arange(sel.numel(), device="cuda"))
+    assert float(d2[sel].abs().max()) < 1e-2
