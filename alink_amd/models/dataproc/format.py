@@ -1,0 +1,696 @@
+"""Format conversion between Columns / CSV / JSON / KV / Vector / Triple, JSON path extraction and the
+string-to-columns parsers.
+
+Reference behaviour (``A/operator/common/dataproc/format/*``, ``StringToColumnsMappers.java``,
+``StringParsers.java``, ``A/common/utils/JsonPathMapper.java``):
+
+* a *reader* turns one input row into a ``key -> string`` map (``FormatReader.read``; ``ColumnsReader``
+  uses ``toString`` of each non-null cell, ``VectorReader`` the index (or schema name) of each entry);
+* a *writer* turns the map into the output cells (``ColumnsWriter`` parses each value with the column
+  type, ``CsvWriter`` quotes values containing the delimiter/quote, ``KvWriter``/``JsonWriter`` iterate
+  the map, ``VectorWriter`` builds a sparse vector from integer keys or a dense string in schema order);
+* the map is a ``java.util.HashMap`` in the reference, so KV/JSON outputs follow HashMap iteration order —
+  reproduced with ``java_hashmap_order`` so the strings are byte-identical to the reference's.
+* ``AnyToTriple`` flattens a row into ``(reserved..., key, value)`` rows; ``TripleToAny`` groups triples
+  by row id and writes each group with a writer (``TripleToAnyBatchOp.java``).
+
+These are host (string) transforms — the reference runs them as Flink ``MapFunction``s; here they run
+per micro-batch on the CPU side of the DAG, columnar where the input allows it.
+"""
+from __future__ import annotations
+
+import json
+import re
+from typing import Any, Dict, List, Optional, Sequence, Tuple
+
+from ...common.javafmt import gson_dumps, java_double_str, java_hashmap_order, java_str
+from ...common.linalg import DenseVector, SparseVector, VectorUtil
+from ...common.mapper import FlatMapper, Mapper, OutputColsHelper, find_col_index, find_col_indices
+from ...common.params import Params
+from ...common.table import Row
+from ...common.types import TableSchema, Types, schema_str_to_schema
+from ...operator.common.io.csv import CsvParser, parse_token
+
+__all__ = ["FormatTransMapper", "AnyToTripleFlatMapper", "triple_to_any_rows", "CsvToColumnsMapper",
+           "JsonToColumnsMapper", "KvToColumnsMapper", "JsonPathMapper", "lenient_json_loads", "json_path_read",
+           "init_format_reader", "init_format_writer"]
+
+
+def _enum_name(v) -> str:
+    return v.name if hasattr(v, "name") else str(v).upper()
+
+
+def _p(params: Params, name: str, default=None):
+    return params.get(name) if params.contains(name) else default
+
+
+# ---------------------------------------------------------------------------------------------------
+# lenient JSON (json-smart / Gson-lenient style: unquoted keys & values, single quotes)
+# ---------------------------------------------------------------------------------------------------
+class _LenientJson:
+    _STOP = set(",:}]")
+
+    def __init__(self, s: str):
+        self.s = s
+        self.i = 0
+
+    def _ws(self):
+        s, n = self.s, len(self.s)
+        while self.i < n and s[self.i] in " \t\r\n":
+            self.i += 1
+
+    def value(self):
+        self._ws()
+        if self.i >= len(self.s):
+            raise ValueError("unexpected end of json")
+        c = self.s[self.i]
+        if c == "{":
+            return self._obj()
+        if c == "[":
+            return self._arr()
+        if c in "\"'":
+            return self._quoted()
+        return self._bare()
+
+    def _quoted(self):
+        q = self.s[self.i]
+        self.i += 1
+        out = []
+        while self.i < len(self.s):
+            c = self.s[self.i]
+            if c == "\\" and self.i + 1 < len(self.s):
+                nxt = self.s[self.i + 1]
+                if nxt == "u":
+                    out.append(chr(int(self.s[self.i + 2:self.i + 6], 16)))
+                    self.i += 6
+                    continue
+                out.append({"n": "\n", "t": "\t", "r": "\r", "b": "\b", "f": "\f"}.get(nxt, nxt))
+                self.i += 2
+                continue
+            if c == q:
+                self.i += 1
+                return "".join(out)
+            out.append(c)
+            self.i += 1
+        raise ValueError("unterminated string")
+
+    def _bare(self):
+        st = self.i
+        while self.i < len(self.s) and self.s[self.i] not in self._STOP:
+            self.i += 1
+        tok = self.s[st:self.i].strip()
+        if tok == "null":
+            return None
+        if tok == "true":
+            return True
+        if tok == "false":
+            return False
+        if re.fullmatch(r"-?\d+", tok):
+            return int(tok)
+        if re.fullmatch(r"-?(\d+\.?\d*|\.\d+)([eE][-+]?\d+)?", tok):
+            return float(tok)
+        return tok
+
+    def _obj(self):
+        self.i += 1
+        out: Dict[str, Any] = {}
+        self._ws()
+        if self.i < len(self.s) and self.s[self.i] == "}":
+            self.i += 1
+            return out
+        while True:
+            self._ws()
+            k = self._quoted() if self.s[self.i] in "\"'" else str(self._bare())
+            self._ws()
+            if self.i >= len(self.s) or self.s[self.i] not in ":=":
+                raise ValueError("expected ':' in json object")
+            self.i += 1
+            out[k] = self.value()
+            self._ws()
+            if self.i >= len(self.s):
+                raise ValueError("unterminated object")
+            if self.s[self.i] == ",":
+                self.i += 1
+                continue
+            if self.s[self.i] == "}":
+                self.i += 1
+                return out
+            raise ValueError("bad json object")
+
+    def _arr(self):
+        self.i += 1
+        out: List[Any] = []
+        self._ws()
+        if self.i < len(self.s) and self.s[self.i] == "]":
+            self.i += 1
+            return out
+        while True:
+            out.append(self.value())
+            self._ws()
+            if self.s[self.i] == ",":
+                self.i += 1
+                continue
+            if self.s[self.i] == "]":
+                self.i += 1
+                return out
+            raise ValueError("bad json array")
+
+
+def lenient_json_loads(s: str):
+    try:
+        return json.loads(s)
+    except (ValueError, TypeError):
+        p = _LenientJson(s)
+        v = p.value()
+        return v
+
+
+_PATH_TOK = re.compile(r"\.\.|\.\*|\.([^.\[\]]+)|\[\s*\*\s*\]|\[\s*(-?\d+)\s*\]|\[\s*['\"]([^'\"]+)['\"]\s*\]")
+
+
+def json_path_read(doc, path: str):
+    """Subset of Jayway JsonPath used by Alink docs: ``$``, ``.name``, ``['name']``, ``[i]``, ``[*]``, ``.*``.
+    A wildcard makes the result a list.  Missing keys raise ``KeyError`` (``PathNotFoundException``)."""
+    path = path.strip()
+    if not path.startswith("$"):
+        path = "$." + path
+    cur = [doc]
+    multi = False
+    pos = 1
+    while pos < len(path):
+        m = _PATH_TOK.match(path, pos)
+        if m is None:
+            raise ValueError(f"bad json path {path}")
+        tok = m.group(0)
+        pos = m.end()
+        nxt = []
+        if tok == "..":
+            raise ValueError("deep scan '..' is not supported")
+        if tok in (".*",) or tok.replace(" ", "") == "[*]":
+            multi = True
+            for c in cur:
+                if isinstance(c, dict):
+                    nxt.extend(c.values())
+                elif isinstance(c, list):
+                    nxt.extend(c)
+        elif m.group(2) is not None:
+            i = int(m.group(2))
+            for c in cur:
+                if not isinstance(c, list):
+                    raise KeyError(path)
+                nxt.append(c[i])
+        else:
+            key = m.group(1) if m.group(1) is not None else m.group(3)
+            for c in cur:
+                if isinstance(c, dict) and key in c:
+                    nxt.append(c[key])
+                elif not multi:
+                    raise KeyError(f"No results for path: {path}")
+        cur = nxt
+    return cur if multi else cur[0]
+
+
+def _gson_of(v) -> str:
+    """``gson.toJson`` of a json-smart value (JSONObject is a HashMap -> HashMap key order)."""
+    return gson_dumps(v, java_map_order=True)
+
+
+def _java_to_string(v) -> str:
+    """``Object.toString`` of a Gson-parsed value (numbers are Doubles, objects LinkedTreeMaps)."""
+    if isinstance(v, bool):
+        return "true" if v else "false"
+    if isinstance(v, (int, float)):
+        return java_double_str(float(v))
+    if isinstance(v, dict):
+        return "{" + ", ".join(f"{k}={_java_to_string(x)}" for k, x in v.items()) + "}"
+    if isinstance(v, list):
+        return "[" + ", ".join(_java_to_string(x) for x in v) + "]"
+    if v is None:
+        return "null"
+    return str(v)
+
+
+# ---------------------------------------------------------------------------------------------------
+# field parsing (Flink FieldParser semantics for the target column type)
+# ---------------------------------------------------------------------------------------------------
+def parse_field(token: Optional[str], t) -> Tuple[bool, Any]:
+    if t == Types.STRING:
+        return True, token
+    if token is None or not str(token).strip():
+        return False, None
+    try:
+        if t in (Types.LONG, Types.INT, Types.SHORT, Types.BYTE):
+            s = str(token).strip()
+            if not re.fullmatch(r"[-+]?\d+", s):
+                return False, None
+            return True, int(s)
+        return True, parse_token(str(token), t)
+    except (ValueError, TypeError):
+        return False, None
+
+
+# ---------------------------------------------------------------------------------------------------
+# readers
+# ---------------------------------------------------------------------------------------------------
+class _Reader:
+    def read(self, row) -> Tuple[bool, Dict[str, Optional[str]]]:
+        raise NotImplementedError
+
+
+class ColumnsReader(_Reader):
+    def __init__(self, idx: List[int], names: List[str]):
+        self.idx, self.names = idx, names
+
+    def read(self, row):
+        out = {}
+        for i, n in zip(self.idx, self.names):
+            v = row[i]
+            if v is not None:
+                out[n] = java_str(v)
+        return True, out
+
+
+class CsvReader(_Reader):
+    def __init__(self, col: int, schema: TableSchema, delim: str, quote: Optional[str]):
+        self.col = col
+        self.names = list(schema.names)
+        self.parser = CsvParser(schema.types, delim, quote)
+
+    def read(self, row):
+        line = row[self.col]
+        if line is None:
+            return False, {}
+        ok, vals = self.parser.parse(line)
+        return ok, {n: (java_str(v) if v is not None else None) for n, v in zip(self.names, vals)}
+
+
+class JsonReader(_Reader):
+    def __init__(self, col: int):
+        self.col = col
+
+    def read(self, row):
+        line = row[self.col]
+        if line is None:
+            return False, {}
+        try:
+            m = lenient_json_loads(line)
+        except ValueError:
+            return False, {}
+        if not isinstance(m, dict):
+            return False, {}
+        return True, {str(k): _java_to_string(v) for k, v in m.items()}
+
+
+class KvReader(_Reader):
+    def __init__(self, col: int, col_delim: str, val_delim: str):
+        self.col, self.cd, self.vd = col, col_delim, val_delim
+
+    def read(self, row):
+        line = row[self.col]
+        out = {}
+        if line is None:
+            return False, out
+        for f in re.split(self.cd, line) if len(self.cd) > 1 else line.split(self.cd):
+            if not f.strip():
+                return False, out
+            kv = re.split(self.vd, f) if len(self.vd) > 1 else f.split(self.vd)
+            if len(kv) != 2:
+                return False, out
+            out[kv[0]] = kv[1]
+        return True, out
+
+
+class VectorReader(_Reader):
+    def __init__(self, col: int, names: Optional[List[str]]):
+        self.col, self.names = col, names
+
+    def read(self, row):
+        v = VectorUtil.getVector(row[self.col])
+        out = {}
+        if v is None:
+            return False, out
+        if isinstance(v, SparseVector):
+            for i, x in zip(v.getIndices().tolist(), v.getValues().tolist()):
+                if self.names is None:
+                    out[str(i)] = java_double_str(x)
+                elif i < len(self.names):
+                    out[self.names[i]] = java_double_str(x)
+        else:
+            data = v.getData().tolist()
+            for i, x in enumerate(data):
+                if self.names is None:
+                    out[str(i)] = java_double_str(x)
+                elif i < len(self.names):
+                    out[self.names[i]] = java_double_str(x)
+        return True, out
+
+
+# ---------------------------------------------------------------------------------------------------
+# writers
+# ---------------------------------------------------------------------------------------------------
+class _Writer:
+    names: List[str]
+    types: list
+
+    def write(self, m: Dict[str, Optional[str]]) -> Tuple[bool, List[Any]]:
+        raise NotImplementedError
+
+
+def _hash_items(m: Dict[str, Any]):
+    return [(k, m[k]) for k in java_hashmap_order(list(m.keys()))]
+
+
+class ColumnsWriter(_Writer):
+    def __init__(self, schema: TableSchema):
+        self.names, self.types = list(schema.names), list(schema.types)
+        self.pos = {n: i for i, n in enumerate(self.names)}
+
+    def write(self, m):
+        out = [None] * len(self.names)
+        for k, v in m.items():
+            i = self.pos.get(k)
+            if i is None:
+                continue
+            ok, pv = parse_field(v, self.types[i])
+            if not ok:
+                return False, out
+            out[i] = pv
+        return True, out
+
+
+class CsvWriter(_Writer):
+    def __init__(self, out_col: str, schema: TableSchema, delim: str, quote: Optional[str]):
+        self.cols = list(schema.names)
+        self.delim, self.quote = delim, quote
+        self.names, self.types = [out_col], [Types.STRING]
+
+    def write(self, m):
+        parts = []
+        for c in self.cols:
+            v = m.get(c)
+            if v is None:
+                parts.append("")
+            elif self.quote and (not v or self.delim in v or self.quote in v):
+                parts.append(self.quote + v.replace(self.quote, self.quote * 3) + self.quote)
+            else:
+                parts.append(v)
+        return True, [self.delim.join(parts)]
+
+
+class JsonWriter(_Writer):
+    def __init__(self, out_col: str):
+        self.names, self.types = [out_col], [Types.STRING]
+
+    def write(self, m):
+        # Gson without serializeNulls drops null map values (JsonConverter.java:117)
+        return True, [gson_dumps({k: v for k, v in m.items() if v is not None}, java_map_order=True)]
+
+
+class KvWriter(_Writer):
+    def __init__(self, out_col: str, col_delim: str, val_delim: str):
+        self.names, self.types = [out_col], [Types.STRING]
+        self.cd, self.vd = col_delim, val_delim
+
+    def write(self, m):
+        return True, [self.cd.join(f"{k}{self.vd}{java_str(v)}" for k, v in _hash_items(m))]
+
+
+class VectorWriter(_Writer):
+    def __init__(self, out_col: str, size: int, from_names: Optional[List[str]]):
+        self.names, self.types = [out_col], [Types.STRING]
+        self.size = int(size) if size is not None else -1
+        self.from_names = from_names
+
+    def write(self, m):
+        if self.from_names is None:
+            try:
+                items = _hash_items(m)
+                idx = [int(k) for k, _ in items]
+                vals = [float(v) for _, v in items]
+            except (TypeError, ValueError):
+                return False, [None]
+            return True, [VectorUtil.toString(SparseVector(self.size, idx, vals))]
+        n = len(self.from_names)
+        prefix = ""
+        if self.size > n:
+            prefix = f"${self.size}$"
+        elif 0 < self.size < n:
+            n = self.size
+        return True, [prefix + " ".join(java_str(m.get(c)) for c in self.from_names[:n])]
+
+
+# ---------------------------------------------------------------------------------------------------
+# factory (FormatTransMapper.initFormatReader / initFormatWriter)
+# ---------------------------------------------------------------------------------------------------
+def init_format_reader(schema: TableSchema, params: Params) -> Tuple[_Reader, Optional[List[str]]]:
+    f = _enum_name(params.get("fromFormat"))
+    names = list(schema.names)
+    if f == "KV":
+        return KvReader(find_col_index(names, params.get("kvCol")), _p(params, "kvColDelimiter", ","),
+                        _p(params, "kvValDelimiter", ":")), None
+    if f == "CSV":
+        sch = schema_str_to_schema(params.get("schemaStr"))
+        return CsvReader(find_col_index(names, params.get("csvCol")), sch, _p(params, "csvFieldDelimiter", ","),
+                         _p(params, "quoteChar", '"')), list(sch.names)
+    if f == "VECTOR":
+        ss = _p(params, "schemaStr")
+        vn = list(schema_str_to_schema(ss).names) if ss else None
+        return VectorReader(find_col_index(names, params.get("vectorCol")), vn), None
+    if f == "JSON":
+        return JsonReader(find_col_index(names, params.get("jsonCol"))), None
+    if f == "COLUMNS":
+        sel = _p(params, "selectedCols") or names
+        return ColumnsReader(find_col_indices(names, sel), list(sel)), list(sel)
+    raise ValueError(f"Can not translate this type : {f}")
+
+
+def init_format_writer(params: Params, from_names: Optional[List[str]]) -> _Writer:
+    t = _enum_name(params.get("toFormat"))
+    if t == "COLUMNS":
+        return ColumnsWriter(schema_str_to_schema(params.get("schemaStr")))
+    if t == "JSON":
+        return JsonWriter(params.get("jsonCol"))
+    if t == "KV":
+        return KvWriter(params.get("kvCol"), _p(params, "kvColDelimiter", ","), _p(params, "kvValDelimiter", ":"))
+    if t == "CSV":
+        return CsvWriter(params.get("csvCol"), schema_str_to_schema(params.get("schemaStr")),
+                         _p(params, "csvFieldDelimiter", ","), _p(params, "quoteChar", '"'))
+    if t == "VECTOR":
+        return VectorWriter(params.get("vectorCol"), _p(params, "vectorSize", -1), from_names)
+    raise ValueError(f"Can not translate to this type : {t}")
+
+
+def _handle_error(params: Params) -> bool:
+    return _enum_name(_p(params, "handleInvalid", "ERROR")) == "ERROR"
+
+
+class FormatTransMapper(Mapper):
+    """``FormatTransMapper.java`` — ``fromFormat``/``toFormat`` params pick the reader and the writer."""
+
+    def __init__(self, dataSchema: TableSchema, params: Optional[Params] = None):
+        super().__init__(dataSchema, params)
+        self.reader, from_names = init_format_reader(dataSchema, self.params)
+        self.writer = init_format_writer(self.params, from_names)
+        self.err = _handle_error(self.params)
+        self.vec_to_cols = (_enum_name(self.params.get("fromFormat")) == "VECTOR"
+                            and _enum_name(self.params.get("toFormat")) == "COLUMNS")
+        self.helper = OutputColsHelper(dataSchema, self.writer.names, self.writer.types,
+                                       _p(self.params, "reservedCols"))
+
+    def _map_row_values(self, row):
+        ok, m = self.reader.read(row)
+        if not ok and self.err:
+            raise RuntimeError(f"Fail to read: {list(row)}")
+        ok, out = self.writer.write(m)
+        if not ok and self.err:
+            raise RuntimeError(f"Fail to write: {gson_dumps(m)}")
+        if self.vec_to_cols:
+            out = [0.0 if v is None else v for v in out]
+        return out
+
+
+class AnyToTripleFlatMapper(FlatMapper):
+    """``AnyToTripleFlatMapper.java`` — one output row per (key, value) of the read map."""
+
+    def __init__(self, dataSchema: TableSchema, params: Optional[Params] = None):
+        super().__init__(dataSchema, params)
+        sch = schema_str_to_schema(self.params.get("tripleColValSchemaStr"))
+        self.kt, self.vt = sch.types[0], sch.types[1]
+        self.reader, _ = init_format_reader(dataSchema, self.params)
+        self.err = _handle_error(self.params)
+        self.helper = OutputColsHelper(dataSchema, list(sch.names), list(sch.types), _p(self.params, "reservedCols"))
+
+    def getOutputSchema(self):
+        return self.helper.getResultSchema()
+
+    def flatMap(self, row) -> List[Row]:
+        ok, m = self.reader.read(row)
+        out = []
+        if not ok:
+            if self.err:
+                raise RuntimeError(f"Fail to read: {list(row)}")
+            return out
+        for k, v in _hash_items(m):
+            if v is None or not str(v).strip():
+                continue
+            ok1, pk = parse_field(k, self.kt)
+            ok2, pv = parse_field(v, self.vt)
+            if ok1 and ok2:
+                out.append(self.helper.getResultRow(row, [pk, pv]))
+            elif self.err:
+                raise RuntimeError(f"Fail to write: {gson_dumps(m)}")
+        return out
+
+
+def triple_to_any_rows(rows: Sequence[Sequence[Any]], params: Params) -> Tuple[List[str], list, List[Row]]:
+    """Group ``(row, col, val)`` triples by row id and write each group (``TripleToAnyBatchOp.ToAny``).
+    Returns output names/types (excluding the row column) and the output rows ``(rowId, cells...)``."""
+    writer = init_format_writer(params, None)
+    err = _handle_error(params)
+    groups: Dict[Any, Dict[str, str]] = {}
+    for r, c, v in rows:
+        groups.setdefault(r, {})[java_str(c)] = java_str(v)
+    out = []
+    for r in sorted(groups, key=lambda x: (x is None, x)):
+        ok, cells = writer.write(groups[r])
+        if not ok:
+            if err:
+                raise RuntimeError(f"Fail to convert: {gson_dumps(groups[r])}")
+            continue
+        out.append(Row((r,) + tuple(cells)))
+    return writer.names, writer.types, out
+
+
+# ---------------------------------------------------------------------------------------------------
+# StringToColumnsMappers (CsvToColumns / JsonToColumns / KvToColumns with schemaStr)
+# ---------------------------------------------------------------------------------------------------
+class _StringToColumns(Mapper):
+    COL_PARAMS: Tuple[str, ...] = ()
+
+    def __init__(self, dataSchema: TableSchema, params: Optional[Params] = None):
+        super().__init__(dataSchema, params)
+        col = None
+        for name in self.COL_PARAMS + ("selectedCol",):
+            col = col or _p(self.params, name)
+        self.idx = find_col_index(dataSchema.names, col)
+        sch = schema_str_to_schema(self.params.get("schemaStr"))
+        self.names, self.types = list(sch.names), list(sch.types)
+        self.err = _handle_error(self.params)
+        self.helper = OutputColsHelper(dataSchema, self.names, self.types, _p(self.params, "reservedCols"))
+
+    def parse(self, text: str) -> Tuple[bool, List[Any]]:
+        raise NotImplementedError
+
+    def _map_row_values(self, row):
+        text = row[self.idx]
+        ok, vals = self.parse(text) if text is not None else (False, [None] * len(self.names))
+        if not ok and self.err:
+            raise RuntimeError(f'Fail to parse "{text}"')
+        return vals
+
+
+class CsvToColumnsMapper(_StringToColumns):
+    COL_PARAMS = ("csvCol",)
+
+    def __init__(self, dataSchema, params=None):
+        super().__init__(dataSchema, params)
+        delim = _p(self.params, "csvFieldDelimiter") or _p(self.params, "fieldDelimiter") or ","
+        self.parser = CsvParser(self.types, delim, _p(self.params, "quoteChar", '"'))
+
+    def parse(self, text):
+        return self.parser.parse(text)
+
+
+class JsonToColumnsMapper(_StringToColumns):
+    COL_PARAMS = ("jsonCol",)
+
+    def parse(self, text):
+        try:
+            doc = lenient_json_loads(text)
+        except ValueError:
+            return False, [None] * len(self.names)
+        out, ok = [], True
+        for n, t in zip(self.names, self.types):
+            try:
+                o = json_path_read(doc, "$." + n)
+            except (KeyError, IndexError, ValueError):
+                o = None
+            if o is None:
+                ok = False
+                out.append(None)
+                continue
+            s = o if isinstance(o, str) else _gson_of(o)
+            good, v = parse_field(s, t)
+            ok = ok and good
+            out.append(v)
+        return ok, out
+
+
+class KvToColumnsMapper(_StringToColumns):
+    COL_PARAMS = ("kvCol",)
+
+    def __init__(self, dataSchema, params=None):
+        super().__init__(dataSchema, params)
+        self.cd = _p(self.params, "kvColDelimiter") or _p(self.params, "colDelimiter") or ","
+        self.vd = _p(self.params, "kvValDelimiter") or _p(self.params, "valDelimiter") or ":"
+        self.pos = {n: i for i, n in enumerate(self.names)}
+
+    def parse(self, text):
+        out = [None] * len(self.names)
+        ok, cnt = True, 0
+        for f in text.split(self.cd):
+            if not f.strip():
+                ok = False
+                continue
+            kv = f.split(self.vd)
+            if len(kv) < 2:
+                ok = False
+                continue
+            i = self.pos.get(kv[0])
+            if i is None:
+                continue
+            good, v = parse_field(kv[1], self.types[i])
+            ok = ok and good
+            out[i] = v
+            cnt += 1
+        if cnt < len(self.names):
+            ok = False
+        return ok, out
+
+
+class JsonPathMapper(Mapper):
+    """``JsonValueBatchOp`` — ``jsonPath[i]`` of the selected column into ``outputCols[i]`` (strings)."""
+
+    def __init__(self, dataSchema, params=None):
+        super().__init__(dataSchema, params)
+        self.idx = find_col_index(dataSchema.names, self.params.get("selectedCol"))
+        self.outs = [c.strip() for c in self.params.get("outputCols")]
+        self.paths = list(self.params.get("jsonPath"))
+        if len(self.paths) != len(self.outs):
+            raise ValueError(f"jsonPath and outputColName mismatch: {len(self.paths)} vs {len(self.outs)}")
+        self.skip = bool(_p(self.params, "skipFailed", False))
+        self.helper = OutputColsHelper(dataSchema, self.outs, [Types.STRING] * len(self.outs),
+                                       _p(self.params, "reservedCols"))
+
+    def _map_row_values(self, row):
+        text = row[self.idx]
+        if text is None or not str(text).strip():
+            if self.skip:
+                return [None] * len(self.paths)
+            raise RuntimeError("empty json string")
+        res = []
+        try:
+            doc = lenient_json_loads(text)
+        except ValueError as e:
+            if not self.skip:
+                raise RuntimeError(f"Fail to getVector json path: {e}")
+            return [None] * len(self.paths)
+        for p in self.paths:
+            try:
+                o = json_path_read(doc, p)
+                res.append(o if isinstance(o, str) else _gson_of(o))
+            except (KeyError, IndexError, ValueError) as e:
+                if not self.skip:
+                    raise RuntimeError(f"Fail to getVector json path: {e}")
+                res.append(None)
+        return res

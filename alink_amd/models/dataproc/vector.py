@@ -189,15 +189,31 @@ class VectorSerializeMapper(Mapper):
 
 
 class VectorToColumnsMapper(Mapper):
+    """``VectorToColumnsMapper`` (``outputCols``) or, when ``schemaStr`` is given instead, the format
+    version ``dataproc/format/VectorToColumnsBatchOp`` (``FormatTransMapper`` VECTOR -> COLUMNS)."""
+
     def __init__(self, dataSchema, params=None):
         super().__init__(dataSchema, params)
         p = self.params
+        self._delegate = None
+        if not (p.contains("outputCols") and p.get("outputCols")) and p.contains("schemaStr") and p.get("schemaStr"):
+            from .format import FormatTransMapper
+            q = p.clone()
+            q.set("fromFormat", "VECTOR")
+            q.set("toFormat", "COLUMNS")
+            if not (q.contains("vectorCol") and q.get("vectorCol")):
+                q.set("vectorCol", p.get("selectedCol"))
+            self._delegate = FormatTransMapper(dataSchema, q)
+            self.helper = self._delegate.helper
+            return
         self.idx = find_col_index(dataSchema.names, p.get("selectedCol"))
         self.outs = p.get("outputCols")
         reserved = p.get("reservedCols") if p.contains("reservedCols") else None
         self.helper = OutputColsHelper(dataSchema, self.outs, [Types.DOUBLE] * len(self.outs), reserved)
 
     def _map_row_values(self, row):
+        if self._delegate is not None:
+            return self._delegate._map_row_values(row)
         v = row[self.idx]
         if v is None:
             return [None] * len(self.outs)

@@ -12,3 +12,4 @@ from .tree import *  # noqa: F401,F403
 from .recommendation import *  # noqa: F401,F403
 from .nlp import *  # noqa: F401,F403
 from .classification_extra import *  # noqa: F401,F403
+from .format import *  # noqa: F401,F403

@@ -226,4 +226,9 @@ class VectorSerializeBatchOp(MapBatchOp):
 
 
 class VectorToColumnsBatchOp(MapBatchOp):
+    """Vector flavour (``selectedCol`` + ``outputCols``) or the format flavour (``vectorCol`` + ``schemaStr``,
+    ``dataproc/format/VectorToColumnsBatchOp``)."""
     MAPPER = V.VectorToColumnsMapper
+    EXTRA_PARAMS = [ParamInfo("vectorCol", str, "Name of a vector column", default=None),
+                    ParamInfo("schemaStr", str, "Formatted schema", default=None),
+                    ParamInfo("handleInvalid", str, "Strategy to handle unseen token", default="ERROR")]

@@ -1,0 +1,123 @@
+"""Format-conversion batch ops: ``XToYBatchOp`` for X, Y in {Columns, Csv, Json, Kv, Vector}, ``XToTriple``,
+``TripleToX``, the schema-driven ``CsvToColumns``/``JsonToColumns``/``KvToColumns`` and ``JsonValue``.
+
+Reference: ``A/operator/batch/dataproc/format/*`` (``BaseFormatTransBatchOp`` = ``MapBatchOp`` over
+``FormatTransMapper`` with fixed ``fromFormat``/``toFormat``; ``AnyToTripleBatchOp`` = ``FlatMapBatchOp`` over
+``AnyToTripleFlatMapper``; ``TripleToAnyBatchOp.java`` groups triples by row and writes each group) and
+``A/operator/batch/dataproc/{CsvToColumns,JsonToColumns,KvToColumns,JsonValue}BatchOp.java``.
+Row-local conversions run on each rank's partition; ``TripleToAny`` gathers the triples, groups them once and
+keeps this rank's block of the grouped rows (like the SQL global ops).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+from ...common.params import ParamInfo, Params
+from ...common.table import MTable
+from ...common.types import TableSchema
+from ...models.dataproc import format as F
+from ...parallel import comm
+from ..base import BatchOperator, gather_table, partition_bounds
+from .utils import FlatMapBatchOp, MapBatchOp
+
+FORMATS = ["Columns", "Csv", "Json", "Kv", "Vector"]
+
+__all__ = ["BaseFormatTransBatchOp", "AnyToTripleBatchOp", "TripleToAnyBatchOp", "CsvToColumnsBatchOp",
+           "JsonToColumnsBatchOp", "KvToColumnsBatchOp", "JsonValueBatchOp"]
+
+
+class BaseFormatTransBatchOp(MapBatchOp):
+    """Generic ``fromFormat`` -> ``toFormat`` conversion (``BaseFormatTransBatchOp.java``)."""
+    MAPPER = F.FormatTransMapper
+    EXTRA_PARAMS = [ParamInfo("fromFormat", str, "the format type of trans from", default=None),
+                    ParamInfo("toFormat", str, "the format type of trans to", default=None)]
+    FROM: Optional[str] = None
+    TO: Optional[str] = None
+
+    def __init__(self, params: Optional[Params] = None, **kw):
+        super().__init__(params, **kw)
+        if self.FROM is not None:
+            self.getParams().set("fromFormat", self.FROM)
+            self.getParams().set("toFormat", self.TO)
+
+
+class AnyToTripleBatchOp(FlatMapBatchOp):
+    """Row -> (reserved cols, key, value) rows (``AnyToTripleBatchOp.java``)."""
+    MAPPER = F.AnyToTripleFlatMapper
+    EXTRA_PARAMS = BaseFormatTransBatchOp.EXTRA_PARAMS
+    FROM: Optional[str] = None
+
+    def __init__(self, params: Optional[Params] = None, **kw):
+        super().__init__(params, **kw)
+        if self.FROM is not None:
+            self.getParams().set("fromFormat", self.FROM)
+
+
+class TripleToAnyBatchOp(BatchOperator):
+    """Group ``(tripleRowCol, tripleColCol, tripleValCol)`` by row and write each group (``TripleToAnyBatchOp.java``)."""
+    EXTRA_PARAMS = BaseFormatTransBatchOp.EXTRA_PARAMS
+    TO: Optional[str] = None
+
+    def __init__(self, params: Optional[Params] = None, **kw):
+        super().__init__(params, **kw)
+        if self.TO is not None:
+            self.getParams().set("toFormat", self.TO)
+
+    def linkFrom(self, *inputs):
+        mt = self.checkAndGetFirst(inputs).getOutputTable()
+        p = self.getParams()
+        rc, cc, vc = p.get("tripleRowCol"), p.get("tripleColCol"), p.get("tripleValCol")
+        full = mt if (mt.replicated or comm.get_world_size() == 1) else gather_table(mt)
+        sel = full.select([rc, cc, vc])
+        names, types, rows = F.triple_to_any_rows(sel.rows(), p)
+        schema = TableSchema([rc] + list(names), [full.col_type(rc)] + list(types))
+        out = MTable.from_rows(rows, schema)
+        if not mt.replicated and comm.get_world_size() > 1:
+            lo, hi = partition_bounds(out.num_rows, self.env)
+            out = out.slice(lo, hi)
+            out.replicated = False
+        else:
+            out.replicated = mt.replicated
+        self.setOutputTable(out)
+        return self
+
+
+class CsvToColumnsBatchOp(MapBatchOp):
+    """CSV string column -> typed columns by ``schemaStr`` (``StringToColumnsMappers.CsvToColumnsMapper``)."""
+    MAPPER = F.CsvToColumnsMapper
+    EXTRA_PARAMS = [ParamInfo("selectedCol", str, "Name of the selected column", default=None),
+                    ParamInfo("fieldDelimiter", str, "Field delimiter", default=None)]
+
+
+class JsonToColumnsBatchOp(MapBatchOp):
+    MAPPER = F.JsonToColumnsMapper
+    EXTRA_PARAMS = [ParamInfo("selectedCol", str, "Name of the selected column", default=None)]
+
+
+class KvToColumnsBatchOp(MapBatchOp):
+    MAPPER = F.KvToColumnsMapper
+    EXTRA_PARAMS = [ParamInfo("selectedCol", str, "Name of the selected column", default=None),
+                    ParamInfo("colDelimiter", str, "Delimiter between key-value pairs", default=None),
+                    ParamInfo("valDelimiter", str, "Delimiter between key and value", default=None)]
+
+
+class JsonValueBatchOp(MapBatchOp):
+    """``jsonPath`` extraction into string columns (``JsonValueBatchOp`` / ``JsonPathMapper.java``)."""
+    MAPPER = F.JsonPathMapper
+
+
+def _make(name, base, attrs):
+    cls = type(name, (base,), dict(attrs, __module__=__name__,
+                                   __doc__=f"{name}: " + ", ".join(f"{k}={v}" for k, v in attrs.items())))
+    globals()[name] = cls
+    __all__.append(name)
+    return cls
+
+
+for _f in FORMATS:
+    for _t in FORMATS:
+        if _f == _t or (_f, _t) in (("Csv", "Columns"), ("Json", "Columns"), ("Kv", "Columns"), ("Vector", "Columns")):
+            continue
+        _make(f"{_f}To{_t}BatchOp", BaseFormatTransBatchOp, {"FROM": _f.upper(), "TO": _t.upper()})
+    _make(f"{_f}ToTripleBatchOp", AnyToTripleBatchOp, {"FROM": _f.upper()})
+    _make(f"TripleTo{_f}BatchOp", TripleToAnyBatchOp, {"TO": _f.upper()})

@@ -8,3 +8,4 @@ from .sql import *  # noqa: F401,F403
 from .dataproc import *  # noqa: F401,F403
 from .evaluation import *  # noqa: F401,F403
 from .onlinelearning import *  # noqa: F401,F403
+from .format import *  # noqa: F401,F403

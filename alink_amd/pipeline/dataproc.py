@@ -1,4 +1,5 @@
 """Data-processing pipeline stages (reference ``A/pipeline/dataproc/**``)."""
+from ..common.params import ParamInfo
 from ..models.dataproc import vector as V
 from .base import MapTransformer
 
@@ -36,3 +37,6 @@ class VectorSizeHint(MapTransformer):
 
 class VectorToColumns(MapTransformer):
     MAPPER = V.VectorToColumnsMapper
+    EXTRA_PARAMS = [ParamInfo("vectorCol", str, "Name of a vector column", default=None),
+                    ParamInfo("schemaStr", str, "Formatted schema", default=None),
+                    ParamInfo("handleInvalid", str, "Strategy to handle unseen token", default="ERROR")]

@@ -1,0 +1,108 @@
+"""Format conversion ops (Columns/CSV/JSON/KV/Vector/Triple), JsonValue and the string-to-columns parsers,
+checked against the reference docs (docs/en/columnstokvbatchop.md, jsonvaluebatchop.md,
+tripletojsonbatchop.md, jsontovectorbatchop.md) and Java HashMap iteration order."""
+import json
+
+import pytest
+
+from alink_amd import *  # noqa: F401,F403
+from alink_amd.common.javafmt import java_hashmap_order
+from alink_amd.models.dataproc.format import json_path_read, lenient_json_loads
+
+ROWS = [('1', '{"f1":"1.0","f2":"2.0"}', '$3$1:1.0 2:2.0', '1:1.0,2:2.0', '1.0,2.0', 1.0, 2.0),
+        ('2', '{"f2":"4.0","f4":"8.0"}', '$3$1:4.0 2:8.0', '1:4.0,2:8.0', '4.0,8.0', 4.0, 8.0)]
+SCHEMA = "row string, json string, vec string, kv string, csv string, f0 double, f1 double"
+
+
+def _data():
+    return MemSourceBatchOp(ROWS, SCHEMA)
+
+
+def test_columns_to_kv_doc():
+    out = ColumnsToKvBatchOp().setSelectedCols(["f0", "f1"]).setReservedCols(["row"]).setKvCol("kv") \
+        .linkFrom(_data()).collect()
+    assert [tuple(r) for r in out] == [("1", "f0:1.0,f1:2.0"), ("2", "f0:4.0,f1:8.0")]
+
+
+def test_columns_to_json_and_back():
+    js = ColumnsToJsonBatchOp().setSelectedCols(["f0", "f1"]).setReservedCols(["row"]).setJsonCol("j") \
+        .linkFrom(_data())
+    assert [r[1] for r in js.collect()] == ['{"f0":"1.0","f1":"2.0"}', '{"f0":"4.0","f1":"8.0"}']
+    back = JsonToColumnsBatchOp().setJsonCol("j").setSchemaStr("f0 double, f1 double").setReservedCols(["row"]) \
+        .linkFrom(js).collect()
+    assert [tuple(r) for r in back] == [("1", 1.0, 2.0), ("2", 4.0, 8.0)]
+
+
+def test_json_to_vector_doc():
+    src = MemSourceBatchOp([('1', '{"1":"1.0","2":"2.0"}'), ('2', '{"2":"4.0","4":"8.0"}')], "row string, json string")
+    out = JsonToVectorBatchOp().setJsonCol("json").setReservedCols(["row"]).setVectorCol("vec").setVectorSize(5) \
+        .linkFrom(src).collect()
+    assert [r[1] for r in out] == ["$5$1:1.0 2:2.0", "$5$2:4.0 4:8.0"]
+
+
+def test_columns_to_vector_and_csv():
+    out = ColumnsToVectorBatchOp().setSelectedCols(["f0", "f1"]).setVectorCol("v").setReservedCols(["row"]) \
+        .linkFrom(_data()).collect()
+    assert [r[1] for r in out] == ["1.0 2.0", "4.0 8.0"]
+    out = ColumnsToCsvBatchOp().setSelectedCols(["f0", "f1"]).setSchemaStr("f0 double, f1 double").setCsvCol("c") \
+        .setReservedCols(["row"]).linkFrom(_data()).collect()
+    assert [r[1] for r in out] == ["1.0,2.0", "4.0,8.0"]
+
+
+def test_vector_to_columns_format_flavour():
+    out = VectorToColumnsBatchOp().setVectorCol("vec").setSchemaStr("f0 double, f1 double, f2 double") \
+        .setReservedCols(["row"]).linkFrom(_data()).collect()
+    assert [tuple(r) for r in out] == [("1", 0.0, 1.0, 2.0), ("2", 0.0, 4.0, 8.0)]
+
+
+def test_csv_kv_to_columns():
+    out = CsvToColumnsBatchOp().setCsvCol("csv").setSchemaStr("a double, b double").setReservedCols(["row"]) \
+        .linkFrom(_data()).collect()
+    assert [tuple(r) for r in out] == [("1", 1.0, 2.0), ("2", 4.0, 8.0)]
+    out = KvToColumnsBatchOp().setKvCol("kv").setSchemaStr("1 double, 2 double").setReservedCols(["row"]) \
+        .linkFrom(_data()).collect()
+    assert [tuple(r) for r in out] == [("1", 1.0, 2.0), ("2", 4.0, 8.0)]
+
+
+def test_triple_round_trip():
+    t = MemSourceBatchOp([(1.0, 'f1', 1.0), (1.0, 'f2', 2.0), (2.0, 'f1', 4.0), (2.0, 'f2', 8.0)],
+                         "row double, col string, val double")
+    out = TripleToJsonBatchOp().setTripleRowCol("row").setTripleColCol("col").setTripleValCol("val") \
+        .setJsonCol("json").linkFrom(t).collect()
+    assert [tuple(r) for r in out] == [(1.0, '{"f1":"1.0","f2":"2.0"}'), (2.0, '{"f1":"4.0","f2":"8.0"}')]
+    cols = TripleToColumnsBatchOp().setTripleRowCol("row").setTripleColCol("col").setTripleValCol("val") \
+        .setSchemaStr("f1 double, f2 double").linkFrom(t).collect()
+    assert [tuple(r) for r in cols] == [(1.0, 1.0, 2.0), (2.0, 4.0, 8.0)]
+    trip = ColumnsToTripleBatchOp().setSelectedCols(["f0", "f1"]).setReservedCols(["row"]) \
+        .setTripleColValSchemaStr("col string, val double").linkFrom(_data()).collect()
+    assert [tuple(r) for r in trip] == [("1", "f0", 1.0), ("1", "f1", 2.0), ("2", "f0", 4.0), ("2", "f1", 8.0)]
+
+
+def test_json_value_doc_lenient_json():
+    j = MemSourceBatchOp([("{a:boy,b:{b1:1,b2:2}}",), ("{a:girl,b:{b1:1,b2:2}}",)], "str string")
+    out = JsonValueBatchOp().setJsonPath(["$.a", "$.b.b1"]).setSelectedCol("str").setOutputCols(["f0", "f1"]) \
+        .linkFrom(j).collect()
+    assert [tuple(r) for r in out] == [("{a:boy,b:{b1:1,b2:2}}", "boy", "1"), ("{a:girl,b:{b1:1,b2:2}}", "girl", "1")]
+    assert json_path_read(lenient_json_loads('{"a":[1,{"x":"y"}]}'), "$.a[1].x") == "y"
+    assert json_path_read({"a": [1, 2]}, "$.a[*]") == [1, 2]
+
+
+def test_hashmap_order_in_kv_writer():
+    # 17 keys forces a resize (cap 32); order must follow java.util.HashMap bucket order, not insertion
+    keys = [f"k{i}" for i in range(17)]
+    row = tuple(float(i) for i in range(17))
+    src = MemSourceBatchOp([row], ", ".join(f"{k} double" for k in keys))
+    kv = ColumnsToKvBatchOp().setSelectedCols(keys).setKvCol("kv").setReservedCols([]).linkFrom(src).collect()[0][0]
+    assert [p.split(":")[0] for p in kv.split(",")] == java_hashmap_order(keys)
+
+
+def test_stream_and_pipeline_twins():
+    s = MemSourceStreamOp(ROWS, SCHEMA)
+    box = []
+    ColumnsToKvStreamOp().setSelectedCols(["f0", "f1"]).setReservedCols(["row"]).setKvCol("kv").linkFrom(s) \
+        .link(CollectStreamOp(box))
+    StreamOperator.execute()
+    assert [tuple(r) for r in box] == [("1", "f0:1.0,f1:2.0"), ("2", "f0:4.0,f1:8.0")]
+    p = Pipeline(ColumnsToKv().setSelectedCols(["f0", "f1"]).setKvCol("kv2"), Select("row, kv2"))
+    assert [tuple(r) for r in p.fit(_data()).transform(_data()).collect()] == \
+        [("1", "f0:1.0,f1:2.0"), ("2", "f0:4.0,f1:8.0")]
