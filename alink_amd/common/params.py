@@ -361,6 +361,19 @@ class WithParams(metaclass=ParamsMeta):
             key = self._param_infos[key]
         return self._params.get(key)
 
+    def resolvedParams(self) -> "Params":
+        """Copy of the params with every declared default filled in (string-keyed ``get`` then works)."""
+        out = self._params.clone()
+        for name, info in self._param_infos.items():
+            if not out.contains(name):
+                try:
+                    v = self._params.get(info)
+                except KeyError:
+                    continue
+                if v is not None:
+                    out.set(info, v)
+        return out
+
     @classmethod
     def paramInfos(cls) -> List[ParamInfo]:
         return list(cls._param_infos.values())

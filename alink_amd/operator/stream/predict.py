@@ -20,6 +20,8 @@ from ...models.nlp import text as _T
 from ...models.nlp import word2vec as _W
 from ...models.recommendation.als import AlsModelMapper
 from ...models.tree.model import GbdtModelMapper, RandomForestModelMapper
+from ...models.regression.glm import GlmModelMapper
+from ...models.regression.isotonic import IsotonicRegressionModelMapper
 from .base import MapStreamOp, ModelMapStreamOp
 
 _PREDICTORS = {
@@ -60,6 +62,8 @@ _PREDICTORS = {
     "BisectingKMeansPredictStreamOp": _BKM.BisectingKMeansModelMapper,
     "LdaPredictStreamOp": _LDA.LdaModelMapper,
     "MultilayerPerceptronPredictStreamOp": _MLP.MlpcModelMapper,
+    "GlmPredictStreamOp": GlmModelMapper,
+    "IsotonicRegPredictStreamOp": IsotonicRegressionModelMapper,
 }
 
 _MAPPERS = {

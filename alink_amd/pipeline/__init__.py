@@ -9,3 +9,4 @@ from .recommendation import *  # noqa: F401,F403
 from .nlp import *  # noqa: F401,F403
 from .classification_extra import *  # noqa: F401,F403
 from .format import *  # noqa: F401,F403
+from .regression_extra import *  # noqa: F401,F403
