@@ -7,7 +7,8 @@ from ...models.classification.naive_bayes import (NaiveBayesTextModelDataConvert
 from ..base import BatchOperator
 from .utils import ModelMapBatchOp
 
-__all__ = ["NaiveBayesTextTrainBatchOp", "NaiveBayesTextPredictBatchOp", "MultilayerPerceptronTrainBatchOp",
+__all__ = ["FmClassifierTrainBatchOp", "FmClassifierPredictBatchOp", "FmRegressorTrainBatchOp",
+           "FmRegressorPredictBatchOp", "NaiveBayesTextTrainBatchOp", "NaiveBayesTextPredictBatchOp", "MultilayerPerceptronTrainBatchOp",
            "MultilayerPerceptronPredictBatchOp"]
 
 
@@ -40,3 +41,41 @@ from ...models.classification.mlp import MlpcModelMapper  # noqa: E402
 
 class MultilayerPerceptronPredictBatchOp(ModelMapBatchOp):
     MAPPER = MlpcModelMapper
+
+
+from ...models.recommendation import fm as _FM  # noqa: E402
+
+
+class _FmTrainBatchOp(BatchOperator):
+    """``FmTrainBatchOp`` (task fixed by the subclass): device mini-batch AdaGrad + model averaging."""
+    TASK = "REGRESSION"
+    _NO_AUTO_PARAMS = True
+
+    def linkFrom(self, *inputs):
+        mt = self.checkAndGetFirst(inputs).getOutputTable()
+        m, lt, info = _FM.train_fm(mt, self.resolvedParams(), self.TASK, self.env)
+        self._train_info = info
+        conv = _FM.FmModelDataConverter(lt)
+        self.setOutputTable(MTable.from_rows(conv.save(m), conv.getModelSchema(), replicated=True))
+        return self
+
+    def getTrainInfo(self):
+        return getattr(self, "_train_info", None)
+
+
+class FmClassifierTrainBatchOp(_FmTrainBatchOp):
+    _NO_AUTO_PARAMS = False
+    TASK = "BINARY_CLASSIFICATION"
+
+
+class FmRegressorTrainBatchOp(_FmTrainBatchOp):
+    _NO_AUTO_PARAMS = False
+    TASK = "REGRESSION"
+
+
+class FmClassifierPredictBatchOp(ModelMapBatchOp):
+    MAPPER = _FM.FmModelMapper
+
+
+class FmRegressorPredictBatchOp(ModelMapBatchOp):
+    MAPPER = _FM.FmModelMapper

@@ -3,7 +3,7 @@ from ..models.classification.naive_bayes import NaiveBayesTextModelMapper
 from ..operator.batch import classification_extra as C
 from .base import MapModel, Trainer
 
-__all__ = ["NaiveBayesTextClassifier", "NaiveBayesTextModel", "MultilayerPerceptronClassifier",
+__all__ = ["FmClassifier", "FmRegressor", "FmModel", "NaiveBayesTextClassifier", "NaiveBayesTextModel", "MultilayerPerceptronClassifier",
            "MultilayerPerceptronClassificationModel"]
 
 
@@ -26,3 +26,20 @@ class MultilayerPerceptronClassifier(Trainer):
 
 class MultilayerPerceptronClassificationModel(MapModel):
     MAPPER = MlpcModelMapper
+
+
+from ..models.recommendation.fm import FmModelMapper  # noqa: E402
+
+
+class FmClassifier(Trainer):
+    TRAIN_OP = C.FmClassifierTrainBatchOp
+    MODEL = "FmModel"
+
+
+class FmRegressor(Trainer):
+    TRAIN_OP = C.FmRegressorTrainBatchOp
+    MODEL = "FmModel"
+
+
+class FmModel(MapModel):
+    MAPPER = FmModelMapper

@@ -120,5 +120,40 @@ def run(rank, world, port, scenario, outdir):
     comm.shutdown()
 
 
+def scenario_glm(out):
+    import json as _j
+    from alink_amd import useLocalEnv, BatchOperator, GlmTrainBatchOp
+    df = _data_frame()
+    useLocalEnv(1)
+    src = BatchOperator.fromDataframe(df, schemaStr="x0 double, x1 double, x2 double, x3 double, y int")
+    op = GlmTrainBatchOp().setFamily("binomial").setFeatureCols(["x0", "x1", "x2", "x3"]).setLabelCol("y")
+    model = src.link(op)
+    out["summary"] = _j.loads(model.getSideOutput(1).collect()[0][0])
+
+
+def scenario_isotonic(out):
+    import json as _j
+    from alink_amd import useLocalEnv, BatchOperator, IsotonicRegTrainBatchOp
+    df = _data_frame()
+    useLocalEnv(1)
+    src = BatchOperator.fromDataframe(df, schemaStr="x0 double, x1 double, x2 double, x3 double, y int")
+    rows = sorted(src.link(IsotonicRegTrainBatchOp().setFeatureCol("x1").setLabelCol("x0")).collect(),
+                  key=lambda r: r[0])
+    out["b"] = _j.loads(rows[1][1])
+    out["v"] = _j.loads(rows[2][1])
+
+
+def scenario_fm(out):
+    from alink_amd import useLocalEnv, BatchOperator, FmClassifierTrainBatchOp, FmClassifierPredictBatchOp
+    df = _data_frame()
+    useLocalEnv(1)
+    src = BatchOperator.fromDataframe(df, schemaStr="x0 double, x1 double, x2 double, x3 double, y int")
+    model = src.link(FmClassifierTrainBatchOp().setFeatureCols(["x0", "x1", "x2", "x3"]).setLabelCol("y")
+                     .setNumEpochs(20).setLearnRate(0.1).setNumFactor(2))
+    pred = FmClassifierPredictBatchOp().setPredictionCol("p").linkFrom(model, src).collect()
+    out["model"] = [list(r) for r in model.collect()]
+    out["acc"] = sum(int(r[-1] == r[-2]) for r in pred) / max(len(pred), 1)
+
+
 if __name__ == "__main__":
     run(int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), sys.argv[4], sys.argv[5])

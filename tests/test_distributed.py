@@ -102,3 +102,24 @@ def test_als_two_processes_equal_single(tmp_path):
     a = np.array([[float(x) for x in r[2].split()] for r in one])
     b = np.array([[float(x) for x in r[2].split()] for r in two[0]["model"]])
     np.testing.assert_allclose(a, b, rtol=1e-4, atol=1e-5)
+
+
+def test_glm_two_processes_equal_single(tmp_path):
+    one = _run("glm", 1, tmp_path)[0]["summary"]
+    two = _run("glm", 2, tmp_path)
+    assert two[0]["summary"] == two[1]["summary"]
+    np.testing.assert_allclose(one["coefficients"], two[0]["summary"]["coefficients"], rtol=1e-9)
+    np.testing.assert_allclose(one["deviance"], two[0]["summary"]["deviance"], rtol=1e-9)
+
+
+def test_isotonic_two_processes_equal_single(tmp_path):
+    one = _run("isotonic", 1, tmp_path)[0]
+    two = _run("isotonic", 2, tmp_path)
+    assert two[0]["b"] == two[1]["b"] == one["b"]
+    np.testing.assert_allclose(one["v"], two[0]["v"], rtol=1e-5, atol=1e-6)  # float32 block sums, as in the reference
+
+
+def test_fm_two_processes_model_averaging(tmp_path):
+    two = _run("fm", 2, tmp_path)
+    assert two[0]["model"] == two[1]["model"]
+    assert two[0]["acc"] > 0.8

@@ -1,0 +1,46 @@
+"""Factorization machine classifier / regressor: learns pairwise interactions, model round trip, stages,
+multi-process model averaging (gloo).  Parity unpinned: the reference ships no FM doc outputs."""
+import json
+
+import numpy as np
+
+from alink_amd import *  # noqa: F401,F403
+from alink_amd.models.recommendation.fm import FmModelDataConverter
+from alink_amd.common.types import Types
+
+
+def _data(n=1500, seed=0):
+    rng = np.random.default_rng(seed)
+    X = rng.normal(size=(n, 6))
+    return X
+
+
+def test_fm_regressor_learns_interaction():
+    X = _data()
+    y = 2 * X[:, 0] * X[:, 1] + X[:, 3]
+    src = MemSourceBatchOp([(" ".join(map(str, x)), float(t)) for x, t in zip(X.tolist(), y)], "vec string, y double")
+    m = FmRegressor().setVectorCol("vec").setLabelCol("y").setNumEpochs(50).setLearnRate(0.1).setNumFactor(4) \
+        .setPredictionCol("p").fit(src)
+    out = m.transform(src).collect()
+    rmse = np.sqrt(np.mean([(r[1] - r[2]) ** 2 for r in out]))
+    assert rmse < 0.1 * y.std()
+
+
+def test_fm_classifier_detail_and_model_format():
+    X = _data(seed=1)
+    logit = 3.0 * X[:, 0] * X[:, 1] - 2.0 * X[:, 2]
+    y = np.where(logit > 0, "b", "a")
+    src = MemSourceBatchOp([(float(a), float(b), float(c), str(t)) for (a, b, c), t in zip(X[:, :3].tolist(), y)],
+                           "f0 double, f1 double, f2 double, label string")
+    train = FmClassifierTrainBatchOp().setFeatureCols(["f0", "f1", "f2"]).setLabelCol("label") \
+        .setNumEpochs(60).setLearnRate(0.1).setNumFactor(4)
+    model = src.link(train)
+    pred = FmClassifierPredictBatchOp().setPredictionCol("p").setPredictionDetailCol("d").linkFrom(model, src) \
+        .collect()
+    acc = np.mean([r[4] == r[3] for r in pred])
+    assert acc > 0.9
+    d = json.loads(pred[0][5])
+    assert set(d) == {"a", "b"} and abs(float(d["a"]) + float(d["b"]) - 1) < 1e-12
+    m = FmModelDataConverter(Types.STRING).load(model.collect())
+    assert m.task == "BINARY_CLASSIFICATION" and m.labelValues[0] == "b" and m.dim == [1, 1, 4]
+    assert len(m.fmModel.factors) == 3 and len(m.fmModel.factors[0]) == 4
