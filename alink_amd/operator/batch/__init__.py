@@ -14,3 +14,4 @@ from .nlp import *  # noqa: F401,F403
 from .classification_extra import *  # noqa: F401,F403
 from .format import *  # noqa: F401,F403
 from .regression_extra import *  # noqa: F401,F403
+from .mining import *  # noqa: F401,F403
