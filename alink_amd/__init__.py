@@ -11,6 +11,7 @@ from .common.params import Params, ParamInfo  # noqa: F401
 from .common.linalg import DenseVector, SparseVector, VectorUtil, DenseMatrix  # noqa: F401
 from .common.table import MTable, Row  # noqa: F401
 from .common.types import TableSchema, Types  # noqa: F401
+from .operator.common.io.db import BaseDB, SqliteDB, DerbyDB, MySqlDB, JdbcDB  # noqa: F401
 from .operator.base import BatchOperator  # noqa: F401
 from .operator.batch import *  # noqa: F401,F403
 from .operator.stream import *  # noqa: F401,F403

@@ -15,3 +15,4 @@ from .classification_extra import *  # noqa: F401,F403
 from .format import *  # noqa: F401,F403
 from .regression_extra import *  # noqa: F401,F403
 from .mining import *  # noqa: F401,F403
+from .db import *  # noqa: F401,F403

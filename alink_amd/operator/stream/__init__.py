@@ -9,3 +9,4 @@ from .dataproc import *  # noqa: F401,F403
 from .evaluation import *  # noqa: F401,F403
 from .onlinelearning import *  # noqa: F401,F403
 from .format import *  # noqa: F401,F403
+from .db import *  # noqa: F401,F403

@@ -56,3 +56,113 @@ class UnionAllStreamOp(StreamOperator):
     def on_batch(self, port, mt):
         from ...common.table import MTable
         self._emit(MTable(self._schema, mt.cols, mt.replicated))
+
+
+# ---------------------------------------------------------------------------------------------------
+# windowed group-by (StreamSqlOperators.windowGroupBy: GROUP BY TUMBLE/HOP/SESSION(proctime, ...), keys)
+# ---------------------------------------------------------------------------------------------------
+import math as _math  # noqa: E402
+import time as _time  # noqa: E402
+
+from ...common.params import ParamInfo  # noqa: E402
+from ...common.table import Column as _Column, MTable as _MTable  # noqa: E402
+
+_UNIT_S = {"SECOND": 1, "MINUTE": 60, "HOUR": 3600, "DAY": 86400, "MONTH": 2592000, "YEAR": 31536000}
+
+
+class WindowGroupByStreamOp(StreamOperator):
+    """Aggregates rows per time window and ``groupByClause`` key; emits each window when it closes (or at
+    end of stream).  Time is the micro-batch arrival time (Flink ``proctime``) unless ``timeCol`` names an
+    event-time column in seconds."""
+    EXTRA_PARAMS = [ParamInfo("timeCol", str, "event-time column (seconds); processing time if null",
+                              default=None)]
+
+    def __init__(self, params: Optional[Params] = None, **kw):
+        super().__init__(params, **kw)
+        self._pending = []          # (t, row)
+        self._watermark = -_math.inf
+
+    def _unit(self):
+        u = self.getIntervalUnit()
+        return _UNIT_S[getattr(u, "name", str(u)).upper()]
+
+    def _kind(self):
+        w = self.getWindowType()
+        return getattr(w, "name", str(w)).upper()
+
+    def linkFrom(self, *inputs):
+        (inp,) = self._connect(*inputs)
+        self._in_schema = inp.getSchema()
+        self._schema = self._aggregate(_MTable.empty(self._in_schema)).schema
+        return self
+
+    def _aggregate(self, mt):
+        by = self.getGroupByClause()
+        if by and by.strip():
+            return E.sql_group_by(mt, by, self.getSelectClause())
+        from ...common.types import Types as _T
+        k = mt.with_columns(["__w"], [_T.INT], [_Column.from_values([0] * mt.num_rows, _T.INT)])
+        return E.sql_group_by(k, "__w", self.getSelectClause())
+
+    def _windows(self, t):
+        L = float(self.getWindowLength() or 0) * self._unit()
+        kind = self._kind()
+        if kind == "HOP":
+            S = float(self.getSlidingLength()) * self._unit()
+            first = _math.floor((t - L) / S) + 1
+            return [(k * S, k * S + L) for k in range(first, _math.floor(t / S) + 1)]
+        return [(_math.floor(t / L) * L, _math.floor(t / L) * L + L)]
+
+    def _flush(self, final=False):
+        if not self._pending:
+            return
+        kind = self._kind()
+        if kind == "SESSION":
+            gap = float(self.getSessionGap()) * self._unit()
+            self._pending.sort(key=lambda x: x[0])
+            sessions, cur = [], [self._pending[0]]
+            for t, r in self._pending[1:]:
+                if t - cur[-1][0] > gap:
+                    sessions.append(cur)
+                    cur = []
+                cur.append((t, r))
+            keep = []
+            if not final and cur and self._watermark - cur[-1][0] <= gap:
+                keep = cur
+            else:
+                sessions.append(cur)
+            for s in sessions:
+                self._emit(self._aggregate(_MTable.from_rows([r for _, r in s], self._in_schema)))
+            self._pending = keep
+            return
+        buckets = {}
+        for t, r in self._pending:
+            for w in self._windows(t):
+                buckets.setdefault(w, []).append((t, r))
+        remaining = {}
+        for w in sorted(buckets):
+            if final or w[1] <= self._watermark:
+                self._emit(self._aggregate(_MTable.from_rows([r for _, r in buckets[w]], self._in_schema)))
+            else:
+                for item in buckets[w]:
+                    remaining[id(item[1])] = item
+        self._pending = list(remaining.values())
+
+    def on_batch(self, port, mt):
+        tc = self.getTimeCol()
+        if tc:
+            ts = [float(x) for x in mt.col(tc).to_list()]
+        else:
+            now = _time.time()
+            ts = [now] * mt.num_rows
+        rows = mt.rows()
+        self._pending.extend(zip(ts, rows))
+        if ts:
+            self._watermark = max(self._watermark, max(ts))
+        self._flush(False)
+
+    def on_finish(self, port):
+        self._flush(True)
+
+
+__all__.append("WindowGroupByStreamOp")

@@ -23,7 +23,7 @@ from ..common.table import MTable, Row
 from ..common.types import TableSchema, Types, schema_str_to_schema, schema_to_schema_str
 from ..operator.base import BatchOperator, gather_table
 
-__all__ = ["PipelineStageBase", "EstimatorBase", "TransformerBase", "ModelBase", "Trainer", "MapTransformer",
+__all__ = ["ModelExporterUtils", "PipelineStageBase", "EstimatorBase", "TransformerBase", "ModelBase", "Trainer", "MapTransformer",
            "MapModel", "Pipeline", "PipelineModel", "LocalPredictor", "STAGE_REGISTRY", "register_stage",
            "PIPELINE_MODEL_SCHEMA"]
 
@@ -441,3 +441,11 @@ def unpack_transformers(rows) -> List[TransformerBase]:
             t.setModelData(MTable.from_rows(mrows, schema, replicated=True))
         out.append(t)
     return out
+
+
+class ModelExporterUtils:
+    """``ModelExporterUtils.java`` — pack pipeline stages into / unpack them from the one-table pipeline model
+    format (``(model_id, model_data)`` with the ``-1`` config row and ``^``-delimited per-stage rows)."""
+    packTransformersArray = staticmethod(pack_transformers)
+    packRows = staticmethod(pack_rows)
+    unpackTransformersArray = staticmethod(unpack_transformers)

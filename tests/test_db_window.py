@@ -1,0 +1,46 @@
+"""DB sources/sinks on the embedded SQLite engine (reference DerbyDB / JdbcDB role), the JDBC retract
+(upsert) sink, and WindowGroupByStreamOp (TUMBLE / HOP / SESSION over an event-time column)."""
+import os
+
+from alink_amd import *  # noqa: F401,F403
+
+
+def test_db_batch_and_stream_round_trip(tmp_path):
+    db = SqliteDB(os.path.join(str(tmp_path), "t.db"))
+    src = MemSourceBatchOp([(1, "a", 1.5), (2, "b", 2.5)], "id bigint, name string, v double")
+    src.link(DBSinkBatchOp(db, "tbl"))
+    assert db.listTableNames() == ["tbl"]
+    assert [tuple(r) for r in DBSourceBatchOp(db, "tbl").collect()] == [(1, "a", 1.5), (2, "b", 2.5)]
+    MemSourceStreamOp([(1, "x", 9.0), (3, "c", 3.5)], "id bigint, name string, v double") \
+        .link(JdbcRetractSinkStreamOp(db, "up", ["id"]))
+    StreamOperator.execute()
+    MemSourceStreamOp([(1, "y", 10.0)], "id bigint, name string, v double") \
+        .link(JdbcRetractSinkStreamOp(db, "up", ["id"]))
+    StreamOperator.execute()
+    assert sorted(tuple(r) for r in DBSourceBatchOp(db, "up").collect()) == [(1, "y", 10.0), (3, "c", 3.5)]
+    box = []
+    DBSourceStreamOp(db, "tbl").link(CollectStreamOp(box))
+    StreamOperator.execute()
+    assert [tuple(r) for r in box] == [(1, "a", 1.5), (2, "b", 2.5)]
+
+
+ROWS = [(0.5, "a", 1.0), (1.2, "a", 2.0), (1.7, "b", 3.0), (2.1, "a", 4.0), (4.0, "b", 5.0)]
+
+
+def _run(op):
+    box = []
+    op.linkFrom(MemSourceStreamOp(ROWS, "ts double, k string, v double")).link(CollectStreamOp(box))
+    StreamOperator.execute()
+    return [tuple(r) for r in box]
+
+
+def test_window_group_by():
+    tumble = _run(WindowGroupByStreamOp().setTimeCol("ts").setWindowLength(1)
+                  .setSelectClause("k, SUM(v) AS s, COUNT(*) AS c").setGroupByClause("k"))
+    assert tumble == [("a", 1.0, 1), ("a", 2.0, 1), ("b", 3.0, 1), ("a", 4.0, 1), ("b", 5.0, 1)]
+    session = _run(WindowGroupByStreamOp().setTimeCol("ts").setWindowType("SESSION").setSessionGap(1)
+                   .setSelectClause("SUM(v) AS s"))
+    assert session == [(10.0,), (5.0,)]
+    hop = _run(WindowGroupByStreamOp().setTimeCol("ts").setWindowType("HOP").setWindowLength(2)
+               .setSlidingLength(1).setSelectClause("SUM(v) AS s"))
+    assert hop == [(1.0,), (6.0,), (9.0,), (4.0,), (5.0,), (5.0,)]
