@@ -16,3 +16,4 @@ from .operator.base import BatchOperator  # noqa: F401
 from .operator.batch import *  # noqa: F401,F403
 from .operator.stream import *  # noqa: F401,F403
 from .pipeline import *  # noqa: F401,F403
+from .connectors import *  # noqa: F401,F403

@@ -44,3 +44,24 @@ def test_window_group_by():
     hop = _run(WindowGroupByStreamOp().setTimeCol("ts").setWindowType("HOP").setWindowLength(2)
                .setSlidingLength(1).setSelectClause("SUM(v) AS s"))
     assert hop == [(1.0,), (6.0,), (9.0,), (4.0,), (5.0,), (5.0,)]
+
+
+def test_kafka_file_broker_and_hive_local_warehouse(tmp_path):
+    broker = "file://" + str(tmp_path / "kafka")
+    MemSourceStreamOp([(1, "a", 1.5), (2, "b", 2.5)], "id bigint, name string, v double") \
+        .link(KafkaSinkStreamOp().setBootstrapServers(broker).setTopic("t1"))
+    StreamOperator.execute()
+    box = []
+    KafkaSourceStreamOp().setBootstrapServers(broker).setTopic("t1").setStartupMode("EARLIEST") \
+        .link(CollectStreamOp(box))
+    StreamOperator.execute()
+    assert [tuple(r) for r in box] == [(None, '{"id":1,"name":"a","v":1.5}', "t1", 0, 0),
+                                       (None, '{"id":2,"name":"b","v":2.5}', "t1", 0, 1)]
+    wh = "file://" + str(tmp_path / "hive")
+    MemSourceBatchOp([(1, "a")], "id bigint, s string").link(
+        HiveSinkBatchOp().setHiveConfDir(wh).setOutputTableName("ht").setPartition("ds=1"))
+    MemSourceBatchOp([(2, "b")], "id bigint, s string").link(
+        HiveSinkBatchOp().setHiveConfDir(wh).setOutputTableName("ht").setPartition("ds=2"))
+    assert [tuple(r) for r in HiveSourceBatchOp().setHiveConfDir(wh).setInputTableName("ht")
+            .setPartitions("ds=2").collect()] == [(2, "b")]
+    assert len(HiveSourceBatchOp().setHiveConfDir(wh).setInputTableName("ht").collect()) == 2
