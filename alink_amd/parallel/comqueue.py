@@ -15,9 +15,24 @@ locally and no broadcast is needed.
 
 Observability: per-superstep wall time and collective bytes are recorded in ``queue.stats``; optional
 ``on_step`` callbacks and a ``roctx`` range per superstep when running on ROCm.
+
+Fault tolerance (the reference has none: ComQueue state lives in the JVM heap and any failure restarts the
+job):
+* ``setCheckpoint(dir, every)`` — after every ``every``-th superstep each rank atomically writes its task
+  state (everything except the partitioned/broadcast inputs, which are rebuilt from the DAG) plus the
+  picklable state of the queue items and criterion; ``exec`` resumes from the newest step ALL ranks have
+  (agreed with one MIN all-reduce), so a killed job restarts at a superstep boundary;
+* ``setWatchdog(seconds)`` — a superstep (its collectives included) that exceeds the limit dumps every
+  thread's stack and terminates the process instead of hanging the job (a stuck RCCL peer);
+* fault injection for tests: ``ALINK_FAULT_INJECT="<rank>:<step>"`` raises ``InjectedFault`` on that rank
+  at the start of that superstep.
 """
 from __future__ import annotations
 
+import faulthandler
+import os
+import pickle
+import sys
 import time
 from typing import Any, Callable, Dict, List, Optional, Sequence
 
@@ -26,11 +41,47 @@ import torch
 
 from . import comm
 
-__all__ = ["ComContext", "ComputeFunction", "CommunicateFunction", "CompareCriterionFunction",
+__all__ = ["InjectedFault", "ComContext", "ComputeFunction", "CommunicateFunction", "CompareCriterionFunction",
            "CompleteResultFunction", "AllReduce", "BaseComQueue", "IterativeComQueue", "ComQueue",
            "ChainedComputation", "AllGather", "Broadcast", "SUM", "MAX", "MIN"]
 
 SUM, MAX, MIN = "sum", "max", "min"
+
+
+class InjectedFault(RuntimeError):
+    """Raised by the ``ALINK_FAULT_INJECT`` hook (tests of checkpoint/resume)."""
+
+
+def _picklable(v) -> bool:
+    try:
+        pickle.dumps(v)
+        return True
+    except Exception:  # noqa: BLE001
+        return False
+
+
+def _to_cpu(v):
+    if isinstance(v, torch.Tensor):
+        return v.detach().cpu()
+    if isinstance(v, list):
+        return [_to_cpu(x) for x in v]
+    if isinstance(v, tuple):
+        return tuple(_to_cpu(x) for x in v)
+    if isinstance(v, dict):
+        return {k: _to_cpu(x) for k, x in v.items()}
+    return v
+
+
+def _to_dev(v, dev):
+    if isinstance(v, torch.Tensor):
+        return v.to(dev)
+    if isinstance(v, list):
+        return [_to_dev(x, dev) for x in v]
+    if isinstance(v, tuple):
+        return tuple(_to_dev(x, dev) for x in v)
+    if isinstance(v, dict):
+        return {k: _to_dev(x, dev) for k, x in v.items()}
+    return v
 
 
 class ComContext:
@@ -216,6 +267,60 @@ class BaseComQueue:
         self.env = None
         self.device = None
         self.sync_device_per_step = False
+        self.ckpt_dir: Optional[str] = None
+        self.ckpt_every = 1
+        self.watchdog_s: Optional[float] = None
+        self.resumed_from = 0
+
+    # ---- fault tolerance ----
+    def setCheckpoint(self, directory: str, every: int = 1):
+        self.ckpt_dir, self.ckpt_every = directory, max(1, int(every))
+        return self
+
+    def setWatchdog(self, seconds: float):
+        self.watchdog_s = float(seconds)
+        return self
+
+    def _ckpt_file(self, rank: int, step: int) -> str:
+        return os.path.join(self.ckpt_dir, f"rank{rank}", f"step{step:08d}.pt")
+
+    def _item_states(self, items):
+        out = []
+        for it in list(items) + [self.criterion]:
+            st = {k: _to_cpu(v) for k, v in getattr(it, "__dict__", {}).items() if _picklable(_to_cpu(v))}
+            out.append(st)
+        return out
+
+    def _save_checkpoint(self, rank, stores, items, skip):
+        state = {"step": self.step_no,
+                 "stores": [{k: _to_cpu(v) for k, v in st.items() if k not in skip and _picklable(_to_cpu(v))}
+                            for st in stores],
+                 "items": self._item_states(items)}
+        path = self._ckpt_file(rank, self.step_no)
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        tmp = path + ".tmp"
+        torch.save(state, tmp)
+        os.replace(tmp, path)
+        for old in os.listdir(os.path.dirname(path)):      # keep the newest two
+            full = os.path.join(os.path.dirname(path), old)
+            if old.endswith(".pt") and full < self._ckpt_file(rank, self.step_no - self.ckpt_every):
+                os.remove(full)
+
+    def _try_resume(self, rank, stores, items) -> int:
+        d = os.path.join(self.ckpt_dir, f"rank{rank}")
+        steps = sorted(int(f[4:12]) for f in os.listdir(d) if f.endswith(".pt")) if os.path.isdir(d) else []
+        mine = torch.tensor([float(steps[-1]) if steps else 0.0], dtype=torch.float64)
+        comm.all_reduce(mine, MIN)
+        step = int(mine.item())
+        if step <= 0 or step not in steps:
+            return 0
+        state = torch.load(self._ckpt_file(rank, step), map_location="cpu", weights_only=False)
+        for st, saved in zip(stores, state["stores"]):
+            st.update(_to_dev(saved, self.device))
+        for it, saved in zip(list(items) + [self.criterion], state["items"]):
+            if it is not None:
+                it.__dict__.update(_to_dev(saved, self.device))
+        return step
 
     # ---- builder API (names as in the reference) ----
     def initWithPartitionedData(self, name: str, data):
@@ -291,11 +396,21 @@ class BaseComQueue:
             for s in stores:
                 s[name] = full
         items = self.optimize()
-        use_roctx = self.device is not None and self.device.type == "cuda" and hasattr(torch.cuda, "nvtx")
         self.step_no = 0
+        if self.ckpt_dir is not None:
+            self.resumed_from = self._try_resume(env.rank, stores, items)
+        inject = os.environ.get("ALINK_FAULT_INJECT")
+        inject = tuple(int(x) for x in inject.split(":")) if inject else None
+        skip = {n for n, _ in self.partitioned} | {n for n, _ in self.broadcast}
+        use_roctx = self.device is not None and self.device.type == "cuda" and hasattr(torch.cuda, "nvtx")
+        self.step_no = self.resumed_from
         stop = False
         while not stop and self.step_no < self.max_iter:
             self.step_no += 1
+            if inject is not None and inject == (env.rank, self.step_no):
+                raise InjectedFault(f"injected fault on rank {env.rank} at superstep {self.step_no}")
+            if self.watchdog_s is not None:
+                faulthandler.dump_traceback_later(self.watchdog_s, exit=True, file=sys.stderr)
             t0 = time.perf_counter()
             b0 = comm.STATS.bytes
             if use_roctx:
@@ -320,8 +435,12 @@ class BaseComQueue:
                 torch.cuda.nvtx.range_pop()
             if self.sync_device_per_step and self.device is not None and self.device.type == "cuda":
                 torch.cuda.synchronize(self.device)
+            if self.watchdog_s is not None:
+                faulthandler.cancel_dump_traceback_later()
             self.stats.append({"step": self.step_no, "wall_s": time.perf_counter() - t0,
                                "comm_bytes": comm.STATS.bytes - b0})
+            if self.ckpt_dir is not None and (self.step_no % self.ckpt_every == 0 or stop):
+                self._save_checkpoint(env.rank, stores, items, skip)
             for fn in self.on_step:
                 fn(self.step_no, self)
         result: List = []

@@ -1,0 +1,80 @@
+"""Superstep checkpoint / resume, injected faults and the watchdog of the BSP engine (the
+reference has none of these)."""
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+from alink_amd import useLocalEnv
+from alink_amd.parallel.comqueue import (AllReduce, CompareCriterionFunction, CompleteResultFunction,
+                                         ComputeFunction, InjectedFault, IterativeComQueue)
+
+
+class Step(ComputeFunction):
+    def __init__(self):
+        self.calls = 0
+
+    def calc(self, ctx):
+        self.calls += 1
+        x = ctx.getObj("x")
+        if x is None:
+            x = torch.zeros(3, dtype=torch.float64)
+        data = ctx.getObj("data")
+        ctx.putObj("x", x + data.sum() * ctx.getStepNo())
+        ctx.putObj("buf", torch.ones(2, dtype=torch.float64) * ctx.getStepNo())
+
+
+class Stop(CompareCriterionFunction):
+    def __init__(self):
+        self.seen = []
+
+    def calc(self, ctx):
+        self.seen.append(ctx.getStepNo())
+        return False
+
+
+class Out(CompleteResultFunction):
+    def calc(self, ctx):
+        return [tuple(ctx.getObj("x").tolist()) + tuple(ctx.getObj("buf").tolist())]
+
+
+def _queue(ckpt=None):
+    q = IterativeComQueue().initWithPartitionedData("data", torch.arange(10, dtype=torch.float64)) \
+        .add(Step()).add(AllReduce("buf")).setCompareCriterionOfNode0(Stop()).closeWith(Out()).setMaxIter(6)
+    if ckpt:
+        q.setCheckpoint(ckpt, every=1)
+    return q
+
+
+def test_checkpoint_resume_after_injected_fault(tmp_path, monkeypatch):
+    useLocalEnv(1, device="cpu")
+    ref = _queue().exec()
+    ck = str(tmp_path / "ck")
+    monkeypatch.setenv("ALINK_FAULT_INJECT", "0:4")
+    with pytest.raises(InjectedFault):
+        _queue(ck).exec()
+    monkeypatch.delenv("ALINK_FAULT_INJECT")
+    q = _queue(ck)
+    res = q.exec()
+    assert q.resumed_from == 3
+    assert res == ref
+    assert q.criterion.seen == [1, 2, 3, 4, 5, 6]      # criterion state restored with the checkpoint
+    assert os.listdir(os.path.join(ck, "rank0"))
+
+
+def test_watchdog_terminates_hung_superstep(tmp_path):
+    code = (
+        "import time, torch\n"
+        "from alink_amd import useLocalEnv\n"
+        "from alink_amd.parallel.comqueue import IterativeComQueue, ComputeFunction\n"
+        "useLocalEnv(1, device='cpu')\n"
+        "class Hang(ComputeFunction):\n"
+        "    def calc(self, ctx):\n"
+        "        time.sleep(30)\n"
+        "IterativeComQueue().add(Hang()).setMaxIter(1).setWatchdog(1.0).exec()\n")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True, timeout=60)
+    assert p.returncode != 0
+    assert "Timeout" in p.stderr or "Thread" in p.stderr
