@@ -308,6 +308,12 @@ class UnaryLossObjFunc(OptimObjFunc):
         return self.unary.loss(data.X.mv(coef), data.y)
 
     def grad_sum(self, data, coef):
+        from ...ops import _lib, linear as lops
+        X = data.X.dense
+        code = lops.loss_code(self.unary)
+        if code is not None and lops.hip_linear_supported(X) and (_lib.available()
+                                                                  or not _lib.torch_fallback_allowed()):
+            return lops.linear_grad_hip(X, data.y, data.w, coef, code[0], code[1])[0]   # one pass over X
         eta = data.X.mv(coef)
         return data.X.rmv(data.w * self.unary.derivative(eta, data.y), coef.shape[0])
 

@@ -1,0 +1,73 @@
+"""Linear-model hot path: fused one-pass loss gradient (kernel K12) — ``csrc/linear.hip``.
+
+``linear_grad(X, y, w, coef, loss)`` returns ``(sum_i w_i l'(x_i.coef, y_i) x_i, sum_i w_i l(.), sum_i w_i)``
+with ONE read of the dense fp64 shard (the torch form reads it twice: ``X @ coef`` then ``X^T g``).
+"""
+from __future__ import annotations
+
+from typing import Dict, Optional, Tuple
+
+import torch
+
+from . import _lib
+
+__all__ = ["linear_grad_hip", "loss_code", "hip_linear_supported"]
+
+_SLABS: Dict[Tuple, torch.Tensor] = {}
+
+
+def loss_code(unary) -> Optional[Tuple[int, float]]:
+    from ..models.linear import objfunc as O
+    t = type(unary)
+    if t is O.LogLossFunc:
+        return 0, 0.0
+    if t is O.LogisticLossFunc:
+        return 1, 0.0
+    if t is O.SquareLossFunc:
+        return 2, 0.0
+    if t is O.HingeLossFunc:
+        return 3, 0.0
+    if t is O.SmoothHingeLossFunc:
+        return 4, 0.0
+    if t is O.PerceptronLossFunc:
+        return 5, 0.0
+    if t is O.ExponentialLossFunc:
+        return 6, 0.0
+    if t is O.HuberLossFunc:
+        return 7, unary.delta
+    if t is O.SvrLossFunc:
+        return 8, unary.epsilon
+    return None
+
+
+def hip_linear_supported(X: torch.Tensor) -> bool:
+    return (X is not None and X.is_cuda and X.dtype == torch.float64 and X.dim() == 2 and 0 < X.shape[1] <= 64
+            and X.shape[0] > 0 and X.is_contiguous())
+
+
+def linear_grad_hip(X: torch.Tensor, y: torch.Tensor, w: torch.Tensor, coef: torch.Tensor, code: int,
+                    prm: float = 0.0) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    L = _lib.require()
+    if not hip_linear_supported(X):
+        raise ValueError("linear_grad_hip needs a contiguous fp64 [n, d<=64] CUDA tensor")
+    n, d = X.shape
+    dev = X.device
+    y = y.to(device=dev, dtype=torch.float64).contiguous()
+    w = w.to(device=dev, dtype=torch.float64).contiguous()
+    c = coef[:d].to(device=dev, dtype=torch.float64).contiguous()
+    if y.shape[0] != n or w.shape[0] != n:
+        raise ValueError("label / weight length mismatch")
+    pad = int(L.alink_linear_grad_pad(d))
+    nblk = max(1, min((n + 255) // 256, 2048))
+    key = (dev.index, nblk, pad)
+    if key not in _SLABS:
+        _SLABS[key] = torch.empty(nblk * (pad + 2), dtype=torch.float64, device=dev)
+    out = torch.empty(d + 2, dtype=torch.float64, device=dev)
+    rc = L.alink_linear_grad_f64(X.data_ptr(), y.data_ptr(), w.data_ptr(), c.data_ptr(), n, d, int(code),
+                                 float(prm), _SLABS[key].data_ptr(), nblk, out.data_ptr(), _lib.stream_ptr(dev))
+    if rc != 0:
+        raise RuntimeError(f"alink_linear_grad_f64 failed: {rc}")
+    g = out[:d]
+    if coef.shape[0] > d:
+        g = torch.cat([g, torch.zeros(coef.shape[0] - d, dtype=g.dtype, device=dev)])
+    return g, out[d], out[d + 1]

@@ -93,3 +93,27 @@ def test_nearest_kernel_exact_candidates():
     idx, d2 = K.nearest_hip(X, X[sel].double())
     assert torch.equal(idx[sel].long(), torch.arange(sel.numel(), device="cuda"))
     assert float(d2[sel].abs().max()) < 1e-2
+
+
+@pytest.mark.parametrize("d", [1, 7, 8, 16, 31, 64])
+@pytest.mark.parametrize("loss", ["log", "logistic", "square", "hinge", "smooth", "perceptron", "exp", "huber", "svr"])
+def test_linear_grad_kernel_matches_fp64_reference(d, loss):
+    """csrc/linear.hip fused gradient vs the torch two-GEMV form of the same unary loss (fp64)."""
+    from alink_amd.models.linear import objfunc as O
+    from alink_amd.ops import linear as lops
+    fn = {"log": O.LogLossFunc(), "logistic": O.LogisticLossFunc(), "square": O.SquareLossFunc(),
+          "hinge": O.HingeLossFunc(), "smooth": O.SmoothHingeLossFunc(), "perceptron": O.PerceptronLossFunc(),
+          "exp": O.ExponentialLossFunc(), "huber": O.HuberLossFunc(0.7), "svr": O.SvrLossFunc(0.2)}[loss]
+    g = torch.Generator(device="cpu").manual_seed(d)
+    n = 50001
+    X = torch.randn(n, d, generator=g, dtype=torch.float64).cuda()
+    y = (torch.randint(0, 2, (n,), generator=g) * 2 - 1).double().cuda()
+    w = torch.rand(n, generator=g, dtype=torch.float64).cuda()
+    coef = (0.3 * torch.randn(d, generator=g, dtype=torch.float64)).cuda()
+    code, prm = lops.loss_code(fn)
+    got, lsum, wsum = lops.linear_grad_hip(X, y, w, coef, code, prm)
+    eta = X @ coef
+    ref = X.T @ (w * fn.derivative(eta, y))
+    torch.testing.assert_close(got, ref, rtol=1e-10, atol=1e-9)
+    torch.testing.assert_close(lsum, (w * fn.loss(eta, y)).sum(), rtol=1e-10, atol=1e-9)
+    torch.testing.assert_close(wsum, w.sum(), rtol=1e-12, atol=1e-9)
