@@ -145,16 +145,27 @@ __global__ __launch_bounds__(THREADS) void linear_grad_kernel(const double* __re
     }
 }
 
-// fixed-order sum of the per-block slabs: out = [grad(d), lossSum, weightSum]
-__global__ void linear_grad_reduce_kernel(const double* __restrict__ slab, int nblk, int dp, int d,
-                                          double* __restrict__ out) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= dp + 2) return;
+// fixed-order sum of the per-block slabs: out = [grad(d), lossSum, weightSum].  One workgroup per output
+// column: thread t sums slabs t, t+256, ... and the 256 partials are combined by a fixed LDS tree, so the
+// result is run-to-run deterministic.  (A single-thread-per-column loop over 2048 slabs was latency-bound
+// at ~0.75 ms, a third of the whole gradient at d = 32.)
+__global__ __launch_bounds__(THREADS) void linear_grad_reduce_kernel(const double* __restrict__ slab, int nblk,
+                                                                     int dp, int d, double* __restrict__ out) {
+    __shared__ double part[THREADS];
+    const int c = blockIdx.x;
     double s = 0.0;
-    for (int b = 0; b < nblk; ++b) s += slab[(int64_t)b * (dp + 2) + c];
-    if (c < d) out[c] = s;
-    else if (c == dp) out[d] = s;
-    else if (c == dp + 1) out[d + 1] = s;
+    for (int b = threadIdx.x; b < nblk; b += THREADS) s += slab[(int64_t)b * (dp + 2) + c];
+    part[threadIdx.x] = s;
+    __syncthreads();
+    for (int off = THREADS / 2; off > 0; off >>= 1) {
+        if (threadIdx.x < off) part[threadIdx.x] += part[threadIdx.x + off];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        if (c < d) out[c] = part[0];
+        else if (c == dp) out[d] = part[0];
+        else if (c == dp + 1) out[d + 1] = part[0];
+    }
 }
 
 template <int DP>
@@ -162,7 +173,7 @@ int launch(const double* X, const double* y, const double* w, const double* coef
            double prm, double* slab, int nblk, double* out, hipStream_t st) {
     hipLaunchKernelGGL(linear_grad_kernel<DP>, dim3(nblk), dim3(THREADS), 0, st, X, y, w, coef, n, d, code, prm,
                        slab);
-    hipLaunchKernelGGL(linear_grad_reduce_kernel, dim3((DP + 2 + 63) / 64), dim3(64), 0, st, slab, nblk, DP, d, out);
+    hipLaunchKernelGGL(linear_grad_reduce_kernel, dim3(DP + 2), dim3(THREADS), 0, st, slab, nblk, DP, d, out);
     return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
