@@ -23,7 +23,7 @@ import numpy as np
 
 from ... import _native
 from ...common.linalg import DenseVector
-from ...common.params import Params
+from ...common.params import ParamInfo, Params
 from ...common.table import MTable
 from ...common.types import TableSchema, Types
 from ...models.common.features import extract_features
@@ -63,6 +63,12 @@ def _ftrl_python(indptr, indices, values, label, w, n, z, alpha, beta, l1, l2):
 
 
 class FtrlTrainStreamOp(StreamOperator):
+    """``updateMode``: ``SEQUENTIAL`` (default; the native host loop, sample order as the reference) or
+    ``HOGWILD`` (the micro-batch is applied on the GPU by ``ops/csrc/ftrl.hip``, one wave per sample, with the
+    model state resident in HBM; needs a GPU)."""
+    EXTRA_PARAMS = [ParamInfo("updateMode", str, "SEQUENTIAL or HOGWILD (GPU, one wave per sample)",
+                              default="SEQUENTIAL")]
+
     def __init__(self, model=None, params: Optional[Params] = None, **kw):
         if isinstance(model, Params):
             model, params = None, model
@@ -96,10 +102,14 @@ class FtrlTrainStreamOp(StreamOperator):
         self._vec_col = _pget(p, "vectorCol")
         self._feat_cols = _pget(p, "featureCols")
         self._vsize = _pget(p, "vectorSize")
+        self._hogwild = str(_pget(p, "updateMode", "SEQUENTIAL")).upper() == "HOGWILD"
+        self._dev_state = None
         _register_upstream_sources(inp)
         return self
 
     def _snapshot(self):
+        if self._dev_state is not None:
+            self._w = self._dev_state[0].cpu().numpy().copy()
         m = self._model
         m.coefVector = DenseVector(self._w.copy())
         m.hasInterceptItem = self._intercept
@@ -151,6 +161,17 @@ class FtrlTrainStreamOp(StreamOperator):
                 labels.append(1.0 if str(v) == str(l0) else 0.0)
         if indices.size and int(indices.max()) >= self._w.size:
             raise ValueError("feature index out of range of the initial model")
+        if self._hogwild:
+            from ...ops.ftrl import ftrl_hogwild
+            if not torch.cuda.is_available():
+                raise RuntimeError("FTRL updateMode HOGWILD needs a GPU")
+            if self._dev_state is None:
+                dev = torch.device("cuda", torch.cuda.current_device())
+                self._dev_state = [torch.as_tensor(a, device=dev).clone() for a in (self._w, self._n, self._z)]
+            ftrl_hogwild(torch.as_tensor(indptr), torch.as_tensor(indices), torch.as_tensor(values),
+                         torch.as_tensor(np.asarray(labels, dtype=np.float64)), *self._dev_state,
+                         self._alpha, self._beta, self._l1, self._l2)
+            return
         if not _native.ftrl_update_csr(indptr, indices, values, np.asarray(labels), self._w, self._n, self._z,
                                        self._alpha, self._beta, self._l1, self._l2):
             _ftrl_python(indptr, indices, values, labels, self._w, self._n, self._z, self._alpha, self._beta,
