@@ -8,6 +8,7 @@ __version__ = "0.1.0"
 from .common.mlenv import (MLEnvironment, MLEnvironmentFactory, useLocalEnv, useRemoteEnv, resetEnv,  # noqa
                            getMLEnv)
 from .common.params import Params, ParamInfo  # noqa: F401
+from .parallel.launch import launch, launch_script  # noqa: F401
 from .common.linalg import DenseVector, SparseVector, VectorUtil, DenseMatrix  # noqa: F401
 from .common.table import MTable, Row  # noqa: F401
 from .common.types import TableSchema, Types  # noqa: F401

@@ -115,8 +115,19 @@ class MLEnvironmentFactory:
             return cls._envs.pop(env_id, None)
 
 
-def useLocalEnv(parallelism: int = 1, device: Optional[str] = None, **kwargs) -> MLEnvironment:
-    """PyAlink entry point: create (and make default) an environment with the given parallelism."""
+def useLocalEnv(parallelism: int = 1, device: Optional[str] = None, spawn: bool = False,
+                timeout_s: Optional[float] = None, **kwargs) -> MLEnvironment:
+    """PyAlink entry point: create (and make default) an environment with the given parallelism.
+
+    ``spawn=True`` outside an SPMD job makes the call self-launching (the reference's local env runs
+    ``parallelism`` real subtasks): the current script is started again as ``parallelism`` ranks (one
+    process per GPU, ``parallel/launch.py``), this process waits for them and exits with their status.
+    Call it before anything touches the GPU."""
+    if spawn and parallelism > 1:
+        from ..parallel.launch import in_launched_job, launch_script
+        import sys
+        if not in_launched_job():
+            sys.exit(launch_script(parallelism, [sys.executable] + sys.argv, timeout_s=timeout_s))
     env = MLEnvironment(parallelism=parallelism, device=device, **kwargs)
     MLEnvironmentFactory.setDefault(env)
     return env

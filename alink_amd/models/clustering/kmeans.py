@@ -181,21 +181,43 @@ def _nearest(X: torch.Tensor, C: torch.Tensor, dist_type: str, chunk=1 << 20) ->
 
 
 def _global_count(n_local: int) -> List[int]:
-    return comm.all_gather_object(int(n_local))
+    t = torch.tensor([int(n_local)], dtype=torch.int64)
+    return [int(v) for v in comm.all_gather_tensor(t).tolist()]
+
+
+_M64 = (1 << 64) - 1
+
+
+def _row_uniform(first_row: int, n: int, seed: int, rnd: int, device) -> torch.Tensor:
+    """Counter-based U(0,1) per *global* row index (splitmix64 of (seed, round, row)): the k-means||
+    oversampling draws are the same for any world size / partitioning, so a P-rank job picks exactly
+    the candidates a 1-rank job picks (the reference's per-subtask Random makes them P-dependent)."""
+    key = (seed * 0x9E3779B97F4A7C15 + rnd * 0xBF58476D1CE4E5B9 + 0x94D049BB133111EB) & _M64
+    key = key - (1 << 64) if key >= (1 << 63) else key
+    z = torch.arange(first_row, first_row + n, dtype=torch.int64, device=device) * 0x2545F491 + key
+
+    def _shr(x, k):  # logical shift right on int64
+        return (x >> k) & ((1 << (64 - k)) - 1)
+    z = (z ^ _shr(z, 30)) * -4658895280553007687      # 0xBF58476D1CE4E5B9 as int64
+    z = (z ^ _shr(z, 27)) * -7723592293110705685      # 0x94D049BB133111EB as int64
+    z = z ^ _shr(z, 31)
+    return (_shr(z, 11).to(torch.float64) + 0.5) * (1.0 / (1 << 53))
 
 
 def _fetch_global_rows(X: torch.Tensor, global_idx: List[int], counts: List[int]) -> torch.Tensor:
-    """Rows by global index (rank-order concatenation), replicated on every rank."""
+    """Rows by global index (rank-order concatenation), replicated on every rank: each rank writes the rows
+    it owns into a zero [m, d] fp64 block and one SUM all-reduce (RCCL on GPU) assembles it — no pickling."""
     rank = comm.get_rank()
     offs = np.concatenate([[0], np.cumsum(counts)])
+    d = max(1, int(X.shape[1])) if X.dim() == 2 else 1
+    out = torch.zeros((len(global_idx), d), dtype=torch.float64, device=X.device)
     mine = [(j, g - offs[rank]) for j, g in enumerate(global_idx) if offs[rank] <= g < offs[rank + 1]]
-    local = [(j, X[i].to(torch.float64).cpu().numpy()) for j, i in mine]
-    parts = comm.all_gather_object(local)
-    rows = [None] * len(global_idx)
-    for p in parts:
-        for j, v in p:
-            rows[j] = v
-    return torch.from_numpy(np.stack(rows)).to(X.device)
+    if mine:
+        dst = torch.as_tensor([j for j, _ in mine], dtype=torch.long, device=X.device)
+        src = torch.as_tensor([int(i) for _, i in mine], dtype=torch.long, device=X.device)
+        out.index_copy_(0, dst, X.index_select(0, src).to(torch.float64))
+    comm.all_reduce(out)
+    return out
 
 
 def _local_kmeans(samples: torch.Tensor, weights: torch.Tensor, k: int, dist_type: str,
@@ -272,19 +294,16 @@ def kmeans_init(X: torch.Tensor, k: int, init_mode: str, init_steps: int, dist_t
     # k-means||
     centers = _fetch_global_rows(X, [int(rng.integers(n))], counts)
     cost = _min_dist_to(X, centers, dist_type)
-    lrng = torch.Generator(device=X.device).manual_seed(seed * 7919 + comm.get_rank() + 1)
-    for _ in range(max(0, init_steps - 1)):
+    first_row = int(sum(counts[:comm.get_rank()]))
+    for rnd in range(max(0, init_steps - 1)):
         tot = torch.tensor([float(cost.sum().item())], dtype=torch.float64)
         comm.all_reduce(tot)
         thre = 2.0 * k / max(float(tot.item()), 1e-300)
-        u = torch.rand(X.shape[0], generator=lrng, dtype=torch.float64, device=X.device)
+        u = _row_uniform(first_row, X.shape[0], seed, rnd, X.device)
         pick = torch.nonzero(u < cost * thre).reshape(-1)
-        local_new = X[pick].to(torch.float64).cpu()
-        parts = comm.all_gather_object(local_new)
-        new = torch.cat([p for p in parts if p.shape[0] > 0]) if any(p.shape[0] > 0 for p in parts) else None
-        if new is None:
+        new = comm.all_gather_varlen(X[pick].to(torch.float64))   # rank order == global row order
+        if new.shape[0] == 0:
             continue
-        new = new.to(X.device)
         centers = torch.cat([centers, new])
         cost = torch.minimum(cost, _min_dist_to(X, new, dist_type))
     if centers.shape[0] <= k:
@@ -396,7 +415,8 @@ def train_kmeans(X: torch.Tensor, k: int, max_iter: int, tol: float, dist_type: 
     if dist_type == "COSINE":
         X = _normalize_rows(X.to(torch.float64)) if X.dtype == torch.float64 else \
             _normalize_rows(X.float()).to(X.dtype)
-    vector_size = max(comm.all_gather_object(int(X.shape[1]) if X.shape[0] else 0))
+    vs = torch.tensor([float(X.shape[1]) if X.shape[0] else 0.0], dtype=torch.float64)
+    vector_size = int(comm.all_reduce(vs, "max").item())
     init = init_centroids if init_centroids is not None else kmeans_init(X, k, init_mode, init_steps, dist_type,
                                                                          seed=seed)
     init = init.to(device=X.device, dtype=torch.float64)

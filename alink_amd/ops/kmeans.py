@@ -20,6 +20,7 @@ from . import _lib
 __all__ = ["assign_accumulate", "assign", "assign_accumulate_torch", "hip_supported", "prepare_centroids"]
 
 _BUF: Dict[Tuple, Tuple[torch.Tensor, torch.Tensor]] = {}
+HIP_CALLS = 0  # launches of the fused HIP assign+accumulate path (bench / tests read it)
 DEFAULT_VARIANT = None  # None -> per-k choice below (measured on MI355X, profiles/kmeans_variants.txt)
 DEFAULT_CONTIGUOUS = True  # v4/v5: contiguous tile run per workgroup (vs grid-strided tiles)
 HIP_D = 128
@@ -59,9 +60,9 @@ def prepare_centroids(C: torch.Tensor, device) -> Tuple[torch.Tensor, torch.Tens
 
 
 def pick_variant(k: int) -> int:
-    """v4 (row-owning waves, 128-row tiles) wins while k <= 64 (two centroid blocks); beyond that the
-    block-owning 8-wave v6 is fastest (1e8 x 128, MI355X: k=32 5.1 ms, k=64 5.5 ms (v4); k=100 8.2 ms (v6))."""
-    return 4 if k <= 64 else 6
+    """v7 (role-split waves, 16x16x32 MFMA, k padded to 16) for every k <= 128; v4 / v6 are kept for A/B
+    measurements (profiles/kmeans_variants.txt)."""
+    return 7
 
 
 def _num_cus(device) -> int:
@@ -69,8 +70,13 @@ def _num_cus(device) -> int:
 
 
 def assign_accumulate_hip(X: torch.Tensor, C: torch.Tensor, grid: Optional[int] = None,
-                          variant: Optional[int] = None, contiguous: Optional[bool] = None) -> torch.Tensor:
+                          variant: Optional[int] = None, contiguous: Optional[bool] = None,
+                          assign_out: Optional[torch.Tensor] = None, mode: int = 0) -> torch.Tensor:
+    """[k, d+1] fp64 sums|counts of this rank's rows.  ``assign_out`` (int32 [N], v7 only) also receives
+    every row's centroid id; ``mode`` 1/2 are v7's load-only / compute-only diagnostics."""
+    global HIP_CALLS
     L = _lib.require()
+    HIP_CALLS += 1
     if variant is None:
         variant = DEFAULT_VARIANT if DEFAULT_VARIANT is not None else pick_variant(C.shape[0])
     dev = X.device
@@ -81,8 +87,14 @@ def assign_accumulate_hip(X: torch.Tensor, C: torch.Tensor, grid: Optional[int] 
     n = X.shape[0]
     if grid is None:
         grid = _num_cus(dev)
-    ntiles = (n + 127) // 128 if variant not in (3, 5, 6) else (n + 63) // 64
-    grid = max(1, min(grid, ntiles))
+    if variant == 7:
+        grid = int(L.alink_kmeans_v7_grid(n, grid))
+    else:
+        ntiles = (n + 127) // 128 if variant not in (3, 5, 6) else (n + 63) // 64
+        grid = max(1, min(grid, ntiles))
+    if assign_out is not None and (variant != 7 or assign_out.dtype != torch.int32 or assign_out.numel() < n
+                                   or assign_out.device != dev or not assign_out.is_contiguous()):
+        raise ValueError("assign_out must be a contiguous int32 [N] tensor on X's device (variant 7)")
     key = (dev.index, grid)
     if key not in _BUF:
         _BUF[key] = (torch.empty((grid, HIP_KMAX, HIP_D), dtype=torch.float32, device=dev),
@@ -90,15 +102,14 @@ def assign_accumulate_hip(X: torch.Tensor, C: torch.Tensor, grid: Optional[int] 
     slab, slab_cnt = _BUF[key]
     out = torch.empty((k, HIP_D + 1), dtype=torch.float64, device=dev)
     st = _lib.stream_ptr(dev)
-    fn = {1: L.alink_kmeans_assign_accum_bf16, 2: L.alink_kmeans_assign_accum_bf16_v2,
-          3: L.alink_kmeans_assign_accum_bf16_v3, 4: L.alink_kmeans_assign_accum_bf16_v4,
-          5: L.alink_kmeans_assign_accum_bf16_v5, 6: L.alink_kmeans_assign_accum_bf16_v6}[variant]
-    if variant == 2 and k > 64:
-        raise ValueError("variant 2 spills registers for k > 64")
-    args = [X.data_ptr(), n, cpad.data_ptr(), ninit.data_ptr(), k, slab.data_ptr(), slab_cnt.data_ptr(), grid, st]
-    if variant in (4, 5, 6):
-        args.append(int(DEFAULT_CONTIGUOUS if contiguous is None else contiguous))
-    rc = fn(*args)
+    if variant == 7:
+        rc = L.alink_kmeans_assign_accum_bf16_v7(X.data_ptr(), n, cpad.data_ptr(), ninit.data_ptr(), k,
+                                                 slab.data_ptr(), slab_cnt.data_ptr(), grid, st,
+                                                 None if assign_out is None else assign_out.data_ptr(), int(mode))
+    else:
+        fn = {4: L.alink_kmeans_assign_accum_bf16_v4, 6: L.alink_kmeans_assign_accum_bf16_v6}[variant]
+        rc = fn(X.data_ptr(), n, cpad.data_ptr(), ninit.data_ptr(), k, slab.data_ptr(), slab_cnt.data_ptr(), grid,
+                st, int(DEFAULT_CONTIGUOUS if contiguous is None else contiguous))
     if rc != 0:
         raise RuntimeError(f"alink_kmeans_assign_accum_bf16 failed: {rc}")
     rc = L.alink_kmeans_reduce_slabs(slab.data_ptr(), slab_cnt.data_ptr(), grid, k, out.data_ptr(), st)

@@ -20,8 +20,11 @@ Fault tolerance (the reference has none: ComQueue state lives in the JVM heap an
 job):
 * ``setCheckpoint(dir, every)`` — after every ``every``-th superstep each rank atomically writes its task
   state (everything except the partitioned/broadcast inputs, which are rebuilt from the DAG) plus the
-  picklable state of the queue items and criterion; ``exec`` resumes from the newest step ALL ranks have
-  (agreed with one MIN all-reduce), so a killed job restarts at a superstep boundary;
+  tensor / plain-data state of the queue items and criterion (no pickled objects: loaded with
+  ``weights_only=True``), the criterion's stop decision and a fingerprint of the job (queue structure,
+  max_iter, layout, partition sizes — a directory of another job is rejected); ``exec`` resumes from the
+  newest step ALL ranks have (agreed with one MIN all-reduce), so a killed job restarts at a superstep
+  boundary, and a job whose checkpoint is the converged superstep returns its result without running on;
 * ``setWatchdog(seconds)`` — a superstep (its collectives included) that exceeds the limit dumps every
   thread's stack and terminates the process instead of hanging the job (a stuck RCCL peer);
 * fault injection for tests: ``ALINK_FAULT_INJECT="<rank>:<step>"`` raises ``InjectedFault`` on that rank
@@ -31,7 +34,6 @@ from __future__ import annotations
 
 import faulthandler
 import os
-import pickle
 import sys
 import time
 from typing import Any, Callable, Dict, List, Optional, Sequence
@@ -52,36 +54,60 @@ class InjectedFault(RuntimeError):
     """Raised by the ``ALINK_FAULT_INJECT`` hook (tests of checkpoint/resume)."""
 
 
-def _picklable(v) -> bool:
-    try:
-        pickle.dumps(v)
-        return True
-    except Exception:  # noqa: BLE001
-        return False
+class _Skip(Exception):
+    pass
 
 
-def _to_cpu(v):
+_SCALARS = (bool, int, float, str, type(None))
+
+
+def _plain(v):
+    """Checkpointable form of ``v``: tensors (on CPU), numpy arrays (as ``{"__np__": tensor}``), scalars and
+    lists / tuples / str-keyed dicts of those.  Anything else raises ``_Skip`` — checkpoints hold no
+    pickled objects, so they load with ``torch.load(weights_only=True)`` (no code runs from the file)."""
     if isinstance(v, torch.Tensor):
         return v.detach().cpu()
+    if isinstance(v, np.ndarray):
+        if v.dtype == object:
+            raise _Skip
+        return {"__np__": torch.from_numpy(np.ascontiguousarray(v))}
+    if isinstance(v, np.generic):
+        return v.item()
+    if isinstance(v, _SCALARS):
+        return v
     if isinstance(v, list):
-        return [_to_cpu(x) for x in v]
+        return [_plain(x) for x in v]
     if isinstance(v, tuple):
-        return tuple(_to_cpu(x) for x in v)
-    if isinstance(v, dict):
-        return {k: _to_cpu(x) for k, x in v.items()}
-    return v
+        return tuple(_plain(x) for x in v)
+    if isinstance(v, dict) and all(isinstance(k, str) for k in v):
+        return {k: _plain(x) for k, x in v.items()}
+    raise _Skip
 
 
-def _to_dev(v, dev):
+def _unplain(v, dev):
     if isinstance(v, torch.Tensor):
-        return v.to(dev)
-    if isinstance(v, list):
-        return [_to_dev(x, dev) for x in v]
-    if isinstance(v, tuple):
-        return tuple(_to_dev(x, dev) for x in v)
+        return v.to(dev) if dev is not None else v
     if isinstance(v, dict):
-        return {k: _to_dev(x, dev) for k, x in v.items()}
+        if set(v) == {"__np__"}:
+            return v["__np__"].numpy()
+        return {k: _unplain(x, dev) for k, x in v.items()}
+    if isinstance(v, list):
+        return [_unplain(x, dev) for x in v]
+    if isinstance(v, tuple):
+        return tuple(_unplain(x, dev) for x in v)
     return v
+
+
+def _plain_items(d: Dict[str, Any], skip=()) -> Dict[str, Any]:
+    out = {}
+    for k, v in d.items():
+        if k in skip:
+            continue
+        try:
+            out[k] = _plain(v)
+        except _Skip:
+            pass
+    return out
 
 
 class ComContext:
@@ -271,6 +297,7 @@ class BaseComQueue:
         self.ckpt_every = 1
         self.watchdog_s: Optional[float] = None
         self.resumed_from = 0
+        self.resumed_stop = False
 
     # ---- fault tolerance ----
     def setCheckpoint(self, directory: str, every: int = 1):
@@ -285,16 +312,24 @@ class BaseComQueue:
         return os.path.join(self.ckpt_dir, f"rank{rank}", f"step{step:08d}.pt")
 
     def _item_states(self, items):
-        out = []
-        for it in list(items) + [self.criterion]:
-            st = {k: _to_cpu(v) for k, v in getattr(it, "__dict__", {}).items() if _picklable(_to_cpu(v))}
-            out.append(st)
-        return out
+        return [_plain_items(getattr(it, "__dict__", {})) for it in list(items) + [self.criterion]]
 
-    def _save_checkpoint(self, rank, stores, items, skip):
-        state = {"step": self.step_no,
-                 "stores": [{k: _to_cpu(v) for k, v in st.items() if k not in skip and _picklable(_to_cpu(v))}
-                            for st in stores],
+    def _fingerprint(self, items, stores) -> str:
+        """Identity of the job a checkpoint belongs to: queue structure, max_iter, world / task layout and
+        the size of every partitioned input (a reused directory from another job is rejected)."""
+        sizes = []
+        for name, data in self.partitioned:
+            sizes.append([name] + [(len(st[name]) if not isinstance(st[name], torch.Tensor)
+                                    else int(st[name].shape[0])) if st.get(name) is not None else -1
+                                   for st in stores])
+        from ..common.mlenv import MLEnvironmentFactory
+        env = self.env or MLEnvironmentFactory.getDefault()
+        return repr(("->".join(it.name() for it in items), type(self.criterion).__name__, self.max_iter,
+                     env.world_size, env.local_tasks, sizes))
+
+    def _save_checkpoint(self, rank, stores, items, skip, stop=False):
+        state = {"step": self.step_no, "stop": bool(stop), "fingerprint": self._fingerprint(items, stores),
+                 "stores": [_plain_items(st, skip) for st in stores],
                  "items": self._item_states(items)}
         path = self._ckpt_file(rank, self.step_no)
         os.makedirs(os.path.dirname(path), exist_ok=True)
@@ -314,12 +349,18 @@ class BaseComQueue:
         step = int(mine.item())
         if step <= 0 or step not in steps:
             return 0
-        state = torch.load(self._ckpt_file(rank, step), map_location="cpu", weights_only=False)
+        state = torch.load(self._ckpt_file(rank, step), map_location="cpu", weights_only=True)
+        fp = self._fingerprint(items, stores)
+        if state.get("fingerprint") != fp:
+            raise RuntimeError(f"checkpoint {self._ckpt_file(rank, step)} belongs to another job "
+                               f"({state.get('fingerprint')!r} != {fp!r}); use an empty checkpoint directory")
         for st, saved in zip(stores, state["stores"]):
-            st.update(_to_dev(saved, self.device))
+            st.update(_unplain(saved, self.device))
         for it, saved in zip(list(items) + [self.criterion], state["items"]):
             if it is not None:
-                it.__dict__.update(_to_dev(saved, self.device))
+                it.__dict__.update(_unplain(saved, None if isinstance(it, CompareCriterionFunction)
+                                            else self.device))
+        self.resumed_stop = bool(state.get("stop", False))
         return step
 
     # ---- builder API (names as in the reference) ----
@@ -404,7 +445,7 @@ class BaseComQueue:
         skip = {n for n, _ in self.partitioned} | {n for n, _ in self.broadcast}
         use_roctx = self.device is not None and self.device.type == "cuda" and hasattr(torch.cuda, "nvtx")
         self.step_no = self.resumed_from
-        stop = False
+        stop = self.resumed_stop        # a checkpoint written at the converged superstep ends the run
         while not stop and self.step_no < self.max_iter:
             self.step_no += 1
             if inject is not None and inject == (env.rank, self.step_no):
@@ -428,8 +469,12 @@ class BaseComQueue:
                 if self.criterion_replicated or ws == 1:
                     dec = bool(self.criterion.calc(ctxs[0]))
                 else:
-                    dec = bool(self.criterion.calc(ctxs[0])) if env.rank == 0 else None
-                    dec = comm.broadcast_object(dec, 0)
+                    # task 0 decides; one 1-element MAX all-reduce (RCCL on GPU) instead of a pickled broadcast
+                    dec = bool(self.criterion.calc(ctxs[0])) if env.rank == 0 else False
+                    flag = torch.tensor([1.0 if dec else 0.0], dtype=torch.float64,
+                                        device=self.device if self.device is not None and
+                                        self.device.type == "cuda" else "cpu")
+                    dec = bool(comm.all_reduce(flag, MAX).item() > 0)
                 stop = dec
             if use_roctx:
                 torch.cuda.nvtx.range_pop()
@@ -440,7 +485,7 @@ class BaseComQueue:
             self.stats.append({"step": self.step_no, "wall_s": time.perf_counter() - t0,
                                "comm_bytes": comm.STATS.bytes - b0})
             if self.ckpt_dir is not None and (self.step_no % self.ckpt_every == 0 or stop):
-                self._save_checkpoint(env.rank, stores, items, skip)
+                self._save_checkpoint(env.rank, stores, items, skip, stop)
             for fn in self.on_step:
                 fn(self.step_no, self)
         result: List = []

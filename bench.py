@@ -9,6 +9,10 @@ all-reduce of the [k, d+1] sums, centroid update and the convergence criterion. 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--rows R] [--k 100] [--dims 128]
     torchrun --nproc-per-node N bench.py --gpus N ...
 
+``--gpus N`` without a launcher around it starts the N ranks itself (``alink_amd/parallel/launch.py``: N
+child processes with RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* set, started before this process touches the
+GPU; rank 0's JSON line is the job's output; a failing or hung rank fails the job).
+
 Prints ONE JSON line on rank 0.  ``value`` = total rows processed per second by the whole job
 (rows x K / max-over-ranks elapsed).  Also reports ``iters_to_converge`` from separate untimed runs with
 epsilon 1e-4: k-means|| initSteps=5 (``iters_to_converge``) and the reference default initSteps=2
@@ -39,15 +43,23 @@ def main():
     ap.add_argument("--k", type=int, default=100)
     ap.add_argument("--dims", type=int, default=128)
     ap.add_argument("--converge-iters", type=int, default=100, help="maxIter of the convergence run (0 = skip)")
+    ap.add_argument("--timeout", type=float, default=1500.0, help="self-launched job time limit (s)")
     a = ap.parse_args()
+
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # self-launch: this parent never initialises the GPU; each child is one rank (one MI355X)
+        from alink_amd.parallel.launch import launch_script
+        sys.exit(launch_script(a.gpus, [sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                               timeout_s=a.timeout))
 
     from alink_amd import useLocalEnv, KMeansTrainBatchOp, RandomVectorSourceBatchOp
     from alink_amd.parallel import comm
     from alink_amd.ops import _lib
 
+    from alink_amd.ops import kmeans as kops
     env = useLocalEnv(1)
-    if env.world_size != a.gpus and env.rank == 0:
-        print(f"[bench] warning: --gpus {a.gpus} but WORLD_SIZE={env.world_size}", file=sys.stderr)
+    if env.world_size != a.gpus:
+        raise SystemExit(f"[bench] --gpus {a.gpus} but the job has WORLD_SIZE={env.world_size}")
     dev = env.device
     if dev.type == "cuda":
         _lib.require()
@@ -76,7 +88,9 @@ def main():
     op._on_step = on_step
     from alink_amd.operator.batch.source import TableSourceBatchOp
     t_tot = time.perf_counter()
+    hip0 = kops.HIP_CALLS
     op.linkFrom(TableSourceBatchOp(data))
+    hip_used = kops.HIP_CALLS > hip0
     t_tot = time.perf_counter() - t_tot
     if a.warmup == 0:
         raise SystemExit("--warmup must be >= 1 (the first superstep includes one-time setup)")
@@ -85,6 +99,7 @@ def main():
     comm.all_reduce(el, "max")
     elapsed = float(el.item())
     stats = op._queue.stats[a.warmup:a.warmup + a.steps]
+    live_k = int(op._queue.final_contexts[0].getObj("k"))
     comm_bytes = sum(s["comm_bytes"] for s in stats) / max(1, len(stats))
 
     # ---- convergence runs (epsilon 1e-4): reference default initSteps=2, and initSteps=5 ----
@@ -96,8 +111,10 @@ def main():
                 .setInitSteps(steps)
             op2.linkFrom(TableSourceBatchOp(data))
             info = op2.getTrainInfo()
+            shift = (info["max_shift"] or [None])[-1]
             conv[f"initSteps{steps}"] = {"iters": info["iterations"], "wall_s": time.perf_counter() - t_c,
-                                         "final_max_shift": (info["max_shift"] or [None])[-1]}
+                                         "final_max_shift": shift,
+                                         "converged": shift is not None and shift < 1e-4}
         iters = conv["initSteps5"]["iters"]
 
     rows_per_s = a.rows * a.steps / elapsed
@@ -113,7 +130,7 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "bf16",
-        "data": "synthetic (Gaussian mixture, 100 components, generated on-device)",
+        "data": f"synthetic (Gaussian mixture, {a.k} components, generated on {dev.type})",
         "config": {"model": "KMeans k=100 (Lloyd, EUCLIDEAN, k-means|| init)", "global_batch": a.rows,
                    "seq_len": a.dims, "rows": a.rows, "dims": a.dims, "k": a.k,
                    "parallelism": f"dp{env.world_size}"},
@@ -122,8 +139,14 @@ def main():
         "iters_to_converge_setting": "epsilon 1e-4, k-means|| initSteps=5; reference default initSteps=2 "
                                      "reported under convergence.initSteps2",
         "convergence": conv,
+        "iters_to_converge_default_init": conv.get("initSteps2", {}).get("iters"),
+        "converged_default_init": conv.get("initSteps2", {}).get("converged"),
+        "live_k": live_k,
+        "effective_config": {"k_requested": a.k, "k_live_in_timed_run": live_k, "init": "K_MEANS_PARALLEL",
+                             "initSteps_timed_run": 2, "epsilon_timed_run": -1.0,
+                             "rows_per_rank": a.rows // env.world_size, "device": str(dev)},
         "allreduce_bytes_per_step": comm_bytes,
-        "hip_kernels": _lib.available(),
+        "hip_kernels": bool(hip_used),
         "datagen_s": t_gen,
         "train_wall_s": t_tot,
     }

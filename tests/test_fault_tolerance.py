@@ -78,3 +78,53 @@ def test_watchdog_terminates_hung_superstep(tmp_path):
     p = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True, timeout=60)
     assert p.returncode != 0
     assert "Timeout" in p.stderr or "Thread" in p.stderr
+
+
+class StopAt(CompareCriterionFunction):
+    def __init__(self, at):
+        self.at, self.seen = at, []
+
+    def calc(self, ctx):
+        self.seen.append(ctx.getStepNo())
+        return ctx.getStepNo() >= self.at
+
+
+def _stop_queue(ckpt, at=3, max_iter=6, n=10):
+    st = Step()
+    q = IterativeComQueue().initWithPartitionedData("data", torch.arange(n, dtype=torch.float64)) \
+        .add(st).add(AllReduce("buf")).setCompareCriterionOfNode0(StopAt(at)).closeWith(Out()) \
+        .setMaxIter(max_iter).setCheckpoint(ckpt, every=2)
+    return q, st
+
+
+def test_resume_from_converged_checkpoint_runs_no_extra_superstep(tmp_path):
+    useLocalEnv(1, device="cpu")
+    ck = str(tmp_path / "ck")
+    q, st = _stop_queue(ck)
+    ref = q.exec()
+    assert q.step_no == 3 and st.calls == 3          # criterion fired at step 3 (checkpointed although 3 % 2)
+    q2, st2 = _stop_queue(ck)
+    res = q2.exec()
+    assert q2.resumed_from == 3 and q2.step_no == 3
+    assert st2.calls == 3                             # restored from the checkpoint, never incremented
+    assert res == ref
+
+
+def test_checkpoint_of_another_job_is_rejected(tmp_path):
+    useLocalEnv(1, device="cpu")
+    ck = str(tmp_path / "ck")
+    _stop_queue(ck)[0].exec()
+    with pytest.raises(RuntimeError, match="another job"):
+        _stop_queue(ck, n=12)[0].exec()               # different partition size
+    with pytest.raises(RuntimeError, match="another job"):
+        _stop_queue(ck, max_iter=9)[0].exec()
+
+
+def test_checkpoint_files_load_without_pickle(tmp_path):
+    useLocalEnv(1, device="cpu")
+    ck = str(tmp_path / "ck")
+    _stop_queue(ck)[0].exec()
+    d = os.path.join(ck, "rank0")
+    for f in os.listdir(d):
+        state = torch.load(os.path.join(d, f), weights_only=True)
+        assert state["stop"] is True or state["step"] < 3

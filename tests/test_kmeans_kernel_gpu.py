@@ -14,34 +14,74 @@ def _data(n, k, seed=0, dev="cuda"):
     return X, C
 
 
-@pytest.mark.parametrize("variant", [1, 3, 4, 5, 6])
-@pytest.mark.parametrize("n,k", [(1, 1), (127, 3), (128, 32), (1000, 33), (4097, 100), (50000, 128), (300001, 100)])
-def test_assign_accumulate_matches_reference(n, k, variant):
+def _own_assignment_check(X, C, got, asg, k):
+    """The kernel's sums/counts must equal the fp64 sums of X by the kernel's OWN assignment, and every
+    assignment must be optimal up to the 2^-17 relative packing of the score (near-ties may go either way)."""
+    n = X.shape[0]
+    a = asg.long()
+    assert int(a.min()) >= 0 and int(a.max()) < k
+    ref = torch.zeros((k, 129), dtype=torch.float64, device=X.device)
+    ref[:, :128].index_add_(0, a, X.double())
+    ref[:, 128].index_add_(0, a, torch.ones(n, dtype=torch.float64, device=X.device))
+    assert torch.equal(got[:, 128], ref[:, 128]), "counts differ from the kernel's own assignment"
+    cnt = ref[:, 128:129]
+    tol = 4e-6 * cnt * float(X.float().abs().max()) + 1e-3
+    assert bool(((got[:, :128] - ref[:, :128]).abs() <= tol).all())
+    Cb = C.to(torch.bfloat16).float()
+    half = 0.5 * (Cb * Cb).sum(1)
+    for s in range(0, n, 1 << 20):
+        sc = X[s:s + (1 << 20)].float() @ Cb.T - half
+        best = sc.max(1).values
+        chosen = sc.gather(1, a[s:s + (1 << 20), None])[:, 0]
+        assert bool((best - chosen <= 2.0 ** -15 * best.abs() + 1e-4).all()), "non-optimal assignment"
+
+
+@pytest.mark.parametrize("n,k", [(1, 1), (63, 3), (64, 16), (65, 17), (1000, 33), (4097, 100), (50000, 128),
+                                 (300001, 100), (123457, 112), (70001, 8)])
+def test_v7_matches_own_assignment_reference(n, k):
     from alink_amd.ops import kmeans as K
     from alink_amd.ops import _lib
     assert _lib.available(), "HIP library must be built and loadable on the GPU box"
     X, C = _data(n, k)
-    got = K.assign_accumulate_hip(X, C, variant=variant)
-    ref = K.assign_accumulate_torch(X, C)
+    asg = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+    got = K.assign_accumulate_hip(X, C, variant=7, assign_out=asg)
     torch.cuda.synchronize()
-    # counts: assignments may differ only for near-ties (relative 2^-16 packing); allow a tiny fraction
-    dc = (got[:, -1] - ref[:, -1]).abs().sum().item()
-    assert dc <= max(2, 1e-4 * n), f"count mismatch {dc}"
-    assert abs(got[:, -1].sum().item() - n) < 0.5
-    if dc == 0:
-        torch.testing.assert_close(got[:, :-1], ref[:, :-1], rtol=1e-5, atol=1e-3 * max(1.0, n / 1000))
+    _own_assignment_check(X, C, got, asg, k)
+    # and against an independent torch argmax: only near-ties may differ
+    ref = K.assign_accumulate_torch(X, C)
+    assert (got[:, -1] - ref[:, -1]).abs().sum().item() <= max(2, 1e-4 * n)
 
 
-@pytest.mark.parametrize("variant,contig", [(1, None), (4, True), (4, False), (5, True), (5, False), (6, True), (6, False)])
-@pytest.mark.parametrize("n,k,grid", [(200, 7, 1), (49157, 100, 3), (33333, 64, 7), (640, 100, 2), (70000, 100, 256)])
-def test_assign_accumulate_small_grid(n, k, grid, variant, contig):
-    """Few workgroups -> long per-workgroup tile loops (pipeline warm-up, steady state and drain)."""
+@pytest.mark.parametrize("n,k,grid", [(200, 7, 1), (49157, 100, 3), (33333, 64, 7), (640, 100, 2), (70000, 100, 256),
+                                      (1000003, 128, 5)])
+def test_v7_small_grid_long_loops(n, k, grid):
+    """Few workgroups -> long per-workgroup tile loops (ring warm-up, steady state, one-hot reuse, drain)."""
     from alink_amd.ops import kmeans as K
     X, C = _data(n, k, seed=11)
-    got = K.assign_accumulate_hip(X, C, grid=grid, variant=variant, contiguous=contig)
+    asg = torch.empty((n,), dtype=torch.int32, device="cuda")
+    got = K.assign_accumulate_hip(X, C, grid=grid, variant=7, assign_out=asg)
+    torch.cuda.synchronize()
+    _own_assignment_check(X, C, got, asg, k)
+
+
+def test_v7_without_assign_output_equals_with():
+    from alink_amd.ops import kmeans as K
+    X, C = _data(100003, 100, seed=4)
+    a = K.assign_accumulate_hip(X, C, variant=7)
+    asg = torch.empty((X.shape[0],), dtype=torch.int32, device="cuda")
+    b = K.assign_accumulate_hip(X, C, variant=7, assign_out=asg)
+    assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("variant,contig", [(4, True), (6, True), (6, False)])
+@pytest.mark.parametrize("n,k", [(4097, 100), (300001, 100), (33333, 64)])
+def test_ab_variants_match_reference(n, k, variant, contig):
+    from alink_amd.ops import kmeans as K
+    X, C = _data(n, k, seed=2)
+    got = K.assign_accumulate_hip(X, C, variant=variant, contiguous=contig)
     ref = K.assign_accumulate_torch(X, C)
     torch.cuda.synchronize()
-    assert (got[:, -1] - ref[:, -1]).abs().sum().item() <= 2
+    assert (got[:, -1] - ref[:, -1]).abs().sum().item() <= max(2, 1e-4 * n)
     assert abs(got[:, -1].sum().item() - n) < 0.5
 
 
@@ -51,15 +91,6 @@ def test_kernel_deterministic():
     a = K.assign_accumulate_hip(X, C)
     b = K.assign_accumulate_hip(X, C)
     assert torch.equal(a, b)
-
-
-@pytest.mark.parametrize("n,k", [(700, 40), (65536, 64), (12345, 17)])
-def test_v2_kernel_small_k(n, k):
-    from alink_amd.ops import kmeans as K
-    X, C = _data(n, k, seed=5)
-    got = K.assign_accumulate_hip(X, C, variant=2)
-    ref = K.assign_accumulate_torch(X, C)
-    assert (got[:, -1] - ref[:, -1]).abs().sum().item() <= 2
 
 
 @pytest.mark.parametrize("d", [64, 128, 256])

@@ -23,7 +23,7 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--torch", action="store_true", help="also time the PyTorch path")
     ap.add_argument("--grid", type=int, default=None)
-    ap.add_argument("--variant", type=int, default=1)
+    ap.add_argument("--variant", type=int, default=7)
     ap.add_argument("--strided", action="store_true", help="v4/v5: grid-strided tile schedule")
     ap.add_argument("--load-only", action="store_true", help="v6: time the LDS-DMA load pipeline alone")
     ap.add_argument("--compute-only", action="store_true", help="v6: time the compute alone (no loads)")
@@ -39,18 +39,25 @@ def main():
         lab = torch.randint(0, k, (e - s,), device=dev, generator=g)
         X[s:e] = (centers[lab] + torch.randn(e - s, d, device=dev, generator=g)).to(torch.bfloat16)
     C = (centers + 0.5 * torch.randn(k, d, device=dev, generator=g)).double()
-    out = K.assign_accumulate_hip(X, C, grid=a.grid, variant=a.variant, contiguous=4 if a.compute_only else (2 + a.strided) if a.load_only else not a.strided)
+    def run(Xs):
+        if a.variant == 7:
+            return K.assign_accumulate_hip(Xs, C, grid=a.grid, variant=7,
+                                           mode=2 if a.compute_only else 1 if a.load_only else 0)
+        return K.assign_accumulate_hip(Xs, C, grid=a.grid, variant=a.variant,
+                                       contiguous=4 if a.compute_only else (2 + a.strided) if a.load_only
+                                       else not a.strided)
+    out = run(X)
     torch.cuda.synchronize()
     res = {"rows": n, "k": k, "variant": a.variant, "strided": a.strided, "load_only": a.load_only, "compute_only": a.compute_only}
     if a.torch:
         ref0 = K.assign_accumulate_torch(X[:2_000_000], C)
-        got0 = K.assign_accumulate_hip(X[:2_000_000].contiguous(), C, grid=a.grid, variant=a.variant, contiguous=4 if a.compute_only else (2 + a.strided) if a.load_only else not a.strided)
+        got0 = run(X[:2_000_000].contiguous())
         res["small_count_diff"] = float((got0[:, -1] - ref0[:, -1]).abs().sum().item())
     times = []
     for _ in range(a.iters):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        out = K.assign_accumulate_hip(X, C, grid=a.grid, variant=a.variant, contiguous=4 if a.compute_only else (2 + a.strided) if a.load_only else not a.strided)
+        out = run(X)
         torch.cuda.synchronize()
         times.append(time.perf_counter() - t0)
     t = sorted(times)[len(times) // 2]
