@@ -87,14 +87,14 @@ def assign_accumulate_hip(X: torch.Tensor, C: torch.Tensor, grid: Optional[int] 
     n = X.shape[0]
     if grid is None:
         grid = _num_cus(dev)
-    if variant == 7:
+    if variant in (7, 8):
         grid = int(L.alink_kmeans_v7_grid(n, grid))
     else:
         ntiles = (n + 127) // 128 if variant not in (3, 5, 6) else (n + 63) // 64
         grid = max(1, min(grid, ntiles))
-    if assign_out is not None and (variant != 7 or assign_out.dtype != torch.int32 or assign_out.numel() < n
+    if assign_out is not None and (variant not in (7, 8) or assign_out.dtype != torch.int32 or assign_out.numel() < n
                                    or assign_out.device != dev or not assign_out.is_contiguous()):
-        raise ValueError("assign_out must be a contiguous int32 [N] tensor on X's device (variant 7)")
+        raise ValueError("assign_out must be a contiguous int32 [N] tensor on X's device (variants 7/8)")
     key = (dev.index, grid)
     if key not in _BUF:
         _BUF[key] = (torch.empty((grid, HIP_KMAX, HIP_D), dtype=torch.float32, device=dev),
@@ -102,10 +102,11 @@ def assign_accumulate_hip(X: torch.Tensor, C: torch.Tensor, grid: Optional[int] 
     slab, slab_cnt = _BUF[key]
     out = torch.empty((k, HIP_D + 1), dtype=torch.float64, device=dev)
     st = _lib.stream_ptr(dev)
-    if variant == 7:
-        rc = L.alink_kmeans_assign_accum_bf16_v7(X.data_ptr(), n, cpad.data_ptr(), ninit.data_ptr(), k,
-                                                 slab.data_ptr(), slab_cnt.data_ptr(), grid, st,
-                                                 None if assign_out is None else assign_out.data_ptr(), int(mode))
+    if variant in (7, 8):
+        fn = L.alink_kmeans_assign_accum_bf16_v8 if variant == 8 else L.alink_kmeans_assign_accum_bf16_v7
+        rc = fn(X.data_ptr(), n, cpad.data_ptr(), ninit.data_ptr(), k,
+                slab.data_ptr(), slab_cnt.data_ptr(), grid, st,
+                None if assign_out is None else assign_out.data_ptr(), int(mode))
     else:
         fn = {4: L.alink_kmeans_assign_accum_bf16_v4, 6: L.alink_kmeans_assign_accum_bf16_v6}[variant]
         rc = fn(X.data_ptr(), n, cpad.data_ptr(), ninit.data_ptr(), k, slab.data_ptr(), slab_cnt.data_ptr(), grid,

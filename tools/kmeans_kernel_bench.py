@@ -40,8 +40,8 @@ def main():
         X[s:e] = (centers[lab] + torch.randn(e - s, d, device=dev, generator=g)).to(torch.bfloat16)
     C = (centers + 0.5 * torch.randn(k, d, device=dev, generator=g)).double()
     def run(Xs):
-        if a.variant == 7:
-            return K.assign_accumulate_hip(Xs, C, grid=a.grid, variant=7,
+        if a.variant in (7, 8):
+            return K.assign_accumulate_hip(Xs, C, grid=a.grid, variant=a.variant,
                                            mode=2 if a.compute_only else 1 if a.load_only else 0)
         return K.assign_accumulate_hip(Xs, C, grid=a.grid, variant=a.variant,
                                        contiguous=4 if a.compute_only else (2 + a.strided) if a.load_only

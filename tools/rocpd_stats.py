@@ -1,0 +1,29 @@
+#!/usr/bin/env python3
+"""Summarise a rocprofv3 SQLite output (``*_results.db``) as a per-kernel stats table (calls, total/avg/min/max
+µs, % of GPU time).  Usage: python tools/rocpd_stats.py DB [--top N] [--match SUBSTR]"""
+import argparse
+import sqlite3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("db")
+    ap.add_argument("--top", type=int, default=25)
+    ap.add_argument("--match", default=None)
+    a = ap.parse_args()
+    c = sqlite3.connect(a.db)
+    cols = [r[1] for r in c.execute("pragma table_info(kernels)")]
+    name = "kernel_name" if "kernel_name" in cols else "name"
+    rows = c.execute(f"select {name}, count(*), sum(end-start), avg(end-start), min(end-start), max(end-start) "
+                     f"from kernels group by {name} order by sum(end-start) desc").fetchall()
+    total = sum(r[2] for r in rows) or 1
+    print(f"{'calls':>6} {'total_us':>11} {'avg_us':>10} {'min_us':>10} {'max_us':>10} {'pct':>6}  kernel")
+    for r in rows[:a.top]:
+        if a.match and a.match not in r[0]:
+            continue
+        print(f"{r[1]:6d} {r[2]/1e3:11.1f} {r[3]/1e3:10.2f} {r[4]/1e3:10.2f} {r[5]/1e3:10.2f} {100*r[2]/total:6.2f}  {r[0][:110]}")
+    print(f"total GPU kernel time: {total/1e6:.3f} ms over {sum(r[1] for r in rows)} dispatches")
+
+
+if __name__ == "__main__":
+    main()
