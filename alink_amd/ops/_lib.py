@@ -35,18 +35,6 @@ def _load():
         _err = f"cannot load {LIB_PATH}: {e}"
         return None
     c_i64, c_int, c_vp = ctypes.c_int64, ctypes.c_int, ctypes.c_void_p
-    L.alink_kmeans_assign_accum_bf16.argtypes = [c_vp, c_i64, c_vp, c_vp, c_int, c_vp, c_vp, c_int, c_vp]
-    L.alink_kmeans_assign_accum_bf16.restype = c_int
-    L.alink_kmeans_assign_accum_bf16_v2.argtypes = [c_vp, c_i64, c_vp, c_vp, c_int, c_vp, c_vp, c_int, c_vp]
-    L.alink_kmeans_assign_accum_bf16_v2.restype = c_int
-    L.alink_kmeans_assign_accum_bf16_v3.argtypes = [c_vp, c_i64, c_vp, c_vp, c_int, c_vp, c_vp, c_int, c_vp]
-    L.alink_kmeans_assign_accum_bf16_v3.restype = c_int
-    L.alink_kmeans_assign_accum_bf16_v4.argtypes = [c_vp, c_i64, c_vp, c_vp, c_int, c_vp, c_vp, c_int, c_vp, c_int]
-    L.alink_kmeans_assign_accum_bf16_v4.restype = c_int
-    L.alink_kmeans_assign_accum_bf16_v5.argtypes = [c_vp, c_i64, c_vp, c_vp, c_int, c_vp, c_vp, c_int, c_vp, c_int]
-    L.alink_kmeans_assign_accum_bf16_v5.restype = c_int
-    L.alink_kmeans_assign_accum_bf16_v6.argtypes = [c_vp, c_i64, c_vp, c_vp, c_int, c_vp, c_vp, c_int, c_vp, c_int]
-    L.alink_kmeans_assign_accum_bf16_v6.restype = c_int
     L.alink_kmeans_reduce_slabs.argtypes = [c_vp, c_vp, c_int, c_int, c_vp, c_vp]
     L.alink_kmeans_reduce_slabs.restype = c_int
     L.alink_kmeans_prep_centroids.argtypes = [c_vp, c_int, c_vp, c_vp, c_vp]
@@ -67,10 +55,7 @@ _EXTRA_SIGNATURES = {
                             _c_vp],
     "alink_tree_node_sums": [_c_vp, _c_vp, _c_vp, _c_i64, _c_int, _c_int, _c_vp, _c_int, _c_vp],
     "alink_tree_route": [_c_vp, _c_i64, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_vp],
-    "alink_logistic_grad": [_c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_int, _c_vp, _c_vp, _c_vp],
     "alink_kmeans_assign_accum_bf16_v7": [_c_vp, _c_i64, _c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_int, _c_vp, _c_vp,
-                                          _c_int],
-    "alink_kmeans_assign_accum_bf16_v8": [_c_vp, _c_i64, _c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_int, _c_vp, _c_vp,
                                           _c_int],
     "alink_kmeans_v7_grid": [_c_i64, _c_int],
     "alink_kmeans_nearest_bf16": [_c_vp, _c_i64, _c_int, _c_vp, _c_vp, _c_int, _c_int, _c_vp, _c_vp, _c_int,

@@ -1,0 +1,85 @@
+// KMeans helpers shared by the fused assign+accumulate kernel (kmeans_v7.hip) — CDNA4 (gfx950 / MI355X).
+//
+//   * kmeans_reduce_slabs: fixed-order fp64 reduction of the per-workgroup fp32 partial sums / counts into the
+//     [k][D+1] buffer that the BSP AllReduce sums across GPUs (the reference's centroidAllReduce buffer,
+//     A/operator/common/clustering/kmeans/KMeansAssignCluster.java:48-63).  Fixed order -> run-to-run
+//     deterministic, independent of workgroup scheduling.
+//   * kmeans_prep_centroids: next-superstep centroid operands from the fp64 centroids (KMeansUpdateCentroids
+//     output): bf16 block [128][D] and the MFMA accumulator init -|c|^2/2, one launch.
+//
+// Earlier assign+accumulate designs (v1-v6: 128-row tiles with LUT one-hot, block-owning waves, ...) and the v8
+// software-pipelined variant are documented with their measurements in profiles/kmeans_variants.txt and
+// profiles/kmeans_v7_v8_pmc.txt; only v7 ships.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace {
+
+constexpr int D = 128;
+
+// fixed-order fp64 reduction of the per-workgroup slabs -> out[k][D+1] (last column = count).
+// Block (c, y): y < 4 -> dims 32y..32y+31, y == 4 -> the count; 8 lane groups stride the slabs (coalesced
+// 128-B rows), then group partials are added in group order, so the result is run-to-run deterministic.
+__global__ __launch_bounds__(256) void kmeans_reduce_slabs_kernel(const float* __restrict__ slab,
+                                                                  const float* __restrict__ slab_cnt, int nslab,
+                                                                  int k, double* __restrict__ out) {
+    __shared__ double part[8][32];
+    const int c = blockIdx.x, y = blockIdx.y;
+    const int d = threadIdx.x & 31, g = threadIdx.x >> 5;
+    double s = 0.0;
+    if (y < 4) {
+        const float* p = slab + (int64_t)c * D + 32 * y + d;
+        for (int w = g; w < nslab; w += 8) s += (double)p[(int64_t)w * 128 * D];
+    } else if (d == 0) {
+        for (int w = g; w < nslab; w += 8) s += (double)slab_cnt[(int64_t)w * 128 + c];
+    }
+    part[g][d] = s;
+    __syncthreads();
+    if (g == 0) {
+        double t = 0.0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) t += part[j][d];
+        if (y < 4) out[(int64_t)c * (D + 1) + 32 * y + d] = t;
+        else if (d == 0) out[(int64_t)c * (D + 1) + D] = t;
+    }
+}
+
+// next-step centroid operands from fp64 centroids C [k][D]: bf16 block [128][D] (zero rows past k) and the
+// accumulator init -|bf16(c)|^2/2 (-3e38 past k), one launch instead of a chain of small torch ops.
+__global__ __launch_bounds__(128) void kmeans_prep_centroids_kernel(const double* __restrict__ C, int k,
+                                                                    __bf16* __restrict__ cpad,
+                                                                    float* __restrict__ ninit) {
+    __shared__ float red[128];
+    const int c = blockIdx.x, d = threadIdx.x;
+    const __bf16 b = c < k ? (__bf16)(float)C[(int64_t)c * D + d] : (__bf16)0.0f;
+    cpad[c * D + d] = b;
+    const float f = (float)b;
+    red[d] = f * f;
+    __syncthreads();
+    for (int off = 64; off > 0; off >>= 1) {
+        if (d < off) red[d] += red[d + off];
+        __syncthreads();
+    }
+    if (d == 0) ninit[c] = c < k ? -0.5f * red[0] : -3.0e38f;
+}
+
+}  // namespace
+
+extern "C" {
+
+int alink_kmeans_reduce_slabs(const float* slab, const float* slab_cnt, int nslab, int k, double* out,
+                              void* stream) {
+    if (k < 1 || k > 128 || nslab < 1) return -1;
+    hipLaunchKernelGGL(kmeans_reduce_slabs_kernel, dim3(k, 5), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                       slab, slab_cnt, nslab, k, out);
+    return (int)hipGetLastError();
+}
+
+int alink_kmeans_prep_centroids(const double* C, int k, void* cpad, float* ninit, void* stream) {
+    if (k < 0 || k > 128) return -1;
+    hipLaunchKernelGGL(kmeans_prep_centroids_kernel, dim3(128), dim3(128), 0, reinterpret_cast<hipStream_t>(stream),
+                       C, k, (__bf16*)cpad, ninit);
+    return (int)hipGetLastError();
+}
+
+}  // extern "C"

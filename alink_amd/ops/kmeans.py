@@ -5,8 +5,8 @@
 ``KMeansUtil.updateSumMatrix`` ``KMeansUtil.java:60-85``) — for this rank's rows, ready for the BSP
 all-reduce.
 
-* GPU, bf16 rows, d == 128, k <= 128: one persistent MFMA kernel (``csrc/kmeans.hip``) + an fp64
-  fixed-order slab reduction (deterministic).
+* GPU, bf16 rows, d == 128, k <= 128: one persistent MFMA kernel (``csrc/kmeans_v7.hip``) + an fp64
+  fixed-order slab reduction (``csrc/kmeans_common.hip``, deterministic).
 * anything else: chunked PyTorch path (fp64 on CPU; on GPU fp32 GEMM of the same bf16-rounded centroids).
 """
 from __future__ import annotations
@@ -21,8 +21,6 @@ __all__ = ["assign_accumulate", "assign", "assign_accumulate_torch", "hip_suppor
 
 _BUF: Dict[Tuple, Tuple[torch.Tensor, torch.Tensor]] = {}
 HIP_CALLS = 0  # launches of the fused HIP assign+accumulate path (bench / tests read it)
-DEFAULT_VARIANT = None  # None -> per-k choice below (measured on MI355X, profiles/kmeans_variants.txt)
-DEFAULT_CONTIGUOUS = True  # v4/v5: contiguous tile run per workgroup (vs grid-strided tiles)
 HIP_D = 128
 HIP_KMAX = 128
 
@@ -59,42 +57,28 @@ def prepare_centroids(C: torch.Tensor, device) -> Tuple[torch.Tensor, torch.Tens
     return cpad, ninit
 
 
-def pick_variant(k: int) -> int:
-    """v7 (role-split waves, 16x16x32 MFMA, k padded to 16) for every k <= 128; v4 / v6 are kept for A/B
-    measurements (profiles/kmeans_variants.txt)."""
-    return 7
-
-
 def _num_cus(device) -> int:
     return torch.cuda.get_device_properties(device).multi_processor_count
 
 
 def assign_accumulate_hip(X: torch.Tensor, C: torch.Tensor, grid: Optional[int] = None,
-                          variant: Optional[int] = None, contiguous: Optional[bool] = None,
                           assign_out: Optional[torch.Tensor] = None, mode: int = 0) -> torch.Tensor:
-    """[k, d+1] fp64 sums|counts of this rank's rows.  ``assign_out`` (int32 [N], v7 only) also receives
-    every row's centroid id; ``mode`` 1/2 are v7's load-only / compute-only diagnostics."""
+    """[k, d+1] fp64 sums|counts of this rank's rows (``csrc/kmeans_v7.hip``: role-split waves on 16x16x32
+    MFMA, LDS-DMA tile ring).  ``assign_out`` (int32 [N]) also receives every row's centroid id; ``mode`` 1/2
+    are the kernel's load-only / compute-only diagnostics (results meaningless)."""
     global HIP_CALLS
     L = _lib.require()
     HIP_CALLS += 1
-    if variant is None:
-        variant = DEFAULT_VARIANT if DEFAULT_VARIANT is not None else pick_variant(C.shape[0])
     dev = X.device
     k = C.shape[0]
     if not hip_supported(X, k):
         raise ValueError("HIP KMeans path needs contiguous bf16 [N,128] on GPU and k <= 128")
+    if assign_out is not None and (assign_out.dtype != torch.int32 or assign_out.numel() < X.shape[0]
+                                   or assign_out.device != dev or not assign_out.is_contiguous()):
+        raise ValueError("assign_out must be a contiguous int32 [N] tensor on X's device")
     cpad, ninit = prepare_centroids(C, dev)
     n = X.shape[0]
-    if grid is None:
-        grid = _num_cus(dev)
-    if variant in (7, 8):
-        grid = int(L.alink_kmeans_v7_grid(n, grid))
-    else:
-        ntiles = (n + 127) // 128 if variant not in (3, 5, 6) else (n + 63) // 64
-        grid = max(1, min(grid, ntiles))
-    if assign_out is not None and (variant not in (7, 8) or assign_out.dtype != torch.int32 or assign_out.numel() < n
-                                   or assign_out.device != dev or not assign_out.is_contiguous()):
-        raise ValueError("assign_out must be a contiguous int32 [N] tensor on X's device (variants 7/8)")
+    grid = int(L.alink_kmeans_v7_grid(n, grid if grid is not None else _num_cus(dev)))
     key = (dev.index, grid)
     if key not in _BUF:
         _BUF[key] = (torch.empty((grid, HIP_KMAX, HIP_D), dtype=torch.float32, device=dev),
@@ -102,17 +86,11 @@ def assign_accumulate_hip(X: torch.Tensor, C: torch.Tensor, grid: Optional[int] 
     slab, slab_cnt = _BUF[key]
     out = torch.empty((k, HIP_D + 1), dtype=torch.float64, device=dev)
     st = _lib.stream_ptr(dev)
-    if variant in (7, 8):
-        fn = L.alink_kmeans_assign_accum_bf16_v8 if variant == 8 else L.alink_kmeans_assign_accum_bf16_v7
-        rc = fn(X.data_ptr(), n, cpad.data_ptr(), ninit.data_ptr(), k,
-                slab.data_ptr(), slab_cnt.data_ptr(), grid, st,
-                None if assign_out is None else assign_out.data_ptr(), int(mode))
-    else:
-        fn = {4: L.alink_kmeans_assign_accum_bf16_v4, 6: L.alink_kmeans_assign_accum_bf16_v6}[variant]
-        rc = fn(X.data_ptr(), n, cpad.data_ptr(), ninit.data_ptr(), k, slab.data_ptr(), slab_cnt.data_ptr(), grid,
-                st, int(DEFAULT_CONTIGUOUS if contiguous is None else contiguous))
+    rc = L.alink_kmeans_assign_accum_bf16_v7(X.data_ptr(), n, cpad.data_ptr(), ninit.data_ptr(), k, slab.data_ptr(),
+                                             slab_cnt.data_ptr(), grid, st,
+                                             None if assign_out is None else assign_out.data_ptr(), int(mode))
     if rc != 0:
-        raise RuntimeError(f"alink_kmeans_assign_accum_bf16 failed: {rc}")
+        raise RuntimeError(f"alink_kmeans_assign_accum_bf16_v7 failed: {rc}")
     rc = L.alink_kmeans_reduce_slabs(slab.data_ptr(), slab_cnt.data_ptr(), grid, k, out.data_ptr(), st)
     if rc != 0:
         raise RuntimeError(f"alink_kmeans_reduce_slabs failed: {rc}")

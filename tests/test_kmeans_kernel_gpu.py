@@ -36,16 +36,15 @@ def _own_assignment_check(X, C, got, asg, k):
         assert bool((best - chosen <= 2.0 ** -15 * best.abs() + 1e-4).all()), "non-optimal assignment"
 
 
-@pytest.mark.parametrize("variant", [7, 8])
 @pytest.mark.parametrize("n,k", [(1, 1), (63, 3), (64, 16), (65, 17), (129, 100), (1000, 33), (4097, 100),
                                  (50000, 128), (300001, 100), (123457, 112), (70001, 8)])
-def test_v7_matches_own_assignment_reference(n, k, variant):
+def test_v7_matches_own_assignment_reference(n, k):
     from alink_amd.ops import kmeans as K
     from alink_amd.ops import _lib
     assert _lib.available(), "HIP library must be built and loadable on the GPU box"
     X, C = _data(n, k)
     asg = torch.full((n,), -1, dtype=torch.int32, device="cuda")
-    got = K.assign_accumulate_hip(X, C, variant=variant, assign_out=asg)
+    got = K.assign_accumulate_hip(X, C, assign_out=asg)
     torch.cuda.synchronize()
     _own_assignment_check(X, C, got, asg, k)
     # and against an independent torch argmax: only near-ties may differ
@@ -53,39 +52,25 @@ def test_v7_matches_own_assignment_reference(n, k, variant):
     assert (got[:, -1] - ref[:, -1]).abs().sum().item() <= max(2, 1e-4 * n)
 
 
-@pytest.mark.parametrize("variant", [7, 8])
 @pytest.mark.parametrize("n,k,grid", [(200, 7, 1), (49157, 100, 3), (33333, 64, 7), (640, 100, 2), (70000, 100, 256),
                                       (1000003, 128, 5), (129, 50, 1), (192, 50, 1), (257, 20, 2)])
-def test_v7_small_grid_long_loops(n, k, grid, variant):
+def test_v7_small_grid_long_loops(n, k, grid):
     """Few workgroups -> long per-workgroup tile loops (ring warm-up, steady state, one-hot reuse, drain)."""
     from alink_amd.ops import kmeans as K
     X, C = _data(n, k, seed=11)
     asg = torch.empty((n,), dtype=torch.int32, device="cuda")
-    got = K.assign_accumulate_hip(X, C, grid=grid, variant=variant, assign_out=asg)
+    got = K.assign_accumulate_hip(X, C, grid=grid, assign_out=asg)
     torch.cuda.synchronize()
     _own_assignment_check(X, C, got, asg, k)
 
 
-@pytest.mark.parametrize("variant", [7, 8])
-def test_v7_without_assign_output_equals_with(variant):
+def test_v7_without_assign_output_equals_with():
     from alink_amd.ops import kmeans as K
     X, C = _data(100003, 100, seed=4)
-    a = K.assign_accumulate_hip(X, C, variant=variant)
+    a = K.assign_accumulate_hip(X, C)
     asg = torch.empty((X.shape[0],), dtype=torch.int32, device="cuda")
-    b = K.assign_accumulate_hip(X, C, variant=variant, assign_out=asg)
+    b = K.assign_accumulate_hip(X, C, assign_out=asg)
     assert torch.equal(a, b)
-
-
-@pytest.mark.parametrize("variant,contig", [(4, True), (6, True), (6, False)])
-@pytest.mark.parametrize("n,k", [(4097, 100), (300001, 100), (33333, 64)])
-def test_ab_variants_match_reference(n, k, variant, contig):
-    from alink_amd.ops import kmeans as K
-    X, C = _data(n, k, seed=2)
-    got = K.assign_accumulate_hip(X, C, variant=variant, contiguous=contig)
-    ref = K.assign_accumulate_torch(X, C)
-    torch.cuda.synchronize()
-    assert (got[:, -1] - ref[:, -1]).abs().sum().item() <= max(2, 1e-4 * n)
-    assert abs(got[:, -1].sum().item() - n) < 0.5
 
 
 def test_kernel_deterministic():

@@ -23,10 +23,8 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--torch", action="store_true", help="also time the PyTorch path")
     ap.add_argument("--grid", type=int, default=None)
-    ap.add_argument("--variant", type=int, default=7)
-    ap.add_argument("--strided", action="store_true", help="v4/v5: grid-strided tile schedule")
-    ap.add_argument("--load-only", action="store_true", help="v6: time the LDS-DMA load pipeline alone")
-    ap.add_argument("--compute-only", action="store_true", help="v6: time the compute alone (no loads)")
+    ap.add_argument("--load-only", action="store_true", help="time the LDS-DMA load pipeline alone")
+    ap.add_argument("--compute-only", action="store_true", help="time the compute alone (no loads)")
     a = ap.parse_args()
     dev = torch.device("cuda")
     n, d, k = a.rows, 128, a.k
@@ -40,15 +38,10 @@ def main():
         X[s:e] = (centers[lab] + torch.randn(e - s, d, device=dev, generator=g)).to(torch.bfloat16)
     C = (centers + 0.5 * torch.randn(k, d, device=dev, generator=g)).double()
     def run(Xs):
-        if a.variant in (7, 8):
-            return K.assign_accumulate_hip(Xs, C, grid=a.grid, variant=a.variant,
-                                           mode=2 if a.compute_only else 1 if a.load_only else 0)
-        return K.assign_accumulate_hip(Xs, C, grid=a.grid, variant=a.variant,
-                                       contiguous=4 if a.compute_only else (2 + a.strided) if a.load_only
-                                       else not a.strided)
+        return K.assign_accumulate_hip(Xs, C, grid=a.grid, mode=2 if a.compute_only else 1 if a.load_only else 0)
     out = run(X)
     torch.cuda.synchronize()
-    res = {"rows": n, "k": k, "variant": a.variant, "strided": a.strided, "load_only": a.load_only, "compute_only": a.compute_only}
+    res = {"rows": n, "k": k, "load_only": a.load_only, "compute_only": a.compute_only}
     if a.torch:
         ref0 = K.assign_accumulate_torch(X[:2_000_000], C)
         got0 = run(X[:2_000_000].contiguous())
