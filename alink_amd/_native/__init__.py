@@ -11,7 +11,8 @@ from typing import List, Optional, Sequence
 
 import numpy as np
 
-__all__ = ["lib", "parse_csv_lines", "murmur3_utf16", "parse_dense_vectors", "ftrl_update_csr"]
+__all__ = ["lib", "parse_csv_lines", "murmur3_utf16", "parse_dense_vectors", "ftrl_update_csr",
+           "ftrl_partial_margin", "ftrl_shard_update"]
 
 _PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libalink_native.so")
 lib = None
@@ -22,6 +23,8 @@ if os.path.exists(_PATH):
         lib.alink_murmur3_utf16_batch.restype = None
         lib.alink_parse_dense_vectors.restype = ctypes.c_int
         lib.alink_ftrl_update_csr.restype = ctypes.c_int
+        lib.alink_ftrl_partial_margin.restype = ctypes.c_int
+        lib.alink_ftrl_shard_update.restype = ctypes.c_int
     except OSError:
         lib = None
 
@@ -137,3 +140,51 @@ def ftrl_update_csr(indptr, indices, values, label, w, n, z, alpha, beta, l1, l2
     if rc != 0:
         raise ValueError("feature index out of range in FTRL update")
     return True
+
+
+def _csr(indptr, indices, values):
+    return (np.ascontiguousarray(indptr, dtype=np.int64), np.ascontiguousarray(indices, dtype=np.int32),
+            np.ascontiguousarray(values, dtype=np.float64))
+
+
+def ftrl_partial_margin(indptr, indices, values, w, lo, hi) -> np.ndarray:
+    """Per-row margin restricted to coordinates [lo, hi) (``w`` is that shard)."""
+    indptr, indices, values = _csr(indptr, indices, values)
+    nrows = len(indptr) - 1
+    out = np.zeros(nrows, dtype=np.float64)
+    if lib is None:
+        for r in range(nrows):
+            s, e = indptr[r], indptr[r + 1]
+            ii = indices[s:e].astype(np.int64)
+            m = (ii >= lo) & (ii < hi)
+            out[r] = float(np.dot(values[s:e][m], w[ii[m] - lo]))
+        return out
+    w = np.ascontiguousarray(w, dtype=np.float64)
+    lib.alink_ftrl_partial_margin(_ptr(indptr), _ptr(indices), _ptr(values), ctypes.c_int64(nrows), _ptr(w),
+                                  ctypes.c_int64(lo), ctypes.c_int64(hi), _ptr(out))
+    return out
+
+
+def ftrl_shard_update(indptr, indices, values, err, w, n, z, lo, hi, alpha, beta, l1, l2) -> None:
+    """In-place FTRL on the owned shard [lo, hi) with per-row ``err = p - y`` fixed for the micro-batch."""
+    indptr, indices, values = _csr(indptr, indices, values)
+    err = np.ascontiguousarray(err, dtype=np.float64)
+    for a in (w, n, z):
+        assert a.dtype == np.float64 and a.flags["C_CONTIGUOUS"]
+    if lib is None:
+        for r in range(len(indptr) - 1):
+            for k in range(indptr[r], indptr[r + 1]):
+                i = int(indices[k]) - lo
+                if i < 0 or i >= hi - lo:
+                    continue
+                g = err[r] * values[k]
+                nn = n[i] + g * g
+                sigma = (np.sqrt(nn) - np.sqrt(n[i])) / alpha
+                z[i] += g - sigma * w[i]
+                n[i] = nn
+                w[i] = 0.0 if abs(z[i]) <= l1 else (np.sign(z[i]) * l1 - z[i]) / (beta + np.sqrt(n[i]) / alpha + l2)
+        return
+    lib.alink_ftrl_shard_update(_ptr(indptr), _ptr(indices), _ptr(values), _ptr(err),
+                                ctypes.c_int64(len(indptr) - 1), _ptr(w), _ptr(n), _ptr(z), ctypes.c_int64(lo),
+                                ctypes.c_int64(hi), ctypes.c_double(alpha), ctypes.c_double(beta),
+                                ctypes.c_double(l1), ctypes.c_double(l2))

@@ -38,4 +38,39 @@ int alink_ftrl_update_csr(const int64_t* indptr, const int32_t* indices, const d
   return 0;
 }
 
+// Feature-sharded micro-batch FTRL (updateMode SHARDED): partial margins of every row on the owned coordinate
+// range [lo, hi) (w is the shard, indexed i - lo) ...
+int alink_ftrl_partial_margin(const int64_t* indptr, const int32_t* indices, const double* values, int64_t nrows,
+                              const double* w, int64_t lo, int64_t hi, double* margin) {
+  for (int64_t r = 0; r < nrows; ++r) {
+    double wx = 0.0;
+    for (int64_t k = indptr[r]; k < indptr[r + 1]; ++k) {
+      const int64_t i = indices[k];
+      if (i >= lo && i < hi) wx += values[k] * w[i - lo];
+    }
+    margin[r] = wx;
+  }
+  return 0;
+}
+
+// ... then the owned coordinates replay their entries in sample order with err[r] = sigmoid(margin_r) - y_r
+// (the all-reduced margins); same per-coordinate order as the GPU kernel, so both give identical bits up to libm.
+int alink_ftrl_shard_update(const int64_t* indptr, const int32_t* indices, const double* values, const double* err,
+                            int64_t nrows, double* w, double* n, double* z, int64_t lo, int64_t hi, double alpha,
+                            double beta, double l1, double l2) {
+  for (int64_t r = 0; r < nrows; ++r) {
+    for (int64_t k = indptr[r]; k < indptr[r + 1]; ++k) {
+      const int64_t i = (int64_t)indices[k] - lo;
+      if (i < 0 || i >= hi - lo) continue;
+      const double g = err[r] * values[k];
+      const double nn = n[i] + g * g;
+      const double sigma = (std::sqrt(nn) - std::sqrt(n[i])) / alpha;
+      z[i] += g - sigma * w[i];
+      n[i] = nn;
+      w[i] = std::fabs(z[i]) <= l1 ? 0.0 : ((z[i] < 0 ? -1.0 : 1.0) * l1 - z[i]) / (beta + std::sqrt(n[i]) / alpha + l2);
+    }
+  }
+  return 0;
+}
+
 }  // extern "C"

@@ -1,4 +1,5 @@
 from .vector import DenseVector, SparseVector, Vector, VectorUtil, VectorIterator
 from .matrix import DenseMatrix
+from .block import SparseBlock
 
-__all__ = ["DenseVector", "SparseVector", "Vector", "VectorUtil", "VectorIterator", "DenseMatrix"]
+__all__ = ["DenseVector", "SparseVector", "Vector", "VectorUtil", "VectorIterator", "DenseMatrix", "SparseBlock"]

@@ -17,7 +17,7 @@ from typing import Any, Iterable, List, Optional, Sequence, Union
 import numpy as np
 import torch
 
-from .linalg import DenseVector, SparseVector, Vector, VectorUtil
+from .linalg import DenseVector, SparseBlock, SparseVector, Vector, VectorUtil
 from .types import TableSchema, Types, AlinkType, is_numeric, schema_str_to_schema
 
 __all__ = ["Row", "Column", "MTable", "infer_type"]
@@ -97,6 +97,11 @@ class Column:
 
     def to_list(self) -> List[Any]:
         v = self.values
+        if isinstance(v, SparseBlock):
+            lst = v.to_list()
+            if self.nulls is not None:
+                lst = [None if m else x for x, m in zip(lst, self.nulls.cpu().tolist())]
+            return lst
         if isinstance(v, torch.Tensor):
             if v.dim() == 2:
                 arr = v.detach().to("cpu", torch.float64).numpy()
@@ -111,6 +116,11 @@ class Column:
     def take(self, idx) -> "Column":
         """Row selection by index tensor/list or boolean mask."""
         v = self.values
+        if isinstance(v, SparseBlock):
+            nn = None
+            if self.nulls is not None:
+                nn = Column(self.nulls.cpu()).take(idx).values
+            return Column(v.take(idx), nn)
         if isinstance(v, torch.Tensor):
             if isinstance(idx, torch.Tensor):
                 ii = idx.to(v.device)
@@ -136,6 +146,12 @@ class Column:
     def concat(cols: List["Column"]) -> "Column":
         if not cols:
             return Column([])
+        if all(isinstance(c.values, SparseBlock) for c in cols):
+            nulls = None
+            if any(c.nulls is not None for c in cols):
+                nulls = torch.cat([c.nulls.cpu() if c.nulls is not None else torch.zeros(len(c), dtype=torch.bool)
+                                   for c in cols])
+            return Column(SparseBlock.concat([c.values for c in cols]), nulls)
         if all(isinstance(c.values, torch.Tensor) for c in cols) and len({c.values.dim() for c in cols}) == 1:
             dev = cols[0].values.device
             vals = torch.cat([c.values.to(dev) for c in cols])

@@ -19,7 +19,7 @@ from typing import List, Optional, Sequence, Tuple
 import numpy as np
 import torch
 
-from ...common.linalg import DenseVector, SparseVector, VectorUtil
+from ...common.linalg import DenseVector, SparseBlock, SparseVector, VectorUtil
 from ...common.table import MTable
 from ...common.types import Types, is_numeric
 from ...parallel import comm
@@ -238,6 +238,10 @@ def extract_features(mt: MTable, feature_cols: Optional[Sequence[str]], vector_c
     if vector_col:
         c = mt.col(vector_col)
         v = c.values
+        if isinstance(v, SparseBlock):       # columnar CSR (GPU feature path): no host round trip
+            d = max(v.size, vector_size or 0)
+            return FeatureMatrix(crow=v.crow.to(device), col=v.col.to(device=device, dtype=torch.int64),
+                                 val=v.val.to(device=device, dtype=dtype), ncols=d)
         if isinstance(v, torch.Tensor) and v.dim() == 2:
             fm = FeatureMatrix(v.to(device=device, dtype=dtype))
             return fm.set_ncols(vector_size) if vector_size else fm

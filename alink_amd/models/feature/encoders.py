@@ -273,20 +273,30 @@ class _EncodeSpec:
                     col.append(SparseVector(size) if ii is None else SparseVector(size, [ii], [1.0]))
                 out.append(Column(col))
             return out
+        # ASSEMBLED_VECTOR: global index = column offset + (drop-last adjusted) bucket, on the env's device
+        from ...ops.feature import csr_assemble
         total = self.assembled_size()
-        col = []
-        for r in range(n):
-            if not valid[r].all():
-                col.append(None)
-                continue
-            ind, start = [], 0
-            for j in range(k):
-                size, ii = self._size_index(j, int(idx[r, j]))
-                if ii is not None:
-                    ind.append(start + ii)
-                start += size
-            col.append(SparseVector(total, ind, [1.0] * len(ind)))
-        return [Column(col)]
+        gidx = np.zeros((k, n), dtype=np.int64)
+        keep = np.zeros((k, n), dtype=bool)
+        start = 0
+        for j in range(k):
+            b = idx[:, j]
+            vs = self.vector_size[j]
+            if self.drop_last:
+                d = self.drop_index[j]
+                size = vs - 1
+                keep[j] = b != d if d is not None else True
+                gidx[j] = start + (np.where(b > d, b - 1, b) if d is not None else b)
+            else:
+                size = vs
+                keep[j] = True
+                gidx[j] = start + b
+            start += size
+        row_ok = valid.all(1)
+        keep &= row_ok[None, :]
+        dev = feature_device()
+        blk = csr_assemble(torch.from_numpy(gidx).to(dev), None, torch.from_numpy(keep).to(dev), total)
+        return [Column(blk, None if row_ok.all() else torch.from_numpy(~row_ok))]
 
 
 # ---------------------------------------------------------------------------------------------------
@@ -333,33 +343,39 @@ class OneHotModelMapper(ModelMapper):
             self.spec.drop_index.append(0 if self.spec.drop_last else None)
 
     def _map_columns(self, mt):
+        """Token lookup per distinct value (pandas factorize: one dict probe per unique token, then a vectorised
+        gather), invalid/else strategies on whole arrays; the assembled vector is built on the env's device by
+        the CSR assembler (``ops/csrc/feature.hip``)."""
+        import pandas as pd
         n, k = mt.num_rows, len(self.cols)
         idx = np.zeros((n, k), dtype=np.int64)
         valid = np.ones((n, k), dtype=bool)
         inv, ee = self.spec.invalid, self.enable_else
         for j, (c, m) in enumerate(zip(self.cols, self.maps)):
             vs = self.spec.vector_size[j]
-            for r, v in enumerate(mt.col(c).to_list()):
-                got = None if v is None else m.get(java_str(v))
-                if got is not None:
-                    idx[r, j] = got
-                    continue
-                if ee and inv == "KEEP":
-                    idx[r, j] = vs - 2 if v is None else vs - 1
-                elif ee:
-                    if v is None:
-                        if inv == "SKIP":
-                            valid[r, j] = False
-                        else:
-                            raise RuntimeError("Input is null!")
-                    else:
-                        idx[r, j] = vs - 1
-                elif inv == "KEEP":
-                    idx[r, j] = vs - 1
-                elif inv == "SKIP":
-                    valid[r, j] = False
-                else:
-                    raise RuntimeError(f"Unseen token: {v}")
+            vals = mt.col(c).to_list()
+            codes, uniq = pd.factorize(pd.Series(vals, dtype=object), use_na_sentinel=True)
+            look = np.asarray([m.get(java_str(u), -1) for u in uniq], dtype=np.int64)
+            got = np.where(codes >= 0, look[np.maximum(codes, 0)] if look.size else -1, -1)
+            is_null = codes < 0
+            unseen = (got < 0) & ~is_null
+            idx[:, j] = np.maximum(got, 0)
+            if ee and inv == "KEEP":
+                idx[is_null, j] = vs - 2
+                idx[unseen, j] = vs - 1
+            elif ee:
+                if is_null.any():
+                    if inv != "SKIP":
+                        raise RuntimeError("Input is null!")
+                    valid[is_null, j] = False
+                idx[unseen, j] = vs - 1
+            elif inv == "KEEP":
+                idx[is_null | unseen, j] = vs - 1
+            elif inv == "SKIP":
+                valid[is_null | unseen, j] = False
+            elif (is_null | unseen).any():
+                bad = vals[int(np.nonzero(is_null | unseen)[0][0])]
+                raise RuntimeError(f"Unseen token: {bad}")
         return self.spec.columns(idx, valid)
 
 
@@ -564,29 +580,40 @@ class FeatureHasherMapper(Mapper):
         self.num_index = murmur3_index(self.num, self.nf) if self.num else np.zeros(0, dtype=np.int64)
 
     def _map_columns(self, mt):
+        """Columnar: one [m, n] entry matrix (numeric: fixed index hash(colName), value; categorical:
+        hash("col=val"), 1.0), hashed and assembled into a row-sorted CSR ``SparseBlock`` on the env's device
+        (``ops/csrc/feature.hip`` on a GPU) — no per-row Python objects."""
+        from ...ops.feature import csr_assemble, murmur3_index
+        dev = feature_device()
         n = mt.num_rows
-        rows_i: List[List[int]] = [[] for _ in range(n)]
-        rows_v: List[List[float]] = [[] for _ in range(n)]
+        m = len(self.num) + len(self.cat)
+        idx = torch.zeros((m, n), dtype=torch.int64, device=dev)
+        val = torch.ones((m, n), dtype=torch.float64, device=dev)
+        valid = torch.zeros((m, n), dtype=torch.bool, device=dev)
         for j, c in enumerate(self.num):
             v, null = _column_array(mt, c)
-            for r in np.nonzero(~null)[0]:
-                rows_i[r].append(int(self.num_index[j]))
-                rows_v[r].append(float(v[r]))
-        for c in self.cat:
+            idx[j] = int(self.num_index[j])
+            val[j] = torch.from_numpy(v).to(dev)
+            valid[j] = torch.from_numpy(~null).to(dev)
+        for j, c in enumerate(self.cat, start=len(self.num)):
             vals = mt.col(c).to_list()
-            present = [r for r, v in enumerate(vals) if v is not None]
-            keys = [c + "=" + java_str(vals[r]) for r in present]
-            idx = murmur3_index(keys, self.nf) if keys else []
-            for r, ii in zip(present, idx):
-                rows_i[r].append(int(ii))
-                rows_v[r].append(1.0)
-        out = []
-        for ii, vv in zip(rows_i, rows_v):
-            acc: Dict[int, float] = {}
-            for a, b in zip(ii, vv):
-                acc[a] = acc.get(a, 0.0) + b
-            out.append(SparseVector(self.nf, acc))
-        return [Column(out)]
+            present = np.asarray([v is not None for v in vals], dtype=bool)
+            if present.any():
+                keys = [java_str(v) for v in vals if v is not None]
+                pos = torch.from_numpy(np.nonzero(present)[0]).to(dev)
+                idx[j, pos] = murmur3_index(keys, self.nf, prefix=c + "=", device=dev).to(dev)
+                valid[j, pos] = True
+        return [Column(csr_assemble(idx, val, valid, self.nf))]
+
+
+def feature_device() -> torch.device:
+    """Device of the default environment when it is a GPU with the HIP library, else the host."""
+    from ...common.mlenv import MLEnvironmentFactory
+    from ...ops import _lib
+    dev = MLEnvironmentFactory.getDefault().device
+    if dev.type == "cuda" and (_lib.available() or not _lib.torch_fallback_allowed()):
+        return dev
+    return torch.device("cpu")
 
 
 class DCTMapper(SISOMapper):

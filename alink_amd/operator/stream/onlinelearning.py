@@ -11,8 +11,7 @@ sample, every ``timeInterval`` seconds and when the stream ends.  Snapshot rows 
 
 Deviation: the reference scales each gradient by ``1/sqrt(ms between the forward and the feedback pass)``
 (``FtrlTrainStreamOp.java:428``), a wall-clock artefact of its Flink feedback loop; here the scale is 1.
-With more than one rank the coefficient vector is sharded by feature range (SURVEY P4) only for the margin;
-each rank applies the identical update to the full vector after an all-gather of the micro-batch.
+Multi-rank: see ``FtrlTrainStreamOp`` (replicated SEQUENTIAL, feature-sharded SHARDED).
 """
 from __future__ import annotations
 
@@ -63,11 +62,27 @@ def _ftrl_python(indptr, indices, values, label, w, n, z, alpha, beta, l1, l2):
 
 
 class FtrlTrainStreamOp(StreamOperator):
-    """``updateMode``: ``SEQUENTIAL`` (default; the native host loop, sample order as the reference) or
-    ``HOGWILD`` (the micro-batch is applied on the GPU by ``ops/csrc/ftrl.hip``, one wave per sample, with the
-    model state resident in HBM; needs a GPU)."""
-    EXTRA_PARAMS = [ParamInfo("updateMode", str, "SEQUENTIAL or HOGWILD (GPU, one wave per sample)",
-                              default="SEQUENTIAL")]
+    """Online FTRL-proximal logistic regression (``FtrlTrainStreamOp.java``).
+
+    ``updateMode``:
+
+    * ``SEQUENTIAL`` (default): sample-by-sample rule in stream order (native host loop).  With P ranks every
+      step all-gathers the ranks' micro-batches (rank order) and every rank applies the identical update to a
+      replicated coefficient vector, so the model equals the 1-rank model on the same global batch sequence.
+    * ``SHARDED``: the reference's distributed design (``FtrlTrainStreamOp.java:72-85`` split info,
+      ``:174-267`` SplitVector, ``:396-420`` partial margins, ``:488-567`` keyed reduce + feedback) at micro-batch
+      granularity: rank r owns the coefficient range [lo_r, hi_r); per step the ranks all-gather the micro-batch,
+      compute partial margins on their range (HIP kernel on GPU), all-reduce them, and replay their coordinates
+      in sample order with the margins of the step start — the reference's feedback staleness bounded to one
+      micro-batch.  Deterministic and independent of the number of ranks.
+    * ``HOGWILD`` (single GPU): ``ops/csrc/ftrl.hip``, one wave per sample, exact atomic n/z, prox pass.
+
+    Every step (and every snapshot decision) is a collective over the ranks, so ranks with different numbers of
+    micro-batches stay in lockstep: a rank whose stream ended keeps joining steps with an empty batch until all
+    ranks are done.  Snapshots: at the first step, whenever any rank's ``timeInterval`` elapsed, and at the end.
+    """
+    EXTRA_PARAMS = [ParamInfo("updateMode", str, "SEQUENTIAL, SHARDED (feature-sharded micro-batch) or HOGWILD "
+                                                 "(GPU, one wave per sample)", default="SEQUENTIAL")]
 
     def __init__(self, model=None, params: Optional[Params] = None, **kw):
         if isinstance(model, Params):
@@ -78,6 +93,7 @@ class FtrlTrainStreamOp(StreamOperator):
         self._init_model = model
 
     def linkFrom(self, *inputs):
+        import torch
         (inp,) = self._connect(*inputs)
         p = self.getParams()
         mt = _model_rows(self._init_model)
@@ -87,9 +103,8 @@ class FtrlTrainStreamOp(StreamOperator):
         self._conv = LinearModelDataConverter(self._label_type)
         base = self._conv.getModelSchema()
         self._schema = TableSchema(["bid", "ntab"] + list(base.names), [Types.LONG, Types.LONG] + list(base.types))
-        self._w = np.array(self._model.coefVector.data, dtype=np.float64)
-        self._n = np.zeros_like(self._w)
-        self._z = np.zeros_like(self._w)
+        w0 = np.array(self._model.coefVector.data, dtype=np.float64)
+        self._dim = int(w0.size)
         self._bid = 0
         self._first = True
         self._t0 = time.time()
@@ -102,80 +117,168 @@ class FtrlTrainStreamOp(StreamOperator):
         self._vec_col = _pget(p, "vectorCol")
         self._feat_cols = _pget(p, "featureCols")
         self._vsize = _pget(p, "vectorSize")
-        self._hogwild = str(_pget(p, "updateMode", "SEQUENTIAL")).upper() == "HOGWILD"
-        self._dev_state = None
+        self._mode = str(_pget(p, "updateMode", "SEQUENTIAL")).upper()
+        if self._mode not in ("SEQUENTIAL", "SHARDED", "HOGWILD"):
+            raise ValueError(f"unknown updateMode {self._mode}")
+        self._ws, self._rank = comm.get_world_size(), comm.get_rank()
+        if self._mode == "HOGWILD" and self._ws > 1:
+            raise ValueError("updateMode HOGWILD is single-rank; use SHARDED for P > 1")
+        # SEQUENTIAL keeps its state on the host (the rule is a serial loop); the others on the rank's GPU
+        gpu = self.env.device.type == "cuda" and self._mode != "SEQUENTIAL"
+        self._dev = self.env.device if gpu else torch.device("cpu")
+        if self._mode == "HOGWILD" and self._dev.type != "cuda":
+            raise RuntimeError("FTRL updateMode HOGWILD needs a GPU")
+        # owned coordinate range (the whole vector unless SHARDED)
+        if self._mode == "SHARDED":
+            per = -(-self._dim // self._ws)
+            self._lo, self._hi = min(self._dim, self._rank * per), min(self._dim, (self._rank + 1) * per)
+        else:
+            self._lo, self._hi = 0, self._dim
+        shard = w0[self._lo:self._hi].copy()
+        if self._dev.type == "cuda":
+            self._state = [torch.as_tensor(a, device=self._dev).clone() for a in (shard, np.zeros_like(shard),
+                                                                                  np.zeros_like(shard))]
+        else:
+            self._state = [shard, np.zeros_like(shard), np.zeros_like(shard)]
         _register_upstream_sources(inp)
         return self
 
+    # ---------------------------------------------------------------- model state
+    def _full_w(self) -> np.ndarray:
+        import torch
+        w = self._state[0]
+        if self._mode != "SHARDED" or self._ws == 1:
+            return (w.cpu().numpy() if isinstance(w, torch.Tensor) else w).copy()
+        per = -(-self._dim // self._ws)
+        t = torch.as_tensor(w, dtype=torch.float64)
+        pad = torch.zeros(per, dtype=torch.float64, device=t.device)
+        pad[:t.shape[0]] = t
+        full = comm.all_gather_tensor(pad if comm._backend() == "nccl" and pad.is_cuda else pad.cpu())
+        return full.cpu().numpy()[:self._dim].copy()
+
     def _snapshot(self):
-        if self._dev_state is not None:
-            self._w = self._dev_state[0].cpu().numpy().copy()
+        w = self._full_w()
         m = self._model
-        m.coefVector = DenseVector(self._w.copy())
+        m.coefVector = DenseVector(w)
         m.hasInterceptItem = self._intercept
         m.vectorColName = self._vec_col
         m.featureNames = list(self._feat_cols) if self._feat_cols else None
         m.modelName = "Logistic Regression"
-        m.vectorSize = self._w.size - 1 if self._intercept else self._w.size
+        m.vectorSize = w.size - 1 if self._intercept else w.size
         rows = self._conv.save(m)
         out = [(self._bid, len(rows)) + tuple(r) for r in rows]
         self._bid += 1
         self._emit(MTable.from_rows(out, self._schema))
 
+    # ---------------------------------------------------------------- stream protocol
     def on_batch(self, port, mt):
+        self._step(mt if mt.num_rows else None)
+
+    def on_finish(self, port):
+        while self._step(None):
+            pass
+        self._snapshot()
+
+    def _step(self, mt) -> bool:
+        """One lockstep step over the ranks; False once every rank's stream has ended (nothing applied)."""
+        import torch
+        csr = self._local_csr(mt) if mt is not None else None
+        due = time.time() - self._t0 > self._interval
+        flags = torch.tensor([0 if csr is None else 1, 1 if due else 0], dtype=torch.int64)
+        if self._ws > 1:
+            flags = comm.all_reduce(flags.to(self._comm_dev()), "max").cpu()
+        active, due = bool(flags[0]), bool(flags[1])
+        if not active:
+            return False
         if self._first:
             self._snapshot()
             self._first = False
-        if mt.num_rows:
-            self._update(mt)
-        if time.time() - self._t0 > self._interval:
+        batch = self._gather(csr) if self._ws > 1 else csr
+        if batch is not None and batch[0].shape[0] > 1:
+            self._apply(*batch)
+        if due:
             self._t0 = time.time()
             self._snapshot()
+        return True
 
-    def on_finish(self, port):
-        self._snapshot()
+    def _comm_dev(self):
+        import torch
+        return self._dev if (comm._backend() == "nccl" and self._dev.type == "cuda") else torch.device("cpu")
 
-    def _update(self, mt: MTable):
+    def _gather(self, csr):
+        """All-gather the ranks' CSR micro-batches in rank order (empty for finished ranks)."""
+        import torch
+        cd = self._comm_dev()
+        if csr is None:
+            csr = (torch.zeros(1, dtype=torch.int64), torch.zeros(0, dtype=torch.int32),
+                   torch.zeros(0, dtype=torch.float64), torch.zeros(0, dtype=torch.float64))
+        indptr, idx, val, lab = (t.to(cd) for t in csr)
+        lens = comm.all_gather_varlen(indptr[1:] - indptr[:-1])
+        gidx = comm.all_gather_varlen(idx)
+        gval = comm.all_gather_varlen(val)
+        glab = comm.all_gather_varlen(lab)
+        gptr = torch.zeros(lens.shape[0] + 1, dtype=torch.int64, device=lens.device)
+        torch.cumsum(lens, 0, out=gptr[1:])
+        return tuple(t.to(self._dev) for t in (gptr, gidx, gval, glab))
+
+    def _local_csr(self, mt: MTable):
         import torch
         p = self.getParams()
-        fm = extract_features(mt, self._feat_cols if self._vec_col is None else None, self._vec_col,
-                              torch.device("cpu"), vector_size=self._vsize)
+        fm = extract_features(mt, self._feat_cols if self._vec_col is None else None, self._vec_col, self._dev,
+                              vector_size=self._vsize)
         if self._intercept:
             fm = fm.prefix_one()
         if fm.is_sparse:
-            indptr = fm.crow.cpu().numpy()
-            indices = fm.col.cpu().numpy()
-            values = fm.val.cpu().double().numpy()
+            indptr, indices, values = fm.crow.to(torch.int64), fm.col.to(torch.int32), fm.val.to(torch.float64)
         else:
-            X = fm.to_dense().double().numpy()
+            X = fm.to_dense().to(torch.float64)
             nrow, d = X.shape
-            indptr = np.arange(nrow + 1, dtype=np.int64) * d
-            indices = np.tile(np.arange(d, dtype=np.int32), nrow)
+            indptr = torch.arange(nrow + 1, dtype=torch.int64, device=X.device) * d
+            indices = torch.arange(d, dtype=torch.int32, device=X.device).repeat(nrow)
             values = X.reshape(-1)
         l0 = self._model.labelValues[0]
-        labels = []
-        for v in mt.column_values(p.get("labelCol")):
+        col = mt.col(p.get("labelCol"))
+        if isinstance(col.values, torch.Tensor) and isinstance(l0, (int, float)) and not isinstance(l0, bool):
+            labels = (col.values.to(torch.float64) == float(l0)).to(torch.float64)
+        else:
+            vals = col.to_list()
             if isinstance(l0, (int, float)) and not isinstance(l0, bool):
-                labels.append(1.0 if float(v) == float(l0) else 0.0)
+                labels = torch.tensor([1.0 if float(v) == float(l0) else 0.0 for v in vals], dtype=torch.float64)
             else:
-                labels.append(1.0 if str(v) == str(l0) else 0.0)
-        if indices.size and int(indices.max()) >= self._w.size:
+                labels = torch.tensor([1.0 if str(v) == str(l0) else 0.0 for v in vals], dtype=torch.float64)
+        if indices.numel() and int(indices.max()) >= self._dim:
             raise ValueError("feature index out of range of the initial model")
-        if self._hogwild:
+        return (indptr.contiguous(), indices.contiguous(), values.contiguous(),
+                labels.to(indptr.device).contiguous())
+
+    def _apply(self, indptr, idx, val, lab):
+        import torch
+        a, b, l1, l2 = self._alpha, self._beta, self._l1, self._l2
+        w, n, z = self._state
+        if self._mode == "HOGWILD":
             from ...ops.ftrl import ftrl_hogwild
-            if not torch.cuda.is_available():
-                raise RuntimeError("FTRL updateMode HOGWILD needs a GPU")
-            if self._dev_state is None:
-                dev = torch.device("cuda", torch.cuda.current_device())
-                self._dev_state = [torch.as_tensor(a, device=dev).clone() for a in (self._w, self._n, self._z)]
-            ftrl_hogwild(torch.as_tensor(indptr), torch.as_tensor(indices), torch.as_tensor(values),
-                         torch.as_tensor(np.asarray(labels, dtype=np.float64)), *self._dev_state,
-                         self._alpha, self._beta, self._l1, self._l2)
+            ftrl_hogwild(indptr, idx, val, lab, w, n, z, a, b, l1, l2)
             return
-        if not _native.ftrl_update_csr(indptr, indices, values, np.asarray(labels), self._w, self._n, self._z,
-                                       self._alpha, self._beta, self._l1, self._l2):
-            _ftrl_python(indptr, indices, values, labels, self._w, self._n, self._z, self._alpha, self._beta,
-                         self._l1, self._l2)
+        if self._mode == "SEQUENTIAL":
+            args = (indptr.numpy(), idx.numpy(), val.numpy(), lab.numpy())
+            if not _native.ftrl_update_csr(*args, w, n, z, a, b, l1, l2):
+                _ftrl_python(*args, w, n, z, a, b, l1, l2)
+            return
+        # SHARDED: partial margins on the owned range -> all-reduce -> per-coordinate replay
+        if isinstance(w, torch.Tensor):
+            from ...ops.ftrl import ftrl_partial_margin_hip, ftrl_shard_update_hip
+            margin = ftrl_partial_margin_hip(indptr, idx, val, w, self._lo, self._hi)
+            if self._ws > 1:
+                margin = comm.all_reduce(margin.to(self._comm_dev()), "sum").to(self._dev)
+            err = (torch.sigmoid(margin) - lab).contiguous()
+            ftrl_shard_update_hip(indptr, idx, val, err, w, n, z, self._lo, self._hi, a, b, l1, l2)
+        else:
+            args = (indptr.numpy(), idx.numpy(), val.numpy())
+            margin = torch.from_numpy(_native.ftrl_partial_margin(*args, w, self._lo, self._hi))
+            if self._ws > 1:
+                margin = comm.all_reduce(margin, "sum")
+            err = (1.0 / (1.0 + np.exp(-margin.numpy()))) - lab.numpy()
+            _native.ftrl_shard_update(*args, err, w, n, z, self._lo, self._hi, a, b, l1, l2)
 
 
 class FtrlPredictStreamOp(StreamOperator):

@@ -1,0 +1,184 @@
+// Feature hot path on CDNA4 (gfx950 / MI355X): Guava-exact murmur3 feature hashing (K26) and the per-row CSR
+// assembler behind FeatureHasher / OneHot / VectorAssembler (K24/K25).
+//
+//   * murmur3: one lane per string, Guava Murmur3_32HashFunction(0).hashUnencodedChars over UTF-16 code units
+//     (chars taken in pairs, low unit first; odd tail unit mixed alone; fmix with 2 * length) of the virtual
+//     string prefix ++ value, so "col=" + value needs no host concatenation.  Output: floorMod(abs(h), nf) with
+//     Java int semantics (abs(INT_MIN) stays negative) — reference FeatureHasherMapper.java:104-106.
+//   * CSR assembler: one 64-lane wave per row, lane j holds the row's entry from input column j (m <= 64):
+//     bitonic sort by (index, column) in registers (__shfl_xor), duplicate indices merged by a segmented suffix
+//     scan (TreeMap.put(index, old + value) of the reference), heads compacted with a ballot prefix count.
+//     Two passes (count -> host cumsum -> write) give row-sorted, unique-index CSR directly on the device.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace {
+
+__device__ __forceinline__ uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+
+__device__ __forceinline__ uint32_t mix_k1(uint32_t k1) {
+    k1 *= 0xcc9e2d51u;
+    k1 = rotl32(k1, 15);
+    return k1 * 0x1b873593u;
+}
+
+__device__ __forceinline__ uint32_t mix_h1(uint32_t h1, uint32_t k1) {
+    h1 ^= k1;
+    h1 = rotl32(h1, 13);
+    return h1 * 5u + 0xe6546b64u;
+}
+
+__device__ __forceinline__ uint32_t fmix(uint32_t h1, uint32_t len_bytes) {
+    h1 ^= len_bytes;
+    h1 ^= h1 >> 16;
+    h1 *= 0x85ebca6bu;
+    h1 ^= h1 >> 13;
+    h1 *= 0xc2b2ae35u;
+    h1 ^= h1 >> 16;
+    return h1;
+}
+
+__global__ __launch_bounds__(256) void murmur3_index_kernel(const uint16_t* __restrict__ units,
+                                                           const int64_t* __restrict__ off, int64_t n,
+                                                           const uint16_t* __restrict__ prefix, int plen,
+                                                           uint32_t seed, int64_t nf, int32_t* __restrict__ hash_out,
+                                                           int32_t* __restrict__ index_out) {
+    for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n; s += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t b = off[s];
+        const int64_t len = (int64_t)plen + (off[s + 1] - b);
+        auto ch = [&](int64_t j) -> uint32_t { return j < plen ? prefix[j] : units[b + j - plen]; };
+        uint32_t h1 = seed;
+        for (int64_t i = 1; i < len; i += 2) h1 = mix_h1(h1, mix_k1(ch(i - 1) | (ch(i) << 16)));
+        if (len & 1) h1 ^= mix_k1(ch(len - 1));
+        const int32_t h = (int32_t)fmix(h1, (uint32_t)(2 * len));
+        if (hash_out != nullptr) hash_out[s] = h;
+        if (index_out != nullptr) {
+            const int64_t a = h == INT32_MIN ? (int64_t)INT32_MIN : (h < 0 ? -(int64_t)h : (int64_t)h);
+            int64_t r = a % nf;                          // Math.floorMod(int, int)
+            if (r < 0) r += nf;
+            index_out[s] = (int32_t)r;
+        }
+    }
+}
+
+constexpr int32_t KEY_NONE = 0x7fffffff;
+
+// sort (key, tag) ascending across the wave with the value riding along; tag = input column (stable order)
+__device__ __forceinline__ void wave_bitonic_sort(int32_t& key, int32_t& tag, double& v, int lane) {
+#pragma unroll
+    for (int k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            const int32_t ok = __shfl_xor(key, j);
+            const int32_t ot = __shfl_xor(tag, j);
+            const double ov = __shfl_xor(v, j);
+            const bool up = (lane & k) == 0;                 // ascending block
+            const bool lower = (lane & j) == 0;              // this lane keeps the smaller of the pair
+            const bool other_less = ok < key || (ok == key && ot < tag);
+            const bool take = lower == up ? other_less : !other_less;
+            if (take) {
+                key = ok;
+                tag = ot;
+                v = ov;
+            }
+        }
+    }
+}
+
+// one row per wave: returns (in registers) the sorted, merged entry of this lane and whether it is a head
+__device__ __forceinline__ bool row_entries(int64_t r, int64_t n, int m, const int32_t* __restrict__ idx,
+                                            const double* __restrict__ val, const uint8_t* __restrict__ valid,
+                                            int lane, int32_t& key, double& sum) {
+    int32_t k = KEY_NONE, tag = lane;
+    double v = 0.0;
+    if (lane < m) {
+        const int64_t p = (int64_t)lane * n + r;
+        if (valid == nullptr || valid[p]) {
+            k = idx[p];
+            v = val != nullptr ? val[p] : 1.0;
+        }
+    }
+    wave_bitonic_sort(k, tag, v, lane);
+    // segmented suffix sum over runs of equal keys (sorted -> runs are contiguous)
+    double s = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const double t = __shfl_down(s, o);
+        const int32_t k2 = __shfl_down(k, o);
+        if (lane + o < 64 && k2 == k) s += t;
+    }
+    const int32_t kp = __shfl_up(k, 1);
+    key = k;
+    sum = s;
+    return k != KEY_NONE && (lane == 0 || kp != k);
+}
+
+__global__ __launch_bounds__(256) void csr_count_kernel(int64_t n, int m, const int32_t* __restrict__ idx,
+                                                       const uint8_t* __restrict__ valid, int64_t* __restrict__ cnt) {
+    const int lane = threadIdx.x & 63;
+    const int64_t w0 = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
+    for (int64_t r = w0; r < n; r += nw) {
+        int32_t key;
+        double s;
+        const bool head = row_entries(r, n, m, idx, nullptr, valid, lane, key, s);
+        const uint64_t heads = __ballot(head);
+        if (lane == 0) cnt[r] = __popcll(heads);
+    }
+}
+
+__global__ __launch_bounds__(256) void csr_write_kernel(int64_t n, int m, const int32_t* __restrict__ idx,
+                                                       const double* __restrict__ val,
+                                                       const uint8_t* __restrict__ valid,
+                                                       const int64_t* __restrict__ crow, int32_t* __restrict__ col,
+                                                       double* __restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t w0 = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
+    for (int64_t r = w0; r < n; r += nw) {
+        int32_t key;
+        double s;
+        const bool head = row_entries(r, n, m, idx, val, valid, lane, key, s);
+        const uint64_t heads = __ballot(head);
+        const int pos = __popcll(heads & ((1ull << lane) - 1ull));
+        if (head) {
+            col[crow[r] + pos] = key;
+            out[crow[r] + pos] = s;
+        }
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+// floorMod(abs(murmur3_32(seed).hashUnencodedChars(prefix + s_i)), nf) for n strings given as UTF-16 code units
+// (units, off[n+1]); hash_out / index_out nullable.
+int alink_murmur3_index(const uint16_t* units, const int64_t* off, int64_t n, const uint16_t* prefix, int plen,
+                        uint32_t seed, int64_t nf, int32_t* hash_out, int32_t* index_out, void* stream) {
+    if (n <= 0) return 0;
+    if (nf <= 0 || plen < 0) return 1;
+    const int64_t blocks = (n + 255) / 256;
+    hipLaunchKernelGGL(murmur3_index_kernel, dim3(blocks < 8192 ? blocks : 8192), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), units, off, n, prefix, plen, seed, nf, hash_out,
+                       index_out);
+    return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+// CSR rows from m <= 64 column-major entry arrays idx/val/valid [m][n] (val nullable -> 1.0, valid nullable ->
+// all valid): pass 1 (out == nullptr) writes cnt[n]; pass 2 writes col/out at crow (cumsum of cnt).
+int alink_csr_assemble(int64_t n, int m, const int32_t* idx, const double* val, const uint8_t* valid, int64_t* cnt,
+                       const int64_t* crow, int32_t* col, double* out, void* stream) {
+    if (n <= 0) return 0;
+    if (m < 1 || m > 64) return 1;
+    const int64_t blocks = (n + 3) / 4;
+    const dim3 grid(blocks < 16384 ? blocks : 16384);
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (out == nullptr)
+        hipLaunchKernelGGL(csr_count_kernel, grid, dim3(256), 0, st, n, m, idx, valid, cnt);
+    else
+        hipLaunchKernelGGL(csr_write_kernel, grid, dim3(256), 0, st, n, m, idx, val, valid, crow, col, out);
+    return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+}  // extern "C"

@@ -60,6 +60,77 @@ __global__ __launch_bounds__(THREADS) void ftrl_hogwild_kernel(const int64_t* __
     }
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// Feature-sharded micro-batch FTRL (updateMode SHARDED; reference FtrlTrainStreamOp.java:174-267
+// SplitVector, :396-420 partial margins, :488-567 keyed reduce + feedback).  Rank r owns coordinates [lo, hi).
+//   1. partial margin of every sample of the (all-gathered) micro-batch on the owned range (one wave per row);
+//      the host all-reduces the margins over the ranks;
+//   2. every owned coordinate replays its entries in sample order (entries pre-sorted by coordinate, stable):
+//      one lane per coordinate, the recurrence is sequential per coordinate and independent across them, so
+//      the result does not depend on the number of ranks or on thread scheduling (deterministic).
+// ---------------------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(THREADS) void ftrl_partial_margin_kernel(const int64_t* __restrict__ indptr,
+                                                                     const int32_t* __restrict__ idx,
+                                                                     const double* __restrict__ val, int64_t nrows,
+                                                                     const double* __restrict__ w, int64_t lo,
+                                                                     int64_t hi, double* __restrict__ margin) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = (int64_t)blockIdx.x * WAVES + (threadIdx.x >> 6);
+    const int64_t nwaves = (int64_t)gridDim.x * WAVES;
+    for (int64_t r = wave; r < nrows; r += nwaves) {
+        const int64_t s = indptr[r], e = indptr[r + 1];
+        double wx = 0.0;
+        for (int64_t k = s + lane; k < e; k += 64) {
+            const int64_t i = idx[k];
+            if (i >= lo && i < hi) wx = fma(val[k], w[i - lo], wx);
+        }
+        for (int off = 32; off > 0; off >>= 1) wx += __shfl_xor(wx, off);
+        if (lane == 0) margin[r] = wx;
+    }
+}
+
+// seg[nseg+1]: boundaries into the coordinate-sorted entry order; g[t] = err[row] * x (gathered for the
+// sorted order in one parallel pass beforehand), coord[q] = the segment's coordinate.  The serial part is then
+// a walk over a contiguous g run: the n / sqrt / denominator chain does not depend on z, so unrolled steps
+// overlap it with the z recurrence.  State arrays are the owned shard (index - lo).
+__global__ __launch_bounds__(256) void ftrl_coord_update_kernel(const int64_t* __restrict__ seg, int64_t nseg,
+                                                               const int64_t* __restrict__ coord,
+                                                               const double* __restrict__ g, double* w, double* n,
+                                                               double* z, int64_t lo, double alpha, double beta,
+                                                               double l1, double l2) {
+    const double ia = 1.0 / alpha;
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nseg; q += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t s = seg[q], e = seg[q + 1];
+        const int64_t i = coord[q] - lo;
+        double wi = w[i], ni = n[i], zi = z[i], sq = sqrt(ni);
+#pragma unroll 4
+        for (int64_t t = s; t < e; ++t) {
+            const double gt = g[t];
+            const double nn = ni + gt * gt;
+            const double sn = sqrt(nn);
+            zi += gt - (sn - sq) * ia * wi;
+            ni = nn;
+            sq = sn;
+            wi = fabs(zi) <= l1 ? 0.0 : ((zi < 0 ? -1.0 : 1.0) * l1 - zi) / (beta + sn * ia + l2);
+        }
+        w[i] = wi;
+        n[i] = ni;
+        z[i] = zi;
+    }
+}
+
+// w_i = prox(z_i, n_i) for the listed coordinates (all when coords == nullptr): makes the Hogwild weights
+// consistent with the exact n/z sums after a contended micro-batch (the racing w stores are last-writer-wins).
+__global__ __launch_bounds__(256) void ftrl_prox_kernel(const int32_t* __restrict__ coords, int64_t m, double* w,
+                                                       const double* __restrict__ n, const double* __restrict__ z,
+                                                       double alpha, double beta, double l1, double l2) {
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < m; q += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = coords != nullptr ? (int64_t)coords[q] : q;
+        const double zi = z[i];
+        w[i] = fabs(zi) <= l1 ? 0.0 : ((zi < 0 ? -1.0 : 1.0) * l1 - zi) / (beta + sqrt(n[i]) / alpha + l2);
+    }
+}
+
 __global__ void ftrl_check_kernel(const int32_t* __restrict__ idx, int64_t nnz, int64_t dim, int* __restrict__ bad) {
     for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nnz; k += (int64_t)gridDim.x * blockDim.x)
         if (idx[k] < 0 || idx[k] >= dim) atomicOr(bad, 1);
@@ -85,6 +156,34 @@ int alink_ftrl_hogwild_f64(const int64_t* indptr, const int32_t* idx, const doub
     if (grid <= 0 || alpha <= 0.0) return 1;
     hipLaunchKernelGGL(ftrl_hogwild_kernel, dim3(grid), dim3(THREADS), 0, reinterpret_cast<hipStream_t>(stream),
                        indptr, idx, val, label, nrows, w, n, z, alpha, beta, l1, l2);
+    return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+int alink_ftrl_partial_margin_f64(const int64_t* indptr, const int32_t* idx, const double* val, int64_t nrows,
+                                  const double* w, int64_t lo, int64_t hi, double* margin, int grid, void* stream) {
+    if (nrows <= 0) return 0;
+    if (grid <= 0 || hi < lo) return 1;
+    hipLaunchKernelGGL(ftrl_partial_margin_kernel, dim3(grid), dim3(THREADS), 0, reinterpret_cast<hipStream_t>(stream),
+                       indptr, idx, val, nrows, w, lo, hi, margin);
+    return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+int alink_ftrl_coord_update_f64(const int64_t* seg, int64_t nseg, const int64_t* coord, const double* g, double* w,
+                                double* n, double* z, int64_t lo, double alpha, double beta, double l1, double l2,
+                                int grid, void* stream) {
+    if (nseg <= 0) return 0;
+    if (grid <= 0 || alpha <= 0.0) return 1;
+    hipLaunchKernelGGL(ftrl_coord_update_kernel, dim3(grid), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), seg,
+                       nseg, coord, g, w, n, z, lo, alpha, beta, l1, l2);
+    return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+int alink_ftrl_prox_f64(const int32_t* coords, int64_t m, double* w, const double* n, const double* z, double alpha,
+                        double beta, double l1, double l2, int grid, void* stream) {
+    if (m <= 0) return 0;
+    if (grid <= 0 || alpha <= 0.0) return 1;
+    hipLaunchKernelGGL(ftrl_prox_kernel, dim3(grid), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), coords, m, w,
+                       n, z, alpha, beta, l1, l2);
     return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 

@@ -3,7 +3,11 @@
 ``ftrl_hogwild(indptr, idx, val, label, w, n, z, ...)`` applies the FTRL-proximal rule of
 ``FtrlTrainStreamOp.java:423-485`` to every CSR row of a micro-batch, one wave per sample, in place on the
 device-resident ``w, n, z`` (fp64).  ``n`` and ``z`` receive exact sums of every sample's contribution; the
-weights a sample reads may be stale, as in the reference's asynchronous feedback loop.
+weights a sample reads may be stale, as in the reference's asynchronous feedback loop.  A prox pass then makes
+``w`` consistent with the final ``n, z``.
+
+The feature-sharded micro-batch update (updateMode SHARDED) is ``ftrl_partial_margin_hip`` (per-rank
+partial margins, all-reduced by the caller) + ``ftrl_shard_update_hip`` (per-coordinate replay in sample order).
 """
 from __future__ import annotations
 
@@ -11,7 +15,7 @@ import torch
 
 from . import _lib
 
-__all__ = ["ftrl_hogwild"]
+__all__ = ["ftrl_hogwild", "ftrl_prox_hip", "ftrl_partial_margin_hip", "ftrl_shard_update_hip"]
 
 
 def ftrl_hogwild(indptr: torch.Tensor, idx: torch.Tensor, val: torch.Tensor, label: torch.Tensor, w: torch.Tensor,
@@ -45,3 +49,74 @@ def ftrl_hogwild(indptr: torch.Tensor, idx: torch.Tensor, val: torch.Tensor, lab
                                   float(l2), grid, st)
     if rc != 0:
         raise RuntimeError(f"alink_ftrl_hogwild_f64 failed: {rc}")
+    # the racing w stores are last-writer-wins: re-derive w = prox(z, n) of every touched coordinate from the
+    # exact atomic n/z sums (same stream, after the update kernel)
+    ftrl_prox_hip(w, n, z, alpha, beta, l1, l2, coords=torch.unique(idx))
+
+
+def _grid(n: int, per: int, cap: int = 4096) -> int:
+    return max(1, min((n + per - 1) // per, cap))
+
+
+def ftrl_prox_hip(w: torch.Tensor, n: torch.Tensor, z: torch.Tensor, alpha: float, beta: float, l1: float, l2: float,
+                  coords: torch.Tensor = None) -> None:
+    """``w_i = prox(z_i, n_i)`` on the device for ``coords`` (int32) or every coordinate."""
+    L = _lib.require()
+    m = w.shape[0] if coords is None else coords.shape[0]
+    if coords is not None:
+        coords = coords.to(device=w.device, dtype=torch.int32).contiguous()
+    rc = L.alink_ftrl_prox_f64(None if coords is None else coords.data_ptr(), m, w.data_ptr(), n.data_ptr(),
+                               z.data_ptr(), float(alpha), float(beta), float(l1), float(l2), _grid(m, 256),
+                               _lib.stream_ptr(w.device))
+    if rc != 0:
+        raise RuntimeError(f"alink_ftrl_prox_f64 failed: {rc}")
+
+
+def ftrl_partial_margin_hip(indptr: torch.Tensor, idx: torch.Tensor, val: torch.Tensor, w: torch.Tensor, lo: int,
+                            hi: int) -> torch.Tensor:
+    """Per-row ``sum_{lo <= i < hi} x_i w_i`` (``w`` = the owned shard) — one wave per row."""
+    L = _lib.require()
+    dev = w.device
+    nrows = indptr.shape[0] - 1
+    out = torch.zeros(max(nrows, 0), dtype=torch.float64, device=dev)
+    if nrows <= 0:
+        return out
+    rc = L.alink_ftrl_partial_margin_f64(indptr.data_ptr(), idx.data_ptr(), val.data_ptr(), nrows, w.data_ptr(),
+                                         int(lo), int(hi), out.data_ptr(), _grid(nrows, 4), _lib.stream_ptr(dev))
+    if rc != 0:
+        raise RuntimeError(f"alink_ftrl_partial_margin_f64 failed: {rc}")
+    return out
+
+
+def ftrl_shard_update_hip(indptr: torch.Tensor, idx: torch.Tensor, val: torch.Tensor, err: torch.Tensor,
+                          w: torch.Tensor, n: torch.Tensor, z: torch.Tensor, lo: int, hi: int, alpha: float,
+                          beta: float, l1: float, l2: float) -> None:
+    """Owned coordinates [lo, hi) replay their entries in sample order with ``err = p - y`` fixed for the
+    micro-batch: entries filtered to the shard, stably sorted by coordinate on the device, one lane per
+    coordinate segment (``ftrl_coord_update_kernel``)."""
+    L = _lib.require()
+    dev = w.device
+    nrows = indptr.shape[0] - 1
+    if nrows <= 0 or idx.numel() == 0:
+        return
+    lens = indptr[1:] - indptr[:-1]
+    erow = torch.repeat_interleave(torch.arange(nrows, device=dev, dtype=torch.int64), lens)
+    ii = idx.to(torch.int64)
+    if lo == 0 and int(ii.max()) < hi:           # every entry is owned: no filtering pass
+        keys, ent = torch.sort(ii, stable=True)
+    else:
+        ent = torch.nonzero((ii >= lo) & (ii < hi), as_tuple=False).reshape(-1)
+        if ent.numel() == 0:
+            return
+        keys, perm = torch.sort(ii[ent], stable=True)
+        ent = ent[perm]
+    g = (err[erow[ent]] * val[ent]).contiguous()          # per-entry gradient, in coordinate-sorted order
+    coord, counts = torch.unique_consecutive(keys, return_counts=True)
+    seg = torch.zeros(counts.numel() + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(counts, 0, out=seg[1:])
+    nseg = counts.numel()
+    rc = L.alink_ftrl_coord_update_f64(seg.data_ptr(), nseg, coord.contiguous().data_ptr(), g.data_ptr(),
+                                       w.data_ptr(), n.data_ptr(), z.data_ptr(), int(lo), float(alpha), float(beta),
+                                       float(l1), float(l2), _grid(nseg, 256), _lib.stream_ptr(dev))
+    if rc != 0:
+        raise RuntimeError(f"alink_ftrl_coord_update_f64 failed: {rc}")

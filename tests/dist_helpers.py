@@ -155,5 +155,44 @@ def scenario_fm(out):
     out["acc"] = sum(int(r[-1] == r[-2]) for r in pred) / max(len(pred), 1)
 
 
+def _ftrl_run(mode, rows, batch):
+    import numpy as np
+    import pandas as pd
+    os.environ["ALINK_STREAM_BATCH"] = str(batch)
+    from alink_amd import (useLocalEnv, BatchOperator, StreamOperator, LogisticRegressionTrainBatchOp,
+                           FtrlTrainStreamOp, CollectStreamOp)
+    useLocalEnv(1)
+    rng = np.random.default_rng(3)
+    X = rng.normal(size=(rows, 5))
+    y = (X @ np.array([1.0, -1.0, 0.5, 0.0, 2.0]) + 0.3 * rng.normal(size=rows) > 0).astype(int) + 1
+    df = pd.DataFrame({f"f{i}": X[:, i] for i in range(5)})
+    df["label"] = y
+    schema = ", ".join(f"f{i} double" for i in range(5)) + ", label int"
+    batch_op = BatchOperator.fromDataframe(df.iloc[:40], schemaStr=schema)
+    stream = StreamOperator.fromDataframe(df, schemaStr=schema)
+    cols = [f"f{i}" for i in range(5)]
+    model = LogisticRegressionTrainBatchOp().setFeatureCols(cols).setLabelCol("label").setMaxIter(3).linkFrom(batch_op)
+    snaps = []
+    FtrlTrainStreamOp(model).setFeatureCols(cols).setLabelCol("label").setTimeInterval(1e9).setAlpha(0.1) \
+        .setBeta(0.1).setL1(0.01).setL2(0.01).setWithIntercept(True).setUpdateMode(mode) \
+        .linkFrom(stream).link(CollectStreamOp(snaps))
+    StreamOperator.execute()
+    last = max(r[0] for r in snaps)
+    return [list(r[2:]) for r in snaps if r[0] == last], sorted({r[0] for r in snaps})
+
+
+def scenario_ftrl_seq(out):
+    out["model"], out["bids"] = _ftrl_run("SEQUENTIAL", 64, 4096)
+
+
+def scenario_ftrl_sharded(out):
+    out["model"], out["bids"] = _ftrl_run("SHARDED", 64, 4096)
+
+
+def scenario_ftrl_uneven(out):
+    # 9 rows, 2-row micro-batches: rank 0 has 3 batches, rank 1 has 2 -> lockstep with empty steps
+    out["model"], out["bids"] = _ftrl_run("SHARDED", 9, 2)
+
+
 if __name__ == "__main__":
     run(int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), sys.argv[4], sys.argv[5])

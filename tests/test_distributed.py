@@ -123,3 +123,37 @@ def test_fm_two_processes_model_averaging(tmp_path):
     two = _run("fm", 2, tmp_path)
     assert two[0]["model"] == two[1]["model"]
     assert two[0]["acc"] > 0.8
+
+
+def _coef(model_rows):
+    meta = [json.loads(r[1]) for r in model_rows if r[0] == 0][0]
+    data = [json.loads(r[1]) for r in model_rows if r[0] == 1048576]
+    return meta, np.asarray(data[0]["coefVector"]["data"] if "coefVector" in data[0] else data[0]["data"])
+
+
+@pytest.mark.parametrize("scenario", ["ftrl_seq", "ftrl_sharded"])
+def test_ftrl_two_processes_equal_single(tmp_path, scenario):
+    """FTRL on 2 ranks (SEQUENTIAL: replicated, all-gathered micro-batches; SHARDED: feature-sharded partial
+    margins + all-reduce) equals the 1-rank model when the global micro-batch sequence is the same."""
+    one = _run(scenario, 1, tmp_path)[0]
+    two = _run(scenario, 2, tmp_path)
+    assert two[0]["model"] == two[1]["model"]           # every rank emits the full model snapshot
+    assert one["bids"] == two[0]["bids"]
+    assert len(one["model"]) == len(two[0]["model"])
+    for a, b in zip(one["model"], two[0]["model"]):
+        assert a[0] == b[0]
+        if a[1] != b[1]:
+            ja, jb = json.loads(a[1]), json.loads(b[1])
+            assert ja.keys() == jb.keys()
+            np.testing.assert_allclose(np.asarray(ja.get("coefVector", {}).get("data", [])),
+                                       np.asarray(jb.get("coefVector", {}).get("data", [])), rtol=1e-12,
+                                       atol=1e-14)
+
+
+def test_ftrl_uneven_micro_batches_lockstep(tmp_path):
+    """Rank 0 has 3 micro-batches, rank 1 has 2: the finished rank joins steps with an empty batch (no hang)."""
+    one = _run("ftrl_uneven", 1, tmp_path)[0]
+    two = _run("ftrl_uneven", 2, tmp_path)
+    assert two[0]["model"] == two[1]["model"]
+    assert two[0]["bids"] == [0, 1]
+    assert len(one["model"]) == len(two[0]["model"])

@@ -83,3 +83,87 @@ def test_ftrl_hogwild_rejects_bad_index():
     with pytest.raises(ValueError):
         ftrl_hogwild(torch.tensor([0, 2]), torch.tensor([1, 9], dtype=torch.int32), torch.ones(2), torch.ones(1), *st,
                      0.1, 1.0, 0.0, 0.0)
+
+
+def _prox(z, n, alpha, beta, l1, l2):
+    return np.where(np.abs(z) <= l1, 0.0, (np.sign(z) * l1 - z) / (beta + np.sqrt(n) / alpha + l2))
+
+
+def test_ftrl_hogwild_weights_consistent_with_n_z_after_contention():
+    """after a contended batch the racing w stores are reconciled — w == prox(z, n) exactly."""
+    rng = np.random.default_rng(5)
+    d, nrows = 50, 20000
+    rows = [list(zip(rng.choice(d, 8, replace=False).tolist(), rng.normal(size=8).tolist())) for _ in range(nrows)]
+    indptr, idx, val = _csr(rows)
+    y = (rng.random(nrows) < 0.5).astype(np.float64)
+    prm = (0.3, 1.0, 0.02, 0.05)
+    w, n, z = _run_gpu(indptr, idx, val, y, np.zeros(d), prm)
+    np.testing.assert_allclose(w, _prox(z, n, *prm), rtol=1e-13, atol=1e-15)
+
+
+def _random_csr(rng, nrows, dim, hot=3):
+    rows = []
+    for _ in range(nrows):
+        k = int(rng.integers(1, 30))
+        cols = set(rng.choice(dim, size=k, replace=False).tolist()) | set(range(hot))   # hot coords in every row
+        rows.append([(c, float(rng.normal())) for c in sorted(cols)])
+    return _csr(rows)
+
+
+@pytest.mark.parametrize("lo,hi", [(0, 5000), (0, 1700), (1700, 5000), (2500, 2600)])
+def test_ftrl_sharded_kernels_match_native(lo, hi):
+    """SHARDED micro-batch FTRL: partial-margin kernel and per-coordinate replay kernel vs the native host rule
+    on one coefficient shard [lo, hi)."""
+    from alink_amd import _native
+    from alink_amd.ops.ftrl import ftrl_partial_margin_hip, ftrl_shard_update_hip
+    rng = np.random.default_rng(lo + hi)
+    dim, nrows = 5000, 3000
+    indptr, idx, val = _random_csr(rng, nrows, dim)
+    y = (rng.random(nrows) < 0.5).astype(np.float64)
+    w0 = rng.normal(size=hi - lo) * 0.1
+    prm = (0.1, 1.0, 0.01, 0.02)
+    ref_m = _native.ftrl_partial_margin(indptr, idx, val, w0, lo, hi)
+    dev = [torch.as_tensor(a).cuda() for a in (indptr, idx, val)]
+    st = [torch.tensor(a, dtype=torch.float64, device="cuda") for a in (w0, np.zeros_like(w0), np.zeros_like(w0))]
+    m = ftrl_partial_margin_hip(*dev, st[0], lo, hi)
+    np.testing.assert_allclose(m.cpu().numpy(), ref_m, rtol=1e-12, atol=1e-13)
+    full = ref_m + rng.normal(size=nrows) * 0.2          # stand-in for the other shards' all-reduced margins
+    err = 1.0 / (1.0 + np.exp(-full)) - y
+    ref = [w0.copy(), np.zeros_like(w0), np.zeros_like(w0)]
+    _native.ftrl_shard_update(indptr, idx, val, err, *ref, lo, hi, *prm)
+    ftrl_shard_update_hip(*dev, torch.as_tensor(err).cuda(), *st, lo, hi, *prm)
+    torch.cuda.synchronize()
+    for g, r in zip(st, ref):
+        np.testing.assert_allclose(g.cpu().numpy(), r, rtol=1e-12, atol=1e-14)
+
+
+def test_ftrl_train_stream_sharded_on_gpu_equals_cpu():
+    """FtrlTrainStreamOp(updateMode=SHARDED) end to end: GPU env (HIP kernels) == CPU env (native host)."""
+    import pandas as pd
+    from alink_amd import (useLocalEnv, BatchOperator, StreamOperator, LogisticRegressionTrainBatchOp,
+                           FtrlTrainStreamOp, CollectStreamOp)
+    from alink_amd.common.mlenv import resetEnv
+    rng = np.random.default_rng(9)
+    X = rng.normal(size=(3000, 6))
+    df = pd.DataFrame({f"f{i}": X[:, i] for i in range(6)})
+    df["label"] = (X @ rng.normal(size=6) > 0).astype(int)
+    schema = ", ".join(f"f{i} double" for i in range(6)) + ", label int"
+    cols = [f"f{i}" for i in range(6)]
+    out = {}
+    for dev in ("cpu", "cuda:0"):
+        resetEnv()
+        useLocalEnv(1, device=dev)
+        model = LogisticRegressionTrainBatchOp().setFeatureCols(cols).setLabelCol("label").setMaxIter(3) \
+            .linkFrom(BatchOperator.fromDataframe(df.iloc[:100], schemaStr=schema))
+        snaps = []
+        FtrlTrainStreamOp(model).setFeatureCols(cols).setLabelCol("label").setTimeInterval(1e9) \
+            .setUpdateMode("SHARDED").setAlpha(0.1).setBeta(1.0).setL1(0.01).setL2(0.01) \
+            .linkFrom(StreamOperator.fromDataframe(df, schemaStr=schema)).link(CollectStreamOp(snaps))
+        StreamOperator.execute()
+        last = max(r[0] for r in snaps)
+        out[dev] = [r for r in snaps if r[0] == last and r[2] == 1048576][0][3]
+    import json
+    a = np.asarray(json.loads(out["cpu"])["coefVector"]["data"])
+    b = np.asarray(json.loads(out["cuda:0"])["coefVector"]["data"])
+    assert np.abs(a).max() > 0
+    np.testing.assert_allclose(b, a, rtol=1e-9, atol=1e-12)
