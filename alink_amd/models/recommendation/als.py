@@ -16,6 +16,9 @@ and the updated rows are all-gathered.  Model table: ``(userCol LONG, itemCol LO
 """
 from __future__ import annotations
 
+import os
+import time
+
 from typing import Dict, List, Optional, Sequence
 
 import numpy as np
@@ -104,9 +107,11 @@ class _Side:
         self.nbr = nbr_idx.to(torch.int32)
         self.rating = rating
         self.raw = raw_ids[self.nodes]            # original ids of the owned nodes
-        self.n_pos = torch.zeros(self.nodes.numel(), dtype=torch.float64, device=rows_idx.device)
-        rows_local = torch.repeat_interleave(torch.arange(self.nodes.numel(), device=rows_idx.device), counts)
-        self.n_pos.index_add_(0, rows_local, (rating > 0).to(torch.float64))
+        # positives per row as a segmented sum over the sorted ratings (cumsum at the row boundaries): an fp64
+        # index_add_ here serialises on the atomics of popular items (tens of seconds at 1e7 ratings on ROCm)
+        cs = torch.zeros(rating.numel() + 1, dtype=torch.int64, device=rows_idx.device)
+        torch.cumsum((rating > 0).to(torch.int64), 0, out=cs[1:])
+        self.n_pos = (cs[self.indptr[1:]] - cs[self.indptr[:-1]]).to(torch.float64)
         self.n_all = counts.to(torch.float64)
 
     def subset(self, mask: torch.Tensor):
@@ -125,7 +130,12 @@ class _Side:
 def _update(side: _Side, mask: torch.Tensor, Y: torch.Tensor, X: torch.Tensor, lam: float, implicit: bool,
             alpha: float, nonneg: bool, YtY: Optional[torch.Tensor]):
     sel, indptr, nbr, rating = side.subset(mask)
-    if sel.numel():
+    if sel.numel() and not nonneg and aops.fused_supported(Y):
+        # GPU: normal equations + Cholesky fused per row (ops/csrc/als.hip), no [m, r, r] tensor in HBM
+        reg = (side.n_pos[sel] if implicit else side.n_all[sel]) * lam
+        x = aops.fused_solve(indptr, nbr, rating, Y, reg, implicit, alpha, YtY)
+        rows = side.nodes[sel]
+    elif sel.numel():
         A, b = aops.normal_equations(indptr, nbr, rating, Y, implicit, alpha)
         A = A.to(torch.float64)
         reg = (side.n_pos[sel] if implicit else side.n_all[sel]) * lam
@@ -143,7 +153,18 @@ def _update(side: _Side, mask: torch.Tensor, Y: torch.Tensor, X: torch.Tensor, l
 
 
 def train_als(mt: MTable, params: Params, env) -> AlsModelData:
+    t_start = time.perf_counter()
     dev = env.device
+    prof = os.environ.get("ALINK_ALS_PROFILE") == "1"
+
+    def mark(what, t0=[t_start]):  # noqa: B006  (per-phase wall time, ALINK_ALS_PROFILE=1)
+        if prof:
+            if dev.type == "cuda":
+                torch.cuda.synchronize(dev)
+            now = time.perf_counter()
+            print(f"[als] {what}: {now - t0[0]:.3f} s", flush=True)
+            t0[0] = now
+
     g = lambda k, d: params.get(k) if params.contains(k) and params.get(k) is not None else d  # noqa: E731
     user_col, item_col, rate_col = params.get("userCol"), params.get("itemCol"), params.get("rateCol")
     rank = int(g("rank", 10))
@@ -157,11 +178,13 @@ def train_als(mt: MTable, params: Params, env) -> AlsModelData:
     u = _ids(mt, user_col, dev)
     it = _ids(mt, item_col, dev)
     r = _vals(mt, rate_col, dev)
+    mark("ids")
     users = torch.unique(comm.all_gather_varlen(torch.unique(u)))
     items = torch.unique(comm.all_gather_varlen(torch.unique(it)))
     ui = torch.searchsorted(users, u)
     ii = torch.searchsorted(items, it)
     ws, me = comm.get_world_size(), comm.get_rank()
+    mark("index")
 
     def shuffle(owner_idx):
         if ws == 1:
@@ -180,15 +203,18 @@ def train_als(mt: MTable, params: Params, env) -> AlsModelData:
     by_user = _Side(su, si, sr, users)
     tu, ti, tr = shuffle(ii)
     by_item = _Side(ti, tu, tr, items)
+    mark("csr")
     gen = torch.Generator().manual_seed(seed)
     U = torch.rand((users.numel(), rank), generator=gen, dtype=torch.float32).to(dev)
     V = torch.rand((items.numel(), rank), generator=gen, dtype=torch.float32).to(dev)
+    mark("init factors")
     for _ in range(num_iter):
-        for side, Y, X in ((by_user, V, U), (by_item, U, V)):
+        for name, (side, Y, X) in (("users", (by_user, V, U)), ("items", (by_item, U, V))):
             YtY = (Y.to(torch.float64).T @ Y.to(torch.float64)) if implicit else None
             for bb in range(nblocks):
                 mask = (side.raw.abs() % nblocks) == bb
                 _update(side, mask, Y, X, lam, implicit, alpha, nonneg, YtY)
+            mark(f"update {name}")
     return AlsModelData(users.cpu().numpy(), U.cpu().numpy(), items.cpu().numpy(), V.cpu().numpy())
 
 

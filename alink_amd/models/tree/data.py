@@ -60,6 +60,24 @@ def numeric_column(mt: MTable, c: str, device) -> (torch.Tensor, torch.Tensor):
     return torch.where(null, torch.zeros_like(v), v), null
 
 
+def _gpu_quantize_ok() -> bool:
+    from ...ops import _lib
+    return _lib.available() or not _lib.torch_fallback_allowed()
+
+
+def _raw_column(mt: MTable, c: str, device):
+    """Numeric column in its own float dtype on ``device`` (null mask or None) — the quantize kernel reads it
+    in place."""
+    col = mt.col(c)
+    if isinstance(col.values, torch.Tensor) and col.values.dim() == 1:
+        v = col.values.to(device)
+        if v.dtype not in (torch.float32, torch.float64):
+            v = v.to(torch.float64)
+        null = col.nulls.to(device) if col.nulls is not None else None
+        return v, null
+    return numeric_column(mt, c, device)
+
+
 def _sort_key(v):
     if isinstance(v, (bool, np.bool_)):
         return (0, int(v))
@@ -158,15 +176,23 @@ def build_bins(mt: MTable, feature_cols: Sequence[str], cat_cols: Sequence[str],
     sample_idx = _sample_rows(n, cap, seed) if cont else np.zeros(0, dtype=np.int64)
     thresholds: List[Optional[np.ndarray]] = [None] * F
     bin_values: List[Optional[np.ndarray]] = [None] * F
+    gpu = torch.device(device).type == "cuda" and _gpu_quantize_ok()
     cols_dev = {}
     if cont:
         sidx = torch.as_tensor(sample_idx, device=device)
         local_samples = []
         for c in cont:
-            v, null = numeric_column(mt, c, device)
-            cols_dev[c] = (v, null)
-            vs, ns = v[sidx], null[sidx]
-            local_samples.append(vs[~ns].cpu().numpy())
+            if gpu:
+                v, null = _raw_column(mt, c, device)        # native dtype, no full-column fp64 copy
+                cols_dev[c] = (v, null)
+                vs = v[sidx].to(torch.float64)
+                ok = ~torch.isnan(vs) if null is None else (~null[sidx] & ~torch.isnan(vs))
+                local_samples.append(vs[ok].cpu().numpy())
+            else:
+                v, null = numeric_column(mt, c, device)
+                cols_dev[c] = (v, null)
+                vs, ns = v[sidx], null[sidx]
+                local_samples.append(vs[~ns].cpu().numpy())
         gathered = comm.all_gather_object(local_samples)
         for j, c in enumerate(cont):
             allv = np.concatenate([g[j] for g in gathered]) if gathered else np.zeros(0)
@@ -188,12 +214,18 @@ def build_bins(mt: MTable, feature_cols: Sequence[str], cat_cols: Sequence[str],
             nbins.append(len(thresholds[fi]) + 1)
     B = max(nbins) + 1
     bins = torch.empty((n, F), dtype=torch.uint8, device=device)
+    if gpu and cont:
+        # K5: all continuous columns in one quantize launch (ops/csrc/tree_split.hip)
+        from ...ops import tree as tops
+        fis = [feature_cols.index(c) for c in cont]
+        tops.quantize([cols_dev[c][0] for c in cont], [cols_dev[c][1] for c in cont], [thresholds[fi] for fi in fis],
+                      fis, n, F, B - 1, bins)
     for fi, c in enumerate(feature_cols):
         if is_cat[fi]:
             m = {t: i for i, t in enumerate(cat_tokens.get(c, []))}
             codes = [m.get(java_str(v), B - 1) if v is not None else B - 1 for v in mt.column_values(c)]
             bins[:, fi] = torch.tensor(codes, dtype=torch.uint8).to(device)
-        else:
+        elif not gpu:
             v, null = cols_dev[c] if c in cols_dev else numeric_column(mt, c, device)
             thr = torch.as_tensor(thresholds[fi], dtype=torch.float64, device=device)
             b = torch.searchsorted(thr, v.contiguous(), right=False) if thr.numel() else torch.zeros_like(

@@ -181,6 +181,9 @@ class TreeBuilder:
         feat_ok [m, F] allowed.  Returns per node (gain, feature, j, multiway flag, perm [m,F,B-1])."""
         cfg = self.cfg
         m, F, B, S = Hn.shape
+        if cfg.kind == "gbdt" and Hn.is_cuda and not bool(self.d.is_cat and any(self.d.is_cat)) \
+                and tops.gpu_kernels_ok():
+            return self._search_gbdt_hip(Hn, feat_order, feat_ok)
         Hv = Hn[:, :, :B - 1, :]
         Hmiss = Hn[:, :, B - 1, :]
         cnt = _count(cfg, Hv)
@@ -249,6 +252,22 @@ class TreeBuilder:
             accept = gbest > cfg.min_info_gain + 1e-6
         else:
             accept = gbest > 0
+        return gbest, fbest, jbest, mbest, accept, perm
+
+    def _search_gbdt_hip(self, Hn, feat_order, feat_ok):
+        """K8 on the GPU (``ops/csrc/tree_split.hip``): one wave per (node, feature) scans the bins; only the
+        [m, F] best gains / bins come back for the per-node feature choice."""
+        cfg = self.cfg
+        m, F, B, S = Hn.shape
+        gain, best_j = tops.gbdt_split(Hn.to(torch.float32), cfg.min_samples_per_leaf, cfg.min_sum_hessian_per_leaf)
+        gain = torch.where(feat_ok, gain, torch.full_like(gain, NEG))
+        ordered = torch.gather(gain, 1, feat_order)
+        gbest, pos = ordered.max(dim=1)
+        fbest = torch.gather(feat_order, 1, pos[:, None])[:, 0]
+        jbest = torch.gather(best_j, 1, fbest[:, None])[:, 0]
+        mbest = torch.zeros(m, dtype=torch.bool, device=Hn.device)
+        accept = gbest > cfg.min_info_gain + 1e-6
+        perm = torch.arange(B - 1, device=Hn.device).expand(m, F, B - 1)
         return gbest, fbest, jbest, mbest, accept, perm
 
     def _multiway_gain(self, Hv, Hmiss, Tv):

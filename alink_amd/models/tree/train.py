@@ -14,6 +14,7 @@ sample, so the whole forest is trained without re-reading or re-binning the tabl
 from __future__ import annotations
 
 import math
+import time
 from typing import Any, List, Optional, Tuple
 
 import numpy as np
@@ -118,7 +119,12 @@ def train_gbdt(mt: MTable, params: Params, env, algo_type: int) -> Tuple[List[tu
         period = float(tot[0] / tot[1]) if float(tot[1]) > 0 else 0.0
         y = (yd - period).to(torch.float32)
     w = _weights(mt, params, dev).to(torch.float32)
+    t_bin = time.perf_counter()
     data = build_bins(mt, feature_cols, cat, max_bins, dev, exact_midpoints=False, seed=seed)
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    t_bin = time.perf_counter() - t_bin
+    t_trees = time.perf_counter()
     cfg = SplitConfig("gbdt", max_depth=depth, min_samples_per_leaf=int(_pget(params, "minSamplesPerLeaf", 100)),
                       min_info_gain=float(_pget(params, "minInfoGain", 0.0)),
                       min_sum_hessian_per_leaf=float(_pget(params, "minSumHessianPerLeaf", 0.0)),
@@ -126,13 +132,13 @@ def train_gbdt(mt: MTable, params: Params, env, algo_type: int) -> Tuple[List[tu
     builder = TreeBuilder(data, cfg)
     n = mt.num_rows
     F = len(feature_cols)
-    row_rng = np.random.default_rng(seed + 7919 * comm.get_rank())
+    row_gen = _row_generator(dev, seed)
     feat_rng = np.random.default_rng(seed + 104729)       # identical on every rank
     pred = torch.zeros(n, dtype=torch.float32, device=dev)
     roots = []
     fmask = np.ones(F, dtype=bool)
     for t in range(num_trees):
-        sample = torch.as_tensor(row_rng.random(n) < sub_ratio, device=dev) if sub_ratio < 1.0 else \
+        sample = (torch.rand(n, generator=row_gen, device=dev) < sub_ratio) if sub_ratio < 1.0 else \
             torch.ones(n, dtype=torch.bool, device=dev)
         if feat_ratio < 1.0:   # InitialTrainningBuffer / Split draw a feature subset for every tree
             fmask = feat_rng.random(F) < feat_ratio
@@ -163,13 +169,23 @@ def train_gbdt(mt: MTable, params: Params, env, algo_type: int) -> Tuple[List[tu
     model = TreeModel(meta, roots, labels, data.indexer_rows or None)
     rows = conv.save(model)
     imp = feature_importance(roots, feature_cols)
-    info = {"numTrees": num_trees, "depth": depth, "bins": data.B}
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    info = {"numTrees": num_trees, "depth": depth, "bins": data.B, "binning_s": t_bin,
+            "trees_s": time.perf_counter() - t_trees}
     return rows, conv, imp, info
 
 
 # ---------------------------------------------------------------------------------------------------
 # random forest / decision tree
 # ---------------------------------------------------------------------------------------------------
+def _row_generator(dev, seed: int) -> torch.Generator:
+    """Per-rank device RNG for row subsampling (Philox on the GPU); rank-distinct streams."""
+    g = torch.Generator(device=dev)
+    g.manual_seed(int(seed) * 1000003 + 7919 * comm.get_rank() + 17)
+    return g
+
+
 def _avg_gain(num_trees: int, tid: int) -> str:
     div, mod = num_trees // 3, num_trees % 3
     start_gini = div if mod < 1 else div + 1
@@ -241,9 +257,8 @@ def train_forest(mt: MTable, params: Params, env, regression: bool) -> Tuple[Lis
         stats = torch.zeros((n, C + 1), dtype=hdt, device=dev)
         stats[torch.arange(n, device=dev), y] = w.to(hdt)
         stats[:, C] = 1.0
-    rng = np.random.default_rng(seed + 7919 * comm.get_rank())
-    # all trees' row samples up front: rand < factor per (row, tree), rows in row-major order
-    draws = rng.random((n, num_trees)) < factor if factor < 1.0 else None
+    # row samples drawn on the device per tree (no [n, numTrees] host matrix)
+    row_gen = _row_generator(dev, seed)
     roots = []
     for t in range(num_trees):
         kind = _gain_for_tree(tree_type, params, num_trees, t)
@@ -254,7 +269,7 @@ def train_forest(mt: MTable, params: Params, env, regression: bool) -> Tuple[Lis
                           max_leaves=int(_pget(params, "maxLeaves", 2 ** 31 - 1)),
                           node_feature_count=node_feats)
         builder = TreeBuilder(data, cfg)
-        sample = torch.as_tensor(draws[:, t], device=dev) if draws is not None else \
+        sample = (torch.rand(n, generator=row_gen, device=dev) < factor) if factor < 1.0 else \
             torch.ones(n, dtype=torch.bool, device=dev)
         # DecisionTree seeds java.util.Random with the same `seed` for every tree
         root, _, _ = builder.build(stats, sample, None, JavaRandom(seed))

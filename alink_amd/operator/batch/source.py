@@ -24,6 +24,7 @@ from ...common.linalg import SparseVector, VectorUtil
 from ...common.params import ParamInfo, Params
 from ...common.table import Column, MTable, Row
 from ...common.types import TableSchema, Types, schema_str_to_schema
+from ...parallel import comm
 from ..base import BatchOperator, partition_bounds, partition_rows
 from ..common.io.csv import CsvParser
 
@@ -40,6 +41,57 @@ def read_text(path: str) -> str:
         path = path[len("file://"):]
     with open(path, "r", encoding="utf-8", newline="") as f:
         return f.read()
+
+
+def read_text_range(path: str, row_delim: str, rank: int, world: int):
+    """(text of the lines whose first byte lies in this rank's byte range, whether the range holds the file's
+    first line) for a local file on a multi-rank job; None when a whole-file read applies (one rank, URLs)."""
+    if world <= 1 or path.startswith(("http://", "https://")):
+        return None
+    if path.startswith("file://"):
+        path = path[len("file://"):]
+    if not os.path.isfile(path):
+        return None
+    size = os.path.getsize(path)
+    lo, hi = size * rank // world, size * (rank + 1) // world
+    d = row_delim.encode("utf-8")
+    with open(path, "rb") as f:
+        if lo > 0:
+            # a line belongs to the range holding its first byte: skip the tail of the previous range's line
+            f.seek(lo - len(d) if lo >= len(d) else 0)
+            head = f.read(len(d)) if lo >= len(d) else b""
+            start = lo
+            if head != d:
+                f.seek(lo)
+                buf = b""
+                while True:
+                    chunk = f.read(1 << 16)
+                    if not chunk:
+                        start = size
+                        break
+                    buf += chunk
+                    k = buf.find(d)
+                    if k >= 0:
+                        start = lo + k + len(d)
+                        break
+            lo = start
+        if lo >= hi:
+            return "", rank == 0
+        f.seek(lo)
+        data = f.read(hi - lo)
+        if not data.endswith(d):
+            rest = b""
+            while True:
+                chunk = f.read(1 << 16)
+                if not chunk:
+                    break
+                k = chunk.find(d)
+                if k >= 0:
+                    rest += chunk[:k + len(d)]
+                    break
+                rest += chunk
+            data += rest
+    return data.decode("utf-8"), lo == 0
 
 
 class BaseSourceBatchOp(BatchOperator):
@@ -145,15 +197,23 @@ class CsvSourceBatchOp(BaseSourceBatchOp):
 
     def initializeDataSource(self):
         schema = schema_str_to_schema(self.getSchemaStr())
-        text = read_text(self.getFilePath())
         row_delim = self.getRowDelimiter() or "\n"
+        path = self.getFilePath()
+        ranged = read_text_range(path, row_delim, comm.get_rank(), comm.get_world_size())
+        if ranged is not None:
+            # byte-range split (CsvSourceBatchOp.java:76-116 / Flink input splits): this rank reads only the
+            # lines that start inside its byte range; partitions stay contiguous in file order
+            text, first = ranged
+        else:
+            text, first = read_text(path), True
         lines = text.split(row_delim)
         if lines and lines[-1] == "":
             lines.pop()
         lines = [l[:-1] if l.endswith("\r") and row_delim == "\n" else l for l in lines]
-        if self.getIgnoreFirstLine() and lines:
+        if self.getIgnoreFirstLine() and lines and first:
             lines = lines[1:]
-        lines = partition_rows(lines, self.env)
+        if ranged is None:
+            lines = partition_rows(lines, self.env)
         quote = self.getParams().get(self._param_infos["quoteChar"])
         delim = self.getFieldDelimiter()
         skip_blank = self.getSkipBlankLine()

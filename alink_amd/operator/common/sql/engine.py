@@ -276,3 +276,62 @@ def sql_minus(a: MTable, b: MTable, all_: bool) -> MTable:
             seen.add(k)
             keep.append(i)
     return a.take(keep)
+
+
+# ---------------------------------------------------------------------------------------------------
+# distributed plan helpers (operator/batch/sql.py): which columns co-partition an operator's inputs
+# ---------------------------------------------------------------------------------------------------
+def join_keys(left: TableSchema, right: TableSchema, predicate: str) -> Tuple[List[int], List[int]]:
+    """Column indices of the equality conjuncts ``a.x = b.y`` of a join predicate (empty: not an equi-join)."""
+    ln, rn = left.names, right.names
+    qual = {"a": (0, ln), "b": (len(ln), rn)}
+    resolve = _resolver(list(ln) + list(rn), qual)
+    eq_l, eq_r = [], []
+    for c in _split_and(parse_expr(predicate)):
+        if c.kind == "cmp" and c.args[0] == "=" and c.args[1].kind == "col" and c.args[2].kind == "col":
+            i, j = resolve(c.args[1].args[0]), resolve(c.args[2].args[0])
+            if i < len(ln) <= j:
+                eq_l.append(i)
+                eq_r.append(j - len(ln))
+            elif j < len(ln) <= i:
+                eq_l.append(j)
+                eq_r.append(i - len(ln))
+    return eq_l, eq_r
+
+
+def group_key_cols(schema: TableSchema, by: str) -> Optional[List[int]]:
+    """Indices of the group-by items when every item is a plain column reference, else None."""
+    resolve = _resolver(schema.names)
+    out = []
+    for p in split_top_level(by):
+        e = parse_expr(p)
+        if e.kind != "col":
+            return None
+        out.append(resolve(e.args[0]))
+    return out
+
+
+def order_key_fn(mt: MTable, clause: str, order: str = "asc"):
+    """Row -> sort key of ``sql_order_by`` (nulls first ascending / last descending, per-key direction), as a
+    ``functools.cmp_to_key`` object usable for splitters and bisection."""
+    import functools
+    keys = []
+    for part in split_top_level(clause):
+        toks = part.split()
+        asc = order.lower() != "desc"
+        if len(toks) > 1 and toks[-1].lower() in ("asc", "desc"):
+            asc = toks[-1].lower() == "asc"
+            part = " ".join(toks[:-1])
+        keys.append((compile_expr(parse_expr(part), _resolver(mt.schema.names)), asc))
+
+    def cmp(x, y):
+        for (f, asc), a, b in zip(keys, x, y):
+            ka = (a is not None, a if a is not None else 0)
+            kb = (b is not None, b if b is not None else 0)
+            if ka != kb:
+                r = -1 if ka < kb else 1
+                return r if asc else -r
+        return 0
+
+    K = functools.cmp_to_key(cmp)
+    return lambda row: K(tuple(f(row) for f, _ in keys))

@@ -7,6 +7,10 @@ register-blocked 8x8 tiles, LDS-staged neighbour factors); CPU: chunked fp64 ``i
 
 ``solve(A, b, nonnegative)``: batched SPD Cholesky solves (rocSOLVER via torch) in fp64 chunks, or a batched
 projected coordinate-descent NNLS (reference ``NNLSSolver``) for the non-negative variant.
+
+``fused_solve(...)``: the GPU default for the unconstrained solve — ``alink_als_fused_solve`` builds each row's
+normal equations in registers (fp64), factors and solves them in LDS, one wave per row; the ``[m, r, r]``
+matrices never touch HBM.  Rows whose matrix is not SPD are re-solved with ``pinv`` on the host side.
 """
 from __future__ import annotations
 
@@ -14,7 +18,7 @@ import torch
 
 from . import _lib
 
-__all__ = ["normal_equations", "normal_equations_torch", "solve", "nnls"]
+__all__ = ["normal_equations", "normal_equations_torch", "solve", "nnls", "fused_solve", "fused_supported"]
 
 
 def normal_equations_torch(indptr, nbr, rating, Y, implicit: bool, alpha: float):
@@ -108,3 +112,47 @@ def solve(A: torch.Tensor, b: torch.Tensor, nonnegative: bool = False, chunk: in
                 x[bad] = (torch.linalg.pinv(Ad[bad]) @ bd[bad][:, :, None])[:, :, 0]
         out[s:s + chunk] = x.to(torch.float32)
     return out
+
+
+def fused_supported(Y: torch.Tensor) -> bool:
+    return Y.is_cuda and Y.shape[1] <= 64 and (_lib.available() or not _lib.torch_fallback_allowed())
+
+
+def fused_solve(indptr: torch.Tensor, nbr: torch.Tensor, rating: torch.Tensor, Y: torch.Tensor, reg: torch.Tensor,
+                implicit: bool = False, alpha: float = 0.0, YtY: torch.Tensor = None) -> torch.Tensor:
+    """x_u (float32 [m, r]) of ``(sum c y y^T + reg_u I [+ YtY]) x = sum w y`` for every CSR row u (GPU)."""
+    L = _lib.require()
+    m = indptr.numel() - 1
+    r = Y.shape[1]
+    dev = Y.device
+    X = torch.empty((max(m, 0), r), dtype=torch.float32, device=dev)
+    if m <= 0:
+        return X
+    indptr = indptr.to(device=dev, dtype=torch.int64).contiguous()
+    nbr = nbr.to(device=dev, dtype=torch.int32).contiguous()
+    rating = rating.to(device=dev, dtype=torch.float32).contiguous()
+    Yf = Y.to(torch.float32).contiguous()
+    if nbr.numel() and int(nbr.max()) >= Yf.shape[0]:
+        raise ValueError("neighbour index out of range")
+    regd = reg.to(device=dev, dtype=torch.float64).contiguous()
+    yty = None if YtY is None else YtY.to(device=dev, dtype=torch.float64).contiguous()
+    status = torch.empty(m, dtype=torch.int32, device=dev)
+    rc = L.alink_als_fused_solve(indptr.data_ptr(), nbr.data_ptr(), rating.data_ptr(), Yf.data_ptr(), m, r,
+                                 int(bool(implicit)), float(alpha), regd.data_ptr(),
+                                 None if yty is None else yty.data_ptr(), X.data_ptr(), status.data_ptr(),
+                                 _lib.stream_ptr(dev))
+    if rc != 0:
+        raise RuntimeError(f"alink_als_fused_solve failed: {rc}")
+    bad = torch.nonzero(status != 0, as_tuple=False).reshape(-1)
+    if bad.numel():                         # singular / indefinite rows: pinv like the chunked solver
+        starts, ends = indptr[:-1][bad], indptr[1:][bad]
+        cnt = ends - starts
+        sub = torch.zeros(bad.numel() + 1, dtype=torch.int64, device=dev)
+        sub[1:] = torch.cumsum(cnt, 0)
+        pos = torch.repeat_interleave(starts - sub[:-1], cnt) + torch.arange(int(sub[-1]), device=dev)
+        A, b = normal_equations_torch(sub, nbr[pos], rating[pos], Yf, implicit, alpha)
+        if yty is not None:
+            A = A + yty[None]
+        A = A + regd[bad][:, None, None] * torch.eye(r, dtype=A.dtype, device=dev)[None]
+        X[bad] = (torch.linalg.pinv(A) @ b[:, :, None])[:, :, 0].to(torch.float32)
+    return X

@@ -18,7 +18,13 @@ import torch
 
 from . import _lib
 
-__all__ = ["histogram", "histogram_torch", "route", "route_torch", "node_sums", "node_sums_torch"]
+__all__ = ["histogram", "histogram_torch", "route", "route_torch", "node_sums", "node_sums_torch", "quantize",
+           "gbdt_split"]
+
+
+def gpu_kernels_ok() -> bool:
+    """HIP kernels are used on GPU tensors unless the library is missing AND the torch fallback is allowed."""
+    return _lib.available() or not _lib.torch_fallback_allowed()
 
 
 def _num_cus(device) -> int:
@@ -147,3 +153,48 @@ def node_sums(node: torch.Tensor, sample: torch.Tensor, stats: torch.Tensor, nno
     if rc != 0:
         raise RuntimeError(f"alink_tree_node_sums failed: {rc}")
     return out[:nnodes]
+
+
+def quantize(cols, nulls, thresholds, out_cols, n: int, F: int, missing: int, out: torch.Tensor) -> None:
+    """K5: bin continuous columns into ``out`` (uint8 [n, F], row-major) on the GPU.  ``cols`` fp32/fp64 device
+    vectors [n], ``nulls`` bool masks or None, ``thresholds`` per column (ascending fp64 numpy), ``out_cols``
+    destination column per input (``bin = #thresholds < x``; NaN / null -> ``missing``)."""
+    L = _lib.require()
+    dev = out.device
+    Fc = len(cols)
+    if Fc == 0 or n == 0:
+        return
+    cols = [c if c.dtype in (torch.float32, torch.float64) else c.to(torch.float64) for c in cols]
+    cols = [c.contiguous() for c in cols]
+    nulls = [None if m is None else m.to(torch.uint8).contiguous() for m in nulls]
+    T = max(1, max(len(t) for t in thresholds))
+    thr = torch.full((Fc, T), float("inf"), dtype=torch.float64)
+    for i, t in enumerate(thresholds):
+        if len(t):
+            thr[i, :len(t)] = torch.as_tensor(t, dtype=torch.float64)
+    meta = torch.tensor([[c.data_ptr() for c in cols], [0 if m is None else m.data_ptr() for m in nulls]],
+                        dtype=torch.int64).to(dev)
+    is32 = torch.tensor([int(c.dtype == torch.float32) for c in cols], dtype=torch.int32).to(dev)
+    oc = torch.tensor(list(out_cols), dtype=torch.int32).to(dev)
+    nt = torch.tensor([len(t) for t in thresholds], dtype=torch.int32).to(dev)
+    thr = thr.to(dev)
+    rc = L.alink_tree_quantize(meta[0].data_ptr(), meta[1].data_ptr(), is32.data_ptr(), oc.data_ptr(), Fc, n, F,
+                               thr.data_ptr(), nt.data_ptr(), T, int(missing), out.data_ptr(), _lib.stream_ptr(dev))
+    if rc != 0:
+        raise RuntimeError(f"alink_tree_quantize failed: {rc}")
+    # keep the pointer tables alive until the kernel has consumed them
+    torch.cuda.current_stream(dev).synchronize()
+
+
+def gbdt_split(H: torch.Tensor, min_leaf: float, min_hess: float, gi: int = 1, hi: int = 2, ci: int = 3):
+    """K8: (best gain [m, F] fp64, best bin [m, F] int64) of the GBDT gain over the fp32 histogram H [m,F,B,S]."""
+    L = _lib.require()
+    m, F, B, S = H.shape
+    H = H.to(torch.float32).contiguous()
+    gain = torch.empty((m, F), dtype=torch.float64, device=H.device)
+    binj = torch.empty((m, F), dtype=torch.int32, device=H.device)
+    rc = L.alink_gbdt_split(H.data_ptr(), m, F, B, S, gi, hi, ci, float(min_leaf), float(min_hess),
+                            gain.data_ptr(), binj.data_ptr(), _lib.stream_ptr(H.device))
+    if rc != 0:
+        raise RuntimeError(f"alink_gbdt_split failed: {rc}")
+    return gain, binj.to(torch.int64)

@@ -194,5 +194,56 @@ def scenario_ftrl_uneven(out):
     out["model"], out["bids"] = _ftrl_run("SHARDED", 9, 2)
 
 
+def scenario_sql(out):
+    """Distributed relational ops: each rank returns its partition of every result."""
+    import numpy as np
+    import pandas as pd
+    from alink_amd import (useLocalEnv, BatchOperator, JoinBatchOp, GroupByBatchOp, DistinctBatchOp,
+                           OrderByBatchOp, UnionBatchOp, IntersectBatchOp, MinusBatchOp, LeftOuterJoinBatchOp)
+    useLocalEnv(1)
+    rng = np.random.default_rng(11)
+    n = 97
+    a = pd.DataFrame({"id": rng.integers(0, 30, n), "name": [f"n{x}" for x in rng.integers(0, 7, n)],
+                      "v": np.round(rng.normal(size=n), 3)})
+    b = pd.DataFrame({"key": rng.integers(0, 40, 61), "w": rng.integers(0, 5, 61).astype(float)})
+    A = BatchOperator.fromDataframe(a, schemaStr="id long, name string, v double")
+    B = BatchOperator.fromDataframe(b, schemaStr="key long, w double")
+    res = {}
+    res["join"] = JoinBatchOp().setJoinPredicate("a.id = b.key").setSelectClause("a.id, a.name, b.w") \
+        .linkFrom(A, B).collect()
+    res["ljoin"] = LeftOuterJoinBatchOp().setJoinPredicate("a.id = b.key").setSelectClause("a.id, b.w") \
+        .linkFrom(A, B).collect()
+    res["group"] = GroupByBatchOp().setGroupByPredicate("name").setSelectClause("name, count(*) as c, sum(v) as s") \
+        .linkFrom(A).collect()
+    res["distinct"] = DistinctBatchOp().linkFrom(A.select("name")).collect()
+    res["order"] = OrderByBatchOp().setClause("v").setOrder("desc").linkFrom(A).collect()
+    res["order_lim"] = OrderByBatchOp().setClause("id, v").setLimit(13).linkFrom(A).collect()
+    ids = A.select("id")
+    keys = B.select("key")
+    res["union"] = UnionBatchOp().linkFrom(ids, keys).collect()
+    res["intersect"] = IntersectBatchOp().linkFrom(ids, keys).collect()
+    res["minus"] = MinusBatchOp().linkFrom(ids, keys).collect()
+    out["res"] = {k: [list(r) for r in v] for k, v in res.items()}
+
+
+def scenario_csv(out):
+    """Byte-range sharded CSV read: every rank parses only its split; gathered rows equal the file."""
+    import os
+    from alink_amd import useLocalEnv, CsvSourceBatchOp
+    from alink_amd.parallel import comm
+    useLocalEnv(1)
+    path = os.path.join(os.environ["ALINK_TEST_TMP"], "data.csv")
+    if comm.get_rank() == 0 and not os.path.exists(path):
+        with open(path + ".tmp", "w") as f:
+            f.write("id,name,v\n")
+            for i in range(503):
+                f.write(f"{i},name{i % 17},{i * 0.5}\n")
+        os.replace(path + ".tmp", path)
+    comm.barrier()
+    op = CsvSourceBatchOp().setFilePath(path).setSchemaStr("id long, name string, v double").setIgnoreFirstLine(True)
+    out["local_rows"] = op.getOutputTable().num_rows
+    out["rows"] = [list(r) for r in op.collect()]
+
+
 if __name__ == "__main__":
     run(int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), sys.argv[4], sys.argv[5])

@@ -25,6 +25,7 @@ def _free_port():
 def _run(scenario, world, tmp_path):
     port = _free_port()
     env = dict(os.environ)
+    env["ALINK_TEST_TMP"] = str(tmp_path)
     env.pop("WORLD_SIZE", None)
     env.pop("RANK", None)
     procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "dist_helpers.py"), str(r), str(world), str(port),
@@ -157,3 +158,27 @@ def test_ftrl_uneven_micro_batches_lockstep(tmp_path):
     assert two[0]["model"] == two[1]["model"]
     assert two[0]["bids"] == [0, 1]
     assert len(one["model"]) == len(two[0]["model"])
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_sql_relational_ops_partitioned_equal_single(tmp_path, world):
+    """join / left join / groupBy / distinct / union / intersect / minus (hash-partitioned) and orderBy (range
+    partitioned, concatenated in rank order) on P ranks equal the 1-rank results."""
+    one = _run("sql", 1, tmp_path)[0]["res"]
+    many = _run("sql", world, tmp_path)
+    for k, ref in one.items():
+        got = many[0]["res"][k]                                # collect(): partitions gathered in rank order
+        assert all(o["res"][k] == got for o in many)
+        if k.startswith("order"):
+            assert got == ref, k
+        else:
+            key = lambda r: [str(x) for x in r]  # noqa: E731
+            assert sorted(got, key=key) == sorted(ref, key=key), k
+
+
+def test_csv_source_byte_range_split(tmp_path):
+    one = _run("csv", 1, tmp_path)[0]
+    three = _run("csv", 3, tmp_path)
+    assert len(one["rows"]) == 503 and one["rows"][0] == [0, "name0", 0.0]
+    assert all(o["rows"] == one["rows"] for o in three)
+    assert sum(o["local_rows"] for o in three) == 503 and max(o["local_rows"] for o in three) < 503

@@ -231,3 +231,57 @@ def test_gbdt_on_gpu_matches_doc():
         .linkFrom(_src().link(train), _src()).collect()
     assert [r[5] for r in out] == [0, 0, 1, 1]
     assert json.loads(out[0][6])["0"] == pytest.approx(P_HI, abs=1e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+def test_hip_quantize_matches_searchsorted(dtype):
+    """K5 quantize kernel vs torch.searchsorted per column (NaN and null mask -> missing bin)."""
+    from alink_amd.ops import tree as tops
+    rng = np.random.default_rng(1)
+    n, F = 50003, 77
+    cols, nulls, thr, outc = [], [], [], []
+    perm = rng.permutation(F)
+    for f in range(F):
+        v = torch.from_numpy(rng.normal(size=n) * (f + 1)).to(dtype)
+        v[torch.from_numpy(rng.random(n) < 0.05)] = float("nan")
+        cols.append(v.cuda())
+        nulls.append(torch.from_numpy(rng.random(n) < 0.03).cuda() if f % 3 == 0 else None)
+        k = int(rng.integers(0, 255))
+        thr.append(np.unique(np.sort(rng.normal(size=k) * (f + 1)).astype(np.float64)))
+        outc.append(int(perm[f]))                 # scattered destination columns
+    out = torch.full((n, F), 222, dtype=torch.uint8, device="cuda")
+    tops.quantize(cols, nulls, thr, outc, n, F, 255, out)
+    for f in range(F):
+        v = cols[f].double()
+        ref = torch.searchsorted(torch.as_tensor(thr[f], device="cuda"), v.contiguous(), right=False)
+        miss = torch.isnan(v) if nulls[f] is None else (torch.isnan(v) | nulls[f])
+        ref = torch.where(miss, torch.full_like(ref, 255), ref)
+        assert torch.equal(out[:, outc[f]].long(), ref), f
+
+
+@pytest.mark.gpu
+def test_hip_gbdt_split_matches_torch_search():
+    """K8 split kernel vs the vectorised torch search on random GBDT histograms."""
+    from alink_amd.models.tree.data import BinnedData
+    from alink_amd.models.tree.engine import SplitConfig, TreeBuilder
+    rng = np.random.default_rng(2)
+    m, F, B = 9, 40, 130
+    cnt = rng.integers(0, 50, size=(m, F, B)).astype(np.float64)
+    cnt[:, :, 17] = 0
+    g = rng.normal(size=(m, F, B)) * cnt
+    h = rng.random((m, F, B)) * cnt
+    H = np.stack([g * g, g, h, cnt], -1).astype(np.float32)
+    Hn = torch.from_numpy(H).cuda().double()
+    data = BinnedData(torch.zeros((1, F), dtype=torch.uint8, device="cuda"), B, [f"f{i}" for i in range(F)],
+                      [False] * F, [B - 1] * F, [np.zeros(B - 2)] * F)
+    tb = TreeBuilder(data, SplitConfig("gbdt", max_depth=6, min_samples_per_leaf=30, min_sum_hessian_per_leaf=1.0))
+    order = torch.arange(F, device="cuda").expand(m, F).clone()
+    ok = torch.ones((m, F), dtype=torch.bool, device="cuda")
+    ok[:, 3] = False
+    got = tb._search_gbdt_hip(Hn, order, ok)
+    data.is_cat = [True] + [False] * (F - 1)      # forces the torch path (categorical present) ...
+    tb.is_cat = torch.zeros(F, dtype=torch.bool, device="cuda")   # ... but with no categorical feature inside
+    ref = tb._search(Hn, order, ok)
+    torch.testing.assert_close(got[0], ref[0], rtol=1e-9, atol=1e-9)
+    assert torch.equal(got[1], ref[1]) and torch.equal(got[2], ref[2]) and torch.equal(got[4], ref[4])

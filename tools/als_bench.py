@@ -1,0 +1,64 @@
+#!/usr/bin/env python3
+"""BASELINE config 4: ALS 1e7 users x 1e6 items, rank 64, 1 GPU (s / iteration, factor-exchange bytes).
+
+Synthetic explicit ratings (no dataset access): ``--ratings`` (user, item, rating) triples, users uniform,
+items Zipf-skewed (popular items have 1e3-1e5 ratings), generated on the device.  Runs the framework's ALS
+training loop (``models/recommendation/als.py``: per side the fused normal-equations + Cholesky kernel, one
+wave per row) for 1 and for 1 + ``--iters`` iterations and reports the difference per iteration, so id
+mapping / CSR construction / model export are excluded from s/iteration.
+
+    python tools/als_bench.py [--users 10000000] [--items 1000000] [--ratings 100000000] [--rank 64]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--users", type=int, default=10_000_000)
+    ap.add_argument("--items", type=int, default=1_000_000)
+    ap.add_argument("--ratings", type=int, default=100_000_000)
+    ap.add_argument("--rank", type=int, default=64)
+    ap.add_argument("--iters", type=int, default=2)
+    a = ap.parse_args()
+    from alink_amd import useLocalEnv
+    from alink_amd.common.params import Params
+    from alink_amd.common.table import Column, MTable
+    from alink_amd.common.types import TableSchema, Types
+    from alink_amd.models.recommendation.als import train_als
+    env = useLocalEnv(1)
+    dev = env.device
+    g = torch.Generator(device=dev).manual_seed(0)
+    u = torch.randint(0, a.users, (a.ratings,), generator=g, device=dev)
+    it = (a.items * torch.rand(a.ratings, generator=g, device=dev) ** 3).long().clamp_max(a.items - 1)
+    rt = torch.randint(1, 6, (a.ratings,), generator=g, device=dev).double()
+    mt = MTable(TableSchema(["u", "i", "r"], [Types.LONG, Types.LONG, Types.DOUBLE]),
+                [Column(u), Column(it), Column(rt)])
+    times = {}
+    for n in (1, 1 + a.iters):
+        p = Params().set("userCol", "u").set("itemCol", "i").set("rateCol", "r").set("rank", a.rank) \
+            .set("numIter", n).set("lambda", 0.1)
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        train_als(mt, p, env)
+        torch.cuda.synchronize()
+        times[n] = time.perf_counter() - t
+    per_iter = (times[1 + a.iters] - times[1]) / a.iters
+    deg = torch.bincount(it, minlength=a.items)
+    print(json.dumps({"users": a.users, "items": a.items, "ratings": a.ratings, "rank": a.rank,
+                      "s_per_iteration": per_iter, "train_1iter_s": times[1],
+                      "max_item_degree": int(deg.max()), "mean_user_degree": a.ratings / a.users,
+                      "factor_bytes_per_iteration": (a.users + a.items) * a.rank * 4,
+                      "solves_per_s": (a.users + a.items) / per_iter, "device": str(dev),
+                      "data": "synthetic ratings (uniform users, Zipf-skewed items)"}))
+
+
+if __name__ == "__main__":
+    main()

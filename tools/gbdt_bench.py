@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--trees", type=int, default=20)
     ap.add_argument("--depth", type=int, default=6)
     ap.add_argument("--bins", type=int, default=128)
+    ap.add_argument("--dtype", default="float64", choices=["float32", "float64"])
     a = ap.parse_args()
     from alink_amd import useLocalEnv, GbdtTrainBatchOp
     from alink_amd.common.table import MTable, Column
@@ -29,13 +30,22 @@ def main():
     env = useLocalEnv(1)
     dev = env.device
     g = torch.Generator(device=dev).manual_seed(0)
-    X = torch.randn((a.rows, a.features), generator=g, device=dev, dtype=torch.float64)
-    w = torch.linspace(-1, 1, a.features, device=dev, dtype=torch.float64)
-    y = ((X @ w + 0.5 * torch.sin(3 * X[:, 0]) + 0.3 * torch.randn(a.rows, generator=g, device=dev,
-                                                                  dtype=torch.float64)) > 0).to(torch.int32)
+    dt = getattr(torch, a.dtype)
+    # one column tensor per feature (the MTable layout), generated on the device
+    score = torch.zeros(a.rows, device=dev, dtype=torch.float32)
+    cols = []
+    for i in range(a.features):
+        x = torch.randn(a.rows, generator=g, device=dev, dtype=torch.float32)
+        score += x * (2.0 * i / max(1, a.features - 1) - 1.0)
+        if i == 0:
+            score += 0.5 * torch.sin(3 * x)
+        cols.append(Column(x.to(dt)))
+    y = ((score + 0.3 * torch.randn(a.rows, generator=g, device=dev)) > 0).to(torch.int32)
+    del score
     names = [f"f{i}" for i in range(a.features)] + ["label"]
-    cols = [Column(X[:, i].contiguous()) for i in range(a.features)] + [Column(y)]
-    mt = MTable(TableSchema(names, [Types.DOUBLE] * a.features + [Types.INT]), cols)
+    cols.append(Column(y))
+    ftype = Types.DOUBLE if a.dtype == "float64" else Types.FLOAT
+    mt = MTable(TableSchema(names, [ftype] * a.features + [Types.INT]), cols)
     from alink_amd.operator.batch.source import TableSourceBatchOp
     src = TableSourceBatchOp(mt)
     op = GbdtTrainBatchOp().setFeatureCols(names[:-1]).setLabelCol("label").setNumTrees(a.trees) \
@@ -48,9 +58,17 @@ def main():
     if dev.type == "cuda":
         torch.cuda.synchronize()
     dt = time.time() - t0
+    info = op.getTrainInfo() if hasattr(op, "getTrainInfo") else {}
+    B = (info or {}).get("bins", a.bins + 1)
+    # bytes of the per-level histogram all-reduce at the deepest level (nodes/2 built slots x F x B x 3 fp32)
+    hist_bytes = (2 ** (a.depth - 1)) // 2 * a.features * B * 3 * 4
     print(json.dumps({"rows": a.rows, "features": a.features, "trees": a.trees, "depth": a.depth,
                       "seconds": round(dt, 3), "ms_per_tree": round(1000 * dt / a.trees, 2),
-                      "row_trees_per_s": a.rows * a.trees / dt, "device": str(dev)}))
+                      "row_trees_per_s": a.rows * a.trees / dt, "device": str(dev), "feature_dtype": a.dtype,
+                      "hist_allreduce_bytes_deepest_level": hist_bytes,
+                      "bin_matrix_bytes": a.rows * a.features, "binning_s": (info or {}).get("binning_s"),
+                      "trees_s": (info or {}).get("trees_s"),
+                      "s_per_tree": ((info or {}).get("trees_s") or dt) / a.trees}))
 
 
 if __name__ == "__main__":
