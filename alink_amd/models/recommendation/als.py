@@ -204,9 +204,11 @@ def train_als(mt: MTable, params: Params, env) -> AlsModelData:
     tu, ti, tr = shuffle(ii)
     by_item = _Side(ti, tu, tr, items)
     mark("csr")
-    gen = torch.Generator().manual_seed(seed)
-    U = torch.rand((users.numel(), rank), generator=gen, dtype=torch.float32).to(dev)
-    V = torch.rand((items.numel(), rank), generator=gen, dtype=torch.float32).to(dev)
+    # random init drawn where the factors live (a 1e7 x 64 host draw + copy costs seconds); the same seed gives
+    # the same factors on every rank
+    gen = torch.Generator(device=dev).manual_seed(seed)
+    U = torch.rand((users.numel(), rank), generator=gen, dtype=torch.float32, device=dev)
+    V = torch.rand((items.numel(), rank), generator=gen, dtype=torch.float32, device=dev)
     mark("init factors")
     for _ in range(num_iter):
         for name, (side, Y, X) in (("users", (by_user, V, U)), ("items", (by_item, U, V))):

@@ -77,7 +77,10 @@ _EXTRA_SIGNATURES = {
     "alink_gbdt_split": [_c_vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_d, _c_d, _c_vp, _c_vp,
                          _c_vp],
     "alink_als_fused_solve": [_c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_int, _c_int, _c_f, _c_vp, _c_vp, _c_vp, _c_vp,
-                              _c_vp],
+                              _c_vp, _c_vp],
+    "alink_als_heavy_solve": [_c_vp, _c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_f, _c_vp, _c_vp, _c_vp, _c_i64, _c_vp,
+                              _c_vp, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp],
+    "alink_als_padded_rank": [_c_int],
     "alink_als_gram_f32": [_c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_int, _c_int, _c_f, _c_vp, _c_vp, _c_vp],
 }
 

@@ -114,6 +114,10 @@ def solve(A: torch.Tensor, b: torch.Tensor, nonnegative: bool = False, chunk: in
     return out
 
 
+HEAVY_DEGREE = 16384     # rows with more neighbours are split across waves (partial Grams)
+HEAVY_CHUNK = 4096
+
+
 def fused_supported(Y: torch.Tensor) -> bool:
     return Y.is_cuda and Y.shape[1] <= 64 and (_lib.available() or not _lib.torch_fallback_allowed())
 
@@ -136,13 +140,39 @@ def fused_solve(indptr: torch.Tensor, nbr: torch.Tensor, rating: torch.Tensor, Y
         raise ValueError("neighbour index out of range")
     regd = reg.to(device=dev, dtype=torch.float64).contiguous()
     yty = None if YtY is None else YtY.to(device=dev, dtype=torch.float64).contiguous()
-    status = torch.empty(m, dtype=torch.int32, device=dev)
-    rc = L.alink_als_fused_solve(indptr.data_ptr(), nbr.data_ptr(), rating.data_ptr(), Yf.data_ptr(), m, r,
-                                 int(bool(implicit)), float(alpha), regd.data_ptr(),
-                                 None if yty is None else yty.data_ptr(), X.data_ptr(), status.data_ptr(),
-                                 _lib.stream_ptr(dev))
-    if rc != 0:
-        raise RuntimeError(f"alink_als_fused_solve failed: {rc}")
+    status = torch.zeros(m, dtype=torch.int32, device=dev)
+    st = _lib.stream_ptr(dev)
+    deg = indptr[1:] - indptr[:-1]
+    heavy = torch.nonzero(deg > HEAVY_DEGREE, as_tuple=False).reshape(-1)
+    light = torch.nonzero(deg <= HEAVY_DEGREE, as_tuple=False).reshape(-1) if heavy.numel() else None
+    nl = m if light is None else light.numel()
+    if nl:
+        rc = L.alink_als_fused_solve(indptr.data_ptr(), nbr.data_ptr(), rating.data_ptr(), Yf.data_ptr(), nl, r,
+                                     int(bool(implicit)), float(alpha), regd.data_ptr(),
+                                     None if yty is None else yty.data_ptr(),
+                                     None if light is None else light.data_ptr(), X.data_ptr(), status.data_ptr(), st)
+        if rc != 0:
+            raise RuntimeError(f"alink_als_fused_solve failed: {rc}")
+    if heavy.numel():
+        # popular items: the neighbour list is split into HEAVY_CHUNK pieces, one wave each (partial Grams
+        # summed in fp64), then one wave per row solves
+        RP = int(L.alink_als_padded_rank(r))
+        hd = deg[heavy]
+        nck = (hd + HEAVY_CHUNK - 1) // HEAVY_CHUNK
+        chunk_row = torch.repeat_interleave(torch.arange(heavy.numel(), device=dev), nck)
+        first = torch.cumsum(nck, 0) - nck
+        chunk_start = indptr[:-1][heavy][chunk_row] + (torch.arange(int(nck.sum()), device=dev) - first[chunk_row]) \
+            * HEAVY_CHUNK
+        G = torch.zeros((heavy.numel(), RP, RP), dtype=torch.float64, device=dev)
+        B = torch.zeros((heavy.numel(), RP), dtype=torch.float64, device=dev)
+        rc = L.alink_als_heavy_solve(indptr.data_ptr(), nbr.data_ptr(), rating.data_ptr(), Yf.data_ptr(), r,
+                                     int(bool(implicit)), float(alpha), regd.data_ptr(),
+                                     None if yty is None else yty.data_ptr(), heavy.data_ptr(), heavy.numel(),
+                                     chunk_row.contiguous().data_ptr(), chunk_start.contiguous().data_ptr(),
+                                     chunk_row.numel(), HEAVY_CHUNK, G.data_ptr(), B.data_ptr(), X.data_ptr(),
+                                     status.data_ptr(), st)
+        if rc != 0:
+            raise RuntimeError(f"alink_als_heavy_solve failed: {rc}")
     bad = torch.nonzero(status != 0, as_tuple=False).reshape(-1)
     if bad.numel():                         # singular / indefinite rows: pinv like the chunked solver
         starts, ends = indptr[:-1][bad], indptr[1:][bad]

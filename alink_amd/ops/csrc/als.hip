@@ -105,10 +105,11 @@ __global__ __launch_bounds__(64) void als_gram(const int64_t* __restrict__ indpt
 // AlsTrain.java:479-545).  One 64-lane wave per row, rank padded to RP:
 //   1. Gram in registers, fp64: lane j owns column j; neighbour y_t is read coalesced (lane j <- y_t[j]) and
 //      its entries are broadcast with v_readlane (y is fp32, so one readlane per entry), acc[i] += c y_i y_j;
-//   2. the column is stored to LDS (column-major, stride RP+1), right-looking Cholesky with lane = row
-//      (pivot broadcast from LDS, trailing update of the lane's row entries), fp64;
-//   3. forward / backward substitution with lane = row, the running vector in a register and the pivot
-//      element broadcast by v_readlane.  A non-positive pivot flags the row (status) for the host fallback.
+//   2. right-looking Cholesky with lane = row entirely in registers (the symmetric Gram column is the row),
+//      pivots and L[j][k] broadcast from their owner lanes by v_readlane, loops fully unrolled so every
+//      register index is static; no LDS, so occupancy is set by the ~2 x RP fp64 registers alone;
+//   3. forward / backward substitution the same way.  A non-positive pivot flags the row (status) for the
+//      host fallback.
 // Padded dimensions carry an identity block, so their solution entries are 0.
 // ---------------------------------------------------------------------------------------------------------------
 __device__ __forceinline__ double readlane_f64(double v, int lane) {
@@ -117,22 +118,47 @@ __device__ __forceinline__ double readlane_f64(double v, int lane) {
   return __hiloint2double(hi, lo);
 }
 
+// Cholesky + both substitutions in registers, lane = row: a[j] = A[lane][j] (symmetric), v = b[lane].  After the
+// call v holds x[lane]; returns non-zero when a pivot was not positive.  Pivots and L[j][k] come from their
+// owner lanes by v_readlane; loops fully unrolled, so every register index is static (no LDS, no scratch).
 template <int RP>
-__global__ __launch_bounds__(64) void als_fused_solve(const int64_t* __restrict__ indptr,
-                                                      const int32_t* __restrict__ nbr,
-                                                      const float* __restrict__ rating, const float* __restrict__ Y,
-                                                      int r, int implicit, float alpha, const double* __restrict__ reg,
-                                                      const double* __restrict__ YtY, float* __restrict__ X,
-                                                      int32_t* __restrict__ status) {
-  constexpr int LD = RP + 1;
-  __shared__ double S[RP * LD];
-  const int64_t row = blockIdx.x;
-  const int lane = threadIdx.x;
-  const int64_t s = indptr[row], e = indptr[row + 1];
-  double acc[RP];
+__device__ __forceinline__ int chol_solve_regs(double (&a)[RP], double& v, int lane) {
+  int bad = 0;
 #pragma unroll
-  for (int i = 0; i < RP; ++i) acc[i] = 0.0;
-  double bj = 0.0;
+  for (int k = 0; k < RP; ++k) {
+    const double d = readlane_f64(a[k], k);
+    bad |= !(d > 0.0);
+    const double piv = sqrt(d > 0.0 ? d : 1.0);
+    const double lik = a[k] * (1.0 / piv);
+#pragma unroll
+    for (int j = k + 1; j < RP; ++j) a[j] -= lik * readlane_f64(lik, j);
+    a[k] = lane > k ? lik : (lane == k ? piv : a[k]);
+  }
+  // L z = b: lane i subtracts L[i][k] z_k (its own a[k]) for k < i
+#pragma unroll
+  for (int k = 0; k < RP; ++k) {
+    const double zk = readlane_f64(v, k) / readlane_f64(a[k], k);
+    v = lane > k ? v - a[k] * zk : (lane == k ? zk : v);
+  }
+  // L^T x = z: x_k final, lanes i < k subtract L[k][i] x_k (L[k][i] = lane k's a[i])
+#pragma unroll
+  for (int k = RP - 1; k >= 0; --k) {
+    const double xk = readlane_f64(v, k) / readlane_f64(a[k], k);
+    if (lane == k) v = xk;
+#pragma unroll
+    for (int i = 0; i < k; ++i) {
+      const double lki = readlane_f64(a[i], k);
+      if (lane == i) v -= lki * xk;
+    }
+  }
+  return bad;
+}
+
+// Gram of neighbours [s, e) of one row into the lane's column (lane j: a[i] += c y_i y_j, v += w y_j)
+template <int RP>
+__device__ __forceinline__ void gram_regs(const int32_t* __restrict__ nbr, const float* __restrict__ rating,
+                                          const float* __restrict__ Y, int r, int implicit, float alpha, int64_t s,
+                                          int64_t e, int lane, double (&a)[RP], double& v) {
   for (int64_t t = s; t < e; ++t) {
     const float yf = lane < r ? Y[(int64_t)nbr[t] * r + lane] : 0.f;
     const float rt = rating[t];
@@ -144,59 +170,91 @@ __global__ __launch_bounds__(64) void als_fused_solve(const int64_t* __restrict_
       c = 1.0;
       w = rt;
     }
-    const double yj = yf;
-    const double cy = c * yj;
+    const double cy = c * (double)yf;
 #pragma unroll
     for (int i = 0; i < RP; ++i) {
       const float yi = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(yf), i));
-      acc[i] = fma((double)yi, cy, acc[i]);
+      a[i] = fma((double)yi, cy, a[i]);
     }
-    bj = fma(w, yj, bj);
+    v = fma(w, (double)yf, v);
   }
-  // regularisation, implicit Y^T Y, identity on padded dimensions; column `lane` -> LDS.  Lanes >= RP
-  // (RP < 64) own nothing: every LDS access below is guarded, their indices would alias other columns.
-  const bool act = lane < RP;
-  const double lam = reg[row];
+}
+
+template <int RP>
+__device__ __forceinline__ void add_reg(double (&a)[RP], int lane, int r, double lam, const double* __restrict__ YtY) {
 #pragma unroll
   for (int i = 0; i < RP; ++i) {
-    double v = acc[i];
-    if (lane < r && i < r && YtY != nullptr) v += YtY[i * r + lane];
-    if (i == lane) v += lane < r ? lam : 1.0;
-    if (act) S[lane * LD + i] = v;
+    if (lane < r && i < r && YtY != nullptr) a[i] += YtY[i * r + lane];
+    if (i == lane) a[i] += lane < r ? lam : 1.0;   // padded dimensions: identity
   }
-  __syncthreads();
-  // Cholesky A = L L^T, lane = row index; L overwrites the lower triangle (column k at S[k*LD + i])
-  int bad = 0;
-  for (int k = 0; k < RP; ++k) {
-    const double d = S[k * LD + k];
-    bad |= !(d > 0.0);
-    const double piv = sqrt(d > 0.0 ? d : 1.0);
-    const double inv = 1.0 / piv;
-    double lik = 0.0;
-    if (act && lane > k) {
-      lik = S[k * LD + lane] * inv;
-      S[k * LD + lane] = lik;
-    }
-    __syncthreads();
-    if (lane == k) S[k * LD + k] = piv;
-    for (int j = k + 1; j < RP; ++j) {
-      const double ljk = S[k * LD + j];            // broadcast: L[j][k]
-      if (act && lane >= j) S[j * LD + lane] -= lik * ljk;
-    }
-    __syncthreads();
+}
+
+// light rows: one wave builds and solves the whole system
+template <int RP>
+__global__ __launch_bounds__(64) void als_fused_solve(const int64_t* __restrict__ indptr,
+                                                      const int32_t* __restrict__ nbr,
+                                                      const float* __restrict__ rating, const float* __restrict__ Y,
+                                                      int r, int implicit, float alpha, const double* __restrict__ reg,
+                                                      const double* __restrict__ YtY, const int64_t* __restrict__ rows,
+                                                      float* __restrict__ X, int32_t* __restrict__ status) {
+  const int64_t row = rows != nullptr ? rows[blockIdx.x] : (int64_t)blockIdx.x;
+  const int lane = threadIdx.x;
+  double a[RP];
+#pragma unroll
+  for (int i = 0; i < RP; ++i) a[i] = 0.0;
+  double v = 0.0;
+  gram_regs<RP>(nbr, rating, Y, r, implicit, alpha, indptr[row], indptr[row + 1], lane, a, v);
+  add_reg<RP>(a, lane, r, reg[row], YtY);
+  const int bad = chol_solve_regs<RP>(a, v, lane);
+  if (lane < r) X[row * r + lane] = (float)v;
+  if (lane == 0) status[row] = bad;
+}
+
+// heavy rows, pass 1: one wave per (row, chunk of `chunk` neighbours) adds its partial Gram / rhs into fp64
+// global accumulators G [nh][RP][RP], B [nh][RP] (device-scope atomics; a 1e6-neighbour item is 1e6/chunk waves
+// instead of one serial wave)
+template <int RP>
+__global__ __launch_bounds__(64) void als_heavy_gram(const int64_t* __restrict__ indptr,
+                                                     const int32_t* __restrict__ nbr,
+                                                     const float* __restrict__ rating, const float* __restrict__ Y,
+                                                     int r, int implicit, float alpha,
+                                                     const int64_t* __restrict__ rows,
+                                                     const int64_t* __restrict__ chunk_row,
+                                                     const int64_t* __restrict__ chunk_start, int64_t chunk,
+                                                     double* __restrict__ G, double* __restrict__ B) {
+  const int lane = threadIdx.x;
+  const int64_t h = chunk_row[blockIdx.x];
+  const int64_t row = rows[h];
+  const int64_t s = chunk_start[blockIdx.x];
+  const int64_t e = min(indptr[row + 1], s + chunk);
+  double a[RP];
+#pragma unroll
+  for (int i = 0; i < RP; ++i) a[i] = 0.0;
+  double v = 0.0;
+  gram_regs<RP>(nbr, rating, Y, r, implicit, alpha, s, e, lane, a, v);
+  if (lane < RP) {
+#pragma unroll
+    for (int i = 0; i < RP; ++i) unsafeAtomicAdd(G + (h * RP + lane) * RP + i, a[i]);
+    unsafeAtomicAdd(B + h * RP + lane, v);
   }
-  // L z = b (lane = row), then L^T x = z
-  double v = bj;
-  for (int k = 0; k < RP; ++k) {
-    const double zk = readlane_f64(v, k) / S[k * LD + k];
-    if (act && lane > k) v -= S[k * LD + lane] * zk;
-    if (lane == k) v = zk;
-  }
-  for (int k = RP - 1; k >= 0; --k) {
-    const double xk = readlane_f64(v, k) / S[k * LD + k];
-    if (lane < k) v -= S[lane * LD + k] * xk;
-    if (lane == k) v = xk;
-  }
+}
+
+// heavy rows, pass 2: solve from the accumulated G / B
+template <int RP>
+__global__ __launch_bounds__(64) void als_heavy_solve(const double* __restrict__ G, const double* __restrict__ B,
+                                                      int r, const double* __restrict__ reg,
+                                                      const double* __restrict__ YtY,
+                                                      const int64_t* __restrict__ rows, float* __restrict__ X,
+                                                      int32_t* __restrict__ status) {
+  const int lane = threadIdx.x;
+  const int64_t h = blockIdx.x;
+  const int64_t row = rows[h];
+  double a[RP];
+#pragma unroll
+  for (int i = 0; i < RP; ++i) a[i] = lane < RP ? G[(h * RP + lane) * RP + i] : 0.0;
+  double v = lane < RP ? B[h * RP + lane] : 0.0;
+  add_reg<RP>(a, lane, r, reg[row], YtY);
+  const int bad = chol_solve_regs<RP>(a, v, lane);
   if (lane < r) X[row * r + lane] = (float)v;
   if (lane == 0) status[row] = bad;
 }
@@ -225,25 +283,43 @@ int alink_als_gram_f32(const int64_t* indptr, const int32_t* nbr, const float* r
 
 // Fused normal equations + Cholesky solve per row: X [m, r] fp32 out, status [m] (non-zero: not SPD -> the
 // caller re-solves that row).  reg [m] fp64 = lambda * n_u; YtY [r, r] fp64 (implicit) or null.  r <= 64.
-int alink_als_fused_solve(const int64_t* indptr, const int32_t* nbr, const float* rating, const float* Y, int64_t m,
-                          int r, int implicit, float alpha, const double* reg, const double* YtY, float* X,
-                          int32_t* status, hipStream_t stream) {
-  if (m <= 0) return 0;
+// rows (nullable): the nrows row ids to solve (light rows); null -> rows 0..nrows-1.
+int alink_als_fused_solve(const int64_t* indptr, const int32_t* nbr, const float* rating, const float* Y,
+                          int64_t nrows, int r, int implicit, float alpha, const double* reg, const double* YtY,
+                          const int64_t* rows, float* X, int32_t* status, hipStream_t stream) {
+  if (nrows <= 0) return 0;
   if (r <= 0 || r > 64) return 1;
-  const dim3 grid((unsigned)m), block(64);
-  if (r <= 8)
-    hipLaunchKernelGGL(als_fused_solve<8>, grid, block, 0, stream, indptr, nbr, rating, Y, r, implicit, alpha, reg,
-                       YtY, X, status);
-  else if (r <= 16)
-    hipLaunchKernelGGL(als_fused_solve<16>, grid, block, 0, stream, indptr, nbr, rating, Y, r, implicit, alpha, reg,
-                       YtY, X, status);
-  else if (r <= 32)
-    hipLaunchKernelGGL(als_fused_solve<32>, grid, block, 0, stream, indptr, nbr, rating, Y, r, implicit, alpha, reg,
-                       YtY, X, status);
-  else
-    hipLaunchKernelGGL(als_fused_solve<64>, grid, block, 0, stream, indptr, nbr, rating, Y, r, implicit, alpha, reg,
-                       YtY, X, status);
+  const dim3 grid((unsigned)nrows), block(64);
+#define ALS_LAUNCH(RP) hipLaunchKernelGGL(als_fused_solve<RP>, grid, block, 0, stream, indptr, nbr, rating, Y, r, \
+                                          implicit, alpha, reg, YtY, rows, X, status)
+  if (r <= 8) ALS_LAUNCH(8);
+  else if (r <= 16) ALS_LAUNCH(16);
+  else if (r <= 32) ALS_LAUNCH(32);
+  else ALS_LAUNCH(64);
+#undef ALS_LAUNCH
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
+
+// Heavy rows (degree >> chunk): nh rows, nchunks (row, start) work items; G [nh][RP][RP] and B [nh][RP] must be
+// zeroed, RP = the padded rank (8/16/32/64, see alink_als_padded_rank).
+int alink_als_heavy_solve(const int64_t* indptr, const int32_t* nbr, const float* rating, const float* Y, int r,
+                          int implicit, float alpha, const double* reg, const double* YtY, const int64_t* rows,
+                          int64_t nh, const int64_t* chunk_row, const int64_t* chunk_start, int64_t nchunks,
+                          int64_t chunk, double* G, double* B, float* X, int32_t* status, hipStream_t stream) {
+  if (nh <= 0) return 0;
+  if (r <= 0 || r > 64 || nchunks <= 0 || chunk <= 0) return 1;
+#define ALS_HEAVY(RP)                                                                                          \
+  hipLaunchKernelGGL(als_heavy_gram<RP>, dim3((unsigned)nchunks), dim3(64), 0, stream, indptr, nbr, rating, Y, r, \
+                     implicit, alpha, rows, chunk_row, chunk_start, chunk, G, B);                              \
+  hipLaunchKernelGGL(als_heavy_solve<RP>, dim3((unsigned)nh), dim3(64), 0, stream, G, B, r, reg, YtY, rows, X, status)
+  if (r <= 8) { ALS_HEAVY(8); }
+  else if (r <= 16) { ALS_HEAVY(16); }
+  else if (r <= 32) { ALS_HEAVY(32); }
+  else { ALS_HEAVY(64); }
+#undef ALS_HEAVY
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+int alink_als_padded_rank(int r) { return r <= 8 ? 8 : r <= 16 ? 16 : r <= 32 ? 32 : 64; }
 
 }  // extern "C"

@@ -134,7 +134,8 @@ def test_hip_als_fused_solve_matches_fp64_torch(r, implicit):
     rng = np.random.default_rng(100 + r)
     m, n = 400, 3000
     counts = rng.integers(0, 60, size=m)
-    counts[5] = 20000
+    counts[5] = 20000                 # > HEAVY_DEGREE: split across waves
+    counts[9] = 40000
     counts[7] = 0
     indptr = torch.zeros(m + 1, dtype=torch.int64)
     indptr[1:] = torch.as_tensor(np.cumsum(counts))
