@@ -314,6 +314,8 @@ class UnaryLossObjFunc(OptimObjFunc):
         if code is not None and lops.hip_linear_supported(X) and (_lib.available()
                                                                   or not _lib.torch_fallback_allowed()):
             return lops.linear_grad_hip(X, data.y, data.w, coef, code[0], code[1])[0]   # one pass over X
+        if code is not None and lops.hip_sparse_supported(data.X):
+            return lops.sparse_grad_hip(data.X, data.y, data.w, coef, code[0], code[1])[0]   # CSR + CSC kernels
         eta = data.X.mv(coef)
         return data.X.rmv(data.w * self.unary.derivative(eta, data.y), coef.shape[0])
 

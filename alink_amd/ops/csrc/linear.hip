@@ -177,6 +177,55 @@ int launch(const double* X, const double* y, const double* w, const double* coef
     return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
+
+// ---------------------------------------------------------------------------------------------------------------
+// Sparse (CSR) gradient, K12 for hashed / one-hot features (UnaryLossObjFunc.java:62-139 on SparseVector data):
+//   pass 1, one wave per row: eta = x . coef (lanes over the row's non-zeros, wave reduction), then lane 0
+//           writes g_r = w_r l'(eta_r, y_r) and lw_r = w_r l(eta_r, y_r);
+//   pass 2, one wave per column over the CSC copy (built once per dataset): grad_j = sum_r x_rj g_r as a
+//           gather + fixed-order wave reduction — no atomics, so hot columns (the intercept, frequent hash
+//           buckets) cost a longer gather instead of serialised fp64 atomics, and the result is deterministic.
+// ---------------------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(THREADS) void csr_row_deriv_kernel(const int64_t* __restrict__ crow,
+                                                               const int32_t* __restrict__ col,
+                                                               const double* __restrict__ val,
+                                                               const double* __restrict__ y,
+                                                               const double* __restrict__ w,
+                                                               const double* __restrict__ coef, int64_t n, int code,
+                                                               double prm, double* __restrict__ g,
+                                                               double* __restrict__ lw) {
+    const int lane = threadIdx.x & 63;
+    const int64_t w0 = (int64_t)blockIdx.x * (THREADS / 64) + (threadIdx.x >> 6);
+    const int64_t nw = (int64_t)gridDim.x * (THREADS / 64);
+    for (int64_t r = w0; r < n; r += nw) {
+        double eta = 0.0;
+        for (int64_t k = crow[r] + lane; k < crow[r + 1]; k += 64) eta = fma(val[k], coef[col[k]], eta);
+        for (int o = 32; o > 0; o >>= 1) eta += __shfl_xor(eta, o);
+        if (lane == 0) {
+            double l, d;
+            loss_and_deriv(code, eta, y[r], prm, l, d);
+            g[r] = w[r] * d;
+            lw[r] = w[r] * l;
+        }
+    }
+}
+
+__global__ __launch_bounds__(THREADS) void csc_gather_kernel(const int64_t* __restrict__ cptr,
+                                                            const int64_t* __restrict__ crow_of,
+                                                            const double* __restrict__ cval,
+                                                            const double* __restrict__ g, int64_t d,
+                                                            double* __restrict__ grad) {
+    const int lane = threadIdx.x & 63;
+    const int64_t w0 = (int64_t)blockIdx.x * (THREADS / 64) + (threadIdx.x >> 6);
+    const int64_t nw = (int64_t)gridDim.x * (THREADS / 64);
+    for (int64_t j = w0; j < d; j += nw) {
+        double s = 0.0;
+        for (int64_t k = cptr[j] + lane; k < cptr[j + 1]; k += 64) s = fma(cval[k], g[crow_of[k]], s);
+        for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+        if (lane == 0) grad[j] = s;
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -193,5 +242,26 @@ int alink_linear_grad_f64(const double* X, const double* y, const double* w, con
 }
 
 int alink_linear_grad_pad(int d) { return d <= 8 ? 8 : d <= 16 ? 16 : d <= 32 ? 32 : 64; }
+
+// CSR pass 1: g [n] = w * l'(x.coef, y), lw [n] = w * l(x.coef, y)
+int alink_csr_row_deriv_f64(const int64_t* crow, const int32_t* col, const double* val, const double* y,
+                            const double* w, const double* coef, int64_t n, int code, double prm, double* g,
+                            double* lw, void* stream) {
+    if (n <= 0) return 0;
+    const int64_t blocks = (n + 3) / 4;
+    hipLaunchKernelGGL(csr_row_deriv_kernel, dim3((unsigned)(blocks < 65536 ? blocks : 65536)), dim3(THREADS), 0,
+                       reinterpret_cast<hipStream_t>(stream), crow, col, val, y, w, coef, n, code, prm, g, lw);
+    return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+// CSC pass 2: grad [d] = X^T g (cptr [d+1], crow_of / cval [nnz] = the CSC copy)
+int alink_csc_gather_f64(const int64_t* cptr, const int64_t* crow_of, const double* cval, const double* g, int64_t d,
+                         double* grad, void* stream) {
+    if (d <= 0) return 0;
+    const int64_t blocks = (d + 3) / 4;
+    hipLaunchKernelGGL(csc_gather_kernel, dim3((unsigned)(blocks < 65536 ? blocks : 65536)), dim3(THREADS), 0,
+                       reinterpret_cast<hipStream_t>(stream), cptr, crow_of, cval, g, d, grad);
+    return hipGetLastError() == hipSuccess ? 0 : 2;
+}
 
 }  // extern "C"

@@ -11,7 +11,7 @@ import torch
 
 from . import _lib
 
-__all__ = ["linear_grad_hip", "loss_code", "hip_linear_supported"]
+__all__ = ["linear_grad_hip", "loss_code", "hip_linear_supported", "sparse_grad_hip", "hip_sparse_supported"]
 
 _SLABS: Dict[Tuple, torch.Tensor] = {}
 
@@ -71,3 +71,58 @@ def linear_grad_hip(X: torch.Tensor, y: torch.Tensor, w: torch.Tensor, coef: tor
     if coef.shape[0] > d:
         g = torch.cat([g, torch.zeros(coef.shape[0] - d, dtype=g.dtype, device=dev)])
     return g, out[d], out[d + 1]
+
+
+def hip_sparse_supported(fm) -> bool:
+    return fm is not None and getattr(fm, "is_sparse", False) and fm.val.is_cuda and \
+        (_lib.available() or not _lib.torch_fallback_allowed())
+
+
+def _csc(fm):
+    """CSC copy of a CSR FeatureMatrix (built once, cached on the matrix): column pointers, row ids, values."""
+    c = getattr(fm, "_csc_cache", None)
+    if c is not None:
+        return c
+    n = fm.nrows
+    dev = fm.val.device
+    rows = torch.repeat_interleave(torch.arange(n, device=dev), fm.crow[1:] - fm.crow[:-1])
+    cols = fm.col.to(torch.int64)
+    key, order = torch.sort(cols, stable=True)
+    d = int(fm.ncols)
+    cptr = torch.zeros(d + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(torch.bincount(key, minlength=d)[:d], 0, out=cptr[1:])
+    c = (cptr, rows[order].contiguous(), fm.val.to(torch.float64)[order].contiguous(),
+         fm.col.to(torch.int32).contiguous(), fm.val.to(torch.float64).contiguous())
+    fm._csc_cache = c
+    return c
+
+
+def sparse_grad_hip(fm, y: torch.Tensor, w: torch.Tensor, coef: torch.Tensor, code: int, prm: float = 0.0):
+    """(sum_i w_i l'(x_i.coef, y_i) x_i [d], sum_i w_i l(.), sum_i w_i) over a CSR FeatureMatrix on the GPU:
+    row pass (wave per row) + column gather over the cached CSC copy (wave per column), no atomics."""
+    L = _lib.require()
+    dev = fm.val.device
+    n = fm.nrows
+    cptr, rows_of, cval, col32, val64 = _csc(fm)
+    d = int(fm.ncols)
+    y = y.to(device=dev, dtype=torch.float64).contiguous()
+    w = w.to(device=dev, dtype=torch.float64).contiguous()
+    c = torch.zeros(max(d, coef.shape[0]), dtype=torch.float64, device=dev)
+    c[:coef.shape[0]] = coef.to(device=dev, dtype=torch.float64)
+    g = torch.empty(n, dtype=torch.float64, device=dev)
+    lw = torch.empty(n, dtype=torch.float64, device=dev)
+    st = _lib.stream_ptr(dev)
+    crow = fm.crow.to(torch.int64).contiguous()
+    rc = L.alink_csr_row_deriv_f64(crow.data_ptr(), col32.data_ptr(), val64.data_ptr(), y.data_ptr(), w.data_ptr(),
+                                   c.data_ptr(), n, int(code), float(prm), g.data_ptr(), lw.data_ptr(), st)
+    if rc != 0:
+        raise RuntimeError(f"alink_csr_row_deriv_f64 failed: {rc}")
+    grad = torch.zeros(coef.shape[0], dtype=torch.float64, device=dev)
+    out = torch.empty(d, dtype=torch.float64, device=dev)
+    rc = L.alink_csc_gather_f64(cptr.data_ptr(), rows_of.data_ptr(), cval.data_ptr(), g.data_ptr(), d,
+                                out.data_ptr(), st)
+    if rc != 0:
+        raise RuntimeError(f"alink_csc_gather_f64 failed: {rc}")
+    m = min(d, coef.shape[0])
+    grad[:m] = out[:m]
+    return grad, lw.sum(), w.sum()
