@@ -18,3 +18,6 @@ from .operator.batch import *  # noqa: F401,F403
 from .operator.stream import *  # noqa: F401,F403
 from .pipeline import *  # noqa: F401,F403
 from .connectors import *  # noqa: F401,F403
+from .common.io_registry import IOType, AnnotationUtils, io_op, db_class, register_builtin as _register_io  # noqa
+
+_register_io()

@@ -44,6 +44,12 @@ def write_lines(path: str, lines, overwrite: bool, num_files: int = 1, row_delim
 
 
 class BaseSinkBatchOp(BatchOperator):
+    @staticmethod
+    def of(params):
+        """Re-create the registered IO operator named by ``params`` (ioName / ioType, reference ``of(params)``)."""
+        from ...common.io_registry import AnnotationUtils, IOType
+        return AnnotationUtils.of(params, IOType.SinkBatch)
+
     def linkFrom(self, *inputs):
         inp = self.checkAndGetFirst(inputs)
         self.sinkFrom(inp)

@@ -95,6 +95,12 @@ def read_text_range(path: str, row_delim: str, rank: int, world: int):
 
 
 class BaseSourceBatchOp(BatchOperator):
+    @staticmethod
+    def of(params):
+        """Re-create the registered IO operator named by ``params`` (ioName / ioType, reference ``of(params)``)."""
+        from ...common.io_registry import AnnotationUtils, IOType
+        return AnnotationUtils.of(params, IOType.SourceBatch)
+
     _NO_AUTO_PARAMS = False
 
     def getOutputTable(self) -> MTable:

@@ -41,22 +41,87 @@ class StreamEngine:
         if op not in self.sinks:
             self.sinks.append(op)
 
-    def run(self):
-        its = [(s, s.batches()) for s in self.sources if s._subscribers]
-        active = list(its)
+    # ---- checkpointing (StreamOperator.setCheckPointConf) ----
+    def _dag(self) -> List["StreamOperator"]:
+        """Every operator reachable from the sources, in a deterministic BFS order (the checkpoint key)."""
+        seen, order, queue = set(), [], list(self.sources)
+        while queue:
+            op = queue.pop(0)
+            if id(op) in seen:
+                continue
+            seen.add(id(op))
+            order.append(op)
+            queue.extend(sub for sub, _ in op._subscribers)
+        return order
+
+    def _ckpt_path(self, conf):
+        import os
+        os.makedirs(conf["dir"], exist_ok=True)
+        from ...parallel import comm
+        return os.path.join(conf["dir"], f"stream_ckpt_rank{comm.get_rank()}.pt")
+
+    def _save(self, conf, consumed):
+        import os
+        import torch
+        state = {"consumed": [int(c) for c in consumed],
+                 "ops": {i: op._state_dict() for i, op in enumerate(self._dag()) if op._state_dict() is not None}}
+        path = self._ckpt_path(conf)
+        torch.save(state, path + ".tmp")
+        os.replace(path + ".tmp", path)          # atomic: a crash mid-write keeps the previous checkpoint
+
+    def _restore(self, conf):
+        import os
+        import torch
+        path = self._ckpt_path(conf)
+        if not os.path.exists(path):
+            return None
+        state = torch.load(path, weights_only=True)
+        dag = self._dag()
+        for i, st in state["ops"].items():
+            dag[int(i)]._load_state_dict(st)
+        return state["consumed"]
+
+    def run(self, checkpoint=None):
+        import time
+        srcs = [s for s in self.sources if s._subscribers]
+        its = [(s, s.batches()) for s in srcs]
+        consumed = [0] * len(its)
+        if checkpoint is not None:
+            done = self._restore(checkpoint)
+            if done is not None:                 # replay: skip what the checkpoint already covers
+                for k, ((src, it), n) in enumerate(zip(its, done)):
+                    for _ in range(n):
+                        next(it, None)
+                    consumed[k] = n
+        last = time.time()
+        active = list(range(len(its)))
         while active:
             nxt = []
-            for src, it in active:
+            for k in active:
+                src, it = its[k]
                 try:
                     mt = next(it)
                 except StopIteration:
                     src._finish()
                     continue
                 src._emit(mt)
-                nxt.append((src, it))
+                consumed[k] += 1
+                nxt.append(k)
             active = nxt
+            if checkpoint is not None and active:
+                every = checkpoint.get("every_batches")
+                due = (every is not None and sum(consumed) % every == 0) or \
+                    (time.time() - last) >= checkpoint["interval_s"]
+                if due:
+                    self._save(checkpoint, consumed)
+                    last = time.time()
         for s in self.sinks:
             s._close()
+        if checkpoint is not None and checkpoint.get("clear_on_finish", True):
+            import os
+            p = self._ckpt_path(checkpoint)
+            if os.path.exists(p):
+                os.remove(p)
         self.sources.clear()
         self.sinks.clear()
 
@@ -154,7 +219,29 @@ class StreamOperator(AlgoOperator):
     @staticmethod
     def execute(env=None):
         env = env or MLEnvironmentFactory.getDefault()
-        _engine(env).run()
+        _engine(env).run(getattr(env, "stream_checkpoint", None))
+
+    @staticmethod
+    def setCheckPointConf(interval_s: float = 1800.0, directory: Optional[str] = None,
+                          every_batches: Optional[int] = None, env=None):
+        """Reference ``StreamOperator.setCheckPointConf`` (``StreamOperator.java:216-239``: a checkpoint every
+        30 min, exactly-once).  Here a checkpoint is a consistent cut at a micro-batch boundary: how many
+        micro-batches every source has delivered plus the state of every stateful operator (``_state_dict``),
+        written atomically to ``directory`` (default ``$ALINK_CKPT_DIR`` or ``./alink_stream_ckpt``) every
+        ``interval_s`` seconds (or ``every_batches`` micro-batches).  Re-running the same program restores the
+        operator state and skips the delivered micro-batches: exactly-once for operator state, at-least-once
+        for external sinks (batches after the checkpoint are emitted again).  A completed run deletes it."""
+        import os
+        env = env or MLEnvironmentFactory.getDefault()
+        env.stream_checkpoint = {"interval_s": float(interval_s), "every_batches": every_batches,
+                                 "dir": directory or os.environ.get("ALINK_CKPT_DIR", "alink_stream_ckpt")}
+
+    # operators with state override these (tensors / numbers / lists / dicts only: loaded with weights_only)
+    def _state_dict(self):
+        return None
+
+    def _load_state_dict(self, state):
+        pass
 
     def select(self, fields):
         from .sql import SelectStreamOp
@@ -190,6 +277,12 @@ class StreamOperator(AlgoOperator):
 
 class StreamSourceOp(StreamOperator):
     """Base of stream sources: ``batches()`` yields micro-batches for this rank."""
+
+    @staticmethod
+    def of(params):
+        """Re-create the registered stream source named by ``params`` (ioName / ioType)."""
+        from ...common.io_registry import AnnotationUtils, IOType
+        return AnnotationUtils.of(params, IOType.SourceStream)
     _NO_AUTO_PARAMS = False
     BATCH_SIZE = 1024
 

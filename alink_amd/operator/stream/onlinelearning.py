@@ -170,6 +170,22 @@ class FtrlTrainStreamOp(StreamOperator):
         self._bid += 1
         self._emit(MTable.from_rows(out, self._schema))
 
+    # ---------------------------------------------------------------- checkpoint state
+    def _state_dict(self):
+        import torch
+        w, n, z = (torch.as_tensor(a).detach().cpu().clone() for a in self._state)
+        return {"w": w, "n": n, "z": z, "bid": int(self._bid), "first": bool(self._first)}
+
+    def _load_state_dict(self, st):
+        import torch
+        for k, key in enumerate(("w", "n", "z")):
+            if isinstance(self._state[k], torch.Tensor):
+                self._state[k].copy_(st[key].to(self._state[k].device))
+            else:
+                self._state[k][:] = st[key].numpy()
+        self._bid = int(st["bid"])
+        self._first = bool(st["first"])
+
     # ---------------------------------------------------------------- stream protocol
     def on_batch(self, port, mt):
         self._step(mt if mt.num_rows else None)

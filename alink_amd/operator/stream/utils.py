@@ -13,6 +13,12 @@ __all__ = ["PrintStreamOp", "CollectStreamOp", "StreamSinkOp"]
 
 
 class StreamSinkOp(StreamOperator):
+    @staticmethod
+    def of(params):
+        """Re-create the registered stream sink named by ``params`` (ioName / ioType)."""
+        from ...common.io_registry import AnnotationUtils, IOType
+        return AnnotationUtils.of(params, IOType.SinkStream)
+
     def linkFrom(self, *inputs):
         (inp,) = self._connect(*inputs)
         self._schema = inp.getSchema()
