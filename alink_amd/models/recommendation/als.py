@@ -256,26 +256,34 @@ class AlsModelMapper(ModelMapper):
 
 
 def als_topk(model: AlsModelData, users: Sequence[int], k: int, device) -> List[tuple]:
-    """Top-``k`` items per requested user by ``u . v`` (one fp32 GEMM + ``topk`` on the device; reference
-    ``AlsPredict.recommendForUsers`` -> ``BlockwiseCross.findTopK``).  Output ``"item:score,..."``."""
+    """Top-``k`` items per requested user by ``u . v`` (reference ``AlsPredict.recommendForUsers`` ->
+    ``BlockwiseCross.findTopK``, ``A/operator/common/recommendation/AlsPredict.java:32-103``).
+
+    This rank's users stay on its device; the item table is split into one block per rank and the blocks
+    rotate around the RCCL ring (``parallel/cross.py``), each merged by the fused score + top-K kernel, so no
+    rank materialises a score matrix or more than two item blocks.  Output ``"item:score,..."``."""
     want = [int(x) for x in users if x is not None and int(x) in model.user_map]
-    if not want:
-        return []
     seen, uniq = set(), []
     for x in want:
         if x not in seen:
             seen.add(x)
             uniq.append(x)
-    U = torch.as_tensor(model.user_factors[[model.user_map[x] for x in uniq]], device=device)
-    V = torch.as_tensor(model.item_factors, device=device)
-    kk = min(k, V.shape[0])
+    from ...parallel.cross import blockwise_topk
+    ws, me = comm.get_world_size(), comm.get_rank()
+    n_items = model.item_factors.shape[0]
+    lo, hi = (me * n_items) // ws, ((me + 1) * n_items) // ws
+    dev = torch.device(device) if device is not None else torch.device("cpu")
+    r = model.item_factors.shape[1] if model.item_factors.ndim == 2 else 0
+    U = torch.as_tensor(np.asarray(model.user_factors[[model.user_map[x] for x in uniq]], dtype=np.float32)
+                        .reshape(len(uniq), r), device=dev)
+    V = torch.as_tensor(np.asarray(model.item_factors[lo:hi], dtype=np.float32).reshape(hi - lo, r), device=dev)
+    kk = min(k, n_items)
+    if kk <= 0:
+        return []
+    val, idx = blockwise_topk(U, V, kk)            # collective: every rank takes part, even with no users
+    val, idx = val.cpu().numpy(), idx.cpu().numpy()
     out = []
-    chunk = 1 << 14
-    for s in range(0, len(uniq), chunk):
-        sc = U[s:s + chunk] @ V.T
-        val, idx = torch.topk(sc, kk, dim=1)
-        val, idx = val.cpu().numpy(), idx.cpu().numpy()
-        for j, uid in enumerate(uniq[s:s + chunk]):
-            items = model.item_ids[idx[j]]
-            out.append((uid, ",".join(f"{int(a)}:{java_float_str(float(b))}" for a, b in zip(items, val[j]))))
+    for j, uid in enumerate(uniq):
+        items = model.item_ids[idx[j]]
+        out.append((uid, ",".join(f"{int(a)}:{java_float_str(float(b))}" for a, b in zip(items, val[j]))))
     return out

@@ -139,9 +139,10 @@ class _Split:
 class TreeBuilder:
     """Grows trees over one ``BinnedData`` (rows stay on the device between trees)."""
 
-    def __init__(self, data: BinnedData, cfg: SplitConfig):
+    def __init__(self, data: BinnedData, cfg: SplitConfig, local: bool = False):
         self.d = data
         self.cfg = cfg
+        self.local = local          # rows of ALL ranks are resident: no histogram / total all-reduce (P7)
         self.dev = data.bins.device
         self.F = len(data.feature_cols)
         self.B = data.B
@@ -162,7 +163,8 @@ class TreeBuilder:
         cols = self._hist_cols(stats.shape[1])
         sub = stats if len(cols) == stats.shape[1] else stats[:, cols].contiguous()
         H = tops.histogram(self.d.bins, slot, sub, nslots, self.B)
-        comm.all_reduce(H, "sum")
+        if not self.local:
+            comm.all_reduce(H, "sum")
         if len(cols) != stats.shape[1]:
             full = torch.zeros(H.shape[:-1] + (stats.shape[1],), dtype=H.dtype, device=H.device)
             full[..., cols] = H
@@ -172,7 +174,8 @@ class TreeBuilder:
     def _node_totals(self, node_of_row, sample, nnodes: int, stats) -> np.ndarray:
         """[nnodes, S] float64 per-node sums over the sampled rows (one pass over rows, then all-reduce)."""
         out = tops.node_sums(node_of_row, sample, stats, nnodes)
-        comm.all_reduce(out, "sum")
+        if not self.local:
+            comm.all_reduce(out, "sum")
         return out[:nnodes].cpu().numpy()
 
     # -------------------------------------------------------------------------------------------

@@ -179,6 +179,15 @@ def train_gbdt(mt: MTable, params: Params, env, algo_type: int) -> Tuple[List[tu
 # ---------------------------------------------------------------------------------------------------
 # random forest / decision tree
 # ---------------------------------------------------------------------------------------------------
+def _tree_generator(dev, seed: int, tree: int, replicated_rows: bool) -> torch.Generator:
+    """Row-sampling stream of one forest tree (Philox on the GPU).  Rows replicated on every rank (tree-parallel)
+    use one stream per tree; partitioned rows add the rank so ranks draw distinct samples of their rows."""
+    g = torch.Generator(device=dev)
+    g.manual_seed((int(seed) * 1000003 + 7919 * int(tree) + (0 if replicated_rows else 104729 * comm.get_rank()))
+                  & 0x7FFFFFFFFFFFFFFF)
+    return g
+
+
 def _row_generator(dev, seed: int) -> torch.Generator:
     """Per-rank device RNG for row subsampling (Philox on the GPU); rank-distinct streams."""
     g = torch.Generator(device=dev)
@@ -257,10 +266,22 @@ def train_forest(mt: MTable, params: Params, env, regression: bool) -> Tuple[Lis
         stats = torch.zeros((n, C + 1), dtype=hdt, device=dev)
         stats[torch.arange(n, device=dev), y] = w.to(hdt)
         stats[:, C] = 1.0
-    # row samples drawn on the device per tree (no [n, numTrees] host matrix)
-    row_gen = _row_generator(dev, seed)
-    roots = []
-    for t in range(num_trees):
+    # P7 tree-parallel forest (createTreeMode "series", the reference default: SampleData tags rows per tree
+    # and AvgPartition sends tree t to worker t % P, BaseRandomForestTrainBatchOp.java:219-262,446-503).  Here
+    # the binned rows (uint8, F bytes/row) and their statistics are all-gathered once over RCCL, rank r grows
+    # trees t = r (mod P) on its own GPU with no per-level collective, and the finished trees are gathered.
+    # "parallel" keeps the data-parallel histogram all-reduce of every tree.
+    ws = comm.get_world_size()
+    series = str(_pget(params, "createTreeMode", "series")).lower() != "parallel" and ws > 1
+    if series:
+        data.bins = comm.all_gather_varlen(data.bins.contiguous())
+        stats = comm.all_gather_varlen(stats.contiguous())
+        n = data.bins.shape[0]
+        mine = [t for t in range(num_trees) if t % ws == comm.get_rank()]
+    else:
+        mine = list(range(num_trees))
+    grown = {}
+    for t in mine:
         kind = _gain_for_tree(tree_type, params, num_trees, t)
         cfg = SplitConfig(kind, max_depth=max_depth, min_samples_per_leaf=msl,
                           n_classes=0 if regression else len(labels),
@@ -268,12 +289,18 @@ def train_forest(mt: MTable, params: Params, env, regression: bool) -> Tuple[Lis
                           min_info_gain=float(_pget(params, "minInfoGain", 0.0)),
                           max_leaves=int(_pget(params, "maxLeaves", 2 ** 31 - 1)),
                           node_feature_count=node_feats)
-        builder = TreeBuilder(data, cfg)
-        sample = (torch.rand(n, generator=row_gen, device=dev) < factor) if factor < 1.0 else \
-            torch.ones(n, dtype=torch.bool, device=dev)
+        builder = TreeBuilder(data, cfg, local=series)
+        # per-tree row sample drawn on the device from a (seed, tree)-keyed stream: the same tree gets the same
+        # sample whichever rank grows it
+        sample = (torch.rand(n, generator=_tree_generator(dev, seed, t, series), device=dev) < factor) \
+            if factor < 1.0 else torch.ones(n, dtype=torch.bool, device=dev)
         # DecisionTree seeds java.util.Random with the same `seed` for every tree
         root, _, _ = builder.build(stats, sample, None, JavaRandom(seed))
-        roots.append(root)
+        grown[t] = root
+    if series:
+        for part in comm.all_gather_object(grown):
+            grown.update(part)
+    roots = [grown[t] for t in range(num_trees)]
     meta = params.clone()
     conv = TreeModelDataConverter(lt)
     model = TreeModel(meta, roots, labels, data.indexer_rows or None)

@@ -92,6 +92,27 @@ def scenario_rf(out):
     out["model"] = [list(r) for r in m.collect()]
 
 
+def scenario_rf_parallel(out):
+    from alink_amd import useLocalEnv, BatchOperator, RandomForestTrainBatchOp
+    df = _data_frame()
+    useLocalEnv(1)
+    src = BatchOperator.fromDataframe(df, schemaStr="x0 double, x1 double, x2 double, x3 double, y int")
+    m = RandomForestTrainBatchOp().setFeatureCols(["x0", "x1", "x2", "x3"]).setLabelCol("y").setNumTrees(3) \
+        .setMaxDepth(5).setCreateTreeMode("parallel").linkFrom(src)
+    out["model"] = [list(r) for r in m.collect()]
+
+
+def scenario_rf_sampled(out):
+    """Tree-parallel forest with row subsampling: tree t's sample does not depend on which rank grows it."""
+    from alink_amd import useLocalEnv, BatchOperator, RandomForestTrainBatchOp
+    df = _data_frame()
+    useLocalEnv(1)
+    src = BatchOperator.fromDataframe(df, schemaStr="x0 double, x1 double, x2 double, x3 double, y int")
+    m = RandomForestTrainBatchOp().setFeatureCols(["x0", "x1", "x2", "x3"]).setLabelCol("y").setNumTrees(5) \
+        .setMaxDepth(4).setSubsamplingRatio(0.6).linkFrom(src)
+    out["model"] = [list(r) for r in m.collect()]
+
+
 def scenario_als(out):
     import numpy as np
     import pandas as pd
@@ -104,6 +125,24 @@ def scenario_als(out):
     m = AlsTrainBatchOp().setUserCol("u").setItemCol("i").setRateCol("r").setRank(6).setNumIter(5) \
         .setNumBlocks(2).linkFrom(src)
     out["model"] = [list(r) for r in m.collect()]
+
+
+def scenario_cross(out):
+    """Ring blockwise top-K: queries and items split unevenly over the ranks."""
+    import numpy as np
+    import torch
+    from alink_amd.parallel import comm
+    from alink_amd.parallel.cross import blockwise_topk
+    comm.init_distributed()
+    ws, me = comm.get_world_size(), comm.get_rank()
+    g = torch.Generator().manual_seed(3)
+    Q = torch.randn(37, 10, generator=g)
+    T = torch.randn(53, 10, generator=g)
+    qb = [0, 5, 20, 37] if ws == 3 else [0, 37]
+    ib = [0, 30, 31, 53] if ws == 3 else [0, 53]
+    for desc in (True, False):
+        v, i = blockwise_topk(Q[qb[me]:qb[me + 1]], T[ib[me]:ib[me + 1]], 7, descending=desc)
+        out["desc" if desc else "asc"] = {"v": v.tolist(), "i": i.tolist(), "q0": qb[me]}
 
 
 def run(rank, world, port, scenario, outdir):

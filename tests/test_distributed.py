@@ -78,9 +78,10 @@ def _tree_nodes(model_rows):
     return out
 
 
-@pytest.mark.parametrize("scenario", ["gbdt", "rf"])
+@pytest.mark.parametrize("scenario", ["gbdt", "rf", "rf_parallel", "rf_sampled"])
 def test_trees_two_processes_equal_single(tmp_path, scenario):
-    """Histogram all-reduce over 2 ranks grows the same trees as one rank (same splits, same leaves)."""
+    """Histogram all-reduce over 2 ranks (gbdt, rf_parallel) and tree-parallel forests (rf, rf_sampled: each rank
+    grows its own trees on the all-gathered bins) give the same trees as one rank."""
     one = _tree_nodes(_run(scenario, 1, tmp_path)[0]["model"])
     two = _run(scenario, 2, tmp_path)
     assert two[0]["model"] == two[1]["model"]
@@ -103,6 +104,26 @@ def test_als_two_processes_equal_single(tmp_path):
     a = np.array([[float(x) for x in r[2].split()] for r in one])
     b = np.array([[float(x) for x in r[2].split()] for r in two[0]["model"]])
     np.testing.assert_allclose(a, b, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("world", [1, 3])
+def test_blockwise_topk_ring(tmp_path, world):
+    """Item blocks rotating around the ring give every query the brute-force top-K (reference
+    BlockwiseCross.findTopK), for uneven query/item blocks and both orders."""
+    import torch
+    outs = _run("cross", world, tmp_path)
+    g = torch.Generator().manual_seed(3)
+    Q = torch.randn(37, 10, generator=g)
+    T = torch.randn(53, 10, generator=g)
+    S = (Q @ T.T).numpy()
+    for key, desc in (("desc", True), ("asc", False)):
+        for o in outs:
+            part = o[key]
+            for r, (vals, ids) in enumerate(zip(part["v"], part["i"])):
+                q = part["q0"] + r
+                order = np.argsort(-S[q] if desc else S[q], kind="stable")[:7]
+                np.testing.assert_allclose(vals, S[q][order], rtol=1e-5, atol=1e-5)
+                assert sorted(ids) == sorted(order.tolist())
 
 
 def test_glm_two_processes_equal_single(tmp_path):
