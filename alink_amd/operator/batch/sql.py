@@ -248,30 +248,18 @@ def registerFunction(name, fn):
     register_function(name, fn)
 
 
-_Q = re.compile(r"^\s*select\s+(?P<sel>.*?)\s+from\s+(?P<tab>[\w`]+)(?:\s+(?:as\s+)?(?P<al>\w+))?"
-                r"(?:\s+where\s+(?P<where>.*?))?(?:\s+group\s+by\s+(?P<gb>.*?))?"
-                r"(?:\s+order\s+by\s+(?P<ob>.*?))?(?:\s+limit\s+(?P<lim>\d+))?\s*$", re.I | re.S)
-
-
 def sql_query(query: str, env=None):
-    """``BatchOperator.sqlQuery``: single-table SELECT [WHERE] [GROUP BY] [ORDER BY] [LIMIT] over tables
-    registered with ``registerTableName``."""
+    """``BatchOperator.sqlQuery`` over tables registered with ``registerTableName``: SELECT [DISTINCT] with
+    joins (inner/left/right/full/cross, comma joins), subqueries in FROM and in expressions, WHERE, GROUP BY,
+    HAVING, UNION/INTERSECT/EXCEPT [ALL], ORDER BY, LIMIT/OFFSET (``operator/common/sql/query.py``)."""
     from ...common.mlenv import MLEnvironmentFactory
+    from ..common.sql.query import execute_query
     from .source import TableSourceBatchOp
     env = env or MLEnvironmentFactory.getDefault()
-    m = _Q.match(query)
-    if not m:
-        raise ValueError(f"unsupported query: {query}")
-    tab = m.group("tab").strip("`")
-    op = env.tables[tab]
-    mt = op.getOutputTable()
-    if m.group("where"):
-        mt = E.sql_where(mt, m.group("where"))
-    if m.group("gb"):
-        mt = _global(env, lambda t: E.sql_group_by(t, m.group("gb"), m.group("sel")), mt)
-    else:
-        mt = E.sql_select(mt, m.group("sel"))
-    if m.group("ob"):
-        mt = _global(env, lambda t: E.sql_order_by(t, m.group("ob"),
-                                                   limit=int(m.group("lim")) if m.group("lim") else None), mt)
-    return TableSourceBatchOp(mt)
+    text = query.strip().rstrip(";")
+    used = [op.getOutputTable() for name, op in env.tables.items()
+            if re.search(r"(?<![\w`])" + re.escape(name) + r"(?![\w`])", text, re.I)]
+    names = [name for name, op in env.tables.items()
+             if re.search(r"(?<![\w`])" + re.escape(name) + r"(?![\w`])", text, re.I)]
+    # every rank evaluates the query over the gathered tables, then keeps its slice (as the other global ops)
+    return TableSourceBatchOp(_global(env, lambda *ts: execute_query(text, dict(zip(names, ts))), *used))

@@ -262,6 +262,11 @@ def scenario_sql(out):
     res["union"] = UnionBatchOp().linkFrom(ids, keys).collect()
     res["intersect"] = IntersectBatchOp().linkFrom(ids, keys).collect()
     res["minus"] = MinusBatchOp().linkFrom(ids, keys).collect()
+    A.registerTableName("ta")
+    B.registerTableName("tb")
+    res["order_sqlquery"] = BatchOperator.sqlQuery(
+        "select t.name, count(*) c, sum(w) sw from ta t join tb u on t.id = u.key "
+        "where u.w > 0 group by t.name having count(*) > 1 order by sw desc, name").collect()
     out["res"] = {k: [list(r) for r in v] for k, v in res.items()}
 
 
