@@ -34,6 +34,7 @@ from ...common.model.converter import SimpleModelDataConverter
 from ...common.params import Params
 from ...common.table import Column, MTable
 from ...common.types import Types
+from ...ops import lda as lops
 from ...parallel import comm
 from ..nlp.text import WORD_DELIMITER, java_split, train_doc_count_vectorizer
 
@@ -155,8 +156,15 @@ def _gibbs(doc, word, cts, n_docs, V, K, params, alpha, beta, seed, dev):
         return nd, nw
 
     nd, nw = counts(z)
+    use_kernel = lops.kernel_supported(dev)
     for _ in range(num_iter):
         nk = nw.sum(0)
+        if use_kernel:
+            # K21: per-token topic walk straight from the count tables (same formula, same uniforms)
+            u = torch.rand(d_tok.numel(), generator=g, device=dev, dtype=torch.float64)
+            z = lops.gibbs_sweep(d_tok, w_tok, z, nd, nw, nk, alpha, beta, V, u)
+            nd, nw = counts(z)
+            continue
         own = torch.nn.functional.one_hot(z, K).to(torch.float64)
         p = (nd[d_tok] - own + alpha) * (nw[w_tok] - own + beta) / (nk[None, :] - own + V * beta)
         cum = torch.cumsum(p, 1)

@@ -276,11 +276,13 @@ def column_stats(fm: FeatureMatrix, d: Optional[int] = None, weights: Optional[t
     d = fm.ncols if d is None else d
     dev = fm.device
     n_local = fm.nrows
+    l1_local = None
     if fm.is_sparse:
         s = torch.zeros(d, dtype=torch.float64, device=dev).index_add_(0, fm.col, fm.val.double())
         s2 = torch.zeros(d, dtype=torch.float64, device=dev).index_add_(0, fm.col, fm.val.double() ** 2)
         nnz = torch.zeros(d, dtype=torch.float64, device=dev).index_add_(
             0, fm.col, (fm.val != 0).double())
+        l1_local = torch.zeros(d, dtype=torch.float64, device=dev).index_add_(0, fm.col, fm.val.double().abs())
         stored = torch.zeros(d, dtype=torch.float64, device=dev).index_add_(
             0, fm.col, torch.ones_like(fm.val, dtype=torch.float64))
         big = torch.full((d,), float("inf"), dtype=torch.float64, device=dev)
@@ -290,26 +292,23 @@ def column_stats(fm: FeatureMatrix, d: Optional[int] = None, weights: Optional[t
         mn = torch.where(has_zero, torch.minimum(mn, torch.zeros_like(mn)), mn)
         mx = torch.where(has_zero, torch.maximum(mx, torch.zeros_like(mx)), mx)
     else:
-        X = fm.dense.double()
+        from ...ops import stats as sops
+        X = fm.dense
         if X.shape[1] < d:
             X = torch.nn.functional.pad(X, (0, d - X.shape[1]))
-        s = X.sum(0)
-        s2 = (X * X).sum(0)
-        nnz = (X != 0).sum(0).double()
-        if X.shape[0]:
-            mn, mx = X.min(0).values, X.max(0).values
-        else:
-            mn = torch.full((d,), float("inf"), dtype=torch.float64, device=dev)
-            mx = -mn
+        # one pass over the native-dtype matrix (HIP K23 on the GPU), fp64 moments
+        cs = sops.colstats(X) if X.shape[1] else sops.colstats_torch(X)
+        s, s2, nnz, mn, mx = cs["sum"], cs["sum2"], cs["nnz"], cs["min"], cs["max"]
+        l1_local = cs["l1"]
     cnt = torch.tensor([float(n_local)], dtype=torch.float64, device=dev)
-    buf = torch.cat([cnt, s, s2, nnz])
+    buf = torch.cat([cnt, s, s2, nnz, l1_local])
     comm.all_reduce(buf, "sum")
     comm.all_reduce(mn, "min")
     comm.all_reduce(mx, "max")
     n = float(buf[0].item())
-    s, s2, nnz = buf[1:1 + d], buf[1 + d:1 + 2 * d], buf[1 + 2 * d:]
+    s, s2, nnz, l1 = buf[1:1 + d], buf[1 + d:1 + 2 * d], buf[1 + 2 * d:1 + 3 * d], buf[1 + 3 * d:]
     mean = s / max(n, 1.0)
     var = (s2 - s * mean) / max(n - 1.0, 1.0) if n > 1 else torch.zeros_like(s)
     std = torch.sqrt(torch.clamp(var, min=0.0))
     return {"count": n, "sum": s, "sum2": s2, "mean": mean, "std": std, "min": mn, "max": mx,
-            "maxAbs": torch.maximum(mn.abs(), mx.abs()), "nnz": nnz, "variance": var}
+            "maxAbs": torch.maximum(mn.abs(), mx.abs()), "nnz": nnz, "variance": var, "l1": l1}

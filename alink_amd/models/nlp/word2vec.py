@@ -28,6 +28,7 @@ from ...common.mapper import SISOMapper, ModelMapper, OutputColsHelper, find_col
 from ...common.params import Params
 from ...common.table import MTable
 from ...common.types import TableSchema, Types
+from ...ops import w2v as wops
 from ...parallel import comm
 from .text import java_split
 
@@ -165,10 +166,20 @@ def train_word2vec(mt: MTable, params: Params, env) -> List[tuple]:
     sync = max(ndocs_total // 100000, 5)
     rng = np.random.default_rng(seed + 7919 * comm.get_rank())
     ws = comm.get_world_size()
+    use_kernel = wops.kernel_supported(dev, dim)
+    H = wops.HuffmanDevice(C, P, lens, dev) if use_kernel else None
     for step in range(sync * num_iter):
         k = step % sync
         lo, hi = (len(docs) * k) // sync, (len(docs) * (k + 1)) // sync
-        cen, ctx = _pairs(docs[lo:hi], window, random_window, rng)
+        if use_kernel:
+            # K20: the window enumeration and every pair's HS update run on the device (Hogwild waves);
+            # shrinks drawn exactly as _pairs draws them
+            sl = [d for d in docs[lo:hi] if len(d) >= 2]
+            shr = [rng.integers(0, window, size=len(d)) if random_window else np.zeros(len(d), np.int64) for d in sl]
+            wops.sg_hs_train(sl, shr, window, H, inp, out, alpha)
+            cen = np.zeros(0)
+        else:
+            cen, ctx = _pairs(docs[lo:hi], window, random_window, rng)
         if cen.size:
             # pairs in one batch read the same (stale) vectors; keep a batch to a few updates per word
             _sgd(inp, out, Ct, Pt, Lt, torch.as_tensor(cen, device=dev), torch.as_tensor(ctx, device=dev), alpha,

@@ -31,6 +31,7 @@ from ...common.params import Params
 from ...common.table import Column, MTable
 from ...common.types import Types
 from ...models.common.features import FeatureMatrix, extract_features
+from ...ops import fm as fops
 from ...parallel import comm
 
 __all__ = ["FmModelData", "FmModelDataConverter", "FmModelMapper", "train_fm", "fm_predict_raw"]
@@ -115,6 +116,8 @@ def fm_predict_raw(fm: FeatureMatrix, w: Optional[torch.Tensor], V: Optional[tor
     """``FmOptimizer.calcY`` for a block of rows: y = b + X w + 1/2 sum_f ((X V)_f^2 - (X^2 V^2)_f)."""
     n = fm.nrows
     dev = fm.device
+    if dim[2] > 0 and V is not None and fops.kernel_supported(fm, V.shape[1]):
+        return fops.fm_forward(fm, w if dim[1] > 0 else None, V.contiguous(), float(bias) if dim[0] > 0 else 0.0)
     y = torch.full((n,), float(bias) if dim[0] > 0 else 0.0, dtype=torch.float64, device=dev)
     vx = None
     if dim[1] > 0 and w is not None:
@@ -219,6 +222,11 @@ def train_fm(mt: MTable, p: Params, task: str, env, micro_batch: int = 512):
                     gb = g + lam[0] * bias
                     sg_b = sg_b + (gb * gb).sum()
                     bias = bias - lr * gb.sum() / torch.sqrt(sg_b + EPS)
+                if dim[2] > 0 and fops.kernel_supported(xb, dim[2]):
+                    # K18: AdaGrad on the touched coordinates only, one wave per coordinate segment
+                    fops.fm_coord_update(xb, g, vx, sw[idx], w if dim[1] > 0 else None,
+                                         sg_w if dim[1] > 0 else None, V, sg_V, use, lr, lam[1], lam[2])
+                    continue
                 if xb.dense is not None:
                     rows = torch.arange(xb.nrows, device=dev).repeat_interleave(vec_size)
                     cols = torch.arange(vec_size, device=dev).repeat(xb.nrows)

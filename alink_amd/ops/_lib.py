@@ -85,6 +85,14 @@ _EXTRA_SIGNATURES = {
     "alink_als_padded_rank": [_c_int],
     "alink_topk_cross_f32": [_c_vp, _c_i64, _c_vp, _c_i64, _c_int, _c_int, _c_int, _c_vp, _c_vp, _c_int, _c_i64,
                              _c_vp],
+    "alink_colstats": [_c_vp, _c_i64, _c_int, _c_int, _c_int, _c_vp, _c_vp],
+    "alink_fm_forward_f64": [_c_vp, _c_vp, _c_vp, _c_i64, _c_int, _c_vp, _c_vp, _c_d, _c_vp, _c_vp, _c_vp],
+    "alink_fm_coord_update_f64": [_c_vp, _c_i64, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_int, _c_vp, _c_vp,
+                                  _c_vp, _c_vp, _c_vp, _c_d, _c_d, _c_d, _c_d, _c_vp],
+    "alink_w2v_sg_hs_f32": [_c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_int, _c_vp, _c_vp, _c_vp, _c_int, _c_vp, _c_vp,
+                            _c_int, _c_f, _c_int, _c_vp],
+    "alink_lda_gibbs": [_c_vp, _c_vp, _c_vp, _c_i64, _c_int, _c_vp, _c_vp, _c_vp, _c_d, _c_d, _c_d, _c_vp, _c_vp,
+                        _c_vp],
     "alink_als_gram_f32": [_c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_int, _c_int, _c_f, _c_vp, _c_vp, _c_vp],
 }
 
