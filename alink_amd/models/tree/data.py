@@ -193,7 +193,7 @@ def build_bins(mt: MTable, feature_cols: Sequence[str], cat_cols: Sequence[str],
                 cols_dev[c] = (v, null)
                 vs, ns = v[sidx], null[sidx]
                 local_samples.append(vs[~ns].cpu().numpy())
-        gathered = comm.all_gather_object(local_samples)
+        gathered = comm.all_gather_arrays(local_samples)          # tensor collectives, no pickling
         for j, c in enumerate(cont):
             allv = np.concatenate([g[j] for g in gathered]) if gathered else np.zeros(0)
             fi = feature_cols.index(c)

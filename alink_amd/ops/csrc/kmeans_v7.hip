@@ -3,7 +3,7 @@
 // One Lloyd superstep over this rank's rows (reference: KMeansAssignCluster.calc -> KMeansUtil.updateSumMatrix,
 // A/operator/common/clustering/kmeans/KMeansUtil.java:60-85) in ONE persistent launch, one 512-thread
 // workgroup per CU, each workgroup streaming a contiguous run of 64-row tiles HBM -> LDS with LDS-DMA
-// (buffer_load ... lds, 4 tiles = 64 KiB in flight, 6-slot ring).  The 8 waves split by ROLE so every SIMD
+// (buffer_load ... lds, 5-6 tiles = 80-96 KiB in flight, Plan<KB>).  The 8 waves split by ROLE so every SIMD
 // pairs a VALU-heavy wave with an MFMA-heavy one (the waves of a workgroup land on the 4 SIMDs round-robin):
 //
 //   distance waves 0..3 (tile i):   rows 16w..16w+15 of the tile
@@ -39,12 +39,22 @@ constexpr int D = 128;
 constexpr int ROWB = D * 2;                // 256 B per row
 constexpr int TR = 64;                     // rows per tile
 constexpr int TILE = TR * ROWB;            // 16 KiB
-constexpr int NBUF = 6;                    // X ring slots: tile i (distance), i-1 (accumulate), 4 in flight
-constexpr int AHEAD = 4;
-constexpr int OHB = 128 * TR * 2;          // one-hot image [128 c][64 rows] bf16 = 16 KiB (double-buffered)
-constexpr int OFF_OH = NBUF * TILE;
-constexpr int OFF_CNT = OFF_OH + 2 * OHB;  // u32 count[128]
-constexpr int LDS_BYTES = OFF_CNT + 128 * 4;
+constexpr int LDS_CAP = 160 * 1024;
+
+// LDS plan per centroid-block count KB: double-buffered one-hot image [16*KB c][64 rows] bf16, u32 count[128],
+// and as deep an X ring as the rest of the 160 KiB allows (6 tiles in flight for k <= 112, 5 for k <= 128;
+// measured 6.37 -> 6.01 ms at k=100 against the 4-deep ring, profiles/kmeans_r2_session4.txt)
+template <int KB>
+struct Plan {
+    static constexpr int OHB = 16 * KB * TR * 2;
+    static constexpr int NBUF_FIT = (LDS_CAP - 2 * OHB - 128 * 4) / TILE;
+    static constexpr int NBUF = NBUF_FIT > 8 ? 8 : NBUF_FIT;   // X ring slots: tile i, i-1, AHEAD in flight
+    static constexpr int AHEAD = NBUF - 2;
+    static constexpr int OFF_OH = NBUF * TILE;
+    static constexpr int OFF_CNT = OFF_OH + 2 * OHB;
+    static constexpr int LDS_BYTES = OFF_CNT + 128 * 4;
+    static_assert(LDS_BYTES <= LDS_CAP && AHEAD >= 3 && AHEAD <= 6, "LDS plan");
+};
 constexpr uint32_t NONE = 0xFFFFu;
 
 enum Mode { FULL = 0, LOAD_ONLY = 1, COMPUTE_ONLY = 2 };
@@ -63,7 +73,9 @@ __device__ __forceinline__ void barrier_lds() {
 
 // wait until this wave's loads of the tile `younger` tiles before the newest one issued have landed
 __device__ __forceinline__ void wait_tile(int younger) {
-    if (younger >= 3) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    if (younger >= 5) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+    else if (younger == 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (younger == 3) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     else if (younger == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     else if (younger == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -103,7 +115,9 @@ __global__ __launch_bounds__(512) void kmeans_v7_kernel(const __bf16* __restrict
                                                         const float* __restrict__ ninit, float* __restrict__ slab,
                                                         float* __restrict__ slab_cnt, int* __restrict__ assign_out,
                                                         int64_t ntiles, int64_t per) {
-    __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
+    using PL = Plan<KB>;
+    constexpr int NBUF = PL::NBUF, AHEAD = PL::AHEAD, OHB = PL::OHB, OFF_OH = PL::OFF_OH, OFF_CNT = PL::OFF_CNT;
+    __shared__ __attribute__((aligned(16))) char lds[PL::LDS_BYTES];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -173,6 +187,9 @@ __global__ __launch_bounds__(512) void kmeans_v7_kernel(const __bf16* __restrict
                 for (int b = 0; b < KB; ++b)
                     acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cf[b][s], xb, acc[b], 0, 0, 0);
             }
+            // all 4*KB MFMAs (KB independent accumulators per k-step) issue before the argmax VALU: without this
+            // fence the scheduler interleaves per-block argmax work and serialises the last MFMA of each chain
+            __builtin_amdgcn_sched_barrier(0);
             float best = -3.4e38f;
 #pragma unroll
             for (int b = 0; b < KB; ++b)

@@ -57,6 +57,19 @@ def prepare_centroids(C: torch.Tensor, device) -> Tuple[torch.Tensor, torch.Tens
     return cpad, ninit
 
 
+KERNEL_VERSIONS = ("v7",)
+DEFAULT_KERNEL = "v7"
+
+
+def kernel_version() -> str:
+    """Fused assign+accumulate kernel (csrc/kmeans_v7.hip; ``ALINK_KMEANS_KERNEL`` selects among the shipped
+    versions — v9, a lagged register-prefetch accumulate, measured no faster and was dropped)."""
+    v = __import__("os").environ.get("ALINK_KMEANS_KERNEL", DEFAULT_KERNEL)
+    if v not in KERNEL_VERSIONS:
+        raise ValueError(f"ALINK_KMEANS_KERNEL must be one of {KERNEL_VERSIONS}")
+    return v
+
+
 def _num_cus(device) -> int:
     return torch.cuda.get_device_properties(device).multi_processor_count
 
@@ -78,7 +91,8 @@ def assign_accumulate_hip(X: torch.Tensor, C: torch.Tensor, grid: Optional[int] 
         raise ValueError("assign_out must be a contiguous int32 [N] tensor on X's device")
     cpad, ninit = prepare_centroids(C, dev)
     n = X.shape[0]
-    grid = int(L.alink_kmeans_v7_grid(n, grid if grid is not None else _num_cus(dev)))
+    ver = kernel_version()
+    grid = int(getattr(L, f"alink_kmeans_{ver}_grid")(n, grid if grid is not None else _num_cus(dev)))
     key = (dev.index, grid)
     if key not in _BUF:
         _BUF[key] = (torch.empty((grid, HIP_KMAX, HIP_D), dtype=torch.float32, device=dev),
@@ -86,11 +100,11 @@ def assign_accumulate_hip(X: torch.Tensor, C: torch.Tensor, grid: Optional[int] 
     slab, slab_cnt = _BUF[key]
     out = torch.empty((k, HIP_D + 1), dtype=torch.float64, device=dev)
     st = _lib.stream_ptr(dev)
-    rc = L.alink_kmeans_assign_accum_bf16_v7(X.data_ptr(), n, cpad.data_ptr(), ninit.data_ptr(), k, slab.data_ptr(),
-                                             slab_cnt.data_ptr(), grid, st,
-                                             None if assign_out is None else assign_out.data_ptr(), int(mode))
+    rc = getattr(L, f"alink_kmeans_assign_accum_bf16_{ver}")(
+        X.data_ptr(), n, cpad.data_ptr(), ninit.data_ptr(), k, slab.data_ptr(), slab_cnt.data_ptr(), grid, st,
+        None if assign_out is None else assign_out.data_ptr(), int(mode))
     if rc != 0:
-        raise RuntimeError(f"alink_kmeans_assign_accum_bf16_v7 failed: {rc}")
+        raise RuntimeError(f"alink_kmeans_assign_accum_bf16_{ver} failed: {rc}")
     rc = L.alink_kmeans_reduce_slabs(slab.data_ptr(), slab_cnt.data_ptr(), grid, k, out.data_ptr(), st)
     if rc != 0:
         raise RuntimeError(f"alink_kmeans_reduce_slabs failed: {rc}")

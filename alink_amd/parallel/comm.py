@@ -36,15 +36,17 @@ class CommStats:
     def __init__(self):
         self.calls = 0
         self.bytes = 0
+        self.oneshot = 0
         self.time_s = 0.0
 
     def reset(self):
         self.calls = 0
         self.bytes = 0
+        self.oneshot = 0
         self.time_s = 0.0
 
     def as_dict(self):
-        return {"collectives": self.calls, "bytes": self.bytes}
+        return {"collectives": self.calls, "bytes": self.bytes, "oneshot": self.oneshot}
 
 
 STATS = CommStats()
@@ -112,11 +114,44 @@ def object_group():
     return _OBJ_GROUP
 
 
+def collective_device() -> torch.device:
+    """Where tensors must live for this job's collectives: the rank's GPU under RCCL, the host under gloo."""
+    return device_for_rank() if _backend() == "nccl" else torch.device("cpu")
+
+
+def all_gather_arrays(arrays: List[np.ndarray], dtype=np.float64) -> List[List[np.ndarray]]:
+    """Gather a list of variable-length 1-D arrays from every rank as TWO tensor collectives (lengths + one
+    packed buffer over RCCL/gloo) instead of a pickled object gather: result[rank][j] = that rank's arrays[j]."""
+    ws = get_world_size()
+    if ws == 1:
+        return [list(arrays)]
+    dev = collective_device()
+    lens = torch.tensor([int(a.size) for a in arrays], dtype=torch.int64)
+    flat = torch.from_numpy(np.ascontiguousarray(np.concatenate(arrays).astype(dtype)) if arrays else
+                            np.zeros(0, dtype))
+    all_lens = all_gather_tensor(lens.to(dev)).cpu().view(ws, len(arrays))
+    all_flat = all_gather_varlen(flat.to(dev)).cpu().numpy()
+    out, off = [], 0
+    for r in range(ws):
+        part = []
+        for j in range(len(arrays)):
+            n = int(all_lens[r, j])
+            part.append(all_flat[off:off + n])
+            off += n
+        out.append(part)
+    return out
+
+
 def _backend() -> str:
     return dist.get_backend() if dist.is_initialized() else "none"
 
 
 _OPS = {"sum": "SUM", "max": "MAX", "min": "MIN", "prod": "PRODUCT"}
+
+
+def _oneshot_max() -> int:
+    from . import oneshot
+    return oneshot.MAX_BYTES if oneshot.enabled() else -1
 
 
 def all_reduce(t: torch.Tensor, op: str = "sum") -> torch.Tensor:
@@ -129,6 +164,14 @@ def all_reduce(t: torch.Tensor, op: str = "sum") -> torch.Tensor:
     rop = getattr(dist.ReduceOp, _OPS[op.lower()])
     STATS.calls += 1
     STATS.bytes += t.numel() * t.element_size()
+    if t.is_cuda and _backend() == "nccl" and op.lower() in ("sum", "max", "min") and \
+            t.dtype in (torch.float32, torch.float64) and t.numel() * t.element_size() <= _oneshot_max():
+        # small buffers: one kernel over IPC-mapped peer memory (parallel/oneshot.py, K31), opt-in
+        from . import oneshot
+        inst = oneshot.get()
+        if inst is not None:
+            STATS.oneshot += 1
+            return inst.all_reduce_(t, op.lower())
     if t.is_cuda and _backend() != "nccl":
         h = t.cpu()
         dist.all_reduce(h, op=rop)

@@ -1,0 +1,183 @@
+"""One-shot xGMI all-reduce for small buffers (kernel ``ops/csrc/allreduce.hip``).
+
+Every rank allocates an uncached staging area (two slots of ``cap_bytes`` + per-block flags), exports it with
+``hipIpcGetMemHandle``, the handles are exchanged once over the host (gloo) group and opened on every peer.  An
+all-reduce is then one kernel on the caller's stream: copy-in, release a sequence number to every peer, poll
+the own flags, sum the P staging slots in rank order.  No RCCL call, no host round trip, bit-identical results
+on all ranks.
+
+Enabled with ``ALINK_ONESHOT_ALLREDUCE=1`` for device tensors of at most ``ALINK_ONESHOT_MAX_BYTES`` (default
+1 MiB) on a ``nccl`` job; ``comm.all_reduce`` falls back to RCCL for anything else.  Setup is collective and
+validated against RCCL on a probe buffer; if any rank fails, every rank disables the path (the decision is
+agreed by a MIN all-reduce, so ranks never diverge between the two implementations).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import List, Optional
+
+import torch
+
+from ..ops import _lib
+
+__all__ = ["OneShot", "get", "enabled", "MAX_BYTES"]
+
+MAX_BYTES = int(os.environ.get("ALINK_ONESHOT_MAX_BYTES", str(1 << 20)))
+BLOCKS = 32
+TIMEOUT_S = float(os.environ.get("ALINK_ONESHOT_TIMEOUT_S", "60"))
+_DT = {torch.float32: 0, torch.float64: 1}
+_OP = {"sum": 0, "max": 1, "min": 2}
+
+
+def _sigs(L):
+    c_vp, c_i64, c_int = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int
+    L.alink_ar_alloc.argtypes = [c_i64, ctypes.POINTER(c_vp)]
+    L.alink_ar_ipc_handle.argtypes = [c_vp, c_vp]
+    L.alink_ar_ipc_open.argtypes = [c_vp, ctypes.POINTER(c_vp)]
+    L.alink_ar_ipc_close.argtypes = [c_vp]
+    L.alink_ar_free.argtypes = [c_vp]
+    L.alink_oneshot_allreduce.argtypes = [c_vp, c_vp, c_i64, c_int, c_int, c_int, c_int, ctypes.c_uint32, c_vp, c_vp,
+                                          c_i64, c_int, c_int, ctypes.c_double, c_vp, c_vp]
+    for f in ("alink_ar_alloc", "alink_ar_ipc_handle", "alink_ar_ipc_open", "alink_ar_ipc_close", "alink_ar_free",
+              "alink_oneshot_allreduce", "alink_ar_handle_size"):
+        getattr(L, f).restype = c_int
+
+
+class OneShot:
+    """Staging buffers + peer tables for ``P`` ranks.  ``bases[p]`` are device addresses valid in this process
+    (IPC-opened for peers, own allocation for ``rank``); a single process may also pass P local allocations
+    (single-GPU tests of the reduction)."""
+
+    def __init__(self, device, P: int, rank: int, cap_bytes: int, bases: List[int], owned: List[int],
+                 opened: List[int]):
+        self.L = _lib.require()
+        _sigs(self.L)
+        self.device, self.P, self.rank, self.cap = device, P, rank, int(cap_bytes)
+        self.owned, self.opened = owned, opened
+        self.flag_off = 2 * self.cap
+        self.peer_data = torch.tensor(bases, dtype=torch.int64, device=device)
+        self.peer_flags = torch.tensor([b + self.flag_off for b in bases], dtype=torch.int64, device=device)
+        self.err = torch.zeros(1, dtype=torch.int32, device=device)
+        self.seq = 0
+        self.calls = 0
+
+    @staticmethod
+    def region_bytes(cap_bytes: int, P: int) -> int:
+        return 2 * cap_bytes + BLOCKS * max(P, 1) * 4 + 256
+
+    @staticmethod
+    def alloc(cap_bytes: int, P: int) -> int:
+        L = _lib.require()
+        _sigs(L)
+        p = ctypes.c_void_p()
+        rc = L.alink_ar_alloc(OneShot.region_bytes(cap_bytes, P), ctypes.byref(p))
+        if rc != 0:
+            raise RuntimeError(f"alink_ar_alloc failed: {rc}")
+        return int(p.value)
+
+    def launch(self, t: torch.Tensor, out: torch.Tensor, op: str = "sum", rank: Optional[int] = None,
+               phases: int = 3, seq: Optional[int] = None) -> torch.Tensor:
+        n = t.numel()
+        if t.dtype not in _DT or n * t.element_size() > self.cap:
+            raise ValueError("one-shot all-reduce: unsupported dtype or buffer larger than the staging slot")
+        if seq is None:
+            self.seq += 1
+            seq = self.seq
+        rc = self.L.alink_oneshot_allreduce(t.data_ptr(), out.data_ptr(), n, _DT[t.dtype], _OP[op], self.P,
+                                            self.rank if rank is None else rank, seq & 0xFFFFFFFF,
+                                            self.peer_data.data_ptr(), self.peer_flags.data_ptr(), self.cap, BLOCKS,
+                                            phases, TIMEOUT_S, self.err.data_ptr(), _lib.stream_ptr(self.device))
+        if rc != 0:
+            raise RuntimeError(f"alink_oneshot_allreduce failed: {rc}")
+        self.calls += 1
+        return out
+
+    def all_reduce_(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
+        flat = t.reshape(-1)
+        src = flat if flat.is_contiguous() else flat.contiguous()
+        res = torch.empty_like(src)
+        self.launch(src, res, op)
+        if self.calls % 256 == 0 and int(self.err.item()) != 0:
+            raise RuntimeError("one-shot all-reduce timed out waiting for a peer (results were poisoned with NaN)")
+        t.copy_(res.view_as(t))
+        return t
+
+    def close(self):
+        for p in self.opened:
+            self.L.alink_ar_ipc_close(ctypes.c_void_p(p))
+        for p in self.owned:
+            self.L.alink_ar_free(ctypes.c_void_p(p))
+        self.opened, self.owned = [], []
+
+
+_INSTANCE: Optional[OneShot] = None
+_TRIED = False
+
+
+def enabled() -> bool:
+    return os.environ.get("ALINK_ONESHOT_ALLREDUCE", "0") == "1"
+
+
+def get() -> Optional[OneShot]:
+    """Collective on first use: every rank of the job must call it at the same point (comm.all_reduce does)."""
+    global _INSTANCE, _TRIED
+    if _TRIED:
+        return _INSTANCE
+    _TRIED = True
+    from . import comm
+    import torch.distributed as dist
+    P, rank = comm.get_world_size(), comm.get_rank()
+    dev = comm.device_for_rank()
+    ok, inst, base, opened = 1.0, None, None, []
+    handles = None
+    try:
+        L = _lib.require()
+        _sigs(L)
+        base = OneShot.alloc(MAX_BYTES, P)
+        hs = int(L.alink_ar_handle_size())
+        buf = ctypes.create_string_buffer(hs)
+        rc = L.alink_ar_ipc_handle(ctypes.c_void_p(base), buf)
+        if rc != 0:
+            raise RuntimeError(f"hipIpcGetMemHandle failed: {rc}")
+        mine = bytes(buf.raw)
+    except Exception:
+        ok, mine = 0.0, b""
+    handles = comm.all_gather_object(mine)
+    bases = []
+    if ok:
+        try:
+            for p in range(P):
+                if p == rank:
+                    bases.append(base)
+                    continue
+                if not handles[p]:
+                    raise RuntimeError("peer has no handle")
+                q = ctypes.c_void_p()
+                rc = L.alink_ar_ipc_open(ctypes.create_string_buffer(handles[p], len(handles[p])), ctypes.byref(q))
+                if rc != 0:
+                    raise RuntimeError(f"hipIpcOpenMemHandle failed: {rc}")
+                opened.append(int(q.value))
+                bases.append(int(q.value))
+            inst = OneShot(dev, P, rank, MAX_BYTES, bases, [base], opened)
+        except Exception:
+            ok = 0.0
+    flag = torch.tensor([ok], dtype=torch.float64, device=dev)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    if flag.item() < 1.0:
+        if inst is not None:
+            inst.close()
+        return None
+    # validate against RCCL on a probe buffer before trusting the path
+    probe = torch.arange(1000, dtype=torch.float64, device=dev) * (rank + 1) + 0.25
+    ref = probe.clone()
+    dist.all_reduce(ref)
+    got = inst.all_reduce_(probe.clone())
+    good = torch.tensor([1.0 if torch.equal(got, ref) and int(inst.err.item()) == 0 else 0.0],
+                        dtype=torch.float64, device=dev)
+    dist.all_reduce(good, op=dist.ReduceOp.MIN)
+    if good.item() < 1.0:
+        inst.close()
+        return None
+    _INSTANCE = inst
+    return inst

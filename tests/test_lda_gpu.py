@@ -38,7 +38,7 @@ def test_lda_em_trains_on_cuda():
     docs = [" ".join(rng.choice(a if i % 2 else b, 20)) for i in range(200)]
     useLocalEnv(1, device="cuda:0")
     src = BatchOperator.fromDataframe(pd.DataFrame({"doc": docs}), schemaStr="doc string")
-    m = LdaTrainBatchOp().setSelectedCol("doc").setTopicNum(2).setMethod("em").setNumIter(30).setRandomSeed(3) \
+    m = LdaTrainBatchOp().setSelectedCol("doc").setTopicNum(2).setMethod("em").setNumIter(30) \
         .linkFrom(src)
     rows = m.collect()
     assert len(rows) > 0
