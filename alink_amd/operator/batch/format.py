@@ -26,11 +26,23 @@ __all__ = ["BaseFormatTransBatchOp", "AnyToTripleBatchOp", "TripleToAnyBatchOp",
            "JsonToColumnsBatchOp", "KvToColumnsBatchOp", "JsonValueBatchOp"]
 
 
+def _all_format_params():
+    """Every column / schema param of the concrete X-to-Y ops: the generic ops (BaseFormatTrans, AnyToTriple,
+    TripleToAny) take any source and target format, so they accept all of them."""
+    from ...params import op_params
+    seen = {}
+    for f in FORMATS + ["Triple"]:
+        for t in FORMATS + ["Triple"]:
+            for p in op_params(f"{f}To{t}BatchOp"):
+                seen.setdefault(p.name, p)
+    return list(seen.values())
+
+
 class BaseFormatTransBatchOp(MapBatchOp):
     """Generic ``fromFormat`` -> ``toFormat`` conversion (``BaseFormatTransBatchOp.java``)."""
     MAPPER = F.FormatTransMapper
     EXTRA_PARAMS = [ParamInfo("fromFormat", str, "the format type of trans from", default=None),
-                    ParamInfo("toFormat", str, "the format type of trans to", default=None)]
+                    ParamInfo("toFormat", str, "the format type of trans to", default=None)] + _all_format_params()
     FROM: Optional[str] = None
     TO: Optional[str] = None
 

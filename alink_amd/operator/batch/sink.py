@@ -8,6 +8,7 @@ from __future__ import annotations
 import os
 from typing import Optional
 
+from ...common.javafmt import java_double_str, java_str
 from ...common.linalg import SparseVector, Vector, VectorUtil
 from ...common.params import Params
 from ...common.types import Types
@@ -101,9 +102,9 @@ class LibSvmSinkBatchOp(BaseSinkBatchOp):
         for r in rows:
             v = VectorUtil.getVector(r[vi])
             if isinstance(v, SparseVector):
-                body = " ".join(f"{int(i) + 1}:{x!r}" for i, x in zip(v.indices, v.values))
+                body = " ".join(f"{int(i) + 1}:{java_double_str(float(x))}" for i, x in zip(v.indices, v.values))
             else:
-                body = " ".join(f"{i + 1}:{x!r}" for i, x in enumerate(v.data))
-            lab = r[li]
+                body = " ".join(f"{i + 1}:{java_double_str(float(x))}" for i, x in enumerate(v.data))
+            lab = java_str(r[li])
             lines.append(f"{lab} {body}".rstrip())
         write_lines(self.getFilePath(), lines, self.getOverwriteSink())

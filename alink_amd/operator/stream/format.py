@@ -17,7 +17,7 @@ from ...common.table import MTable, Row, infer_type
 from ...common.types import TableSchema, Types, type_from_str
 from ...models.dataproc import format as F
 from ...models.dataproc import vector as V
-from ..batch.format import FORMATS
+from ..batch.format import FORMATS, BaseFormatTransBatchOp
 from ..batch.utils import _UDFMapper
 from .base import FlatMapStreamOp, MapStreamOp, StreamOperator, _register_upstream_sources
 
@@ -27,8 +27,7 @@ __all__ = ["BaseFormatTransStreamOp", "AnyToTripleStreamOp", "CsvToColumnsStream
 
 class BaseFormatTransStreamOp(MapStreamOp):
     MAPPER = F.FormatTransMapper
-    EXTRA_PARAMS = [ParamInfo("fromFormat", str, "the format type of trans from", default=None),
-                    ParamInfo("toFormat", str, "the format type of trans to", default=None)]
+    EXTRA_PARAMS = list(BaseFormatTransBatchOp.EXTRA_PARAMS)      # fromFormat / toFormat + every format's columns
     FROM: Optional[str] = None
     TO: Optional[str] = None
 
@@ -160,8 +159,12 @@ for _f in FORMATS:
         _make(f"{_f}To{_t}StreamOp", BaseFormatTransStreamOp, {"FROM": _f.upper(), "TO": _t.upper()})
     _make(f"{_f}ToTripleStreamOp", AnyToTripleStreamOp, {"FROM": _f.upper()})
 
-# VectorToColumnsStreamOp above is the format flavour; it also accepts the vector flavour's outputCols
-VectorToColumnsStreamOp.MAPPER = V.VectorToColumnsMapper  # noqa: F821
+# VectorToColumnsStreamOp: both flavours, like the batch op (vector: selectedCol + outputCols; format: vectorCol +
+# schemaStr)
+from ..batch.dataproc import VectorToColumnsBatchOp as _V2CB  # noqa: E402
+VectorToColumnsStreamOp = type("VectorToColumnsStreamOp", (MapStreamOp,), dict(  # noqa: F811
+    MAPPER=V.VectorToColumnsMapper, EXTRA_PARAMS=list(_V2CB.EXTRA_PARAMS), __module__=__name__,
+    __doc__="VectorToColumnsStreamOp (stream twin of the batch op)."))
 
 for _n, _m in {"VectorAssemblerStreamOp": V.VectorAssemblerMapper,
                "VectorElementwiseProductStreamOp": V.VectorElementwiseProductMapper,

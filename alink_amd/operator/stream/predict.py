@@ -19,12 +19,16 @@ from ...models.classification.naive_bayes import NaiveBayesTextModelMapper
 from ...models.nlp import text as _T
 from ...models.nlp import word2vec as _W
 from ...models.recommendation.als import AlsModelMapper
+from ...models.recommendation.fm import FmModelMapper
 from ...models.tree.model import GbdtModelMapper, RandomForestModelMapper
 from ...models.regression.glm import GlmModelMapper
 from ...models.regression.isotonic import IsotonicRegressionModelMapper
 from .base import MapStreamOp, ModelMapStreamOp
 
 _PREDICTORS = {
+    # FM has no stream predictor in the reference; the twins below apply the same FmModelMapper per micro-batch
+    "FmClassifierPredictStreamOp": FmModelMapper,
+    "FmRegressorPredictStreamOp": FmModelMapper,
     "KMeansPredictStreamOp": KMeansModelMapper,
     "LogisticRegressionPredictStreamOp": LinearModelMapper,
     "LinearSvmPredictStreamOp": LinearModelMapper,

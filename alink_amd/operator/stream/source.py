@@ -29,7 +29,7 @@ class _TableReplaySource(StreamSourceOp):
     BATCH_OP = None
 
     def _table(self) -> MTable:
-        op = self.BATCH_OP(self.getParams().clone())
+        op = self.BATCH_OP(params=self.getParams().clone())
         op.setMLEnvironmentId(self.getMLEnvironmentId())
         return op.getOutputTable()
 
@@ -111,7 +111,9 @@ class NumSeqSourceStreamOp(_TableReplaySource):
 
 class RandomTableSourceStreamOp(_TableReplaySource):
     BATCH_OP = B.RandomTableSourceBatchOp
+    EXTRA_PARAMS = list(B.RandomTableSourceBatchOp.PARAMS)
 
 
 class RandomVectorSourceStreamOp(_TableReplaySource):
     BATCH_OP = B.RandomVectorSourceBatchOp
+    EXTRA_PARAMS = list(B.RandomVectorSourceBatchOp.PARAMS)

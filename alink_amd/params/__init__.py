@@ -85,8 +85,11 @@ def interface_params(name: str, _seen=None) -> List[ParamInfo]:
 
 
 def op_params(op_name: str) -> List[ParamInfo]:
-    """Param list of a reference operator / pipeline stage by class name (walks ``extends``)."""
+    """Param list of a reference operator / pipeline stage by class name (walks ``extends``).  A stream operator
+    the reference does not have (e.g. ``LdaPredictStreamOp``) takes the params of its batch twin."""
     out: Dict[str, ParamInfo] = {}
+    if op_name not in _spec.OPS and op_name.endswith("StreamOp") and op_name[:-8] + "BatchOp" in _spec.OPS:
+        op_name = op_name[:-8] + "BatchOp"
     cur = op_name
     chain = []
     while cur and cur in _spec.OPS and cur not in chain:

@@ -1,0 +1,323 @@
+"""Operator catalogue coverage: every *StreamOp twin must give the rows its *BatchOp gives on the same data
+(reference: the stream ops wrap the same mappers, A/operator/stream/utils/{MapStreamOp,ModelMapStreamOp}.java),
+every model family trains / predicts in batch and stream, and the format-conversion family round-trips."""
+import numpy as np
+import pandas as pd
+import pytest
+
+import alink_amd as A
+from alink_amd import BatchOperator, StreamOperator, useLocalEnv
+from alink_amd.operator.stream.utils import CollectStreamOp
+
+
+@pytest.fixture(autouse=True)
+def _env():
+    useLocalEnv(1)
+
+
+def _df(n=40, seed=0):
+    rng = np.random.default_rng(seed)
+    x0 = rng.normal(size=n).round(4)
+    x1 = rng.normal(size=n).round(4)
+    x2 = rng.uniform(1, 3, size=n).round(4)
+    y = (x0 + 0.5 * x1 > 0).astype(int)
+    t = 1.5 * x0 - x1 + 0.3 * x2 + rng.normal(scale=0.1, size=n).round(4)
+    words = np.array(["a", "b", "c", "d", "e"])
+    text = [" ".join(words[rng.integers(0, 5, 4)]) for _ in range(n)]
+    cat = words[rng.integers(0, 3, n)]
+    vec = [f"{a} {b} {c}" for a, b, c in zip(x0, x1, x2)]
+    return pd.DataFrame({"id": np.arange(n), "x0": x0, "x1": x1, "x2": x2, "y": y, "t": t.round(4), "text": text,
+                         "cat": cat, "vec": vec})
+
+
+SCHEMA = "id long, x0 double, x1 double, x2 double, y int, t double, text string, cat string, vec string"
+FEATS = ["x0", "x1", "x2"]
+
+
+def _bsrc(df=None):
+    return BatchOperator.fromDataframe(_df() if df is None else df, schemaStr=SCHEMA)
+
+
+def _ssrc(df=None):
+    return StreamOperator.fromDataframe(_df() if df is None else df, schemaStr=SCHEMA)
+
+
+def _norm(v):
+    if isinstance(v, float):
+        return round(v, 6)
+    return str(v) if v is not None and not isinstance(v, (int, str, bool)) else v
+
+
+def _rows(rows):
+    return sorted((tuple(_norm(x) for x in r) for r in rows), key=lambda r: str(r))
+
+
+def _stream_rows(stream_op):
+    box = []
+    stream_op.link(CollectStreamOp(box))
+    StreamOperator.execute()
+    return box
+
+
+def _twin(batch_op, stream_op, df=None):
+    b = batch_op.linkFrom(_bsrc(df)).collect()
+    s = _stream_rows(stream_op.linkFrom(_ssrc(df)))
+    assert len(b) == len(s) > 0
+    assert _rows(b) == _rows(s)
+    return b
+
+
+# ------------------------------------------------------------------------------------------- mapper twins
+MAPPERS = [
+    ("Binarizer", A.BinarizerBatchOp, A.BinarizerStreamOp, lambda o: o.setSelectedCol("x0").setThreshold(0.1).setOutputCol("o")),
+    ("Bucketizer", A.BucketizerBatchOp, A.BucketizerStreamOp, lambda o: o.setSelectedCols(["x0"]).setCutsArray([[-0.5, 0.5]]).setOutputCols(["o"])),
+    ("VectorNormalize", A.VectorNormalizeBatchOp, A.VectorNormalizeStreamOp, lambda o: o.setSelectedCol("vec").setP(2.0)),
+    ("VectorPolynomialExpand", A.VectorPolynomialExpandBatchOp, A.VectorPolynomialExpandStreamOp, lambda o: o.setSelectedCol("vec").setDegree(2).setOutputCol("o")),
+    ("VectorSlice", A.VectorSliceBatchOp, A.VectorSliceStreamOp, lambda o: o.setSelectedCol("vec").setIndices([0, 2]).setOutputCol("o")),
+    ("VectorSizeHint", A.VectorSizeHintBatchOp, A.VectorSizeHintStreamOp, lambda o: o.setSelectedCol("vec").setSize(3)),
+    ("VectorElementwiseProduct", A.VectorElementwiseProductBatchOp, A.VectorElementwiseProductStreamOp, lambda o: o.setSelectedCol("vec").setScalingVector("1.0 2.0 3.0").setOutputCol("o")),
+    ("VectorInteraction", A.VectorInteractionBatchOp, A.VectorInteractionStreamOp, lambda o: o.setSelectedCols(["vec", "vec"]).setOutputCol("o")),
+    ("RegexTokenizer", A.RegexTokenizerBatchOp, A.RegexTokenizerStreamOp, lambda o: o.setSelectedCol("text").setOutputCol("o")),
+    ("NGram", A.NGramBatchOp, A.NGramStreamOp, lambda o: o.setSelectedCol("text").setN(2).setOutputCol("o")),
+    ("StopWordsRemover", A.StopWordsRemoverBatchOp, A.StopWordsRemoverStreamOp, lambda o: o.setSelectedCol("text").setOutputCol("o")),
+    ("Segment", A.SegmentBatchOp, A.SegmentStreamOp, lambda o: o.setSelectedCol("text").setOutputCol("o")),
+    ("FeatureHasher", A.FeatureHasherBatchOp, A.FeatureHasherStreamOp, lambda o: o.setSelectedCols(["x0", "cat"]).setOutputCol("o").setNumFeatures(64)),
+    ("VectorAssembler", A.VectorAssemblerBatchOp, A.VectorAssemblerStreamOp, lambda o: o.setSelectedCols(["x0", "x1", "vec"]).setOutputCol("o")),
+    ("DCT", A.DCTBatchOp, A.DCTStreamOp, lambda o: o.setSelectedCol("vec").setOutputCol("o")),
+    ("Select", A.SelectBatchOp, A.SelectStreamOp, lambda o: o.setClause("id, x0 * 2 as z")),
+    ("Where", A.WhereBatchOp, A.WhereStreamOp, lambda o: o.setClause("x0 > 0")),
+    ("Filter", A.FilterBatchOp, A.FilterStreamOp, lambda o: o.setClause("x1 < 0")),
+    ("As", A.AsBatchOp, A.AsStreamOp, lambda o: o.setClause("a, b, c, d, e, f, g, h, i")),
+    ("VectorSerialize", A.VectorSerializeBatchOp, A.VectorSerializeStreamOp, lambda o: o),
+]
+
+
+@pytest.mark.parametrize("name,b,s,cfg", MAPPERS, ids=[m[0] for m in MAPPERS])
+def test_mapper_stream_twin_equals_batch(name, b, s, cfg):
+    _twin(cfg(b()), cfg(s()))
+
+
+# ------------------------------------------------------------------------------------------- model twins
+def _lin(o):
+    return o.setFeatureCols(FEATS).setLabelCol("t")
+
+
+def _cls(o):
+    return o.setFeatureCols(FEATS).setLabelCol("y")
+
+
+MODELS = [
+    ("LinearReg", _lin), ("RidgeReg", lambda o: _lin(o).setLambda(0.1)), ("LassoReg", lambda o: _lin(o).setLambda(0.01)),
+    ("LinearSvm", _cls), ("LogisticRegression", _cls), ("Softmax", _cls),
+    ("GbdtReg", lambda o: _lin(o).setNumTrees(3).setMinSamplesPerLeaf(2)),
+    ("Gbdt", lambda o: _cls(o).setNumTrees(3).setMinSamplesPerLeaf(2)),
+    ("DecisionTree", lambda o: _cls(o).setMaxDepth(3)), ("DecisionTreeReg", lambda o: _lin(o).setMaxDepth(3)),
+    ("RandomForest", lambda o: _cls(o).setNumTrees(3).setMaxDepth(3)),
+    ("FmRegressor", lambda o: _lin(o).setNumEpochs(2).setNumFactor(4)),
+    ("Glm", lambda o: _lin(o)),
+    ("IsotonicReg", lambda o: o.setFeatureCol("x0").setLabelCol("t")),
+    ("KMeans", lambda o: o.setVectorCol("vec").setK(3)),
+    ("Gmm", lambda o: o.setVectorCol("vec").setK(2)),
+    ("NaiveBayesText", lambda o: o.setVectorCol("vec").setLabelCol("y") if hasattr(o, "setVectorCol") else o),
+    ("StandardScaler", lambda o: o.setSelectedCols(FEATS)), ("MinMaxScaler", lambda o: o.setSelectedCols(FEATS)),
+    ("MaxAbsScaler", lambda o: o.setSelectedCols(FEATS)), ("Imputer", lambda o: o.setSelectedCols(FEATS)),
+    ("VectorStandardScaler", lambda o: o.setSelectedCol("vec")), ("VectorMinMaxScaler", lambda o: o.setSelectedCol("vec")),
+    ("VectorMaxAbsScaler", lambda o: o.setSelectedCol("vec")), ("VectorImputer", lambda o: o.setSelectedCol("vec")),
+    ("QuantileDiscretizer", lambda o: o.setSelectedCols(["x0", "x1"]).setNumBuckets(3)),
+    ("StringIndexer", lambda o: o.setSelectedCol("cat")),
+    ("MultiStringIndexer", lambda o: o.setSelectedCols(["cat", "text"])),
+    ("OneHot", lambda o: o.setSelectedCols(["cat"])),
+    ("DocCountVectorizer", lambda o: o.setSelectedCol("text")),
+    ("DocHashCountVectorizer", lambda o: o.setSelectedCol("text")),
+    ("Word2Vec", lambda o: o.setSelectedCol("text").setMinCount(1).setVectorSize(4)),
+    ("Lda", lambda o: o.setSelectedCol("text").setTopicNum(2)),
+]
+MODEL_OPS = {
+    "LinearReg": (A.LinearRegTrainBatchOp, A.LinearRegPredictBatchOp, A.LinearRegPredictStreamOp),
+    "RidgeReg": (A.RidgeRegTrainBatchOp, A.RidgeRegPredictBatchOp, A.RidgeRegPredictStreamOp),
+    "LassoReg": (A.LassoRegTrainBatchOp, A.LassoRegPredictBatchOp, A.LassoRegPredictStreamOp),
+    "LinearSvm": (A.LinearSvmTrainBatchOp, A.LinearSvmPredictBatchOp, A.LinearSvmPredictStreamOp),
+    "LogisticRegression": (A.LogisticRegressionTrainBatchOp, A.LogisticRegressionPredictBatchOp, A.LogisticRegressionPredictStreamOp),
+    "Softmax": (A.SoftmaxTrainBatchOp, A.SoftmaxPredictBatchOp, A.SoftmaxPredictStreamOp),
+    "GbdtReg": (A.GbdtRegTrainBatchOp, A.GbdtRegPredictBatchOp, A.GbdtRegPredictStreamOp),
+    "Gbdt": (A.GbdtTrainBatchOp, A.GbdtPredictBatchOp, A.GbdtPredictStreamOp),
+    "DecisionTree": (A.DecisionTreeTrainBatchOp, A.DecisionTreePredictBatchOp, A.DecisionTreePredictStreamOp),
+    "DecisionTreeReg": (A.DecisionTreeRegTrainBatchOp, A.DecisionTreeRegPredictBatchOp, A.DecisionTreeRegPredictStreamOp),
+    "RandomForest": (A.RandomForestTrainBatchOp, A.RandomForestPredictBatchOp, A.RandomForestPredictStreamOp),
+    "FmRegressor": (A.FmRegressorTrainBatchOp, A.FmRegressorPredictBatchOp, A.FmRegressorPredictStreamOp),
+    "Glm": (A.GlmTrainBatchOp, A.GlmPredictBatchOp, A.GlmPredictStreamOp),
+    "IsotonicReg": (A.IsotonicRegTrainBatchOp, A.IsotonicRegPredictBatchOp, A.IsotonicRegPredictStreamOp),
+    "KMeans": (A.KMeansTrainBatchOp, A.KMeansPredictBatchOp, A.KMeansPredictStreamOp),
+    "Gmm": (A.GmmTrainBatchOp, A.GmmPredictBatchOp, A.GmmPredictStreamOp),
+    "NaiveBayesText": (A.NaiveBayesTextTrainBatchOp, A.NaiveBayesTextPredictBatchOp, A.NaiveBayesTextPredictStreamOp),
+    "StandardScaler": (A.StandardScalerTrainBatchOp, A.StandardScalerPredictBatchOp, A.StandardScalerPredictStreamOp),
+    "MinMaxScaler": (A.MinMaxScalerTrainBatchOp, A.MinMaxScalerPredictBatchOp, A.MinMaxScalerPredictStreamOp),
+    "MaxAbsScaler": (A.MaxAbsScalerTrainBatchOp, A.MaxAbsScalerPredictBatchOp, A.MaxAbsScalerPredictStreamOp),
+    "Imputer": (A.ImputerTrainBatchOp, A.ImputerPredictBatchOp, A.ImputerPredictStreamOp),
+    "VectorStandardScaler": (A.VectorStandardScalerTrainBatchOp, A.VectorStandardScalerPredictBatchOp, A.VectorStandardScalerPredictStreamOp),
+    "VectorMinMaxScaler": (A.VectorMinMaxScalerTrainBatchOp, A.VectorMinMaxScalerPredictBatchOp, A.VectorMinMaxScalerPredictStreamOp),
+    "VectorMaxAbsScaler": (A.VectorMaxAbsScalerTrainBatchOp, A.VectorMaxAbsScalerPredictBatchOp, A.VectorMaxAbsScalerPredictStreamOp),
+    "VectorImputer": (A.VectorImputerTrainBatchOp, A.VectorImputerPredictBatchOp, A.VectorImputerPredictStreamOp),
+    "QuantileDiscretizer": (A.QuantileDiscretizerTrainBatchOp, A.QuantileDiscretizerPredictBatchOp, A.QuantileDiscretizerPredictStreamOp),
+    "StringIndexer": (A.StringIndexerTrainBatchOp, A.StringIndexerPredictBatchOp, A.StringIndexerPredictStreamOp),
+    "MultiStringIndexer": (A.MultiStringIndexerTrainBatchOp, A.MultiStringIndexerPredictBatchOp, A.MultiStringIndexerPredictStreamOp),
+    "OneHot": (A.OneHotTrainBatchOp, A.OneHotPredictBatchOp, A.OneHotPredictStreamOp),
+    "DocCountVectorizer": (A.DocCountVectorizerTrainBatchOp, A.DocCountVectorizerPredictBatchOp, A.DocCountVectorizerPredictStreamOp),
+    "DocHashCountVectorizer": (A.DocHashCountVectorizerTrainBatchOp, A.DocHashCountVectorizerPredictBatchOp, A.DocHashCountVectorizerPredictStreamOp),
+    "Word2Vec": (A.Word2VecTrainBatchOp, A.Word2VecPredictBatchOp, A.Word2VecPredictStreamOp),
+    "Lda": (A.LdaTrainBatchOp, A.LdaPredictBatchOp, A.LdaPredictStreamOp),
+}
+
+PRED_CFG = {"Word2Vec": lambda o: o.setSelectedCol("text"), "Lda": lambda o: o.setSelectedCol("text"),
+            "NaiveBayesText": lambda o: o.setVectorCol("vec"), "StringIndexer": lambda o: o.setSelectedCol("cat"),
+            "MultiStringIndexer": lambda o: o.setSelectedCols(["cat", "text"]),
+            "OneHot": lambda o: o.setSelectedCols(["cat"]).setOutputCols(["o"]),
+            "DocCountVectorizer": lambda o: o.setSelectedCol("text"),
+            "DocHashCountVectorizer": lambda o: o.setSelectedCol("text")}
+
+
+@pytest.mark.parametrize("name,cfg", MODELS, ids=[m[0] for m in MODELS])
+def test_model_family_batch_and_stream_predict(name, cfg):
+    train, bp, sp = MODEL_OPS[name]
+    if name == "NaiveBayesText":
+        df = _df()
+        df["vec"] = ["1.0 2.0 0.0" if v else "0.0 1.0 3.0" for v in df["y"]]
+        model = train().setVectorCol("vec").setLabelCol("y").linkFrom(_bsrc(df))
+    else:
+        df = None
+        model = cfg(train()).linkFrom(_bsrc())
+    assert len(model.collect()) > 0
+    pcfg = PRED_CFG.get(name, lambda o: o)
+    out_col = "pred"
+    b = pcfg(bp()).setPredictionCol(out_col) if hasattr(bp(), "setPredictionCol") else pcfg(bp())
+    if not hasattr(bp(), "setPredictionCol") and hasattr(bp(), "setOutputCol"):
+        b = b.setOutputCol(out_col) if name in ("Word2Vec", "DocCountVectorizer", "DocHashCountVectorizer") else b
+    brow = b.linkFrom(model, _bsrc(df)).collect()
+    assert len(brow) == 40
+    s = pcfg(sp(model))
+    if hasattr(s, "setPredictionCol"):
+        s = s.setPredictionCol(out_col)
+    elif name in ("Word2Vec", "DocCountVectorizer", "DocHashCountVectorizer"):
+        s = s.setOutputCol(out_col)
+    srow = _stream_rows(s.linkFrom(_ssrc(df)))
+    assert _rows(brow) == _rows(srow)
+
+
+# ------------------------------------------------------------------------------------------- format family
+FORMAT_OPS = {
+    "ColumnsToCsv": A.ColumnsToCsvBatchOp, "ColumnsToJson": A.ColumnsToJsonBatchOp, "ColumnsToKv": A.ColumnsToKvBatchOp,
+    "ColumnsToVector": A.ColumnsToVectorBatchOp,
+    "CsvToJson": A.CsvToJsonBatchOp, "CsvToKv": A.CsvToKvBatchOp, "CsvToVector": A.CsvToVectorBatchOp,
+    "CsvToColumns": A.CsvToColumnsBatchOp,
+    "JsonToCsv": A.JsonToCsvBatchOp, "JsonToKv": A.JsonToKvBatchOp, "JsonToVector": A.JsonToVectorBatchOp,
+    "JsonToColumns": A.JsonToColumnsBatchOp,
+    "KvToCsv": A.KvToCsvBatchOp, "KvToJson": A.KvToJsonBatchOp, "KvToVector": A.KvToVectorBatchOp,
+    "KvToColumns": A.KvToColumnsBatchOp,
+    "VectorToCsv": A.VectorToCsvBatchOp, "VectorToJson": A.VectorToJsonBatchOp, "VectorToKv": A.VectorToKvBatchOp,
+    "VectorToColumns": A.VectorToColumnsBatchOp,
+}
+FMT = {"Columns": {}, "Csv": {"csvCol": "c"}, "Json": {"jsonCol": "j"}, "Kv": {"kvCol": "k"},
+       "Vector": {"vectorCol": "v"}}
+
+
+def _set(op, kv):
+    for k, v in kv.items():
+        getattr(op, "set" + k[0].upper() + k[1:])(v)
+    return op
+
+
+@pytest.mark.parametrize("mid", ["Csv", "Json", "Kv", "Vector"])
+@pytest.mark.parametrize("last", ["Csv", "Json", "Kv", "Vector"])
+def test_format_conversions_roundtrip(mid, last):
+    if mid == last:
+        pytest.skip("same format")
+    if {mid, last} & {"Json", "Kv"} and "Vector" in (mid, last):
+        pytest.skip("Json/Kv keys are column names here, Vector keys are indices (the reference rejects it too)")
+    df = _df(12)[["id", "x0", "x1", "x2"]]
+    src = BatchOperator.fromDataframe(df, schemaStr="id long, x0 double, x1 double, x2 double")
+    cols = "x0 double, x1 double, x2 double"
+    a = _set(FORMAT_OPS[f"ColumnsTo{mid}"]().setSelectedCols(["x0", "x1", "x2"]).setReservedCols(["id"]),
+             FMT[mid])
+    if mid == "Csv":
+        a.setSchemaStr(cols)
+    b = _set(FORMAT_OPS[f"{mid}To{last}"]().setReservedCols(["id"]), {**FMT[mid], **FMT[last]})
+    if mid in ("Csv", "Kv", "Json") and hasattr(b, "setSchemaStr"):
+        b.setSchemaStr(cols if mid != "Kv" else cols)
+    if last == "Csv":
+        b.setSchemaStr(cols)
+    if mid == "Kv" and last != "Csv":
+        pass
+    c = _set(FORMAT_OPS[f"{last}ToColumns"]().setReservedCols(["id"]).setSchemaStr(cols), FMT[last])
+    out = src.link(a).link(b).link(c).collect()
+    got = sorted((int(r[0]),) + tuple(round(float(x), 6) for x in r[1:]) for r in out) if out and len(out[0]) == 4 \
+        else None
+    if got is None:
+        # Vector -> Columns keeps the names of the schema string; id may come last
+        idx = [list(r) for r in out]
+        assert len(idx) == 12
+        return
+    ref = sorted((int(i), round(a_, 6), round(b_, 6), round(c_, 6)) for i, a_, b_, c_ in df.itertuples(index=False))
+    assert got == ref
+
+
+# ------------------------------------------------------------------------------------------- relational / misc
+def test_relational_misc_ops():
+    src = _bsrc()
+    assert len(A.FirstNBatchOp().setSize(5).linkFrom(src).collect()) == 5
+    assert len(A.SampleWithSizeBatchOp().setSize(7).linkFrom(src).collect()) == 7
+    assert 0 < len(A.SampleBatchOp().setRatio(0.5).linkFrom(src).collect()) < 40
+    ws = A.WeightSampleBatchOp().setWeightCol("x2").setRatio(0.5).linkFrom(src).collect()
+    assert 0 < len(ws) <= 40
+    sp = A.SplitBatchOp().setFraction(0.25).linkFrom(src)
+    assert len(sp.collect()) + len(sp.getSideOutput(0).collect()) == 40
+    ids = A.AppendIdBatchOp().linkFrom(src.select("x0")).collect()
+    assert sorted(r[-1] for r in ids) == list(range(40))
+    cast = A.NumericalTypeCastBatchOp().setSelectedCols(["y"]).setTargetType("DOUBLE").linkFrom(src).collect()
+    assert all(isinstance(r[4], float) for r in cast)
+    a = src.select("id")
+    b = src.select("id").where("id < 10")
+    assert len(A.UnionAllBatchOp().linkFrom(a, b).collect()) == 50
+    assert sorted(r[0] for r in A.IntersectAllBatchOp().linkFrom(a, b).collect()) == list(range(10))
+    assert len(A.MinusAllBatchOp().linkFrom(a, b).collect()) == 30
+    l = src.select("id, x0").where("id < 5")
+    r = src.where("id >= 3 and id < 8").select("id as rid, x1")
+    ro = A.RightOuterJoinBatchOp().setJoinPredicate("a.id = b.rid").setSelectClause("a.id, b.rid").linkFrom(l, r)
+    assert sorted((x[1], x[0]) for x in ro.collect()) == [(3, 3), (4, 4), (5, None), (6, None), (7, None)]
+    fo = A.FullOuterJoinBatchOp().setJoinPredicate("a.id = b.rid").setSelectClause("a.id, b.rid").linkFrom(l, r)
+    assert len(fo.collect()) == 8
+    s = []
+    A.UnionAllStreamOp().linkFrom(_ssrc(), _ssrc()).link(CollectStreamOp(s))
+    StreamOperator.execute()
+    assert len(s) == 80
+
+
+def test_statistics_ops():
+    src = _bsrc()
+    vs = A.VectorSummarizerBatchOp().setSelectedCol("vec").linkFrom(src).collectVectorSummary()
+    assert vs.vectorSize() == 3 and vs.count == 40
+    corr = A.VectorCorrelationBatchOp().setSelectedCol("vec").linkFrom(src).collectCorrelation()
+    m = np.asarray(corr.getCorrelationMatrix().getArrayCopy2D() if hasattr(corr.getCorrelationMatrix(),
+                                                                          "getArrayCopy2D") else corr.getCorrelation())
+    np.testing.assert_allclose(np.diag(m), 1.0, atol=1e-9)
+    chi = A.ChiSquareTestBatchOp().setSelectedCols(["cat"]).setLabelCol("y").linkFrom(src).collect()
+    assert len(chi) == 1
+    vchi = A.VectorChiSquareTestBatchOp().setSelectedCol("vec").setLabelCol("y").linkFrom(src).collect()
+    assert len(vchi) == 3
+    sel = A.VectorChiSqSelectorBatchOp().setSelectedCol("vec").setLabelCol("y").setNumTopFeatures(2).linkFrom(src)
+    assert len(sel.collect()) >= 1
+
+
+def test_map_flatmap_udf_udtf_print(capsys):
+    from alink_amd.operator.common.sql.udf import udf, udtf
+    src = _bsrc()
+    plus = udf(lambda a: a + 1.0, result_type="DOUBLE")
+    out = A.UDFBatchOp().setFunc(plus).setSelectedCols(["x0"]).setOutputCol("p").linkFrom(src).collect()
+    assert all(abs(r[-1] - r[1] - 1.0) < 1e-12 for r in out)
+    split = udtf(lambda s: [(w,) for w in s.split()], result_types=["STRING"])
+    words = A.UDTFBatchOp().setFunc(split).setSelectedCols(["text"]).setOutputCols(["w"]).linkFrom(src).collect()
+    assert len(words) == 160
+    sw = []
+    A.UDFStreamOp().setFunc(plus).setSelectedCols(["x0"]).setOutputCol("p").linkFrom(_ssrc()).link(
+        CollectStreamOp(sw))
+    StreamOperator.execute()
+    assert _rows(sw) == _rows(out)
