@@ -14,7 +14,10 @@ import numpy as np
 __all__ = ["lib", "parse_csv_lines", "murmur3_utf16", "parse_dense_vectors", "ftrl_update_csr",
            "ftrl_partial_margin", "ftrl_shard_update"]
 
-_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libalink_native.so")
+# ALINK_NATIVE_LIB points at another build of the same sources (e.g. the AddressSanitizer build of
+# tools/asan_host.py)
+_PATH = os.environ.get("ALINK_NATIVE_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                           "libalink_native.so")
 lib = None
 if os.path.exists(_PATH):
     try:

@@ -422,6 +422,8 @@ def train_kmeans(X: torch.Tensor, k: int, max_iter: int, tol: float, dist_type: 
     init = init.to(device=X.device, dtype=torch.float64)
     q = (IterativeComQueue()
          .setMLEnvironment(env)
+         .setJobName("KMeans")
+         .setRowsPerStep(int(X.shape[0]))
          .initWithPartitionedData(TRAIN_DATA, X)
          .initWithBroadcastData(INIT_CENTROID, init)
          .add(KMeansPreallocateCentroid())

@@ -237,6 +237,8 @@ class UpdateModel(ComputeFunction):
             cur.f = losses[pos]
         step = ctx.getStepNo()
         curve[step - 1] = cur.f
+        if ctx.getTaskId() == 0:
+            ctx.logMetric("loss", cur.f)
         k = step - 1
         if self.method == OptimMethodName.OWLQN:
             sK, _ = ctx.getObj(SKYK)
@@ -412,8 +414,12 @@ def optimize(obj: OptimObjFunc, data: LabeledData, dim: int, params: Params, met
     if init_coef is None:
         init_coef = torch.zeros(dim, dtype=torch.float64, device=dev)
         init_coef[0] = 1.0e-3   # Optimizer.initCoefZeros
-    q = IterativeComQueue().setMLEnvironment(env)
+    q = IterativeComQueue().setMLEnvironment(env).setJobName(f"optim.{method}")
     q.initWithPartitionedData(TRAIN, data)
+    try:
+        q.setRowsPerStep(len(data))
+    except TypeError:
+        pass
     q.initWithBroadcastData(MODEL, init_coef.to(dev))
     q.initWithBroadcastData(OBJ, obj)
     q.add(_Preallocate(max_iter, method))

@@ -19,6 +19,7 @@ from ..common.params import ParamInfo, Params, WithParams
 from ..common.table import MTable, Row
 from ..common.types import TableSchema
 from ..parallel import comm
+from ..utils import trace as _trace
 
 __all__ = ["AlgoOperator", "BatchOperator", "gather_table", "gather_rows", "partition_rows", "format_rows",
            "register_op"]
@@ -94,9 +95,29 @@ def format_rows(names, rows) -> str:
     return "\n".join(lines)
 
 
+def _traced_link(fn, opname):
+    """``linkFrom`` as an ``op`` span of the timeline (``utils.trace``; one attribute check when tracing is off)."""
+    import functools
+
+    @functools.wraps(fn)
+    def linkFrom(self, *inputs):
+        if not _trace.enabled():
+            return fn(self, *inputs)
+        with _trace.span(opname, "op"):
+            return fn(self, *inputs)
+    linkFrom._alink_traced = True
+    return linkFrom
+
+
 class AlgoOperator(WithParams):
     _NO_AUTO_PARAMS = True
     PARAMS = [ParamInfo("MLEnvironmentId", int, "ID of ML environment.", default=0)]
+
+    def __init_subclass__(cls, **kw):
+        super().__init_subclass__(**kw)
+        lf = cls.__dict__.get("linkFrom")
+        if lf is not None and not getattr(lf, "_alink_traced", False):
+            cls.linkFrom = _traced_link(lf, cls.__name__)
 
     def __init__(self, params: Optional[Params] = None, **kwargs):
         super().__init__(params, **kwargs)

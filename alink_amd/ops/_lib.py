@@ -43,6 +43,12 @@ def _load():
         if hasattr(L, name):
             getattr(L, name).argtypes = argtypes
             getattr(L, name).restype = c_int
+    # every entry point is a ``kernel`` span on the timeline when utils.trace is on (host launch cost + device
+    # time from HIP events on the caller's stream); one flag check per call otherwise
+    from ..utils import trace
+    for name in ["alink_kmeans_reduce_slabs", "alink_kmeans_prep_centroids"] + list(_EXTRA_SIGNATURES):
+        if hasattr(L, name) and not name.endswith(("_grid", "_pad", "_padded_rank")):
+            setattr(L, name, trace.traced_call(getattr(L, name), name[len("alink_"):]))
     _lib = L
     return _lib
 

@@ -15,13 +15,16 @@ With world size 1 every call is a local no-op.
 from __future__ import annotations
 
 import datetime
+import functools
 import os
-import pickle
+import time
 from typing import Any, List, Optional
 
 import numpy as np
 import torch
 import torch.distributed as dist
+
+from ..utils import trace as _trace
 
 __all__ = ["init_distributed", "get_rank", "get_world_size", "is_distributed", "all_reduce", "all_gather_object",
            "broadcast_object", "barrier", "all_gather_tensor", "all_to_all_objects", "reduce_scatter",
@@ -46,10 +49,42 @@ class CommStats:
         self.time_s = 0.0
 
     def as_dict(self):
-        return {"collectives": self.calls, "bytes": self.bytes, "oneshot": self.oneshot}
+        return {"collectives": self.calls, "bytes": self.bytes, "oneshot": self.oneshot, "time_s": self.time_s}
 
 
 STATS = CommStats()
+
+
+def _collective(fn):
+    """Time a collective (host wall time into ``STATS.time_s``; a ``collective`` span with device timing on the
+    tracer's gpu track when tracing is on).  Nested collectives (e.g. the count exchange inside an all-to-all)
+    are timed once, by the outermost call."""
+    name = fn.__name__
+
+    @functools.wraps(fn)
+    def wrapper(*a, **kw):
+        if not is_distributed():
+            return fn(*a, **kw)
+        if getattr(_NEST, "v", False):
+            return fn(*a, **kw)
+        t = a[0] if a and isinstance(a[0], torch.Tensor) else None
+        _NEST.v = True
+        t0 = time.perf_counter()
+        try:
+            if _trace.enabled():
+                nb = int(t.numel() * t.element_size()) if t is not None else 0
+                with _trace.span(name, "collective", device=t is not None and t.is_cuda, bytes=nb,
+                                 backend=_backend()):
+                    return fn(*a, **kw)
+            return fn(*a, **kw)
+        finally:
+            STATS.time_s += time.perf_counter() - t0
+            _NEST.v = False
+    return wrapper
+
+
+import threading as _threading  # noqa: E402
+_NEST = _threading.local()
 
 
 def is_distributed() -> bool:
@@ -119,6 +154,7 @@ def collective_device() -> torch.device:
     return device_for_rank() if _backend() == "nccl" else torch.device("cpu")
 
 
+@_collective
 def all_gather_arrays(arrays: List[np.ndarray], dtype=np.float64) -> List[List[np.ndarray]]:
     """Gather a list of variable-length 1-D arrays from every rank as TWO tensor collectives (lengths + one
     packed buffer over RCCL/gloo) instead of a pickled object gather: result[rank][j] = that rank's arrays[j]."""
@@ -154,6 +190,7 @@ def _oneshot_max() -> int:
     return oneshot.MAX_BYTES if oneshot.enabled() else -1
 
 
+@_collective
 def all_reduce(t: torch.Tensor, op: str = "sum") -> torch.Tensor:
     """In-place all-reduce of a tensor (SUM/MAX/MIN, reference ``AllReduce.java:125-159``).
 
@@ -186,6 +223,7 @@ def all_reduce(t: torch.Tensor, op: str = "sum") -> torch.Tensor:
     return t
 
 
+@_collective
 def all_reduce_coalesced(ts: List[torch.Tensor], op: str = "sum") -> List[torch.Tensor]:
     """Fuse several small same-dtype buffers into one collective (latency-bound regime)."""
     if not is_distributed() or not ts:
@@ -200,6 +238,7 @@ def all_reduce_coalesced(ts: List[torch.Tensor], op: str = "sum") -> List[torch.
     return ts
 
 
+@_collective
 def reduce_scatter(t: torch.Tensor, op: str = "sum") -> torch.Tensor:
     """Reduce-scatter along dim 0 (t.shape[0] must divide world size); returns this rank's block."""
     ws = get_world_size()
@@ -218,6 +257,7 @@ def reduce_scatter(t: torch.Tensor, op: str = "sum") -> torch.Tensor:
     return full[r * out.shape[0]:(r + 1) * out.shape[0]].clone()
 
 
+@_collective
 def all_gather_tensor(t: torch.Tensor) -> torch.Tensor:
     """Concatenate equally-shaped tensors from all ranks along dim 0."""
     ws = get_world_size()
@@ -233,6 +273,7 @@ def all_gather_tensor(t: torch.Tensor) -> torch.Tensor:
     return torch.cat(parts).to(t.device)
 
 
+@_collective
 def all_gather_varlen(t: torch.Tensor) -> torch.Tensor:
     """Concatenate tensors whose dim-0 length differs per rank (pads to the max length, one collective)."""
     ws = get_world_size()
@@ -247,6 +288,7 @@ def all_gather_varlen(t: torch.Tensor) -> torch.Tensor:
     return torch.cat([full[i * mx:i * mx + lens[i]] for i in range(ws)])
 
 
+@_collective
 def all_to_all_tensors(send: List[torch.Tensor]) -> List[torch.Tensor]:
     """Tensor all-to-all (``send[j]`` -> rank j; same trailing shape/dtype): one ``all_to_all_single`` after a
     count exchange.  This is the request/response shuffle of the reference's ALS (``AlsTrain.java:283-389``)
@@ -273,6 +315,7 @@ def all_to_all_tensors(send: List[torch.Tensor]) -> List[torch.Tensor]:
     return [x.reshape((x.shape[0],) + tail) for x in res]
 
 
+@_collective
 def all_gather_object(obj: Any) -> List[Any]:
     ws = get_world_size()
     if ws == 1:
@@ -283,6 +326,7 @@ def all_gather_object(obj: Any) -> List[Any]:
     return out
 
 
+@_collective
 def broadcast_object(obj: Any, src: int = 0) -> Any:
     if get_world_size() == 1:
         return obj
@@ -292,6 +336,7 @@ def broadcast_object(obj: Any, src: int = 0) -> Any:
     return box[0]
 
 
+@_collective
 def all_to_all_objects(send: List[Any]) -> List[Any]:
     """Object all-to-all: ``send[j]`` goes to rank j; returns the list received from every rank."""
     ws = get_world_size()
@@ -302,6 +347,7 @@ def all_to_all_objects(send: List[Any]) -> List[Any]:
     return [gathered[src][r] for src in range(ws)]
 
 
+@_collective
 def barrier():
     if is_distributed():
         if _backend() == "nccl":

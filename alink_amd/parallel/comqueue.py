@@ -13,8 +13,10 @@ RCCL (GPU) / gloo (CPU).  The criterion of task 0 decides termination; when the 
 bit-identical on every rank after an all-reduce (``criterion_replicated=True``) each rank evaluates it
 locally and no broadcast is needed.
 
-Observability: per-superstep wall time and collective bytes are recorded in ``queue.stats``; optional
-``on_step`` callbacks and a ``roctx`` range per superstep when running on ROCm.
+Observability: every superstep produces one structured record (``queue.stats`` and
+``utils.metrics``: wall time, collective calls / bytes / time, ``rows_per_s`` when the algorithm declared
+``setRowsPerStep``, plus fields logged by items through ``logMetric``); with tracing on
+(``utils.trace``) each superstep and each compute / communicate item is a timeline span and a roctx range.
 
 Fault tolerance (the reference has none: ComQueue state lives in the JVM heap and any failure restarts the
 job):
@@ -42,6 +44,8 @@ import numpy as np
 import torch
 
 from . import comm
+from ..utils import metrics as _metrics
+from ..utils import trace as _trace
 
 __all__ = ["InjectedFault", "ComContext", "ComputeFunction", "CommunicateFunction", "CompareCriterionFunction",
            "CompleteResultFunction", "AllReduce", "BaseComQueue", "IterativeComQueue", "ComQueue",
@@ -56,6 +60,17 @@ class InjectedFault(RuntimeError):
 
 class _Skip(Exception):
     pass
+
+
+class _NullCtx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
+_NULL = _NullCtx()
 
 
 _SCALARS = (bool, int, float, str, type(None))
@@ -141,6 +156,10 @@ class ComContext:
     @property
     def device(self):
         return self._queue.device
+
+    def logMetric(self, name: str, value):
+        """Attach ``name=value`` to this superstep's metrics record (``utils.metrics``)."""
+        self._queue.logMetric(name, value)
 
 
 class ComputeFunction:
@@ -298,6 +317,9 @@ class BaseComQueue:
         self.watchdog_s: Optional[float] = None
         self.resumed_from = 0
         self.resumed_stop = False
+        self.rows_per_step = 0
+        self.job_name = None
+        self._step_metrics: Dict[str, Any] = {}
 
     # ---- fault tolerance ----
     def setCheckpoint(self, directory: str, every: int = 1):
@@ -397,6 +419,23 @@ class BaseComQueue:
         self.on_step.append(fn)
         return self
 
+    # ---- metrics ----
+    def setRowsPerStep(self, n: int):
+        """Rows one superstep processes on this rank (the per-step record then carries ``rows_per_s``)."""
+        self.rows_per_step = int(n)
+        return self
+
+    def setJobName(self, name: str):
+        self.job_name = name
+        return self
+
+    def logMetric(self, name: str, value):
+        """Attach ``name=value`` to the current superstep's record (e.g. the loss of an optimizer step)."""
+        if isinstance(value, torch.Tensor):
+            value = value.item()
+        self._step_metrics[name] = value
+        return self
+
     def optimize(self) -> List[Any]:
         """Fuse runs of adjacent compute items (reference ``BaseComQueue.optimize`` :470-495)."""
         out: List[Any] = []
@@ -444,6 +483,7 @@ class BaseComQueue:
         inject = tuple(int(x) for x in inject.split(":")) if inject else None
         skip = {n for n, _ in self.partitioned} | {n for n, _ in self.broadcast}
         use_roctx = self.device is not None and self.device.type == "cuda" and hasattr(torch.cuda, "nvtx")
+        job = self.job_name or "->".join(it.name() for it in items)
         self.step_no = self.resumed_from
         stop = self.resumed_stop        # a checkpoint written at the converged superstep ends the run
         while not stop and self.step_no < self.max_iter:
@@ -453,18 +493,24 @@ class BaseComQueue:
             if self.watchdog_s is not None:
                 faulthandler.dump_traceback_later(self.watchdog_s, exit=True, file=sys.stderr)
             t0 = time.perf_counter()
-            b0 = comm.STATS.bytes
-            if use_roctx:
+            b0, c0, s0 = comm.STATS.bytes, comm.STATS.calls, comm.STATS.time_s
+            self._step_metrics = {}
+            tracing = _trace.enabled()
+            if use_roctx and not tracing:
                 try:
                     torch.cuda.nvtx.range_push(f"superstep {self.step_no}")
                 except Exception:
                     use_roctx = False
+            step_span = _trace.span(f"superstep {self.step_no}", "superstep", job=job) if tracing else None
+            if step_span is not None:
+                step_span.__enter__()
             for it in items:
-                if isinstance(it, CommunicateFunction):
-                    it.communicate(ctxs, self)
-                else:
-                    for c in ctxs:
-                        it.calc(c)
+                with (_trace.span(it.name(), "item") if tracing else _NULL):
+                    if isinstance(it, CommunicateFunction):
+                        it.communicate(ctxs, self)
+                    else:
+                        for c in ctxs:
+                            it.calc(c)
             if self.criterion is not None:
                 if self.criterion_replicated or ws == 1:
                     dec = bool(self.criterion.calc(ctxs[0]))
@@ -476,14 +522,25 @@ class BaseComQueue:
                                         self.device.type == "cuda" else "cpu")
                     dec = bool(comm.all_reduce(flag, MAX).item() > 0)
                 stop = dec
-            if use_roctx:
+            if step_span is not None:
+                step_span.__exit__(None, None, None)
+            elif use_roctx:
                 torch.cuda.nvtx.range_pop()
             if self.sync_device_per_step and self.device is not None and self.device.type == "cuda":
                 torch.cuda.synchronize(self.device)
             if self.watchdog_s is not None:
                 faulthandler.cancel_dump_traceback_later()
-            self.stats.append({"step": self.step_no, "wall_s": time.perf_counter() - t0,
-                               "comm_bytes": comm.STATS.bytes - b0})
+            wall = time.perf_counter() - t0
+            rec = {"job": job, "step": self.step_no, "wall_s": wall, "comm_bytes": comm.STATS.bytes - b0,
+                   "comm_calls": comm.STATS.calls - c0, "comm_s": comm.STATS.time_s - s0}
+            if self.rows_per_step:
+                rec["rows"] = self.rows_per_step
+                rec["rows_per_s"] = self.rows_per_step / wall if wall > 0 else 0.0
+            rec.update(self._step_metrics)
+            self.stats.append(rec)
+            _metrics.record("superstep", **rec)
+            if tracing:
+                _trace.counter("comm_bytes", bytes=rec["comm_bytes"])
             if self.ckpt_dir is not None and (self.step_no % self.ckpt_every == 0 or stop):
                 self._save_checkpoint(env.rank, stores, items, skip, stop)
             for fn in self.on_step:

@@ -289,5 +289,19 @@ def scenario_csv(out):
     out["rows"] = [list(r) for r in op.collect()]
 
 
+def scenario_trace(out):
+    """Timeline + metrics on a 2-rank KMeans: op / superstep / item / collective spans per rank."""
+    import os
+    from alink_amd.utils import trace, metrics
+    trace.reset()
+    trace.enable(os.path.join(os.environ["ALINK_TEST_TMP"], "trace_{rank}.json"))
+    metrics.clear()
+    scenario_kmeans({})
+    path = trace.dump()
+    trace.disable()
+    out["trace"] = path
+    out["steps"] = [r for r in metrics.records("superstep") if r.get("job") == "KMeans"]
+
+
 if __name__ == "__main__":
     run(int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), sys.argv[4], sys.argv[5])
