@@ -37,10 +37,13 @@ class MapBatchOp(BatchOperator):
         return self
 
 
-def load_model_mapper(mapper_cls, model_table: MTable, data_schema: TableSchema, params: Params) -> ModelMapper:
-    model_full = gather_table(model_table)
-    mapper = mapper_cls(model_full.schema, data_schema, params)
-    mapper.loadModel(model_full.rows())
+def load_model_mapper(mapper_cls, model, data_schema: TableSchema, params: Params) -> ModelMapper:
+    """Build and open a ``ModelMapper`` from a model table (broadcast source), a ``ModelSource`` or a
+    ``DataBridge`` (``common/directreader.py``)."""
+    from ...common.directreader import model_source_of
+    src = model_source_of(model)
+    mapper = mapper_cls(src.getSchema(), data_schema, params)
+    mapper.loadModel(src.getModelRows())
     mapper.open()
     return mapper
 

@@ -338,7 +338,11 @@ class ModelMapStreamOp(StreamOperator):
     def linkFrom(self, *inputs):
         (inp,) = self._connect(*inputs)
         from ..batch.utils import load_model_mapper
-        self._mapper = load_model_mapper(self.MAPPER, self._model_op.getOutputTable(), inp.getSchema(),
+        from ...common.directreader import DataBridgeModelSource, DirectReader
+        # the batch model reaches the stream through DirectReader under the configured policy
+        # (reference ModelMapStreamOp.java:39-56 -> DataBridgeModelSource)
+        self._bridge = DirectReader.collect(self._model_op)
+        self._mapper = load_model_mapper(self.MAPPER, DataBridgeModelSource(self._bridge), inp.getSchema(),
                                          self.getParams())
         self._schema = self._mapper.getOutputSchema()
         _register_upstream_sources(inp)

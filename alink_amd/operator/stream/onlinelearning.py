@@ -44,8 +44,10 @@ def _pget(p: Params, name, default=None):
 
 
 def _model_rows(op):
-    from ..base import gather_table
-    return gather_table(op.getOutputTable())
+    """Warm-start model through DirectReader (reference FtrlTrainStreamOp reads its init model with
+    ``DirectReader.collect`` / ``directRead``)."""
+    from ...common.directreader import DirectReader
+    return DirectReader.collect(op).readTable()
 
 
 def _ftrl_python(indptr, indices, values, label, w, n, z, alpha, beta, l1, l2):
