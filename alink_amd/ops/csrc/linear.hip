@@ -10,7 +10,8 @@
 //   accumulators (wave shuffles + LDS) into one fp64 slab row, and a second kernel sums the slabs in a fixed
 //   order (run-to-run deterministic), writing [grad_0..grad_{d-1}, lossSum, weightSum].
 //
-// Dense fp64 (the reference trains in double), d <= 64.  Loss codes:
+// Dense fp64 (the reference trains in double): d <= 32 lane-per-row (below), 32 < d <= 1024 lanes-over-columns
+// (linear_grad_wide_kernel: 1.54 -> see profiles/linear_grad_wide_r2.txt at d = 64).  Loss codes:
 //   0 log (LR)  1 logistic (log / ln2)  2 square  3 hinge  4 smooth hinge  5 perceptron  6 exponential
 //   7 huber(param = delta)  8 svr(param = epsilon)
 #include <hip/hip_runtime.h>
@@ -168,6 +169,143 @@ __global__ __launch_bounds__(THREADS) void linear_grad_reduce_kernel(const doubl
     }
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// Wide rows, 32 < d <= 1024: lanes over COLUMNS (lane l owns columns l + 64j, j < NC), RG rows per wave step.
+//   * loads: each row is read as NC fully coalesced 512-B wave loads (no per-lane row strides);
+//   * eta of the RG rows by a transposing butterfly: log2(RG) exchange steps halve the live row count while
+//     pairing lanes (RG/2 + RG/4 + ... + 1 shuffles), then 6 - log2(RG) plain steps — RG + 5 - log2 RG
+//     shuffles for RG rows instead of 6 RG; afterwards lane l holds the eta of row rowof(l);
+//   * the loss derivative is evaluated by the 64/RG lanes of each row, g_r broadcast back (RG shuffles),
+//     acc[j] += g_r x_r[j] — per-lane column accumulators need no cross-lane reduction at the end.
+// Blocks grid-stride over row groups; the block partials go to the same slab layout as the narrow kernel
+// ([nblk][DP + 2], DP = 64 NC), so the fixed-order reduce kernel below serves both.
+// ---------------------------------------------------------------------------------------------------------------
+template <int RG>
+__device__ __forceinline__ double eta_butterfly(double (&v)[RG], int lane) {
+    // exchange steps: xor 32, 16, ... (one per halving of the live row set)
+#pragma unroll
+    for (int live = RG, bit = 32; live > 1; live >>= 1, bit >>= 1) {
+        const bool hi = (lane & bit) != 0;
+#pragma unroll
+        for (int i = 0; i < live / 2; ++i) {
+            const double keep = hi ? v[i + live / 2] : v[i];
+            const double send = hi ? v[i] : v[i + live / 2];
+            v[i] = keep + __shfl_xor(send, bit);
+        }
+    }
+    double s = v[0];
+    constexpr int LOGRG = RG == 1 ? 0 : RG == 2 ? 1 : RG == 4 ? 2 : 3;
+#pragma unroll
+    for (int bit = 32 >> LOGRG; bit > 0; bit >>= 1) s += __shfl_xor(s, bit);
+    return s;
+}
+
+// row (within the group) whose eta lane l holds after eta_butterfly<RG>
+template <int RG>
+__device__ __forceinline__ int row_of_lane(int lane) {
+    int r = 0;
+#pragma unroll
+    for (int live = RG, bit = 32; live > 1; live >>= 1, bit >>= 1) r = 2 * r + ((lane & bit) ? 1 : 0);
+    return r;
+}
+
+template <int RG>
+__device__ __forceinline__ int lane_of_row(int r) {
+    int l = 0;
+    // bits of r from the most significant (first exchange step, lane bit 32) down
+    constexpr int LOGRG = RG == 1 ? 0 : RG == 2 ? 1 : RG == 4 ? 2 : 3;
+#pragma unroll
+    for (int s = 0; s < LOGRG; ++s) l |= ((r >> (LOGRG - 1 - s)) & 1) ? (32 >> s) : 0;
+    return l;
+}
+
+template <int NC, int RG>
+__global__ __launch_bounds__(THREADS) void linear_grad_wide_kernel(const double* __restrict__ X,
+                                                                  const double* __restrict__ y,
+                                                                  const double* __restrict__ wt,
+                                                                  const double* __restrict__ coef, int64_t n, int d,
+                                                                  int code, double prm, double* __restrict__ slab) {
+    constexpr int DP = 64 * NC;
+    constexpr int NW = THREADS / 64;
+    __shared__ double red[NW][DP + 2];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    double cf[NC], acc[NC];
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+        const int c = lane + 64 * j;
+        cf[j] = c < d ? coef[c] : 0.0;
+        acc[j] = 0.0;
+    }
+    double lsum = 0.0, wsum = 0.0;
+    const int myrow = row_of_lane<RG>(lane);
+    const bool row_leader = (lane & ((64 / RG) - 1)) == 0;   // one of the 64/RG lanes holding its row's eta
+    const int64_t ngroups = (n + RG - 1) / RG;
+    const int64_t gstride = (int64_t)gridDim.x * NW;
+    for (int64_t grp = (int64_t)blockIdx.x * NW + wave; grp < ngroups; grp += gstride) {
+        const int64_t r0 = grp * RG;
+        double x[RG][NC], part[RG];
+#pragma unroll
+        for (int r = 0; r < RG; ++r) {
+            const bool ok = r0 + r < n;
+            const double* xr = X + (r0 + r) * d;
+            double p = 0.0;
+#pragma unroll
+            for (int j = 0; j < NC; ++j) {
+                const int c = lane + 64 * j;
+                x[r][j] = (ok && c < d) ? xr[c] : 0.0;
+                p = fma(x[r][j], cf[j], p);
+            }
+            part[r] = p;
+        }
+        const double eta = eta_butterfly<RG>(part, lane);
+        const int64_t rr = r0 + myrow;
+        double gl = 0.0;
+        if (rr < n) {
+            const double wi = wt[rr];
+            double l, g;
+            loss_and_deriv(code, eta, y[rr], prm, l, g);
+            gl = g * wi;
+            if (row_leader) {
+                lsum = fma(wi, l, lsum);
+                wsum += wi;
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < RG; ++r) {
+            const double gr = __shfl(gl, lane_of_row<RG>(r));
+#pragma unroll
+            for (int j = 0; j < NC; ++j) acc[j] = fma(gr, x[r][j], acc[j]);
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        lsum += __shfl_xor(lsum, off);
+        wsum += __shfl_xor(wsum, off);
+    }
+#pragma unroll
+    for (int j = 0; j < NC; ++j) red[wave][lane + 64 * j] = acc[j];
+    if (lane == 0) {
+        red[wave][DP] = lsum;
+        red[wave][DP + 1] = wsum;
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < DP + 2; c += THREADS) {
+        double v = 0.0;
+#pragma unroll
+        for (int q = 0; q < NW; ++q) v += red[q][c];
+        slab[(int64_t)blockIdx.x * (DP + 2) + c] = v;
+    }
+}
+
+template <int NC, int RG>
+int launch_wide(const double* X, const double* y, const double* w, const double* coef, int64_t n, int d,
+                       int code, double prm, double* slab, int nblk, double* out, hipStream_t st) {
+    hipLaunchKernelGGL((linear_grad_wide_kernel<NC, RG>), dim3(nblk), dim3(THREADS), 0, st, X, y, w, coef, n, d, code,
+                       prm, slab);
+    hipLaunchKernelGGL(linear_grad_reduce_kernel, dim3(64 * NC + 2), dim3(THREADS), 0, st, slab, nblk, 64 * NC, d,
+                       out);
+    return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
 template <int DP>
 int launch(const double* X, const double* y, const double* w, const double* coef, int64_t n, int d, int code,
            double prm, double* slab, int nblk, double* out, hipStream_t st) {
@@ -241,7 +379,33 @@ int alink_linear_grad_f64(const double* X, const double* y, const double* w, con
     return launch<64>(X, y, w, coef, n, d, code, prm, slab, nblk, out, st);
 }
 
-int alink_linear_grad_pad(int d) { return d <= 8 ? 8 : d <= 16 ? 16 : d <= 32 ? 32 : 64; }
+int alink_linear_grad_pad(int d) {
+    if (d > 64 && d <= 1024) {
+        const int nc = (d + 63) / 64;
+        return 64 * (nc <= 8 ? nc : nc <= 12 ? 12 : 16);     // the NC instantiated for d (launch switch below)
+    }
+    return d <= 8 ? 8 : d <= 16 ? 16 : d <= 32 ? 32 : 64;
+}
+
+// wide dense rows, 32 < d <= 1024 (slab: nblk * (alink_linear_grad_pad(d) + 2) doubles, out d + 2)
+int alink_linear_grad_wide_f64(const double* X, const double* y, const double* w, const double* coef, int64_t n,
+                               int d, int code, double prm, double* slab, int nblk, double* out, void* stream) {
+    if (n <= 0 || d <= 32 || d > 1024 || nblk <= 0 || code < 0 || code > 8) return 1;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    switch ((d + 63) / 64) {
+        case 1: return launch_wide<1, 8>(X, y, w, coef, n, d, code, prm, slab, nblk, out, st);
+        case 2: return launch_wide<2, 8>(X, y, w, coef, n, d, code, prm, slab, nblk, out, st);
+        case 3: return launch_wide<3, 8>(X, y, w, coef, n, d, code, prm, slab, nblk, out, st);
+        case 4: return launch_wide<4, 8>(X, y, w, coef, n, d, code, prm, slab, nblk, out, st);
+        case 5: return launch_wide<5, 4>(X, y, w, coef, n, d, code, prm, slab, nblk, out, st);
+        case 6: return launch_wide<6, 4>(X, y, w, coef, n, d, code, prm, slab, nblk, out, st);
+        case 7: return launch_wide<7, 4>(X, y, w, coef, n, d, code, prm, slab, nblk, out, st);
+        case 8: return launch_wide<8, 4>(X, y, w, coef, n, d, code, prm, slab, nblk, out, st);
+        case 9: case 10: case 11: case 12:
+            return launch_wide<12, 2>(X, y, w, coef, n, d, code, prm, slab, nblk, out, st);
+        default: return launch_wide<16, 2>(X, y, w, coef, n, d, code, prm, slab, nblk, out, st);
+    }
+}
 
 // CSR pass 1: g [n] = w * l'(x.coef, y), lw [n] = w * l(x.coef, y)
 int alink_csr_row_deriv_f64(const int64_t* crow, const int32_t* col, const double* val, const double* y,

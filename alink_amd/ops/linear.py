@@ -40,8 +40,11 @@ def loss_code(unary) -> Optional[Tuple[int, float]]:
     return None
 
 
+MAX_D = 1024     # d <= 32: lane-per-row kernel; 32 < d <= 1024: lanes-over-columns kernel (csrc/linear.hip)
+
+
 def hip_linear_supported(X: torch.Tensor) -> bool:
-    return (X is not None and X.is_cuda and X.dtype == torch.float64 and X.dim() == 2 and 0 < X.shape[1] <= 64
+    return (X is not None and X.is_cuda and X.dtype == torch.float64 and X.dim() == 2 and 0 < X.shape[1] <= MAX_D
             and X.shape[0] > 0 and X.is_contiguous())
 
 
@@ -49,7 +52,7 @@ def linear_grad_hip(X: torch.Tensor, y: torch.Tensor, w: torch.Tensor, coef: tor
                     prm: float = 0.0) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
     L = _lib.require()
     if not hip_linear_supported(X):
-        raise ValueError("linear_grad_hip needs a contiguous fp64 [n, d<=64] CUDA tensor")
+        raise ValueError(f"linear_grad_hip needs a contiguous fp64 [n, d<={MAX_D}] CUDA tensor")
     n, d = X.shape
     dev = X.device
     y = y.to(device=dev, dtype=torch.float64).contiguous()
@@ -58,15 +61,18 @@ def linear_grad_hip(X: torch.Tensor, y: torch.Tensor, w: torch.Tensor, coef: tor
     if y.shape[0] != n or w.shape[0] != n:
         raise ValueError("label / weight length mismatch")
     pad = int(L.alink_linear_grad_pad(d))
-    nblk = max(1, min((n + 255) // 256, 2048))
+    wide = d > 32
+    # narrow: one row per lane (256 rows per block); wide: one row group per wave, 2 blocks per CU resident
+    nblk = max(1, min((n + 255) // 256, 2048)) if not wide else max(1, min((n + 7) // 8, 1024))
     key = (dev.index, nblk, pad)
     if key not in _SLABS:
         _SLABS[key] = torch.empty(nblk * (pad + 2), dtype=torch.float64, device=dev)
     out = torch.empty(d + 2, dtype=torch.float64, device=dev)
-    rc = L.alink_linear_grad_f64(X.data_ptr(), y.data_ptr(), w.data_ptr(), c.data_ptr(), n, d, int(code),
-                                 float(prm), _SLABS[key].data_ptr(), nblk, out.data_ptr(), _lib.stream_ptr(dev))
+    fn = L.alink_linear_grad_wide_f64 if wide else L.alink_linear_grad_f64
+    rc = fn(X.data_ptr(), y.data_ptr(), w.data_ptr(), c.data_ptr(), n, d, int(code), float(prm),
+            _SLABS[key].data_ptr(), nblk, out.data_ptr(), _lib.stream_ptr(dev))
     if rc != 0:
-        raise RuntimeError(f"alink_linear_grad_f64 failed: {rc}")
+        raise RuntimeError(f"alink_linear_grad{'_wide' if wide else ''}_f64 failed: {rc}")
     g = out[:d]
     if coef.shape[0] > d:
         g = torch.cat([g, torch.zeros(coef.shape[0] - d, dtype=g.dtype, device=dev)])

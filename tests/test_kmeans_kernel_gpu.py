@@ -114,7 +114,7 @@ def test_nearest_kernel_exact_candidates():
     assert float(d2[sel].abs().max()) < 1e-2
 
 
-@pytest.mark.parametrize("d", [1, 7, 8, 16, 31, 64])
+@pytest.mark.parametrize("d", [1, 7, 8, 16, 31, 64, 65, 128, 200, 256, 300, 512, 700, 1024])
 @pytest.mark.parametrize("loss", ["log", "logistic", "square", "hinge", "smooth", "perceptron", "exp", "huber", "svr"])
 def test_linear_grad_kernel_matches_fp64_reference(d, loss):
     """csrc/linear.hip fused gradient vs the torch two-GEMV form of the same unary loss (fp64)."""
@@ -124,7 +124,7 @@ def test_linear_grad_kernel_matches_fp64_reference(d, loss):
           "hinge": O.HingeLossFunc(), "smooth": O.SmoothHingeLossFunc(), "perceptron": O.PerceptronLossFunc(),
           "exp": O.ExponentialLossFunc(), "huber": O.HuberLossFunc(0.7), "svr": O.SvrLossFunc(0.2)}[loss]
     g = torch.Generator(device="cpu").manual_seed(d)
-    n = 50001
+    n = 50001 if d <= 256 else 20011
     X = torch.randn(n, d, generator=g, dtype=torch.float64).cuda()
     y = (torch.randint(0, 2, (n,), generator=g) * 2 - 1).double().cuda()
     w = torch.rand(n, generator=g, dtype=torch.float64).cuda()
