@@ -47,7 +47,7 @@ def _load():
     # time from HIP events on the caller's stream); one flag check per call otherwise
     from ..utils import trace
     for name in ["alink_kmeans_reduce_slabs", "alink_kmeans_prep_centroids"] + list(_EXTRA_SIGNATURES):
-        if hasattr(L, name) and not name.endswith(("_grid", "_pad", "_padded_rank")):
+        if hasattr(L, name) and not name.endswith(("_grid", "_pad", "_padded_rank", "_kmax")):
             setattr(L, name, trace.traced_call(getattr(L, name), name[len("alink_"):]))
     _lib = L
     return _lib
@@ -69,6 +69,8 @@ _EXTRA_SIGNATURES = {
     "alink_linear_grad_f64": [_c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_int, _c_int, _c_d, _c_vp, _c_int, _c_vp,
                               _c_vp],
     "alink_linear_grad_pad": [_c_int],
+    "alink_kmeans_accum_bf16": [_c_vp, _c_i64, _c_int, _c_vp, _c_vp, _c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp],
+    "alink_kmeans_accum_kmax": [_c_int],
     "alink_linear_grad_wide_f64": [_c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_int, _c_int, _c_d, _c_vp, _c_int, _c_vp,
                                    _c_vp],
     "alink_csr_row_deriv_f64": [_c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_int, _c_d, _c_vp, _c_vp, _c_vp],

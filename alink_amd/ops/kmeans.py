@@ -5,8 +5,11 @@
 ``KMeansUtil.updateSumMatrix`` ``KMeansUtil.java:60-85``) — for this rank's rows, ready for the BSP
 all-reduce.
 
-* GPU, bf16 rows, d == 128, k <= 128: one persistent MFMA kernel (``csrc/kmeans_v7.hip``) + an fp64
-  fixed-order slab reduction (``csrc/kmeans_common.hip``, deterministic).
+* GPU, bf16 rows, d == 128, k <= 128, unweighted: one persistent MFMA kernel (``csrc/kmeans_v7.hip``) + an
+  fp64 fixed-order slab reduction (``csrc/kmeans_common.hip``, deterministic).
+* GPU, bf16 rows, d in {64, 128, 256}, k <= 256 (512 at d = 64), optionally weighted: two passes — the MFMA
+  nearest-centroid kernel (``csrc/kmeans_nearest.hip``) then the LDS accumulate-by-index kernel
+  (``csrc/kmeans_accum.hip``), again with a fixed-order fp64 reduction.
 * anything else: chunked PyTorch path (fp64 on CPU; on GPU fp32 GEMM of the same bf16-rounded centroids).
 """
 from __future__ import annotations
@@ -17,7 +20,8 @@ import torch
 
 from . import _lib
 
-__all__ = ["assign_accumulate", "assign", "assign_accumulate_torch", "hip_supported", "prepare_centroids"]
+__all__ = ["assign_accumulate", "assign", "assign_accumulate_torch", "hip_supported", "prepare_centroids",
+           "general_supported", "assign_accumulate_general_hip", "accumulate_by_index_hip"]
 
 _BUF: Dict[Tuple, Tuple[torch.Tensor, torch.Tensor]] = {}
 HIP_CALLS = 0  # launches of the fused HIP assign+accumulate path (bench / tests read it)
@@ -140,10 +144,61 @@ def assign_accumulate_torch(X: torch.Tensor, C: torch.Tensor, weights: Optional[
     return out
 
 
+def general_supported(X: torch.Tensor, k: int) -> bool:
+    """Shapes of the two-pass HIP path (nearest + accumulate-by-index)."""
+    return nearest_supported(X) and 1 <= k <= (512 if X.shape[1] == 64 else 256)
+
+
+GENERAL_CALLS = 0
+_ACC: Dict[Tuple, Tuple[torch.Tensor, torch.Tensor]] = {}
+
+
+def accumulate_by_index_hip(X: torch.Tensor, idx: torch.Tensor, k: int,
+                            weights: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """[k, d+1] fp64 ``[sum_r w_r x_r | sum_r w_r]`` per index value (``csrc/kmeans_accum.hip``)."""
+    L = _lib.require()
+    n, d = X.shape
+    dev = X.device
+    if idx.dtype != torch.int32 or idx.numel() != n or idx.device != dev:
+        raise ValueError("idx must be int32 [N] on X's device")
+    w = None
+    if weights is not None:
+        w = weights.to(device=dev, dtype=torch.float32).contiguous()
+        if w.numel() != n:
+            raise ValueError("weights length mismatch")
+    nchunk = max(1, min(_num_cus(dev), (n + 4095) // 4096))
+    key = (dev.index, nchunk, k, d)
+    if key not in _ACC:
+        _ACC.clear()
+        _ACC[key] = (torch.empty(nchunk * k * d, dtype=torch.float32, device=dev),
+                     torch.empty(nchunk * k, dtype=torch.float32, device=dev))
+    slab, slab_cnt = _ACC[key]
+    out = torch.empty((k, d + 1), dtype=torch.float64, device=dev)
+    rc = L.alink_kmeans_accum_bf16(X.data_ptr(), n, d, idx.contiguous().data_ptr(),
+                                   None if w is None else w.data_ptr(), k, nchunk, slab.data_ptr(),
+                                   slab_cnt.data_ptr(), out.data_ptr(), _lib.stream_ptr(dev))
+    if rc != 0:
+        raise RuntimeError(f"alink_kmeans_accum_bf16 failed: {rc}")
+    return out
+
+
+def assign_accumulate_general_hip(X: torch.Tensor, C: torch.Tensor,
+                                  weights: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Two-pass HIP path for the shapes v7 does not cover (d 64/256, k up to 256/512, weighted rows)."""
+    global GENERAL_CALLS
+    if not general_supported(X, C.shape[0]):
+        raise ValueError("general HIP KMeans path needs contiguous bf16 [N, D in (64,128,256)] and k <= 256")
+    GENERAL_CALLS += 1
+    idx, _ = nearest_hip(X, C)
+    return accumulate_by_index_hip(X, idx, C.shape[0], weights)
+
+
 def assign_accumulate(X: torch.Tensor, C: torch.Tensor, weights: Optional[torch.Tensor] = None) -> torch.Tensor:
-    if weights is None and hip_supported(X, C.shape[0]):
-        if _lib.available() or not _lib.torch_fallback_allowed():
-            return assign_accumulate_hip(X, C)
+    hip_ok = _lib.available() or not _lib.torch_fallback_allowed()
+    if weights is None and hip_supported(X, C.shape[0]) and hip_ok:
+        return assign_accumulate_hip(X, C)
+    if general_supported(X, C.shape[0]) and hip_ok:
+        return assign_accumulate_general_hip(X, C, weights)
     return assign_accumulate_torch(X, C, weights)
 
 
