@@ -326,6 +326,13 @@ class UnaryLossObjFunc(OptimObjFunc):
     def calc_search_values(self, data, coef, dirv, beta, num_step):
         if not len(data):
             return torch.zeros(num_step + 1, dtype=coef.dtype, device=coef.device)
+        from ...ops import _lib, linear as lops
+        X = data.X.dense
+        code = lops.loss_code(self.unary)
+        if code is not None and lops.hip_linear_supported(X) and num_step + 1 <= lops.SEARCH_MAX_STEPS and \
+                (_lib.available() or not _lib.torch_fallback_allowed()) and not lops.k14_disabled():
+            # K14: both margins and all num_step+1 losses in one pass over X
+            return lops.search_losses_hip(X, data.y, data.w, coef, dirv, code[0], code[1], beta, num_step + 1)
         E = data.X.mm(torch.stack([coef, dirv], 1))  # one pass over X for both margins
         steps = torch.arange(num_step + 1, dtype=coef.dtype, device=coef.device)
         etas = E[:, :1] - steps[None, :] * (E[:, 1:2] * beta)

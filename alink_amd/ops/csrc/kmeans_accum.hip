@@ -8,11 +8,11 @@
 // idx[N], then this kernel forms Sum[c][:] += w_r x_r and Cnt[c] += w_r.
 //
 // Layout: grid (row chunk b, dim slice s), DS = 128 dims per slice (64 when D == 64); a 512-thread workgroup
-// keeps its slice of the k x DS fp32 partial sums in LDS (k <= 256 at DS = 128 -> 128 KiB, k <= 512 at DS = 64),
-// 8 waves walk the chunk's rows, each lane loading DS/64 bf16 of a row (one coalesced 128/256-B wave load) and
-// adding them with ds_add_f32 into row idx[r] of the LDS table (consecutive lanes -> consecutive banks, no
-// conflicts; different rows of one wave never collide because a wave handles one row per instruction).
-// Rows are prefetched 4 deep per wave (loads issued before the LDS adds of the previous group).  At the end
+// keeps its slice of the k x DS fp32 partial sums in LDS (k <= 256 at DS = 128 -> 145 KiB, k <= 512 at DS = 64),
+// 8 waves walk the chunk's rows: every wave instruction loads 1 KiB = DS/8 lanes x 16 B per row, 64/(DS/8) rows,
+// 8 such loads in flight per wave (64 KiB per CU: the first version, one 256-B row per wave instruction and 4 in
+// flight, was latency-bound at 0.4 TB/s), then ds_add_f32 into row idx[r] of the LDS table with the table
+// columns permuted (lane l's element j -> column j*DS/8 + l) so consecutive lanes hit consecutive banks.  At the end
 // the table goes to slab[b][c][D] (fp32) and a fixed-order fp64 reduction over chunks (kmeans_accum_reduce)
 // forms [k][D+1].  Counts of unweighted rows are exact (integers < 2^24 per chunk); the fp32 sums inside a chunk
 // depend on the LDS atomic order (rounding-level run-to-run differences, unlike v7's MFMA path).
@@ -23,7 +23,18 @@ namespace {
 
 constexpr int THREADS = 512;
 constexpr int NW = THREADS / 64;
-constexpr int PF = 4;                 // rows in flight per wave
+constexpr int U = 8;                  // 1-KiB wave loads in flight per wave (8 KiB / wave, 64 KiB / CU)
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// LDS table row stride RS = DS + 16 (DS = 128: the 2 rows a 32-lane half touches per ds_add_f32 sit in different
+// bank halves when their centroid ids differ in parity) or DS + 8 (DS = 64: 4 rows per half, bank offsets 8c mod 32)
+template <int DS>
+struct Tab {
+    static constexpr int RS = DS == 64 ? DS + 8 : DS + 16;
+    static constexpr int LPR = DS / 8;              // lanes per row: each lane loads 8 bf16 (16 B)
+    static constexpr int RPI = 64 / LPR;            // rows per wave instruction (4 at DS=128, 8 at DS=64)
+};
 
 template <int DS>
 __global__ __launch_bounds__(THREADS) void kmeans_accum_kernel(const __bf16* __restrict__ X, int64_t N, int D,
@@ -31,52 +42,56 @@ __global__ __launch_bounds__(THREADS) void kmeans_accum_kernel(const __bf16* __r
                                                                const float* __restrict__ w, int k,
                                                                int64_t rows_per_chunk, float* __restrict__ slab,
                                                                float* __restrict__ slab_cnt) {
-    extern __shared__ float tab[];          // [k][DS] then cnt[k]
-    constexpr int PER = DS / 64;            // dims per lane (1 or 2)
+    using T = Tab<DS>;
+    extern __shared__ float tab[];          // [k][RS] then cnt[k]
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int b = blockIdx.x, s = blockIdx.y;
     const int d0 = s * DS;
-    float* cnt = tab + k * DS;
-    for (int e = threadIdx.x; e < k * DS + k; e += THREADS) tab[e] = 0.f;
+    float* cnt = tab + k * T::RS;
+    for (int e = threadIdx.x; e < k * T::RS + k; e += THREADS) tab[e] = 0.f;
     __syncthreads();
     const int64_t r_lo = (int64_t)b * rows_per_chunk;
     const int64_t r_hi = r_lo + rows_per_chunk < N ? r_lo + rows_per_chunk : N;
-    const bool do_cnt = s == 0 && lane == 0;
-    for (int64_t r0 = r_lo + (int64_t)wave * PF; r0 < r_hi; r0 += (int64_t)NW * PF) {
-        float xv[PF][PER];
-        int c[PF];
-        float wr[PF];
+    const int sub = lane / T::LPR;          // which of the RPI rows of an instruction this lane serves
+    const int l = lane % T::LPR;            // 16-B column chunk of that row
+    const bool do_cnt = s == 0 && l == 0;
+    constexpr int ROWS_PER_ITER = NW * U * T::RPI;
+    for (int64_t base = r_lo + (int64_t)wave * U * T::RPI; base < r_hi; base += ROWS_PER_ITER) {
+        f32x4 lo[U], hi[U];
+        int c[U];
+        float wr[U];
 #pragma unroll
-        for (int q = 0; q < PF; ++q) {
-            const int64_t r = r0 + q;
+        for (int u = 0; u < U; ++u) {
+            const int64_t r = base + u * T::RPI + sub;
             const bool ok = r < r_hi;
-            c[q] = ok ? idx[r] : -1;
-            wr[q] = ok ? (w != nullptr ? w[r] : 1.f) : 0.f;
-            const __bf16* xr = X + (ok ? r : r_lo) * D + d0 + PER * lane;
-            if constexpr (PER == 2) {
-                const uint32_t v = *reinterpret_cast<const uint32_t*>(xr);
-                xv[q][0] = __uint_as_float(v << 16);
-                xv[q][1] = __uint_as_float(v & 0xFFFF0000u);
-            } else {
-                xv[q][0] = (float)xr[0];
-            }
+            c[u] = ok ? idx[r] : -1;
+            wr[u] = ok ? (w != nullptr ? w[r] : 1.f) : 0.f;
+            const uint4 v = *reinterpret_cast<const uint4*>(X + (ok ? r : r_lo) * D + d0 + 8 * l);
+            lo[u] = f32x4{__uint_as_float(v.x << 16), __uint_as_float(v.x & 0xFFFF0000u),
+                          __uint_as_float(v.y << 16), __uint_as_float(v.y & 0xFFFF0000u)};
+            hi[u] = f32x4{__uint_as_float(v.z << 16), __uint_as_float(v.z & 0xFFFF0000u),
+                          __uint_as_float(v.w << 16), __uint_as_float(v.w & 0xFFFF0000u)};
         }
 #pragma unroll
-        for (int q = 0; q < PF; ++q) {
-            const int cq = __builtin_amdgcn_readfirstlane(c[q]);
-            if (cq < 0 || cq >= k) continue;
-            float* row = tab + cq * DS + PER * lane;
+        for (int u = 0; u < U; ++u) {
+            if (c[u] < 0 || c[u] >= k) continue;
+            // table column of element j of this lane's chunk: j * LPR + l (consecutive lanes -> consecutive banks)
+            float* row = tab + c[u] * T::RS + l;
 #pragma unroll
-            for (int j = 0; j < PER; ++j)
-                __hip_atomic_fetch_add(row + j, wr[q] * xv[q][j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (do_cnt) __hip_atomic_fetch_add(cnt + cq, wr[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            for (int j = 0; j < 4; ++j) {
+                __hip_atomic_fetch_add(row + j * T::LPR, wr[u] * lo[u][j], __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_fetch_add(row + (j + 4) * T::LPR, wr[u] * hi[u][j], __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+            if (do_cnt) __hip_atomic_fetch_add(cnt + c[u], wr[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
     }
     __syncthreads();
     float* out = slab + (int64_t)b * k * D;
     for (int e = threadIdx.x; e < k * DS; e += THREADS) {
-        const int cc = e / DS, dd = e - cc * DS;
-        out[(int64_t)cc * D + d0 + dd] = tab[e];
+        const int cc = e / DS, dd = e - cc * DS;        // dd = 8 * l + j  <->  table column j * LPR + l
+        out[(int64_t)cc * D + d0 + dd] = tab[cc * T::RS + (dd & 7) * T::LPR + (dd >> 3)];
     }
     if (s == 0)
         for (int cc = threadIdx.x; cc < k; cc += THREADS) slab_cnt[(int64_t)b * k + cc] = cnt[cc];
@@ -104,7 +119,7 @@ __global__ __launch_bounds__(256) void kmeans_accum_reduce_kernel(const float* _
 extern "C" {
 
 // max k for a feature width D (the LDS table of one dim slice must fit the 160 KiB LDS)
-int alink_kmeans_accum_kmax(int D) { return D == 64 ? 512 : 256; }
+int alink_kmeans_accum_kmax(int D) { return D == 64 ? 512 : 256; }   // (k * (RS + 1)) * 4 B <= 160 KiB
 
 // slab: nchunk * k * D floats, slab_cnt: nchunk * k floats, out: k * (D + 1) doubles.  idx int32 [N] in [0, k)
 // (other values are skipped), w nullable fp32 [N].  D == 64 or D % 128 == 0, D <= 1024.  Returns 0 or an error.
@@ -118,18 +133,18 @@ int alink_kmeans_accum_bf16(const void* X, int64_t N, int D, const int* idx, con
     static bool attr_set = false;  // > 64 KiB of dynamic LDS must be opted into once per kernel
     if (!attr_set) {
         if (hipFuncSetAttribute(reinterpret_cast<const void*>(kmeans_accum_kernel<64>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (512 * 64 + 512) * 4) != hipSuccess ||
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (512 * 72 + 512) * 4) != hipSuccess ||
             hipFuncSetAttribute(reinterpret_cast<const void*>(kmeans_accum_kernel<128>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (256 * 128 + 256) * 4) != hipSuccess)
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (256 * 144 + 256) * 4) != hipSuccess)
             return 3;
         attr_set = true;
     }
     if (D == 64) {
-        const size_t lds = (size_t)(k * 64 + k) * sizeof(float);
+        const size_t lds = (size_t)(k * Tab<64>::RS + k) * sizeof(float);
         hipLaunchKernelGGL(kmeans_accum_kernel<64>, dim3(nchunk, 1), dim3(THREADS), lds, st, (const __bf16*)X, N, D,
                            idx, w, k, per, slab, slab_cnt);
     } else {
-        const size_t lds = (size_t)(k * 128 + k) * sizeof(float);
+        const size_t lds = (size_t)(k * Tab<128>::RS + k) * sizeof(float);
         hipLaunchKernelGGL(kmeans_accum_kernel<128>, dim3(nchunk, D / 128), dim3(THREADS), lds, st,
                            (const __bf16*)X, N, D, idx, w, k, per, slab, slab_cnt);
     }

@@ -306,6 +306,102 @@ int launch_wide(const double* X, const double* y, const double* w, const double*
     return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// K14: losses of the adaptive line search in ONE pass over X (reference CalcLosses / UnaryLossObjFunc
+// calcSearchValues, A/operator/common/optim/subfunc/CalcLosses.java:41-65, UnaryLossObjFunc.java:98-139):
+//   e0 = x.coef, e1 = x.dir (both margins from the same registers), then for s = 0..S
+//   loss_s += w l(e0 - s beta e1, y).  Same lanes-over-columns layout and transposing butterfly as the wide
+// gradient kernel (both margins reduced together); per-block partial losses -> fixed-order slab reduction.
+// ---------------------------------------------------------------------------------------------------------------
+constexpr int MAX_STEPS = 16;
+
+template <int NC, int RG>
+__global__ __launch_bounds__(THREADS) void linear_search_kernel(const double* __restrict__ X,
+                                                               const double* __restrict__ y,
+                                                               const double* __restrict__ wt,
+                                                               const double* __restrict__ coef,
+                                                               const double* __restrict__ dir, int64_t n, int d,
+                                                               int code, double prm, double beta, int nsteps,
+                                                               double* __restrict__ slab) {
+    constexpr int NW = THREADS / 64;
+    __shared__ double red[NW][MAX_STEPS];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    double cf[NC], dv[NC];
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+        const int c = lane + 64 * j;
+        cf[j] = c < d ? coef[c] : 0.0;
+        dv[j] = c < d ? dir[c] : 0.0;
+    }
+    double lacc[MAX_STEPS];
+#pragma unroll
+    for (int s = 0; s < MAX_STEPS; ++s) lacc[s] = 0.0;
+    const int myrow = row_of_lane<RG>(lane);
+    const bool row_leader = (lane & ((64 / RG) - 1)) == 0;
+    const int64_t ngroups = (n + RG - 1) / RG;
+    const int64_t gstride = (int64_t)gridDim.x * NW;
+    for (int64_t grp = (int64_t)blockIdx.x * NW + wave; grp < ngroups; grp += gstride) {
+        const int64_t r0 = grp * RG;
+        double p0[RG], p1[RG];
+#pragma unroll
+        for (int r = 0; r < RG; ++r) {
+            const bool ok = r0 + r < n;
+            const double* xr = X + (r0 + r) * d;
+            double a = 0.0, b = 0.0;
+#pragma unroll
+            for (int j = 0; j < NC; ++j) {
+                const int c = lane + 64 * j;
+                const double v = (ok && c < d) ? xr[c] : 0.0;
+                a = fma(v, cf[j], a);
+                b = fma(v, dv[j], b);
+            }
+            p0[r] = a;
+            p1[r] = b;
+        }
+        const double e0 = eta_butterfly<RG>(p0, lane);
+        const double e1 = eta_butterfly<RG>(p1, lane);
+        const int64_t rr = r0 + myrow;
+        if (rr < n && row_leader) {
+            const double wi = wt[rr], yi = y[rr];
+#pragma unroll
+            for (int s = 0; s < MAX_STEPS; ++s) {
+                if (s < nsteps) {
+                    double l, g;
+                    loss_and_deriv(code, e0 - (double)s * beta * e1, yi, prm, l, g);
+                    lacc[s] = fma(wi, l, lacc[s]);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int s = 0; s < MAX_STEPS; ++s) {
+        double v = lacc[s];
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+        if (lane == 0) red[wave][s] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < MAX_STEPS + 2) {
+        const int c = threadIdx.x;
+        double v = 0.0;
+        if (c < MAX_STEPS)
+#pragma unroll
+            for (int q = 0; q < NW; ++q) v += red[q][c];
+        slab[(int64_t)blockIdx.x * (MAX_STEPS + 2) + c] = v;
+    }
+}
+
+template <int NC, int RG>
+int launch_search(const double* X, const double* y, const double* w, const double* coef, const double* dir,
+                  int64_t n, int d, int code, double prm, double beta, int nsteps, double* slab, int nblk,
+                  double* out, hipStream_t st) {
+    hipLaunchKernelGGL((linear_search_kernel<NC, RG>), dim3(nblk), dim3(THREADS), 0, st, X, y, w, coef, dir, n, d,
+                       code, prm, beta, nsteps, slab);
+    // out[0..nsteps) = per-step loss sums (fixed order over blocks); columns past nsteps are zero
+    hipLaunchKernelGGL(linear_grad_reduce_kernel, dim3(MAX_STEPS), dim3(THREADS), 0, st, slab, nblk, MAX_STEPS,
+                       MAX_STEPS, out);
+    return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
 template <int DP>
 int launch(const double* X, const double* y, const double* w, const double* coef, int64_t n, int d, int code,
            double prm, double* slab, int nblk, double* out, hipStream_t st) {
@@ -377,6 +473,26 @@ int alink_linear_grad_f64(const double* X, const double* y, const double* w, con
     if (d <= 16) return launch<16>(X, y, w, coef, n, d, code, prm, slab, nblk, out, st);
     if (d <= 32) return launch<32>(X, y, w, coef, n, d, code, prm, slab, nblk, out, st);
     return launch<64>(X, y, w, coef, n, d, code, prm, slab, nblk, out, st);
+}
+
+// K14 line-search losses: out[s] = sum_i w_i l(x_i.coef - s beta x_i.dir, y_i), s < nsteps <= 16, d <= 1024.
+// slab: nblk * 18 doubles, out: 16 doubles.
+int alink_linear_search_f64(const double* X, const double* y, const double* w, const double* coef, const double* dir,
+                            int64_t n, int d, int code, double prm, double beta, int nsteps, double* slab, int nblk,
+                            double* out, void* stream) {
+    if (n <= 0 || d <= 0 || d > 1024 || nblk <= 0 || code < 0 || code > 8 || nsteps < 1 || nsteps > MAX_STEPS)
+        return 1;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    switch ((d + 63) / 64) {
+        case 1: return launch_search<1, 8>(X, y, w, coef, dir, n, d, code, prm, beta, nsteps, slab, nblk, out, st);
+        case 2: return launch_search<2, 8>(X, y, w, coef, dir, n, d, code, prm, beta, nsteps, slab, nblk, out, st);
+        case 3: case 4:
+            return launch_search<4, 4>(X, y, w, coef, dir, n, d, code, prm, beta, nsteps, slab, nblk, out, st);
+        case 5: case 6: case 7: case 8:
+            return launch_search<8, 2>(X, y, w, coef, dir, n, d, code, prm, beta, nsteps, slab, nblk, out, st);
+        default:
+            return launch_search<16, 1>(X, y, w, coef, dir, n, d, code, prm, beta, nsteps, slab, nblk, out, st);
+    }
 }
 
 int alink_linear_grad_pad(int d) {

@@ -11,7 +11,8 @@ import torch
 
 from . import _lib
 
-__all__ = ["linear_grad_hip", "loss_code", "hip_linear_supported", "sparse_grad_hip", "hip_sparse_supported"]
+__all__ = ["linear_grad_hip", "loss_code", "hip_linear_supported", "sparse_grad_hip", "hip_sparse_supported",
+           "search_losses_hip"]
 
 _SLABS: Dict[Tuple, torch.Tensor] = {}
 
@@ -77,6 +78,41 @@ def linear_grad_hip(X: torch.Tensor, y: torch.Tensor, w: torch.Tensor, coef: tor
     if coef.shape[0] > d:
         g = torch.cat([g, torch.zeros(coef.shape[0] - d, dtype=g.dtype, device=dev)])
     return g, out[d], out[d + 1]
+
+
+SEARCH_MAX_STEPS = 16
+
+
+def k14_disabled() -> bool:
+    """``ALINK_DISABLE_K14=1``: line search through the torch GEMM form (A/B diagnostics, tools/lr_train_bench.py)."""
+    import os
+    return os.environ.get("ALINK_DISABLE_K14", "0") == "1"
+
+
+def search_losses_hip(X: torch.Tensor, y: torch.Tensor, w: torch.Tensor, coef: torch.Tensor, dirv: torch.Tensor,
+                      code: int, prm: float, beta: float, nsteps: int) -> torch.Tensor:
+    """K14: ``[sum_i w_i l(x_i.coef - s beta x_i.dir, y_i) for s < nsteps]`` in one pass over the dense fp64 X
+    (``csrc/linear.hip`` linear_search_kernel; the torch form is an [n,d]x[d,2] fp64 GEMM plus elementwise)."""
+    L = _lib.require()
+    if not hip_linear_supported(X) or not 1 <= nsteps <= SEARCH_MAX_STEPS:
+        raise ValueError("search_losses_hip needs a contiguous fp64 [n, d<=1024] CUDA tensor and <= 16 steps")
+    n, d = X.shape
+    dev = X.device
+    y = y.to(device=dev, dtype=torch.float64).contiguous()
+    w = w.to(device=dev, dtype=torch.float64).contiguous()
+    c = coef[:d].to(device=dev, dtype=torch.float64).contiguous()
+    dv = dirv[:d].to(device=dev, dtype=torch.float64).contiguous()
+    nblk = max(1, min((n + 7) // 8, 1024))
+    key = (dev.index, nblk, "search")
+    if key not in _SLABS:
+        _SLABS[key] = torch.empty(nblk * (SEARCH_MAX_STEPS + 2), dtype=torch.float64, device=dev)
+    out = torch.empty(SEARCH_MAX_STEPS, dtype=torch.float64, device=dev)
+    rc = L.alink_linear_search_f64(X.data_ptr(), y.data_ptr(), w.data_ptr(), c.data_ptr(), dv.data_ptr(), n, d,
+                                   int(code), float(prm), float(beta), int(nsteps), _SLABS[key].data_ptr(), nblk,
+                                   out.data_ptr(), _lib.stream_ptr(dev))
+    if rc != 0:
+        raise RuntimeError(f"alink_linear_search_f64 failed: {rc}")
+    return out[:nsteps]
 
 
 def hip_sparse_supported(fm) -> bool:

@@ -136,3 +136,28 @@ def test_linear_grad_kernel_matches_fp64_reference(d, loss):
     torch.testing.assert_close(got, ref, rtol=1e-10, atol=1e-9)
     torch.testing.assert_close(lsum, (w * fn.loss(eta, y)).sum(), rtol=1e-10, atol=1e-9)
     torch.testing.assert_close(wsum, w.sum(), rtol=1e-12, atol=1e-9)
+
+
+@pytest.mark.parametrize("d", [3, 32, 64, 100, 256, 700])
+@pytest.mark.parametrize("loss", ["log", "square", "smooth", "huber", "svr"])
+def test_linear_search_losses_kernel_matches_fp64(d, loss):
+    """K14 fused line-search losses (csrc/linear.hip) vs the torch [n,d]x[d,2] GEMM + elementwise form."""
+    from alink_amd.models.linear import objfunc as O
+    from alink_amd.ops import linear as lops
+    fn = {"log": O.LogLossFunc(), "square": O.SquareLossFunc(), "smooth": O.SmoothHingeLossFunc(),
+          "huber": O.HuberLossFunc(0.7), "svr": O.SvrLossFunc(0.2)}[loss]
+    g = torch.Generator(device="cpu").manual_seed(d + 7)
+    n = 40007
+    X = torch.randn(n, d, generator=g, dtype=torch.float64).cuda()
+    y = (torch.randint(0, 2, (n,), generator=g) * 2 - 1).double().cuda()
+    w = torch.rand(n, generator=g, dtype=torch.float64).cuda()
+    coef = (0.3 * torch.randn(d, generator=g, dtype=torch.float64)).cuda()
+    dirv = (0.1 * torch.randn(d, generator=g, dtype=torch.float64)).cuda()
+    code, prm = lops.loss_code(fn)
+    for nsteps, beta in [(5, 0.25), (16, 0.1), (1, 1.0)]:
+        got = lops.search_losses_hip(X, y, w, coef, dirv, code, prm, beta, nsteps)
+        E = X @ torch.stack([coef, dirv], 1)
+        steps = torch.arange(nsteps, dtype=torch.float64, device="cuda")
+        etas = E[:, :1] - steps[None, :] * (E[:, 1:2] * beta)
+        ref = (fn.loss(etas, y[:, None]) * w[:, None]).sum(0)
+        torch.testing.assert_close(got, ref, rtol=1e-10, atol=1e-8)
