@@ -109,7 +109,7 @@ __device__ __forceinline__ float pack_max(float best, float v, uint32_t c) {
     return fmaxf(best, __uint_as_float((__float_as_uint(v) & 0xFFFFFF80u) | c));
 }
 
-template <int KB, int MODE>
+template <int KB, int MODE, bool PF>
 __global__ __launch_bounds__(512) void kmeans_v7_kernel(const __bf16* __restrict__ Xp, int64_t N,
                                                         const __bf16* __restrict__ Cp,
                                                         const float* __restrict__ ninit, float* __restrict__ slab,
@@ -147,8 +147,10 @@ __global__ __launch_bounds__(512) void kmeans_v7_kernel(const __bf16* __restrict
     // per-iteration prologue shared by both roles: tile i has landed (own loads + barrier), refill the ring
     auto pre = [&](int64_t i) {
         if (MODE != COMPUTE_ONLY) {
+            const int64_t need = PF ? (i + 1 < my_ntiles ? i + 1 : my_ntiles - 1) : i;   // newest tile needed
             if (i < my_ntiles) {
-                const int64_t younger = my_ntiles - 1 - i;
+                const int64_t issued = (i + AHEAD - 1 < my_ntiles - 1 ? i + AHEAD - 1 : my_ntiles - 1);
+                const int64_t younger = issued - need;
                 wait_tile(younger < AHEAD - 1 ? (int)younger : AHEAD - 1);
             }
         }
@@ -173,16 +175,26 @@ __global__ __launch_bounds__(512) void kmeans_v7_kernel(const __bf16* __restrict
 #pragma unroll
         for (int s = 0; s < 4; ++s) xr[s] = xoff(myrow, s + 4 * g);
         uint32_t prev1 = NONE, prev2 = NONE;
+        bf16x8 xnext[4];     // PF: this wave's fragments of tile i+1, read right after barrier i
         for (int64_t i = 0; i <= my_ntiles; ++i) {
             pre(i);
             if (MODE == LOAD_ONLY || i >= my_ntiles) continue;
             const char* xt = lds + (int)(i % NBUF) * TILE;
+            bf16x8 xcur[4];
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+                xcur[s] = (PF && i > 0) ? xnext[s] : *reinterpret_cast<const bf16x8*>(xt + xr[s]);
+            if (PF && i + 1 < my_ntiles) {
+                const char* xn = lds + (int)((i + 1) % NBUF) * TILE;
+#pragma unroll
+                for (int s = 0; s < 4; ++s) xnext[s] = *reinterpret_cast<const bf16x8*>(xn + xr[s]);
+            }
             f32x4 acc[KB];
 #pragma unroll
             for (int b = 0; b < KB; ++b) acc[b] = nin[b];
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
-                const bf16x8 xb = *reinterpret_cast<const bf16x8*>(xt + xr[s]);
+                const bf16x8 xb = xcur[s];
 #pragma unroll
                 for (int b = 0; b < KB; ++b)
                     acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cf[b][s], xb, acc[b], 0, 0, 0);
@@ -283,20 +295,30 @@ __global__ __launch_bounds__(512) void kmeans_v7_kernel(const __bf16* __restrict
         slab_cnt[(int64_t)blockIdx.x * 128 + tid] = tid < 16 * KB ? (float)cnt[tid] : 0.f;
 }
 
+template <int KB, bool PF>
+hipError_t launch_kb_pf(int mode, dim3 grid, hipStream_t st, const __bf16* X, int64_t N, const __bf16* C,
+                        const float* ninit, float* slab, float* slab_cnt, int* assign_out, int64_t ntiles,
+                        int64_t per) {
+    if (mode == LOAD_ONLY)
+        hipLaunchKernelGGL((kmeans_v7_kernel<KB, LOAD_ONLY, PF>), grid, dim3(512), 0, st, X, N, C, ninit, slab,
+                           slab_cnt, assign_out, ntiles, per);
+    else if (mode == COMPUTE_ONLY)
+        hipLaunchKernelGGL((kmeans_v7_kernel<KB, COMPUTE_ONLY, PF>), grid, dim3(512), 0, st, X, N, C, ninit, slab,
+                           slab_cnt, assign_out, ntiles, per);
+    else
+        hipLaunchKernelGGL((kmeans_v7_kernel<KB, FULL, PF>), grid, dim3(512), 0, st, X, N, C, ninit, slab,
+                           slab_cnt, assign_out, ntiles, per);
+    return hipGetLastError();
+}
+
+// mode bits 0-1: 0 full, 1 load only, 2 compute only; bit 4: distance-fragment prefetch variant (PF)
 template <int KB>
 hipError_t launch_kb(int mode, dim3 grid, hipStream_t st, const __bf16* X, int64_t N, const __bf16* C,
                      const float* ninit, float* slab, float* slab_cnt, int* assign_out, int64_t ntiles,
                      int64_t per) {
-    if (mode == LOAD_ONLY)
-        hipLaunchKernelGGL((kmeans_v7_kernel<KB, LOAD_ONLY>), grid, dim3(512), 0, st, X, N, C, ninit, slab,
-                           slab_cnt, assign_out, ntiles, per);
-    else if (mode == COMPUTE_ONLY)
-        hipLaunchKernelGGL((kmeans_v7_kernel<KB, COMPUTE_ONLY>), grid, dim3(512), 0, st, X, N, C, ninit, slab,
-                           slab_cnt, assign_out, ntiles, per);
-    else
-        hipLaunchKernelGGL((kmeans_v7_kernel<KB, FULL>), grid, dim3(512), 0, st, X, N, C, ninit, slab, slab_cnt,
-                           assign_out, ntiles, per);
-    return hipGetLastError();
+    if (mode & 16)
+        return launch_kb_pf<KB, true>(mode & 3, grid, st, X, N, C, ninit, slab, slab_cnt, assign_out, ntiles, per);
+    return launch_kb_pf<KB, false>(mode & 3, grid, st, X, N, C, ninit, slab, slab_cnt, assign_out, ntiles, per);
 }
 
 }  // namespace

@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--grid", type=int, default=None)
     ap.add_argument("--load-only", action="store_true", help="time the LDS-DMA load pipeline alone")
     ap.add_argument("--compute-only", action="store_true", help="time the compute alone (no loads)")
+    ap.add_argument("--pf", action="store_true", help="distance-fragment prefetch variant (mode bit 16)")
     a = ap.parse_args()
     dev = torch.device("cuda")
     n, d, k = a.rows, 128, a.k
@@ -38,10 +39,11 @@ def main():
         X[s:e] = (centers[lab] + torch.randn(e - s, d, device=dev, generator=g)).to(torch.bfloat16)
     C = (centers + 0.5 * torch.randn(k, d, device=dev, generator=g)).double()
     def run(Xs):
-        return K.assign_accumulate_hip(Xs, C, grid=a.grid, mode=2 if a.compute_only else 1 if a.load_only else 0)
+        m = 2 if a.compute_only else 1 if a.load_only else 0
+        return K.assign_accumulate_hip(Xs, C, grid=a.grid, mode=m | (16 if a.pf else 0))
     out = run(X)
     torch.cuda.synchronize()
-    res = {"rows": n, "k": k, "load_only": a.load_only, "compute_only": a.compute_only}
+    res = {"rows": n, "k": k, "load_only": a.load_only, "compute_only": a.compute_only, "pf": a.pf}
     if a.torch:
         ref0 = K.assign_accumulate_torch(X[:2_000_000], C)
         got0 = run(X[:2_000_000].contiguous())
