@@ -47,12 +47,13 @@ constexpr int LDS_CAP = 160 * 1024;
 template <int KB>
 struct Plan {
     static constexpr int OHB = 16 * KB * TR * 2;
-    static constexpr int NBUF_FIT = (LDS_CAP - 2 * OHB - 128 * 4) / TILE;
+    static constexpr int NBUF_FIT = (LDS_CAP - 2 * OHB - 128 * 4 - 512) / TILE;
     static constexpr int NBUF = NBUF_FIT > 8 ? 8 : NBUF_FIT;   // X ring slots: tile i, i-1, AHEAD in flight
     static constexpr int AHEAD = NBUF - 2;
     static constexpr int OFF_OH = NBUF * TILE;
     static constexpr int OFF_CNT = OFF_OH + 2 * OHB;
-    static constexpr int LDS_BYTES = OFF_CNT + 128 * 4;
+    static constexpr int OFF_PAD = OFF_CNT + 128 * 4;          // VAR 2: landing pad of the L2 touch loads
+    static constexpr int LDS_BYTES = OFF_PAD + 2 * 256;
     static_assert(LDS_BYTES <= LDS_CAP && AHEAD >= 3 && AHEAD <= 6, "LDS plan");
 };
 constexpr uint32_t NONE = 0xFFFFu;
@@ -79,6 +80,64 @@ __device__ __forceinline__ void wait_tile(int younger) {
     else if (younger == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     else if (younger == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// VAR >= 1: the 4 accumulate waves issue 4 pieces per tile each
+__device__ __forceinline__ void wait_tile4(int younger) {
+    if (younger >= 5) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+    else if (younger == 4) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else if (younger == 3) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    else if (younger == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (younger == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// stage one 64-row tile with NP pieces per wave (NP = 2: all 8 waves; NP = 4: the 4 accumulate waves, `wave` =
+// 0..3 among them); rows past N read as zero (buffer bounds)
+template <int NP>
+__device__ __forceinline__ void stage_np(char* lds, int slot, const char* X, int64_t row0, int64_t N,
+                                         const uint32_t (&voff)[4], int wave) {
+    const int64_t rem = (N - row0) * ROWB;
+    const int nbytes = rem < TILE ? (int)rem : TILE;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(X + row0 * ROWB), (short)0, nbytes, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+        const uint32_t m0v = __builtin_amdgcn_readfirstlane(
+            (uint32_t)(uintptr_t)(LDS_AS void*)(lds + slot * TILE + i * (TILE / NP) + wave * 1024));
+        uint32_t keep;
+        asm volatile(
+            "s_mov_b32 %0, m0\n\t"
+            "s_mov_b32 m0, %3\n\t"
+            "s_nop 0\n\t"
+            "buffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
+            "s_mov_b32 m0, %0"
+            : "=&s"(keep)
+            : "v"(voff[i]), "s"(rs), "s"(m0v)
+            : "memory");
+    }
+}
+
+// VAR 2: touch every 128-B line of a future tile (one dword per line, landing in a per-wave LDS pad) so its
+// LDS-DMA, issued PD iterations later, hits L2 instead of HBM: the ring depth is bounded by LDS, L2 is not
+__device__ __forceinline__ void touch_l2(char* lds, int pad_off, const char* X, int64_t row0, int64_t N, int half,
+                                         int lane) {
+    const int64_t rem = (N - row0) * ROWB;
+    const int nbytes = rem <= 0 ? 0 : (rem < TILE ? (int)rem : TILE);
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(X + (rem > 0 ? row0 : 0) * ROWB), (short)0, nbytes, 0x00020000);
+    const uint32_t m0v = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(LDS_AS void*)(lds + pad_off));
+    const uint32_t off = (uint32_t)((half * 64 + lane) * 128);
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %3\n\t"
+        "s_nop 0\n\t"
+        "buffer_load_dword %1, %2, 0 offen lds\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(off), "s"(rs), "s"(m0v)
+        : "memory");
 }
 
 // stage one 64-row tile: 16 LDS-DMA pieces of 1 KiB, two per wave; rows past N read as zero (buffer bounds)
@@ -109,7 +168,7 @@ __device__ __forceinline__ float pack_max(float best, float v, uint32_t c) {
     return fmaxf(best, __uint_as_float((__float_as_uint(v) & 0xFFFFFF80u) | c));
 }
 
-template <int KB, int MODE, bool PF>
+template <int KB, int MODE, int VAR>
 __global__ __launch_bounds__(512) void kmeans_v7_kernel(const __bf16* __restrict__ Xp, int64_t N,
                                                         const __bf16* __restrict__ Cp,
                                                         const float* __restrict__ ninit, float* __restrict__ slab,
@@ -117,6 +176,11 @@ __global__ __launch_bounds__(512) void kmeans_v7_kernel(const __bf16* __restrict
                                                         int64_t ntiles, int64_t per) {
     using PL = Plan<KB>;
     constexpr int NBUF = PL::NBUF, AHEAD = PL::AHEAD, OHB = PL::OHB, OFF_OH = PL::OFF_OH, OFF_CNT = PL::OFF_CNT;
+    // VAR 0: all 8 waves stage 2 pieces per tile.  VAR 1: the accumulate waves stage all 16 pieces (4 each), so
+    // the distance waves — the critical role — carry no LDS-DMA issue cost and no vmcnt waits.  VAR 2: VAR 1 +
+    // distance waves 0/1 touch tile i + AHEAD + PD into L2 (PD = 3).
+    constexpr int PD = 3;
+    constexpr bool ACC_DMA = VAR >= 1;
     __shared__ __attribute__((aligned(16))) char lds[PL::LDS_BYTES];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -127,17 +191,26 @@ __global__ __launch_bounds__(512) void kmeans_v7_kernel(const __bf16* __restrict
     const int64_t tbase = (int64_t)blockIdx.x * per;
     const int64_t my_ntiles = ntiles > tbase ? (ntiles - tbase < per ? ntiles - tbase : per) : 0;
 
-    uint32_t voff[2];
+    uint32_t voff[4];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        const int p = i * 8192 + tid * 16;      // linear LDS byte this lane's DMA fills
+    for (int i = 0; i < 4; ++i) {
+        // VAR 0: pieces i < 2 of 8 KiB halves over 512 threads; ACC_DMA: pieces i < 4 of 4 KiB over 256 threads
+        const int p = ACC_DMA ? i * 4096 + (tid & 255) * 16 : (i & 1) * 8192 + tid * 16;
         const int row = p >> 8;
         const int chl = ((p >> 4) & 15) ^ xsw(row);
         voff[i] = (uint32_t)(row * ROWB + chl * 16);
     }
-    if (MODE != COMPUTE_ONLY)
+    const bool dma_wave = !ACC_DMA || wave >= 4;
+    auto stage_tile = [&](int slot, int64_t t) {
+        if constexpr (ACC_DMA) stage_np<4>(lds, slot, X, (tbase + t) * TR, N, voff, wave - 4);
+        else stage(lds, slot, X, (tbase + t) * TR, N, *reinterpret_cast<const uint32_t(*)[2]>(voff), wave);
+    };
+    if (MODE != COMPUTE_ONLY && dma_wave)
         for (int s = 0; s < AHEAD; ++s)
-            if (s < my_ntiles) stage(lds, s, X, (tbase + s) * TR, N, voff, wave);
+            if (s < my_ntiles) stage_tile(s, s);
+    if (VAR == 2 && MODE != COMPUTE_ONLY && wave < 2)
+        for (int s = AHEAD; s < AHEAD + PD; ++s)
+            if (s < my_ntiles) touch_l2(lds, PL::OFF_PAD + 256 * wave, X, (tbase + s) * TR, N, wave, lane);
     {
         for (int e = tid * 16; e < 2 * OHB + 128 * 4; e += 512 * 16)
             *reinterpret_cast<f32x4*>(lds + OFF_OH + e) = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -146,17 +219,19 @@ __global__ __launch_bounds__(512) void kmeans_v7_kernel(const __bf16* __restrict
 
     // per-iteration prologue shared by both roles: tile i has landed (own loads + barrier), refill the ring
     auto pre = [&](int64_t i) {
-        if (MODE != COMPUTE_ONLY) {
-            const int64_t need = PF ? (i + 1 < my_ntiles ? i + 1 : my_ntiles - 1) : i;   // newest tile needed
+        if (MODE != COMPUTE_ONLY && dma_wave) {
             if (i < my_ntiles) {
-                const int64_t issued = (i + AHEAD - 1 < my_ntiles - 1 ? i + AHEAD - 1 : my_ntiles - 1);
-                const int64_t younger = issued - need;
-                wait_tile(younger < AHEAD - 1 ? (int)younger : AHEAD - 1);
+                const int64_t younger = my_ntiles - 1 - i;
+                const int y = younger < AHEAD - 1 ? (int)younger : AHEAD - 1;
+                if constexpr (ACC_DMA) wait_tile4(y);
+                else wait_tile(y);
             }
         }
         barrier_lds();
-        if (MODE != COMPUTE_ONLY && i + AHEAD < my_ntiles)
-            stage(lds, (int)((i + AHEAD) % NBUF), X, (tbase + i + AHEAD) * TR, N, voff, wave);
+        if (MODE != COMPUTE_ONLY && dma_wave && i + AHEAD < my_ntiles)
+            stage_tile((int)((i + AHEAD) % NBUF), i + AHEAD);
+        if (VAR == 2 && MODE != COMPUTE_ONLY && wave < 2 && i + AHEAD + PD < my_ntiles)
+            touch_l2(lds, PL::OFF_PAD + 256 * wave, X, (tbase + i + AHEAD + PD) * TR, N, wave, lane);
     };
 
     if (wave < 4) {
@@ -175,26 +250,16 @@ __global__ __launch_bounds__(512) void kmeans_v7_kernel(const __bf16* __restrict
 #pragma unroll
         for (int s = 0; s < 4; ++s) xr[s] = xoff(myrow, s + 4 * g);
         uint32_t prev1 = NONE, prev2 = NONE;
-        bf16x8 xnext[4];     // PF: this wave's fragments of tile i+1, read right after barrier i
         for (int64_t i = 0; i <= my_ntiles; ++i) {
             pre(i);
             if (MODE == LOAD_ONLY || i >= my_ntiles) continue;
             const char* xt = lds + (int)(i % NBUF) * TILE;
-            bf16x8 xcur[4];
-#pragma unroll
-            for (int s = 0; s < 4; ++s)
-                xcur[s] = (PF && i > 0) ? xnext[s] : *reinterpret_cast<const bf16x8*>(xt + xr[s]);
-            if (PF && i + 1 < my_ntiles) {
-                const char* xn = lds + (int)((i + 1) % NBUF) * TILE;
-#pragma unroll
-                for (int s = 0; s < 4; ++s) xnext[s] = *reinterpret_cast<const bf16x8*>(xn + xr[s]);
-            }
             f32x4 acc[KB];
 #pragma unroll
             for (int b = 0; b < KB; ++b) acc[b] = nin[b];
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
-                const bf16x8 xb = xcur[s];
+                const bf16x8 xb = *reinterpret_cast<const bf16x8*>(xt + xr[s]);
 #pragma unroll
                 for (int b = 0; b < KB; ++b)
                     acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cf[b][s], xb, acc[b], 0, 0, 0);
@@ -293,32 +358,36 @@ __global__ __launch_bounds__(512) void kmeans_v7_kernel(const __bf16* __restrict
     }
     if (MODE != LOAD_ONLY && tid < 128)
         slab_cnt[(int64_t)blockIdx.x * 128 + tid] = tid < 16 * KB ? (float)cnt[tid] : 0.f;
+    if (VAR == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-template <int KB, bool PF>
-hipError_t launch_kb_pf(int mode, dim3 grid, hipStream_t st, const __bf16* X, int64_t N, const __bf16* C,
-                        const float* ninit, float* slab, float* slab_cnt, int* assign_out, int64_t ntiles,
-                        int64_t per) {
+template <int KB, int VAR>
+hipError_t launch_kb_var(int mode, dim3 grid, hipStream_t st, const __bf16* X, int64_t N, const __bf16* C,
+                         const float* ninit, float* slab, float* slab_cnt, int* assign_out, int64_t ntiles,
+                         int64_t per) {
     if (mode == LOAD_ONLY)
-        hipLaunchKernelGGL((kmeans_v7_kernel<KB, LOAD_ONLY, PF>), grid, dim3(512), 0, st, X, N, C, ninit, slab,
+        hipLaunchKernelGGL((kmeans_v7_kernel<KB, LOAD_ONLY, VAR>), grid, dim3(512), 0, st, X, N, C, ninit, slab,
                            slab_cnt, assign_out, ntiles, per);
     else if (mode == COMPUTE_ONLY)
-        hipLaunchKernelGGL((kmeans_v7_kernel<KB, COMPUTE_ONLY, PF>), grid, dim3(512), 0, st, X, N, C, ninit, slab,
-                           slab_cnt, assign_out, ntiles, per);
+        hipLaunchKernelGGL((kmeans_v7_kernel<KB, COMPUTE_ONLY, VAR>), grid, dim3(512), 0, st, X, N, C, ninit,
+                           slab, slab_cnt, assign_out, ntiles, per);
     else
-        hipLaunchKernelGGL((kmeans_v7_kernel<KB, FULL, PF>), grid, dim3(512), 0, st, X, N, C, ninit, slab,
+        hipLaunchKernelGGL((kmeans_v7_kernel<KB, FULL, VAR>), grid, dim3(512), 0, st, X, N, C, ninit, slab,
                            slab_cnt, assign_out, ntiles, per);
     return hipGetLastError();
 }
 
-// mode bits 0-1: 0 full, 1 load only, 2 compute only; bit 4: distance-fragment prefetch variant (PF)
+// mode bits 0-1: 0 full, 1 load only, 2 compute only; bits 4-5: DMA variant (VAR, see the kernel)
 template <int KB>
 hipError_t launch_kb(int mode, dim3 grid, hipStream_t st, const __bf16* X, int64_t N, const __bf16* C,
                      const float* ninit, float* slab, float* slab_cnt, int* assign_out, int64_t ntiles,
                      int64_t per) {
-    if (mode & 16)
-        return launch_kb_pf<KB, true>(mode & 3, grid, st, X, N, C, ninit, slab, slab_cnt, assign_out, ntiles, per);
-    return launch_kb_pf<KB, false>(mode & 3, grid, st, X, N, C, ninit, slab, slab_cnt, assign_out, ntiles, per);
+    const int var = (mode >> 4) & 3;
+    if (var == 1)
+        return launch_kb_var<KB, 1>(mode & 3, grid, st, X, N, C, ninit, slab, slab_cnt, assign_out, ntiles, per);
+    if (var == 2)
+        return launch_kb_var<KB, 2>(mode & 3, grid, st, X, N, C, ninit, slab, slab_cnt, assign_out, ntiles, per);
+    return launch_kb_var<KB, 0>(mode & 3, grid, st, X, N, C, ninit, slab, slab_cnt, assign_out, ntiles, per);
 }
 
 }  // namespace

@@ -62,9 +62,9 @@ def prepare_centroids(C: torch.Tensor, device) -> Tuple[torch.Tensor, torch.Tens
 
 
 KERNEL_VERSIONS = ("v7",)
-# v7 PF variant: each distance wave reads its fragments of tile i+1 right after barrier i (their DMA waited one
-# iteration earlier), so its MFMAs of the next tile start without an LDS round trip after the barrier
-V7_PREFETCH = __import__("os").environ.get("ALINK_KMEANS_V7_PF", "0") == "1"
+# v7 DMA variant (csrc/kmeans_v7.hip VAR): 0 = all waves stage the tile ring, 1 = accumulate waves stage it all
+# (distance waves carry no DMA issue cost / vmcnt waits), 2 = 1 + L2 touch of the tile 3 iterations past the ring
+V7_VAR = int(__import__("os").environ.get("ALINK_KMEANS_V7_VAR", "0"))
 DEFAULT_KERNEL = "v7"
 
 
@@ -107,8 +107,8 @@ def assign_accumulate_hip(X: torch.Tensor, C: torch.Tensor, grid: Optional[int] 
     slab, slab_cnt = _BUF[key]
     out = torch.empty((k, HIP_D + 1), dtype=torch.float64, device=dev)
     st = _lib.stream_ptr(dev)
-    if V7_PREFETCH and mode == 0:
-        mode = 16      # distance-fragment prefetch variant (csrc/kmeans_v7.hip, template PF)
+    if V7_VAR and mode < 16:
+        mode |= V7_VAR << 4
     rc = getattr(L, f"alink_kmeans_assign_accum_bf16_{ver}")(
         X.data_ptr(), n, cpad.data_ptr(), ninit.data_ptr(), k, slab.data_ptr(), slab_cnt.data_ptr(), grid, st,
         None if assign_out is None else assign_out.data_ptr(), int(mode))

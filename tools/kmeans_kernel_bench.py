@@ -25,7 +25,7 @@ def main():
     ap.add_argument("--grid", type=int, default=None)
     ap.add_argument("--load-only", action="store_true", help="time the LDS-DMA load pipeline alone")
     ap.add_argument("--compute-only", action="store_true", help="time the compute alone (no loads)")
-    ap.add_argument("--pf", action="store_true", help="distance-fragment prefetch variant (mode bit 16)")
+    ap.add_argument("--var", type=int, default=0, help="v7 DMA variant (mode bits 4-5)")
     a = ap.parse_args()
     dev = torch.device("cuda")
     n, d, k = a.rows, 128, a.k
@@ -40,10 +40,10 @@ def main():
     C = (centers + 0.5 * torch.randn(k, d, device=dev, generator=g)).double()
     def run(Xs):
         m = 2 if a.compute_only else 1 if a.load_only else 0
-        return K.assign_accumulate_hip(Xs, C, grid=a.grid, mode=m | (16 if a.pf else 0))
+        return K.assign_accumulate_hip(Xs, C, grid=a.grid, mode=m | (a.var << 4))
     out = run(X)
     torch.cuda.synchronize()
-    res = {"rows": n, "k": k, "load_only": a.load_only, "compute_only": a.compute_only, "pf": a.pf}
+    res = {"rows": n, "k": k, "load_only": a.load_only, "compute_only": a.compute_only, "var": a.var}
     if a.torch:
         ref0 = K.assign_accumulate_torch(X[:2_000_000], C)
         got0 = run(X[:2_000_000].contiguous())
