@@ -228,13 +228,21 @@ def _local_kmeans(samples: torch.Tensor, weights: torch.Tensor, k: int, dist_typ
     over ALL candidates when the set is small (<= 4096, the usual k-means|| output, O(k m^2) on the device),
     else over 2 + ln k sampled trials.  The reference samples one candidate per pick with plain distance
     weights, which in high dimension (within-cluster spread comparable to cluster separation) regularly
-    seeds two centroids in one true cluster and then needs tens of Lloyd steps to creep apart."""
+    seeds two centroids in one true cluster and then needs tens of Lloyd steps to creep apart.
+
+    ``ALINK_KMEANS_SEEDING=reference`` selects the reference's rule instead (one candidate per pick, sampled with
+    probability proportional to weight x cost), for reference-faithful runs."""
+    import os
     rng = np.random.default_rng(seed)
     n = samples.shape[0]
     w = weights.to(torch.float64)
     D = _seed_cost(pairwise_distance(samples, samples, dist_type), dist_type)  # [n, n]
-    exhaustive = n <= 4096
-    trials = 2 + int(np.log(max(k, 2)))
+    reference_rule = os.environ.get("ALINK_KMEANS_SEEDING", "greedy").lower() == "reference"
+    if reference_rule:
+        trials = 1
+    exhaustive = n <= 4096 and not reference_rule
+    if not reference_rule:
+        trials = 2 + int(np.log(max(k, 2)))
     cum = torch.cumsum(w, 0).cpu().numpy()
     idx = int(min(np.searchsorted(cum, rng.random() * cum[-1], side="left"), n - 1))
     chosen = [idx]

@@ -180,7 +180,7 @@ __global__ __launch_bounds__(512) void kmeans_v7_kernel(const __bf16* __restrict
     // the distance waves — the critical role — carry no LDS-DMA issue cost and no vmcnt waits.  VAR 2: VAR 1 +
     // distance waves 0/1 touch tile i + AHEAD + PD into L2 (PD = 3).
     constexpr int PD = 3;
-    constexpr bool ACC_DMA = VAR >= 1;
+    constexpr bool ACC_DMA = VAR >= 1;      // VAR 3: VAR 1 + s_setprio 1 on the distance waves
     __shared__ __attribute__((aligned(16))) char lds[PL::LDS_BYTES];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -236,6 +236,7 @@ __global__ __launch_bounds__(512) void kmeans_v7_kernel(const __bf16* __restrict
 
     if (wave < 4) {
         // ------------------------------ distance / argmax role ------------------------------
+        if (VAR == 3) __builtin_amdgcn_s_setprio(1);
         const int myrow = 16 * wave + li;
         bf16x8 cf[KB][4];
         f32x4 nin[KB];
@@ -377,12 +378,15 @@ hipError_t launch_kb_var(int mode, dim3 grid, hipStream_t st, const __bf16* X, i
     return hipGetLastError();
 }
 
-// mode bits 0-1: 0 full, 1 load only, 2 compute only; bits 4-5: DMA variant (VAR, see the kernel)
+// mode bits 0-1: 0 full, 1 load only, 2 compute only; bits 4-5: variant (VAR, see the kernel); the default
+// (mode < 16 from the wrapper) is VAR 1: 5.80-5.91 -> 5.50-5.54 ms at k = 100 (profiles/kmeans_r2_session5.txt)
 template <int KB>
 hipError_t launch_kb(int mode, dim3 grid, hipStream_t st, const __bf16* X, int64_t N, const __bf16* C,
                      const float* ninit, float* slab, float* slab_cnt, int* assign_out, int64_t ntiles,
                      int64_t per) {
     const int var = (mode >> 4) & 3;
+    if (var == 3)
+        return launch_kb_var<KB, 3>(mode & 3, grid, st, X, N, C, ninit, slab, slab_cnt, assign_out, ntiles, per);
     if (var == 1)
         return launch_kb_var<KB, 1>(mode & 3, grid, st, X, N, C, ninit, slab, slab_cnt, assign_out, ntiles, per);
     if (var == 2)

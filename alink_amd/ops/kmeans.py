@@ -62,9 +62,11 @@ def prepare_centroids(C: torch.Tensor, device) -> Tuple[torch.Tensor, torch.Tens
 
 
 KERNEL_VERSIONS = ("v7",)
-# v7 DMA variant (csrc/kmeans_v7.hip VAR): 0 = all waves stage the tile ring, 1 = accumulate waves stage it all
-# (distance waves carry no DMA issue cost / vmcnt waits), 2 = 1 + L2 touch of the tile 3 iterations past the ring
-V7_VAR = int(__import__("os").environ.get("ALINK_KMEANS_V7_VAR", "0"))
+# v7 variant (csrc/kmeans_v7.hip VAR): 0 = all 8 waves stage the tile ring; 1 (default) = the accumulate waves
+# stage it all, so the distance waves (the critical role) carry no LDS-DMA issue cost or vmcnt waits
+# (-4..5 %); 2 = 1 + an L2 touch of the tile 3 iterations past the ring (slower); 3 = 1 + s_setprio on the
+# distance waves
+V7_VAR = int(__import__("os").environ.get("ALINK_KMEANS_V7_VAR", "1"))
 DEFAULT_KERNEL = "v7"
 
 
@@ -107,7 +109,7 @@ def assign_accumulate_hip(X: torch.Tensor, C: torch.Tensor, grid: Optional[int] 
     slab, slab_cnt = _BUF[key]
     out = torch.empty((k, HIP_D + 1), dtype=torch.float64, device=dev)
     st = _lib.stream_ptr(dev)
-    if V7_VAR and mode < 16:
+    if mode < 16:
         mode |= V7_VAR << 4
     rc = getattr(L, f"alink_kmeans_assign_accum_bf16_{ver}")(
         X.data_ptr(), n, cpad.data_ptr(), ninit.data_ptr(), k, slab.data_ptr(), slab_cnt.data_ptr(), grid, st,

@@ -71,3 +71,18 @@ def test_kmeans_init_modes_and_cosine(init):
         op = KMeansTrainBatchOp().setVectorCol("v").setK(3).setInitMode(init).setDistanceType(dt).linkFrom(data)
         out = KMeansPredictBatchOp().setPredictionCol("p").setPredictionDetailCol("d").linkFrom(op, data).collect()
         assert len(out) == 300 and all(0 <= r[1] < 3 for r in out)
+
+
+def test_reference_seeding_rule_flag(monkeypatch):
+    """ALINK_KMEANS_SEEDING=reference: one sampled candidate per pick (LocalKmeansFunc); both rules give k
+    distinct centroids from the candidate set."""
+    import torch
+    from alink_amd.models.clustering.kmeans import _local_kmeans
+    g = torch.Generator().manual_seed(0)
+    pts = torch.cat([torch.randn(50, 4, generator=g, dtype=torch.float64) + 10 * i for i in range(5)])
+    w = torch.ones(pts.shape[0], dtype=torch.float64)
+    for rule in ("greedy", "reference"):
+        monkeypatch.setenv("ALINK_KMEANS_SEEDING", rule)
+        C = _local_kmeans(pts, w, 5, "EUCLIDEAN", seed=3)
+        assert C.shape == (5, 4)
+        assert len({tuple(torch.round(c / 10).tolist()) for c in C}) >= 4
