@@ -340,6 +340,11 @@ class KMeansAssignCluster(ComputeFunction):
         k = ctx.getObj(K)
         X = ctx.getObj(TRAIN_DATA)
         C = cur[1][:k]
+        spec = ctx.getObj(SPEC_BUF)
+        ctx.removeObj(SPEC_BUF)
+        if spec is not None and spec[0] == (ctx.getStepNo(), kops._ckey(C)):
+            ctx.putObj(CENTROID_ALL_REDUCE, spec[1])    # launched by the previous superstep's update
+            return
         if X is None or X.shape[0] == 0:
             buf = torch.zeros((k, C.shape[1] + 1), dtype=torch.float64, device=C.device)
         else:
@@ -347,18 +352,74 @@ class KMeansAssignCluster(ComputeFunction):
         ctx.putObj(CENTROID_ALL_REDUCE, buf)
 
 
+def _lib_ok() -> bool:
+    return kops._lib.available()
+
+
+SPEC_BUF = "speculativeAllReduceBuf"
+
+
 class KMeansUpdateCentroids(ComputeFunction):
-    def __init__(self, dist_type: str):
+    """``speculate``: after the fused HIP update, the NEXT superstep's assign kernel is queued on the new
+    centroids before the host waits for the update's 16-byte stats (empty flag, max shift), so the GPU runs
+    straight through the host's criterion / engine bookkeeping.  The queued result is used only if that next
+    superstep runs with exactly these centroids (no empty-cluster compaction, not converged, not the last
+    step); otherwise it is dropped — results are identical either way.  ``sync_steps``: supersteps after which
+    nothing may be queued ahead (a caller that times supersteps, e.g. bench.py, synchronises there)."""
+
+    def __init__(self, dist_type: str, max_iter: int = 2 ** 31 - 1, sync_steps=(), speculate: bool = True):
         self.dist_type = dist_type
+        self.max_iter = int(max_iter)
+        self.sync_steps = set(sync_steps or ())
+        self.speculate = speculate
 
     def calc(self, ctx):
         tgt = ctx.getObj(CENTROID2) if ctx.getStepNo() % 2 == 0 else ctx.getObj(CENTROID1)
+        old = ctx.getObj(CENTROID1) if ctx.getStepNo() % 2 == 0 else ctx.getObj(CENTROID2)
         buf = ctx.getObj(CENTROID_ALL_REDUCE)
         d = buf.shape[1] - 1
         cnt = buf[:, d]
-        # one small D2H read decides the (rare) empty-cluster compaction on the host; the common
-        # all-non-empty step stays a single device division (no mask indexing / nonzero syncs)
-        empty = (cnt <= 0).nonzero().reshape(-1).tolist() if bool((cnt <= 0).any().item()) else []
+        prev = old[1] if old is not None and old[1] is not None else None
+        if self.dist_type == "EUCLIDEAN" and kops.update_supported(buf) and \
+                (_lib_ok() or not kops._lib.torch_fallback_allowed()):
+            # fused HIP update: C, the shift vs prev, the empty flag and the next step's MFMA operands in one
+            # launch + one 16-byte read
+            step = ctx.getStepNo()
+            X = ctx.getObj(TRAIN_DATA)
+            spec_ok = (self.speculate and step >= 2 and step < self.max_iter and step not in self.sync_steps
+                       and X is not None and X.shape[0] > 0 and kops.hip_supported(X, buf.shape[0]))
+            C, read = kops.update_centroids_hip(buf, prev, deferred=True)
+            if spec_ok:
+                ctx.putObj(SPEC_BUF, ((step + 1, kops._ckey(C)), kops.assign_accumulate_hip(X, C)))
+            shift, has_empty = read()
+            if has_empty:
+                ctx.removeObj(SPEC_BUF)
+            if not has_empty:
+                ctx.putObj("maxShift", shift)
+                tgt[0] = ctx.getStepNo()
+                tgt[1] = C
+                ctx.putObj("lastWeights", cnt)
+                ctx.putObj(K, int(C.shape[0]))
+                return
+        # ONE small D2H read per superstep: the (rare) empty-cluster flag together with the max centroid shift
+        # the termination criterion needs (the criterion then reads the host float instead of syncing again)
+        C = buf[:, :d] / cnt[:, None]
+        if self.dist_type == "COSINE":
+            C = _normalize_rows(C)
+        empty_any = (cnt <= 0).any().to(C.dtype)
+        shift = None
+        if prev is not None and prev.shape == C.shape and self.dist_type not in ("COSINE", "HAVERSINE"):
+            flag, shift = torch.stack([empty_any, (C - prev).norm(dim=1).max()]).tolist()
+        else:
+            flag = empty_any.item()
+        empty = (cnt <= 0).nonzero().reshape(-1).tolist() if flag > 0 else []
+        ctx.putObj("maxShift", None if empty else shift)
+        if not empty:
+            tgt[0] = ctx.getStepNo()
+            tgt[1] = C
+            ctx.putObj("lastWeights", cnt)
+            ctx.putObj(K, int(C.shape[0]))
+            return
         if empty:
             keep = torch.as_tensor([i for i in range(buf.shape[0]) if i not in set(empty)], dtype=torch.long,
                                    device=buf.device)
@@ -384,6 +445,10 @@ class KMeansIterTermination(CompareCriterionFunction):
         b = ctx.getObj(CENTROID2)[1][:k]
         if a.shape != b.shape:
             return False
+        pre = ctx.getObj("maxShift")          # computed with the update's single D2H read (EUCLIDEAN)
+        if pre is not None and self.dist_type not in ("COSINE", "HAVERSINE"):
+            self.history.append(float(pre))
+            return float(pre) < self.tol
         if self.dist_type == "COSINE":
             d = 1.0 - (a * b).sum(1)
         elif self.dist_type == "HAVERSINE":
@@ -416,7 +481,7 @@ class KMeansOutputModel(CompleteResultFunction):
 
 def train_kmeans(X: torch.Tensor, k: int, max_iter: int, tol: float, dist_type: str, init_mode: str,
                  init_steps: int, vector_col: Optional[str], env, lat_col=None, lon_col=None,
-                 init_centroids: Optional[torch.Tensor] = None, on_step=None, seed: int = 0):
+                 init_centroids: Optional[torch.Tensor] = None, on_step=None, seed: int = 0, sync_steps=()):
     """Run the KMeans BSP queue on this rank's rows ``X`` ([n, d] on the env device); returns
     (model rows, queue)."""
     dist_type = dist_type.upper()
@@ -437,7 +502,7 @@ def train_kmeans(X: torch.Tensor, k: int, max_iter: int, tol: float, dist_type: 
          .add(KMeansPreallocateCentroid())
          .add(KMeansAssignCluster())
          .add(AllReduce(CENTROID_ALL_REDUCE))
-         .add(KMeansUpdateCentroids(dist_type))
+         .add(KMeansUpdateCentroids(dist_type, max_iter, sync_steps))
          .setCompareCriterionOfNode0(KMeansIterTermination(dist_type, tol), replicated=True)
          .closeWith(KMeansOutputModel(dist_type, vector_col, lat_col, lon_col))
          .setMaxIter(max_iter))

@@ -46,7 +46,8 @@ class KMeansTrainBatchOp(BatchOperator):
         im = im.name if hasattr(im, "name") else str(im)
         rows, q = train_kmeans(X, self.getK(), self.getMaxIter(), self.getEpsilon(), dt, im, self.getInitSteps(),
                                self.getVectorCol(), env, seed=self.getParams().get(self._param_infos["randomSeed"]),
-                               on_step=getattr(self, "_on_step", None))
+                               on_step=getattr(self, "_on_step", None),
+                               sync_steps=getattr(self, "_sync_steps", ()))
         self._queue = q
         self.setOutputTable(MTable.from_rows(rows, KMeansModelDataConverter().getModelSchema(), replicated=True))
         return self

@@ -63,9 +63,68 @@ __global__ __launch_bounds__(128) void kmeans_prep_centroids_kernel(const double
     if (d == 0) ninit[c] = c < k ? -0.5f * red[0] : -3.0e38f;
 }
 
+// fused centroid update after the all-reduce (reference KMeansUpdateCentroidsAndSetAllReduce + the termination
+// test KMeansIterTermination, A/operator/common/clustering/kmeans/): one workgroup per padded centroid row
+//   C[c] = sum[c] / cnt[c]                       (fp64, written for c < k)
+//   cpad[c] = bf16(C[c]), ninit[c] = -|cpad[c]|^2/2   (the NEXT superstep's MFMA operands: no separate prep launch)
+//   stat[0] = max_c ||C[c] - prev[c]||  (fp64 bits, atomicMax: non-negative doubles order as unsigned integers)
+//   stat[1] = 1 if any cnt[c] <= 0 (the host then redoes the update with empty-cluster compaction)
+// replacing ~8 small torch launches + the prep launch of the next step and giving the host ONE 16-byte read.
+__global__ __launch_bounds__(128) void kmeans_update_kernel(const double* __restrict__ buf, int k,
+                                                            const double* __restrict__ prev,
+                                                            double* __restrict__ C, __bf16* __restrict__ cpad,
+                                                            float* __restrict__ ninit,
+                                                            unsigned long long* __restrict__ stat) {
+    __shared__ float red[128];
+    __shared__ double redd[128];
+    const int c = blockIdx.x, d = threadIdx.x;
+    double v = 0.0;
+    bool empty = false;
+    if (c < k) {
+        const double cnt = buf[(int64_t)c * (D + 1) + D];
+        empty = !(cnt > 0.0);
+        v = empty ? 0.0 : buf[(int64_t)c * (D + 1) + d] / cnt;
+        C[(int64_t)c * D + d] = v;
+    }
+    const __bf16 b = (__bf16)(float)v;
+    cpad[c * D + d] = b;
+    const float f = (float)b;
+    red[d] = f * f;
+    const double df = (c < k && prev != nullptr) ? v - prev[(int64_t)c * D + d] : 0.0;
+    redd[d] = df * df;
+    __syncthreads();
+    for (int off = 64; off > 0; off >>= 1) {
+        if (d < off) {
+            red[d] += red[d + off];
+            redd[d] += redd[d + off];
+        }
+        __syncthreads();
+    }
+    if (d == 0) {
+        ninit[c] = c < k ? -0.5f * red[0] : -3.0e38f;
+        if (c < k) {
+            const double sh = sqrt(redd[0]);
+            atomicMax(stat, (unsigned long long)__double_as_longlong(sh));
+            if (empty) atomicMax(stat + 1, 1ull);
+        }
+    }
+}
+
 }  // namespace
 
 extern "C" {
+
+// buf [k][D+1] (sums | count), prev [k][D] (nullable), C out [k][D], cpad [128][D] bf16, ninit [128],
+// stat [2] u64 (zeroed here): max shift (double bits), any-empty flag
+int alink_kmeans_update(const double* buf, int k, const double* prev, double* C, void* cpad, float* ninit,
+                        unsigned long long* stat, void* stream) {
+    if (k < 1 || k > 128) return -1;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (hipMemsetAsync(stat, 0, 2 * sizeof(unsigned long long), st) != hipSuccess) return -2;
+    hipLaunchKernelGGL(kmeans_update_kernel, dim3(128), dim3(128), 0, st, buf, k, prev, C, (__bf16*)cpad, ninit,
+                       stat);
+    return (int)hipGetLastError();
+}
 
 int alink_kmeans_reduce_slabs(const float* slab, const float* slab_cnt, int nslab, int k, double* out,
                               void* stream) {

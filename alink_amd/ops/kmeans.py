@@ -16,6 +16,7 @@ from __future__ import annotations
 
 from typing import Dict, Optional, Tuple
 
+import numpy as np
 import torch
 
 from . import _lib
@@ -37,11 +38,21 @@ def hip_supported(X: torch.Tensor, k: int) -> bool:
 _PREP = {}
 
 
+_PREPARED = {}    # device -> (key of the centroid tensor whose operands sit in _PREP[device])
+
+
+def _ckey(C: torch.Tensor):
+    return (C.data_ptr(), tuple(C.shape), C._version)
+
+
 def prepare_centroids(C: torch.Tensor, device) -> Tuple[torch.Tensor, torch.Tensor]:
     """Padded bf16 centroid block [128,128] and accumulator init -|c|^2/2 (of the bf16-rounded centroids).
-    fp64 centroids on the GPU go through one HIP launch into per-device buffers (stream-ordered reuse)."""
+    fp64 centroids on the GPU go through one HIP launch into per-device buffers (stream-ordered reuse); when
+    ``update_centroids_hip`` already wrote the operands of exactly this tensor, nothing is launched."""
     k = C.shape[0]
     if C.is_cuda and C.dtype == torch.float64 and C.shape[1] == HIP_D and k <= HIP_KMAX:
+        if _PREPARED.get(C.device.index) == _ckey(C) and C.device.index in _PREP:
+            return _PREP[C.device.index]
         L = _lib.require()
         key = C.device.index
         if key not in _PREP:
@@ -52,6 +63,7 @@ def prepare_centroids(C: torch.Tensor, device) -> Tuple[torch.Tensor, torch.Tens
         rc = L.alink_kmeans_prep_centroids(Cc.data_ptr(), k, cpad.data_ptr(), ninit.data_ptr(), _lib.stream_ptr(C.device))
         if rc != 0:
             raise RuntimeError(f"alink_kmeans_prep_centroids failed: {rc}")
+        _PREPARED[key] = _ckey(C) if Cc is C else None
         return cpad, ninit
     cb = C.to(device=device, dtype=torch.bfloat16)
     cpad = torch.zeros((HIP_KMAX, HIP_D), dtype=torch.bfloat16, device=device)
@@ -79,8 +91,15 @@ def kernel_version() -> str:
     return v
 
 
+_CUS: Dict[int, int] = {}
+_GRID: Dict[Tuple, int] = {}
+
+
 def _num_cus(device) -> int:
-    return torch.cuda.get_device_properties(device).multi_processor_count
+    idx = torch.device(device).index or 0
+    if idx not in _CUS:
+        _CUS[idx] = torch.cuda.get_device_properties(device).multi_processor_count
+    return _CUS[idx]
 
 
 def assign_accumulate_hip(X: torch.Tensor, C: torch.Tensor, grid: Optional[int] = None,
@@ -101,7 +120,10 @@ def assign_accumulate_hip(X: torch.Tensor, C: torch.Tensor, grid: Optional[int] 
     cpad, ninit = prepare_centroids(C, dev)
     n = X.shape[0]
     ver = kernel_version()
-    grid = int(getattr(L, f"alink_kmeans_{ver}_grid")(n, grid if grid is not None else _num_cus(dev)))
+    gkey = (ver, n, grid, dev.index)
+    if gkey not in _GRID:      # per-shape launch geometry (one ctypes call per shape, not per superstep)
+        _GRID[gkey] = int(getattr(L, f"alink_kmeans_{ver}_grid")(n, grid if grid is not None else _num_cus(dev)))
+    grid = _GRID[gkey]
     key = (dev.index, grid)
     if key not in _BUF:
         _BUF[key] = (torch.empty((grid, HIP_KMAX, HIP_D), dtype=torch.float32, device=dev),
@@ -120,6 +142,56 @@ def assign_accumulate_hip(X: torch.Tensor, C: torch.Tensor, grid: Optional[int] 
     if rc != 0:
         raise RuntimeError(f"alink_kmeans_reduce_slabs failed: {rc}")
     return out
+
+
+_STAT = {}
+
+
+def update_supported(buf: torch.Tensor) -> bool:
+    return buf.is_cuda and buf.dtype == torch.float64 and buf.dim() == 2 and buf.shape[1] == HIP_D + 1 and \
+        1 <= buf.shape[0] <= HIP_KMAX and buf.is_contiguous()
+
+
+def update_centroids_hip(buf: torch.Tensor, prev: Optional[torch.Tensor], deferred: bool = False):
+    """Fused Lloyd update on the all-reduced ``[k, 129]`` buffer (``csrc/kmeans_common.hip``): returns
+    ``(C [k,128] fp64, max_shift vs prev or None, any_empty)`` with ONE 16-byte device->host read, and leaves
+    the next superstep's bf16 operands prepared (``prepare_centroids`` of the returned C launches nothing).
+    ``deferred=True`` returns ``(C, read)`` instead: ``read()`` waits for the stats later, so the caller can queue
+    more GPU work (the next superstep's assign kernel) first."""
+    L = _lib.require()
+    dev = buf.device
+    k = buf.shape[0]
+    if dev.index not in _PREP:
+        _PREP[dev.index] = (torch.empty((HIP_KMAX, HIP_D), dtype=torch.bfloat16, device=dev),
+                            torch.empty((HIP_KMAX,), dtype=torch.float32, device=dev))
+    if dev.index not in _STAT:
+        _STAT[dev.index] = (torch.empty(2, dtype=torch.int64, device=dev),
+                            torch.empty(2, dtype=torch.int64, pin_memory=True))
+    stat, host = _STAT[dev.index]
+    cpad, ninit = _PREP[dev.index]
+    use_prev = prev is not None and prev.is_cuda and prev.dtype == torch.float64 and tuple(prev.shape) == (k, HIP_D)
+    pv = prev.contiguous() if use_prev else None
+    C = torch.empty((k, HIP_D), dtype=torch.float64, device=dev)
+    rc = L.alink_kmeans_update(buf.data_ptr(), k, None if pv is None else pv.data_ptr(), C.data_ptr(),
+                               cpad.data_ptr(), ninit.data_ptr(), stat.data_ptr(), _lib.stream_ptr(dev))
+    if rc != 0:
+        raise RuntimeError(f"alink_kmeans_update failed: {rc}")
+    host.copy_(stat, non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record(torch.cuda.current_stream(dev))
+    _PREPARED[dev.index] = _ckey(C)
+
+    def read():
+        """Wait for THIS update's 16-byte stats only (work queued after it, e.g. a speculative next-step
+        kernel, keeps running) and return (max_shift or None, any_empty)."""
+        ev.synchronize()
+        shift_bits, empty = int(host[0]), int(host[1])
+        shift = float(np.frombuffer(np.int64(shift_bits).tobytes(), dtype=np.float64)[0]) if use_prev else None
+        return shift, bool(empty)
+    if deferred:
+        return C, read
+    shift, empty = read()
+    return C, shift, empty
 
 
 def _scores(Xc: torch.Tensor, C: torch.Tensor, emulate_bf16: bool) -> torch.Tensor:

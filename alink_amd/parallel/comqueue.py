@@ -233,6 +233,9 @@ class AllReduce(CommunicateFunction):
         if self.length is not None:
             n = int(contexts[0].getObj(self.length))
         t0, kind = _as_tensor(present[0])
+        if len(bufs) == 1 and n is None and kind == "torch" and t0.is_contiguous():
+            comm.all_reduce(t0.view(-1), self.op)      # one task per process (one GPU): reduce in place
+            return
         view = (lambda t: t.reshape(-1)[:n]) if n is not None else (lambda t: t.reshape(-1))
         acc = view(t0).clone()
         for b in present[1:]:

@@ -86,6 +86,7 @@ def main():
 
     op = KMeansTrainBatchOp().setVectorCol("vec").setK(a.k).setMaxIter(a.warmup + a.steps).setEpsilon(-1.0)
     op._on_step = on_step
+    op._sync_steps = (a.warmup, a.warmup + a.steps)   # nothing queued across the timing marks
     from alink_amd.operator.batch.source import TableSourceBatchOp
     t_tot = time.perf_counter()
     hip0 = kops.HIP_CALLS

@@ -161,3 +161,48 @@ def test_linear_search_losses_kernel_matches_fp64(d, loss):
         etas = E[:, :1] - steps[None, :] * (E[:, 1:2] * beta)
         ref = (fn.loss(etas, y[:, None]) * w[:, None]).sum(0)
         torch.testing.assert_close(got, ref, rtol=1e-10, atol=1e-8)
+
+
+@pytest.mark.parametrize("k", [1, 37, 100, 128])
+def test_fused_centroid_update_matches_torch(k):
+    """csrc/kmeans_common.hip kmeans_update: C = sums / counts, max shift vs prev (fp64), empty flag, and the next
+    superstep's bf16 operands identical to a fresh prep launch."""
+    from alink_amd.ops import kmeans as K
+    g = torch.Generator(device="cuda").manual_seed(k)
+    buf = torch.randn(k, 129, device="cuda", dtype=torch.float64, generator=g) * 100
+    buf[:, 128] = torch.randint(1, 1000, (k,), device="cuda", generator=g).double()
+    prev = torch.randn(k, 128, device="cuda", dtype=torch.float64, generator=g)
+    C, shift, empty = K.update_centroids_hip(buf, prev)
+    ref = buf[:, :128] / buf[:, 128:]
+    torch.testing.assert_close(C, ref, rtol=0, atol=0)
+    assert not empty
+    assert abs(shift - float((ref - prev).norm(dim=1).max())) <= 1e-12 * max(1.0, shift)
+    cpad, ninit = K.prepare_centroids(C, C.device)            # cached: no launch
+    cpad2, ninit2 = [t.clone() for t in (cpad, ninit)]
+    K._PREPARED.clear()
+    cpad3, ninit3 = K.prepare_centroids(C, C.device)          # fresh prep launch
+    assert torch.equal(cpad2, cpad3) and torch.equal(ninit2, ninit3)
+    buf[k // 2, 128] = 0.0
+    _, _, empty = K.update_centroids_hip(buf, None)
+    assert empty
+
+
+def test_speculative_next_step_launch_gives_identical_model():
+    """KMeansUpdateCentroids queues the next superstep's assign kernel before reading the update stats; the
+    trained model must be bit-identical to a run without speculation (sync after every step), incl. a run that
+    converges early (the queued kernel of the step after convergence is dropped)."""
+    from alink_amd import useLocalEnv
+    from alink_amd.models.clustering.kmeans import train_kmeans
+    env = useLocalEnv(1, device="cuda:0")
+    g = torch.Generator(device="cuda").manual_seed(5)
+    k = 40
+    centers = torch.randn(k, 128, device="cuda", generator=g) * 4
+    lab = torch.randint(0, k, (400_000,), device="cuda", generator=g)
+    X = (centers[lab] + torch.randn(lab.numel(), 128, device="cuda", generator=g)).to(torch.bfloat16)
+    init = (centers + 0.5 * torch.randn(k, 128, device="cuda", generator=g)).double()
+    for tol in (-1.0, 1e-4):
+        a, qa = train_kmeans(X, k, 12, tol, "EUCLIDEAN", "RANDOM", 2, "v", env, init_centroids=init)
+        b, qb = train_kmeans(X, k, 12, tol, "EUCLIDEAN", "RANDOM", 2, "v", env, init_centroids=init,
+                             sync_steps=range(100))
+        assert len(qa.stats) == len(qb.stats)
+        assert [list(r) for r in a] == [list(r) for r in b]
