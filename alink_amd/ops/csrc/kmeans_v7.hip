@@ -47,13 +47,12 @@ constexpr int LDS_CAP = 160 * 1024;
 template <int KB>
 struct Plan {
     static constexpr int OHB = 16 * KB * TR * 2;
-    static constexpr int NBUF_FIT = (LDS_CAP - 2 * OHB - 128 * 4 - 512) / TILE;
+    static constexpr int NBUF_FIT = (LDS_CAP - 2 * OHB - 128 * 4) / TILE;
     static constexpr int NBUF = NBUF_FIT > 8 ? 8 : NBUF_FIT;   // X ring slots: tile i, i-1, AHEAD in flight
     static constexpr int AHEAD = NBUF - 2;
     static constexpr int OFF_OH = NBUF * TILE;
     static constexpr int OFF_CNT = OFF_OH + 2 * OHB;
-    static constexpr int OFF_PAD = OFF_CNT + 128 * 4;          // VAR 2: landing pad of the L2 touch loads
-    static constexpr int LDS_BYTES = OFF_PAD + 2 * 256;
+    static constexpr int LDS_BYTES = OFF_CNT + 128 * 4;
     static_assert(LDS_BYTES <= LDS_CAP && AHEAD >= 3 && AHEAD <= 6, "LDS plan");
 };
 constexpr uint32_t NONE = 0xFFFFu;
@@ -118,28 +117,6 @@ __device__ __forceinline__ void stage_np(char* lds, int slot, const char* X, int
     }
 }
 
-// VAR 2: touch every 128-B line of a future tile (one dword per line, landing in a per-wave LDS pad) so its
-// LDS-DMA, issued PD iterations later, hits L2 instead of HBM: the ring depth is bounded by LDS, L2 is not
-__device__ __forceinline__ void touch_l2(char* lds, int pad_off, const char* X, int64_t row0, int64_t N, int half,
-                                         int lane) {
-    const int64_t rem = (N - row0) * ROWB;
-    const int nbytes = rem <= 0 ? 0 : (rem < TILE ? (int)rem : TILE);
-    const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc((void*)(X + (rem > 0 ? row0 : 0) * ROWB), (short)0, nbytes, 0x00020000);
-    const uint32_t m0v = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(LDS_AS void*)(lds + pad_off));
-    const uint32_t off = (uint32_t)((half * 64 + lane) * 128);
-    uint32_t keep;
-    asm volatile(
-        "s_mov_b32 %0, m0\n\t"
-        "s_mov_b32 m0, %3\n\t"
-        "s_nop 0\n\t"
-        "buffer_load_dword %1, %2, 0 offen lds\n\t"
-        "s_mov_b32 m0, %0"
-        : "=&s"(keep)
-        : "v"(off), "s"(rs), "s"(m0v)
-        : "memory");
-}
-
 // stage one 64-row tile: 16 LDS-DMA pieces of 1 KiB, two per wave; rows past N read as zero (buffer bounds)
 __device__ __forceinline__ void stage(char* lds, int slot, const char* X, int64_t row0, int64_t N,
                                       const uint32_t (&voff)[2], int wave) {
@@ -176,11 +153,11 @@ __global__ __launch_bounds__(512) void kmeans_v7_kernel(const __bf16* __restrict
                                                         int64_t ntiles, int64_t per) {
     using PL = Plan<KB>;
     constexpr int NBUF = PL::NBUF, AHEAD = PL::AHEAD, OHB = PL::OHB, OFF_OH = PL::OFF_OH, OFF_CNT = PL::OFF_CNT;
-    // VAR 0: all 8 waves stage 2 pieces per tile.  VAR 1: the accumulate waves stage all 16 pieces (4 each), so
-    // the distance waves — the critical role — carry no LDS-DMA issue cost and no vmcnt waits.  VAR 2: VAR 1 +
-    // distance waves 0/1 touch tile i + AHEAD + PD into L2 (PD = 3).
-    constexpr int PD = 3;
-    constexpr bool ACC_DMA = VAR >= 1;      // VAR 3: VAR 1 + s_setprio 1 on the distance waves
+    // VAR 0: all 8 waves stage 2 pieces per tile.  VAR 1 (default): the accumulate waves stage all 16 pieces
+    // (4 each), so the distance waves — the critical role — carry no LDS-DMA issue cost and no vmcnt waits.
+    // (Measured and dropped, profiles/kmeans_r2_session5.txt: an L2 touch of tile i+AHEAD+3, s_setprio on the
+    // distance waves, a pairwise-tree argmax, reading tile i+1's distance fragments after barrier i.)
+    constexpr bool ACC_DMA = VAR >= 1;
     __shared__ __attribute__((aligned(16))) char lds[PL::LDS_BYTES];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -208,9 +185,6 @@ __global__ __launch_bounds__(512) void kmeans_v7_kernel(const __bf16* __restrict
     if (MODE != COMPUTE_ONLY && dma_wave)
         for (int s = 0; s < AHEAD; ++s)
             if (s < my_ntiles) stage_tile(s, s);
-    if (VAR == 2 && MODE != COMPUTE_ONLY && wave < 2)
-        for (int s = AHEAD; s < AHEAD + PD; ++s)
-            if (s < my_ntiles) touch_l2(lds, PL::OFF_PAD + 256 * wave, X, (tbase + s) * TR, N, wave, lane);
     {
         for (int e = tid * 16; e < 2 * OHB + 128 * 4; e += 512 * 16)
             *reinterpret_cast<f32x4*>(lds + OFF_OH + e) = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -230,13 +204,10 @@ __global__ __launch_bounds__(512) void kmeans_v7_kernel(const __bf16* __restrict
         barrier_lds();
         if (MODE != COMPUTE_ONLY && dma_wave && i + AHEAD < my_ntiles)
             stage_tile((int)((i + AHEAD) % NBUF), i + AHEAD);
-        if (VAR == 2 && MODE != COMPUTE_ONLY && wave < 2 && i + AHEAD + PD < my_ntiles)
-            touch_l2(lds, PL::OFF_PAD + 256 * wave, X, (tbase + i + AHEAD + PD) * TR, N, wave, lane);
     };
 
     if (wave < 4) {
         // ------------------------------ distance / argmax role ------------------------------
-        if (VAR == 3) __builtin_amdgcn_s_setprio(1);
         const int myrow = 16 * wave + li;
         bf16x8 cf[KB][4];
         f32x4 nin[KB];
@@ -359,7 +330,6 @@ __global__ __launch_bounds__(512) void kmeans_v7_kernel(const __bf16* __restrict
     }
     if (MODE != LOAD_ONLY && tid < 128)
         slab_cnt[(int64_t)blockIdx.x * 128 + tid] = tid < 16 * KB ? (float)cnt[tid] : 0.f;
-    if (VAR == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 template <int KB, int VAR>
@@ -378,19 +348,14 @@ hipError_t launch_kb_var(int mode, dim3 grid, hipStream_t st, const __bf16* X, i
     return hipGetLastError();
 }
 
-// mode bits 0-1: 0 full, 1 load only, 2 compute only; bits 4-5: variant (VAR, see the kernel); the default
+// mode bits 0-1: 0 full, 1 load only, 2 compute only; bit 4: variant (VAR, see the kernel); the default
 // (mode < 16 from the wrapper) is VAR 1: 5.80-5.91 -> 5.50-5.54 ms at k = 100 (profiles/kmeans_r2_session5.txt)
 template <int KB>
 hipError_t launch_kb(int mode, dim3 grid, hipStream_t st, const __bf16* X, int64_t N, const __bf16* C,
                      const float* ninit, float* slab, float* slab_cnt, int* assign_out, int64_t ntiles,
                      int64_t per) {
-    const int var = (mode >> 4) & 3;
-    if (var == 3)
-        return launch_kb_var<KB, 3>(mode & 3, grid, st, X, N, C, ninit, slab, slab_cnt, assign_out, ntiles, per);
-    if (var == 1)
+    if ((mode >> 4) & 1)
         return launch_kb_var<KB, 1>(mode & 3, grid, st, X, N, C, ninit, slab, slab_cnt, assign_out, ntiles, per);
-    if (var == 2)
-        return launch_kb_var<KB, 2>(mode & 3, grid, st, X, N, C, ninit, slab, slab_cnt, assign_out, ntiles, per);
     return launch_kb_var<KB, 0>(mode & 3, grid, st, X, N, C, ninit, slab, slab_cnt, assign_out, ntiles, per);
 }
 

@@ -76,8 +76,6 @@ def prepare_centroids(C: torch.Tensor, device) -> Tuple[torch.Tensor, torch.Tens
 KERNEL_VERSIONS = ("v7",)
 # v7 variant (csrc/kmeans_v7.hip VAR): 0 = all 8 waves stage the tile ring; 1 (default) = the accumulate waves
 # stage it all, so the distance waves (the critical role) carry no LDS-DMA issue cost or vmcnt waits
-# (-4..5 %); 2 = 1 + an L2 touch of the tile 3 iterations past the ring (slower); 3 = 1 + s_setprio on the
-# distance waves
 V7_VAR = int(__import__("os").environ.get("ALINK_KMEANS_V7_VAR", "1"))
 DEFAULT_KERNEL = "v7"
 
