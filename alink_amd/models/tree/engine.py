@@ -149,6 +149,15 @@ class TreeBuilder:
         self.is_cat = torch.tensor(data.is_cat, dtype=torch.bool, device=self.dev)
         self.nbins = torch.tensor(data.nbins, dtype=torch.long, device=self.dev)
         self.hist_dtype = torch.float32 if data.bins.is_cuda else torch.float64
+        # feature-parallel histograms (reference ConstructLocalBin / CalBestSplit split the feature space across
+        # tasks): GBDT on continuous features over P > 1 ranks reduce-SCATTERS every histogram by feature block
+        # (each rank receives 1/P of it instead of the full all-reduce), searches its block, and only the [m, F]
+        # best gains / bins and the chosen feature's [B, S] row per node are exchanged afterwards
+        ws = comm.get_world_size()
+        self.fshard = (not local and ws > 1 and cfg.kind == "gbdt" and not any(data.is_cat)
+                       and __import__("os").environ.get("ALINK_GBDT_FEATURE_SHARD", "1") == "1")
+        self.Fb = -(-self.F // ws) if self.fshard else self.F          # features per rank (padded)
+        self.f_lo = comm.get_rank() * self.Fb if self.fshard else 0
 
     # -------------------------------------------------------------------------------------------
     def _hist_cols(self, S: int) -> List[int]:
@@ -163,7 +172,15 @@ class TreeBuilder:
         cols = self._hist_cols(stats.shape[1])
         sub = stats if len(cols) == stats.shape[1] else stats[:, cols].contiguous()
         H = tops.histogram(self.d.bins, slot, sub, nslots, self.B)
-        if not self.local:
+        if self.fshard:
+            # [slots, F, B, S] -> feature-major, pad F to P * Fb, reduce-scatter -> this rank's [slots, Fb, B, S]
+            ws = comm.get_world_size()
+            Ht = H.transpose(0, 1)
+            if ws * self.Fb != self.F:
+                Ht = torch.cat([Ht, torch.zeros((ws * self.Fb - self.F,) + tuple(Ht.shape[1:]), dtype=H.dtype,
+                                                device=H.device)])
+            H = comm.reduce_scatter(Ht.contiguous(), "sum").transpose(0, 1).contiguous()
+        elif not self.local:
             comm.all_reduce(H, "sum")
         if len(cols) != stats.shape[1]:
             full = torch.zeros(H.shape[:-1] + (stats.shape[1],), dtype=H.dtype, device=H.device)
@@ -256,6 +273,65 @@ class TreeBuilder:
         else:
             accept = gbest > 0
         return gbest, fbest, jbest, mbest, accept, perm
+
+    def _feature_gains_gbdt(self, Hn):
+        """Per-(node, feature) best gain and bin of GBDT binary splits on continuous features: K8 on the GPU,
+        the same scan in torch elsewhere.  Hn [m, Fx, B, S] -> (gain [m, Fx] float64, best_j [m, Fx])."""
+        cfg = self.cfg
+        m, Fx, B, S = Hn.shape
+        if Hn.is_cuda and tops.gpu_kernels_ok():
+            gain, best_j = tops.gbdt_split(Hn.to(torch.float32), cfg.min_samples_per_leaf,
+                                           cfg.min_sum_hessian_per_leaf)
+            return gain.to(torch.float64), best_j.to(torch.int64)
+        Hv = Hn[:, :, :B - 1, :]
+        Hmiss = Hn[:, :, B - 1, :]
+        L = torch.cumsum(Hv, dim=2)
+        T = L[:, :, -1, :] + Hmiss
+        R = T[:, :, None, :] - L
+        gain = _binary_gain(cfg, T[:, :, None, :].expand_as(L), L, R)
+        HT = T[..., 2][:, :, None]
+        HL, HR = L[..., 2], T[..., 2][:, :, None] - L[..., 2]
+        cT = _count(cfg, T)[:, :, None]
+        cL = _count(cfg, L)
+        ratio = HL / torch.where(HT < 1e-6, torch.ones_like(HT), HT)
+        ok = (HT >= 1e-6) & (ratio >= 1e-7) & (ratio <= 1.0 - 1e-7)
+        ok &= (cL >= cfg.min_samples_per_leaf) & (cT - cL >= cfg.min_samples_per_leaf)
+        ok &= (HL >= cfg.min_sum_hessian_per_leaf) & (HR >= cfg.min_sum_hessian_per_leaf)
+        gain = torch.where(ok, gain, torch.full_like(gain, NEG))
+        g, j = gain.max(dim=2)
+        return g, j
+
+    SHARDED_SEARCHES = 0
+
+    def _search_sharded(self, Hn, feat_order, feat_ok):
+        """Feature-sharded split search: this rank scans its feature block, the [m, F] gains / bins of all
+        blocks are all-gathered (small), and every rank picks the same best feature per node in ``feat_order``
+        (identical tie-breaking to the replicated search).  Returns also the chosen features' [m, B, S]
+        histogram rows, all-reduced from their owners."""
+        cfg = self.cfg
+        m = Hn.shape[0]
+        ws = comm.get_world_size()
+        TreeBuilder.SHARDED_SEARCHES += 1
+        g_loc, j_loc = self._feature_gains_gbdt(Hn)                          # [m, Fb]
+        packed = torch.stack([g_loc, j_loc.to(torch.float64)], 0).contiguous()  # [2, m, Fb]
+        allp = comm.all_gather_tensor(packed.reshape(1, 2, m, self.Fb).to(comm.collective_device()))
+        allp = allp.to(Hn.device).reshape(ws, 2, m, self.Fb).permute(1, 2, 0, 3).reshape(2, m, ws * self.Fb)
+        gain, best_j = allp[0][:, :self.F], allp[1][:, :self.F].to(torch.int64)
+        gain = torch.where(feat_ok, gain, torch.full_like(gain, NEG))
+        ordered = torch.gather(gain, 1, feat_order)
+        gbest, pos = ordered.max(dim=1)
+        fbest = torch.gather(feat_order, 1, pos[:, None])[:, 0]
+        jbest = torch.gather(best_j, 1, fbest[:, None])[:, 0]
+        accept = gbest > cfg.min_info_gain + 1e-6
+        # chosen feature's histogram row per node: owners contribute, everyone else adds zeros
+        loc = fbest - self.f_lo
+        mine = (loc >= 0) & (loc < self.Fb)
+        rows = torch.zeros((m,) + tuple(Hn.shape[2:]), dtype=torch.float64, device=Hn.device)
+        if bool(mine.any()):
+            idx = torch.nonzero(mine).reshape(-1)
+            rows[idx] = Hn[idx, loc[idx]].to(torch.float64)
+        comm.all_reduce(rows, "sum")
+        return gbest, fbest, jbest, accept, rows
 
     def _search_gbdt_hip(self, Hn, feat_order, feat_ok):
         """K8 on the GPU (``ops/csrc/tree_split.hip``): one wave per (node, feature) scans the bins; only the
@@ -454,12 +530,18 @@ class TreeBuilder:
                         pf = level[i].order
                         order[r_] = torch.as_tensor(pf, device=dev)
                         ok[r_, torch.as_tensor(pf[:k], device=dev)] = True
-                gbest, fbest, jbest, mbest, accept, perm = self._search(Hn, order, ok)
+                if self.fshard:
+                    gbest, fbest, jbest, accept, rows_t = self._search_sharded(Hn, order, ok)
+                    mbest = torch.zeros(m, dtype=torch.bool, device=dev)
+                    rows_host = rows_t.cpu().numpy()                                     # [m, B, S]
+                    perm_host = np.broadcast_to(np.arange(B - 1), (m, B - 1))
+                else:
+                    gbest, fbest, jbest, mbest, accept, perm = self._search(Hn, order, ok)
+                    rows_host = Hn[torch.arange(m, device=dev), fbest].cpu().numpy()      # [m, B, S]
+                    perm_host = perm[torch.arange(m, device=dev), fbest].cpu().numpy()    # [m, B-1]
                 acc = accept.cpu().numpy()
                 fb, jb, mb, gb = (fbest.cpu().numpy(), jbest.cpu().numpy(), mbest.cpu().numpy(),
                                   gbest.cpu().numpy())
-                rows_host = Hn[torch.arange(m, device=dev), fbest].cpu().numpy()      # [m, B, S]
-                perm_host = perm[torch.arange(m, device=dev), fbest].cpu().numpy()    # [m, B-1]
                 for r_, i in enumerate(cand):
                     if acc[r_]:
                         splits[i] = self._materialise(rows_host[r_], int(fb[r_]), int(jb[r_]), bool(mb[r_]),

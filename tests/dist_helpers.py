@@ -82,6 +82,26 @@ def scenario_gbdt(out):
     out["model"] = [list(r) for r in m.collect()]
 
 
+def scenario_gbdt_wide(out):
+    """7 continuous features (not a multiple of the world size): feature-sharded histograms with a padded block."""
+    import numpy as np
+    import pandas as pd
+    from alink_amd import useLocalEnv, BatchOperator, GbdtTrainBatchOp
+    from alink_amd.models.tree.engine import TreeBuilder
+    rng = np.random.default_rng(11)
+    X = rng.normal(size=(900, 7))
+    y = (X @ np.array([1.0, -2.0, 0.5, 0.0, 1.5, -0.7, 0.3]) + 0.3 * np.sin(3 * X[:, 3]) > 0).astype(int)
+    df = pd.DataFrame({f"x{i}": X[:, i] for i in range(7)})
+    df["y"] = y
+    useLocalEnv(1)
+    src = BatchOperator.fromDataframe(df, schemaStr=", ".join(f"x{i} double" for i in range(7)) + ", y int")
+    before = TreeBuilder.SHARDED_SEARCHES
+    m = GbdtTrainBatchOp().setFeatureCols([f"x{i}" for i in range(7)]).setLabelCol("y").setNumTrees(4) \
+        .setMinSamplesPerLeaf(5).setMaxDepth(5).linkFrom(src)
+    out["model"] = [list(r) for r in m.collect()]
+    out["sharded"] = TreeBuilder.SHARDED_SEARCHES - before
+
+
 def scenario_rf(out):
     from alink_amd import useLocalEnv, BatchOperator, RandomForestTrainBatchOp
     df = _data_frame()

@@ -78,7 +78,7 @@ def _tree_nodes(model_rows):
     return out
 
 
-@pytest.mark.parametrize("scenario", ["gbdt", "rf", "rf_parallel", "rf_sampled"])
+@pytest.mark.parametrize("scenario", ["gbdt", "gbdt_wide", "rf", "rf_parallel", "rf_sampled"])
 def test_trees_two_processes_equal_single(tmp_path, scenario):
     """Histogram all-reduce over 2 ranks (gbdt, rf_parallel) and tree-parallel forests (rf, rf_sampled: each rank
     grows its own trees on the all-gathered bins) give the same trees as one rank."""
@@ -89,6 +89,22 @@ def test_trees_two_processes_equal_single(tmp_path, scenario):
     assert len(one) == len(t2)
     for a, b in zip(one, t2):
         assert a["id"] == b["id"] and a.get("nextIds") == b.get("nextIds")
+        assert a["node"]["featureIndex"] == b["node"]["featureIndex"]
+        assert a["node"].get("continuousSplit") == pytest.approx(b["node"].get("continuousSplit"))
+        np.testing.assert_allclose(a["node"]["counter"]["distributions"], b["node"]["counter"]["distributions"],
+                                   rtol=1e-5, atol=1e-7)
+
+
+def test_gbdt_feature_sharded_histograms_three_ranks(tmp_path):
+    """GBDT over 3 ranks reduce-scatters histograms by feature block (7 features -> blocks of 3, last padded) and
+    grows the same trees as one rank."""
+    one = _run("gbdt_wide", 1, tmp_path)[0]
+    three = _run("gbdt_wide", 3, tmp_path)
+    assert one["sharded"] == 0 and all(o["sharded"] > 0 for o in three)
+    assert three[0]["model"] == three[1]["model"] == three[2]["model"]
+    ta, tb = _tree_nodes(one["model"]), _tree_nodes(three[0]["model"])
+    assert len(ta) == len(tb)
+    for a, b in zip(ta, tb):
         assert a["node"]["featureIndex"] == b["node"]["featureIndex"]
         assert a["node"].get("continuousSplit") == pytest.approx(b["node"].get("continuousSplit"))
         np.testing.assert_allclose(a["node"]["counter"]["distributions"], b["node"]["counter"]["distributions"],
