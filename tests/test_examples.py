@@ -18,7 +18,8 @@ def _run(name, device, rows, tmp_path, extra=()):
 
 
 @pytest.mark.parametrize("name,rows,check", [("kmeans", 150, "purity:"), ("gbdt", 3000, "AUC:"),
-                                             ("als", 20000, "RMSE:"), ("ftrl", 3000, "final window: AUC")])
+                                             ("als", 20000, "RMSE:"), ("ftrl", 3000, "final window: AUC"),
+                                             ("observability", 5000, "stream predictions: 5000")])
 def test_example_cpu(name, rows, check, tmp_path):
     out = _run(name, "cpu", rows, tmp_path)
     assert check in out
@@ -27,7 +28,8 @@ def test_example_cpu(name, rows, check, tmp_path):
 @pytest.mark.gpu
 @pytest.mark.parametrize("name,rows,check,extra", [("kmeans", 150, "purity:", ()), ("gbdt", 20000, "AUC:", ()),
                                                    ("als", 100000, "RMSE:", ()),
-                                                   ("ftrl", 20000, "final window: AUC", ("--mode", "SHARDED"))])
+                                                   ("ftrl", 20000, "final window: AUC", ("--mode", "SHARDED")),
+                                                   ("observability", 20000, "stream predictions: 20000", ())])
 def test_example_gpu(name, rows, check, extra, tmp_path):
     out = _run(name, "cuda:0", rows, tmp_path, extra)
     assert check in out
