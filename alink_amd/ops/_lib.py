@@ -74,6 +74,7 @@ _EXTRA_SIGNATURES = {
     "alink_kmeans_update": [_c_vp, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp],
     "alink_kmeans_accum_bf16": [_c_vp, _c_i64, _c_int, _c_vp, _c_vp, _c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp],
     "alink_kmeans_accum_kmax": [_c_int],
+    "alink_kmeans_accum_mfma_bf16": [_c_vp, _c_i64, _c_vp, _c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp],
     "alink_linear_grad_wide_f64": [_c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_int, _c_int, _c_d, _c_vp, _c_int, _c_vp,
                                    _c_vp],
     "alink_csr_row_deriv_f64": [_c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_int, _c_d, _c_vp, _c_vp, _c_vp],

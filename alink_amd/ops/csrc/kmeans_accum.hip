@@ -19,6 +19,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "kmeans_tile.h"
+
 namespace {
 
 constexpr int THREADS = 512;
@@ -114,6 +116,169 @@ __global__ __launch_bounds__(256) void kmeans_accum_reduce_kernel(const float* _
     out[e] = acc;
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// MFMA accumulate-by-index (D = 128, k <= 256, unweighted): the v7 kernel's one-hot GEMM role fed by idx instead
+// of a distance pass.  512 threads: waves 0-3 turn the ids of their 16 rows of every 64-row tile into the
+// double-buffered bf16 one-hot image Onehot[c][row] (ids prefetched two tiles ahead; an entry is cleared by the
+// same lane two tiles later) and bump count[c]; waves 4-7 stage the LDS-DMA tile ring (4 pieces each) and run
+// Sum[c][32a..32a+31] += Onehot[c][rows] . X[rows][..] on v_mfma_f32_16x16x32_bf16 with transposed ds_read_tr16
+// B fragments — 2*KB*2 MFMAs per tile per wave instead of one LDS float atomic per (row, dim).
+// Output: slab [grid][k][128] fp32, slab_cnt [grid][k] -> kmeans_accum_reduce_kernel (fixed-order fp64).
+// ---------------------------------------------------------------------------------------------------------------
+template <int KB>
+struct AccPlan {
+    static constexpr int OHB = 16 * KB * kmtile::TR * 2;
+    static constexpr int NBUF_FIT = (kmtile::LDS_CAP - 2 * OHB - 256 * 4) / kmtile::TILE;
+    static constexpr int NBUF = NBUF_FIT > 8 ? 8 : NBUF_FIT;
+    static constexpr int AHEAD = NBUF - 2;
+    static constexpr int OFF_OH = NBUF * kmtile::TILE;
+    static constexpr int OFF_CNT = OFF_OH + 2 * OHB;
+    static constexpr int LDS_BYTES = OFF_CNT + 256 * 4;
+    static_assert(LDS_BYTES <= kmtile::LDS_CAP && AHEAD >= 3 && AHEAD <= 6, "LDS plan");
+};
+
+__device__ __forceinline__ void wait_tile4_acc(int younger) { kmtile::wait_tile4(younger); }
+
+template <int KB>
+__global__ __launch_bounds__(512) void kmeans_accum_mfma_kernel(const __bf16* __restrict__ Xp, int64_t N,
+                                                                const int* __restrict__ idx, int k,
+                                                                float* __restrict__ slab,
+                                                                float* __restrict__ slab_cnt, int64_t ntiles,
+                                                                int64_t per) {
+    using namespace kmtile;
+    using PL = AccPlan<KB>;
+    constexpr int NBUF = PL::NBUF, AHEAD = PL::AHEAD, OHB = PL::OHB, OFF_OH = PL::OFF_OH, OFF_CNT = PL::OFF_CNT;
+    __shared__ __attribute__((aligned(16))) char lds[PL::LDS_BYTES];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int g = lane >> 4;
+    const int li = lane & 15;
+    const char* X = reinterpret_cast<const char*>(Xp);
+    const int64_t tbase = (int64_t)blockIdx.x * per;
+    const int64_t my_ntiles = ntiles > tbase ? (ntiles - tbase < per ? ntiles - tbase : per) : 0;
+    uint32_t voff[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int p = i * 4096 + (tid & 255) * 16;
+        const int row = p >> 8;
+        const int chl = ((p >> 4) & 15) ^ xsw(row);
+        voff[i] = (uint32_t)(row * ROWB + chl * 16);
+    }
+    const bool dma_wave = wave >= 4;
+    if (dma_wave)
+        for (int s = 0; s < AHEAD; ++s)
+            if (s < my_ntiles) stage_np<4>(lds, s, X, (tbase + s) * TR, N, voff, wave - 4);
+    for (int e = tid * 16; e < 2 * OHB + 256 * 4; e += 512 * 16)
+        *reinterpret_cast<f32x4*>(lds + OFF_OH + e) = f32x4{0.f, 0.f, 0.f, 0.f};
+    uint32_t* cnt = reinterpret_cast<uint32_t*>(lds + OFF_CNT);
+    auto pre = [&](int64_t i) {
+        if (dma_wave && i < my_ntiles) {
+            const int64_t younger = my_ntiles - 1 - i;
+            wait_tile4_acc(younger < AHEAD - 1 ? (int)younger : AHEAD - 1);
+        }
+        barrier_lds();
+        if (dma_wave && i + AHEAD < my_ntiles)
+            stage_np<4>(lds, (int)((i + AHEAD) % NBUF), X, (tbase + i + AHEAD) * TR, N, voff, wave - 4);
+    };
+    if (wave < 4) {
+        // ------------------------------ index role ------------------------------
+        const int myrow = 16 * wave + li;
+        auto load_id = [&](int64_t t) -> int {
+            const int64_t grow = (tbase + t) * TR + myrow;
+            return (g == 0 && t < my_ntiles && grow < N) ? idx[grow] : -1;
+        };
+        int q0 = load_id(0), q1 = load_id(1);
+        uint32_t prev1 = NONE, prev2 = NONE;
+        for (int64_t i = 0; i <= my_ntiles; ++i) {
+            pre(i);
+            if (i >= my_ntiles) continue;
+            const int c = q0;
+            q0 = q1;
+            q1 = load_id(i + 2);
+            if (g == 0) {
+                uint16_t* oh = reinterpret_cast<uint16_t*>(lds + OFF_OH + (int)(i & 1) * OHB);
+                if (prev2 != NONE) oh[ohoff((int)prev2, myrow) >> 1] = 0;
+                prev2 = prev1;
+                prev1 = NONE;
+                if (c >= 0 && c < k) {
+                    oh[ohoff(c, myrow) >> 1] = 0x3F80;     // bf16 1.0
+                    __hip_atomic_fetch_add(cnt + c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    prev1 = (uint32_t)c;
+                }
+            }
+        }
+        barrier_lds();
+    } else {
+        // ------------------------------ one-hot accumulate role (as kmeans_v7.hip) ------------------------------
+        const int a = wave - 4;
+        const uint32_t lbase = (uint32_t)(uintptr_t)(LDS_AS void*)lds;
+        int trl[2][2], trh[2][2];
+        {
+            const int q = li >> 2, p = li & 3;
+#pragma unroll
+            for (int d = 0; d < 2; ++d)
+#pragma unroll
+                for (int s2 = 0; s2 < 2; ++s2) {
+                    const int ch = 2 * (2 * a + d) + (p >> 1);
+                    trl[d][s2] = xoff(32 * s2 + 8 * g + q, ch) + 8 * (p & 1);
+                    trh[d][s2] = xoff(32 * s2 + 8 * g + q + 4, ch) + 8 * (p & 1);
+                }
+        }
+        f32x4 sums[KB][2];
+#pragma unroll
+        for (int b = 0; b < KB; ++b)
+#pragma unroll
+            for (int d = 0; d < 2; ++d) sums[b][d] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int64_t i = 0; i <= my_ntiles; ++i) {
+            pre(i);
+            if (i == 0) continue;
+            const int xt = (int)((i - 1) % NBUF) * TILE;
+            const char* oh = lds + OFF_OH + (int)((i - 1) & 1) * OHB;
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) {
+                bf16x8 bx[2];
+#pragma unroll
+                for (int d = 0; d < 2; ++d) {
+                    const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+                        (LDS_AS bf16x4*)(uintptr_t)(lbase + xt + trl[d][s2]));
+                    const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+                        (LDS_AS bf16x4*)(uintptr_t)(lbase + xt + trh[d][s2]));
+                    bx[d] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                }
+#pragma unroll
+                for (int b = 0; b < KB; ++b) {
+                    const int c = 16 * b + li;
+                    const bf16x8 oa = *reinterpret_cast<const bf16x8*>(
+                        oh + c * (TR * 2) + 16 * ((4 * s2 + g) ^ ((c >> 1) & 7)));
+#pragma unroll
+                    for (int d = 0; d < 2; ++d)
+                        sums[b][d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(oa, bx[d], sums[b][d], 0, 0, 0);
+                }
+            }
+        }
+        barrier_lds();
+        float* S = slab + (int64_t)blockIdx.x * k * D;
+#pragma unroll
+        for (int b = 0; b < KB; ++b)
+#pragma unroll
+            for (int d = 0; d < 2; ++d)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int c = 16 * b + 4 * g + r;
+                    if (c < k) S[(int64_t)c * D + 16 * (2 * a + d) + li] = sums[b][d][r];
+                }
+    }
+    for (int c = tid; c < k; c += 512) slab_cnt[(int64_t)blockIdx.x * k + c] = (float)cnt[c];
+}
+
+template <int KB>
+void launch_acc_mfma(dim3 grid, hipStream_t st, const __bf16* X, int64_t N, const int* idx, int k, float* slab,
+                     float* slab_cnt, int64_t ntiles, int64_t per) {
+    hipLaunchKernelGGL(kmeans_accum_mfma_kernel<KB>, grid, dim3(512), 0, st, X, N, idx, k, slab, slab_cnt, ntiles,
+                       per);
+}
+
 }  // namespace
 
 extern "C" {
@@ -152,6 +317,32 @@ int alink_kmeans_accum_bf16(const void* X, int64_t N, int D, const int* idx, con
     const int64_t total = (int64_t)k * (D + 1);
     hipLaunchKernelGGL(kmeans_accum_reduce_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, slab,
                        slab_cnt, nchunk, k, D, out);
+    return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+// MFMA accumulate-by-index for D = 128, k <= 256 (unweighted).  Returns the number of workgroups used through
+// the slab layout contract: slab [grid_used][k][128], slab_cnt [grid_used][k] (size them for `grid`).
+int alink_kmeans_accum_mfma_bf16(const void* X, int64_t N, const int* idx, int k, int grid, float* slab,
+                                 float* slab_cnt, double* out, void* stream) {
+    if (N <= 0 || k < 1 || k > 256 || grid <= 0) return 1;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const int64_t ntiles = (N + kmtile::TR - 1) / kmtile::TR;
+    if (grid > ntiles) grid = (int)ntiles;
+    const int64_t per = (ntiles + grid - 1) / grid;
+    const int g2 = (int)((ntiles + per - 1) / per);
+    const __bf16* Xb = (const __bf16*)X;
+    switch ((k + 15) / 16) {
+#define ACASE(V) \
+        case V: launch_acc_mfma<V>(dim3(g2), st, Xb, N, idx, k, slab, slab_cnt, ntiles, per); break;
+        ACASE(1) ACASE(2) ACASE(3) ACASE(4) ACASE(5) ACASE(6) ACASE(7) ACASE(8) ACASE(9) ACASE(10) ACASE(11)
+        ACASE(12) ACASE(13) ACASE(14) ACASE(15)
+#undef ACASE
+        default: launch_acc_mfma<16>(dim3(g2), st, Xb, N, idx, k, slab, slab_cnt, ntiles, per); break;
+    }
+    if (hipGetLastError() != hipSuccess) return 2;
+    const int64_t total = (int64_t)k * 129;
+    hipLaunchKernelGGL(kmeans_accum_reduce_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, slab,
+                       slab_cnt, g2, k, 128, out);
     return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 

@@ -8,8 +8,8 @@ all-reduce.
 * GPU, bf16 rows, d == 128, k <= 128, unweighted: one persistent MFMA kernel (``csrc/kmeans_v7.hip``) + an
   fp64 fixed-order slab reduction (``csrc/kmeans_common.hip``, deterministic).
 * GPU, bf16 rows, d in {64, 128, 256}, k <= 256 (512 at d = 64), optionally weighted: two passes — the MFMA
-  nearest-centroid kernel (``csrc/kmeans_nearest.hip``) then the LDS accumulate-by-index kernel
-  (``csrc/kmeans_accum.hip``), again with a fixed-order fp64 reduction.
+  nearest-centroid kernel (``csrc/kmeans_nearest.hip``) then accumulate-by-index (``csrc/kmeans_accum.hip``:
+  the MFMA one-hot GEMM for unweighted d = 128, LDS float atomics otherwise), with a fixed-order fp64 reduction.
 * anything else: chunked PyTorch path (fp64 on CPU; on GPU fp32 GEMM of the same bf16-rounded centroids).
 """
 from __future__ import annotations
@@ -243,6 +243,21 @@ def accumulate_by_index_hip(X: torch.Tensor, idx: torch.Tensor, k: int,
         w = weights.to(device=dev, dtype=torch.float32).contiguous()
         if w.numel() != n:
             raise ValueError("weights length mismatch")
+    if d == HIP_D and w is None and k <= 256:
+        # MFMA one-hot GEMM fed by idx (csrc/kmeans_accum.hip kmeans_accum_mfma_kernel)
+        grid = _num_cus(dev)
+        key = (dev.index, grid, k, d, "mfma")
+        if key not in _ACC:
+            _ACC.clear()
+            _ACC[key] = (torch.empty(grid * k * d, dtype=torch.float32, device=dev),
+                         torch.empty(grid * k, dtype=torch.float32, device=dev))
+        slab, slab_cnt = _ACC[key]
+        out = torch.empty((k, d + 1), dtype=torch.float64, device=dev)
+        rc = L.alink_kmeans_accum_mfma_bf16(X.data_ptr(), n, idx.contiguous().data_ptr(), k, grid, slab.data_ptr(),
+                                            slab_cnt.data_ptr(), out.data_ptr(), _lib.stream_ptr(dev))
+        if rc != 0:
+            raise RuntimeError(f"alink_kmeans_accum_mfma_bf16 failed: {rc}")
+        return out
     nchunk = max(1, min(_num_cus(dev), (n + 4095) // 4096))
     key = (dev.index, nchunk, k, d)
     if key not in _ACC:
