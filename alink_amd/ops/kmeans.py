@@ -243,6 +243,27 @@ def accumulate_by_index_hip(X: torch.Tensor, idx: torch.Tensor, k: int,
         w = weights.to(device=dev, dtype=torch.float32).contiguous()
         if w.numel() != n:
             raise ValueError("weights length mismatch")
+    if d == HIP_D // 2 and w is None and k <= 256 and X.is_contiguous() and n >= 2:
+        # d = 64 on the d = 128 MFMA kernel: view row v = (row 2v | row 2v+1); pass A one-hot by idx[2v] keeps
+        # dims 0..63, pass B by idx[2v+1] keeps dims 64..127 — two reads of X at MFMA speed instead of one pass of
+        # LDS float atomics (an odd last row is added on the host side)
+        m = n // 2
+        Xv = X[:2 * m].view(m, HIP_D)
+        outA = accumulate_by_index_hip(Xv, idx[0:2 * m:2].contiguous(), k)
+        outB = accumulate_by_index_hip(Xv, idx[1:2 * m:2].contiguous(), k)
+        out = torch.cat([outA[:, :d] + outB[:, d:HIP_D], outA[:, HIP_D:] + outB[:, HIP_D:]], 1)
+        if n % 2:
+            c = int(idx[n - 1].item())
+            if 0 <= c < k:
+                out[c, :d] += X[n - 1].to(torch.float64)
+                out[c, d] += 1.0
+        return out
+    if d == 2 * HIP_D and w is None and k <= 128 and X.is_contiguous():
+        # d = 256 on the d = 128 MFMA kernel: row r = view rows 2r (dims 0..127) and 2r+1 (dims 128..255), the
+        # second half accumulated under virtual centroid c + k (same bytes read, one-hot GEMM of 2k rows)
+        idx2 = torch.stack([idx, torch.where(idx >= 0, idx + k, idx)], 1).reshape(-1).contiguous()
+        out2 = accumulate_by_index_hip(X.view(2 * n, HIP_D), idx2, 2 * k)
+        return torch.cat([out2[:k, :HIP_D], out2[k:, :HIP_D], out2[:k, HIP_D:]], 1)
     if d == HIP_D and w is None and k <= 256:
         # MFMA one-hot GEMM fed by idx (csrc/kmeans_accum.hip kmeans_accum_mfma_kernel)
         grid = _num_cus(dev)
