@@ -22,6 +22,7 @@ from ...common.model.converter import RichModelDataConverter, SimpleModelDataCon
 from ...common.params import Params
 from ...common.table import Column, MTable
 from ...common.types import AlinkType, TableSchema, Types
+from ...ops import elementwise as ew
 from ..common.features import extract_features
 from ..statistics.summary import TableSummary, table_summary, vector_summary
 
@@ -157,6 +158,8 @@ class _ColumnScalerMapper(ModelMapper):
 class StandardScalerModelMapper(_ColumnScalerMapper):
     def _transform(self, j, v, nulls):
         mean, std = float(self.model.arrays[0][j]), float(self.model.arrays[1][j])
+        if v.is_cuda:   # K27 fused transform (one pass, bit-identical)
+            return ew.col_transform(v, "standard", [mean], [std])
         return (v - mean) / std if std > 0 else torch.zeros_like(v)
 
 
@@ -164,6 +167,8 @@ class MinMaxScalerModelMapper(_ColumnScalerMapper):
     def _transform(self, j, v, nulls):
         lo, hi = float(self.model.meta.get("min")), float(self.model.meta.get("max"))
         emin, emax = float(self.model.arrays[0][j]), float(self.model.arrays[1][j])
+        if v.is_cuda:
+            return ew.col_transform(v, "minmax", [emin], [emax], lo, hi)
         if emin != emax:
             return (v - emin) / (emax - emin) * (hi - lo) + lo
         return torch.full_like(v, 0.5 * (hi + lo))
@@ -172,6 +177,8 @@ class MinMaxScalerModelMapper(_ColumnScalerMapper):
 class MaxAbsScalerModelMapper(_ColumnScalerMapper):
     def _transform(self, j, v, nulls):
         m = float(self.model.arrays[0][j])
+        if v.is_cuda:
+            return ew.col_transform(v, "maxabs", [m])
         return v if m == 0 else v / m
 
 
@@ -267,6 +274,11 @@ class VectorScalerModelMapper(ModelMapper):
         m = self.model
         a = [torch.as_tensor(x, dtype=torch.float64, device=X.device) if x is not None else None for x in m.arrays]
         d = X.shape[1]
+        if X.is_cuda and m.kind in ("standard", "minmax", "maxabs"):   # K27: one fused pass over the block
+            if m.kind == "minmax":
+                return ew.col_transform(X, "minmax", a[0][:d], a[1][:d], float(m.meta.get("min")),
+                                        float(m.meta.get("max")))
+            return ew.col_transform(X, m.kind, a[0][:d], a[1][:d] if m.kind == "standard" else None)
         if m.kind == "standard":
             mean, std = a[0][:d], a[1][:d]
             return torch.where(std > 0, (X - mean) / torch.where(std > 0, std, torch.ones_like(std)),
@@ -285,7 +297,8 @@ class VectorScalerModelMapper(ModelMapper):
     def _map_columns(self, mt):
         c = mt.col(self.vc)
         if isinstance(c.values, torch.Tensor) and c.values.dim() == 2:
-            return [Column(self._scale(c.values.double()))]
+            X = c.values
+            return [Column(self._scale(X if X.is_cuda and X.dtype == torch.float32 else X.double()))]
         out = []
         for v in c.to_list():
             if v is None:

@@ -24,6 +24,7 @@ from ...common.jrandom import JavaRandom
 from ...common.params import Params
 from ...common.table import MTable
 from ...common.types import TableSchema, Types
+from ...ops import elementwise as ew
 from ...parallel import comm
 from .data import build_bins, categorical_cols, distinct_labels, numeric_column
 from .engine import SplitConfig, TreeBuilder
@@ -142,23 +143,14 @@ def train_gbdt(mt: MTable, params: Params, env, algo_type: int) -> Tuple[List[tu
             torch.ones(n, dtype=torch.bool, device=dev)
         if feat_ratio < 1.0:   # InitialTrainningBuffer / Split draw a feature subset for every tree
             fmask = feat_rng.random(F) < feat_ratio
-        if algo_type == 1:
-            p = torch.sigmoid(pred.double())
-            g = (p - y.double()).float()
-            h = (p * (1.0 - p)).float()
-        else:
-            g = pred - y
-            h = torch.ones_like(g)
-        g, h = g * w, h * w
-        stats = torch.stack([g * g, g, h, torch.ones_like(g)], dim=1)
+        # K6: {g*g, g, h, 1} row records in one fused pass (logistic g/h in fp64, weights applied in fp32)
+        stats = ew.gbdt_grad_stats(pred, y, w, 1 if algo_type == 1 else 0)
         root, codes, leaves = builder.build(stats, sample, fmask)
         roots.append(root)
         # Split.java: predBuf = (float) (curPred + leftCounter.sum / leftCounter.weightSum)
         vals = torch.tensor([lf.counter.distributions[0] if lf.counter and lf.counter.distributions else 0.0
                              for lf in leaves] or [0.0], dtype=torch.float64, device=dev)
-        leaf = (-1 - codes.long()).clamp(min=0, max=vals.numel() - 1)
-        inc = torch.where(codes < 0, vals[leaf], torch.zeros_like(vals[leaf]))
-        pred = (pred.double() + inc).float()
+        pred = ew.gbdt_leaf_update(pred, codes.to(torch.int32), vals)
     meta = params.clone()
     meta.set("featureCols", feature_cols).set("labelCol", label_col).set("categoricalCols", cat)
     meta.set("numTrees", num_trees).set("maxDepth", depth).set("algoType", algo_type)
