@@ -21,6 +21,7 @@ from typing import Optional, Tuple
 
 import torch
 
+from ...ops import softmax as softmax_ops
 from ..common.features import FeatureMatrix
 
 __all__ = ["LabeledData", "UnaryLossFunc", "LogLossFunc", "LogisticLossFunc", "SquareLossFunc", "HingeLossFunc",
@@ -371,12 +372,9 @@ class SoftmaxObjFunc(OptimObjFunc):
         return torch.exp(eta - lse[:, None])
 
     def grad_sum(self, data, coef):
-        eta = self._eta(data, coef)
-        phi = self._phi(eta)
-        yk = data.y.long()
-        rows = torch.nonzero(yk < self.k1).reshape(-1)
-        phi[rows, yk[rows]] -= 1.0
-        G = data.X.rmm(phi * data.w[:, None], coef.shape[0] // self.k1)  # [m, k1]
+        # K16: w * (softmax - onehot) in one fused pass over the logits (torch formulas on the CPU)
+        R, _ = softmax_ops.softmax_grad(self._eta(data, coef), data.y, data.w)
+        G = data.X.rmm(R, coef.shape[0] // self.k1)  # [m, k1]
         return G.T.reshape(-1)
 
     def hessian_sum(self, data, coef):
@@ -395,17 +393,9 @@ class SoftmaxObjFunc(OptimObjFunc):
     def calc_search_values(self, data, coef, dirv, beta, num_step):
         if not len(data):
             return torch.zeros(num_step + 1, dtype=coef.dtype, device=coef.device)
-        ec = self._eta(data, coef)
-        ed = self._eta(data, dirv) * beta
-        out = []
-        for i in range(num_step + 1):
-            e = ec - i * ed
-            lse = self._logsumexp1(e)
-            yk = data.y.long()
-            lin = torch.where(yk < self.k1, e.gather(1, yk.clamp(max=self.k1 - 1)[:, None])[:, 0],
-                              torch.zeros_like(data.y))
-            out.append(((lse - lin) * data.w).sum())
-        return torch.stack(out)
+        # every trial step's loss from one read of the two logit blocks (K16 search epilogue)
+        return softmax_ops.softmax_search(self._eta(data, coef), self._eta(data, dirv), data.y, data.w, beta,
+                                          num_step + 1)
 
 
 class AftRegObjFunc(OptimObjFunc):
