@@ -30,6 +30,7 @@ from ...common.model.converter import SimpleModelDataConverter
 from ...common.params import Params
 from ...common.table import Column, MTable
 from ...common.types import Types
+from ...ops import gmm as gmm_ops
 from ...parallel import comm
 from ..common.features import extract_features, global_vector_size
 
@@ -113,12 +114,17 @@ def train_gmm(mt: MTable, params: Params, env) -> List[tuple]:
     S = torch.as_tensor(covs, device=dev)
     w = torch.as_tensor(weights, device=dev)
     prev = 0.0
+    # K22: centre once by the global mean, then every E-step is one GEMM for all components plus one fused
+    # log-density / log-sum-exp / responsibility kernel (ops/gmm.py)
+    xs_n = torch.cat([X.sum(0), torch.tensor([float(X.shape[0])], dtype=X.dtype, device=dev)])
+    comm.all_reduce(xs_n, "sum")
+    xbar = xs_n[:d] / xs_n[d].clamp(min=1.0)
+    X0 = X - xbar
     for step in range(1, max_iter + 1):
-        lp = gaussian_logpdf(X, mu, S) + torch.log(w)[None, :]
-        lse = torch.logsumexp(lp, dim=1)
-        R = torch.exp(lp - lse[:, None])
+        Wr, logdet, rank = _root_inv(S)
+        R, lse_sum = gmm_ops.estep(X0, mu - xbar, Wr, logdet, rank, torch.log(w))
         stats = torch.cat([R.sum(0), (R.T @ X).reshape(-1),
-                           torch.einsum("nk,nd,ne->kde", R, X, X).reshape(-1), lse.sum().reshape(1),
+                           torch.einsum("nk,nd,ne->kde", R, X, X).reshape(-1), lse_sum.reshape(1),
                            torch.tensor([float(X.shape[0])], dtype=X.dtype, device=dev)])
         comm.all_reduce(stats, "sum")
         rs = stats[:k]
