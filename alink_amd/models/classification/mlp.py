@@ -21,6 +21,7 @@ from typing import List, Sequence
 import numpy as np
 import torch
 
+from ...ops import mlp as mlp_ops
 from ...common.javafmt import gson_dumps, java_str
 from ...common.jrandom import JavaRandom
 from ...common.linalg import DenseVector
@@ -79,6 +80,9 @@ class MlpObjFunc(OptimObjFunc):
             return self._ce(data, coef)
 
     def grad_sum(self, data, coef):
+        X = data.X.to_dense()
+        if mlp_ops.kernel_supported(X, self.layers):   # K17: explicit backprop, GEMMs + fused HIP epilogues
+            return mlp_ops.mlp_grad(X, data.y, data.w, coef.detach(), self.layers)[0]
         w = coef.detach().clone().requires_grad_(True)
         loss = (self._ce(data, w) * data.w).sum()
         (g,) = torch.autograd.grad(loss, w)

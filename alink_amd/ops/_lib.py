@@ -115,6 +115,9 @@ _EXTRA_SIGNATURES = {
     "alink_softmax_search_f64": [_c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_int, _c_d, _c_int, _c_vp, _c_vp],
     "alink_gmm_grid": [_c_i64],
     "alink_gmm_estep_f64": [_c_vp, _c_i64, _c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp],
+    "alink_softmax_full_grad_f64": [_c_vp, _c_vp, _c_vp, _c_i64, _c_int, _c_vp, _c_vp, _c_vp],
+    "alink_bias_sigmoid_f64": [_c_vp, _c_i64, _c_int, _c_vp, _c_vp],
+    "alink_sigmoid_bwd_f64": [_c_vp, _c_vp, _c_i64, _c_vp],
     "alink_als_gram_f32": [_c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_int, _c_int, _c_f, _c_vp, _c_vp, _c_vp],
 }
 

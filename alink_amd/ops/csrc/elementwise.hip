@@ -1,5 +1,5 @@
 // Fused elementwise kernels on CDNA4 (gfx950 / MI355X): SURVEY §2.13 K6 (GBDT gradient / hessian statistics and
-// the per-tree prediction update) and K27 (scaler / imputer / binarizer transforms of dense column blocks).
+// the per-tree prediction update), K17 (MLP bias + sigmoid forward / sigmoid backward epilogues) and K27 (scaler / imputer / binarizer transforms of dense column blocks).
 //
 // All of these are pure HBM streams: one read of each operand and one write of the result, replacing chains of
 // 5-12 torch elementwise launches (each re-reading and re-writing the whole column).  Arithmetic is done in the
@@ -107,6 +107,27 @@ __global__ __launch_bounds__(TB) void col_transform_kernel(const T* __restrict__
   }
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// K17: MLP hidden-layer epilogues around the hipBLASLt GEMMs
+//   forward:  Z[i, j] = 1 / (1 + exp(-(Z[i, j] + b[j])))      (bias + sigmoid in place)
+//   backward: G[i] *= S[i] (1 - S[i])                           (sigmoid derivative in place)
+// ---------------------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(TB) void bias_sigmoid_kernel(double* __restrict__ Z, int64_t total, int d,
+                                                          const double* __restrict__ b) {
+  for (int64_t e = (int64_t)blockIdx.x * TB + threadIdx.x; e < total; e += (int64_t)gridDim.x * TB) {
+    const double z = Z[e] + b[e % d];
+    Z[e] = 1.0 / (1.0 + exp(-z));
+  }
+}
+
+__global__ __launch_bounds__(TB) void sigmoid_bwd_kernel(double* __restrict__ G, const double* __restrict__ S,
+                                                         int64_t total) {
+  for (int64_t e = (int64_t)blockIdx.x * TB + threadIdx.x; e < total; e += (int64_t)gridDim.x * TB) {
+    const double s = S[e];
+    G[e] = G[e] * (s * (1.0 - s));
+  }
+}
+
 template <typename T>
 hipError_t launch_transform(const void* X, int64_t total, int d, int mode, const double* a, const double* b,
                             double lo, double hi, double* out, hipStream_t s) {
@@ -141,6 +162,21 @@ int alink_gbdt_leaf_update(void* pred, const void* codes, const void* vals, int 
   if (nvals <= 0) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(gbdt_leaf_update_kernel, dim3(grid_for(n)), dim3(TB), 0, (hipStream_t)stream, (float*)pred,
                      (const int32_t*)codes, (const double*)vals, nvals, n);
+  return (int)hipGetLastError();
+}
+
+int alink_bias_sigmoid_f64(void* Z, int64_t n, int d, const void* b, void* stream) {
+  if (n <= 0 || d <= 0) return 0;
+  const int64_t total = n * (int64_t)d;
+  hipLaunchKernelGGL(bias_sigmoid_kernel, dim3(grid_for(total)), dim3(TB), 0, (hipStream_t)stream, (double*)Z, total,
+                     d, (const double*)b);
+  return (int)hipGetLastError();
+}
+
+int alink_sigmoid_bwd_f64(void* G, const void* S, int64_t total, void* stream) {
+  if (total <= 0) return 0;
+  hipLaunchKernelGGL(sigmoid_bwd_kernel, dim3(grid_for(total)), dim3(TB), 0, (hipStream_t)stream, (double*)G,
+                     (const double*)S, total);
   return (int)hipGetLastError();
 }
 

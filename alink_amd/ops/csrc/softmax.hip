@@ -42,20 +42,20 @@ __device__ __forceinline__ void block_sum_store(double v, double* lds, double* d
 }
 
 // log(exp(0) + sum_j exp(e_j)) with the pivot's zero logit included (max-shifted like torch.logsumexp)
-template <int KMAX>
+template <int KMAX, bool PIVOT = true>
 __device__ __forceinline__ double lse_pivot(const double (&e)[KMAX], int k1) {
-  double m = 0.0;
+  double m = PIVOT ? 0.0 : e[0];
 #pragma unroll
   for (int j = 0; j < KMAX; ++j)
     if (j < k1) m = e[j] > m ? e[j] : m;
-  double s = exp(-m);
+  double s = PIVOT ? exp(-m) : 0.0;
 #pragma unroll
   for (int j = 0; j < KMAX; ++j)
     if (j < k1) s += exp(e[j] - m);
   return m + log(s);
 }
 
-template <int KMAX>
+template <int KMAX, bool PIVOT>
 __global__ __launch_bounds__(TB) void softmax_grad_kernel(const double* __restrict__ eta,
                                                           const double* __restrict__ y,
                                                           const double* __restrict__ w, int64_t n, int k1,
@@ -67,7 +67,7 @@ __global__ __launch_bounds__(TB) void softmax_grad_kernel(const double* __restri
     const double* row = eta + i * k1;
 #pragma unroll
     for (int j = 0; j < KMAX; ++j) e[j] = j < k1 ? row[j] : 0.0;
-    const double lse = lse_pivot<KMAX>(e, k1);
+    const double lse = lse_pivot<KMAX, PIVOT>(e, k1);
     const int yk = (int)y[i];
     const double wi = w[i];
     double lin = 0.0;
@@ -150,9 +150,25 @@ int alink_softmax_grad_f64(const void* eta, const void* y, const void* w, int64_
   const double *e = (const double*)eta, *yy = (const double*)y, *ww = (const double*)w;
   double *r = (double*)R, *p = (double*)part;
   if (k1 <= 0) return (int)hipErrorInvalidValue;
-  if (k1 <= 4) hipLaunchKernelGGL(softmax_grad_kernel<4>, grid, block, 0, s, e, yy, ww, n, k1, r, p);
-  else if (k1 <= 16) hipLaunchKernelGGL(softmax_grad_kernel<16>, grid, block, 0, s, e, yy, ww, n, k1, r, p);
-  else if (k1 <= 32) hipLaunchKernelGGL(softmax_grad_kernel<32>, grid, block, 0, s, e, yy, ww, n, k1, r, p);
+  if (k1 <= 4) hipLaunchKernelGGL((softmax_grad_kernel<4, true>), grid, block, 0, s, e, yy, ww, n, k1, r, p);
+  else if (k1 <= 16) hipLaunchKernelGGL((softmax_grad_kernel<16, true>), grid, block, 0, s, e, yy, ww, n, k1, r, p);
+  else if (k1 <= 32) hipLaunchKernelGGL((softmax_grad_kernel<32, true>), grid, block, 0, s, e, yy, ww, n, k1, r, p);
+  else return (int)hipErrorInvalidValue;
+  return (int)hipGetLastError();
+}
+
+// the same without a pivot class (all K logits free, labels in [0, K)): the MLP's softmax cross-entropy output layer
+int alink_softmax_full_grad_f64(const void* z, const void* y, const void* w, int64_t n, int K, void* R, void* part,
+                                void* stream) {
+  if (n <= 0) return 0;
+  const dim3 grid(grid_for(n)), block(TB);
+  hipStream_t s = (hipStream_t)stream;
+  const double *e = (const double*)z, *yy = (const double*)y, *ww = (const double*)w;
+  double *r = (double*)R, *p = (double*)part;
+  if (K <= 0) return (int)hipErrorInvalidValue;
+  if (K <= 4) hipLaunchKernelGGL((softmax_grad_kernel<4, false>), grid, block, 0, s, e, yy, ww, n, K, r, p);
+  else if (K <= 16) hipLaunchKernelGGL((softmax_grad_kernel<16, false>), grid, block, 0, s, e, yy, ww, n, K, r, p);
+  else if (K <= 32) hipLaunchKernelGGL((softmax_grad_kernel<32, false>), grid, block, 0, s, e, yy, ww, n, K, r, p);
   else return (int)hipErrorInvalidValue;
   return (int)hipGetLastError();
 }

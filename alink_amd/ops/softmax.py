@@ -86,3 +86,12 @@ def softmax_search(ec, ed, y, w, beta: float, nsteps: int) -> torch.Tensor:
     if rc != 0:
         raise RuntimeError(f"alink_softmax_search_f64 failed: {rc}")
     return part.sum(0)
+
+
+def softmax_full_grad_torch(z, y, w) -> Tuple[torch.Tensor, torch.Tensor]:
+    """No pivot class: ``w * (softmax(z) - onehot(y))`` and ``sum w (lse - z[y])`` (the MLP output layer)."""
+    lse = torch.logsumexp(z, 1)
+    P = torch.exp(z - lse[:, None])
+    yk = y.long()
+    P[torch.arange(z.shape[0], device=z.device), yk] -= 1.0
+    return P * w[:, None], ((lse - z.gather(1, yk[:, None])[:, 0]) * w).sum()

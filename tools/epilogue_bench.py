@@ -1,9 +1,13 @@
 """Times the fused epilogue kernels (K16 softmax, K22 GMM E-step, K6 GBDT g/h, K27 scaler) against the torch
 chains they replace on one GPU.  Prints one line per case."""
 import math
+import os
+import sys
 import time
 
 import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from alink_amd.models.clustering.gmm import _root_inv
 from alink_amd.ops import elementwise as ew
@@ -61,6 +65,24 @@ def main():
     b = timeit(lambda: ew.col_transform_torch(X, "minmax", lo, hi, 0.0, 1.0))
     print(f"K27 min-max scaler {tuple(X.shape)} fp64: kernel {a:.3f} ms ({X.numel() * 16 / a / 1e9:.2f} TB/s)  "
           f"torch {b:.3f} ms  ({b / a:.1f}x)")
+    del X, pred, yy, ww
+    from alink_amd.ops import mlp as M
+    from alink_amd.models.classification.mlp import mlp_forward, weight_size
+    layers = [64, 128, 64, 10]
+    n = 1_000_000
+    X = torch.randn(n, layers[0], device=dev, dtype=torch.float64, generator=g)
+    y = torch.randint(0, layers[-1], (n,), device=dev, generator=g).double()
+    w = torch.ones(n, device=dev, dtype=torch.float64)
+    coef = torch.randn(weight_size(layers), device=dev, dtype=torch.float64, generator=g) * 0.1
+
+    def autograd_step():
+        wt = coef.clone().requires_grad_(True)
+        P = mlp_forward(X, wt, layers)
+        loss = (-torch.log(P.gather(1, y.long()[:, None])[:, 0].clamp_min(1e-300)) * w).sum()
+        return torch.autograd.grad(loss, wt)[0]
+    a = timeit(lambda: M.mlp_grad(X, y, w, coef, layers))
+    b = timeit(autograd_step)
+    print(f"K17 MLP grad {layers} n={n} fp64: explicit+kernels {a:.3f} ms  autograd {b:.3f} ms  ({b / a:.1f}x)")
 
 
 if __name__ == "__main__":
