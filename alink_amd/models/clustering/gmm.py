@@ -78,6 +78,22 @@ def gaussian_logpdf(X: torch.Tensor, mean: torch.Tensor, cov: torch.Tensor) -> t
     return out
 
 
+def _weighted_syrk(R: torch.Tensor, X: torch.Tensor) -> torch.Tensor:
+    """[k, d, d] = sum_i R[i, k] x_i x_i^T.  On the GPU one [k*d, rows] x [rows, d] hipBLASLt GEMM per row chunk of
+    at most ~1 GiB of (R (x) X) operand; the CPU keeps the einsum."""
+    n, k = R.shape
+    d = X.shape[1]
+    if not X.is_cuda:
+        return torch.einsum("nk,nd,ne->kde", R, X, X)
+    out = torch.zeros((k * d, d), dtype=X.dtype, device=X.device)
+    rows = max(1, min(n, (1 << 30) // (8 * max(1, k * d))))
+    for s in range(0, n, rows):
+        e = min(n, s + rows)
+        A = (R[s:e, :, None] * X[s:e, None, :]).reshape(e - s, k * d)
+        out.addmm_(A.T, X[s:e])
+    return out.reshape(k, d, d)
+
+
 def train_gmm(mt: MTable, params: Params, env) -> List[tuple]:
     dev = env.device
     vcol = params.get("vectorCol")
@@ -124,7 +140,7 @@ def train_gmm(mt: MTable, params: Params, env) -> List[tuple]:
         Wr, logdet, rank = _root_inv(S)
         R, lse_sum = gmm_ops.estep(X0, mu - xbar, Wr, logdet, rank, torch.log(w))
         stats = torch.cat([R.sum(0), (R.T @ X).reshape(-1),
-                           torch.einsum("nk,nd,ne->kde", R, X, X).reshape(-1), lse_sum.reshape(1),
+                           _weighted_syrk(R, X).reshape(-1), lse_sum.reshape(1),
                            torch.tensor([float(X.shape[0])], dtype=X.dtype, device=dev)])
         comm.all_reduce(stats, "sum")
         rs = stats[:k]

@@ -47,3 +47,11 @@ def test_gmm_train_cuda_equals_cpu():
         preds[dev] = [r[-1] for r in GmmPredictBatchOp().setPredictionCol("p").linkFrom(m, src).collect()]
     useLocalEnv(1, device="cpu")
     assert preds["cpu"] == preds["cuda:0"]
+
+
+def test_weighted_syrk_matches_einsum():
+    from alink_amd.models.clustering.gmm import _weighted_syrk
+    g = torch.Generator(device="cuda").manual_seed(11)
+    R = torch.rand(40001, 6, device="cuda", dtype=torch.float64, generator=g)
+    X = torch.randn(40001, 9, device="cuda", dtype=torch.float64, generator=g)
+    torch.testing.assert_close(_weighted_syrk(R, X), torch.einsum("nk,nd,ne->kde", R, X, X), rtol=1e-11, atol=1e-9)
