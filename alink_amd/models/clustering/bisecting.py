@@ -22,6 +22,7 @@ from typing import Dict, List
 import numpy as np
 import torch
 
+from ...ops.gemm import tn_matmul
 from ...common.javafmt import gson_dumps
 from ...common.jrandom import JavaRandom
 from ...common.linalg import DenseVector
@@ -70,7 +71,7 @@ def _summaries(X, node, ids: List[int], cosine: bool):
         vec = Xs / torch.sqrt(norm2)[:, None] if cosine else Xs
         # segment sums as one [m, n] x [n, d + 2] GEMM (few segments: atomics would serialise)
         onehot = torch.nn.functional.one_hot(ps, m).to(X.dtype)
-        stats += onehot.T @ torch.cat([vec, torch.ones_like(norm2)[:, None], norm2[:, None]], 1)
+        stats += tn_matmul(onehot, torch.cat([vec, torch.ones_like(norm2)[:, None], norm2[:, None]], 1))
     comm.all_reduce(stats, "sum")
     out = {}
     S = stats.cpu().numpy()

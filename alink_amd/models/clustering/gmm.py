@@ -23,6 +23,7 @@ from typing import List, Optional
 import numpy as np
 import torch
 
+from ...ops.gemm import tn_matmul
 from ...common.javafmt import gson_dumps
 from ...common.linalg import DenseVector, VectorUtil
 from ...common.mapper import OutputColsHelper, RichModelMapper
@@ -90,7 +91,7 @@ def _weighted_syrk(R: torch.Tensor, X: torch.Tensor) -> torch.Tensor:
     for s in range(0, n, rows):
         e = min(n, s + rows)
         A = (R[s:e, :, None] * X[s:e, None, :]).reshape(e - s, k * d)
-        out.addmm_(A.T, X[s:e])
+        out += tn_matmul(A, X[s:e])
     return out.reshape(k, d, d)
 
 
@@ -139,7 +140,7 @@ def train_gmm(mt: MTable, params: Params, env) -> List[tuple]:
     for step in range(1, max_iter + 1):
         Wr, logdet, rank = _root_inv(S)
         R, lse_sum = gmm_ops.estep(X0, mu - xbar, Wr, logdet, rank, torch.log(w))
-        stats = torch.cat([R.sum(0), (R.T @ X).reshape(-1),
+        stats = torch.cat([R.sum(0), tn_matmul(R, X).reshape(-1),
                            _weighted_syrk(R, X).reshape(-1), lse_sum.reshape(1),
                            torch.tensor([float(X.shape[0])], dtype=X.dtype, device=dev)])
         comm.all_reduce(stats, "sum")

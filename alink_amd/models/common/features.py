@@ -19,6 +19,7 @@ from typing import List, Optional, Sequence, Tuple
 import numpy as np
 import torch
 
+from ...ops.gemm import tn_matmul
 from ...common.linalg import DenseVector, SparseBlock, SparseVector, VectorUtil
 from ...common.table import MTable
 from ...common.types import Types, is_numeric
@@ -122,7 +123,7 @@ class FeatureMatrix:
         """X^T g -> [d]."""
         d = self._ncols if d is None else d
         if self.dense is not None:
-            out = self.dense.T @ g
+            out = tn_matmul(self.dense, g)
             return out if d == self._ncols else torch.nn.functional.pad(out, (0, d - self._ncols))
         out = torch.zeros(d, dtype=g.dtype, device=g.device)
         if self.val.numel() == 0:
@@ -133,7 +134,7 @@ class FeatureMatrix:
         """X^T G for G [n, k] -> [d, k]."""
         d = self._ncols if d is None else d
         if self.dense is not None:
-            out = self.dense.T @ G
+            out = tn_matmul(self.dense, G)
             return out if d == self._ncols else torch.nn.functional.pad(out, (0, 0, 0, d - self._ncols))
         out = torch.zeros((d, G.shape[1]), dtype=G.dtype, device=G.device)
         if self.val.numel() == 0:
@@ -145,10 +146,10 @@ class FeatureMatrix:
         d = self._ncols if d is None else d
         if self.dense is not None:
             Xd = self.dense
-            out = Xd.T @ (Xd * h[:, None])
+            out = tn_matmul(Xd, Xd * h[:, None])
             return out if d == self._ncols else torch.nn.functional.pad(out, (0, d - self._ncols, 0, d - self._ncols))
         D = self.to_dense(d)
-        return D.T @ (D * h[:, None])
+        return tn_matmul(D, D * h[:, None])
 
     # -- transforms --
     def to_dense(self, d: Optional[int] = None) -> torch.Tensor:

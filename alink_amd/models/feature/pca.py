@@ -17,6 +17,7 @@ from typing import List, Optional
 import numpy as np
 import torch
 
+from ...ops.gemm import tn_matmul
 from ...common.javafmt import gson_dumps
 from ...common.linalg import DenseVector, VectorUtil
 from ...common.mapper import ModelMapper, OutputColsHelper, find_col_index
@@ -68,7 +69,7 @@ def train_pca(mt: MTable, params: Params, env) -> List[tuple]:
     if X.shape[1] < d:
         X = torch.nn.functional.pad(X, (0, d - X.shape[1]))
     n = torch.tensor([float(X.shape[0])], dtype=torch.float64, device=X.device)
-    buf = torch.cat([n, X.sum(0), (X * X).sum(0), (X.T @ X).reshape(-1)])
+    buf = torch.cat([n, X.sum(0), (X * X).sum(0), tn_matmul(X, X).reshape(-1)])
     comm.all_reduce(buf, "sum")
     cnt = float(buf[0])
     s = buf[1:1 + d].cpu().numpy()

@@ -19,6 +19,7 @@ from typing import List, Optional, Sequence
 import numpy as np
 import torch
 
+from ...ops.gemm import tn_matmul
 from ...common.javafmt import gson_dumps
 from ...common.mapper import ModelMapper, OutputColsHelper
 from ...common.model import SimpleModelDataConverter
@@ -343,7 +344,7 @@ def _weight_stats(X: torch.Tensor, b: torch.Tensor, w: torch.Tensor) -> np.ndarr
     """All-reduced ``[count, wwSum, G]`` with ``G = [X|1|b]^T diag(w) [X|1|b]`` (one GEMM per rank)."""
     n = X.shape[0]
     Z = torch.cat([X, torch.ones((n, 1), dtype=X.dtype, device=X.device), b[:, None]], 1)
-    G = Z.T @ (Z * w[:, None])
+    G = tn_matmul(Z, Z * w[:, None])
     head = torch.stack([torch.tensor(float(n), dtype=X.dtype, device=X.device), (w * w).sum()])
     buf = torch.cat([head, G.reshape(-1)])
     comm.all_reduce(buf, "sum")

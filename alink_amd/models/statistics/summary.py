@@ -18,6 +18,7 @@ from typing import Any, List, Optional, Sequence
 import numpy as np
 import torch
 
+from ...ops.gemm import tn_matmul
 from ...common.javafmt import gson_dumps
 from ...common.linalg import DenseMatrix, DenseVector, SparseVector, VectorUtil
 from ...common.model.converter import SimpleModelDataConverter
@@ -298,7 +299,7 @@ def _rank_global(v: torch.Tensor) -> torch.Tensor:
 def _pearson(X: torch.Tensor) -> np.ndarray:
     n_loc = torch.tensor([float(X.shape[0])], dtype=torch.float64, device=X.device)
     s = X.sum(0)
-    G = X.T @ X
+    G = tn_matmul(X, X)
     buf = torch.cat([n_loc, s, G.reshape(-1)])
     comm.all_reduce(buf, "sum")
     d = X.shape[1]

@@ -13,6 +13,7 @@ from typing import Sequence, Tuple
 
 import torch
 
+from .gemm import tn_matmul
 from . import _lib
 
 __all__ = ["mlp_grad", "kernel_supported", "KMAX"]
@@ -65,7 +66,7 @@ def mlp_grad(X: torch.Tensor, y: torch.Tensor, w: torch.Tensor, coef: torch.Tens
     grads = [None] * len(params)
     for i in range(len(params) - 1, -1, -1):
         W, _ = params[i]
-        grads[i] = ((hs[i].T @ D).reshape(-1), D.sum(0))
+        grads[i] = (tn_matmul(hs[i], D).reshape(-1), D.sum(0))
         if i > 0:
             D = (D @ W.T).contiguous()
             rc = L.alink_sigmoid_bwd_f64(D.data_ptr(), hs[i].data_ptr(), D.numel(), st)
