@@ -24,6 +24,7 @@ from typing import Dict, List, Optional, Sequence
 import numpy as np
 import torch
 
+from ...ops.gemm import tn_matmul
 from ...common.javafmt import java_float_str
 from ...common.mapper import ModelMapper, OutputColsHelper, find_col_index
 from ...common.params import Params
@@ -212,7 +213,7 @@ def train_als(mt: MTable, params: Params, env) -> AlsModelData:
     mark("init factors")
     for _ in range(num_iter):
         for name, (side, Y, X) in (("users", (by_user, V, U)), ("items", (by_item, U, V))):
-            YtY = (Y.to(torch.float64).T @ Y.to(torch.float64)) if implicit else None
+            YtY = tn_matmul(Y.to(torch.float64), Y.to(torch.float64)) if implicit else None
             for bb in range(nblocks):
                 mask = (side.raw.abs() % nblocks) == bb
                 _update(side, mask, Y, X, lam, implicit, alpha, nonneg, YtY)
