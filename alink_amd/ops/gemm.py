@@ -11,7 +11,7 @@ from __future__ import annotations
 
 import torch
 
-__all__ = ["tn_matmul", "CHUNK"]
+__all__ = ["tn_matmul", "split_k", "CHUNK"]
 
 CHUNK = 2048          # rows per batch entry
 _MIN_ROWS = 4 * CHUNK
@@ -24,12 +24,20 @@ def tn_matmul(A: torch.Tensor, B: torch.Tensor) -> torch.Tensor:
         return A.T @ B
     if B.dim() == 1:
         return tn_matmul(A, B[:, None])[:, 0]
-    c = n // CHUNK
-    m = c * CHUNK
+    return split_k(A, B, CHUNK)
+
+
+def split_k(A: torch.Tensor, B: torch.Tensor, chunk: int) -> torch.Tensor:
+    """``A.T @ B`` as one batched GEMM over ``chunk``-row slices (+ the ragged tail), any device."""
+    n = A.shape[0]
+    c = n // chunk
+    m = c * chunk
     a, b = A.shape[1], B.shape[1]
     A = A.contiguous()
     B = B.contiguous()
-    out = torch.bmm(A[:m].view(c, CHUNK, a).transpose(1, 2), B[:m].view(c, CHUNK, b)).sum(0)
+    if c == 0:
+        return A.T @ B
+    out = torch.bmm(A[:m].view(c, chunk, a).transpose(1, 2), B[:m].view(c, chunk, b)).sum(0)
     if m < n:
         out.addmm_(A[m:].T, B[m:])
     return out
