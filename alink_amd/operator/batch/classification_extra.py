@@ -4,6 +4,7 @@ from __future__ import annotations
 from ...common.table import MTable
 from ...models.classification.naive_bayes import (NaiveBayesTextModelDataConverter, NaiveBayesTextModelMapper,
                                                   train_naive_bayes_text)
+from .modelinfo import FmModelInfoBatchOp, WithModelInfoBatchOp
 from ..base import BatchOperator
 from .utils import ModelMapBatchOp
 
@@ -46,14 +47,19 @@ class MultilayerPerceptronPredictBatchOp(ModelMapBatchOp):
 from ...models.recommendation import fm as _FM  # noqa: E402
 
 
-class _FmTrainBatchOp(BatchOperator):
-    """``FmTrainBatchOp`` (task fixed by the subclass): device mini-batch AdaGrad + model averaging."""
+class _FmTrainBatchOp(BatchOperator, WithModelInfoBatchOp):
+    """``FmTrainBatchOp`` (task fixed by the subclass): device mini-batch AdaGrad + model averaging; model info via
+    ``FmModelInfoBatchOp`` (``BaseFmTrainBatchOp.java:555``)."""
     TASK = "REGRESSION"
     _NO_AUTO_PARAMS = True
+
+    def getModelInfoBatchOp(self):
+        return FmModelInfoBatchOp(getattr(self, "_label_type", None)).linkFrom(self)
 
     def linkFrom(self, *inputs):
         mt = self.checkAndGetFirst(inputs).getOutputTable()
         m, lt, info = _FM.train_fm(mt, self.resolvedParams(), self.TASK, self.env)
+        self._label_type = lt
         self._train_info = info
         conv = _FM.FmModelDataConverter(lt)
         self.setOutputTable(MTable.from_rows(conv.save(m), conv.getModelSchema(), replicated=True))
