@@ -123,7 +123,11 @@ def init_distributed(backend: Optional[str] = None, timeout_s: float = 1800.0) -
         backend = os.environ.get("ALINK_DIST_BACKEND")
     if backend is None:
         cpu_only = os.environ.get("ALINK_DEVICE", "").startswith("cpu")
-        backend = "nccl" if torch.cuda.is_available() and not cpu_only else "gloo"
+        # RCCL needs one GPU per rank: more local ranks than GPUs (a P-way local env on a smaller box) run their
+        # collectives over gloo, with ranks sharing the GPUs round-robin for compute
+        local_ws = int(os.environ.get("LOCAL_WORLD_SIZE", str(ws)))
+        oversubscribed = torch.cuda.device_count() < local_ws
+        backend = "nccl" if torch.cuda.is_available() and not cpu_only and not oversubscribed else "gloo"
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     kw = {}
     if backend == "nccl":
