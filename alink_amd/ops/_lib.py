@@ -71,7 +71,7 @@ _EXTRA_SIGNATURES = {
     "alink_linear_grad_pad": [_c_int],
     "alink_linear_search_f64": [_c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_int, _c_int, _c_d, _c_d, _c_int, _c_vp,
                                 _c_int, _c_vp, _c_vp],
-    "alink_kmeans_update": [_c_vp, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp],
+    "alink_kmeans_update": [_c_vp, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_int, _c_vp],
     "alink_kmeans_accum_bf16": [_c_vp, _c_i64, _c_int, _c_vp, _c_vp, _c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp],
     "alink_kmeans_accum_kmax": [_c_int],
     "alink_kmeans_accum_mfma_bf16": [_c_vp, _c_i64, _c_vp, _c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp],

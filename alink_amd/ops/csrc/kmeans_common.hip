@@ -66,7 +66,8 @@ __global__ __launch_bounds__(128) void kmeans_prep_centroids_kernel(const double
 // fused centroid update after the all-reduce (reference KMeansUpdateCentroidsAndSetAllReduce + the termination
 // test KMeansIterTermination, A/operator/common/clustering/kmeans/): one workgroup per padded centroid row
 //   C[c] = sum[c] / cnt[c]                       (fp64, written for c < k)
-//   cpad[c] = bf16(C[c]), ninit[c] = -|cpad[c]|^2/2   (the NEXT superstep's MFMA operands: no separate prep launch)
+//   cpad[c] = bf16(C[c]) (or the held operand, hyst), ninit[c] = -|cpad[c]|^2/2   (the NEXT superstep's MFMA
+//   operands: no separate prep launch)
 //   stat[0] = max_c ||C[c] - prev[c]||  (fp64 bits, atomicMax: non-negative doubles order as unsigned integers)
 //   stat[1] = 1 if any cnt[c] <= 0 (the host then redoes the update with empty-cluster compaction)
 // replacing ~8 small torch launches + the prep launch of the next step and giving the host ONE 16-byte read.
@@ -74,7 +75,7 @@ __global__ __launch_bounds__(128) void kmeans_update_kernel(const double* __rest
                                                             const double* __restrict__ prev,
                                                             double* __restrict__ C, __bf16* __restrict__ cpad,
                                                             float* __restrict__ ninit,
-                                                            unsigned long long* __restrict__ stat) {
+                                                            unsigned long long* __restrict__ stat, int hyst) {
     __shared__ float red[128];
     __shared__ double redd[128];
     const int c = blockIdx.x, d = threadIdx.x;
@@ -86,7 +87,15 @@ __global__ __launch_bounds__(128) void kmeans_update_kernel(const double* __rest
         v = empty ? 0.0 : buf[(int64_t)c * (D + 1) + d] / cnt;
         C[(int64_t)c * D + d] = v;
     }
-    const __bf16 b = (__bf16)(float)v;
+    __bf16 b = (__bf16)(float)v;
+    if (hyst && c < k) {
+        // operand hysteresis: keep the current bf16 operand while the fp64 centroid stays within one bf16 ulp of
+        // it.  Round-to-nearest re-quantisation every step lets boundary rows flip on sub-ulp centroid jitter,
+        // which keeps Lloyd cycling at a ~2e-3 shift floor above epsilon; with the operand held, the
+        // assignments (and hence the fp64 centroids) become exactly stationary and the shift reaches 0.
+        const float ob = (float)cpad[c * D + d];
+        if (ob != 0.0f && fabs(v - (double)ob) < (double)ldexpf(1.0f, ilogbf(ob) - 7)) b = (__bf16)ob;
+    }
     cpad[c * D + d] = b;
     const float f = (float)b;
     red[d] = f * f;
@@ -116,13 +125,15 @@ extern "C" {
 
 // buf [k][D+1] (sums | count), prev [k][D] (nullable), C out [k][D], cpad [128][D] bf16, ninit [128],
 // stat [2] u64 (zeroed here): max shift (double bits), any-empty flag
+// hyst != 0: bf16 operand hysteresis (keep cpad[c][d] while |C[c][d] - cpad[c][d]| < 1 bf16 ulp; cpad must hold
+// the operands of the step just run, or any bf16 values: a kept value is always within one ulp of C)
 int alink_kmeans_update(const double* buf, int k, const double* prev, double* C, void* cpad, float* ninit,
-                        unsigned long long* stat, void* stream) {
+                        unsigned long long* stat, int hyst, void* stream) {
     if (k < 1 || k > 128) return -1;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     if (hipMemsetAsync(stat, 0, 2 * sizeof(unsigned long long), st) != hipSuccess) return -2;
     hipLaunchKernelGGL(kmeans_update_kernel, dim3(128), dim3(128), 0, st, buf, k, prev, C, (__bf16*)cpad, ninit,
-                       stat);
+                       stat, hyst);
     return (int)hipGetLastError();
 }
 

@@ -14,6 +14,7 @@ all-reduce.
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, Optional, Tuple
 
 import numpy as np
@@ -150,7 +151,13 @@ def update_supported(buf: torch.Tensor) -> bool:
         1 <= buf.shape[0] <= HIP_KMAX and buf.is_contiguous()
 
 
-def update_centroids_hip(buf: torch.Tensor, prev: Optional[torch.Tensor], deferred: bool = False):
+def operand_hysteresis() -> bool:
+    """bf16 centroid-operand hysteresis in the fused update (default on; ``ALINK_KMEANS_HYSTERESIS=0`` disables)."""
+    return os.environ.get("ALINK_KMEANS_HYSTERESIS", "1") != "0"
+
+
+def update_centroids_hip(buf: torch.Tensor, prev: Optional[torch.Tensor], deferred: bool = False,
+                         hysteresis: Optional[bool] = None):
     """Fused Lloyd update on the all-reduced ``[k, 129]`` buffer (``csrc/kmeans_common.hip``): returns
     ``(C [k,128] fp64, max_shift vs prev or None, any_empty)`` with ONE 16-byte device->host read, and leaves
     the next superstep's bf16 operands prepared (``prepare_centroids`` of the returned C launches nothing).
@@ -170,8 +177,11 @@ def update_centroids_hip(buf: torch.Tensor, prev: Optional[torch.Tensor], deferr
     use_prev = prev is not None and prev.is_cuda and prev.dtype == torch.float64 and tuple(prev.shape) == (k, HIP_D)
     pv = prev.contiguous() if use_prev else None
     C = torch.empty((k, HIP_D), dtype=torch.float64, device=dev)
+    if hysteresis is None:
+        hysteresis = operand_hysteresis()
     rc = L.alink_kmeans_update(buf.data_ptr(), k, None if pv is None else pv.data_ptr(), C.data_ptr(),
-                               cpad.data_ptr(), ninit.data_ptr(), stat.data_ptr(), _lib.stream_ptr(dev))
+                               cpad.data_ptr(), ninit.data_ptr(), stat.data_ptr(), int(bool(hysteresis)),
+                               _lib.stream_ptr(dev))
     if rc != 0:
         raise RuntimeError(f"alink_kmeans_update failed: {rc}")
     host.copy_(stat, non_blocking=True)

@@ -172,7 +172,7 @@ def test_fused_centroid_update_matches_torch(k):
     buf = torch.randn(k, 129, device="cuda", dtype=torch.float64, generator=g) * 100
     buf[:, 128] = torch.randint(1, 1000, (k,), device="cuda", generator=g).double()
     prev = torch.randn(k, 128, device="cuda", dtype=torch.float64, generator=g)
-    C, shift, empty = K.update_centroids_hip(buf, prev)
+    C, shift, empty = K.update_centroids_hip(buf, prev, hysteresis=False)
     ref = buf[:, :128] / buf[:, 128:]
     torch.testing.assert_close(C, ref, rtol=0, atol=0)
     assert not empty
@@ -183,8 +183,35 @@ def test_fused_centroid_update_matches_torch(k):
     cpad3, ninit3 = K.prepare_centroids(C, C.device)          # fresh prep launch
     assert torch.equal(cpad2, cpad3) and torch.equal(ninit2, ninit3)
     buf[k // 2, 128] = 0.0
-    _, _, empty = K.update_centroids_hip(buf, None)
+    _, _, empty = K.update_centroids_hip(buf, None, hysteresis=False)
     assert empty
+
+
+def test_update_operand_hysteresis():
+    """With hysteresis the next-step bf16 operand is held while the fp64 centroid stays within one bf16 ulp of it,
+    and re-rounded otherwise; ninit always matches the operands actually written."""
+    from alink_amd.ops import kmeans as K
+    k = 50
+    g = torch.Generator(device="cuda").manual_seed(3)
+    buf = torch.randn(k, 129, device="cuda", dtype=torch.float64, generator=g) * 100
+    buf[:, 128] = torch.randint(1, 1000, (k,), device="cuda", generator=g).double()
+    C0, _, _ = K.update_centroids_hip(buf, None, hysteresis=False)
+    cpad, ninit = K._PREP[C0.device.index]
+    held = cpad[:k].clone()
+    # nudge every centroid by a quarter ulp of its operand (stays within one ulp -> held), and row 0 by 3 ulps
+    ob = held.float().double()
+    ulp = torch.ldexp(torch.ones_like(ob), torch.frexp(ob.float())[1].double().long() - 8).double()
+    C1 = C0 + 0.25 * ulp
+    C1[0] = C0[0] + 3.0 * ulp[0]
+    buf2 = buf.clone()
+    buf2[:, :128] = C1 * buf[:, 128:]
+    C, _, _ = K.update_centroids_hip(buf2, C0, hysteresis=True)
+    cpad, ninit = K._PREP[C.device.index]
+    nz = held[1:] != 0
+    assert torch.equal(cpad[1:k][nz], held[1:][nz])
+    assert torch.equal(cpad[0], C[0].float().to(torch.bfloat16))
+    f = cpad[:k].float()
+    torch.testing.assert_close(ninit[:k], -0.5 * (f * f).sum(1), rtol=1e-6, atol=1e-3)
 
 
 def test_speculative_next_step_launch_gives_identical_model():
