@@ -88,13 +88,24 @@ __global__ __launch_bounds__(128) void kmeans_update_kernel(const double* __rest
         C[(int64_t)c * D + d] = v;
     }
     __bf16 b = (__bf16)(float)v;
-    if (hyst && c < k) {
-        // operand hysteresis: keep the current bf16 operand while the fp64 centroid stays within one bf16 ulp of
-        // it.  Round-to-nearest re-quantisation every step lets boundary rows flip on sub-ulp centroid jitter,
-        // which keeps Lloyd cycling at a ~2e-3 shift floor above epsilon; with the operand held, the
-        // assignments (and hence the fp64 centroids) become exactly stationary and the shift reaches 0.
-        const float ob = (float)cpad[c * D + d];
-        if (ob != 0.0f && fabs(v - (double)ob) < (double)ldexpf(1.0f, ilogbf(ob) - 7)) b = (__bf16)ob;
+    if (hyst) {
+        // operand hysteresis: keep the current bf16 operand while the fp64 centroid stays within one bf16 ulp
+        // of the row's largest coordinate (the resolution the bf16 dot product has anyway).  Re-quantising every
+        // step lets boundary rows flip on sub-ulp centroid jitter, which keeps Lloyd cycling at a ~2e-3 shift
+        // floor above epsilon; with the operands held, the assignments (and hence the fp64 centroids) become
+        // exactly stationary and the shift reaches 0.
+        red[d] = (float)fabs(v);
+        __syncthreads();
+        for (int off = 64; off > 0; off >>= 1) {
+            if (d < off) red[d] = fmaxf(red[d], red[d + off]);
+            __syncthreads();
+        }
+        const float m = red[0];
+        __syncthreads();
+        if (c < k && m > 0.0f) {
+            const float ob = (float)cpad[c * D + d];
+            if (fabs(v - (double)ob) < (double)ldexpf(1.0f, ilogbf(m) - 7)) b = (__bf16)ob;
+        }
     }
     cpad[c * D + d] = b;
     const float f = (float)b;
@@ -125,8 +136,8 @@ extern "C" {
 
 // buf [k][D+1] (sums | count), prev [k][D] (nullable), C out [k][D], cpad [128][D] bf16, ninit [128],
 // stat [2] u64 (zeroed here): max shift (double bits), any-empty flag
-// hyst != 0: bf16 operand hysteresis (keep cpad[c][d] while |C[c][d] - cpad[c][d]| < 1 bf16 ulp; cpad must hold
-// the operands of the step just run, or any bf16 values: a kept value is always within one ulp of C)
+// hyst != 0: bf16 operand hysteresis (keep cpad[c][d] while |C[c][d] - cpad[c][d]| < one bf16 ulp of max_d |C[c][d]|;
+// cpad should hold the operands of the step just run, but any contents are safe: a kept value is that close to C)
 int alink_kmeans_update(const double* buf, int k, const double* prev, double* C, void* cpad, float* ninit,
                         unsigned long long* stat, int hyst, void* stream) {
     if (k < 1 || k > 128) return -1;

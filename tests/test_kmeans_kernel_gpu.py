@@ -188,7 +188,8 @@ def test_fused_centroid_update_matches_torch(k):
 
 
 def test_update_operand_hysteresis():
-    """With hysteresis the next-step bf16 operand is held while the fp64 centroid stays within one bf16 ulp of it,
+    """With hysteresis the next-step bf16 operand is held while the fp64 centroid stays within one bf16 ulp of the
+    row's largest coordinate,
     and re-rounded otherwise; ninit always matches the operands actually written."""
     from alink_amd.ops import kmeans as K
     k = 50
@@ -198,17 +199,17 @@ def test_update_operand_hysteresis():
     C0, _, _ = K.update_centroids_hip(buf, None, hysteresis=False)
     cpad, ninit = K._PREP[C0.device.index]
     held = cpad[:k].clone()
-    # nudge every centroid by a quarter ulp of its operand (stays within one ulp -> held), and row 0 by 3 ulps
-    ob = held.float().double()
-    ulp = torch.ldexp(torch.ones_like(ob), torch.frexp(ob.float())[1].double().long() - 8).double()
+    # nudge every centroid by a quarter ulp of its row's largest operand (within the one-ulp band -> held), and
+    # row 0 by 3 such ulps (outside -> re-rounded)
+    m = C0.abs().amax(1, keepdim=True).float()
+    ulp = torch.ldexp(torch.ones_like(m), torch.frexp(m)[1] - 8).double()
     C1 = C0 + 0.25 * ulp
     C1[0] = C0[0] + 3.0 * ulp[0]
     buf2 = buf.clone()
     buf2[:, :128] = C1 * buf[:, 128:]
     C, _, _ = K.update_centroids_hip(buf2, C0, hysteresis=True)
     cpad, ninit = K._PREP[C.device.index]
-    nz = held[1:] != 0
-    assert torch.equal(cpad[1:k][nz], held[1:][nz])
+    assert torch.equal(cpad[1:k], held[1:])
     assert torch.equal(cpad[0], C[0].float().to(torch.bfloat16))
     f = cpad[:k].float()
     torch.testing.assert_close(ninit[:k], -0.5 * (f * f).sum(1), rtol=1e-6, atol=1e-3)
