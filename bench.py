@@ -15,9 +15,10 @@ GPU; rank 0's JSON line is the job's output; a failing or hung rank fails the jo
 
 Prints ONE JSON line on rank 0.  ``value`` = total rows processed per second by the whole job
 (rows x K / max-over-ranks elapsed).  Also reports ``iters_to_converge`` from separate untimed runs with
-epsilon 1e-4: k-means|| initSteps=5 (``iters_to_converge``) and the reference default initSteps=2
-(``convergence.initSteps2``: a single oversampling round of 2k candidates misses ~10% of the 100 mixture
-components, after which Lloyd creeps for >100 supersteps — the same algorithm as the reference).
+epsilon 1e-4 at the reference default init (k-means|| initSteps=2, ``convergence.initSteps2``), plus initSteps=5
+for comparison (``convergence.initSteps5``).  The fused update holds each bf16 centroid operand while its fp64
+centroid stays within one bf16 ulp (ops/csrc/kmeans_common.hip), so Lloyd reaches an exactly stationary
+assignment; with plain re-quantisation every step it cycled at a ~2e-3 shift floor and never met epsilon.
 """
 from __future__ import annotations
 
@@ -116,7 +117,7 @@ def main():
             conv[f"initSteps{steps}"] = {"iters": info["iterations"], "wall_s": time.perf_counter() - t_c,
                                          "final_max_shift": shift,
                                          "converged": shift is not None and shift < 1e-4}
-        iters = conv["initSteps5"]["iters"]
+        iters = conv["initSteps2"]["iters"]
 
     rows_per_s = a.rows * a.steps / elapsed
     res = {
@@ -137,8 +138,8 @@ def main():
                    "parallelism": f"dp{env.world_size}"},
         "rows_per_s_per_gpu": rows_per_s / env.world_size,
         "iters_to_converge": iters,
-        "iters_to_converge_setting": "epsilon 1e-4, k-means|| initSteps=5; reference default initSteps=2 "
-                                     "reported under convergence.initSteps2",
+        "iters_to_converge_setting": "epsilon 1e-4, k-means|| initSteps=2 (reference default); initSteps=5 "
+                                     "under convergence.initSteps5",
         "convergence": conv,
         "iters_to_converge_default_init": conv.get("initSteps2", {}).get("iters"),
         "converged_default_init": conv.get("initSteps2", {}).get("converged"),
