@@ -305,6 +305,27 @@ def accumulate_by_index_hip(X: torch.Tensor, idx: torch.Tensor, k: int,
     return out
 
 
+_HELD: Dict[Tuple, torch.Tensor] = {}
+
+
+def held_operand(C: torch.Tensor) -> torch.Tensor:
+    """bf16 centroid operand with the same hysteresis as the fused update kernel (kmeans_common.hip): a coordinate
+    keeps its previous operand while the fp64 centroid stays within one bf16 ulp of the row's largest coordinate,
+    so Lloyd reaches an exactly stationary assignment instead of cycling on re-quantisation jitter."""
+    Cb = C.to(torch.bfloat16)
+    key = (C.device.index, tuple(C.shape))
+    prev = _HELD.get(key)
+    if prev is not None and operand_hysteresis():
+        m = C.abs().amax(1, keepdim=True).float()
+        band = torch.ldexp(torch.ones_like(m), torch.frexp(m)[1] - 8).double()
+        keep = ((C.double() - prev.double()).abs() < band) & (m > 0)
+        Cb = torch.where(keep, prev, Cb)
+    if len(_HELD) > 8:
+        _HELD.clear()
+    _HELD[key] = Cb
+    return Cb
+
+
 def assign_accumulate_general_hip(X: torch.Tensor, C: torch.Tensor,
                                   weights: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Two-pass HIP path for the shapes v7 does not cover (d 64/256, k up to 256/512, weighted rows)."""
@@ -312,7 +333,7 @@ def assign_accumulate_general_hip(X: torch.Tensor, C: torch.Tensor,
     if not general_supported(X, C.shape[0]):
         raise ValueError("general HIP KMeans path needs contiguous bf16 [N, D in (64,128,256)] and k <= 256")
     GENERAL_CALLS += 1
-    idx, _ = nearest_hip(X, C)
+    idx, _ = nearest_hip(X, held_operand(C) if C.dtype != torch.bfloat16 else C)
     return accumulate_by_index_hip(X, idx, C.shape[0], weights)
 
 
