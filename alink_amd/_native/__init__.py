@@ -12,7 +12,7 @@ from typing import List, Optional, Sequence
 import numpy as np
 
 __all__ = ["lib", "parse_csv_lines", "murmur3_utf16", "parse_dense_vectors", "ftrl_update_csr",
-           "ftrl_partial_margin", "ftrl_shard_update"]
+           "ftrl_partial_margin", "ftrl_shard_update", "parse_binary_detail"]
 
 # ALINK_NATIVE_LIB points at another build of the same sources (e.g. the AddressSanitizer build of
 # tools/asan_host.py)
@@ -28,6 +28,7 @@ if os.path.exists(_PATH):
         lib.alink_ftrl_update_csr.restype = ctypes.c_int
         lib.alink_ftrl_partial_margin.restype = ctypes.c_int
         lib.alink_ftrl_shard_update.restype = ctypes.c_int
+        lib.alink_parse_binary_detail.restype = ctypes.c_int64
     except OSError:
         lib = None
 
@@ -108,6 +109,28 @@ def murmur3_utf16(strings: Sequence[str], seed: int = 0) -> Optional[np.ndarray]
     lib.alink_murmur3_utf16_batch(_ptr(chars), _ptr(off), ctypes.c_int64(len(units)), ctypes.c_uint32(seed),
                                   _ptr(out))
     return out
+
+
+def parse_binary_detail(strings: Sequence[str], key0: str, key1: str):
+    """(p0, p1) float64 arrays: the probabilities of labels ``key0`` / ``key1`` in two-entry detail JSON strings,
+    or None (library missing, or a string outside the plain two-entry form: the caller parses it as JSON)."""
+    if lib is None or getattr(lib, "alink_parse_binary_detail", None) is None:
+        return None
+    try:
+        enc = [s.encode("utf-8") for s in strings]
+    except AttributeError:
+        return None
+    off = np.zeros(len(enc) + 1, dtype=np.int64)
+    if enc:
+        np.cumsum([len(b) for b in enc], out=off[1:])
+    buf = b"".join(enc)
+    k0, k1 = key0.encode("utf-8"), key1.encode("utf-8")
+    p0 = np.zeros(len(enc), dtype=np.float64)
+    p1 = np.zeros(len(enc), dtype=np.float64)
+    bad = lib.alink_parse_binary_detail(ctypes.c_char_p(buf), _ptr(off), ctypes.c_int64(len(enc)), ctypes.c_char_p(k0),
+                                        ctypes.c_int(len(k0)), ctypes.c_char_p(k1), ctypes.c_int(len(k1)), _ptr(p0),
+                                        _ptr(p1))
+    return None if bad != 0 else (p0, p1)
 
 
 def parse_dense_vectors(strings: Sequence[str], d: int) -> Optional[np.ndarray]:

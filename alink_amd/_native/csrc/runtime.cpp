@@ -199,6 +199,67 @@ int alink_parse_dense_vectors(const char* buf, const int64_t* off, int64_t n, in
     return err >= 0 ? (int)(-1 - err) : 0;
 }
 
+// Binary prediction-detail strings {"<label>":p,"<label>":p} (the predictors' detail column, parsed per row by
+// BinaryClassMetrics / EvalBinaryClassBatchOp): probability of key0 and key1 for each of n strings.  Returns 0, or
+// the 1-based index of the first string it cannot read (not exactly two plain "key":number entries, an escape in a
+// key, a missing key), in which case the caller parses with the general JSON reader.
+static inline const char* skip_ws(const char* p, const char* e) {
+    while (p < e && (*p == ' ' || *p == '\t' || *p == '\n' || *p == '\r')) ++p;
+    return p;
+}
+
+int64_t alink_parse_binary_detail(const char* buf, const int64_t* off, int64_t n, const char* key0, int len0,
+                                  const char* key1, int len1, double* p0, double* p1) {
+    for (int64_t i = 0; i < n; ++i) {
+        const char* p = buf + off[i];
+        const char* e = buf + off[i + 1];
+        bool got0 = false, got1 = false;
+        int entries = 0;
+        p = skip_ws(p, e);
+        if (p >= e || *p != '{') return i + 1;
+        ++p;
+        while (true) {
+            p = skip_ws(p, e);
+            if (p >= e || *p != '"') return i + 1;
+            const char* ks = ++p;
+            while (p < e && *p != '"') {
+                if (*p == '\\') return i + 1;
+                ++p;
+            }
+            if (p >= e) return i + 1;
+            const int klen = (int)(p - ks);
+            ++p;
+            p = skip_ws(p, e);
+            if (p >= e || *p != ':') return i + 1;
+            p = skip_ws(p + 1, e);
+            char num[64];
+            int nl = 0;
+            while (p < e && nl < 63 && *p != ',' && *p != '}' && *p != ' ') num[nl++] = *p++;
+            num[nl] = 0;
+            char* endp = nullptr;
+            const double v = strtod(num, &endp);
+            if (nl == 0 || endp != num + nl) return i + 1;
+            if (klen == len0 && memcmp(ks, key0, len0) == 0) {
+                p0[i] = v;
+                got0 = true;
+            } else if (klen == len1 && memcmp(ks, key1, len1) == 0) {
+                p1[i] = v;
+                got1 = true;
+            }
+            ++entries;
+            p = skip_ws(p, e);
+            if (p < e && *p == ',') {
+                ++p;
+                continue;
+            }
+            if (p < e && *p == '}') break;
+            return i + 1;
+        }
+        if (entries != 2 || !got0 || !got1) return i + 1;
+    }
+    return 0;
+}
+
 int alink_native_version() { return 1; }
 
 }  // extern "C"

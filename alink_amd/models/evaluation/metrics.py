@@ -166,6 +166,10 @@ def parse_detail(s: str) -> Dict[str, float]:
 def binary_summary(labels_col: Sequence[Any], details: Sequence[str], label_array: List[str], device=None):
     """(positiveBin, negativeBin, logLoss, total) over all ranks."""
     dev = device or torch.device("cpu")
+    fast = _binary_detail_native(labels_col, details, label_array)
+    if fast is not None:
+        pos_p, is_pos, ll, keep = fast
+        return _binary_bins(pos_p, is_pos, ll, keep, dev)
     pos_p, is_pos, ll, keep = [], [], 0.0, 0
     for lab, det in zip(labels_col, details):
         if lab is None or det is None:
@@ -182,9 +186,40 @@ def binary_summary(labels_col: Sequence[Any], details: Sequence[str], label_arra
         pos_p.append(p)
         is_pos.append(lab == label_array[0])
         keep += 1
-    p = torch.tensor(pos_p, dtype=torch.float64, device=dev)
+    return _binary_bins(pos_p, is_pos, ll, keep, dev)
+
+
+def _binary_detail_native(labels_col, details, label_array: List[str]):
+    """Bulk path of the per-row detail parsing above: the host C++ parser reads plain two-entry detail strings
+    (``_native.parse_binary_detail``) and the checks run vectorised; None -> the caller's JSON loop (which also
+    produces the exact error messages)."""
+    from ... import _native
+    if len(label_array) != 2:
+        return None
+    labs = [None if l is None else str(l) for l in labels_col]
+    lset = set(label_array)
+    keep_idx = [i for i, (l, d) in enumerate(zip(labs, details)) if l is not None and d is not None and l in lset]
+    dets = [details[i] for i in keep_idx]
+    if any(not isinstance(d, str) for d in dets):
+        return None
+    parsed = _native.parse_binary_detail(dets, label_array[0], label_array[1])
+    if parsed is None:
+        return None
+    p0, p1 = parsed
+    if not (np.all((p0 >= 0.0) & (p0 <= 1.0) & (p1 >= 0.0) & (p1 <= 1.0))
+            and np.all(np.abs(p0 + p1 - 1.0) < PROB_SUM_EPS)):
+        return None
+    is_pos = np.array([labs[i] == label_array[0] for i in keep_idx], dtype=bool)
+    pl = np.where(is_pos, p0, p1)
+    terms = -np.log(np.clip(pl, LOG_LOSS_EPS, 1 - LOG_LOSS_EPS))
+    ll = float(np.cumsum(terms)[-1]) if len(terms) else 0.0       # the loop's left-to-right summation order
+    return p0, is_pos, ll, len(keep_idx)
+
+
+def _binary_bins(pos_p, is_pos, ll, keep, dev):
+    p = torch.as_tensor(np.asarray(pos_p, dtype=np.float64), device=dev)
     idx = torch.where(p == 1.0, torch.full_like(p, DETAIL_BIN_NUMBER - 1), torch.floor(p * DETAIL_BIN_NUMBER)).long()
-    lbl = torch.tensor(is_pos, dtype=torch.bool, device=dev)
+    lbl = torch.as_tensor(np.asarray(is_pos, dtype=bool), device=dev)
     ok = (idx >= 0) & (idx < DETAIL_BIN_NUMBER)
     posb = torch.bincount(idx[ok & lbl], minlength=DETAIL_BIN_NUMBER).double()
     negb = torch.bincount(idx[ok & ~lbl], minlength=DETAIL_BIN_NUMBER).double()
