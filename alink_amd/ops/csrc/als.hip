@@ -28,15 +28,25 @@ __global__ __launch_bounds__(64) void als_gram(const int64_t* __restrict__ indpt
   const int li = lane / G, lj = lane % G;
   const bool active = lane < G * G;
   const int64_t s = indptr[row], e = indptr[row + 1];
-  float acc[8][8];
-  float bacc[8];
+  // fp32 FMAs within a 32-neighbour tile, tile partials folded into fp64 so high-degree rows (popular items,
+  // ~1e5 neighbours) keep fp64-level accuracy like the torch path (normal_equations_torch accumulates in fp64)
+  double dacc[8][8];
+  double dbacc[8];
 #pragma unroll
   for (int a = 0; a < 8; ++a) {
-    bacc[a] = 0.f;
+    dbacc[a] = 0.0;
 #pragma unroll
-    for (int c = 0; c < 8; ++c) acc[a][c] = 0.f;
+    for (int c = 0; c < 8; ++c) dacc[a][c] = 0.0;
   }
   for (int64_t t0 = s; t0 < e; t0 += kTile) {
+    float acc[8][8];
+    float bacc[8];
+#pragma unroll
+    for (int a = 0; a < 8; ++a) {
+      bacc[a] = 0.f;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) acc[a][c] = 0.f;
+    }
     const int cnt = (int)((e - t0) < kTile ? (e - t0) : kTile);
     for (int idx = lane; idx < kTile * RP; idx += 64) {
       const int t = idx / RP, k = idx - (idx / RP) * RP;
@@ -79,6 +89,12 @@ __global__ __launch_bounds__(64) void als_gram(const int64_t* __restrict__ indpt
           for (int a = 0; a < 8; ++a) bacc[a] = fmaf(w, yi[a], bacc[a]);
         }
       }
+#pragma unroll
+      for (int a = 0; a < 8; ++a) {
+        dbacc[a] += (double)bacc[a];
+#pragma unroll
+        for (int b = 0; b < 8; ++b) dacc[a][b] += (double)acc[a][b];
+      }
     }
     __syncthreads();
   }
@@ -91,9 +107,9 @@ __global__ __launch_bounds__(64) void als_gram(const int64_t* __restrict__ indpt
 #pragma unroll
     for (int b = 0; b < 8; ++b) {
       const int j = lj * 8 + b;
-      if (j < r) Au[i * r + j] = acc[a][b];
+      if (j < r) Au[i * r + j] = (float)dacc[a][b];
     }
-    if (lj == 0) bvec[row * (int64_t)r + i] = bacc[a];
+    if (lj == 0) bvec[row * (int64_t)r + i] = (float)dbacc[a];
   }
 }
 

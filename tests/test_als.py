@@ -126,6 +126,26 @@ def test_hip_als_normal_equations(r, implicit):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("r", [10, 64])
+def test_hip_als_normal_equations_high_degree_row(r):
+    """ADVICE r1 (als.hip fp32 accumulation): one row with 1e5 neighbours against the fp64 torch Gram. Tile
+    partials fold into fp64, so the error stays near one fp32 rounding of the result (plain fp32 running sums
+    drift to ~1e-5 relative at this degree)."""
+    import alink_amd.ops._lib as L
+    assert L.available()
+    rng = np.random.default_rng(7)
+    n, deg = 4000, 100_000
+    indptr = torch.tensor([0, deg, deg + 5], dtype=torch.int64)
+    nbr = torch.as_tensor(rng.integers(0, n, size=deg + 5), dtype=torch.int32)
+    rt = torch.as_tensor(rng.uniform(0.5, 5.0, size=deg + 5), dtype=torch.float32)
+    Y = torch.as_tensor(1.0 + 0.3 * rng.normal(size=(n, r)), dtype=torch.float32)
+    A0, b0 = aops.normal_equations_torch(indptr, nbr, rt, Y, False, 0.0)
+    A1, b1 = aops.normal_equations(indptr.cuda(), nbr.cuda(), rt.cuda(), Y.cuda(), False, 0.0)
+    np.testing.assert_allclose(A1.cpu().double().numpy(), A0.numpy(), rtol=2e-6)
+    np.testing.assert_allclose(b1.cpu().double().numpy(), b0.numpy(), rtol=2e-6)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("r", [3, 10, 16, 40, 64])
 @pytest.mark.parametrize("implicit", [False, True])
 def test_hip_als_fused_solve_matches_fp64_torch(r, implicit):
