@@ -342,7 +342,7 @@ class KMeansAssignCluster(ComputeFunction):
         C = cur[1][:k]
         spec = ctx.getObj(SPEC_BUF)
         ctx.removeObj(SPEC_BUF)
-        if spec is not None and spec[0] == (ctx.getStepNo(), kops._ckey(C)):
+        if spec is not None and spec[0][0] == ctx.getStepNo() and kops.key_matches(spec[0][1], C):
             ctx.putObj(CENTROID_ALL_REDUCE, spec[1])    # launched by the previous superstep's update
             return
         if X is None or X.shape[0] == 0:

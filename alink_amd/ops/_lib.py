@@ -64,6 +64,9 @@ _EXTRA_SIGNATURES = {
     "alink_kmeans_assign_accum_bf16_v7": [_c_vp, _c_i64, _c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_int, _c_vp, _c_vp,
                                           _c_int],
     "alink_kmeans_v7_grid": [_c_i64, _c_int],
+    "alink_kmeans_assign_accum_bf16_v10": [_c_vp, _c_i64, _c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_int, _c_vp, _c_vp,
+                                           _c_int],
+    "alink_kmeans_v10_grid": [_c_i64, _c_int],
     "alink_kmeans_nearest_bf16": [_c_vp, _c_i64, _c_int, _c_vp, _c_vp, _c_int, _c_int, _c_vp, _c_vp, _c_int,
                                   _c_int, _c_vp],
     "alink_linear_grad_f64": [_c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_int, _c_int, _c_d, _c_vp, _c_int, _c_vp,

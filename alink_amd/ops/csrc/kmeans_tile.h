@@ -43,8 +43,9 @@ __device__ __forceinline__ void wait_tile4(int younger) {
 }
 
 // stage one 64-row tile with NP pieces per wave (NP = 2: all 8 waves; NP = 4: the 4 accumulate waves, `wave` =
-// 0..3 among them); rows past N read as zero (buffer bounds)
-template <int NP>
+// 0..3 among them); rows past N read as zero (buffer bounds).  NT = 1 issues the pieces with the streaming
+// (non-temporal) cache policy: X is read once per superstep, so there is nothing to keep in L2
+template <int NP, int NT = 0>
 __device__ __forceinline__ void stage_np(char* lds, int slot, const char* X, int64_t row0, int64_t N,
                                          const uint32_t (&voff)[4], int wave) {
     const int64_t rem = (N - row0) * ROWB;
@@ -56,15 +57,44 @@ __device__ __forceinline__ void stage_np(char* lds, int slot, const char* X, int
         const uint32_t m0v = __builtin_amdgcn_readfirstlane(
             (uint32_t)(uintptr_t)(LDS_AS void*)(lds + slot * TILE + i * (TILE / NP) + wave * 1024));
         uint32_t keep;
-        asm volatile(
-            "s_mov_b32 %0, m0\n\t"
-            "s_mov_b32 m0, %3\n\t"
-            "s_nop 0\n\t"
-            "buffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
-            "s_mov_b32 m0, %0"
-            : "=&s"(keep)
-            : "v"(voff[i]), "s"(rs), "s"(m0v)
-            : "memory");
+        if constexpr (NT)
+            asm volatile(
+                "s_mov_b32 %0, m0\n\t"
+                "s_mov_b32 m0, %3\n\t"
+                "s_nop 0\n\t"
+                "buffer_load_dwordx4 %1, %2, 0 offen nt lds\n\t"
+                "s_mov_b32 m0, %0"
+                : "=&s"(keep)
+                : "v"(voff[i]), "s"(rs), "s"(m0v)
+                : "memory");
+        else
+            asm volatile(
+                "s_mov_b32 %0, m0\n\t"
+                "s_mov_b32 m0, %3\n\t"
+                "s_nop 0\n\t"
+                "buffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
+                "s_mov_b32 m0, %0"
+                : "=&s"(keep)
+                : "v"(voff[i]), "s"(rs), "s"(m0v)
+                : "memory");
+    }
+}
+
+// s_waitcnt vmcnt(N) for a compile-time N (0..63)
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+    static_assert(N >= 0 && N < 64, "vmcnt range");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// wait until the tile `younger` tiles before the newest one issued has landed, NP pieces per tile per wave
+template <int NP, int MAXY>
+__device__ __forceinline__ void wait_tile_np(int younger) {
+    if constexpr (MAXY <= 0) {
+        wait_vm<0>();
+    } else {
+        if (younger >= MAXY) wait_vm<NP * MAXY>();
+        else wait_tile_np<NP, MAXY - 1>(younger);
     }
 }
 

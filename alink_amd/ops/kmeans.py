@@ -15,6 +15,7 @@ all-reduce.
 from __future__ import annotations
 
 import os
+import weakref
 from typing import Dict, Optional, Tuple
 
 import numpy as np
@@ -39,11 +40,27 @@ def hip_supported(X: torch.Tensor, k: int) -> bool:
 _PREP = {}
 
 
-_PREPARED = {}    # device -> (key of the centroid tensor whose operands sit in _PREP[device])
+_PREPARED = {}    # device -> (weakref to the centroid tensor whose operands sit in _PREP[device], its _version)
 
 
 def _ckey(C: torch.Tensor):
-    return (C.data_ptr(), tuple(C.shape), C._version)
+    """Identity of a centroid tensor that cannot alias: a weak reference to the tensor owning the memory
+    (compared by object identity; views resolve to their base) plus (data_ptr, shape, version).  The address
+    alone could match a fresh tensor that the caching allocator placed where a freed one was — e.g. the next
+    KMeans job's initial centroids."""
+    base = C if C._base is None else C._base
+    return (weakref.ref(base), C.data_ptr(), tuple(C.shape), C._version)
+
+
+def key_matches(key, C: torch.Tensor) -> bool:
+    if key is None:
+        return False
+    base = C if C._base is None else C._base
+    return key[0]() is base and key[1:] == (C.data_ptr(), tuple(C.shape), C._version)
+
+
+def _prepared_is(dev_index, C: torch.Tensor) -> bool:
+    return key_matches(_PREPARED.get(dev_index), C)
 
 
 def prepare_centroids(C: torch.Tensor, device) -> Tuple[torch.Tensor, torch.Tensor]:
@@ -52,7 +69,7 @@ def prepare_centroids(C: torch.Tensor, device) -> Tuple[torch.Tensor, torch.Tens
     ``update_centroids_hip`` already wrote the operands of exactly this tensor, nothing is launched."""
     k = C.shape[0]
     if C.is_cuda and C.dtype == torch.float64 and C.shape[1] == HIP_D and k <= HIP_KMAX:
-        if _PREPARED.get(C.device.index) == _ckey(C) and C.device.index in _PREP:
+        if _prepared_is(C.device.index, C) and C.device.index in _PREP:
             return _PREP[C.device.index]
         L = _lib.require()
         key = C.device.index
@@ -74,19 +91,26 @@ def prepare_centroids(C: torch.Tensor, device) -> Tuple[torch.Tensor, torch.Tens
     return cpad, ninit
 
 
-KERNEL_VERSIONS = ("v7",)
+KERNEL_VERSIONS = ("v7", "v10")
 # v7 variant (csrc/kmeans_v7.hip VAR): 0 = all 8 waves stage the tile ring; 1 (default) = the accumulate waves
 # stage it all, so the distance waves (the critical role) carry no LDS-DMA issue cost or vmcnt waits
-V7_VAR = int(__import__("os").environ.get("ALINK_KMEANS_V7_VAR", "1"))
-DEFAULT_KERNEL = "v7"
+V7_VAR = int(os.environ.get("ALINK_KMEANS_V7_VAR", "1"))
+# v10 launch flags (csrc/kmeans_v10.hip mode bits 4-5): 1 = non-temporal X loads, 2 = 9-slot ring
+V10_FLAGS = int(os.environ.get("ALINK_KMEANS_V10_FLAGS", "0"))
+V10_KMAX = 112
 
 
-def kernel_version() -> str:
-    """Fused assign+accumulate kernel (csrc/kmeans_v7.hip; ``ALINK_KMEANS_KERNEL`` selects among the shipped
-    versions — v9, a lagged register-prefetch accumulate, measured no faster and was dropped)."""
-    v = __import__("os").environ.get("ALINK_KMEANS_KERNEL", DEFAULT_KERNEL)
-    if v not in KERNEL_VERSIONS:
+def kernel_version(k: int = 100) -> str:
+    """Fused assign+accumulate kernel for k centroids: v10 (csrc/kmeans_v10.hip: MFMA distances + register
+    accumulate) for k <= 112, v7 (csrc/kmeans_v7.hip: one-hot MFMA accumulate) above.  ``ALINK_KMEANS_KERNEL``
+    forces one (v10 only where k <= 112)."""
+    v = os.environ.get("ALINK_KMEANS_KERNEL")
+    if v is not None and v not in KERNEL_VERSIONS:
         raise ValueError(f"ALINK_KMEANS_KERNEL must be one of {KERNEL_VERSIONS}")
+    if v is None:
+        v = "v10" if k <= V10_KMAX else "v7"
+    if v == "v10" and k > V10_KMAX:
+        v = "v7"
     return v
 
 
@@ -118,7 +142,7 @@ def assign_accumulate_hip(X: torch.Tensor, C: torch.Tensor, grid: Optional[int] 
         raise ValueError("assign_out must be a contiguous int32 [N] tensor on X's device")
     cpad, ninit = prepare_centroids(C, dev)
     n = X.shape[0]
-    ver = kernel_version()
+    ver = kernel_version(k)
     gkey = (ver, n, grid, dev.index)
     if gkey not in _GRID:      # per-shape launch geometry (one ctypes call per shape, not per superstep)
         _GRID[gkey] = int(getattr(L, f"alink_kmeans_{ver}_grid")(n, grid if grid is not None else _num_cus(dev)))
@@ -131,7 +155,7 @@ def assign_accumulate_hip(X: torch.Tensor, C: torch.Tensor, grid: Optional[int] 
     out = torch.empty((k, HIP_D + 1), dtype=torch.float64, device=dev)
     st = _lib.stream_ptr(dev)
     if mode < 16:
-        mode |= V7_VAR << 4
+        mode |= (V7_VAR << 4) if ver == "v7" else (V10_FLAGS << 4)
     rc = getattr(L, f"alink_kmeans_assign_accum_bf16_{ver}")(
         X.data_ptr(), n, cpad.data_ptr(), ninit.data_ptr(), k, slab.data_ptr(), slab_cnt.data_ptr(), grid, st,
         None if assign_out is None else assign_out.data_ptr(), int(mode))

@@ -252,9 +252,11 @@ def reduce_scatter(t: torch.Tensor, op: str = "sum") -> torch.Tensor:
     out = torch.empty((t.shape[0] // ws,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
     STATS.calls += 1
     STATS.bytes += t.numel() * t.element_size()
-    if _backend() == "nccl" and t.is_cuda:
-        dist.reduce_scatter_tensor(out, t.contiguous(), op=rop)
-        return out
+    if _backend() == "nccl":
+        d = t if t.is_cuda else t.to(device_for_rank())
+        o = out if t.is_cuda else torch.empty(out.shape, dtype=t.dtype, device=d.device)
+        dist.reduce_scatter_tensor(o, d.contiguous(), op=rop)
+        return out if t.is_cuda else o.cpu()
     full = t.clone()
     all_reduce(full, op)
     r = get_rank()
@@ -268,10 +270,12 @@ def all_gather_tensor(t: torch.Tensor) -> torch.Tensor:
     if ws == 1:
         return t
     STATS.calls += 1
-    if _backend() == "nccl" and t.is_cuda:
-        out = torch.empty((ws * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
-        dist.all_gather_into_tensor(out, t.contiguous())
-        return out
+    if _backend() == "nccl":
+        # RCCL has no host path: host inputs are staged through the rank's GPU and the result returned on the host
+        d = t if t.is_cuda else t.to(device_for_rank())
+        out = torch.empty((ws * d.shape[0],) + tuple(d.shape[1:]), dtype=d.dtype, device=d.device)
+        dist.all_gather_into_tensor(out, d.contiguous())
+        return out if t.is_cuda else out.cpu()
     parts = [torch.empty_like(t.cpu()) for _ in range(ws)]
     dist.all_gather(parts, t.cpu().contiguous())
     return torch.cat(parts).to(t.device)
@@ -283,8 +287,8 @@ def all_gather_varlen(t: torch.Tensor) -> torch.Tensor:
     ws = get_world_size()
     if ws == 1:
         return t
-    n = torch.tensor([t.shape[0]], dtype=torch.int64, device=t.device if _backend() == "nccl" else "cpu")
-    lens = all_gather_tensor(n).cpu().tolist()
+    n = torch.tensor([t.shape[0]], dtype=torch.int64)
+    lens = all_gather_tensor(n).tolist()
     mx = max(lens)
     pad = torch.zeros((mx,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
     pad[:t.shape[0]] = t
@@ -303,14 +307,16 @@ def all_to_all_tensors(send: List[torch.Tensor]) -> List[torch.Tensor]:
     dev = send[0].device
     tail = tuple(send[0].shape[1:])
     counts = torch.tensor([x.shape[0] for x in send], dtype=torch.int64)
-    all_counts = all_gather_tensor(counts.to(dev) if _backend() == "nccl" else counts).cpu().view(ws, ws)
+    all_counts = all_gather_tensor(counts).view(ws, ws)
     recv_counts = all_counts[:, get_rank()].tolist()
     flat = torch.cat([x.reshape(x.shape[0], -1) for x in send]) if send else torch.empty(0)
     width = int(np.prod(tail)) if tail else 1
     STATS.calls += 1
-    if _backend() == "nccl" and dev.type == "cuda":
-        out = torch.empty((sum(recv_counts), width), dtype=flat.dtype, device=dev)
-        dist.all_to_all_single(out, flat.reshape(-1, width).contiguous(), recv_counts, counts.tolist())
+    if _backend() == "nccl":
+        cdev = dev if dev.type == "cuda" else device_for_rank()
+        out = torch.empty((sum(recv_counts), width), dtype=flat.dtype, device=cdev)
+        dist.all_to_all_single(out, flat.reshape(-1, width).to(cdev).contiguous(), recv_counts, counts.tolist())
+        out = out.to(dev)
     else:
         out = torch.empty((sum(recv_counts), width), dtype=flat.dtype)
         dist.all_to_all_single(out, flat.reshape(-1, width).cpu().contiguous(), recv_counts, counts.tolist())

@@ -36,9 +36,16 @@ def _own_assignment_check(X, C, got, asg, k):
         assert bool((best - chosen <= 2.0 ** -15 * best.abs() + 1e-4).all()), "non-optimal assignment"
 
 
+@pytest.fixture(params=["v7", "v10"])
+def kernel(request, monkeypatch):
+    """Run a test on both fused kernels (v10 serves k <= 112; above that the call falls back to v7)."""
+    monkeypatch.setenv("ALINK_KMEANS_KERNEL", request.param)
+    return request.param
+
+
 @pytest.mark.parametrize("n,k", [(1, 1), (63, 3), (64, 16), (65, 17), (129, 100), (1000, 33), (4097, 100),
                                  (50000, 128), (300001, 100), (123457, 112), (70001, 8)])
-def test_v7_matches_own_assignment_reference(n, k):
+def test_v7_matches_own_assignment_reference(n, k, kernel):
     from alink_amd.ops import kmeans as K
     from alink_amd.ops import _lib
     assert _lib.available(), "HIP library must be built and loadable on the GPU box"
@@ -54,7 +61,7 @@ def test_v7_matches_own_assignment_reference(n, k):
 
 @pytest.mark.parametrize("n,k,grid", [(200, 7, 1), (49157, 100, 3), (33333, 64, 7), (640, 100, 2), (70000, 100, 256),
                                       (1000003, 128, 5), (129, 50, 1), (192, 50, 1), (257, 20, 2)])
-def test_v7_small_grid_long_loops(n, k, grid):
+def test_v7_small_grid_long_loops(n, k, grid, kernel):
     """Few workgroups -> long per-workgroup tile loops (ring warm-up, steady state, one-hot reuse, drain)."""
     from alink_amd.ops import kmeans as K
     X, C = _data(n, k, seed=11)
@@ -64,7 +71,7 @@ def test_v7_small_grid_long_loops(n, k, grid):
     _own_assignment_check(X, C, got, asg, k)
 
 
-def test_v7_without_assign_output_equals_with():
+def test_v7_without_assign_output_equals_with(kernel):
     from alink_amd.ops import kmeans as K
     X, C = _data(100003, 100, seed=4)
     a = K.assign_accumulate_hip(X, C)
@@ -73,7 +80,40 @@ def test_v7_without_assign_output_equals_with():
     assert torch.equal(a, b)
 
 
-def test_kernel_deterministic():
+@pytest.mark.parametrize("flags", [1, 2, 3])
+@pytest.mark.parametrize("n,k,grid", [(300001, 100, None), (49157, 97, 3), (4097, 16, None)])
+def test_v10_launch_variants_bit_identical(n, k, grid, flags, monkeypatch):
+    """Non-temporal loads (flag 1) and the 9-slot ring (flag 2) change only the load schedule: the sums are
+    bit-identical to the default launch."""
+    from alink_amd.ops import kmeans as K
+    X, C = _data(n, k, seed=9)
+    monkeypatch.setattr(K, "V10_FLAGS", 0)
+    a = K.assign_accumulate_hip(X, C, grid=grid)
+    monkeypatch.setattr(K, "V10_FLAGS", flags)
+    b = K.assign_accumulate_hip(X, C, grid=grid)
+    assert K.kernel_version(k) == "v10"
+    assert torch.equal(a, b)
+
+
+def test_v10_and_v7_agree():
+    """Same assignments (same distance MFMAs and argmax), sums equal up to fp32 summation order."""
+    import os
+    from alink_amd.ops import kmeans as K
+    X, C = _data(500000, 100, seed=5)
+    n = X.shape[0]
+    out = {}
+    for v in ("v7", "v10"):
+        os.environ["ALINK_KMEANS_KERNEL"] = v
+        asg = torch.empty((n,), dtype=torch.int32, device="cuda")
+        out[v] = (K.assign_accumulate_hip(X, C, assign_out=asg), asg)
+    del os.environ["ALINK_KMEANS_KERNEL"]
+    assert torch.equal(out["v7"][1], out["v10"][1])
+    assert torch.equal(out["v7"][0][:, 128], out["v10"][0][:, 128])
+    cnt = out["v7"][0][:, 128:129]
+    assert bool(((out["v7"][0][:, :128] - out["v10"][0][:, :128]).abs() <= 4e-6 * cnt * 8 + 1e-3).all())
+
+
+def test_kernel_deterministic(kernel):
     from alink_amd.ops import kmeans as K
     X, C = _data(200000, 100, seed=3)
     a = K.assign_accumulate_hip(X, C)

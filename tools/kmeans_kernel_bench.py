@@ -1,7 +1,14 @@
 #!/usr/bin/env python3
-"""Micro-benchmark of the fused KMeans assign+accumulate HIP kernel vs the PyTorch path.
+"""Micro-benchmark of the fused KMeans assign+accumulate HIP kernels (v7 / v10) on one GPU.
 
-python tools/kmeans_kernel_bench.py --rows 100000000 --k 100 --iters 10
+One data set, several launch configurations in one process (data generation of 1e8 rows is the slow part):
+
+python tools/kmeans_kernel_bench.py --rows 100000000 --k 100 --iters 10 \
+    --configs v7:0,v10:0,v10:1,v10:2 --modes 0,1,2 --sub-rows 12500000
+
+A config is ``kernel:flags`` (v7 flags = DMA variant bits 4-5, v10 flags = 1 non-temporal loads, 2 nine-slot
+ring); modes are 0 full, 1 load pipeline only, 2 compute only.  ``--sub-rows`` also times the first R rows
+(the per-rank shape of an 8-GPU job).  Prints one JSON line per (rows, config, mode).
 """
 import argparse
 import json
@@ -19,13 +26,13 @@ from alink_amd.ops import kmeans as K  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, default=100_000_000)
+    ap.add_argument("--sub-rows", type=str, default="", help="comma list of smaller row counts to time as well")
     ap.add_argument("--k", type=int, default=100)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--torch", action="store_true", help="also time the PyTorch path")
     ap.add_argument("--grid", type=int, default=None)
-    ap.add_argument("--load-only", action="store_true", help="time the LDS-DMA load pipeline alone")
-    ap.add_argument("--compute-only", action="store_true", help="time the compute alone (no loads)")
-    ap.add_argument("--var", type=int, default=0, help="v7 DMA variant (mode bits 4-5)")
+    ap.add_argument("--configs", type=str, default="v10:0")
+    ap.add_argument("--modes", type=str, default="0")
     a = ap.parse_args()
     dev = torch.device("cuda")
     n, d, k = a.rows, 128, a.k
@@ -38,36 +45,44 @@ def main():
         lab = torch.randint(0, k, (e - s,), device=dev, generator=g)
         X[s:e] = (centers[lab] + torch.randn(e - s, d, device=dev, generator=g)).to(torch.bfloat16)
     C = (centers + 0.5 * torch.randn(k, d, device=dev, generator=g)).double()
-    def run(Xs):
-        m = 2 if a.compute_only else 1 if a.load_only else 0
-        return K.assign_accumulate_hip(Xs, C, grid=a.grid, mode=m | (a.var << 4))
-    out = run(X)
-    torch.cuda.synchronize()
-    res = {"rows": n, "k": k, "load_only": a.load_only, "compute_only": a.compute_only, "var": a.var}
-    if a.torch:
-        ref0 = K.assign_accumulate_torch(X[:2_000_000], C)
-        got0 = run(X[:2_000_000].contiguous())
-        res["small_count_diff"] = float((got0[:, -1] - ref0[:, -1]).abs().sum().item())
-    times = []
-    for _ in range(a.iters):
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        out = run(X)
-        torch.cuda.synchronize()
-        times.append(time.perf_counter() - t0)
-    t = sorted(times)[len(times) // 2]
-    res.update({"hip_ms": t * 1e3, "hip_rows_per_s": n / t, "hip_GBps": n * d * 2 / t / 1e9,
-                "hip_TFLOPs_eff": 4.0 * n * d * 128 / t / 1e12})
+    row_list = [n] + [int(r) for r in a.sub_rows.split(",") if r]
+    ref_small = None
+    for rows in row_list:
+        Xs = X[:rows]
+        for cfg in a.configs.split(","):
+            ver, flags = cfg.split(":")
+            os.environ["ALINK_KMEANS_KERNEL"] = ver
+            for m in [int(v) for v in a.modes.split(",")]:
+                def run():
+                    return K.assign_accumulate_hip(Xs, C, grid=a.grid, mode=m | (int(flags) << 4))
+                out = run()
+                torch.cuda.synchronize()
+                res = {"rows": rows, "k": k, "kernel": K.kernel_version(k), "flags": int(flags), "mode": m}
+                if m == 0 and rows == n:
+                    if ref_small is None:
+                        ref_small = K.assign_accumulate_torch(X[:2_000_000], C)
+                    got0 = K.assign_accumulate_hip(X[:2_000_000], C, grid=a.grid, mode=int(flags) << 4)
+                    res["small_count_diff_vs_torch"] = float((got0[:, -1] - ref_small[:, -1]).abs().sum().item())
+                times = []
+                for _ in range(a.iters):
+                    torch.cuda.synchronize()
+                    t0 = time.perf_counter()
+                    out = run()
+                    torch.cuda.synchronize()
+                    times.append(time.perf_counter() - t0)
+                t = sorted(times)[len(times) // 2]
+                res.update({"ms": round(t * 1e3, 4), "rows_per_s": rows / t, "TBps": rows * d * 2 / t / 1e12,
+                            "min_ms": round(min(times) * 1e3, 4)})
+                print(json.dumps(res), flush=True)
+    os.environ.pop("ALINK_KMEANS_KERNEL", None)
     if a.torch:
         ref = K.assign_accumulate_torch(X, C)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         ref = K.assign_accumulate_torch(X, C)
         torch.cuda.synchronize()
-        tt = time.perf_counter() - t0
-        res.update({"torch_ms": tt * 1e3, "speedup_vs_torch": tt / t,
-                    "count_diff": float((out[:, -1] - ref[:, -1]).abs().sum().item())})
-    print(json.dumps(res))
+        print(json.dumps({"torch_ms": (time.perf_counter() - t0) * 1e3,
+                          "count_diff": float((out[:, -1] - ref[:, -1]).abs().sum().item())}))
 
 
 if __name__ == "__main__":
