@@ -54,74 +54,134 @@ class StreamEngine:
             queue.extend(sub for sub, _ in op._subscribers)
         return order
 
-    def _ckpt_path(self, conf):
+    def _fingerprint(self) -> str:
+        """Identity of the stream job a checkpoint belongs to: operator classes + params along the DAG order."""
+        import hashlib
+        h = hashlib.sha1()
+        for op in self._dag():
+            h.update(type(op).__name__.encode())
+            try:
+                h.update(op.getParams().toJson().encode())
+            except Exception:       # pragma: no cover - params that do not serialise still pin the class
+                pass
+        return h.hexdigest()
+
+    def _ckpt_files(self, conf):
+        """This rank's checkpoint files as {round: path}."""
         import os
-        os.makedirs(conf["dir"], exist_ok=True)
+        import re
         from ...parallel import comm
-        return os.path.join(conf["dir"], f"stream_ckpt_rank{comm.get_rank()}.pt")
+        os.makedirs(conf["dir"], exist_ok=True)
+        pat = re.compile(rf"stream_ckpt_rank{comm.get_rank()}_round(\d+)\.pt$")
+        out = {}
+        for f in os.listdir(conf["dir"]):
+            m = pat.match(f)
+            if m:
+                out[int(m.group(1))] = os.path.join(conf["dir"], f)
+        return out
 
-    def _save(self, conf, consumed):
+    def _save(self, conf, consumed, rnd, fp):
+        """Write this rank's state at micro-batch round ``rnd`` atomically and keep the last two rounds (so the
+        ranks can always agree on a round every rank has completely written, see ``_restore``)."""
         import os
         import torch
-        state = {"consumed": [int(c) for c in consumed],
+        from ...parallel import comm
+        state = {"round": int(rnd), "fingerprint": fp, "consumed": [int(c) for c in consumed],
                  "ops": {i: op._state_dict() for i, op in enumerate(self._dag()) if op._state_dict() is not None}}
-        path = self._ckpt_path(conf)
+        path = os.path.join(conf["dir"], f"stream_ckpt_rank{comm.get_rank()}_round{int(rnd)}.pt")
         torch.save(state, path + ".tmp")
-        os.replace(path + ".tmp", path)          # atomic: a crash mid-write keeps the previous checkpoint
+        os.replace(path + ".tmp", path)          # atomic: a crash mid-write keeps the previous checkpoints
+        files = self._ckpt_files(conf)
+        for r in sorted(files)[:-2]:
+            os.remove(files[r])
 
-    def _restore(self, conf):
-        import os
+    def _restore(self, conf, fp):
+        """Agree on the newest round every rank holds (MIN all-reduce of each rank's newest round), load it, and
+        return (consumed counts, round) — or None when some rank has no checkpoint (fresh start everywhere)."""
         import torch
-        path = self._ckpt_path(conf)
-        if not os.path.exists(path):
+        from ...parallel import comm
+        files = self._ckpt_files(conf)
+        latest = torch.tensor([max(files) if files else -1], dtype=torch.int64)
+        if comm.get_world_size() > 1:
+            comm.all_reduce(latest, "min")
+        rnd = int(latest.item())
+        if rnd < 0:
             return None
-        state = torch.load(path, weights_only=True)
+        if rnd not in files:
+            raise RuntimeError(f"stream checkpoint round {rnd} missing on rank {comm.get_rank()} ({conf['dir']})")
+        state = torch.load(files[rnd], weights_only=True)
+        if state.get("fingerprint") != fp:
+            raise RuntimeError(f"stream checkpoint in {conf['dir']} was written by a different stream job "
+                               "(operator DAG / params differ); remove it or use another directory")
         dag = self._dag()
         for i, st in state["ops"].items():
             dag[int(i)]._load_state_dict(st)
-        return state["consumed"]
+        return state["consumed"], rnd
 
     def run(self, checkpoint=None):
+        """Drive every source to exhaustion, one micro-batch per source per round.
+
+        With a checkpoint conf on a multi-rank job the rounds are a LOCKSTEP protocol: every round ends with one
+        MAX all-reduce of (any source still live, checkpoint due), a rank whose sources ended keeps emitting empty
+        micro-batches until every rank's have, and a checkpoint is written by all ranks at the same round — a
+        consistent cut (the reference's Flink checkpoint barrier, ``StreamOperator.java:216-239``)."""
         import time
+        import torch
+        from ...parallel import comm
         srcs = [s for s in self.sources if s._subscribers]
         its = [(s, s.batches()) for s in srcs]
         consumed = [0] * len(its)
+        lockstep = checkpoint is not None and comm.get_world_size() > 1
+        fp = self._fingerprint() if checkpoint is not None else None
+        rnd = 0
         if checkpoint is not None:
-            done = self._restore(checkpoint)
-            if done is not None:                 # replay: skip what the checkpoint already covers
+            got = self._restore(checkpoint, fp)
+            if got is not None:                  # replay: skip what the checkpoint already covers
+                done, rnd = got
                 for k, ((src, it), n) in enumerate(zip(its, done)):
                     for _ in range(n):
                         next(it, None)
                     consumed[k] = n
         last = time.time()
-        active = list(range(len(its)))
-        while active:
-            nxt = []
-            for k in active:
-                src, it = its[k]
-                try:
-                    mt = next(it)
-                except StopIteration:
-                    src._finish()
-                    continue
-                src._emit(mt)
-                consumed[k] += 1
-                nxt.append(k)
-            active = nxt
-            if checkpoint is not None and active:
-                every = checkpoint.get("every_batches")
-                due = (every is not None and sum(consumed) % every == 0) or \
-                    (time.time() - last) >= checkpoint["interval_s"]
-                if due:
-                    self._save(checkpoint, consumed)
-                    last = time.time()
+        ended = set()
+        while True:
+            live = False
+            for k, (src, it) in enumerate(its):
+                mt = None
+                if k not in ended:
+                    try:
+                        mt = next(it)
+                    except StopIteration:
+                        ended.add(k)
+                        if not lockstep:
+                            src._finish()
+                if mt is not None:
+                    src._emit(mt)
+                    consumed[k] += 1
+                    live = True
+                elif lockstep:
+                    src._emit(MTable.empty(src.getSchema()))
+            rnd += 1
+            due = checkpoint is not None and (
+                (checkpoint.get("every_batches") is not None and rnd % checkpoint["every_batches"] == 0)
+                or (time.time() - last) >= checkpoint["interval_s"])
+            if lockstep:
+                flags = comm.all_reduce(torch.tensor([int(live), int(due)], dtype=torch.int64), "max")
+                live, due = bool(flags[0]), bool(flags[1])
+            if not live:
+                break
+            if due:
+                self._save(checkpoint, consumed, rnd, fp)
+                last = time.time()
+        if lockstep:
+            for src, _ in its:
+                src._finish()
         for s in self.sinks:
             s._close()
         if checkpoint is not None and checkpoint.get("clear_on_finish", True):
             import os
-            p = self._ckpt_path(checkpoint)
-            if os.path.exists(p):
-                os.remove(p)
+            for f in self._ckpt_files(checkpoint).values():
+                os.remove(f)
         self.sources.clear()
         self.sinks.clear()
 

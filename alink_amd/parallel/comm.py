@@ -144,6 +144,13 @@ def init_distributed(backend: Optional[str] = None, timeout_s: float = 1800.0) -
 
 def shutdown():
     global _OBJ_GROUP
+    from . import oneshot
+    if oneshot._INSTANCE is not None and dist.is_available() and dist.is_initialized():
+        # peers may still be reading this rank's staging slot in their last one-shot call: drain every rank's
+        # stream, meet on the host group, then unmap / free
+        torch.cuda.synchronize(oneshot._INSTANCE.device)
+        dist.barrier(group=_OBJ_GROUP)
+    oneshot.reset()
     if dist.is_available() and dist.is_initialized():
         dist.destroy_process_group()
     _OBJ_GROUP = None
@@ -189,9 +196,9 @@ def _backend() -> str:
 _OPS = {"sum": "SUM", "max": "MAX", "min": "MIN", "prod": "PRODUCT"}
 
 
-def _oneshot_max() -> int:
+def _oneshot_max(backend: str) -> int:
     from . import oneshot
-    return oneshot.MAX_BYTES if oneshot.enabled() else -1
+    return oneshot.MAX_BYTES if oneshot.enabled(backend) else -1
 
 
 @_collective
@@ -205,9 +212,11 @@ def all_reduce(t: torch.Tensor, op: str = "sum") -> torch.Tensor:
     rop = getattr(dist.ReduceOp, _OPS[op.lower()])
     STATS.calls += 1
     STATS.bytes += t.numel() * t.element_size()
-    if t.is_cuda and _backend() == "nccl" and op.lower() in ("sum", "max", "min") and \
-            t.dtype in (torch.float32, torch.float64) and t.numel() * t.element_size() <= _oneshot_max():
-        # small buffers: one kernel over IPC-mapped peer memory (parallel/oneshot.py, K31), opt-in
+    be = _backend()
+    if t.is_cuda and op.lower() in ("sum", "max", "min") and t.dtype in (torch.float32, torch.float64) and \
+            t.numel() * t.element_size() <= _oneshot_max(be):
+        # small device buffers: one kernel over IPC-mapped peer memory (parallel/oneshot.py, K31) — default on
+        # RCCL jobs; on gloo jobs whose ranks share a GPU only when forced (ALINK_ONESHOT_ALLREDUCE=1)
         from . import oneshot
         inst = oneshot.get()
         if inst is not None:

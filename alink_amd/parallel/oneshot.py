@@ -6,10 +6,18 @@ all-reduce is then one kernel on the caller's stream: copy-in, release a sequenc
 the own flags, sum the P staging slots in rank order.  No RCCL call, no host round trip, bit-identical results
 on all ranks.
 
-Enabled with ``ALINK_ONESHOT_ALLREDUCE=1`` for device tensors of at most ``ALINK_ONESHOT_MAX_BYTES`` (default
-1 MiB) on a ``nccl`` job; ``comm.all_reduce`` falls back to RCCL for anything else.  Setup is collective and
-validated against RCCL on a probe buffer; if any rank fails, every rank disables the path (the decision is
-agreed by a MIN all-reduce, so ranks never diverge between the two implementations).
+Used by ``comm.all_reduce`` for device tensors of at most ``ALINK_ONESHOT_MAX_BYTES`` (default 1 MiB):
+
+* ``ALINK_ONESHOT_ALLREDUCE`` unset / ``auto`` (default): on ``nccl`` (RCCL) jobs;
+* ``1``: also on ``gloo`` jobs whose ranks hold device tensors (several ranks sharing a GPU — the multi-process
+  rehearsal of an 8-GPU job on one card; the IPC handles are real either way);
+* ``0``: never (RCCL / gloo for everything).
+
+Setup is collective and validated on a probe buffer against the exact rank-order sum; if any rank fails, every
+rank disables the path (the decision is agreed by a MIN all-reduce over the host group, so ranks never diverge
+between the two implementations).  A peer that does not arrive within ``ALINK_ONESHOT_TIMEOUT_S`` (300 s) makes
+the kernel write NaN and set an error word; the host reads that word back asynchronously after every call and
+raises on the next call (``ALINK_ONESHOT_CHECK=1``: synchronously, on the same call).
 """
 from __future__ import annotations
 
@@ -25,7 +33,8 @@ __all__ = ["OneShot", "get", "enabled", "MAX_BYTES"]
 
 MAX_BYTES = int(os.environ.get("ALINK_ONESHOT_MAX_BYTES", str(1 << 20)))
 BLOCKS = 32
-TIMEOUT_S = float(os.environ.get("ALINK_ONESHOT_TIMEOUT_S", "60"))
+TIMEOUT_S = float(os.environ.get("ALINK_ONESHOT_TIMEOUT_S", "300"))
+SYNC_CHECK = os.environ.get("ALINK_ONESHOT_CHECK", "0") == "1"
 _DT = {torch.float32: 0, torch.float64: 1}
 _OP = {"sum": 0, "max": 1, "min": 2}
 
@@ -59,6 +68,8 @@ class OneShot:
         self.peer_data = torch.tensor(bases, dtype=torch.int64, device=device)
         self.peer_flags = torch.tensor([b + self.flag_off for b in bases], dtype=torch.int64, device=device)
         self.err = torch.zeros(1, dtype=torch.int32, device=device)
+        self._err_host = torch.zeros(1, dtype=torch.int32, pin_memory=torch.cuda.is_available())
+        self._err_ev = None
         self.seq = 0
         self.calls = 0
 
@@ -93,13 +104,33 @@ class OneShot:
         self.calls += 1
         return out
 
+    def _raise_if_failed(self, value: int):
+        if value != 0:
+            self.err.zero_()
+            self._err_host.zero_()
+            self._err_ev = None
+            raise RuntimeError("one-shot all-reduce timed out waiting for a peer (results were poisoned with NaN)")
+
+    def check(self, wait: bool = False):
+        """Raise if an earlier call timed out.  Non-blocking by default: the error word of the previous call is
+        read back asynchronously (pinned copy + event) and examined once that copy has landed."""
+        if self._err_ev is not None and (wait or self._err_ev.query()):
+            self._err_ev.synchronize()
+            self._raise_if_failed(int(self._err_host[0]))
+            self._err_ev = None
+
     def all_reduce_(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
+        self.check()
         flat = t.reshape(-1)
         src = flat if flat.is_contiguous() else flat.contiguous()
         res = torch.empty_like(src)
         self.launch(src, res, op)
-        if self.calls % 256 == 0 and int(self.err.item()) != 0:
-            raise RuntimeError("one-shot all-reduce timed out waiting for a peer (results were poisoned with NaN)")
+        if SYNC_CHECK:
+            self._raise_if_failed(int(self.err.item()))
+        elif self._err_ev is None:
+            self._err_host.copy_(self.err, non_blocking=True)
+            self._err_ev = torch.cuda.Event()
+            self._err_ev.record(torch.cuda.current_stream(self.device))
         t.copy_(res.view_as(t))
         return t
 
@@ -115,8 +146,32 @@ _INSTANCE: Optional[OneShot] = None
 _TRIED = False
 
 
-def enabled() -> bool:
-    return os.environ.get("ALINK_ONESHOT_ALLREDUCE", "0") == "1"
+def mode() -> str:
+    v = os.environ.get("ALINK_ONESHOT_ALLREDUCE", "auto").lower()
+    return {"1": "force", "0": "off", "auto": "auto", "force": "force", "off": "off"}.get(v, "auto")
+
+
+def enabled(backend: str = "nccl") -> bool:
+    """Whether comm.all_reduce routes small device buffers through the one-shot kernel on this backend."""
+    m = mode()
+    return m == "force" or (m == "auto" and backend == "nccl")
+
+
+def _host_min(x: float) -> float:
+    """MIN all-reduce of one float over the host (gloo) group: valid on nccl and gloo jobs alike."""
+    import torch.distributed as dist
+    from . import comm
+    t = torch.tensor([x], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=comm.object_group())
+    return float(t.item())
+
+
+def reset():
+    """Drop the instance (tests; a new process group needs a new setup)."""
+    global _INSTANCE, _TRIED
+    if _INSTANCE is not None:
+        _INSTANCE.close()
+    _INSTANCE, _TRIED = None, False
 
 
 def get() -> Optional[OneShot]:
@@ -126,11 +181,11 @@ def get() -> Optional[OneShot]:
         return _INSTANCE
     _TRIED = True
     from . import comm
-    import torch.distributed as dist
     P, rank = comm.get_world_size(), comm.get_rank()
     dev = comm.device_for_rank()
     ok, inst, base, opened = 1.0, None, None, []
     handles = None
+    L = None
     try:
         L = _lib.require()
         _sigs(L)
@@ -162,21 +217,25 @@ def get() -> Optional[OneShot]:
             inst = OneShot(dev, P, rank, MAX_BYTES, bases, [base], opened)
         except Exception:
             ok = 0.0
-    flag = torch.tensor([ok], dtype=torch.float64, device=dev)
-    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-    if flag.item() < 1.0:
+    if _host_min(ok) < 1.0:
         if inst is not None:
             inst.close()
+        else:                       # failure paths: release what this rank did allocate / open
+            for q in opened:
+                L.alink_ar_ipc_close(ctypes.c_void_p(q))
+            if base is not None:
+                L.alink_ar_free(ctypes.c_void_p(base))
         return None
-    # validate against RCCL on a probe buffer before trusting the path
+    # validate on a probe buffer: the exact rank-order sum every rank can compute locally (integers in fp64)
     probe = torch.arange(1000, dtype=torch.float64, device=dev) * (rank + 1) + 0.25
-    ref = probe.clone()
-    dist.all_reduce(ref)
-    got = inst.all_reduce_(probe.clone())
-    good = torch.tensor([1.0 if torch.equal(got, ref) and int(inst.err.item()) == 0 else 0.0],
-                        dtype=torch.float64, device=dev)
-    dist.all_reduce(good, op=dist.ReduceOp.MIN)
-    if good.item() < 1.0:
+    ref = torch.arange(1000, dtype=torch.float64, device=dev) * (P * (P + 1) // 2) + 0.25 * P
+    try:
+        got = inst.all_reduce_(probe.clone())
+        torch.cuda.synchronize(dev)
+        good = 1.0 if torch.equal(got, ref) and int(inst.err.item()) == 0 else 0.0
+    except Exception:
+        good = 0.0
+    if _host_min(good) < 1.0:
         inst.close()
         return None
     _INSTANCE = inst

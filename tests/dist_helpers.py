@@ -253,6 +253,52 @@ def scenario_ftrl_uneven(out):
     out["model"], out["bids"] = _ftrl_run("SHARDED", 9, 2)
 
 
+def scenario_ftrl_ckpt(out):
+    """Lockstep stream checkpoint on P ranks (phase from ALINK_TEST_PHASE): ``ref`` runs through, ``crash`` dies
+    inside the 6th FTRL step on every rank, ``resume`` restarts from the agreed checkpoint round."""
+    import numpy as np
+    import pandas as pd
+    from alink_amd import (useLocalEnv, BatchOperator, StreamOperator, LogisticRegressionTrainBatchOp,
+                           FtrlTrainStreamOp, CollectStreamOp)
+    from alink_amd.operator.stream import onlinelearning as ol
+    phase = os.environ["ALINK_TEST_PHASE"]
+    os.environ["ALINK_STREAM_BATCH"] = "7"
+    useLocalEnv(1)
+    rng = np.random.default_rng(5)
+    X = rng.normal(size=(150, 4))
+    df = pd.DataFrame({f"f{i}": X[:, i] for i in range(4)})
+    df["label"] = (X @ np.array([1.0, -1.0, 0.5, 0.2]) > 0).astype(int)
+    schema = ", ".join(f"f{i} double" for i in range(4)) + ", label int"
+    cols = [f"f{i}" for i in range(4)]
+    model = LogisticRegressionTrainBatchOp().setFeatureCols(cols).setLabelCol("label").setMaxIter(3) \
+        .linkFrom(BatchOperator.fromDataframe(df.iloc[:40], schemaStr=schema))
+    ckdir = os.path.join(os.environ["ALINK_TEST_TMP"], "ck_" + ("ref" if phase == "ref" else "run"))
+    StreamOperator.setCheckPointConf(interval_s=1e9, directory=ckdir, every_batches=2)
+    snaps = []
+    FtrlTrainStreamOp(model).setFeatureCols(cols).setLabelCol("label").setTimeInterval(1e9) \
+        .setUpdateMode("SHARDED").linkFrom(StreamOperator.fromDataframe(df, schemaStr=schema)) \
+        .link(CollectStreamOp(snaps))
+    if phase == "crash":
+        orig = ol.FtrlTrainStreamOp._apply
+        calls = {"n": 0}
+
+        def boom(self, *a):
+            calls["n"] += 1
+            if calls["n"] > 5:
+                raise RuntimeError("injected crash")
+            return orig(self, *a)
+        ol.FtrlTrainStreamOp._apply = boom
+    try:
+        StreamOperator.execute()
+    except RuntimeError as e:
+        out["crashed"] = str(e)
+        out["files"] = sorted(os.listdir(ckdir))
+        return
+    last = max(r[0] for r in snaps)
+    out["model"] = [list(r[2:]) for r in snaps if r[0] == last]
+    out["left"] = sorted(os.listdir(ckdir))
+
+
 def scenario_sql(out):
     """Distributed relational ops: each rank returns its partition of every result."""
     import numpy as np

@@ -1,0 +1,79 @@
+"""Rank processes for tests/test_multiprocess_gpu.py: P processes sharing ONE MI355X (gloo host group, device
+tensors on cuda:0, collectives of small device buffers through the one-shot IPC kernel) — the rehearsal of an
+8-GPU job on a 1-GPU box.  Each rank writes <outdir>/<scenario>_<world>_<rank>.json."""
+import json
+import os
+import sys
+import traceback
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def _rank_tensor(r, n, dtype, seed):
+    import torch
+    g = torch.Generator().manual_seed(seed * 7919 + r)
+    return (torch.randn(n, generator=g, dtype=torch.float64) * (r + 1)).to(dtype)
+
+
+def scenario_oneshot(out):
+    """Bit-exact rank-order reductions through the one-shot kernel, several sizes / dtypes / ops."""
+    import torch
+    from alink_amd.parallel import comm, oneshot
+    comm.init_distributed()
+    ws, me = comm.get_world_size(), comm.get_rank()
+    dev = comm.device_for_rank()
+    checks = []
+    for seed, (n, dtype, op) in enumerate([(1, torch.float64, "sum"), (129 * 100, torch.float64, "sum"),
+                                           (5000, torch.float32, "sum"), (77777, torch.float64, "max"),
+                                           (3, torch.float32, "min"), (131072, torch.float64, "sum")]):
+        for rep in range(3):                      # the staging slots alternate with the sequence number
+            x = _rank_tensor(me, n, dtype, seed * 10 + rep).to(dev)
+            comm.all_reduce(x, op)
+            parts = [_rank_tensor(r, n, dtype, seed * 10 + rep) for r in range(ws)]
+            ref = parts[0].clone()
+            for p in parts[1:]:
+                ref = ref + p if op == "sum" else (torch.maximum(ref, p) if op == "max" else torch.minimum(ref, p))
+            checks.append(bool(torch.equal(x.cpu(), ref)))
+    inst = oneshot._INSTANCE
+    out["checks"] = checks
+    out["oneshot_calls"] = comm.STATS.oneshot
+    out["instance"] = inst is not None
+    out["backend"] = comm._backend()
+    out["peers_opened"] = len(inst.opened) if inst is not None else -1
+
+
+def scenario_kmeans(out):
+    """KMeans on bf16 [N,128] (v10 fused kernel) with the [k,129] all-reduce on the one-shot path."""
+    from alink_amd import useLocalEnv, KMeansTrainBatchOp, RandomVectorSourceBatchOp
+    from alink_amd.parallel import comm
+    env = useLocalEnv(1)
+    src = RandomVectorSourceBatchOp().setNumRows(200_003).setSize(128).setNumClusters(20).setClusterStd(1.0) \
+        .setCenterScale(4.0).setDtype("bf16").setSeed(17).setOutputCol("vec")
+    op = KMeansTrainBatchOp().setVectorCol("vec").setK(20).setMaxIter(12).setEpsilon(-1.0).setInitMode("RANDOM") \
+        .linkFrom(src)
+    rows = op.collect()
+    out["model"] = [[r[0], r[1]] for r in rows]
+    out["iterations"] = op.getTrainInfo()["iterations"]
+    out["oneshot_calls"] = comm.STATS.oneshot
+    out["backend"] = comm._backend()
+    out["device"] = str(env.device)
+
+
+def run(rank, world, port, scenario, outdir):
+    os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
+                       "LOCAL_WORLD_SIZE": str(world), "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    out = {}
+    try:
+        globals()["scenario_" + scenario](out)
+    except Exception:
+        out["error"] = traceback.format_exc()
+    with open(os.path.join(outdir, f"{scenario}_{world}_{rank}.json"), "w") as f:
+        json.dump(out, f)
+    from alink_amd.parallel import comm
+    comm.shutdown()
+
+
+if __name__ == "__main__":
+    run(int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), sys.argv[4], sys.argv[5])

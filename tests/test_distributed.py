@@ -197,6 +197,27 @@ def test_ftrl_uneven_micro_batches_lockstep(tmp_path):
     assert len(one["model"]) == len(two[0]["model"])
 
 
+def test_stream_checkpoint_lockstep_resume_two_ranks(tmp_path, monkeypatch):
+    """Multi-rank stream checkpoint: every rank saves at the same micro-batch round (a consistent cut), keeps the
+    last two rounds, and a restart agrees on the newest round EVERY rank holds (rank 1's newest file is deleted
+    here, as if it died before writing it) — the resumed model equals an uninterrupted run."""
+    monkeypatch.setenv("ALINK_TEST_PHASE", "ref")
+    ref = _run("ftrl_ckpt", 2, tmp_path)
+    monkeypatch.setenv("ALINK_TEST_PHASE", "crash")
+    crashed = _run("ftrl_ckpt", 2, tmp_path)
+    assert all("crashed" in o for o in crashed), crashed
+    ck = tmp_path / "ck_run"
+    r1 = sorted(ck.glob("stream_ckpt_rank1_round*.pt"), key=lambda p: int(p.stem.split("round")[1]))
+    r0 = sorted(ck.glob("stream_ckpt_rank0_round*.pt"), key=lambda p: int(p.stem.split("round")[1]))
+    assert len(r0) == 2 and len(r1) == 2, (r0, r1, crashed)   # the last two rounds are kept per rank
+    assert [p.name.split("_round")[1] for p in r0] == [p.name.split("_round")[1] for p in r1]
+    r1[-1].unlink()
+    monkeypatch.setenv("ALINK_TEST_PHASE", "resume")
+    resumed = _run("ftrl_ckpt", 2, tmp_path)
+    assert resumed[0]["model"] == resumed[1]["model"] == ref[0]["model"], (resumed, ref)
+    assert not list(ck.iterdir()) and not list((tmp_path / "ck_ref").iterdir())   # cleared after completed runs
+
+
 @pytest.mark.parametrize("world", [2, 4])
 def test_sql_relational_ops_partitioned_equal_single(tmp_path, world):
     """join / left join / groupBy / distinct / union / intersect / minus (hash-partitioned) and orderBy (range

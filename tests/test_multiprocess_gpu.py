@@ -1,0 +1,76 @@
+"""Collectives between real GPU processes: P ranks (2 and 4) share the box's MI355X, exchange real
+hipIpcGetMemHandle handles and reduce through the one-shot kernel (ops/csrc/allreduce.hip) — the path an 8-GPU
+RCCL job uses for its small BSP buffers (KMeans [k, d+1] sums, criterion scalars)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run(scenario, world, tmp_path, timeout=150):
+    port = _free_port()
+    env = dict(os.environ)
+    env["ALINK_ONESHOT_ALLREDUCE"] = "1"          # gloo host group + device tensors: force the one-shot path
+    env["ALINK_ONESHOT_TIMEOUT_S"] = "30"
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE"):
+        env.pop(k, None)
+    procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "mp_gpu_helpers.py"), str(r), str(world),
+                               str(port), scenario, str(tmp_path)], env=env) for r in range(world)]
+    try:
+        for p in procs:
+            p.wait(timeout=timeout)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    outs = []
+    for r in range(world):
+        with open(os.path.join(str(tmp_path), f"{scenario}_{world}_{r}.json")) as f:
+            o = json.load(f)
+        assert "error" not in o, o.get("error")
+        outs.append(o)
+    return outs
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_oneshot_between_processes_bit_exact(tmp_path, world):
+    outs = _run("oneshot", world, tmp_path)
+    for o in outs:
+        assert o["backend"] == "gloo" and o["instance"] and o["peers_opened"] == world - 1
+        assert all(o["checks"]), o["checks"]
+        assert o["oneshot_calls"] >= len(o["checks"])
+
+
+def test_kmeans_multiprocess_gpu_matches_one_rank(tmp_path):
+    one = _run("kmeans", 1, tmp_path)[0]
+    for world in (2, 4):
+        outs = _run("kmeans", world, tmp_path)
+        for o in outs:
+            assert o["iterations"] == one["iterations"]
+            assert o["oneshot_calls"] > 0
+            assert o["model"] == outs[0]["model"]            # bit-identical on every rank
+        # per-rank fp32 partial sums differ from the 1-rank partition: centroids agree to rounding (a near-tie
+        # row may flip between two centroids)
+        a = [json.loads(r[1]) for r in one["model"] if r[0] > 0]
+        b = [json.loads(r[1]) for r in outs[0]["model"] if r[0] > 0]
+        assert len(a) == len(b)
+        for x, y in zip(a, b):
+            assert abs(x["weight"] - y["weight"]) <= max(2.0, 1e-4 * x["weight"])
+            np.testing.assert_allclose(np.asarray(x["vec"]["data"]), np.asarray(y["vec"]["data"]), rtol=1e-4,
+                                       atol=1e-4)
