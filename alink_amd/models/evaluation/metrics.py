@@ -198,8 +198,10 @@ def _binary_detail_native(labels_col, details, label_array: List[str]):
         return None
     labs = [None if l is None else str(l) for l in labels_col]
     lset = set(label_array)
-    keep_idx = [i for i, (l, d) in enumerate(zip(labs, details)) if l is not None and d is not None and l in lset]
-    dets = [details[i] for i in keep_idx]
+    # parse and check EVERY non-null (label, detail) row, as the JSON loop does, so both paths accept and
+    # reject the same inputs; only then keep the rows whose label is one of the two
+    nn_idx = [i for i, (l, d) in enumerate(zip(labs, details)) if l is not None and d is not None]
+    dets = [details[i] for i in nn_idx]
     if any(not isinstance(d, str) for d in dets):
         return None
     parsed = _native.parse_binary_detail(dets, label_array[0], label_array[1])
@@ -209,6 +211,9 @@ def _binary_detail_native(labels_col, details, label_array: List[str]):
     if not (np.all((p0 >= 0.0) & (p0 <= 1.0) & (p1 >= 0.0) & (p1 <= 1.0))
             and np.all(np.abs(p0 + p1 - 1.0) < PROB_SUM_EPS)):
         return None
+    sel = np.array([labs[i] in lset for i in nn_idx], dtype=bool)
+    keep_idx = [i for i, m in zip(nn_idx, sel) if m]
+    p0, p1 = p0[sel], p1[sel]
     is_pos = np.array([labs[i] == label_array[0] for i in keep_idx], dtype=bool)
     pl = np.where(is_pos, p0, p1)
     terms = -np.log(np.clip(pl, LOG_LOSS_EPS, 1 - LOG_LOSS_EPS))

@@ -36,3 +36,16 @@ def test_native_detail_rejects_other_forms():
     assert _native.parse_binary_detail(['{"a":x,"b":0.5}'], "a", "b") is None
     p0, p1 = _native.parse_binary_detail(['{"a":0.25,"b":0.75}', ' { "b" : 1e-3 , "a" : 0.999 } '], "a", "b")
     assert list(p0) == [0.25, 0.999] and list(p1) == [0.75, 1e-3]
+
+
+@pytest.mark.skipif(_native.lib is None, reason="native runtime not built")
+def test_native_and_json_paths_reject_the_same_rows(monkeypatch):
+    """A malformed detail on a row whose label is NOT one of the two still fails (the JSON loop parses every
+    non-null row), whichever path runs."""
+    labs, dets = _data(200, 1)
+    labs[3], dets[3] = "zzz", '{"a":0.5,"b":0.25,"c":0.25}'
+    with pytest.raises(ValueError):
+        M.binary_summary(labs, dets, ["a", "b"])
+    monkeypatch.setattr(M, "_binary_detail_native", lambda *a: None)
+    with pytest.raises(ValueError):
+        M.binary_summary(labs, dets, ["a", "b"])

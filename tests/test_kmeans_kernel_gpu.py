@@ -80,11 +80,11 @@ def test_v7_without_assign_output_equals_with(kernel):
     assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("flags", [1, 2, 3])
+@pytest.mark.parametrize("flags", [1])
 @pytest.mark.parametrize("n,k,grid", [(300001, 100, None), (49157, 97, 3), (4097, 16, None)])
 def test_v10_launch_variants_bit_identical(n, k, grid, flags, monkeypatch):
-    """Non-temporal loads (flag 1) and the 9-slot ring (flag 2) change only the load schedule: the sums are
-    bit-identical to the default launch."""
+    """The load cache policy (flag 1: default policy instead of non-temporal) changes only the load schedule:
+    the sums are bit-identical to the default launch."""
     from alink_amd.ops import kmeans as K
     X, C = _data(n, k, seed=9)
     monkeypatch.setattr(K, "V10_FLAGS", 0)
