@@ -95,8 +95,10 @@ KERNEL_VERSIONS = ("v7", "v10")
 # v7 variant (csrc/kmeans_v7.hip VAR): 0 = all 8 waves stage the tile ring; 1 (default) = the accumulate waves
 # stage it all, so the distance waves (the critical role) carry no LDS-DMA issue cost or vmcnt waits
 V7_VAR = int(os.environ.get("ALINK_KMEANS_V7_VAR", "1"))
-# v10 launch flags (csrc/kmeans_v10.hip mode bit 4): 1 = default-policy X loads instead of non-temporal
-V10_FLAGS = int(os.environ.get("ALINK_KMEANS_V10_FLAGS", "0"))
+# v10 launch flags (csrc/kmeans_v10.hip mode bit 4): 1 (default) = default-policy X loads, 0 = non-temporal.
+# Under the full kernel the default policy measured 2-5 % faster on every box (profiles/kmeans_v10_r3.txt),
+# although the load pipeline alone streams faster with nt
+V10_FLAGS = int(os.environ.get("ALINK_KMEANS_V10_FLAGS", "1"))
 V10_KMAX = 112
 
 

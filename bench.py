@@ -104,19 +104,29 @@ def main():
     live_k = int(op._queue.final_contexts[0].getObj("k"))
     comm_bytes = sum(s["comm_bytes"] for s in stats) / max(1, len(stats))
 
-    # ---- convergence runs (epsilon 1e-4): reference default initSteps=2, and initSteps=5 ----
+    # ---- convergence runs (epsilon 1e-4): reference default initSteps=2, initSteps=5, and initSteps=2 with the
+    # reference's own k-means++ seeding rule on the k-means|| candidates (ALINK_KMEANS_SEEDING=reference) ----
     iters, conv = None, {}
     if a.converge_iters > 0:
-        for steps in (2, 5):
+        for tag, steps, seeding in (("initSteps2", 2, None), ("initSteps5", 5, None),
+                                    ("reference_seeding", 2, "reference")):
+            old = os.environ.get("ALINK_KMEANS_SEEDING")
+            if seeding is not None:
+                os.environ["ALINK_KMEANS_SEEDING"] = seeding
             t_c = time.perf_counter()
             op2 = KMeansTrainBatchOp().setVectorCol("vec").setK(a.k).setMaxIter(a.converge_iters) \
                 .setInitSteps(steps)
             op2.linkFrom(TableSourceBatchOp(data))
             info = op2.getTrainInfo()
+            if seeding is not None:
+                if old is None:
+                    os.environ.pop("ALINK_KMEANS_SEEDING", None)
+                else:
+                    os.environ["ALINK_KMEANS_SEEDING"] = old
             shift = (info["max_shift"] or [None])[-1]
-            conv[f"initSteps{steps}"] = {"iters": info["iterations"], "wall_s": time.perf_counter() - t_c,
-                                         "final_max_shift": shift,
-                                         "converged": shift is not None and shift < 1e-4}
+            conv[tag] = {"iters": info["iterations"], "wall_s": time.perf_counter() - t_c,
+                         "final_max_shift": shift, "converged": shift is not None and shift < 1e-4,
+                         "seeding": seeding or "greedy k-means++ (default)"}
         iters = conv["initSteps2"]["iters"]
 
     rows_per_s = a.rows * a.steps / elapsed
@@ -139,7 +149,9 @@ def main():
         "rows_per_s_per_gpu": rows_per_s / env.world_size,
         "iters_to_converge": iters,
         "iters_to_converge_setting": "epsilon 1e-4, k-means|| initSteps=2 (reference default); initSteps=5 "
-                                     "under convergence.initSteps5",
+                                     "under convergence.initSteps5; the reference's sampled k-means++ seeding "
+                                     "under convergence.reference_seeding",
+        "iters_to_converge_reference_seeding": conv.get("reference_seeding", {}).get("iters"),
         "convergence": conv,
         "iters_to_converge_default_init": conv.get("initSteps2", {}).get("iters"),
         "converged_default_init": conv.get("initSteps2", {}).get("converged"),
