@@ -12,7 +12,7 @@ from typing import List, Optional, Sequence
 import numpy as np
 
 __all__ = ["lib", "parse_csv_lines", "murmur3_utf16", "parse_dense_vectors", "ftrl_update_csr",
-           "ftrl_partial_margin", "ftrl_shard_update", "parse_binary_detail"]
+           "ftrl_partial_margin", "ftrl_shard_update", "parse_binary_detail", "java_double_join"]
 
 # ALINK_NATIVE_LIB points at another build of the same sources (e.g. the AddressSanitizer build of
 # tools/asan_host.py)
@@ -29,6 +29,8 @@ if os.path.exists(_PATH):
         lib.alink_ftrl_partial_margin.restype = ctypes.c_int
         lib.alink_ftrl_shard_update.restype = ctypes.c_int
         lib.alink_parse_binary_detail.restype = ctypes.c_int64
+        if hasattr(lib, "alink_java_double_join"):
+            lib.alink_java_double_join.restype = ctypes.c_int64
     except OSError:
         lib = None
 
@@ -109,6 +111,16 @@ def murmur3_utf16(strings: Sequence[str], seed: int = 0) -> Optional[np.ndarray]
     lib.alink_murmur3_utf16_batch(_ptr(chars), _ptr(off), ctypes.c_int64(len(units)), ctypes.c_uint32(seed),
                                   _ptr(out))
     return out
+
+
+def java_double_join(x) -> Optional[str]:
+    """``",".join(java_double_str(v) for v in x)`` for a float array, in C++ (or None without the library)."""
+    if lib is None or getattr(lib, "alink_java_double_join", None) is None:
+        return None
+    a = np.ascontiguousarray(np.asarray(x, dtype=np.float64))
+    buf = np.empty(26 * max(a.size, 1) + 16, dtype=np.uint8)     # no zero fill
+    n = lib.alink_java_double_join(_ptr(a), ctypes.c_int64(a.size), _ptr(buf))
+    return buf[:n].tobytes().decode("ascii")
 
 
 def parse_binary_detail(strings: Sequence[str], key0: str, key1: str):

@@ -263,3 +263,81 @@ int64_t alink_parse_binary_detail(const char* buf, const int64_t* off, int64_t n
 int alink_native_version() { return 1; }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------------------------------------------
+// java.lang.Double.toString for arrays (model snapshots: 1e6 FTRL coefficients, GLM / linear model vectors).
+// Digits are the shortest round-trip decimal (std::to_chars, the digits Python's repr gives the reference
+// formatter common/javafmt.py:java_double_str); layout per the JVM rules: plain decimal with at least one
+// fractional digit for |x| in [1e-3, 1e7), else d.dddE<n>.  Writes "v0,v1,...,vn-1" (no brackets) into out
+// (capacity >= 26 * n) and returns the length.
+// ---------------------------------------------------------------------------------------------------------------
+#include <charconv>
+#include <vector>
+#include <cmath>
+#include <cstring>
+
+static int java_double_to(double x, char* out) {
+    if (std::isnan(x)) { std::memcpy(out, "NaN", 3); return 3; }
+    if (std::isinf(x)) {
+        if (x > 0) { std::memcpy(out, "Infinity", 8); return 8; }
+        std::memcpy(out, "-Infinity", 9); return 9;
+    }
+    int p = 0;
+    if (x == 0.0) {
+        if (std::signbit(x)) out[p++] = '-';
+        std::memcpy(out + p, "0.0", 3);
+        return p + 3;
+    }
+    if (x < 0) out[p++] = '-';
+    const double ax = std::fabs(x);
+    char buf[40];
+    const auto res = std::to_chars(buf, buf + sizeof(buf), ax, std::chars_format::scientific);
+    const char* e = static_cast<const char*>(std::memchr(buf, 'e', (size_t)(res.ptr - buf)));
+    char digits[24];
+    int nd = 0;
+    digits[nd++] = buf[0];
+    for (const char* c = buf + 2; c < e; ++c) digits[nd++] = *c;     // after "d."
+    while (nd > 1 && digits[nd - 1] == '0') --nd;
+    int ex = 0;
+    {
+        const char* c = e + 1;
+        bool neg = false;
+        if (*c == '-') { neg = true; ++c; } else if (*c == '+') { ++c; }
+        for (; c < res.ptr; ++c) ex = ex * 10 + (*c - '0');
+        if (neg) ex = -ex;
+    }
+    const int point = ex + 1;   // value = 0.digits * 10^point
+    if (ax >= 1e-3 && ax < 1e7) {
+        if (point <= 0) {
+            out[p++] = '0'; out[p++] = '.';
+            for (int i = 0; i < -point; ++i) out[p++] = '0';
+            for (int i = 0; i < nd; ++i) out[p++] = digits[i];
+        } else if (point >= nd) {
+            for (int i = 0; i < nd; ++i) out[p++] = digits[i];
+            for (int i = nd; i < point; ++i) out[p++] = '0';
+            out[p++] = '.'; out[p++] = '0';
+        } else {
+            for (int i = 0; i < point; ++i) out[p++] = digits[i];
+            out[p++] = '.';
+            for (int i = point; i < nd; ++i) out[p++] = digits[i];
+        }
+        return p;
+    }
+    out[p++] = digits[0];
+    out[p++] = '.';
+    if (nd > 1) for (int i = 1; i < nd; ++i) out[p++] = digits[i];
+    else out[p++] = '0';
+    out[p++] = 'E';
+    const auto r2 = std::to_chars(out + p, out + p + 8, ex);
+    return (int)(r2.ptr - out);
+}
+
+extern "C" int64_t alink_java_double_join(const double* x, int64_t n, char* out) {
+    // one thread: ~90 ns per value (1e6 coefficients ~0.1 s); an OpenMP split measured slower on the 8-CPU host
+    int64_t p = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        if (i) out[p++] = ',';
+        p += java_double_to(x[i], out + p);
+    }
+    return p;
+}

@@ -153,6 +153,12 @@ def gson_dumps(v: Any, java_map_order: bool = True) -> str:
     if isinstance(v, dict):
         keys = java_hashmap_order(list(v.keys())) if java_map_order else list(v.keys())
         return "{" + ",".join(_gson_escape(str(k)) + ":" + gson_dumps(v[k], java_map_order) for k in keys) + "}"
+    if isinstance(v, np.ndarray) and v.dtype.kind == "f" and v.ndim == 1 and v.size >= 64:
+        # large float vectors (model coefficients): the host C++ formatter, same digits and layout
+        from .. import _native
+        body = _native.java_double_join(v)
+        if body is not None:
+            return "[" + body + "]"
     if isinstance(v, (list, tuple)) or (hasattr(v, "tolist") and not isinstance(v, str)):
         seq = v.tolist() if hasattr(v, "tolist") else v
         return "[" + ",".join(gson_dumps(e, java_map_order) for e in seq) + "]"

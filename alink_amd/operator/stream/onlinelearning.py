@@ -15,6 +15,7 @@ Multi-rank: see ``FtrlTrainStreamOp`` (replicated SEQUENTIAL, feature-sharded SH
 """
 from __future__ import annotations
 
+import os
 import time
 from typing import List, Optional
 
@@ -73,18 +74,26 @@ class FtrlTrainStreamOp(StreamOperator):
       replicated coefficient vector, so the model equals the 1-rank model on the same global batch sequence.
     * ``SHARDED``: the reference's distributed design (``FtrlTrainStreamOp.java:72-85`` split info,
       ``:174-267`` SplitVector, ``:396-420`` partial margins, ``:488-567`` keyed reduce + feedback) at micro-batch
-      granularity: rank r owns the coefficient range [lo_r, hi_r); per step the ranks all-gather the micro-batch,
-      compute partial margins on their range (HIP kernel on GPU), all-reduce them, and replay their coordinates
-      in sample order with the margins of the step start — the reference's feedback staleness bounded to one
-      micro-batch.  Deterministic and independent of the number of ranks.
+      granularity: rank r owns the coefficient range [lo_r, hi_r).  Per step every rank splits its OWN samples by
+      coefficient range and sends shard j only the entries in j's range (one all-to-all: each rank receives
+      ~1/P of the global batch's nonzeros); each shard computes partial margins of the global batch on its range
+      (HIP kernel on GPU), the margins are summed per sample (all-reduce), and each shard replays its
+      coordinates in global sample order with the margins of the step start — the reference's feedback
+      staleness bounded to one micro-batch.  Deterministic and independent of the number of ranks.
+    * ``DATA_PARALLEL``: replicated coefficients, the ranks' micro-batches form one global step: every rank
+      scores its own samples, the per-coordinate gradient sums (g, g^2) are all-reduced as one dense buffer
+      (RCCL), and every rank applies the same mini-batch FTRL-proximal update (n += sum g^2, z += sum g - sigma w).
+      Throughput grows with P; per-sample ordering inside a micro-batch is not kept (a different, mini-batch
+      rule than SEQUENTIAL / SHARDED).
     * ``HOGWILD`` (single GPU): ``ops/csrc/ftrl.hip``, one wave per sample, exact atomic n/z, prox pass.
 
     Every step (and every snapshot decision) is a collective over the ranks, so ranks with different numbers of
     micro-batches stay in lockstep: a rank whose stream ended keeps joining steps with an empty batch until all
     ranks are done.  Snapshots: at the first step, whenever any rank's ``timeInterval`` elapsed, and at the end.
     """
-    EXTRA_PARAMS = [ParamInfo("updateMode", str, "SEQUENTIAL, SHARDED (feature-sharded micro-batch) or HOGWILD "
-                                                 "(GPU, one wave per sample)", default="SEQUENTIAL")]
+    EXTRA_PARAMS = [ParamInfo("updateMode", str, "SEQUENTIAL, SHARDED (feature-sharded micro-batch), DATA_PARALLEL "
+                                                 "(replicated, all-reduced mini-batch gradients) or HOGWILD (GPU, "
+                                                 "one wave per sample)", default="SEQUENTIAL")]
 
     def __init__(self, model=None, params: Optional[Params] = None, **kw):
         if isinstance(model, Params):
@@ -120,9 +129,10 @@ class FtrlTrainStreamOp(StreamOperator):
         self._feat_cols = _pget(p, "featureCols")
         self._vsize = _pget(p, "vectorSize")
         self._mode = str(_pget(p, "updateMode", "SEQUENTIAL")).upper()
-        if self._mode not in ("SEQUENTIAL", "SHARDED", "HOGWILD"):
+        if self._mode not in ("SEQUENTIAL", "SHARDED", "DATA_PARALLEL", "HOGWILD"):
             raise ValueError(f"unknown updateMode {self._mode}")
         self._ws, self._rank = comm.get_world_size(), comm.get_rank()
+        self.recv_nnz = []          # SHARDED: nonzeros this shard received per step (observability / tests)
         if self._mode == "HOGWILD" and self._ws > 1:
             raise ValueError("updateMode HOGWILD is single-rank; use SHARDED for P > 1")
         # SEQUENTIAL keeps its state on the host (the rule is a serial loop); the others on the rank's GPU
@@ -202,22 +212,97 @@ class FtrlTrainStreamOp(StreamOperator):
         import torch
         csr = self._local_csr(mt) if mt is not None else None
         due = time.time() - self._t0 > self._interval
-        flags = torch.tensor([0 if csr is None else 1, 1 if due else 0], dtype=torch.int64)
+        nloc = 0 if csr is None else int(csr[0].numel() - 1)
+        info = torch.tensor([[0 if csr is None else 1, 1 if due else 0, nloc]], dtype=torch.int64)
         if self._ws > 1:
-            flags = comm.all_reduce(flags.to(self._comm_dev()), "max").cpu()
-        active, due = bool(flags[0]), bool(flags[1])
+            info = comm.all_gather_tensor(info)                   # [P, 3]: live, due, samples per rank
+        active, due = bool(info[:, 0].max()), bool(info[:, 1].max())
+        counts = [int(c) for c in info[:, 2].tolist()]
         if not active:
             return False
         if self._first:
             self._snapshot()
             self._first = False
-        batch = self._gather(csr) if self._ws > 1 else csr
-        if batch is not None and batch[0].shape[0] > 1:
-            self._apply(*batch)
+        if self._mode == "DATA_PARALLEL":
+            self._dp_step(csr)
+        elif self._ws == 1:
+            if csr is not None and csr[0].shape[0] > 1:
+                self._apply(*csr)
+        elif self._mode == "SHARDED" and os.environ.get("ALINK_FTRL_SHARDED_EXCHANGE", "split") != "allgather":
+            self._sharded_step(csr, counts)
+        else:                           # SEQUENTIAL (and SHARDED's all-gather exchange, kept for comparison)
+            batch = self._gather(csr)
+            if batch is not None and batch[0].shape[0] > 1:
+                self._apply(*batch)
         if due:
             self._t0 = time.time()
             self._snapshot()
         return True
+
+    def _sharded_step(self, csr, counts):
+        """SplitVector exchange (``FtrlTrainStreamOp.java:174-267``): this rank's samples split by coefficient
+        range, shard j receiving only the entries in [lo_j, hi_j) (one all-to-all), then partial margins over the
+        global batch, a per-sample margin all-reduce and the in-order replay of the owned coordinates."""
+        import torch
+        P = self._ws
+        per = -(-self._dim // P)
+        cd = self._comm_dev()
+        offset = sum(counts[:self._rank])
+        G = sum(counts)
+        if csr is None:
+            send = [torch.zeros((0, 3), dtype=torch.float64, device=cd) for _ in range(P)]
+            lab = torch.zeros(0, dtype=torch.float64, device=cd)
+        else:
+            indptr, idx, val, lab = (t.to(cd) for t in csr)
+            rows = torch.repeat_interleave(torch.arange(indptr.numel() - 1, device=cd, dtype=torch.int64) + offset,
+                                           indptr[1:] - indptr[:-1])
+            owner = idx.to(torch.int64) // per
+            ent = torch.stack([rows.to(torch.float64), idx.to(torch.float64), val.to(torch.float64)], 1)
+            order = torch.argsort(owner, stable=True)            # by destination, sample order kept inside
+            ent = ent[order]
+            split = torch.bincount(owner, minlength=P).tolist()
+            send = list(torch.split(ent, split))
+        recv = comm.all_to_all_tensors(send)                     # from every source rank, in rank order
+        ent = torch.cat(recv) if recv else torch.zeros((0, 3), dtype=torch.float64, device=cd)
+        self.recv_nnz.append(int(ent.shape[0]))
+        glab = comm.all_gather_varlen(lab.to(torch.float64))      # labels of the global batch, rank order
+        grow = ent[:, 0].to(torch.int64)
+        gptr = torch.zeros(G + 1, dtype=torch.int64, device=cd)
+        if ent.shape[0]:
+            torch.cumsum(torch.bincount(grow, minlength=G), 0, out=gptr[1:])
+        gidx = ent[:, 1].to(torch.int32).contiguous()
+        gval = ent[:, 2].contiguous()
+        dev = self._dev
+        gptr, gidx, gval, glab = (t.to(dev) for t in (gptr, gidx, gval, glab))
+        a, b, l1, l2 = self._alpha, self._beta, self._l1, self._l2
+        w, n, z = self._state
+        if isinstance(w, torch.Tensor):
+            from ...ops.ftrl import ftrl_partial_margin_hip, ftrl_shard_update_hip
+            margin = ftrl_partial_margin_hip(gptr, gidx, gval, w, self._lo, self._hi)
+            margin = comm.all_reduce(margin.to(cd), "sum").to(dev)
+            err = (torch.sigmoid(margin) - glab).contiguous()
+            ftrl_shard_update_hip(gptr, gidx, gval, err, w, n, z, self._lo, self._hi, a, b, l1, l2)
+        else:
+            args = (gptr.numpy(), gidx.numpy(), gval.numpy())
+            margin = torch.from_numpy(_native.ftrl_partial_margin(*args, w, self._lo, self._hi))
+            margin = comm.all_reduce(margin, "sum")
+            err = (1.0 / (1.0 + np.exp(-margin.numpy()))) - glab.numpy()
+            _native.ftrl_shard_update(*args, err, w, n, z, self._lo, self._hi, a, b, l1, l2)
+
+    def _dp_step(self, csr):
+        """DATA_PARALLEL: local scoring, one dense all-reduce of the per-coordinate (sum g, sum g^2), identical
+        mini-batch FTRL-proximal update on every rank (``ops/ftrl.py``)."""
+        import torch
+        from ...ops.ftrl import ftrl_dp_gradients, ftrl_dp_update
+        w, n, z = (a if isinstance(a, torch.Tensor) else torch.from_numpy(a) for a in self._state)
+        dev = w.device
+        if csr is not None and csr[0].numel() > 1:
+            gq, _ = ftrl_dp_gradients(*(t.to(dev) for t in csr), w)
+        else:
+            gq = torch.zeros((2, self._dim), dtype=torch.float64, device=dev)
+        if self._ws > 1:
+            gq = comm.all_reduce(gq.to(self._comm_dev()), "sum").to(dev)
+        ftrl_dp_update(gq, w, n, z, self._alpha, self._beta, self._l1, self._l2)
 
     def _comm_dev(self):
         import torch

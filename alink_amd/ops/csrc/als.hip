@@ -205,23 +205,151 @@ __device__ __forceinline__ void add_reg(double (&a)[RP], int lane, int r, double
   }
 }
 
-// light rows: one wave builds and solves the whole system
+// ---------------------------------------------------------------------------------------------------------------
+// Light rows, v2: one 64-lane wave per row, lane i = row i of the system, four rows per 256-thread workgroup.
+//   Gram:  the neighbour factors are loaded 8 rows at a time (one coalesced fp32 load per lane each), staged as
+//          fp64 in the wave's LDS slice and read back as broadcast ds_read_b128 pairs: a_i[j] += c_t y_i y_j is
+//          one fp64 FMA per entry with no cross-lane moves (v1 paid two v_readlane per entry).
+//   Solve: Gauss-Jordan elimination WITHOUT pivoting on the SPD system (the trailing block stays symmetric, so
+//          the pivot row's trailing part equals the pivot column: one ds_write_b64 per lane broadcasts it).  Every
+//          lane i != k eliminates column k from its row (a_i[j] -= (a_i[k]/a_kk) a_k[j], j > k) and its rhs; after
+//          RP steps the system is diagonal and x_i = v_i / a_ii — no back substitution, no per-entry readlane
+//          chain (v1's register Cholesky ran at 1 wave per SIMD, latency-bound on v_readlane hazards).
+//   Precision: fp64 throughout (reference NormalEquation + LAPACK dposv are fp64).  A non-positive pivot flags
+//   the row for the host pinv fallback.
+// ---------------------------------------------------------------------------------------------------------------
+constexpr int GJ_WAVES = 4;
+constexpr int GJ_NB = 2;     // LDS rows per wave (neighbour staging double buffer; the GJ pivot row uses row 0)
+
 template <int RP>
-__global__ __launch_bounds__(64) void als_fused_solve(const int64_t* __restrict__ indptr,
-                                                      const int32_t* __restrict__ nbr,
-                                                      const float* __restrict__ rating, const float* __restrict__ Y,
-                                                      int r, int implicit, float alpha, const double* __restrict__ reg,
-                                                      const double* __restrict__ YtY, const int64_t* __restrict__ rows,
-                                                      float* __restrict__ X, int32_t* __restrict__ status) {
-  const int64_t row = rows != nullptr ? rows[blockIdx.x] : (int64_t)blockIdx.x;
-  const int lane = threadIdx.x;
+__device__ __forceinline__ void lds_wave_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// a[j] += coef * buf[j] for j in [j0, RP) (j0 and RP compile-time after unrolling): broadcast ds_read_b128 in
+// batches of 8 entries, the next batch's reads issued before this batch's FMAs, scheduling fences between batches
+// (at most 32 VGPRs of reads in flight next to the 2*RP of the row)
+template <int RP>
+__device__ __forceinline__ void axpy_bcast(double (&a)[RP], double coef, const double* buf, int j0) {
+  constexpr int NB = 8;
+  const int jb0 = j0 & ~(NB - 1);
+  double2 q[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) q[u] = *reinterpret_cast<const double2*>(buf + jb0 + 2 * u);
+#pragma unroll
+  for (int jb = 0; jb < RP; jb += NB) {
+    if (jb < jb0) continue;
+    double2 n[4];
+    if (jb + NB < RP) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) n[u] = *reinterpret_cast<const double2*>(buf + jb + NB + 2 * u);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      // the empty volatile asm pins each update here: without it the compiler defers updates of far columns
+      // to their use, keeping every step's broadcast values live (hundreds of VGPRs, scratch spills)
+      if (jb + 2 * u >= j0) {
+        a[jb + 2 * u] = fma(coef, q[u].x, a[jb + 2 * u]);
+        asm volatile("" : "+v"(a[jb + 2 * u]));
+      }
+      if (jb + 2 * u + 1 >= j0) {
+        a[jb + 2 * u + 1] = fma(coef, q[u].y, a[jb + 2 * u + 1]);
+        asm volatile("" : "+v"(a[jb + 2 * u + 1]));
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (jb + NB < RP) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) q[u] = n[u];
+    }
+  }
+}
+
+// Gram of neighbours [s, e) for one row, lane i = row i (a[j] += c y_i y_j, v += w y_i): neighbour t's factor row
+// (one coalesced fp32 load, prefetched one neighbour ahead) is staged as fp64 in one of two LDS rows and read
+// back as broadcast pairs
+template <int RP>
+__device__ __forceinline__ void gram_lds(const int32_t* __restrict__ nbr, const float* __restrict__ rating,
+                                         const float* __restrict__ Y, int r, int implicit, float alpha, int64_t s,
+                                         int64_t e, int lane, double (&a)[RP], double& v, double* buf) {
+  float ynext = (s < e && lane < r) ? Y[(int64_t)nbr[s] * r + lane] : 0.f;
+  for (int64_t t = s; t < e; ++t) {
+    const float yf = ynext;
+    if (t + 1 < e) ynext = lane < r ? Y[(int64_t)nbr[t + 1] * r + lane] : 0.f;
+    double* row = buf + (int)(t & 1) * RP;
+    row[lane] = (double)yf;
+    lds_wave_sync<RP>();
+    const float rt = rating[t];
+    double c, w;
+    if (implicit) {
+      c = rt > 0.f ? (double)alpha * rt : 0.0;
+      w = rt > 0.f ? 1.0 + c : 0.0;
+    } else {
+      c = 1.0;
+      w = rt;
+    }
+    axpy_bcast<RP>(a, c * (double)yf, row, 0);
+    v = fma(w, (double)yf, v);
+  }
+  lds_wave_sync<RP>();
+}
+
+// Gauss-Jordan on the SPD system in registers (lane = row), pivot rows broadcast through buf; after the last
+// step v = x_i.  One step per template instance (K compile-time: every register index static; a 64-step
+// `#pragma unroll` loop exceeds the unroller's size limit and would fall back to scratch-indexed arrays).
+template <int RP, int K>
+struct GJStep {
+  static __device__ __forceinline__ void run(double (&a)[RP], double& v, double& diag, int& bad, int lane,
+                                             double* buf) {
+    __builtin_amdgcn_sched_barrier(0);   // one step at a time: keeps the register pressure at a[] + a few
+    buf[lane] = a[K];                    // column K = row K of the symmetric trailing block
+    lds_wave_sync<RP>();
+    const double p = readlane_f64(a[K], K);
+    const double vk = readlane_f64(v, K);
+    bad |= !(p > 0.0);
+    const double rp = 1.0 / (p > 0.0 ? p : 1.0);
+    const double f = lane == K ? 0.0 : a[K] * rp;
+    diag = lane == K ? p : diag;
+    if constexpr (K + 1 < RP) axpy_bcast<RP>(a, -f, buf, K + 1);   // a_i[j] -= f_i a_K[j], j > K
+    v = fma(-f, vk, v);
+    lds_wave_sync<RP>();
+    if constexpr (K + 1 < RP) GJStep<RP, K + 1>::run(a, v, diag, bad, lane, buf);
+  }
+};
+
+template <int RP>
+__device__ __forceinline__ int gj_solve(double (&a)[RP], double& v, int lane, double* buf) {
+  int bad = 0;
+  double diag = 1.0;
+  GJStep<RP, 0>::run(a, v, diag, bad, lane, buf);
+  v = v / (diag > 0.0 ? diag : 1.0);
+  return bad;
+}
+
+template <int RP>
+__global__ __launch_bounds__(64 * GJ_WAVES) void als_fused_solve(const int64_t* __restrict__ indptr,
+                                                                 const int32_t* __restrict__ nbr,
+                                                                 const float* __restrict__ rating,
+                                                                 const float* __restrict__ Y, int r, int implicit,
+                                                                 float alpha, const double* __restrict__ reg,
+                                                                 const double* __restrict__ YtY,
+                                                                 const int64_t* __restrict__ rows, int64_t nrows,
+                                                                 float* __restrict__ X, int32_t* __restrict__ status) {
+  __shared__ __attribute__((aligned(16))) double lbuf[GJ_WAVES][GJ_NB * RP];
+  const int w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int64_t idx = (int64_t)blockIdx.x * GJ_WAVES + w;
+  if (idx >= nrows) return;              // whole wave: no block-wide barrier below
+  const int64_t row = rows != nullptr ? rows[idx] : idx;
+  double* buf = lbuf[w];
   double a[RP];
 #pragma unroll
   for (int i = 0; i < RP; ++i) a[i] = 0.0;
   double v = 0.0;
-  gram_regs<RP>(nbr, rating, Y, r, implicit, alpha, indptr[row], indptr[row + 1], lane, a, v);
+  gram_lds<RP>(nbr, rating, Y, r, implicit, alpha, indptr[row], indptr[row + 1], lane, a, v, buf);
   add_reg<RP>(a, lane, r, reg[row], YtY);
-  const int bad = chol_solve_regs<RP>(a, v, lane);
+  const int bad = gj_solve<RP>(a, v, lane, buf);
   if (lane < r) X[row * r + lane] = (float)v;
   if (lane == 0) status[row] = bad;
 }
@@ -305,9 +433,9 @@ int alink_als_fused_solve(const int64_t* indptr, const int32_t* nbr, const float
                           const int64_t* rows, float* X, int32_t* status, hipStream_t stream) {
   if (nrows <= 0) return 0;
   if (r <= 0 || r > 64) return 1;
-  const dim3 grid((unsigned)nrows), block(64);
+  const dim3 grid((unsigned)((nrows + GJ_WAVES - 1) / GJ_WAVES)), block(64 * GJ_WAVES);
 #define ALS_LAUNCH(RP) hipLaunchKernelGGL(als_fused_solve<RP>, grid, block, 0, stream, indptr, nbr, rating, Y, r, \
-                                          implicit, alpha, reg, YtY, rows, X, status)
+                                          implicit, alpha, reg, YtY, rows, nrows, X, status)
   if (r <= 8) ALS_LAUNCH(8);
   else if (r <= 16) ALS_LAUNCH(16);
   else if (r <= 32) ALS_LAUNCH(32);

@@ -15,7 +15,8 @@ import torch
 
 from . import _lib
 
-__all__ = ["ftrl_hogwild", "ftrl_prox_hip", "ftrl_partial_margin_hip", "ftrl_shard_update_hip"]
+__all__ = ["ftrl_hogwild", "ftrl_prox_hip", "ftrl_partial_margin_hip", "ftrl_shard_update_hip", "ftrl_dp_gradients",
+           "ftrl_dp_update"]
 
 
 def ftrl_hogwild(indptr: torch.Tensor, idx: torch.Tensor, val: torch.Tensor, label: torch.Tensor, w: torch.Tensor,
@@ -120,3 +121,39 @@ def ftrl_shard_update_hip(indptr: torch.Tensor, idx: torch.Tensor, val: torch.Te
                                        float(l1), float(l2), _grid(nseg, 256), _lib.stream_ptr(dev))
     if rc != 0:
         raise RuntimeError(f"alink_ftrl_coord_update_f64 failed: {rc}")
+
+
+def ftrl_dp_gradients(indptr: torch.Tensor, idx: torch.Tensor, val: torch.Tensor, label: torch.Tensor,
+                      w: torch.Tensor):
+    """DATA_PARALLEL mini-batch: margins of the local samples with the current w, and the per-coordinate
+    gradient sums ``gq = [sum g, sum g^2]`` ([2, dim] fp64, g = (sigmoid(margin) - y) x) — the one dense buffer
+    the ranks all-reduce per step.  Returns (gq, margin)."""
+    dev = w.device
+    dim = w.numel()
+    gq = torch.zeros((2, dim), dtype=torch.float64, device=dev)
+    nrow = indptr.numel() - 1
+    if nrow <= 0:
+        return gq, torch.zeros(0, dtype=torch.float64, device=dev)
+    rows = torch.repeat_interleave(torch.arange(nrow, device=dev), indptr[1:] - indptr[:-1])
+    il = idx.to(torch.int64)
+    margin = torch.zeros(nrow, dtype=torch.float64, device=dev)
+    margin.index_add_(0, rows, w[il] * val)
+    err = torch.sigmoid(margin) - label.to(torch.float64)
+    g = err[rows] * val
+    gq[0].index_add_(0, il, g)
+    gq[1].index_add_(0, il, g * g)
+    return gq, margin
+
+
+def ftrl_dp_update(gq: torch.Tensor, w: torch.Tensor, n: torch.Tensor, z: torch.Tensor, alpha: float, beta: float,
+                   l1: float, l2: float) -> None:
+    """Mini-batch FTRL-proximal step from the (all-reduced) gradient sums, in place on w, n, z: for every touched
+    coordinate sigma = (sqrt(n + sum g^2) - sqrt(n)) / alpha, z += sum g - sigma w, n += sum g^2,
+    w = prox(z, n) (reference per-sample rule FtrlTrainStreamOp.java:396-420 applied once per mini-batch)."""
+    touched = gq[1] > 0
+    sigma = (torch.sqrt(n + gq[1]) - torch.sqrt(n)) / alpha
+    z += torch.where(touched, gq[0] - sigma * w, torch.zeros_like(z))
+    n += gq[1]
+    denom = (beta + torch.sqrt(n)) / alpha + l2
+    neww = torch.where(z.abs() <= l1, torch.zeros_like(z), -(z - torch.sign(z) * l1) / denom)
+    w.copy_(torch.where(touched, neww, w))

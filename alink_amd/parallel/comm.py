@@ -318,8 +318,8 @@ def all_to_all_tensors(send: List[torch.Tensor]) -> List[torch.Tensor]:
     counts = torch.tensor([x.shape[0] for x in send], dtype=torch.int64)
     all_counts = all_gather_tensor(counts).view(ws, ws)
     recv_counts = all_counts[:, get_rank()].tolist()
-    flat = torch.cat([x.reshape(x.shape[0], -1) for x in send]) if send else torch.empty(0)
     width = int(np.prod(tail)) if tail else 1
+    flat = torch.cat([x.reshape(x.shape[0], width) for x in send]) if send else torch.empty(0)
     STATS.calls += 1
     if _backend() == "nccl":
         cdev = dev if dev.type == "cuda" else device_for_rank()

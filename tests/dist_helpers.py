@@ -232,11 +232,12 @@ def _ftrl_run(mode, rows, batch):
     cols = [f"f{i}" for i in range(5)]
     model = LogisticRegressionTrainBatchOp().setFeatureCols(cols).setLabelCol("label").setMaxIter(3).linkFrom(batch_op)
     snaps = []
-    FtrlTrainStreamOp(model).setFeatureCols(cols).setLabelCol("label").setTimeInterval(1e9).setAlpha(0.1) \
-        .setBeta(0.1).setL1(0.01).setL2(0.01).setWithIntercept(True).setUpdateMode(mode) \
-        .linkFrom(stream).link(CollectStreamOp(snaps))
+    op = FtrlTrainStreamOp(model).setFeatureCols(cols).setLabelCol("label").setTimeInterval(1e9).setAlpha(0.1) \
+        .setBeta(0.1).setL1(0.01).setL2(0.01).setWithIntercept(True).setUpdateMode(mode)
+    op.linkFrom(stream).link(CollectStreamOp(snaps))
     StreamOperator.execute()
     last = max(r[0] for r in snaps)
+    _ftrl_run.recv_nnz = list(op.recv_nnz)
     return [list(r[2:]) for r in snaps if r[0] == last], sorted({r[0] for r in snaps})
 
 
@@ -246,6 +247,22 @@ def scenario_ftrl_seq(out):
 
 def scenario_ftrl_sharded(out):
     out["model"], out["bids"] = _ftrl_run("SHARDED", 64, 4096)
+
+
+def scenario_ftrl_sharded_split(out):
+    """SplitVector exchange: each shard receives only the nonzeros in its coefficient range."""
+    out["model"], out["bids"] = _ftrl_run("SHARDED", 400, 30)
+    out["recv_nnz"] = _ftrl_run.recv_nnz
+
+
+def scenario_ftrl_sharded_allgather(out):
+    """The same steps with the whole micro-batch all-gathered to every shard (the round-2 exchange)."""
+    os.environ["ALINK_FTRL_SHARDED_EXCHANGE"] = "allgather"
+    out["model"], out["bids"] = _ftrl_run("SHARDED", 400, 30)
+
+
+def scenario_ftrl_dp(out):
+    out["model"], out["bids"] = _ftrl_run("DATA_PARALLEL", 400, 4096)
 
 
 def scenario_ftrl_uneven(out):

@@ -96,3 +96,20 @@ def test_schema_strings():
 def test_hashmap_order_examples():
     assert java_hashmap_order(["distanceType", "k", "vectorSize", "vectorCol", "latitudeCol", "longitudeCol"]) == \
         ["vectorCol", "latitudeCol", "longitudeCol", "distanceType", "k", "vectorSize"]
+
+
+def test_native_java_double_join_matches_python_formatter():
+    """The C++ Double.toString formatter used for large model vectors (snapshots) gives the same strings as the
+    Python reference formatter, edge cases included."""
+    import numpy as np
+    from alink_amd import _native
+    from alink_amd.common.javafmt import java_double_str, gson_dumps
+    if _native.lib is None or getattr(_native.lib, "alink_java_double_join", None) is None:
+        import pytest
+        pytest.skip("native runtime not built")
+    rng = np.random.default_rng(3)
+    xs = np.concatenate([rng.normal(size=5000) * 10.0 ** rng.integers(-15, 15, size=5000),
+                         [0.0, -0.0, 1e-3, 9.99e-4, 1e7, 9999999.999999998, 1.0, -100.0, float("nan"), float("inf"),
+                          -float("inf"), 5e-324, 1.7976931348623157e308, 0.1 + 0.2, 1e21, 1e-5, 123456789.0]])
+    assert _native.java_double_join(xs).split(",") == [java_double_str(float(v)) for v in xs]
+    assert gson_dumps(xs) == "[" + ",".join(java_double_str(float(v)) for v in xs) + "]"

@@ -188,6 +188,47 @@ def test_ftrl_two_processes_equal_single(tmp_path, scenario):
                                        atol=1e-14)
 
 
+@pytest.mark.parametrize("world", [2, 4])
+def test_ftrl_sharded_split_vector_exchange(tmp_path, world):
+    """SHARDED with the SplitVector exchange (each shard receives only the nonzeros of its coefficient range,
+    ``FtrlTrainStreamOp.java:174-267``) equals the all-gather exchange on the same global steps, while every shard
+    receives ~1/P of each step's nonzeros."""
+    split = _run("ftrl_sharded_split", world, tmp_path)
+    ag = _run("ftrl_sharded_allgather", world, tmp_path)
+    for o in split[1:]:
+        assert o["model"] == split[0]["model"]
+    assert split[0]["bids"] == ag[0]["bids"]
+    for a, b in zip(ag[0]["model"], split[0]["model"]):
+        assert a[0] == b[0]
+        if a[1] != b[1]:
+            ja, jb = json.loads(a[1]), json.loads(b[1])
+            np.testing.assert_allclose(np.asarray(ja.get("coefVector", {}).get("data", [])),
+                                       np.asarray(jb.get("coefVector", {}).get("data", [])), rtol=1e-12, atol=1e-14)
+    # 6 coefficients (intercept + 5 dense features): shard j owns ceil(6/P) columns and gets only those entries
+    per_rank = np.asarray([o["recv_nnz"] for o in split], dtype=float)     # [P, steps]
+    step_total = per_rank.sum(0)
+    per = -(-6 // world)
+    for r in range(world):
+        owned = max(0, min(6, (r + 1) * per) - r * per)
+        np.testing.assert_allclose(per_rank[r], step_total * owned / 6.0)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_ftrl_data_parallel_equal_single(tmp_path, world):
+    """DATA_PARALLEL (replicated w, all-reduced mini-batch gradients): P ranks whose micro-batches form the
+    same global step as one rank's batch give the same model up to summation order."""
+    one = _run("ftrl_dp", 1, tmp_path)[0]
+    outs = _run("ftrl_dp", world, tmp_path)
+    for o in outs[1:]:
+        assert o["model"] == outs[0]["model"]
+    assert one["bids"] == outs[0]["bids"]
+    for a, b in zip(one["model"], outs[0]["model"]):
+        if a[1] != b[1]:
+            ja, jb = json.loads(a[1]), json.loads(b[1])
+            np.testing.assert_allclose(np.asarray(ja.get("coefVector", {}).get("data", [])),
+                                       np.asarray(jb.get("coefVector", {}).get("data", [])), rtol=1e-10, atol=1e-12)
+
+
 def test_ftrl_uneven_micro_batches_lockstep(tmp_path):
     """Rank 0 has 3 micro-batches, rank 1 has 2: the finished rank joins steps with an empty batch (no hang)."""
     one = _run("ftrl_uneven", 1, tmp_path)[0]

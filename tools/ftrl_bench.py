@@ -59,14 +59,15 @@ def main():
     ap.add_argument("--hash-strings", type=int, default=1_000_000)
     a = ap.parse_args()
     from alink_amd.ops import _lib
-    from alink_amd.ops.ftrl import ftrl_hogwild, ftrl_partial_margin_hip, ftrl_shard_update_hip
+    from alink_amd.ops.ftrl import (ftrl_hogwild, ftrl_partial_margin_hip, ftrl_shard_update_hip, ftrl_dp_gradients,
+                                    ftrl_dp_update)
     dev = torch.device("cuda")
     _lib.require()
     prm = (0.1, 1.0, 0.01, 0.01)   # alpha, beta, l1, l2 (FTRLExample: 0.1, 0.1, 0.01, 0.01 with beta 0.1)
     stream = make_stream(a.dim, a.batch, a.warmup + a.batches, a.fields, dev)
     res = {"config": {"dim": a.dim, "batch": a.batch, "batches": a.batches, "nnz_per_sample": a.fields + 1},
            "data": "synthetic hashed click stream (skewed categorical fields, hidden logistic model)"}
-    for mode in ("SHARDED", "HOGWILD"):
+    for mode in ("SHARDED", "HOGWILD", "DATA_PARALLEL"):
         w = torch.zeros(a.dim, dtype=torch.float64, device=dev)
         n = torch.zeros_like(w)
         z = torch.zeros_like(w)
@@ -81,6 +82,10 @@ def main():
                 losses.append(m)
                 err = (torch.sigmoid(m) - y).contiguous()
                 ftrl_shard_update_hip(indptr, idx, val, err, w, n, z, 0, a.dim, *prm)
+            elif mode == "DATA_PARALLEL":
+                gq, m = ftrl_dp_gradients(indptr, idx, val, y, w)     # P ranks: gq is all-reduced here
+                losses.append(m)
+                ftrl_dp_update(gq, w, n, z, *prm)
             else:
                 losses.append(ftrl_partial_margin_hip(indptr, idx, val, w, 0, a.dim))
                 ftrl_hogwild(indptr, idx, val, y, w, n, z, *prm)
@@ -89,7 +94,7 @@ def main():
         ll = [logloss(m, s[3]) for m, s in zip(losses, stream)]
         res[mode] = {"samples_per_s": a.batch * a.batches / el, "ms_per_batch": el / a.batches * 1e3,
                      "prequential_logloss_first": ll[0], "prequential_logloss_last": ll[-1],
-                     "scoring_included": mode == "HOGWILD"}
+                     "scoring_included": mode != "SHARDED"}
         if mode == "SHARDED":
             w_sharded = w
     # model snapshot latency: device -> host + Alink linear model table rows
