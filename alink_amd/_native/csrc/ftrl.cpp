@@ -62,12 +62,16 @@ int alink_ftrl_shard_update(const int64_t* indptr, const int32_t* indices, const
     for (int64_t k = indptr[r]; k < indptr[r + 1]; ++k) {
       const int64_t i = (int64_t)indices[k] - lo;
       if (i < 0 || i >= hi - lo) continue;
+      // same arithmetic as the GPU replay (ops/csrc/ftrl.hip ftrl_coord_update_kernel)
+      const double ia = 1.0 / alpha;
       const double g = err[r] * values[k];
       const double nn = n[i] + g * g;
-      const double sigma = (std::sqrt(nn) - std::sqrt(n[i])) / alpha;
+      const double sn = std::sqrt(nn);
+      const double sigma = (sn - std::sqrt(n[i])) * ia;
+      const double rden = 1.0 / (beta + sn * ia + l2);
       z[i] += g - sigma * w[i];
       n[i] = nn;
-      w[i] = std::fabs(z[i]) <= l1 ? 0.0 : ((z[i] < 0 ? -1.0 : 1.0) * l1 - z[i]) / (beta + std::sqrt(n[i]) / alpha + l2);
+      w[i] = std::fabs(z[i]) <= l1 ? 0.0 : (std::copysign(l1, z[i]) - z[i]) * rden;
     }
   }
   return 0;

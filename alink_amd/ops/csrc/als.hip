@@ -277,7 +277,7 @@ __device__ __forceinline__ void gram_lds(const int32_t* __restrict__ nbr, const 
   for (int64_t t = s; t < e; ++t) {
     const float yf = ynext;
     if (t + 1 < e) ynext = lane < r ? Y[(int64_t)nbr[t + 1] * r + lane] : 0.f;
-    double* row = buf + (int)(t & 1) * RP;
+    double* row = buf + (int)(t & 1) * 64;
     row[lane] = (double)yf;
     lds_wave_sync<RP>();
     const float rt = rating[t];
@@ -336,7 +336,8 @@ __global__ __launch_bounds__(64 * GJ_WAVES) void als_fused_solve(const int64_t* 
                                                                  const double* __restrict__ YtY,
                                                                  const int64_t* __restrict__ rows, int64_t nrows,
                                                                  float* __restrict__ X, int32_t* __restrict__ status) {
-  __shared__ __attribute__((aligned(16))) double lbuf[GJ_WAVES][GJ_NB * RP];
+  // every lane writes its own entry (64 per row, whatever RP is): rows of 64 doubles
+  __shared__ __attribute__((aligned(16))) double lbuf[GJ_WAVES][GJ_NB * 64];
   const int w = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
   const int64_t idx = (int64_t)blockIdx.x * GJ_WAVES + w;

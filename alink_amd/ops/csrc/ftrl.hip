@@ -103,15 +103,21 @@ __global__ __launch_bounds__(256) void ftrl_coord_update_kernel(const int64_t* _
         const int64_t s = seg[q], e = seg[q + 1];
         const int64_t i = coord[q] - lo;
         double wi = w[i], ni = n[i], zi = z[i], sq = sqrt(ni);
-#pragma unroll 4
+        // The only serial dependence is z -> w -> z: sigma_t and the prox denominator depend on n alone (a prefix
+        // sum of g^2), so their sqrt / reciprocal sit off the chain and the unrolled loop overlaps them with
+        // earlier steps; the chain itself is two FMAs, a compare/select and a multiply per step (it was a full
+        // fp64 IEEE division per step: a hot coordinate such as the intercept is a 65536-step chain per batch).
+#pragma unroll 8
         for (int64_t t = s; t < e; ++t) {
             const double gt = g[t];
             const double nn = ni + gt * gt;
             const double sn = sqrt(nn);
-            zi += gt - (sn - sq) * ia * wi;
+            const double sigma = (sn - sq) * ia;
+            const double rden = 1.0 / (beta + sn * ia + l2);
+            zi += gt - sigma * wi;
             ni = nn;
             sq = sn;
-            wi = fabs(zi) <= l1 ? 0.0 : ((zi < 0 ? -1.0 : 1.0) * l1 - zi) / (beta + sn * ia + l2);
+            wi = fabs(zi) <= l1 ? 0.0 : (copysign(l1, zi) - zi) * rden;
         }
         w[i] = wi;
         n[i] = ni;
