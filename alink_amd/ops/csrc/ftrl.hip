@@ -97,10 +97,11 @@ __global__ __launch_bounds__(256) void ftrl_coord_update_kernel(const int64_t* _
                                                                const int64_t* __restrict__ coord,
                                                                const double* __restrict__ g, double* w, double* n,
                                                                double* z, int64_t lo, double alpha, double beta,
-                                                               double l1, double l2) {
+                                                               double l1, double l2, int64_t maxlen) {
     const double ia = 1.0 / alpha;
     for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nseg; q += (int64_t)gridDim.x * blockDim.x) {
         const int64_t s = seg[q], e = seg[q + 1];
+        if (e - s > maxlen) continue;                 // ftrl_coord_long_kernel's segment
         const int64_t i = coord[q] - lo;
         double wi = w[i], ni = n[i], zi = z[i], sq = sqrt(ni);
         // The only serial dependence is z -> w -> z: sigma_t and the prox denominator depend on n alone (a prefix
@@ -119,6 +120,100 @@ __global__ __launch_bounds__(256) void ftrl_coord_update_kernel(const int64_t* _
             sq = sn;
             wi = fabs(zi) <= l1 ? 0.0 : (copysign(l1, zi) - zi) * rden;
         }
+        w[i] = wi;
+        n[i] = ni;
+        z[i] = zi;
+    }
+}
+
+// Long segments (hot coordinates: the intercept is in every sample) get a whole wave, 64 entries per chunk: the
+// lanes load g coalesced, form n_t by a wave prefix sum of g^2 and compute sigma_t and the prox reciprocal r_t in
+// parallel.  The z -> w chain is then speculated: while sign(z) and |z| > l1 do not change, prox is affine in z,
+// so each step is an affine map z_t = a_t z_{t-1} + b_t (a_t = 1 + sigma_t r_{t-1}, b_t = g_t - sigma_t sgn l1
+// r_{t-1}; a_t = 1, b_t = g_t in the |z| <= l1 regime) and the chunk is a wave prefix scan of map compositions.
+// The regime is guessed from the chunk's first step (computed exactly from the carried w) and checked on every
+// z_{t-1}; a chunk whose z crosses a regime boundary replays step by step with the per-step operands broadcast
+// by v_readlane.  (A single lane walking a 65536-step intercept segment cost ~190 ns per step; the serial
+// broadcast replay ~76 ns; the scan ~6 steps of 64-lane shuffles per 64 entries.)
+__device__ __forceinline__ double readlane_d(double v, int l) {
+    const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+    return __hiloint2double(hi, lo);
+}
+
+__device__ __forceinline__ double prox_r(double zv, double l1, double r) {
+    return fabs(zv) <= l1 ? 0.0 : (copysign(l1, zv) - zv) * r;
+}
+
+__device__ __forceinline__ int regime(double zv, double l1) { return fabs(zv) <= l1 ? 0 : (zv > 0.0 ? 1 : -1); }
+
+__global__ __launch_bounds__(64) void ftrl_coord_long_kernel(const int64_t* __restrict__ seg,
+                                                            const int64_t* __restrict__ coord,
+                                                            const int64_t* __restrict__ lsegs,
+                                                            const double* __restrict__ g, double* w, double* n,
+                                                            double* z, int64_t lo, double alpha, double beta,
+                                                            double l1, double l2) {
+    const int lane = threadIdx.x;
+    const int64_t q = lsegs[blockIdx.x];
+    const int64_t s = seg[q], e = seg[q + 1];
+    const int64_t i = coord[q] - lo;
+    const double ia = 1.0 / alpha;
+    double wi = w[i], ni = n[i], zi = z[i];
+    for (int64_t t0 = s; t0 < e; t0 += 64) {
+        const int cnt = (int)(e - t0 < 64 ? e - t0 : 64);
+        const double gl = lane < cnt ? g[t0 + lane] : 0.0;
+        double ps = gl * gl;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const double o = __shfl_up(ps, d);
+            if (lane >= d) ps += o;
+        }
+        // every shuffle runs with all lanes active (a bpermute from a lane masked off by a branch reads 0)
+        const double nl = ni + ps;
+        const double snl = sqrt(nl);
+        const double up = __shfl_up(snl, 1);
+        const double sprev = lane == 0 ? sqrt(ni) : up;
+        const double sig = (snl - sprev) * ia;
+        const double rden = 1.0 / (beta + snl * ia + l2);
+        const double rprev = __shfl_up(rden, 1);
+        // step 0 is exact from the carried w; its result fixes the guessed regime of the chunk
+        const double z0 = zi + gl - sig * wi;                       // meaningful on lane 0
+        const int guess = regime(readlane_d(z0, 0), l1);
+        double am, bm;
+        if (lane == 0) {
+            am = 1.0;
+            bm = gl - sig * wi;
+        } else if (lane < cnt && guess != 0) {
+            am = 1.0 + sig * rprev;
+            bm = gl - sig * (guess * l1) * rprev;
+        } else {
+            am = 1.0;
+            bm = lane < cnt ? gl : 0.0;
+        }
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const double ao = __shfl_up(am, d), bo = __shfl_up(bm, d);
+            if (lane >= d) {
+                bm = fma(am, bo, bm);
+                am *= ao;
+            }
+        }
+        const double zl = fma(am, zi, bm);                           // z after this lane's step
+        const double zprev = __shfl_up(zl, 1);
+        const bool bad = lane >= 1 && lane < cnt && regime(zprev, l1) != guess;
+        if (__ballot(bad) == 0) {
+            zi = readlane_d(zl, cnt - 1);
+            wi = prox_r(zi, l1, readlane_d(rden, cnt - 1));
+        } else {
+            for (int u = 0; u < cnt; ++u) {
+                const double gu = readlane_d(gl, u), su = readlane_d(sig, u), ru = readlane_d(rden, u);
+                zi += gu - su * wi;
+                wi = prox_r(zi, l1, ru);
+            }
+        }
+        ni = readlane_d(nl, cnt - 1);
+    }
+    if (lane == 0) {
         w[i] = wi;
         n[i] = ni;
         z[i] = zi;
@@ -176,11 +271,22 @@ int alink_ftrl_partial_margin_f64(const int64_t* indptr, const int32_t* idx, con
 
 int alink_ftrl_coord_update_f64(const int64_t* seg, int64_t nseg, const int64_t* coord, const double* g, double* w,
                                 double* n, double* z, int64_t lo, double alpha, double beta, double l1, double l2,
-                                int grid, void* stream) {
+                                int64_t maxlen, int grid, void* stream) {
     if (nseg <= 0) return 0;
     if (grid <= 0 || alpha <= 0.0) return 1;
     hipLaunchKernelGGL(ftrl_coord_update_kernel, dim3(grid), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), seg,
-                       nseg, coord, g, w, n, z, lo, alpha, beta, l1, l2);
+                       nseg, coord, g, w, n, z, lo, alpha, beta, l1, l2, maxlen);
+    return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+// long segments (lsegs: nlong segment ids), one wave each
+int alink_ftrl_coord_long_f64(const int64_t* seg, const int64_t* coord, const int64_t* lsegs, int64_t nlong,
+                              const double* g, double* w, double* n, double* z, int64_t lo, double alpha, double beta,
+                              double l1, double l2, void* stream) {
+    if (nlong <= 0) return 0;
+    if (alpha <= 0.0) return 1;
+    hipLaunchKernelGGL(ftrl_coord_long_kernel, dim3((unsigned)nlong), dim3(64), 0,
+                       reinterpret_cast<hipStream_t>(stream), seg, coord, lsegs, g, w, n, z, lo, alpha, beta, l1, l2);
     return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 

@@ -55,6 +55,9 @@ def ftrl_hogwild(indptr: torch.Tensor, idx: torch.Tensor, val: torch.Tensor, lab
     ftrl_prox_hip(w, n, z, alpha, beta, l1, l2, coords=torch.unique(idx))
 
 
+LONG_SEGMENT = 256
+
+
 def _grid(n: int, per: int, cap: int = 4096) -> int:
     return max(1, min((n + per - 1) // per, cap))
 
@@ -94,7 +97,8 @@ def ftrl_shard_update_hip(indptr: torch.Tensor, idx: torch.Tensor, val: torch.Te
                           beta: float, l1: float, l2: float) -> None:
     """Owned coordinates [lo, hi) replay their entries in sample order with ``err = p - y`` fixed for the
     micro-batch: entries filtered to the shard, stably sorted by coordinate on the device, one lane per
-    coordinate segment (``ftrl_coord_update_kernel``)."""
+    coordinate segment (``ftrl_coord_update_kernel``), one wave per segment longer than ``LONG_SEGMENT``
+    (``ftrl_coord_long_kernel``)."""
     L = _lib.require()
     dev = w.device
     nrows = indptr.shape[0] - 1
@@ -116,11 +120,24 @@ def ftrl_shard_update_hip(indptr: torch.Tensor, idx: torch.Tensor, val: torch.Te
     seg = torch.zeros(counts.numel() + 1, dtype=torch.int64, device=dev)
     torch.cumsum(counts, 0, out=seg[1:])
     nseg = counts.numel()
-    rc = L.alink_ftrl_coord_update_f64(seg.data_ptr(), nseg, coord.contiguous().data_ptr(), g.data_ptr(),
-                                       w.data_ptr(), n.data_ptr(), z.data_ptr(), int(lo), float(alpha), float(beta),
-                                       float(l1), float(l2), _grid(nseg, 256), _lib.stream_ptr(dev))
-    if rc != 0:
-        raise RuntimeError(f"alink_ftrl_coord_update_f64 failed: {rc}")
+    coord = coord.contiguous()
+    st = _lib.stream_ptr(dev)
+    # segments longer than LONG_SEGMENT (the intercept, hot categorical values) replay on one wave each with
+    # their off-chain terms computed lane-parallel; the rest one lane per segment
+    lsegs = torch.nonzero(counts > LONG_SEGMENT, as_tuple=False).reshape(-1).contiguous()
+    nlong = lsegs.numel()
+    if nlong < nseg:
+        rc = L.alink_ftrl_coord_update_f64(seg.data_ptr(), nseg, coord.data_ptr(), g.data_ptr(), w.data_ptr(),
+                                           n.data_ptr(), z.data_ptr(), int(lo), float(alpha), float(beta), float(l1),
+                                           float(l2), LONG_SEGMENT, _grid(nseg, 256), st)
+        if rc != 0:
+            raise RuntimeError(f"alink_ftrl_coord_update_f64 failed: {rc}")
+    if nlong:
+        rc = L.alink_ftrl_coord_long_f64(seg.data_ptr(), coord.data_ptr(), lsegs.data_ptr(), nlong, g.data_ptr(),
+                                         w.data_ptr(), n.data_ptr(), z.data_ptr(), int(lo), float(alpha), float(beta),
+                                         float(l1), float(l2), st)
+        if rc != 0:
+            raise RuntimeError(f"alink_ftrl_coord_long_f64 failed: {rc}")
 
 
 def ftrl_dp_gradients(indptr: torch.Tensor, idx: torch.Tensor, val: torch.Tensor, label: torch.Tensor,

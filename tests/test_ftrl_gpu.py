@@ -137,6 +137,32 @@ def test_ftrl_sharded_kernels_match_native(lo, hi):
         np.testing.assert_allclose(g.cpu().numpy(), r, rtol=1e-12, atol=1e-14)
 
 
+def test_ftrl_shard_update_long_segments_match_native():
+    """Coordinates with more than LONG_SEGMENT entries replay on one wave each (lane-parallel n / sigma /
+    reciprocal, serial z -> w chain); lengths straddle the threshold and the 64-entry chunking."""
+    from alink_amd import _native
+    from alink_amd.ops.ftrl import LONG_SEGMENT, ftrl_shard_update_hip
+    rng = np.random.default_rng(11)
+    nrows, dim = 1100, 40
+    lens = {0: nrows, 1: LONG_SEGMENT + 1, 2: LONG_SEGMENT, 3: 64, 4: 65, 5: 129, 6: 640, 7: 1}
+    rows = []
+    for r in range(nrows):
+        cols = {c for c, L in lens.items() if r < L} | set(rng.choice(np.arange(8, dim), 3, replace=False).tolist())
+        rows.append([(c, float(rng.normal())) for c in sorted(cols)])
+    indptr, idx, val = _csr(rows)
+    err = rng.normal(size=nrows) * 0.5
+    prm = (0.1, 1.0, 0.01, 0.02)
+    w0 = rng.normal(size=dim) * 0.1
+    ref = [w0.copy(), np.zeros(dim), np.zeros(dim)]
+    _native.ftrl_shard_update(indptr, idx, val, err, *ref, 0, dim, *prm)
+    dev = [torch.as_tensor(a).cuda() for a in (indptr, idx, val)]
+    st = [torch.tensor(a, dtype=torch.float64, device="cuda") for a in (w0, np.zeros(dim), np.zeros(dim))]
+    ftrl_shard_update_hip(*dev, torch.as_tensor(err).cuda(), *st, 0, dim, *prm)
+    torch.cuda.synchronize()
+    for g, r in zip(st, ref):
+        np.testing.assert_allclose(g.cpu().numpy(), r, rtol=1e-11, atol=1e-13)
+
+
 def test_ftrl_train_stream_sharded_on_gpu_equals_cpu():
     """FtrlTrainStreamOp(updateMode=SHARDED) end to end: GPU env (HIP kernels) == CPU env (native host)."""
     import pandas as pd
