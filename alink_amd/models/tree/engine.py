@@ -157,6 +157,7 @@ class TreeBuilder:
         self.fshard = (not local and ws > 1 and cfg.kind == "gbdt" and not any(data.is_cat)
                        and __import__("os").environ.get("ALINK_GBDT_FEATURE_SHARD", "1") == "1")
         self.Fb = -(-self.F // ws) if self.fshard else self.F          # features per rank (padded)
+        self._hist_sub = None          # (stats tensor, histogram columns, FmStats) of the tree being built
         self.f_lo = comm.get_rank() * self.Fb if self.fshard else 0
 
     # -------------------------------------------------------------------------------------------
@@ -166,12 +167,18 @@ class TreeBuilder:
         return [1, 2, 3] if self.cfg.kind == "gbdt" else list(range(S))
 
     def _histograms(self, node_of_row, sample, slot_of_node: torch.Tensor, nslots: int, stats) -> torch.Tensor:
-        slot = torch.full_like(node_of_row, -1)
-        act = sample & (node_of_row >= 0) & (node_of_row < slot_of_node.numel())
-        slot[act] = slot_of_node[node_of_row[act].long()].to(slot.dtype)
+        nn = slot_of_node.numel()
+        act = sample & (node_of_row >= 0) & (node_of_row < nn)
+        slot = torch.where(act, slot_of_node[node_of_row.clamp(0, max(nn - 1, 0)).long()].to(node_of_row.dtype),
+                           torch.full_like(node_of_row, -1))
         cols = self._hist_cols(stats.shape[1])
-        sub = stats if len(cols) == stats.shape[1] else stats[:, cols].contiguous()
-        H = tops.histogram(self.d.bins, slot, sub, nslots, self.B)
+        if self._hist_sub is None or self._hist_sub[0] is not stats:
+            sub = stats if len(cols) == stats.shape[1] else stats[:, cols].contiguous()
+            # the fixed-point kernel's quantised statistics are built once per tree, not once per level
+            prep = tops.FmStats(sub) if tops.fm_eligible(self.d.bins, len(cols), self.B) else None
+            self._hist_sub = (stats, sub, prep)
+        _, sub, prep = self._hist_sub
+        H = tops.histogram(self.d.bins, slot, sub, nslots, self.B, prep=prep)
         if self.fshard:
             # [slots, F, B, S] -> feature-major, pad F to P * Fb, reduce-scatter -> this rank's [slots, Fb, B, S]
             ws = comm.get_world_size()
@@ -590,6 +597,7 @@ class TreeBuilder:
             level_hist = {}
             level = nxt
         self._prev_hist = {}
+        self._hist_sub = None
         # leaf probabilities (split nodes keep raw counters)
         for lf in leaves:
             lf.make_leaf_prob()

@@ -212,6 +212,150 @@ __global__ __launch_bounds__(kThreads) void tree_node_sums_global(const int32_t*
   }
 }
 
+// ---------------------------------------------------------------------------------------------------------
+// Fixed-point bank-private histogram (the production GPU path for S <= 4).
+//
+// Measured on MI355X (tools/micro/lds_atomic_bench.hip, 8 waves per CU): ds_add_f32 costs ~193 cycles per
+// wave-instruction even with 64 distinct conflict-free addresses, ds_add_u32 ~6.  So the statistics are
+// accumulated as 64-bit fixed point (integer LDS atomics): the host quantises every statistic column to int32
+// with a power-of-two scale putting max|column| just below 2^30 (per-value resolution 2^-30 of the column's
+// range, finer than an fp32 ulp of the typical sum), and the int64 bins cannot overflow below 2^33 rows.
+// Integer sums are exact and order-independent: the histogram is bitwise deterministic and equal across
+// partitionings of the rows.
+//
+// A workgroup owns one row chunk of ONE slot (rows pre-grouped by slot: ridx = row ids sorted stably by slot,
+// q = their quantised statistics in that order, 4 x int32 per row) and one group of 32 features.  A wave
+// takes rows in pairs: lanes 0-31 = features of row i, lanes 32-63 = the same features of row i+1; the LDS
+// histogram is [bin][stat][32 features] int64, so each half-wave's 32 lanes hit 32 distinct, conflict-free
+// 8-byte slots whatever the bins.  Row ids and statistics are wave-uniform scalar loads.
+//
+// XCD grouping: dispatch puts block ids b, b+8, b+16, b+24 on the same XCD at about the same time; they take
+// the four 32-feature quarters of the same rows' 128-B cache lines.  Each block stores its partial histogram
+// into an int64 slab (no global atomics, no zeroing); tree_hist_fm_reduce sums a slot's chunks and scales.
+constexpr int kFmThreads = 1024;   // 16 waves: the single LDS-resident workgroup per CU hides HBM latency
+constexpr int kFmPairs = 8;          // row pairs per batch and wave
+
+template <int S, bool IDX>
+__global__ __launch_bounds__(kFmThreads) void tree_hist_fm(const uint8_t* __restrict__ bins, int F,
+                                                           const int32_t* __restrict__ ridx,
+                                                           const int32_t* __restrict__ q,
+                                                           const int32_t* __restrict__ chunk_rows, int nchunks,
+                                                           int nfg, int B, long long* __restrict__ slab) {
+  extern __shared__ long long lq[];
+  const int bid = blockIdx.x;
+  const int nquad = (nfg + 3) >> 2;
+  const int quad_id = (bid >> 5) * 8 + (bid & 7);
+  const int c = quad_id / nquad;
+  const int fg = (quad_id - c * nquad) * 4 + ((bid >> 3) & 3);
+  if (c >= nchunks || fg >= nfg) return;                 // whole block, before any barrier
+  const int n_e = B * S * 32;
+  for (int i = threadIdx.x; i < n_e; i += kFmThreads) lq[i] = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int half = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int f = fg * 32 + (lane & 31);
+  const bool valid = f < F;
+  const uint8_t* bcol = bins + (valid ? f : 0);
+  const int rb = chunk_rows[c], re = chunk_rows[c + 1];
+  constexpr int nw = kFmThreads / 64;
+  const int len = re - rb;
+  const int per = ((len + nw - 1) / nw + 1) & ~1;        // even rows per wave
+  const int i0 = rb + min(len, wave * per), i1 = rb + min(len, (wave + 1) * per);
+  unsigned long long* lb = reinterpret_cast<unsigned long long*>(lq) + (lane & 31);
+  const int bmax = B - 1;
+  int i = i0;
+  for (; i + 2 * kFmPairs <= i1; i += 2 * kFmPairs) {
+    // row ids and both rows' statistics of every pair: wave-uniform scalar loads, issued together ahead of
+    // the batch's LDS atomics (both count in lgkmcnt).  Per-lane vector loads of the statistics cost the
+    // texture path 16 + 8 cycles per pair (64 lanes x 24 B, duplicates included) -- more than the atomics.
+    int qs[kFmPairs][8];
+    int bb[kFmPairs];
+#pragma unroll
+    for (int u = 0; u < kFmPairs; ++u) {
+      const int64_t r0 = IDX ? (int64_t)ridx[i + 2 * u] : (int64_t)(i + 2 * u);
+      const int64_t r1 = IDX ? (int64_t)ridx[i + 2 * u + 1] : (int64_t)(i + 2 * u + 1);
+      bb[u] = bcol[(half ? r1 : r0) * F];
+    }
+#pragma unroll
+    for (int u = 0; u < kFmPairs; ++u)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qs[u][j] = q[(int64_t)(i + 2 * u) * 4 + j];
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < kFmPairs; ++u) {
+      unsigned long long* hp = lb + min(bb[u], bmax) * (S * 32);
+      if (valid) {
+#pragma unroll
+        for (int k = 0; k < S; ++k) {
+          const int lo = qs[u][k], hi = qs[u][4 + k];       // select by value: an index would go to scratch
+          const int v = half ? hi : lo;
+          atomicAdd(hp + k * 32, (unsigned long long)(long long)v);
+        }
+      }
+    }
+  }
+  for (; i < i1; i += 2) {
+    const bool has1 = i + 1 < i1;
+    const int64_t r0 = IDX ? (int64_t)ridx[i] : (int64_t)i;
+    const int64_t r1 = has1 ? (IDX ? (int64_t)ridx[i + 1] : (int64_t)(i + 1)) : r0;
+    const int b = bcol[(half ? r1 : r0) * F];
+    unsigned long long* hp = lb + min(b, bmax) * (S * 32);
+    if (valid && (half == 0 || has1)) {
+#pragma unroll
+      for (int k = 0; k < S; ++k)
+        atomicAdd(hp + k * 32, (unsigned long long)(long long)q[(int64_t)(i + half) * 4 + k]);
+    }
+  }
+  __syncthreads();
+  long long* dst = slab + ((int64_t)c * nfg + fg) * n_e;
+  for (int j = threadIdx.x; j < n_e; j += kFmThreads) dst[j] = lq[j];
+}
+
+// H[slot][fg*32 + l][b][k] = inv_scale[k] * sum over the slot's chunks of slab[chunk][fg][b][k][l] (exact int64
+// sums); a block owns (slot, feature group, 8 bins) and transposes through LDS (row stride 33: conflict-free).
+constexpr int kRedBins = 8;
+__global__ __launch_bounds__(256) void tree_hist_fm_reduce(const long long* __restrict__ slab,
+                                                           const int32_t* __restrict__ slot_chunk, int nfg, int F,
+                                                           int B, int S, const double* __restrict__ inv_scale,
+                                                           float* __restrict__ H) {
+  __shared__ float tile[kRedBins * 4 * 33];
+  const int s = blockIdx.x / nfg, fg = blockIdx.x - (blockIdx.x / nfg) * nfg;
+  const int b0 = blockIdx.y * kRedBins;
+  const int nb = min(kRedBins, B - b0);
+  const int n_e = B * S * 32;
+  const int m = nb * S * 32;
+  const int cs = slot_chunk[s], ce = slot_chunk[s + 1];
+  for (int t = threadIdx.x; t < m; t += 256) {
+    long long acc = 0;
+    for (int j = cs; j < ce; ++j) acc += slab[((int64_t)j * nfg + fg) * n_e + (int64_t)b0 * S * 32 + t];
+    const int k = (t >> 5) % S;
+    tile[(t >> 5) * 33 + (t & 31)] = (float)((double)acc * inv_scale[k]);
+  }
+  __syncthreads();
+  const int w = nb * S;
+  for (int t = threadIdx.x; t < 32 * w; t += 256) {
+    const int l = t / w, j = t - (t / w) * w;
+    const int f = fg * 32 + l;
+    if (f < F) H[(((int64_t)s * F + f) * B + b0) * S + j] = tile[j * 33 + l];
+  }
+}
+
+template <int S>
+int launch_fm(bool idx, int64_t grid, size_t lds, hipStream_t stream, const uint8_t* bins, int F, const int32_t* ridx,
+              const int32_t* sst, const int32_t* chunk_rows, int nchunks, int nfg, int B, long long* slab) {
+  const void* k = idx ? reinterpret_cast<const void*>(tree_hist_fm<S, true>)
+                      : reinterpret_cast<const void*>(tree_hist_fm<S, false>);
+  if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return 3;
+  if (idx)
+    hipLaunchKernelGGL((tree_hist_fm<S, true>), dim3((unsigned)grid), dim3(kFmThreads), lds, stream, bins, F, ridx, sst,
+                       chunk_rows, nchunks, nfg, B, slab);
+  else
+    hipLaunchKernelGGL((tree_hist_fm<S, false>), dim3((unsigned)grid), dim3(kFmThreads), lds, stream, bins, F, ridx,
+                       sst, chunk_rows, nchunks, nfg, B, slab);
+  return 0;
+}
+
 }  // namespace
 
 extern "C" {
@@ -292,6 +436,34 @@ int alink_tree_hist_f32(const uint8_t* bins, int64_t n, int F, const int32_t* sl
     hipLaunchKernelGGL(tree_hist_lds, grid, dim3(kThreads), lds, stream, bins, n, F, slot, stats, S, B, spg, FG,
                        rows_per_block, hist);
   }
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+// Fixed-point histogram (tree_hist_fm): rows grouped by slot.  ridx: [total] row ids sorted by slot (nullptr =
+// identity: rows 0..total-1 all in slot 0); q: [total, 4] int32 quantised statistics in that order;
+// chunk_rows: [nchunks+1] row offsets (each chunk inside one slot); slot_chunk: [nslots+1] chunk ranges per
+// slot; inv_scale: [S] fp64 (device); slab: [nchunks, nfg, B, S, 32] int64 scratch; H: [nslots, F, B, S] fp32
+// (fully written, no zeroing needed).
+int alink_tree_hist_fm(const uint8_t* bins, int F, const int32_t* ridx, const int32_t* q, const int32_t* chunk_rows,
+                       int nchunks, const int32_t* slot_chunk, int nslots, int S, int B, const double* inv_scale,
+                       long long* slab, float* H, hipStream_t stream) {
+  if (nslots <= 0) return 0;
+  if (F <= 0 || S < 1 || S > 4 || B <= 0 || B > 256) return 1;
+  const size_t lds = (size_t)B * S * 32 * sizeof(long long);
+  if (lds > 160 * 1024) return 1;
+  const int nfg = (F + 31) / 32;
+  if (nchunks > 0) {
+    const int64_t quads = (int64_t)nchunks * ((nfg + 3) / 4);
+    const int64_t grid = (quads + 7) / 8 * 32;
+    if (grid > 0x7fffffff) return 1;
+    const int rc = S == 1 ? launch_fm<1>(ridx != nullptr, grid, lds, stream, bins, F, ridx, q, chunk_rows, nchunks, nfg, B, slab)
+                 : S == 2 ? launch_fm<2>(ridx != nullptr, grid, lds, stream, bins, F, ridx, q, chunk_rows, nchunks, nfg, B, slab)
+                 : S == 3 ? launch_fm<3>(ridx != nullptr, grid, lds, stream, bins, F, ridx, q, chunk_rows, nchunks, nfg, B, slab)
+                          : launch_fm<4>(ridx != nullptr, grid, lds, stream, bins, F, ridx, q, chunk_rows, nchunks, nfg, B, slab);
+    if (rc != 0) return rc;
+  }
+  hipLaunchKernelGGL(tree_hist_fm_reduce, dim3((unsigned)(nslots * nfg), (unsigned)((B + kRedBins - 1) / kRedBins)),
+                     dim3(256), 0, stream, slab, slot_chunk, nfg, F, B, S, inv_scale, H);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 

@@ -9,8 +9,11 @@ Reference: ``ConstructLocalBin.java:135-166`` (GBDT ``(g^2, g, h, 1)``) and ``pa
 (``Split.java:64-195``): ``node[r] = base[v] + route_tab[v, bins[r, feat[v]]]`` for an internal node ``v``
 and ``node[r] = base[v]`` (a negative leaf code) for a leaf.
 
-On a GPU the HIP kernels in ``csrc/tree_hist.hip`` run (fp32 LDS-privatised atomics); on the CPU the
-fp64 ``index_add_`` reference below is used.
+On a GPU the HIP kernels in ``csrc/tree_hist.hip`` run: by default ``tree_hist_fm`` (rows grouped by slot, a
+workgroup per (row chunk, 32-feature group), int64 fixed-point bank-private LDS histograms — LDS float
+atomics are ~30x slower than integer ones on gfx950 — and per-chunk slabs summed exactly); the older fp32
+LDS-atomic kernels stay for S > 4 or very wide bins.  On the CPU the fp64 ``index_add_`` reference
+below is used.
 """
 from __future__ import annotations
 
@@ -18,7 +21,7 @@ import torch
 
 from . import _lib
 
-__all__ = ["histogram", "histogram_torch", "route", "route_torch", "node_sums", "node_sums_torch", "quantize",
+__all__ = ["FmStats", "histogram", "histogram_torch", "route", "route_torch", "node_sums", "node_sums_torch", "quantize",
            "gbdt_split"]
 
 
@@ -52,13 +55,114 @@ def histogram_torch(bins: torch.Tensor, slot: torch.Tensor, stats: torch.Tensor,
 
 import os
 
-# 0: row-per-lane kernel (S in 2..4), 1: (row, feature)-pair kernel
-HIST_VARIANT = int(os.environ.get("ALINK_TREE_HIST_VARIANT", "0"))
+# 2: fixed-point bank-private feature-group kernel over slot-grouped rows (S <= 4, B * S <= 640; default),
+# 0: row-per-lane fp32-atomic kernel, 1: (row, feature)-pair fp32-atomic kernel
+HIST_VARIANT = int(os.environ.get("ALINK_TREE_HIST_VARIANT", "2"))
+FM_TARGET_BLOCKS = 2048       # histogram workgroups per launch (one 32-feature group x one row chunk each)
+FM_MIN_ROWS = 8192            # rows per chunk floor: the LDS clear + slab store amortise over >= 0.5 MB of bins
+
+
+def fm_plan(counts, nfg: int):
+    """Chunking of slot-grouped rows for ``tree_hist_fm``: ``counts[s]`` rows of slot s (consecutive in the
+    sorted order).  Returns (chunk_rows [nchunks+1], slot_chunk [nslots+1]) as int32 numpy arrays."""
+    import numpy as np
+    counts = np.asarray(counts, dtype=np.int64)
+    total = int(counts.sum())
+    R = max(FM_MIN_ROWS, -(-total * nfg // FM_TARGET_BLOCKS)) if total else FM_MIN_ROWS
+    nch = -(-counts // R)
+    slot_chunk = np.zeros(counts.size + 1, dtype=np.int64)
+    np.cumsum(nch, out=slot_chunk[1:])
+    starts = np.zeros(counts.size + 1, dtype=np.int64)
+    np.cumsum(counts, out=starts[1:])
+    bounds = [0]
+    for s_, c in enumerate(counts):
+        if c == 0:
+            continue
+        k = int(nch[s_])
+        edges = starts[s_] + (np.arange(1, k + 1, dtype=np.int64) * c) // k
+        bounds.extend(edges.tolist())
+    return np.asarray(bounds, dtype=np.int32), slot_chunk.astype(np.int32)
+
+
+def fm_scales(stats: torch.Tensor):
+    """Per-column power-of-two fixed-point scales for ``tree_hist_fm``: max|column| * scale < 2^30, so every
+    row's value fits int32 and no int64 bin sum can overflow below 2^33 rows."""
+    import math
+    # column-major copy first: a dim-0 reduction of a row-major [n, S] tensor is a slow strided kernel
+    amax = stats.t().contiguous().abs().amax(dim=1).double().cpu().numpy() if stats.numel() else []
+    scales = []
+    for m in amax:
+        m = float(m)
+        if not math.isfinite(m):
+            raise ValueError("non-finite tree statistics")
+        e = 30 - math.ceil(math.log2(m)) - 1 if m > 0 else 0
+        scales.append(math.ldexp(1.0, max(min(e, 1000), -1000)))
+    return scales
+
+
+class FmStats:
+    """Row statistics quantised once for ``tree_hist_fm`` (per tree: the statistics do not change between the
+    levels): ``q`` [n, 4] int32 fixed point, ``inv`` [S] fp64 device scales back to floats."""
+
+    def __init__(self, stats: torch.Tensor):
+        n, S = stats.shape
+        self.S = S
+        self.n = n
+        scales = fm_scales(stats)
+        dev = stats.device
+        self.q = torch.zeros((n, 4), dtype=torch.int32, device=dev)
+        self.q[:, :S] = torch.round(stats.double() * torch.tensor(scales, dtype=torch.float64, device=dev)) \
+            .to(torch.int32)
+        self.inv = torch.tensor([1.0 / x for x in scales], dtype=torch.float64, device=dev)
+
+
+def _histogram_fm(L, bins, slot, stats, nslots: int, B: int, prep: "FmStats" = None) -> torch.Tensor:
+    """``tree_hist_fm`` path: rows grouped by slot (stable sort of the slot keys, or the identity when every row
+    is in slot 0), statistics quantised to int64 fixed point (``prep``, or here) and gathered into that order,
+    chunk plan, kernel + exact fixed-order reduce."""
+    dev = bins.device
+    n, F = bins.shape
+    S = stats.shape[1] if stats is not None else prep.S
+    if prep is None:
+        prep = FmStats(stats)
+    act = (slot >= 0) & (slot < nslots)
+    if nslots == 1 and bool(act.all()):
+        ridx = None
+        counts = [n]
+        q = prep.q
+    else:
+        key = torch.where(act, slot, torch.full_like(slot, nslots))
+        counts_t = torch.bincount(key.to(torch.int64), minlength=nslots + 1)[:nslots]
+        _, order = torch.sort(key, stable=True)
+        counts = counts_t.cpu().numpy()
+        total = int(counts.sum())
+        ridx = order[:total].to(torch.int32).contiguous()
+        q = prep.q[order[:total]]
+    nfg = (F + 31) // 32
+    chunk_rows, slot_chunk = fm_plan(counts, nfg)
+    nchunks = chunk_rows.size - 1
+    cr = torch.from_numpy(chunk_rows).to(dev)
+    scn = torch.from_numpy(slot_chunk).to(dev)
+    slab = torch.empty(max(nchunks, 1) * nfg * B * S * 32, dtype=torch.int64, device=dev)
+    hist = torch.empty((nslots, F, B, S), dtype=torch.float32, device=dev)
+    rc = L.alink_tree_hist_fm(bins.data_ptr(), F, None if ridx is None else ridx.data_ptr(), q.data_ptr(),
+                              cr.data_ptr(), nchunks, scn.data_ptr(), nslots, S, B, prep.inv.data_ptr(),
+                              slab.data_ptr(), hist.data_ptr(), _lib.stream_ptr(dev))
+    if rc != 0:
+        raise RuntimeError(f"alink_tree_hist_fm failed: {rc}")
+    return hist
+
+
+def fm_eligible(bins: torch.Tensor, S: int, B: int, variant: int = None) -> bool:
+    v = HIST_VARIANT if variant is None else int(variant)
+    return bins.is_cuda and v == 2 and S <= 4 and B * S * 256 <= 160 * 1024 and bins.shape[0] < 2 ** 31 \
+        and _lib.available()
 
 
 def histogram(bins: torch.Tensor, slot: torch.Tensor, stats: torch.Tensor, nslots: int, B: int,
-              variant: int = None) -> torch.Tensor:
-    """[nslots, F, B, S] histogram (fp32 on GPU via HIP, fp64 on CPU)."""
+              variant: int = None, prep: FmStats = None) -> torch.Tensor:
+    """[nslots, F, B, S] histogram (fp32 on GPU via HIP, fp64 on CPU).  ``prep``: the statistics already
+    quantised for the fixed-point kernel (``FmStats(stats)``, reused across the levels of a tree)."""
     if not bins.is_cuda:
         return histogram_torch(bins, slot, stats, nslots, B)
     if not _lib.available() and _lib.torch_fallback_allowed():
@@ -74,6 +178,8 @@ def histogram(bins: torch.Tensor, slot: torch.Tensor, stats: torch.Tensor, nslot
     stats = stats.to(torch.float32).contiguous()
     if slot.shape[0] != n or stats.shape[0] != n:
         raise ValueError("slot/stats row count mismatch")
+    if fm_eligible(bins, S, B, variant) and nslots > 0:
+        return _histogram_fm(L, bins, slot, stats, nslots, B, prep)
     hist = torch.zeros((nslots, F, B, S), dtype=torch.float32, device=bins.device)
     if n == 0 or nslots == 0:
         return hist

@@ -208,7 +208,7 @@ def test_hip_histogram_and_route_match_torch():
         slot = torch.as_tensor(rng.integers(-1, nslots, size=n), dtype=torch.int32)
         stats = torch.as_tensor(rng.normal(size=(n, S)), dtype=torch.float32)
         ref = tops.histogram_torch(bins, slot, stats.double(), nslots, B)
-        for variant in (0, 1):
+        for variant in (0, 1, 2):
             got = tops.histogram(bins.cuda(), slot.cuda(), stats.cuda(), nslots, B, variant=variant).cpu().double()
             np.testing.assert_allclose(got.numpy(), ref.numpy(), rtol=1e-4, atol=2e-3)
     n, F = 70001, 5
@@ -220,6 +220,43 @@ def test_hip_histogram_and_route_match_torch():
     exp = tops.route_torch(bins, node, feat, base, route)
     got = tops.route(bins.cuda(), node.cuda().clone(), feat.cuda(), base.cuda(), route.cuda()).cpu()
     np.testing.assert_array_equal(got.numpy(), exp.numpy())
+
+
+def test_fm_plan_chunks_cover_slots_in_order():
+    plan_rows, slot_chunk = tops.fm_plan([0, 5, 100000, 0, 3], nfg=16)
+    assert plan_rows[0] == 0 and plan_rows[-1] == 100008
+    assert list(np.diff(slot_chunk)) == [0, 1, -(-100000 // max(tops.FM_MIN_ROWS, -(-100008 * 16 // tops.FM_TARGET_BLOCKS))), 0, 1]
+    # every chunk lies inside one slot's row range
+    starts = np.cumsum([0, 0, 5, 100000, 0, 3])
+    for s_ in range(5):
+        for c in range(slot_chunk[s_], slot_chunk[s_ + 1]):
+            assert starts[s_] <= plan_rows[c] < plan_rows[c + 1] <= starts[s_ + 1]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,F,B,S,nslots,sampled", [
+    (200000, 130, 129, 3, 1, False),      # identity row order, odd feature-group count (pair exits)
+    (150000, 130, 129, 3, 1, True),       # root with unsampled rows -> sorted path
+    (120000, 64, 129, 3, 64, True),       # deep level: many slots, some empty
+    (60000, 100, 33, 4, 7, True),
+    (60000, 1000, 17, 2, 3, True),
+    (30000, 65, 200, 1, 5, True),
+])
+def test_hip_histogram_fm_matches_torch(n, F, B, S, nslots, sampled):
+    """Bank-private feature-group histogram (tree_hist_fm + fixed-order slab reduce) vs the fp64 reference."""
+    rng = np.random.default_rng(n + F + B)
+    bins = torch.as_tensor(rng.integers(0, B, size=(n, F)), dtype=torch.uint8)
+    if nslots == 1:
+        slot = torch.zeros(n, dtype=torch.int32)
+        if sampled:
+            slot[torch.as_tensor(rng.random(n) < 0.3)] = -1
+    else:
+        slot = torch.as_tensor(rng.integers(-1, nslots, size=n), dtype=torch.int32)
+        slot[slot == 3] = -1                       # slot 3 empty
+    stats = torch.as_tensor(rng.normal(size=(n, S)), dtype=torch.float32)
+    ref = tops.histogram_torch(bins, slot, stats.double(), nslots, B)
+    got = tops.histogram(bins.cuda(), slot.cuda(), stats.cuda(), nslots, B, variant=2).cpu().double()
+    np.testing.assert_allclose(got.numpy(), ref.numpy(), rtol=1e-4, atol=2e-3)
 
 
 @pytest.mark.gpu
