@@ -156,7 +156,8 @@ class TreeBuilder:
         ws = comm.get_world_size()
         self.fshard = (not local and ws > 1 and cfg.kind == "gbdt" and not any(data.is_cat)
                        and __import__("os").environ.get("ALINK_GBDT_FEATURE_SHARD", "1") == "1")
-        self.Fb = -(-self.F // ws) if self.fshard else self.F          # features per rank (padded)
+        # features per rank, padded to whole 32-feature groups (the histogram kernel's unit)
+        self.Fb = -(-self.F // (ws * 32)) * 32 if self.fshard else self.F
         self._hist_sub = None          # (stats tensor, histogram columns, FmStats) of the tree being built
         self.f_lo = comm.get_rank() * self.Fb if self.fshard else 0
 
@@ -178,22 +179,45 @@ class TreeBuilder:
             prep = tops.FmStats(sub) if tops.fm_eligible(self.d.bins, len(cols), self.B) else None
             self._hist_sub = (stats, sub, prep)
         _, sub, prep = self._hist_sub
-        H = tops.histogram(self.d.bins, slot, sub, nslots, self.B, prep=prep)
+        TreeBuilder.HIST_BYTES.append(nslots * self.F * self.B * len(cols) * 4)
         if self.fshard:
-            # [slots, F, B, S] -> feature-major, pad F to P * Fb, reduce-scatter -> this rank's [slots, Fb, B, S]
-            ws = comm.get_world_size()
-            Ht = H.transpose(0, 1)
-            if ws * self.Fb != self.F:
-                Ht = torch.cat([Ht, torch.zeros((ws * self.Fb - self.F,) + tuple(Ht.shape[1:]), dtype=H.dtype,
-                                                device=H.device)])
-            H = comm.reduce_scatter(Ht.contiguous(), "sum").transpose(0, 1).contiguous()
-        elif not self.local:
-            comm.all_reduce(H, "sum")
+            H = self._histograms_sharded(slot, sub, nslots, prep)
+        else:
+            H = tops.histogram(self.d.bins, slot, sub, nslots, self.B, prep=prep)
+            if not self.local:
+                comm.all_reduce(H, "sum")
         if len(cols) != stats.shape[1]:
             full = torch.zeros(H.shape[:-1] + (stats.shape[1],), dtype=H.dtype, device=H.device)
             full[..., cols] = H
             H = full
         return H
+
+    RS_BLOCKS = int(__import__("os").environ.get("ALINK_GBDT_RS_BLOCKS", "4"))
+    RS_BYTES: List[int] = []          # reduce-scattered bytes per histogram piece (observability)
+    HIST_BYTES: List[int] = []        # full-width fp32 histogram bytes per histogram call (levels in order)
+
+    def _histograms_sharded(self, slot, sub, nslots: int, prep) -> torch.Tensor:
+        """Feature-block reduce-scatter overlapped with the histogram build: every rank's
+        block of Fb features is cut into G pieces; piece c of ALL ranks' blocks is built as one feature-major
+        histogram ([P * piece, slots, B, S]) and its reduce-scatter is issued asynchronously (RCCL comm stream)
+        while piece c+1 builds.  This rank keeps [slots, Fb, B, S] of its own block."""
+        ws = comm.get_world_size()
+        gpr = self.Fb // 32                                  # 32-feature groups per rank block
+        G = max(1, min(self.RS_BLOCKS, gpr))
+        ps = -(-gpr // G)                                    # groups per piece (last piece padded)
+        pend, real = [], []
+        pad = 1 << 26                                        # a group index past every feature: zero rows
+        for c in range(G):
+            lo = c * ps
+            if lo >= gpr:
+                break
+            fgs = [j * gpr + lo + t if lo + t < gpr else pad for j in range(ws) for t in range(ps)]
+            Hc = tops.histogram_groups(self.d.bins, slot, sub, nslots, self.B, fgs, prep)
+            TreeBuilder.RS_BYTES.append(int(Hc.numel() * Hc.element_size()))
+            pend.append(comm.reduce_scatter_async(Hc, "sum"))
+            real.append(min(ps, gpr - lo) * 32)
+        parts = [p.wait()[:k] for p, k in zip(pend, real)]
+        return torch.cat(parts).transpose(0, 1).contiguous()            # [slots, Fb, B, S]
 
     def _node_totals(self, node_of_row, sample, nnodes: int, stats) -> np.ndarray:
         """[nnodes, S] float64 per-node sums over the sampled rows (one pass over rows, then all-reduce)."""

@@ -240,14 +240,16 @@ __global__ __launch_bounds__(kFmThreads) void tree_hist_fm(const uint8_t* __rest
                                                            const int32_t* __restrict__ ridx,
                                                            const int32_t* __restrict__ q,
                                                            const int32_t* __restrict__ chunk_rows, int nchunks,
-                                                           int nfg, int B, long long* __restrict__ slab) {
+                                                           const int32_t* __restrict__ fgl, int nfg, int B,
+                                                           long long* __restrict__ slab) {
   extern __shared__ long long lq[];
   const int bid = blockIdx.x;
   const int nquad = (nfg + 3) >> 2;
   const int quad_id = (bid >> 5) * 8 + (bid & 7);
   const int c = quad_id / nquad;
-  const int fg = (quad_id - c * nquad) * 4 + ((bid >> 3) & 3);
-  if (c >= nchunks || fg >= nfg) return;                 // whole block, before any barrier
+  const int pos = (quad_id - c * nquad) * 4 + ((bid >> 3) & 3);   // entry of the feature-group list
+  if (c >= nchunks || pos >= nfg) return;                // whole block, before any barrier
+  const int fg = fgl != nullptr ? fgl[pos] : pos;
   const int n_e = B * S * 32;
   for (int i = threadIdx.x; i < n_e; i += kFmThreads) lq[i] = 0;
   __syncthreads();
@@ -308,19 +310,23 @@ __global__ __launch_bounds__(kFmThreads) void tree_hist_fm(const uint8_t* __rest
     }
   }
   __syncthreads();
-  long long* dst = slab + ((int64_t)c * nfg + fg) * n_e;
+  long long* dst = slab + ((int64_t)c * nfg + pos) * n_e;
   for (int j = threadIdx.x; j < n_e; j += kFmThreads) dst[j] = lq[j];
 }
 
-// H[slot][fg*32 + l][b][k] = inv_scale[k] * sum over the slot's chunks of slab[chunk][fg][b][k][l] (exact int64
-// sums); a block owns (slot, feature group, 8 bins) and transposes through LDS (row stride 33: conflict-free).
+// H[slot][fg*32 + l][b][k] = inv_scale[k] * sum over the slot's chunks of slab[chunk][pos][b][k][l] (exact int64
+// sums), fg = fgl[pos]; feature-major mode writes Hfm[pos*32 + l][slot][b][k] instead (every row, zeros for
+// features >= F: the layout a per-rank reduce-scatter sends).  A block owns (slot, list entry, 8 bins) and
+// transposes through LDS (row stride 33: conflict-free).
 constexpr int kRedBins = 8;
 __global__ __launch_bounds__(256) void tree_hist_fm_reduce(const long long* __restrict__ slab,
-                                                           const int32_t* __restrict__ slot_chunk, int nfg, int F,
-                                                           int B, int S, const double* __restrict__ inv_scale,
-                                                           float* __restrict__ H) {
+                                                           const int32_t* __restrict__ slot_chunk,
+                                                           const int32_t* __restrict__ fgl, int nfg, int nslots,
+                                                           int F, int B, int S, const double* __restrict__ inv_scale,
+                                                           int feat_major, float* __restrict__ H) {
   __shared__ float tile[kRedBins * 4 * 33];
-  const int s = blockIdx.x / nfg, fg = blockIdx.x - (blockIdx.x / nfg) * nfg;
+  const int s = blockIdx.x / nfg, pos = blockIdx.x - (blockIdx.x / nfg) * nfg;
+  const int fg = fgl != nullptr ? fgl[pos] : pos;
   const int b0 = blockIdx.y * kRedBins;
   const int nb = min(kRedBins, B - b0);
   const int n_e = B * S * 32;
@@ -328,7 +334,7 @@ __global__ __launch_bounds__(256) void tree_hist_fm_reduce(const long long* __re
   const int cs = slot_chunk[s], ce = slot_chunk[s + 1];
   for (int t = threadIdx.x; t < m; t += 256) {
     long long acc = 0;
-    for (int j = cs; j < ce; ++j) acc += slab[((int64_t)j * nfg + fg) * n_e + (int64_t)b0 * S * 32 + t];
+    for (int j = cs; j < ce; ++j) acc += slab[((int64_t)j * nfg + pos) * n_e + (int64_t)b0 * S * 32 + t];
     const int k = (t >> 5) % S;
     tile[(t >> 5) * 33 + (t & 31)] = (float)((double)acc * inv_scale[k]);
   }
@@ -336,23 +342,28 @@ __global__ __launch_bounds__(256) void tree_hist_fm_reduce(const long long* __re
   const int w = nb * S;
   for (int t = threadIdx.x; t < 32 * w; t += 256) {
     const int l = t / w, j = t - (t / w) * w;
-    const int f = fg * 32 + l;
-    if (f < F) H[(((int64_t)s * F + f) * B + b0) * S + j] = tile[j * 33 + l];
+    if (feat_major) {
+      H[(((int64_t)(pos * 32 + l) * nslots + s) * B + b0) * S + j] = tile[j * 33 + l];
+    } else {
+      const int f = fg * 32 + l;
+      if (f < F) H[(((int64_t)s * F + f) * B + b0) * S + j] = tile[j * 33 + l];
+    }
   }
 }
 
 template <int S>
 int launch_fm(bool idx, int64_t grid, size_t lds, hipStream_t stream, const uint8_t* bins, int F, const int32_t* ridx,
-              const int32_t* sst, const int32_t* chunk_rows, int nchunks, int nfg, int B, long long* slab) {
+              const int32_t* sst, const int32_t* chunk_rows, int nchunks, const int32_t* fgl, int nfg, int B,
+              long long* slab) {
   const void* k = idx ? reinterpret_cast<const void*>(tree_hist_fm<S, true>)
                       : reinterpret_cast<const void*>(tree_hist_fm<S, false>);
   if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return 3;
   if (idx)
     hipLaunchKernelGGL((tree_hist_fm<S, true>), dim3((unsigned)grid), dim3(kFmThreads), lds, stream, bins, F, ridx, sst,
-                       chunk_rows, nchunks, nfg, B, slab);
+                       chunk_rows, nchunks, fgl, nfg, B, slab);
   else
     hipLaunchKernelGGL((tree_hist_fm<S, false>), dim3((unsigned)grid), dim3(kFmThreads), lds, stream, bins, F, ridx,
-                       sst, chunk_rows, nchunks, nfg, B, slab);
+                       sst, chunk_rows, nchunks, fgl, nfg, B, slab);
   return 0;
 }
 
@@ -442,28 +453,30 @@ int alink_tree_hist_f32(const uint8_t* bins, int64_t n, int F, const int32_t* sl
 // Fixed-point histogram (tree_hist_fm): rows grouped by slot.  ridx: [total] row ids sorted by slot (nullptr =
 // identity: rows 0..total-1 all in slot 0); q: [total, 4] int32 quantised statistics in that order;
 // chunk_rows: [nchunks+1] row offsets (each chunk inside one slot); slot_chunk: [nslots+1] chunk ranges per
-// slot; inv_scale: [S] fp64 (device); slab: [nchunks, nfg, B, S, 32] int64 scratch; H: [nslots, F, B, S] fp32
-// (fully written, no zeroing needed).
+// slot; fgl: [nfl] 32-feature groups to build (nullptr: all, nfl ignored); inv_scale: [S] fp64 (device);
+// slab: [nchunks, nfl, B, S, 32] int64 scratch; H: [nslots, F, B, S] fp32, or with feat_major
+// [nfl * 32, nslots, B, S] (fully written, no zeroing needed).
 int alink_tree_hist_fm(const uint8_t* bins, int F, const int32_t* ridx, const int32_t* q, const int32_t* chunk_rows,
-                       int nchunks, const int32_t* slot_chunk, int nslots, int S, int B, const double* inv_scale,
-                       long long* slab, float* H, hipStream_t stream) {
+                       int nchunks, const int32_t* slot_chunk, int nslots, int S, int B, const int32_t* fgl, int nfl,
+                       int feat_major, const double* inv_scale, long long* slab, float* H, hipStream_t stream) {
   if (nslots <= 0) return 0;
   if (F <= 0 || S < 1 || S > 4 || B <= 0 || B > 256) return 1;
   const size_t lds = (size_t)B * S * 32 * sizeof(long long);
   if (lds > 160 * 1024) return 1;
-  const int nfg = (F + 31) / 32;
+  const int nfg = fgl != nullptr ? nfl : (F + 31) / 32;
+  if (nfg <= 0) return 0;
   if (nchunks > 0) {
     const int64_t quads = (int64_t)nchunks * ((nfg + 3) / 4);
     const int64_t grid = (quads + 7) / 8 * 32;
     if (grid > 0x7fffffff) return 1;
-    const int rc = S == 1 ? launch_fm<1>(ridx != nullptr, grid, lds, stream, bins, F, ridx, q, chunk_rows, nchunks, nfg, B, slab)
-                 : S == 2 ? launch_fm<2>(ridx != nullptr, grid, lds, stream, bins, F, ridx, q, chunk_rows, nchunks, nfg, B, slab)
-                 : S == 3 ? launch_fm<3>(ridx != nullptr, grid, lds, stream, bins, F, ridx, q, chunk_rows, nchunks, nfg, B, slab)
-                          : launch_fm<4>(ridx != nullptr, grid, lds, stream, bins, F, ridx, q, chunk_rows, nchunks, nfg, B, slab);
+    const int rc = S == 1 ? launch_fm<1>(ridx != nullptr, grid, lds, stream, bins, F, ridx, q, chunk_rows, nchunks, fgl, nfg, B, slab)
+                 : S == 2 ? launch_fm<2>(ridx != nullptr, grid, lds, stream, bins, F, ridx, q, chunk_rows, nchunks, fgl, nfg, B, slab)
+                 : S == 3 ? launch_fm<3>(ridx != nullptr, grid, lds, stream, bins, F, ridx, q, chunk_rows, nchunks, fgl, nfg, B, slab)
+                          : launch_fm<4>(ridx != nullptr, grid, lds, stream, bins, F, ridx, q, chunk_rows, nchunks, fgl, nfg, B, slab);
     if (rc != 0) return rc;
   }
   hipLaunchKernelGGL(tree_hist_fm_reduce, dim3((unsigned)(nslots * nfg), (unsigned)((B + kRedBins - 1) / kRedBins)),
-                     dim3(256), 0, stream, slab, slot_chunk, nfg, F, B, S, inv_scale, H);
+                     dim3(256), 0, stream, slab, slot_chunk, fgl, nfg, nslots, F, B, S, inv_scale, feat_major, H);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 

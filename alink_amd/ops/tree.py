@@ -21,7 +21,7 @@ import torch
 
 from . import _lib
 
-__all__ = ["FmStats", "histogram", "histogram_torch", "route", "route_torch", "node_sums", "node_sums_torch", "quantize",
+__all__ = ["FmStats", "histogram", "histogram_groups", "histogram_torch", "route", "route_torch", "node_sums", "node_sums_torch", "quantize",
            "gbdt_split"]
 
 
@@ -116,10 +116,11 @@ class FmStats:
         self.inv = torch.tensor([1.0 / x for x in scales], dtype=torch.float64, device=dev)
 
 
-def _histogram_fm(L, bins, slot, stats, nslots: int, B: int, prep: "FmStats" = None) -> torch.Tensor:
+def _histogram_fm(L, bins, slot, stats, nslots: int, B: int, prep: "FmStats" = None, fgroups=None) -> torch.Tensor:
     """``tree_hist_fm`` path: rows grouped by slot (stable sort of the slot keys, or the identity when every row
     is in slot 0), statistics quantised to int64 fixed point (``prep``, or here) and gathered into that order,
-    chunk plan, kernel + exact fixed-order reduce."""
+    chunk plan, kernel + exact fixed-order reduce.  ``fgroups`` (int sequence of 32-feature groups): build only
+    those, feature-major ``[len(fgroups) * 32, nslots, B, S]``."""
     dev = bins.device
     n, F = bins.shape
     S = stats.shape[1] if stats is not None else prep.S
@@ -138,19 +139,50 @@ def _histogram_fm(L, bins, slot, stats, nslots: int, B: int, prep: "FmStats" = N
         total = int(counts.sum())
         ridx = order[:total].to(torch.int32).contiguous()
         q = prep.q[order[:total]]
-    nfg = (F + 31) // 32
+    if fgroups is None:
+        nfg, fgl = (F + 31) // 32, None
+        hist = torch.empty((nslots, F, B, S), dtype=torch.float32, device=dev)
+    else:
+        nfg = len(fgroups)
+        fgl = torch.as_tensor(list(fgroups), dtype=torch.int32).to(dev)
+        hist = torch.empty((nfg * 32, nslots, B, S), dtype=torch.float32, device=dev)
+        if nfg == 0:
+            return hist
     chunk_rows, slot_chunk = fm_plan(counts, nfg)
     nchunks = chunk_rows.size - 1
     cr = torch.from_numpy(chunk_rows).to(dev)
     scn = torch.from_numpy(slot_chunk).to(dev)
     slab = torch.empty(max(nchunks, 1) * nfg * B * S * 32, dtype=torch.int64, device=dev)
-    hist = torch.empty((nslots, F, B, S), dtype=torch.float32, device=dev)
     rc = L.alink_tree_hist_fm(bins.data_ptr(), F, None if ridx is None else ridx.data_ptr(), q.data_ptr(),
-                              cr.data_ptr(), nchunks, scn.data_ptr(), nslots, S, B, prep.inv.data_ptr(),
-                              slab.data_ptr(), hist.data_ptr(), _lib.stream_ptr(dev))
+                              cr.data_ptr(), nchunks, scn.data_ptr(), nslots, S, B,
+                              None if fgl is None else fgl.data_ptr(), nfg, int(fgl is not None),
+                              prep.inv.data_ptr(), slab.data_ptr(), hist.data_ptr(), _lib.stream_ptr(dev))
     if rc != 0:
         raise RuntimeError(f"alink_tree_hist_fm failed: {rc}")
     return hist
+
+
+def histogram_groups(bins: torch.Tensor, slot: torch.Tensor, stats: torch.Tensor, nslots: int, B: int,
+                     fgroups, prep: "FmStats" = None) -> torch.Tensor:
+    """Feature-major histogram of the 32-feature groups ``fgroups`` only: ``[len(fgroups) * 32, nslots, B, S]``
+    (features >= F, e.g. padding groups of the last rank's block, are zero rows) — the unit a per-rank
+    feature-block reduce-scatter sends.  GPU: the fixed-point kernel over the listed groups; CPU: the fp64
+    reference over the selected columns."""
+    n, F = bins.shape
+    S = stats.shape[1]
+    if fm_eligible(bins, S, B):
+        return _histogram_fm(_lib.require(), bins, slot.to(torch.int32).contiguous(), stats, nslots, B, prep,
+                             fgroups=fgroups)
+    feats = torch.tensor([g * 32 + l for g in fgroups for l in range(32)], dtype=torch.long)
+    out = torch.zeros((feats.numel(), nslots, B, S), dtype=torch.float32 if bins.is_cuda else torch.float64,
+                      device=bins.device)
+    ok = (feats < F).nonzero().reshape(-1)
+    if ok.numel():
+        sub = bins[:, feats[ok].to(bins.device)].contiguous()
+        h = histogram_torch(sub, slot, stats, nslots, B, dtype=out.dtype) if not bins.is_cuda else \
+            histogram(sub, slot, stats, nslots, B)
+        out[ok.to(out.device)] = h.transpose(0, 1).to(out.dtype)
+    return out
 
 
 def fm_eligible(bins: torch.Tensor, S: int, B: int, variant: int = None) -> bool:

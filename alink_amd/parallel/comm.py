@@ -28,7 +28,8 @@ from ..utils import trace as _trace
 
 __all__ = ["init_distributed", "get_rank", "get_world_size", "is_distributed", "all_reduce", "all_gather_object",
            "broadcast_object", "barrier", "all_gather_tensor", "all_to_all_objects", "reduce_scatter",
-           "object_group", "device_for_rank", "CommStats", "STATS", "shutdown", "all_reduce_coalesced"]
+           "object_group", "device_for_rank", "CommStats", "STATS", "shutdown", "all_reduce_coalesced",
+           "Pending", "reduce_scatter_async"]
 
 _OBJ_GROUP = None
 
@@ -270,6 +271,54 @@ def reduce_scatter(t: torch.Tensor, op: str = "sum") -> torch.Tensor:
     all_reduce(full, op)
     r = get_rank()
     return full[r * out.shape[0]:(r + 1) * out.shape[0]].clone()
+
+
+class Pending:
+    """Handle of an in-flight collective (``*_async``).  Under RCCL the collective runs on the process group's
+    own communication stream: issuing it records an event on the caller's current stream that the comm
+    stream waits on, so kernels the caller launches afterwards overlap with it; ``wait()`` makes the caller's
+    current stream wait on the collective's completion event (no host block) and returns the result.  Under
+    gloo the collective runs on gloo's thread and ``wait()`` joins it."""
+
+    __slots__ = ("_work", "_result", "_post", "_keep")
+
+    def __init__(self, result, work=None, post=None, keep=()):
+        self._work = work
+        self._result = result
+        self._post = post
+        self._keep = keep            # inputs must outlive the collective
+
+    def wait(self) -> torch.Tensor:
+        if self._work is not None:
+            self._work.wait()
+            self._work = None
+        if self._post is not None:
+            self._result = self._post(self._result)
+            self._post = None
+        self._keep = ()
+        return self._result
+
+
+def reduce_scatter_async(t: torch.Tensor, op: str = "sum") -> Pending:
+    """Asynchronous ``reduce_scatter`` (dim 0 split over ranks): returns a ``Pending`` whose ``wait()`` yields
+    this rank's block.  Used to overlap per-block histogram reductions with building the next block."""
+    ws = get_world_size()
+    if ws == 1:
+        return Pending(t)
+    rop = getattr(dist.ReduceOp, _OPS[op.lower()])
+    STATS.calls += 1
+    STATS.bytes += t.numel() * t.element_size()
+    rows = t.shape[0] // ws
+    if _backend() == "nccl":
+        d = (t if t.is_cuda else t.to(device_for_rank())).contiguous()
+        o = torch.empty((rows,) + tuple(t.shape[1:]), dtype=t.dtype, device=d.device)
+        work = dist.reduce_scatter_tensor(o, d, op=rop, async_op=True)
+        return Pending(o, work, None if t.is_cuda else (lambda x: x.cpu()), keep=(d,))
+    full = t.detach().cpu().clone()
+    work = dist.all_reduce(full, op=rop, async_op=True)
+    r = get_rank()
+    dev = t.device
+    return Pending(full, work, lambda x: x[r * rows:(r + 1) * rows].clone().to(dev))
 
 
 @_collective

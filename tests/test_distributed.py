@@ -96,13 +96,30 @@ def test_trees_two_processes_equal_single(tmp_path, scenario):
 
 
 def test_gbdt_feature_sharded_histograms_three_ranks(tmp_path):
-    """GBDT over 3 ranks reduce-scatters histograms by feature block (7 features -> blocks of 3, last padded) and
-    grows the same trees as one rank."""
+    """GBDT over 3 ranks reduce-scatters histograms by feature block (7 features -> 32-feature blocks, the other
+    ranks' blocks all padding) and grows the same trees as one rank."""
     one = _run("gbdt_wide", 1, tmp_path)[0]
     three = _run("gbdt_wide", 3, tmp_path)
     assert one["sharded"] == 0 and all(o["sharded"] > 0 for o in three)
     assert three[0]["model"] == three[1]["model"] == three[2]["model"]
     ta, tb = _tree_nodes(one["model"]), _tree_nodes(three[0]["model"])
+    assert len(ta) == len(tb)
+    for a, b in zip(ta, tb):
+        assert a["node"]["featureIndex"] == b["node"]["featureIndex"]
+        assert a["node"].get("continuousSplit") == pytest.approx(b["node"].get("continuousSplit"))
+        np.testing.assert_allclose(a["node"]["counter"]["distributions"], b["node"]["counter"]["distributions"],
+                                   rtol=1e-5, atol=1e-7)
+
+
+def test_gbdt_pipelined_feature_block_reduce_scatter_two_ranks(tmp_path):
+    """200 features over 2 ranks: each histogram is built and reduce-scattered in 4 feature pieces (the
+    reduce-scatter of piece c in flight while piece c+1 builds); the trees equal the 1-rank trees."""
+    one = _run("gbdt_many", 1, tmp_path)[0]
+    two = _run("gbdt_many", 2, tmp_path)
+    assert one["sharded"] == 0 and all(o["sharded"] > 0 for o in two)
+    assert all(o["rs_calls"] >= 4 and o["rs_calls"] % 4 == 0 for o in two)      # 4 pieces per histogram
+    assert two[0]["model"] == two[1]["model"]
+    ta, tb = _tree_nodes(one["model"]), _tree_nodes(two[0]["model"])
     assert len(ta) == len(tb)
     for a, b in zip(ta, tb):
         assert a["node"]["featureIndex"] == b["node"]["featureIndex"]

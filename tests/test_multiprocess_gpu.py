@@ -74,3 +74,18 @@ def test_kmeans_multiprocess_gpu_matches_one_rank(tmp_path):
             assert abs(x["weight"] - y["weight"]) <= max(2.0, 1e-4 * x["weight"])
             np.testing.assert_allclose(np.asarray(x["vec"]["data"]), np.asarray(y["vec"]["data"]), rtol=1e-4,
                                        atol=1e-4)
+
+
+def test_gbdt_feature_sharded_multiprocess_gpu_matches_one_rank(tmp_path):
+    """2 ranks on one GPU: device histograms of each rank's feature pieces, asynchronous per-piece
+    reduce-scatter, and the same trees as one rank (the fixed-point histogram sums are exact, so the split
+    choices cannot depend on the partitioning)."""
+    one = _run("gbdt", 1, tmp_path)[0]
+    two = _run("gbdt", 2, tmp_path)
+    assert "cuda" in one["device"]
+    assert one["sharded"] == 0 and all(o["sharded"] > 0 and o["rs_calls"] > 0 for o in two)
+    assert two[0]["model"] == two[1]["model"]
+    import json as _json
+    ta = [_json.loads(r[1]) for r in one["model"] if r[0] >= 0 and r[1]]
+    tb = [_json.loads(r[1]) for r in two[0]["model"] if r[0] >= 0 and r[1]]
+    assert len(ta) == len(tb)

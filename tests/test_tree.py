@@ -260,6 +260,23 @@ def test_hip_histogram_fm_matches_torch(n, F, B, S, nslots, sampled):
 
 
 @pytest.mark.gpu
+def test_hip_histogram_groups_feature_major_matches_torch():
+    """Feature-block build for the pipelined reduce-scatter: listed 32-feature groups (incl. padding groups past
+    F), feature-major output, vs the fp64 reference."""
+    rng = np.random.default_rng(5)
+    n, F, B, S, nslots = 50000, 100, 65, 3, 6
+    bins = torch.as_tensor(rng.integers(0, B, size=(n, F)), dtype=torch.uint8)
+    slot = torch.as_tensor(rng.integers(-1, nslots, size=n), dtype=torch.int32)
+    stats = torch.as_tensor(rng.normal(size=(n, S)), dtype=torch.float32)
+    groups = [2, 3, 1 << 26, 0]
+    got = tops.histogram_groups(bins.cuda(), slot.cuda(), stats.cuda(), nslots, B, groups).cpu().double()
+    ref = tops.histogram_groups(bins, slot, stats.double(), nslots, B, groups)
+    assert got.shape == (128, nslots, B, S)
+    np.testing.assert_allclose(got.numpy(), ref.numpy(), rtol=1e-4, atol=2e-3)
+    assert float(got[64:96].abs().sum()) == 0.0 and float(got[36:64].abs().sum()) == 0.0    # f >= F: zeros
+
+
+@pytest.mark.gpu
 def test_gbdt_on_gpu_matches_doc():
     useLocalEnv(1)
     train = GbdtTrainBatchOp().setLearningRate(1.0).setNumTrees(3).setMinSamplesPerLeaf(1) \

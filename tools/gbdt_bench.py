@@ -23,6 +23,8 @@ def main():
     ap.add_argument("--depth", type=int, default=6)
     ap.add_argument("--bins", type=int, default=128)
     ap.add_argument("--dtype", default="float64", choices=["float32", "float64"])
+    ap.add_argument("--ranks", type=int, default=8,
+                    help="world size for the projected per-rank reduce-scatter traffic per level")
     a = ap.parse_args()
     from alink_amd import useLocalEnv, GbdtTrainBatchOp
     from alink_amd.common.table import MTable, Column
@@ -50,6 +52,8 @@ def main():
     src = TableSourceBatchOp(mt)
     op = GbdtTrainBatchOp().setFeatureCols(names[:-1]).setLabelCol("label").setNumTrees(a.trees) \
         .setMaxDepth(a.depth).setMaxBins(a.bins).setMinSamplesPerLeaf(100)
+    from alink_amd.models.tree.engine import TreeBuilder
+    TreeBuilder.HIST_BYTES.clear()
     if dev.type == "cuda":
         torch.cuda.synchronize()
     t0 = time.time()
@@ -68,7 +72,13 @@ def main():
                       "hist_allreduce_bytes_deepest_level": hist_bytes,
                       "bin_matrix_bytes": a.rows * a.features, "binning_s": (info or {}).get("binning_s"),
                       "trees_s": (info or {}).get("trees_s"),
-                      "s_per_tree": ((info or {}).get("trees_s") or dt) / a.trees}))
+                      "s_per_tree": ((info or {}).get("trees_s") or dt) / a.trees,
+                      # histogram calls of the whole run (root + one per level per tree): the full-width bytes
+                      # every rank reduce-scatters, and what one rank sends = (P-1)/P of it at P = --ranks
+                      "hist_bytes_per_level_tree0": TreeBuilder.HIST_BYTES[:a.depth],
+                      "reduce_scatter_send_bytes_per_rank_per_tree": int(sum(TreeBuilder.HIST_BYTES) / a.trees
+                                                                          * (a.ranks - 1) / a.ranks),
+                      "projected_ranks": a.ranks}))
 
 
 if __name__ == "__main__":
