@@ -11,7 +11,7 @@ from typing import List, Optional, Sequence
 
 import numpy as np
 
-__all__ = ["lib", "parse_csv_lines", "murmur3_utf16", "parse_dense_vectors", "ftrl_update_csr",
+__all__ = ["lib", "parse_csv_lines", "murmur3_utf16", "murmur3_bytes", "murmur3_utf8", "parse_dense_vectors", "ftrl_update_csr",
            "ftrl_partial_margin", "ftrl_shard_update", "parse_binary_detail", "java_double_join"]
 
 # ALINK_NATIVE_LIB points at another build of the same sources (e.g. the AddressSanitizer build of
@@ -24,6 +24,9 @@ if os.path.exists(_PATH):
         lib = ctypes.CDLL(_PATH)
         lib.alink_csv_parse.restype = ctypes.c_int
         lib.alink_murmur3_utf16_batch.restype = None
+        if hasattr(lib, "alink_murmur3_bytes_batch"):
+            lib.alink_murmur3_bytes_batch.restype = None
+            lib.alink_murmur3_utf8_batch.restype = None
         lib.alink_parse_dense_vectors.restype = ctypes.c_int
         lib.alink_ftrl_update_csr.restype = ctypes.c_int
         lib.alink_ftrl_partial_margin.restype = ctypes.c_int
@@ -110,6 +113,30 @@ def murmur3_utf16(strings: Sequence[str], seed: int = 0) -> Optional[np.ndarray]
     out = np.zeros(len(units), dtype=np.int32)
     lib.alink_murmur3_utf16_batch(_ptr(chars), _ptr(off), ctypes.c_int64(len(units)), ctypes.c_uint32(seed),
                                   _ptr(out))
+    return out
+
+
+def murmur3_bytes(data: np.ndarray, off: np.ndarray, seed: int = 0) -> Optional[np.ndarray]:
+    """MurmurHash3_x86_32 of packed byte strings (uint8 ``data``, int64 ``off[n+1]``) -> int32 [n]."""
+    if lib is None or not hasattr(lib, "alink_murmur3_bytes_batch"):
+        return None
+    data = np.ascontiguousarray(data, dtype=np.uint8) if data.size else np.zeros(1, np.uint8)
+    off = np.ascontiguousarray(off, dtype=np.int64)
+    out = np.zeros(off.size - 1, dtype=np.int32)
+    lib.alink_murmur3_bytes_batch(_ptr(data), _ptr(off), ctypes.c_int64(out.size), ctypes.c_uint32(seed), _ptr(out))
+    return out
+
+
+def murmur3_utf8(data: np.ndarray, off: np.ndarray, prefix: str = "", seed: int = 0) -> Optional[np.ndarray]:
+    """Guava ``hashUnencodedChars(prefix + s)`` of packed UTF-8 strings -> int32 [n]."""
+    if lib is None or not hasattr(lib, "alink_murmur3_utf8_batch"):
+        return None
+    data = np.ascontiguousarray(data, dtype=np.uint8) if data.size else np.zeros(1, np.uint8)
+    off = np.ascontiguousarray(off, dtype=np.int64)
+    pu = np.frombuffer(prefix.encode("utf-16-le"), dtype=np.uint16).copy() if prefix else np.zeros(1, np.uint16)
+    out = np.zeros(off.size - 1, dtype=np.int32)
+    lib.alink_murmur3_utf8_batch(_ptr(data), _ptr(off), ctypes.c_int64(out.size), _ptr(pu),
+                                 ctypes.c_int(len(prefix.encode("utf-16-le")) // 2), ctypes.c_uint32(seed), _ptr(out))
     return out
 
 

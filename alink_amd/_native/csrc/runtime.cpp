@@ -168,6 +168,70 @@ void alink_murmur3_utf16_batch(const uint16_t* chars, const int64_t* off, int64_
     for (int64_t i = 0; i < n; ++i) out[i] = murmur3_utf16(chars + off[i], off[i + 1] - off[i], seed);
 }
 
+// MurmurHash3_x86_32(seed) over raw bytes (Guava murmur3_32().hashBytes) for n packed strings (bytes, off[n+1])
+void alink_murmur3_bytes_batch(const uint8_t* bytes, const int64_t* off, int64_t n, uint32_t seed, int32_t* out) {
+#pragma omp parallel for schedule(static) if (n > 65536)
+    for (int64_t s = 0; s < n; ++s) {
+        const uint8_t* p = bytes + off[s];
+        const int64_t len = off[s + 1] - off[s];
+        uint32_t h1 = seed;
+        const int64_t nb = len >> 2;
+        for (int64_t i = 0; i < nb; ++i) {
+            uint32_t k;
+            std::memcpy(&k, p + 4 * i, 4);
+            h1 = mix_h1(h1, mix_k1(k));
+        }
+        uint32_t k1 = 0;
+        const uint8_t* t = p + 4 * nb;
+        switch (len & 3) {
+            case 3: k1 ^= (uint32_t)t[2] << 16; [[fallthrough]];
+            case 2: k1 ^= (uint32_t)t[1] << 8; [[fallthrough]];
+            case 1: k1 ^= t[0]; h1 ^= mix_k1(k1);
+        }
+        out[s] = (int32_t)fmix(h1, (uint32_t)len);
+    }
+}
+
+// Guava hashUnencodedChars(seed) of prefix (UTF-16 units) ++ the packed UTF-8 strings, decoded to UTF-16 units
+// on the fly (the host twin of the HIP murmur3_utf8_index_kernel)
+void alink_murmur3_utf8_batch(const uint8_t* bytes, const int64_t* off, int64_t n, const uint16_t* prefix, int plen,
+                              uint32_t seed, int32_t* out) {
+#pragma omp parallel for schedule(static) if (n > 65536)
+    for (int64_t s = 0; s < n; ++s) {
+        uint32_t h1 = seed, pending = 0;
+        int64_t cnt = 0;
+        auto push = [&](uint32_t u) {
+            if (cnt & 1) h1 = mix_h1(h1, mix_k1(pending | (u << 16)));
+            else pending = u;
+            ++cnt;
+        };
+        for (int j = 0; j < plen; ++j) push(prefix[j]);
+        const uint8_t* p = bytes + off[s];
+        const int64_t len = off[s + 1] - off[s];
+        for (int64_t i = 0; i < len;) {
+            const uint32_t b0 = p[i];
+            uint32_t cp;
+            if (b0 < 0x80u) { cp = b0; i += 1; }
+            else if (b0 < 0xE0u && i + 1 < len) { cp = ((b0 & 0x1Fu) << 6) | (p[i + 1] & 0x3Fu); i += 2; }
+            else if (b0 < 0xF0u && i + 2 < len) {
+                cp = ((b0 & 0x0Fu) << 12) | ((p[i + 1] & 0x3Fu) << 6) | (p[i + 2] & 0x3Fu); i += 3;
+            } else if (i + 3 < len) {
+                cp = ((b0 & 0x07u) << 18) | ((p[i + 1] & 0x3Fu) << 12) | ((p[i + 2] & 0x3Fu) << 6) | (p[i + 3] & 0x3Fu);
+                i += 4;
+            } else { cp = 0xFFFDu; i += 1; }
+            if (cp >= 0x10000u) {
+                const uint32_t c = cp - 0x10000u;
+                push(0xD800u + (c >> 10));
+                push(0xDC00u + (c & 0x3FFu));
+            } else {
+                push(cp);
+            }
+        }
+        if (cnt & 1) h1 ^= mix_k1(pending);
+        out[s] = (int32_t)fmix(h1, (uint32_t)(2 * cnt));
+    }
+}
+
 // dense vector strings -> row-major [n][d] doubles (missing tail = 0); returns -1 - row on error
 int alink_parse_dense_vectors(const char* buf, const int64_t* off, int64_t n, int64_t d, double* out) {
     int64_t err = -1;

@@ -7,7 +7,9 @@ or — for small tables such as models — a full *replicated* copy.
 Columns are stored natively:
   * numeric/boolean -> 1-D ``torch.Tensor`` (+ optional bool null mask), on CPU or the rank's GPU;
   * dense-vector block -> 2-D ``torch.Tensor`` ``[n, d]`` (bf16/fp32/fp64), e.g. GPU-resident features;
-  * everything else (strings, mixed vectors, objects) -> Python ``list`` (``None`` = SQL NULL).
+  * strings -> Python ``list``, or a packed ``StringBlock`` (UTF-8 bytes + offsets tensors, host or device:
+    what shuffles, key hashing and the feature hasher move and read in bulk);
+  * everything else (mixed vectors, objects) -> Python ``list`` (``None`` = SQL NULL).
 Row-level access (``rows()``/``collect()``) materialises Python values (``DenseVector`` for vector blocks).
 """
 from __future__ import annotations
@@ -18,6 +20,7 @@ import numpy as np
 import torch
 
 from .linalg import DenseVector, SparseBlock, SparseVector, Vector, VectorUtil
+from .strings import StringBlock
 from .types import TableSchema, Types, AlinkType, is_numeric, schema_str_to_schema
 
 __all__ = ["Row", "Column", "MTable", "infer_type"]
@@ -97,6 +100,8 @@ class Column:
 
     def to_list(self) -> List[Any]:
         v = self.values
+        if isinstance(v, StringBlock):
+            return v.to_list()
         if isinstance(v, SparseBlock):
             lst = v.to_list()
             if self.nulls is not None:
@@ -116,6 +121,8 @@ class Column:
     def take(self, idx) -> "Column":
         """Row selection by index tensor/list or boolean mask."""
         v = self.values
+        if isinstance(v, StringBlock):
+            return Column(v.take(idx))
         if isinstance(v, SparseBlock):
             nn = None
             if self.nulls is not None:
@@ -146,6 +153,8 @@ class Column:
     def concat(cols: List["Column"]) -> "Column":
         if not cols:
             return Column([])
+        if all(isinstance(c.values, StringBlock) for c in cols):
+            return Column(StringBlock.concat([c.values for c in cols]))
         if all(isinstance(c.values, SparseBlock) for c in cols):
             nulls = None
             if any(c.nulls is not None for c in cols):

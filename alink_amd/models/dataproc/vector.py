@@ -81,53 +81,51 @@ class VectorAssemblerMapper(MISOMapper):
             elif all(p.dtype in (torch.bfloat16, torch.float32, torch.float16) for p in parts):
                 dt = torch.float32
             return [Column(torch.cat([p.to(dt) for p in parts], 1))]
-        if cols and any(isinstance(c.values, SparseBlock) for c in cols) and all(
-                c.nulls is None and (isinstance(c.values, SparseBlock) or isinstance(c.values, torch.Tensor))
-                for c in cols):
-            return [Column(_assemble_blocks([c.values for c in cols]))]
+        blocks = [_block_of(c) for c in cols]
+        if cols and all(b is not None for b in blocks):
+            # columnar path (K24): numeric / dense-vector / sparse / dense-vector-string columns, NULLs handled
+            # per handleInvalid (KEEP with a NULL changes that row's vector size: per-row path below)
+            anynull = None
+            for _, m in blocks:
+                if m is not None:
+                    anynull = m if anynull is None else (anynull | m)
+            blocks = [b for b, _ in blocks]
+            if anynull is not None and bool(anynull.any()):
+                if self.handle == "ERROR":
+                    raise ValueError("null value is found in vector assembler inputs.")
+                if self.handle != "SKIP":
+                    return super()._map_columns(mt)
+            else:
+                anynull = None
+            from ...ops.feature import vector_assemble
+            sb, _ = vector_assemble(blocks, mt.num_rows, skip=anynull, dense_ratio=RATIO)
+            return [Column(sb, anynull)]
         return super()._map_columns(mt)
 
 
-def _assemble_blocks(parts) -> SparseBlock:
-    """VectorAssembler over numeric / dense-block / SparseBlock columns, on the device (kernel K24): every row
-    is the concatenation of its parts' entries shifted by the running position (dense parts contribute every
-    value, zeros included — ``map.put(pos++, v)`` of ``VectorAssemblerMapper.java:88-104``), so rows stay
-    sorted without a merge; ``dense_ratio`` keeps the reference's per-row dense/sparse output rule."""
-    dev = next(p.device for p in parts if isinstance(p, SparseBlock))
-    n = len(parts[0]) if isinstance(parts[0], SparseBlock) else int(parts[0].shape[0])
-    lens, entries, pos = [], [], 0
-    for p in parts:
-        if isinstance(p, SparseBlock):
-            p = p.to(dev)
-            ln = p.crow[1:] - p.crow[:-1]
-            entries.append((p.crow[:-1], p.col.to(torch.int64) + pos, p.val, ln))
-            pos += p.size
-        else:
-            t = p.to(dev).reshape(n, -1).to(torch.float64)
-            d = t.shape[1]
-            ln = torch.full((n,), d, dtype=torch.int64, device=dev)
-            base = torch.arange(n, device=dev, dtype=torch.int64) * d
-            entries.append((base, (torch.arange(d, device=dev, dtype=torch.int64) + pos).repeat(n), t.reshape(-1), ln))
-            pos += d
-        lens.append(ln)
-    tot = torch.stack(lens).sum(0)
-    crow = torch.zeros(n + 1, dtype=torch.int64, device=dev)
-    torch.cumsum(tot, 0, out=crow[1:])
-    nnz = int(crow[-1])
-    col = torch.empty(nnz, dtype=torch.int32, device=dev)
-    val = torch.empty(nnz, dtype=torch.float64, device=dev)
-    before = torch.zeros(n, dtype=torch.int64, device=dev)
-    for (src_start, c, v, ln) in entries:
-        m = int(ln.sum())
-        if m:
-            rid = torch.repeat_interleave(torch.arange(n, device=dev), ln)
-            k = torch.arange(m, device=dev) - (torch.cumsum(ln, 0) - ln)[rid]
-            dst = crow[:-1][rid] + before[rid] + k
-            src = src_start[rid] + k
-            col[dst] = c[src].to(torch.int32)
-            val[dst] = v[src].to(torch.float64)
-        before += ln
-    return SparseBlock(crow, col, val, pos, dense_ratio=RATIO)
+def _block_of(c: Column):
+    """(tensor / SparseBlock, null mask or None) of a column for the columnar assembler, or None (per-row
+    path): numeric / dense-vector blocks as they are, dense-vector strings of one width parsed natively."""
+    v = c.values
+    if isinstance(v, (torch.Tensor, SparseBlock)):
+        return v, (c.nulls.cpu() if c.nulls is not None else None)
+    vals = c.to_list()
+    if not vals or not all(isinstance(x, str) or x is None for x in vals):
+        return None
+    present = [x for x in vals if x is not None]
+    if not present:
+        return None
+    toks = [len(x.replace(",", " ").split()) for x in present]
+    d = toks[0]
+    if d == 0 or any(t != d for t in toks) or any(x.lstrip().startswith("$") or ":" in x for x in present) \
+            or not all(x.isascii() for x in present):
+        return None
+    from ... import _native
+    arr = _native.parse_dense_vectors([x if x is not None else "" for x in vals], d)
+    if arr is None:
+        return None
+    nulls = torch.tensor([x is None for x in vals], dtype=torch.bool)
+    return torch.from_numpy(arr), (nulls if bool(nulls.any()) else None)
 
 
 class VectorNormalizeMapper(SISOMapper):

@@ -595,7 +595,15 @@ class FeatureHasherMapper(Mapper):
             idx[j] = int(self.num_index[j])
             val[j] = torch.from_numpy(v).to(dev)
             valid[j] = torch.from_numpy(~null).to(dev)
+        from ...common.strings import StringBlock
         for j, c in enumerate(self.cat, start=len(self.num)):
+            colv = mt.col(c).values
+            if isinstance(colv, StringBlock):
+                # packed UTF-8 column: hashed where it lives, no per-row Python strings
+                blk = colv.to(dev)
+                idx[j] = murmur3_index(blk, self.nf, prefix=c + "=", device=dev).to(dev)
+                valid[j] = ~blk.null_mask()
+                continue
             vals = mt.col(c).to_list()
             present = np.asarray([v is not None for v in vals], dtype=bool)
             if present.any():

@@ -206,7 +206,7 @@ class TreeBuilder:
         G = max(1, min(self.RS_BLOCKS, gpr))
         ps = -(-gpr // G)                                    # groups per piece (last piece padded)
         pend, real = [], []
-        pad = 1 << 26                                        # a group index past every feature: zero rows
+        pad = tops.PAD_GROUP                                 # a group index past every feature: zero rows
         for c in range(G):
             lo = c * ps
             if lo >= gpr:

@@ -61,6 +61,99 @@ __global__ __launch_bounds__(256) void murmur3_index_kernel(const uint16_t* __re
     }
 }
 
+// UTF-8 input: lane decodes its string's code points and feeds the UTF-16 code units (surrogate pairs above
+// U+FFFF) to the same pairwise mixing, so a packed UTF-8 StringBlock hashes Guava-exactly with no host pass.
+struct U16Mixer {
+    uint32_t h1, pending;
+    int64_t n;  // code units so far
+    __device__ __forceinline__ void push(uint32_t u) {
+        if (n & 1) h1 = mix_h1(h1, mix_k1(pending | (u << 16)));
+        else pending = u;
+        ++n;
+    }
+    __device__ __forceinline__ uint32_t finish() {
+        if (n & 1) h1 ^= mix_k1(pending);
+        return fmix(h1, (uint32_t)(2 * n));
+    }
+};
+
+__device__ __forceinline__ void push_utf8(U16Mixer& m, const uint8_t* __restrict__ p, int64_t len) {
+    for (int64_t i = 0; i < len;) {
+        const uint32_t b0 = p[i];
+        uint32_t cp;
+        if (b0 < 0x80u) {
+            cp = b0;
+            i += 1;
+        } else if (b0 < 0xE0u && i + 1 < len) {
+            cp = ((b0 & 0x1Fu) << 6) | (p[i + 1] & 0x3Fu);
+            i += 2;
+        } else if (b0 < 0xF0u && i + 2 < len) {
+            cp = ((b0 & 0x0Fu) << 12) | ((p[i + 1] & 0x3Fu) << 6) | (p[i + 2] & 0x3Fu);
+            i += 3;
+        } else if (i + 3 < len) {
+            cp = ((b0 & 0x07u) << 18) | ((p[i + 1] & 0x3Fu) << 12) | ((p[i + 2] & 0x3Fu) << 6) | (p[i + 3] & 0x3Fu);
+            i += 4;
+        } else {
+            cp = 0xFFFDu;  // truncated sequence (not produced by Python's encoder)
+            i += 1;
+        }
+        if (cp >= 0x10000u) {
+            const uint32_t c = cp - 0x10000u;
+            m.push(0xD800u + (c >> 10));
+            m.push(0xDC00u + (c & 0x3FFu));
+        } else {
+            m.push(cp);
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void murmur3_utf8_index_kernel(const uint8_t* __restrict__ bytes,
+                                                                const int64_t* __restrict__ off, int64_t n,
+                                                                const uint16_t* __restrict__ prefix, int plen,
+                                                                uint32_t seed, int64_t nf,
+                                                                int32_t* __restrict__ hash_out,
+                                                                int32_t* __restrict__ index_out) {
+    for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n; s += (int64_t)gridDim.x * blockDim.x) {
+        U16Mixer m{seed, 0u, 0};
+        for (int j = 0; j < plen; ++j) m.push(prefix[j]);
+        const int64_t b = off[s];
+        push_utf8(m, bytes + b, off[s + 1] - b);
+        const int32_t h = (int32_t)m.finish();
+        if (hash_out != nullptr) hash_out[s] = h;
+        if (index_out != nullptr) {
+            const int64_t a = h == INT32_MIN ? (int64_t)INT32_MIN : (h < 0 ? -(int64_t)h : (int64_t)h);
+            int64_t r = a % nf;
+            if (r < 0) r += nf;
+            index_out[s] = (int32_t)r;
+        }
+    }
+}
+
+// MurmurHash3_x86_32 over raw bytes (Guava murmur3_32().hashBytes): shuffle keys of packed string columns.
+__global__ __launch_bounds__(256) void murmur3_bytes_kernel(const uint8_t* __restrict__ bytes,
+                                                           const int64_t* __restrict__ off, int64_t n, uint32_t seed,
+                                                           int32_t* __restrict__ out) {
+    for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n; s += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t b = off[s], len = off[s + 1] - b;
+        const uint8_t* p = bytes + b;
+        uint32_t h1 = seed;
+        const int64_t nb = len >> 2;
+        for (int64_t i = 0; i < nb; ++i) {
+            const uint32_t k = (uint32_t)p[4 * i] | ((uint32_t)p[4 * i + 1] << 8) | ((uint32_t)p[4 * i + 2] << 16) |
+                               ((uint32_t)p[4 * i + 3] << 24);
+            h1 = mix_h1(h1, mix_k1(k));
+        }
+        uint32_t k1 = 0;
+        const uint8_t* t = p + 4 * nb;
+        switch (len & 3) {
+            case 3: k1 ^= (uint32_t)t[2] << 16; [[fallthrough]];
+            case 2: k1 ^= (uint32_t)t[1] << 8; [[fallthrough]];
+            case 1: k1 ^= t[0]; h1 ^= mix_k1(k1);
+        }
+        out[s] = (int32_t)fmix(h1, (uint32_t)len);
+    }
+}
+
 constexpr int32_t KEY_NONE = 0x7fffffff;
 
 // sort (key, tag) ascending across the wave with the value riding along; tag = input column (stable order)
@@ -148,6 +241,56 @@ __global__ __launch_bounds__(256) void csr_write_kernel(int64_t n, int m, const 
     }
 }
 
+// VectorAssembler (K24, reference VectorAssemblerMapper.java:50-106): every output row is the concatenation of
+// its parts' entries, each shifted by the running position (dense parts contribute every value, zeros included;
+// sparse parts their stored entries), so the CSR row is sorted by construction.  One wave per row, lanes
+// copy each part's run (coalesced); a NULL part contributes nothing and does not advance the position
+// (handleInvalid KEEP; SKIP / ERROR are decided on the host).  Part descriptor (8 x int64 per part):
+//   kind (0 dense fp64, 1 dense fp32, 2 dense bf16, 3 CSR fp64), width (dense: columns; CSR: vector size),
+//   val ptr, crow ptr (CSR), col ptr (CSR, int32), nulls ptr (uint8, nullable), 0, 0.
+__global__ __launch_bounds__(256) void vector_assemble_kernel(int64_t n, int P, const int64_t* __restrict__ desc,
+                                                             const int64_t* __restrict__ out_crow,
+                                                             int32_t* __restrict__ out_col,
+                                                             double* __restrict__ out_val) {
+    const int lane = threadIdx.x & 63;
+    const int64_t w0 = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
+    for (int64_t r = w0; r < n; r += nw) {
+        int64_t o = out_crow[r];
+        int64_t pos = 0;
+        for (int p = 0; p < P; ++p) {
+            const int64_t* d = desc + 8 * p;
+            const int kind = (int)d[0];
+            const int64_t width = d[1];
+            const uint8_t* nulls = reinterpret_cast<const uint8_t*>(d[5]);
+            if (nulls != nullptr && nulls[r]) continue;
+            if (kind == 3) {
+                const int64_t* crow = reinterpret_cast<const int64_t*>(d[3]);
+                const int32_t* col = reinterpret_cast<const int32_t*>(d[4]);
+                const double* val = reinterpret_cast<const double*>(d[2]);
+                const int64_t s = crow[r], L = crow[r + 1] - s;
+                for (int64_t j = lane; j < L; j += 64) {
+                    out_col[o + j] = (int32_t)(pos + col[s + j]);
+                    out_val[o + j] = val[s + j];
+                }
+                o += L;
+            } else {
+                const int64_t base = r * width;
+                for (int64_t j = lane; j < width; j += 64) {
+                    double v;
+                    if (kind == 0) v = reinterpret_cast<const double*>(d[2])[base + j];
+                    else if (kind == 1) v = (double)reinterpret_cast<const float*>(d[2])[base + j];
+                    else v = (double)__uint_as_float((uint32_t)reinterpret_cast<const uint16_t*>(d[2])[base + j] << 16);
+                    out_col[o + j] = (int32_t)(pos + j);
+                    out_val[o + j] = v;
+                }
+                o += width;
+            }
+            pos += width;
+        }
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -162,6 +305,39 @@ int alink_murmur3_index(const uint16_t* units, const int64_t* off, int64_t n, co
     hipLaunchKernelGGL(murmur3_index_kernel, dim3(blocks < 8192 ? blocks : 8192), dim3(256), 0,
                        reinterpret_cast<hipStream_t>(stream), units, off, n, prefix, plen, seed, nf, hash_out,
                        index_out);
+    return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+// As alink_murmur3_index for strings given as packed UTF-8 (bytes, off[n+1]): UTF-16 units decoded in-lane.
+int alink_murmur3_utf8_index(const uint8_t* bytes, const int64_t* off, int64_t n, const uint16_t* prefix, int plen,
+                             uint32_t seed, int64_t nf, int32_t* hash_out, int32_t* index_out, void* stream) {
+    if (n <= 0) return 0;
+    if (nf <= 0 || plen < 0) return 1;
+    const int64_t blocks = (n + 255) / 256;
+    hipLaunchKernelGGL(murmur3_utf8_index_kernel, dim3(blocks < 8192 ? blocks : 8192), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), bytes, off, n, prefix, plen, seed, nf, hash_out,
+                       index_out);
+    return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+// MurmurHash3_x86_32(seed) of every packed byte string (bytes, off[n+1]) -> out[n].
+int alink_murmur3_bytes(const uint8_t* bytes, const int64_t* off, int64_t n, uint32_t seed, int32_t* out,
+                        void* stream) {
+    if (n <= 0) return 0;
+    const int64_t blocks = (n + 255) / 256;
+    hipLaunchKernelGGL(murmur3_bytes_kernel, dim3(blocks < 8192 ? blocks : 8192), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), bytes, off, n, seed, out);
+    return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+// VectorAssembler rows: desc [P][8] int64 part descriptors (device), out_crow [n+1] (host-computed prefix of
+// the per-row entry counts), out_col / out_val [out_crow[n]].
+int alink_vector_assemble(int64_t n, int P, const int64_t* desc, const int64_t* out_crow, int32_t* out_col,
+                          double* out_val, void* stream) {
+    if (n <= 0 || P <= 0) return 0;
+    const int64_t blocks = (n + 3) / 4;
+    hipLaunchKernelGGL(vector_assemble_kernel, dim3(blocks < 16384 ? blocks : 16384), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), n, P, desc, out_crow, out_col, out_val);
     return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 

@@ -256,8 +256,8 @@ __global__ __launch_bounds__(kFmThreads) void tree_hist_fm(const uint8_t* __rest
   const int lane = threadIdx.x & 63;
   const int half = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int f = fg * 32 + (lane & 31);
-  const bool valid = f < F;
+  const int64_t f = (int64_t)fg * 32 + (lane & 31);      // fg may be a padding group far past F
+  const bool valid = fg >= 0 && f < F;
   const uint8_t* bcol = bins + (valid ? f : 0);
   const int rb = chunk_rows[c], re = chunk_rows[c + 1];
   constexpr int nw = kFmThreads / 64;
@@ -345,8 +345,8 @@ __global__ __launch_bounds__(256) void tree_hist_fm_reduce(const long long* __re
     if (feat_major) {
       H[(((int64_t)(pos * 32 + l) * nslots + s) * B + b0) * S + j] = tile[j * 33 + l];
     } else {
-      const int f = fg * 32 + l;
-      if (f < F) H[(((int64_t)s * F + f) * B + b0) * S + j] = tile[j * 33 + l];
+      const int64_t f = (int64_t)fg * 32 + l;
+      if (fg >= 0 && f < F) H[(((int64_t)s * F + f) * B + b0) * S + j] = tile[j * 33 + l];
     }
   }
 }

@@ -1,8 +1,9 @@
 """Feature hot path (kernels K24-K26) — ``csrc/feature.hip``.
 
 * ``murmur3_index(strings, nf, prefix, device)``: ``floorMod(abs(murmur3_32(0).hashUnencodedChars(prefix + s)),
-  nf)`` (Guava-exact, reference ``FeatureHasherMapper.java:104-106``) for a batch of strings; on a GPU the hash
-  runs on the device over the strings' UTF-16 code units (one lane per string), on the host in C++.
+  nf)`` (Guava-exact, reference ``FeatureHasherMapper.java:104-106``) for a list of strings or a packed UTF-8
+  ``StringBlock``; on a GPU one lane per string decodes UTF-8 to UTF-16 code units and hashes them on the
+  device, on the host the C++ twin does.
 * ``csr_assemble(idx, val, valid, size)``: per-row CSR from ``m`` column-major entry arrays ``[m, n]`` — rows
   sorted by index, duplicate indices summed (the reference's ``TreeMap`` accumulation) — one wave per row on
   the GPU, vectorised torch on the host.  Returns a ``SparseBlock``.
@@ -19,7 +20,7 @@ import torch
 from ..common.linalg.block import SparseBlock
 from . import _lib
 
-__all__ = ["utf16_units", "murmur3_index", "csr_assemble"]
+__all__ = ["utf16_units", "murmur3_index", "csr_assemble", "vector_assemble"]
 
 
 def utf16_units(strings: Sequence[str]):
@@ -37,27 +38,23 @@ def utf16_units(strings: Sequence[str]):
     return units, off
 
 
-def murmur3_index(strings: Sequence[str], nf: int, prefix: str = "", device=None) -> torch.Tensor:
-    """int64 feature indices of ``prefix + s`` for every string (see module doc)."""
+def murmur3_index(strings, nf: int, prefix: str = "", device=None) -> torch.Tensor:
+    """int64 feature indices of ``prefix + s`` for every string (see module doc).  ``strings``: a list of str or
+    a packed ``StringBlock``; on a GPU the UTF-8 bytes go to the device once and the kernel decodes the UTF-16
+    code units Guava hashes (``ops/strings.py``)."""
+    from ..common.strings import StringBlock
+    from .strings import murmur3_utf8_index
     device = torch.device(device) if device is not None else torch.device("cpu")
-    n = len(strings)
-    if device.type != "cuda":
-        from ..models.feature.encoders import murmur3_index as host_index
-        return torch.from_numpy(np.asarray(host_index([prefix + s for s in strings], nf), dtype=np.int64))
-    L = _lib.require()
-    out = torch.empty(n, dtype=torch.int32, device=device)
-    if n == 0:
-        return out.to(torch.int64)
-    units, off = utf16_units(strings)
-    u = torch.from_numpy(units if units.size else np.zeros(1, np.uint16)).to(device)
-    o = torch.from_numpy(off).to(device)
-    pu, _ = utf16_units([prefix])
-    p = torch.from_numpy(pu if pu.size else np.zeros(1, np.uint16)).to(device)
-    rc = L.alink_murmur3_index(u.data_ptr(), o.data_ptr(), n, p.data_ptr(), int(pu.size), 0, int(nf), None,
-                               out.data_ptr(), _lib.stream_ptr(device))
-    if rc != 0:
-        raise RuntimeError(f"alink_murmur3_index failed: {rc}")
-    return out.to(torch.int64)
+    if isinstance(strings, StringBlock):
+        block = strings
+    else:
+        if device.type != "cuda":
+            from ..models.feature.encoders import murmur3_index as host_index
+            return torch.from_numpy(np.asarray(host_index([prefix + s for s in strings], nf), dtype=np.int64))
+        block = StringBlock.from_list(strings)
+    if device.type == "cuda":
+        _lib.require()
+    return murmur3_utf8_index(block.to(device), nf, prefix)
 
 
 def csr_assemble(idx: torch.Tensor, val: Optional[torch.Tensor], valid: Optional[torch.Tensor], size: int,
@@ -103,3 +100,103 @@ def csr_assemble(idx: torch.Tensor, val: Optional[torch.Tensor], valid: Optional
     crow = torch.zeros(n + 1, dtype=torch.int64, device=dev)
     torch.cumsum(torch.bincount(urow, minlength=n), 0, out=crow[1:])
     return SparseBlock(crow, (uk % (int(size) + 1)).to(torch.int32), sums, size, dense_ratio)
+
+
+_DENSE_KIND = {torch.float64: 0, torch.float32: 1, torch.bfloat16: 2}
+
+
+def vector_assemble(parts, n: int, skip: Optional[torch.Tensor] = None, dense_ratio: Optional[float] = None,
+                    use_kernel: bool = True):
+    """K24 VectorAssembler over column blocks: ``parts`` are [n] / [n, d] tensors (numeric or dense-vector
+    columns) and ``SparseBlock`` s; row r of the result is their concatenation with every part's entries shifted
+    by the running position (``VectorAssemblerMapper.java:50-106``).  ``skip`` [n] bool: rows that become NULL
+    (handleInvalid SKIP).  On a GPU one HIP wave per row writes the CSR directly (``csrc/feature.hip``); on the
+    host the same layout is built with vectorised torch (``use_kernel=False`` forces that path anywhere, for
+    comparison).  Returns (SparseBlock, size)."""
+    dev = None
+    for p in parts:
+        d_ = p.crow.device if isinstance(p, SparseBlock) else p.device
+        if d_.type == "cuda":
+            dev = d_
+            break
+    if dev is None:
+        dev = parts[0].crow.device if isinstance(parts[0], SparseBlock) else parts[0].device
+    norm, lens, size = [], [], 0
+    for p in parts:
+        if isinstance(p, SparseBlock):
+            p = p.to(dev)
+            ln = p.crow[1:] - p.crow[:-1]
+            norm.append(("csr", p))
+            w = int(p.size)
+        else:
+            t = p.to(dev)
+            t = t.reshape(n, -1)
+            if t.dtype not in _DENSE_KIND:
+                t = t.to(torch.float64)
+            t = t.contiguous()
+            w = int(t.shape[1])
+            ln = torch.full((n,), w, dtype=torch.int64, device=dev)
+            norm.append(("dense", t))
+        if skip is not None:
+            ln = torch.where(skip.to(dev), torch.zeros_like(ln), ln)
+        lens.append(ln)
+        size += w
+    crow = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    if lens:
+        torch.cumsum(torch.stack(lens).sum(0), 0, out=crow[1:])
+    nnz = int(crow[-1]) if n else 0
+    col = torch.empty(nnz, dtype=torch.int32, device=dev)
+    val = torch.empty(nnz, dtype=torch.float64, device=dev)
+    if dev.type == "cuda" and n and nnz and use_kernel:
+        L = _lib.require()
+        sk = None if skip is None else skip.to(dev).to(torch.uint8).contiguous()
+        desc = torch.zeros((len(norm), 8), dtype=torch.int64)
+        for i, (kind, p) in enumerate(norm):
+            if kind == "csr":
+                desc[i, 0] = 3
+                desc[i, 1] = int(p.size)
+                desc[i, 2] = p.val.to(torch.float64).contiguous().data_ptr() if p.val.dtype == torch.float64 \
+                    and p.val.is_contiguous() else _keep(p.val.to(torch.float64).contiguous()).data_ptr()
+                desc[i, 3] = p.crow.data_ptr()
+                cc = p.col if p.col.dtype == torch.int32 and p.col.is_contiguous() else \
+                    _keep(p.col.to(torch.int32).contiguous())
+                desc[i, 4] = cc.data_ptr()
+            else:
+                desc[i, 0] = _DENSE_KIND[p.dtype]
+                desc[i, 1] = int(p.shape[1])
+                desc[i, 2] = p.data_ptr()
+            desc[i, 5] = 0 if sk is None else sk.data_ptr()
+        ddesc = desc.to(dev)
+        rc = L.alink_vector_assemble(n, len(norm), ddesc.data_ptr(), crow.data_ptr(), col.data_ptr(), val.data_ptr(),
+                                     _lib.stream_ptr(dev))
+        if rc != 0:
+            raise RuntimeError(f"alink_vector_assemble failed: {rc}")
+        torch.cuda.current_stream(dev).synchronize()      # the descriptor's raw pointers must outlive the kernel
+        _KEEP.clear()
+    elif nnz:
+        before = torch.zeros(n, dtype=torch.int64, device=dev)
+        pos = 0
+        for (kind, p), ln in zip(norm, lens):
+            m = int(ln.sum())
+            if m:
+                rid = torch.repeat_interleave(torch.arange(n, device=dev), ln)
+                k = torch.arange(m, device=dev) - (torch.cumsum(ln, 0) - ln)[rid]
+                dst = crow[:-1][rid] + before[rid] + k
+                if kind == "csr":
+                    src = p.crow[:-1][rid] + k
+                    col[dst] = (p.col[src].to(torch.int64) + pos).to(torch.int32)
+                    val[dst] = p.val[src].to(torch.float64)
+                else:
+                    col[dst] = (k + pos).to(torch.int32)
+                    val[dst] = p[rid, k].to(torch.float64)
+            before += ln
+            pos += int(p.size) if kind == "csr" else int(p.shape[1])
+    return SparseBlock(crow, col, val, size, dense_ratio), size
+
+
+_KEEP = []
+
+
+def _keep(t):
+    _KEEP.append(t)
+    return t

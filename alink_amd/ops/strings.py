@@ -1,0 +1,106 @@
+"""Bulk hashing of packed string columns (``common/strings.StringBlock``) — ``csrc/feature.hip`` on the device,
+the same functions in the C++ runtime on the host (bit-identical, so every rank of a job partitions alike
+whichever side hashed).
+
+* ``hash_bytes(block)``: MurmurHash3_x86_32(0) of every string's UTF-8 bytes (Guava ``hashBytes``) — the key
+  hash of the relational shuffle (``parallel/shuffle.py``).
+* ``murmur3_utf8_index(block, nf, prefix)``: Guava ``hashUnencodedChars(prefix + s)`` (UTF-16 code units,
+  decoded from the UTF-8 bytes inside the kernel) -> ``floorMod(abs(h), nf)``: the FeatureHasher / one-hot
+  path of ``FeatureHasherMapper.java:104-106`` without any host string handling.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from ..common.strings import StringBlock
+from . import _lib
+
+__all__ = ["hash_bytes", "murmur3_utf8_index", "murmur3_bytes_py"]
+
+
+def murmur3_bytes_py(b: bytes, seed: int = 0) -> int:
+    """Pure-Python MurmurHash3_x86_32 (test reference / last-resort fallback), signed int32."""
+    c1, c2, m = 0xcc9e2d51, 0x1b873593, 0xFFFFFFFF
+    h = seed & m
+    n = len(b) // 4
+    for i in range(n):
+        k = int.from_bytes(b[4 * i:4 * i + 4], "little")
+        k = (k * c1) & m
+        k = ((k << 15) | (k >> 17)) & m
+        k = (k * c2) & m
+        h ^= k
+        h = ((h << 13) | (h >> 19)) & m
+        h = (h * 5 + 0xe6546b64) & m
+    t = b[4 * n:]
+    k = 0
+    if len(t) >= 3:
+        k ^= t[2] << 16
+    if len(t) >= 2:
+        k ^= t[1] << 8
+    if len(t) >= 1:
+        k ^= t[0]
+        k = (k * c1) & m
+        k = ((k << 15) | (k >> 17)) & m
+        k = (k * c2) & m
+        h ^= k
+    h ^= len(b)
+    h ^= h >> 16
+    h = (h * 0x85ebca6b) & m
+    h ^= h >> 13
+    h = (h * 0xc2b2ae35) & m
+    h ^= h >> 16
+    return h - (1 << 32) if h & 0x80000000 else h
+
+
+def hash_bytes(block: StringBlock, seed: int = 0) -> torch.Tensor:
+    """int32 [n] murmur3 of each string's bytes, on the block's device (nulls hash their empty range)."""
+    n = len(block)
+    dev = block.device
+    if n == 0:
+        return torch.zeros(0, dtype=torch.int32, device=dev)
+    if dev.type == "cuda":
+        L = _lib.require()
+        data = block.data if block.nbytes else torch.zeros(1, dtype=torch.uint8, device=dev)
+        out = torch.empty(n, dtype=torch.int32, device=dev)
+        rc = L.alink_murmur3_bytes(data.data_ptr(), block.offsets.contiguous().data_ptr(), n, seed & 0xFFFFFFFF,
+                                   out.data_ptr(), _lib.stream_ptr(dev))
+        if rc != 0:
+            raise RuntimeError(f"alink_murmur3_bytes failed: {rc}")
+        return out
+    from .. import _native
+    data, off = block.data.numpy(), block.offsets.numpy()
+    h = _native.murmur3_bytes(data, off, seed)
+    if h is None:
+        raw = data.tobytes()
+        h = np.asarray([murmur3_bytes_py(raw[off[i]:off[i + 1]], seed) for i in range(n)], dtype=np.int32)
+    return torch.from_numpy(h)
+
+
+def murmur3_utf8_index(block: StringBlock, nf: int, prefix: str = "", seed: int = 0) -> torch.Tensor:
+    """int64 [n] ``floorMod(abs(murmur3_32(seed).hashUnencodedChars(prefix + s)), nf)`` on the block's device."""
+    n = len(block)
+    dev = block.device
+    if n == 0:
+        return torch.zeros(0, dtype=torch.int64, device=dev)
+    pu = np.frombuffer(prefix.encode("utf-16-le"), dtype=np.uint16).copy() if prefix else np.zeros(1, np.uint16)
+    plen = len(prefix.encode("utf-16-le")) // 2
+    if dev.type == "cuda":
+        L = _lib.require()
+        data = block.data if block.nbytes else torch.zeros(1, dtype=torch.uint8, device=dev)
+        p = torch.from_numpy(pu).to(dev)
+        out = torch.empty(n, dtype=torch.int32, device=dev)
+        rc = L.alink_murmur3_utf8_index(data.data_ptr(), block.offsets.contiguous().data_ptr(), n, p.data_ptr(),
+                                        plen, seed & 0xFFFFFFFF, int(nf), None, out.data_ptr(), _lib.stream_ptr(dev))
+        if rc != 0:
+            raise RuntimeError(f"alink_murmur3_utf8_index failed: {rc}")
+        return out.to(torch.int64)
+    from .. import _native
+    h = _native.murmur3_utf8(block.data.numpy(), block.offsets.numpy(), prefix, seed)
+    if h is None:
+        from ..models.feature.encoders import murmur3_index as host_index
+        return torch.from_numpy(np.asarray(host_index([prefix + (s or "") for s in block.to_list()], nf),
+                                           dtype=np.int64))
+    a = np.abs(h.astype(np.int64))
+    a = np.where(h == np.iinfo(np.int32).min, np.int64(np.iinfo(np.int32).min), a)   # Java abs(MIN_VALUE)
+    return torch.from_numpy(np.mod(a, int(nf)))

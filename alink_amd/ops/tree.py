@@ -144,6 +144,8 @@ def _histogram_fm(L, bins, slot, stats, nslots: int, B: int, prep: "FmStats" = N
         hist = torch.empty((nslots, F, B, S), dtype=torch.float32, device=dev)
     else:
         nfg = len(fgroups)
+        if any(not 0 <= int(g) < PAD_GROUP + 1 for g in fgroups):
+            raise ValueError("feature group out of range")
         fgl = torch.as_tensor(list(fgroups), dtype=torch.int32).to(dev)
         hist = torch.empty((nfg * 32, nslots, B, S), dtype=torch.float32, device=dev)
         if nfg == 0:
@@ -160,6 +162,9 @@ def _histogram_fm(L, bins, slot, stats, nslots: int, B: int, prep: "FmStats" = N
     if rc != 0:
         raise RuntimeError(f"alink_tree_hist_fm failed: {rc}")
     return hist
+
+
+PAD_GROUP = 1 << 24       # a 32-feature group index past every feature (zero rows in histogram_groups)
 
 
 def histogram_groups(bins: torch.Tensor, slot: torch.Tensor, stats: torch.Tensor, nslots: int, B: int,

@@ -29,7 +29,7 @@ from ..utils import trace as _trace
 __all__ = ["init_distributed", "get_rank", "get_world_size", "is_distributed", "all_reduce", "all_gather_object",
            "broadcast_object", "barrier", "all_gather_tensor", "all_to_all_objects", "reduce_scatter",
            "object_group", "device_for_rank", "CommStats", "STATS", "shutdown", "all_reduce_coalesced",
-           "Pending", "reduce_scatter_async"]
+           "Pending", "reduce_scatter_async", "all_to_all_bytes", "all_to_all_strings"]
 
 _OBJ_GROUP = None
 
@@ -38,19 +38,18 @@ class CommStats:
     """Per-process counters: number of collectives and bytes reduced (observability)."""
 
     def __init__(self):
-        self.calls = 0
-        self.bytes = 0
-        self.oneshot = 0
-        self.time_s = 0.0
+        self.reset()
 
     def reset(self):
         self.calls = 0
         self.bytes = 0
         self.oneshot = 0
         self.time_s = 0.0
+        self.string_bytes = 0      # packed string bytes sent through all_to_all_strings
 
     def as_dict(self):
-        return {"collectives": self.calls, "bytes": self.bytes, "oneshot": self.oneshot, "time_s": self.time_s}
+        return {"collectives": self.calls, "bytes": self.bytes, "oneshot": self.oneshot, "time_s": self.time_s,
+                "string_bytes": self.string_bytes}
 
 
 STATS = CommStats()
@@ -370,6 +369,7 @@ def all_to_all_tensors(send: List[torch.Tensor]) -> List[torch.Tensor]:
     width = int(np.prod(tail)) if tail else 1
     flat = torch.cat([x.reshape(x.shape[0], width) for x in send]) if send else torch.empty(0)
     STATS.calls += 1
+    STATS.bytes += int(flat.numel() * flat.element_size())
     if _backend() == "nccl":
         cdev = dev if dev.type == "cuda" else device_for_rank()
         out = torch.empty((sum(recv_counts), width), dtype=flat.dtype, device=cdev)
@@ -405,14 +405,67 @@ def broadcast_object(obj: Any, src: int = 0) -> Any:
 
 
 @_collective
+def _is_str_list(x) -> bool:
+    return isinstance(x, list) and all(v is None or isinstance(v, str) for v in x)
+
+
+def all_to_all_bytes(send: List[bytes]) -> List[bytes]:
+    """Byte-string all-to-all: ``send[j]`` -> rank j, as one lengths + one packed uint8 ``all_to_all_single``
+    (RCCL / gloo) — O(N) bytes in total, no gather of every rank's data on every rank."""
+    ws = get_world_size()
+    if ws == 1:
+        return [send[0]]
+    dev = collective_device()
+    lens = [torch.tensor([len(b)], dtype=torch.int64, device=dev) for b in send]
+    parts = [torch.frombuffer(bytearray(b), dtype=torch.uint8).to(dev) if len(b) else
+             torch.zeros(0, dtype=torch.uint8, device=dev) for b in send]
+    rl = torch.cat(all_to_all_tensors(lens)).cpu().tolist()
+    rb = torch.cat(all_to_all_tensors(parts)).cpu().numpy().tobytes()
+    out, off = [], 0
+    for n in rl:
+        out.append(rb[off:off + n])
+        off += n
+    return out
+
+
 def all_to_all_objects(send: List[Any]) -> List[Any]:
-    """Object all-to-all: ``send[j]`` goes to rank j; returns the list received from every rank."""
+    """Object all-to-all: ``send[j]`` goes to rank j; returns the list received from every rank.  Lists of
+    strings travel as packed UTF-8 (lengths, -1 = None, + bytes); anything else as one pickled byte string per
+    destination — both as tensor all-to-alls whose total traffic is the data itself."""
     ws = get_world_size()
     if ws == 1:
         return list(send)
-    gathered = all_gather_object(send)
-    r = get_rank()
-    return [gathered[src][r] for src in range(ws)]
+    if all(_is_str_list(p) for p in send):
+        flags = all_gather_object(True)
+        if all(flags):
+            from ..common.strings import StringBlock
+            blocks = [StringBlock.from_list(p) for p in send]
+            got = all_to_all_strings(blocks)
+            return [b.to_list() for b in got]
+    else:
+        all_gather_object(False)
+    import pickle
+    payload = [pickle.dumps(p, protocol=pickle.HIGHEST_PROTOCOL) for p in send]
+    # bytes produced by this job's own ranks (never external input)
+    return [pickle.loads(b) for b in all_to_all_bytes(payload)]
+
+
+def all_to_all_strings(send) -> list:
+    """``StringBlock`` all-to-all: ``send[j]`` -> rank j; returns the blocks received from every rank (source
+    order).  Two tensor all-to-alls: per-string byte lengths (-1 marks NULL) and the concatenated bytes."""
+    from ..common.strings import StringBlock
+    ws = get_world_size()
+    if ws == 1:
+        return [send[0]]
+    lens = [torch.where(b.null_mask(), torch.full_like(b.lengths(), -1), b.lengths()) for b in send]
+    rl = all_to_all_tensors(lens)
+    rb = all_to_all_tensors([b.data for b in send])
+    out = []
+    for L, B in zip(rl, rb):
+        nulls = L < 0
+        out.append(StringBlock.from_parts(L.clamp(min=0), B, nulls if bool(nulls.any()) else None))
+    STATS.string_bytes += sum(b.nbytes for b in send)
+    return out
 
 
 @_collective

@@ -292,6 +292,28 @@ def test_sql_relational_ops_partitioned_equal_single(tmp_path, world):
             assert sorted(got, key=key) == sorted(ref, key=key), k
 
 
+@pytest.mark.parametrize("world", [2, 4])
+def test_string_shuffle_packed_bytes_balanced(tmp_path, world):
+    """Hash shuffle of a string-keyed table: string columns move as packed UTF-8 (received as StringBlock), every
+    key lands on exactly one rank, no row is lost or altered, each rank receives ~1/P of all string bytes, and
+    the key hash is the same function on every rank."""
+    outs = _run("shuffle_strings", world, tmp_path)
+    assert all(o["is_block"] == [True, True] for o in outs)
+    sent = sorted(map(json.dumps, (r for o in outs for r in o["sent_rows"])))
+    recv = sorted(map(json.dumps, (r for o in outs for r in o["recv_rows"])))
+    assert sent == recv
+    seen = {}
+    for r, o in enumerate(outs):
+        for k in o["keys"]:
+            assert seen.setdefault(k, r) == r                 # co-partitioned: one owner per key
+    total = sum(o["string_bytes_total_local"] for o in outs)
+    for o in outs:
+        assert abs(o["string_bytes_recv"] - total / world) <= 0.08 * total / world, (o["string_bytes_recv"], total)
+    # same key -> same hash on every rank (no per-process salt)
+    assert all(o["hash_sample"] == outs[0]["hash_sample"] for o in outs)
+    assert len(set(outs[0]["hash_sample"])) == len(outs[0]["hash_sample"])
+
+
 def test_csv_source_byte_range_split(tmp_path):
     one = _run("csv", 1, tmp_path)[0]
     three = _run("csv", 3, tmp_path)

@@ -268,7 +268,7 @@ def test_hip_histogram_groups_feature_major_matches_torch():
     bins = torch.as_tensor(rng.integers(0, B, size=(n, F)), dtype=torch.uint8)
     slot = torch.as_tensor(rng.integers(-1, nslots, size=n), dtype=torch.int32)
     stats = torch.as_tensor(rng.normal(size=(n, S)), dtype=torch.float32)
-    groups = [2, 3, 1 << 26, 0]
+    groups = [2, 3, tops.PAD_GROUP, 0]
     got = tops.histogram_groups(bins.cuda(), slot.cuda(), stats.cuda(), nslots, B, groups).cpu().double()
     ref = tops.histogram_groups(bins, slot, stats.double(), nslots, B, groups)
     assert got.shape == (128, nslots, B, S)
