@@ -243,50 +243,57 @@ __global__ __launch_bounds__(256) void csr_write_kernel(int64_t n, int m, const 
 
 // VectorAssembler (K24, reference VectorAssemblerMapper.java:50-106): every output row is the concatenation of
 // its parts' entries, each shifted by the running position (dense parts contribute every value, zeros included;
-// sparse parts their stored entries), so the CSR row is sorted by construction.  One wave per row, lanes
-// copy each part's run (coalesced); a NULL part contributes nothing and does not advance the position
-// (handleInvalid KEEP; SKIP / ERROR are decided on the host).  Part descriptor (8 x int64 per part):
+// sparse parts their stored entries), so the CSR row is sorted by construction.  One thread per (part, row):
+// threads of a wave take consecutive rows of one part (coalesced reads of the part), find their run's offset
+// in the output row from the earlier parts' run lengths, and copy the run.  A NULL row (handleInvalid SKIP,
+// decided on the host) contributes nothing.  Part descriptor (8 x int64 per part):
 //   kind (0 dense fp64, 1 dense fp32, 2 dense bf16, 3 CSR fp64), width (dense: columns; CSR: vector size),
-//   val ptr, crow ptr (CSR), col ptr (CSR, int32), nulls ptr (uint8, nullable), 0, 0.
+//   val ptr, crow ptr (CSR), col ptr (CSR, int32), nulls ptr (uint8, nullable), position of the part's first
+//   column in the output vector, 0.
+__device__ __forceinline__ int64_t part_len(const int64_t* __restrict__ d, int64_t r) {
+    const uint8_t* nulls = reinterpret_cast<const uint8_t*>(d[5]);
+    if (nulls != nullptr && nulls[r]) return 0;
+    if (d[0] == 3) {
+        const int64_t* crow = reinterpret_cast<const int64_t*>(d[3]);
+        return crow[r + 1] - crow[r];
+    }
+    return d[1];
+}
+
 __global__ __launch_bounds__(256) void vector_assemble_kernel(int64_t n, int P, const int64_t* __restrict__ desc,
                                                              const int64_t* __restrict__ out_crow,
                                                              int32_t* __restrict__ out_col,
                                                              double* __restrict__ out_val) {
-    const int lane = threadIdx.x & 63;
-    const int64_t w0 = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
-    for (int64_t r = w0; r < n; r += nw) {
+    const int64_t total = n * P;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+         t += (int64_t)gridDim.x * blockDim.x) {
+        const int p = (int)(t / n);
+        const int64_t r = t - (int64_t)p * n;
+        const int64_t* d = desc + 8 * p;
+        const int64_t L = part_len(d, r);
+        if (L == 0) continue;
         int64_t o = out_crow[r];
-        int64_t pos = 0;
-        for (int p = 0; p < P; ++p) {
-            const int64_t* d = desc + 8 * p;
-            const int kind = (int)d[0];
-            const int64_t width = d[1];
-            const uint8_t* nulls = reinterpret_cast<const uint8_t*>(d[5]);
-            if (nulls != nullptr && nulls[r]) continue;
-            if (kind == 3) {
-                const int64_t* crow = reinterpret_cast<const int64_t*>(d[3]);
-                const int32_t* col = reinterpret_cast<const int32_t*>(d[4]);
-                const double* val = reinterpret_cast<const double*>(d[2]);
-                const int64_t s = crow[r], L = crow[r + 1] - s;
-                for (int64_t j = lane; j < L; j += 64) {
-                    out_col[o + j] = (int32_t)(pos + col[s + j]);
-                    out_val[o + j] = val[s + j];
-                }
-                o += L;
-            } else {
-                const int64_t base = r * width;
-                for (int64_t j = lane; j < width; j += 64) {
-                    double v;
-                    if (kind == 0) v = reinterpret_cast<const double*>(d[2])[base + j];
-                    else if (kind == 1) v = (double)reinterpret_cast<const float*>(d[2])[base + j];
-                    else v = (double)__uint_as_float((uint32_t)reinterpret_cast<const uint16_t*>(d[2])[base + j] << 16);
-                    out_col[o + j] = (int32_t)(pos + j);
-                    out_val[o + j] = v;
-                }
-                o += width;
+        for (int q = 0; q < p; ++q) o += part_len(desc + 8 * q, r);
+        const int64_t pos = d[6];
+        const int kind = (int)d[0];
+        if (kind == 3) {
+            const int64_t s = reinterpret_cast<const int64_t*>(d[3])[r];
+            const int32_t* col = reinterpret_cast<const int32_t*>(d[4]) + s;
+            const double* val = reinterpret_cast<const double*>(d[2]) + s;
+            for (int64_t j = 0; j < L; ++j) {
+                out_col[o + j] = (int32_t)(pos + col[j]);
+                out_val[o + j] = val[j];
             }
-            pos += width;
+        } else {
+            const int64_t base = r * L;
+            for (int64_t j = 0; j < L; ++j) {
+                double v;
+                if (kind == 0) v = reinterpret_cast<const double*>(d[2])[base + j];
+                else if (kind == 1) v = (double)reinterpret_cast<const float*>(d[2])[base + j];
+                else v = (double)__uint_as_float((uint32_t)reinterpret_cast<const uint16_t*>(d[2])[base + j] << 16);
+                out_col[o + j] = (int32_t)(pos + j);
+                out_val[o + j] = v;
+            }
         }
     }
 }
@@ -335,8 +342,8 @@ int alink_murmur3_bytes(const uint8_t* bytes, const int64_t* off, int64_t n, uin
 int alink_vector_assemble(int64_t n, int P, const int64_t* desc, const int64_t* out_crow, int32_t* out_col,
                           double* out_val, void* stream) {
     if (n <= 0 || P <= 0) return 0;
-    const int64_t blocks = (n + 3) / 4;
-    hipLaunchKernelGGL(vector_assemble_kernel, dim3(blocks < 16384 ? blocks : 16384), dim3(256), 0,
+    const int64_t blocks = (n * P + 255) / 256;
+    hipLaunchKernelGGL(vector_assemble_kernel, dim3(blocks < 65536 ? blocks : 65536), dim3(256), 0,
                        reinterpret_cast<hipStream_t>(stream), n, P, desc, out_crow, out_col, out_val);
     return hipGetLastError() == hipSuccess ? 0 : 2;
 }

@@ -151,7 +151,10 @@ def vector_assemble(parts, n: int, skip: Optional[torch.Tensor] = None, dense_ra
         L = _lib.require()
         sk = None if skip is None else skip.to(dev).to(torch.uint8).contiguous()
         desc = torch.zeros((len(norm), 8), dtype=torch.int64)
+        pos = 0
         for i, (kind, p) in enumerate(norm):
+            desc[i, 6] = pos
+            pos += int(p.size) if kind == "csr" else int(p.shape[1])
             if kind == "csr":
                 desc[i, 0] = 3
                 desc[i, 1] = int(p.size)
