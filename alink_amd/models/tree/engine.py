@@ -235,6 +235,10 @@ class TreeBuilder:
         if cfg.kind == "gbdt" and Hn.is_cuda and not bool(self.d.is_cat and any(self.d.is_cat)) \
                 and tops.gpu_kernels_ok():
             return self._search_gbdt_hip(Hn, feat_order, feat_ok)
+        if Hn.is_cuda and tops.gpu_kernels_ok():
+            out = self._search_hip(Hn, feat_order, feat_ok)
+            if out is not None:
+                return out
         Hv = Hn[:, :, :B - 1, :]
         Hmiss = Hn[:, :, B - 1, :]
         cnt = _count(cfg, Hv)
@@ -379,6 +383,35 @@ class TreeBuilder:
         accept = gbest > cfg.min_info_gain + 1e-6
         perm = torch.arange(B - 1, device=Hn.device).expand(m, F, B - 1)
         return gbest, fbest, jbest, mbest, accept, perm
+
+    def _search_hip(self, Hn, feat_order, feat_ok):
+        """Categorical GBDT and RF / decision-tree criteria on the GPU (``ops/csrc/tree_split.hip``
+        ``tree_split_kernel``): one wave per (node, feature) orders the bins, scans the statistics and picks the
+        first best admissible split; C4.5 multi-way gains of categorical features (information-gain criteria)
+        stay a vectorised torch reduction.  The order (perm) is rebuilt on the host for the chosen features only
+        (returned as None)."""
+        cfg = self.cfg
+        m, F, B, S = Hn.shape
+        res = tops.tree_split(Hn, cfg.kind, self.is_cat, cfg.n_classes, cfg.min_samples_per_leaf,
+                              cfg.min_sum_hessian_per_leaf, cfg.min_sample_ratio_per_child, cfg.min_info_gain)
+        if res is None:
+            return None
+        best_j_gain, best_j = res
+        multi = torch.zeros((m, F), dtype=torch.bool, device=Hn.device)
+        if cfg.kind in ("infogain", "infogainratio") and bool(self.is_cat.any()):
+            Hv = Hn[:, :, :B - 1, :]
+            mg = self._multiway_gain(Hv, Hn[:, :, B - 1, :], Hv.sum(2))
+            catf = self.is_cat[None, :].expand(m, F)
+            best_j_gain = torch.where(catf, mg, best_j_gain)
+            multi = catf.clone()
+        best_j_gain = torch.where(feat_ok, best_j_gain, torch.full_like(best_j_gain, NEG))
+        ordered = torch.gather(best_j_gain, 1, feat_order)
+        gbest, pos = ordered.max(dim=1)
+        fbest = torch.gather(feat_order, 1, pos[:, None])[:, 0]
+        jbest = torch.gather(best_j, 1, fbest[:, None])[:, 0]
+        mbest = torch.gather(multi, 1, fbest[:, None])[:, 0]
+        accept = gbest > (cfg.min_info_gain + 1e-6 if cfg.kind == "gbdt" else 0)
+        return gbest, fbest, jbest, mbest, accept, None
 
     def _multiway_gain(self, Hv, Hmiss, Tv):
         """C4.5 split on every non-empty category (``CategoricalSplitter.bestSplitInfo``)."""
@@ -569,7 +602,13 @@ class TreeBuilder:
                 else:
                     gbest, fbest, jbest, mbest, accept, perm = self._search(Hn, order, ok)
                     rows_host = Hn[torch.arange(m, device=dev), fbest].cpu().numpy()      # [m, B, S]
-                    perm_host = perm[torch.arange(m, device=dev), fbest].cpu().numpy()    # [m, B-1]
+                    if perm is None:                     # GPU search: rebuild the chosen features' order
+                        fb_np = fbest.cpu().numpy()
+                        perm_host = np.stack([tops.split_order_key(rows_host[r_], cfg.kind, cfg.n_classes,
+                                                                   bool(self.d.is_cat[int(fb_np[r_])]))
+                                              for r_ in range(m)]) if m else np.zeros((0, B - 1), np.int64)
+                    else:
+                        perm_host = perm[torch.arange(m, device=dev), fbest].cpu().numpy()    # [m, B-1]
                 acc = accept.cpu().numpy()
                 fb, jb, mb, gb = (fbest.cpu().numpy(), jbest.cpu().numpy(), mbest.cpu().numpy(),
                                   gbest.cpu().numpy())

@@ -150,6 +150,200 @@ __global__ __launch_bounds__(256) void gbdt_split_kernel(const float* __restrict
     }
 }
 
+// K8/K10 general split search (reference CalBestSplit.java:98-218 for GBDT incl. categorical bins ordered by
+// g/h, seriestree/CategoricalSplitter + ContinuousSplitter + Criteria.java for RF / decision trees: Gini,
+// information gain, gain ratio, MSE).  One 64-lane wave per (node, feature):
+//   1. categorical features: every candidate bin's ordering key (GBDT g/h, MSE mean, classification class-0
+//      share; empty bins last) goes to LDS and each bin's rank in the stable order (key, bin) is counted
+//      against all bins -> perm[rank] = bin (continuous features keep the identity order);
+//   2. the S statistics of the bins in that order: lane-local sums of 4 positions, a wave exclusive scan per
+//      statistic, then a sequential walk over the lane's 4 positions gives the left statistics L at every
+//      candidate, R = T - L;
+//   3. the criterion's gain with the same admissibility rules as the vectorised torch search, and the first
+//      maximum over positions.  Output per (node, feature): best gain (-inf if none) and its position j in the
+//      sorted order (left child = perm[0..j]).
+constexpr int kMaxS = 33;
+enum Crit { C_GBDT = 0, C_GINI = 1, C_INFO = 2, C_RATIO = 3, C_MSE = 4 };
+
+__device__ __forceinline__ double lg2(double p) { return p > 0.0 ? log(p) * 1.4426950408889634 : 0.0; }
+
+template <int S>
+struct Imp {
+  // weight and impurity of a statistics vector (engine._weight / engine._impurity)
+  __device__ static double weight(const double* x, int crit, int ncls) {
+    if (crit == C_GBDT) return x[2];
+    if (crit == C_MSE) return x[0];
+    double w = 0.0;
+    for (int k = 0; k < ncls; ++k) w += x[k];
+    return w;
+  }
+  __device__ static double impurity(const double* x, int crit, int ncls) {
+    const double w = weight(x, crit, ncls);
+    if (w < 1e-15) return 0.0;
+    if (crit == C_MSE) {
+      const double mean = x[1] / w;
+      return x[2] / w - mean * mean;
+    }
+    double acc = 0.0;
+    for (int k = 0; k < ncls; ++k) {
+      const double p = x[k] / w;
+      acc += crit == C_GINI ? p * p : p * lg2(p);
+    }
+    return crit == C_GINI ? 1.0 - acc : -acc;
+  }
+};
+
+template <int S>
+__global__ __launch_bounds__(256) void tree_split_kernel(const float* __restrict__ H, int m, int F, int B, int crit,
+                                                        int ncls, const uint8_t* __restrict__ is_cat,
+                                                        double min_leaf, double min_hess, double min_ratio,
+                                                        double min_gain, double* __restrict__ best_gain,
+                                                        int32_t* __restrict__ best_pos) {
+  __shared__ double skey[4][256];
+  __shared__ int sperm[4][256];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t wave = (int64_t)blockIdx.x * 4 + wv;
+  if (wave >= (int64_t)m * F) return;                  // whole wave: no block barrier below
+  const int f = (int)(wave % F);
+  const float* h = H + wave * (int64_t)B * S;          // [B][S]
+  const int nb = B - 1;
+  const bool cat = is_cat[f] != 0;
+  // ---- 1. order
+  if (cat) {
+    for (int b = lane; b < nb; b += 64) {
+      const float* x = h + b * S;
+      double key;
+      if (crit == C_GBDT) {
+        const double g = x[1], hh = x[2];
+        key = hh < 1e-6 ? -1.0 : g / hh;
+      } else {
+        // MSE: mean label; classification: share of class 0 (engine._search); empty bins sort last
+        const double cnt = x[S - 1];
+        double ww = 0.0;
+        if (crit == C_MSE) ww = x[0];
+        else
+          for (int k = 0; k < ncls; ++k) ww += x[k];
+        const double num = crit == C_MSE ? (double)x[1] : (double)x[0];
+        key = cnt > 0.0 ? num / (ww == 0.0 ? 1.0 : ww) : INFINITY;
+      }
+      skey[wv][b] = key;
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_s_waitcnt(0xc07f);                  // lgkmcnt(0): this wave's LDS stores landed
+    for (int b = lane; b < nb; b += 64) {
+      const double kb = skey[wv][b];
+      int rank = 0;
+      for (int c = 0; c < nb; ++c) {
+        const double kc = skey[wv][c];
+        rank += (kc < kb || (kc == kb && c < b)) ? 1 : 0;
+      }
+      sperm[wv][rank] = b;
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+  }
+  // ---- 2. prefix statistics in sorted order
+  double lsum[S];
+#pragma unroll
+  for (int k = 0; k < S; ++k) lsum[k] = 0.0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int pos = 4 * lane + q;
+    if (pos < nb) {
+      const int b = cat ? sperm[wv][pos] : pos;
+#pragma unroll
+      for (int k = 0; k < S; ++k) lsum[k] += (double)h[b * S + k];
+    }
+  }
+  double off[S], tot[S];
+#pragma unroll
+  for (int k = 0; k < S; ++k) {
+    double e = lsum[k];
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const double t = __shfl_up(e, o);
+      if (lane >= o) e += t;
+    }
+    tot[k] = __shfl(e, 63);                               // all candidate bins (missing excluded)
+    off[k] = e - lsum[k];
+  }
+  double miss[S];
+#pragma unroll
+  for (int k = 0; k < S; ++k) miss[k] = (double)h[nb * S + k];
+  // totals the gain is taken against: GBDT includes the missing bin (it goes right), the others do not
+  double T[S];
+#pragma unroll
+  for (int k = 0; k < S; ++k) T[k] = crit == C_GBDT ? tot[k] + miss[k] : tot[k];
+  const double wT = Imp<S>::weight(T, crit, ncls);
+  const double impT = crit == C_GBDT ? 0.0 : Imp<S>::impurity(T, crit, ncls);
+  const double cM = miss[S - 1];
+  // ---- 3. walk the lane's positions
+  double bestv = -INFINITY;
+  int bestp = 0x7fffffff;
+  double L[S];
+#pragma unroll
+  for (int k = 0; k < S; ++k) L[k] = off[k];
+  for (int q = 0; q < 4; ++q) {
+    const int pos = 4 * lane + q;
+    if (pos >= nb) break;
+    const int b = cat ? sperm[wv][pos] : pos;
+    const double cb = (double)h[b * S + (S - 1)];
+#pragma unroll
+    for (int k = 0; k < S; ++k) L[k] += (double)h[b * S + k];
+    double R[S];
+#pragma unroll
+    for (int k = 0; k < S; ++k) R[k] = T[k] - L[k];
+    double gain;
+    bool ok;
+    if (crit == C_GBDT) {
+      const double G = T[1], Ht = T[2], GL = L[1], HL = L[2], GR = G - GL, HR = Ht - HL;
+      gain = (HL != 0.0 && HR != 0.0)
+                 ? fabs(GL * GL / HL + GR * GR / HR - G * G / (Ht == 0.0 ? 1.0 : Ht)) : 0.0;
+      const double ratio = HL / (Ht < 1e-6 ? 1.0 : Ht);
+      const double cT = T[S - 1], cL = L[S - 1];
+      ok = Ht >= 1e-6 && ratio >= 1e-7 && ratio <= 1.0 - 1e-7 && cL >= min_leaf && cT - cL >= min_leaf &&
+           HL >= min_hess && HR >= min_hess;
+    } else {
+      const double safe = wT < 1e-15 ? 1.0 : wT;
+      const double pl = Imp<S>::weight(L, crit, ncls) / safe, pr = Imp<S>::weight(R, crit, ncls) / safe;
+      gain = impT - pl * Imp<S>::impurity(L, crit, ncls) - pr * Imp<S>::impurity(R, crit, ncls);
+      if (crit == C_RATIO) {
+        const double iv = -(pl * lg2(pl) + pr * lg2(pr));
+        gain = iv < 1e-15 ? 0.0 : gain / iv;
+      }
+      if (wT < 1e-15) gain = 0.0;
+      const double cL = L[S - 1], cR = R[S - 1], cT = cL + cR;
+      const double den = cT + cM == 0.0 ? 1.0 : cT + cM;
+      ok = cL > 0.0 && cR > 0.0 && min_leaf <= cL + cM && min_leaf <= cR + cM && min_ratio <= (cL + cM) / den &&
+           min_ratio <= (cR + cM) / den && (!cat || cb > 0.0) && gain > 0.0 && gain >= min_gain;
+    }
+    const double v = ok ? gain : -INFINITY;
+    if (v > bestv) {
+      bestv = v;
+      bestp = pos;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double ov = __shfl_xor(bestv, o);
+    const int op = __shfl_xor(bestp, o);
+    if (ov > bestv || (ov == bestv && op < bestp)) {
+      bestv = ov;
+      bestp = op;
+    }
+  }
+  if (lane == 0) {
+    best_gain[wave] = bestv;
+    best_pos[wave] = bestp == 0x7fffffff ? 0 : bestp;
+  }
+}
+
+template <int S>
+void launch_split(dim3 grid, hipStream_t st, const float* H, int m, int F, int B, int crit, int ncls,
+                  const uint8_t* is_cat, double a, double b, double c, double d, double* g, int32_t* p) {
+  hipLaunchKernelGGL(tree_split_kernel<S>, grid, dim3(256), 0, st, H, m, F, B, crit, ncls, is_cat, a, b, c, d, g, p);
+}
+
 }  // namespace
 
 extern "C" {
@@ -177,6 +371,33 @@ int alink_gbdt_split(const float* H, int m, int F, int B, int S, int gi, int hi,
     hipLaunchKernelGGL(gbdt_split_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0,
                        reinterpret_cast<hipStream_t>(stream), H, m, F, B, S, gi, hi, ci, min_leaf, min_hess, best_gain,
                        best_bin);
+    return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+}  // extern "C"
+
+extern "C" {
+
+// General best-split search (categorical + continuous, GBDT / Gini / InfoGain / InfoGainRatio / MSE) over the
+// fp32 histogram H [m][F][B][S]; is_cat [F] uint8 (device).  S must be one of the instantiated sizes.
+int alink_tree_split(const float* H, int m, int F, int B, int S, int crit, int ncls, const uint8_t* is_cat,
+                     double min_leaf, double min_hess, double min_ratio, double min_gain, double* best_gain,
+                     int32_t* best_pos, void* stream) {
+    if (m <= 0 || F <= 0) return 0;
+    if (B < 2 || B > 257 || crit < 0 || crit > 4) return 1;
+    if (crit == C_GBDT && S != 4 && S != 3) return 1;
+    const int64_t waves = (int64_t)m * F;
+    const dim3 grid((unsigned)((waves + 3) / 4));
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    switch (S) {
+        case 3: launch_split<3>(grid, st, H, m, F, B, crit, ncls, is_cat, min_leaf, min_hess, min_ratio, min_gain, best_gain, best_pos); break;
+        case 4: launch_split<4>(grid, st, H, m, F, B, crit, ncls, is_cat, min_leaf, min_hess, min_ratio, min_gain, best_gain, best_pos); break;
+        case 5: launch_split<5>(grid, st, H, m, F, B, crit, ncls, is_cat, min_leaf, min_hess, min_ratio, min_gain, best_gain, best_pos); break;
+        case 6: launch_split<6>(grid, st, H, m, F, B, crit, ncls, is_cat, min_leaf, min_hess, min_ratio, min_gain, best_gain, best_pos); break;
+        case 8: launch_split<8>(grid, st, H, m, F, B, crit, ncls, is_cat, min_leaf, min_hess, min_ratio, min_gain, best_gain, best_pos); break;
+        case 11: launch_split<11>(grid, st, H, m, F, B, crit, ncls, is_cat, min_leaf, min_hess, min_ratio, min_gain, best_gain, best_pos); break;
+        default: return 3;   // caller falls back to the torch search
+    }
     return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 

@@ -341,3 +341,55 @@ def gbdt_split(H: torch.Tensor, min_leaf: float, min_hess: float, gi: int = 1, h
     if rc != 0:
         raise RuntimeError(f"alink_gbdt_split failed: {rc}")
     return gain, binj.to(torch.int64)
+
+
+SPLIT_S = (3, 4, 5, 6, 8, 11)
+_CRIT = {"gbdt": 0, "gini": 1, "infogain": 2, "infogainratio": 3, "mse": 4}
+
+
+def tree_split(H: torch.Tensor, kind: str, is_cat: torch.Tensor, n_classes: int, min_leaf: float,
+               min_hess: float, min_ratio: float, min_gain: float):
+    """K8/K10 general split search on the GPU: (best gain [m, F] fp64 (-inf: none), best position [m, F] int64 in
+    the per-(node, feature) bin order — the stable (key, bin) order for categorical features, the bin order for
+    continuous ones).  ``None`` when the statistic count has no compiled instantiation (torch search)."""
+    m, F, B, S = H.shape
+    if S not in SPLIT_S or B > 257:
+        return None
+    L = _lib.require()
+    H = H.to(torch.float32).contiguous()
+    cat = is_cat.to(device=H.device, dtype=torch.uint8).contiguous()
+    gain = torch.empty((m, F), dtype=torch.float64, device=H.device)
+    pos = torch.empty((m, F), dtype=torch.int32, device=H.device)
+    rc = L.alink_tree_split(H.data_ptr(), m, F, B, S, _CRIT[kind], int(n_classes), cat.data_ptr(), float(min_leaf),
+                            float(min_hess), float(min_ratio), float(min_gain), gain.data_ptr(), pos.data_ptr(),
+                            _lib.stream_ptr(H.device))
+    if rc == 3:
+        return None
+    if rc != 0:
+        raise RuntimeError(f"alink_tree_split failed: {rc}")
+    return gain, pos.to(torch.int64)
+
+
+def split_order_key(h, kind: str, n_classes: int, categorical: bool):
+    """Host twin of the kernel's ordering: stable argsort of the candidate bins' keys ([B, S] row of one node and
+    feature) — engine._materialise uses it to rebuild the chosen categorical split's left set."""
+    import numpy as np
+    h = np.asarray(h, dtype=np.float64)
+    Hv = h[:-1]
+    nb = Hv.shape[0]
+    if not categorical:
+        return np.arange(nb)
+    if kind == "gbdt":
+        g, hh = Hv[:, 1], Hv[:, 2]
+        key = np.where(hh < 1e-6, -1.0, g / np.where(hh < 1e-6, 1.0, hh))
+    else:
+        cnt = Hv[:, -1]
+        if kind == "mse":
+            w = Hv[:, 0]
+        else:
+            w = np.zeros(nb)
+            for k in range(n_classes):            # the kernel's summation order
+                w = w + Hv[:, k]
+        num = Hv[:, 1] if kind == "mse" else Hv[:, 0]
+        key = np.where(cnt > 0, num / np.where(w == 0, 1.0, w), np.inf)
+    return np.argsort(key, kind="stable")

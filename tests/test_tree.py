@@ -276,6 +276,58 @@ def test_hip_histogram_groups_feature_major_matches_torch():
     assert float(got[64:96].abs().sum()) == 0.0 and float(got[36:64].abs().sum()) == 0.0    # f >= F: zeros
 
 
+def _rand_hist(rng, kind, m, F, B, ncls):
+    cnt = rng.integers(0, 6, size=(m, F, B)) * (rng.random((m, F, B)) < 0.8)
+    if kind in ("gini", "infogain", "infogainratio"):
+        cls = np.stack([rng.binomial(cnt, 0.3 + 0.4 * rng.random((m, F, B))) for _ in range(ncls - 1)], -1)
+        cls = np.minimum(cls, cnt[..., None])
+        rest = np.clip(cnt - cls.sum(-1), 0, None)
+        H = np.concatenate([cls, rest[..., None], (cls.sum(-1) + rest)[..., None]], -1).astype(np.float64)
+    elif kind == "mse":
+        y = rng.normal(size=(m, F, B)) * cnt
+        H = np.stack([cnt, y, y * y / np.maximum(cnt, 1) + cnt, cnt], -1).astype(np.float64)
+    else:
+        g = rng.normal(size=(m, F, B)) * cnt
+        h = 0.25 * cnt * rng.random((m, F, B))
+        H = np.stack([g * g, g, h, cnt], -1).astype(np.float64)
+    return torch.as_tensor(H.astype(np.float32).astype(np.float64))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,ncls", [("gbdt", 0), ("gini", 2), ("infogain", 3), ("infogainratio", 2), ("mse", 0),
+                                       ("gini", 7)])
+def test_hip_general_split_search_matches_torch(kind, ncls):
+    """tree_split_kernel (categorical order by key, S-stat scan, criterion gain, first best) == the torch
+    search of TreeBuilder._search, mixed categorical / continuous features."""
+    from types import SimpleNamespace
+    from alink_amd.models.tree.engine import SplitConfig, TreeBuilder
+    rng = np.random.default_rng(7 + ncls)
+    m, F, B = 9, 12, 17
+    Hn = _rand_hist(rng, kind, m, F, B, ncls)
+    is_cat = [bool(f % 3 == 0) for f in range(F)]
+    cfg = SplitConfig(kind=kind, max_depth=5, min_samples_per_leaf=2, n_classes=ncls,
+                      min_sample_ratio_per_child=0.01)
+    tb = SimpleNamespace(cfg=cfg, d=SimpleNamespace(is_cat=is_cat), _multiway_gain=None)
+    tb.is_cat = torch.tensor(is_cat)
+    tb._multiway_gain = lambda *a: TreeBuilder._multiway_gain(tb, *a)
+    order = torch.arange(F).expand(m, F).clone()
+    ok = torch.ones((m, F), dtype=torch.bool)
+    g0, f0, j0, mb0, a0, perm = TreeBuilder._search(tb, Hn, order, ok)
+    tbg = SimpleNamespace(cfg=cfg, d=tb.d, is_cat=tb.is_cat.cuda())
+    tbg._multiway_gain = lambda *a: TreeBuilder._multiway_gain(tbg, *a)
+    g1, f1, j1, mb1, a1, _ = TreeBuilder._search_hip(tbg, Hn.cuda(), order.cuda(), ok.cuda())
+    np.testing.assert_allclose(g1.cpu().numpy(), g0.numpy(), rtol=1e-9, atol=1e-12)
+    assert f1.cpu().tolist() == f0.tolist() and mb1.cpu().tolist() == mb0.tolist()
+    assert a1.cpu().tolist() == a0.tolist()
+    for r in range(m):
+        if not bool(a0[r]) or bool(mb0[r]):
+            continue
+        f = int(f0[r])
+        assert int(j1[r]) == int(j0[r])
+        po = tops.split_order_key(Hn[r, f].numpy(), kind, ncls, is_cat[f])
+        assert sorted(po[:int(j0[r]) + 1].tolist()) == sorted(perm[r, f, :int(j0[r]) + 1].tolist())
+
+
 @pytest.mark.gpu
 def test_gbdt_on_gpu_matches_doc():
     useLocalEnv(1)
