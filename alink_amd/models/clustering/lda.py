@@ -76,8 +76,11 @@ def _corpus(mt: MTable, col: str, vocab: dict, dev):
 
 def e_step(doc, word, cts, n_docs, expElogbeta_T, alpha, gamma0, max_iter=100, tol=1e-3):
     """Batched document E-step.  expElogbeta_T: [V, K]; gamma0: [D, K].  Returns (gamma, expElogtheta,
-    phinorm per token)."""
+    phinorm per token).  On a GPU with K <= 256: the HIP kernel (one wave per document, all iterations in
+    registers, ``ops/lda.estep``); elsewhere the vectorised torch loop below."""
     K = expElogbeta_T.shape[1]
+    if gamma0.is_cuda and K <= 256 and n_docs > 0 and lops.kernel_supported(gamma0.device):
+        return lops.estep(doc, word, cts, n_docs, expElogbeta_T, alpha, gamma0, max_iter, tol)
     gamma = gamma0.clone()
     active = torch.ones(n_docs, dtype=torch.bool, device=gamma.device)
     eb = expElogbeta_T[word]                                  # [T, K]

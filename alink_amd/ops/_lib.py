@@ -118,6 +118,8 @@ _EXTRA_SIGNATURES = {
     "alink_w2v_sg_hs_f32": [_c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_int, _c_vp, _c_vp, _c_vp, _c_int, _c_vp, _c_vp,
                             _c_int, _c_f, _c_int, _c_vp],
     "alink_lda_gibbs": [_c_vp, _c_vp, _c_vp, _c_i64, _c_int, _c_vp, _c_vp, _c_vp, _c_d, _c_d, _c_d, _c_vp, _c_vp,
+                        _c_int, _c_vp],
+    "alink_lda_estep": [_c_vp, _c_vp, _c_vp, _c_i64, _c_int, _c_vp, _c_vp, _c_vp, _c_int, _c_d, _c_vp, _c_vp, _c_vp,
                         _c_vp],
     "alink_gbdt_grad_stats": [_c_vp, _c_vp, _c_vp, _c_i64, _c_int, _c_vp, _c_vp],
     "alink_gbdt_leaf_update": [_c_vp, _c_vp, _c_vp, _c_int, _c_i64, _c_vp],
