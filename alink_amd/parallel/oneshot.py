@@ -95,10 +95,13 @@ class OneShot:
         if seq is None:
             self.seq += 1
             seq = self.seq
-        rc = self.L.alink_oneshot_allreduce(t.data_ptr(), out.data_ptr(), n, _DT[t.dtype], _OP[op], self.P,
-                                            self.rank if rank is None else rank, seq & 0xFFFFFFFF,
-                                            self.peer_data.data_ptr(), self.peer_flags.data_ptr(), self.cap, BLOCKS,
-                                            phases, TIMEOUT_S, self.err.data_ptr(), _lib.stream_ptr(self.device))
+        from ..utils import trace as _trace
+        with _trace.span("oneshot_allreduce", "kernel", device=True, bytes=int(n * t.element_size()), P=self.P):
+            rc = self.L.alink_oneshot_allreduce(t.data_ptr(), out.data_ptr(), n, _DT[t.dtype], _OP[op], self.P,
+                                                self.rank if rank is None else rank, seq & 0xFFFFFFFF,
+                                                self.peer_data.data_ptr(), self.peer_flags.data_ptr(), self.cap,
+                                                BLOCKS, phases, TIMEOUT_S, self.err.data_ptr(),
+                                                _lib.stream_ptr(self.device))
         if rc != 0:
             raise RuntimeError(f"alink_oneshot_allreduce failed: {rc}")
         self.calls += 1
@@ -174,12 +177,16 @@ def reset():
     _INSTANCE, _TRIED = None, False
 
 
+SETUP_ERROR: Optional[str] = None     # why the last setup fell back to the collective library (diagnostics)
+
+
 def get() -> Optional[OneShot]:
     """Collective on first use: every rank of the job must call it at the same point (comm.all_reduce does)."""
-    global _INSTANCE, _TRIED
+    global _INSTANCE, _TRIED, SETUP_ERROR
     if _TRIED:
         return _INSTANCE
     _TRIED = True
+    SETUP_ERROR = None
     from . import comm
     P, rank = comm.get_world_size(), comm.get_rank()
     dev = comm.device_for_rank()
@@ -196,8 +203,9 @@ def get() -> Optional[OneShot]:
         if rc != 0:
             raise RuntimeError(f"hipIpcGetMemHandle failed: {rc}")
         mine = bytes(buf.raw)
-    except Exception:
+    except Exception as e:
         ok, mine = 0.0, b""
+        SETUP_ERROR = f"alloc/handle: {e!r}"
     handles = comm.all_gather_object(mine)
     bases = []
     if ok:
@@ -215,9 +223,11 @@ def get() -> Optional[OneShot]:
                 opened.append(int(q.value))
                 bases.append(int(q.value))
             inst = OneShot(dev, P, rank, MAX_BYTES, bases, [base], opened)
-        except Exception:
+        except Exception as e:
             ok = 0.0
+            SETUP_ERROR = f"ipc open: {e!r}"
     if _host_min(ok) < 1.0:
+        SETUP_ERROR = SETUP_ERROR or "a peer failed to set up"
         if inst is not None:
             inst.close()
         else:                       # failure paths: release what this rank did allocate / open
@@ -233,9 +243,13 @@ def get() -> Optional[OneShot]:
         got = inst.all_reduce_(probe.clone())
         torch.cuda.synchronize(dev)
         good = 1.0 if torch.equal(got, ref) and int(inst.err.item()) == 0 else 0.0
-    except Exception:
+        if not good:
+            SETUP_ERROR = "probe mismatch"
+    except Exception as e:
         good = 0.0
+        SETUP_ERROR = f"probe: {e!r}"
     if _host_min(good) < 1.0:
+        SETUP_ERROR = SETUP_ERROR or "a peer's probe failed"
         inst.close()
         return None
     _INSTANCE = inst

@@ -58,6 +58,8 @@ def scenario_kmeans(out):
     out["iterations"] = op.getTrainInfo()["iterations"]
     out["oneshot_calls"] = comm.STATS.oneshot
     out["backend"] = comm._backend()
+    from alink_amd.parallel import oneshot
+    out["oneshot_setup_error"] = oneshot.SETUP_ERROR
     out["device"] = str(env.device)
 
 
