@@ -52,22 +52,76 @@ def gather_table(mt: MTable, env: Optional[MLEnvironment] = None) -> MTable:
         return None
     if mt.replicated or comm.get_world_size() == 1:
         return mt
-    parts = comm.all_gather_object(_to_host(mt))
-    out = MTable.concat(parts)
+    out = _gather_columnar(mt)
     out.replicated = True
     return out
 
 
-def _to_host(mt: MTable) -> MTable:
+def _col_kind(c) -> tuple:
+    """Wire form of a column for the columnar gather: ('tensor', dtype, trailing shape), ('sparse',),
+    ('string',) or ('object',)."""
+    import torch
+    from ..common.linalg.block import SparseBlock
+    from ..common.strings import StringBlock
+    v = c.values
+    if isinstance(v, torch.Tensor):
+        return ("tensor", str(v.dtype), tuple(v.shape[1:]))
+    if isinstance(v, SparseBlock):
+        return ("sparse",)
+    if isinstance(v, StringBlock) or (isinstance(v, list) and all(x is None or isinstance(x, str) for x in v)):
+        return ("string",)
+    return ("object",)
+
+
+def _gather_columnar(mt: MTable) -> MTable:
+    """Partitions concatenated in rank order, one column at a time in its native form: tensor columns (numeric,
+    dense-vector blocks) and their null masks by a variable-length tensor all-gather (RCCL / gloo), sparse
+    blocks as (row lengths, col, val), string columns as packed UTF-8 (lengths, -1 = NULL, + bytes); only
+    columns of arbitrary Python objects are pickled.  Replaces a pickled all-gather of whole tables."""
+    import torch
+    from ..common.linalg.block import SparseBlock
+    from ..common.strings import StringBlock
     from ..common.table import Column
+    kinds = [_col_kind(c) for c in mt.cols]
+    allk = comm.all_gather_object(kinds)
+    cdev = comm.collective_device()
     cols = []
-    for c in mt.cols:
+    for i, c in enumerate(mt.cols):
+        ks = {k[i] for k in allk}
+        kind = next(iter(ks)) if len(ks) == 1 else ("object",)
         v = c.values
-        if hasattr(v, "is_cuda") and v.is_cuda:
-            cols.append(Column(v.cpu(), c.nulls.cpu() if c.nulls is not None else None))
+        if kind[0] == "tensor":
+            vals = comm.all_gather_varlen(v.to(cdev)).cpu()
+            nulls = None
+            flags = comm.all_gather_object(c.nulls is not None)
+            if any(flags):
+                m = c.nulls if c.nulls is not None else torch.zeros(v.shape[0], dtype=torch.bool)
+                nulls = comm.all_gather_varlen(m.to(torch.uint8).to(cdev)).cpu().to(torch.bool)
+            cols.append(Column(vals, nulls))
+        elif kind[0] == "sparse":
+            ln = (v.crow[1:] - v.crow[:-1]).to(cdev)
+            rl = comm.all_gather_varlen(ln).cpu()
+            col = comm.all_gather_varlen(v.col.to(cdev)).cpu()
+            val = comm.all_gather_varlen(v.val.to(cdev)).cpu()
+            size = max(comm.all_gather_object(int(v.size)))
+            crow = torch.zeros(rl.numel() + 1, dtype=torch.int64)
+            torch.cumsum(rl, 0, out=crow[1:])
+            nulls = None
+            if any(comm.all_gather_object(c.nulls is not None)):
+                m = c.nulls if c.nulls is not None else torch.zeros(len(v), dtype=torch.bool)
+                nulls = comm.all_gather_varlen(m.to(torch.uint8).to(cdev)).cpu().to(torch.bool)
+            cols.append(Column(SparseBlock(crow, col, val, size, getattr(v, "dense_ratio", None)), nulls))
+        elif kind[0] == "string":
+            blk = v if isinstance(v, StringBlock) else StringBlock.from_list(c.to_list())
+            ln = torch.where(blk.null_mask(), torch.full_like(blk.lengths(), -1), blk.lengths())
+            rl = comm.all_gather_varlen(ln.to(cdev)).cpu()
+            data = comm.all_gather_varlen(blk.data.to(cdev)).cpu()
+            nulls = rl < 0
+            cols.append(Column(StringBlock.from_parts(rl.clamp(min=0), data, nulls if bool(nulls.any()) else None)))
         else:
-            cols.append(c)
-    return MTable(mt.schema, cols, mt.replicated)
+            parts = comm.all_gather_object(c.to_list())
+            cols.append(Column([x for p in parts for x in p]))
+    return MTable(mt.schema, cols, True)
 
 
 def gather_rows(mt: MTable) -> List[Row]:

@@ -29,7 +29,7 @@ from ..utils import trace as _trace
 __all__ = ["init_distributed", "get_rank", "get_world_size", "is_distributed", "all_reduce", "all_gather_object",
            "broadcast_object", "barrier", "all_gather_tensor", "all_to_all_objects", "reduce_scatter",
            "object_group", "device_for_rank", "CommStats", "STATS", "shutdown", "all_reduce_coalesced",
-           "Pending", "reduce_scatter_async", "all_to_all_bytes", "all_to_all_strings"]
+           "Pending", "reduce_scatter_async", "all_to_all_bytes", "all_to_all_strings", "comm_stream"]
 
 _OBJ_GROUP = None
 
@@ -195,6 +195,44 @@ def _backend() -> str:
 
 _OPS = {"sum": "SUM", "max": "MAX", "min": "MIN", "prod": "PRODUCT"}
 
+# ---------------------------------------------------------------------------------------------------------
+# Comm-stream discipline: every RCCL collective is issued from a dedicated high-priority
+# communication stream per device.  The comm stream first waits on an event of the caller's (compute) stream
+# -- the inputs are ready -- and the caller's stream later waits on an event recorded on the comm stream after
+# the collective -- the outputs are ready.  Synchronous calls insert that wait immediately; ``*_async`` calls
+# return a ``Pending`` whose ``wait()`` inserts it, so compute launched in between overlaps the collective.
+# Tensors touched on the comm stream are ``record_stream``-ed so the caching allocator cannot recycle them early.
+_COMM_STREAMS = {}
+
+
+def comm_stream(dev: torch.device) -> "torch.cuda.Stream":
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    s = _COMM_STREAMS.get(idx)
+    if s is None:
+        s = torch.cuda.Stream(device=torch.device("cuda", idx), priority=-1)
+        _COMM_STREAMS[idx] = s
+    return s
+
+
+def _on_comm_stream(dev: torch.device, tensors, issue, wait_now: bool = True):
+    """Run ``issue()`` (which enqueues RCCL work) on the comm stream of ``dev``.  Returns (result, done event)."""
+    cur = torch.cuda.current_stream(dev)
+    cs = comm_stream(dev)
+    ready = torch.cuda.Event()
+    ready.record(cur)
+    cs.wait_event(ready)
+    with torch.cuda.stream(cs):
+        res = issue()
+        done = torch.cuda.Event()
+        done.record(cs)
+    for t in tensors:
+        if t is not None and t.is_cuda:
+            t.record_stream(cs)
+    if wait_now:
+        cur.wait_event(done)
+    return res, done
+
+
 
 def _oneshot_max(backend: str) -> int:
     from . import oneshot
@@ -229,8 +267,11 @@ def all_reduce(t: torch.Tensor, op: str = "sum") -> torch.Tensor:
         return t
     if (not t.is_cuda) and _backend() == "nccl":
         d = t.to(device_for_rank())
-        dist.all_reduce(d, op=rop)
+        _on_comm_stream(d.device, [d], lambda: dist.all_reduce(d, op=rop))
         t.copy_(d.cpu())
+        return t
+    if t.is_cuda:
+        _on_comm_stream(t.device, [t], lambda: dist.all_reduce(t, op=rop))
         return t
     dist.all_reduce(t, op=rop)
     return t
@@ -262,9 +303,9 @@ def reduce_scatter(t: torch.Tensor, op: str = "sum") -> torch.Tensor:
     STATS.calls += 1
     STATS.bytes += t.numel() * t.element_size()
     if _backend() == "nccl":
-        d = t if t.is_cuda else t.to(device_for_rank())
+        d = (t if t.is_cuda else t.to(device_for_rank())).contiguous()
         o = out if t.is_cuda else torch.empty(out.shape, dtype=t.dtype, device=d.device)
-        dist.reduce_scatter_tensor(o, d.contiguous(), op=rop)
+        _on_comm_stream(d.device, [d, o], lambda: dist.reduce_scatter_tensor(o, d, op=rop))
         return out if t.is_cuda else o.cpu()
     full = t.clone()
     all_reduce(full, op)
@@ -272,12 +313,17 @@ def reduce_scatter(t: torch.Tensor, op: str = "sum") -> torch.Tensor:
     return full[r * out.shape[0]:(r + 1) * out.shape[0]].clone()
 
 
+def _wait_event(dev, ev, x):
+    torch.cuda.current_stream(dev).wait_event(ev)
+    return x
+
+
 class Pending:
-    """Handle of an in-flight collective (``*_async``).  Under RCCL the collective runs on the process group's
-    own communication stream: issuing it records an event on the caller's current stream that the comm
-    stream waits on, so kernels the caller launches afterwards overlap with it; ``wait()`` makes the caller's
-    current stream wait on the collective's completion event (no host block) and returns the result.  Under
-    gloo the collective runs on gloo's thread and ``wait()`` joins it."""
+    """Handle of an in-flight collective (``*_async``).  Under RCCL the collective is issued from the dedicated
+    comm stream (``comm_stream``) after an event wait on the caller's stream, so kernels the caller launches
+    afterwards overlap with it; ``wait()`` makes the caller's current stream wait on the event recorded on the
+    comm stream after the collective (no host block) and returns the result.  Under gloo the collective runs
+    on gloo's thread and ``wait()`` joins it."""
 
     __slots__ = ("_work", "_result", "_post", "_keep")
 
@@ -311,8 +357,14 @@ def reduce_scatter_async(t: torch.Tensor, op: str = "sum") -> Pending:
     if _backend() == "nccl":
         d = (t if t.is_cuda else t.to(device_for_rank())).contiguous()
         o = torch.empty((rows,) + tuple(t.shape[1:]), dtype=t.dtype, device=d.device)
-        work = dist.reduce_scatter_tensor(o, d, op=rop, async_op=True)
-        return Pending(o, work, None if t.is_cuda else (lambda x: x.cpu()), keep=(d,))
+
+        def issue():
+            w = dist.reduce_scatter_tensor(o, d, op=rop, async_op=True)
+            w.wait()                         # comm stream waits on RCCL's stream (no host block)
+        _, done = _on_comm_stream(d.device, [d, o], issue, wait_now=False)
+        dev = d.device
+        return Pending(o, None, (lambda x: _wait_event(dev, done, x)) if t.is_cuda else
+                       (lambda x: _wait_event(dev, done, x).cpu()), keep=(d,))
     full = t.detach().cpu().clone()
     work = dist.all_reduce(full, op=rop, async_op=True)
     r = get_rank()
@@ -329,9 +381,9 @@ def all_gather_tensor(t: torch.Tensor) -> torch.Tensor:
     STATS.calls += 1
     if _backend() == "nccl":
         # RCCL has no host path: host inputs are staged through the rank's GPU and the result returned on the host
-        d = t if t.is_cuda else t.to(device_for_rank())
+        d = (t if t.is_cuda else t.to(device_for_rank())).contiguous()
         out = torch.empty((ws * d.shape[0],) + tuple(d.shape[1:]), dtype=d.dtype, device=d.device)
-        dist.all_gather_into_tensor(out, d.contiguous())
+        _on_comm_stream(d.device, [d, out], lambda: dist.all_gather_into_tensor(out, d))
         return out if t.is_cuda else out.cpu()
     parts = [torch.empty_like(t.cpu()) for _ in range(ws)]
     dist.all_gather(parts, t.cpu().contiguous())
@@ -373,7 +425,8 @@ def all_to_all_tensors(send: List[torch.Tensor]) -> List[torch.Tensor]:
     if _backend() == "nccl":
         cdev = dev if dev.type == "cuda" else device_for_rank()
         out = torch.empty((sum(recv_counts), width), dtype=flat.dtype, device=cdev)
-        dist.all_to_all_single(out, flat.reshape(-1, width).to(cdev).contiguous(), recv_counts, counts.tolist())
+        src = flat.reshape(-1, width).to(cdev).contiguous()
+        _on_comm_stream(cdev, [src, out], lambda: dist.all_to_all_single(out, src, recv_counts, counts.tolist()))
         out = out.to(dev)
     else:
         out = torch.empty((sum(recv_counts), width), dtype=flat.dtype)

@@ -374,6 +374,34 @@ def scenario_shuffle_strings(out):
     out["hash_keys"] = [str(x) for x in fixed]
 
 
+def scenario_gather(out):
+    """gather_table moves columns in native form (no whole-table pickle): tensors, null masks, sparse blocks,
+    packed strings; object columns alone pickled."""
+    import torch
+    from alink_amd.common.linalg import DenseVector
+    from alink_amd.common.linalg.block import SparseBlock
+    from alink_amd.common.strings import StringBlock
+    from alink_amd.common.table import Column, MTable
+    from alink_amd.common.types import TableSchema, Types
+    from alink_amd.operator.base import gather_table
+    from alink_amd.parallel import comm
+    comm.init_distributed()
+    me = comm.get_rank()
+    n = 5 + me
+    x = torch.arange(n, dtype=torch.float64) + 100 * me
+    nm = torch.zeros(n, dtype=torch.bool)
+    nm[1] = True
+    s = [f"r{me}-{i}-\u00e9" if i != 2 else None for i in range(n)]
+    crow = torch.arange(n + 1, dtype=torch.int64)
+    sb = SparseBlock(crow, torch.full((n,), me, dtype=torch.int32), torch.ones(n, dtype=torch.float64), 8)
+    objs = [{"k": me, "i": i} for i in range(n)]
+    mt = MTable(TableSchema(["x", "s", "v", "o"], [Types.DOUBLE, Types.STRING, Types.SPARSE_VECTOR, Types.STRING]),
+                [Column(x, nm), Column(s), Column(sb), Column(objs)], False)
+    full = gather_table(mt)
+    out["kinds"] = [type(c.values).__name__ for c in full.cols]
+    out["rows"] = [[str(v) for v in r] for r in full.rows()]
+
+
 def scenario_sql(out):
     """Distributed relational ops: each rank returns its partition of every result."""
     import numpy as np

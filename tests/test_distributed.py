@@ -314,6 +314,19 @@ def test_string_shuffle_packed_bytes_balanced(tmp_path, world):
     assert len(set(outs[0]["hash_sample"])) == len(outs[0]["hash_sample"])
 
 
+def test_gather_table_columnar_three_ranks(tmp_path):
+    """gather_table (collect, sinks, tuning, pipeline save) concatenates partitions in rank order with native
+    column transport: tensors + null masks, sparse blocks and packed strings; objects pickled."""
+    outs = _run("gather", 3, tmp_path)
+    assert all(o["rows"] == outs[0]["rows"] for o in outs)
+    assert outs[0]["kinds"] == ["Tensor", "StringBlock", "SparseBlock", "list"]
+    rows = outs[0]["rows"]
+    assert len(rows) == 5 + 6 + 7
+    assert rows[0][0] == "0.0" and rows[1][0] == "None" and rows[5][0] == "100.0"
+    assert rows[2][1] == "None" and rows[5][1] == "r1-0-\u00e9"
+    assert rows[17][3] == str({"k": 2, "i": 6})
+
+
 def test_csv_source_byte_range_split(tmp_path):
     one = _run("csv", 1, tmp_path)[0]
     three = _run("csv", 3, tmp_path)
