@@ -116,6 +116,9 @@ def solve(A: torch.Tensor, b: torch.Tensor, nonnegative: bool = False, chunk: in
 
 HEAVY_DEGREE = 16384     # rows with more neighbours are split across waves (partial Grams)
 HEAVY_CHUNK = 4096
+# rank 33..64: heavy rows' partial Grams on the matrix cores (als_heavy_gram_mfma: exact bf16 x3 split, fp64
+# folding per 32 neighbours); 0 keeps the fp64 VALU kernel
+HEAVY_MFMA = int(__import__("os").environ.get("ALINK_ALS_HEAVY_MFMA", "1"))
 
 
 def fused_supported(Y: torch.Tensor) -> bool:
@@ -170,7 +173,7 @@ def fused_solve(indptr: torch.Tensor, nbr: torch.Tensor, rating: torch.Tensor, Y
                                      None if yty is None else yty.data_ptr(), heavy.data_ptr(), heavy.numel(),
                                      chunk_row.contiguous().data_ptr(), chunk_start.contiguous().data_ptr(),
                                      chunk_row.numel(), HEAVY_CHUNK, G.data_ptr(), B.data_ptr(), X.data_ptr(),
-                                     status.data_ptr(), st)
+                                     status.data_ptr(), HEAVY_MFMA, st)
         if rc != 0:
             raise RuntimeError(f"alink_als_heavy_solve failed: {rc}")
     bad = torch.nonzero(status != 0, as_tuple=False).reshape(-1)

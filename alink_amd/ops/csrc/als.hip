@@ -384,6 +384,127 @@ __global__ __launch_bounds__(64) void als_heavy_gram(const int64_t* __restrict__
   }
 }
 
+// heavy rows, pass 1 on MFMA (rank 64): a 256-thread workgroup per (row, chunk) forms the chunk's partial Gram
+// G = sum_t c_t y_t y_t^T as Y_c^T Y_c on the bf16 matrix cores without losing fp32 accuracy: every fp32 factor
+// value is split exactly into three bf16 pieces y = hi + mid + lo, and the six cross products with magnitude
+// >= 2^-16 (hi.hi, hi.mid, mid.hi, mid.mid, hi.lo, lo.hi) run as v_mfma_f32_16x16x32_bf16 -- each bf16 x bf16
+// product is exact in fp32, the dropped terms are <= 2^-23 relative.  The fp32 MFMA accumulator covers one
+// 32-neighbour step only and is folded into fp64 registers after it, so accumulation error does not grow with
+// the degree.  Workgroup layout: the 32 neighbours' rows are staged in LDS as [piece][dim][k] bf16 (row stride
+// 40 elements: the 16 lanes of a ds_read_b128 group hit disjoint banks); wave w owns Gram tile row w (tiles
+// (w, 0..3) of 16 x 16).  The rhs sum_t w_t y_t accumulates in LDS fp64.  Partial G / B are added to the global
+// fp64 accumulators as before.  (The VALU version: 64 fp64 FMAs per neighbour per lane, one wave per chunk.)
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+constexpr int kHK = 32;                 // neighbours per MFMA K-step
+constexpr int kHS = 40;                 // LDS row stride (bf16 elements) of a [dim][k] piece
+
+__device__ __forceinline__ void split3(float y, __bf16& hi, __bf16& mid, __bf16& lo) {
+  hi = (__bf16)y;
+  const float r1 = y - (float)hi;
+  mid = (__bf16)r1;
+  lo = (__bf16)(r1 - (float)mid);
+}
+
+template <bool IMPL>
+__global__ __launch_bounds__(256) void als_heavy_gram_mfma(const int64_t* __restrict__ indptr,
+                                                           const int32_t* __restrict__ nbr,
+                                                           const float* __restrict__ rating,
+                                                           const float* __restrict__ Y, int r, float alpha,
+                                                           const int64_t* __restrict__ rows,
+                                                           const int64_t* __restrict__ chunk_row,
+                                                           const int64_t* __restrict__ chunk_start, int64_t chunk,
+                                                           double* __restrict__ G, double* __restrict__ B) {
+  // pieces 0..2: B side (y); IMPL adds pieces 3..5: A side (c y)
+  constexpr int NP = IMPL ? 6 : 3;
+  __shared__ __bf16 sp[NP][64 * kHS];
+  __shared__ double srhs[64];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int64_t h = chunk_row[blockIdx.x];
+  const int64_t row = rows[h];
+  const int64_t s = chunk_start[blockIdx.x];
+  const int64_t e = min(indptr[row + 1], s + chunk);
+  if (tid < 64) srhs[tid] = 0.0;
+  double g64[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) g64[j][i] = 0.0;
+  const int sk = tid >> 3, sd = (tid & 7) * 8;        // staging: neighbour sk, dims sd .. sd+7
+  const int li = lane & 15, kg = (lane >> 4) * 8;
+  for (int64_t t0 = s; t0 < e; t0 += kHK) {
+    __syncthreads();                                    // previous step's fragments consumed
+    {
+      const int64_t t = t0 + sk;
+      float yv[8];
+      float c = 0.f, wr = 0.f;
+      if (t < e) {
+        const float* yr = Y + (int64_t)nbr[t] * r;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) yv[q] = sd + q < r ? yr[sd + q] : 0.f;
+        const float rt = rating[t];
+        if (IMPL) {
+          c = rt > 0.f ? alpha * rt : 0.f;
+          wr = rt > 0.f ? 1.f + c : 0.f;
+        } else {
+          c = 1.f;
+          wr = rt;
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) yv[q] = 0.f;
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        __bf16 a, b, d;
+        split3(yv[q], a, b, d);
+        const int o = (sd + q) * kHS + sk;
+        sp[0][o] = a;
+        sp[1][o] = b;
+        sp[2][o] = d;
+        if (IMPL) {
+          split3(c * yv[q], a, b, d);
+          sp[3][o] = a;
+          sp[4][o] = b;
+          sp[5][o] = d;
+        }
+        if (wr != 0.f) atomicAdd(&srhs[sd + q], (double)wr * (double)yv[q]);
+      }
+    }
+    __syncthreads();
+    constexpr int AO = IMPL ? 3 : 0;
+    bf16x8_t a[3];
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+      a[p] = *reinterpret_cast<const bf16x8_t*>(&sp[AO + p][(16 * w + li) * kHS + kg]);
+#pragma unroll
+    for (int J = 0; J < 4; ++J) {
+      bf16x8_t b[3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) b[p] = *reinterpret_cast<const bf16x8_t*>(&sp[p][(16 * J + li) * kHS + kg]);
+      f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[0], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[1], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[0], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[1], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[2], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[0], acc, 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) g64[J][i] += (double)acc[i];
+    }
+  }
+  __syncthreads();
+  // lane l of wave w holds tile (w, J) entries [m = 4 (l >> 4) + i][n = l & 15]
+#pragma unroll
+  for (int J = 0; J < 4; ++J)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int gm = 16 * w + 4 * (lane >> 4) + i, gn = 16 * J + (lane & 15);
+      unsafeAtomicAdd(G + (h * 64 + gm) * 64 + gn, g64[J][i]);
+    }
+  if (tid < 64) unsafeAtomicAdd(B + h * 64 + tid, srhs[tid]);
+}
+
 // heavy rows, pass 2: solve from the accumulated G / B
 template <int RP>
 __global__ __launch_bounds__(64) void als_heavy_solve(const double* __restrict__ G, const double* __restrict__ B,
@@ -450,7 +571,8 @@ int alink_als_fused_solve(const int64_t* indptr, const int32_t* nbr, const float
 int alink_als_heavy_solve(const int64_t* indptr, const int32_t* nbr, const float* rating, const float* Y, int r,
                           int implicit, float alpha, const double* reg, const double* YtY, const int64_t* rows,
                           int64_t nh, const int64_t* chunk_row, const int64_t* chunk_start, int64_t nchunks,
-                          int64_t chunk, double* G, double* B, float* X, int32_t* status, hipStream_t stream) {
+                          int64_t chunk, double* G, double* B, float* X, int32_t* status, int heavy_mfma,
+                          hipStream_t stream) {
   if (nh <= 0) return 0;
   if (r <= 0 || r > 64 || nchunks <= 0 || chunk <= 0) return 1;
 #define ALS_HEAVY(RP)                                                                                          \
@@ -460,7 +582,17 @@ int alink_als_heavy_solve(const int64_t* indptr, const int32_t* nbr, const float
   if (r <= 8) { ALS_HEAVY(8); }
   else if (r <= 16) { ALS_HEAVY(16); }
   else if (r <= 32) { ALS_HEAVY(32); }
-  else { ALS_HEAVY(64); }
+  else if (heavy_mfma) {
+    // rank 33..64: partial Grams on the matrix cores (exact bf16 x3 split), then the same solve
+    if (implicit)
+      hipLaunchKernelGGL(als_heavy_gram_mfma<true>, dim3((unsigned)nchunks), dim3(256), 0, stream, indptr, nbr, rating,
+                         Y, r, alpha, rows, chunk_row, chunk_start, chunk, G, B);
+    else
+      hipLaunchKernelGGL(als_heavy_gram_mfma<false>, dim3((unsigned)nchunks), dim3(256), 0, stream, indptr, nbr,
+                         rating, Y, r, alpha, rows, chunk_row, chunk_start, chunk, G, B);
+    hipLaunchKernelGGL(als_heavy_solve<64>, dim3((unsigned)nh), dim3(64), 0, stream, G, B, r, reg, YtY, rows, X,
+                       status);
+  } else { ALS_HEAVY(64); }
 #undef ALS_HEAVY
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }

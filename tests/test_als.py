@@ -191,3 +191,27 @@ def test_als_train_on_gpu_matches_docs():
     out = AlsPredictBatchOp().setUserCol("user").setItemCol("item").setPredictionCol("pred") \
         .linkFrom(model, data).collect()
     np.testing.assert_allclose([r[3] for r in out], REF, atol=1e-2)   # random init, as the CPU doc test
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("implicit", [False, True])
+def test_hip_als_heavy_mfma_gram_matches_valu(implicit, monkeypatch):
+    """Heavy rows at rank 64: the MFMA partial Gram (bf16 x3 exact split, per-step fp64 folding) gives the same
+    solutions as the fp64 VALU Gram to fp32 resolution."""
+    rng = np.random.default_rng(3)
+    m, n, r = 6, 5000, 64
+    counts = np.array([30000, 17000, 5, 50000, 0, 20001])
+    indptr = torch.zeros(m + 1, dtype=torch.int64)
+    indptr[1:] = torch.as_tensor(np.cumsum(counts))
+    nnz = int(indptr[-1])
+    nbr = torch.as_tensor(rng.integers(0, n, size=nnz), dtype=torch.int32)
+    rt = torch.as_tensor(rng.integers(1, 6, size=nnz).astype(np.float32))
+    Y = torch.as_tensor(rng.normal(size=(n, r)) * 0.3, dtype=torch.float32)
+    reg = torch.as_tensor(np.maximum(counts, 1) * 0.05, dtype=torch.float64)
+    YtY = (Y.double().T @ Y.double()).cuda() if implicit else None
+    args = (indptr.cuda(), nbr.cuda(), rt.cuda(), Y.cuda(), reg.cuda(), implicit, 2.0, YtY)
+    monkeypatch.setattr(aops, "HEAVY_MFMA", 1)
+    a = aops.fused_solve(*args).cpu().double().numpy()
+    monkeypatch.setattr(aops, "HEAVY_MFMA", 0)
+    b = aops.fused_solve(*args).cpu().double().numpy()
+    np.testing.assert_allclose(a, b, rtol=2e-5, atol=2e-6)
