@@ -106,8 +106,39 @@ def sql_select(mt: MTable, clause: str) -> MTable:
         names = _names_for(items)
         return MTable(TableSchema(names, [mt.schema.types[i] for i in idx]), [mt.cols[i] for i in idx],
                       mt.replicated)
+    cols = _select_columnar(mt, items)
+    if cols is not None:
+        return cols
     rows, schema = _select_rows(mt.rows(), mt.schema, clause)
     return MTable.from_rows(rows, schema, mt.replicated)
+
+
+def _select_columnar(mt: MTable, items) -> Optional[MTable]:
+    """Whole-column evaluation of a projection (``vexpr``) when every item is a column or a columnar
+    expression; None -> the row path."""
+    from ....common.table import Column
+    from .vexpr import try_evaluate
+    if mt.num_rows == 0 or any(it.expr.has_agg() for it in items):
+        return None
+    resolve = _resolver(mt.schema.names)
+    cols, types = [], []
+    for it in items:
+        if it.expr.kind == "col":
+            i = resolve(it.expr.args[0])
+            cols.append(mt.cols[i])
+            types.append(mt.schema.types[i])
+            continue
+        r = try_evaluate(it.expr, mt, resolve)
+        if r is None:
+            return None
+        vals, nulls = r
+        sample = Column(vals[:100].cpu(), None if nulls is None else nulls[:100].cpu()).to_list()
+        t = _out_type(it.expr, mt.schema, sample, resolve)
+        if t.torch_dtype is not None and vals.dtype != t.torch_dtype:
+            vals = vals.to(t.torch_dtype)
+        cols.append(Column(vals, nulls if nulls is not None and bool(nulls.any()) else None))
+        types.append(t)
+    return MTable(TableSchema(_names_for(items), types), cols, mt.replicated)
 
 
 def sql_as(mt: MTable, clause: str) -> MTable:
@@ -118,7 +149,14 @@ def sql_as(mt: MTable, clause: str) -> MTable:
 
 
 def sql_where(mt: MTable, clause: str) -> MTable:
-    f = compile_expr(parse_expr(clause), _resolver(mt.schema.names))
+    e = parse_expr(clause)
+    if mt.num_rows and not e.has_agg():
+        from .vexpr import try_evaluate
+        r = try_evaluate(e, mt, _resolver(mt.schema.names))
+        if r is not None and r[0].dtype == __import__("torch").bool:
+            keep = r[0] if r[1] is None else (r[0] & ~r[1])      # only TRUE rows survive (NULL drops)
+            return mt.take(keep)
+    f = compile_expr(e, _resolver(mt.schema.names))
     keep = [i for i, r in enumerate(mt.rows()) if f(r) is True]
     return mt.take(keep)
 
@@ -129,6 +167,16 @@ def _key(v):
 
 
 def sql_distinct(mt: MTable) -> MTable:
+    import torch
+    if mt.num_rows:
+        dev = next((c.values.device for c in mt.cols if isinstance(c.values, torch.Tensor)), torch.device("cpu"))
+        code = _row_codes(mt, range(len(mt.cols)), dev)
+        if code is not None:
+            # first occurrence of every distinct row, in row order (columnar: no per-row tuples)
+            n = mt.num_rows
+            first = torch.full((int(code.max()) + 1,), n, dtype=torch.int64, device=dev).scatter_reduce(
+                0, code, torch.arange(n, device=dev), "amin", include_self=True)
+            return mt.take(torch.sort(first)[0])
     seen = set()
     keep = []
     for i, r in enumerate(mt.rows()):
@@ -163,7 +211,131 @@ def sql_order_by(mt: MTable, clause: str, order: str = "asc", limit=None, offset
     return mt.take(idx)
 
 
+def _factorize(c) -> Tuple[Any, int]:
+    """(int64 codes [n] on the column's device, number of codes) of one key column; NULL -> its own code."""
+    import torch
+    v = c.values
+    if isinstance(v, torch.Tensor) and v.dim() == 1:
+        uniq, inv = torch.unique(v, return_inverse=True)
+        k = int(uniq.numel())
+        if c.nulls is not None:
+            inv = torch.where(c.nulls.to(inv.device), torch.full_like(inv, k), inv)
+            k += 1
+        return inv.to(torch.int64), k
+    vals = c.to_list()
+    if not all(x is None or isinstance(x, (str, int, float, bool)) for x in vals):
+        return None, 0
+    codes, table = [], {}
+    for x in vals:
+        codes.append(table.setdefault(_key(x), len(table)))
+    return torch.tensor(codes, dtype=torch.int64), len(table)
+
+
+def _row_codes(mt: MTable, idx, dev):
+    """Dense int64 code per row of the column tuple ``idx`` (equal tuples <-> equal codes), or None."""
+    import torch
+    code = torch.zeros(mt.num_rows, dtype=torch.int64, device=dev)
+    for i in idx:
+        ci, k = _factorize(mt.cols[i])
+        if ci is None:
+            return None
+        code = torch.unique(code * k + ci.to(dev), return_inverse=True)[1]     # stays < n: no overflow
+    return code
+
+
+def _group_by_columnar(mt: MTable, by: str, select: str) -> Optional[MTable]:
+    """GROUP BY plain key columns with COUNT / SUM / AVG / MIN / MAX over numeric tensor columns, evaluated per
+    column: key codes -> group ids in first-appearance order (the row path's OrderedDict order), then
+    bincount / index_add / scatter_reduce over the rows.  None -> the row path."""
+    import torch
+    from ....common.table import Column
+    if mt.num_rows == 0:
+        return None
+    resolve = _resolver(mt.schema.names)
+    keys = [parse_expr(p) for p in split_top_level(by)]
+    if any(k.kind != "col" for k in keys):
+        return None
+    kidx = [resolve(k.args[0]) for k in keys]
+    items = _expand_star(parse_select_list(select), mt.schema)
+    for it in items:
+        e = it.expr
+        if e.kind == "col":
+            if resolve(e.args[0]) not in kidx:
+                return None
+        elif e.kind == "agg":
+            name, args, distinct = e.args
+            if distinct or name not in ("COUNT", "SUM", "AVG", "MIN", "MAX") or len(args) != 1:
+                return None
+            if args[0].kind == "star":
+                if name != "COUNT":
+                    return None
+            elif args[0].kind != "col":
+                return None
+            else:
+                c = mt.cols[resolve(args[0].args[0])]
+                if not (isinstance(c.values, torch.Tensor) and c.values.dim() == 1 and c.values.dtype != torch.bool):
+                    return None
+        else:
+            return None
+    n = mt.num_rows
+    dev = next((c.values.device for c in mt.cols if isinstance(c.values, torch.Tensor)), torch.device("cpu"))
+    gid = _row_codes(mt, kidx, dev)
+    if gid is None:
+        return None
+    G = int(gid.max()) + 1
+    first = torch.full((G,), n, dtype=torch.int64, device=dev).scatter_reduce(
+        0, gid, torch.arange(n, device=dev), "amin", include_self=True)
+    order = torch.argsort(first)                      # groups in first-appearance order
+    rank = torch.empty_like(order)
+    rank[order] = torch.arange(G, device=dev)
+    g = rank[gid]                                     # group index per row, first-appearance numbering
+    firsts = first[order]
+    cols, types = [], []
+    for it in items:
+        e = it.expr
+        if e.kind == "col":
+            i = resolve(e.args[0])
+            cols.append(mt.cols[i].take(firsts.cpu() if not isinstance(mt.cols[i].values, torch.Tensor) else firsts))
+            types.append(mt.schema.types[i])
+            continue
+        name, args, _ = e.args
+        if args[0].kind == "star":
+            cnt = torch.bincount(g, minlength=G)
+            cols.append(Column(cnt))
+            types.append(Types.LONG)
+            continue
+        c = mt.cols[resolve(args[0].args[0])]
+        v = c.values.to(dev)
+        ok = ~c.nulls.to(dev) if c.nulls is not None else torch.ones(n, dtype=torch.bool, device=dev)
+        cnt = torch.bincount(g[ok], minlength=G)
+        empty = cnt == 0
+        if name == "COUNT":
+            cols.append(Column(cnt))
+            types.append(Types.LONG)
+            continue
+        isint = not v.dtype.is_floating_point
+        vv = v.to(torch.int64 if isint else torch.float64)[ok]
+        gg = g[ok]
+        if name in ("SUM", "AVG"):
+            acc = torch.zeros(G, dtype=vv.dtype, device=dev).index_add_(0, gg, vv)
+            res = acc if name == "SUM" else acc.to(torch.float64) / cnt.clamp(min=1)
+        else:
+            init = torch.zeros(G, dtype=vv.dtype, device=dev)
+            res = init.scatter_reduce(0, gg, vv, "amin" if name == "MIN" else "amax", include_self=False)
+        nulls = empty if bool(empty.any()) else None
+        col = Column(res, nulls)
+        t = _out_type(e, mt.schema, col.take(slice(0, 100)).to_list(), resolve)
+        if t.torch_dtype is not None and res.dtype != t.torch_dtype:
+            col = Column(res.to(t.torch_dtype), nulls)
+        cols.append(col)
+        types.append(t)
+    return MTable(TableSchema(_names_for(items), types), cols)
+
+
 def sql_group_by(mt: MTable, by: str, select: str) -> MTable:
+    out = _group_by_columnar(mt, by, select)
+    if out is not None:
+        return out
     resolve = _resolver(mt.schema.names)
     kfs = [compile_expr(parse_expr(p), resolve) for p in split_top_level(by)]
     groups: "OrderedDict[tuple, List[Row]]" = OrderedDict()
