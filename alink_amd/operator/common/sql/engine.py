@@ -173,9 +173,7 @@ def sql_distinct(mt: MTable) -> MTable:
         code = _row_codes(mt, range(len(mt.cols)), dev)
         if code is not None:
             # first occurrence of every distinct row, in row order (columnar: no per-row tuples)
-            n = mt.num_rows
-            first = torch.full((int(code.max()) + 1,), n, dtype=torch.int64, device=dev).scatter_reduce(
-                0, code, torch.arange(n, device=dev), "amin", include_self=True)
+            first = _first_index(code, int(code.max()) + 1)
             return mt.take(torch.sort(first)[0])
     seen = set()
     keep = []
@@ -243,6 +241,15 @@ def _row_codes(mt: MTable, idx, dev):
     return code
 
 
+def _first_index(code, G: int):
+    """[G] first row index of every code value (codes dense in [0, G)), from one stable sort (no atomics)."""
+    import torch
+    o = torch.argsort(code, stable=True)
+    cnt = torch.bincount(code, minlength=G)
+    starts = torch.cumsum(cnt, 0) - cnt
+    return o[starts]
+
+
 def _group_by_columnar(mt: MTable, by: str, select: str) -> Optional[MTable]:
     """GROUP BY plain key columns with COUNT / SUM / AVG / MIN / MAX over numeric tensor columns, evaluated per
     column: key codes -> group ids in first-appearance order (the row path's OrderedDict order), then
@@ -283,8 +290,7 @@ def _group_by_columnar(mt: MTable, by: str, select: str) -> Optional[MTable]:
     if gid is None:
         return None
     G = int(gid.max()) + 1
-    first = torch.full((G,), n, dtype=torch.int64, device=dev).scatter_reduce(
-        0, gid, torch.arange(n, device=dev), "amin", include_self=True)
+    first = _first_index(gid, G)
     order = torch.argsort(first)                      # groups in first-appearance order
     rank = torch.empty_like(order)
     rank[order] = torch.arange(G, device=dev)
@@ -314,14 +320,25 @@ def _group_by_columnar(mt: MTable, by: str, select: str) -> Optional[MTable]:
             types.append(Types.LONG)
             continue
         isint = not v.dtype.is_floating_point
-        vv = v.to(torch.int64 if isint else torch.float64)[ok]
+        # segmented reductions over the rows sorted (stably) by group: no atomics on a handful of hot group
+        # addresses, and the summation order is the row order within each group (the row path's)
         gg = g[ok]
+        o = torch.argsort(gg, stable=True)
+        vv = v.to(torch.int64 if isint else torch.float64)[ok][o]
         if name in ("SUM", "AVG"):
-            acc = torch.zeros(G, dtype=vv.dtype, device=dev).index_add_(0, gg, vv)
+            if isint:
+                cs = torch.zeros(vv.numel() + 1, dtype=torch.int64, device=dev)
+                torch.cumsum(vv, 0, out=cs[1:])
+                ends = torch.cumsum(cnt, 0)
+                acc = cs[ends] - cs[ends - cnt]
+            else:
+                acc = torch.segment_reduce(vv, "sum", lengths=cnt)
             res = acc if name == "SUM" else acc.to(torch.float64) / cnt.clamp(min=1)
         else:
-            init = torch.zeros(G, dtype=vv.dtype, device=dev)
-            res = init.scatter_reduce(0, gg, vv, "amin" if name == "MIN" else "amax", include_self=False)
+            res = torch.segment_reduce(vv.to(torch.float64), "min" if name == "MIN" else "max", lengths=cnt)
+            res = torch.where(empty, torch.zeros_like(res), res)
+            if isint:
+                res = res.to(torch.int64)
         nulls = empty if bool(empty.any()) else None
         col = Column(res, nulls)
         t = _out_type(e, mt.schema, col.take(slice(0, 100)).to_list(), resolve)

@@ -85,7 +85,8 @@ class FtrlTrainStreamOp(StreamOperator):
       (RCCL), and every rank applies the same mini-batch FTRL-proximal update (n += sum g^2, z += sum g - sigma w).
       Throughput grows with P; per-sample ordering inside a micro-batch is not kept (a different, mini-batch
       rule than SEQUENTIAL / SHARDED).
-    * ``HOGWILD`` (single GPU): ``ops/csrc/ftrl.hip``, one wave per sample, exact atomic n/z, prox pass.
+    * ``HOGWILD`` (GPU): ``ops/csrc/ftrl.hip``, one wave per sample, exact atomic n/z, prox pass; with P ranks
+      every rank runs it on its own micro-batch and the (dn, dz) increments are all-reduced each step.
 
     Every step (and every snapshot decision) is a collective over the ranks, so ranks with different numbers of
     micro-batches stay in lockstep: a rank whose stream ended keeps joining steps with an empty batch until all
@@ -133,8 +134,6 @@ class FtrlTrainStreamOp(StreamOperator):
             raise ValueError(f"unknown updateMode {self._mode}")
         self._ws, self._rank = comm.get_world_size(), comm.get_rank()
         self.recv_nnz = []          # SHARDED: nonzeros this shard received per step (observability / tests)
-        if self._mode == "HOGWILD" and self._ws > 1:
-            raise ValueError("updateMode HOGWILD is single-rank; use SHARDED for P > 1")
         # SEQUENTIAL keeps its state on the host (the rule is a serial loop); the others on the rank's GPU
         gpu = self.env.device.type == "cuda" and self._mode != "SEQUENTIAL"
         self._dev = self.env.device if gpu else torch.device("cpu")
@@ -225,6 +224,8 @@ class FtrlTrainStreamOp(StreamOperator):
             self._first = False
         if self._mode == "DATA_PARALLEL":
             self._dp_step(csr)
+        elif self._mode == "HOGWILD" and self._ws > 1:
+            self._hogwild_step(csr)
         elif self._ws == 1:
             if csr is not None and csr[0].shape[0] > 1:
                 self._apply(*csr)
@@ -303,6 +304,24 @@ class FtrlTrainStreamOp(StreamOperator):
         if self._ws > 1:
             gq = comm.all_reduce(gq.to(self._comm_dev()), "sum").to(dev)
         ftrl_dp_update(gq, w, n, z, self._alpha, self._beta, self._l1, self._l2)
+
+    def _hogwild_step(self, csr):
+        """HOGWILD over P ranks: every rank runs the one-wave-per-sample Hogwild kernel on its OWN micro-batch
+        from the shared state of the step start, the per-coordinate increments (dn, dz) of all ranks are summed
+        (one dense all-reduce) and added to that state, and w = prox(z, n) is re-derived.  Within a rank samples
+        race as in the single-GPU mode; across ranks a sample sees the other ranks' updates one micro-batch late
+        (the reference's asynchronous feedback loop, bounded staleness)."""
+        import torch
+        from ...ops.ftrl import ftrl_hogwild, ftrl_prox_hip
+        w, n, z = self._state
+        n0, z0 = n.clone(), z.clone()
+        if csr is not None and csr[0].numel() > 1:
+            ftrl_hogwild(*(t.to(self._dev) for t in csr), w, n, z, self._alpha, self._beta, self._l1, self._l2)
+        d = torch.stack([n - n0, z - z0])
+        d = comm.all_reduce(d.to(self._comm_dev()), "sum").to(self._dev)
+        n.copy_(n0 + d[0])
+        z.copy_(z0 + d[1])
+        ftrl_prox_hip(w, n, z, self._alpha, self._beta, self._l1, self._l2)
 
     def _comm_dev(self):
         import torch

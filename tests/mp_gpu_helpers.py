@@ -90,6 +90,40 @@ def scenario_gbdt(out):
     out["device"] = str(env.device)
 
 
+def scenario_ftrl_hogwild(out):
+    """FTRL updateMode HOGWILD over P ranks sharing the GPU: local Hogwild kernel + all-reduced (dn, dz)."""
+    import numpy as np
+    import pandas as pd
+    from alink_amd import (useLocalEnv, BatchOperator, StreamOperator, LogisticRegressionTrainBatchOp,
+                           FtrlTrainStreamOp, CollectStreamOp)
+    from alink_amd.parallel import comm
+    os.environ["ALINK_STREAM_BATCH"] = "64"
+    env = useLocalEnv(1)
+    rng = np.random.default_rng(5)
+    X = rng.normal(size=(2000, 6))
+    wt = np.array([1.0, -1.0, 0.5, 0.2, -0.7, 0.0])
+    df = pd.DataFrame({f"f{i}": X[:, i] for i in range(6)})
+    df["label"] = (X @ wt + 0.3 * rng.normal(size=2000) > 0).astype(int)
+    schema = ", ".join(f"f{i} double" for i in range(6)) + ", label int"
+    cols = [f"f{i}" for i in range(6)]
+    model = LogisticRegressionTrainBatchOp().setFeatureCols(cols).setLabelCol("label").setMaxIter(2) \
+        .linkFrom(BatchOperator.fromDataframe(df.iloc[:50], schemaStr=schema))
+    snaps = []
+    FtrlTrainStreamOp(model).setFeatureCols(cols).setLabelCol("label").setTimeInterval(1e9) \
+        .setUpdateMode("HOGWILD").setAlpha(0.1).setBeta(1.0).linkFrom(
+            StreamOperator.fromDataframe(df, schemaStr=schema)).link(CollectStreamOp(snaps))
+    StreamOperator.execute()
+    last = max(r[0] for r in snaps)
+    coef = [r for r in snaps if r[0] == last and r[2] == 1048576][0][3]
+    w = np.asarray(json.loads(coef)["coefVector"]["data"])
+    out["coef"] = w.tolist()
+    m = X @ w[1:] + w[0] if w.size == 7 else X @ w[:6]
+    y = df["label"].to_numpy()
+    out["acc"] = float(((m > 0).astype(int) == y).mean())
+    out["backend"] = comm._backend()
+    out["device"] = str(env.device)
+
+
 def run(rank, world, port, scenario, outdir):
     os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
                        "LOCAL_WORLD_SIZE": str(world), "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})

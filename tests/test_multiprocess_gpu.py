@@ -89,3 +89,13 @@ def test_gbdt_feature_sharded_multiprocess_gpu_matches_one_rank(tmp_path):
     ta = [_json.loads(r[1]) for r in one["model"] if r[0] >= 0 and r[1]]
     tb = [_json.loads(r[1]) for r in two[0]["model"] if r[0] >= 0 and r[1]]
     assert len(ta) == len(tb)
+
+
+def test_ftrl_hogwild_multiprocess_gpu(tmp_path):
+    """HOGWILD FTRL over 2 ranks on one GPU: every rank ends with the same replicated model, and it learns as
+    well as the 1-rank Hogwild model (cross-rank staleness is one micro-batch)."""
+    one = _run("ftrl_hogwild", 1, tmp_path)[0]
+    two = _run("ftrl_hogwild", 2, tmp_path)
+    assert "cuda" in one["device"]
+    assert two[0]["coef"] == two[1]["coef"]
+    assert one["acc"] > 0.85 and two[0]["acc"] > one["acc"] - 0.03
