@@ -92,6 +92,16 @@ def scenario_gbdt(out):
 
 def scenario_ftrl_hogwild(out):
     """FTRL updateMode HOGWILD over P ranks sharing the GPU: local Hogwild kernel + all-reduced (dn, dz)."""
+    _ftrl_mode(out, "HOGWILD")
+
+
+def scenario_ftrl_sharded(out):
+    """FTRL updateMode SHARDED over P ranks sharing the GPU: SplitVector all-to-all of device CSR entries,
+    partial-margin HIP kernel, margin all-reduce, per-coordinate replay kernel on each rank's range."""
+    _ftrl_mode(out, "SHARDED")
+
+
+def _ftrl_mode(out, mode):
     import numpy as np
     import pandas as pd
     from alink_amd import (useLocalEnv, BatchOperator, StreamOperator, LogisticRegressionTrainBatchOp,
@@ -110,7 +120,7 @@ def scenario_ftrl_hogwild(out):
         .linkFrom(BatchOperator.fromDataframe(df.iloc[:50], schemaStr=schema))
     snaps = []
     FtrlTrainStreamOp(model).setFeatureCols(cols).setLabelCol("label").setTimeInterval(1e9) \
-        .setUpdateMode("HOGWILD").setAlpha(0.1).setBeta(1.0).linkFrom(
+        .setUpdateMode(mode).setAlpha(0.1).setBeta(1.0).linkFrom(
             StreamOperator.fromDataframe(df, schemaStr=schema)).link(CollectStreamOp(snaps))
     StreamOperator.execute()
     last = max(r[0] for r in snaps)
@@ -122,6 +132,26 @@ def scenario_ftrl_hogwild(out):
     out["acc"] = float(((m > 0).astype(int) == y).mean())
     out["backend"] = comm._backend()
     out["device"] = str(env.device)
+
+
+def scenario_cross_gpu(out):
+    """Ring blockwise top-K with device query / item blocks (the top-K merge kernel on the GPU)."""
+    import torch
+    from alink_amd.parallel import comm
+    from alink_amd.parallel.cross import blockwise_topk
+    comm.init_distributed()
+    ws, me = comm.get_world_size(), comm.get_rank()
+    g = torch.Generator().manual_seed(3)
+    Q = torch.randn(300, 16, generator=g)
+    T = torch.randn(5000, 16, generator=g)
+    qb = [round(i * 300 / ws) for i in range(ws + 1)]
+    ib = [0] + sorted(int(x) for x in torch.randint(1, 5000, (ws - 1,), generator=g).tolist()) + [5000]
+    dev = comm.device_for_rank()
+    v, i = blockwise_topk(Q[qb[me]:qb[me + 1]].to(dev), T[ib[me]:ib[me + 1]].to(dev), 10)
+    ref_v, ref_i = torch.topk(Q[qb[me]:qb[me + 1]] @ T.T, 10, dim=1)
+    out["ids_equal"] = bool(torch.equal(i.cpu(), ref_i))
+    out["max_abs_diff"] = float((v.cpu() - ref_v).abs().max())
+    out["on_device"] = v.is_cuda
 
 
 def run(rank, world, port, scenario, outdir):

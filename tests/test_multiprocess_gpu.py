@@ -99,3 +99,19 @@ def test_ftrl_hogwild_multiprocess_gpu(tmp_path):
     assert "cuda" in one["device"]
     assert two[0]["coef"] == two[1]["coef"]
     assert one["acc"] > 0.85 and two[0]["acc"] > one["acc"] - 0.03
+
+
+def test_ftrl_sharded_multiprocess_gpu(tmp_path):
+    """SHARDED FTRL with device tensors over 2 ranks (SplitVector all-to-all, partial-margin and replay HIP
+    kernels per coefficient range): both ranks assemble the same model and it learns as well as 1 rank (the
+    ranks' micro-batches form different global steps than one rank's, so the models are not bit-equal)."""
+    one = _run("ftrl_sharded", 1, tmp_path)[0]
+    two = _run("ftrl_sharded", 2, tmp_path)
+    assert two[0]["coef"] == two[1]["coef"]
+    assert one["acc"] > 0.85 and two[0]["acc"] > one["acc"] - 0.03
+
+
+def test_ring_topk_multiprocess_gpu(tmp_path):
+    """Ring blockwise top-K with device blocks over 2 ranks == torch.topk of the full score matrix."""
+    for o in _run("cross_gpu", 2, tmp_path):
+        assert o["on_device"] and o["ids_equal"] and o["max_abs_diff"] < 1e-4
