@@ -298,6 +298,72 @@ __global__ __launch_bounds__(256) void vector_assemble_kernel(int64_t n, int P, 
     }
 }
 
+// VectorAssembler v2 (P <= 16 parts): one 256-thread workgroup per 256 rows.  Thread t first forms row r0+t's
+// run offsets per part (LDS), then the workgroup walks its contiguous output range element by element: each
+// thread finds its element's row by binary search over the LDS row starts and its part by a scan of the row's
+// run offsets, reads the source entry and writes col / val -- consecutive threads write consecutive entries
+// (coalesced stores; v1 wrote one row-run per thread, 64 scattered runs per store instruction).
+constexpr int kVaRows = 256;
+constexpr int kVaMaxP = 16;
+
+__global__ __launch_bounds__(256) void vector_assemble_v2_kernel(int64_t n, int P, const int64_t* __restrict__ desc,
+                                                                const int64_t* __restrict__ out_crow,
+                                                                int32_t* __restrict__ out_col,
+                                                                double* __restrict__ out_val) {
+  __shared__ int32_t roff[kVaMaxP + 1][kVaRows];        // run start of part p inside row t (p = P: row length)
+  __shared__ int32_t rstart[kVaRows + 1];              // row start inside the workgroup's output range
+  __shared__ int64_t d_s[kVaMaxP * 8];
+  const int t = threadIdx.x;
+  const int64_t r0 = (int64_t)blockIdx.x * kVaRows;
+  const int nr = (int)min((int64_t)kVaRows, n - r0);
+  for (int i = t; i < P * 8; i += 256) d_s[i] = desc[i];
+  __syncthreads();
+  const int64_t base = out_crow[r0];
+  if (t < nr) {
+    int32_t o = 0;
+    for (int p = 0; p < P; ++p) {
+      roff[p][t] = o;
+      o += (int32_t)part_len(d_s + 8 * p, r0 + t);
+    }
+    roff[P][t] = o;
+    rstart[t] = (int32_t)(out_crow[r0 + t] - base);
+  }
+  if (t == 0) rstart[nr] = (int32_t)(out_crow[r0 + nr] - base);
+  __syncthreads();
+  const int32_t total = rstart[nr];
+  for (int32_t e = t; e < total; e += 256) {
+    int lo = 0, hi = nr;                                 // last row with rstart <= e
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (rstart[mid] <= e) lo = mid;
+      else hi = mid;
+    }
+    const int row = lo;
+    const int32_t j = e - rstart[row];
+    int p = 0;
+    while (p + 1 < P && roff[p + 1][row] <= j) ++p;
+    const int64_t* d = d_s + 8 * p;
+    const int64_t k = j - roff[p][row];
+    const int64_t r = r0 + row;
+    const int kind = (int)d[0];
+    int32_t c;
+    double v;
+    if (kind == 3) {
+      const int64_t s = reinterpret_cast<const int64_t*>(d[3])[r] + k;
+      c = (int32_t)(d[6] + reinterpret_cast<const int32_t*>(d[4])[s]);
+      v = reinterpret_cast<const double*>(d[2])[s];
+    } else {
+      const int64_t src = r * d[1] + k;
+      c = (int32_t)(d[6] + k);
+      if (kind == 0) v = reinterpret_cast<const double*>(d[2])[src];
+      else if (kind == 1) v = (double)reinterpret_cast<const float*>(d[2])[src];
+      else v = (double)__uint_as_float((uint32_t)reinterpret_cast<const uint16_t*>(d[2])[src] << 16);
+    }
+    out_col[base + e] = c;
+    out_val[base + e] = v;
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -338,10 +404,17 @@ int alink_murmur3_bytes(const uint8_t* bytes, const int64_t* off, int64_t n, uin
 }
 
 // VectorAssembler rows: desc [P][8] int64 part descriptors (device), out_crow [n+1] (host-computed prefix of
-// the per-row entry counts), out_col / out_val [out_crow[n]].
+// the per-row entry counts), out_col / out_val [out_crow[n]].  variant 2: element-parallel workgroups (P <= 16,
+// rows shorter than 2^22 entries), else one thread per (part, row).
 int alink_vector_assemble(int64_t n, int P, const int64_t* desc, const int64_t* out_crow, int32_t* out_col,
-                          double* out_val, void* stream) {
+                          double* out_val, int variant, void* stream) {
     if (n <= 0 || P <= 0) return 0;
+    if (P <= kVaMaxP && variant == 2) {
+        const int64_t nb = (n + kVaRows - 1) / kVaRows;
+        hipLaunchKernelGGL(vector_assemble_v2_kernel, dim3((unsigned)nb), dim3(256), 0,
+                           reinterpret_cast<hipStream_t>(stream), n, P, desc, out_crow, out_col, out_val);
+        return hipGetLastError() == hipSuccess ? 0 : 2;
+    }
     const int64_t blocks = (n * P + 255) / 256;
     hipLaunchKernelGGL(vector_assemble_kernel, dim3(blocks < 65536 ? blocks : 65536), dim3(256), 0,
                        reinterpret_cast<hipStream_t>(stream), n, P, desc, out_crow, out_col, out_val);

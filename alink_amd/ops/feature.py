@@ -103,6 +103,8 @@ def csr_assemble(idx: torch.Tensor, val: Optional[torch.Tensor], valid: Optional
 
 
 _DENSE_KIND = {torch.float64: 0, torch.float32: 1, torch.bfloat16: 2}
+# 2: element-parallel VectorAssembler workgroups (coalesced stores), 1: thread per (part, row)
+VA_VARIANT = int(__import__("os").environ.get("ALINK_VA_VARIANT", "2"))
 
 
 def vector_assemble(parts, n: int, skip: Optional[torch.Tensor] = None, dense_ratio: Optional[float] = None,
@@ -170,7 +172,10 @@ def vector_assemble(parts, n: int, skip: Optional[torch.Tensor] = None, dense_ra
                 desc[i, 2] = p.data_ptr()
             desc[i, 5] = 0 if sk is None else sk.data_ptr()
         ddesc = desc.to(dev)
+        tot = crow[1:] - crow[:-1]
+        variant = 2 if len(norm) <= 16 and int(tot.max()) < (1 << 22) else 1
         rc = L.alink_vector_assemble(n, len(norm), ddesc.data_ptr(), crow.data_ptr(), col.data_ptr(), val.data_ptr(),
+                                     VA_VARIANT if VA_VARIANT in (1, 2) and variant == 2 else variant,
                                      _lib.stream_ptr(dev))
         if rc != 0:
             raise RuntimeError(f"alink_vector_assemble failed: {rc}")

@@ -79,9 +79,13 @@ def test_columnar_assembler_error_on_null():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("variant", [1, 2])
 @pytest.mark.parametrize("handle,nulls", [("ERROR", False), ("SKIP", True)])
-def test_hip_vector_assemble_equals_host(handle, nulls):
-    """The HIP kernel path (device columns) equals the host columnar path and the per-row rule."""
+def test_hip_vector_assemble_equals_host(handle, nulls, variant, monkeypatch):
+    """The HIP kernel paths (device columns; v1 thread per (part, row), v2 element-parallel workgroups) equal
+    the host columnar path and the per-row rule."""
+    import alink_amd.ops.feature as FE
+    monkeypatch.setattr(FE, "VA_VARIANT", variant)
     host = _table(3000, 5, nulls)
     dev = _table(3000, 5, nulls, dev="cuda")
     m = _mapper(host, handle)

@@ -35,7 +35,9 @@ def main():
     parts.append(SparseBlock(crow, col, torch.randn(nnz, device=dev, generator=g, dtype=torch.float64), 1000))
     res = {"rows": n}
     out = {}
-    for name, uk in (("kernel", True), ("torch", False)):
+    import alink_amd.ops.feature as FE
+    for name, uk, var in (("kernel_v1", True, 1), ("kernel", True, 2), ("torch", False, 2)):
+        FE.VA_VARIANT = var
         sb, _ = vector_assemble(parts, n, use_kernel=uk)
         torch.cuda.synchronize()
         ts = []
@@ -50,6 +52,7 @@ def main():
     res["equal"] = bool(torch.equal(a_.crow, b_.crow) and torch.equal(a_.col, b_.col) and torch.equal(a_.val, b_.val))
     res["nnz"] = int(a_.crow[-1])
     res["speedup"] = round(res["torch_ms"] / res["kernel_ms"], 2)
+    res["v1_equal"] = bool(torch.equal(out["kernel_v1"].col, a_.col) and torch.equal(out["kernel_v1"].val, a_.val))
     res["kernel_GBps_written"] = round(res["nnz"] * 12 / (res["kernel_ms"] * 1e-3) / 1e9, 1)
     print(json.dumps(res))
 
