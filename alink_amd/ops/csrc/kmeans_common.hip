@@ -26,13 +26,26 @@ __global__ __launch_bounds__(256) void kmeans_reduce_slabs_kernel(const float* _
     __shared__ double part[8][32];
     const int c = blockIdx.x, y = blockIdx.y;
     const int d = threadIdx.x & 31, g = threadIdx.x >> 5;
-    double s = 0.0;
+    // four independent partial sums per thread (slabs g, g+8, g+16, g+24 mod 32): the loads of a thread are
+    // in flight together instead of one dependent chain; the combination order is fixed -> deterministic
+    double s4[4] = {0.0, 0.0, 0.0, 0.0};
     if (y < 4) {
         const float* p = slab + (int64_t)c * D + 32 * y + d;
-        for (int w = g; w < nslab; w += 8) s += (double)p[(int64_t)w * 128 * D];
+        int w = g;
+        for (; w + 24 < nslab; w += 32) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) s4[j] += (double)p[(int64_t)(w + 8 * j) * 128 * D];
+        }
+        for (int j = 0; w < nslab; w += 8, ++j) s4[j & 3] += (double)p[(int64_t)w * 128 * D];
     } else if (d == 0) {
-        for (int w = g; w < nslab; w += 8) s += (double)slab_cnt[(int64_t)w * 128 + c];
+        int w = g;
+        for (; w + 24 < nslab; w += 32) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) s4[j] += (double)slab_cnt[(int64_t)(w + 8 * j) * 128 + c];
+        }
+        for (int j = 0; w < nslab; w += 8, ++j) s4[j & 3] += (double)slab_cnt[(int64_t)w * 128 + c];
     }
+    const double s = (s4[0] + s4[1]) + (s4[2] + s4[3]);
     part[g][d] = s;
     __syncthreads();
     if (g == 0) {
