@@ -116,7 +116,8 @@ def test_trace_kernel_device_track(tmp_path):
         evs = json.load(f)["traceEvents"]
     host = [e for e in evs if e.get("cat") == "kernel"]
     gpu = [e for e in evs if e.get("cat") == "kernel.gpu"]
-    assert any(e["name"] == "kmeans_assign_accum_bf16_v7" for e in host)
-    v7 = [e for e in gpu if e["name"] == "kmeans_assign_accum_bf16_v7"]
-    assert len(v7) == 3 and all(e["dur"] > 0 for e in v7)
+    name = f"kmeans_assign_accum_bf16_{kops.kernel_version(16)}"      # the production kernel for k = 16
+    assert any(e["name"] == name for e in host)
+    ks = [e for e in gpu if e["name"] == name]
+    assert len(ks) == 3 and all(e["dur"] > 0 for e in ks)
     assert all(e["tid"] == "gpu" for e in gpu)
