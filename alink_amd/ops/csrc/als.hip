@@ -295,25 +295,43 @@ __device__ __forceinline__ void gram_lds(const int32_t* __restrict__ nbr, const 
   lds_wave_sync<RP>();
 }
 
-// Gauss-Jordan on the SPD system in registers (lane = row), pivot rows broadcast through buf; after the last
-// step v = x_i.  One step per template instance (K compile-time: every register index static; a 64-step
-// `#pragma unroll` loop exceeds the unroller's size limit and would fall back to scratch-indexed arrays).
+// 1 / p to ~1 ulp: v_rcp_f64 + two Newton steps (the IEEE division sequence is ~4x longer and sits on the
+// step's dependence chain)
+__device__ __forceinline__ double rcp_f64(double p) {
+  double r = __builtin_amdgcn_rcp(p);
+  r = fma(fma(-p, r, 1.0), r, r);
+  r = fma(fma(-p, r, 1.0), r, r);
+  return r;
+}
+
+// Gauss-Jordan on the SPD system in registers (lane = row), pivot columns broadcast through two alternating LDS
+// rows; after the last step v = x_i.  Software-pipelined across steps: step K updates column K+1 first and
+// writes it to the other row immediately, so the LDS write -> read latency of step K+1's broadcast overlaps the
+// rest of step K's row update (and no trailing wait is needed: step K+1 starts with the wait that also retires
+// step K's reads before anything overwrites their row).  One step per template instance (K compile-time: every
+// register index static; a 64-step `#pragma unroll` loop exceeds the unroller's size limit and would fall back to
+// scratch-indexed arrays).
 template <int RP, int K>
 struct GJStep {
   static __device__ __forceinline__ void run(double (&a)[RP], double& v, double& diag, int& bad, int lane,
                                              double* buf) {
     __builtin_amdgcn_sched_barrier(0);   // one step at a time: keeps the register pressure at a[] + a few
-    buf[lane] = a[K];                    // column K = row K of the symmetric trailing block
+    double* cur = buf + (K & 1) * 64;    // column K (written by step K-1, or before step 0)
+    double* nxt = buf + ((K + 1) & 1) * 64;
     lds_wave_sync<RP>();
     const double p = readlane_f64(a[K], K);
     const double vk = readlane_f64(v, K);
     bad |= !(p > 0.0);
-    const double rp = 1.0 / (p > 0.0 ? p : 1.0);
+    const double rp = rcp_f64(p > 0.0 ? p : 1.0);
     const double f = lane == K ? 0.0 : a[K] * rp;
     diag = lane == K ? p : diag;
-    if constexpr (K + 1 < RP) axpy_bcast<RP>(a, -f, buf, K + 1);   // a_i[j] -= f_i a_K[j], j > K
+    if constexpr (K + 1 < RP) {
+      a[K + 1] = fma(-f, cur[K + 1], a[K + 1]);
+      asm volatile("" : "+v"(a[K + 1]));
+      nxt[lane] = a[K + 1];              // next step's pivot column, in flight during the rest of this step
+      if constexpr (K + 2 < RP) axpy_bcast<RP>(a, -f, cur, K + 2);   // a_i[j] -= f_i a_K[j], j > K + 1
+    }
     v = fma(-f, vk, v);
-    lds_wave_sync<RP>();
     if constexpr (K + 1 < RP) GJStep<RP, K + 1>::run(a, v, diag, bad, lane, buf);
   }
 };
@@ -322,7 +340,10 @@ template <int RP>
 __device__ __forceinline__ int gj_solve(double (&a)[RP], double& v, int lane, double* buf) {
   int bad = 0;
   double diag = 1.0;
+  lds_wave_sync<RP>();                   // the Gram phase's last reads of buf are done
+  buf[lane] = a[0];
   GJStep<RP, 0>::run(a, v, diag, bad, lane, buf);
+  lds_wave_sync<RP>();
   v = v / (diag > 0.0 ? diag : 1.0);
   return bad;
 }
