@@ -128,8 +128,36 @@ class _Side:
         return sel, indptr, self.nbr[pos], self.rating[pos]
 
 
+GATHER_BLOCKS = int(os.environ.get("ALINK_ALS_GATHER_BLOCKS", "4"))
+
+
 def _update(side: _Side, mask: torch.Tensor, Y: torch.Tensor, X: torch.Tensor, lam: float, implicit: bool,
             alpha: float, nonneg: bool, YtY: Optional[torch.Tensor]):
+    """Solve this rank's rows of ``side`` against ``Y`` and replicate them into ``X``.  Over P ranks the rows are
+    solved in GATHER_BLOCKS pieces: the all-gather of piece b runs on the comm stream (asynchronous) while piece
+    b+1 solves (SURVEY §7.1 compute / communication overlap; the reference's AlsTrain exchanges factor blocks
+    by shuffle, ``AlsTrain.java:283-389``)."""
+    ws = comm.get_world_size()
+    if ws > 1 and GATHER_BLOCKS > 1:
+        sel_all = torch.nonzero(mask, as_tuple=False).reshape(-1)
+        bounds = [(len(sel_all) * b) // GATHER_BLOCKS for b in range(GATHER_BLOCKS + 1)]
+        pend = []
+        for b in range(GATHER_BLOCKS):
+            m = torch.zeros_like(mask)
+            m[sel_all[bounds[b]:bounds[b + 1]]] = True
+            rows, x = _solve(side, m, Y, X, lam, implicit, alpha, nonneg, YtY)
+            pend.append((comm.all_gather_varlen_async(rows), comm.all_gather_varlen_async(x)))
+        for pr, px in pend:
+            X[pr.wait()] = px.wait().to(X.dtype)
+        return
+    rows, x = _solve(side, mask, Y, X, lam, implicit, alpha, nonneg, YtY)
+    rows_all = comm.all_gather_varlen(rows)
+    x_all = comm.all_gather_varlen(x)
+    X[rows_all] = x_all.to(X.dtype)
+
+
+def _solve(side: _Side, mask: torch.Tensor, Y: torch.Tensor, X: torch.Tensor, lam: float, implicit: bool,
+           alpha: float, nonneg: bool, YtY: Optional[torch.Tensor]):
     sel, indptr, nbr, rating = side.subset(mask)
     if sel.numel() and not nonneg and aops.fused_supported(Y):
         # GPU: normal equations + Cholesky fused per row (ops/csrc/als.hip), no [m, r, r] tensor in HBM
@@ -148,9 +176,7 @@ def _update(side: _Side, mask: torch.Tensor, Y: torch.Tensor, X: torch.Tensor, l
     else:
         x = torch.zeros((0, X.shape[1]), dtype=torch.float32, device=X.device)
         rows = torch.zeros(0, dtype=torch.int64, device=X.device)
-    rows_all = comm.all_gather_varlen(rows)
-    x_all = comm.all_gather_varlen(x)
-    X[rows_all] = x_all.to(X.dtype)
+    return rows, x
 
 
 def train_als(mt: MTable, params: Params, env) -> AlsModelData:

@@ -94,7 +94,10 @@ class FtrlTrainStreamOp(StreamOperator):
     """
     EXTRA_PARAMS = [ParamInfo("updateMode", str, "SEQUENTIAL, SHARDED (feature-sharded micro-batch), DATA_PARALLEL "
                                                  "(replicated, all-reduced mini-batch gradients) or HOGWILD (GPU, "
-                                                 "one wave per sample)", default="SEQUENTIAL")]
+                                                 "one wave per sample)", default="SEQUENTIAL"),
+                    ParamInfo("asyncGradReduce", bool, "DATA_PARALLEL: overlap the gradient all-reduce of a step "
+                                                       "with scoring the next (one-step-stale gradients)",
+                              default=False)]
 
     def __init__(self, model=None, params: Optional[Params] = None, **kw):
         if isinstance(model, Params):
@@ -130,6 +133,8 @@ class FtrlTrainStreamOp(StreamOperator):
         self._feat_cols = _pget(p, "featureCols")
         self._vsize = _pget(p, "vectorSize")
         self._mode = str(_pget(p, "updateMode", "SEQUENTIAL")).upper()
+        self._async_reduce = bool(_pget(p, "asyncGradReduce", False))
+        self._pending = None
         if self._mode not in ("SEQUENTIAL", "SHARDED", "DATA_PARALLEL", "HOGWILD"):
             raise ValueError(f"unknown updateMode {self._mode}")
         self._ws, self._rank = comm.get_world_size(), comm.get_rank()
@@ -184,6 +189,7 @@ class FtrlTrainStreamOp(StreamOperator):
     # ---------------------------------------------------------------- checkpoint state
     def _state_dict(self):
         import torch
+        self._drain()
         w, n, z = (torch.as_tensor(a).detach().cpu().clone() for a in self._state)
         return {"w": w, "n": n, "z": z, "bid": int(self._bid), "first": bool(self._first)}
 
@@ -204,6 +210,7 @@ class FtrlTrainStreamOp(StreamOperator):
     def on_finish(self, port):
         while self._step(None):
             pass
+        self._drain()
         self._snapshot()
 
     def _step(self, mt) -> bool:
@@ -237,6 +244,7 @@ class FtrlTrainStreamOp(StreamOperator):
                 self._apply(*batch)
         if due:
             self._t0 = time.time()
+            self._drain()
             self._snapshot()
         return True
 
@@ -292,7 +300,9 @@ class FtrlTrainStreamOp(StreamOperator):
 
     def _dp_step(self, csr):
         """DATA_PARALLEL: local scoring, one dense all-reduce of the per-coordinate (sum g, sum g^2), identical
-        mini-batch FTRL-proximal update on every rank (``ops/ftrl.py``)."""
+        mini-batch FTRL-proximal update on every rank (``ops/ftrl.py``).  ``asyncGradReduce``: the all-reduce of
+        step t runs on the comm stream while step t+1 scores (gradients one micro-batch stale, BASELINE config 5's
+        async RCCL gradient reduce); step t's update is applied when step t+1's reduce is issued."""
         import torch
         from ...ops.ftrl import ftrl_dp_gradients, ftrl_dp_update
         w, n, z = (a if isinstance(a, torch.Tensor) else torch.from_numpy(a) for a in self._state)
@@ -301,9 +311,24 @@ class FtrlTrainStreamOp(StreamOperator):
             gq, _ = ftrl_dp_gradients(*(t.to(dev) for t in csr), w)
         else:
             gq = torch.zeros((2, self._dim), dtype=torch.float64, device=dev)
+        if self._ws > 1 and self._async_reduce:
+            prev = self._pending
+            self._pending = comm.all_reduce_async(gq.to(self._comm_dev()), "sum")
+            if prev is not None:
+                ftrl_dp_update(prev.wait().to(dev), w, n, z, self._alpha, self._beta, self._l1, self._l2)
+            return
         if self._ws > 1:
             gq = comm.all_reduce(gq.to(self._comm_dev()), "sum").to(dev)
         ftrl_dp_update(gq, w, n, z, self._alpha, self._beta, self._l1, self._l2)
+
+    def _drain(self):
+        """Apply the last in-flight asynchronous gradient reduce (before a snapshot or the end)."""
+        if getattr(self, "_pending", None) is not None:
+            import torch
+            from ...ops.ftrl import ftrl_dp_update
+            w, n, z = (a if isinstance(a, torch.Tensor) else torch.from_numpy(a) for a in self._state)
+            ftrl_dp_update(self._pending.wait().to(w.device), w, n, z, self._alpha, self._beta, self._l1, self._l2)
+            self._pending = None
 
     def _hogwild_step(self, csr):
         """HOGWILD over P ranks: every rank runs the one-wave-per-sample Hogwild kernel on its OWN micro-batch

@@ -29,7 +29,8 @@ from ..utils import trace as _trace
 __all__ = ["init_distributed", "get_rank", "get_world_size", "is_distributed", "all_reduce", "all_gather_object",
            "broadcast_object", "barrier", "all_gather_tensor", "all_to_all_objects", "reduce_scatter",
            "object_group", "device_for_rank", "CommStats", "STATS", "shutdown", "all_reduce_coalesced",
-           "Pending", "reduce_scatter_async", "all_to_all_bytes", "all_to_all_strings", "comm_stream"]
+           "Pending", "reduce_scatter_async", "all_gather_varlen_async", "all_reduce_async", "all_to_all_bytes", "all_to_all_strings",
+           "comm_stream"]
 
 _OBJ_GROUP = None
 
@@ -370,6 +371,66 @@ def reduce_scatter_async(t: torch.Tensor, op: str = "sum") -> Pending:
     r = get_rank()
     dev = t.device
     return Pending(full, work, lambda x: x[r * rows:(r + 1) * rows].clone().to(dev))
+
+
+def all_reduce_async(t: torch.Tensor, op: str = "sum") -> Pending:
+    """Asynchronous in-place ``all_reduce``: issued from the comm stream (RCCL) or gloo's thread; ``wait()``
+    returns ``t`` holding the reduction (the caller's stream waits on the collective's event)."""
+    if not is_distributed():
+        return Pending(t)
+    rop = getattr(dist.ReduceOp, _OPS[op.lower()])
+    STATS.calls += 1
+    STATS.bytes += t.numel() * t.element_size()
+    if _backend() == "nccl":
+        d = t if t.is_cuda else t.to(device_for_rank())
+
+        def issue():
+            w = dist.all_reduce(d, op=rop, async_op=True)
+            w.wait()
+        _, done = _on_comm_stream(d.device, [d], issue, wait_now=False)
+        dev = d.device
+        if t.is_cuda:
+            return Pending(t, None, lambda x: _wait_event(dev, done, x))
+        return Pending(t, None, lambda x: x.copy_(_wait_event(dev, done, d).cpu()))
+    h = t if not t.is_cuda else t.cpu()
+    work = dist.all_reduce(h, op=rop, async_op=True)
+    return Pending(t, work, (lambda x: x) if h is t else (lambda x: x.copy_(h)), keep=(h,))
+
+
+def all_gather_varlen_async(t: torch.Tensor) -> Pending:
+    """Asynchronous ``all_gather_varlen``: the (tiny) length exchange runs now, the padded payload gather is
+    issued from the comm stream (RCCL) or gloo's thread; ``wait()`` returns the rank-order concatenation."""
+    ws = get_world_size()
+    if ws == 1:
+        return Pending(t)
+    n = torch.tensor([t.shape[0]], dtype=torch.int64)
+    lens = all_gather_tensor(n).tolist()
+    mx = max(lens)
+    tail = tuple(t.shape[1:])
+    STATS.calls += 1
+    STATS.bytes += int(mx * ws * (t.element_size() * (int(np.prod(tail)) if tail else 1)))
+
+    def unpad(full):
+        return torch.cat([full[i * mx:i * mx + lens[i]] for i in range(ws)])
+    if _backend() == "nccl":
+        d = t if t.is_cuda else t.to(device_for_rank())
+        pad = torch.zeros((mx,) + tail, dtype=t.dtype, device=d.device)
+        pad[:t.shape[0]] = d
+        out = torch.empty((ws * mx,) + tail, dtype=t.dtype, device=d.device)
+
+        def issue():
+            w = dist.all_gather_into_tensor(out, pad, async_op=True)
+            w.wait()
+        _, done = _on_comm_stream(d.device, [pad, out], issue, wait_now=False)
+        dev, host = d.device, not t.is_cuda
+        return Pending(out, None, lambda x: (lambda y: y.cpu() if host else y)(unpad(_wait_event(dev, done, x))),
+                       keep=(pad,))
+    pad = torch.zeros((mx,) + tail, dtype=t.dtype)
+    pad[:t.shape[0]] = t.cpu()
+    parts = [torch.empty_like(pad) for _ in range(ws)]
+    work = dist.all_gather(parts, pad, async_op=True)
+    dev = t.device
+    return Pending(parts, work, lambda ps: unpad(torch.cat(ps)).to(dev), keep=(pad,))
 
 
 @_collective

@@ -237,7 +237,7 @@ def scenario_fm(out):
     out["acc"] = sum(int(r[-1] == r[-2]) for r in pred) / max(len(pred), 1)
 
 
-def _ftrl_run(mode, rows, batch):
+def _ftrl_run(mode, rows, batch, async_reduce=False):
     import numpy as np
     import pandas as pd
     os.environ["ALINK_STREAM_BATCH"] = str(batch)
@@ -257,6 +257,8 @@ def _ftrl_run(mode, rows, batch):
     snaps = []
     op = FtrlTrainStreamOp(model).setFeatureCols(cols).setLabelCol("label").setTimeInterval(1e9).setAlpha(0.1) \
         .setBeta(0.1).setL1(0.01).setL2(0.01).setWithIntercept(True).setUpdateMode(mode)
+    if async_reduce:
+        op.set("asyncGradReduce", True)
     op.linkFrom(stream).link(CollectStreamOp(snaps))
     StreamOperator.execute()
     last = max(r[0] for r in snaps)
@@ -286,6 +288,14 @@ def scenario_ftrl_sharded_allgather(out):
 
 def scenario_ftrl_dp(out):
     out["model"], out["bids"] = _ftrl_run("DATA_PARALLEL", 400, 4096)
+
+
+def scenario_ftrl_dp_async(out):
+    """DATA_PARALLEL with the gradient all-reduce overlapped with the next step (one-step-stale gradients)."""
+    out["model"], out["bids"] = _ftrl_run("DATA_PARALLEL", 400, 25, async_reduce=True)
+    out["sync"], _ = _ftrl_run("DATA_PARALLEL", 400, 25)
+    out["one_async"], _ = _ftrl_run("DATA_PARALLEL", 400, 4096, async_reduce=True)
+    out["one_sync"], _ = _ftrl_run("DATA_PARALLEL", 400, 4096)
 
 
 def scenario_ftrl_uneven(out):

@@ -101,7 +101,13 @@ def scenario_ftrl_sharded(out):
     _ftrl_mode(out, "SHARDED")
 
 
-def _ftrl_mode(out, mode):
+def scenario_ftrl_dp_async(out):
+    """FTRL DATA_PARALLEL with asyncGradReduce: the (sum g, sum g^2) all-reduce runs on the comm stream while the
+    next micro-batch scores."""
+    _ftrl_mode(out, "DATA_PARALLEL", async_reduce=True)
+
+
+def _ftrl_mode(out, mode, async_reduce=False):
     import numpy as np
     import pandas as pd
     from alink_amd import (useLocalEnv, BatchOperator, StreamOperator, LogisticRegressionTrainBatchOp,
@@ -119,9 +125,11 @@ def _ftrl_mode(out, mode):
     model = LogisticRegressionTrainBatchOp().setFeatureCols(cols).setLabelCol("label").setMaxIter(2) \
         .linkFrom(BatchOperator.fromDataframe(df.iloc[:50], schemaStr=schema))
     snaps = []
-    FtrlTrainStreamOp(model).setFeatureCols(cols).setLabelCol("label").setTimeInterval(1e9) \
-        .setUpdateMode(mode).setAlpha(0.1).setBeta(1.0).linkFrom(
-            StreamOperator.fromDataframe(df, schemaStr=schema)).link(CollectStreamOp(snaps))
+    op = FtrlTrainStreamOp(model).setFeatureCols(cols).setLabelCol("label").setTimeInterval(1e9) \
+        .setUpdateMode(mode).setAlpha(0.1).setBeta(1.0)
+    if async_reduce:
+        op.set("asyncGradReduce", True)
+    op.linkFrom(StreamOperator.fromDataframe(df, schemaStr=schema)).link(CollectStreamOp(snaps))
     StreamOperator.execute()
     last = max(r[0] for r in snaps)
     coef = [r for r in snaps if r[0] == last and r[2] == 1048576][0][3]

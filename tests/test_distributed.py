@@ -246,6 +246,25 @@ def test_ftrl_data_parallel_equal_single(tmp_path, world):
                                        np.asarray(jb.get("coefVector", {}).get("data", [])), rtol=1e-10, atol=1e-12)
 
 
+def _coefs(model):
+    for r in model:
+        if r[1] and "coefVector" in r[1]:
+            return np.asarray(json.loads(r[1])["coefVector"]["data"])
+    raise AssertionError("no coefficient row in the model")
+
+
+def test_ftrl_data_parallel_async_grad_reduce(tmp_path):
+    """asyncGradReduce: ranks stay identical; one global step equals the synchronous mode; many steps stay close
+    to it (gradients one step stale)."""
+    outs = _run("ftrl_dp_async", 2, tmp_path)
+    assert outs[0]["model"] == outs[1]["model"]
+    np.testing.assert_allclose(_coefs(outs[0]["one_async"]), _coefs(outs[0]["one_sync"]), rtol=1e-12, atol=1e-14)
+    a, s = _coefs(outs[0]["model"]), _coefs(outs[0]["sync"])
+    assert np.all(np.isfinite(a))
+    assert np.corrcoef(a, s)[0, 1] > 0.95
+    assert not np.allclose(a, s, rtol=1e-9, atol=1e-12)          # the overlap really changed the schedule
+
+
 def test_ftrl_uneven_micro_batches_lockstep(tmp_path):
     """Rank 0 has 3 micro-batches, rank 1 has 2: the finished rank joins steps with an empty batch (no hang)."""
     one = _run("ftrl_uneven", 1, tmp_path)[0]

@@ -111,6 +111,15 @@ def test_ftrl_sharded_multiprocess_gpu(tmp_path):
     assert one["acc"] > 0.85 and two[0]["acc"] > one["acc"] - 0.03
 
 
+def test_ftrl_dp_async_multiprocess_gpu(tmp_path):
+    """DATA_PARALLEL FTRL with the gradient all-reduce overlapped on the RCCL comm stream (asyncGradReduce):
+    replicated model identical on both ranks, learns as well as 1 rank."""
+    one = _run("ftrl_dp_async", 1, tmp_path)[0]
+    two = _run("ftrl_dp_async", 2, tmp_path)
+    assert two[0]["coef"] == two[1]["coef"]
+    assert one["acc"] > 0.85 and two[0]["acc"] > one["acc"] - 0.03
+
+
 def test_ring_topk_multiprocess_gpu(tmp_path):
     """Ring blockwise top-K with device blocks over 2 ranks == torch.topk of the full score matrix."""
     for o in _run("cross_gpu", 2, tmp_path):
