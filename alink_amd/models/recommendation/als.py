@@ -179,6 +179,9 @@ def _solve(side: _Side, mask: torch.Tensor, Y: torch.Tensor, X: torch.Tensor, la
     return rows, x
 
 
+ITER_SECONDS: List[float] = []     # wall time of each iteration of the last train_als (ALINK_ALS_TIME_ITERS=1)
+
+
 def train_als(mt: MTable, params: Params, env) -> AlsModelData:
     t_start = time.perf_counter()
     dev = env.device
@@ -237,13 +240,23 @@ def train_als(mt: MTable, params: Params, env) -> AlsModelData:
     U = torch.rand((users.numel(), rank), generator=gen, dtype=torch.float32, device=dev)
     V = torch.rand((items.numel(), rank), generator=gen, dtype=torch.float32, device=dev)
     mark("init factors")
+    timed = os.environ.get("ALINK_ALS_TIME_ITERS") == "1"
+    ITER_SECONDS.clear()
     for _ in range(num_iter):
+        if timed:
+            if dev.type == "cuda":
+                torch.cuda.synchronize(dev)
+            t_it = time.perf_counter()
         for name, (side, Y, X) in (("users", (by_user, V, U)), ("items", (by_item, U, V))):
             YtY = tn_matmul(Y.to(torch.float64), Y.to(torch.float64)) if implicit else None
             for bb in range(nblocks):
                 mask = (side.raw.abs() % nblocks) == bb
                 _update(side, mask, Y, X, lam, implicit, alpha, nonneg, YtY)
             mark(f"update {name}")
+        if timed:
+            if dev.type == "cuda":
+                torch.cuda.synchronize(dev)
+            ITER_SECONDS.append(time.perf_counter() - t_it)
     return AlsModelData(users.cpu().numpy(), U.cpu().numpy(), items.cpu().numpy(), V.cpu().numpy())
 
 

@@ -119,6 +119,11 @@ HEAVY_CHUNK = 4096
 # rank 33..64: heavy rows' partial Grams on the matrix cores (als_heavy_gram_mfma: exact bf16 x3 split, fp64
 # folding per 32 neighbours); 0 keeps the fp64 VALU kernel
 HEAVY_MFMA = int(__import__("os").environ.get("ALINK_ALS_HEAVY_MFMA", "1"))
+# explicit rows with <= 8 / 16 / 32 neighbours (below the padded rank): m x m push-through solve
+# (alink_als_woodbury_solve) instead of the r x r system; 0 disables
+WOODBURY = int(__import__("os").environ.get("ALINK_ALS_WOODBURY", "1"))
+WOODBURY_BUCKETS = tuple(int(x) for x in __import__("os").environ.get("ALINK_ALS_WOODBURY_BUCKETS", "8,16,32")
+                         .split(","))
 
 
 def fused_supported(Y: torch.Tensor) -> bool:
@@ -147,7 +152,25 @@ def fused_solve(indptr: torch.Tensor, nbr: torch.Tensor, rating: torch.Tensor, Y
     st = _lib.stream_ptr(dev)
     deg = indptr[1:] - indptr[:-1]
     heavy = torch.nonzero(deg > HEAVY_DEGREE, as_tuple=False).reshape(-1)
-    light = torch.nonzero(deg <= HEAVY_DEGREE, as_tuple=False).reshape(-1) if heavy.numel() else None
+    RP = int(L.alink_als_padded_rank(r))
+    buckets = [P for P in WOODBURY_BUCKETS if WOODBURY and not implicit and yty is None and P < RP]
+    small = torch.zeros_like(deg, dtype=torch.bool)
+    lo = -1
+    for P in buckets:
+        sel = (deg > lo) & (deg <= P)
+        small |= sel
+        ids = torch.nonzero(sel, as_tuple=False).reshape(-1)
+        lo = P
+        if ids.numel():
+            rc = L.alink_als_woodbury_solve(indptr.data_ptr(), nbr.data_ptr(), rating.data_ptr(), Yf.data_ptr(),
+                                            ids.numel(), r, regd.data_ptr(), ids.data_ptr(), P, X.data_ptr(),
+                                            status.data_ptr(), st)
+            if rc != 0:
+                raise RuntimeError(f"alink_als_woodbury_solve failed: {rc}")
+    if heavy.numel() or buckets:
+        light = torch.nonzero((deg <= HEAVY_DEGREE) & ~small, as_tuple=False).reshape(-1)
+    else:
+        light = None
     nl = m if light is None else light.numel()
     if nl:
         rc = L.alink_als_fused_solve(indptr.data_ptr(), nbr.data_ptr(), rating.data_ptr(), Yf.data_ptr(), nl, r,
@@ -159,7 +182,6 @@ def fused_solve(indptr: torch.Tensor, nbr: torch.Tensor, rating: torch.Tensor, Y
     if heavy.numel():
         # popular items: the neighbour list is split into HEAVY_CHUNK pieces, one wave each (partial Grams
         # summed in fp64), then one wave per row solves
-        RP = int(L.alink_als_padded_rank(r))
         hd = deg[heavy]
         nck = (hd + HEAVY_CHUNK - 1) // HEAVY_CHUNK
         chunk_row = torch.repeat_interleave(torch.arange(heavy.numel(), device=dev), nck)
@@ -187,5 +209,8 @@ def fused_solve(indptr: torch.Tensor, nbr: torch.Tensor, rating: torch.Tensor, Y
         if yty is not None:
             A = A + yty[None]
         A = A + regd[bad][:, None, None] * torch.eye(r, dtype=A.dtype, device=dev)[None]
-        X[bad] = (torch.linalg.pinv(A) @ b[:, :, None])[:, :, 0].to(torch.float32)
+        # symmetric pinv (eigh) on the host: rocSOLVER's batched SVD does not converge on rank-deficient systems,
+        # and these rows are rare
+        Ah = torch.linalg.pinv(A.cpu(), hermitian=True)
+        X[bad] = (Ah @ b.cpu()[:, :, None])[:, :, 0].to(device=dev, dtype=torch.float32)
     return X

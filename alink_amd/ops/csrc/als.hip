@@ -219,7 +219,7 @@ __device__ __forceinline__ void add_reg(double (&a)[RP], int lane, int r, double
 //   the row for the host pinv fallback.
 // ---------------------------------------------------------------------------------------------------------------
 constexpr int GJ_WAVES = 4;
-constexpr int GJ_NB = 2;     // LDS rows per wave (neighbour staging double buffer; the GJ pivot row uses row 0)
+constexpr int GJ_NB = 16;    // LDS rows per wave (neighbour staging, two batches of 8; the GJ pivot rows use 0-1)
 
 template <int RP>
 __device__ __forceinline__ void lds_wave_sync() {
@@ -266,31 +266,56 @@ __device__ __forceinline__ void axpy_bcast(double (&a)[RP], double coef, const d
   }
 }
 
-// Gram of neighbours [s, e) for one row, lane i = row i (a[j] += c y_i y_j, v += w y_i): neighbour t's factor row
-// (one coalesced fp32 load, prefetched one neighbour ahead) is staged as fp64 in one of two LDS rows and read
-// back as broadcast pairs
+// Gram of neighbours [s, e) for one row, lane i = row i (a[j] += c y_i y_j, v += w y_i): neighbours are gathered
+// GB_ROWS at a time (one coalesced fp32 row load per lane each, the next batch's loads issued before this batch's
+// FMAs, so a wave keeps GB_ROWS rows in flight instead of one), staged as fp64 in one of two LDS batches and read
+// back as broadcast pairs.  Branch-free: past-the-end neighbours load a valid row and get weight 0 (a guarded load
+// or a guarded axpy makes the compiler copy the whole register row at every join).
+constexpr int GB_ROWS = 8;
+
 template <int RP>
 __device__ __forceinline__ void gram_lds(const int32_t* __restrict__ nbr, const float* __restrict__ rating,
                                          const float* __restrict__ Y, int r, int implicit, float alpha, int64_t s,
                                          int64_t e, int lane, double (&a)[RP], double& v, double* buf) {
-  float ynext = (s < e && lane < r) ? Y[(int64_t)nbr[s] * r + lane] : 0.f;
-  for (int64_t t = s; t < e; ++t) {
-    const float yf = ynext;
-    if (t + 1 < e) ynext = lane < r ? Y[(int64_t)nbr[t + 1] * r + lane] : 0.f;
-    double* row = buf + (int)(t & 1) * 64;
-    row[lane] = (double)yf;
-    lds_wave_sync<RP>();
-    const float rt = rating[t];
-    double c, w;
-    if (implicit) {
-      c = rt > 0.f ? (double)alpha * rt : 0.0;
-      w = rt > 0.f ? 1.0 + c : 0.0;
-    } else {
-      c = 1.0;
-      w = rt;
+  if (s >= e) return;
+  const int col = lane < r ? lane : r - 1;
+  float yn[GB_ROWS];
+#pragma unroll
+  for (int u = 0; u < GB_ROWS; ++u) {
+    const int64_t t = s + u < e ? s + u : e - 1;
+    yn[u] = Y[(int64_t)nbr[t] * r + col];
+  }
+  int nb = 0;
+  for (int64_t t0 = s; t0 < e; t0 += GB_ROWS, ++nb) {
+    float yc[GB_ROWS];
+#pragma unroll
+    for (int u = 0; u < GB_ROWS; ++u) yc[u] = lane < r ? yn[u] : 0.f;
+#pragma unroll
+    for (int u = 0; u < GB_ROWS; ++u) {   // next batch (clamped: the last batch reloads row e - 1)
+      const int64_t t = t0 + GB_ROWS + u < e ? t0 + GB_ROWS + u : e - 1;
+      yn[u] = Y[(int64_t)nbr[t] * r + col];
     }
-    axpy_bcast<RP>(a, c * (double)yf, row, 0);
-    v = fma(w, (double)yf, v);
+    double* rows = buf + (nb & 1) * (GB_ROWS * 64);
+#pragma unroll
+    for (int u = 0; u < GB_ROWS; ++u) rows[u * 64 + lane] = (double)yc[u];
+    lds_wave_sync<RP>();
+#pragma unroll
+    for (int u = 0; u < GB_ROWS; ++u) {
+      const bool live = t0 + u < e;
+      const float rt = rating[live ? t0 + u : e - 1];
+      double c, w;
+      if (implicit) {
+        c = rt > 0.f ? (double)alpha * rt : 0.0;
+        w = rt > 0.f ? 1.0 + c : 0.0;
+      } else {
+        c = 1.0;
+        w = rt;
+      }
+      c = live ? c : 0.0;
+      w = live ? w : 0.0;
+      axpy_bcast<RP>(a, c * (double)yc[u], rows + u * 64, 0);
+      v = fma(w, (double)yc[u], v);
+    }
   }
   lds_wave_sync<RP>();
 }
@@ -359,7 +384,7 @@ __global__ __launch_bounds__(64 * GJ_WAVES) void als_fused_solve(const int64_t* 
                                                                  float* __restrict__ X, int32_t* __restrict__ status) {
   // every lane writes its own entry (64 per row, whatever RP is): rows of 64 doubles
   __shared__ __attribute__((aligned(16))) double lbuf[GJ_WAVES][GJ_NB * 64];
-  const int w = threadIdx.x >> 6;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform row bounds -> scalar loads
   const int lane = threadIdx.x & 63;
   const int64_t idx = (int64_t)blockIdx.x * GJ_WAVES + w;
   if (idx >= nrows) return;              // whole wave: no block-wide barrier below
@@ -374,6 +399,98 @@ __global__ __launch_bounds__(64 * GJ_WAVES) void als_fused_solve(const int64_t* 
   const int bad = gj_solve<RP>(a, v, lane, buf);
   if (lane < r) X[row * r + lane] = (float)v;
   if (lane == 0) status[row] = bad;
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// Explicit-feedback rows with few neighbours (m <= P < RP): the push-through identity
+//     (Y_u^T Y_u + reg I_r)^{-1} Y_u^T r_u  =  Y_u^T (Y_u Y_u^T + reg I_m)^{-1} r_u
+// turns the r x r system into an m x m one (padded to P with an identity block).  A user with 10 ratings at rank
+// 64 solves 16 Gauss-Jordan steps over 16 columns instead of 64 over 64 (the r x r path is LDS-broadcast bound,
+// see profiles/als_r3.txt).  One wave per row, lane = (i, q): row i = lane % P of the small system, k-chunk
+// q = lane / P of the rank for the Gram; the Q = 64 / P partial dot products are summed with xor shuffles, then
+// the same Gauss-Jordan as the r x r path (gj_solve<P>), then x = Y_u^T a with lane = rank entry.  fp64 throughout;
+// the reference solves the r x r normal equations (NormalEquation.java:44-92) — the solutions agree to fp64
+// rounding.  m > P flags the row for the host fallback.
+// ---------------------------------------------------------------------------------------------------------------
+constexpr int WB_WAVES = 4;
+constexpr int WB_LD = 66;    // LDS row stride (doubles) of the staged factors
+
+template <int P>
+__global__ __launch_bounds__(64 * WB_WAVES) void als_woodbury_solve(const int64_t* __restrict__ indptr,
+                                                                    const int32_t* __restrict__ nbr,
+                                                                    const float* __restrict__ rating,
+                                                                    const float* __restrict__ Y, int r,
+                                                                    const double* __restrict__ reg,
+                                                                    const int64_t* __restrict__ rows, int64_t nrows,
+                                                                    float* __restrict__ X,
+                                                                    int32_t* __restrict__ status) {
+  constexpr int Q = 64 / P;
+  constexpr int KC = 64 / Q;
+  __shared__ __attribute__((aligned(16))) double ybuf[WB_WAVES][P * WB_LD];
+  __shared__ __attribute__((aligned(16))) double gbuf[WB_WAVES][2 * 64];
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: every branch on m is scalar
+  const int lane = threadIdx.x & 63;
+  const int64_t idx = (int64_t)blockIdx.x * WB_WAVES + w;
+  if (idx >= nrows) return;              // whole wave: no block-wide barrier below
+  const int64_t row = rows[idx];
+  const int64_t s = indptr[row];
+  const int64_t deg = indptr[row + 1] - s;
+  const int m = __builtin_amdgcn_readfirstlane(deg > P ? 0 : (int)deg);
+  double* yb = ybuf[w];
+  // stage Y_u (fp32 -> fp64), rows t >= m zero; all P loads issued before the stores
+  const int nb = lane < m ? nbr[s + lane] : 0;
+  float yv[P];
+#pragma unroll
+  for (int t = 0; t < P; ++t) {
+    // branch-free and traffic-free padding: a buffer resource over row it with 0 records for t >= m (and lanes
+    // >= r past the record end) returns 0 without touching memory (a guarded load would make the compiler copy
+    // arrays at every join; a clamped one would fetch P - m dead rows)
+    const int it = __builtin_amdgcn_readlane(nb, t);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(Y + (int64_t)it * r), (short)0, t < m ? r * 4 : 0, 0x00020000);
+    yv[t] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, lane * 4, 0, 0));
+  }
+#pragma unroll
+  for (int t = 0; t < P; ++t) yb[t * WB_LD + lane] = (double)yv[t];
+  lds_wave_sync<P>();
+  // Gram K = Y_u Y_u^T: lane (i, q) sums entries [q KC, (q + 1) KC) of y_i . y_j, then xor-reduce over q
+  const int i = lane % P;
+  const int q = lane / P;
+  double yi[KC];
+#pragma unroll
+  for (int k = 0; k < KC; k += 2) {
+    const double2 t2 = *reinterpret_cast<const double2*>(yb + i * WB_LD + q * KC + k);
+    yi[k] = t2.x;
+    yi[k + 1] = t2.y;
+  }
+  double a[P];
+  const double dg = i < m ? reg[row] : 1.0;       // padded rows: identity
+#pragma unroll
+  for (int j = 0; j < P; ++j) {
+    double acc = 0.0;
+    if (j < m) {                         // wave-uniform; only acc is live across the branch
+      double c0 = 0.0, c1 = 0.0;
+#pragma unroll
+      for (int k = 0; k < KC; k += 2) {
+        const double2 yj = *reinterpret_cast<const double2*>(yb + j * WB_LD + q * KC + k);
+        c0 = fma(yi[k], yj.x, c0);
+        c1 = fma(yi[k + 1], yj.y, c1);
+      }
+      acc = c0 + c1;
+#pragma unroll
+      for (int o = P; o < 64; o <<= 1) acc += __shfl_xor(acc, o);
+    }
+    a[j] = acc + (j == i ? dg : 0.0);
+    __builtin_amdgcn_sched_barrier(0);   // one column at a time (unfenced, every column's reads get hoisted)
+  }
+  double v = i < m ? (double)rating[s + i] : 0.0;
+  const int bad = gj_solve<P>(a, v, lane, gbuf[w]);
+  // x = Y_u^T a, lane = rank entry
+  double x = 0.0;
+#pragma unroll
+  for (int t = 0; t < P; ++t) x = fma(readlane_f64(v, t), yb[t * WB_LD + lane], x);   // rows t >= m are 0
+  if (lane < r) X[row * r + lane] = (float)x;
+  if (lane == 0) status[row] = bad | (deg > P);
 }
 
 // heavy rows, pass 1: one wave per (row, chunk of `chunk` neighbours) adds its partial Gram / rhs into fp64
@@ -615,6 +732,27 @@ int alink_als_heavy_solve(const int64_t* indptr, const int32_t* nbr, const float
                        status);
   } else { ALS_HEAVY(64); }
 #undef ALS_HEAVY
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+// Explicit rows with at most P (8, 16 or 32) neighbours, P < padded rank: the m x m push-through solve above.
+int alink_als_woodbury_solve(const int64_t* indptr, const int32_t* nbr, const float* rating, const float* Y,
+                             int64_t nrows, int r, const double* reg, const int64_t* rows, int P, float* X,
+                             int32_t* status, hipStream_t stream) {
+  if (nrows <= 0) return 0;
+  if (r <= 0 || r > 64 || rows == nullptr) return 1;
+  const dim3 grid((unsigned)((nrows + WB_WAVES - 1) / WB_WAVES)), block(64 * WB_WAVES);
+  if (P == 8)
+    hipLaunchKernelGGL(als_woodbury_solve<8>, grid, block, 0, stream, indptr, nbr, rating, Y, r, reg, rows, nrows,
+                       X, status);
+  else if (P == 16)
+    hipLaunchKernelGGL(als_woodbury_solve<16>, grid, block, 0, stream, indptr, nbr, rating, Y, r, reg, rows, nrows,
+                       X, status);
+  else if (P == 32)
+    hipLaunchKernelGGL(als_woodbury_solve<32>, grid, block, 0, stream, indptr, nbr, rating, Y, r, reg, rows, nrows,
+                       X, status);
+  else
+    return 1;
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 

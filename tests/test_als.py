@@ -215,3 +215,35 @@ def test_hip_als_heavy_mfma_gram_matches_valu(implicit, monkeypatch):
     monkeypatch.setattr(aops, "HEAVY_MFMA", 0)
     b = aops.fused_solve(*args).cpu().double().numpy()
     np.testing.assert_allclose(a, b, rtol=2e-5, atol=2e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("r", [24, 40, 64])
+def test_hip_als_woodbury_small_rows_match_rxr(r, monkeypatch):
+    """Explicit rows with <= 32 neighbours take the m x m push-through solve; it equals the r x r fused solve and
+    fp64 Cholesky (rows with 0, 1, 16, 17, 32 and 33 neighbours, repeated neighbours, and lambda = 0 rows that
+    fall back to pinv: the minimum-norm solution either way)."""
+    rng = np.random.default_rng(7 + r)
+    n = 900
+    counts = np.concatenate([[0, 1, 16, 17, 32, 33, 2, 5], rng.integers(0, 40, size=3000)])
+    m = counts.size
+    indptr = torch.zeros(m + 1, dtype=torch.int64)
+    indptr[1:] = torch.as_tensor(np.cumsum(counts))
+    nnz = int(indptr[-1])
+    nbr = rng.integers(0, n, size=nnz)
+    nbr[int(indptr[6]):int(indptr[7])] = nbr[int(indptr[6])]          # the 2-neighbour row repeats one item
+    nbr = torch.as_tensor(nbr, dtype=torch.int32)
+    rt = torch.as_tensor(rng.integers(1, 6, size=nnz).astype(np.float32))
+    Y = torch.as_tensor(rng.normal(size=(n, r)) * 0.3, dtype=torch.float32)
+    reg = torch.as_tensor(counts * 0.05, dtype=torch.float64)
+    reg[7] = 0.0                                                        # 5 neighbours, no regulariser
+    args = (indptr.cuda(), nbr.cuda(), rt.cuda(), Y.cuda(), reg.cuda(), False, 0.0, None)
+    monkeypatch.setattr(aops, "WOODBURY", 1)
+    a = aops.fused_solve(*args).cpu().double().numpy()
+    monkeypatch.setattr(aops, "WOODBURY", 0)
+    b = aops.fused_solve(*args).cpu().double().numpy()
+    np.testing.assert_allclose(a, b, rtol=2e-5, atol=2e-6)
+    A, bb = aops.normal_equations_torch(indptr, nbr, rt, Y, False, 0.0)
+    A = A + reg[:, None, None] * torch.eye(r, dtype=torch.float64)[None]
+    ref = (torch.linalg.pinv(A) @ bb[:, :, None])[:, :, 0].numpy()
+    np.testing.assert_allclose(a, ref, rtol=2e-4, atol=2e-5)
