@@ -518,11 +518,11 @@ def broadcast_object(obj: Any, src: int = 0) -> Any:
     return box[0]
 
 
-@_collective
 def _is_str_list(x) -> bool:
     return isinstance(x, list) and all(v is None or isinstance(v, str) for v in x)
 
 
+@_collective
 def all_to_all_bytes(send: List[bytes]) -> List[bytes]:
     """Byte-string all-to-all: ``send[j]`` -> rank j, as one lengths + one packed uint8 ``all_to_all_single``
     (RCCL / gloo) — O(N) bytes in total, no gather of every rank's data on every rank."""
