@@ -128,8 +128,12 @@ def _sgd(inp, out, C, P, lens, cen, ctx, alpha, batch):
         q = torch.floor((f.clamp(-6.0, 6.0 - 1e-9) + 6.0) * 84.0) / 84.0 - 6.0   # sigmoid-table abscissa
         g = (1.0 - code - torch.sigmoid(q)) * alpha * valid
         neu1e = (g[..., None] * o).sum(1)
-        out.index_add_(0, nodes.reshape(-1), (g[..., None] * h[:, None, :]).reshape(-1, h.shape[1]))
-        inp.index_add_(0, x, neu1e)
+        # every pair of a batch reads the same stale vectors, so a word occurring m times would take m
+        # uncorrected steps at once (hot words of a Zipf corpus diverge); it takes their mean instead
+        cn = torch.bincount(nodes[mask], minlength=out.shape[0]).clamp(min=1).to(g.dtype)
+        cx = torch.bincount(x, minlength=inp.shape[0]).to(g.dtype)
+        out.index_add_(0, nodes.reshape(-1), ((g / cn[nodes])[..., None] * h[:, None, :]).reshape(-1, h.shape[1]))
+        inp.index_add_(0, x, neu1e / cx[x][:, None])
 
 
 def train_word2vec(mt: MTable, params: Params, env) -> List[tuple]:

@@ -47,7 +47,7 @@ def _load():
     # time from HIP events on the caller's stream); one flag check per call otherwise
     from ..utils import trace
     for name in ["alink_kmeans_reduce_slabs", "alink_kmeans_prep_centroids"] + list(_EXTRA_SIGNATURES):
-        if hasattr(L, name) and not name.endswith(("_grid", "_pad", "_padded_rank", "_kmax")):
+        if hasattr(L, name) and not name.endswith(("_grid", "_pad", "_padded_rank", "_kmax", "_alloc", "_free")):
             setattr(L, name, trace.traced_call(getattr(L, name), name[len("alink_"):]))
     _lib = L
     return _lib
@@ -76,7 +76,9 @@ _EXTRA_SIGNATURES = {
     "alink_linear_grad_pad": [_c_int],
     "alink_linear_search_f64": [_c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_int, _c_int, _c_d, _c_d, _c_int, _c_vp,
                                 _c_int, _c_vp, _c_vp],
-    "alink_kmeans_update": [_c_vp, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_int, _c_vp],
+    "alink_kmeans_update": [_c_vp, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_int, _c_vp, _c_vp],
+    "alink_kmeans_host_stat_alloc": [ctypes.POINTER(_c_vp), ctypes.POINTER(_c_vp)],
+    "alink_kmeans_host_stat_free": [_c_vp],
     "alink_kmeans_accum_bf16": [_c_vp, _c_i64, _c_int, _c_vp, _c_vp, _c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp],
     "alink_kmeans_accum_kmax": [_c_int],
     "alink_kmeans_accum_mfma_bf16": [_c_vp, _c_i64, _c_vp, _c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp],

@@ -12,6 +12,7 @@
 // profiles/kmeans_v7_v8_pmc.txt; only v7 ships.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <cstring>
 
 namespace {
 
@@ -88,7 +89,8 @@ __global__ __launch_bounds__(128) void kmeans_update_kernel(const double* __rest
                                                             const double* __restrict__ prev,
                                                             double* __restrict__ C, __bf16* __restrict__ cpad,
                                                             float* __restrict__ ninit,
-                                                            unsigned long long* __restrict__ stat, int hyst) {
+                                                            unsigned long long* __restrict__ stat, int hyst,
+                                                            unsigned long long* __restrict__ host_out) {
     __shared__ float red[128];
     __shared__ double redd[128];
     const int c = blockIdx.x, d = threadIdx.x;
@@ -140,6 +142,22 @@ __global__ __launch_bounds__(128) void kmeans_update_kernel(const double* __rest
             atomicMax(stat, (unsigned long long)__double_as_longlong(sh));
             if (empty) atomicMax(stat + 1, 1ull);
         }
+        if (host_out != nullptr) {
+            // last block to finish publishes the two stats straight into mapped host memory and re-arms the
+            // device words (stat[2] = ticket) for the next launch: no memset before and no copy after the kernel
+            __threadfence();
+            const unsigned long long t = atomicAdd(stat + 2, 1ull);
+            if (t == (unsigned long long)gridDim.x - 1) {
+                __threadfence();
+                const unsigned long long s0 = atomicAdd(stat, 0ull), s1 = atomicAdd(stat + 1, 0ull);
+                __hip_atomic_store(host_out, s0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(host_out + 1, s1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __threadfence_system();
+                atomicExch(stat, 0ull);
+                atomicExch(stat + 1, 0ull);
+                atomicExch(stat + 2, 0ull);
+            }
+        }
     }
 }
 
@@ -148,18 +166,32 @@ __global__ __launch_bounds__(128) void kmeans_update_kernel(const double* __rest
 extern "C" {
 
 // buf [k][D+1] (sums | count), prev [k][D] (nullable), C out [k][D], cpad [128][D] bf16, ninit [128],
-// stat [2] u64 (zeroed here): max shift (double bits), any-empty flag
+// stat [3] u64 device words: max shift (double bits), any-empty flag, completion ticket.
+// host_out == nullptr: stat[0..1] are zeroed here (memset) and hold the result after the kernel.
+// host_out != nullptr (device address of mapped host memory, alink_kmeans_host_stat_alloc): stat must be all-zero
+// before the FIRST launch; the kernel's last block writes host_out[0..1] and re-zeroes stat itself.
 // hyst != 0: bf16 operand hysteresis (keep cpad[c][d] while |C[c][d] - cpad[c][d]| < one bf16 ulp of max_d |C[c][d]|;
 // cpad should hold the operands of the step just run, but any contents are safe: a kept value is that close to C)
 int alink_kmeans_update(const double* buf, int k, const double* prev, double* C, void* cpad, float* ninit,
-                        unsigned long long* stat, int hyst, void* stream) {
+                        unsigned long long* stat, int hyst, unsigned long long* host_out, void* stream) {
     if (k < 1 || k > 128) return -1;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    if (hipMemsetAsync(stat, 0, 2 * sizeof(unsigned long long), st) != hipSuccess) return -2;
+    if (host_out == nullptr && hipMemsetAsync(stat, 0, 2 * sizeof(unsigned long long), st) != hipSuccess) return -2;
     hipLaunchKernelGGL(kmeans_update_kernel, dim3(128), dim3(128), 0, st, buf, k, prev, C, (__bf16*)cpad, ninit,
-                       stat, hyst);
+                       stat, hyst, host_out);
     return (int)hipGetLastError();
 }
+
+// 32 bytes of mapped, coherent pinned host memory for the update's stats: *host = host address, *dev = the
+// address kernels write through.
+int alink_kmeans_host_stat_alloc(void** host, void** dev) {
+    hipError_t e = hipHostMalloc(host, 32, hipHostMallocMapped);
+    if (e != hipSuccess) return (int)e;
+    memset(*host, 0, 32);
+    return (int)hipHostGetDevicePointer(dev, *host, 0);
+}
+
+int alink_kmeans_host_stat_free(void* host) { return (int)hipHostFree(host); }
 
 int alink_kmeans_reduce_slabs(const float* slab, const float* slab_cnt, int nslab, int k, double* out,
                               void* stream) {

@@ -172,6 +172,39 @@ def assign_accumulate_hip(X: torch.Tensor, C: torch.Tensor, grid: Optional[int] 
 _STAT = {}
 
 
+class _HostStat:
+    """Per-device result words of the fused update: ``stat`` (3 device u64: max-shift bits, empty flag, the
+    kernel's completion ticket; all-zero between launches) and 16 bytes of mapped pinned host memory that the
+    kernel's last block writes directly, so a superstep needs neither a memset before the update nor a
+    device->host copy after it.  If mapped host memory cannot be had, the update falls back to memset + copy."""
+
+    def __init__(self, L, dev):
+        import ctypes
+        self.stat = torch.zeros(3, dtype=torch.int64, device=dev)
+        self.host, self.dev_ptr, self._view = None, None, None
+        h, d = ctypes.c_void_p(), ctypes.c_void_p()
+        if os.environ.get("ALINK_KMEANS_HOST_STAT", "1") != "0" and \
+                L.alink_kmeans_host_stat_alloc(ctypes.byref(h), ctypes.byref(d)) == 0 and d.value:
+            self._hptr, self.dev_ptr = h.value, d.value
+            self._view = np.ctypeslib.as_array((ctypes.c_uint64 * 2).from_address(h.value))
+            self._L = L
+        else:
+            self.host = torch.empty(2, dtype=torch.int64, pin_memory=True)
+
+    def values(self):
+        if self._view is not None:
+            return int(self._view[0]), int(self._view[1])
+        return int(self.host[0]), int(self.host[1])
+
+    def __del__(self):
+        try:
+            if self._view is not None:
+                self._view = None
+                self._L.alink_kmeans_host_stat_free(self._hptr)
+        except Exception:
+            pass
+
+
 def update_supported(buf: torch.Tensor) -> bool:
     return buf.is_cuda and buf.dtype == torch.float64 and buf.dim() == 2 and buf.shape[1] == HIP_D + 1 and \
         1 <= buf.shape[0] <= HIP_KMAX and buf.is_contiguous()
@@ -196,9 +229,9 @@ def update_centroids_hip(buf: torch.Tensor, prev: Optional[torch.Tensor], deferr
         _PREP[dev.index] = (torch.empty((HIP_KMAX, HIP_D), dtype=torch.bfloat16, device=dev),
                             torch.empty((HIP_KMAX,), dtype=torch.float32, device=dev))
     if dev.index not in _STAT:
-        _STAT[dev.index] = (torch.empty(2, dtype=torch.int64, device=dev),
-                            torch.empty(2, dtype=torch.int64, pin_memory=True))
-    stat, host = _STAT[dev.index]
+        _STAT[dev.index] = _HostStat(L, dev)
+    hs = _STAT[dev.index]
+    stat = hs.stat
     cpad, ninit = _PREP[dev.index]
     use_prev = prev is not None and prev.is_cuda and prev.dtype == torch.float64 and tuple(prev.shape) == (k, HIP_D)
     pv = prev.contiguous() if use_prev else None
@@ -207,10 +240,11 @@ def update_centroids_hip(buf: torch.Tensor, prev: Optional[torch.Tensor], deferr
         hysteresis = operand_hysteresis()
     rc = L.alink_kmeans_update(buf.data_ptr(), k, None if pv is None else pv.data_ptr(), C.data_ptr(),
                                cpad.data_ptr(), ninit.data_ptr(), stat.data_ptr(), int(bool(hysteresis)),
-                               _lib.stream_ptr(dev))
+                               hs.dev_ptr, _lib.stream_ptr(dev))
     if rc != 0:
         raise RuntimeError(f"alink_kmeans_update failed: {rc}")
-    host.copy_(stat, non_blocking=True)
+    if hs.dev_ptr is None:
+        hs.host.copy_(stat[:2], non_blocking=True)
     ev = torch.cuda.Event()
     ev.record(torch.cuda.current_stream(dev))
     _PREPARED[dev.index] = _ckey(C)
@@ -219,7 +253,7 @@ def update_centroids_hip(buf: torch.Tensor, prev: Optional[torch.Tensor], deferr
         """Wait for THIS update's 16-byte stats only (work queued after it, e.g. a speculative next-step
         kernel, keeps running) and return (max_shift or None, any_empty)."""
         ev.synchronize()
-        shift_bits, empty = int(host[0]), int(host[1])
+        shift_bits, empty = hs.values()
         shift = float(np.frombuffer(np.int64(shift_bits).tobytes(), dtype=np.float64)[0]) if use_prev else None
         return shift, bool(empty)
     if deferred:
