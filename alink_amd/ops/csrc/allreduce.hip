@@ -32,7 +32,36 @@ __device__ __forceinline__ T combine(T a, T b) {
     return b < a || b != b ? b : a;
 }
 
-template <typename T, int OP>
+// sum slice [lo, hi) of the P staging slots in rank order.  PP > 0: P is a compile-time constant, so the P remote
+// loads of an element are all in flight before the first add (one xGMI round trip per element instead of P);
+// PP == 0: runtime P (P > 8).
+template <typename T, int OP, int PP>
+__device__ __forceinline__ void sum_slots(char* const* __restrict__ peer_data, int P, int64_t slot_off, int64_t lo,
+                                          int64_t hi, bool bad, T* __restrict__ out) {
+    const int tid = threadIdx.x;
+    if constexpr (PP > 0) {
+        const T* src[PP];
+#pragma unroll
+        for (int p = 0; p < PP; ++p) src[p] = reinterpret_cast<const T*>(peer_data[p] + slot_off);
+        for (int64_t i = lo + tid; i < hi; i += TB) {
+            T v[PP];
+#pragma unroll
+            for (int p = 0; p < PP; ++p) v[p] = src[p][i];
+            T acc = v[0];
+#pragma unroll
+            for (int p = 1; p < PP; ++p) acc = combine<T, OP>(acc, v[p]);
+            out[i] = bad ? (T)__builtin_nan("") : acc;
+        }
+    } else {
+        for (int64_t i = lo + tid; i < hi; i += TB) {
+            T acc = reinterpret_cast<const T*>(peer_data[0] + slot_off)[i];
+            for (int p = 1; p < P; ++p) acc = combine<T, OP>(acc, reinterpret_cast<const T*>(peer_data[p] + slot_off)[i]);
+            out[i] = bad ? (T)__builtin_nan("") : acc;
+        }
+    }
+}
+
+template <typename T, int OP, int PP>
 __global__ __launch_bounds__(TB) void oneshot_kernel(const T* __restrict__ in, T* __restrict__ out, int64_t n,
                                                      int P, int rank, uint32_t seq, char* const* __restrict__ peer_data,
                                                      uint32_t* const* __restrict__ peer_flags, int64_t slot_bytes,
@@ -68,11 +97,30 @@ __global__ __launch_bounds__(TB) void oneshot_kernel(const T* __restrict__ in, T
         __syncthreads();
         __threadfence_system();
         const bool bad = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
-        for (int64_t i = lo + tid; i < hi; i += TB) {
-            T acc = reinterpret_cast<const T*>(peer_data[0] + slot_off)[i];
-            for (int p = 1; p < P; ++p) acc = combine<T, OP>(acc, reinterpret_cast<const T*>(peer_data[p] + slot_off)[i]);
-            out[i] = bad ? (T)__builtin_nan("") : acc;
-        }
+        sum_slots<T, OP, PP>(peer_data, P, slot_off, lo, hi, bad, out);
+    }
+}
+
+template <typename T, int OP, int PP>
+void launch_p(const T* i, T* o, int64_t n, int P, int rank, uint32_t seq, char* const* pd, uint32_t* const* pf,
+              int64_t slot_bytes, int blocks, int phases, uint64_t deadline, int* err, hipStream_t st) {
+    hipLaunchKernelGGL((oneshot_kernel<T, OP, PP>), dim3(blocks), dim3(TB), 0, st, i, o, n, P, rank, seq, pd, pf,
+                       slot_bytes, phases, deadline, err);
+}
+
+template <typename T, int OP>
+void launch_op(const T* i, T* o, int64_t n, int P, int rank, uint32_t seq, char* const* pd, uint32_t* const* pf,
+               int64_t slot_bytes, int blocks, int phases, uint64_t deadline, int* err, hipStream_t st) {
+    switch (P) {
+        case 1: launch_p<T, OP, 1>(i, o, n, P, rank, seq, pd, pf, slot_bytes, blocks, phases, deadline, err, st); break;
+        case 2: launch_p<T, OP, 2>(i, o, n, P, rank, seq, pd, pf, slot_bytes, blocks, phases, deadline, err, st); break;
+        case 3: launch_p<T, OP, 3>(i, o, n, P, rank, seq, pd, pf, slot_bytes, blocks, phases, deadline, err, st); break;
+        case 4: launch_p<T, OP, 4>(i, o, n, P, rank, seq, pd, pf, slot_bytes, blocks, phases, deadline, err, st); break;
+        case 5: launch_p<T, OP, 5>(i, o, n, P, rank, seq, pd, pf, slot_bytes, blocks, phases, deadline, err, st); break;
+        case 6: launch_p<T, OP, 6>(i, o, n, P, rank, seq, pd, pf, slot_bytes, blocks, phases, deadline, err, st); break;
+        case 7: launch_p<T, OP, 7>(i, o, n, P, rank, seq, pd, pf, slot_bytes, blocks, phases, deadline, err, st); break;
+        case 8: launch_p<T, OP, 8>(i, o, n, P, rank, seq, pd, pf, slot_bytes, blocks, phases, deadline, err, st); break;
+        default: launch_p<T, OP, 0>(i, o, n, P, rank, seq, pd, pf, slot_bytes, blocks, phases, deadline, err, st); break;
     }
 }
 
@@ -82,9 +130,9 @@ int launch(int op, const void* in, void* out, int64_t n, int P, int rank, uint32
     const T* i = reinterpret_cast<const T*>(in);
     T* o = reinterpret_cast<T*>(out);
     switch (op) {
-        case 0: hipLaunchKernelGGL((oneshot_kernel<T, 0>), dim3(blocks), dim3(TB), 0, st, i, o, n, P, rank, seq, pd, pf, slot_bytes, phases, deadline, err); break;
-        case 1: hipLaunchKernelGGL((oneshot_kernel<T, 1>), dim3(blocks), dim3(TB), 0, st, i, o, n, P, rank, seq, pd, pf, slot_bytes, phases, deadline, err); break;
-        case 2: hipLaunchKernelGGL((oneshot_kernel<T, 2>), dim3(blocks), dim3(TB), 0, st, i, o, n, P, rank, seq, pd, pf, slot_bytes, phases, deadline, err); break;
+        case 0: launch_op<T, 0>(i, o, n, P, rank, seq, pd, pf, slot_bytes, blocks, phases, deadline, err, st); break;
+        case 1: launch_op<T, 1>(i, o, n, P, rank, seq, pd, pf, slot_bytes, blocks, phases, deadline, err, st); break;
+        case 2: launch_op<T, 2>(i, o, n, P, rank, seq, pd, pf, slot_bytes, blocks, phases, deadline, err, st); break;
         default: return -2;
     }
     return (int)hipGetLastError();

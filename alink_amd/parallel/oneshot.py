@@ -32,7 +32,7 @@ from ..ops import _lib
 __all__ = ["OneShot", "get", "enabled", "MAX_BYTES"]
 
 MAX_BYTES = int(os.environ.get("ALINK_ONESHOT_MAX_BYTES", str(1 << 20)))
-BLOCKS = 32
+BLOCKS = 64
 TIMEOUT_S = float(os.environ.get("ALINK_ONESHOT_TIMEOUT_S", "300"))
 SYNC_CHECK = os.environ.get("ALINK_ONESHOT_CHECK", "0") == "1"
 _DT = {torch.float32: 0, torch.float64: 1}

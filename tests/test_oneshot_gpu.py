@@ -8,16 +8,16 @@ from alink_amd.parallel.oneshot import OneShot
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("P", [1, 2, 3, 8])
+@pytest.mark.parametrize("P", [1, 2, 3, 8, 12])
 @pytest.mark.parametrize("dtype,op", [(torch.float64, "sum"), (torch.float32, "sum"), (torch.float64, "max"),
                                       (torch.float32, "min")])
 def test_oneshot_reduction_matches_torch(P, dtype, op):
-    cap = 1 << 16
+    cap = 1 << 19
     bases = [OneShot.alloc(cap, P) for _ in range(P)]
     views = [OneShot("cuda", P, r, cap, bases, [], []) for r in range(P)]
     try:
-        for call in range(3):                      # slots alternate with the sequence number
-            n = [1, 1000, 5000][call]
+        for call in range(4):                      # slots alternate with the sequence number
+            n = [1, 1000, 5000, 60000][call]       # last: several elements per thread (P <= 8: unrolled loads)
             xs = [torch.randn(n, device="cuda", dtype=dtype) for _ in range(P)]
             outs = [torch.empty_like(x) for x in xs]
             seq = call + 1
