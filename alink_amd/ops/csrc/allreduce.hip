@@ -37,7 +37,7 @@ __device__ __forceinline__ T combine(T a, T b) {
 // PP == 0: runtime P (P > 8).
 template <typename T, int OP, int PP>
 __device__ __forceinline__ void sum_slots(char* const* __restrict__ peer_data, int P, int64_t slot_off, int64_t lo,
-                                          int64_t hi, bool bad, T* __restrict__ out) {
+                                          int64_t hi, bool bad, T* out) {
     const int tid = threadIdx.x;
     if constexpr (PP > 0) {
         const T* src[PP];
@@ -62,10 +62,11 @@ __device__ __forceinline__ void sum_slots(char* const* __restrict__ peer_data, i
 }
 
 template <typename T, int OP, int PP>
-__global__ __launch_bounds__(TB) void oneshot_kernel(const T* __restrict__ in, T* __restrict__ out, int64_t n,
+__global__ __launch_bounds__(TB) void oneshot_kernel(const T* in, T* out, int64_t n,
                                                      int P, int rank, uint32_t seq, char* const* __restrict__ peer_data,
                                                      uint32_t* const* __restrict__ peer_flags, int64_t slot_bytes,
-                                                     int phases, uint64_t deadline_spins, int* __restrict__ err) {
+                                                     int phases, uint64_t deadline_spins, int* __restrict__ err,
+                                                     int* __restrict__ host_err) {
     const int tid = threadIdx.x;
     const int b = blockIdx.x;
     const int nb = gridDim.x;
@@ -89,6 +90,8 @@ __global__ __launch_bounds__(TB) void oneshot_kernel(const T* __restrict__ in, T
             while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != seq) {
                 if (++spins > deadline_spins) {
                     atomicOr(err, 1);
+                    if (host_err != nullptr)          // mapped host word: the host sees the failure without a copy
+                        __hip_atomic_store(host_err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     break;
                 }
                 __builtin_amdgcn_s_sleep(2);
@@ -103,36 +106,37 @@ __global__ __launch_bounds__(TB) void oneshot_kernel(const T* __restrict__ in, T
 
 template <typename T, int OP, int PP>
 void launch_p(const T* i, T* o, int64_t n, int P, int rank, uint32_t seq, char* const* pd, uint32_t* const* pf,
-              int64_t slot_bytes, int blocks, int phases, uint64_t deadline, int* err, hipStream_t st) {
+              int64_t slot_bytes, int blocks, int phases, uint64_t deadline, int* err, int* herr, hipStream_t st) {
     hipLaunchKernelGGL((oneshot_kernel<T, OP, PP>), dim3(blocks), dim3(TB), 0, st, i, o, n, P, rank, seq, pd, pf,
-                       slot_bytes, phases, deadline, err);
+                       slot_bytes, phases, deadline, err, herr);
 }
 
 template <typename T, int OP>
 void launch_op(const T* i, T* o, int64_t n, int P, int rank, uint32_t seq, char* const* pd, uint32_t* const* pf,
-               int64_t slot_bytes, int blocks, int phases, uint64_t deadline, int* err, hipStream_t st) {
+               int64_t slot_bytes, int blocks, int phases, uint64_t deadline, int* err, int* herr, hipStream_t st) {
     switch (P) {
-        case 1: launch_p<T, OP, 1>(i, o, n, P, rank, seq, pd, pf, slot_bytes, blocks, phases, deadline, err, st); break;
-        case 2: launch_p<T, OP, 2>(i, o, n, P, rank, seq, pd, pf, slot_bytes, blocks, phases, deadline, err, st); break;
-        case 3: launch_p<T, OP, 3>(i, o, n, P, rank, seq, pd, pf, slot_bytes, blocks, phases, deadline, err, st); break;
-        case 4: launch_p<T, OP, 4>(i, o, n, P, rank, seq, pd, pf, slot_bytes, blocks, phases, deadline, err, st); break;
-        case 5: launch_p<T, OP, 5>(i, o, n, P, rank, seq, pd, pf, slot_bytes, blocks, phases, deadline, err, st); break;
-        case 6: launch_p<T, OP, 6>(i, o, n, P, rank, seq, pd, pf, slot_bytes, blocks, phases, deadline, err, st); break;
-        case 7: launch_p<T, OP, 7>(i, o, n, P, rank, seq, pd, pf, slot_bytes, blocks, phases, deadline, err, st); break;
-        case 8: launch_p<T, OP, 8>(i, o, n, P, rank, seq, pd, pf, slot_bytes, blocks, phases, deadline, err, st); break;
-        default: launch_p<T, OP, 0>(i, o, n, P, rank, seq, pd, pf, slot_bytes, blocks, phases, deadline, err, st); break;
+        case 1: launch_p<T, OP, 1>(i, o, n, P, rank, seq, pd, pf, slot_bytes, blocks, phases, deadline, err, herr, st); break;
+        case 2: launch_p<T, OP, 2>(i, o, n, P, rank, seq, pd, pf, slot_bytes, blocks, phases, deadline, err, herr, st); break;
+        case 3: launch_p<T, OP, 3>(i, o, n, P, rank, seq, pd, pf, slot_bytes, blocks, phases, deadline, err, herr, st); break;
+        case 4: launch_p<T, OP, 4>(i, o, n, P, rank, seq, pd, pf, slot_bytes, blocks, phases, deadline, err, herr, st); break;
+        case 5: launch_p<T, OP, 5>(i, o, n, P, rank, seq, pd, pf, slot_bytes, blocks, phases, deadline, err, herr, st); break;
+        case 6: launch_p<T, OP, 6>(i, o, n, P, rank, seq, pd, pf, slot_bytes, blocks, phases, deadline, err, herr, st); break;
+        case 7: launch_p<T, OP, 7>(i, o, n, P, rank, seq, pd, pf, slot_bytes, blocks, phases, deadline, err, herr, st); break;
+        case 8: launch_p<T, OP, 8>(i, o, n, P, rank, seq, pd, pf, slot_bytes, blocks, phases, deadline, err, herr, st); break;
+        default: launch_p<T, OP, 0>(i, o, n, P, rank, seq, pd, pf, slot_bytes, blocks, phases, deadline, err, herr, st); break;
     }
 }
 
 template <typename T>
 int launch(int op, const void* in, void* out, int64_t n, int P, int rank, uint32_t seq, char* const* pd,
-           uint32_t* const* pf, int64_t slot_bytes, int blocks, int phases, uint64_t deadline, int* err, hipStream_t st) {
+           uint32_t* const* pf, int64_t slot_bytes, int blocks, int phases, uint64_t deadline, int* err, int* herr,
+           hipStream_t st) {
     const T* i = reinterpret_cast<const T*>(in);
     T* o = reinterpret_cast<T*>(out);
     switch (op) {
-        case 0: launch_op<T, 0>(i, o, n, P, rank, seq, pd, pf, slot_bytes, blocks, phases, deadline, err, st); break;
-        case 1: launch_op<T, 1>(i, o, n, P, rank, seq, pd, pf, slot_bytes, blocks, phases, deadline, err, st); break;
-        case 2: launch_op<T, 2>(i, o, n, P, rank, seq, pd, pf, slot_bytes, blocks, phases, deadline, err, st); break;
+        case 0: launch_op<T, 0>(i, o, n, P, rank, seq, pd, pf, slot_bytes, blocks, phases, deadline, err, herr, st); break;
+        case 1: launch_op<T, 1>(i, o, n, P, rank, seq, pd, pf, slot_bytes, blocks, phases, deadline, err, herr, st); break;
+        case 2: launch_op<T, 2>(i, o, n, P, rank, seq, pd, pf, slot_bytes, blocks, phases, deadline, err, herr, st); break;
         default: return -2;
     }
     return (int)hipGetLastError();
@@ -170,11 +174,23 @@ int alink_ar_ipc_close(void* p) { return (int)hipIpcCloseMemHandle(p); }
 
 int alink_ar_handle_size() { return (int)sizeof(hipIpcMemHandle_t); }
 
+// one zeroed 64-byte line of mapped, coherent pinned host memory: *host = host address, *dev = kernel address
+int alink_ar_host_word_alloc(void** host, void** dev) {
+    hipError_t e = hipHostMalloc(host, 64, hipHostMallocMapped);
+    if (e != hipSuccess) return (int)e;
+    memset(*host, 0, 64);
+    return (int)hipHostGetDevicePointer(dev, *host, 0);
+}
+
+int alink_ar_host_word_free(void* host) { return (int)hipHostFree(host); }
+
 // peer_data / peer_flags: device arrays of P pointers (this rank's own entries included).
 // dtype 0 f32, 1 f64; op 0 sum, 1 max, 2 min.
+// in == out is allowed (in-place).  host_err (nullable): device address of a mapped host word that a timed-out
+// call also sets (alink_ar_host_word_alloc), so the host can poll for failures without copying err back.
 int alink_oneshot_allreduce(const void* in, void* out, int64_t n, int dtype, int op, int P, int rank, uint32_t seq,
                             void* const* peer_data, void* const* peer_flags, int64_t slot_bytes, int blocks,
-                            int phases, double timeout_s, int* err, void* stream) {
+                            int phases, double timeout_s, int* err, int* host_err, void* stream) {
     if (n <= 0) return 0;
     if (P < 1 || rank < 0 || rank >= P || blocks < 1 || blocks > 1024 || P > TB) return -1;
     const int64_t esz = dtype == 0 ? 4 : 8;
@@ -184,8 +200,10 @@ int alink_oneshot_allreduce(const void* in, void* out, int64_t n, int dtype, int
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     char* const* pd = reinterpret_cast<char* const*>(peer_data);
     uint32_t* const* pf = reinterpret_cast<uint32_t* const*>(peer_flags);
-    if (dtype == 0) return launch<float>(op, in, out, n, P, rank, seq, pd, pf, slot_bytes, blocks, phases, deadline, err, st);
-    if (dtype == 1) return launch<double>(op, in, out, n, P, rank, seq, pd, pf, slot_bytes, blocks, phases, deadline, err, st);
+    if (dtype == 0)
+        return launch<float>(op, in, out, n, P, rank, seq, pd, pf, slot_bytes, blocks, phases, deadline, err, host_err, st);
+    if (dtype == 1)
+        return launch<double>(op, in, out, n, P, rank, seq, pd, pf, slot_bytes, blocks, phases, deadline, err, host_err, st);
     return -2;
 }
 

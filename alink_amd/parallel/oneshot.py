@@ -47,9 +47,11 @@ def _sigs(L):
     L.alink_ar_ipc_close.argtypes = [c_vp]
     L.alink_ar_free.argtypes = [c_vp]
     L.alink_oneshot_allreduce.argtypes = [c_vp, c_vp, c_i64, c_int, c_int, c_int, c_int, ctypes.c_uint32, c_vp, c_vp,
-                                          c_i64, c_int, c_int, ctypes.c_double, c_vp, c_vp]
+                                          c_i64, c_int, c_int, ctypes.c_double, c_vp, c_vp, c_vp]
+    L.alink_ar_host_word_alloc.argtypes = [ctypes.POINTER(c_vp), ctypes.POINTER(c_vp)]
+    L.alink_ar_host_word_free.argtypes = [c_vp]
     for f in ("alink_ar_alloc", "alink_ar_ipc_handle", "alink_ar_ipc_open", "alink_ar_ipc_close", "alink_ar_free",
-              "alink_oneshot_allreduce", "alink_ar_handle_size"):
+              "alink_oneshot_allreduce", "alink_ar_handle_size", "alink_ar_host_word_alloc", "alink_ar_host_word_free"):
         getattr(L, f).restype = c_int
 
 
@@ -68,6 +70,13 @@ class OneShot:
         self.peer_data = torch.tensor(bases, dtype=torch.int64, device=device)
         self.peer_flags = torch.tensor([b + self.flag_off for b in bases], dtype=torch.int64, device=device)
         self.err = torch.zeros(1, dtype=torch.int32, device=device)
+        # the kernel also sets a mapped host word on a timeout, so the per-call check is a host read (no copy)
+        self._hword, self._hword_dev, self._hview = None, None, None
+        h, d = ctypes.c_void_p(), ctypes.c_void_p()
+        if self.L.alink_ar_host_word_alloc(ctypes.byref(h), ctypes.byref(d)) == 0 and d.value:
+            import numpy as np
+            self._hword, self._hword_dev = h.value, d.value
+            self._hview = np.ctypeslib.as_array((ctypes.c_int32 * 1).from_address(h.value))
         self._err_host = torch.zeros(1, dtype=torch.int32, pin_memory=torch.cuda.is_available())
         self._err_ev = None
         self.seq = 0
@@ -100,7 +109,7 @@ class OneShot:
             rc = self.L.alink_oneshot_allreduce(t.data_ptr(), out.data_ptr(), n, _DT[t.dtype], _OP[op], self.P,
                                                 self.rank if rank is None else rank, seq & 0xFFFFFFFF,
                                                 self.peer_data.data_ptr(), self.peer_flags.data_ptr(), self.cap,
-                                                BLOCKS, phases, TIMEOUT_S, self.err.data_ptr(),
+                                                BLOCKS, phases, TIMEOUT_S, self.err.data_ptr(), self._hword_dev,
                                                 _lib.stream_ptr(self.device))
         if rc != 0:
             raise RuntimeError(f"alink_oneshot_allreduce failed: {rc}")
@@ -111,12 +120,19 @@ class OneShot:
         if value != 0:
             self.err.zero_()
             self._err_host.zero_()
+            if self._hview is not None:
+                self._hview[0] = 0
             self._err_ev = None
             raise RuntimeError("one-shot all-reduce timed out waiting for a peer (results were poisoned with NaN)")
 
     def check(self, wait: bool = False):
         """Raise if an earlier call timed out.  Non-blocking by default: the error word of the previous call is
         read back asynchronously (pinned copy + event) and examined once that copy has landed."""
+        if self._hview is not None:
+            if wait:
+                torch.cuda.current_stream(self.device).synchronize()
+            self._raise_if_failed(int(self._hview[0]))
+            return
         if self._err_ev is not None and (wait or self._err_ev.query()):
             self._err_ev.synchronize()
             self._raise_if_failed(int(self._err_host[0]))
@@ -124,20 +140,25 @@ class OneShot:
 
     def all_reduce_(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
         self.check()
-        flat = t.reshape(-1)
-        src = flat if flat.is_contiguous() else flat.contiguous()
-        res = torch.empty_like(src)
-        self.launch(src, res, op)
+        # in place: a block copies its slice of the input to the staging slot before it signals, and writes the
+        # same slice of the result only after every rank's signal (no result buffer, no copy back)
+        flat = t.view(-1) if t.is_contiguous() else t.reshape(-1).contiguous()
+        self.launch(flat, flat, op)
         if SYNC_CHECK:
             self._raise_if_failed(int(self.err.item()))
-        elif self._err_ev is None:
+        elif self._hview is None and self._err_ev is None:
             self._err_host.copy_(self.err, non_blocking=True)
             self._err_ev = torch.cuda.Event()
             self._err_ev.record(torch.cuda.current_stream(self.device))
-        t.copy_(res.view_as(t))
+        if flat.data_ptr() != t.data_ptr():
+            t.copy_(flat.view_as(t))
         return t
 
     def close(self):
+        if self._hword is not None:
+            self._hview = None
+            self.L.alink_ar_host_word_free(ctypes.c_void_p(self._hword))
+            self._hword, self._hword_dev = None, None
         for p in self.opened:
             self.L.alink_ar_ipc_close(ctypes.c_void_p(p))
         for p in self.owned:

@@ -53,4 +53,16 @@ def test_oneshot_missing_peer_times_out_with_nan(monkeypatch):
     v.launch(x, out, "sum", phases=3, seq=1)     # peer 1 never signals
     torch.cuda.synchronize()
     assert int(v.err.item()) == 1 and bool(torch.isnan(out).all())
+    # the mapped host word carries the failure too: the next call's check raises without a device copy
+    with pytest.raises(RuntimeError, match="timed out"):
+        v.check()
+    assert int(v.err.item()) == 0                    # re-armed after raising
+    # in-place all_reduce_ of a non-contiguous tensor (staged through a contiguous copy) on a healthy 1-rank view
+    one = OneShot("cuda", 1, 0, cap, [bases[0]], [], [])
+    y = torch.arange(24, dtype=torch.float64, device="cuda").view(4, 6).t()
+    ref = y.clone()
+    one.all_reduce_(y)
+    torch.cuda.synchronize()
+    assert torch.equal(y, ref)
+    one.close()
     v.close()
