@@ -114,33 +114,109 @@ class CalcLosses(ComputeFunction):
         ctx.putObj(LOSS_AR, vec.to(torch.float64).clone())
 
 
+def _two_loop_body(S, Y, dirv):
+    """S, Y: [l, d] corrections in order (oldest first)."""
+    dots = (S * Y).sum(1)
+    rho = torch.where(dots > 0, 1.0 / torch.where(dots <= 0, torch.ones_like(dots), dots),
+                      torch.zeros_like(dots))
+    l = S.shape[0]
+    alpha = [None] * l
+    for i in range(l - 1, -1, -1):
+        alpha[i] = rho[i] * (S[i] * dirv).sum()
+        dirv = dirv - alpha[i] * Y[i]
+    for i in range(l):
+        beta_i = rho[i] * (Y[i] * dirv).sum()
+        dirv = dirv + (alpha[i] - beta_i) * S[i]
+    return dirv
+
+
+# ---- hipGraph replay of the two-loop ----------------------------------------------------------------------
+# The recursion is ~6 l + 4 small kernels (l <= 10 corrections) whose launch cost, not their bytes, sets the time
+# of an L-BFGS superstep at moderate sizes.  Once the history is full (l = m, every superstep from k = m + 1 on)
+# it is captured ONCE per history as a HIP graph and replayed as a single launch: the history tensors are
+# updated in place between supersteps; the rotation of the circular history is a device scalar set by a fill
+# kernel before each replay (order = (0..m-1 + delta) mod m gathered inside the graph, no host->device copy);
+# inputs / outputs go through static vectors.  The first m supersteps (l < m, each l seen once) run eagerly.
+# ALINK_HIP_GRAPHS=0 runs everything eagerly.
+import gc as _gc  # noqa: E402
+import os as _os  # noqa: E402
+import weakref as _weakref  # noqa: E402
+
+_GRAPHS = {}      # id(sK) -> (weakref to sK, {(yK ptr, d, dtype): (graph, static dir, delta, static out)})
+GRAPH_MAX_DIM = 1 << 22            # above this each op is bandwidth-bound and launch cost no longer matters
+GRAPH_STATS = {"captures": 0, "replays": 0}
+
+
+def graphs_enabled() -> bool:
+    return _os.environ.get("ALINK_HIP_GRAPHS", "1") != "0"
+
+
+def _two_loop_rotating(sK, yK, dirv, delta):
+    m = sK.shape[0]
+    order = torch.remainder(torch.arange(m, device=sK.device) + delta, m)
+    return _two_loop_body(sK.index_select(0, order), yK.index_select(0, order), dirv)
+
+
+def _two_loop_graph(sK, yK, start_dir, delta: int):
+    hit = _GRAPHS.get(id(sK))
+    if hit is not None and hit[0]() is sK:
+        per = hit[1]
+    else:                    # identity, not tensor equality; the entry (and its graphs) dies with the history
+        per = {}
+        key_id = id(sK)
+        _GRAPHS[key_id] = (_weakref.ref(sK, lambda _r, i=key_id: _GRAPHS.pop(i, None)), per)
+    key = (yK.data_ptr(), start_dir.shape[0], start_dir.dtype)
+    ent = per.get(key)
+    if ent is None:
+        din = start_dir.clone()
+        dl = torch.zeros((), dtype=torch.int64, device=start_dir.device)
+        dl.fill_(delta)
+        cur = torch.cuda.current_stream(start_dir.device)
+        side = torch.cuda.Stream(device=start_dir.device)
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):            # warm-up outside capture (lazy module / kernel loads)
+            _two_loop_rotating(sK, yK, din.clone(), dl)
+        cur.wait_stream(side)
+        g = torch.cuda.CUDAGraph()
+        # no Python GC inside the capture: a collected object that releases a HIP resource (an event, an older
+        # graph of a dead history) would issue a HIP call on the capturing stream and abort the capture
+        gc_was = _gc.isenabled()
+        _gc.disable()
+        try:
+            with torch.cuda.graph(g):
+                dout = _two_loop_rotating(sK, yK, din.clone(), dl)
+        finally:
+            if gc_was:
+                _gc.enable()
+        ent = (g, din, dl, dout)
+        per[key] = ent
+        GRAPH_STATS["captures"] += 1
+    g, din, dl, dout = ent
+    din.copy_(start_dir)
+    dl.fill_(delta)
+    g.replay()
+    GRAPH_STATS["replays"] += 1
+    return dout.clone()
+
+
 def _two_loop(ctx, grad_vec, start_dir, k):
     """L-BFGS two-loop recursion over the stored corrections (``Lbfgs.CalDirection`` :109-175).
 
     Kept entirely on the device: a correction pair with ``s.y == 0`` is skipped in the reference; here its
     ``rho`` is 0, which makes the same update a no-op without a host round trip.  Pairs with ``s.y < 0``
     (impossible for the convex linear losses, common for the MLP objective) are skipped the same way so
-    the direction stays a descent direction."""
+    the direction stays a descent direction.  On a GPU the recursion replays as one HIP graph."""
     sK, yK = ctx.getObj(SKYK)
     m = NUM_CORRECTIONS
-    dirv = start_dir.clone()
     delta = k - m if k > m else 0
     l = k if k <= m else m
     if l == 0:
-        return dirv
+        return start_dir.clone()
     order = [(i + delta) % m for i in range(l)]
-    S, Y = sK[order], yK[order]                      # [l, d]
-    dots = (S * Y).sum(1)
-    rho = torch.where(dots > 0, 1.0 / torch.where(dots <= 0, torch.ones_like(dots), dots),
-                      torch.zeros_like(dots))
-    alpha = torch.zeros(l, dtype=dirv.dtype, device=dirv.device)
-    for i in range(l - 1, -1, -1):
-        alpha[i] = rho[i] * torch.dot(S[i], dirv)
-        dirv = dirv - alpha[i] * Y[i]
-    for i in range(l):
-        beta_i = rho[i] * torch.dot(Y[i], dirv)
-        dirv = dirv + (alpha[i] - beta_i) * S[i]
-    return dirv
+    if l == m and start_dir.is_cuda and graphs_enabled() and start_dir.dim() == 1 and \
+            start_dir.shape[0] <= GRAPH_MAX_DIM and sK.is_contiguous() and yK.is_contiguous():
+        return _two_loop_graph(sK, yK, start_dir.contiguous(), delta)
+    return _two_loop_body(sK[order], yK[order], start_dir.clone())
 
 
 def _update_history(ctx, grad_vec, k):

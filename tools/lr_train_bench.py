@@ -1,6 +1,7 @@
 """Whole LogisticRegressionTrainBatchOp (L-BFGS, fp64, dense features) on the GPU: per-iteration time with the
 K12 gradient + K14 line-search kernels, vs the same run with ALINK_DISABLE_K14=1 (torch GEMM line search).
-Usage: python tools/lr_train_bench.py [rows] [dims]"""
+Usage: python tools/lr_train_bench.py [rows] [dims]
+       python tools/lr_train_bench.py --graphs [rows] [dims]   (two-loop as a HIP graph vs eager)"""
 import json
 import os
 import sys
@@ -32,7 +33,24 @@ def run(n, d, iters):
     return (time.perf_counter() - t) / iters * 1e3, float(curve[-1]) if len(curve) else None
 
 
+def main_graphs(n, d):
+    """Per-iteration time with the two-loop replayed as a HIP graph (default) vs eager (ALINK_HIP_GRAPHS=0)."""
+    from alink_amd.models.linear import optim
+    out = {"rows": n, "dims": d}
+    for flag in ("0", "1", "0", "1"):
+        os.environ["ALINK_HIP_GRAPHS"] = flag
+        ms, loss = run(n, d, 100)
+        out.setdefault("ms_per_iter_graphs" if flag == "1" else "ms_per_iter_eager", []).append(round(ms, 3))
+        out["final_loss_graphs" if flag == "1" else "final_loss_eager"] = loss
+    out["graph_captures"], out["graph_replays"] = optim.GRAPH_STATS["captures"], optim.GRAPH_STATS["replays"]
+    print(json.dumps(out), flush=True)
+
+
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "--graphs":
+        for n in ([int(sys.argv[2])] if len(sys.argv) > 2 else [100_000, 4_000_000]):
+            main_graphs(n, int(sys.argv[3]) if len(sys.argv) > 3 else 28)
+        return
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 4_000_000
     for d in ([int(sys.argv[2])] if len(sys.argv) > 2 else [28, 128, 512]):
         os.environ["ALINK_DISABLE_K14"] = "1"
