@@ -231,13 +231,16 @@ def _local_kmeans(samples: torch.Tensor, weights: torch.Tensor, k: int, dist_typ
     seeds two centroids in one true cluster and then needs tens of Lloyd steps to creep apart.
 
     ``ALINK_KMEANS_SEEDING=reference`` selects the reference's rule instead (one candidate per pick, sampled with
-    probability proportional to weight x cost), for reference-faithful runs."""
+    probability proportional to weight x cost, the cost being the PLAIN distance as in
+    ``LocalKmeansFunc.sampleInitialCentroids``), for reference-faithful runs."""
     import os
     rng = np.random.default_rng(seed)
     n = samples.shape[0]
     w = weights.to(torch.float64)
-    D = _seed_cost(pairwise_distance(samples, samples, dist_type), dist_type)  # [n, n]
     reference_rule = os.environ.get("ALINK_KMEANS_SEEDING", "greedy").lower() == "reference"
+    D = pairwise_distance(samples, samples, dist_type)                                      # [n, n]
+    if not reference_rule:
+        D = _seed_cost(D, dist_type)
     if reference_rule:
         trials = 1
     exhaustive = n <= 4096 and not reference_rule
