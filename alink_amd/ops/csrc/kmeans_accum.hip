@@ -7,17 +7,19 @@
 // KMeansUtil.java:60-85) — runs as two passes: the MFMA nearest-centroid kernel (kmeans_nearest.hip) writes
 // idx[N], then this kernel forms Sum[c][:] += w_r x_r and Cnt[c] += w_r.
 //
-// Layout: grid (row chunk b, dim slice s), DS = 128 dims per slice (64 when D == 64); a 512-thread workgroup
-// keeps its slice of the k x DS fp32 partial sums in LDS (k <= 256 at DS = 128 -> 145 KiB, k <= 512 at DS = 64),
-// 8 waves walk the chunk's rows: every wave instruction loads 1 KiB = DS/8 lanes x 16 B per row, 64/(DS/8) rows,
+// Layout: grid (row chunk b, dim slice s), DS = 64 dims per slice; a 512-thread workgroup keeps its slice of the
+// k x DS partial sums of up to 256 centroids (grid z: centroid blocks) in an fp64 LDS table (k * 73 * 8 B <=
+// 146 KiB; ds_add_f64 ~9 cycles per wave-instruction on gfx950 against ~193 for ds_add_f32).
+// 8 waves walk the chunk's rows: every wave instruction loads 1 KiB = 8 lanes x 16 B per row, 8 rows,
 // 8 such loads in flight per wave (64 KiB per CU: the first version, one 256-B row per wave instruction and 4 in
-// flight, was latency-bound at 0.4 TB/s), then ds_add_f32 into row idx[r] of the LDS table with the table
+// flight, was latency-bound at 0.4 TB/s), then atomic adds into row idx[r] of the LDS table with the table
 // columns permuted (lane l's element j -> column j*DS/8 + l) so consecutive lanes hit consecutive banks.  At the end
 // the table goes to slab[b][c][D] (fp32) and a fixed-order fp64 reduction over chunks (kmeans_accum_reduce)
-// forms [k][D+1].  Counts of unweighted rows are exact (integers < 2^24 per chunk); the fp32 sums inside a chunk
-// depend on the LDS atomic order (rounding-level run-to-run differences, unlike v7's MFMA path).
+// forms [k][D+1].  Counts of unweighted rows are exact; the partial sums inside a chunk depend on the LDS atomic
+// order at the rounding level of the table type (run-to-run differences, unlike v7's MFMA path).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "kmeans_tile.h"
 
@@ -26,11 +28,12 @@ namespace {
 constexpr int THREADS = 512;
 constexpr int NW = THREADS / 64;
 constexpr int U = 8;                  // 1-KiB wave loads in flight per wave (8 KiB / wave, 64 KiB / CU)
+constexpr int KBLK = 256;             // centroids per fp64 LDS table (k * 73 * 8 B <= 146 KiB)
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-// LDS table row stride RS = DS + 16 (DS = 128: the 2 rows a 32-lane half touches per ds_add_f32 sit in different
-// bank halves when their centroid ids differ in parity) or DS + 8 (DS = 64: 4 rows per half, bank offsets 8c mod 32)
+// LDS table row stride RS = DS + 8 elements at DS = 64 (rows of one wave instruction land on different banks);
+// DS + 16 at DS = 128 (no longer launched)
 template <int DS>
 struct Tab {
     static constexpr int RS = DS == 64 ? DS + 8 : DS + 16;
@@ -38,19 +41,26 @@ struct Tab {
     static constexpr int RPI = 64 / LPR;            // rows per wave instruction (4 at DS=128, 8 at DS=64)
 };
 
-template <int DS>
+// AT = the LDS table type.  double (k <= 256, DS = 64): measured on gfx950, one wave-instruction of ds_add_f64 costs
+// ~9 cycles against ~193 for ds_add_f32 (profiles/gbdt_r3.txt, LDS atomic probe), so the fp64 table is both the
+// faster and the more accurate one; the products w * x are formed exactly in fp64.  float: k up to 512 at D = 64.
+template <int DS, typename AT>
 __global__ __launch_bounds__(THREADS) void kmeans_accum_kernel(const __bf16* __restrict__ X, int64_t N, int D,
                                                                const int* __restrict__ idx,
-                                                               const float* __restrict__ w, int k,
+                                                               const float* __restrict__ w, int k_total,
                                                                int64_t rows_per_chunk, float* __restrict__ slab,
                                                                float* __restrict__ slab_cnt) {
     using T = Tab<DS>;
-    extern __shared__ float tab[];          // [k][RS] then cnt[k]
+    // blockIdx.z = centroid block: this workgroup's table holds centroids [c_base, c_base + k) only
+    const int c_base = (int)blockIdx.z * KBLK;
+    const int k = k_total - c_base < KBLK ? k_total - c_base : KBLK;
+    extern __shared__ __align__(16) unsigned char lds_raw[];
+    AT* tab = reinterpret_cast<AT*>(lds_raw);   // [k][RS] then cnt[k]
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int b = blockIdx.x, s = blockIdx.y;
     const int d0 = s * DS;
-    float* cnt = tab + k * T::RS;
-    for (int e = threadIdx.x; e < k * T::RS + k; e += THREADS) tab[e] = 0.f;
+    AT* cnt = tab + k * T::RS;
+    for (int e = threadIdx.x; e < k * T::RS + k; e += THREADS) tab[e] = (AT)0;
     __syncthreads();
     const int64_t r_lo = (int64_t)b * rows_per_chunk;
     const int64_t r_hi = r_lo + rows_per_chunk < N ? r_lo + rows_per_chunk : N;
@@ -66,7 +76,7 @@ __global__ __launch_bounds__(THREADS) void kmeans_accum_kernel(const __bf16* __r
         for (int u = 0; u < U; ++u) {
             const int64_t r = base + u * T::RPI + sub;
             const bool ok = r < r_hi;
-            c[u] = ok ? idx[r] : -1;
+            c[u] = ok ? idx[r] - c_base : -1;
             wr[u] = ok ? (w != nullptr ? w[r] : 1.f) : 0.f;
             const uint4 v = *reinterpret_cast<const uint4*>(X + (ok ? r : r_lo) * D + d0 + 8 * l);
             lo[u] = f32x4{__uint_as_float(v.x << 16), __uint_as_float(v.x & 0xFFFF0000u),
@@ -78,25 +88,26 @@ __global__ __launch_bounds__(THREADS) void kmeans_accum_kernel(const __bf16* __r
         for (int u = 0; u < U; ++u) {
             if (c[u] < 0 || c[u] >= k) continue;
             // table column of element j of this lane's chunk: j * LPR + l (consecutive lanes -> consecutive banks)
-            float* row = tab + c[u] * T::RS + l;
+            AT* row = tab + c[u] * T::RS + l;
+            const AT wa = (AT)wr[u];
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                __hip_atomic_fetch_add(row + j * T::LPR, wr[u] * lo[u][j], __ATOMIC_RELAXED,
+                __hip_atomic_fetch_add(row + j * T::LPR, wa * (AT)lo[u][j], __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_WORKGROUP);
-                __hip_atomic_fetch_add(row + (j + 4) * T::LPR, wr[u] * hi[u][j], __ATOMIC_RELAXED,
+                __hip_atomic_fetch_add(row + (j + 4) * T::LPR, wa * (AT)hi[u][j], __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_WORKGROUP);
             }
-            if (do_cnt) __hip_atomic_fetch_add(cnt + c[u], wr[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (do_cnt) __hip_atomic_fetch_add(cnt + c[u], wa, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
     }
     __syncthreads();
-    float* out = slab + (int64_t)b * k * D;
+    float* out = slab + ((int64_t)b * k_total + c_base) * D;
     for (int e = threadIdx.x; e < k * DS; e += THREADS) {
         const int cc = e / DS, dd = e - cc * DS;        // dd = 8 * l + j  <->  table column j * LPR + l
-        out[(int64_t)cc * D + d0 + dd] = tab[cc * T::RS + (dd & 7) * T::LPR + (dd >> 3)];
+        out[(int64_t)cc * D + d0 + dd] = (float)tab[cc * T::RS + (dd & 7) * T::LPR + (dd >> 3)];
     }
     if (s == 0)
-        for (int cc = threadIdx.x; cc < k; cc += THREADS) slab_cnt[(int64_t)b * k + cc] = cnt[cc];
+        for (int cc = threadIdx.x; cc < k; cc += THREADS) slab_cnt[(int64_t)b * k_total + c_base + cc] = (float)cnt[cc];
 }
 
 // out[c][0..D) = sum_b slab[b][c][:], out[c][D] = sum_b slab_cnt[b][c]; fp64, fixed order over b
@@ -297,20 +308,25 @@ int alink_kmeans_accum_bf16(const void* X, int64_t N, int D, const int* idx, con
     const int64_t per = (N + nchunk - 1) / nchunk;
     static bool attr_set = false;  // > 64 KiB of dynamic LDS must be opted into once per kernel
     if (!attr_set) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void*>(kmeans_accum_kernel<64>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (512 * 72 + 512) * 4) != hipSuccess ||
-            hipFuncSetAttribute(reinterpret_cast<const void*>(kmeans_accum_kernel<128>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (256 * 144 + 256) * 4) != hipSuccess)
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(kmeans_accum_kernel<64, float>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (KBLK * 72 + KBLK) * 4) != hipSuccess ||
+            hipFuncSetAttribute(reinterpret_cast<const void*>(kmeans_accum_kernel<64, double>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (KBLK * 72 + KBLK) * 8) != hipSuccess)
             return 3;
         attr_set = true;
     }
-    if (D == 64) {
-        const size_t lds = (size_t)(k * Tab<64>::RS + k) * sizeof(float);
-        hipLaunchKernelGGL(kmeans_accum_kernel<64>, dim3(nchunk, 1), dim3(THREADS), lds, st, (const __bf16*)X, N, D,
-                           idx, w, k, per, slab, slab_cnt);
+    // one workgroup per (row chunk, 64-dim slice, block of <= 256 centroids); k > 256 re-reads the chunk's rows
+    // once per centroid block (an fp64 table of 512 centroids would not fit the LDS)
+    const int kb = (k + KBLK - 1) / KBLK;
+    const int kl = k < KBLK ? k : KBLK;
+    static const bool force_f32 = getenv("ALINK_KMEANS_ACC_F32") != nullptr;   // A/B diagnostic (tools/)
+    if (!force_f32) {
+        const size_t lds = (size_t)(kl * Tab<64>::RS + kl) * sizeof(double);
+        hipLaunchKernelGGL((kmeans_accum_kernel<64, double>), dim3(nchunk, D / 64, kb), dim3(THREADS), lds, st,
+                           (const __bf16*)X, N, D, idx, w, k, per, slab, slab_cnt);
     } else {
-        const size_t lds = (size_t)(k * Tab<128>::RS + k) * sizeof(float);
-        hipLaunchKernelGGL(kmeans_accum_kernel<128>, dim3(nchunk, D / 128), dim3(THREADS), lds, st,
+        const size_t lds = (size_t)(kl * Tab<64>::RS + kl) * sizeof(float);
+        hipLaunchKernelGGL((kmeans_accum_kernel<64, float>), dim3(nchunk, D / 64, kb), dim3(THREADS), lds, st,
                            (const __bf16*)X, N, D, idx, w, k, per, slab, slab_cnt);
     }
     if (hipGetLastError() != hipSuccess) return 2;
