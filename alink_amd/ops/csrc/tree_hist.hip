@@ -8,9 +8,10 @@
 //  * bins are a row-major uint8 matrix [n, F] (one byte per (row, feature), <= 255 bins + a missing bin),
 //    so consecutive lanes read consecutive feature bytes of a row: fully coalesced 256-byte wave loads.
 //  * each workgroup owns a contiguous row range and a feature group; it privatises the
-//    [slots x features x bins x stats] histogram in LDS (ds_add_f32 atomics — native, no CAS loop) and
-//    flushes non-zero entries once with global fp32 atomics.  Per-(slot, feature) rows are padded by one
-//    float so lanes working on neighbouring features land in different LDS banks.
+//    [slots x features x bins x stats] histogram in LDS as fp64 (ds_add_f64: ~9 cycles per wave-instruction on
+//    gfx950 against ~193 for the native ds_add_f32 — see the K7 note at tree_hist_fm) and flushes non-zero
+//    entries once with global fp32 atomics.  Per-(slot, feature) rows are padded by one element so lanes
+//    working on neighbouring features land in different LDS banks.
 //  * when even one feature of all slots does not fit the LDS budget the slots are split into groups
 //    (grid.z); past 8 groups (very deep / wide levels, few rows per node) the kernel accumulates straight
 //    into global memory instead, where contention is negligible.
@@ -28,13 +29,13 @@ __global__ __launch_bounds__(kThreads) void tree_hist_lds(
     const uint8_t* __restrict__ bins, int64_t n, int F, const int32_t* __restrict__ slot,
     const float* __restrict__ stats, int S, int B, int slots_per_group, int FG, int64_t rows_per_block,
     float* __restrict__ hist) {
-  extern __shared__ float sh[];
+  extern __shared__ double sh[];   // fp64: ds_add_f64 ~9 cyc vs ds_add_f32 ~193 (K7 note below)
   const int fstride = B * S + 1;
   const int f0 = blockIdx.y * FG;
   const int fg = min(FG, F - f0);
   const int slot0 = blockIdx.z * slots_per_group;
   const int lds_n = slots_per_group * FG * fstride;
-  for (int i = threadIdx.x; i < lds_n; i += kThreads) sh[i] = 0.f;
+  for (int i = threadIdx.x; i < lds_n; i += kThreads) sh[i] = 0.0;
   __syncthreads();
 
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
@@ -48,11 +49,11 @@ __global__ __launch_bounds__(kThreads) void tree_hist_lds(
       const int s = slot[r] - slot0;
       if ((unsigned)s >= (unsigned)slots_per_group) continue;
       const int b = bins[r * F + f0 + f];
-      float* h = sh + (s * FG + f) * fstride + b * S;
+      double* h = sh + (s * FG + f) * fstride + b * S;
       const float* st = stats + r * S;
       for (int k = 0; k < S; ++k) {
         const float v = st[k];
-        if (v != 0.f) atomicAdd(h + k, v);
+        if (v != 0.f) atomicAdd(h + k, (double)v);
       }
     }
   }
@@ -61,7 +62,7 @@ __global__ __launch_bounds__(kThreads) void tree_hist_lds(
   // flush: LDS index i -> (slot s, local feature f, bin*S + k)
   const int bs = B * S;
   for (int i = threadIdx.x; i < lds_n; i += kThreads) {
-    const float v = sh[i];
+    const float v = (float)sh[i];
     if (v == 0.f) continue;
     const int sf = i / fstride;
     const int rem = i - sf * fstride;
@@ -82,24 +83,24 @@ __global__ __launch_bounds__(kThreads) void tree_hist_rows(
     const uint8_t* __restrict__ bins, int64_t n, int F, const int32_t* __restrict__ slot,
     const float* __restrict__ stats, int B, int slots_per_group, int FG, int64_t rows_per_block,
     float* __restrict__ hist) {
-  extern __shared__ float sh[];
+  extern __shared__ double sh[];   // fp64: ds_add_f64 ~9 cyc vs ds_add_f32 ~193 (K7 note below)
   const int fstride = B * S + 1;
   const int f0 = blockIdx.y * FG;
   const int fg = min(FG, F - f0);
   const int slot0 = blockIdx.z * slots_per_group;
   const int lds_n = slots_per_group * FG * fstride;
-  for (int i = threadIdx.x; i < lds_n; i += kThreads) sh[i] = 0.f;
+  for (int i = threadIdx.x; i < lds_n; i += kThreads) sh[i] = 0.0;
   __syncthreads();
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
   const int64_t r1 = min(n, r0 + rows_per_block);
   for (int64_t r = r0 + threadIdx.x; r < r1; r += kThreads) {
     const int s = slot[r] - slot0;
     if ((unsigned)s >= (unsigned)slots_per_group) continue;
-    float v[S];
+    double v[S];
 #pragma unroll
-    for (int k = 0; k < S; ++k) v[k] = stats[r * S + k];
+    for (int k = 0; k < S; ++k) v[k] = (double)stats[r * S + k];
     const uint8_t* br = bins + r * F + f0;
-    float* base = sh + s * FG * fstride;
+    double* base = sh + s * FG * fstride;
     int f = 0;
     // 16 feature bytes per load when the row slice is 16-B aligned (F % 16 == 0, f0 % 16 == 0): one dwordx4
     // instead of 16 byte loads per lane
@@ -109,14 +110,14 @@ __global__ __launch_bounds__(kThreads) void tree_hist_rows(
         const uint32_t w4[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
-          float* h = base + (f + j) * fstride + (int)((w4[j >> 2] >> (8 * (j & 3))) & 0xffu) * S;
+          double* h = base + (f + j) * fstride + (int)((w4[j >> 2] >> (8 * (j & 3))) & 0xffu) * S;
 #pragma unroll
           for (int k = 0; k < S; ++k) atomicAdd(h + k, v[k]);
         }
       }
     }
     for (; f < fg; ++f) {
-      float* h = base + f * fstride + (int)br[f] * S;
+      double* h = base + f * fstride + (int)br[f] * S;
 #pragma unroll
       for (int k = 0; k < S; ++k) atomicAdd(h + k, v[k]);
     }
@@ -124,7 +125,7 @@ __global__ __launch_bounds__(kThreads) void tree_hist_rows(
   __syncthreads();
   const int bs = B * S;
   for (int i = threadIdx.x; i < lds_n; i += kThreads) {
-    const float val = sh[i];
+    const float val = (float)sh[i];
     if (val == 0.f) continue;
     const int sf = i / fstride;
     const int rem = i - sf * fstride;
@@ -399,7 +400,7 @@ int alink_tree_hist_f32(const uint8_t* bins, int64_t n, int F, const int32_t* sl
                         int S, int B, int nslots, float* hist, int num_cus, int variant, hipStream_t stream) {
   if (n <= 0 || nslots <= 0) return 0;
   if (F <= 0 || S <= 0 || B <= 0 || B > 256) return 1;
-  const int unit = (B * S + 1) * (int)sizeof(float);  // one (slot, feature) row in LDS
+  const int unit = (B * S + 1) * (int)sizeof(double);  // one (slot, feature) row of the fp64 LDS table
   const int max_units = kLdsBudget / unit;
   int FG, spg, groups;
   if (max_units >= nslots) {
