@@ -3,7 +3,8 @@
 Every rank allocates an uncached staging area (two slots of ``cap_bytes`` + per-block flags), exports it with
 ``hipIpcGetMemHandle``, the handles are exchanged once over the host (gloo) group and opened on every peer.  An
 all-reduce is then one kernel on the caller's stream: copy-in, release a sequence number to every peer, poll
-the own flags, sum the P staging slots in rank order.  No RCCL call, no host round trip, bit-identical results
+the own flags, sum the P staging slots in rank order (for P <= 8 the P remote loads of an element are issued
+together, so a slice costs one xGMI round trip, not P).  No RCCL call, no host round trip, bit-identical results
 on all ranks.
 
 Used by ``comm.all_reduce`` for device tensors of at most ``ALINK_ONESHOT_MAX_BYTES`` (default 1 MiB):
@@ -16,8 +17,11 @@ Used by ``comm.all_reduce`` for device tensors of at most ``ALINK_ONESHOT_MAX_BY
 Setup is collective and validated on a probe buffer against the exact rank-order sum; if any rank fails, every
 rank disables the path (the decision is agreed by a MIN all-reduce over the host group, so ranks never diverge
 between the two implementations).  A peer that does not arrive within ``ALINK_ONESHOT_TIMEOUT_S`` (300 s) makes
-the kernel write NaN and set an error word; the host reads that word back asynchronously after every call and
-raises on the next call (``ALINK_ONESHOT_CHECK=1``: synchronously, on the same call).
+the kernel write NaN and set an error word, on the device and in a mapped pinned host word; the host polls the
+host word (a plain memory read, no copy) at the start of every call and raises (``ALINK_ONESHOT_CHECK=1``:
+synchronously, on the same call).  The reduction runs in place on the caller's tensor: each workgroup copies its
+slice to the staging slot before signalling and writes the same slice of the result only after every rank's
+signal.
 """
 from __future__ import annotations
 
