@@ -143,7 +143,8 @@ import os as _os  # noqa: E402
 import weakref as _weakref  # noqa: E402
 
 _GRAPHS = {}      # id(sK) -> (weakref to sK, {(yK ptr, d, dtype): (graph, static dir, delta, static out)})
-GRAPH_MAX_DIM = 1 << 22            # above this each op is bandwidth-bound and launch cost no longer matters
+GRAPH_MAX_DIM = 1 << 20            # above this each op is bandwidth-bound (launch cost no longer matters) and the
+#                                    graph pool would hold 2 x m x d fp64 of gathered history
 GRAPH_STATS = {"captures": 0, "replays": 0}
 
 
