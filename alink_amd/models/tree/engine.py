@@ -18,6 +18,8 @@ node) cross to the host to build the model objects.
 """
 from __future__ import annotations
 
+import collections
+
 import math
 from dataclasses import dataclass
 from typing import List, Optional, Tuple
@@ -193,8 +195,10 @@ class TreeBuilder:
         return H
 
     RS_BLOCKS = int(__import__("os").environ.get("ALINK_GBDT_RS_BLOCKS", "4"))
-    RS_BYTES: List[int] = []          # reduce-scattered bytes per histogram piece (observability)
-    HIST_BYTES: List[int] = []        # full-width fp32 histogram bytes per histogram call (levels in order)
+    # observability (bounded: long trainings and many jobs in one process must not grow them without limit)
+    RS_BYTES = collections.deque(maxlen=4096)     # reduce-scattered bytes per histogram piece (latest)
+    RS_CALLS = 0                                  # reduce-scattered histogram pieces (all time)
+    HIST_BYTES = collections.deque(maxlen=4096)   # full-width fp32 histogram bytes per histogram call (latest)
 
     def _histograms_sharded(self, slot, sub, nslots: int, prep) -> torch.Tensor:
         """Feature-block reduce-scatter overlapped with the histogram build: every rank's
@@ -214,6 +218,7 @@ class TreeBuilder:
             fgs = [j * gpr + lo + t if lo + t < gpr else pad for j in range(ws) for t in range(ps)]
             Hc = tops.histogram_groups(self.d.bins, slot, sub, nslots, self.B, fgs, prep)
             TreeBuilder.RS_BYTES.append(int(Hc.numel() * Hc.element_size()))
+            TreeBuilder.RS_CALLS += 1
             pend.append(comm.reduce_scatter_async(Hc, "sum"))
             real.append(min(ps, gpr - lo) * 32)
         parts = [p.wait()[:k] for p, k in zip(pend, real)]

@@ -9,7 +9,7 @@
 //   1. workgroup b copies slice b of the local input into this rank's staging slot (seq & 1) — double-buffered,
 //      so a slot is rewritten only after every peer has finished reading it (they signalled the next call);
 //   2. it releases (system scope) seq into flag[b][rank] of EVERY peer's flag array;
-//   3. it spins (bounded by a real-time deadline) until flag[b][p] == seq for all p in its own array;
+//   3. it spins (bounded by a real-time deadline) until flag[b][p] >= seq (mod 2^32) for all p in its own array;
 //   4. it reads slice b of all P staging slots over xGMI and sums them in rank order 0..P-1 — the same order
 //      on every rank, so all ranks hold bit-identical results (the determinism RCCL does not promise).
 //
@@ -87,7 +87,9 @@ __global__ __launch_bounds__(TB) void oneshot_kernel(const T* in, T* out, int64_
         if (tid < P) {
             const uint32_t* f = peer_flags[rank] + (int64_t)b * P + tid;
             uint64_t spins = 0;
-            while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != seq) {
+            // wrap-safe: a peer may already have finished call seq and signalled seq + 1 before this wave's
+            // first poll (a preempted wave, ranks time-sharing a GPU); any flag at or past seq means "arrived"
+            while ((int32_t)(__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - seq) < 0) {
                 if (++spins > deadline_spins) {
                     atomicOr(err, 1);
                     if (host_err != nullptr)          // mapped host word: the host sees the failure without a copy

@@ -10,7 +10,10 @@ collectives go through ``torch.distributed``:
   traffic never serialises through GPU memory;
 * ``gloo`` alone for CPU-only runs / tests (the analogue of Flink's LocalEnvironment).
 
-With world size 1 every call is a local no-op.
+With world size 1 every call is a local no-op, unless ``ALINK_COMM_FORCE_COLLECTIVE=1``: then a 1-rank process
+group is created (``init_distributed``) and every wrapper takes its real collective branch (RCCL on a GPU box,
+gloo on the host).  That is how the RCCL branches of an 8-GPU job are exercised on a 1-GPU box: RCCL refuses two
+ranks on one device ("Duplicate GPU detected"), but a 1-rank RCCL communicator runs every collective for real.
 """
 from __future__ import annotations
 
@@ -30,7 +33,7 @@ __all__ = ["init_distributed", "get_rank", "get_world_size", "is_distributed", "
            "broadcast_object", "barrier", "all_gather_tensor", "all_to_all_objects", "reduce_scatter",
            "object_group", "device_for_rank", "CommStats", "STATS", "shutdown", "all_reduce_coalesced",
            "Pending", "reduce_scatter_async", "all_gather_varlen_async", "all_reduce_async", "all_to_all_bytes", "all_to_all_strings",
-           "comm_stream"]
+           "comm_stream", "force_collective", "device_timing", "device_timing_collect"]
 
 _OBJ_GROUP = None
 
@@ -56,10 +59,33 @@ class CommStats:
 STATS = CommStats()
 
 
+_DEV_TIMING = {"on": False, "events": []}
+
+
+def device_timing(on: bool = True):
+    """Device-time every outermost collective on a device tensor: a timing event pair around it on the caller's
+    stream (the span a compute kernel behind it waits for: RCCL on the comm stream or the one-shot kernel,
+    including any wait for slower peers).  Read with ``device_timing_collect``."""
+    _DEV_TIMING["on"] = bool(on)
+
+
+def device_timing_collect():
+    """(count, total seconds, per-name totals) of the collectives timed since the last collect; synchronises the
+    recorded events."""
+    evs, _DEV_TIMING["events"] = _DEV_TIMING["events"], []
+    tot, per = 0.0, {}
+    for name, s, e in evs:
+        e.synchronize()
+        dt = s.elapsed_time(e) * 1e-3
+        tot += dt
+        per[name] = per.get(name, 0.0) + dt
+    return len(evs), tot, per
+
+
 def _collective(fn):
     """Time a collective (host wall time into ``STATS.time_s``; a ``collective`` span with device timing on the
-    tracer's gpu track when tracing is on).  Nested collectives (e.g. the count exchange inside an all-to-all)
-    are timed once, by the outermost call."""
+    tracer's gpu track when tracing is on; device events under ``device_timing``).  Nested collectives (e.g. the
+    count exchange inside an all-to-all) are timed once, by the outermost call."""
     name = fn.__name__
 
     @functools.wraps(fn)
@@ -71,6 +97,10 @@ def _collective(fn):
         t = a[0] if a and isinstance(a[0], torch.Tensor) else None
         _NEST.v = True
         t0 = time.perf_counter()
+        ev = None
+        if _DEV_TIMING["on"] and t is not None and t.is_cuda:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record(torch.cuda.current_stream(t.device))
         try:
             if _trace.enabled():
                 nb = int(t.numel() * t.element_size()) if t is not None else 0
@@ -79,6 +109,9 @@ def _collective(fn):
                     return fn(*a, **kw)
             return fn(*a, **kw)
         finally:
+            if ev is not None:
+                ev[1].record(torch.cuda.current_stream(t.device))
+                _DEV_TIMING["events"].append((name, ev[0], ev[1]))
             STATS.time_s += time.perf_counter() - t0
             _NEST.v = False
     return wrapper
@@ -88,8 +121,16 @@ import threading as _threading  # noqa: E402
 _NEST = _threading.local()
 
 
+def force_collective() -> bool:
+    """``ALINK_COMM_FORCE_COLLECTIVE=1``: a 1-rank group still runs every collective (test / rehearsal switch)."""
+    return os.environ.get("ALINK_COMM_FORCE_COLLECTIVE", "0") == "1"
+
+
 def is_distributed() -> bool:
-    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+    """True when collectives must run: a multi-rank group, or any group under ``force_collective()``."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return False
+    return dist.get_world_size() > 1 or force_collective()
 
 
 def get_rank() -> int:
@@ -116,10 +157,20 @@ def init_distributed(backend: Optional[str] = None, timeout_s: float = 1800.0) -
     if not dist.is_available():
         return False
     if dist.is_initialized():
-        return dist.get_world_size() > 1
+        return is_distributed()
     ws = int(os.environ.get("WORLD_SIZE", "1"))
-    if ws <= 1:
+    if ws <= 1 and not force_collective():
         return False
+    if ws <= 1:
+        # forced 1-rank group (no launcher): rank 0 of 1 on a private rendezvous port
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
+        os.environ.setdefault("LOCAL_RANK", "0")
+        if "MASTER_PORT" not in os.environ:
+            import socket
+            with socket.socket() as sk:
+                sk.bind(("127.0.0.1", 0))
+                os.environ["MASTER_PORT"] = str(sk.getsockname()[1])
     if backend is None:
         backend = os.environ.get("ALINK_DIST_BACKEND")
     if backend is None:
@@ -140,21 +191,31 @@ def init_distributed(backend: Optional[str] = None, timeout_s: float = 1800.0) -
         _OBJ_GROUP = dist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=timeout_s))
     else:
         _OBJ_GROUP = None
-    return True
+    return is_distributed()
 
 
 def shutdown():
+    """Tear down the one-shot staging and the process groups.  A one-shot timeout on the job's LAST reduction
+    (which no later call would check) is raised here, after the cleanup."""
     global _OBJ_GROUP
     from . import oneshot
+    failure = None
     if oneshot._INSTANCE is not None and dist.is_available() and dist.is_initialized():
         # peers may still be reading this rank's staging slot in their last one-shot call: drain every rank's
         # stream, meet on the host group, then unmap / free
         torch.cuda.synchronize(oneshot._INSTANCE.device)
+        try:
+            oneshot._INSTANCE.check(wait=True)
+        except RuntimeError as e:
+            failure = e
         dist.barrier(group=_OBJ_GROUP)
     oneshot.reset()
     if dist.is_available() and dist.is_initialized():
         dist.destroy_process_group()
     _OBJ_GROUP = None
+    _COMM_STREAMS.clear()
+    if failure is not None:
+        raise failure
 
 
 def object_group():
@@ -171,7 +232,7 @@ def all_gather_arrays(arrays: List[np.ndarray], dtype=np.float64) -> List[List[n
     """Gather a list of variable-length 1-D arrays from every rank as TWO tensor collectives (lengths + one
     packed buffer over RCCL/gloo) instead of a pickled object gather: result[rank][j] = that rank's arrays[j]."""
     ws = get_world_size()
-    if ws == 1:
+    if not is_distributed():
         return [list(arrays)]
     dev = collective_device()
     lens = torch.tensor([int(a.size) for a in arrays], dtype=torch.int64)
@@ -297,7 +358,7 @@ def all_reduce_coalesced(ts: List[torch.Tensor], op: str = "sum") -> List[torch.
 def reduce_scatter(t: torch.Tensor, op: str = "sum") -> torch.Tensor:
     """Reduce-scatter along dim 0 (t.shape[0] must divide world size); returns this rank's block."""
     ws = get_world_size()
-    if ws == 1:
+    if not is_distributed():
         return t
     rop = getattr(dist.ReduceOp, _OPS[op.lower()])
     out = torch.empty((t.shape[0] // ws,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
@@ -349,7 +410,7 @@ def reduce_scatter_async(t: torch.Tensor, op: str = "sum") -> Pending:
     """Asynchronous ``reduce_scatter`` (dim 0 split over ranks): returns a ``Pending`` whose ``wait()`` yields
     this rank's block.  Used to overlap per-block histogram reductions with building the next block."""
     ws = get_world_size()
-    if ws == 1:
+    if not is_distributed():
         return Pending(t)
     rop = getattr(dist.ReduceOp, _OPS[op.lower()])
     STATS.calls += 1
@@ -401,7 +462,7 @@ def all_gather_varlen_async(t: torch.Tensor) -> Pending:
     """Asynchronous ``all_gather_varlen``: the (tiny) length exchange runs now, the padded payload gather is
     issued from the comm stream (RCCL) or gloo's thread; ``wait()`` returns the rank-order concatenation."""
     ws = get_world_size()
-    if ws == 1:
+    if not is_distributed():
         return Pending(t)
     n = torch.tensor([t.shape[0]], dtype=torch.int64)
     lens = all_gather_tensor(n).tolist()
@@ -437,7 +498,7 @@ def all_gather_varlen_async(t: torch.Tensor) -> Pending:
 def all_gather_tensor(t: torch.Tensor) -> torch.Tensor:
     """Concatenate equally-shaped tensors from all ranks along dim 0."""
     ws = get_world_size()
-    if ws == 1:
+    if not is_distributed():
         return t
     STATS.calls += 1
     if _backend() == "nccl":
@@ -455,7 +516,7 @@ def all_gather_tensor(t: torch.Tensor) -> torch.Tensor:
 def all_gather_varlen(t: torch.Tensor) -> torch.Tensor:
     """Concatenate tensors whose dim-0 length differs per rank (pads to the max length, one collective)."""
     ws = get_world_size()
-    if ws == 1:
+    if not is_distributed():
         return t
     n = torch.tensor([t.shape[0]], dtype=torch.int64)
     lens = all_gather_tensor(n).tolist()
@@ -472,7 +533,7 @@ def all_to_all_tensors(send: List[torch.Tensor]) -> List[torch.Tensor]:
     count exchange.  This is the request/response shuffle of the reference's ALS (``AlsTrain.java:283-389``)
     done as a single RCCL all-to-all(v)."""
     ws = get_world_size()
-    if ws == 1:
+    if not is_distributed():
         return [send[0]]
     dev = send[0].device
     tail = tuple(send[0].shape[1:])
@@ -500,7 +561,7 @@ def all_to_all_tensors(send: List[torch.Tensor]) -> List[torch.Tensor]:
 @_collective
 def all_gather_object(obj: Any) -> List[Any]:
     ws = get_world_size()
-    if ws == 1:
+    if not is_distributed():
         return [obj]
     out: List[Any] = [None] * ws
     STATS.calls += 1
@@ -510,7 +571,7 @@ def all_gather_object(obj: Any) -> List[Any]:
 
 @_collective
 def broadcast_object(obj: Any, src: int = 0) -> Any:
-    if get_world_size() == 1:
+    if not is_distributed():
         return obj
     box = [obj]
     STATS.calls += 1
@@ -527,7 +588,7 @@ def all_to_all_bytes(send: List[bytes]) -> List[bytes]:
     """Byte-string all-to-all: ``send[j]`` -> rank j, as one lengths + one packed uint8 ``all_to_all_single``
     (RCCL / gloo) — O(N) bytes in total, no gather of every rank's data on every rank."""
     ws = get_world_size()
-    if ws == 1:
+    if not is_distributed():
         return [send[0]]
     dev = collective_device()
     lens = [torch.tensor([len(b)], dtype=torch.int64, device=dev) for b in send]
@@ -547,7 +608,7 @@ def all_to_all_objects(send: List[Any]) -> List[Any]:
     strings travel as packed UTF-8 (lengths, -1 = None, + bytes); anything else as one pickled byte string per
     destination — both as tensor all-to-alls whose total traffic is the data itself."""
     ws = get_world_size()
-    if ws == 1:
+    if not is_distributed():
         return list(send)
     if all(_is_str_list(p) for p in send):
         flags = all_gather_object(True)
@@ -569,7 +630,7 @@ def all_to_all_strings(send) -> list:
     order).  Two tensor all-to-alls: per-string byte lengths (-1 marks NULL) and the concatenated bytes."""
     from ..common.strings import StringBlock
     ws = get_world_size()
-    if ws == 1:
+    if not is_distributed():
         return [send[0]]
     lens = [torch.where(b.null_mask(), torch.full_like(b.lengths(), -1), b.lengths()) for b in send]
     rl = all_to_all_tensors(lens)

@@ -3,7 +3,7 @@
 Every rank allocates an uncached staging area (two slots of ``cap_bytes`` + per-block flags), exports it with
 ``hipIpcGetMemHandle``, the handles are exchanged once over the host (gloo) group and opened on every peer.  An
 all-reduce is then one kernel on the caller's stream: copy-in, release a sequence number to every peer, poll
-the own flags, sum the P staging slots in rank order (for P <= 8 the P remote loads of an element are issued
+the own flags (wrap-safe: a flag at or past the call's sequence number counts), sum the P staging slots in rank order (for P <= 8 the P remote loads of an element are issued
 together, so a slice costs one xGMI round trip, not P).  No RCCL call, no host round trip, bit-identical results
 on all ranks.
 
@@ -38,6 +38,9 @@ __all__ = ["OneShot", "get", "enabled", "MAX_BYTES"]
 MAX_BYTES = int(os.environ.get("ALINK_ONESHOT_MAX_BYTES", str(1 << 20)))
 BLOCKS = 64
 TIMEOUT_S = float(os.environ.get("ALINK_ONESHOT_TIMEOUT_S", "300"))
+# the setup probe waits at most this long for peers: a node whose cross-GPU stores never become visible falls back
+# to RCCL after seconds instead of stalling the job for TIMEOUT_S
+PROBE_TIMEOUT_S = float(os.environ.get("ALINK_ONESHOT_PROBE_TIMEOUT_S", "20"))
 SYNC_CHECK = os.environ.get("ALINK_ONESHOT_CHECK", "0") == "1"
 _DT = {torch.float32: 0, torch.float64: 1}
 _OP = {"sum": 0, "max": 1, "min": 2}
@@ -101,7 +104,7 @@ class OneShot:
         return int(p.value)
 
     def launch(self, t: torch.Tensor, out: torch.Tensor, op: str = "sum", rank: Optional[int] = None,
-               phases: int = 3, seq: Optional[int] = None) -> torch.Tensor:
+               phases: int = 3, seq: Optional[int] = None, timeout_s: Optional[float] = None) -> torch.Tensor:
         n = t.numel()
         if t.dtype not in _DT or n * t.element_size() > self.cap:
             raise ValueError("one-shot all-reduce: unsupported dtype or buffer larger than the staging slot")
@@ -109,11 +112,12 @@ class OneShot:
             self.seq += 1
             seq = self.seq
         from ..utils import trace as _trace
+        tmo = TIMEOUT_S if timeout_s is None else float(timeout_s)
         with _trace.span("oneshot_allreduce", "kernel", device=True, bytes=int(n * t.element_size()), P=self.P):
             rc = self.L.alink_oneshot_allreduce(t.data_ptr(), out.data_ptr(), n, _DT[t.dtype], _OP[op], self.P,
                                                 self.rank if rank is None else rank, seq & 0xFFFFFFFF,
                                                 self.peer_data.data_ptr(), self.peer_flags.data_ptr(), self.cap,
-                                                BLOCKS, phases, TIMEOUT_S, self.err.data_ptr(), self._hword_dev,
+                                                BLOCKS, phases, tmo, self.err.data_ptr(), self._hword_dev,
                                                 _lib.stream_ptr(self.device))
         if rc != 0:
             raise RuntimeError(f"alink_oneshot_allreduce failed: {rc}")
@@ -142,12 +146,12 @@ class OneShot:
             self._raise_if_failed(int(self._err_host[0]))
             self._err_ev = None
 
-    def all_reduce_(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
+    def all_reduce_(self, t: torch.Tensor, op: str = "sum", timeout_s: Optional[float] = None) -> torch.Tensor:
         self.check()
         # in place: a block copies its slice of the input to the staging slot before it signals, and writes the
         # same slice of the result only after every rank's signal (no result buffer, no copy back)
         flat = t.view(-1) if t.is_contiguous() else t.reshape(-1).contiguous()
-        self.launch(flat, flat, op)
+        self.launch(flat, flat, op, timeout_s=timeout_s)
         if SYNC_CHECK:
             self._raise_if_failed(int(self.err.item()))
         elif self._hview is None and self._err_ev is None:
@@ -265,7 +269,7 @@ def get() -> Optional[OneShot]:
     probe = torch.arange(1000, dtype=torch.float64, device=dev) * (rank + 1) + 0.25
     ref = torch.arange(1000, dtype=torch.float64, device=dev) * (P * (P + 1) // 2) + 0.25 * P
     try:
-        got = inst.all_reduce_(probe.clone())
+        got = inst.all_reduce_(probe.clone(), timeout_s=min(TIMEOUT_S, PROBE_TIMEOUT_S))
         torch.cuda.synchronize(dev)
         good = 1.0 if torch.equal(got, ref) and int(inst.err.item()) == 0 else 0.0
         if not good:

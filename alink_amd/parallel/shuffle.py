@@ -97,29 +97,60 @@ def _object_strings(vals) -> StringBlock:
     return StringBlock.from_list(out)
 
 
-def _column_hash(c: Column) -> torch.Tensor:
-    """int64 [n] in [0, 2^32) on the column's device; NULL rows hash to a constant."""
-    from ..ops.strings import hash_bytes
+def _is_num(x) -> bool:
+    return isinstance(x, (int, float, np.integer, np.floating)) and not isinstance(x, bool)
+
+
+def _hash_kind(c: Column) -> str:
+    """How this rank's part of a column would hash on its own: ``num`` (numeric tensor, or numbers in an object
+    column), ``str`` (strings), ``null`` (nothing but NULLs: compatible with any kind) or ``obj`` (mixed)."""
     v = c.values
     if isinstance(v, torch.Tensor) and v.dim() == 1:
+        return "num"
+    if isinstance(v, StringBlock):
+        return "str"
+    vals = c.to_list()
+    if all(x is None for x in vals):
+        return "null"
+    if all(x is None or isinstance(x, str) for x in vals):
+        return "str"
+    if all(x is None or _is_num(x) for x in vals):
+        return "num"
+    return "obj"
+
+
+def _agree_kind(kinds) -> str:
+    """One hash kind every rank uses for a column (equal keys must hash equally wherever they live)."""
+    ks = {k for k in kinds if k != "null"}
+    if not ks:
+        return "num"
+    return ks.pop() if len(ks) == 1 else "obj"
+
+
+def _column_hash(c: Column, kind: str = None) -> torch.Tensor:
+    """int64 [n] in [0, 2^32) on the column's device; NULL rows hash to a constant.  ``kind`` (agreed across
+    ranks by ``key_hash``) forces the hash family; None = this column's own ``_hash_kind``."""
+    from ..ops.strings import hash_bytes
+    kind = kind or _hash_kind(c)
+    if kind == "null":
+        kind = "num"
+    v = c.values
+    if kind == "num" and isinstance(v, torch.Tensor) and v.dim() == 1:
         h = _numeric_hash(v)
         nulls = c.nulls.to(h.device) if c.nulls is not None else None
+    elif kind == "num":
+        # numbers in an object column hash as numbers (same bits as a numeric column of those values)
+        vals = c.to_list()
+        h = _numeric_hash(torch.tensor([0.0 if x is None else float(x) for x in vals], dtype=torch.float64))
+        nulls = torch.tensor([x is None for x in vals], dtype=torch.bool)
     else:
-        if isinstance(v, StringBlock):
+        if kind == "str" and isinstance(v, StringBlock):
             blk = v
+        elif kind == "str":
+            blk = StringBlock.from_list(c.to_list())
         else:
-            vals = c.to_list()
-            if all(x is None or isinstance(x, str) for x in vals):
-                blk = StringBlock.from_list(vals)
-            else:
-                # numbers in an object column hash as numbers (same bits as a numeric column of those values)
-                if all(x is None or (isinstance(x, (int, float, np.integer, np.floating)) and not isinstance(x, bool))
-                       for x in vals):
-                    h = _numeric_hash(torch.tensor([0.0 if x is None else float(x) for x in vals],
-                                                   dtype=torch.float64))
-                    nulls = torch.tensor([x is None for x in vals], dtype=torch.bool)
-                    return torch.where(nulls, torch.full_like(h, _NULL_HASH), h)
-                blk = _object_strings(vals)
+            # mixed on some rank: every rank hashes the Java string form of every value
+            blk = v if isinstance(v, StringBlock) else _object_strings(c.to_list())
         h = hash_bytes(blk).to(torch.int64) & _M32
         nulls = blk.nulls
     if nulls is not None:
@@ -128,11 +159,16 @@ def _column_hash(c: Column) -> torch.Tensor:
 
 
 def key_hash(mt: MTable, cols: Sequence[int]) -> np.ndarray:
-    """int64 non-negative hash of the key columns of every row (identical on every rank)."""
+    """int64 non-negative hash of the key columns of every row (identical on every rank).  Collective when the
+    job is distributed: the per-column hash family is agreed across ranks first."""
     n = mt.num_rows
+    kinds = [_hash_kind(mt.cols[c]) for c in cols]
+    if comm.is_distributed():
+        everyone = comm.all_gather_object(kinds)
+        kinds = [_agree_kind([k[i] for k in everyone]) for i in range(len(cols))]
     h = torch.zeros(n, dtype=torch.int64)
-    for c in cols:
-        hc = _column_hash(mt.cols[c]).cpu()
+    for c, kind in zip(cols, kinds):
+        hc = _column_hash(mt.cols[c], kind).cpu()
         h = (h * 31 + hc) & _M32
     return (h & 0x7FFFFFFF).numpy()
 
@@ -154,10 +190,12 @@ def exchange(mt: MTable, dest: np.ndarray) -> MTable:
     bounds = np.concatenate([[0], np.cumsum(counts)])
     me = comm.get_rank()
     STATS.rows_sent += int(mt.num_rows - counts[me])
-    # the string decision must agree across ranks (a column may be all-None on one rank)
-    is_str = [_is_string_column(c) for c in mt.cols]
-    agreed = comm.all_gather_object(is_str)
-    is_str = [all(a[i] for a in agreed) for i in range(len(mt.cols))]
+    # the string decision and the presence of a NULL mask must agree across ranks (a column may be all-None, or
+    # NULL-free, on some ranks only): ONE object gather of both, so every rank issues the same collectives
+    local = [(_is_string_column(c), c.nulls is not None) for c in mt.cols]
+    agreed = comm.all_gather_object(local)
+    is_str = [all(a[i][0] for a in agreed) for i in range(len(mt.cols))]
+    any_nulls = [any(a[i][1] for a in agreed) for i in range(len(mt.cols))]
     cols = []
     for ci, c in enumerate(mt.cols):
         v = c.values
@@ -170,7 +208,7 @@ def exchange(mt: MTable, dest: np.ndarray) -> MTable:
             STATS.tensor_bytes_recv += int(recv.numel() * recv.element_size())
             val = recv.reshape((recv.shape[0],) + tuple(v.shape[1:])) if v.dim() > 1 else recv[:, 0]
             nulls = None
-            if c.nulls is not None or any(x for x in comm.all_gather_object(c.nulls is not None)):
+            if any_nulls[ci]:
                 nm = c.nulls if c.nulls is not None else torch.zeros(v.shape[0], dtype=torch.bool)
                 nm = nm.cpu()[torch.as_tensor(order)]
                 nparts = [nm[bounds[j]:bounds[j + 1]].to(torch.uint8)[:, None] for j in range(ws)]

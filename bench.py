@@ -14,11 +14,18 @@ child processes with RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* set, started before thi
 GPU; rank 0's JSON line is the job's output; a failing or hung rank fails the job).
 
 Prints ONE JSON line on rank 0.  ``value`` = total rows processed per second by the whole job
-(rows x K / max-over-ranks elapsed).  Also reports ``iters_to_converge`` from separate untimed runs with
-epsilon 1e-4 at the reference default init (k-means|| initSteps=2, ``convergence.initSteps2``), plus initSteps=5
-for comparison (``convergence.initSteps5``).  The fused update holds each bf16 centroid operand while its fp64
-centroid stays within one bf16 ulp (ops/csrc/kmeans_common.hip), so Lloyd reaches an exactly stationary
-assignment; with plain re-quantisation every step it cycled at a ~2e-3 shift floor and never met epsilon.
+(rows x K / max-over-ranks elapsed).  Also reports ``iters_to_converge`` from a separate untimed run with
+epsilon 1e-4 at the reference defaults (k-means|| initSteps=2 and the reference's sampled k-means++ seeding over
+the candidates, ``convergence.reference``), plus the opt-in greedy seeding (``convergence.greedy``) and
+initSteps=5 for comparison; every run reports its final SSE (sum of squared distances to the nearest centroid)
+and live k.  The fused update holds each bf16 centroid operand while its fp64 centroid stays within one bf16 ulp
+(ops/csrc/kmeans_common.hip), so Lloyd reaches an exactly stationary assignment.
+
+Communication fields: ``comm_backend`` (nccl = RCCL, gloo, or none for a 1-rank job), ``oneshot_used`` (the
+[k, d+1] all-reduce went through the one-shot xGMI kernel), ``allreduce_us_per_step`` (device time of the
+superstep's collectives, event-timed on the compute stream, i.e. including the wait for the slowest rank) and
+``allreduce_calls_per_step``.  ``ALINK_COMM_FORCE_COLLECTIVE=1`` makes a 1-rank job run its collectives for
+real (the RCCL path of a multi-GPU job, on one GPU).
 """
 from __future__ import annotations
 
@@ -33,6 +40,25 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import torch  # noqa: E402
 
 METRIC = "rows/sec/node + iters-to-converge, KMeans k=100 1e8-row×128-dim at 1/2/4/8 MI355X"
+
+
+def _sse(data, op, dev) -> float:
+    """Sum over all rows (all ranks) of the squared Euclidean distance to the nearest centroid of ``op``'s model
+    (fp32 GEMM in 4M-row chunks, fp64 accumulation)."""
+    from alink_amd.models.clustering.kmeans import KMeansModelDataConverter
+    from alink_amd.parallel import comm
+    md = KMeansModelDataConverter().load(op.collect())
+    X = data.col("vec").values
+    C = torch.as_tensor(md.centroids, dtype=torch.float32, device=X.device)
+    cn = (C * C).sum(1)
+    tot = torch.zeros((), dtype=torch.float64, device=X.device)
+    for lo in range(0, X.shape[0], 1 << 22):
+        x = X[lo:lo + (1 << 22)].to(torch.float32)
+        d = (x * x).sum(1, keepdim=True) - 2.0 * (x @ C.T) + cn[None, :]
+        tot += d.min(1).values.clamp_min(0).sum(dtype=torch.float64)
+    t = tot.reshape(1).to(comm.collective_device())
+    comm.all_reduce(t)
+    return float(t.item())
 
 
 def main():
@@ -84,6 +110,12 @@ def main():
             if dev.type == "cuda":
                 torch.cuda.synchronize(dev)
             marks[step] = time.perf_counter()
+            if step == a.warmup:
+                comm.device_timing_collect()                  # drop warmup events
+                marks["oneshot0"] = comm.STATS.oneshot
+                comm.device_timing(dev.type == "cuda")
+            else:
+                comm.device_timing(False)
 
     op = KMeansTrainBatchOp().setVectorCol("vec").setK(a.k).setMaxIter(a.warmup + a.steps).setEpsilon(-1.0)
     op._on_step = on_step
@@ -98,36 +130,44 @@ def main():
         raise SystemExit("--warmup must be >= 1 (the first superstep includes one-time setup)")
     elapsed = marks[a.warmup + a.steps] - marks[a.warmup]
     el = torch.tensor([elapsed], dtype=torch.float64)
-    comm.all_reduce(el, "max")
-    elapsed = float(el.item())
+    n_ev, dev_comm_s, _ = comm.device_timing_collect()
+    oneshot_calls = comm.STATS.oneshot - marks.get("oneshot0", comm.STATS.oneshot)
+    comm_backend = comm._backend() if comm.is_distributed() else "none"
+    el_max = el.clone()
+    comm.all_reduce(el_max, "max")
+    elapsed = float(el_max.item())
+    cst = torch.tensor([dev_comm_s], dtype=torch.float64)
+    comm.all_reduce(cst, "max")
+    dev_comm_s = float(cst.item())
     stats = op._queue.stats[a.warmup:a.warmup + a.steps]
     live_k = int(op._queue.final_contexts[0].getObj("k"))
     comm_bytes = sum(s["comm_bytes"] for s in stats) / max(1, len(stats))
+    timed_sse = _sse(data, op, dev)
 
-    # ---- convergence runs (epsilon 1e-4): reference default initSteps=2, initSteps=5, and initSteps=2 with the
-    # reference's own k-means++ seeding rule on the k-means|| candidates (ALINK_KMEANS_SEEDING=reference) ----
+    # ---- convergence runs (epsilon 1e-4): the reference defaults (k-means|| initSteps=2, the reference's sampled
+    # k-means++ seeding over the candidates), the opt-in greedy seeding, and initSteps=5 ----
     iters, conv = None, {}
     if a.converge_iters > 0:
-        for tag, steps, seeding in (("initSteps2", 2, None), ("initSteps5", 5, None),
-                                    ("reference_seeding", 2, "reference")):
+        for tag, steps, seeding in (("reference", 2, "reference"), ("greedy", 2, "greedy"),
+                                    ("initSteps5", 5, "reference")):
             old = os.environ.get("ALINK_KMEANS_SEEDING")
-            if seeding is not None:
-                os.environ["ALINK_KMEANS_SEEDING"] = seeding
+            os.environ["ALINK_KMEANS_SEEDING"] = seeding
             t_c = time.perf_counter()
             op2 = KMeansTrainBatchOp().setVectorCol("vec").setK(a.k).setMaxIter(a.converge_iters) \
                 .setInitSteps(steps)
             op2.linkFrom(TableSourceBatchOp(data))
+            wall = time.perf_counter() - t_c
             info = op2.getTrainInfo()
-            if seeding is not None:
-                if old is None:
-                    os.environ.pop("ALINK_KMEANS_SEEDING", None)
-                else:
-                    os.environ["ALINK_KMEANS_SEEDING"] = old
+            if old is None:
+                os.environ.pop("ALINK_KMEANS_SEEDING", None)
+            else:
+                os.environ["ALINK_KMEANS_SEEDING"] = old
             shift = (info["max_shift"] or [None])[-1]
-            conv[tag] = {"iters": info["iterations"], "wall_s": time.perf_counter() - t_c,
+            conv[tag] = {"iters": info["iterations"], "wall_s": wall, "initSteps": steps,
                          "final_max_shift": shift, "converged": shift is not None and shift < 1e-4,
-                         "seeding": seeding or "greedy k-means++ (default)"}
-        iters = conv["initSteps2"]["iters"]
+                         "seeding": seeding, "live_k": int(op2._queue.final_contexts[0].getObj("k")),
+                         "sse": _sse(data, op2, dev)}
+        iters = conv["reference"]["iters"]
 
     rows_per_s = a.rows * a.steps / elapsed
     res = {
@@ -148,17 +188,21 @@ def main():
                    "parallelism": f"dp{env.world_size}"},
         "rows_per_s_per_gpu": rows_per_s / env.world_size,
         "iters_to_converge": iters,
-        "iters_to_converge_setting": "epsilon 1e-4, k-means|| initSteps=2 (reference default); initSteps=5 "
-                                     "under convergence.initSteps5; the reference's sampled k-means++ seeding "
-                                     "under convergence.reference_seeding",
-        "iters_to_converge_reference_seeding": conv.get("reference_seeding", {}).get("iters"),
+        "iters_to_converge_setting": "epsilon 1e-4 (max centroid shift), maxIter 100, k-means|| initSteps=2 with "
+                                     "the reference's sampled k-means++ seeding over the candidates (the "
+                                     "reference defaults); convergence.greedy = opt-in greedy seeding, "
+                                     "convergence.initSteps5 = initSteps 5",
+        "converged": conv.get("reference", {}).get("converged"),
         "convergence": conv,
-        "iters_to_converge_default_init": conv.get("initSteps2", {}).get("iters"),
-        "converged_default_init": conv.get("initSteps2", {}).get("converged"),
         "live_k": live_k,
+        "sse_timed_run": timed_sse,
         "effective_config": {"k_requested": a.k, "k_live_in_timed_run": live_k, "init": "K_MEANS_PARALLEL",
-                             "initSteps_timed_run": 2, "epsilon_timed_run": -1.0,
+                             "initSteps_timed_run": 2, "seeding": "reference", "epsilon_timed_run": -1.0,
                              "rows_per_rank": a.rows // env.world_size, "device": str(dev)},
+        "comm_backend": comm_backend,
+        "oneshot_used": oneshot_calls > 0,
+        "allreduce_us_per_step": dev_comm_s / a.steps * 1e6,
+        "allreduce_calls_per_step": n_ev / a.steps,
         "allreduce_bytes_per_step": comm_bytes,
         "hip_kernels": bool(hip_used),
         "datagen_s": t_gen,

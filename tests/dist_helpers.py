@@ -117,12 +117,12 @@ def scenario_gbdt_many(out):
     useLocalEnv(1)
     src = BatchOperator.fromDataframe(df, schemaStr=", ".join(f"x{i} double" for i in range(200)) + ", y int")
     before = TreeBuilder.SHARDED_SEARCHES
-    nrs = len(TreeBuilder.RS_BYTES)
+    nrs = TreeBuilder.RS_CALLS
     m = GbdtTrainBatchOp().setFeatureCols([f"x{i}" for i in range(200)]).setLabelCol("y").setNumTrees(2) \
         .setMinSamplesPerLeaf(5).setMaxDepth(4).linkFrom(src)
     out["model"] = [list(r) for r in m.collect()]
     out["sharded"] = TreeBuilder.SHARDED_SEARCHES - before
-    out["rs_calls"] = len(TreeBuilder.RS_BYTES) - nrs
+    out["rs_calls"] = TreeBuilder.RS_CALLS - nrs
 
 
 def scenario_rf(out):
@@ -382,6 +382,27 @@ def scenario_shuffle_strings(out):
                  [Column(fixed), Column(torch.arange(len(fixed), dtype=torch.int64))])
     out["hash_sample"] = shuffle.key_hash(fmt, [0, 1]).tolist()
     out["hash_keys"] = [str(x) for x in fixed]
+
+
+def scenario_shuffle_partial_nulls(out):
+    """Only rank 0's value column carries a NULL mask, and the object key column holds numbers on rank 0 but a
+    mix of numbers and strings on rank 1: every rank must issue the same collectives (no deadlock) and equal
+    keys must co-locate (one agreed hash family per column)."""
+    import torch
+    from alink_amd.common.table import Column, MTable
+    from alink_amd.common.types import TableSchema, Types
+    from alink_amd.parallel import comm, shuffle
+    comm.init_distributed()
+    me = comm.get_rank()
+    n = 40
+    v = torch.arange(n, dtype=torch.float64) + 1000 * me
+    nulls = (torch.arange(n) % 5 == 0) if me == 0 else None
+    keys = [i % 7 for i in range(n)] if me == 0 else [(i % 7 if i % 3 else str(i % 7)) for i in range(n)]
+    mt = MTable(TableSchema(["k", "v"], [Types.STRING, Types.DOUBLE]), [Column(keys), Column(v, nulls)])
+    part = shuffle.hash_partition(mt, [0])
+    out["rows"] = [[str(r[0]), r[1]] for r in part.rows()]
+    out["sent"] = [[str(k), (None if nulls is not None and bool(nulls[i]) else float(v[i]))]
+                   for i, k in enumerate(keys)]
 
 
 def scenario_gather(out):

@@ -63,6 +63,40 @@ def scenario_kmeans(out):
     out["device"] = str(env.device)
 
 
+def scenario_kmeans_headline(out):
+    """The bench's configuration (bf16 Gaussian mixture, k=100, d=128, k-means|| init with the reference
+    seeding) at ``ALINK_REH_ROWS`` rows (default 1e8) for ``ALINK_REH_ITERS`` Lloyd supersteps: the model, the
+    one-shot count and the device time of the supersteps' collectives."""
+    import torch
+    from alink_amd import useLocalEnv, KMeansTrainBatchOp, RandomVectorSourceBatchOp
+    from alink_amd.operator.batch.source import TableSourceBatchOp
+    from alink_amd.parallel import comm, oneshot
+    env = useLocalEnv(1)
+    rows = int(float(os.environ.get("ALINK_REH_ROWS", "1e8")))
+    iters = int(os.environ.get("ALINK_REH_ITERS", "8"))
+    src = RandomVectorSourceBatchOp().setNumRows(rows).setSize(128).setNumClusters(100).setClusterStd(1.0) \
+        .setCenterScale(4.0).setDtype("bf16").setSeed(2024).setOutputCol("vec")
+    data = src.getOutputTable()
+    comm.device_timing(env.device.type == "cuda")
+    op = KMeansTrainBatchOp().setVectorCol("vec").setK(100).setMaxIter(iters).setEpsilon(-1.0) \
+        .linkFrom(TableSourceBatchOp(data))
+    res = op.collect()
+    comm.device_timing(False)
+    n_ev, dev_s, per = comm.device_timing_collect()
+    out["model"] = [[r[0], r[1]] for r in res]
+    out["iterations"] = op.getTrainInfo()["iterations"]
+    out["oneshot_calls"] = comm.STATS.oneshot
+    out["oneshot_P"] = oneshot._INSTANCE.P if oneshot._INSTANCE is not None else None
+    out["oneshot_setup_error"] = oneshot.SETUP_ERROR
+    out["backend"] = comm._backend()
+    out["rows_local"] = int(data.num_rows)
+    out["collective_device_us"] = {k: round(v * 1e6, 1) for k, v in per.items()}
+    out["collectives_timed"] = n_ev
+    out["device"] = str(env.device)
+    if env.device.type == "cuda":
+        torch.cuda.synchronize()
+
+
 def scenario_gbdt(out):
     """GBDT with 160 continuous features on the GPU: the feature-sharded histogram (fixed-point kernel over this
     rank's 32-feature pieces) and the pipelined asynchronous reduce-scatter with device tensors."""
@@ -80,12 +114,12 @@ def scenario_gbdt(out):
     env = useLocalEnv(1)
     src = BatchOperator.fromDataframe(df, schemaStr=", ".join(f"x{i} double" for i in range(160)) + ", y int")
     before = TreeBuilder.SHARDED_SEARCHES
-    nrs = len(TreeBuilder.RS_BYTES)
+    nrs = TreeBuilder.RS_CALLS
     m = GbdtTrainBatchOp().setFeatureCols([f"x{i}" for i in range(160)]).setLabelCol("y").setNumTrees(3) \
         .setMinSamplesPerLeaf(10).setMaxDepth(5).linkFrom(src)
     out["model"] = [list(r) for r in m.collect()]
     out["sharded"] = TreeBuilder.SHARDED_SEARCHES - before
-    out["rs_calls"] = len(TreeBuilder.RS_BYTES) - nrs
+    out["rs_calls"] = TreeBuilder.RS_CALLS - nrs
     out["backend"] = comm._backend()
     out["device"] = str(env.device)
 

@@ -333,6 +333,21 @@ def test_string_shuffle_packed_bytes_balanced(tmp_path, world):
     assert len(set(outs[0]["hash_sample"])) == len(outs[0]["hash_sample"])
 
 
+@pytest.mark.parametrize("world", [2, 3])
+def test_shuffle_nulls_on_some_ranks_and_mixed_key_kinds(tmp_path, world):
+    """NULL masks on a subset of ranks and per-rank differing object-key kinds: the exchange completes, no row is
+    lost, NULLs survive, and every key (1 and '1' hash alike as strings once any rank mixes kinds) has one owner."""
+    outs = _run("shuffle_partial_nulls", world, tmp_path)
+    sent = sorted(map(json.dumps, (r for o in outs for r in o["sent"])))
+    recv = sorted(map(json.dumps, (r for o in outs for r in o["rows"])))
+    assert sent == recv
+    assert any(r[1] is None for o in outs for r in o["rows"])
+    owner = {}
+    for r, o in enumerate(outs):
+        for k, _ in o["rows"]:
+            assert owner.setdefault(k, r) == r, k
+
+
 def test_gather_table_columnar_three_ranks(tmp_path):
     """gather_table (collect, sinks, tuning, pipeline save) concatenates partitions in rank order with native
     column transport: tensors + null masks, sparse blocks and packed strings; objects pickled."""

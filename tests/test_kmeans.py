@@ -74,7 +74,7 @@ def test_kmeans_init_modes_and_cosine(init):
 
 
 def test_reference_seeding_rule_flag(monkeypatch):
-    """ALINK_KMEANS_SEEDING=reference: one sampled candidate per pick (LocalKmeansFunc); both rules give k
+    """Default (reference) rule: one sampled candidate per pick (LocalKmeansFunc); greedy opt-in; both give k
     distinct centroids from the candidate set."""
     import torch
     from alink_amd.models.clustering.kmeans import _local_kmeans

@@ -66,3 +66,68 @@ def test_oneshot_missing_peer_times_out_with_nan(monkeypatch):
     assert torch.equal(y, ref)
     one.close()
     v.close()
+
+
+def _fold_sum(xs):
+    acc = xs[0].clone()
+    for x in xs[1:]:
+        acc = acc + x
+    return acc
+
+
+def test_oneshot_peer_already_signalled_next_call():
+    """Wrap-safe poll: peers 1 and 2 finish call s and signal call s+1 before rank 0's wave first polls for
+    s (a preempted wave, ranks time-sharing a GPU).  Rank 0's flags then read s+1, never s; it must still
+    complete call s from the untouched slot s&1, and then call s+1."""
+    P, cap = 3, 1 << 16
+    bases = [OneShot.alloc(cap, P) for _ in range(P)]
+    views = [OneShot("cuda", P, r, cap, bases, [], []) for r in range(P)]
+    try:
+        n = 4000
+        s = 7
+        xa = [torch.randn(n, device="cuda", dtype=torch.float64) for _ in range(P)]
+        xb = [torch.randn(n, device="cuda", dtype=torch.float64) for _ in range(P)]
+        oa = [torch.empty_like(x) for x in xa]
+        ob = [torch.empty_like(x) for x in xb]
+        for r in range(P):
+            views[r].launch(xa[r], oa[r], "sum", phases=1, seq=s)
+        for r in (1, 2):
+            views[r].launch(xa[r], oa[r], "sum", phases=2, seq=s)
+            views[r].launch(xb[r], ob[r], "sum", phases=1, seq=s + 1)      # now one call ahead of rank 0
+        views[0].launch(xa[0], oa[0], "sum", phases=2, seq=s)
+        torch.cuda.synchronize()
+        assert int(views[0].err.item()) == 0
+        views[0].launch(xb[0], ob[0], "sum", phases=1, seq=s + 1)
+        for r in range(P):
+            views[r].launch(xb[r], ob[r], "sum", phases=2, seq=s + 1)
+        torch.cuda.synchronize()
+        ra, rb = _fold_sum(xa), _fold_sum(xb)
+        for r in range(P):
+            assert torch.equal(oa[r], ra) and torch.equal(ob[r], rb), r
+        assert all(int(v.err.item()) == 0 for v in views)
+    finally:
+        views[0].owned = bases
+        views[0].close()
+
+
+def test_oneshot_sequence_number_wraps():
+    """Sequence numbers are 32-bit: calls 2^32-2, 2^32-1, 0, 1 reduce correctly (the slot alternates with the
+    low bit, the arrival test is modular)."""
+    P, cap = 2, 1 << 14
+    bases = [OneShot.alloc(cap, P) for _ in range(P)]
+    views = [OneShot("cuda", P, r, cap, bases, [], []) for r in range(P)]
+    try:
+        for s in (0xFFFFFFFE, 0xFFFFFFFF, 0x100000000, 0x100000001):
+            xs = [torch.randn(300, device="cuda", dtype=torch.float32) for _ in range(P)]
+            outs = [torch.empty_like(x) for x in xs]
+            for r in range(P):
+                views[r].launch(xs[r], outs[r], "sum", phases=1, seq=s)
+            for r in range(P):
+                views[r].launch(xs[r], outs[r], "sum", phases=2, seq=s)
+            torch.cuda.synchronize()
+            ref = _fold_sum(xs)
+            assert all(torch.equal(o, ref) for o in outs), hex(s)
+        assert all(int(v.err.item()) == 0 for v in views)
+    finally:
+        views[0].owned = bases
+        views[0].close()

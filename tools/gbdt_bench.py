@@ -75,7 +75,7 @@ def main():
                       "s_per_tree": ((info or {}).get("trees_s") or dt) / a.trees,
                       # histogram calls of the whole run (root + one per level per tree): the full-width bytes
                       # every rank reduce-scatters, and what one rank sends = (P-1)/P of it at P = --ranks
-                      "hist_bytes_per_level_tree0": TreeBuilder.HIST_BYTES[:a.depth],
+                      "hist_bytes_per_level_tree0": list(TreeBuilder.HIST_BYTES)[:a.depth],
                       "reduce_scatter_send_bytes_per_rank_per_tree": int(sum(TreeBuilder.HIST_BYTES) / a.trees
                                                                           * (a.ranks - 1) / a.ranks),
                       "projected_ranks": a.ranks}))

@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--scenario", default="kmeans")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "rehearsal"))
     ap.add_argument("--timeout", type=int, default=240)
+    ap.add_argument("--compare", default=None, help="a <scenario>_1_0.json of a 1-rank run: compare the KMeans "
+                    "model of every rank with it (tests/test_multiprocess_gpu.py tolerances)")
     a = ap.parse_args()
     os.makedirs(a.out, exist_ok=True)
     port = _port()
@@ -80,8 +82,38 @@ def main():
             "gpu_track_kernels": {k: {"n": len(v), "mean_us": round(sum(v) / len(v), 2)} for k, v in sorted(kern.items())},
             "scenario_oneshot_calls": res.get("oneshot_calls"), "backend": res.get("backend"),
             "oneshot_setup_error": res.get("oneshot_setup_error"), "error": (res.get("error") or "")[-400:]})
+    if a.compare:
+        summary["compare"] = _compare(a.compare, [os.path.join(a.out, f"{a.scenario}_{a.world}_{r}.json")
+                                                  for r in range(a.world)])
     print(json.dumps(summary))
     return 0
+
+
+def _compare(ref_path, rank_paths):
+    """Every rank's model bit-identical to rank 0's; rank 0's centroids equal to the 1-rank run's up to fp32
+    partial-sum rounding (weights within max(2, 1e-4 w), coordinates rtol = atol = 1e-4)."""
+    import numpy as np
+    with open(ref_path) as f:
+        one = json.load(f)
+    outs = []
+    for p in rank_paths:
+        with open(p) as f:
+            outs.append(json.load(f))
+    a = [json.loads(r[1]) for r in one["model"] if r[0] > 0]
+    b = [json.loads(r[1]) for r in outs[0]["model"] if r[0] > 0]
+    res = {"ranks_identical": all(o["model"] == outs[0]["model"] for o in outs),
+           "iterations": [one.get("iterations"), outs[0].get("iterations")], "k": [len(a), len(b)]}
+    if len(a) == len(b):
+        dw = [abs(x["weight"] - y["weight"]) for x, y in zip(a, b)]
+        dv = [float(np.max(np.abs(np.asarray(x["vec"]["data"]) - np.asarray(y["vec"]["data"])))) for x, y in zip(a, b)]
+        res["max_weight_diff"] = max(dw)
+        res["max_coord_diff"] = max(dv)
+        res["within_tolerance"] = all(d <= max(2.0, 1e-4 * x["weight"]) for d, x in zip(dw, a)) and \
+            all(np.allclose(np.asarray(x["vec"]["data"]), np.asarray(y["vec"]["data"]), rtol=1e-4, atol=1e-4)
+                for x, y in zip(a, b))
+    else:
+        res["within_tolerance"] = False
+    return res
 
 
 if __name__ == "__main__":
