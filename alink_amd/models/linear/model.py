@@ -6,7 +6,11 @@ SoftmaxModelMapper}.java``, ``A/operator/common/regression/AFTModelMapper.java``
 Model table = ``LabeledModelDataConverter`` layout: meta row (modelName, hasInterceptItem, linearModelType,
 [vectorCol, vectorSize], labelCol), one data row with the Gson JSON of ``ModelData``
 (``featureColNames``, ``featureColTypes``, ``coefVector``, ``coefVectors``; nulls written) and the label
-values as auxiliary rows in the ``label_value`` column.
+values as auxiliary rows in the ``label_value`` column.  Also loaded: label values carried in the meta
+(``labelValues``, ``LinearModelDataConverter.java:61-64``), and the legacy 4-column format still written by
+PAI online learning (``LinearModelDataConverter.java:77-85`` -> ``LinearModelData.loadOldFromatModel``
+``:116-157``): meta JSON at id 0, the data JSON split over ids 1.., labels recovered from the meta
+``labelValues`` typed by ``labelTypeName``.
 
 Prediction is batched: the partition's features become one FeatureMatrix and margins are a single GEMV
 (GEMM for softmax) on the device; detail strings are formatted on the host.
@@ -44,6 +48,9 @@ VECTOR_COL = ParamInfo("vectorCol", str, "vector column")
 VECTOR_SIZE = ParamInfo("vectorSize", int, "vector size")
 LABEL_COL = ParamInfo("labelCol", str, "label column")
 NUM_CLASSES = ParamInfo("numClasses", int, "number of classes")
+LABEL_VALUES = "labelValues"                                      # ModelParamName.LABEL_VALUES (Object[])
+LABEL_TYPE_NAME = ParamInfo("labelTypeName", str, "label type name", alias=("labelType",))
+IS_OLD_FORMAT = ParamInfo("isOldFormat", bool, "legacy 4-column model")
 
 _TYPE_NAMES = {Types.DOUBLE: "double", Types.FLOAT: "float", Types.LONG: "long", Types.INT: "int",
                Types.SHORT: "short", Types.BOOLEAN: "bool", Types.BYTE: "byte", Types.DECIMAL: "double"}
@@ -108,8 +115,19 @@ class LinearModelDataConverter(LabeledModelDataConverter):
         m.vectorSize = meta.get(VECTOR_SIZE) if meta.contains(VECTOR_SIZE) else 0
         m.vectorColName = meta.get(VECTOR_COL) if meta.contains(VECTOR_COL) else None
         m.labelName = meta.get(LABEL_COL) if meta.contains(LABEL_COL) else None
-        m.labelValues = list(labels) if labels else None
         m.labelType = self.labelType
+        m.labelValues = None
+        if meta.contains(LABEL_VALUES):
+            raw = meta.get(LABEL_VALUES)
+            if isinstance(raw, str):
+                raw = json.loads(raw)
+            m.labelValues = [_recover_label(v, m.labelType) for v in raw] if raw is not None else None
+        if labels:
+            # the auxiliary label rows win (the reference overrides the meta values with them; an EMPTY aux
+            # list keeps the meta values here instead of erasing them)
+            m.labelValues = list(labels)
+        if len(data) != 1:
+            raise RuntimeError("Not valid model.")
         d = json.loads(data[0])
         m.featureNames = d.get("featureColNames")
         m.featureTypes = d.get("featureColTypes")
@@ -124,9 +142,33 @@ class LinearModelDataConverter(LabeledModelDataConverter):
 
     def load(self, rows):
         rows = [tuple(r) for r in rows]
-        if rows and len(rows[0]) == 4:
-            raise NotImplementedError("legacy 4-column linear model format is not supported")
+        if rows and len(rows[0]) == 4:         # old format model, still used in PAI online learning
+            return self._load_old_format(rows)
         return super().load(rows)
+
+    def _load_old_format(self, rows) -> LinearModelData:
+        """``LinearModelData.loadOldFromatModel``: rows (id, string, *, *); id 0 = meta JSON, ids 1..m-1 = the
+        data JSON in pieces, concatenated in id order up to the first missing id."""
+        from ...common.types import type_from_str
+        m = len(rows)
+        meta_str, pieces = "", [None] * m
+        for r in rows:
+            idx = int(r[0])
+            if idx == 0:
+                meta_str = r[1]
+            elif 1 <= idx <= m:
+                pieces[idx - 1] = r[1]
+        buf = []
+        for p in pieces:
+            if p is None:
+                break
+            buf.append(p)
+        meta = Params.fromJson(meta_str)
+        meta.set(IS_OLD_FORMAT, True)
+        # recoverLabelsFromOldFormatModel: the label type is the meta's Flink type string
+        label_type = type_from_str(meta.get(LABEL_TYPE_NAME)) if meta.contains(LABEL_TYPE_NAME) else self.labelType
+        conv = LinearModelDataConverter(label_type)
+        return conv.deserializeModel(meta, ["".join(buf)], [])
 
 
 def _recover_label(v, t: Optional[AlinkType]):
@@ -163,8 +205,10 @@ class _LinearMapperBase(RichModelMapper):
     def loadModel(self, modelRows):
         conv = LinearModelDataConverter(LinearModelDataConverter.extractLabelType(self.modelSchema))
         self.model = conv.load(modelRows)
+        if self.model.labelType is None:
+            self.model.labelType = conv.labelType
         if self.model.labelValues is not None:
-            self.model.labelValues = [_recover_label(v, conv.labelType) for v in self.model.labelValues]
+            self.model.labelValues = [_recover_label(v, self.model.labelType) for v in self.model.labelValues]
         if self.vector_col is None and self.model.featureNames is None:
             self.vector_col = self.model.vectorColName
         # rebuild helper with the resolved prediction type

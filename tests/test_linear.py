@@ -122,3 +122,70 @@ def test_lasso_sparsity_and_pipeline_save_load(tmp_path):
     p2 = pm2.transform(b).collectToDataframe()["p"].values
     np.testing.assert_allclose(p1, p2)
     assert np.corrcoef(p1, y)[0, 1] > 0.99
+
+
+def _legacy_rows(rows, chunk=9):
+    """The reference's old 4-column layout (LinearModelData.loadOldFromatModel): id 0 = meta JSON (with the label
+    values and the Flink label type name), ids 1.. = the ModelData JSON cut into pieces, two unused columns."""
+    from alink_amd.common.params import Params
+    meta = Params.fromJson(rows[0][1])
+    labels = [r[2] for r in rows[2:]]
+    meta.set("labelValues", labels)
+    meta.set("labelTypeName", "INT")
+    data = rows[1][1]
+    pieces = [data[i:i + chunk] for i in range(0, len(data), chunk)]
+    out = [(0, meta.toJson(), None, None)] + [(i + 1, p, None, None) for i, p in enumerate(pieces)]
+    return out[::-1]                                   # row order must not matter (ids order the pieces)
+
+
+def test_legacy_four_column_linear_model_predicts_like_three_column():
+    """Legacy 4-column LR model (LinearModelDataConverter.java:77-85 -> LinearModelData.java:116-157) == its
+    3-column equivalent in batch predict, LocalPredictor (detail included) and as the FTRL warm start."""
+    from alink_amd import LogisticRegressionModel, FtrlTrainStreamOp, StreamOperator, CollectStreamOp
+    from alink_amd.common.table import MTable
+    from alink_amd.common.types import schema_str_to_schema
+    from alink_amd.models.linear.model import LinearModelDataConverter
+    from alink_amd.operator.batch.source import TableSourceBatchOp
+    b = _op(label_last=2)
+    model = LogisticRegressionTrainBatchOp().setFeatureCols(["f0", "f1"]).setLabelCol("label").linkFrom(b)
+    rows = [tuple(r) for r in model.collect()]
+    legacy = MTable.from_rows(_legacy_rows(rows), schema_str_to_schema(
+        "model_id bigint, model_info string, label_value string, model_extra string"), replicated=True)
+    m3 = LinearModelDataConverter().load(rows)
+    m4 = LinearModelDataConverter().load(legacy.rows())
+    assert m4.labelValues == [2, 1] and m4.coefVector.data.tolist() == m3.coefVector.data.tolist()
+    assert m4.featureNames == ["f0", "f1"] and m4.linearModelType.name == "LR"
+    p3 = LogisticRegressionPredictBatchOp().setPredictionCol("p").setPredictionDetailCol("d").linkFrom(model, b) \
+        .collect()
+    p4 = LogisticRegressionPredictBatchOp().setPredictionCol("p").setPredictionDetailCol("d") \
+        .linkFrom(TableSourceBatchOp(legacy), b).collect()
+    assert [tuple(r) for r in p4] == [tuple(r) for r in p3]
+    lp = LogisticRegressionModel().setPredictionCol("p").setPredictionDetailCol("d").setModelData(legacy) \
+        .getLocalPredictor("f0 int, f1 int, label int")
+    assert [tuple(lp.map(r[:3])) for r in b.collect()] == [tuple(r) for r in p3]
+    # FTRL warm start from either format: identical snapshots
+    df = pd.DataFrame({"f0": DATA[:, 0], "f1": DATA[:, 1], "label": [1, 1, 2, 1, 1, 2, 1, 2]})
+    snaps = {}
+    for tag, init in (("three", model), ("four", TableSourceBatchOp(legacy))):
+        got = []
+        FtrlTrainStreamOp(init).setFeatureCols(["f0", "f1"]).setLabelCol("label").setTimeInterval(1e9) \
+            .linkFrom(StreamOperator.fromDataframe(df, schemaStr="f0 int, f1 int, label int")) \
+            .link(CollectStreamOp(got))
+        StreamOperator.execute()
+        snaps[tag] = [tuple(r) for r in got]
+    assert snaps["three"] and snaps["four"] == snaps["three"]
+
+
+def test_meta_label_values_without_aux_rows():
+    """Label values carried only in the meta (LinearModelDataConverter.java:61-64) are recovered with the
+    converter's label type."""
+    from alink_amd.common.params import Params
+    from alink_amd.common.types import Types
+    from alink_amd.models.linear.model import LinearModelDataConverter
+    b = _op(label_last=2)
+    rows = [tuple(r) for r in LogisticRegressionTrainBatchOp().setFeatureCols(["f0", "f1"]).setLabelCol("label")
+            .linkFrom(b).collect()]
+    meta = Params.fromJson(rows[0][1])
+    meta.set("labelValues", [2.0, 1.0])
+    m = LinearModelDataConverter(Types.LONG).load([(rows[0][0], meta.toJson(), None), rows[1]])
+    assert m.labelValues == [2, 1] and all(isinstance(v, int) for v in m.labelValues)
