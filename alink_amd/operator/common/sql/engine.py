@@ -97,30 +97,30 @@ def _select_rows(rows: List[Row], schema: TableSchema, clause: str, qualifiers=N
     return out, TableSchema(names, types)
 
 
-def sql_select(mt: MTable, clause: str) -> MTable:
+def sql_select(mt: MTable, clause: str, qualifiers: Optional[dict] = None) -> MTable:
     items = _expand_star(parse_select_list(clause), mt.schema)
+    resolve = _resolver(mt.schema.names, qualifiers)
     # pure column projection: keep native column storage (tensors stay on device)
     if all(it.expr.kind == "col" for it in items):
-        resolve = _resolver(mt.schema.names)
         idx = [resolve(it.expr.args[0]) for it in items]
         names = _names_for(items)
         return MTable(TableSchema(names, [mt.schema.types[i] for i in idx]), [mt.cols[i] for i in idx],
                       mt.replicated)
-    cols = _select_columnar(mt, items)
+    cols = _select_columnar(mt, items, resolve)
     if cols is not None:
         return cols
-    rows, schema = _select_rows(mt.rows(), mt.schema, clause)
+    rows, schema = _select_rows(mt.rows(), mt.schema, clause, qualifiers)
     return MTable.from_rows(rows, schema, mt.replicated)
 
 
-def _select_columnar(mt: MTable, items) -> Optional[MTable]:
+def _select_columnar(mt: MTable, items, resolve=None) -> Optional[MTable]:
     """Whole-column evaluation of a projection (``vexpr``) when every item is a column or a columnar
     expression; None -> the row path."""
     from ....common.table import Column
     from .vexpr import try_evaluate
     if mt.num_rows == 0 or any(it.expr.has_agg() for it in items):
         return None
-    resolve = _resolver(mt.schema.names)
+    resolve = resolve or _resolver(mt.schema.names)
     cols, types = [], []
     for it in items:
         if it.expr.kind == "col":
@@ -391,6 +391,10 @@ def sql_join(left: MTable, right: MTable, predicate: str, select: str = "*", how
             elif j < len(ln) <= i:
                 eq_l.append(j)
                 eq_r.append(i - len(ln))
+    if eq_l:
+        res = _join_columnar(left, right, pred, eq_l, eq_r, how, select, schema, qual, resolve)
+        if res is not None:
+            return res
     pf = compile_expr(pred, resolve)
     lrows, rrows = left.rows(), right.rows()
     nl, nr = (None,) * len(ln), (None,) * len(rn)
@@ -430,6 +434,185 @@ def sql_join(left: MTable, right: MTable, predicate: str, select: str = "*", how
     return MTable.from_rows(rows, sch)
 
 
+# ---------------------------------------------------------------------------------------------------
+# columnar equi-join and set operations: joint key codes -> sort / searchsorted on the key columns' device
+# ---------------------------------------------------------------------------------------------------
+def _null_mask(c) -> "torch.Tensor":
+    import torch
+    from ....common.strings import StringBlock
+    v = c.values
+    if isinstance(v, StringBlock):
+        return v.null_mask().cpu()
+    if isinstance(v, torch.Tensor):
+        return c.nulls.cpu() if c.nulls is not None else torch.zeros(int(v.shape[0]), dtype=torch.bool)
+    return torch.tensor([x is None for x in v], dtype=torch.bool)
+
+
+def _joint_codes(lcols, rcols, dev):
+    """int64 codes of the key tuples of both sides over one shared dictionary (equal tuples <-> equal codes);
+    a row with a NULL in any key gets -1 (left) / -2 (right), so it matches nothing (SQL ``=`` on NULL is not
+    TRUE).  None when a key column cannot be factorised columnar."""
+    import torch
+    from ....common.table import Column
+    nl = len(lcols[0]) if lcols else 0
+    code = None
+    lnull = torch.zeros(nl, dtype=torch.bool)
+    rnull = torch.zeros(len(rcols[0]) if rcols else 0, dtype=torch.bool)
+    for lc, rc in zip(lcols, rcols):
+        lv, rv = lc.values, rc.values
+        if isinstance(lv, torch.Tensor) and isinstance(rv, torch.Tensor):
+            if lv.dim() != 1 or rv.dim() != 1 or (lv.dtype == torch.bool) != (rv.dtype == torch.bool):
+                return None
+            if lv.dtype != rv.dtype:       # 1 = 1.0 (the row path compares Python numbers)
+                lc = Column(lv.to(torch.float64), lc.nulls)
+                rc = Column(rv.to(torch.float64), rc.nulls)
+        elif isinstance(lv, torch.Tensor) or isinstance(rv, torch.Tensor):
+            return None                    # tensor vs object keys: leave the mixed semantics to the row path
+        ci, k = _factorize(Column.concat([lc, rc]))
+        if ci is None:
+            return None
+        ci = ci.to(dev)
+        code = ci if code is None else torch.unique(code * k + ci, return_inverse=True)[1]
+        lnull |= _null_mask(lc)
+        rnull |= _null_mask(rc)
+    lk, rk = code[:nl].clone(), code[nl:].clone()
+    lk[lnull.to(dev)] = -1
+    rk[rnull.to(dev)] = -2
+    return lk, rk
+
+
+def _take_or_null(c, idx, n: int):
+    """Rows ``idx`` of column ``c`` (length ``n``); index -1 yields NULL (outer-join padding)."""
+    import torch
+    from ....common.linalg.block import SparseBlock
+    from ....common.strings import StringBlock
+    from ....common.table import Column
+    neg = idx < 0
+    if not bool(neg.any()):
+        return c.take(idx)
+    v = c.values
+    ii = torch.where(neg, torch.full_like(idx, n), idx)          # row n = an appended NULL row
+    if isinstance(v, StringBlock):
+        return Column(StringBlock.concat([v, StringBlock.from_list([None], device=v.device)]).take(ii.to(v.device)))
+    if isinstance(v, torch.Tensor) and v.dim() == 1:
+        vals = torch.cat([v, torch.zeros(1, dtype=v.dtype, device=v.device)])[ii.to(v.device)]
+        base = c.nulls.to(v.device) if c.nulls is not None else torch.zeros(n, dtype=torch.bool, device=v.device)
+        nulls = torch.cat([base, torch.ones(1, dtype=torch.bool, device=v.device)])[ii.to(v.device)]
+        return Column(vals, nulls)
+    lst = c.to_list() + [None]
+    return Column([lst[i] for i in ii.cpu().tolist()])
+
+
+def _join_columnar(left, right, pred, eq_l, eq_r, how, select, schema, qual, resolve) -> Optional[MTable]:
+    """Equi-join without per-row Python: joint key codes, a stable sort of the right side's codes, per left
+    row a searchsorted range of matching right rows (repeat_interleave expands the pairs), the residual
+    conjuncts evaluated columnar (``vexpr``) on the candidate pairs, outer padding by index -1.  Output row
+    order equals the row path's: left rows in order with their matches in right-row order, then (right / full)
+    the unmatched right rows in order.  None -> the row path."""
+    import torch
+    from ....common.table import Column
+    from .vexpr import try_evaluate
+    nl, nr = left.num_rows, right.num_rows
+    dev = next((c.values.device for c in [left.cols[i] for i in eq_l] + [right.cols[j] for j in eq_r]
+                if isinstance(c.values, torch.Tensor)), torch.device("cpu"))
+    if nl and nr:
+        codes = _joint_codes([left.cols[i] for i in eq_l], [right.cols[j] for j in eq_r], dev)
+        if codes is None:
+            return None
+        lk, rk = codes
+        order = torch.argsort(rk, stable=True)
+        rs = rk[order]
+        lo = torch.searchsorted(rs, lk, right=False)
+        cnt = torch.searchsorted(rs, lk, right=True) - lo
+        cnt = torch.where(lk < 0, torch.zeros_like(cnt), cnt)
+        li = torch.repeat_interleave(torch.arange(nl, device=dev), cnt)
+        off = torch.cumsum(cnt, 0) - cnt
+        ri = order[torch.arange(li.numel(), device=dev) - off[li] + lo[li]]
+    else:
+        li = torch.zeros(0, dtype=torch.int64, device=dev)
+        ri = torch.zeros(0, dtype=torch.int64, device=dev)
+    # residual conjuncts (everything but the key equalities): columnar on the candidate pairs
+    eqs = set(zip(eq_l, eq_r))
+    rest = []
+    for c in _split_and(pred):
+        if c.kind == "cmp" and c.args[0] == "=" and c.args[1].kind == "col" and c.args[2].kind == "col":
+            i, j = resolve(c.args[1].args[0]), resolve(c.args[2].args[0])
+            if (i, j - len(left.cols)) in eqs or (j, i - len(left.cols)) in eqs:
+                continue
+        rest.append(c)
+    if rest and li.numel():
+        cand = MTable(schema, [c.take(li) for c in left.cols] + [c.take(ri) for c in right.cols])
+        keep = None
+        for c in rest:
+            r = try_evaluate(c, cand, resolve)
+            if r is None or r[0].dtype != torch.bool:
+                f = compile_expr(c, resolve)
+                m = torch.tensor([f(row) is True for row in cand.rows()], dtype=torch.bool, device=dev)
+            else:
+                m = (r[0] if r[1] is None else r[0] & ~r[1]).to(dev)
+            keep = m if keep is None else keep & m
+        li, ri = li[keep], ri[keep]
+    if how in ("left", "full"):
+        hit = torch.zeros(nl, dtype=torch.bool, device=dev)
+        hit[li] = True
+        ul = torch.nonzero(~hit).reshape(-1)
+        if ul.numel():
+            li = torch.cat([li, ul])
+            ri = torch.cat([ri, torch.full_like(ul, -1)])
+            o = torch.argsort(li, stable=True)            # unmatched left rows at their position
+            li, ri = li[o], ri[o]
+    if how in ("right", "full"):
+        hit = torch.zeros(nr, dtype=torch.bool, device=dev)
+        hit[ri[ri >= 0]] = True
+        ur = torch.nonzero(~hit).reshape(-1)
+        li = torch.cat([li, torch.full_like(ur, -1)])
+        ri = torch.cat([ri, ur])
+    joined = MTable(schema, [_take_or_null(c, li, nl) for c in left.cols] +
+                    [_take_or_null(c, ri, nr) for c in right.cols])
+    return sql_select(joined, select, qual)
+
+
+def _set_codes(a: MTable, b: MTable):
+    """Row codes of ``a`` and ``b`` over one dictionary (NULLs equal each other, as set operations treat them);
+    None -> the row path."""
+    import torch
+    if a.num_rows == 0 or b.num_rows == 0:
+        return None
+    both = MTable.concat([a, MTable(a.schema, b.cols, a.replicated)])
+    dev = next((c.values.device for c in both.cols if isinstance(c.values, torch.Tensor)), torch.device("cpu"))
+    code = _row_codes(both, range(len(both.cols)), dev)
+    if code is None:
+        return None
+    return code[:a.num_rows], code[a.num_rows:], int(code.max()) + 1
+
+
+def _occurrence_rank(code):
+    """Per row: how many earlier rows carry the same code (stable)."""
+    import torch
+    o = torch.argsort(code, stable=True)
+    sc = code[o]
+    pos = torch.arange(code.numel(), device=code.device)
+    start = torch.searchsorted(sc, sc, right=False)
+    rank = torch.empty_like(o)
+    rank[o] = pos - start
+    return rank
+
+
+def _set_op_columnar(a: MTable, b: MTable, all_: bool, keep_common: bool) -> Optional[MTable]:
+    import torch
+    sc = _set_codes(a, b)
+    if sc is None:
+        return None
+    ca, cb, G = sc
+    nb = torch.bincount(cb, minlength=G)
+    r = _occurrence_rank(ca)
+    if all_:
+        keep = r < nb[ca] if keep_common else r >= nb[ca]
+    else:
+        keep = (r == 0) & ((nb[ca] > 0) if keep_common else (nb[ca] == 0))
+    return a.take(torch.nonzero(keep).reshape(-1))
+
+
 def sql_union(a: MTable, b: MTable, all_: bool) -> MTable:
     b2 = MTable(a.schema, b.cols, a.replicated)
     u = MTable.concat([a, b2])
@@ -437,6 +620,9 @@ def sql_union(a: MTable, b: MTable, all_: bool) -> MTable:
 
 
 def sql_intersect(a: MTable, b: MTable, all_: bool) -> MTable:
+    res = _set_op_columnar(a, b, all_, True)
+    if res is not None:
+        return res
     cb = Counter(tuple(_key(v) for v in r) for r in b.rows())
     keep, seen = [], set()
     for i, r in enumerate(a.rows()):
@@ -452,6 +638,9 @@ def sql_intersect(a: MTable, b: MTable, all_: bool) -> MTable:
 
 
 def sql_minus(a: MTable, b: MTable, all_: bool) -> MTable:
+    res = _set_op_columnar(a, b, all_, False)
+    if res is not None:
+        return res
     cb = Counter(tuple(_key(v) for v in r) for r in b.rows())
     keep, seen = [], set()
     for i, r in enumerate(a.rows()):
