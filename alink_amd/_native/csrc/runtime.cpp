@@ -298,7 +298,16 @@ int64_t alink_parse_binary_detail(const char* buf, const int64_t* off, int64_t n
             p = skip_ws(p + 1, e);
             char num[64];
             int nl = 0;
-            while (p < e && nl < 63 && *p != ',' && *p != '}' && *p != ' ') num[nl++] = *p++;
+            // a number, or a number in a JSON string (HashMap<String,String> details: {"1":"0.3",...})
+            const bool quoted = p < e && *p == '"';
+            if (quoted) {
+                ++p;
+                while (p < e && nl < 63 && *p != '"') num[nl++] = *p++;
+                if (p >= e || *p != '"') return i + 1;
+                ++p;
+            } else {
+                while (p < e && nl < 63 && *p != ',' && *p != '}' && *p != ' ') num[nl++] = *p++;
+            }
             num[nl] = 0;
             char* endp = nullptr;
             const double v = strtod(num, &endp);

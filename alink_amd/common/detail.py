@@ -1,0 +1,74 @@
+"""Prediction-detail column kept columnar.
+
+Alink's ``predictionDetailCol`` holds, per row, the Gson JSON of a ``HashMap<String, String>`` label ->
+``Double.toString(probability)`` (``LinearModelMapper.java`` / ``SoftmaxModelMapper.java``).  Formatting that string
+for every row and parsing it back in a downstream evaluator is the dominant host cost of a scoring pipeline
+(the FTRL predict -> evaluate stream of BASELINE config 5).  A ``DetailBlock`` keeps the (labels, probability
+matrix) pair instead and materialises the strings only when something reads them (``to_list``, a sink, a row
+view): byte-identical to the eager strings, since both come from ``models/linear/model._detail_json``.
+Columnar consumers (``EvalBinaryClassStreamOp`` / batch evaluation) read ``probs`` directly.
+"""
+from __future__ import annotations
+
+from typing import Any, List, Optional, Sequence
+
+import numpy as np
+
+__all__ = ["DetailBlock"]
+
+
+class DetailBlock:
+    """``n`` detail strings as ``labels`` (K label values, the mapper's order) and ``probs`` ([n, K] float64
+    numpy, ``probs[i, k]`` = probability of ``labels[k]``).  ``nulls`` (optional bool [n]) marks NULL rows."""
+
+    __slots__ = ("labels", "probs", "nulls", "_list")
+
+    def __init__(self, labels: Sequence[Any], probs: np.ndarray, nulls: Optional[np.ndarray] = None):
+        self.labels = list(labels)
+        self.probs = np.asarray(probs, dtype=np.float64).reshape(-1, len(self.labels))
+        self.nulls = None if nulls is None or not np.any(nulls) else np.asarray(nulls, dtype=bool)
+        self._list: Optional[List[Optional[str]]] = None
+
+    def __len__(self) -> int:
+        return int(self.probs.shape[0])
+
+    def to_list(self) -> List[Optional[str]]:
+        if self._list is None:
+            from ..models.linear.model import _detail_json
+            out = _detail_json(self.labels, self.probs) if len(self) else []
+            if self.nulls is not None:
+                out = [None if m else s for s, m in zip(out, self.nulls.tolist())]
+            self._list = out
+        return self._list
+
+    def __iter__(self):
+        return iter(self.to_list())
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return self.take(i).to_list()
+        return self.to_list()[i]
+
+    def take(self, idx) -> "DetailBlock":
+        if isinstance(idx, slice):
+            sel = idx
+        else:
+            if hasattr(idx, "detach"):
+                idx = idx.detach().cpu().numpy()
+            sel = np.asarray(idx)
+            if sel.dtype != bool:
+                sel = sel.astype(np.int64)
+        return DetailBlock(self.labels, self.probs[sel], None if self.nulls is None else self.nulls[sel])
+
+    @staticmethod
+    def concat(blocks: Sequence["DetailBlock"]) -> Optional["DetailBlock"]:
+        """One block, or None when the blocks' label sets differ (the caller falls back to strings)."""
+        if not blocks or any(b.labels != blocks[0].labels for b in blocks):
+            return None
+        nulls = None
+        if any(b.nulls is not None for b in blocks):
+            nulls = np.concatenate([b.nulls if b.nulls is not None else np.zeros(len(b), bool) for b in blocks])
+        return DetailBlock(blocks[0].labels, np.concatenate([b.probs for b in blocks]), nulls)
+
+    def __repr__(self):
+        return f"DetailBlock(n={len(self)}, labels={self.labels})"

@@ -8,6 +8,7 @@ iteration order.  To read *and write* byte-compatible models we reproduce those 
 from __future__ import annotations
 
 import math
+import re
 from typing import Any, Dict, Iterable, List
 
 __all__ = [
@@ -90,7 +91,12 @@ def java_float_str(x: float) -> str:
         java_double_str(float(np.format_float_scientific(f, unique=True)))
 
 
+_NEEDS_ESCAPE = re.compile('["\\\\\x00-\x1f\u2028\u2029]')
+
+
 def _gson_escape(s: str) -> str:
+    if _NEEDS_ESCAPE.search(s) is None:          # the common case: nothing to escape
+        return '"' + s + '"'
     out: List[str] = ['"']
     for ch in s:
         o = ord(ch)
@@ -159,6 +165,9 @@ def gson_dumps(v: Any, java_map_order: bool = True) -> str:
         body = _native.java_double_join(v)
         if body is not None:
             return "[" + body + "]"
+    if isinstance(v, (list, tuple)) and len(v) >= 64 and all(type(e) is float for e in v):
+        # long Python float lists (metric curves) through the same C++ formatter
+        return gson_dumps(np.asarray(v, dtype=np.float64), java_map_order)
     if isinstance(v, (list, tuple)) or (hasattr(v, "tolist") and not isinstance(v, str)):
         seq = v.tolist() if hasattr(v, "tolist") else v
         return "[" + ",".join(gson_dumps(e, java_map_order) for e in seq) + "]"

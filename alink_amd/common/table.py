@@ -21,6 +21,7 @@ import torch
 
 from .linalg import DenseVector, SparseBlock, SparseVector, Vector, VectorUtil
 from .strings import StringBlock
+from .detail import DetailBlock
 from .types import TableSchema, Types, AlinkType, is_numeric, schema_str_to_schema
 
 __all__ = ["Row", "Column", "MTable", "infer_type"]
@@ -100,7 +101,7 @@ class Column:
 
     def to_list(self) -> List[Any]:
         v = self.values
-        if isinstance(v, StringBlock):
+        if isinstance(v, (StringBlock, DetailBlock)):
             return v.to_list()
         if isinstance(v, SparseBlock):
             lst = v.to_list()
@@ -121,7 +122,7 @@ class Column:
     def take(self, idx) -> "Column":
         """Row selection by index tensor/list or boolean mask."""
         v = self.values
-        if isinstance(v, StringBlock):
+        if isinstance(v, (StringBlock, DetailBlock)):
             return Column(v.take(idx))
         if isinstance(v, SparseBlock):
             nn = None
@@ -155,6 +156,10 @@ class Column:
             return Column([])
         if all(isinstance(c.values, StringBlock) for c in cols):
             return Column(StringBlock.concat([c.values for c in cols]))
+        if all(isinstance(c.values, DetailBlock) for c in cols):
+            blk = DetailBlock.concat([c.values for c in cols])
+            if blk is not None:
+                return Column(blk)
         if all(isinstance(c.values, SparseBlock) for c in cols):
             nulls = None
             if any(c.nulls is not None for c in cols):

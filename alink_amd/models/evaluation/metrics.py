@@ -425,6 +425,54 @@ def _area(x, y):
     return float(np.sum((x[1:] - x[:-1]) * (y[1:] + y[:-1]) / 2)) if len(x) > 1 else 0.0
 
 
+def _sample_thresholds(thr: np.ndarray) -> List[int]:
+    """Indices kept by the reference's threshold sampling over the descending thresholds (index 0, then every
+    threshold at least PROBABILITY_INTERVAL below the last kept one, plus any within PROBABILITY_ERROR of 0.5).
+    Jumps between kept points with a binary search (the predicate is monotone in i) and settles the exact
+    boundary with the scalar comparison, so the result equals the per-element scan."""
+    n1 = len(thr)
+    step = PROBABILITY_INTERVAL - PROBABILITY_ERROR
+    halves = np.nonzero(np.abs(thr - 0.5) < PROBABILITY_ERROR)[0].tolist()
+    neg = -thr                                           # ascending
+    keep, pre, i, h = [0], thr[0], 0, 0
+    while i < n1:
+        j = int(np.searchsorted(neg, -(pre - step), side="left"))
+        j = max(j, i)
+        while j > i and abs(pre - thr[j - 1]) >= step:
+            j -= 1
+        while j < n1 and not abs(pre - thr[j]) >= step:
+            j += 1
+        while h < len(halves) and halves[h] < i:
+            h += 1
+        if h < len(halves) and halves[h] < j:
+            j = halves[h]
+        if j >= n1:
+            break
+        keep.append(j)
+        pre = thr[j]
+        i = j + 1
+    return keep
+
+
+def _vdiv(a, b):
+    with np.errstate(divide="ignore", invalid="ignore"):
+        return np.where(b == 0, 0.0, a / np.where(b == 0, 1.0, b))
+
+
+def _binary_arrays(TP, FP, FN, TN):
+    """``_COMPUTATIONS`` of class 0 over arrays of 2x2 confusion counts."""
+    total = TP + FP + FN + TN
+    pa = (TP + TN) / total
+    pe = ((TP + FN) * (TP + FP) + (TN + FP) * (TN + FN)) / (total * total)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        kappa = np.where(pe < 1, (pa - pe) / np.where(pe < 1, 1 - pe, 1.0), 1.0)
+    tnr, tpr = _vdiv(TN, FP + TN), _vdiv(TP, TP + FN)
+    return {"TrueNegativeRate": tnr, "TruePositiveRate": tpr, "FalseNegativeRate": _vdiv(FN, TP + FN),
+            "FalsePositiveRate": _vdiv(FP, FP + TN), "Precision": _vdiv(TP, TP + FP), "Specificity": tnr,
+            "Sensitivity": tpr, "Recall": tpr, "F1": _vdiv(2 * TP, 2 * TP + FP + FN), "Accuracy": (TP + TN) / total,
+            "Kappa": kappa}
+
+
 def binary_metrics(posb: np.ndarray, negb: np.ndarray, labels: List[str], logloss: float, total: int
                    ) -> BinaryClassMetrics:
     """``BinaryMetricsSummary.toMetrics`` :72-...: full curves for AUC/PRC/KS, 0.001-sampled curves and
@@ -460,29 +508,24 @@ def binary_metrics(posb: np.ndarray, negb: np.ndarray, labels: List[str], loglos
     _set(params, "PRC", _area(pr_x, pr_y))
     _set(params, "K-S", float(np.max(np.abs(roc_x - roc_y))))
     # sampling of thresholds at 0.001 resolution (plus the 0.5 point)
-    keep = [0]
-    pre = thr[0]
-    for i in range(n1):
-        if abs(pre - thr[i]) >= PROBABILITY_INTERVAL - PROBABILITY_ERROR or abs(thr[i] - 0.5) < PROBABILITY_ERROR:
-            keep.append(i)
-            pre = thr[i]
-    keep = np.asarray(keep)
+    keep = np.asarray(_sample_thresholds(thr))
     _set(params, "RocCurve", [roc_x[keep].tolist(), roc_y[keep].tolist()])
     _set(params, "RecallPrecisionCurve", [pr_x[keep].tolist(), pr_y[keep].tolist()])
     _set(params, "LiftChart", [lift_x[keep].tolist(), lift_y[keep].tolist()])
     sk = keep[1:]
     s_thr = thr[sk]
-    mats = []
-    for i in sk:
-        mats.append(np.array([[tp[i], fp[i]], [total_true - tp[i], total_false - fp[i]]]))
     _set(params, "ThresholdArray", s_thr.tolist())
-    cms = [_CM(m) for m in mats]
-    for name, fn in _COMPUTATIONS:
-        _set(params, name + "Array", [float(fn(c, 0)) for c in cms])
+    # per-threshold 2x2 confusion counts of class 0, every computation vectorised over the thresholds (the same
+    # float64 operations, in the same order, as the per-matrix _CM computers)
+    TP, FP = tp[sk], fp[sk]
+    FN, TN = float(total_true) - TP, float(total_false) - FP
+    for name, arr in _binary_arrays(TP, FP, FN, TN).items():
+        _set(params, name + "Array", arr.tolist())
     if logloss >= 0:
         _set(params, "LogLoss", logloss / total)
     mid_i = int(np.argmin(np.abs(s_thr - 0.5)))
-    c = cms[mid_i]
+    i = sk[mid_i]
+    c = _CM(np.array([[tp[i], fp[i]], [total_true - tp[i], total_false - fp[i]]]))
     _set(params, "Precision", float(_precision(c, 0)))
     _set(params, "Recall", float(_tpr(c, 0)))
     _set(params, "F1", float(_f1(c, 0)))

@@ -25,6 +25,7 @@ import numpy as np
 import torch
 
 from ...common.javafmt import gson_dumps, java_double_str, java_hashmap_order
+from ...common.detail import DetailBlock
 from ...common.linalg import DenseVector
 from ...common.mapper import RichModelMapper
 from ...common.model.converter import LabeledModelDataConverter
@@ -218,6 +219,22 @@ class _LinearMapperBase(RichModelMapper):
         reserved = self.params.get("reservedCols") if self.params.contains("reservedCols") else None
         self.helper = OutputColsHelper(self.dataSchema, names, types, reserved)
 
+    def swapCoef(self, w) -> None:
+        """Hot swap of the coefficient vector of a loaded model (online learning snapshots with unchanged
+        meta and labels)."""
+        self.model.coefVector = DenseVector(np.asarray(w, dtype=np.float64))
+        self._coef_cache = None
+
+    def _coef(self, dev) -> torch.Tensor:
+        """The coefficient vector on ``dev``, cached until the model changes (no per-batch H2D copy of a
+        1e6-dim vector in a serving loop)."""
+        cv = self.model.coefVector
+        c = getattr(self, "_coef_cache", None)
+        if c is None or c[0] is not cv or c[1].device != dev:
+            c = (cv, torch.as_tensor(cv.data, dtype=torch.float64, device=dev))
+            self._coef_cache = c
+        return c[1]
+
     def _features(self, mt: MTable) -> FeatureMatrix:
         m = self.model
         fm = extract_features(mt, m.featureNames if self.vector_col is None else None, self.vector_col,
@@ -244,14 +261,22 @@ def _dev(mt: MTable):
 
 
 def _detail_json(labels: Sequence[Any], probs: np.ndarray) -> List[str]:
-    """HashMap<String,String> of label -> Double.toString(prob), Gson-serialised in Java HashMap order."""
+    """HashMap<String,String> of label -> Double.toString(prob), Gson-serialised in Java HashMap order.
+    Batched: every probability is formatted by the C++ Double.toString twin in one call and the rows are
+    assembled from one per-table template (the keys and their order are the same on every row)."""
+    from ... import _native
     keys = [str(l) for l in labels]
     order = java_hashmap_order(keys)
-    out = []
-    for row in probs:
-        out.append(gson_dumps({k: java_double_str(float(row[keys.index(k)])) for k in order},
-                              java_map_order=True))
-    return out
+    probs = np.asarray(probs, dtype=np.float64)
+    cols = [keys.index(k) for k in order]
+    body = _native.java_double_join(np.ascontiguousarray(probs[:, cols]).reshape(-1)) if probs.size else ""
+    if body is None:
+        return [gson_dumps({k: java_double_str(float(row[keys.index(k)])) for k in order}, java_map_order=True)
+                for row in probs]
+    strs = body.split(",") if probs.size else []
+    K = len(order)
+    tmpl = "{" + ",".join(gson_dumps(k) + ':"%s"' for k in order) + "}"
+    return [tmpl % tuple(strs[i * K:(i + 1) * K]) for i in range(probs.shape[0])]
 
 
 class LinearModelMapper(_LinearMapperBase):
@@ -264,7 +289,7 @@ class LinearModelMapper(_LinearMapperBase):
     def _map_columns(self, mt):
         m = self.model
         fm = self._features(mt)
-        coef = torch.as_tensor(m.coefVector.data, dtype=torch.float64, device=fm.device)
+        coef = self._coef(fm.device)
         dot = fm.mv(coef).cpu().numpy() if mt.num_rows else np.zeros(0)
         tname = m.linearModelType.name
         out = []
@@ -272,12 +297,18 @@ class LinearModelMapper(_LinearMapperBase):
             out.append(Column(torch.from_numpy(dot.copy())))
         else:
             lv = m.labelValues
-            preds = [lv[0] if v >= 0 else lv[1] for v in dot]
-            out.append(Column.from_values(preds, self.helper.out_types[0]))
+            t = self.helper.out_types[0]
+            if t.torch_dtype is not None and all(isinstance(x, (int, float)) and not isinstance(x, bool) for x in lv):
+                preds = torch.where(torch.from_numpy(dot >= 0), torch.tensor(lv[0], dtype=t.torch_dtype),
+                                    torch.tensor(lv[1], dtype=t.torch_dtype))
+                out.append(Column(preds))
+            else:
+                out.append(Column.from_values([lv[0] if v >= 0 else lv[1] for v in dot], t))
         if self.detail_col:
             if tname in ("LR", "SVM"):
                 prob = 1.0 - 1.0 / (1.0 + np.exp(dot))
-                out.append(Column(_detail_json(m.labelValues, np.stack([prob, 1 - prob], 1))))
+                # columnar detail: strings are formatted only if a consumer reads them (common/detail.py)
+                out.append(Column(DetailBlock(m.labelValues, np.stack([prob, 1 - prob], 1))))
             else:
                 out.append(Column([None] * mt.num_rows))
         return out

@@ -2,12 +2,18 @@
 ``A/operator/stream/onlinelearning/{FtrlTrainStreamOp,FtrlPredictStreamOp}.java``).
 
 ``FtrlTrainStreamOp(initModel)`` warm-starts from a batch-trained linear model (collected once, as the
-reference's ``DirectReader``), updates coefficients sample by sample with FTRL-proximal (native C++ loop
-``_native/csrc/ftrl.cpp`` — the update is inherently sequential) and emits a model snapshot at the first
-sample, every ``timeInterval`` seconds and when the stream ends.  Snapshot rows are
-``(bid, ntab, model_id, model_info, label_value)``: ``bid`` = snapshot number, ``ntab`` = rows per snapshot.
-``FtrlPredictStreamOp(initModel).linkFrom(models, data)`` re-assembles snapshots and hot-swaps the
-``LinearModelMapper`` between micro-batches.
+reference's ``DirectReader``), updates the coefficients per micro-batch in one of four ``updateMode``s (see the
+class docstring: SEQUENTIAL = the reference's sample-by-sample rule in the native C++ loop
+``_native/csrc/ftrl.cpp``; SHARDED = the reference's feature-sharded design with HIP partial-margin / replay
+kernels; DATA_PARALLEL = replicated mini-batch FTRL with an (optionally asynchronous) RCCL gradient all-reduce;
+HOGWILD = one GPU wave per sample) and emits a model snapshot at the first step, every ``timeInterval`` seconds
+and when the stream ends.  Snapshot rows are ``(bid, ntab, model_id, model_info, label_value)``: ``bid`` =
+snapshot number, ``ntab`` = rows per snapshot.  ``FtrlPredictStreamOp(initModel).linkFrom(models, data)``
+re-assembles snapshots and hot-swaps the ``LinearModelMapper`` between micro-batches; a snapshot produced in
+the same process also carries its coefficient vector, so the hot swap skips re-parsing the JSON rows.
+
+Per step the ranks agree on liveness, snapshot due-ness and per-rank sample counts with one host-group
+all-gather (``comm.host_all_gather``: never a device copy or a GPU-stream sync under RCCL).
 
 Deviation: the reference scales each gradient by ``1/sqrt(ms between the forward and the feedback pass)``
 (``FtrlTrainStreamOp.java:428``), a wall-clock artefact of its Flink feedback loop; here the scale is 1.
@@ -139,6 +145,7 @@ class FtrlTrainStreamOp(StreamOperator):
             raise ValueError(f"unknown updateMode {self._mode}")
         self._ws, self._rank = comm.get_world_size(), comm.get_rank()
         self.recv_nnz = []          # SHARDED: nonzeros this shard received per step (observability / tests)
+        self.snapshot_log = []      # per snapshot: bid, perf_counter at its start and at its emission
         # SEQUENTIAL keeps its state on the host (the rule is a serial loop); the others on the rank's GPU
         gpu = self.env.device.type == "cuda" and self._mode != "SEQUENTIAL"
         self._dev = self.env.device if gpu else torch.device("cpu")
@@ -173,6 +180,7 @@ class FtrlTrainStreamOp(StreamOperator):
         return full.cpu().numpy()[:self._dim].copy()
 
     def _snapshot(self):
+        t_begin = time.perf_counter()
         w = self._full_w()
         m = self._model
         m.coefVector = DenseVector(w)
@@ -183,8 +191,12 @@ class FtrlTrainStreamOp(StreamOperator):
         m.vectorSize = w.size - 1 if self._intercept else w.size
         rows = self._conv.save(m)
         out = [(self._bid, len(rows)) + tuple(r) for r in rows]
+        snap = MTable.from_rows(out, self._schema)
+        # in-process subscribers (FtrlPredictStreamOp) hot-swap from the vector itself, not by re-parsing JSON
+        snap.ftrl_coef = (self._bid, w, rows[0][1])
+        self.snapshot_log.append({"bid": self._bid, "t_begin": t_begin, "t_emit": time.perf_counter()})
         self._bid += 1
-        self._emit(MTable.from_rows(out, self._schema))
+        self._emit(snap)
 
     # ---------------------------------------------------------------- checkpoint state
     def _state_dict(self):
@@ -221,7 +233,8 @@ class FtrlTrainStreamOp(StreamOperator):
         nloc = 0 if csr is None else int(csr[0].numel() - 1)
         info = torch.tensor([[0 if csr is None else 1, 1 if due else 0, nloc]], dtype=torch.int64)
         if self._ws > 1:
-            info = comm.all_gather_tensor(info)                   # [P, 3]: live, due, samples per rank
+            # [P, 3]: live, due, samples per rank — over the host group: the rank's GPU stream is never synced
+            info = comm.host_all_gather(info)
         active, due = bool(info[:, 0].max()), bool(info[:, 1].max())
         counts = [int(c) for c in info[:, 2].tolist()]
         if not active:
@@ -259,28 +272,30 @@ class FtrlTrainStreamOp(StreamOperator):
         offset = sum(counts[:self._rank])
         G = sum(counts)
         if csr is None:
-            send = [torch.zeros((0, 3), dtype=torch.float64, device=cd) for _ in range(P)]
+            send = [torch.zeros((0, 3), dtype=torch.int64, device=cd) for _ in range(P)]
             lab = torch.zeros(0, dtype=torch.float64, device=cd)
         else:
             indptr, idx, val, lab = (t.to(cd) for t in csr)
             rows = torch.repeat_interleave(torch.arange(indptr.numel() - 1, device=cd, dtype=torch.int64) + offset,
                                            indptr[1:] - indptr[:-1])
             owner = idx.to(torch.int64) // per
-            ent = torch.stack([rows.to(torch.float64), idx.to(torch.float64), val.to(torch.float64)], 1)
+            # one int64 entry per nonzero: global row id, coordinate, and the fp64 value's bits (exact)
+            ent = torch.stack([rows, idx.to(torch.int64), val.to(torch.float64).view(torch.int64)], 1)
             order = torch.argsort(owner, stable=True)            # by destination, sample order kept inside
             ent = ent[order]
             split = torch.bincount(owner, minlength=P).tolist()
             send = list(torch.split(ent, split))
         recv = comm.all_to_all_tensors(send)                     # from every source rank, in rank order
-        ent = torch.cat(recv) if recv else torch.zeros((0, 3), dtype=torch.float64, device=cd)
+        ent = torch.cat(recv) if recv else torch.zeros((0, 3), dtype=torch.int64, device=cd)
         self.recv_nnz.append(int(ent.shape[0]))
-        glab = comm.all_gather_varlen(lab.to(torch.float64))      # labels of the global batch, rank order
-        grow = ent[:, 0].to(torch.int64)
+        # labels of the global batch in rank order; the per-rank counts are known from the step's control gather
+        glab = comm.all_gather_varlen(lab.to(torch.float64), lens=counts)
+        grow = ent[:, 0]
         gptr = torch.zeros(G + 1, dtype=torch.int64, device=cd)
         if ent.shape[0]:
             torch.cumsum(torch.bincount(grow, minlength=G), 0, out=gptr[1:])
         gidx = ent[:, 1].to(torch.int32).contiguous()
-        gval = ent[:, 2].contiguous()
+        gval = ent[:, 2].contiguous().view(torch.float64)
         dev = self._dev
         gptr, gidx, gval, glab = (t.to(dev) for t in (gptr, gidx, gval, glab))
         a, b, l1, l2 = self._alpha, self._beta, self._l1, self._l2
@@ -446,18 +461,28 @@ class FtrlPredictStreamOp(StreamOperator):
         self._mapper.loadModel(mt.rows())
         self._schema = self._mapper.getOutputSchema()
         self._buffers = {}
+        self._meta = None
+        self.swap_log = {}          # bid -> perf_counter when the snapshot became the serving model
         _register_upstream_sources(models)
         _register_upstream_sources(data)
         return self
 
     def on_batch(self, port, mt):
         if port == 0:
+            fast = getattr(mt, "ftrl_coef", None)
+            if fast is not None and self._meta == fast[2] and not self._buffers:
+                # same meta as the serving model: swap the coefficient vector only (rows stay the record)
+                self._mapper.swapCoef(fast[1])
+                self.swap_log[int(fast[0])] = time.perf_counter()
+                return
             for r in mt.rows():
                 bid, ntab = int(r[0]), int(r[1])
                 buf = self._buffers.setdefault(bid, [])
                 buf.append(tuple(r[2:]))
                 if len(buf) == ntab:
                     self._mapper.loadModel(buf)
+                    self._meta = next((x[1] for x in buf if int(x[0]) == 0), None)
                     del self._buffers[bid]
+                    self.swap_log[bid] = time.perf_counter()
         else:
             self._emit(self._mapper.map_table(mt))

@@ -33,7 +33,7 @@ __all__ = ["init_distributed", "get_rank", "get_world_size", "is_distributed", "
            "broadcast_object", "barrier", "all_gather_tensor", "all_to_all_objects", "reduce_scatter",
            "object_group", "device_for_rank", "CommStats", "STATS", "shutdown", "all_reduce_coalesced",
            "Pending", "reduce_scatter_async", "all_gather_varlen_async", "all_reduce_async", "all_to_all_bytes", "all_to_all_strings",
-           "comm_stream", "force_collective", "device_timing", "device_timing_collect"]
+           "comm_stream", "force_collective", "device_timing", "device_timing_collect", "host_all_gather"]
 
 _OBJ_GROUP = None
 
@@ -513,13 +513,30 @@ def all_gather_tensor(t: torch.Tensor) -> torch.Tensor:
 
 
 @_collective
-def all_gather_varlen(t: torch.Tensor) -> torch.Tensor:
-    """Concatenate tensors whose dim-0 length differs per rank (pads to the max length, one collective)."""
+def host_all_gather(t: torch.Tensor) -> torch.Tensor:
+    """All-gather of a small HOST tensor over the host (gloo) group — the control plane of lockstep loops
+    (liveness flags, per-rank counts).  Under RCCL this never touches the device: no H2D / D2H copy and no
+    synchronisation of the rank's GPU stream, so queued kernels keep running while the ranks agree."""
     ws = get_world_size()
     if not is_distributed():
         return t
-    n = torch.tensor([t.shape[0]], dtype=torch.int64)
-    lens = all_gather_tensor(n).tolist()
+    STATS.calls += 1
+    h = t.detach().cpu().contiguous()
+    parts = [torch.empty_like(h) for _ in range(ws)]
+    dist.all_gather(parts, h, group=_OBJ_GROUP)
+    return torch.cat(parts)
+
+
+@_collective
+def all_gather_varlen(t: torch.Tensor, lens: Optional[List[int]] = None) -> torch.Tensor:
+    """Concatenate tensors whose dim-0 length differs per rank (pads to the max length, one collective).
+    ``lens`` (every rank's length, when the caller already knows them) skips the length exchange."""
+    ws = get_world_size()
+    if not is_distributed():
+        return t
+    if lens is None:
+        n = torch.tensor([t.shape[0]], dtype=torch.int64)
+        lens = all_gather_tensor(n).tolist()
     mx = max(lens)
     pad = torch.zeros((mx,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
     pad[:t.shape[0]] = t

@@ -104,6 +104,10 @@ def checks(out):
     vx = [torch.arange(lens[r] * 2, dtype=torch.int64).view(lens[r], 2) + 100 * r for r in range(ws)]
     got = comm.all_gather_varlen(vx[me].to(dev))
     ok("all_gather_varlen", torch.equal(got.cpu(), torch.cat(vx)))
+    got = comm.all_gather_varlen(vx[me].to(dev), lens=lens)
+    ok("all_gather_varlen.known_lens", torch.equal(got.cpu(), torch.cat(vx)))
+    got = comm.host_all_gather(torch.tensor([[me, 2 * me, 7]], dtype=torch.int64))
+    ok("host_all_gather", torch.equal(got, torch.tensor([[r, 2 * r, 7] for r in range(ws)], dtype=torch.int64)))
     got = comm.all_gather_varlen_async(vx[me].to(dev)).wait()
     ok("all_gather_varlen_async", torch.equal(got.cpu(), torch.cat(vx)))
     got = comm.all_gather_varlen_async(vx[me].clone()).wait()

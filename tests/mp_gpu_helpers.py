@@ -76,10 +76,14 @@ def scenario_kmeans_headline(out):
     iters = int(os.environ.get("ALINK_REH_ITERS", "8"))
     src = RandomVectorSourceBatchOp().setNumRows(rows).setSize(128).setNumClusters(100).setClusterStd(1.0) \
         .setCenterScale(4.0).setDtype("bf16").setSeed(2024).setOutputCol("vec")
+    import time
+    t0 = time.time()
     data = src.getOutputTable()
+    print(f"[rank {env.rank}] data {data.num_rows} rows {time.time() - t0:.1f}s", flush=True)
     comm.device_timing(env.device.type == "cuda")
-    op = KMeansTrainBatchOp().setVectorCol("vec").setK(100).setMaxIter(iters).setEpsilon(-1.0) \
-        .linkFrom(TableSourceBatchOp(data))
+    op = KMeansTrainBatchOp().setVectorCol("vec").setK(100).setMaxIter(iters).setEpsilon(-1.0)
+    op._on_step = lambda step, q: print(f"[rank {env.rank}] superstep {step} {time.time() - t0:.1f}s", flush=True)
+    op.linkFrom(TableSourceBatchOp(data))
     res = op.collect()
     comm.device_timing(False)
     n_ev, dev_s, per = comm.device_timing_collect()
