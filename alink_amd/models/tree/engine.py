@@ -156,12 +156,20 @@ class TreeBuilder:
         # (each rank receives 1/P of it instead of the full all-reduce), searches its block, and only the [m, F]
         # best gains / bins and the chosen feature's [B, S] row per node are exchanged afterwards
         ws = comm.get_world_size()
-        self.fshard = (not local and ws > 1 and cfg.kind == "gbdt" and not any(data.is_cat)
+        # every criterion shards: GBDT (continuous and categorical) and the RF / decision-tree criteria of the
+        # parallel (data-partitioned) mode; tree-parallel forests (local=True) hold all rows and never reduce
+        self.fshard = (not local and ws > 1
                        and __import__("os").environ.get("ALINK_GBDT_FEATURE_SHARD", "1") == "1")
         # features per rank, padded to whole 32-feature groups (the histogram kernel's unit)
         self.Fb = -(-self.F // (ws * 32)) * 32 if self.fshard else self.F
         self._hist_sub = None          # (stats tensor, histogram columns, FmStats) of the tree being built
         self.f_lo = comm.get_rank() * self.Fb if self.fshard else 0
+        # categorical flags of this rank's feature block (padding features: continuous, all-zero rows)
+        cat_loc = torch.zeros(self.Fb, dtype=torch.bool, device=self.dev)
+        n_loc = max(0, min(self.F, self.f_lo + self.Fb) - self.f_lo)
+        if n_loc:
+            cat_loc[:n_loc] = self.is_cat[self.f_lo:self.f_lo + n_loc]
+        self.is_cat_local = cat_loc
 
     # -------------------------------------------------------------------------------------------
     def _hist_cols(self, S: int) -> List[int]:
@@ -196,7 +204,7 @@ class TreeBuilder:
 
     RS_BLOCKS = int(__import__("os").environ.get("ALINK_GBDT_RS_BLOCKS", "4"))
     # observability (bounded: long trainings and many jobs in one process must not grow them without limit)
-    RS_BYTES = collections.deque(maxlen=4096)     # reduce-scattered bytes per histogram piece (latest)
+    RS_BYTES = collections.deque(maxlen=4096)     # reduce-scatter input bytes (fp32) per histogram piece (latest)
     RS_CALLS = 0                                  # reduce-scattered histogram pieces (all time)
     HIST_BYTES = collections.deque(maxlen=4096)   # full-width fp32 histogram bytes per histogram call (latest)
 
@@ -217,7 +225,7 @@ class TreeBuilder:
                 break
             fgs = [j * gpr + lo + t if lo + t < gpr else pad for j in range(ws) for t in range(ps)]
             Hc = tops.histogram_groups(self.d.bins, slot, sub, nslots, self.B, fgs, prep)
-            TreeBuilder.RS_BYTES.append(int(Hc.numel() * Hc.element_size()))
+            TreeBuilder.RS_BYTES.append(int(Hc.numel() * 4))            # fp32-equivalent, as HIST_BYTES
             TreeBuilder.RS_CALLS += 1
             pend.append(comm.reduce_scatter_async(Hc, "sum"))
             real.append(min(ps, gpr - lo) * 32)
@@ -234,16 +242,54 @@ class TreeBuilder:
     # -------------------------------------------------------------------------------------------
     def _search(self, Hn: torch.Tensor, feat_order: torch.Tensor, feat_ok: torch.Tensor):
         """Best split per node.  Hn [m, F, B, S] (float64); feat_order [m, F] (scan order of features);
-        feat_ok [m, F] allowed.  Returns per node (gain, feature, j, multiway flag, perm [m,F,B-1])."""
+        feat_ok [m, F] allowed.  Returns per node (gain, feature, j, multi-way flag, accept, perm [m, F, B-1] or
+        None = rebuild the chosen features' bin order on the host)."""
+        gain, best_j, multi, perm = self._feature_best(Hn, self.is_cat)
+        return self._choose(gain, best_j, multi, feat_order, feat_ok) + (perm,)
+
+    def _choose(self, best_j_gain, best_j, multi, feat_order, feat_ok):
+        """Per node, the first feature in ``feat_order`` with the largest admissible gain (the reference's scan
+        order, ties included)."""
+        cfg = self.cfg
+        best_j_gain = torch.where(feat_ok, best_j_gain, torch.full_like(best_j_gain, NEG))
+        ordered = torch.gather(best_j_gain, 1, feat_order)
+        gbest, pos = ordered.max(dim=1)
+        fbest = torch.gather(feat_order, 1, pos[:, None])[:, 0]
+        jbest = torch.gather(best_j, 1, fbest[:, None])[:, 0]
+        mbest = torch.gather(multi, 1, fbest[:, None])[:, 0]
+        accept = gbest > (cfg.min_info_gain + 1e-6 if cfg.kind == "gbdt" else 0)
+        return gbest, fbest, jbest, mbest, accept
+
+    def _feature_best(self, Hn: torch.Tensor, is_cat: torch.Tensor):
+        """Per (node, feature): best admissible gain [m, F] float64 (NEG: none), its position in the feature's
+        bin order [m, F], the multi-way flag [m, F] and the bin order perm [m, F, B-1] (None when the GPU kernel
+        searched: the chosen features' order is rebuilt on the host).  ``is_cat`` [F] are the flags of the
+        features of ``Hn`` (all features, or one rank's block under feature sharding).
+
+        Precision: the histograms are exact fixed-point sums rounded once to fp32 (``Hn`` holds those fp32
+        values); every gain below — the K8 / K10 kernels and the torch scans alike — is computed in fp64 from
+        them, so GPU and host differ only by the fp64 summation order of the prefix sums (relative 1e-16), not
+        by fp32 rounding of the gains."""
         cfg = self.cfg
         m, F, B, S = Hn.shape
-        if cfg.kind == "gbdt" and Hn.is_cuda and not bool(self.d.is_cat and any(self.d.is_cat)) \
-                and tops.gpu_kernels_ok():
-            return self._search_gbdt_hip(Hn, feat_order, feat_ok)
+        anycat = bool(is_cat.any())
+        if cfg.kind == "gbdt" and not anycat:
+            g, j = self._feature_gains_gbdt(Hn)
+            return g, j, torch.zeros((m, F), dtype=torch.bool, device=Hn.device), \
+                torch.arange(B - 1, device=Hn.device).expand(m, F, B - 1)
         if Hn.is_cuda and tops.gpu_kernels_ok():
-            out = self._search_hip(Hn, feat_order, feat_ok)
-            if out is not None:
-                return out
+            res = tops.tree_split(Hn, cfg.kind, is_cat, cfg.n_classes, cfg.min_samples_per_leaf,
+                                  cfg.min_sum_hessian_per_leaf, cfg.min_sample_ratio_per_child, cfg.min_info_gain)
+            if res is not None:
+                best_j_gain, best_j = res
+                multi = torch.zeros((m, F), dtype=torch.bool, device=Hn.device)
+                if cfg.kind in ("infogain", "infogainratio") and anycat:
+                    Hv = Hn[:, :, :B - 1, :]
+                    mg = self._multiway_gain(Hv, Hn[:, :, B - 1, :], Hv.sum(2))
+                    catf = is_cat[None, :].expand(m, F)
+                    best_j_gain = torch.where(catf, mg, best_j_gain)
+                    multi = catf.clone()
+                return best_j_gain, best_j, multi, None
         Hv = Hn[:, :, :B - 1, :]
         Hmiss = Hn[:, :, B - 1, :]
         cnt = _count(cfg, Hv)
@@ -260,7 +306,7 @@ class TreeBuilder:
             w = _weight(cfg, Hv)
             key = torch.where(cnt > 0, Hv[..., 0] / torch.where(w == 0, torch.ones_like(w), w),
                               torch.full_like(w, float("inf")))
-        iscat = self.is_cat[None, :, None].expand(m, F, B - 1)
+        iscat = is_cat[None, :, None].expand(m, F, B - 1)
         key = torch.where(iscat, key, binpos)
         key, perm = torch.sort(key, dim=2, stable=True)
         Hs = torch.gather(Hv, 2, perm[..., None].expand(m, F, B - 1, S))
@@ -297,22 +343,12 @@ class TreeBuilder:
         gain = torch.where(ok, gain, torch.full_like(gain, NEG))
         best_j_gain, best_j = gain.max(dim=2)       # first max along bins
         multi = torch.zeros((m, F), dtype=torch.bool, device=Hn.device)
-        if cfg.kind in ("infogain", "infogainratio") and bool(self.is_cat.any()):
+        if cfg.kind in ("infogain", "infogainratio") and anycat:
             mg = self._multiway_gain(Hv, Hmiss, Tv)
-            catf = self.is_cat[None, :].expand(m, F)
+            catf = is_cat[None, :].expand(m, F)
             best_j_gain = torch.where(catf, mg, best_j_gain)
             multi = catf.clone()
-        best_j_gain = torch.where(feat_ok, best_j_gain, torch.full_like(best_j_gain, NEG))
-        ordered = torch.gather(best_j_gain, 1, feat_order)
-        gbest, pos = ordered.max(dim=1)
-        fbest = torch.gather(feat_order, 1, pos[:, None])[:, 0]
-        jbest = torch.gather(best_j, 1, fbest[:, None])[:, 0]
-        mbest = torch.gather(multi, 1, fbest[:, None])[:, 0]
-        if cfg.kind == "gbdt":
-            accept = gbest > cfg.min_info_gain + 1e-6
-        else:
-            accept = gbest > 0
-        return gbest, fbest, jbest, mbest, accept, perm
+        return best_j_gain, best_j, multi, perm
 
     def _feature_gains_gbdt(self, Hn):
         """Per-(node, feature) best gain and bin of GBDT binary splits on continuous features: K8 on the GPU,
@@ -344,79 +380,39 @@ class TreeBuilder:
     SHARDED_SEARCHES = 0
 
     def _search_sharded(self, Hn, feat_order, feat_ok):
-        """Feature-sharded split search: this rank scans its feature block, the [m, F] gains / bins of all
-        blocks are all-gathered (small), and every rank picks the same best feature per node in ``feat_order``
-        (identical tie-breaking to the replicated search).  Returns also the chosen features' [m, B, S]
-        histogram rows, all-reduced from their owners."""
-        cfg = self.cfg
+        """Feature-sharded split search (reference ``CalBestSplit.java:122-153`` / ``TreeObj.java:321-390``: each
+        task searches the features it owns): this rank scans its feature block — any criterion, categorical
+        features included (their bin order is per (node, feature), so local to the owner) — the [m, Fb] best
+        gains / positions / multi-way flags of all blocks are all-gathered (small), and every rank picks the same
+        best feature per node in ``feat_order`` (identical tie-breaking to the replicated search).  Returns also
+        the chosen features' [m, B, S] histogram rows, all-reduced from their owners."""
         m = Hn.shape[0]
         ws = comm.get_world_size()
         TreeBuilder.SHARDED_SEARCHES += 1
-        g_loc, j_loc = self._feature_gains_gbdt(Hn)                          # [m, Fb]
-        packed = torch.stack([g_loc, j_loc.to(torch.float64)], 0).contiguous()  # [2, m, Fb]
-        allp = comm.all_gather_tensor(packed.reshape(1, 2, m, self.Fb).to(comm.collective_device()))
-        allp = allp.to(Hn.device).reshape(ws, 2, m, self.Fb).permute(1, 2, 0, 3).reshape(2, m, ws * self.Fb)
+        g_loc, j_loc, multi_loc, perm_loc = self._feature_best(Hn, self.is_cat_local)   # [m, Fb]
+        packed = torch.stack([g_loc.to(torch.float64), j_loc.to(torch.float64), multi_loc.to(torch.float64)], 0)
+        allp = comm.all_gather_tensor(packed.contiguous().reshape(1, 3, m, self.Fb).to(comm.collective_device()))
+        allp = allp.to(Hn.device).reshape(ws, 3, m, self.Fb).permute(1, 2, 0, 3).reshape(3, m, ws * self.Fb)
         gain, best_j = allp[0][:, :self.F], allp[1][:, :self.F].to(torch.int64)
-        gain = torch.where(feat_ok, gain, torch.full_like(gain, NEG))
-        ordered = torch.gather(gain, 1, feat_order)
-        gbest, pos = ordered.max(dim=1)
-        fbest = torch.gather(feat_order, 1, pos[:, None])[:, 0]
-        jbest = torch.gather(best_j, 1, fbest[:, None])[:, 0]
-        accept = gbest > cfg.min_info_gain + 1e-6
+        multi = allp[2][:, :self.F] > 0.5
+        gbest, fbest, jbest, mbest, accept = self._choose(gain, best_j, multi, feat_order, feat_ok)
         # chosen feature's histogram row per node: owners contribute, everyone else adds zeros
         loc = fbest - self.f_lo
         mine = (loc >= 0) & (loc < self.Fb)
-        rows = torch.zeros((m,) + tuple(Hn.shape[2:]), dtype=torch.float64, device=Hn.device)
+        B = Hn.shape[2]
+        # the owner's bin order of the chosen feature travels with its row when the torch scan produced one (the
+        # GPU kernels' order is rebuilt on the host from the row instead, like the replicated search)
+        width = B * Hn.shape[3] + (B - 1 if perm_loc is not None else 0)
+        rows = torch.zeros((m, width), dtype=torch.float64, device=Hn.device)
         if bool(mine.any()):
             idx = torch.nonzero(mine).reshape(-1)
-            rows[idx] = Hn[idx, loc[idx]].to(torch.float64)
+            rows[idx, :B * Hn.shape[3]] = Hn[idx, loc[idx]].to(torch.float64).reshape(idx.numel(), -1)
+            if perm_loc is not None:
+                rows[idx, B * Hn.shape[3]:] = perm_loc[idx, loc[idx]].to(torch.float64)
         comm.all_reduce(rows, "sum")
-        return gbest, fbest, jbest, accept, rows
-
-    def _search_gbdt_hip(self, Hn, feat_order, feat_ok):
-        """K8 on the GPU (``ops/csrc/tree_split.hip``): one wave per (node, feature) scans the bins; only the
-        [m, F] best gains / bins come back for the per-node feature choice."""
-        cfg = self.cfg
-        m, F, B, S = Hn.shape
-        gain, best_j = tops.gbdt_split(Hn.to(torch.float32), cfg.min_samples_per_leaf, cfg.min_sum_hessian_per_leaf)
-        gain = torch.where(feat_ok, gain, torch.full_like(gain, NEG))
-        ordered = torch.gather(gain, 1, feat_order)
-        gbest, pos = ordered.max(dim=1)
-        fbest = torch.gather(feat_order, 1, pos[:, None])[:, 0]
-        jbest = torch.gather(best_j, 1, fbest[:, None])[:, 0]
-        mbest = torch.zeros(m, dtype=torch.bool, device=Hn.device)
-        accept = gbest > cfg.min_info_gain + 1e-6
-        perm = torch.arange(B - 1, device=Hn.device).expand(m, F, B - 1)
-        return gbest, fbest, jbest, mbest, accept, perm
-
-    def _search_hip(self, Hn, feat_order, feat_ok):
-        """Categorical GBDT and RF / decision-tree criteria on the GPU (``ops/csrc/tree_split.hip``
-        ``tree_split_kernel``): one wave per (node, feature) orders the bins, scans the statistics and picks the
-        first best admissible split; C4.5 multi-way gains of categorical features (information-gain criteria)
-        stay a vectorised torch reduction.  The order (perm) is rebuilt on the host for the chosen features only
-        (returned as None)."""
-        cfg = self.cfg
-        m, F, B, S = Hn.shape
-        res = tops.tree_split(Hn, cfg.kind, self.is_cat, cfg.n_classes, cfg.min_samples_per_leaf,
-                              cfg.min_sum_hessian_per_leaf, cfg.min_sample_ratio_per_child, cfg.min_info_gain)
-        if res is None:
-            return None
-        best_j_gain, best_j = res
-        multi = torch.zeros((m, F), dtype=torch.bool, device=Hn.device)
-        if cfg.kind in ("infogain", "infogainratio") and bool(self.is_cat.any()):
-            Hv = Hn[:, :, :B - 1, :]
-            mg = self._multiway_gain(Hv, Hn[:, :, B - 1, :], Hv.sum(2))
-            catf = self.is_cat[None, :].expand(m, F)
-            best_j_gain = torch.where(catf, mg, best_j_gain)
-            multi = catf.clone()
-        best_j_gain = torch.where(feat_ok, best_j_gain, torch.full_like(best_j_gain, NEG))
-        ordered = torch.gather(best_j_gain, 1, feat_order)
-        gbest, pos = ordered.max(dim=1)
-        fbest = torch.gather(feat_order, 1, pos[:, None])[:, 0]
-        jbest = torch.gather(best_j, 1, fbest[:, None])[:, 0]
-        mbest = torch.gather(multi, 1, fbest[:, None])[:, 0]
-        accept = gbest > (cfg.min_info_gain + 1e-6 if cfg.kind == "gbdt" else 0)
-        return gbest, fbest, jbest, mbest, accept, None
+        hist_rows = rows[:, :B * Hn.shape[3]].reshape((m,) + tuple(Hn.shape[2:]))
+        perm_rows = rows[:, B * Hn.shape[3]:].to(torch.int64) if perm_loc is not None else None
+        return gbest, fbest, jbest, mbest, accept, hist_rows, perm_rows
 
     def _multiway_gain(self, Hv, Hmiss, Tv):
         """C4.5 split on every non-empty category (``CategoricalSplitter.bestSplitInfo``)."""
@@ -600,20 +596,19 @@ class TreeBuilder:
                         order[r_] = torch.as_tensor(pf, device=dev)
                         ok[r_, torch.as_tensor(pf[:k], device=dev)] = True
                 if self.fshard:
-                    gbest, fbest, jbest, accept, rows_t = self._search_sharded(Hn, order, ok)
-                    mbest = torch.zeros(m, dtype=torch.bool, device=dev)
+                    gbest, fbest, jbest, mbest, accept, rows_t, prow = self._search_sharded(Hn, order, ok)
                     rows_host = rows_t.cpu().numpy()                                     # [m, B, S]
-                    perm_host = np.broadcast_to(np.arange(B - 1), (m, B - 1))
+                    perm = None if prow is None else prow[:, None, :].expand(m, F, B - 1)
                 else:
                     gbest, fbest, jbest, mbest, accept, perm = self._search(Hn, order, ok)
                     rows_host = Hn[torch.arange(m, device=dev), fbest].cpu().numpy()      # [m, B, S]
-                    if perm is None:                     # GPU search: rebuild the chosen features' order
-                        fb_np = fbest.cpu().numpy()
-                        perm_host = np.stack([tops.split_order_key(rows_host[r_], cfg.kind, cfg.n_classes,
-                                                                   bool(self.d.is_cat[int(fb_np[r_])]))
-                                              for r_ in range(m)]) if m else np.zeros((0, B - 1), np.int64)
-                    else:
-                        perm_host = perm[torch.arange(m, device=dev), fbest].cpu().numpy()    # [m, B-1]
+                if perm is None:                     # GPU / sharded search: rebuild the chosen features' order
+                    fb_np = fbest.cpu().numpy()
+                    perm_host = np.stack([tops.split_order_key(rows_host[r_], cfg.kind, cfg.n_classes,
+                                                               bool(self.d.is_cat[int(fb_np[r_])]))
+                                          for r_ in range(m)]) if m else np.zeros((0, B - 1), np.int64)
+                else:
+                    perm_host = perm[torch.arange(m, device=dev), fbest].cpu().numpy()    # [m, B-1]
                 acc = accept.cpu().numpy()
                 fb, jb, mb, gb = (fbest.cpu().numpy(), jbest.cpu().numpy(), mbest.cpu().numpy(),
                                   gbest.cpu().numpy())

@@ -125,6 +125,63 @@ def scenario_gbdt_many(out):
     out["rs_calls"] = TreeBuilder.RS_CALLS - nrs
 
 
+def _tree_cat(out, kind):
+    """Mixed categorical / continuous features under feature sharding (categorical bin orders are per (node,
+    feature), so the owner of the feature computes them): ``kind`` = gbdt | gini | infogain | mse."""
+    import numpy as np
+    import pandas as pd
+    from alink_amd import (useLocalEnv, BatchOperator, GbdtTrainBatchOp, RandomForestTrainBatchOp,
+                           RandomForestRegTrainBatchOp)
+    from alink_amd.models.tree.engine import TreeBuilder
+    rng = np.random.default_rng(31)
+    n = 1200
+    c1 = rng.integers(0, 6, n)
+    c2 = rng.integers(0, 9, n)
+    X = rng.normal(size=(n, 5))
+    score = X @ np.array([1.0, -1.0, 0.5, 0.0, 0.8]) + np.array([0.9, -0.8, 0.1, 1.2, -1.1, 0.0])[c1] \
+        + 0.4 * np.cos(c2)
+    df = pd.DataFrame({f"x{i}": X[:, i] for i in range(5)})
+    df["c1"] = [f"a{v}" for v in c1]
+    df["c2"] = [f"b{v}" for v in c2]
+    df["y"] = (score > 0).astype(int) if kind != "mse" else np.round(score, 4)
+    useLocalEnv(1)
+    feats = [f"x{i}" for i in range(5)] + ["c1", "c2"]
+    schema = ", ".join(f"x{i} double" for i in range(5)) + ", c1 string, c2 string, " + \
+        ("y double" if kind == "mse" else "y int")
+    src = BatchOperator.fromDataframe(df, schemaStr=schema)
+    s0, r0, h0 = TreeBuilder.SHARDED_SEARCHES, sum(TreeBuilder.RS_BYTES), sum(TreeBuilder.HIST_BYTES)
+    nr, nh = len(TreeBuilder.RS_BYTES), len(TreeBuilder.HIST_BYTES)
+    if kind == "gbdt":
+        op = GbdtTrainBatchOp().setNumTrees(3).setMinSamplesPerLeaf(10).setMaxDepth(4)
+    elif kind == "mse":
+        op = RandomForestRegTrainBatchOp().setNumTrees(2).setMaxDepth(4).setCreateTreeMode("parallel") \
+            .setSubsamplingRatio(1.0)
+    else:
+        op = RandomForestTrainBatchOp().setNumTrees(2).setMaxDepth(4).setCreateTreeMode("parallel") \
+            .setTreeType(kind.upper()).setSubsamplingRatio(1.0)
+    m = op.setFeatureCols(feats).setCategoricalCols(["c1", "c2"]).setLabelCol("y").linkFrom(src)
+    out["model"] = [list(r) for r in m.collect()]
+    out["sharded"] = TreeBuilder.SHARDED_SEARCHES - s0
+    out["rs_bytes"] = sum(list(TreeBuilder.RS_BYTES)[nr:]) if len(TreeBuilder.RS_BYTES) > nr else 0
+    out["hist_bytes"] = sum(list(TreeBuilder.HIST_BYTES)[nh:])
+
+
+def scenario_tree_cat_gbdt(out):
+    _tree_cat(out, "gbdt")
+
+
+def scenario_tree_cat_gini(out):
+    _tree_cat(out, "gini")
+
+
+def scenario_tree_cat_infogain(out):
+    _tree_cat(out, "infogain")
+
+
+def scenario_tree_cat_mse(out):
+    _tree_cat(out, "mse")
+
+
 def scenario_rf(out):
     from alink_amd import useLocalEnv, BatchOperator, RandomForestTrainBatchOp
     df = _data_frame()

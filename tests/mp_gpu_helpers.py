@@ -9,6 +9,9 @@ import traceback
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
+HERE = os.path.dirname(os.path.abspath(__file__))
+if HERE not in sys.path:
+    sys.path.insert(0, HERE)
 
 
 def _rank_tensor(r, n, dtype, seed):
@@ -99,6 +102,46 @@ def scenario_kmeans_headline(out):
     out["device"] = str(env.device)
     if env.device.type == "cuda":
         torch.cuda.synchronize()
+
+
+def scenario_als(out):
+    """ALS with device tensors over the ranks sharing the GPU: owner-partitioned ratings, the request/response
+    all-to-all and the pipelined factor all-gather on device tensors; plus the reference doc example
+    (docs/en/als.md) predictions."""
+    import numpy as np
+    import pandas as pd
+    from alink_amd import useLocalEnv, BatchOperator, AlsTrainBatchOp, AlsPredictBatchOp
+    from alink_amd.parallel import comm
+    env = useLocalEnv(1)
+    rng = np.random.default_rng(5)
+    uu, ii = np.nonzero(rng.random((600, 400)) < 0.05)
+    df = pd.DataFrame({"u": uu * 3 + 1, "i": ii * 7 + 2, "r": np.round(rng.normal(size=uu.size), 3)})
+    src = BatchOperator.fromDataframe(df, schemaStr="u bigint, i bigint, r double")
+    m = AlsTrainBatchOp().setUserCol("u").setItemCol("i").setRateCol("r").setRank(8).setNumIter(6) \
+        .setLambda(0.1).linkFrom(src)
+    out["model"] = [list(r) for r in m.collect()]
+    doc = np.array([[1, 1, 0.6], [2, 2, 0.8], [2, 3, 0.6], [4, 1, 0.6], [4, 2, 0.3], [4, 3, 0.4]])
+    ddf = pd.DataFrame({"user": doc[:, 0].astype(int), "item": doc[:, 1].astype(int), "rating": doc[:, 2]})
+    dsrc = BatchOperator.fromDataframe(ddf, schemaStr="user bigint, item bigint, rating double")
+    dm = AlsTrainBatchOp().setUserCol("user").setItemCol("item").setRateCol("rating").setNumIter(10).setRank(10) \
+        .setLambda(0.01).linkFrom(dsrc)
+    pred = AlsPredictBatchOp().setUserCol("user").setItemCol("item").setPredictionCol("p").linkFrom(dm, dsrc)
+    out["doc_pred"] = sorted((int(r[0]), int(r[1]), float(r[3])) for r in pred.collect())
+    out["backend"] = comm._backend()
+    out["device"] = str(env.device)
+    out["comm_calls"] = comm.STATS.calls
+
+
+def scenario_tree_cat_gbdt(out):
+    """Categorical GBDT, feature-sharded over the ranks sharing the GPU (tests/dist_helpers._tree_cat)."""
+    from dist_helpers import _tree_cat
+    _tree_cat(out, "gbdt")
+
+
+def scenario_tree_cat_gini(out):
+    """Parallel-mode RF (gini, categorical features), feature-sharded on the GPU."""
+    from dist_helpers import _tree_cat
+    _tree_cat(out, "gini")
 
 
 def scenario_gbdt(out):

@@ -111,6 +111,31 @@ def test_gbdt_feature_sharded_histograms_three_ranks(tmp_path):
                                    rtol=1e-5, atol=1e-7)
 
 
+@pytest.mark.parametrize("kind,world", [("gbdt", 2), ("gbdt", 3), ("gini", 2), ("infogain", 2), ("mse", 3)])
+def test_feature_sharded_categorical_and_rf_criteria(tmp_path, kind, world):
+    """Feature-sharded histograms + split search for categorical GBDT and the parallel-mode RF criteria (gini,
+    C4.5 information gain with multi-way categorical splits, MSE): the same trees as one rank, and every rank
+    reduce-scatters exactly the full (padded) histogram: it sends (P-1)/P of it and keeps its own 1/P block,
+    instead of all-reducing the whole histogram."""
+    one = _run("tree_cat_" + kind, 1, tmp_path)[0]
+    many = _run("tree_cat_" + kind, world, tmp_path)
+    assert one["sharded"] == 0 and all(o["sharded"] > 0 for o in many)
+    assert all(o["model"] == many[0]["model"] for o in many)
+    ta, tb = _tree_nodes(one["model"]), _tree_nodes(many[0]["model"])
+    assert len(ta) == len(tb) and len(ta) > 3
+    for a, b in zip(ta, tb):
+        assert a["id"] == b["id"] and a.get("nextIds") == b.get("nextIds")
+        assert a["node"]["featureIndex"] == b["node"]["featureIndex"]
+        assert a["node"].get("categoricalSplit") == b["node"].get("categoricalSplit")
+        assert a["node"].get("continuousSplit") == pytest.approx(b["node"].get("continuousSplit"))
+        np.testing.assert_allclose(a["node"]["counter"]["distributions"], b["node"]["counter"]["distributions"],
+                                   rtol=1e-5, atol=1e-7)
+    assert any(a["node"].get("categoricalSplit") for a in ta)          # categorical splits were chosen
+    F, Fb = 7, 32                                                      # 7 features -> one 32-feature block per rank
+    for o in many:
+        assert o["rs_bytes"] == o["hist_bytes"] * world * Fb // F
+
+
 def test_gbdt_pipelined_feature_block_reduce_scatter_two_ranks(tmp_path):
     """200 features over 2 ranks: each histogram is built and reduce-scattered in 4 feature pieces (the
     reduce-scatter of piece c in flight while piece c+1 builds); the trees equal the 1-rank trees."""

@@ -14,6 +14,10 @@ pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
+def _tree_nodes(model_rows):
+    return [json.loads(r[1]) for r in model_rows[1:] if r[1] is not None and r[1].startswith('{"node"')]
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -85,10 +89,34 @@ def test_gbdt_feature_sharded_multiprocess_gpu_matches_one_rank(tmp_path):
     assert "cuda" in one["device"]
     assert one["sharded"] == 0 and all(o["sharded"] > 0 and o["rs_calls"] > 0 for o in two)
     assert two[0]["model"] == two[1]["model"]
-    import json as _json
-    ta = [_json.loads(r[1]) for r in one["model"] if r[0] >= 0 and r[1]]
-    tb = [_json.loads(r[1]) for r in two[0]["model"] if r[0] >= 0 and r[1]]
-    assert len(ta) == len(tb)
+    ta, tb = _tree_nodes(one["model"]), _tree_nodes(two[0]["model"])
+    assert len(ta) == len(tb) and len(ta) > 3
+    for a, b in zip(ta, tb):
+        # exact fixed-point histograms: identical split features and thresholds on every node
+        assert a["id"] == b["id"] and a.get("nextIds") == b.get("nextIds")
+        assert a["node"]["featureIndex"] == b["node"]["featureIndex"]
+        assert a["node"].get("continuousSplit") == b["node"].get("continuousSplit")
+        np.testing.assert_allclose(a["node"]["counter"]["distributions"], b["node"]["counter"]["distributions"],
+                                   rtol=1e-9, atol=1e-12)
+
+
+@pytest.mark.parametrize("kind", ["gbdt", "gini"])
+def test_feature_sharded_categorical_trees_multiprocess_gpu(tmp_path, kind):
+    """Categorical GBDT / parallel-mode RF over 2 ranks on the GPU: feature-block reduce-scatter of the device
+    histograms, K8/K10 split kernels on each rank's block, owner-side categorical bin order -> the 1-rank trees."""
+    one = _run("tree_cat_" + kind, 1, tmp_path)[0]
+    two = _run("tree_cat_" + kind, 2, tmp_path)
+    assert one["sharded"] == 0 and all(o["sharded"] > 0 for o in two)
+    assert two[0]["model"] == two[1]["model"]
+    ta, tb = _tree_nodes(one["model"]), _tree_nodes(two[0]["model"])
+    assert len(ta) == len(tb) and len(ta) > 3
+    for a, b in zip(ta, tb):
+        assert a["id"] == b["id"] and a.get("nextIds") == b.get("nextIds")
+        assert a["node"]["featureIndex"] == b["node"]["featureIndex"]
+        assert a["node"].get("categoricalSplit") == b["node"].get("categoricalSplit")
+        assert a["node"].get("continuousSplit") == b["node"].get("continuousSplit")
+    assert any(a["node"].get("categoricalSplit") for a in ta)
+    assert all(o["rs_bytes"] == o["hist_bytes"] * 2 * 32 // 7 for o in two)
 
 
 def test_ftrl_hogwild_multiprocess_gpu(tmp_path):
@@ -112,12 +140,31 @@ def test_ftrl_sharded_multiprocess_gpu(tmp_path):
 
 
 def test_ftrl_dp_async_multiprocess_gpu(tmp_path):
-    """DATA_PARALLEL FTRL with the gradient all-reduce overlapped on the RCCL comm stream (asyncGradReduce):
-    replicated model identical on both ranks, learns as well as 1 rank."""
+    """DATA_PARALLEL FTRL with asyncGradReduce (the (sum g, sum g^2) all-reduce of step t in flight while step
+    t+1 scores): replicated model identical on both ranks, learns as well as 1 rank.  The ranks share one GPU, so
+    the job runs on gloo and the in-flight reduce is gloo's async work (device tensors staged through the host);
+    the RCCL comm-stream variant of all_reduce_async is exercised by
+    tests/test_comm_wrappers.py::test_comm_wrappers_rccl_one_rank_* (a 1-rank RCCL group)."""
     one = _run("ftrl_dp_async", 1, tmp_path)[0]
     two = _run("ftrl_dp_async", 2, tmp_path)
     assert two[0]["coef"] == two[1]["coef"]
     assert one["acc"] > 0.85 and two[0]["acc"] > one["acc"] - 0.03
+
+
+def test_als_multiprocess_gpu_matches_one_rank(tmp_path):
+    """ALS over 2 ranks sharing the GPU (device factor tensors through the all-to-all request/response exchange
+    and the pipelined all-gather) == 1 rank within the solve tolerance, and the reference doc predictions."""
+    one = _run("als", 1, tmp_path)[0]
+    two = _run("als", 2, tmp_path)
+    assert "cuda" in one["device"] and two[0]["comm_calls"] > 0
+    assert two[0]["model"] == two[1]["model"]
+    assert [r[:2] for r in one["model"]] == [r[:2] for r in two[0]["model"]]
+    a = np.array([[float(x) for x in r[2].split()] for r in one["model"]])
+    b = np.array([[float(x) for x in r[2].split()] for r in two[0]["model"]])
+    np.testing.assert_allclose(a, b, rtol=1e-4, atol=1e-5)
+    ref = [0.579622, 0.766851, 0.581079, 0.574481, 0.298500, 0.382157]
+    for o in [one] + two:
+        np.testing.assert_allclose([p for _, _, p in o["doc_pred"]], ref, atol=1e-2)
 
 
 def test_ring_topk_multiprocess_gpu(tmp_path):
