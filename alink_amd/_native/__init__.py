@@ -12,7 +12,8 @@ from typing import List, Optional, Sequence
 import numpy as np
 
 __all__ = ["lib", "parse_csv_lines", "murmur3_utf16", "murmur3_bytes", "murmur3_utf8", "parse_dense_vectors", "ftrl_update_csr",
-           "ftrl_partial_margin", "ftrl_shard_update", "parse_binary_detail", "java_double_join"]
+           "ftrl_partial_margin", "ftrl_shard_update", "parse_binary_detail", "java_double_join",
+           "java_double_rows"]
 
 # ALINK_NATIVE_LIB points at another build of the same sources (e.g. the AddressSanitizer build of
 # tools/asan_host.py)
@@ -34,6 +35,8 @@ if os.path.exists(_PATH):
         lib.alink_parse_binary_detail.restype = ctypes.c_int64
         if hasattr(lib, "alink_java_double_join"):
             lib.alink_java_double_join.restype = ctypes.c_int64
+        if hasattr(lib, "alink_java_double_rows"):
+            lib.alink_java_double_rows.restype = ctypes.c_int64
     except OSError:
         lib = None
 
@@ -148,6 +151,24 @@ def java_double_join(x) -> Optional[str]:
     buf = np.empty(26 * max(a.size, 1) + 16, dtype=np.uint8)     # no zero fill
     n = lib.alink_java_double_join(_ptr(a), ctypes.c_int64(a.size), _ptr(buf))
     return buf[:n].tobytes().decode("ascii")
+
+
+def java_double_rows(x, sep: str = " ") -> Optional[List[str]]:
+    """One string per row of a 2-D float array: ``sep.join(java_double_str(v) for v in row)`` (Alink's dense
+    vector string), formatted in C++; None without the library."""
+    if lib is None or getattr(lib, "alink_java_double_rows", None) is None:
+        return None
+    a = np.ascontiguousarray(np.asarray(x, dtype=np.float64))
+    if a.ndim != 2:
+        raise ValueError("java_double_rows needs a 2-D array")
+    n, k = a.shape
+    buf = np.empty(26 * max(a.size, 1) + 16, dtype=np.uint8)
+    ends = np.zeros(max(n, 1), dtype=np.int64)
+    total = lib.alink_java_double_rows(_ptr(a), ctypes.c_int64(n), ctypes.c_int64(k), ctypes.c_char(sep.encode()),
+                                       _ptr(buf), _ptr(ends))
+    text = buf[:total].tobytes().decode("ascii")
+    starts = np.concatenate([[0], ends[:n - 1]]) if n else np.zeros(0, np.int64)
+    return [text[s:e] for s, e in zip(starts.tolist(), ends[:n].tolist())]
 
 
 def parse_binary_detail(strings: Sequence[str], key0: str, key1: str):

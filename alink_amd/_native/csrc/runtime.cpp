@@ -405,6 +405,21 @@ static int java_double_to(double x, char* out) {
     return (int)(r2.ptr - out);
 }
 
+// n rows of k values: row i = java_double(x[i*k]) sep ... sep java_double(x[i*k+k-1]), rows written back to back;
+// row_end[i] = end offset of row i in out (dense-vector strings of a prediction detail column, VectorUtil.toString)
+extern "C" int64_t alink_java_double_rows(const double* x, int64_t n, int64_t k, char sep, char* out,
+                                          int64_t* row_end) {
+    int64_t p = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        for (int64_t j = 0; j < k; ++j) {
+            if (j) out[p++] = sep;
+            p += java_double_to(x[i * k + j], out + p);
+        }
+        row_end[i] = p;
+    }
+    return p;
+}
+
 extern "C" int64_t alink_java_double_join(const double* x, int64_t n, char* out) {
     // one thread: ~90 ns per value (1e6 coefficients ~0.1 s); an OpenMP split measured slower on the 8-CPU host
     int64_t p = 0;

@@ -28,6 +28,7 @@ from __future__ import annotations
 
 import json
 import math
+import os
 from typing import List, Optional
 
 import numpy as np
@@ -489,6 +490,12 @@ def train_kmeans(X: torch.Tensor, k: int, max_iter: int, tol: float, dist_type: 
     """Run the KMeans BSP queue on this rank's rows ``X`` ([n, d] on the env device); returns
     (model rows, queue)."""
     dist_type = dist_type.upper()
+    # opt-in device precision for fp64 feature matrices (VectorAssembler output): ALINK_KMEANS_INPUT=fp32 runs the
+    # fp32 GEMM-assign + HIP accumulate path, =bf16 the fused bf16 MFMA kernels (a one-time cast of this rank's
+    # rows; profiles/kmeans_fp32_r4.txt records the centroid deltas against fp64)
+    cast = os.environ.get("ALINK_KMEANS_INPUT", "").lower()
+    if cast in ("fp32", "bf16") and X.is_cuda and X.dtype == torch.float64 and dist_type == "EUCLIDEAN":
+        X = X.to(torch.float32 if cast == "fp32" else torch.bfloat16).contiguous()
     if dist_type == "COSINE":
         X = _normalize_rows(X.to(torch.float64)) if X.dtype == torch.float64 else \
             _normalize_rows(X.float()).to(X.dtype)
@@ -556,9 +563,25 @@ class KMeansModelMapper(ModelMapper):
             v = c.values
             if isinstance(v, torch.Tensor) and v.dim() == 2:
                 return v, None
-            vecs = [VectorUtil.getVector(x) for x in v]
-            nulls = [x is None for x in vecs]
             d = self.C.shape[1]
+            from ...common.linalg.block import SparseBlock
+            if isinstance(v, SparseBlock):
+                dense = v.to_dense(torch.float64)
+                if dense.shape[1] >= d:
+                    dense = dense[:, :d]        # indices past the model's size are ignored, as the per-row path
+                else:
+                    dense = torch.cat([dense, dense.new_zeros((dense.shape[0], d - dense.shape[1]))], 1)
+                nl = c.nulls.cpu().tolist() if c.nulls is not None else None
+                return dense, nl
+            vals = c.to_list()
+            if vals and all(isinstance(x, str) and "$" not in x and ":" not in x for x in vals):
+                # dense vector strings ("1.0 2.0 ..."): the C++ parser, no per-row Python vectors
+                from ... import _native
+                arr = _native.parse_dense_vectors(vals, d)
+                if arr is not None:
+                    return torch.from_numpy(arr), None
+            vecs = [VectorUtil.getVector(x) for x in vals]
+            nulls = [x is None for x in vecs]
             arr = np.zeros((len(vecs), d))
             for i, x in enumerate(vecs):
                 if x is None:
@@ -599,15 +622,14 @@ class KMeansModelMapper(ModelMapper):
                                          Types.LONG)
         if self.detail_col:
             probs = prob_from_distances(dist_all).cpu().numpy()
-            order = self.model.ids
-            det = []
-            for r in range(probs.shape[0]):
-                if nulls is not None and nulls[r]:
-                    det.append(None)
-                    continue
-                v = np.zeros(probs.shape[1])
-                v[order] = probs[r]
-                det.append(VectorUtil.toString(DenseVector(v)))
+            full = np.zeros_like(probs)
+            full[:, self.model.ids] = probs          # cluster-id order, as the per-row DenseVector was
+            from ... import _native
+            det = _native.java_double_rows(full, " ")
+            if det is None:
+                det = [VectorUtil.toString(DenseVector(r)) for r in full]
+            if nulls is not None and any(nulls):
+                det = [None if nl else s_ for s_, nl in zip(det, nulls)]
             outs.append(Column(det))
         if self.dist_col:
             bd = best.to(torch.float64).cpu()

@@ -273,14 +273,17 @@ class TreeBuilder:
         cfg = self.cfg
         m, F, B, S = Hn.shape
         anycat = bool(is_cat.any())
+        gpu = Hn.is_cuda and tops.gpu_kernels_ok()
         if cfg.kind == "gbdt" and not anycat:
             g, j = self._feature_gains_gbdt(Hn)
+            # perm is None exactly when the GPU kernels search, whatever this block's features are: under feature
+            # sharding every rank must take the same branch (the perm rows travel in the owner all-reduce)
             return g, j, torch.zeros((m, F), dtype=torch.bool, device=Hn.device), \
-                torch.arange(B - 1, device=Hn.device).expand(m, F, B - 1)
-        if Hn.is_cuda and tops.gpu_kernels_ok():
+                None if gpu else torch.arange(B - 1, device=Hn.device).expand(m, F, B - 1)
+        if gpu:
             res = tops.tree_split(Hn, cfg.kind, is_cat, cfg.n_classes, cfg.min_samples_per_leaf,
                                   cfg.min_sum_hessian_per_leaf, cfg.min_sample_ratio_per_child, cfg.min_info_gain)
-            if res is not None:
+            if res is not None:           # None (no instantiation for this S): the torch scan below, on every rank
                 best_j_gain, best_j = res
                 multi = torch.zeros((m, F), dtype=torch.bool, device=Hn.device)
                 if cfg.kind in ("infogain", "infogainratio") and anycat:

@@ -80,6 +80,7 @@ _EXTRA_SIGNATURES = {
     "alink_kmeans_host_stat_alloc": [ctypes.POINTER(_c_vp), ctypes.POINTER(_c_vp)],
     "alink_kmeans_host_stat_free": [_c_vp],
     "alink_kmeans_accum_bf16": [_c_vp, _c_i64, _c_int, _c_vp, _c_vp, _c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp],
+    "alink_kmeans_accum_f32": [_c_vp, _c_i64, _c_int, _c_vp, _c_vp, _c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp],
     "alink_kmeans_accum_kmax": [_c_int],
     "alink_kmeans_accum_mfma_bf16": [_c_vp, _c_i64, _c_vp, _c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp],
     "alink_linear_grad_wide_f64": [_c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_int, _c_int, _c_d, _c_vp, _c_int, _c_vp,

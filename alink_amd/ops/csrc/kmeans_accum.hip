@@ -44,8 +44,10 @@ struct Tab {
 // AT = the LDS table type.  double (k <= 256, DS = 64): measured on gfx950, one wave-instruction of ds_add_f64 costs
 // ~9 cycles against ~193 for ds_add_f32 (profiles/gbdt_r3.txt, LDS atomic probe), so the fp64 table is both the
 // faster and the more accurate one; the products w * x are formed exactly in fp64.  float: k up to 512 at D = 64.
-template <int DS, typename AT>
-__global__ __launch_bounds__(THREADS) void kmeans_accum_kernel(const __bf16* __restrict__ X, int64_t N, int D,
+// TIn = the row type: __bf16 (one 16-B load = 8 elements per lane) or float (two 16-B loads per lane, the same
+// 8-element chunk per lane and the same table layout)
+template <int DS, typename AT, typename TIn = __bf16>
+__global__ __launch_bounds__(THREADS) void kmeans_accum_kernel(const TIn* __restrict__ X, int64_t N, int D,
                                                                const int* __restrict__ idx,
                                                                const float* __restrict__ w, int k_total,
                                                                int64_t rows_per_chunk, float* __restrict__ slab,
@@ -78,11 +80,17 @@ __global__ __launch_bounds__(THREADS) void kmeans_accum_kernel(const __bf16* __r
             const bool ok = r < r_hi;
             c[u] = ok ? idx[r] - c_base : -1;
             wr[u] = ok ? (w != nullptr ? w[r] : 1.f) : 0.f;
-            const uint4 v = *reinterpret_cast<const uint4*>(X + (ok ? r : r_lo) * D + d0 + 8 * l);
-            lo[u] = f32x4{__uint_as_float(v.x << 16), __uint_as_float(v.x & 0xFFFF0000u),
-                          __uint_as_float(v.y << 16), __uint_as_float(v.y & 0xFFFF0000u)};
-            hi[u] = f32x4{__uint_as_float(v.z << 16), __uint_as_float(v.z & 0xFFFF0000u),
-                          __uint_as_float(v.w << 16), __uint_as_float(v.w & 0xFFFF0000u)};
+            if constexpr (sizeof(TIn) == 2) {
+                const uint4 v = *reinterpret_cast<const uint4*>(X + (ok ? r : r_lo) * D + d0 + 8 * l);
+                lo[u] = f32x4{__uint_as_float(v.x << 16), __uint_as_float(v.x & 0xFFFF0000u),
+                              __uint_as_float(v.y << 16), __uint_as_float(v.y & 0xFFFF0000u)};
+                hi[u] = f32x4{__uint_as_float(v.z << 16), __uint_as_float(v.z & 0xFFFF0000u),
+                              __uint_as_float(v.w << 16), __uint_as_float(v.w & 0xFFFF0000u)};
+            } else {
+                const f32x4* p = reinterpret_cast<const f32x4*>(X + (ok ? r : r_lo) * D + d0 + 8 * l);
+                lo[u] = p[0];
+                hi[u] = p[1];
+            }
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -290,27 +298,22 @@ void launch_acc_mfma(dim3 grid, hipStream_t st, const __bf16* X, int64_t N, cons
                        per);
 }
 
-}  // namespace
-
-extern "C" {
-
 // max k for a feature width D (the LDS table of one dim slice must fit the 160 KiB LDS)
-int alink_kmeans_accum_kmax(int D) { return D == 64 ? 512 : 256; }   // (k * (RS + 1)) * 4 B <= 160 KiB
+int accum_kmax(int D) { return D == 64 ? 512 : 256; }   // (k * (RS + 1)) * 4 B <= 160 KiB
 
-// slab: nchunk * k * D floats, slab_cnt: nchunk * k floats, out: k * (D + 1) doubles.  idx int32 [N] in [0, k)
-// (other values are skipped), w nullable fp32 [N].  D == 64 or D % 128 == 0, D <= 1024.  Returns 0 or an error.
-int alink_kmeans_accum_bf16(const void* X, int64_t N, int D, const int* idx, const float* w, int k, int nchunk,
-                            float* slab, float* slab_cnt, double* out, void* stream) {
-    if (N <= 0 || !(D == 64 || (D % 128 == 0 && D <= 1024)) || k < 1 || k > alink_kmeans_accum_kmax(D) ||
+template <typename TIn>
+int accum_launch(const void* X, int64_t N, int D, const int* idx, const float* w, int k, int nchunk,
+                 float* slab, float* slab_cnt, double* out, void* stream) {
+    if (N <= 0 || !(D == 64 || (D % 128 == 0 && D <= 1024)) || k < 1 || k > accum_kmax(D) ||
         nchunk < 1)
         return 1;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     const int64_t per = (N + nchunk - 1) / nchunk;
-    static bool attr_set = false;  // > 64 KiB of dynamic LDS must be opted into once per kernel
+    static bool attr_set = false;  // > 64 KiB of dynamic LDS must be opted into once per kernel (per TIn)
     if (!attr_set) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void*>(kmeans_accum_kernel<64, float>),
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(kmeans_accum_kernel<64, float, TIn>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (KBLK * 72 + KBLK) * 4) != hipSuccess ||
-            hipFuncSetAttribute(reinterpret_cast<const void*>(kmeans_accum_kernel<64, double>),
+            hipFuncSetAttribute(reinterpret_cast<const void*>(kmeans_accum_kernel<64, double, TIn>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (KBLK * 72 + KBLK) * 8) != hipSuccess)
             return 3;
         attr_set = true;
@@ -322,18 +325,38 @@ int alink_kmeans_accum_bf16(const void* X, int64_t N, int D, const int* idx, con
     static const bool force_f32 = getenv("ALINK_KMEANS_ACC_F32") != nullptr;   // A/B diagnostic (tools/)
     if (!force_f32) {
         const size_t lds = (size_t)(kl * Tab<64>::RS + kl) * sizeof(double);
-        hipLaunchKernelGGL((kmeans_accum_kernel<64, double>), dim3(nchunk, D / 64, kb), dim3(THREADS), lds, st,
-                           (const __bf16*)X, N, D, idx, w, k, per, slab, slab_cnt);
+        hipLaunchKernelGGL((kmeans_accum_kernel<64, double, TIn>), dim3(nchunk, D / 64, kb), dim3(THREADS), lds, st,
+                           (const TIn*)X, N, D, idx, w, k, per, slab, slab_cnt);
     } else {
         const size_t lds = (size_t)(kl * Tab<64>::RS + kl) * sizeof(float);
-        hipLaunchKernelGGL((kmeans_accum_kernel<64, float>), dim3(nchunk, D / 64, kb), dim3(THREADS), lds, st,
-                           (const __bf16*)X, N, D, idx, w, k, per, slab, slab_cnt);
+        hipLaunchKernelGGL((kmeans_accum_kernel<64, float, TIn>), dim3(nchunk, D / 64, kb), dim3(THREADS), lds, st,
+                           (const TIn*)X, N, D, idx, w, k, per, slab, slab_cnt);
     }
     if (hipGetLastError() != hipSuccess) return 2;
     const int64_t total = (int64_t)k * (D + 1);
     hipLaunchKernelGGL(kmeans_accum_reduce_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, slab,
                        slab_cnt, nchunk, k, D, out);
     return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+}  // namespace
+
+extern "C" {
+
+int alink_kmeans_accum_kmax(int D) { return accum_kmax(D); }
+
+// slab: nchunk * k * D floats, slab_cnt: nchunk * k floats, out: k * (D + 1) doubles.  idx int32 [N] in [0, k)
+// (other values are skipped), w nullable fp32 [N].  D == 64 or D % 128 == 0, D <= 1024.  Returns 0 or an error.
+int alink_kmeans_accum_bf16(const void* X, int64_t N, int D, const int* idx, const float* w, int k, int nchunk,
+                            float* slab, float* slab_cnt, double* out, void* stream) {
+    return accum_launch<__bf16>(X, N, D, idx, w, k, nchunk, slab, slab_cnt, out, stream);
+}
+
+// the same accumulate-by-index over fp32 rows (KMeans on fp32 feature matrices: the assignment comes from an fp32
+// GEMM + argmax, ops/kmeans.assign_accumulate_f32_hip); 16-B aligned rows, same D / k limits
+int alink_kmeans_accum_f32(const void* X, int64_t N, int D, const int* idx, const float* w, int k, int nchunk,
+                           float* slab, float* slab_cnt, double* out, void* stream) {
+    return accum_launch<float>(X, N, D, idx, w, k, nchunk, slab, slab_cnt, out, stream);
 }
 
 // MFMA accumulate-by-index for D = 128, k <= 256 (unweighted).  Returns the number of workgroups used through

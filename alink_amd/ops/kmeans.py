@@ -5,11 +5,18 @@
 ``KMeansUtil.updateSumMatrix`` ``KMeansUtil.java:60-85``) — for this rank's rows, ready for the BSP
 all-reduce.
 
-* GPU, bf16 rows, d == 128, k <= 128, unweighted: one persistent MFMA kernel (``csrc/kmeans_v7.hip``) + an
-  fp64 fixed-order slab reduction (``csrc/kmeans_common.hip``, deterministic).
+* GPU, bf16 rows, d == 128, k <= 128, unweighted: one persistent fused kernel + an fp64 fixed-order slab
+  reduction (``csrc/kmeans_common.hip``, deterministic): ``csrc/kmeans_v10.hip`` for k <= 112 (the production
+  kernel: MFMA distances, register-resident VALU accumulate; ``kernel_version``), ``csrc/kmeans_v7.hip`` for
+  112 < k <= 128 (MFMA distances + one-hot MFMA accumulate).
 * GPU, bf16 rows, d in {64, 128, 256}, k <= 256 (512 at d = 64), optionally weighted: two passes — the MFMA
   nearest-centroid kernel (``csrc/kmeans_nearest.hip``) then accumulate-by-index (``csrc/kmeans_accum.hip``:
   the MFMA one-hot GEMM for unweighted d = 128, LDS float atomics otherwise), with a fixed-order fp64 reduction.
+* GPU, fp32 rows, d = 64 or a multiple of 128 up to 1024, k <= 256 (512 at d = 64), optionally weighted: the
+  nearest centroid from a chunked fp32 GEMM (hipBLASLt) + argmax, then the accumulate-by-index kernel over the
+  fp32 rows (``csrc/kmeans_accum.hip`` ``alink_kmeans_accum_f32``: fp64 LDS table, fixed-order fp64 reduction).
+  fp64 feature matrices (VectorAssembler output) reach it through ``ALINK_KMEANS_INPUT=fp32`` (a one-time cast,
+  see ``models/clustering/kmeans.train_kmeans``; ``bf16`` selects the fused bf16 kernels instead).
 * anything else: chunked PyTorch path (fp64 on CPU; on GPU fp32 GEMM of the same bf16-rounded centroids).
 """
 from __future__ import annotations
@@ -24,7 +31,8 @@ import torch
 from . import _lib
 
 __all__ = ["assign_accumulate", "assign", "assign_accumulate_torch", "hip_supported", "prepare_centroids",
-           "general_supported", "assign_accumulate_general_hip", "accumulate_by_index_hip"]
+           "general_supported", "assign_accumulate_general_hip", "accumulate_by_index_hip", "f32_supported",
+           "assign_accumulate_f32_hip", "assign_f32"]
 
 _BUF: Dict[Tuple, Tuple[torch.Tensor, torch.Tensor]] = {}
 HIP_CALLS = 0  # launches of the fused HIP assign+accumulate path (bench / tests read it)
@@ -129,9 +137,10 @@ def _num_cus(device) -> int:
 
 def assign_accumulate_hip(X: torch.Tensor, C: torch.Tensor, grid: Optional[int] = None,
                           assign_out: Optional[torch.Tensor] = None, mode: int = 0) -> torch.Tensor:
-    """[k, d+1] fp64 sums|counts of this rank's rows (``csrc/kmeans_v7.hip``: role-split waves on 16x16x32
-    MFMA, LDS-DMA tile ring).  ``assign_out`` (int32 [N]) also receives every row's centroid id; ``mode`` 1/2
-    are the kernel's load-only / compute-only diagnostics (results meaningless)."""
+    """[k, d+1] fp64 sums|counts of this rank's rows (``csrc/kmeans_v10.hip`` for k <= 112, else
+    ``csrc/kmeans_v7.hip``: role-split waves on 16x16x32 MFMA, LDS-DMA tile ring; ``kernel_version``).
+    ``assign_out`` (int32 [N]) also receives every row's centroid id; ``mode`` 1/2 are the kernel's load-only /
+    compute-only diagnostics (results meaningless)."""
     global HIP_CALLS
     L = _lib.require()
     HIP_CALLS += 1
@@ -313,6 +322,8 @@ def accumulate_by_index_hip(X: torch.Tensor, idx: torch.Tensor, k: int,
         w = weights.to(device=dev, dtype=torch.float32).contiguous()
         if w.numel() != n:
             raise ValueError("weights length mismatch")
+    if X.dtype == torch.float32:
+        return _accumulate_f32(L, X, idx, k, w)
     if d == HIP_D // 2 and w is None and k <= 256 and X.is_contiguous() and n >= 2:
         # d = 64 on the d = 128 MFMA kernel: view row v = (row 2v | row 2v+1); pass A one-hot by idx[2v] keeps
         # dims 0..63, pass B by idx[2v+1] keeps dims 64..127 — two reads of X at MFMA speed instead of one pass of
@@ -365,6 +376,58 @@ def accumulate_by_index_hip(X: torch.Tensor, idx: torch.Tensor, k: int,
     return out
 
 
+def _accumulate_f32(L, X: torch.Tensor, idx: torch.Tensor, k: int, w: Optional[torch.Tensor]) -> torch.Tensor:
+    n, d = X.shape
+    dev = X.device
+    if not f32_supported(X, k):
+        raise ValueError("fp32 accumulate needs contiguous 16-B aligned fp32 [N, D] (D = 64 or a multiple of 128 "
+                         "up to 1024) on the GPU and k within the LDS table limit")
+    nchunk = max(1, min(_num_cus(dev), (n + 4095) // 4096))
+    key = (dev.index, nchunk, k, d, "f32")
+    if key not in _ACC:
+        _ACC.clear()
+        _ACC[key] = (torch.empty(nchunk * k * d, dtype=torch.float32, device=dev),
+                     torch.empty(nchunk * k, dtype=torch.float32, device=dev))
+    slab, slab_cnt = _ACC[key]
+    out = torch.empty((k, d + 1), dtype=torch.float64, device=dev)
+    rc = L.alink_kmeans_accum_f32(X.data_ptr(), n, d, idx.contiguous().data_ptr(), None if w is None else w.data_ptr(),
+                                  k, nchunk, slab.data_ptr(), slab_cnt.data_ptr(), out.data_ptr(), _lib.stream_ptr(dev))
+    if rc != 0:
+        raise RuntimeError(f"alink_kmeans_accum_f32 failed: {rc}")
+    return out
+
+
+def f32_supported(X: torch.Tensor, k: int) -> bool:
+    """Shapes of the fp32 path (GEMM assignment + fp32 accumulate-by-index kernel)."""
+    if not (X.is_cuda and X.dtype == torch.float32 and X.dim() == 2 and X.shape[0] > 0 and X.is_contiguous()
+            and X.data_ptr() % 16 == 0):
+        return False
+    d = X.shape[1]
+    return (d == 64 or (d % 128 == 0 and d <= 1024)) and 1 <= k <= (512 if d == 64 else 256)
+
+
+F32_CALLS = 0
+
+
+def assign_f32(X: torch.Tensor, C: torch.Tensor, chunk: int = 1 << 21) -> torch.Tensor:
+    """int32 nearest-centroid index of every fp32 row: x.c - |c|^2/2 by an fp32 GEMM per chunk, argmax."""
+    Cf = C.to(device=X.device, dtype=torch.float32)
+    half = 0.5 * (Cf * Cf).sum(1)
+    idx = torch.empty(X.shape[0], dtype=torch.int32, device=X.device)
+    for s in range(0, X.shape[0], chunk):
+        sc = torch.addmm(half.neg()[None, :], X[s:s + chunk], Cf.T)
+        idx[s:s + chunk] = sc.argmax(1).to(torch.int32)
+    return idx
+
+
+def assign_accumulate_f32_hip(X: torch.Tensor, C: torch.Tensor,
+                              weights: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """[k, d+1] fp64 sums|counts over fp32 rows: ``assign_f32`` + the fp32 accumulate-by-index kernel."""
+    global F32_CALLS
+    F32_CALLS += 1
+    return accumulate_by_index_hip(X, assign_f32(X, C), C.shape[0], weights)
+
+
 _HELD: Dict[Tuple, torch.Tensor] = {}
 
 
@@ -403,6 +466,8 @@ def assign_accumulate(X: torch.Tensor, C: torch.Tensor, weights: Optional[torch.
         return assign_accumulate_hip(X, C)
     if general_supported(X, C.shape[0]) and hip_ok:
         return assign_accumulate_general_hip(X, C, weights)
+    if f32_supported(X, C.shape[0]) and hip_ok:
+        return assign_accumulate_f32_hip(X, C, weights)
     return assign_accumulate_torch(X, C, weights)
 
 
