@@ -19,57 +19,81 @@
 
 namespace {
 
-constexpr int QR = 128;   // rows per quantize tile
-constexpr int QF = 16;    // features per quantize tile (16 x 256 fp64 thresholds = 32 KiB LDS)
+constexpr int QR = 128;    // rows per quantize tile
+constexpr int QF = 16;     // features per quantize tile (16 x 256 fp64 thresholds = 32 KiB LDS)
+constexpr int QRB = 4096;  // rows per workgroup: the thresholds are staged once per 4096 rows, not per tile
 
 template <typename T>
 __device__ __forceinline__ double ldv(const void* p, int64_t i) {
     return (double)reinterpret_cast<const T*>(p)[i];
 }
 
+// K5 quantize: bin = #thresholds < x (lower bound; NaN / null -> missing), row-major uint8 output.  A workgroup
+// owns QF features x QRB rows: it stages the features' thresholds in LDS once (padded to TP = a power of two
+// with +inf), then walks its rows in 128-row tiles; every thread bins 8 (row, feature) elements per tile with
+// a BRANCHLESS binary search, the 8 searches interleaved (ILP instead of 8 dependent LDS-latency chains), and
+// the tile goes out as 16-byte row pieces.
 __global__ __launch_bounds__(256) void tree_quantize_kernel(const int64_t* __restrict__ col_ptr,
                                                            const int64_t* __restrict__ null_ptr,
                                                            const int32_t* __restrict__ col_is_f32,
                                                            const int32_t* __restrict__ out_col, int Fc, int64_t n,
-                                                           int F, const double* __restrict__ thr,
-                                                           const int32_t* __restrict__ nthr, int T, int missing,
-                                                           uint8_t* __restrict__ out) {
-    extern __shared__ double sthr[];                       // [QF][T]
+                                                           int F, const double* __restrict__ thr, int T, int TP,
+                                                           int missing, uint8_t* __restrict__ out) {
+    extern __shared__ double sthr[];                       // [QF][TP]
     __shared__ uint8_t tile[QR][QF];
     const int f0 = blockIdx.y * QF;
     const int fg = min(QF, Fc - f0);
-    for (int i = threadIdx.x; i < fg * T; i += 256) sthr[i] = thr[(int64_t)f0 * T + i];
-    __syncthreads();
-    const int64_t r0 = (int64_t)blockIdx.x * QR;
-    // lane -> (row, feature): consecutive lanes take consecutive rows of one feature (coalesced column reads)
-    for (int e = threadIdx.x; e < QR * QF; e += 256) {
-        const int f = e / QR, rl = e - f * QR;
-        const int64_t r = r0 + rl;
-        if (f >= fg || r >= n) continue;
-        const int c = f0 + f;
-        const double x = col_is_f32[c] ? ldv<float>((const void*)col_ptr[c], r) : ldv<double>((const void*)col_ptr[c], r);
-        const uint8_t* nm = reinterpret_cast<const uint8_t*>(null_ptr[c]);
-        int b;
-        if (x != x || (nm != nullptr && nm[r])) {
-            b = missing;
-        } else {
-            int lo = 0, hi = nthr[c];
-            const double* t = sthr + f * T;
-            while (lo < hi) {
-                const int mid = (lo + hi) >> 1;
-                if (t[mid] < x) lo = mid + 1;
-                else hi = mid;
-            }
-            b = lo;
-        }
-        tile[rl][f] = (uint8_t)b;
+    for (int i = threadIdx.x; i < QF * TP; i += 256) {
+        const int f = i / TP, j = i - f * TP;
+        sthr[i] = (f < fg && j < T) ? thr[(int64_t)(f0 + f) * T + j] : __builtin_inf();
     }
     __syncthreads();
-    // write back: rows of fg bytes at out[r][out_col[f0 + f]]; contiguous when the output columns are
-    for (int e = threadIdx.x; e < QR * QF; e += 256) {
-        const int rl = e / QF, f = e - rl * QF;
+    const int rl = threadIdx.x & (QR - 1);
+    const int fsub = threadIdx.x >> 7;                     // 0 / 1: this thread's features are fsub + 2 i
+    const void* cp[8];
+    const uint8_t* np[8];
+    bool f32[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int c = f0 + min(fsub + 2 * i, fg - 1);
+        cp[i] = (const void*)col_ptr[c];
+        np[i] = reinterpret_cast<const uint8_t*>(null_ptr[c]);
+        f32[i] = col_is_f32[c] != 0;
+    }
+    const int64_t rb0 = (int64_t)blockIdx.x * QRB;
+    const int64_t rb1 = rb0 + QRB < n ? rb0 + QRB : n;
+    for (int64_t r0 = rb0; r0 < rb1; r0 += QR) {
         const int64_t r = r0 + rl;
-        if (f < fg && r < n) out[r * F + out_col[f0 + f]] = tile[rl][f];
+        const bool rok = r < rb1;
+        double x[8];
+        int pos[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            x[i] = rok ? (f32[i] ? ldv<float>(cp[i], r) : ldv<double>(cp[i], r)) : 0.0;
+            pos[i] = 0;
+        }
+        for (int step = TP >> 1; step >= 1; step >>= 1) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+                pos[i] += sthr[(fsub + 2 * i) * TP + pos[i] + step - 1] < x[i] ? step : 0;
+        }
+        if (TP == 1) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) pos[i] = sthr[(fsub + 2 * i) * TP] < x[i] ? 1 : 0;
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int f = fsub + 2 * i;
+            const bool miss = x[i] != x[i] || (rok && np[i] != nullptr && np[i][r]);
+            if (f < fg) tile[rl][f] = (uint8_t)(miss ? missing : pos[i]);
+        }
+        __syncthreads();
+        for (int e = threadIdx.x; e < QR * QF; e += 256) {
+            const int tr = e / QF, f = e - tr * QF;
+            const int64_t rr = r0 + tr;
+            if (f < fg && rr < rb1) out[rr * F + out_col[f0 + f]] = tile[tr][f];
+        }
+        __syncthreads();
     }
 }
 
@@ -355,10 +379,13 @@ int alink_tree_quantize(const int64_t* col_ptr, const int64_t* null_ptr, const i
                         int T, int missing, uint8_t* out, void* stream) {
     if (n <= 0 || Fc <= 0) return 0;
     if (T < 1 || T > 256 || missing < 0 || missing > 255) return 1;
-    const dim3 grid((unsigned)((n + QR - 1) / QR), (unsigned)((Fc + QF - 1) / QF));
-    hipLaunchKernelGGL(tree_quantize_kernel, grid, dim3(256), (size_t)QF * T * sizeof(double),
+    (void)nthr;                           // padded with +inf past each column's count: the search needs no count
+    int TP = 1;
+    while (TP < T) TP <<= 1;
+    const dim3 grid((unsigned)((n + QRB - 1) / QRB), (unsigned)((Fc + QF - 1) / QF));
+    hipLaunchKernelGGL(tree_quantize_kernel, grid, dim3(256), (size_t)QF * TP * sizeof(double),
                        reinterpret_cast<hipStream_t>(stream), col_ptr, null_ptr, col_is_f32, out_col, Fc, n, F, thr,
-                       nthr, T, missing, out);
+                       T, TP, missing, out);
     return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
