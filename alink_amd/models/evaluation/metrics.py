@@ -189,6 +189,75 @@ def binary_summary(labels_col: Sequence[Any], details: Sequence[str], label_arra
     return _binary_bins(pos_p, is_pos, ll, keep, dev)
 
 
+def _label_codes(label_col):
+    """(distinct label strings, per-row index into them, null mask) of a label Column, computed per distinct value
+    (torch.unique on tensor columns) instead of per row."""
+    vals = label_col.values
+    if isinstance(vals, torch.Tensor) and vals.dim() == 1:
+        lab = vals.detach().cpu()
+        uniq, inv = torch.unique(lab, return_inverse=True)
+        ustr = [str(v) for v in uniq.tolist()]
+        lnull = label_col.nulls.cpu().numpy() if label_col.nulls is not None else np.zeros(len(inv), bool)
+        return ustr, inv.numpy(), lnull
+    lst = label_col.to_list()
+    ustr = sorted({str(v) for v in lst if v is not None})
+    pos = {u: i for i, u in enumerate(ustr)}
+    inv = np.asarray([pos[str(v)] if v is not None else 0 for v in lst], dtype=np.int64)
+    return ustr, inv, np.asarray([v is None for v in lst], dtype=bool)
+
+
+def detail_block_keys(label_col, blk) -> set:
+    """Label strings a ``DetailBlock`` detail column and its label column contribute to the label index (the
+    keys every row's detail map would show, plus the labels of the rows that have a detail)."""
+    ustr, inv, lnull = _label_codes(label_col)
+    ok = ~lnull if blk.nulls is None else (~lnull & ~blk.nulls)
+    keys = {str(x) for x in blk.labels}
+    if ok.any():
+        keys |= {ustr[i] for i in np.unique(inv[ok]).tolist()}
+    return keys
+
+
+def detail_block_valid(blk, label_array: List[str]) -> bool:
+    """This rank's block can be summarised columnar: its two labels are the index's, probabilities in [0, 1]
+    summing to 1 (``parse_detail``'s checks)."""
+    keys = [str(x) for x in blk.labels]
+    if len(keys) != 2 or set(keys) != set(label_array):
+        return False
+    pr = blk.probs
+    if not len(pr):
+        return True
+    c0, c1 = keys.index(label_array[0]), keys.index(label_array[1])
+    return bool(np.all((pr >= 0.0) & (pr <= 1.0)) and np.all(np.abs(pr[:, c0] + pr[:, c1] - 1.0) < PROB_SUM_EPS))
+
+
+def binary_summary_block(label_col, blk, label_array: List[str], device=None):
+    """``binary_summary`` straight from a ``common/detail.DetailBlock`` (no detail strings): the same
+    (positiveBin, negativeBin, logLoss, total) over all ranks — the strings are ``Double.toString`` of these same
+    doubles, which parse back exactly.  None when the block's labels are not the two of ``label_array`` or a
+    probability is out of range (the caller then takes the string path and its exact errors)."""
+    # the fall-back decision is collective (the string path's all-reduce must run on every rank or on none)
+    valid = float(detail_block_valid(blk, label_array))
+    if comm.is_distributed():
+        valid = min(comm.all_gather_object(valid))
+    if valid < 1.0:
+        return None
+    keys = [str(x) for x in blk.labels]
+    ustr, inv, lnull = _label_codes(label_col)
+    ok = ~lnull if blk.nulls is None else (~lnull & ~blk.nulls)
+    c0, c1 = keys.index(label_array[0]), keys.index(label_array[1])
+    pr = blk.probs
+    code = np.array([0 if u == label_array[0] else (1 if u == label_array[1] else -1) for u in ustr],
+                    dtype=np.int64)
+    rc = code[inv] if len(code) else np.zeros(0, np.int64)
+    sel = ok & (rc >= 0)
+    is_pos = rc[sel] == 0
+    p0 = pr[sel, c0]
+    pl = np.where(is_pos, p0, pr[sel, c1])
+    terms = -np.log(np.clip(pl, LOG_LOSS_EPS, 1 - LOG_LOSS_EPS))
+    ll = float(np.cumsum(terms)[-1]) if len(terms) else 0.0       # the loop's left-to-right summation order
+    return _binary_bins(p0, is_pos, ll, int(sel.sum()), device or torch.device("cpu"))
+
+
 def _binary_detail_native(labels_col, details, label_array: List[str]):
     """Bulk path of the per-row detail parsing above: the host C++ parser reads plain two-entry detail strings
     (``_native.parse_binary_detail``) and the checks run vectorised; None -> the caller's JSON loop (which also

@@ -69,6 +69,20 @@ class _EvalClass(_EvalBase):
         labels = mt.column_values(label_col)
         dev = self.env.device
         if detail_col:
+            from ...common.detail import DetailBlock
+            dcol = mt.col(detail_col)
+            if self.BINARY and isinstance(dcol.values, DetailBlock):
+                # columnar detail (probabilities, not strings): label set and bins without per-row parsing
+                label_set = set()
+                for part in comm.all_gather_object(sorted(M.detail_block_keys(mt.col(label_col), dcol.values))):
+                    label_set.update(part)
+                arr = M.build_label_index(label_set, True, pos)
+                fast = M.binary_summary_block(mt.col(label_col), dcol.values, arr, dev)
+                if fast is not None:
+                    pb, nb, ll, n = fast
+                    if n == 0:
+                        raise ValueError("Please check the evaluation input! there is no effective row!")
+                    return self._out(M.binary_metrics(pb, nb, arr, ll, n))
             details = mt.column_values(detail_col)
             keys = set()
             for l, d in zip(labels, details):

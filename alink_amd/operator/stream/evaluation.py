@@ -64,45 +64,12 @@ class _EvalStream(StreamOperator):
         return ("m",) + M.multi_summary_from_pred(labels, preds, self._labels)
 
     def _binary_columnar(self, lcol, blk, p):
-        """Binary summary straight from a ``DetailBlock`` (no detail strings): positive-class probability column,
-        label match by distinct value, log-loss in row order — the values ``binary_summary`` computes from the
-        strings (the strings are ``Double.toString`` of these same doubles, which parse back exactly)."""
-        import numpy as np
-        import torch
-        keys = [str(x) for x in blk.labels]
-        lab = lcol.values
-        if isinstance(lab, torch.Tensor) and lab.dim() == 1:
-            lab = lab.detach().cpu()
-            uniq, inv = torch.unique(lab, return_inverse=True)
-            ustr = [str(v) for v in uniq.tolist()]
-            inv = inv.numpy()
-            lnull = lcol.nulls.cpu().numpy() if lcol.nulls is not None else np.zeros(len(inv), bool)
-        else:
-            vals = lcol.to_list()
-            ustr = sorted({str(v) for v in vals if v is not None})
-            pos = {u: i for i, u in enumerate(ustr)}
-            inv = np.asarray([pos[str(v)] if v is not None else 0 for v in vals], dtype=np.int64)
-            lnull = np.asarray([v is None for v in vals], dtype=bool)
-        ok = ~lnull if blk.nulls is None else (~lnull & ~blk.nulls)
+        """Binary summary straight from a ``DetailBlock`` (no detail strings; ``metrics.binary_summary_block``)."""
         if self._labels is None:
-            present = {ustr[i] for i in np.unique(inv[ok]).tolist()} if ok.any() else set()
-            self._labels = M.build_label_index(set(keys) | present, True, _pget(p, "positiveLabelValueString"))
-        la = self._labels
-        if set(keys) != set(la):
-            return None
-        c0, c1 = keys.index(la[0]), keys.index(la[1])
-        pr = blk.probs
-        if not (np.all((pr >= 0.0) & (pr <= 1.0)) and np.all(np.abs(pr[:, c0] + pr[:, c1] - 1.0) < M.PROB_SUM_EPS)):
-            return None
-        code = np.array([0 if u == la[0] else (1 if u == la[1] else -1) for u in ustr], dtype=np.int64)
-        rc = code[inv] if len(code) else np.zeros(0, np.int64)
-        sel = ok & (rc >= 0)
-        is_pos = rc[sel] == 0
-        p0 = pr[sel, c0]
-        pl = np.where(is_pos, p0, pr[sel, c1])
-        terms = -np.log(np.clip(pl, M.LOG_LOSS_EPS, 1 - M.LOG_LOSS_EPS))
-        ll = float(np.cumsum(terms)[-1]) if len(terms) else 0.0
-        return ("b",) + M._binary_bins(p0, is_pos, ll, int(sel.sum()), torch.device("cpu"))
+            self._labels = M.build_label_index(M.detail_block_keys(lcol, blk), True,
+                                               _pget(p, "positiveLabelValueString"))
+        res = M.binary_summary_block(lcol, blk, self._labels)
+        return None if res is None else ("b",) + res
 
     @staticmethod
     def _metrics(s, labels):

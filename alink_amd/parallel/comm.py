@@ -200,7 +200,7 @@ def shutdown():
     global _OBJ_GROUP
     from . import oneshot
     failure = None
-    if oneshot._INSTANCE is not None and dist.is_available() and dist.is_initialized():
+    if oneshot._INSTANCE is not None:
         # peers may still be reading this rank's staging slot in their last one-shot call: drain every rank's
         # stream, meet on the host group, then unmap / free
         torch.cuda.synchronize(oneshot._INSTANCE.device)
@@ -208,7 +208,8 @@ def shutdown():
             oneshot._INSTANCE.check(wait=True)
         except RuntimeError as e:
             failure = e
-        dist.barrier(group=_OBJ_GROUP)
+        if dist.is_available() and dist.is_initialized():
+            dist.barrier(group=_OBJ_GROUP)
     oneshot.reset()
     if dist.is_available() and dist.is_initialized():
         dist.destroy_process_group()

@@ -81,3 +81,34 @@ def test_eval_binary_stream_window_and_all():
     assert [r[0] for r in box] == ["window", "all"]
     auc = json.loads(json.loads(box[1][1])["AUC"])
     assert auc == pytest.approx(0.8333333333333333)
+
+
+def test_binary_eval_on_columnar_detail_equals_string_detail():
+    """EvalBinaryClassBatchOp / EvalBinaryClassStreamOp on a LinearModelMapper detail column (columnar
+    DetailBlock: probabilities, no strings) give the same metrics as on the materialised JSON strings."""
+    import numpy as np
+    import pandas as pd
+    from alink_amd import (BatchOperator, LogisticRegressionTrainBatchOp, LogisticRegressionPredictBatchOp,
+                           EvalBinaryClassBatchOp)
+    from alink_amd.common.detail import DetailBlock
+    from alink_amd.common.table import Column, MTable
+    from alink_amd.operator.batch.source import TableSourceBatchOp
+    rng = np.random.default_rng(3)
+    X = rng.normal(size=(3000, 4))
+    y = (X @ np.array([1.0, -0.5, 0.3, 0.0]) + 0.5 * rng.normal(size=3000) > 0).astype(int)
+    df = pd.DataFrame({f"x{i}": X[:, i] for i in range(4)})
+    df["y"] = y
+    src = BatchOperator.fromDataframe(df, schemaStr="x0 double, x1 double, x2 double, x3 double, y int")
+    model = LogisticRegressionTrainBatchOp().setFeatureCols([f"x{i}" for i in range(4)]).setLabelCol("y") \
+        .linkFrom(src)
+    pred = LogisticRegressionPredictBatchOp().setPredictionCol("p").setPredictionDetailCol("d") \
+        .linkFrom(model, src)
+    mt = pred.getOutputTable()
+    di = mt.schema.names.index("d")
+    assert isinstance(mt.cols[di].values, DetailBlock)
+    strs = MTable(mt.schema, [c if i != di else Column(c.to_list()) for i, c in enumerate(mt.cols)])
+    a = EvalBinaryClassBatchOp().setLabelCol("y").setPredictionDetailCol("d").linkFrom(pred).collectMetrics()
+    b = EvalBinaryClassBatchOp().setLabelCol("y").setPredictionDetailCol("d") \
+        .linkFrom(TableSourceBatchOp(strs)).collectMetrics()
+    for name in ("AUC", "LogLoss", "Accuracy", "PRC", "F1", "Precision"):
+        assert getattr(a, "get" + name)() == getattr(b, "get" + name)(), name

@@ -131,3 +131,20 @@ def test_oneshot_sequence_number_wraps():
     finally:
         views[0].owned = bases
         views[0].close()
+
+
+def test_timeout_on_the_last_reduction_raises_at_shutdown(monkeypatch):
+    """A peer that never arrives for the job's LAST one-shot reduction (no later call would check the error word)
+    makes comm.shutdown() raise after its cleanup instead of letting a NaN model pass silently."""
+    import alink_amd.parallel.oneshot as O
+    from alink_amd.parallel import comm
+    monkeypatch.setattr(O, "TIMEOUT_S", 0.05)
+    cap = 1 << 12
+    bases = [OneShot.alloc(cap, 2) for _ in range(2)]
+    v = OneShot("cuda", 2, 0, cap, bases, bases, [])
+    x = torch.ones(64, dtype=torch.float64, device="cuda")
+    v.all_reduce_(x)                                   # peer 1 never signals
+    monkeypatch.setattr(O, "_INSTANCE", v)
+    with pytest.raises(RuntimeError, match="timed out"):
+        comm.shutdown()
+    assert O._INSTANCE is None                         # cleaned up before raising
