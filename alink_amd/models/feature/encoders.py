@@ -52,16 +52,41 @@ def _ename(v, default):
 # ---------------------------------------------------------------------------------------------------
 # token dictionaries
 # ---------------------------------------------------------------------------------------------------
+def _column_token_counts(col) -> Dict[str, int]:
+    """Token (``String.valueOf``) -> count of one column without a per-cell Python loop: numeric / boolean tensor
+    columns count distinct values with ``torch.unique`` (formatting each distinct value once), string columns
+    go through ``collections.Counter`` (C) over the values."""
+    from collections import Counter
+    v = col.values
+    if isinstance(v, torch.Tensor) and v.dim() == 1:
+        x = v if col.nulls is None else v[~col.nulls.to(v.device)]
+        if x.numel() == 0:
+            return {}
+        x = x.detach().cpu()
+        out: Dict[str, int] = {}
+        if x.dtype.is_floating_point:
+            # torch.unique merges -0.0 into 0.0 (and splits NaNs): String.valueOf keeps "-0.0" apart, NaN as one
+            negz = (x == 0) & torch.signbit(x)
+            nz = int(negz.sum())
+            if nz:
+                out["-0.0"] = nz
+                x = x[~negz]
+        uniq, cnt = torch.unique(x, return_counts=True)
+        for u, c in zip(uniq.tolist(), cnt.tolist()):
+            k = java_str(u)
+            out[k] = out.get(k, 0) + int(c)
+        return out
+    vals = col.to_list()
+    if all(x is None or isinstance(x, str) for x in vals):
+        cnt = Counter(vals)
+        cnt.pop(None, None)
+        return dict(cnt)
+    cnt = Counter(java_str(x) for x in vals if x is not None)
+    return dict(cnt)
+
+
 def _global_token_counts(mt: MTable, cols: Sequence[str]) -> List[Dict[str, int]]:
-    local = []
-    for c in cols:
-        cnt: Dict[str, int] = {}
-        for v in mt.col(c).to_list():
-            if v is None:
-                continue
-            k = java_str(v)
-            cnt[k] = cnt.get(k, 0) + 1
-        local.append(cnt)
+    local = [_column_token_counts(mt.col(c)) for c in cols]
     merged = [dict() for _ in cols]
     for part in comm.all_gather_object(local):
         for i, d in enumerate(part):
