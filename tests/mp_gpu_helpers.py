@@ -223,6 +223,73 @@ def _ftrl_mode(out, mode, async_reduce=False):
     out["device"] = str(env.device)
 
 
+def _ftrl_pipeline(out, mode):
+    """The BASELINE config-5 StreamOp pipeline at test size (tools/ftrl_pipeline_bench.py): every rank streams
+    its block of one synthetic click log -> FeatureHasher -> FtrlTrainStreamOp (``mode``) -> FtrlPredictStreamOp
+    -> EvalBinaryClassStreamOp; the final cumulative metrics and the last snapshot's coefficients."""
+    import json as _json
+    import numpy as np
+    from alink_amd import (useLocalEnv, FeatureHasherBatchOp, LogisticRegressionTrainBatchOp, FtrlTrainStreamOp,
+                           FtrlPredictStreamOp, EvalBinaryClassStreamOp, FeatureHasherStreamOp, StreamOperator,
+                           CollectStreamOp)
+    from alink_amd.operator.batch.source import TableSourceBatchOp
+    from alink_amd.operator.stream.source import TableSourceStreamOp
+    from alink_amd.parallel import comm
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from ftrl_pipeline_bench import click_table
+    os.environ["ALINK_STREAM_BATCH"] = os.environ.get("ALINK_TEST_BATCH", "4096")
+    env = useLocalEnv(1)
+    fields = [f"C{f + 1}" for f in range(8)]
+    full = click_table(20_000 + 122_880, 8, 500, env.device, seed=7)
+    init_tab = full.slice(0, 20_000)
+    ws, me = comm.get_world_size(), comm.get_rank()
+    # rank r streams the r-th micro-batch of every group of ws consecutive ones: global step t of P ranks then holds
+    # exactly the rows one rank streams at P x the micro-batch (rank order == row order)
+    import torch
+    mb = int(os.environ["ALINK_STREAM_BATCH"])
+    rows = torch.arange(122_880).view(-1, mb)[me::ws].reshape(-1) + 20_000
+    part = full.take(rows)
+
+    def hasher(cls):
+        return cls().setSelectedCols(fields).setCategoricalCols(fields).setOutputCol("vec").setNumFeatures(20000) \
+            .setReservedCols(["label"])
+    init_vec = hasher(FeatureHasherBatchOp).linkFrom(TableSourceBatchOp(init_tab))
+    # the warm start model is trained on the replicated first rows (identical on every rank)
+    init_vec.getOutputTable().replicated = True
+    init_model = LogisticRegressionTrainBatchOp().setVectorCol("vec").setLabelCol("label").setMaxIter(10) \
+        .linkFrom(init_vec)
+    hashed = hasher(FeatureHasherStreamOp).linkFrom(TableSourceStreamOp(part))
+    # a snapshot every micro-batch: the predictor serves the model of the previous step (prequential evaluation)
+    train = FtrlTrainStreamOp(init_model).setVectorCol("vec").setLabelCol("label").setTimeInterval(0.0) \
+        .setAlpha(0.1).setBeta(0.1).setL1(0.01).setL2(0.01).setUpdateMode(mode).linkFrom(hashed)
+    snaps = []
+    train.link(CollectStreamOp(snaps))
+    pred = FtrlPredictStreamOp(init_model).setVectorCol("vec").setPredictionCol("pred") \
+        .setPredictionDetailCol("detail").setReservedCols(["label"]).linkFrom(train, hashed)
+    box = []
+    EvalBinaryClassStreamOp().setLabelCol("label").setPredictionDetailCol("detail").linkFrom(pred) \
+        .link(CollectStreamOp(box))
+    StreamOperator.execute()
+    last = _json.loads([r for r in box if r[0] == "all"][-1][1])
+    out["auc"] = float(last["AUC"])
+    out["logloss"] = float(last["LogLoss"])
+    out["total"] = int(last["TotalSamples"])
+    from alink_amd.models.linear.model import LinearModelDataConverter
+    lb = max(r[0] for r in snaps)
+    m = LinearModelDataConverter().load([tuple(r[2:]) for r in snaps if r[0] == lb])
+    out["coef_head"] = np.asarray(m.coefVector.data)[:50].tolist()
+    out["backend"] = comm._backend()
+    out["device"] = str(env.device)
+
+
+def scenario_ftrl_pipeline_sharded(out):
+    _ftrl_pipeline(out, "SHARDED")
+
+
+def scenario_ftrl_pipeline_dp(out):
+    _ftrl_pipeline(out, "DATA_PARALLEL")
+
+
 def scenario_cross_gpu(out):
     """Ring blockwise top-K with device query / item blocks (the top-K merge kernel on the GPU)."""
     import torch

@@ -167,6 +167,23 @@ def test_als_multiprocess_gpu_matches_one_rank(tmp_path):
         np.testing.assert_allclose([p for _, _, p in o["doc_pred"]], ref, atol=1e-2)
 
 
+@pytest.mark.parametrize("mode", ["sharded", "dp"])
+def test_ftrl_stream_pipeline_multiprocess_gpu(tmp_path, mode, monkeypatch):
+    """The config-5 StreamOp pipeline (source -> FeatureHasher -> FtrlTrain -> FtrlPredict -> EvalBinaryClass) over
+    2 ranks on the GPU, each streaming 4096-row micro-batches, against 1 rank streaming 8192-row micro-batches of
+    the same rows (the same global steps): every rank ends with the same model, the prequential evaluation covers
+    the whole stream on every rank (all-reduced bins), and model and AUC match 1 rank."""
+    monkeypatch.setenv("ALINK_TEST_BATCH", "8192")
+    one = _run("ftrl_pipeline_" + mode, 1, tmp_path, timeout=240)[0]
+    monkeypatch.setenv("ALINK_TEST_BATCH", "4096")
+    two = _run("ftrl_pipeline_" + mode, 2, tmp_path, timeout=240)
+    assert "cuda" in one["device"]
+    assert two[0]["coef_head"] == two[1]["coef_head"]
+    assert one["total"] == 122_880 and all(o["total"] == 122_880 for o in two)
+    assert one["auc"] > 0.65 and abs(two[0]["auc"] - one["auc"]) < 0.01
+    np.testing.assert_allclose(two[0]["coef_head"], one["coef_head"], rtol=1e-6, atol=1e-9)
+
+
 def test_ring_topk_multiprocess_gpu(tmp_path):
     """Ring blockwise top-K with device blocks over 2 ranks == torch.topk of the full score matrix."""
     for o in _run("cross_gpu", 2, tmp_path):
