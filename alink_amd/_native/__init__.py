@@ -13,7 +13,7 @@ import numpy as np
 
 __all__ = ["lib", "parse_csv_lines", "murmur3_utf16", "murmur3_bytes", "murmur3_utf8", "parse_dense_vectors", "ftrl_update_csr",
            "ftrl_partial_margin", "ftrl_shard_update", "parse_binary_detail", "java_double_join",
-           "java_double_rows"]
+           "java_double_rows", "sample_thresholds"]
 
 # ALINK_NATIVE_LIB points at another build of the same sources (e.g. the AddressSanitizer build of
 # tools/asan_host.py)
@@ -37,6 +37,8 @@ if os.path.exists(_PATH):
             lib.alink_java_double_join.restype = ctypes.c_int64
         if hasattr(lib, "alink_java_double_rows"):
             lib.alink_java_double_rows.restype = ctypes.c_int64
+        if hasattr(lib, "alink_sample_thresholds"):
+            lib.alink_sample_thresholds.restype = ctypes.c_int64
     except OSError:
         lib = None
 
@@ -169,6 +171,18 @@ def java_double_rows(x, sep: str = " ") -> Optional[List[str]]:
     text = buf[:total].tobytes().decode("ascii")
     starts = np.concatenate([[0], ends[:n - 1]]) if n else np.zeros(0, np.int64)
     return [text[s:e] for s, e in zip(starts.tolist(), ends[:n].tolist())]
+
+
+def sample_thresholds(thr, step: float, err: float) -> Optional[np.ndarray]:
+    """Kept indices of the curve-threshold sampling (index 0, then each threshold at least ``step`` below the
+    last kept one or within ``err`` of 0.5) as int64, scanned in C++; None without the library."""
+    if lib is None or getattr(lib, "alink_sample_thresholds", None) is None:
+        return None
+    a = np.ascontiguousarray(np.asarray(thr, dtype=np.float64))
+    keep = np.empty(max(a.size, 1), dtype=np.int64)
+    m = lib.alink_sample_thresholds(_ptr(a), ctypes.c_int64(a.size), ctypes.c_double(step), ctypes.c_double(err),
+                                    _ptr(keep))
+    return keep[:m]
 
 
 def parse_binary_detail(strings: Sequence[str], key0: str, key1: str):

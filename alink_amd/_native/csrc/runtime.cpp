@@ -420,6 +420,22 @@ extern "C" int64_t alink_java_double_rows(const double* x, int64_t n, int64_t k,
     return p;
 }
 
+// Threshold sampling of a binary-classification curve over descending thresholds: index 0, then every index
+// whose threshold is at least `step` below the last kept one, or within `err` of 0.5 (one sequential scan).
+extern "C" int64_t alink_sample_thresholds(const double* thr, int64_t n, double step, double err, int64_t* keep) {
+    if (n <= 0) return 0;
+    int64_t m = 0;
+    keep[m++] = 0;
+    double pre = thr[0];
+    for (int64_t i = 1; i < n; ++i) {
+        if (std::fabs(pre - thr[i]) >= step || std::fabs(thr[i] - 0.5) < err) {
+            keep[m++] = i;
+            pre = thr[i];
+        }
+    }
+    return m;
+}
+
 extern "C" int64_t alink_java_double_join(const double* x, int64_t n, char* out) {
     // one thread: ~90 ns per value (1e6 coefficients ~0.1 s); an OpenMP split measured slower on the 8-CPU host
     int64_t p = 0;

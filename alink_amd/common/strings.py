@@ -130,6 +130,13 @@ class StringBlock:
         """Rows by index (tensor / sequence / numpy / boolean mask / slice), as one byte gather."""
         dev = self.device
         n = len(self)
+        if isinstance(idx, slice) and idx.step in (None, 1):
+            # contiguous rows (stream micro-batches, MTable.slice): one byte-range view, offsets rebased
+            a, b, _ = idx.indices(n)
+            b = max(a, b)
+            bounds = self.offsets[[a, b]].tolist()
+            return StringBlock(self.data[bounds[0]:bounds[1]], self.offsets[a:b + 1] - bounds[0],
+                               None if self.nulls is None else self.nulls[a:b])
         if isinstance(idx, slice):
             idx = torch.arange(n, device=dev)[idx]
         elif isinstance(idx, torch.Tensor):

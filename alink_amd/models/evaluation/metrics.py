@@ -20,6 +20,7 @@ from typing import Any, Dict, List, Optional, Sequence
 import numpy as np
 import torch
 
+from ... import _native
 from ...common.javafmt import gson_dumps
 from ...common.params import Params
 from ...parallel import comm
@@ -548,8 +549,9 @@ def binary_metrics(posb: np.ndarray, negb: np.ndarray, labels: List[str], loglos
     threshold arrays, confusion matrix at the threshold nearest 0.5."""
     eff = np.nonzero((posb != 0) | (negb != 0))[0]
     mid = DETAIL_BIN_NUMBER // 2
-    if mid not in set(eff.tolist()):
-        eff = np.sort(np.append(eff, mid))
+    at = int(np.searchsorted(eff, mid))
+    if at == len(eff) or eff[at] != mid:
+        eff = np.insert(eff, at, mid)
     total_true, total_false = int(posb[eff].sum()), int(negb[eff].sum())
     if total_true + total_false != total:
         raise ValueError("The effective number in bins must be equal to total!")
@@ -576,20 +578,23 @@ def binary_metrics(posb: np.ndarray, negb: np.ndarray, labels: List[str], loglos
     _set(params, "AUC", _area(roc_x, roc_y))
     _set(params, "PRC", _area(pr_x, pr_y))
     _set(params, "K-S", float(np.max(np.abs(roc_x - roc_y))))
-    # sampling of thresholds at 0.001 resolution (plus the 0.5 point)
-    keep = np.asarray(_sample_thresholds(thr))
-    _set(params, "RocCurve", [roc_x[keep].tolist(), roc_y[keep].tolist()])
-    _set(params, "RecallPrecisionCurve", [pr_x[keep].tolist(), pr_y[keep].tolist()])
-    _set(params, "LiftChart", [lift_x[keep].tolist(), lift_y[keep].tolist()])
+    # sampling of thresholds at 0.001 resolution (plus the 0.5 point); float64 arrays go to the Params JSON
+    # writer as they are (same Double.toString digits as their tolist(), formatted in C++ when long)
+    keep = _native.sample_thresholds(thr, PROBABILITY_INTERVAL - PROBABILITY_ERROR, PROBABILITY_ERROR)
+    if keep is None:
+        keep = np.asarray(_sample_thresholds(thr))
+    _set(params, "RocCurve", [roc_x[keep], roc_y[keep]])
+    _set(params, "RecallPrecisionCurve", [pr_x[keep], pr_y[keep]])
+    _set(params, "LiftChart", [lift_x[keep], lift_y[keep]])
     sk = keep[1:]
     s_thr = thr[sk]
-    _set(params, "ThresholdArray", s_thr.tolist())
+    _set(params, "ThresholdArray", s_thr)
     # per-threshold 2x2 confusion counts of class 0, every computation vectorised over the thresholds (the same
     # float64 operations, in the same order, as the per-matrix _CM computers)
     TP, FP = tp[sk], fp[sk]
     FN, TN = float(total_true) - TP, float(total_false) - FP
     for name, arr in _binary_arrays(TP, FP, FN, TN).items():
-        _set(params, name + "Array", arr.tolist())
+        _set(params, name + "Array", arr)
     if logloss >= 0:
         _set(params, "LogLoss", logloss / total)
     mid_i = int(np.argmin(np.abs(s_thr - 0.5)))

@@ -1,15 +1,22 @@
 """Streaming evaluation (reference ``A/operator/stream/evaluation/{EvalBinaryClassStreamOp,EvalMultiClassStreamOp}``,
-``BaseEvalClassStreamOp.java:44-90``): for every window (= micro-batch here) two rows are emitted —
-``("window", metrics of the window)`` and ``("all", metrics of everything seen so far)`` — in the schema
-``(Statistics STRING, Data STRING)``.  The cumulative summary is kept as merged histograms/matrices."""
+``operator/common/evaluation/BaseEvalClassStreamOp.java:44-90``): processing-time windows of ``timeInterval``
+seconds (default 3, ``timeWindowAll`` in the reference).  Every micro-batch is reduced to a summary (binned
+positive / negative counts, or a confusion matrix) and merged into the open window; when the window has been open
+``timeInterval`` seconds — on any rank, agreed over the host group — two rows are emitted: ``("window", metrics of
+the window)`` and ``("all", metrics of everything seen so far)``, in the schema ``(Statistics STRING, Data
+STRING)``.  The open window is flushed when the stream ends.  ``timeInterval`` 0 emits after every micro-batch."""
 from __future__ import annotations
 
+import time
+
 import numpy as np
+import torch
 
 from ...common.detail import DetailBlock
 from ...common.table import MTable
 from ...common.types import TableSchema, Types
 from ...models.evaluation import metrics as M
+from ...parallel import comm
 from .base import StreamOperator
 
 __all__ = ["EvalBinaryClassStreamOp", "EvalMultiClassStreamOp"]
@@ -31,6 +38,8 @@ class _EvalStream(StreamOperator):
         self._connect(*inputs)
         self._schema = _SCHEMA
         self._acc = None
+        self._win = None
+        self._win_t0 = None
         self._labels = None
         return self
 
@@ -86,16 +95,40 @@ class _EvalStream(StreamOperator):
         ll = a[2] + b[2] if a[2] >= 0 and b[2] >= 0 else -1.0
         return ("m", a[1] + b[1], ll, a[3] + b[3])
 
-    def on_batch(self, port, mt):
-        if mt.num_rows == 0:
-            return
-        s = self._summary(mt)
-        if s[-1] == 0:
+    def _interval(self) -> float:
+        v = _pget(self.getParams(), "timeInterval")
+        return 3.0 if v is None else float(v)
+
+    def _window_due(self) -> bool:
+        """Whether the open window has lasted ``timeInterval`` seconds; under a process group every rank takes
+        the same decision (the longest-open window of any rank), so the emitted windows line up."""
+        age = time.perf_counter() - self._win_t0 if self._win_t0 is not None else 0.0
+        if comm.is_distributed():
+            age = float(comm.host_all_gather(torch.tensor([age], dtype=torch.float64)).max())
+        return age >= self._interval()
+
+    def _emit_window(self):
+        s, self._win, self._win_t0 = self._win, None, None
+        if s is None or s[-1] == 0:
             return
         self._acc = self._merge(self._acc, s)
         rows = [("window", self._metrics(s, self._labels).serialize()[0]),
                 ("all", self._metrics(self._acc, self._labels).serialize()[0])]
         self._emit(MTable.from_rows(rows, _SCHEMA))
+
+    def on_batch(self, port, mt):
+        if mt.num_rows == 0:
+            return
+        s = self._summary(mt)
+        if s[-1] != 0:
+            if self._win_t0 is None:
+                self._win_t0 = time.perf_counter()
+            self._win = self._merge(self._win, s)
+        if self._window_due():
+            self._emit_window()
+
+    def on_finish(self, port):
+        self._emit_window()
 
 
 class EvalBinaryClassStreamOp(_EvalStream):

@@ -294,6 +294,34 @@ def scenario_fm(out):
     out["acc"] = sum(int(r[-1] == r[-2]) for r in pred) / max(len(pred), 1)
 
 
+def scenario_eval_stream_windows(out):
+    """EvalBinaryClassStreamOp with 1 s windows while rank 1 stalls 0.3 s per micro-batch: the window decision
+    is agreed over the host group, so both ranks emit the same windows with the same (all-reduced) metrics."""
+    import time
+    import numpy as np
+    import pandas as pd
+    os.environ["ALINK_STREAM_BATCH"] = "40"
+    from alink_amd import useLocalEnv, StreamOperator, EvalBinaryClassStreamOp, CollectStreamOp
+    from alink_amd.parallel import comm
+    useLocalEnv(1)
+    rng = np.random.default_rng(5)
+    p = rng.random(480)
+    y = (rng.random(480) < p).astype(int)
+    df = pd.DataFrame({"label": y, "detail": [f'{{"1":{v},"0":{1 - v}}}' for v in p]})
+    box = []
+    ev = EvalBinaryClassStreamOp().setLabelCol("label").setPredictionDetailCol("detail").setTimeInterval(1)
+    ev.linkFrom(StreamOperator.fromDataframe(df, schemaStr="label int, detail string")).link(CollectStreamOp(box))
+    if comm.get_rank() == 1:
+        orig = ev.on_batch
+
+        def slow(port, mt):
+            time.sleep(0.3)
+            return orig(port, mt)
+        ev.on_batch = slow
+    StreamOperator.execute()
+    out["rows"] = [list(r) for r in box]
+
+
 def _ftrl_run(mode, rows, batch, async_reduce=False):
     import numpy as np
     import pandas as pd

@@ -392,3 +392,11 @@ def test_csv_source_byte_range_split(tmp_path):
     assert len(one["rows"]) == 503 and one["rows"][0] == [0, "name0", 0.0]
     assert all(o["rows"] == one["rows"] for o in three)
     assert sum(o["local_rows"] for o in three) == 503 and max(o["local_rows"] for o in three) < 503
+
+
+def test_eval_stream_windows_agree_across_ranks(tmp_path):
+    outs = _run("eval_stream_windows", 2, tmp_path)
+    a, b = outs[0]["rows"], outs[1]["rows"]
+    assert [r[0] for r in a] == [r[0] for r in b]
+    assert len(a) >= 4                                   # rank 1's stalls close at least one window early
+    assert json.loads(a[-1][1])["TotalSamples"] == json.loads(b[-1][1])["TotalSamples"]

@@ -83,6 +83,28 @@ def test_eval_binary_stream_window_and_all():
     assert auc == pytest.approx(0.8333333333333333)
 
 
+def test_eval_stream_processing_time_windows(monkeypatch):
+    """Windows follow ``timeInterval`` (reference ``timeWindowAll``): 0 -> one window per micro-batch; the default
+    3 s over a sub-second stream -> one window flushed at the end.  The final "all" row is the same either way."""
+    monkeypatch.setenv("ALINK_STREAM_BATCH", "2")
+    _, df = _in()
+    out = {}
+    for ti in (0, None):
+        box = []
+        src = StreamOperator.fromDataframe(df, schemaStr="label string, detailInput string")
+        op = EvalBinaryClassStreamOp().setLabelCol("label").setPredictionDetailCol("detailInput")
+        if ti is not None:
+            op.setTimeInterval(ti)
+        op.linkFrom(src).link(CollectStreamOp(box))
+        StreamOperator.execute()
+        out[ti] = box
+    assert [r[0] for r in out[0]] == ["window", "all"] * 3            # 5 rows in micro-batches of 2
+    assert [r[0] for r in out[None]] == ["window", "all"]
+    assert out[0][-1][1] == out[None][-1][1] == out[None][0][1]
+    win = [json.loads(r[1]) for r in out[0] if r[0] == "window"]
+    assert [int(json.loads(w["TotalSamples"])) for w in win] == [2, 2, 1]
+
+
 def test_binary_eval_on_columnar_detail_equals_string_detail():
     """EvalBinaryClassBatchOp / EvalBinaryClassStreamOp on a LinearModelMapper detail column (columnar
     DetailBlock: probabilities, no strings) give the same metrics as on the materialised JSON strings."""
