@@ -307,15 +307,17 @@ def test_hip_general_split_search_matches_torch(kind, ncls):
     is_cat = [bool(f % 3 == 0) for f in range(F)]
     cfg = SplitConfig(kind=kind, max_depth=5, min_samples_per_leaf=2, n_classes=ncls,
                       min_sample_ratio_per_child=0.01)
-    tb = SimpleNamespace(cfg=cfg, d=SimpleNamespace(is_cat=is_cat), _multiway_gain=None)
-    tb.is_cat = torch.tensor(is_cat)
-    tb._multiway_gain = lambda *a: TreeBuilder._multiway_gain(tb, *a)
+    def builder(dev):
+        tb = TreeBuilder.__new__(TreeBuilder)         # only the search state: cfg, data flags, is_cat
+        tb.cfg, tb.d, tb.is_cat = cfg, SimpleNamespace(is_cat=is_cat), torch.tensor(is_cat, device=dev)
+        return tb
     order = torch.arange(F).expand(m, F).clone()
     ok = torch.ones((m, F), dtype=torch.bool)
-    g0, f0, j0, mb0, a0, perm = TreeBuilder._search(tb, Hn, order, ok)
-    tbg = SimpleNamespace(cfg=cfg, d=tb.d, is_cat=tb.is_cat.cuda())
-    tbg._multiway_gain = lambda *a: TreeBuilder._multiway_gain(tbg, *a)
-    g1, f1, j1, mb1, a1, _ = TreeBuilder._search_hip(tbg, Hn.cuda(), order.cuda(), ok.cuda())
+    g0, f0, j0, mb0, a0, perm = builder("cpu")._search(Hn, order, ok)
+    assert tops.gpu_kernels_ok()
+    g1, f1, j1, mb1, a1, perm1 = builder("cuda")._search(Hn.cuda(), order.cuda(), ok.cuda())
+    if Hn.shape[3] in tops.SPLIT_S:
+        assert perm1 is None                          # the HIP search ran (no bin order back)
     np.testing.assert_allclose(g1.cpu().numpy(), g0.numpy(), rtol=1e-9, atol=1e-12)
     assert f1.cpu().tolist() == f0.tolist() and mb1.cpu().tolist() == mb0.tolist()
     assert a1.cpu().tolist() == a0.tolist()
@@ -385,9 +387,13 @@ def test_hip_gbdt_split_matches_torch_search():
     order = torch.arange(F, device="cuda").expand(m, F).clone()
     ok = torch.ones((m, F), dtype=torch.bool, device="cuda")
     ok[:, 3] = False
-    got = tb._search_gbdt_hip(Hn, order, ok)
-    data.is_cat = [True] + [False] * (F - 1)      # forces the torch path (categorical present) ...
-    tb.is_cat = torch.zeros(F, dtype=torch.bool, device="cuda")   # ... but with no categorical feature inside
-    ref = tb._search(Hn, order, ok)
+    got = tb._search(Hn, order, ok)                # K8 on the device (continuous GBDT)
+    assert got[5] is None
+    saved = tops.gpu_kernels_ok
+    tops.gpu_kernels_ok = lambda: False            # the vectorised torch search on the same device tensors
+    try:
+        ref = tb._search(Hn, order, ok)
+    finally:
+        tops.gpu_kernels_ok = saved
     torch.testing.assert_close(got[0], ref[0], rtol=1e-9, atol=1e-9)
     assert torch.equal(got[1], ref[1]) and torch.equal(got[2], ref[2]) and torch.equal(got[4], ref[4])

@@ -43,19 +43,19 @@ def main():
         H = H.float().double()
         is_cat = [f % 10 < 3 for f in range(F)]               # 30 % categorical features
         cfg = SplitConfig(kind=kind, max_depth=8, min_samples_per_leaf=5, n_classes=ncls)
-        tb = SimpleNamespace(cfg=cfg, d=SimpleNamespace(is_cat=is_cat), is_cat=torch.tensor(is_cat, device=dev))
-        tb._multiway_gain = lambda *x, tb=tb: TreeBuilder._multiway_gain(tb, *x)
+        tb = TreeBuilder.__new__(TreeBuilder)          # only the search state: cfg, data flags, is_cat
+        tb.cfg, tb.d, tb.is_cat = cfg, SimpleNamespace(is_cat=is_cat), torch.tensor(is_cat, device=dev)
         order = torch.arange(F, device=dev).expand(m, F).clone()
         ok = torch.ones((m, F), dtype=torch.bool, device=dev)
         res = {"criterion": kind, "nodes": m, "features": F, "bins": B, "S": S}
         outs = {}
         for name in ("hip", "torch"):
-            r = (TreeBuilder._search_hip(tb, H, order, ok) if name == "hip" else _torch_search(tb, H, order, ok))
+            r = (TreeBuilder._search(tb, H, order, ok) if name == "hip" else _torch_search(tb, H, order, ok))
             torch.cuda.synchronize()
             ts = []
             for _ in range(a.iters):
                 t0 = time.perf_counter()
-                r = (TreeBuilder._search_hip(tb, H, order, ok) if name == "hip" else _torch_search(tb, H, order, ok))
+                r = (TreeBuilder._search(tb, H, order, ok) if name == "hip" else _torch_search(tb, H, order, ok))
                 torch.cuda.synchronize()
                 ts.append(time.perf_counter() - t0)
             outs[name] = r
