@@ -317,14 +317,14 @@ class BatchOperator(AlgoOperator):
         return self
 
     def lazyPrintStatistics(self, title=None):
-        from .batch.statistics import SummarizerBatchOp
+        from .batch.feature import SummarizerBatchOp
         s = SummarizerBatchOp().setMLEnvironmentId(self.getMLEnvironmentId())
         self.link(s)
         s.lazyPrintSummary(title)
         return self
 
     def collectStatistics(self):
-        from .batch.statistics import SummarizerBatchOp
+        from .batch.feature import SummarizerBatchOp
         s = SummarizerBatchOp().setMLEnvironmentId(self.getMLEnvironmentId())
         self.link(s)
         return s.collectSummary()

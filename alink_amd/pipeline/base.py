@@ -83,7 +83,31 @@ class PipelineStageBase(WithParams):
         register_stage(cls)
 
 
-class TransformerBase(PipelineStageBase):
+def _lazy_get(stage, name, default=None):
+    p = stage.getParams()
+    return p.get(name) if p.contains(name) else default
+
+
+class _LazyPrintTransformInfo:
+    """``HasLazyPrintTransformInfo`` (reference ``common/lazy/HasLazyPrintTransformInfo.java``): the enabled
+    flags live in the stage's params, so a model built from a Trainer's params inherits them, and a later
+    ``enable*`` on the model overrides what it inherited."""
+
+    def enableLazyPrintTransformData(self, n: int = -1, title: Optional[str] = None):
+        p = self.getParams()
+        p.set("lazyPrintTransformDataEnabled", True)
+        p.set("lazyPrintTransformDataNum", int(n))
+        p.set("lazyPrintTransformDataTitle", title)
+        return self
+
+    def enableLazyPrintTransformStat(self, title: Optional[str] = None):
+        p = self.getParams()
+        p.set("lazyPrintTransformStatEnabled", True)
+        p.set("lazyPrintTransformStatTitle", title)
+        return self
+
+
+class TransformerBase(_LazyPrintTransformInfo, PipelineStageBase):
     def transform(self, input):
         from ..operator.stream.base import StreamOperator
         if isinstance(input, StreamOperator):
@@ -92,8 +116,17 @@ class TransformerBase(PipelineStageBase):
             from ..operator.batch.source import TableSourceBatchOp
             input = TableSourceBatchOp(input)
         out = self.transformBatch(input)
-        lazy = self.env.lazy.genLazyTransformResult(self)
-        lazy.addValue(out)
+        return self._post_process_transform(out)
+
+    def _post_process_transform(self, out):
+        """Reference ``TransformerBase.postProcessTransformResult``: record the result, then register the enabled
+        lazy prints on it (they fire at the next execution)."""
+        self.env.lazy.genLazyTransformResult(self).addValue(out)
+        if _lazy_get(self, "lazyPrintTransformDataEnabled", False):
+            out.lazyPrint(_lazy_get(self, "lazyPrintTransformDataNum", -1),
+                          _lazy_get(self, "lazyPrintTransformDataTitle"))
+        if _lazy_get(self, "lazyPrintTransformStatEnabled", False):
+            out.lazyPrintStatistics(_lazy_get(self, "lazyPrintTransformStatTitle"))
         return out
 
     def transformBatch(self, input: BatchOperator) -> BatchOperator:
@@ -101,15 +134,6 @@ class TransformerBase(PipelineStageBase):
 
     def transformStream(self, input):
         raise NotImplementedError(f"{type(self).__name__} does not support stream transform")
-
-    # lazy observation of transform results (HasLazyPrintTransformInfo)
-    def enableLazyPrintTransformData(self, n: int = -1, title: Optional[str] = None):
-        self.env.lazy.genLazyTransformResult(self).addCallback(lambda op: op.lazyPrint(n, title))
-        return self
-
-    def enableLazyPrintTransformStat(self, title: Optional[str] = None):
-        self.env.lazy.genLazyTransformResult(self).addCallback(lambda op: op.lazyPrintStatistics(title))
-        return self
 
 
 class ModelBase(TransformerBase):
@@ -149,7 +173,7 @@ class EstimatorBase(PipelineStageBase):
         raise NotImplementedError("Only support batch fit!")
 
 
-class Trainer(EstimatorBase):
+class Trainer(_LazyPrintTransformInfo, EstimatorBase):
     """``fit = createModel(train(in).getOutputTable())`` (reference ``Trainer.java:33-111``)."""
     TRAIN_OP = None
     MODEL = None
@@ -164,25 +188,27 @@ class Trainer(EstimatorBase):
     def fitBatch(self, input):
         op = self.train(input)
         lm = self.env.lazy
+        # postProcessTrainOp: record the train op and register the enabled train / model info prints on it
         lm.genLazyTrainOp(self).addValue(op)
+        if _lazy_get(self, "lazyPrintTrainInfoEnabled", False) and hasattr(op, "lazyPrintTrainInfo"):
+            op.lazyPrintTrainInfo(_lazy_get(self, "lazyPrintTrainInfoTitle"))
+        if _lazy_get(self, "lazyPrintModelInfoEnabled", False) and hasattr(op, "lazyPrintModelInfo"):
+            op.lazyPrintModelInfo(_lazy_get(self, "lazyPrintModelInfoTitle"))
+        # postProcessModel: the model is built from this trainer's params, so it inherits the transform flags
         model = self.createModel(op.getOutputTable())
         lm.genLazyModel(self).addValue(model)
         self._train_op = op
         return model
 
-    # lazy info hooks (WithTrainInfo / WithModelInfoBatchOp)
+    # HasLazyPrintTrainInfo / HasLazyPrintModelInfo: flags in params, applied to the train op of each fit
     def enableLazyPrintTrainInfo(self, title: Optional[str] = None):
-        def cb(op):
-            if hasattr(op, "lazyPrintTrainInfo"):
-                op.lazyPrintTrainInfo(title)
-        self.env.lazy.genLazyTrainOp(self).addCallback(cb)
+        self.getParams().set("lazyPrintTrainInfoEnabled", True)
+        self.getParams().set("lazyPrintTrainInfoTitle", title)
         return self
 
     def enableLazyPrintModelInfo(self, title: Optional[str] = None):
-        def cb(op):
-            if hasattr(op, "lazyPrintModelInfo"):
-                op.lazyPrintModelInfo(title)
-        self.env.lazy.genLazyTrainOp(self).addCallback(cb)
+        self.getParams().set("lazyPrintModelInfoEnabled", True)
+        self.getParams().set("lazyPrintModelInfoTitle", title)
         return self
 
 
