@@ -114,3 +114,91 @@ def test_non_default_environment(capsys):
         MLEnvironmentFactory.remove(env_id)
     out = capsys.readouterr().out
     assert "===== MODEL INFO =====" in out and "===== TRAINER TRANSFORM STAT =====" in out
+
+
+# ---- BatchOperator lazy sinks (reference BatchOperatorLazyTest.java) ----
+ROWS = [(1, 1, 0.6), (2, 2, 0.8), (2, 3, 0.6), (4, 1, 0.6), (4, 2, 0.3), (4, 3, 0.4)]
+
+
+def _mem(cols, env_id=None):
+    from alink_amd import MemSourceBatchOp
+    op = MemSourceBatchOp(ROWS, cols)
+    return op if env_id is None else op.setMLEnvironmentId(env_id)
+
+
+def _header(cols):
+    return "|".join(cols)
+
+
+def test_lazy_print_fires_in_execute(capsys):
+    _mem(["u", "i", "r"]).lazyPrint(-1, "This is table 1")
+    _mem(["uu", "ii", "rr"]).lazyPrint(-1, "This is table 2")
+    BatchOperator.execute()
+    out = capsys.readouterr().out
+    assert "This is table 1" in out and "This is table 2" in out
+
+
+def test_lazy_print_fires_in_collect_and_print(capsys):
+    a, b = _mem(["u", "i", "r"]), _mem(["uu", "ii", "rr"])
+    a.lazyPrint(-1)
+    b.lazyPrint(-1)
+    assert len(_mem(["uuu", "iii", "rrr"]).collect()) == len(ROWS)
+    out = capsys.readouterr().out.replace(" ", "")
+    assert _header(a.getColNames()) in out and _header(b.getColNames()) in out
+    a.lazyPrint(-1)
+    _mem(["uuu", "iii", "rrr"]).print()
+    out = capsys.readouterr().out.replace(" ", "")
+    assert _header(a.getColNames()) in out and _header(["uuu", "iii", "rrr"]) in out
+
+
+def test_lazy_collect_callbacks_in_print(capsys):
+    got = []
+    _mem(["u", "i", "r"]).lazyCollect(lambda d: got.append(("cb1", len(d))), lambda d: got.append(("cb2", len(d))))
+    _mem(["uu", "ii", "rr"]).lazyPrint(-1)
+    _mem(["uuu", "iii", "rrr"]).print()
+    assert got == [("cb1", len(ROWS)), ("cb2", len(ROWS))]
+    assert _header(["uu", "ii", "rr"]) in capsys.readouterr().out.replace(" ", "")
+
+
+def test_exception_in_lazy_collect_propagates():
+    def boom(_):
+        raise AssertionError("callback failed")
+    _mem(["u", "i", "r"]).lazyCollect(lambda d: None, boom)
+    with pytest.raises(AssertionError):
+        BatchOperator.execute()
+
+
+def test_lazy_statistics(capsys):
+    _mem(["u", "i", "r"]).lazyPrintStatistics("==== TITLE ====")
+    BatchOperator.execute()
+    out = capsys.readouterr().out
+    for word in ("==== TITLE ====", "numMissingValue", "count", "normL1", "normL2"):
+        assert word in out, word
+
+
+def test_sinks_fire_once(capsys):
+    from alink_amd import FirstNBatchOp
+    a = _mem(["label", "u", "i"])
+    a.lazyPrint(-1, "This is table 1")
+    BatchOperator.execute()
+    assert "This is table 1" in capsys.readouterr().out
+    _mem(["label", "u", "i"]).print()
+    assert "This is table 1" not in capsys.readouterr().out
+    b = _mem(["label", "u", "i"])
+    b.lazyPrint(-1, "This is table 2")
+    FirstNBatchOp().setSize(10).linkFrom(b).print()
+    assert "This is table 2" in capsys.readouterr().out
+    FirstNBatchOp().setSize(10).linkFrom(b).print()
+    assert "This is table 2" not in capsys.readouterr().out
+
+
+def test_lazy_print_in_non_default_env(capsys):
+    env_id = MLEnvironmentFactory.getNewMLEnvironmentId()
+    try:
+        _mem(["u", "i", "r"], env_id).lazyPrint(-1, "This is table 1")
+        _mem(["uu", "ii", "rr"], env_id).lazyPrint(-1, "This is table 2")
+        BatchOperator.execute(MLEnvironmentFactory.get(env_id))
+    finally:
+        MLEnvironmentFactory.remove(env_id)
+    out = capsys.readouterr().out
+    assert "This is table 1" in out and "This is table 2" in out
