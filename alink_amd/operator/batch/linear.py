@@ -10,6 +10,7 @@ from ...common.table import MTable
 from ...models.linear.model import AFTModelMapper, LinearModelDataConverter, LinearModelMapper, SoftmaxModelMapper
 from ...models.linear.train import train_aft, train_linear, train_softmax
 from ..base import BatchOperator, format_rows
+from .modelinfo import WithTrainInfo
 from .utils import ModelMapBatchOp
 
 __all__ = ["BaseLinearModelTrainBatchOp", "LogisticRegressionTrainBatchOp", "LogisticRegressionPredictBatchOp",
@@ -19,27 +20,56 @@ __all__ = ["BaseLinearModelTrainBatchOp", "LogisticRegressionTrainBatchOp", "Log
            "AftSurvivalRegPredictBatchOp"]
 
 
-class _WithTrainInfo:
+class LinearTrainInfo:
+    """Convergence summary of a linear train op: iterations and loss curve."""
+
+    def __init__(self, info: dict):
+        info = info or {}
+        self.numIter = info.get("numIter")
+        curve = info.get("lossCurve")
+        self.lossCurve = [] if curve is None else [float(v) for v in curve]
+
+    def __str__(self):
+        return f"numIter: {self.numIter}, final loss: {self.lossCurve[-1] if self.lossCurve else None}"
+
+
+class LinearModelSummary:
+    """Model summary of a linear train op: model name, intercept flag and coefficients."""
+
+    def __init__(self, model):
+        self.modelName = model.modelName
+        self.hasInterceptItem = model.hasInterceptItem
+        self.coefVector = model.coefVector
+
+    def __str__(self):
+        return f"model: {self.modelName}, intercept: {self.hasInterceptItem}, coef: {self.coefVector}"
+
+
+class _WithTrainInfo(WithTrainInfo):
     _train_info: dict = None
 
     def getTrainInfo(self):
         return self._train_info
 
-    def lazyPrintTrainInfo(self, title=None):
-        info = self._train_info or {}
-        if title:
-            print(title)
-        curve = info.get("lossCurve")
-        print(f"numIter: {info.get('numIter')}, final loss: {curve[-1] if curve is not None and len(curve) else None}")
+    def createTrainInfo(self):
+        return LinearTrainInfo(self._train_info)
+
+    # model summary, lazy like the train info (the reference's WithModelInfoBatchOp protocol)
+    def collectModelInfo(self):
+        return LinearModelSummary(self._model)
+
+    def lazyCollectModelInfo(self, *callbacks):
+        cbs = list(callbacks[0]) if len(callbacks) == 1 and isinstance(callbacks[0], (list, tuple)) else callbacks
+        self.lazyCollect(lambda _rows: [cb(self.collectModelInfo()) for cb in cbs])
         return self
 
     def lazyPrintModelInfo(self, title=None):
-        if title:
-            print(title)
-        m = getattr(self, "_model", None)
-        if m is not None:
-            print(f"model: {m.modelName}, intercept: {m.hasInterceptItem}, coef: {m.coefVector}")
-        return self
+        def show(info):
+            if self.env.rank == 0:
+                if title is not None:
+                    print(title)
+                print(info)
+        return self.lazyCollectModelInfo(show)
 
 
 class BaseLinearModelTrainBatchOp(BatchOperator, _WithTrainInfo):

@@ -15,7 +15,7 @@ import numpy as np
 
 from ..base import BatchOperator
 
-__all__ = ["ExtractModelInfoBatchOp", "WithModelInfoBatchOp", "FmModelInfo", "FmModelInfoBatchOp"]
+__all__ = ["ExtractModelInfoBatchOp", "WithModelInfoBatchOp", "WithTrainInfo", "FmModelInfo", "FmModelInfoBatchOp"]
 
 
 class ExtractModelInfoBatchOp(BatchOperator):
@@ -73,6 +73,36 @@ class WithModelInfoBatchOp:
 
     def collectModelInfo(self):
         return self._info_op().collectModelInfo()
+
+
+class WithTrainInfo:
+    """Train-information mixin for train ops (reference ``A/common/lazy/WithTrainInfo.java``): ``createTrainInfo``
+    builds the summary object; ``collectTrainInfo`` returns it now, ``lazyCollectTrainInfo`` / ``lazyPrintTrainInfo``
+    hand it to callbacks at the next execution (``execute`` / ``collect`` / ``print``), on rank 0 for prints."""
+
+    def createTrainInfo(self):
+        raise NotImplementedError
+
+    def collectTrainInfo(self):
+        return self.createTrainInfo()
+
+    def lazyCollectTrainInfo(self, *callbacks: Callable[[Any], None]):
+        cbs = list(callbacks[0]) if len(callbacks) == 1 and isinstance(callbacks[0], (list, tuple)) else callbacks
+
+        def fire(_rows):
+            info = self.createTrainInfo()
+            for cb in cbs:
+                cb(info)
+        self.lazyCollect(fire)
+        return self
+
+    def lazyPrintTrainInfo(self, title=None):
+        def show(info):
+            if self.env.rank == 0:
+                if title is not None:
+                    print(title)
+                print(info)
+        return self.lazyCollectTrainInfo(show)
 
 
 def _fmt8(x: float) -> str:

@@ -11,6 +11,7 @@ from ...common.table import MTable
 from ...models.tree.model import GbdtModelMapper, RandomForestModelMapper
 from ...models.tree.train import IMPORTANCE_SCHEMA, train_forest, train_gbdt
 from ..base import BatchOperator
+from .modelinfo import WithTrainInfo
 from .utils import ModelMapBatchOp
 
 __all__ = ["GbdtTrainBatchOp", "GbdtRegTrainBatchOp", "GbdtPredictBatchOp", "GbdtRegPredictBatchOp",
@@ -19,17 +20,14 @@ __all__ = ["GbdtTrainBatchOp", "GbdtRegTrainBatchOp", "GbdtPredictBatchOp", "Gbd
            "DecisionTreePredictBatchOp", "DecisionTreeRegPredictBatchOp"]
 
 
-class _TreeTrainInfo:
+class _TreeTrainInfo(WithTrainInfo):
     _train_info: dict = None
 
     def getTrainInfo(self):
         return self._train_info
 
-    def lazyPrintTrainInfo(self, title=None):
-        if title:
-            print(title)
-        print(self._train_info)
-        return self
+    def createTrainInfo(self):
+        return self._train_info
 
 
 class BaseGbdtTrainBatchOp(BatchOperator, _TreeTrainInfo):

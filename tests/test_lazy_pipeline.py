@@ -202,3 +202,55 @@ def test_lazy_print_in_non_default_env(capsys):
         MLEnvironmentFactory.remove(env_id)
     out = capsys.readouterr().out
     assert "This is table 1" in out and "This is table 2" in out
+
+
+# ---- train / model info (reference TrainModelInfoTest.java) and LazyEvaluation (LazyEvaluationTest.java) ----
+def _lr_op(env_id=None):
+    from alink_amd import LogisticRegressionTrainBatchOp
+    op = LogisticRegressionTrainBatchOp().setFeatureCols(["u", "i", "r"]).setLabelCol("label").setMaxIter(5)
+    if env_id is not None:
+        op.setMLEnvironmentId(env_id)
+    return op.linkFrom(_src(env_id=env_id))
+
+
+def test_train_and_model_info_collect():
+    op = _lr_op()
+    assert str(op.collectTrainInfo()).startswith("numIter: ")
+    assert str(op.collectModelInfo()).startswith("model: Logistic Regression, intercept: True, coef: ")
+
+
+def test_lazy_train_and_model_info_fire_on_execute(capsys):
+    env_id = MLEnvironmentFactory.getNewMLEnvironmentId()
+    try:
+        op = _lr_op(env_id)
+        got = []
+        op.lazyCollectModelInfo(lambda d: got.append(("model", str(d))))
+        op.lazyCollectTrainInfo(lambda d: got.append(("train", d.numIter)))
+        op.lazyPrintTrainInfo("======= TRAIN INFO =======")
+        assert got == [] and "TRAIN INFO" not in capsys.readouterr().out      # nothing before the execution
+        BatchOperator.execute(MLEnvironmentFactory.get(env_id))
+    finally:
+        MLEnvironmentFactory.remove(env_id)
+    assert [k for k, _ in got] == ["model", "train"] and got[1][1] >= 1
+    out = capsys.readouterr().out
+    assert "======= TRAIN INFO =======" in out and "numIter: " in out
+
+
+def test_lazy_evaluation_values_and_callbacks():
+    from alink_amd.common.lazy import LazyEvaluation
+    seen = []
+    lz = LazyEvaluation()
+    lz.addCallback(lambda d: seen.append(d - 1))
+    for v in (100, 300, 400):
+        lz.addValue(v)
+    lz.addCallback(lambda d: seen.append(d + 1))
+    lz.addValue(200)
+    lz.addCallback(lambda d: seen.append(d + 2))
+    assert lz.getLatestValue() == 200
+    assert len(seen) == 12                        # 4 values x 3 callbacks
+    with pytest.raises(RuntimeError):
+        LazyEvaluation().getLatestValue()
+    bad = LazyEvaluation()
+    bad.addCallback(lambda d: (_ for _ in ()).throw(ValueError("callback failed")))
+    with pytest.raises(ValueError):
+        bad.addValue(1)
