@@ -456,7 +456,17 @@ class BaseComQueue:
         return out
 
     def __str__(self):
-        return "->".join(it.name() for it in self.optimize())
+        """The reference's ``BaseComQueue.toString`` JSON: complete-result and criterion class names, maxIter,
+        the session (ML environment) id and the optimized queue as class names (fused runs of compute
+        functions show as ``ChainedComputation``)."""
+        import json
+
+        def cls(o):
+            return None if o is None else type(o).__name__
+        env_id = getattr(self.env, "env_id", 0) if self.env is not None else 0
+        return json.dumps({"completeResult": cls(self.complete), "maxIter": self.max_iter, "sessionId": env_id,
+                           "queue": ",".join(cls(it) for it in self.optimize()),
+                           "compareCriterion": cls(self.criterion)}, separators=(",", ":"))
 
     # ---- execution ----
     def exec(self) -> List:
