@@ -9,7 +9,7 @@ from .common.mlenv import (MLEnvironment, MLEnvironmentFactory, useLocalEnv, use
                            getMLEnv)
 from .common.params import Params, ParamInfo  # noqa: F401
 from .parallel.launch import launch, launch_script  # noqa: F401
-from .common.linalg import DenseVector, SparseVector, VectorUtil, DenseMatrix  # noqa: F401
+from .common.linalg import DenseVector, SparseVector, VectorUtil, DenseMatrix, BLAS, MatVecOp, NormalEquation  # noqa: F401,E501
 from .common.table import MTable, Row  # noqa: F401
 from .common.types import TableSchema, Types  # noqa: F401
 from .operator.common.io.db import BaseDB, SqliteDB, DerbyDB, MySqlDB, JdbcDB  # noqa: F401

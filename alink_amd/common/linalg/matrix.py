@@ -23,9 +23,13 @@ class DenseMatrix:
             self.a = a.copy()
         elif len(args) == 2:
             self.a = np.zeros((int(args[0]), int(args[1])), dtype=np.float64)
-        elif len(args) == 3:  # (m, n, column-major data)
-            m, n, data = args
-            self.a = np.asarray(data, dtype=np.float64).reshape(n, m).T.copy()
+        elif len(args) in (3, 4):  # (m, n, data[, inRowMajor]) — column-major unless inRowMajor
+            m, n, data = int(args[0]), int(args[1]), args[2]
+            arr = np.asarray(data, dtype=np.float64).reshape(-1)
+            if arr.size != m * n:
+                raise ValueError("Size not match.")
+            row_major = bool(args[3]) if len(args) == 4 else False
+            self.a = arr.reshape(m, n).copy() if row_major else arr.reshape(n, m).T.copy()
         else:
             self.a = np.zeros((0, 0))
 
@@ -43,16 +47,25 @@ class DenseMatrix:
         return self.a.T.reshape(-1)
 
     @staticmethod
-    def eye(n):
-        return DenseMatrix(np.eye(n))
+    def eye(m, n=None):
+        return DenseMatrix(np.eye(m, m if n is None else n))
 
     @staticmethod
     def zeros(m, n):
         return DenseMatrix(m, n)
 
     @staticmethod
+    def ones(m, n):
+        return DenseMatrix(np.ones((m, n)))
+
+    @staticmethod
     def rand(m, n, seed=None):
         return DenseMatrix(np.random.default_rng(seed).random((m, n)))
+
+    @staticmethod
+    def randSymmetric(n, seed=None):
+        r = np.random.default_rng(seed).random((n, n))
+        return DenseMatrix(np.triu(r) + np.triu(r, 1).T)
 
     def numRows(self):
         return self.a.shape[0]
@@ -72,6 +85,22 @@ class DenseMatrix:
     def getArrayCopy2D(self):
         return self.a.copy()
 
+    def getArrayCopy1D(self, inRowMajor: bool):
+        return (self.a if inRowMajor else self.a.T).reshape(-1).copy()
+
+    def selectRows(self, rows):
+        return DenseMatrix(self.a[np.asarray(rows, dtype=np.int64)])
+
+    def getSubMatrix(self, m0, m1, n0, n1):
+        """Rows [m0, m1), columns [n0, n1)."""
+        return DenseMatrix(self.a[m0:m1, n0:n1])
+
+    def setSubMatrix(self, sub, m0, m1, n0, n1):
+        self.a[m0:m1, n0:n1] = sub.a if isinstance(sub, DenseMatrix) else np.asarray(sub)
+
+    def sum(self):
+        return float(self.a.sum())
+
     def getData(self):
         return self.data
 
@@ -85,17 +114,26 @@ class DenseMatrix:
         return DenseMatrix(self.a.T)
 
     def multiplies(self, o):
+        from .vector import SparseVector
         if isinstance(o, DenseMatrix):
             return DenseMatrix(self.a @ o.a)
         if isinstance(o, DenseVector):
             return DenseVector(self.a @ o.data)
+        if isinstance(o, SparseVector):
+            return DenseVector(self.a[:, o.indices.astype(np.int64)] @ o.values)
         return DenseMatrix(self.a @ np.asarray(o))
 
     def plus(self, o):
         return DenseMatrix(self.a + (o.a if isinstance(o, DenseMatrix) else o))
 
+    def plusEquals(self, o):
+        self.a += o.a if isinstance(o, DenseMatrix) else o
+
     def minus(self, o):
         return DenseMatrix(self.a - o.a)
+
+    def minusEquals(self, o):
+        self.a -= o.a
 
     def scale(self, v):
         return DenseMatrix(self.a * v)
@@ -128,6 +166,11 @@ class DenseMatrix:
     def norm2(self):
         return float(np.linalg.norm(self.a, 2))
 
+    def cond(self):
+        """Two-norm condition number (largest / smallest singular value)."""
+        sv = np.linalg.svd(self.a, compute_uv=False)
+        return float(sv[0] / sv[min(self.a.shape) - 1])
+
     def normF(self):
         return float(np.linalg.norm(self.a))
 
@@ -142,6 +185,15 @@ class DenseMatrix:
 
     def __eq__(self, o):
         return isinstance(o, DenseMatrix) and np.array_equal(o.a, self.a)
+
+    def toString(self):
+        """``mat[m,n]:`` then one line per row, values as Java ``Double.toString`` (reference ``toString``)."""
+        from ..javafmt import java_double_str
+        lines = [f"mat[{self.m},{self.n}]:"]
+        lines += ["  " + ",".join(java_double_str(float(v)) for v in row) for row in self.a]
+        return "\n".join(lines) + "\n"
+
+    __str__ = toString
 
     def __repr__(self):
         return f"DenseMatrix({self.a.tolist()})"

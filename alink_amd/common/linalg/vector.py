@@ -300,6 +300,14 @@ class SparseVector(Vector):
                 out_v.append(v)
         return SparseVector(len(indices), out_i, out_v)
 
+    def outer(self, o: Optional["SparseVector"] = None):
+        """Outer product self * o^T as a DenseMatrix (size x o.size)."""
+        from .matrix import DenseMatrix
+        o = self if o is None else o
+        m = np.zeros((self.size(), o.size()))
+        m[np.ix_(self.indices.astype(np.int64), o.indices.astype(np.int64))] = np.outer(self.values, o.values)
+        return DenseMatrix(m)
+
     def removeZeroValues(self):
         m = self.values != 0
         self.indices, self.values = self.indices[m], self.values[m]
