@@ -83,7 +83,7 @@ def main():
     ap.add_argument("--fields", type=int, default=20)
     ap.add_argument("--per-field", type=int, default=100_000)
     ap.add_argument("--mode", default="SHARDED", help="SHARDED | DATA_PARALLEL | HOGWILD | SEQUENTIAL")
-    ap.add_argument("--interval", type=float, default=1.0, help="FTRL snapshot interval (s)")
+    ap.add_argument("--interval", type=int, default=1, help="FTRL snapshot interval (integer seconds, as the reference)")
     ap.add_argument("--async-reduce", action="store_true")
     a = ap.parse_args()
     os.environ["ALINK_STREAM_BATCH"] = str(a.batch)
