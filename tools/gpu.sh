@@ -36,7 +36,9 @@ case "$step" in
   prof)
     name=$1; secs=$2; shift 2
     cd /tmp && timeout -k 10 "$secs" rocprofv3 --kernel-trace --stats -d "$O/prof_$name" -o "$name" -- "$@" \
-      > "$O/prof_$name.log" 2>&1 && echo "PROF_OK $name" || { tail -30 "$O/prof_$name.log"; exit 1; } ;;
+      > "$O/prof_$name.log" 2>&1 && echo "PROF_OK $name" || { tail -30 "$O/prof_$name.log"; exit 1; }
+    # gpurun copies back at most 64 MiB: keep the stats, compress the per-dispatch traces
+    find "$O/prof_$name" -name '*.csv' -size +1M -exec gzip -9 {} \; ;;
   pmc)
     name=$1; ctrs=$2; secs=$3; shift 3
     cd /tmp && timeout -s KILL "$secs" rocprofv3 --pmc $ctrs --output-format csv -d "$O/pmc_$name" -o "$name" -- "$@" \
