@@ -131,12 +131,11 @@ class StringBlock:
         dev = self.device
         n = len(self)
         if isinstance(idx, slice) and idx.step in (None, 1):
-            # contiguous rows (stream micro-batches, MTable.slice): one byte-range view, offsets rebased
+            # contiguous rows (MTable.slice): one byte-range view, offsets rebased
             a, b, _ = idx.indices(n)
             b = max(a, b)
-            bounds = self.offsets[[a, b]].tolist()
-            return StringBlock(self.data[bounds[0]:bounds[1]], self.offsets[a:b + 1] - bounds[0],
-                               None if self.nulls is None else self.nulls[a:b])
+            ba, bb = self.offsets[[a, b]].tolist()
+            return self.row_range(a, b, ba, bb)
         if isinstance(idx, slice):
             idx = torch.arange(n, device=dev)[idx]
         elif isinstance(idx, torch.Tensor):
@@ -165,6 +164,12 @@ class StringBlock:
             data = torch.zeros(0, dtype=torch.uint8, device=dev)
         nulls = None if self.nulls is None else self.nulls[idx]
         return StringBlock(data, off, nulls)
+
+    def row_range(self, a: int, b: int, byte_a: int, byte_b: int) -> "StringBlock":
+        """Rows [a, b) given their byte range [byte_a, byte_b) = offsets[a], offsets[b] (known to the caller, e.g.
+        the micro-batch boundaries of a stream source read in one copy): a view, no device synchronisation."""
+        return StringBlock(self.data[byte_a:byte_b], self.offsets[a:b + 1] - byte_a,
+                           None if self.nulls is None else self.nulls[a:b])
 
     @staticmethod
     def concat(blocks: Sequence["StringBlock"]) -> "StringBlock":

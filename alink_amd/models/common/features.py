@@ -106,6 +106,9 @@ class FeatureMatrix:
             return self.dense @ v[: self._ncols]
         if self.val.numel() == 0:
             return torch.zeros(self.nrows, dtype=v.dtype, device=v.device)
+        if v.is_cuda and v.dtype == torch.float64 and self.val.dtype == torch.float64:
+            from ...ops.feature import csr_mv         # HIP: G lanes per row, fixed-order sum, no atomics
+            return csr_mv(self.crow, self.col, self.val, v)
         prod = self.val * v[self.col]
         out = torch.zeros(self.nrows, dtype=v.dtype, device=v.device)
         return out.index_add_(0, self.row_ids(), prod)

@@ -11,8 +11,11 @@ from __future__ import annotations
 import os
 from typing import Iterator, Optional
 
+import torch
+
 from ...common.params import Params
-from ...common.table import MTable
+from ...common.strings import StringBlock
+from ...common.table import Column, MTable
 from ..batch import source as B
 from .base import StreamSourceOp
 
@@ -46,8 +49,19 @@ class _TableReplaySource(StreamSourceOp):
         self._ensure_schema()
         mt = self._mt
         bs = max(1, _batch_rows())
-        for s in range(0, mt.num_rows, bs):
-            yield mt.slice(s, min(mt.num_rows, s + bs))
+        bounds = list(range(0, mt.num_rows, bs)) + [mt.num_rows]
+        # byte offsets of every micro-batch boundary of every string column, read once for the whole stream
+        # (slicing a device string block otherwise costs one device-to-host copy per column per micro-batch)
+        byte_bounds = {}
+        for ci, c in enumerate(mt.cols):
+            if isinstance(c.values, StringBlock):
+                off = c.values.offsets
+                byte_bounds[ci] = off[torch.as_tensor(bounds, device=off.device)].tolist()
+        for i in range(len(bounds) - 1):
+            a, b = bounds[i], bounds[i + 1]
+            cols = [Column(c.values.row_range(a, b, byte_bounds[ci][i], byte_bounds[ci][i + 1]))
+                    if ci in byte_bounds else c.take(slice(a, b)) for ci, c in enumerate(mt.cols)]
+            yield MTable(mt.schema, cols, mt.replicated)
 
 
 class TableSourceStreamOp(_TableReplaySource):

@@ -101,6 +101,7 @@ _EXTRA_SIGNATURES = {
     "alink_vector_assemble": [_c_i64, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_int, _c_vp],
     "alink_murmur3_index": [_c_vp, _c_vp, _c_i64, _c_vp, _c_int, ctypes.c_uint32, _c_i64, _c_vp, _c_vp, _c_vp],
     "alink_csr_assemble": [_c_i64, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp],
+    "alink_csr_mv_f64": [_c_vp, _c_vp, _c_int, _c_vp, _c_i64, _c_vp, _c_vp, _c_d, _c_vp],
     "alink_tree_quantize": [_c_vp, _c_vp, _c_vp, _c_vp, _c_int, _c_i64, _c_int, _c_vp, _c_vp, _c_int, _c_int, _c_vp,
                             _c_vp],
     "alink_tree_split": [_c_vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_vp, _c_d, _c_d, _c_d, _c_d, _c_vp,

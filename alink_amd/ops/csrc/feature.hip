@@ -241,6 +241,28 @@ __global__ __launch_bounds__(256) void csr_write_kernel(int64_t n, int m, const 
     }
 }
 
+// CSR matrix-vector product out[r] = sum_k val[k] * v[col[k]] over row r's entries (FeatureMatrix.mv: linear /
+// FTRL margins).  G lanes per row (G a power of two <= 64 picked from the mean row length), each lane a strided
+// run of the row's entries, then a fixed-order xor-shuffle tree within the group: deterministic, no atomics
+// (torch's index_add_ of the per-entry products serialises on the rows' addresses).
+template <int G, typename I>
+__global__ __launch_bounds__(256) void csr_mv_kernel(const int64_t* __restrict__ crow, const I* __restrict__ col,
+                                                    const double* __restrict__ val, int64_t nrows,
+                                                    const double* __restrict__ v, double* __restrict__ out) {
+    const int sub = threadIdx.x & (G - 1);
+    const int64_t g0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / G;
+    const int64_t ng = (int64_t)gridDim.x * blockDim.x / G;
+    // r is uniform across a group's G lanes, so a group enters and leaves the loop together (shuffle-safe)
+    for (int64_t r = g0; r < nrows; r += ng) {
+        const int64_t s = crow[r], e = crow[r + 1];
+        double acc = 0.0;
+        for (int64_t k = s + sub; k < e; k += G) acc = fma(val[k], v[(int64_t)col[k]], acc);
+#pragma unroll
+        for (int o = G >> 1; o > 0; o >>= 1) acc += __shfl_xor(acc, o, G);
+        if (sub == 0) out[r] = acc;
+    }
+}
+
 // VectorAssembler (K24, reference VectorAssemblerMapper.java:50-106): every output row is the concatenation of
 // its parts' entries, each shifted by the running position (dense parts contribute every value, zeros included;
 // sparse parts their stored entries), so the CSR row is sorted by construction.  One thread per (part, row):
@@ -423,6 +445,29 @@ int alink_vector_assemble(int64_t n, int P, const int64_t* desc, const int64_t* 
 
 // CSR rows from m <= 64 column-major entry arrays idx/val/valid [m][n] (val nullable -> 1.0, valid nullable ->
 // all valid): pass 1 (out == nullptr) writes cnt[n]; pass 2 writes col/out at crow (cumsum of cnt).
+// out[nrows] = CSR(crow, col, val) @ v; col int32 (idx64 = 0) or int64 (idx64 = 1); mean_nnz picks lanes per row
+int alink_csr_mv_f64(const int64_t* crow, const void* col, int idx64, const double* val, int64_t nrows,
+                     const double* v, double* out, double mean_nnz, void* stream) {
+    if (nrows <= 0) return 0;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const int G = mean_nnz > 48 ? 64 : mean_nnz > 24 ? 32 : mean_nnz > 12 ? 16 : mean_nnz > 6 ? 8 : 4;
+    const int64_t groups = nrows;
+    int64_t blocks = (groups * G + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+#define ALINK_CSR_MV(GG)                                                                                          \
+    if (G == GG) {                                                                                                \
+        if (idx64)                                                                                                \
+            hipLaunchKernelGGL((csr_mv_kernel<GG, int64_t>), dim3(blocks), dim3(256), 0, st, crow,                \
+                               reinterpret_cast<const int64_t*>(col), val, nrows, v, out);                        \
+        else                                                                                                      \
+            hipLaunchKernelGGL((csr_mv_kernel<GG, int32_t>), dim3(blocks), dim3(256), 0, st, crow,                \
+                               reinterpret_cast<const int32_t*>(col), val, nrows, v, out);                        \
+    }
+    ALINK_CSR_MV(4) ALINK_CSR_MV(8) ALINK_CSR_MV(16) ALINK_CSR_MV(32) ALINK_CSR_MV(64)
+#undef ALINK_CSR_MV
+    return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
 int alink_csr_assemble(int64_t n, int m, const int32_t* idx, const double* val, const uint8_t* valid, int64_t* cnt,
                        const int64_t* crow, int32_t* col, double* out, void* stream) {
     if (n <= 0) return 0;

@@ -4,6 +4,8 @@
   nf)`` (Guava-exact, reference ``FeatureHasherMapper.java:104-106``) for a list of strings or a packed UTF-8
   ``StringBlock``; on a GPU one lane per string decodes UTF-8 to UTF-16 code units and hashes them on the
   device, on the host the C++ twin does.
+* ``csr_mv(crow, col, val, v)``: CSR matrix-vector product (margins of linear / FTRL models), G lanes per row
+  with a fixed-order shuffle reduction — deterministic, no atomics.
 * ``csr_assemble(idx, val, valid, size)``: per-row CSR from ``m`` column-major entry arrays ``[m, n]`` — rows
   sorted by index, duplicate indices summed (the reference's ``TreeMap`` accumulation) — one wave per row on
   the GPU, vectorised torch on the host.  Returns a ``SparseBlock``.
@@ -20,7 +22,9 @@ import torch
 from ..common.linalg.block import SparseBlock
 from . import _lib
 
-__all__ = ["utf16_units", "murmur3_index", "csr_assemble", "vector_assemble"]
+__all__ = ["utf16_units", "murmur3_index", "csr_assemble", "vector_assemble", "csr_mv"]
+
+CSR_MV_CALLS = 0     # HIP SpMV launches (tests check the device path ran)
 
 
 def utf16_units(strings: Sequence[str]):
@@ -208,3 +212,25 @@ _KEEP = []
 def _keep(t):
     _KEEP.append(t)
     return t
+
+
+def csr_mv(crow: torch.Tensor, col: torch.Tensor, val: torch.Tensor, v: torch.Tensor) -> torch.Tensor:
+    """``out[r] = sum_k val[k] * v[col[k]]`` for the CSR rows (fp64) on the GPU (``alink_csr_mv_f64``)."""
+    global CSR_MV_CALLS
+    L = _lib.require()
+    dev = val.device
+    n = int(crow.numel()) - 1
+    out = torch.empty(n, dtype=torch.float64, device=dev)
+    if n <= 0:
+        return out
+    crow = crow.to(torch.int64).contiguous()
+    col = col.contiguous() if col.dtype in (torch.int32, torch.int64) else col.to(torch.int64).contiguous()
+    val = val.to(torch.float64).contiguous()
+    v = v.to(torch.float64).contiguous()
+    mean_nnz = float(col.numel()) / n
+    rc = L.alink_csr_mv_f64(crow.data_ptr(), col.data_ptr(), int(col.dtype == torch.int64), val.data_ptr(), n,
+                            v.data_ptr(), out.data_ptr(), mean_nnz, _lib.stream_ptr(dev))
+    if rc != 0:
+        raise RuntimeError(f"alink_csr_mv_f64 failed: {rc}")
+    CSR_MV_CALLS += 1
+    return out

@@ -105,3 +105,29 @@ def test_hashed_features_into_vector_assembler_and_lr_on_gpu():
     a = json.loads([r for r in out["cpu"] if r[0] == 1048576][0][1])["coefVector"]["data"]
     b = json.loads([r for r in out["cuda:0"] if r[0] == 1048576][0][1])["coefVector"]["data"]
     np.testing.assert_allclose(b, a, rtol=1e-6, atol=1e-8)
+
+
+@pytest.mark.parametrize("mean_len,idx_dtype", [(3, torch.int32), (21, torch.int64), (40, torch.int32),
+                                                (150, torch.int64)])
+def test_csr_mv_matches_fp64_reference(mean_len, idx_dtype):
+    """HIP CSR SpMV (FeatureMatrix.mv on the GPU) == the fp64 segment sum, rows of length 0..3x the mean."""
+    from alink_amd.models.common.features import FeatureMatrix
+    from alink_amd.ops import feature as F
+    g = torch.Generator().manual_seed(mean_len)
+    n, d = 5000, 100_000
+    lens = torch.randint(0, 3 * mean_len + 1, (n,), generator=g)
+    lens[::97] = 0
+    crow = torch.zeros(n + 1, dtype=torch.int64)
+    crow[1:] = torch.cumsum(lens, 0)
+    nnz = int(crow[-1])
+    col = torch.randint(0, d, (nnz,), generator=g).to(idx_dtype)
+    val = torch.randn(nnz, generator=g, dtype=torch.float64)
+    v = torch.randn(d, generator=g, dtype=torch.float64)
+    rows = torch.repeat_interleave(torch.arange(n), lens)
+    ref = torch.zeros(n, dtype=torch.float64).index_add_(0, rows, val * v[col.long()])
+    calls = F.CSR_MV_CALLS
+    fm = FeatureMatrix(crow=crow.cuda(), col=col.cuda(), val=val.cuda(), ncols=d)
+    got = fm.mv(v.cuda())
+    assert F.CSR_MV_CALLS == calls + 1
+    torch.testing.assert_close(got.cpu(), ref, rtol=1e-12, atol=1e-12)
+    assert torch.equal(fm.mv(v.cuda()), got)                 # deterministic
