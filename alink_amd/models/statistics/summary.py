@@ -286,6 +286,12 @@ class CorrelationResult:
         return _fmt_table(["colName"] + list(names), [[names[i]] + list(arr[i]) for i in range(arr.shape[0])])
 
 
+def _is_spearman(method) -> bool:
+    """The reference's enum spells it ``SPEAMAN`` (``HasMethod`` of CorrelationBatchOp); accept both spellings."""
+    m = str(getattr(method, "name", method)).upper()
+    return m in ("SPEAMAN", "SPEARMAN")
+
+
 def _rank_global(v: torch.Tensor) -> torch.Tensor:
     """Average ranks (1-based, ties averaged) of the GLOBAL column, returned for this rank's rows."""
     parts = comm.all_gather_object(v.cpu().numpy())
@@ -294,6 +300,25 @@ def _rank_global(v: torch.Tensor) -> torch.Tensor:
     ranks = rankdata(full, method="average")
     off = int(sum(len(p) for p in parts[:comm.get_rank()]))
     return torch.as_tensor(ranks[off:off + v.shape[0]], dtype=torch.float64, device=v.device)
+
+
+def _pearson_pairwise(X: torch.Tensor, valid: torch.Tensor) -> np.ndarray:
+    """Pearson correlation over pairwise-complete rows (reference ``TableSummarizer.correlation``: every pair of
+    columns uses the rows where both are present).  Five d x d moment matrices from four GEMMs over the masked
+    values, all-reduced in one buffer: n_ij, sum x_i, sum x_i^2 (over the pair's rows), sum x_i x_j."""
+    M = valid.to(X.dtype)
+    A = torch.where(valid, X, torch.zeros_like(X))
+    d = X.shape[1]
+    mom = torch.stack([tn_matmul(M, M), tn_matmul(A, M), tn_matmul(A * A, M), tn_matmul(A, A)])
+    comm.all_reduce(mom, "sum")
+    N, Sx, Sxx, Sxy = mom[0], mom[1], mom[2], mom[3]
+    Sy, Syy = Sx.T, Sxx.T
+    num = N * Sxy - Sx * Sy
+    den = torch.sqrt(torch.clamp(N * Sxx - Sx * Sx, min=0.0) * torch.clamp(N * Syy - Sy * Sy, min=0.0))
+    corr = torch.where((den == 0) | (N < 2), torch.full_like(num, float("nan")), num / torch.where(den == 0,
+                                                                                             torch.ones_like(den), den))
+    corr.fill_diagonal_(1.0)
+    return corr.cpu().numpy() if d else np.zeros((0, 0))
 
 
 def _pearson(X: torch.Tensor) -> np.ndarray:
@@ -315,10 +340,28 @@ def _pearson(X: torch.Tensor) -> np.ndarray:
 
 def correlation(mt: MTable, cols: Sequence[str], method: str = "PEARSON", device=None) -> CorrelationResult:
     dev = device or torch.device("cpu")
-    X = extract_features(mt, list(cols), None, dev).dense.double()
-    if method.upper() == "SPEARMAN":
-        X = torch.stack([_rank_global(X[:, j]) for j in range(X.shape[1])], 1) if X.shape[1] else X
-    return CorrelationResult(_pearson(X), list(cols))
+    from ..tree.data import numeric_column
+    vals, nulls = zip(*[numeric_column(mt, c, dev) for c in cols]) if cols else ((), ())
+    nulls_any = comm.all_gather_object(bool(any(bool(m.any()) for m in nulls)))
+    if not any(nulls_any):
+        X = extract_features(mt, list(cols), None, dev).dense.double()
+        if _is_spearman(method):
+            X = torch.stack([_rank_global(X[:, j]) for j in range(X.shape[1])], 1) if X.shape[1] else X
+        return CorrelationResult(_pearson(X), list(cols))
+    # NULL / NaN cells: pairwise-complete statistics (Spearman ranks the present values of each column)
+    X = torch.stack(vals, 1)
+    valid = ~torch.stack(nulls, 1)
+    if _is_spearman(method):
+        X = torch.stack([_rank_present_global(X[:, j], valid[:, j]) for j in range(X.shape[1])], 1)
+    return CorrelationResult(_pearson_pairwise(X, valid), list(cols))
+
+
+def _rank_present_global(v: torch.Tensor, ok: torch.Tensor) -> torch.Tensor:
+    """Average ranks among the column's present values (global over ranks); absent cells get 0 (masked)."""
+    out = torch.zeros_like(v)
+    idx = torch.nonzero(ok).reshape(-1)
+    out[idx] = _rank_global(v[idx])
+    return out
 
 
 def vector_correlation(mt: MTable, vector_col: str, method: str = "PEARSON", device=None) -> CorrelationResult:
@@ -326,7 +369,7 @@ def vector_correlation(mt: MTable, vector_col: str, method: str = "PEARSON", dev
     fm = extract_features(mt, None, vector_col, dev)
     d = max(comm.all_gather_object(int(fm.ncols)))
     X = fm.to_dense(d).double()
-    if method.upper() == "SPEARMAN":
+    if _is_spearman(method):
         X = torch.stack([_rank_global(X[:, j]) for j in range(X.shape[1])], 1)
     return CorrelationResult(_pearson(X), None)
 

@@ -134,3 +134,27 @@ def test_binary_eval_on_columnar_detail_equals_string_detail():
         .linkFrom(TableSourceBatchOp(strs)).collectMetrics()
     for name in ("AUC", "LogLoss", "Accuracy", "PRC", "F1", "Precision"):
         assert getattr(a, "get" + name)() == getattr(b, "get" + name)(), name
+
+
+def test_binary_metrics_from_bins_reference_values():
+    """BinaryClassMetricsTest.saveAsParamsTest (reference operator/common/evaluation): positive bins at 0.7 / 0.8 /
+    0.9, negative bins at 0.6 / 0.75, log loss 2.987 over 5 samples -> the doc's metric values."""
+    from alink_amd.models.evaluation import metrics as M
+    pos = np.zeros(M.DETAIL_BIN_NUMBER)
+    neg = np.zeros(M.DETAIL_BIN_NUMBER)
+    pos[[70000, 80000, 90000]] = 1
+    neg[[60000, 75000]] = 1
+    m = M.binary_metrics(pos, neg, ["0", "1"], 2.987, 5)
+    expect = {"Prc": 0.9027777777777777, "MacroRecall": 0.5, "MacroSpecificity": 0.5, "Auc": 0.8333333333333333,
+              "MacroAccuracy": 0.6, "MicroFalseNegativeRate": 0.4, "WeightedRecall": 0.6, "WeightedPrecision": 0.36,
+              "MacroPrecision": 0.3, "MicroTruePositiveRate": 0.6, "MacroKappa": 0.0, "MicroSpecificity": 0.6,
+              "MacroF1": 0.375, "WeightedKappa": 0.0, "WeightedTruePositiveRate": 0.6, "TotalSamples": 5,
+              "MicroTrueNegativeRate": 0.6, "MicroSensitivity": 0.6, "WeightedAccuracy": 0.6,
+              "Ks": 0.6666666666666666, "Accuracy": 0.6, "WeightedFalseNegativeRate": 0.4, "MicroF1": 0.6,
+              "WeightedSpecificity": 0.4, "WeightedF1": 0.45, "MicroAccuracy": 0.6, "WeightedTrueNegativeRate": 0.4,
+              "Kappa": 0.0, "MacroSensitivity": 0.5, "WeightedSensitivity": 0.6, "MicroRecall": 0.6,
+              "MicroFalsePositiveRate": 0.4, "WeightedFalsePositiveRate": 0.6, "MicroPrecision": 0.6,
+              "MacroTrueNegativeRate": 0.5, "MicroKappa": 0.2}
+    for name, v in expect.items():
+        assert getattr(m, "get" + name)() == pytest.approx(v, abs=0.01), name
+    assert m.getLogLoss() == pytest.approx(2.987 / 5)

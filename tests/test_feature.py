@@ -105,3 +105,25 @@ def test_quantile_discretizer_and_summarizer():
     assert s.mean("x") == pytest.approx(df["x"].mean()) and s.standardDeviation("y") == pytest.approx(df["y"].std())
     c = CorrelationBatchOp().setSelectedCols(["x", "y"]).linkFrom(op).collectCorrelation().getCorrelation()
     assert c[0, 1] == pytest.approx(np.corrcoef(df["x"], df["y"])[0, 1])
+
+
+def test_correlation_pairwise_complete_and_spearman():
+    """TableSummarizerTest (reference operator/common/statistics/basicstatistic): with NULLs, every column pair
+    uses the rows where both are present (long/int vs double -> -1.0 on the two shared rows); the reference's
+    method enum spells Spearman ``SPEAMAN``."""
+    from alink_amd import CorrelationBatchOp, SummarizerBatchOp
+    from alink_amd.operator.batch.source import MemSourceBatchOp
+    rows = [(1, 1, 2.0), (2, 2, -3.0), (None, None, 2.0), (0, 0, None)]
+    src = MemSourceBatchOp(rows, "f_long long, f_int int, f_double double")
+    cols = ["f_long", "f_int", "f_double"]
+    c = CorrelationBatchOp().setSelectedCols(cols).linkFrom(src).collectCorrelation().getCorrelationMatrix()
+    np.testing.assert_allclose(c.getArrayCopy2D(), [[1, 1, -1], [1, 1, -1], [-1, -1, 1]], atol=1e-12)
+    s = SummarizerBatchOp().setSelectedCols(cols).linkFrom(src).collectSummary()
+    assert [s.sum(x) for x in cols] == [3.0, 3.0, 1.0]
+    assert [s.normL2(x) ** 2 for x in cols] == pytest.approx([5.0, 5.0, 17.0])
+    assert [s.min(x) for x in cols] == [0.0, 0.0, -3.0] and [s.max(x) for x in cols] == [2.0, 2.0, 2.0]
+    assert s.variance("f_double") == pytest.approx(8.333333333333334)
+    src2 = MemSourceBatchOp([(1.0, 3.0), (2.0, 1.0), (3.0, 2.0), (4.0, 10.0)], "a double, b double")
+    sp = CorrelationBatchOp().setSelectedCols(["a", "b"]).setMethod("SPEAMAN").linkFrom(src2) \
+        .collectCorrelation().getCorrelationMatrix()
+    assert sp.get(0, 1) == pytest.approx(0.4)                 # 1 - 6 * 6 / (4 * 15)
