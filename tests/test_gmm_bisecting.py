@@ -3,6 +3,7 @@ import json
 
 import numpy as np
 import pandas as pd
+import pytest
 
 from alink_amd import *  # noqa: F401,F403
 from alink_amd.models.clustering.gmm import pack_cov, unpack_cov
@@ -72,3 +73,35 @@ def test_bisecting_kmeans_k4():
     assert all(len(set(row)) == 1 for row in labels) and len({row[0] for row in labels}) == 4
     p = [float(x) for x in out[0][2].split(" ")]
     assert abs(sum(p) - 1.0) < 1e-12
+
+
+BISECT_ROWS = [
+    (0, '{"vectorCol":"\\"Y\\"","distanceType":"\\"EUCLIDEAN\\"","k":"3","vectorSize":"3"}'),
+    (1048576, '{"clusterId":1,"size":6,"center":{"data":[4.6,4.6,4.6]},"cost":364.61999999999995}'),
+    (2097152, '{"clusterId":2,"size":3,"center":{"data":[0.1,0.1,0.1]},"cost":0.06}'),
+    (3145728, '{"clusterId":3,"size":3,"center":{"data":[9.1,9.1,9.1]},"cost":0.06000000000005912}'),
+    (4194304, '{"clusterId":6,"size":1,"center":{"data":[9.0,9.0,9.0]},"cost":0.0}'),
+    (5242880, '{"clusterId":7,"size":2,"center":{"data":[9.149999999999999,9.149999999999999,9.149999999999999]},'
+              '"cost":0.015000000000100044}')]
+
+
+@pytest.mark.parametrize("detail", [False, True])
+def test_bisecting_model_mapper_reference_rows(detail):
+    """BisectingKMeansModelMapperTest (reference operator/common/clustering/kmeans): the tree of cluster ids
+    1 -> (2, 3), 3 -> (6, 7); "0 0 0" lands in leaf cluster 2 = prediction 0, detail "0.5 0.25 0.25"."""
+    from alink_amd.common.params import Params
+    from alink_amd.common.types import TableSchema, Types
+    from alink_amd.models.clustering import bisecting as B
+    conv = [c for n, c in vars(B).items() if n.endswith("ModelDataConverter") and isinstance(c, type)][0]
+    p = Params().set("predictionCol", "pred")
+    if detail:
+        p.set("predictionDetailCol", "detail")
+    m = B.BisectingKMeansModelMapper(conv().getModelSchema(), TableSchema(["Y"], [Types.STRING]), p)
+    m.loadModel(BISECT_ROWS)
+    out = m.map(("0 0 0",))
+    assert out[1] == 0
+    if detail:
+        assert out[2] == "0.5 0.25 0.25"
+        assert m.getOutputSchema() == TableSchema(["Y", "pred", "detail"], [Types.STRING, Types.LONG, Types.STRING])
+    else:
+        assert m.getOutputSchema() == TableSchema(["Y", "pred"], [Types.STRING, Types.LONG])

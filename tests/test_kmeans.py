@@ -135,3 +135,42 @@ def test_native_java_double_rows_equals_vector_tostring():
     a[0, :] = [0.0, -0.0, 1e-3, 9.999999e6, 1e7, -1e-4, 123456789.0]
     rows = _native.java_double_rows(a, " ")
     assert rows == [VectorUtil.toString(DenseVector(r)) for r in a]
+
+
+OLD_META = ('{"vectorCol":"\\"Y\\"","latitudeCol":null,"longitudeCol":null,"distanceType":"\\"EUCLIDEAN\\"",'
+            '"k":"2","modelSchema":"\\"model_id bigint,model_info string\\"","isNewFormat":"true",'
+            '"vectorSize":"3"}')
+HAV_META = ('{"vectorCol":null,"latitudeCol":"\\"f1\\"","longitudeCol":"\\"f0\\"","distanceType":"\\"HAVERSINE\\"",'
+            '"k":"2","modelSchema":"\\"model_id bigint,model_info string\\"","isNewFormat":"true",'
+            '"vectorSize":"2"}')
+
+
+@pytest.mark.parametrize("rows", [
+    # KMeansOldModelMapper1Test: OldClusterSummary with the center as a DenseVector JSON string
+    [(0, OLD_META), (1048576, '{"center":"{\\"data\\":[9.1,9.1,9.1]}","clusterId":0,"weight":3.0}'),
+     (2097152, '{"center":"{\\"data\\":[0.1,0.1,0.1]}","clusterId":1,"weight":3.0}')],
+    # KMeansOldModelMapper2Test: no modelSchema / isNewFormat in the meta, center as "[x, y, z]", vec null
+    [(0, '{"vectorCol":"\\"Y\\"","latitudeCol":null,"longitudeCol":null,"distanceType":"\\"EUCLIDEAN\\"",'
+         '"k":"2","vectorSize":"3"}'),
+     (1048576, '{"clusterId":0,"weight":3.0,"center":"[9.1, 9.1, 9.1]","vec":null}'),
+     (2097152, '{"clusterId":1,"weight":3.0,"center":"[0.1, 0.1, 0.1]","vec":null}')]])
+def test_kmeans_old_model_formats(rows):
+    from alink_amd.models.clustering.kmeans import KMeansModelMapper, KMeansModelDataConverter
+    from alink_amd.common.params import Params
+    m = KMeansModelMapper(KMeansModelDataConverter().getModelSchema(), TableSchema(["Y"], [Types.STRING]),
+                          Params().set("predictionCol", "pred"))
+    m.loadModel(rows)
+    assert m.map(("0 0 0",))[1] == 1
+    assert m.getOutputSchema() == TableSchema(["Y", "pred"], [Types.STRING, Types.LONG])
+
+
+def test_kmeans_old_model_haversine():
+    from alink_amd.models.clustering.kmeans import KMeansModelMapper, KMeansModelDataConverter
+    from alink_amd.common.params import Params
+    rows = [(0, HAV_META), (1048576, '{"center":"{\\"data\\":[8.33,9.0]}","clusterId":0,"weight":3.0}'),
+            (2097152, '{"center":"{\\"data\\":[1.0,1.33]}","clusterId":1,"weight":3.0}')]
+    m = KMeansModelMapper(KMeansModelDataConverter().getModelSchema(),
+                          TableSchema(["f0", "f1"], [Types.DOUBLE, Types.DOUBLE]), Params().set("predictionCol", "pred"))
+    m.loadModel(rows)
+    assert m.map((0.0, 0.0))[2] == 1
+    assert m.getOutputSchema() == TableSchema(["f0", "f1", "pred"], [Types.DOUBLE, Types.DOUBLE, Types.LONG])
