@@ -8,7 +8,7 @@ The batched path concatenates numeric / dense-block columns directly on the devi
 """
 from __future__ import annotations
 
-import itertools
+import math
 from typing import List
 
 import numpy as np
@@ -179,21 +179,65 @@ class VectorInteractionMapper(MISOMapper):
         return DenseVector(np.outer(b, a).reshape(-1))
 
 
+def poly_size(num_features: int, degree: int) -> int:
+    """Number of monomials of total degree <= ``degree`` in ``num_features`` variables, constant included
+    (reference ``PolynomialExpansionMapper.getPolySize``)."""
+    return math.comb(num_features + degree, degree)
+
+
+def _expand_dense(vals, last, degree, mult, out, cur):
+    # monomial order of the reference (Spark's): recursion over the last feature's power, lower features first
+    if mult == 0.0:
+        pass
+    elif degree == 0 or last < 0:
+        if cur >= 0:
+            out[cur] = mult
+    else:
+        v, alpha, start, i = vals[last], mult, cur, 0
+        while i <= degree and alpha != 0.0:
+            start = _expand_dense(vals, last - 1, degree - i, alpha, out, start)
+            i += 1
+            alpha *= v
+    return cur + poly_size(last + 1, degree)
+
+
+def _expand_sparse(idx, vals, last, last_feature, degree, mult, out_i, out_v, cur):
+    if mult == 0.0:
+        pass
+    elif degree == 0 or last < 0:
+        if cur >= 0:
+            out_i.append(cur)
+            out_v.append(mult)
+    else:
+        v, alpha, start, i = vals[last], mult, cur, 0
+        last_feature1 = int(idx[last]) - 1
+        while i <= degree and alpha != 0.0:
+            start = _expand_sparse(idx, vals, last - 1, last_feature1, degree - i, alpha, out_i, out_v, start)
+            i += 1
+            alpha *= v
+    return cur + poly_size(last_feature + 1, degree)
+
+
 class VectorPolynomialExpandMapper(SISOMapper):
+    """All monomials of degree 1..``degree`` (reference ``PolynomialExpansionMapper.java``): dense in, dense out;
+    sparse in, sparse out over the stored entries; size ``poly_size(n, degree) - 1``."""
+
     def outputType(self):
         return Types.VECTOR
 
     def mapColumn(self, v):
         if v is None:
             return None
-        x = VectorUtil.getVector(v).toDense().data
+        vec = VectorUtil.getVector(v)
         degree = int(self.params.get("degree")) if self.params.contains("degree") else 2
-        out = []
-        n = len(x)
-        # Spark/Alink ordering: for degree expansion generate monomials in lexicographic order of exponents
-        for deg in range(1, degree + 1):
-            for comb in itertools.combinations_with_replacement(range(n), deg):
-                out.append(float(np.prod([x[i] for i in comb])))
+        if isinstance(vec, SparseVector):
+            out_i, out_v = [], []
+            _expand_sparse(vec.indices, vec.values, len(vec.indices) - 1, vec.size() - 1, degree, 1.0, out_i, out_v,
+                           -1)
+            return SparseVector(poly_size(vec.size(), degree) - 1, out_i, out_v)
+        x = vec.data
+        out = np.zeros(poly_size(len(x), degree) - 1)
+        _expand_dense(x, len(x) - 1, degree, 1.0, out, -1)
         return DenseVector(out)
 
 

@@ -3,6 +3,8 @@ checked against the reference docs (docs/en/columnstokvbatchop.md, jsonvaluebatc
 tripletojsonbatchop.md, jsontovectorbatchop.md) and Java HashMap iteration order."""
 import json
 
+import numpy as np
+
 import pytest
 
 from alink_amd import *  # noqa: F401,F403
@@ -106,3 +108,23 @@ def test_stream_and_pipeline_twins():
     p = Pipeline(ColumnsToKv().setSelectedCols(["f0", "f1"]).setKvCol("kv2"), Select("row, kv2"))
     assert [tuple(r) for r in p.fit(_data()).transform(_data()).collect()] == \
         [("1", "f0:1.0,f1:2.0"), ("2", "f0:4.0,f1:8.0")]
+
+
+def test_polynomial_expansion_reference_order():
+    """PolynomialExpansionMapperTest (reference operator/common/dataproc/vector): Spark's monomial order, dense in
+    -> dense out, sparse in -> sparse out, sizes C(n + d, d) - 1."""
+    from alink_amd import VectorPolynomialExpandBatchOp
+    from alink_amd.common.linalg import DenseVector, SparseVector
+    from alink_amd.models.dataproc.vector import poly_size
+    from alink_amd.operator.batch.source import MemSourceBatchOp
+    src = MemSourceBatchOp([(DenseVector([3.0, 4.0]),), (SparseVector(3, [0, 2], [2.0, 3.0]),)], "vec vector")
+    out = VectorPolynomialExpandBatchOp().setSelectedCol("vec").setOutputCol("res").setDegree(2).linkFrom(src) \
+        .collect()
+    assert out[0][1] == DenseVector([3.0, 9.0, 4.0, 12.0, 16.0])
+    assert out[1][1] == SparseVector(9, [0, 1, 5, 6, 8], [2.0, 4.0, 3.0, 6.0, 9.0])
+    assert poly_size(4, 4) == 70 and poly_size(65, 2) == 2211
+    d3 = VectorPolynomialExpandBatchOp().setSelectedCol("vec").setDegree(3).linkFrom(
+        MemSourceBatchOp([(DenseVector([2.0, 0.0, 1.5]),)], "vec vector")).collect()[0][0]
+    sp3 = VectorPolynomialExpandBatchOp().setSelectedCol("vec").setDegree(3).linkFrom(
+        MemSourceBatchOp([(SparseVector(3, [0, 2], [2.0, 1.5]),)], "vec vector")).collect()[0][0]
+    np.testing.assert_array_equal(sp3.toDenseVector().getData(), d3.getData())   # same monomials either way
