@@ -82,7 +82,8 @@ def cluster_metrics(mt: MTable, params: Params, env) -> ClusterMetrics:
         sub = mt.take(rows)
         X = extract_features(sub, None, vec_col, dev).to_dense().double()
         cid = torch.tensor([index[str(preds[i])] for i in rows], dtype=torch.long, device=dev)
-        if dist == "COSINE":
+        if dist != "EUCLIDEAN":
+            # reference getClusterStatistics: every non-Euclidean distance (COSINE, CITYBLOCK) sums unit vectors
             X = X / X.norm(dim=1, keepdim=True).clamp_min(1e-300)
         d = X.shape[1]
         d = max(comm.all_gather_object(int(d)))
@@ -97,15 +98,21 @@ def cluster_metrics(mt: MTable, params: Params, env) -> ClusterMetrics:
         mean = s / cnt.clamp_min(1.0)[:, None]
 
         def dfun(a, b):
+            # ContinuousDistance.calc of the metric (CosineDistance divides by both norms; CITYBLOCK = ManHattan)
             if dist == "COSINE":
-                return 1.0 - (a * b).sum(-1)
+                cross = a.norm(dim=-1) * b.norm(dim=-1)
+                dot = (a * b).sum(-1)
+                return 1.0 - torch.where(cross > 0, dot / torch.where(cross > 0, cross, torch.ones_like(cross)),
+                                         torch.zeros_like(dot))
+            if dist == "CITYBLOCK":
+                return (a - b).abs().sum(-1)
             return torch.sqrt(((a - b) ** 2).sum(-1).clamp_min(0.0))
 
         own = dfun(X, mean[cid])
         dsum = torch.zeros(k, dtype=torch.float64, device=dev).index_add_(0, cid, own)
         d2sum = torch.zeros(k, dtype=torch.float64, device=dev).index_add_(0, cid, own * own)
-        # silhouette (closed form over cluster sums)
-        if dist == "COSINE":
+        # silhouette (closed form over cluster sums; the reference's non-Euclidean form uses 1 - x.mean)
+        if dist != "EUCLIDEAN":
             dis = 1.0 - X @ mean.T                                         # [n, k]
             cur = torch.where(cnt[cid] > 1, dis.gather(1, cid[:, None])[:, 0] * cnt[cid] / (cnt[cid] - 1),
                               torch.zeros_like(own))

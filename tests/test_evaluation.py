@@ -158,3 +158,59 @@ def test_binary_metrics_from_bins_reference_values():
     for name, v in expect.items():
         assert getattr(m, "get" + name)() == pytest.approx(v, abs=0.01), name
     assert m.getLogLoss() == pytest.approx(2.987 / 5)
+
+
+def _ref_cluster_metrics(X, cid, dist):
+    """The reference ClusterEvaluationUtil / ClusterMetricsSummary formulas, written out in numpy."""
+    ks = sorted(set(cid))
+    if dist != "EUCLIDEAN":
+        X = X / np.linalg.norm(X, axis=1, keepdims=True)
+
+    def d(a, b):
+        if dist == "COSINE":
+            return 1.0 - a @ b / (np.linalg.norm(a) * np.linalg.norm(b))
+        if dist == "CITYBLOCK":
+            return np.abs(a - b).sum()
+        return np.linalg.norm(a - b)
+    mean = {k: X[cid == k].mean(0) for k in ks}
+    cnt = {k: int((cid == k).sum()) for k in ks}
+    dsum = {k: sum(d(mean[k], x) for x in X[cid == k]) for k in ks}
+    d2 = {k: sum(d(mean[k], x) ** 2 for x in X[cid == k]) for k in ks}
+    n2 = {k: float((X[cid == k] ** 2).sum()) for k in ks}
+    gmean = sum(mean[k] * cnt[k] for k in ks) / len(X)
+    ssb = sum(d(mean[k], gmean) ** 2 * cnt[k] for k in ks)
+    ssw = sum(d2.values())
+    comp = {k: dsum[k] / cnt[k] for k in ks}
+    sil = 0.0
+    for x, c in zip(X, cid):
+        cur, nb = 0.0, np.inf
+        for k in ks:
+            if dist == "EUCLIDEAN":
+                dis = cnt[k] * (x @ x) - 2 * cnt[k] * (x @ mean[k]) + n2[k]
+                if k == c:
+                    cur = dis / (cnt[k] - 1) if cnt[k] > 1 else 0.0
+                else:
+                    nb = min(nb, dis / cnt[k])
+            else:
+                dis = 1.0 - x @ mean[k]
+                if k == c:
+                    cur = dis * cnt[k] / (cnt[k] - 1) if cnt[k] > 1 else 0.0
+                else:
+                    nb = min(nb, dis)
+        sil += 1 - cur / nb if cur < nb else nb / cur - 1
+    return {"Ssb": ssb, "Ssw": ssw, "Compactness": sum(comp.values()) / len(ks),
+            "SilhouetteCoefficient": sil / len(X)}
+
+
+@pytest.mark.parametrize("dist", ["EUCLIDEAN", "COSINE", "CITYBLOCK"])
+def test_eval_cluster_distance_types_match_reference_formulas(dist):
+    from alink_amd import EvalClusterBatchOp
+    rng = np.random.default_rng(4)
+    X = np.abs(rng.normal(size=(60, 3))) + np.repeat(np.eye(3) * 3, 20, axis=0)
+    cid = np.repeat(np.arange(3), 20)
+    df = pd.DataFrame({"vec": [" ".join(map(str, r)) for r in X], "pred": cid})
+    src = BatchOperator.fromDataframe(df, schemaStr="vec string, pred int")
+    m = EvalClusterBatchOp().setVectorCol("vec").setPredictionCol("pred").setDistanceType(dist).linkFrom(src) \
+        .collectMetrics()
+    for name, v in _ref_cluster_metrics(X, cid, dist).items():
+        assert getattr(m, "get" + name)() == pytest.approx(v, rel=1e-9, abs=1e-12), name
