@@ -113,3 +113,27 @@ def test_softmax_hessian_diagonal():
     expect = [20.008609951451433, 20.060220545670703, 20.172295036435074, 20.34483342374455, 20.577835707599135,
               20.008609951941853, 20.060220576228186, 20.172295149343217, 20.344833671286942, 20.57783614205936]
     np.testing.assert_allclose(torch.diagonal(H).numpy(), expect, rtol=1e-10)
+
+
+def test_unary_loss_function_properties():
+    """UnaryLossFuncTest (reference operator/common/linear/unarylossfunc): margin losses decrease in the margin,
+    are symmetric in (eta, y) -> (-eta, -y), convex; regression losses vanish and are flat at the target."""
+    from alink_amd.models.linear import objfunc as O
+    t = lambda v: torch.tensor(v, dtype=torch.float64)     # noqa: E731
+
+    def f(fn, eta, y):
+        return float(fn(t(eta), t(y)))
+    for lf in (O.ExponentialLossFunc(), O.HingeLossFunc(), O.LogisticLossFunc(), O.LogLossFunc(),
+               O.PerceptronLossFunc(), O.ZeroOneLossFunc()):
+        name = type(lf).__name__
+        assert f(lf.loss, -1.0, 1.0) > 1.0 - 1e-10, name
+        assert f(lf.loss, 1.0, 1.0) < 0.5, name
+        assert f(lf.loss, -0.5, 1.0) - f(lf.loss, 0.5, 1.0) > 0.49, name
+        assert f(lf.loss, -0.5, 1.0) == f(lf.loss, 0.5, -1.0), name
+        assert f(lf.derivative, -0.5, 1.0) <= f(lf.derivative, 0.5, 1.0), name
+        assert f(lf.second_derivative, -0.5, 1.0) >= f(lf.second_derivative, 0.5, 1.0), name
+    for lf in (O.SquareLossFunc(), O.SvrLossFunc(1.0), O.HuberLossFunc(1.0)):
+        name = type(lf).__name__
+        assert abs(f(lf.loss, 0.0, 0.0)) < 1e-10 and abs(f(lf.derivative, 0.0, 0.0)) < 1e-10, name
+        assert f(lf.derivative, -0.5, 0.0) == -f(lf.derivative, 0.5, 0.0), name
+        assert f(lf.second_derivative, -0.5, 0.0) == f(lf.second_derivative, 0.5, 0.0), name
