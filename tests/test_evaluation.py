@@ -214,3 +214,37 @@ def test_eval_cluster_distance_types_match_reference_formulas(dist):
         .collectMetrics()
     for name, v in _ref_cluster_metrics(X, cid, dist).items():
         assert getattr(m, "get" + name)() == pytest.approx(v, rel=1e-9, abs=1e-12), name
+
+
+def test_multiclass_metrics_reference_values():
+    """MultiClassMetricsTest.saveAsParamsTest (reference operator/common/evaluation)."""
+    from alink_amd.models.evaluation import metrics as M
+    m = M.multi_metrics(np.array([[0, 3, 1], [1, 1, 1], [2, 0, 4]], dtype=np.float64), ["0", "1", "2"], 0.4, 13)
+    expect = {"MacroRecall": 0.3055555555555555, "MacroSpecificity": 0.6973544973544974,
+              "MacroAccuracy": 0.5897435897435898, "MicroFalseNegativeRate": 0.6153846153846154,
+              "WeightedRecall": 0.38461538461538464, "WeightedPrecision": 0.41025641025641024,
+              "MacroPrecision": 0.3333333333333333, "MicroTruePositiveRate": 0.38461538461538464,
+              "MacroKappa": 0.01753139066571909, "MicroSpecificity": 0.6923076923076923,
+              "MacroF1": 0.31746031746031744, "WeightedKappa": 0.10234541577825165,
+              "WeightedTruePositiveRate": 0.38461538461538464, "MicroTrueNegativeRate": 0.6923076923076923,
+              "MicroSensitivity": 0.38461538461538464, "WeightedAccuracy": 0.6153846153846154,
+              "Accuracy": 0.38461538461538464, "WeightedFalseNegativeRate": 0.6153846153846154,
+              "MicroF1": 0.38461538461538464, "WeightedSpecificity": 0.7074481074481075,
+              "WeightedF1": 0.39560439560439564, "MicroAccuracy": 0.5897435897435898,
+              "WeightedTrueNegativeRate": 0.7074481074481075, "Kappa": 0.04587155963302759,
+              "MacroSensitivity": 0.3055555555555555, "WeightedSensitivity": 0.38461538461538464,
+              "MicroRecall": 0.38461538461538464, "MacroFalseNegativeRate": 0.6944444444444445,
+              "MicroFalsePositiveRate": 0.3076923076923077, "WeightedFalsePositiveRate": 0.29255189255189257,
+              "MicroPrecision": 0.38461538461538464, "MacroTrueNegativeRate": 0.6973544973544974,
+              "MicroKappa": 0.0769230769230769}
+    for name, v in expect.items():
+        assert getattr(m, "get" + name)() == pytest.approx(v, rel=1e-9, abs=1e-12), name
+    assert m.getLogLoss() == pytest.approx(0.4 / 13)
+
+
+def test_regression_metrics_reference_values():
+    """RegressionMetricsTest.saveAsParamsTest: sums (y, y^2, pred, pred^2, mae, sse, mape, total)."""
+    from alink_amd.models.evaluation import metrics as M
+    m = M.regression_metrics(np.array([1.6, 0.66, 2.8, 1.599, 1.2, 0.38, 7.08, 5]))
+    for name, v in {"R2": -1.56, "Sse": 0.38, "Mape": 141.6, "Rmse": 0.27, "Mae": 0.24, "Ssr": 0.31}.items():
+        assert getattr(m, "get" + name)() == pytest.approx(v, abs=0.01), name
