@@ -189,3 +189,52 @@ def test_meta_label_values_without_aux_rows():
     meta.set("labelValues", [2.0, 1.0])
     m = LinearModelDataConverter(Types.LONG).load([(rows[0][0], meta.toJson(), None), rows[1]])
     assert m.labelValues == [2, 1] and all(isinstance(v, int) for v in m.labelValues)
+
+
+SOFTMAX_ROWS = [
+    (0, '{"hasInterceptItem":"true","modelName":"\\"softmax\\"","labelType":"4","modelSchema":"\\"model_id bigint,'
+        'model_info string,label_type int\\"","isNewFormat":"true"}', None),
+    (1048576, '{"featureColNames":["f0","f1","f2"],"coefVector":{"data":[172.15928828045577,-18.99714734506609,'
+              '-93.78617647691524,27.419236408736307,-825.863312143001,-47.67468533510818,97.56887933300092,'
+              '87.33950982847793]}}', None),
+    (2097152, None, None), (2147483647 * 1048576, None, 1), (2147483647 * 1048576 + 1, None, 2),
+    (2147483647 * 1048576 + 2, None, 3)]
+
+
+@pytest.mark.parametrize("reserved", [[], None])
+def test_softmax_model_mapper_reference_rows(reserved):
+    """SoftmaxModelMapperTest (reference operator/common/classification): 3-column model table with integer
+    labels in the label_type column; (1, 7, 9) -> label 2, with and without reserved columns."""
+    from alink_amd.common.params import Params
+    from alink_amd.common.types import TableSchema, Types
+    from alink_amd.models.linear.model import SoftmaxModelMapper
+    ms = TableSchema(["model_id", "model_info", "label_type"], [Types.LONG, Types.STRING, Types.INT])
+    ds = TableSchema(["f0", "f1", "f2"], [Types.DOUBLE] * 3)
+    p = Params().set("predictionCol", "pred")
+    if reserved is not None:
+        p.set("reservedCols", reserved)
+    m = SoftmaxModelMapper(ms, ds, p)
+    m.loadModel(SOFTMAX_ROWS)
+    out = m.map((1.0, 7.0, 9.0))
+    assert out[-1] == 2
+    names = ["pred"] if reserved == [] else ["f0", "f1", "f2", "pred"]
+    assert m.getOutputSchema() == TableSchema(names, [Types.DOUBLE] * (len(names) - 1) + [Types.INT])
+
+
+def test_aft_model_mapper_reference_rows():
+    """AFTRegressionMapperTest (reference operator/common/regression): a prediction column already in the input
+    is overwritten in place; exp(x . coef) for "1.560 -0.605" = 5.71."""
+    from alink_amd.common.params import Params
+    from alink_amd.common.types import TableSchema, Types
+    from alink_amd.models.linear.model import AFTModelMapper
+    rows = [(0, '{"hasInterceptItem":"true","vectorColName":"\\"features\\"","modelName":"\\"AFTSurvivalRegTrainBatchOp'
+                '\\"","labelType":"8","modelSchema":"\\"model_id bigint,model_info string,label_type double\\"",'
+                '"isNewFormat":"true","linearModelType":"\\"AFT\\"","vectorSize":"2"}', None),
+            (1048576, '{"coefVector":{"data":[2.6380946835087933,-0.49631115827728234,0.19844422562555475,'
+                      '1.5472345338855131]}}', None)]
+    ms = TableSchema(["model_id", "model_info", "label_type"], [Types.LONG, Types.STRING, Types.DOUBLE])
+    ds = TableSchema(["vector", "pred"], [Types.STRING, Types.DOUBLE])
+    m = AFTModelMapper(ms, ds, Params().set("vectorCol", "vector").set("predictionCol", "pred"))
+    m.loadModel(rows)
+    assert float(m.map(("1.560 -0.605", None))[1]) == pytest.approx(5.71, abs=0.01)
+    assert m.getOutputSchema() == ds
