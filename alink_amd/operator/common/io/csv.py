@@ -7,13 +7,14 @@ is built; this module is the reference implementation and fallback.
 """
 from __future__ import annotations
 
+import datetime
 from typing import List, Optional, Sequence, Tuple
 
 from ....common.javafmt import java_double_str
 from ....common.linalg import Vector, VectorUtil
 from ....common.types import AlinkType, Types
 
-__all__ = ["CsvParser", "CsvFormatter", "parse_token"]
+__all__ = ["CsvParser", "CsvFormatter", "parse_token", "parse_timestamp", "format_timestamp"]
 
 
 def parse_token(tok: str, t: AlinkType):
@@ -35,7 +36,33 @@ def parse_token(tok: str, t: AlinkType):
         raise ValueError(s)
     if t in (Types.VECTOR, Types.DENSE_VECTOR, Types.SPARSE_VECTOR):
         return VectorUtil.parse(s)
+    if t == Types.TIMESTAMP:
+        return parse_timestamp(s)
+    if t == Types.DATE:
+        return datetime.date.fromisoformat(s)
+    if t == Types.TIME:
+        return datetime.time.fromisoformat(s)
     return s
+
+
+def parse_timestamp(s: str) -> datetime.datetime:
+    """``java.sql.Timestamp.valueOf``: ``yyyy-[m]m-[d]d hh:mm:ss[.f...]`` (fraction up to nanoseconds; Python keeps
+    microseconds)."""
+    date, _, clock = s.strip().partition(" ")
+    y, mo, d = (int(x) for x in date.split("-"))
+    hms, _, frac = clock.partition(".")
+    h, mi, sec = (int(x) for x in hms.split(":"))
+    if frac and (not frac.isdigit() or len(frac) > 9):
+        raise ValueError(s)
+    micro = int((frac + "000000000")[:9]) // 1000 if frac else 0
+    return datetime.datetime(y, mo, d, h, mi, sec, micro)
+
+
+def format_timestamp(v: datetime.datetime) -> str:
+    """``java.sql.Timestamp.toString``: nanoseconds with trailing zeros removed, at least one digit."""
+    nanos = v.microsecond * 1000
+    frac = "0" if nanos == 0 else f"{nanos:09d}".rstrip("0")
+    return f"{v.year:04d}-{v.month:02d}-{v.day:02d} {v.hour:02d}:{v.minute:02d}:{v.second:02d}.{frac}"
 
 
 class CsvParser:
@@ -115,6 +142,10 @@ class CsvFormatter:
             return s
         if isinstance(v, bool):
             return "true" if v else "false"
+        if isinstance(v, datetime.datetime):
+            return format_timestamp(v)
+        if isinstance(v, (datetime.date, datetime.time)):
+            return v.isoformat()
         if isinstance(v, float):
             return java_double_str(v)
         return str(v)
