@@ -128,3 +128,25 @@ def test_polynomial_expansion_reference_order():
     sp3 = VectorPolynomialExpandBatchOp().setSelectedCol("vec").setDegree(3).linkFrom(
         MemSourceBatchOp([(SparseVector(3, [0, 2], [2.0, 1.5]),)], "vec vector")).collect()[0][0]
     np.testing.assert_array_equal(sp3.toDenseVector().getData(), d3.getData())   # same monomials either way
+
+
+def test_string_parsers_reference_cases():
+    """StringParsersTest (reference operator/common/dataproc): JSON with numbers of every form, KV with date /
+    time / timestamp columns, CSV with a multi-character separator."""
+    import datetime
+    from alink_amd.operator.batch.source import MemSourceBatchOp
+    kv = "f1=1,f2=2.0,f3=false,f4=val,f5=2018-09-10,f6=14:22:20,f7=2018-09-10 14:22:20"
+    out = KvToColumnsBatchOp().setKvCol("kv").setKvValDelimiter("=").setSchemaStr(
+        "f1 bigint, f2 double, f3 boolean, f4 string, f5 date, f6 time, f7 timestamp").linkFrom(
+        MemSourceBatchOp([(kv,)], "kv string")).collect()[0]
+    assert tuple(out[1:]) == (1, 2.0, False, "val", datetime.date(2018, 9, 10), datetime.time(14, 22, 20),
+                              datetime.datetime(2018, 9, 10, 14, 22, 20))
+    js = ('{\n  "media_name": "Titanic",\n  "title": "Titanic",\n  "compare_point": 0.0001,\n  "spider_point": 0.0000,'
+          '\n  "search_point": 0.6,\n  "collection_id": 123456,\n  "media_id": 3214\n}')
+    out = JsonToColumnsBatchOp().setJsonCol("j").setSchemaStr(
+        "media_name string, title string, compare_point double, spider_point double, search_point double, "
+        "collection_id bigint, media_id bigint").linkFrom(MemSourceBatchOp([(js,)], "j string")).collect()[0]
+    assert tuple(out[1:]) == ("Titanic", "Titanic", 0.0001, 0.0, 0.6, 123456, 3214)
+    out = CsvToColumnsBatchOp().setCsvCol("c").setFieldDelimiter("____").setSchemaStr(
+        "a string, b string, c2 string").linkFrom(MemSourceBatchOp([("hello_____world____",)], "c string")).collect()
+    assert tuple(out[0][1:]) == ("hello", "_world", None)
