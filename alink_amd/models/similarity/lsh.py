@@ -113,7 +113,11 @@ class MinHashLSH:
         for i in range(T):
             hv = np.full((rows.n, P), HASH_PRIME, dtype=np.int64)
             if rows.idx.size:
-                cur = ((1 + rows.idx)[:, None] * self.A[i][None, :] + self.B[i][None, :]) % HASH_PRIME
+                # the reference's (int)((1L + index) * a + b) % HASH_PRIME: the cast to int comes first (the
+                # product wraps to 32 bits), then Java's truncating remainder, which keeps the sign
+                v = (1 + rows.idx.astype(np.int64))[:, None] * self.A[i][None, :] + self.B[i][None, :]
+                w = ((v + (1 << 31)) % (1 << 32)) - (1 << 31)
+                cur = np.fmod(w, HASH_PRIME)
                 nz = counts > 0
                 starts = rows.ptr[:-1][nz]
                 hv[nz] = np.minimum.reduceat(cur, starts, axis=0)

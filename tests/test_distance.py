@@ -62,3 +62,18 @@ def test_pairwise_on_torch_rows_matches_cdist():
     X, Y = torch.randn(50, 8, generator=g, dtype=torch.float64), torch.randn(30, 8, generator=g, dtype=torch.float64)
     torch.testing.assert_close(EuclideanDistance().pairwise(X, Y), torch.cdist(X, Y), rtol=1e-9, atol=1e-9)
     torch.testing.assert_close(ManHattanDistance().pairwise(X, Y), torch.cdist(X, Y, p=1.0))
+
+
+def test_lsh_hash_functions_reference_values():
+    """MinHashLSHTest / BucketRandomProjectionLSHTest (reference operator/common/feature): table hashes of seed 0,
+    2 projections x 2 tables (BRP: width 1 over 5 dims), and the key distances."""
+    from alink_amd.models.similarity.lsh import BucketRandomProjectionLSH, MinHashLSH, _Rows
+    rows = _Rows([DenseVector([1, 2, 3, 4, 5]), SparseVector(5, [0, 4], [1.0, 4.0])])
+    assert MinHashLSH(0, 2, 2).hash(rows).tolist() == [[478212008, -1798305157], [-967745172, -594675602]]
+    brp = BucketRandomProjectionLSH(0, 5, 2, 2, 1.0)
+    assert brp.hash(rows, torch.device("cpu")).tolist() == [[-348137008, 1394862530], [-802232505, 1759100286]]
+    a = _Rows([DenseVector([1, 0, 0, 2, 0]), SparseVector(10, [0, 4, 5, 7, 9], [1.0] * 5)])
+    b = _Rows([DenseVector([0, 1, 0, 2, 1]), SparseVector(10, [0, 1, 3, 5, 9], [1.0] * 5)])
+    ij = np.array([0, 1])
+    np.testing.assert_allclose(MinHashLSH.distance(a, ij, b, ij), [0.75, 0.5714], atol=1e-3)
+    np.testing.assert_allclose(brp.distance_fn(torch.device("cpu"))(a, ij, b, ij), [1.732, 2.0], atol=1e-3)
