@@ -58,7 +58,9 @@ def unpack_cov(v, d: int) -> np.ndarray:
 
 
 def _root_inv(cov: torch.Tensor):
-    """(W [k, d, d], log-pseudo-determinant [k], rank [k]) with x^T Sigma^+ x = |x W|^2."""
+    """(W [k, d, d], log-pseudo-determinant [k], normaliser dimension [k]) with x^T Sigma^+ x = |x W|^2.  The
+    (2 pi)^(-k/2) factor uses the full dimension d even for a singular covariance, as the reference
+    (``MultivariateGaussian.java:89-115``: ``u = -0.5 * (k * log(2 pi) + logPseudoDet)`` with k = mean size)."""
     lam, U = torch.linalg.eigh(cov)
     tol = _EPS * lam.max(dim=-1, keepdim=True).values * cov.shape[-1]
     keep = lam > tol
@@ -66,7 +68,7 @@ def _root_inv(cov: torch.Tensor):
                            torch.zeros_like(lam))
     W = U * inv_sqrt[..., None, :]
     logdet = torch.where(keep, torch.log(torch.where(keep, lam, torch.ones_like(lam))), torch.zeros_like(lam)).sum(-1)
-    return W, logdet, keep.sum(-1).to(cov.dtype)
+    return W, logdet, torch.full_like(logdet, float(cov.shape[-1]))
 
 
 def gaussian_logpdf(X: torch.Tensor, mean: torch.Tensor, cov: torch.Tensor) -> torch.Tensor:
@@ -77,6 +79,26 @@ def gaussian_logpdf(X: torch.Tensor, mean: torch.Tensor, cov: torch.Tensor) -> t
         z = (X - mean[j]) @ W[j]
         out[:, j] = -0.5 * (rank[j] * math.log(2 * math.pi) + logdet[j]) - 0.5 * (z * z).sum(1)
     return out
+
+
+class MultivariateGaussian:
+    """Gaussian density with a possibly singular covariance (reference
+    ``A/operator/common/statistics/basicstatistic/MultivariateGaussian.java``): pseudo-inverse and
+    pseudo-determinant over the eigenvalues above ``eps * max * d``, as the GMM E-step uses."""
+
+    def __init__(self, mean, cov):
+        mu = mean.getData() if hasattr(mean, "getData") else mean
+        sig = cov.getArrayCopy2D() if hasattr(cov, "getArrayCopy2D") else cov
+        self.mean = torch.as_tensor(np.asarray(mu, dtype=np.float64))[None, :]
+        self.cov = torch.as_tensor(np.asarray(sig, dtype=np.float64))[None, :, :]
+
+    def logpdf(self, x) -> float:
+        v = x.getData() if hasattr(x, "getData") else x
+        X = torch.as_tensor(np.asarray(v, dtype=np.float64))[None, :]
+        return float(gaussian_logpdf(X, self.mean, self.cov)[0, 0])
+
+    def pdf(self, x) -> float:
+        return math.exp(self.logpdf(x))
 
 
 def _weighted_syrk(R: torch.Tensor, X: torch.Tensor) -> torch.Tensor:

@@ -105,3 +105,28 @@ def test_bisecting_model_mapper_reference_rows(detail):
         assert m.getOutputSchema() == TableSchema(["Y", "pred", "detail"], [Types.STRING, Types.LONG, Types.STRING])
     else:
         assert m.getOutputSchema() == TableSchema(["Y", "pred"], [Types.STRING, Types.LONG])
+
+
+def test_multivariate_gaussian_reference_values():
+    """MultivariateGaussianTest (reference operator/common/statistics/basicstatistic), degenerate covariance
+    included (pseudo-inverse / pseudo-determinant)."""
+    from alink_amd.common.linalg import DenseMatrix, DenseVector
+    from alink_amd.models.clustering.gmm import MultivariateGaussian
+    tol = 1e-5
+    mu1 = DenseVector.zeros(1)
+    g1 = MultivariateGaussian(mu1, DenseMatrix.ones(1, 1))
+    assert g1.pdf(DenseVector([0.0])) == pytest.approx(0.39894, abs=tol)
+    assert g1.pdf(DenseVector([1.5])) == pytest.approx(0.12952, abs=tol)
+    g2 = MultivariateGaussian(mu1, DenseMatrix.ones(1, 1).scale(4.0))
+    assert g2.pdf(DenseVector([0.0])) == pytest.approx(0.19947, abs=tol)
+    assert g2.pdf(DenseVector([1.5])) == pytest.approx(0.15057, abs=tol)
+    mu = DenseVector.zeros(2)
+    m1 = MultivariateGaussian(mu, DenseMatrix.eye(2))
+    assert m1.pdf(DenseVector.zeros(2)) == pytest.approx(0.15915, abs=tol)
+    assert m1.pdf(DenseVector.ones(2)) == pytest.approx(0.05855, abs=tol)
+    m2 = MultivariateGaussian(mu, DenseMatrix(2, 2, [4.0, -1.0, -1.0, 2.0]))
+    assert m2.pdf(DenseVector.zeros(2)) == pytest.approx(0.060155, abs=tol)
+    assert m2.pdf(DenseVector.ones(2)) == pytest.approx(0.033971, abs=tol)
+    deg = MultivariateGaussian(mu, DenseMatrix(2, 2, [1.0, 1.0, 1.0, 1.0]))
+    assert deg.pdf(DenseVector.zeros(2)) == pytest.approx(0.11254, abs=tol)
+    assert deg.pdf(DenseVector.ones(2)) == pytest.approx(0.068259, abs=tol)
