@@ -30,7 +30,7 @@ from ...common.table import Column, MTable
 from ...common.types import Types
 from ...parallel import comm
 
-__all__ = ["java_split", "TokenizerMapper", "RegexTokenizerMapper", "StopWordsRemoverMapper", "NGramMapper",
+__all__ = ["java_split", "DocWordSplitCount", "TokenizerMapper", "RegexTokenizerMapper", "StopWordsRemoverMapper", "NGramMapper",
            "SegmentMapper", "JiebaSegmenter", "DocCountVectorizerModelMapper", "DocHashCountVectorizerModelMapper",
            "train_doc_count_vectorizer", "train_doc_hash_count_vectorizer", "FEATURE_TYPES", "WORD_DELIMITER"]
 
@@ -350,6 +350,22 @@ FEATURE_TYPES = {
 
 def _ename(v, default):
     return default if v is None else str(getattr(v, "name", v)).upper()
+
+
+class DocWordSplitCount:
+    """Table function doc -> (word, count) rows, words in first-occurrence order (reference
+    ``A/operator/common/nlp/DocWordSplitCount.java``); usable with ``BatchOperator.udtf``."""
+
+    result_types = ["STRING", "LONG"]
+
+    def __init__(self, delimiter: str = " "):
+        self.delimiter = delimiter
+
+    def __call__(self, doc):
+        if doc is None:
+            return []
+        counts = Counter(w for w in java_split(str(doc), self.delimiter) if w)
+        return [(w, int(c)) for w, c in counts.items()]
 
 
 def _merge_counters(local: Counter) -> Counter:

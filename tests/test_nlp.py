@@ -143,3 +143,12 @@ def test_word2vec_batched_hs_learns_on_zipf_topics():
     final = loss()
     assert final < 0.6, final
     assert torch.isfinite(inp).all() and float(inp.abs().max()) < 10
+
+
+def test_doc_word_split_count_table_function():
+    """DocWordSplitCountTest (reference operator/common/nlp): "a b c d a b c" -> (a,2) (b,2) (c,2) (d,1)."""
+    from alink_amd.models.nlp.text import DocWordSplitCount
+    from alink_amd.operator.batch.source import MemSourceBatchOp
+    out = MemSourceBatchOp([("a b c d a b c",)], "f0 string").udtf("f0", ["w", "cnt"], DocWordSplitCount(" "), []) \
+        .collect()
+    assert [tuple(r) for r in out] == [("a", 2), ("b", 2), ("c", 2), ("d", 1)]
