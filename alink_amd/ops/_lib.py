@@ -104,6 +104,7 @@ _EXTRA_SIGNATURES = {
     "alink_csr_mv_f64": [_c_vp, _c_vp, _c_int, _c_vp, _c_i64, _c_vp, _c_vp, _c_d, _c_vp],
     "alink_tree_quantize": [_c_vp, _c_vp, _c_vp, _c_vp, _c_int, _c_i64, _c_int, _c_vp, _c_vp, _c_int, _c_int, _c_vp,
                             _c_vp],
+    "alink_tree_quantize_f32": [_c_vp, _c_vp, _c_vp, _c_int, _c_i64, _c_int, _c_vp, _c_int, _c_int, _c_vp, _c_vp],
     "alink_tree_split": [_c_vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_vp, _c_d, _c_d, _c_d, _c_d, _c_vp,
                          _c_vp, _c_vp],
     "alink_gbdt_split": [_c_vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_d, _c_d, _c_vp, _c_vp,

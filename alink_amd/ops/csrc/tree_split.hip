@@ -368,6 +368,89 @@ void launch_split(dim3 grid, hipStream_t st, const float* H, int m, int F, int B
   hipLaunchKernelGGL(tree_split_kernel<S>, grid, dim3(256), 0, st, H, m, F, B, crit, ncls, is_cat, a, b, c, d, g, p);
 }
 
+
+// K5 for fp32 columns with fp32 thresholds: u[j] = the smallest float strictly greater than the fp64 threshold
+// t[j] (NaN for the +inf padding), so for any fp32 x: t[j] < x  <=>  u[j] <= x, and the bin count
+// #{t < x} is exact while the LDS table and every search read are half the size of the fp64 kernel's.  A
+// workgroup owns QF2 = 32 features x QRB rows; a tile is 64 rows x 32 features (thread = row t & 63, features
+// (t >> 6) + 4 i, i < 8: a wave reads 64 consecutive rows of one column per load).  Each tile row goes out as
+// four 8-byte stores when the group's 32 destination columns are contiguous and 8-byte aligned (F % 8 == 0),
+// otherwise byte by byte.
+constexpr int QF2 = 32;
+constexpr int QR2 = 64;
+
+__global__ __launch_bounds__(256) void tree_quantize_f32_kernel(const int64_t* __restrict__ col_ptr,
+                                                               const int64_t* __restrict__ null_ptr,
+                                                               const int32_t* __restrict__ out_col, int Fc,
+                                                               int64_t n, int F, const float* __restrict__ thr,
+                                                               int TP, int missing, uint8_t* __restrict__ out) {
+    extern __shared__ float sthr32[];                      // [QF2][TP]
+    __shared__ uint8_t tile[QR2][QF2];
+    const int f0 = blockIdx.y * QF2;
+    const int fg = min(QF2, Fc - f0);
+    for (int i = threadIdx.x; i < QF2 * TP; i += 256) {
+        const int f = i / TP;
+        sthr32[i] = f < fg ? thr[(int64_t)(f0 + f) * TP + (i - f * TP)] : __builtin_nanf("");
+    }
+    // 8-byte row pieces: the group's destinations are out_col[f0] .. out_col[f0] + 31 and 8-aligned
+    bool vec = fg == QF2 && (F & 7) == 0 && (out_col[f0] & 7) == 0;
+    for (int f = 1; vec && f < QF2; ++f) vec = out_col[f0 + f] == out_col[f0] + f;
+    __syncthreads();
+    const int rl = threadIdx.x & (QR2 - 1);
+    const int fsub = threadIdx.x >> 6;
+    const float* cp[8];
+    const uint8_t* np[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int c = f0 + min(fsub + 4 * i, fg - 1);
+        cp[i] = reinterpret_cast<const float*>(col_ptr[c]);
+        np[i] = reinterpret_cast<const uint8_t*>(null_ptr[c]);
+    }
+    const int64_t rb0 = (int64_t)blockIdx.x * QRB;
+    const int64_t rb1 = rb0 + QRB < n ? rb0 + QRB : n;
+    for (int64_t r0 = rb0; r0 < rb1; r0 += QR2) {
+        const int64_t r = r0 + rl;
+        const bool rok = r < rb1;
+        float x[8];
+        int pos[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            x[i] = rok ? cp[i][r] : 0.0f;
+            pos[i] = 0;
+        }
+        for (int step = TP >> 1; step >= 1; step >>= 1) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+                pos[i] += sthr32[(fsub + 4 * i) * TP + pos[i] + step - 1] <= x[i] ? step : 0;
+        }
+        if (TP == 1) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) pos[i] = sthr32[(fsub + 4 * i) * TP] <= x[i] ? 1 : 0;
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int f = fsub + 4 * i;
+            const bool miss = x[i] != x[i] || (rok && np[i] != nullptr && np[i][r]);
+            if (f < fg) tile[rl][f] = (uint8_t)(miss ? missing : pos[i]);
+        }
+        __syncthreads();
+        if (vec) {
+            const int tr = threadIdx.x >> 2, q = threadIdx.x & 3;       // 64 rows x 4 pieces of 8 bytes
+            const int64_t rr = r0 + tr;
+            if (rr < rb1)
+                *reinterpret_cast<uint64_t*>(out + rr * F + out_col[f0] + 8 * q) =
+                    *reinterpret_cast<const uint64_t*>(&tile[tr][8 * q]);
+        } else {
+            for (int e = threadIdx.x; e < QR2 * QF2; e += 256) {
+                const int tr = e / QF2, f = e - tr * QF2;
+                const int64_t rr = r0 + tr;
+                if (f < fg && rr < rb1) out[rr * F + out_col[f0 + f]] = tile[tr][f];
+            }
+        }
+        __syncthreads();
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -386,6 +469,18 @@ int alink_tree_quantize(const int64_t* col_ptr, const int64_t* null_ptr, const i
     hipLaunchKernelGGL(tree_quantize_kernel, grid, dim3(256), (size_t)QF * TP * sizeof(double),
                        reinterpret_cast<hipStream_t>(stream), col_ptr, null_ptr, col_is_f32, out_col, Fc, n, F, thr,
                        T, TP, missing, out);
+    return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+// fp32 columns, fp32 "smallest float above the threshold" tables [Fc][TP] (TP a power of two <= 256, NaN pad)
+int alink_tree_quantize_f32(const int64_t* col_ptr, const int64_t* null_ptr, const int32_t* out_col, int Fc,
+                            int64_t n, int F, const float* thr, int TP, int missing, uint8_t* out, void* stream) {
+    if (n <= 0 || Fc <= 0) return 0;
+    if (TP < 1 || TP > 256 || (TP & (TP - 1)) != 0 || missing < 0 || missing > 255) return 1;
+    const dim3 grid((unsigned)((n + QRB - 1) / QRB), (unsigned)((Fc + QF2 - 1) / QF2));
+    hipLaunchKernelGGL(tree_quantize_f32_kernel, grid, dim3(256), (size_t)QF2 * TP * sizeof(float),
+                       reinterpret_cast<hipStream_t>(stream), col_ptr, null_ptr, out_col, Fc, n, F, thr, TP, missing,
+                       out);
     return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 

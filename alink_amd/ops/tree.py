@@ -17,6 +17,7 @@ below is used.
 """
 from __future__ import annotations
 
+import numpy as np
 import torch
 
 from . import _lib
@@ -311,6 +312,39 @@ def node_sums(node: torch.Tensor, sample: torch.Tensor, stats: torch.Tensor, nno
     return out[:nnodes]
 
 
+def f32_threshold_table(thresholds, TP: int) -> np.ndarray:
+    """[F, TP] float32: per threshold t the smallest float strictly greater than t, NaN padding; for every fp32 x
+    ``t < x  <=>  u <= x``, so an fp32 search counts the fp64 thresholds below x exactly."""
+    tab = np.full((len(thresholds), TP), np.nan, dtype=np.float32)
+    for i, t in enumerate(thresholds):
+        t = np.asarray(t, dtype=np.float64)
+        if t.size:
+            u = t.astype(np.float32)
+            low = u.astype(np.float64) <= t
+            u[low] = np.nextafter(u[low], np.float32(np.inf))
+            tab[i, :t.size] = u
+    return tab
+
+
+def _quantize_f32(L, cols, nulls, thresholds, out_cols, n, F, missing, out):
+    dev = out.device
+    T = max(1, max(len(t) for t in thresholds))
+    TP = 1
+    while TP < T:
+        TP <<= 1
+    cols = [c.contiguous() for c in cols]
+    nulls = [None if m is None else m.to(torch.uint8).contiguous() for m in nulls]
+    meta = torch.tensor([[c.data_ptr() for c in cols], [0 if m is None else m.data_ptr() for m in nulls]],
+                        dtype=torch.int64).to(dev)
+    oc = torch.tensor(list(out_cols), dtype=torch.int32).to(dev)
+    thr = torch.from_numpy(f32_threshold_table(thresholds, TP)).to(dev)
+    rc = L.alink_tree_quantize_f32(meta[0].data_ptr(), meta[1].data_ptr(), oc.data_ptr(), len(cols), n, F,
+                                   thr.data_ptr(), TP, int(missing), out.data_ptr(), _lib.stream_ptr(dev))
+    if rc != 0:
+        raise RuntimeError(f"alink_tree_quantize_f32 failed: {rc}")
+    torch.cuda.current_stream(dev).synchronize()      # the pointer tables must outlive the kernel
+
+
 def quantize(cols, nulls, thresholds, out_cols, n: int, F: int, missing: int, out: torch.Tensor) -> None:
     """K5: bin continuous columns into ``out`` (uint8 [n, F], row-major) on the GPU.  ``cols`` fp32/fp64 device
     vectors [n], ``nulls`` bool masks or None, ``thresholds`` per column (ascending fp64 numpy), ``out_cols``
@@ -321,6 +355,17 @@ def quantize(cols, nulls, thresholds, out_cols, n: int, F: int, missing: int, ou
     if Fc == 0 or n == 0:
         return
     cols = [c if c.dtype in (torch.float32, torch.float64) else c.to(torch.float64) for c in cols]
+    f32 = [i for i, c in enumerate(cols) if c.dtype == torch.float32]
+    if f32:
+        # fp32 columns: exact fp32 threshold tables, half the LDS traffic of the fp64 search (quantize_f32)
+        _quantize_f32(L, [cols[i] for i in f32], [nulls[i] for i in f32], [thresholds[i] for i in f32],
+                      [out_cols[i] for i in f32], n, F, missing, out)
+        rest = [i for i in range(Fc) if cols[i].dtype != torch.float32]
+        if not rest:
+            return
+        cols, nulls = [cols[i] for i in rest], [nulls[i] for i in rest]
+        thresholds, out_cols = [thresholds[i] for i in rest], [out_cols[i] for i in rest]
+        Fc = len(cols)
     cols = [c.contiguous() for c in cols]
     nulls = [None if m is None else m.to(torch.uint8).contiguous() for m in nulls]
     T = max(1, max(len(t) for t in thresholds))

@@ -397,3 +397,32 @@ def test_hip_gbdt_split_matches_torch_search():
         tops.gpu_kernels_ok = saved
     torch.testing.assert_close(got[0], ref[0], rtol=1e-9, atol=1e-9)
     assert torch.equal(got[1], ref[1]) and torch.equal(got[2], ref[2]) and torch.equal(got[4], ref[4])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("F,contiguous", [(64, True), (72, True), (40, False)])
+def test_hip_quantize_f32_exact_at_thresholds(F, contiguous):
+    """fp32 quantize (fp32 'smallest float above t' tables): values exactly at, just above and just below every
+    fp64 threshold land where torch.searchsorted over fp64 puts them; contiguous 8-aligned destinations take the
+    8-byte row-piece stores, scattered ones the byte path."""
+    from alink_amd.ops import tree as tops
+    rng = np.random.default_rng(F)
+    n = 20011
+    cols, thr, outc = [], [], []
+    perm = np.arange(F) if contiguous else rng.permutation(F)
+    for f in range(F):
+        t = np.unique(rng.normal(size=int(rng.integers(1, 256))) * (f + 1))
+        t32 = t.astype(np.float32)
+        pool = np.concatenate([t32, np.nextafter(t32, np.float32(np.inf)), np.nextafter(t32, np.float32(-np.inf)),
+                               (rng.normal(size=64) * (f + 1)).astype(np.float32), np.float32([np.nan, 0.0])])
+        v = torch.from_numpy(rng.choice(pool, size=n).astype(np.float32))
+        cols.append(v.cuda())
+        thr.append(t)
+        outc.append(int(perm[f]))
+    out = torch.full((n, F), 222, dtype=torch.uint8, device="cuda")
+    tops.quantize(cols, [None] * F, thr, outc, n, F, 255, out)
+    for f in range(F):
+        v = cols[f].double()
+        ref = torch.searchsorted(torch.as_tensor(thr[f], device="cuda"), v.contiguous(), right=False)
+        ref = torch.where(torch.isnan(v), torch.full_like(ref, 255), ref)
+        assert torch.equal(out[:, outc[f]].long(), ref), f
