@@ -173,10 +173,20 @@ class VectorInteractionMapper(MISOMapper):
         return Types.VECTOR
 
     def mapColumns(self, vals):
+        """Reference ``VectorInteractionMapper``: dense x dense -> entry i * |b| + j = a_i b_j; sparse x sparse ->
+        entry |a| * j + i (the reference's sparse layout); a dense / sparse mix is an error."""
+        if len(vals) != 2:
+            raise ValueError("VectorInteraction only support two input columns.")
         if any(v is None for v in vals):
             return None
-        a, b = [VectorUtil.getVector(x).toDense().data for x in vals[:2]]
-        return DenseVector(np.outer(b, a).reshape(-1))
+        a, b = VectorUtil.getVector(vals[0]), VectorUtil.getVector(vals[1])
+        if isinstance(a, SparseVector) != isinstance(b, SparseVector):
+            raise ValueError("Make sure the two input vectors are both dense or sparse.")
+        if isinstance(a, SparseVector):
+            idx = (a.size() * b.indices.astype(np.int64)[None, :] + a.indices.astype(np.int64)[:, None]).reshape(-1)
+            val = np.outer(a.values, b.values).reshape(-1)
+            return SparseVector(a.size() * b.size(), idx, val)
+        return DenseVector(np.outer(a.data, b.data).reshape(-1))
 
 
 def poly_size(num_features: int, degree: int) -> int:

@@ -150,3 +150,30 @@ def test_string_parsers_reference_cases():
     out = CsvToColumnsBatchOp().setCsvCol("c").setFieldDelimiter("____").setSchemaStr(
         "a string, b string, c2 string").linkFrom(MemSourceBatchOp([("hello_____world____",)], "c string")).collect()
     assert tuple(out[0][1:]) == ("hello", "_world", None)
+
+
+def test_vector_mappers_reference_values():
+    """Vector{Interaction,ElementwiseProduct,Normalize,Slice}MapperTest (reference operator/common/dataproc/vector)."""
+    from alink_amd.common.linalg import DenseVector, SparseVector
+    from alink_amd.operator.batch.source import MemSourceBatchOp
+
+    def run(op, *vals, schema="vec vector"):
+        return op.linkFrom(MemSourceBatchOp([tuple(vals)], schema)).collect()[0][-1]
+    d34 = DenseVector([3.0, 4.0])
+    assert run(VectorInteractionBatchOp().setSelectedCols(["a", "b"]).setOutputCol("o"), d34, d34,
+               schema="a vector, b vector") == DenseVector([9.0, 12.0, 12.0, 16.0])
+    assert run(VectorInteractionBatchOp().setSelectedCols(["a", "b"]).setOutputCol("o"), d34,
+               DenseVector([1.0, 2.0, 5.0]), schema="a vector, b vector") == \
+        DenseVector([3.0, 6.0, 15.0, 4.0, 8.0, 20.0])                       # a_i * b_j at i * |b| + j
+    s = SparseVector(10, [0, 9], [1.0, 4.0])
+    assert run(VectorInteractionBatchOp().setSelectedCols(["a", "b"]).setOutputCol("o"), s, s,
+               schema="a vector, b vector") == SparseVector(100, [0, 9, 90, 99], [1.0, 4.0, 4.0, 16.0])
+    assert run(VectorElementwiseProductBatchOp().setSelectedCol("vec").setScalingVector("3.0 4.5"), d34) == \
+        DenseVector([9.0, 18.0])
+    assert run(VectorElementwiseProductBatchOp().setSelectedCol("vec").setOutputCol("res")
+               .setScalingVector("$10$1:3.0 2:10.0 9:4.5"), SparseVector(10, [1, 5, 9], [2.0, 4.0, 3.0])) == \
+        SparseVector(10, [1, 5, 9], [6.0, 0.0, 13.5])
+    assert run(VectorNormalizeBatchOp().setSelectedCol("vec").setP(2.0), d34) == DenseVector([0.6, 0.8])
+    assert run(VectorNormalizeBatchOp().setSelectedCol("vec").setOutputCol("res").setP(1.0),
+               DenseVector([2.0, 3.0])) == DenseVector([0.4, 0.6])
+    assert run(VectorSliceBatchOp().setSelectedCol("vec").setIndices([0, 1]), DenseVector([3.0, 4.0, 3.0])) == d34
