@@ -59,14 +59,27 @@ class ScalerConverter(RichModelDataConverter):
         return list(self.types)
 
     def serializeModel(self, m: ScalerModelData):
-        meta = m.meta.clone()
-        meta.set("scalerKind", m.kind)
+        # exactly the reference converters' meta (Standard: withMean/withStd; MinMax: selectedCols/min/max;
+        # MaxAbs: selectedCols; Imputer: strategy/selectedCols[/fillValue]) and data rows (JSON double arrays)
         data = [gson_dumps([float(x) for x in a]) if a is not None else "null" for a in m.arrays]
-        return meta, data, []
+        return m.meta.clone(), data, []
 
     def deserializeModel(self, meta, data, aux):
         arrays = [None if d == "null" else np.asarray(json.loads(d), dtype=np.float64) for d in data]
-        return ScalerModelData(meta.get("scalerKind"), meta, arrays, None)
+        return ScalerModelData(infer_scaler_kind(meta), meta, arrays, None)
+
+
+def infer_scaler_kind(meta: Params) -> str:
+    """The model kind from the reference's meta keys (models written before round 4 also carry scalerKind)."""
+    if meta.contains("scalerKind"):
+        return str(meta.get("scalerKind"))
+    if meta.contains("strategy"):
+        return "imputer"
+    if meta.contains("withMean") or meta.contains("withStd"):
+        return "standard"
+    if meta.contains("min") and meta.contains("max"):
+        return "minmax"
+    return "maxabs"
 
 
 def train_scaler(kind: str, mt: MTable, params: Params, env) -> MTable:
@@ -188,7 +201,7 @@ class ImputerModelMapper(_ColumnScalerMapper):
 
     def _map_columns(self, mt):
         out = []
-        vals = self.model.arrays[0]
+        vals = self.model.arrays[0] if self.model.arrays else None
         fill = self.model.meta.get("fillValue") if self.model.meta.contains("fillValue") else None
         for j, c in enumerate(self.cols):
             t = self.col_types[j]
@@ -320,7 +333,7 @@ class VectorScalerModelMapper(ModelMapper):
 class VectorImputerModelMapper(VectorScalerModelMapper):
     def _map_columns(self, mt):
         m = self.model
-        vals = m.arrays[0]
+        vals = m.arrays[0] if m.arrays else None
         fill = float(m.meta.get("fillValue")) if vals is None else None
         out = []
         for v in mt.col(self.vc).to_list():

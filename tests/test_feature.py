@@ -127,3 +127,47 @@ def test_correlation_pairwise_complete_and_spearman():
     sp = CorrelationBatchOp().setSelectedCols(["a", "b"]).setMethod("SPEAMAN").linkFrom(src2) \
         .collectCorrelation().getCorrelationMatrix()
     assert sp.get(0, 1) == pytest.approx(0.4)                 # 1 - 6 * 6 / (4 * 15)
+
+
+def _mapper_table(rows, names, types):
+    from alink_amd.common.types import TableSchema
+    return rows, TableSchema(names, types)
+
+
+def test_scaler_and_imputer_mappers_on_reference_model_rows():
+    """{Imputer,StandardScaler,MinMaxScaler,MaxAbsScaler}MapperTest (reference operator/common/dataproc): the
+    reference's model tables (no scalerKind key) load and transform in place, arrays in model-column order."""
+    from alink_amd.common.params import Params
+    from alink_amd.common.types import TableSchema, Types
+    from alink_amd.models.feature import scalers as S
+    T = Types
+    ms = TableSchema(["model_id", "model_info", "f_double", "f_long", "f_int"], [T.LONG, T.STRING, T.DOUBLE, T.LONG,
+                                                                                   T.INT])
+    ds = TableSchema(["f_string", "f_long", "f_int", "f_double", "f_boolean"],
+                     [T.STRING, T.LONG, T.INT, T.DOUBLE, T.BOOLEAN])
+    for strat, vals, expect in (("mean", "[0.3333333333333333,1.0,1.0]", (1, 1, 0.3333333333333333)),
+                                ("min", "[-3.0,0.0,0.0]", (0, 0, -3.0)), ("min", "[2.0, 2.0, 2.0]", (2, 2, 2.0))):
+        m = S.ImputerModelMapper(ms, ds, Params())
+        m.loadModel([(0, '{"selectedCols":"[\\"f_double\\",\\"f_long\\",\\"f_int\\"]","strategy":"\\"%s\\""}' % strat,
+                      None, None, None), (1048576, vals, None, None, None)])
+        r = m.map(("a", None, None, None, True))
+        assert (r[1], r[2]) == expect[:2] and type(r[1]) is int and r[3] == pytest.approx(expect[2])
+    msb = TableSchema(["model_id", "model_info", "f_double", "f_long", "f_int", "f_boolean"],
+                      [T.LONG, T.STRING, T.DOUBLE, T.LONG, T.INT, T.BOOLEAN])
+    m = S.ImputerModelMapper(msb, ds, Params())
+    m.loadModel([(0, '{"selectedCols":"[\\"f_double\\",\\"f_long\\",\\"f_int\\",\\"f_boolean\\"]","fillValue":"\\"0\\"",'
+                     '"strategy":"\\"VALUE\\""}', None, None, None, None)])
+    assert tuple(m.map(("a", None, None, None, None))[1:]) == (0, 0, 0.0, False)
+    m = S.StandardScalerModelMapper(ms, ds, Params())
+    m.loadModel([(0, '{"withMean":"true","withStd":"true"}', None, None, None),
+                 (1048576, "[1.0,1.0,0.2]", None, None, None), (2097152, "[1.0,1.0,1.0]", None, None, None)])
+    assert tuple(m.map(("a", 1, 1, 2.0, True))[1:4]) == pytest.approx((0.0, 0.8, 1.0))
+    m = S.MinMaxScalerModelMapper(ms, ds, Params())
+    m.loadModel([(0, '{"min":"0.0","max":"1.0","selectedCols":"[\\"f_long\\",\\"f_int\\",\\"f_double\\"]"}', None, None,
+                  None), (1048576, "[0.0,0.0,-3.0]", None, None, None), (2097152, "[2.0, 2.0, 2.0]", None, None, None)])
+    assert tuple(m.map(("d", 1, 1, 2.0, True))[1:4]) == pytest.approx((0.5, 0.8, 1.0))
+    m = S.MaxAbsScalerModelMapper(TableSchema(["model_id", "model_info", "f0", "f1"], [T.LONG, T.STRING, T.DOUBLE,
+                                                                                     T.DOUBLE]),
+                                  TableSchema(["f0", "f1"], [T.DOUBLE, T.DOUBLE]), Params())
+    m.loadModel([(0, '{"selectedCols":"[\\"f0\\",\\"f1\\"]"}', None, None), (1048576, "[4.0,3.0]", None, None)])
+    assert tuple(m.map((1.0, 2.0))) == pytest.approx((0.25, 0.6666666666666666))
