@@ -457,6 +457,58 @@ FUNCTIONS: Dict[str, Callable] = {
 }
 
 
+def _pad(s, n, pad, left):
+    """Flink LPAD / RPAD: NULL for a negative length or an empty pad; truncation when ``n`` <= len(s)."""
+    n = int(n)
+    if n < 0 or not pad:
+        return None
+    if n <= len(s):
+        return s[:n]
+    fill = (pad * (n // len(pad) + 1))[:n - len(s)]
+    return fill + s if left else s + fill
+
+
+def _sha(bits):
+    import hashlib
+    algo = {1: hashlib.sha1, 224: hashlib.sha224, 256: hashlib.sha256, 384: hashlib.sha384, 512: hashlib.sha512}
+    return lambda s: algo[bits](s.encode("utf-8")).hexdigest()
+
+
+def _sha2(s, bits):
+    b = int(bits)
+    if b == 0:
+        b = 256
+    if b not in (224, 256, 384, 512):
+        return None
+    return _sha(b)(s)
+
+
+def _log(a, b=None):
+    # LOG(x) = ln x; LOG(base, x) = ln x / ln base (reference MathFunctions.LOG / LOG_WITH_BASE)
+    return math.log(a) if b is None else math.log(b) / math.log(a)
+
+
+# the reference's registered scalar functions (common/sql/functions MathFunctions, StringFunctions) and the Flink
+# built-ins they complete
+FUNCTIONS.update({
+    "LOG": _nullsafe(_log), "SINH": _nullsafe(math.sinh), "COSH": _nullsafe(math.cosh), "TANH": _nullsafe(math.tanh),
+    "COT": _nullsafe(lambda a: 1.0 / math.tan(a)), "ATAN2": _nullsafe(math.atan2),
+    "DEGREES": _nullsafe(math.degrees), "RADIANS": _nullsafe(math.radians),
+    "TRUNCATE": _nullsafe(lambda a, n=0: math.trunc(a * 10 ** int(n)) / 10 ** int(n) if int(n) else
+                          (math.trunc(a) if isinstance(a, int) else float(math.trunc(a)))),
+    "BIN": _nullsafe(lambda v: format(int(v) & 0xFFFFFFFFFFFFFFFF, "b")),       # Long.toBinaryString
+    "HEX": _nullsafe(lambda v: v.encode("utf-8").hex().upper() if isinstance(v, str)
+                     else format(int(v) & 0xFFFFFFFFFFFFFFFF, "x")),                 # Long.toHexString / bytes
+    "LPAD": _nullsafe(lambda s, n, p: _pad(s, n, p, True)),
+    "RPAD": _nullsafe(lambda s, n, p: _pad(s, n, p, False)),
+    "SHA1": _nullsafe(_sha(1)), "SHA224": _nullsafe(_sha(224)), "SHA256": _nullsafe(_sha(256)),
+    "SHA384": _nullsafe(_sha(384)), "SHA512": _nullsafe(_sha(512)), "SHA2": _nullsafe(_sha2),
+    "UUID": lambda: str(__import__("uuid").uuid4()),
+    "INITCAP": _nullsafe(lambda s: re.sub(r"[A-Za-z0-9]+", lambda m: m.group(0)[0].upper() + m.group(0)[1:].lower(), s)),
+    "REPEAT": _nullsafe(lambda s, n: s * max(0, int(n))),
+})
+
+
 def _agg(name, vals, distinct):
     vals = [v for v in vals if v is not None]
     if distinct:

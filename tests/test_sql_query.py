@@ -77,3 +77,31 @@ def test_parse_errors():
     with pytest.raises(ValueError):
         parse_query("select a from t join u")
     assert math.isfinite(len(parse_query("select a from t;").body.items))
+
+
+def test_reference_scalar_functions():
+    """MathFunctionsTest / StringFunctionsTest (reference common/sql/functions) through select."""
+    import hashlib
+    import math
+    import re
+    from alink_amd.operator.batch.source import MemSourceBatchOp
+    src = MemSourceBatchOp([(10.0, "HelloWorld", "hello,world", 100, "foobar", "foothebar", "hi", "SGVsbG9Xb3JsZA==")],
+                           "v double, s string, h string, n long, f string, g string, t string, b string")
+
+    def q(e):
+        return src.select(e + " AS r").collect()[0][0]
+    assert q("LOG2(v)") == pytest.approx(math.log(10) / math.log(2))
+    assert q("LOG(v)") == pytest.approx(math.log(10))
+    assert q("LOG(3, v)") == pytest.approx(math.log(10) / math.log(3))
+    assert (q("SINH(v)"), q("COSH(v)"), q("TANH(v)")) == pytest.approx((math.sinh(10), math.cosh(10), math.tanh(10)))
+    assert q("BIN(n)") == "1100100" and q("HEX(n)") == "64" and q("HEX(h)") == "68656C6C6F2C776F726C64"
+    assert q("FROM_BASE64(b)") == "HelloWorld" and q("TO_BASE64(s)") == "SGVsbG9Xb3JsZA=="
+    assert q("LPAD(t, 4, '??')") == "??hi" and q("RPAD(t, 4, '??')") == "hi??"
+    assert q("REGEXP_REPLACE(f, 'oo|ar', '')") == "fb"
+    assert q("REGEXP_EXTRACT(g, 'foo(.*?)(bar)', 2)") == "bar"
+    assert q("MD5(s)") == hashlib.md5(b"HelloWorld").hexdigest()
+    assert q("SHA1(s)") == hashlib.sha1(b"HelloWorld").hexdigest()
+    for bits in (224, 256, 384, 512):
+        assert q(f"SHA{bits}(s)") == getattr(hashlib, f"sha{bits}")(b"HelloWorld").hexdigest()
+    assert q("SHA2(s, 384)") == hashlib.sha384(b"HelloWorld").hexdigest()
+    assert re.fullmatch("[0-9a-f]{8}-[0-9a-f]{4}-[1-5][0-9a-f]{3}-[89ab][0-9a-f]{3}-[0-9a-f]{12}", q("UUID()"))
