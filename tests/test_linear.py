@@ -238,3 +238,33 @@ def test_aft_model_mapper_reference_rows():
     m.loadModel(rows)
     assert float(m.map(("1.560 -0.605", None))[1]) == pytest.approx(5.71, abs=0.01)
     assert m.getOutputSchema() == ds
+
+
+REG_ROWS = [("$3$0:1.0 1:7.0 2:9.0", "1.0 7.0 9.0", 1.0, 7.0, 9.0, 16.8),
+            ("$3$0:1.0 1:3.0 2:3.0", "1.0 3.0 3.0", 1.0, 3.0, 3.0, 6.7),
+            ("$3$0:1.0 1:2.0 2:4.0", "1.0 2.0 4.0", 1.0, 2.0, 4.0, 6.9),
+            ("$3$0:1.0 1:3.0 2:4.0", "1.0 3.0 4.0", 1.0, 3.0, 4.0, 8.0)]
+
+
+@pytest.mark.parametrize("name,expect", [
+    ("LinearRegression", {16.8: (16.814789059973744, 16.814789059973744, 16.814788687904162),
+                          6.7: (6.773942836224718, 6.773942836224718, 6.773943529327923)}),
+    ("RidgeRegression", {16.8: (16.653595680699425, 16.653595680699425, 16.384437074591887),
+                         6.7: (6.825267886078004, 6.825267886078004, 7.425378715755974)}),
+    ("LassoRegression", {16.8: (16.784611802507232, 16.784611802507232, 16.78209421260283),
+                         6.7: (6.7713287283076, 6.7713287283076, 6.826846826823054)})])
+def test_regression_pipelines_reference_predictions(name, expect):
+    """pipeline/regression/{Linear,Ridge,Lasso}RegressionTest: feature columns, dense vector and sparse vector
+    (no mean centring for sparse input, hence the different regularised fit) give the reference's predictions."""
+    import alink_amd as A
+    from alink_amd.operator.batch.source import MemSourceBatchOp
+    data = MemSourceBatchOp(REG_ROWS, ["svec", "vec", "f0", "f1", "f2", "label"])
+
+    def mk():
+        m = getattr(A, name)().setLabelCol("label")
+        return m if name == "LinearRegression" else m.setLambda(0.01)
+    pl = A.Pipeline().add(mk().setFeatureCols(["f0", "f1", "f2"]).setPredictionCol("p1")) \
+        .add(mk().setVectorCol("vec").setPredictionCol("p2")).add(mk().setVectorCol("svec").setPredictionCol("p3"))
+    got = {r[0]: tuple(r[1:]) for r in pl.fit(data).transform(data).select(["label", "p1", "p2", "p3"]).collect()}
+    for label, e in expect.items():
+        assert got[label] == pytest.approx(e, abs=1e-5), (label, got[label])
