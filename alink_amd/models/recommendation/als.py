@@ -45,6 +45,12 @@ class AlsModelData:
         self.user_map = {int(u): i for i, u in enumerate(self.user_ids)}
         self.item_map = {int(u): i for i, u in enumerate(self.item_ids)}
 
+    # the reference's field names (AlsModelData.java: userIds, userFactors, itemIds, itemFactors)
+    userIds = property(lambda self: self.user_ids)
+    userFactors = property(lambda self: self.user_factors)
+    itemIds = property(lambda self: self.item_ids)
+    itemFactors = property(lambda self: self.item_factors)
+
 
 def _factor_str(f: np.ndarray) -> str:
     return " ".join(java_float_str(float(x)) for x in f)

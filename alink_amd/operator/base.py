@@ -155,6 +155,8 @@ def _traced_link(fn, opname):
 
     @functools.wraps(fn)
     def linkFrom(self, *inputs):
+        if any(isinstance(t, MTable) for t in inputs):     # a model table (PipelineModel.getModelData()) as input
+            inputs = tuple(BatchOperator.fromTable(t) if isinstance(t, MTable) else t for t in inputs)
         if not _trace.enabled():
             return fn(self, *inputs)
         with _trace.span(opname, "op"):
@@ -253,6 +255,12 @@ class BatchOperator(AlgoOperator):
 
     def getSideOutputCount(self) -> int:
         return len(self._side_outputs)
+
+    @staticmethod
+    def fromTable(table: MTable) -> "BatchOperator":
+        """A batch operator over an existing table (reference ``BatchOperator.fromTable``)."""
+        from .batch.source import TableSourceBatchOp
+        return TableSourceBatchOp(table)
 
     # ---- execution / observation ----
     @classmethod

@@ -89,6 +89,48 @@ def test_als_recovers_low_rank_matrix():
     assert rmse < 0.05 * R.std()
 
 
+
+def _pipeline_als(**kw):
+    als = ALS().setUserCol("user").setItemCol("item").setRateCol("rating").setLambda(0.01).setRank(10) \
+        .setNumIter(10).setPredictionCol("predicted_rating")
+    for k, v in kw.items():
+        getattr(als, "set" + k[0].upper() + k[1:])(v)
+    return als
+
+
+def _mae(pred):
+    return EvalRegressionBatchOp().setLabelCol("rating").setPredictionCol("predicted_rating").linkFrom(pred) \
+        .collectMetrics().getMae()
+
+
+def test_als_pipeline_reference_cases():
+    """pipeline/recommendation/ALSTest: explicit and non-negative fits reach MAE < 0.02 through the pipeline model
+    and AlsPredictBatchOp over ``model.getModelData()``; non-negative factors are >= 0; an unseen user predicts
+    null; implicit preferences separate positive from non-positive ratings (MAE < 0.02 on the 0/1 labels)."""
+    from alink_amd.operator.batch.source import MemSourceBatchOp
+    data = MemSourceBatchOp([(1, 1, 0.6), (2, 2, 0.8), (2, 3, 0.6), (3, 1, 0.6), (3, 2, 0.3), (3, 3, 0.4)],
+                            "user bigint, item bigint, rating double")
+    predict = AlsPredictBatchOp().setUserCol("user").setItemCol("item").setPredictionCol("predicted_rating")
+    model = _pipeline_als().fit(data)
+    assert _mae(model.transform(data)) < 0.02
+    assert _mae(predict.linkFrom(model.getModelData(), data)) < 0.02
+
+    model = _pipeline_als(nonnegative=True).fit(data)
+    assert _mae(model.transform(data)) < 0.02
+    md = AlsModelDataConverter.load(BatchOperator.fromTable(model.getModelData()).collect())
+    assert (np.asarray(md.userFactors) >= 0).all() and (np.asarray(md.itemFactors) >= 0).all()
+    unseen = MemSourceBatchOp([(4, 1)], "user bigint, item bigint")
+    for out in (model.transform(unseen), AlsPredictBatchOp().setUserCol("user").setItemCol("item")
+                .setPredictionCol("predicted_rating").linkFrom(model.getModelData(), unseen)):
+        assert [tuple(r) for r in out.collect()] == [(4, 1, None)]
+
+    rows2 = [(1, 1, 6.0), (1, 2, -10.0), (1, 3, -5.0), (2, 1, 0.0), (2, 2, 8.0), (2, 3, 6.0), (3, 1, 6.0),
+             (3, 2, 3.0), (3, 3, 0.1)]
+    data2 = MemSourceBatchOp(rows2, "user bigint, item bigint, rating double")
+    pred = _pipeline_als(implicitPrefs=True).fit(data2).transform(data2) \
+        .select("(case rating > 0 when true then 1 else 0 end) as rating, predicted_rating")
+    assert _mae(pred) < 0.02
+
 def test_normal_equations_torch_matches_dense():
     rng = np.random.default_rng(1)
     Y = torch.as_tensor(rng.normal(size=(7, 5)), dtype=torch.float32)
