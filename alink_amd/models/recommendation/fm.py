@@ -341,7 +341,7 @@ class FmModelMapper(RichModelMapper):
         y, _ = fm_predict_raw(fm, w, V, self.m.fmModel.bias, self.m.dim)
         if self.m.task == "REGRESSION":
             pred = Column(y)
-            det = [gson_dumps({"label": float(v)}) for v in y.tolist()] if self.detail_col else None
+            det = ['{"label":%f}' % v for v in y.tolist()]   # FmModelMapper.java:92 String.format %f if self.detail_col else None
         else:
             pr = torch.sigmoid(y).tolist()
             l0, l1 = self.m.labelValues[0], self.m.labelValues[1]

@@ -17,6 +17,13 @@ class GeneralizedLinearRegression(Trainer):
 class GeneralizedLinearRegressionModel(MapModel):
     MAPPER = GlmModelMapper
 
+    def evaluate(self, data):
+        """GLM summary (coefficients, deviance, AIC, ...) of ``data`` under this model (reference
+        ``GeneralizedLinearRegressionModel.evaluate``)."""
+        from ..operator.base import BatchOperator
+        return R.GlmEvaluationBatchOp(self.getParams().clone()).linkFrom(
+            BatchOperator.fromTable(self.getModelData()).setMLEnvironmentId(self.getMLEnvironmentId()), data)
+
 
 class IsotonicRegression(Trainer):
     TRAIN_OP = R.IsotonicRegTrainBatchOp

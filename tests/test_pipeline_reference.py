@@ -104,3 +104,79 @@ def test_one_vs_rest_iris():
     model = A.OneVsRest().setClassifier(gbdt).setNumClass(3).fit(src)
     model.setPredictionCol("pred_result").setPredictionDetailCol("pred_detail")
     assert _accuracy(model.transform(src)) > 0.9
+
+
+# ---- pipeline/regression/{AFTRegTest, GeneralizedLinearRegressionTest, IsotonicRegressionTest}, FmTest ----
+AFT_DENSE = [(1.218, 1.0, "1.560,-0.605"), (2.949, 0.0, "0.346,2.158"), (3.627, 0.0, "1.380,0.231"),
+             (0.273, 1.0, "0.520,1.151"), (4.199, 0.0, "0.795,-0.226")]
+AFT_INTERCEPT = [5.70, 18.10, 7.36, 13.62, 9.03]
+AFT_NO_INTERCEPT = [10.05, 19.26, 17.45, 9.14, 3.54]
+
+
+def _aft_predict(data, with_intercept, **cols):
+    train = A.AftSurvivalRegTrainBatchOp().setLabelCol("label").setCensorCol("censor").setWithIntercept(with_intercept)
+    train = train.setFeatureCols(cols["features"]) if "features" in cols else train.setVectorCol("features")
+    pred = A.AftSurvivalRegPredictBatchOp().setPredictionCol("pred").linkFrom(train.linkFrom(data), data)
+    return [r[0] for r in pred.select(["pred"]).collect()]
+
+
+def test_aft_survival_regression_reference_predictions():
+    data = MemSourceBatchOp(AFT_DENSE, ["label", "censor", "features"])
+    sparse = MemSourceBatchOp([(a, b, "$10$3:%s,7:%s" % tuple(v.split(","))) for a, b, v in AFT_DENSE],
+                              ["label", "censor", "features"])
+    feats = MemSourceBatchOp([(a, b) + tuple(float(x) for x in v.split(",")) for a, b, v in AFT_DENSE],
+                             ["label", "censor", "f0", "f1"])
+    model = A.Pipeline().add(A.AftSurvivalRegression().setVectorCol("features").setLabelCol("label")
+                             .setCensorCol("censor").setPredictionCol("result")).fit(data)
+    assert [r[0] for r in model.transform(data).select(["result"]).collect()] == pytest.approx(AFT_INTERCEPT, abs=0.1)
+    assert _aft_predict(data, True) == pytest.approx(AFT_INTERCEPT, abs=0.1)
+    assert _aft_predict(data, False) == pytest.approx(AFT_NO_INTERCEPT, abs=0.1)
+    assert _aft_predict(sparse, False) == pytest.approx(AFT_NO_INTERCEPT, abs=0.1)
+    assert _aft_predict(feats, False, features=["f0", "f1"]) == pytest.approx(AFT_NO_INTERCEPT, abs=0.1)
+
+
+def test_glm_gamma_log_reference_rmse_and_evaluate():
+    import json
+    import math
+    g = [[1, 5, 118, 69], [2, 10, 58, 35], [3, 15, 42, 26], [4, 20, 35, 21], [5, 30, 27, 18], [6, 40, 25, 16],
+         [7, 60, 21, 13], [8, 80, 19, 12], [9, 100, 18, 12]]
+    src = MemSourceBatchOp([(math.log(a[1]), float(a[2]), float(a[3]), 1.0, 2.0) for a in g],
+                           ["u", "lot1", "lot2", "offset", "weights"])
+    model = A.GeneralizedLinearRegression().setFamily("gamma").setLink("Log").setRegParam(0.3).setFitIntercept(False) \
+        .setMaxIter(10).setOffsetCol("offset").setWeightCol("weights").setFeatureCols(["lot1", "lot2"]) \
+        .setLabelCol("u").setPredictionCol("pred").fit(src)
+    rmse = A.EvalRegressionBatchOp().setLabelCol("u").setPredictionCol("pred").linkFrom(model.transform(src)) \
+        .collectMetrics().getRmse()
+    assert rmse == pytest.approx(0.7751000666424476, abs=1e-9)
+    summary = json.loads(model.evaluate(src).collect()[0][0])
+    assert summary["rank"] == 2 and summary["intercept"] == 0.0 and len(summary["pValues"]) == 2
+
+
+def test_isotonic_regression_pipeline_reference():
+    rows = [(0.35, 1), (0.6, 1), (0.55, 1), (0.5, 1), (0.18, 0), (0.1, 1), (0.8, 1), (0.45, 0), (0.4, 1), (0.7, 0),
+            (0.02, 1), (0.3, 0), (0.27, 1), (0.2, 0), (0.9, 1)]
+    expect = [0.66, 0.75, 0.75, 0.75, 0.5, 0.5, 0.75, 0.66, 0.66, 0.75, 0.5, 0.5, 0.5, 0.5, 0.75]
+    model = A.Pipeline().add(A.IsotonicRegression().setFeatureCol("feature").setLabelCol("label")
+                             .setPredictionCol("result")).fit(MemSourceBatchOp(rows, ["feature", "label"]))
+    got = [r[0] for r in model.transform(MemSourceBatchOp(rows, ["feature", "label"])).select(["result"]).collect()]
+    assert got == pytest.approx(expect, abs=0.01)
+    out = []
+    model.transform(MemSourceStreamOp(rows, ["feature", "label"])).select(["result"]).collect_to(out)
+    A.StreamOperator.execute()
+    assert [r[0] for r in out] == pytest.approx(expect, abs=0.01)
+
+
+def test_fm_classifier_regressor_pipeline():
+    """FmTest: adagrad FM, 10 epochs; the reference prints the results.  Here the classifier separates the training
+    labels and the regressor's detail is the reference's ``{"label":%f}``."""
+    data = MemSourceBatchOp([("0:1.1 5:2.0", 1.0), ("1:2.1 6:3.1", 1.0), ("2:3.1 7:2.2", 1.0), ("3:1.2 8:3.2", 0.0),
+                             ("4:1.2 9:4.2", 0.0)], ["vec", "label"])
+
+    def fm(C):
+        return C().setVectorCol("vec").setLabelCol("label").setNumEpochs(10).setInitStdev(0.01).setLearnRate(0.1) \
+            .setEpsilon(0.0001).setPredictionCol("pred").setPredictionDetailCol("details")
+    rows = fm(A.FmClassifier).fit(data).transform(data).select(["label", "pred"]).collect()
+    assert all(r[0] == r[1] for r in rows)
+    rows = fm(A.FmRegressor).fit(data).transform(data).select(["pred", "details"]).collect()
+    for pred, det in rows:
+        assert det == '{"label":%f}' % pred
