@@ -39,6 +39,8 @@ if os.path.exists(_PATH):
             lib.alink_java_double_rows.restype = ctypes.c_int64
         if hasattr(lib, "alink_sample_thresholds"):
             lib.alink_sample_thresholds.restype = ctypes.c_int64
+        if hasattr(lib, "alink_binary_bins"):
+            lib.alink_binary_bins.restype = None
     except OSError:
         lib = None
 
@@ -183,6 +185,23 @@ def sample_thresholds(thr, step: float, err: float) -> Optional[np.ndarray]:
     m = lib.alink_sample_thresholds(_ptr(a), ctypes.c_int64(a.size), ctypes.c_double(step), ctypes.c_double(err),
                                     _ptr(keep))
     return keep[:m]
+
+
+def binary_bins(probs: np.ndarray, c0: int, c1: int, code: np.ndarray, ok: Optional[np.ndarray], B: int,
+                eps: float):
+    """(bins int64 [2B]: positive then negative half, log loss, kept rows) of a binary detail block in one C++
+    pass (``alink_binary_bins``); None without the library."""
+    if lib is None or getattr(lib, "alink_binary_bins", None) is None:
+        return None
+    pr = np.ascontiguousarray(probs, dtype=np.float64)
+    cd = np.ascontiguousarray(code, dtype=np.int64)
+    okb = None if ok is None else np.ascontiguousarray(ok, dtype=np.uint8)
+    bins = np.zeros(2 * B, dtype=np.int64)
+    out2 = np.zeros(2, dtype=np.float64)
+    lib.alink_binary_bins(_ptr(pr), ctypes.c_int64(pr.shape[0]), ctypes.c_int(pr.shape[1]), ctypes.c_int(c0),
+                          ctypes.c_int(c1), _ptr(cd), None if okb is None else _ptr(okb), ctypes.c_int(B),
+                          ctypes.c_double(eps), _ptr(bins), _ptr(out2))
+    return bins, float(out2[0]), int(out2[1])
 
 
 def parse_binary_detail(strings: Sequence[str], key0: str, key1: str):

@@ -196,10 +196,17 @@ def _label_codes(label_col):
     vals = label_col.values
     if isinstance(vals, torch.Tensor) and vals.dim() == 1:
         lab = vals.detach().cpu()
+        lnull = label_col.nulls.cpu().numpy() if label_col.nulls is not None else np.zeros(len(lab), bool)
+        if lab.dtype in (torch.int8, torch.int16, torch.int32, torch.int64, torch.uint8) and len(lab):
+            a = lab.numpy().astype(np.int64)
+            lo = int(a.min())
+            span = int(a.max()) - lo + 1
+            if span <= 1 << 16:                   # small integer range: presence table instead of a sort
+                present = np.bincount(a - lo, minlength=span) > 0
+                slot = np.cumsum(present) - 1
+                return [str(v) for v in (np.flatnonzero(present) + lo).tolist()], slot[a - lo], lnull
         uniq, inv = torch.unique(lab, return_inverse=True)
-        ustr = [str(v) for v in uniq.tolist()]
-        lnull = label_col.nulls.cpu().numpy() if label_col.nulls is not None else np.zeros(len(inv), bool)
-        return ustr, inv.numpy(), lnull
+        return [str(v) for v in uniq.tolist()], inv.numpy(), lnull
     lst = label_col.to_list()
     ustr = sorted({str(v) for v in lst if v is not None})
     pos = {u: i for i, u in enumerate(ustr)}
@@ -250,6 +257,10 @@ def binary_summary_block(label_col, blk, label_array: List[str], device=None):
     code = np.array([0 if u == label_array[0] else (1 if u == label_array[1] else -1) for u in ustr],
                     dtype=np.int64)
     rc = code[inv] if len(code) else np.zeros(0, np.int64)
+    nat = _native.binary_bins(pr, c0, c1, rc, ok, DETAIL_BIN_NUMBER, LOG_LOSS_EPS)
+    if nat is not None:                           # one C++ pass: bins + row-order log loss
+        bins, ll, keep = nat
+        return _reduce_bins(bins.astype(np.float64), ll, keep, device or torch.device("cpu"))
     sel = ok & (rc >= 0)
     is_pos = rc[sel] == 0
     p0 = pr[sel, c0]
@@ -292,17 +303,27 @@ def _binary_detail_native(labels_col, details, label_array: List[str]):
 
 
 def _binary_bins(pos_p, is_pos, ll, keep, dev):
-    p = torch.as_tensor(np.asarray(pos_p, dtype=np.float64), device=dev)
-    idx = torch.where(p == 1.0, torch.full_like(p, DETAIL_BIN_NUMBER - 1), torch.floor(p * DETAIL_BIN_NUMBER)).long()
-    lbl = torch.as_tensor(np.asarray(is_pos, dtype=bool), device=dev)
-    ok = (idx >= 0) & (idx < DETAIL_BIN_NUMBER)
-    posb = torch.bincount(idx[ok & lbl], minlength=DETAIL_BIN_NUMBER).double()
-    negb = torch.bincount(idx[ok & ~lbl], minlength=DETAIL_BIN_NUMBER).double()
-    buf = torch.cat([posb, negb, torch.tensor([ll, float(keep)], dtype=torch.float64, device=dev)])
-    comm.all_reduce(buf, "sum")
-    b = buf.cpu().numpy()
-    return (b[:DETAIL_BIN_NUMBER].astype(np.int64), b[DETAIL_BIN_NUMBER:2 * DETAIL_BIN_NUMBER].astype(np.int64),
-            float(b[-2]), int(b[-1]))
+    """(positiveBin, negativeBin, logLoss, total) summed over ranks: one numpy bincount over 2 * BINS slots
+    (positive rows in the first half); the all-reduce only runs under a process group."""
+    p = np.asarray(pos_p, dtype=np.float64)
+    lbl = np.asarray(is_pos, dtype=bool)
+    B = DETAIL_BIN_NUMBER
+    idx = np.where(p == 1.0, B - 1, np.floor(p * B))
+    ok = (idx >= 0) & (idx < B)
+    slot = idx[ok].astype(np.int64) + np.where(lbl[ok], 0, B)
+    return _reduce_bins(np.bincount(slot, minlength=2 * B).astype(np.float64), ll, keep, dev)
+
+
+def _reduce_bins(bins2, ll, keep, dev):
+    B = DETAIL_BIN_NUMBER
+    buf = np.zeros(2 * B + 2, dtype=np.float64)
+    buf[:2 * B] = bins2
+    buf[-2:] = (ll, float(keep))
+    if comm.is_distributed():
+        t = torch.from_numpy(buf).to(dev)
+        comm.all_reduce(t, "sum")
+        buf = t.cpu().numpy()
+    return buf[:B].astype(np.int64), buf[B:2 * B].astype(np.int64), float(buf[-2]), int(buf[-1])
 
 
 def multi_summary_from_detail(labels_col, details, label_array: List[str], device=None):

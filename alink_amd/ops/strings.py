@@ -77,6 +77,21 @@ def hash_bytes(block: StringBlock, seed: int = 0) -> torch.Tensor:
     return torch.from_numpy(h)
 
 
+_PREFIX_CACHE: dict = {}
+
+
+def _device_prefix(pu: np.ndarray, prefix: str, dev) -> torch.Tensor:
+    """The UTF-16 prefix on the device, uploaded once per (prefix, device): a stream's FeatureHasher hashes the
+    same column prefixes every micro-batch (was one host-to-device copy per column per batch)."""
+    key = (prefix, str(dev))
+    t = _PREFIX_CACHE.get(key)
+    if t is None:
+        if len(_PREFIX_CACHE) > 4096:
+            _PREFIX_CACHE.clear()
+        t = _PREFIX_CACHE[key] = torch.from_numpy(pu).to(dev)
+    return t
+
+
 def murmur3_utf8_index(block: StringBlock, nf: int, prefix: str = "", seed: int = 0) -> torch.Tensor:
     """int64 [n] ``floorMod(abs(murmur3_32(seed).hashUnencodedChars(prefix + s)), nf)`` on the block's device."""
     n = len(block)
@@ -88,7 +103,7 @@ def murmur3_utf8_index(block: StringBlock, nf: int, prefix: str = "", seed: int 
     if dev.type == "cuda":
         L = _lib.require()
         data = block.data if block.nbytes else torch.zeros(1, dtype=torch.uint8, device=dev)
-        p = torch.from_numpy(pu).to(dev)
+        p = _device_prefix(pu, prefix, dev)
         out = torch.empty(n, dtype=torch.int32, device=dev)
         rc = L.alink_murmur3_utf8_index(data.data_ptr(), block.offsets.contiguous().data_ptr(), n, p.data_ptr(),
                                         plen, seed & 0xFFFFFFFF, int(nf), None, out.data_ptr(), _lib.stream_ptr(dev))

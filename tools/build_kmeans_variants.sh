@@ -4,7 +4,8 @@
 #   pk       : one v_pk_add_f32 per row (accumulate body "pk")
 #   pair     : -DKM10_PAIRMAX=1 (both distance tiles of a pair in one MFMA stage loop)
 #   pkpair   : pk + pair
-#   dot2     : -DKM10_ACC_B32=1 + body "dot2" (ds_read_b32 + 2 v_dot2_f32_bf16 per row)
+#   d16      : -DKM10_ACC_B32=0 (two ds_read_u16_d16_hi + two v_add_f32 per row; the default before round 4)
+#   dot2     : -DKM10_ACC_B32=1 + body "dot2" (ds_read_b32 + 2 v_dot2_f32_bf16 per row; the default now)
 #   dot2pair : dot2 + pair
 set -e
 cd "$(dirname "$0")/.."
@@ -20,8 +21,9 @@ build_var() {
   objs=$(ls build/hip/*.o | grep -v kmeans_v10)
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "variants/libalink_hip_$name.so" $objs "$d/kmeans_v10.o"
 }
-build_var pk pk ""
-build_var pair base "-DKM10_PAIRMAX=1"
-build_var pkpair pk "-DKM10_PAIRMAX=1"
+build_var d16 base "-DKM10_ACC_B32=0"
+build_var pk pk "-DKM10_ACC_B32=0"
+build_var pair base "-DKM10_ACC_B32=0 -DKM10_PAIRMAX=1"
+build_var pkpair pk "-DKM10_ACC_B32=0 -DKM10_PAIRMAX=1"
 build_var dot2 dot2 "-DKM10_ACC_B32=1"
 build_var dot2pair dot2 "-DKM10_ACC_B32=1 -DKM10_PAIRMAX=1"
