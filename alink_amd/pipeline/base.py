@@ -236,18 +236,18 @@ class MapModel(ModelBase):
         from ..operator.batch.source import TableSourceBatchOp
         from ..operator.batch.utils import ModelMapBatchOp
         return ModelMapBatchOp(self.getParams(), mapper=self.MAPPER).linkFrom(
-            TableSourceBatchOp(self.modelData), input)
+            TableSourceBatchOp(self.getModelData()), input)
 
     def transformStream(self, input):
         from ..operator.batch.source import TableSourceBatchOp
         from ..operator.stream.base import ModelMapStreamOp
-        return ModelMapStreamOp(TableSourceBatchOp(self.modelData), self.getParams(),
+        return ModelMapStreamOp(TableSourceBatchOp(self.getModelData()), self.getParams(),
                                 mapper=self.MAPPER).linkFrom(input)
 
     def getLocalPredictor(self, inputSchema):
         if isinstance(inputSchema, str):
             inputSchema = schema_str_to_schema(inputSchema)
-        full = gather_table(self.modelData)
+        full = gather_table(self.getModelData())
         m = self.MAPPER(full.schema, inputSchema, self.getParams())
         m.loadModel(full.rows())
         m.open()

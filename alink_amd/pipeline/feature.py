@@ -29,6 +29,39 @@ for _n, _mapper in (("StandardScaler", S.StandardScalerModelMapper), ("MinMaxSca
 _stage("OneHotEncoderModel", MapModel, MAPPER=E.OneHotModelMapper)
 _stage("OneHotEncoder", Trainer, TRAIN_OP=F.OneHotTrainBatchOp, MODEL="OneHotEncoderModel")
 _stage("IndexToString", MapModel, MAPPER=E.IndexToStringModelMapper)
+
+# StringIndexerModel.registeredModel: a model fitted with ``modelName`` is found by name from IndexToString
+# (reference pipeline/dataproc/StringIndexerModel.java:20-50, IndexToString.java:66-72)
+_REGISTERED_STRING_INDEXERS: dict = {}
+
+
+def _model_name(stage):
+    p = stage.getParams()
+    try:
+        return p.get("modelName") if p.contains("modelName") else None
+    except KeyError:
+        return None
+
+
+def _register_string_indexer(self, data):
+    MapModel.setModelData(self, data)
+    name = _model_name(self)
+    if name is not None:
+        _REGISTERED_STRING_INDEXERS[name] = self
+    return self
+
+
+def _index_to_string_model_data(self):
+    if self.modelData is None:
+        name = _model_name(self)
+        if name not in _REGISTERED_STRING_INDEXERS:
+            raise ValueError(f"Can't find StringIndexerModel with name: {name}")
+        self.setModelData(_REGISTERED_STRING_INDEXERS[name].getModelData())
+    return self.modelData
+
+
+StringIndexerModel.setModelData = _register_string_indexer          # noqa: F821 (defined by _stage)
+IndexToString.getModelData = _index_to_string_model_data            # noqa: F821
 _stage("Binarizer", MapTransformer, MAPPER=E.BinarizerMapper)
 _stage("Bucketizer", MapTransformer, MAPPER=E.BucketizerMapper)
 _stage("FeatureHasher", MapTransformer, MAPPER=E.FeatureHasherMapper)

@@ -180,3 +180,50 @@ def test_fm_classifier_regressor_pipeline():
     rows = fm(A.FmRegressor).fit(data).transform(data).select(["pred", "details"]).collect()
     for pred, det in rows:
         assert det == '{"label":%f}' % pred
+
+
+# ---- pipeline/dataproc/{StringIndexerTest, IndexToStringTest, MultiStringIndexerTest} ----
+SPORTS = [("football",), ("football",), ("football",), ("basketball",), ("basketball",), ("tennis",)]
+
+
+@pytest.mark.parametrize("order,tokens", [("frequency_asc", ["tennis", "basketball", "football"]),
+                                          ("alphabet_desc", ["tennis", "football", "basketball"])])
+def test_string_indexer_orders(order, tokens):
+    data = MemSourceBatchOp(SPORTS, ["f0"])
+    rows = A.StringIndexer().setSelectedCol("f0").setOutputCol("f0_indexed").setStringOrderType(order).fit(data) \
+        .transform(data).collect()
+    assert all(r[1] == tokens.index(r[0]) for r in rows)
+
+
+def test_string_indexer_random_and_index_to_string_by_model_name():
+    data = MemSourceBatchOp(SPORTS, ["f0"])
+    model = A.StringIndexer().setSelectedCol("f0").setOutputCol("f0_indexed").setStringOrderType("random").fit(data)
+    assert len(A.BatchOperator.fromTable(model.getModelData()).collect()) == 3
+    indexed = A.StringIndexer().setModelName("string_indexer_model").setSelectedCol("f0").setOutputCol("f0_indexed") \
+        .setStringOrderType("frequency_asc").fit(data).transform(data)
+    back = A.IndexToString().setModelName("string_indexer_model").setSelectedCol("f0_indexed") \
+        .setOutputCol("f0_indxed_unindexed").transform(indexed).collect()
+    assert all(r[0] == r[2] for r in back) and len(back) == 6
+    with pytest.raises(ValueError):
+        A.IndexToString().setModelName("no_such_model").setSelectedCol("f0_indexed").setOutputCol("x") \
+            .transform(indexed).collect()
+
+
+def test_multi_string_indexer_reference():
+    rows = [("a", 1), (None, 1), ("b", 1), ("b", 3)]
+    map1 = {"a": 1, "b": 0, None: None}
+    map2 = {1: 0, 3: 1}
+    data = MemSourceBatchOp(rows, "f0 string, f1 bigint")
+    out = A.MultiStringIndexer().setSelectedCols(["f0", "f1"]).setOutputCols(["f0_index", "f1_index"]) \
+        .setHandleInvalid("skip").setStringOrderType("frequency_desc").fit(data).transform(data)
+    assert len(out.getColNames()) == 4
+    res = out.collect()
+    assert len(res) == 4
+    assert all(r[2] == map1[r[0]] and r[3] == map2[r[1]] for r in res)
+    train = A.MultiStringIndexerTrainBatchOp().setSelectedCols(["f1", "f0"]).setStringOrderType("frequency_desc") \
+        .linkFrom(data)
+    pred = A.MultiStringIndexerPredictBatchOp().setSelectedCols(["f0"]).setReservedCols(["f0"]) \
+        .setOutputCols(["f0_index"]).setHandleInvalid("skip").linkFrom(train, data)
+    assert pred.getColNames() == ["f0", "f0_index"]
+    res = pred.collect()
+    assert len(res) == 4 and all(r[1] == map1[r[0]] for r in res)
