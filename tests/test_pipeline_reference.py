@@ -227,3 +227,53 @@ def test_multi_string_indexer_reference():
     assert pred.getColNames() == ["f0", "f0_index"]
     res = pred.collect()
     assert len(res) == 4 and all(r[1] == map1[r[0]] for r in res)
+
+
+# ---- pipeline/dataproc/{ImputerTest, MinMaxScalerTest, StandardScalerTest, MaxAbsScalerTest} ----
+MIXED_SCHEMA = "id string, f_string string, f_long bigint, f_int int, f_double double, f_boolean boolean"
+MIXED = [("0", "a", 1, 1, 2.0, True), ("1", None, 2, 2, -3.0, True), ("2", "c", None, None, 2.0, False),
+         ("3", "a", 0, 0, None, None)]
+
+
+def _batch_and_stream(model, rows, schema):
+    batch = {r[0]: tuple(r) for r in model.transform(MemSourceBatchOp(rows, schema)).collect()}
+    out = []
+    model.transform(MemSourceStreamOp(rows, schema)).collect_to(out)
+    A.StreamOperator.execute()
+    assert {r[0]: tuple(r) for r in out} == batch
+    return batch
+
+
+def test_imputer_value_strategy_reference():
+    model = A.Imputer().setSelectedCols(["f_double", "f_long", "f_int"]).setStrategy("value").setFillValue("1") \
+        .fit(MemSourceBatchOp(MIXED, MIXED_SCHEMA))
+    got = _batch_and_stream(model, MIXED, MIXED_SCHEMA)
+    expect = {"0": (1, 1, 2.0), "1": (2, 2, -3.0), "2": (1, 1, 2.0), "3": (0, 0, 1.0)}
+    assert {k: v[2:5] for k, v in got.items()} == expect
+
+
+def test_min_max_scaler_reference():
+    cols = ["f_long", "f_int", "f_double"]
+    model = A.MinMaxScaler().setSelectedCols(cols).setOutputCols(cols).fit(MemSourceBatchOp(MIXED, MIXED_SCHEMA))
+    got = _batch_and_stream(model, MIXED, MIXED_SCHEMA)
+    expect = {"0": (0.5, 0.5, 1.0), "1": (1.0, 1.0, 0.0), "2": (None, None, 1.0), "3": (0.0, 0.0, None)}
+    assert {k: v[2:5] for k, v in got.items()} == expect
+
+
+def test_standard_scaler_reference():
+    rows = [("0", "a", 1, 1, 0.2, True), ("1", None, 2, 2, None, True), ("2", "c", None, None, None, False),
+            ("3", "a", 0, 0, None, None)]
+    model = A.StandardScaler().setSelectedCols(["f_long", "f_int", "f_double"]).setWithMean(True).setWithStd(True) \
+        .fit(MemSourceBatchOp(rows, MIXED_SCHEMA))
+    got = _batch_and_stream(model, rows, MIXED_SCHEMA)
+    expect = {"0": (0.0, 0.0, 0.0), "1": (1.0, 1.0, None), "2": (None, None, None), "3": (-1.0, -1.0, None)}
+    assert {k: v[2:5] for k, v in got.items()} == expect
+
+
+def test_max_abs_scaler_reference():
+    rows = [("0", 1.0, 2.0), ("1", -1.0, -3.0), ("2", 4.0, 2.0), ("3", None, None)]
+    schema = "id string, f0 double, f1 double"
+    model = A.MaxAbsScaler().setSelectedCols(["f0", "f1"]).fit(MemSourceBatchOp(rows, schema))
+    got = _batch_and_stream(model, rows, schema)
+    assert {k: v[1:] for k, v in got.items()} == {"0": (0.25, 0.6666666666666666), "1": (-0.25, -1.0),
+                                                 "2": (1.0, 0.6666666666666666), "3": (None, None)}
