@@ -277,3 +277,62 @@ def test_max_abs_scaler_reference():
     got = _batch_and_stream(model, rows, schema)
     assert {k: v[1:] for k, v in got.items()} == {"0": (0.25, 0.6666666666666666), "1": (-0.25, -1.0),
                                                  "2": (1.0, 0.6666666666666666), "3": (None, None)}
+
+
+# ---- pipeline/dataproc/vector/*Test ----
+VEC_ROWS = [("0", "$6$1:2.0 2:3.0 5:4.3", "3.0 2.0 3.0", "1 4 6 8", "$6$1:2.0 2:3.0 5:4.3"),
+            ("1", "$8$1:2.0 2:3.0 7:4.3", "3.0 2.0 3.0", "1 4 6 8", "$6$1:2.0 2:3.0 5:4.3"),
+            ("2", "$8$1:2.0 2:3.0 7:4.3", "2.0 3.0", "1 4 6 8", "$6$1:2.0 2:3.0 5:4.3")]
+VEC_COLS = ["id", "c0", "c1", "c2", "c3"]
+
+
+def _vec_out(stage):
+    from alink_amd.common.linalg import VectorUtil
+    rows = stage.transform(MemSourceBatchOp(VEC_ROWS, VEC_COLS)).collect()
+    out = []
+    stage.transform(MemSourceStreamOp(VEC_ROWS, VEC_COLS)).collect_to(out)
+    A.StreamOperator.execute()
+    assert [str(r[-1]) for r in out] == [str(r[-1]) for r in rows]
+    return {r[0]: VectorUtil.getVector(r[-1]) if isinstance(r[-1], str) else r[-1] for r in rows}
+
+
+def _vec(s):
+    from alink_amd.common.linalg import VectorUtil
+    return VectorUtil.getVector(s)
+
+
+@pytest.mark.parametrize("stage,expect", [
+    (lambda: A.VectorAssembler().setSelectedCols(["c0", "c1", "c2"]).setOutputCol("table2vec"),
+     {"0": "0.0 2.0 3.0 0.0 0.0 4.3 3.0 2.0 3.0 1.0 4.0 6.0 8.0",
+      "1": "$15$1:2.0 2:3.0 7:4.3 8:3.0 9:2.0 10:3.0 11:1.0 12:4.0 13:6.0 14:8.0",
+      "2": "$14$1:2.0 2:3.0 7:4.3 8:2.0 9:3.0 10:1.0 11:4.0 12:6.0 13:8.0"}),
+    (lambda: A.VectorElementwiseProduct().setSelectedCol("c1").setScalingVector("3.0 2.0 3.0")
+     .setOutputCol("product_result"), {"0": "9.0 4.0 9.0", "1": "9.0 4.0 9.0", "2": "6.0 6.0"}),
+    (lambda: A.VectorInteraction().setSelectedCols(["c0", "c3"]).setOutputCol("product_result"),
+     {"0": "$36$7:4.0 8:6.0 11:8.6 13:6.0 14:9.0 17:12.899999999999999 31:8.6 32:12.899999999999999 35:18.49",
+      "1": "$48$9:4.0 10:6.0 15:8.6 17:6.0 18:9.0 23:12.899999999999999 41:8.6 42:12.899999999999999 47:18.49",
+      "2": "$48$9:4.0 10:6.0 15:8.6 17:6.0 18:9.0 23:12.899999999999999 41:8.6 42:12.899999999999999 47:18.49"}),
+    (lambda: A.VectorNormalizer().setP(2.0).setOutputCol("pm").setSelectedCol("c0"),
+     {"0": "$6$1:0.35640489924669927 2:0.5346073488700489 5:0.7662705333804034",
+      "1": "$8$1:0.35640489924669927 2:0.5346073488700489 7:0.7662705333804034",
+      "2": "$8$1:0.35640489924669927 2:0.5346073488700489 7:0.7662705333804034"}),
+    (lambda: A.VectorPolynomialExpand().setDegree(2).setOutputCol("outv").setSelectedCol("c1"),
+     {"0": "3.0 9.0 2.0 6.0 4.0 3.0 9.0 6.0 9.0", "1": "3.0 9.0 2.0 6.0 4.0 3.0 9.0 6.0 9.0",
+      "2": "2.0 4.0 3.0 6.0 9.0"})], ids=["assembler", "elementwise", "interaction", "normalize", "poly"])
+def test_vector_transformers_reference(stage, expect):
+    got = _vec_out(stage())
+    assert {k: str(v) for k, v in got.items()} == {k: str(_vec(v)) for k, v in expect.items()}
+    assert all(type(got[k]) is type(_vec(v)) for k, v in expect.items())
+
+
+def test_vector_imputer_and_min_max_reference():
+    rows = [("0", "1, 3, NaN"), ("1", "0:-1.0 1:-3.0"), ("2", "0:4.0 1:2.0")]
+    data = MemSourceBatchOp(rows, ["id", "vec"])
+    got = {r[0]: str(r[1]) for r in A.VectorImputer().setSelectedCol("vec").setStrategy("value").setFillValue(-7.0)
+           .fit(data).transform(data).collect()}
+    assert got == {"0": str(_vec("1.0 3.0 -7.0")), "1": str(_vec("0:-1.0 1:-3.0")), "2": str(_vec("0:4.0 1:2.0"))}
+    rows = [("0", "1.0 2.0"), ("1", "-1.0 -3.0"), ("2", "4.0 2.0")]
+    data = MemSourceBatchOp(rows, ["id", "vec"])
+    got = {r[0]: str(r[1]) for r in A.VectorMinMaxScaler().setSelectedCol("vec").setMax(2).setMin(-3).fit(data)
+           .transform(data).collect()}
+    assert got == {"0": "-1.0 2.0", "1": "-3.0 -3.0", "2": "2.0 2.0"}
