@@ -312,6 +312,13 @@ def _make_setter(info: ParamInfo):
     def setter(self, *values):
         if len(values) == 1:
             v = values[0]
+        elif info.name == "cutsArray" and len(values) == 2:
+            # BucketizerParams.setCutsArray(double[] flatCuts, int[] lengths): consecutive runs per column
+            flat, lens = list(values[0]), [int(x) for x in values[1]]
+            if sum(lens) != len(flat):
+                raise ValueError("cutsArray lengths do not add up to the number of cuts")
+            starts = [sum(lens[:i]) for i in range(len(lens))]
+            v = [flat[a:a + n] for a, n in zip(starts, lens)]
         elif isinstance(info.value_type, list):
             v = list(values)
         else:

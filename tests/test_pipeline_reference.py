@@ -336,3 +336,86 @@ def test_vector_imputer_and_min_max_reference():
     got = {r[0]: str(r[1]) for r in A.VectorMinMaxScaler().setSelectedCol("vec").setMax(2).setMin(-3).fit(data)
            .transform(data).collect()}
     assert got == {"0": "-1.0 2.0", "1": "-3.0 -3.0", "2": "2.0 2.0"}
+
+
+# ---- pipeline/feature/*Test, pipeline/nlp/*Test ----
+def test_binarizer_bucketizer_feature_hasher_reference():
+    rows = [(1.218, 16.0, "1.560 -0.605"), (2.949, 4.0, "0.346 2.158"), (3.627, 2.0, "1.380 0.231"),
+            (0.273, 15.0, "0.520 1.151"), (4.199, 7.0, "0.795 -0.226")]
+    data = MemSourceBatchOp(rows, ["label", "censor", "features"])
+    got = A.Binarizer().setSelectedCol("censor").setThreshold(8.0).transform(data).select(["censor"]).collect()
+    assert [r[0] for r in got] == [1.0, 0.0, 0.0, 1.0, 0.0]
+
+    cuts = [[-0.5, 0.0, 0.5], [-0.3, 0.0, 0.3, 0.4]]
+    data = MemSourceBatchOp([(-999.9, -999.9), (-0.5, -0.2), (-0.3, -0.1), (0.0, 0.0), (0.2, 0.4), (999.9, 999.9)],
+                            ["features1", "features2"])
+    op = A.Bucketizer().setSelectedCols(["features1", "features2"]).setOutputCols(["bucket1", "bucket2"]) \
+        .setCutsArray(cuts)
+    assert [r[0] for r in op.transform(data).select(["bucket1"]).collect()] == [0, 0, 1, 1, 2, 3]
+    flat = A.Bucketizer().setCutsArray([-0.5, 0.0, 0.5, -0.3, 0.0, 0.3, 0.4], [3, 4])
+    assert flat.getParams().get("cutsArray") == cuts
+
+    data = MemSourceBatchOp([(1.1, True, "2", "A"), (1.1, False, "2", "B"), (1.1, True, "1", "B"), (2.2, True, "1", "A")],
+                            "double double, bool boolean, number string, str string")
+    got = A.FeatureHasher().setSelectedCols(["double", "bool", "number", "str"]).setNumFeatures(100) \
+        .setOutputCol("features").transform(data).select(["features"]).collect()
+    assert [str(r[0]) for r in got] == ["$100$9:1.0 38:1.1 45:1.0 95:1.0", "$100$9:1.0 30:1.0 38:1.1 76:1.0",
+                                        "$100$11:1.0 38:1.1 76:1.0 95:1.0", "$100$11:1.0 38:2.2 45:1.0 95:1.0"]
+
+
+def test_one_hot_reference_sizes():
+    from alink_amd.common.linalg import VectorUtil
+    rows = [("0", "doc0", "天", 4), ("1", "doc0", "地", 5), ("2", "doc0", "人", 1), ("3", "doc1", None, 3),
+            ("4", None, "人", 2), ("5", "doc1", "合", 4), ("6", "doc1", "一", 4), ("7", "doc2", "清", 3),
+            ("8", "doc2", "一", 2), ("9", "doc2", "色", 2)]
+    schema = "id string, docid string, word string, cnt bigint"
+    pred = [("0", "doc0", "天", 4), ("1", "doc2", None, 3)]
+    model = A.Pipeline().add(A.OneHotEncoder().setSelectedCols(["docid", "word", "cnt"]).setOutputCols(["results"])
+                             .setDropLast(False)) \
+        .add(A.VectorAssembler().setSelectedCols(["cnt", "results"]).setOutputCol("outN")) \
+        .fit(MemSourceBatchOp(rows, schema))
+    got = model.transform(MemSourceBatchOp(pred, schema)).select(["docid", "outN"]).collect()
+    assert [VectorUtil.getVector(str(r[1])).size() for r in got] == [19, 19]
+    train = A.OneHotTrainBatchOp().setSelectedCols(["docid", "word", "cnt"]).linkFrom(MemSourceBatchOp(rows, schema))
+    got = A.OneHotPredictBatchOp().setOutputCols(["results"]).setDropLast(False) \
+        .linkFrom(train, MemSourceBatchOp(pred, schema)).collect()
+    assert [VectorUtil.getVector(str(r[4])).size() for r in got] == [18, 18]
+
+
+def test_text_transformers_reference():
+    data = MemSourceBatchOp([(0, "That is an English book", 1), (1, "Have a good day", 1)], ["id", "sentence", "label"])
+    model = A.Pipeline().add(A.DocCountVectorizer().setSelectedCol("sentence").setOutputCol("features")
+                             .setFeatureType("TF")).fit(data)
+    vecs = [r[0] for r in model.transform(data).select(["features"]).collect()]
+    assert [len(v.getValues()) for v in vecs] == [5, 4]
+    assert all(abs(x - 0.2) < 0.1 for x in vecs[0].getValues())
+    assert all(abs(x - 0.25) < 0.1 for x in vecs[1].getValues())
+
+    data = MemSourceBatchOp([(0, "a b c d a a", 1), (1, "c c b a e", 1)], ["id", "sentence", "label"])
+    got = A.DocHashCountVectorizer().setSelectedCol("sentence").setNumFeatures(10).setOutputCol("res").fit(data) \
+        .transform(data).select(["res"]).collect()
+    assert [str(r[0]) for r in got] == ["$10$3:1.0 4:3.0 5:1.0 7:1.0", "$10$4:1.0 5:2.0 6:1.0 7:1.0"]
+
+    def one(stage, text, col):
+        return stage.transform(MemSourceBatchOp([(0, text)], ["id", "sentence"])).select([col]).collect()[0][0]
+    assert one(A.NGram().setSelectedCol("sentence"), "a a b b c c a", "sentence") == "a_a a_b b_b b_c c_c c_a"
+    assert one(A.RegexTokenizer().setSelectedCol("sentence").setGaps(False).setMinTokenLength(2).setToLowerCase(True)
+               .setOutputCol("token").setPattern("\\w+"), "Hello this is a good book!", "token") == \
+        "hello this is good book"
+    assert one(A.StopWordsRemover().setSelectedCol("sentence").setOutputCol("output"), "This is a good book",
+               "output") == "good book"
+    assert one(A.Tokenizer().setSelectedCol("sentence").setOutputCol("token"), "Hello this is a good book",
+               "token") == "hello this is a good book"
+
+
+def test_word2vec_and_pca_pipelines_reference():
+    src = MemSourceBatchOp([(0, "老王 是 我们 团队 里 最胖 的"), (1, "老黄 是 第二 胖 的"), (2, "胖"), (3, "胖 胖 胖")],
+                           "docid bigint, content string")
+    assert len(A.Word2Vec().setSelectedCol("content").setOutputCol("output").setMinCount(1).fit(src).transform(src)
+               .collect()) == 4
+    src = MemSourceBatchOp([(1, "0.1 0.2 0.3 0.4"), (2, "0.2 0.1 0.2 0.6"), (3, "0.2 0.3 0.5 0.4"),
+                            (4, "0.3 0.1 0.3 0.7"), (5, "0.4 0.2 0.4 0.4")], ["id", "vec"])
+    pred = A.PCA().setK(3).setCalculationType("CORR").setPredictionCol("pred").setReservedCols(["id"]) \
+        .setVectorCol("vec").fit(src).transform(src)
+    summary = A.VectorSummarizerBatchOp().setSelectedCol("pred").linkFrom(pred).collectVectorSummary()
+    assert abs(summary.sum().get(0)) == pytest.approx(4.840575043553453, abs=1e-3)

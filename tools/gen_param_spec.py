@@ -139,7 +139,12 @@ def main():
                 if mm and tok and not tok.startswith(("private", "public", "final")):
                     members.append(mm.group(1))
             if members:
-                enums.setdefault(m.group(1), members)
+                # the simple name belongs to a top-level enum (its own file) over a nested one of the same name
+                # (nlp FeatureType vs FeatureMeta.FeatureType)
+                if fname == m.group(1):
+                    enums[m.group(1)] = members
+                else:
+                    enums.setdefault(m.group(1), members)
                 enums[fname + "." + m.group(1)] = members
         # interfaces
         im = re.search(r"public\s+interface\s+(\w+)\s*(?:<[^{]*?>)?\s*(?:extends\s+([^{]*))?\{", src)
