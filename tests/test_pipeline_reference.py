@@ -419,3 +419,72 @@ def test_word2vec_and_pca_pipelines_reference():
         .setVectorCol("vec").fit(src).transform(src)
     summary = A.VectorSummarizerBatchOp().setSelectedCol("pred").linkFrom(pred).collectVectorSummary()
     assert abs(summary.sum().get(0)) == pytest.approx(4.840575043553453, abs=1e-3)
+
+
+# ---- pipeline/{PipelineTest, ModelSaveAndLoadTest} ----
+def _counting_stages():
+    from alink_amd.pipeline.base import EstimatorBase, ModelBase, TransformerBase
+    calls = {}
+
+    class T(TransformerBase):
+        def __init__(self, name):
+            super().__init__()
+            self.name = name
+
+        def transform(self, input):
+            calls[self.name] = calls.get(self.name, 0) + 1
+            return input
+
+    class M(ModelBase):
+        def __init__(self, name):
+            super().__init__()
+            self.name = name
+
+        def transform(self, input):
+            calls["model_" + self.name] = calls.get("model_" + self.name, 0) + 1
+            return input
+
+    class E(EstimatorBase):
+        def __init__(self, name):
+            super().__init__()
+            self.name = name
+
+        def fit(self, input):
+            calls["fit_" + self.name] = calls.get("fit_" + self.name, 0) + 1
+            return M(self.name)
+    return calls, T, E
+
+
+def test_pipeline_fit_transforms_only_up_to_last_estimator():
+    """PipelineTest.testFit / testFitWithoutEstimators: stages before the last estimator transform once, the last
+    estimator is fitted but its model never transforms, later transformers are untouched."""
+    calls, T, E = _counting_stages()
+    data = MemSourceBatchOp([(1,)], ["colName"])
+    A.Pipeline().add(T("s1")).add(T("s2")).add(E("s3")).add(T("s4")).add(E("s5")).add(T("s6")).fit(data)
+    assert calls == {"s1": 1, "s2": 1, "fit_s3": 1, "model_s3": 1, "s4": 1, "fit_s5": 1}
+    calls, T, E = _counting_stages()
+    A.Pipeline().add(T("s1")).add(T("s2")).add(T("s3")).add(T("s4")).fit(data)
+    assert calls == {}
+
+
+def _mlp_pipeline():
+    va = A.VectorAssembler().setSelectedCols(FEATS).setOutputCol("features")
+    mlp = A.MultilayerPerceptronClassifier().setVectorCol("features").setLabelCol("category").setLayers([4, 5, 3]) \
+        .setMaxIter(100).setPredictionCol("pred_label").setPredictionDetailCol("pred_detail") \
+        .setReservedCols(["category"])
+    return A.Pipeline().add(va).add(mlp)
+
+
+def test_pipeline_model_save_and_load(tmp_path):
+    src, _ = _iris()
+    path = str(tmp_path / "pipeline_model.csv")
+    _mlp_pipeline().fit(src).save(path)
+    A.BatchOperator.execute()
+    model = A.PipelineModel.load(path)
+    assert model.transform(src).count() == 150
+    row = model.getLocalPredictor(src.getSchema()).map((4.8, 3.4, 1.9, 0.2, "Iris-setosa"))
+    assert len(row) == 3 and row[0] == "Iris-setosa" and row[1] == "Iris-setosa"
+    # save -> load -> save round trip, and a pipeline nested in a pipeline
+    again = A.PipelineModel.load(_mlp_pipeline().fit(src).save()).save()
+    assert again.count() > 3
+    assert A.PipelineModel.load(A.Pipeline().add(_mlp_pipeline()).fit(src).save()).transform(src).count() == 150
