@@ -488,3 +488,53 @@ def test_pipeline_model_save_and_load(tmp_path):
     again = A.PipelineModel.load(_mlp_pipeline().fit(src).save()).save()
     assert again.count() > 3
     assert A.PipelineModel.load(A.Pipeline().add(_mlp_pipeline()).fit(src).save()).transform(src).count() == 150
+
+
+# ---- pipeline/clustering/{KMeansTest, BisectingKMeansTest, GaussianMixtureTest} ----
+SIX = [("0 0 0",), ("0.1 0.1 0.1",), ("0.2 0.2 0.2",), ("9 9 9",), ("9.1 9.1 9.1",), ("9.2 9.2 9.2",)]
+
+
+def test_kmeans_pipeline_distances_reference():
+    data = MemSourceBatchOp(SIX, ["vector"])
+    model = A.Pipeline().add(A.KMeans().setVectorCol("vector").setPredictionCol("pred")
+                             .setPredictionDistanceCol("distance").setK(2)).fit(data)
+    got = [r[0] for r in model.transform(data).select(["distance"]).collect()]
+    assert got == pytest.approx([0.173, 0, 0.173, 0.173, 0, 0.173], abs=0.01)
+
+
+def test_bisecting_kmeans_pipeline_reference():
+    """BisectingKMeansTest: the reference expects [0, 0, 0, 1, 2, 2]; the two 3-point groups have the same cost up
+    to rounding (0.06 vs 0.06 - 5e-14 here), so which one is bisected depends on the summation order -- Flink's
+    partial aggregates in the reference.  Checked: the groups separate and exactly one is split in two; iris
+    ARI / NMI / RI as the reference's."""
+    data = MemSourceBatchOp(SIX, ["vector"])
+    model = A.Pipeline().add(A.BisectingKMeans().setVectorCol("vector").setPredictionCol("pred").setK(3)
+                             .setMaxIter(10)).fit(data)
+    pred = [r[0] for r in model.transform(data).select(["pred"]).collect()]
+    low, high = set(pred[:3]), set(pred[3:])
+    assert not low & high and sorted([len(low), len(high)]) == [1, 2] and set(pred) == {0, 1, 2}
+
+    src, _ = _iris()
+    va = A.VectorAssembler().setSelectedCols(FEATS).setReservedCols(["category"]).setOutputCol("features")
+    bk = A.BisectingKMeans().setK(3).setMaxIter(100).setVectorCol("features").setReservedCols(["category"]) \
+        .setPredictionCol("pred")
+    m = A.EvalClusterBatchOp().setPredictionCol("pred").setLabelCol("category") \
+        .linkFrom(A.Pipeline().add(va).add(bk).fit(src).transform(src)).collectMetrics()
+    assert m.getAri() == pytest.approx(0.68, abs=0.01)
+    assert m.getNmi() == pytest.approx(0.69, abs=0.01)
+    assert m.getRi() == pytest.approx(0.85, abs=0.01)
+
+
+def test_gaussian_mixture_univariate_reference():
+    import json
+    xs = ["-5.1971", "-2.5359", "-3.8220", "-5.2211", "-5.0602", "4.7118", "6.8989", "3.4592", "4.6322", "5.7048",
+          "4.6567", "5.5026", "4.5605", "5.2043", "6.2734"]
+    model = A.GaussianMixture().setPredictionCol("cluster_id").setPredictionDetailCol("cluster_detail") \
+        .setVectorCol("x").setTol(0.).fit(MemSourceBatchOp([(x,) for x in xs], ["x"]))
+    rows = A.BatchOperator.fromTable(model.getModelData()).collect()
+    clusters = sorted((json.loads(r[1]) for r in rows if r[0] > 0), key=lambda c: c["weight"])
+    expect = [(1.0 / 3.0, -4.3673, 1.1098), (2.0 / 3.0, 5.1604, 0.86644)]
+    for c, (w, mean, cov) in zip(clusters, expect):
+        assert c["weight"] == pytest.approx(w, abs=1e-2)
+        assert c["mean"]["data"][0] == pytest.approx(mean, abs=1e-2)
+        assert c["cov"]["data"][0] == pytest.approx(cov, abs=1e-2)
