@@ -1,6 +1,9 @@
 #!/usr/bin/env python3
 """Summarise a rocprofv3 SQLite output (``*_results.db``) as a per-kernel stats table (calls, total/avg/min/max
-µs, % of GPU time).  Usage: python tools/rocpd_stats.py DB [--top N] [--match SUBSTR]"""
+µs, % of GPU time).  Usage: python tools/rocpd_stats.py DB [--top N] [--match SUBSTR] [--timeline ANCHOR]
+
+--timeline ANCHOR prints, for the last two launches of the kernel whose name contains ANCHOR, every kernel in
+between with its start offset and duration (one superstep of an iterative job, launch gaps included)."""
 import argparse
 import sqlite3
 
@@ -10,6 +13,7 @@ def main():
     ap.add_argument("db")
     ap.add_argument("--top", type=int, default=25)
     ap.add_argument("--match", default=None)
+    ap.add_argument("--timeline", default=None)
     a = ap.parse_args()
     c = sqlite3.connect(a.db)
     cols = [r[1] for r in c.execute("pragma table_info(kernels)")]
@@ -23,6 +27,15 @@ def main():
             continue
         print(f"{r[1]:6d} {r[2]/1e3:11.1f} {r[3]/1e3:10.2f} {r[4]/1e3:10.2f} {r[5]/1e3:10.2f} {100*r[2]/total:6.2f}  {r[0][:110]}")
     print(f"total GPU kernel time: {total/1e6:.3f} ms over {sum(r[1] for r in rows)} dispatches")
+    if a.timeline:
+        ks = c.execute(f"select {name}, start, end from kernels order by start").fetchall()
+        anchors = [i for i, k in enumerate(ks) if a.timeline in k[0]]
+        if len(anchors) >= 2:
+            i0, i1 = anchors[-2], anchors[-1]
+            t0 = ks[i0][1]
+            print(f"\ntimeline between the last two '{a.timeline}' launches (offset_us, dur_us, kernel):")
+            for k in ks[i0:i1 + 1]:
+                print(f"  {(k[1] - t0) / 1e3:10.1f} {(k[2] - k[1]) / 1e3:9.1f}  {k[0][:100]}")
 
 
 if __name__ == "__main__":
