@@ -10,7 +10,10 @@ beta = 1.01 for ``em`` and 1/K for ``online``; ``em`` keeps the ``(V + 1) x K`` 
 of the corpus, optionally re-estimating alpha by Newton steps (``UpdateLambdaAndAlpha``); the document E-step
 iterates ``gamma_d = alpha + e^{E log theta_d} * (sum_w c_w / phinorm_w e^{E log beta_w})`` until the mean
 change is below 1e-3 (``LdaUtil.getTopicDistributionMethod``); the model meta records alphaArray,
-betaArray, topicNum, vocabularySize, method, logLikelihood and logPerplexity (= -LL / #tokens).
+betaArray, topicNum, vocabularySize, method, logLikelihood and logPerplexity as the reference defines them: for
+``em`` the token log-likelihood over -LL / vocabularySize (``EmLogLikelihood``, ``BuildEmLdaModel``), for
+``online`` the variational bound (``online_log_likelihood``) over -LL / the last mini-batch's token count
+(``OnlineLogLikelihood``, ``BuildOnlineLdaModel``).
 
 Differences: the Gibbs sampler includes the document-topic factor ``(n_dk + alpha)`` of collapsed LDA (the
 reference's ``EmCorpusStep`` samples from the word factor only), and sweeps all tokens of a rank in
@@ -99,6 +102,38 @@ def e_step(doc, word, cts, n_docs, expElogbeta_T, alpha, gamma0, max_iter=100, t
     return gamma, et, phinorm
 
 
+def online_log_likelihood(gamma, doc, word, cts, lam, alpha, beta, task_num: int = 1) -> float:
+    """The online-LDA variational bound of ``OnlineLogLikelihood.logLikelihood`` (reference
+    A/operator/common/clustering/lda/OnlineLogLikelihood.java:33-70) for documents whose E-step gammas are
+    ``gamma`` [D, K] (tokens: ``doc``/``word``/``cts``; ``lam`` [K, V] topic-word Dirichlet, ``alpha`` [K]):
+      sum_d [ sum_w c_dw logsumexp_k(E[log theta_dk] + E[log beta_kw]) + sum_k (alpha_k - gamma_dk) E[log theta_dk]
+              + sum_k (lgamma(gamma_dk) - lgamma(alpha_k)) + lgamma(sum alpha) - lgamma(sum_k gamma_dk) ]
+      + ( sum (beta - lam) E[log beta] + sum (lgamma(lam) - lgamma(beta)) - sum_k (lgamma(sum_v lam_kv)
+          - lgamma(beta V)) ) / task_num
+    Every rank passes its own documents; the caller sums the returned parts over ranks (each adds 1/task_num of
+    the topics part, as the reference's tasks do).  Documents without tokens are skipped (the reference's
+    corpus holds none)."""
+    K, V = lam.shape
+    elog_beta = _dir_exp(lam)                                         # [K, V]
+    has = torch.zeros(gamma.shape[0], dtype=torch.bool, device=gamma.device)
+    if doc.numel():
+        has[doc] = True
+    g = gamma[has]
+    elog_theta_all = _dir_exp(gamma)
+    corpus = 0.0
+    if doc.numel():
+        tok = torch.logsumexp(elog_theta_all[doc] + elog_beta.T[word], dim=1)
+        corpus += float((cts * tok).sum())
+    if g.shape[0]:
+        et = elog_theta_all[has]
+        corpus += float(((alpha[None, :] - g) * et).sum())
+        corpus += float((torch.lgamma(g) - torch.lgamma(alpha)[None, :]).sum())
+        corpus += float(g.shape[0] * torch.lgamma(alpha.sum()) - torch.lgamma(g.sum(1)).sum())
+    topics = float(((beta - lam) * elog_beta).sum() + (torch.lgamma(lam) - math.lgamma(beta)).sum()
+                   - (torch.lgamma(lam.sum(1)) - math.lgamma(beta * V)).sum())
+    return corpus + topics / task_num
+
+
 def _online(doc, word, cts, n_docs, V, K, params, alpha0, eta, seed, dev):
     num_iter = int(_pget(params, "numIter", 10))
     tau0 = float(_pget(params, "onlineLearningOffset", 1024.0))
@@ -124,10 +159,11 @@ def _online(doc, word, cts, n_docs, V, K, params, alpha0, eta, seed, dev):
         stat = torch.zeros((V, K), dtype=torch.float64, device=dev)
         stat.index_add_(0, w_b, et[d_b] * (c_b / phinorm)[:, None])
         logphat = (_dir_exp(gamma)).sum(0) if nb else torch.zeros(K, dtype=torch.float64, device=dev)
-        buf = torch.cat([stat.reshape(-1), logphat, torch.tensor([float(nb)], dtype=torch.float64, device=dev)])
+        buf = torch.cat([stat.reshape(-1), logphat,
+                         torch.tensor([float(nb), float(c_b.sum()) if nb else 0.0], dtype=torch.float64, device=dev)])
         comm.all_reduce(buf, "sum")
         stat = buf[:V * K].reshape(V, K).T * expElogbeta
-        logphat, B = buf[V * K:V * K + K], float(buf[-1])
+        logphat, B, last_words = buf[V * K:V * K + K], float(buf[-2]), float(buf[-1])
         rho = (tau0 + t) ** (-kappa)
         if B > 0:
             lam = (1 - rho) * lam + rho * (eta + (total_docs / B) * stat)
@@ -140,7 +176,7 @@ def _online(doc, word, cts, n_docs, V, K, params, alpha0, eta, seed, dev):
                 dalpha = -(gradf - b) / q
                 if bool((rho * dalpha + alpha > 0).all()):
                     alpha = alpha + rho * dalpha
-    return lam, alpha
+    return lam, alpha, (last_words if num_iter >= 1 else 0.0)
 
 
 def _gibbs(doc, word, cts, n_docs, V, K, params, alpha, beta, seed, dev):
@@ -195,11 +231,10 @@ def train_lda(mt: MTable, params: Params, env) -> List[tuple]:
     doc, word, cts, n_docs = _corpus(mt, col, vocab, dev)
     alpha = float(_pget(params, "alpha", -1.0))
     beta = float(_pget(params, "beta", -1.0))
-    n_tokens = float(sum(comm.all_gather_object(float(cts.sum()))))
     if method == "online":
         alpha = 1.0 / K if alpha == -1 else alpha
         beta = 1.0 / K if beta == -1 else beta
-        lam, alpha_vec = _online(doc, word, cts, n_docs, V, K, params, alpha, beta, seed, dev)
+        lam, alpha_vec, last_words = _online(doc, word, cts, n_docs, V, K, params, alpha, beta, seed, dev)
         topic = lam / lam.sum(1, keepdim=True)
         matrix = DenseMatrix(lam.cpu().numpy())                      # K x V
         alphas = alpha_vec.cpu().numpy().tolist()
@@ -217,11 +252,22 @@ def train_lda(mt: MTable, params: Params, env) -> List[tuple]:
         topic = ((nw + beta) / (nw.sum(0) + V * beta)[None, :]).T     # K x V
         theta = (nd + alpha) / (nd + alpha).sum(1, keepdim=True)
         m_name = "em"
-    probs = (theta[doc] * topic.T[word]).sum(1) if doc.numel() else torch.zeros(0, dtype=torch.float64, device=dev)
-    ll = torch.tensor([float((cts * torch.log(probs)).sum()) if doc.numel() else 0.0], dtype=torch.float64)
+    if m_name == "online":
+        # the variational bound (OnlineLogLikelihood) over -LL / the last step's sampled token count
+        # (BuildOnlineLdaModel.java:66-70)
+        part = online_log_likelihood(gamma, doc, word, cts, lam, alpha_vec, beta, comm.get_world_size())
+        denom = max(round(last_words), 1)
+    else:
+        # EmLogLikelihood: sum over tokens of log(theta_d . phi_w), over -LL / vocabularySize
+        # (BuildEmLdaModel.java:54-55)
+        probs = (theta[doc] * topic.T[word]).sum(1) if doc.numel() else \
+            torch.zeros(0, dtype=torch.float64, device=dev)
+        part = float((cts * torch.log(probs)).sum()) if doc.numel() else 0.0
+        denom = max(V, 1)
+    ll = torch.tensor([part], dtype=torch.float64)
     comm.all_reduce(ll, "sum")
     ll = float(ll[0])
-    meta = Params().set("logPerplexity", -ll / max(n_tokens, 1.0)).set("betaArray", [beta] * K) \
+    meta = Params().set("logPerplexity", -ll / denom).set("betaArray", [beta] * K) \
         .set("logLikelihood", ll).set("method", m_name).set("alphaArray", alphas).set("topicNum", K) \
         .set("vocabularySize", V)
     data = [gson_dumps(matrix, java_map_order=False)] + vocab_list
