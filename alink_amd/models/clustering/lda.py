@@ -134,6 +134,29 @@ def online_log_likelihood(gamma, doc, word, cts, lam, alpha, beta, task_num: int
     return corpus + topics / task_num
 
 
+def update_lambda_alpha(lam, alpha, batch, logphat, n_docs_batch: float, t: int, tau0: float, kappa: float,
+                        eta: float, rate: float, optimize_alpha: bool):
+    """One online step (reference ``UpdateLambdaAndAlpha.calculateLambdaAndAlpha``):
+    ``lambda <- (1 - rho) lambda + rho (eta + batch / subSamplingRate)`` with ``rho = (tau0 + t)^-kappa`` and
+    ``batch`` = the mini-batch's word-topic statistics times exp(E[log beta]) of the old lambda; then a Newton
+    step on alpha from the batch's summed E[log theta] (``logphat``), kept only if every component stays > 0."""
+    rho = (tau0 + t) ** (-kappa)
+    if n_docs_batch <= 0:
+        return lam, alpha
+    lam = (1 - rho) * lam + rho * (eta + batch / rate)
+    if optimize_alpha:
+        B = n_docs_batch
+        lp = logphat / B
+        gradf = B * (-torch.digamma(alpha) + torch.digamma(alpha.sum()) + lp)
+        c = B * torch.polygamma(1, alpha.sum())
+        q = -B * torch.polygamma(1, alpha)
+        b = (gradf / q).sum() / (1.0 / c + (1.0 / q).sum())
+        dalpha = -(gradf - b) / q
+        if bool((rho * dalpha + alpha > 0).all()):
+            alpha = alpha + rho * dalpha
+    return lam, alpha
+
+
 def _online(doc, word, cts, n_docs, V, K, params, alpha0, eta, seed, dev):
     num_iter = int(_pget(params, "numIter", 10))
     tau0 = float(_pget(params, "onlineLearningOffset", 1024.0))
@@ -142,8 +165,8 @@ def _online(doc, word, cts, n_docs, V, K, params, alpha0, eta, seed, dev):
     opt_alpha = bool(_pget(params, "optimizeDocConcentration", True))
     lam = torch.from_numpy(np.random.default_rng(seed).gamma(100.0, 1.0 / 100.0, size=(K, V))).to(dev)
     alpha = torch.full((K,), alpha0, dtype=torch.float64, device=dev)
-    total_docs = sum(comm.all_gather_object(int(n_docs)))
     rng = np.random.default_rng(seed + 7919 * comm.get_rank())
+    last_words = 0.0
     for t in range(1, num_iter + 1):
         pick = rng.random(n_docs) < rate
         if not pick.any() and n_docs:
@@ -164,19 +187,8 @@ def _online(doc, word, cts, n_docs, V, K, params, alpha0, eta, seed, dev):
         comm.all_reduce(buf, "sum")
         stat = buf[:V * K].reshape(V, K).T * expElogbeta
         logphat, B, last_words = buf[V * K:V * K + K], float(buf[-2]), float(buf[-1])
-        rho = (tau0 + t) ** (-kappa)
-        if B > 0:
-            lam = (1 - rho) * lam + rho * (eta + (total_docs / B) * stat)
-            if opt_alpha:
-                lp = logphat / B
-                gradf = B * (-torch.digamma(alpha) + torch.digamma(alpha.sum()) + lp)
-                c = B * torch.polygamma(1, alpha.sum())
-                q = -B * torch.polygamma(1, alpha)
-                b = (gradf / q).sum() / (1.0 / c + (1.0 / q).sum())
-                dalpha = -(gradf - b) / q
-                if bool((rho * dalpha + alpha > 0).all()):
-                    alpha = alpha + rho * dalpha
-    return lam, alpha, (last_words if num_iter >= 1 else 0.0)
+        lam, alpha = update_lambda_alpha(lam, alpha, stat, logphat, B, t, tau0, kappa, eta, rate, opt_alpha)
+    return lam, alpha, last_words
 
 
 def _gibbs(doc, word, cts, n_docs, V, K, params, alpha, beta, seed, dev):

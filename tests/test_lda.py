@@ -44,36 +44,39 @@ def test_lda_doc_corpus(method):
     assert len(m.transform(src).collect()) == 12
 
 
+# OnlineLogLikelihoodTest / UpdateLambdaAndAlphaTest data: 12 documents over 11 words, lambda [5 x 11]
+LL_DOCS = ["0:1 1:2 2:6 3:0 4:2 5:3 6:1 7:1 8:0 9:0 10:3", "0:1 1:3 2:0 3:1 4:3 5:0 6:0 7:2 8:0 9:0 10:1",
+        "0:1 1:4 2:1 3:0 4:0 5:4 6:9 7:0 8:1 9:2 10:0", "0:2 1:1 2:0 3:3 4:0 5:0 6:5 7:0 8:2 9:3 10:9",
+        "0:3 1:1 2:1 3:9 4:3 5:0 6:2 7:0 8:0 9:1 10:3", "0:4 1:2 2:0 3:3 4:4 5:5 6:1 7:1 8:1 9:4 10:0",
+        "0:2 1:1 2:0 3:3 4:0 5:0 6:5 7:0 8:2 9:2 10:9", "0:1 1:1 2:1 3:9 4:2 5:1 6:2 7:0 8:0 9:1 10:3",
+        "0:4 1:4 2:0 3:3 4:4 5:2 6:1 7:3 8:0 9:0 10:0", "0:2 1:8 2:2 3:0 4:3 5:0 6:2 7:0 8:2 9:7 10:2",
+        "0:1 1:1 2:1 3:9 4:0 5:2 6:2 7:0 8:0 9:3 10:3", "0:4 1:1 2:0 3:0 4:4 5:5 6:1 7:3 8:0 9:1 10:0"]
+LL_LAMBDA = [0.8936825549031158, 0.9650683744577933, 1.1760851442955271, 0.889011463028263, 1.0355502890838704,
+        1.1720254142865503, 0.8496512959061578, 1.1564109073902848, 0.8528198328651976, 1.072261907065107,
+        1.0112487630821958, 1.0288027427394206, 1.1256918577237478, 1.0641131417250107, 0.9830788207753957,
+        0.9519235842178695, 1.0531103642783968, 1.0846663792488604, 0.9317316401779444, 0.9816247167440154,
+        0.953061129524052, 0.8836097897537777, 0.8539728772760822, 1.109432137460693, 0.9801693423689286,
+        0.9385725168762017, 1.009886079821316, 0.9741390218380398, 0.8734624459614093, 0.8548583255850564,
+        0.8934120594879987, 1.0200469492393616, 0.9461610896051537, 1.1912819895664948, 0.9650275833536232,
+        0.9312815665885328, 0.984681817963758, 1.1412711858668625, 1.1159082714127344, 1.0219124026668207,
+        1.1052645047308647, 1.1380919062139254, 0.9684793634316371, 1.023922805813918, 1.0777999541431174,
+        0.8730213177341947, 1.0353598060502658, 1.047104264664753, 1.1284793487722498, 0.8898021261569816,
+        1.1634869627283706, 0.817874601150865, 1.0424867867765728, 1.167773175905418, 0.915224402643435]
+
+
 def test_online_log_likelihood_reference_value():
     """OnlineLogLikelihoodTest.testCalc: 12 documents over 11 words, lambda [5 x 11], alpha 0.2..0.6, beta 0.2, one
     task; the reference warm-starts every document's E-step from the previous document's gamma (first from
     0.7..1.1) and gets -833.0890905595685 (asserted to 1e-3)."""
     import torch
     from alink_amd.models.clustering.lda import e_step, online_log_likelihood, _dir_exp
-    docs = ["0:1 1:2 2:6 3:0 4:2 5:3 6:1 7:1 8:0 9:0 10:3", "0:1 1:3 2:0 3:1 4:3 5:0 6:0 7:2 8:0 9:0 10:1",
-            "0:1 1:4 2:1 3:0 4:0 5:4 6:9 7:0 8:1 9:2 10:0", "0:2 1:1 2:0 3:3 4:0 5:0 6:5 7:0 8:2 9:3 10:9",
-            "0:3 1:1 2:1 3:9 4:3 5:0 6:2 7:0 8:0 9:1 10:3", "0:4 1:2 2:0 3:3 4:4 5:5 6:1 7:1 8:1 9:4 10:0",
-            "0:2 1:1 2:0 3:3 4:0 5:0 6:5 7:0 8:2 9:2 10:9", "0:1 1:1 2:1 3:9 4:2 5:1 6:2 7:0 8:0 9:1 10:3",
-            "0:4 1:4 2:0 3:3 4:4 5:2 6:1 7:3 8:0 9:0 10:0", "0:2 1:8 2:2 3:0 4:3 5:0 6:2 7:0 8:2 9:7 10:2",
-            "0:1 1:1 2:1 3:9 4:0 5:2 6:2 7:0 8:0 9:3 10:3", "0:4 1:1 2:0 3:0 4:4 5:5 6:1 7:3 8:0 9:1 10:0"]
-    temp = [0.8936825549031158, 0.9650683744577933, 1.1760851442955271, 0.889011463028263, 1.0355502890838704,
-            1.1720254142865503, 0.8496512959061578, 1.1564109073902848, 0.8528198328651976, 1.072261907065107,
-            1.0112487630821958, 1.0288027427394206, 1.1256918577237478, 1.0641131417250107, 0.9830788207753957,
-            0.9519235842178695, 1.0531103642783968, 1.0846663792488604, 0.9317316401779444, 0.9816247167440154,
-            0.953061129524052, 0.8836097897537777, 0.8539728772760822, 1.109432137460693, 0.9801693423689286,
-            0.9385725168762017, 1.009886079821316, 0.9741390218380398, 0.8734624459614093, 0.8548583255850564,
-            0.8934120594879987, 1.0200469492393616, 0.9461610896051537, 1.1912819895664948, 0.9650275833536232,
-            0.9312815665885328, 0.984681817963758, 1.1412711858668625, 1.1159082714127344, 1.0219124026668207,
-            1.1052645047308647, 1.1380919062139254, 0.9684793634316371, 1.023922805813918, 1.0777999541431174,
-            0.8730213177341947, 1.0353598060502658, 1.047104264664753, 1.1284793487722498, 0.8898021261569816,
-            1.1634869627283706, 0.817874601150865, 1.0424867867765728, 1.167773175905418, 0.915224402643435]
     f64 = torch.float64
-    lam = torch.tensor(temp, dtype=f64).reshape(5, 11)        # DenseMatrix(11, 5, colMajor).transpose()
+    lam = torch.tensor(LL_LAMBDA, dtype=f64).reshape(5, 11)        # DenseMatrix(11, 5, colMajor).transpose()
     alpha = torch.tensor([0.2, 0.3, 0.4, 0.5, 0.6], dtype=f64)
     eb_T = torch.exp(_dir_exp(lam)).T
     gamma = torch.tensor([[0.7, 0.8, 0.9, 1.0, 1.1]], dtype=f64)
     rows, D, W, C = [], [], [], []
-    for d, s in enumerate(docs):
+    for d, s in enumerate(LL_DOCS):
         pairs = [(int(a), float(b)) for a, b in (t.split(":") for t in s.split()) if float(b) != 0.0]
         w = torch.tensor([p[0] for p in pairs])
         c = torch.tensor([p[1] for p in pairs], dtype=f64)
@@ -84,3 +87,29 @@ def test_online_log_likelihood_reference_value():
         C.append(c)
     ll = online_log_likelihood(torch.stack(rows), torch.tensor(D), torch.cat(W), torch.cat(C), lam, alpha, 0.2, 1)
     assert ll == pytest.approx(-833.0890905595685, abs=1e-3)
+
+
+def test_update_lambda_and_alpha_reference_value():
+    """UpdateLambdaAndAlphaTest.calcTest: the corpus step over the 12 documents (E-steps warm-started from the
+    previous document's gamma, first 0.7..1.1), then one lambda / alpha update with t = 1, tau0 1024, kappa 0.51,
+    eta 0.2, subsampling 1, alpha optimised: lambda[1][1] = 1.101515812903741, alpha[1] = 0.29431646104704223."""
+    import torch
+    from alink_amd.models.clustering.lda import e_step, update_lambda_alpha, _dir_exp
+    f64 = torch.float64
+    lam = torch.tensor(LL_LAMBDA, dtype=f64).reshape(5, 11)
+    alpha = torch.tensor([0.2, 0.3, 0.4, 0.5, 0.6], dtype=f64)
+    ebeta = torch.exp(_dir_exp(lam))
+    gamma = torch.tensor([[0.7, 0.8, 0.9, 1.0, 1.1]], dtype=f64)
+    stat = torch.zeros(5, 11, dtype=f64)
+    logphat = torch.zeros(5, dtype=f64)
+    for s in LL_DOCS:
+        pairs = [(int(a), float(b)) for a, b in (t.split(":") for t in s.split()) if float(b) != 0.0]
+        w = torch.tensor([p[0] for p in pairs])
+        c = torch.tensor([p[1] for p in pairs], dtype=f64)
+        gamma, et, phinorm = e_step(torch.zeros(len(pairs), dtype=torch.long), w, c, 1, ebeta.T, alpha, gamma,
+                                    max_iter=10000)
+        stat[:, w] += et[0][:, None] * (c / phinorm)[None, :]
+        logphat += _dir_exp(gamma)[0]
+    lam2, alpha2 = update_lambda_alpha(lam, alpha, stat * ebeta, logphat, 12, 1, 1024.0, 0.51, 0.2, 1.0, True)
+    assert float(lam2[1, 1]) == pytest.approx(1.101515812903741, abs=1e-3)
+    assert float(alpha2[1]) == pytest.approx(0.29431646104704223, abs=1e-3)
