@@ -411,27 +411,28 @@ class AftRegObjFunc(OptimObjFunc):
         return torch.ones_like(data.w)
 
     def _parts(self, data, coef):
-        beta = coef[:-1]
+        # x . coef over the vector's own length (AftRegObjFunc.getDotProduct): training vectors have d - 1
+        # entries, so log(sigma) stays out of the product
         log_sigma = coef[-1]
         sigma = torch.exp(log_sigma)
-        eps = (data.y - data.X.mv(beta)) / sigma
-        return beta, log_sigma, sigma, eps
+        eps = (data.y - data.X.mv(coef)) / sigma
+        return log_sigma, sigma, eps
 
     def loss_per_sample(self, data, coef):
-        _, log_sigma, _, eps = self._parts(data, coef)
+        log_sigma, _, eps = self._parts(data, coef)
         return data.w * (log_sigma - eps) + torch.exp(eps)
 
     def grad_sum(self, data, coef):
-        _, _, sigma, eps = self._parts(data, coef)
+        d = coef.shape[0]
+        _, sigma, eps = self._parts(data, coef)
         mult = data.w - torch.exp(eps)
-        g = data.X.rmv(mult / sigma, coef.shape[0] - 1)
-        last = (data.w + mult * eps).sum()
-        return torch.cat([g, last.reshape(1)])
+        g = data.X.rmv(mult / sigma, d).clone()
+        g[d - 1] += (data.w + mult * eps).sum()
+        return g
 
     def hessian_sum(self, data, coef):
         d = coef.shape[0]
-        _, _, sigma, eps = self._parts(data, coef)
-        H = torch.zeros((d, d), dtype=coef.dtype, device=coef.device)
-        H[:d - 1, :d - 1] = data.X.gram(torch.exp(eps) / (sigma * sigma), d - 1)
-        H[d - 1, d - 1] = (eps * (torch.exp(eps) * (1 + eps) - data.w)).sum()
+        _, sigma, eps = self._parts(data, coef)
+        H = data.X.gram(torch.exp(eps) / (sigma * sigma), d).clone()
+        H[d - 1, d - 1] += (eps * (torch.exp(eps) * (1 + eps) - data.w)).sum()
         return H

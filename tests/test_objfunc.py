@@ -137,3 +137,44 @@ def test_unary_loss_function_properties():
         assert abs(f(lf.loss, 0.0, 0.0)) < 1e-10 and abs(f(lf.derivative, 0.0, 0.0)) < 1e-10, name
         assert f(lf.derivative, -0.5, 0.0) == -f(lf.derivative, 0.5, 0.0), name
         assert f(lf.second_derivative, -0.5, 0.0) == f(lf.second_derivative, 0.5, 0.0), name
+
+
+# ---- AftObjFuncTest: 100 samples of 10 entries (x_j = j + 0.01 i), censor 1, label 1; the vectors are as long
+# as the coefficients, so the dot product covers log(sigma) too (AftRegObjFunc.getDotProduct) ----
+def _aft_data():
+    rows = [[j + 0.01 * i for j in range(D)] for i in range(100)]
+    return _data(rows, [1.0] * 100, [1.0] * 100)
+
+
+def _aft(l1=0.1, l2=0.1):
+    from alink_amd.models.linear.objfunc import AftRegObjFunc
+    return AftRegObjFunc(l1=l1, l2=l2)
+
+
+AFT_COEF = torch.tensor([1.0 + 0.01 * i for i in range(D)], dtype=torch.float64)
+AFT_SEARCH = [1858.0906639, 1854.4931528, 1846.4415772, 1833.475521, 1815.0990642, 1790.7783532, 1759.9390144,
+              1721.9634027, 1676.1876744, 1621.8986742]
+
+
+def test_aft_search_values():
+    dirv = torch.full((D,), 0.1, dtype=torch.float64)
+    got = _aft().calc_search_values(_aft_data(), AFT_COEF, dirv, 0.5, 10)
+    np.testing.assert_allclose(np.round(got[:D].numpy(), 7), AFT_SEARCH, atol=1e-9)
+    got = _aft().constraint_calc_search_values(_aft_data(), AFT_COEF, dirv, 0.5, 10)
+    np.testing.assert_allclose(np.round(got[:D].numpy(), 7), AFT_SEARCH, atol=1e-9)
+
+
+def test_aft_objective_and_gradient():
+    f, _ = _aft().calc_obj_value(_aft_data(), AFT_COEF)
+    assert round(float(f), 7) == 20.7187566
+    g, _ = _aft().calc_gradient(_aft_data(), AFT_COEF)
+    expect = [0.4664272, 0.8046436, 1.1428601, 1.4810766, 1.8192931, 2.1575096, 2.495726, 2.8339425, 3.172159,
+              -12.9805304]
+    np.testing.assert_allclose(np.round(g.numpy(), 7), expect, atol=1e-9)
+
+
+def test_aft_hessian_diagonal():
+    H, _, _, _ = _aft(1e-2, 1e-2).calc_hessian_gradient_loss(_aft_data(), AFT_COEF)
+    expect = [2.0000000510094984, 2.000000737376146, 2.000002340193193, 2.00000485946064, 2.000008295178487,
+              2.0000126473467335, 2.0000179159653797, 2.000024101034426, 2.000031202553872, 1751.091754655224]
+    np.testing.assert_allclose(torch.diagonal(H).numpy(), expect, rtol=1e-12)
