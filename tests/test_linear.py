@@ -268,3 +268,27 @@ def test_regression_pipelines_reference_predictions(name, expect):
     got = {r[0]: tuple(r[1:]) for r in pl.fit(data).transform(data).select(["label", "p1", "p2", "p3"]).collect()}
     for label, e in expect.items():
         assert got[label] == pytest.approx(e, abs=1e-5), (label, got[label])
+
+
+def test_linear_model_mapper_reference_rows():
+    """LinearModelMapperTest: a new-format LR model table with an INT label column; prediction 1 for (1, 1, 0, 1),
+    output schema ``pred INT`` with reservedCols [] and the input columns + ``pred`` otherwise."""
+    from alink_amd.common.params import Params
+    from alink_amd.common.types import schema_str_to_schema
+    from alink_amd.models.linear.model import LinearModelMapper
+    rows = [(0, '{"hasInterceptItem":"true","modelName":"\\"Logistic Regression\\"","labelType":"4",'
+                '"modelSchema":"\\"model_id bigint,model_info string,label_type int\\"","isNewFormat":"true",'
+                '"linearModelType":"\\"LR\\""}', None),
+            (1048576, '{"featureColNames":["f0","f1","f2","f3"],"coefVector":{"data":[-9.634910228989458,'
+                      '45.508924427487486,-22.06146649207175,-20.926964828123506,45.508924427487486]}}', None),
+            (2147483647 * 1048576, None, 1), (2147483647 * 1048576 + 1, None, 0)]
+    ms = schema_str_to_schema("model_id bigint, model_info string, label_type int")
+    ds = schema_str_to_schema("f0 double, f1 double, f2 double, f3 double")
+    m = LinearModelMapper(ms, ds, Params().set("predictionCol", "pred").set("reservedCols", []))
+    m.loadModel(rows)
+    assert tuple(m.map((1.0, 1.0, 0.0, 1.0))) == (1,)
+    assert m.getOutputSchema().getFieldNames() == ["pred"] and str(m.getOutputSchema().getFieldTypes()[0]) == "INT"
+    m = LinearModelMapper(ms, ds, Params().set("predictionCol", "pred"))
+    m.loadModel(rows)
+    assert tuple(m.map((1.0, 1.0, 0.0, 1.0)))[4] == 1
+    assert m.getOutputSchema().getFieldNames() == ["f0", "f1", "f2", "f3", "pred"]
