@@ -117,6 +117,15 @@ class IsotonicRegressionConverter(SimpleModelDataConverter):
         return m
 
 
+def _meta_first(meta: Params, *names):
+    for n in names:
+        if meta.contains(n):
+            v = meta.get(n)
+            if v is not None:
+                return v
+    return None
+
+
 class IsotonicRegressionModelMapper(ModelMapper):
     """Binary search of the feature in the boundaries, linear interpolation between neighbours."""
 
@@ -129,8 +138,9 @@ class IsotonicRegressionModelMapper(ModelMapper):
     def loadModel(self, modelRows):
         self.m = IsotonicRegressionConverter().load(modelRows)
         meta = self.m.meta
-        self.vector_col = meta.get("vectorCol") if meta.contains("vectorCol") else None
-        self.feature_col = meta.get("featureCol") if meta.contains("featureCol") else None
+        # ParamInfo aliases of the reference meta (vectorColName / featureColName in older models)
+        self.vector_col = _meta_first(meta, "vectorCol", "vectorColName", "tensorColName", "vecColName")
+        self.feature_col = _meta_first(meta, "featureCol", "featureColName")
         self.index = int(meta.get("featureIndex")) if meta.contains("featureIndex") else 0
         self.b = np.asarray(self.m.boundaries, dtype=np.float64)
         self.v = np.asarray(self.m.values, dtype=np.float64)

@@ -104,3 +104,28 @@ def test_isotonic_antitonic_and_vector_input():
         .setIsotonic(False).linkFrom(src)
     vals = json.loads(sorted(model.collect(), key=lambda r: r[0])[2][1])
     assert all(a >= b for a, b in zip(vals, vals[1:]))
+
+
+ISO_META = ('{"vectorColName":%s,"modelName":"\\"IsotonicRegressionModel\\"","featureColName":%s,"featureIndex":"0",'
+            '"modelSchema":"\\"model_id bigint,model_info string\\"","isNewFormat":"true"}')
+ISO_ROWS = [(1048576, "[0.02,0.1,0.2,0.27,0.3,0.35,0.45,0.5,0.7,0.8,0.9]"),
+            (2097152, "[0.0,0.3333333333333333,0.3333333333333333,0.5,0.5,0.6666666666666666,0.6666666666666666,"
+                      "0.75,0.75,1.0,1.0]")]
+
+
+@pytest.mark.parametrize("vector", [False, True])
+def test_isotonic_mapper_reference_model_rows(vector):
+    """IsotonicRegressionModelMapperTest: model meta with the old ``featureColName`` / ``vectorColName`` keys
+    (aliases of featureCol / vectorCol); 0.35 -> 0.66, vector "0.81, 0.35" (index 0) -> 1.0.  (The reference
+    declares the vector column DOUBLE and feeds a string; here it is a string column.)"""
+    from alink_amd.common.params import Params
+    from alink_amd.common.types import schema_str_to_schema
+    from alink_amd.models.regression.isotonic import IsotonicRegressionModelMapper
+    meta = ISO_META % (('"\\"vector\\""', "null") if vector else ("null", '"\\"feature\\""'))
+    ms = schema_str_to_schema("model_id bigint, model_info string")
+    ds = schema_str_to_schema("vector string" if vector else "feature double")
+    m = IsotonicRegressionModelMapper(ms, ds, Params().set("predictionCol", "pred"))
+    m.loadModel([(0, meta)] + ISO_ROWS)
+    out = m.map(("0.81, 0.35",) if vector else (0.35,))
+    assert float(out[1]) == pytest.approx(1.0 if vector else 0.66, abs=0.01)
+    assert m.getOutputSchema().getFieldNames() == (["vector", "pred"] if vector else ["feature", "pred"])
