@@ -174,3 +174,18 @@ def test_kmeans_old_model_haversine():
     m.loadModel(rows)
     assert m.map((0.0, 0.0))[2] == 1
     assert m.getOutputSchema() == TableSchema(["f0", "f1", "pred"], [Types.DOUBLE, Types.DOUBLE, Types.LONG])
+
+
+def test_update_sum_matrix_reference():
+    """KMeansUtilTest.updateSumMatrix{,Sparse}Test: k=2 centroids (9.1, 9.1, 9.1) / (0.1, 0.1, 0.1); rows i * (1,1,1)
+    and the sparse rows with i^2 at index i % 3 (i < 10) give the [k][d + 1] sums + counts
+    [35,35,35,5, 10,10,10,5] and [117,65,89,6, 9,1,4,4]."""
+    import torch
+    from alink_amd.ops.kmeans import assign_accumulate_torch
+    C = torch.tensor([[9.1] * 3, [0.1] * 3], dtype=torch.float64)
+    X = torch.stack([torch.full((3,), float(i), dtype=torch.float64) for i in range(10)])
+    assert assign_accumulate_torch(X, C).flatten().tolist() == [35.0, 35.0, 35.0, 5.0, 10.0, 10.0, 10.0, 5.0]
+    X = torch.zeros(10, 3, dtype=torch.float64)
+    for i in range(10):
+        X[i, i % 3] = i * i
+    assert assign_accumulate_torch(X, C).flatten().tolist() == [117.0, 65.0, 89.0, 6.0, 9.0, 1.0, 4.0, 4.0]
