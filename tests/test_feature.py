@@ -171,3 +171,18 @@ def test_scaler_and_imputer_mappers_on_reference_model_rows():
                                   TableSchema(["f0", "f1"], [T.DOUBLE, T.DOUBLE]), Params())
     m.loadModel([(0, '{"selectedCols":"[\\"f0\\",\\"f1\\"]"}', None, None), (1048576, "[4.0,3.0]", None, None)])
     assert tuple(m.map((1.0, 2.0))) == pytest.approx((0.25, 0.6666666666666666))
+
+
+@pytest.mark.parametrize("selector,expect", [("NumTopFeatures", [0, 2]), ("PERCENTILE", [0, 2]),
+                                             ("FPR", [0, 1, 2, 3]), ("FDR", [0, 1, 2, 3, 4]), ("FWE", [0])])
+def test_chisq_selector_rules_reference(selector, expect):
+    """ChiSquareTestTest.testChiSqSelector*: five features with p-values 0.1, 0.3, 0.2, 0.4, 0.5; numTopFeatures 2,
+    percentile / fpr / fdr / fwe 0.5."""
+    from types import SimpleNamespace
+    from alink_amd.common.params import Params
+    from alink_amd.operator.batch.feature import _chisq_select
+    results = [SimpleNamespace(p=v) for v in (0.1, 0.3, 0.2, 0.4, 0.5)]
+    p = Params().set("selectorType", selector).set("numTopFeatures", 2).set("percentile", 0.5).set("fpr", 0.5) \
+        .set("fdr", 0.5).set("fwe", 0.5)
+    got = _chisq_select(results, p)
+    assert len(got) == len(expect) and got[:2] == expect[:2]
