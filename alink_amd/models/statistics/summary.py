@@ -38,6 +38,13 @@ def _fmt_table(names, rows):
     return format_rows(names, rows)
 
 
+class _Count(int):
+    """The row count: an int that can also be called, as the reference's ``count()`` method."""
+
+    def __call__(self) -> int:
+        return int(self)
+
+
 class TableSummary:
     """count / sum / squareSum / min / max / normL1 / numMissingValue of the selected columns (statistics for
     the numeric ones, counts for all) — ``TableSummary.java``; accessors take a column name."""
@@ -45,7 +52,7 @@ class TableSummary:
     def __init__(self, names, num_idx, count, s, s2, mn, mx, l1, nmv):
         self.colNames = list(names)
         self.numericalColIndices = list(num_idx)
-        self.count = int(count)
+        self.count = _Count(count)
         self._sum, self._s2, self._mn, self._mx, self._l1, self._nmv = s, s2, mn, mx, l1, nmv
 
     def _idx(self, col):
@@ -189,7 +196,7 @@ class VectorSummary:
 
     def __init__(self, count, sum_, sum2, mn, mx, l1, nnz, sparse: bool):
         self.count, self._sum, self._s2, self._mn, self._mx, self._l1, self._nnz = \
-            int(count), sum_, sum2, mn, mx, l1, nnz
+            _Count(count), sum_, sum2, mn, mx, l1, nnz
         self.sparse = sparse
 
     def vectorSize(self):

@@ -186,3 +186,20 @@ def test_chisq_selector_rules_reference(selector, expect):
         .set("fdr", 0.5).set("fwe", 0.5)
     got = _chisq_select(results, p)
     assert len(got) == len(expect) and got[:2] == expect[:2]
+
+
+def test_table_summary_reference():
+    """TableSummaryTest: 4 rows, 5 columns, f_double = 2, -3, 2, NULL."""
+    import alink_amd as A
+    from alink_amd.operator.batch.source import MemSourceBatchOp
+    d = MemSourceBatchOp([("a", 1, 1, 2.0, True), (None, 2, 2, -3.0, True), ("c", None, None, 2.0, False),
+                          ("a", 0, 0, None, None)],
+                         "f_string string, f_long bigint, f_int int, f_double double, f_boolean boolean")
+    s = A.SummarizerBatchOp().linkFrom(d).collectSummary()
+    assert len(s.colNames) == 5 and s.count() == 4 and s.count == 4
+    assert s.numMissingValue("f_double") == 1 and s.numValidValue("f_double") == 3
+    assert s.max("f_double") == 2.0 and s.min("f_int") == 0.0
+    assert s.mean("f_double") == pytest.approx(0.3333333333333333, abs=1e-3)
+    assert s.variance("f_double") == pytest.approx(8.333333333333334, abs=1e-3)
+    assert s.standardDeviation("f_double") == pytest.approx(2.886751345948129, abs=1e-3)
+    assert s.normL1("f_double") == pytest.approx(7.0) and s.normL2("f_double") == pytest.approx(4.123105625617661)
