@@ -209,36 +209,48 @@ class VectorSummary:
             return SparseVector(len(a), nz, a[nz])
         return DenseVector(a.copy())
 
-    def sum(self):
-        return self._vec(self._sum)
+    @property
+    def colNum(self) -> int:
+        return len(self._sum)
 
-    def mean(self):
-        return self._vec(self._sum / max(self.count, 1))
+    def _at(self, arr, idx):
+        # every statistic takes an optional column index, as the reference's max(int) / max() pair
+        return self._vec(arr) if idx is None else float(np.asarray(arr, dtype=np.float64)[idx])
 
-    def variance(self):
+    def sum(self, idx=None):
+        return self._at(self._sum, idx)
+
+    def mean(self, idx=None):
+        return self._at(self._sum / max(self.count, 1), idx)
+
+    def _variance(self):
         n = self.count
         if n <= 1:
-            return self._vec(np.zeros_like(self._sum))
-        return self._vec(np.maximum(0.0, (self._s2 - self._sum * self._sum / n) / (n - 1)))
+            return np.zeros_like(np.asarray(self._sum, dtype=np.float64))
+        return np.maximum(0.0, (self._s2 - self._sum * self._sum / n) / (n - 1))
 
-    def standardDeviation(self):
-        v = self.variance()
-        return self._vec(np.sqrt(v.toDenseVector().data if hasattr(v, "toDenseVector") else v.data))
+    def variance(self, idx=None):
+        return self._at(self._variance(), idx)
 
-    def min(self):
-        return self._vec(self._mn)
+    def standardDeviation(self, idx=None):
+        return self._at(np.sqrt(self._variance()), idx)
 
-    def max(self):
-        return self._vec(self._mx)
+    def min(self, idx=None):
+        return self._at(self._mn, idx)
 
-    def normL1(self):
-        return self._vec(self._l1)
+    def max(self, idx=None):
+        return self._at(self._mx, idx)
 
-    def normL2(self):
-        return self._vec(np.sqrt(self._s2))
+    def normL1(self, idx=None):
+        return self._at(self._l1, idx)
 
-    def numNonZero(self):
-        return self._vec(self._nnz)
+    def normL2(self, idx=None):
+        return self._at(np.sqrt(self._s2), idx)
+
+    def numNonZero(self, idx=None):
+        # a DenseVector for sparse summaries too (SparseVectorSummary.numNonZero)
+        a = np.asarray(self._nnz, dtype=np.float64)
+        return DenseVector(a.copy()) if idx is None else float(a[idx])
 
     def __str__(self):
         head = ["id", "count", "sum", "mean", "variance", "standardDeviation", "min", "max", "normL1", "normL2"]

@@ -203,3 +203,46 @@ def test_table_summary_reference():
     assert s.variance("f_double") == pytest.approx(8.333333333333334, abs=1e-3)
     assert s.standardDeviation("f_double") == pytest.approx(2.886751345948129, abs=1e-3)
     assert s.normL1("f_double") == pytest.approx(7.0) and s.normL2("f_double") == pytest.approx(4.123105625617661)
+
+
+def _vector_summary(rows):
+    import alink_amd as A
+    from alink_amd.operator.batch.source import MemSourceBatchOp
+    return A.VectorSummarizerBatchOp().setSelectedCol("v").linkFrom(MemSourceBatchOp([(r,) for r in rows], ["v"])) \
+        .collectVectorSummary()
+
+
+def _dense(v):
+    return list(v.toDenseVector().data) if hasattr(v, "toDenseVector") else list(v.data)
+
+
+def test_sparse_vector_summary_reference():
+    """SparseVectorSummaryTest: implicit zeros count in min / max / variance; numNonZero is dense."""
+    s = _vector_summary(["$5$0:1.0 1:-1.0 2:3.0", "$5$1:2.0 2:-2.0 3:3.0", "$5$2:3.0 3:-3.0 4:3.0",
+                         "$5$0:4.0 2:-4.0 3:3.0", "$5$0:5.0 1:-5.0 4:3.0"])
+    assert s.colNum == 5 and s.vectorSize() == 5
+    got = [s.max(1), s.min(1), s.sum(1), s.mean(1), s.variance(1), s.standardDeviation(1), s.normL1(1), s.normL2(1),
+           s.numNonZero(1)]
+    assert got == pytest.approx([2.0, -5.0, -4.0, -0.8, 6.7, 2.588436, 8.0, 5.477226, 3], abs=1e-3)
+    from alink_amd.common.linalg import DenseVector, SparseVector
+    assert isinstance(s.numNonZero(), DenseVector) and list(s.numNonZero().data) == [3.0, 3.0, 4.0, 3.0, 2.0]
+    assert isinstance(s.max(), SparseVector)
+    expect = {"max": [5.0, 2.0, 3.0, 3.0, 3.0], "min": [0.0, -5.0, -4.0, -3.0, 0.0], "sum": [10.0, -4.0, 0.0, 3.0, 6.0],
+              "mean": [2.0, -0.8, 0.0, 0.6, 1.2], "variance": [5.5, 6.7, 9.5, 6.3, 2.7],
+              "standardDeviation": [2.345208, 2.588436, 3.082207, 2.509980, 1.643168],
+              "normL1": [10, 8.0, 12.0, 9.0, 6.0], "normL2": [6.480741, 5.477226, 6.164414, 5.196152, 4.242641]}
+    for name, e in expect.items():
+        assert _dense(getattr(s, name)()) == pytest.approx(e, abs=1e-3), name
+
+
+def test_dense_vector_summary_reference():
+    """DenseVectorSummaryTest."""
+    s = _vector_summary(["1.0 -1.0 3.0", "2.0 -2.0 3.0", "3.0 -3.0 3.0", "4.0 -4.0 3.0", "5.0 -5.0 3.0"])
+    assert s.vectorSize() == 3 and s.count() == 5
+    got = [s.max(1), s.min(1), s.sum(1), s.mean(1), s.variance(1), s.standardDeviation(1), s.normL1(1), s.normL2(1)]
+    assert got == pytest.approx([-1.0, -5.0, -15.0, -3.0, 2.5, 1.5811, 15.0, 7.416198], abs=1e-3)
+    expect = {"max": [5.0, -1.0, 3.0], "min": [1.0, -5.0, 3.0], "sum": [15.0, -15.0, 15.0], "mean": [3.0, -3.0, 3.0],
+              "variance": [2.5, 2.5, 0.0], "standardDeviation": [1.5811, 1.5811, 0.0], "normL1": [15, 15, 15],
+              "normL2": [7.416198, 7.416198, 6.7082]}
+    for name, e in expect.items():
+        assert _dense(getattr(s, name)()) == pytest.approx(e, abs=1e-3), name
