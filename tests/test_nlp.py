@@ -152,3 +152,33 @@ def test_doc_word_split_count_table_function():
     out = MemSourceBatchOp([("a b c d a b c",)], "f0 string").udtf("f0", ["w", "cnt"], DocWordSplitCount(" "), []) \
         .collect()
     assert [tuple(r) for r in out] == [("a", 2), ("b", 2), ("c", 2), ("d", 1)]
+
+
+DCV_VOCAB = [("i", 0.6931471805599453, 6), ("e", 0.1823215567939546, 2), ("a", 0.4054651081081644, 0),
+             ("b", 0.1823215567939546, 1), ("c", 0.6931471805599453, 7), ("h", 0.4054651081081644, 3),
+             ("d", 0.6931471805599453, 4), ("j", 0.6931471805599453, 5), ("g", 0.6931471805599453, 8),
+             ("n", 1.0986122886681098, 9), ("f", 1.0986122886681098, 10)]
+
+
+@pytest.mark.parametrize("ftype,min_tf,text,expect", [
+    ("WORD_COUNT", "1.0", "a b c d e a a", "$11$0:3.0 1:1.0 2:1.0 4:1.0 7:1.0"),
+    ("TF_IDF", "1.0", "a b c d e", "$11$0:0.08109302162163289 1:0.03646431135879092 2:0.03646431135879092 "
+                                   "4:0.13862943611198905 7:0.13862943611198905"),
+    ("TF", "1.0", "a b c d e", "$11$0:0.2 1:0.2 2:0.2 4:0.2 7:0.2"),
+    ("BINARY", "0.2", "a b c d e a a b e", "$11$0:1.0 1:1.0 2:1.0"),
+    ("BINARY", "0.2", "a b c d", "$11$0:1.0 1:1.0 4:1.0 7:1.0")])
+def test_doc_count_vectorizer_mapper_reference(ftype, min_tf, text, expect):
+    """DocCountVectorizerModelMapperTest: the reference's 11-word model rows; minTF 0.2 keeps words with at least
+    20 % of the document's tokens."""
+    from alink_amd.common.params import Params
+    from alink_amd.common.types import schema_str_to_schema
+    from alink_amd.models.nlp.text import DocCountVectorizerModelMapper
+    rows = [(0, '{"minTF":"%s","featureType":"\\"%s\\""}' % (min_tf, ftype))] + \
+        [((i + 1) * 1048576, '{"f0":"%s","f1":%r,"f2":%d}' % v) for i, v in enumerate(DCV_VOCAB)]
+    p = Params().set("selectedCol", "sentence")
+    if ftype == "TF":
+        p.set("outputCol", "output")
+    m = DocCountVectorizerModelMapper(schema_str_to_schema("model_id bigint, model_info string"),
+                                      schema_str_to_schema("sentence string"), p)
+    m.loadModel(rows)
+    assert str(m.map((text,))[-1]) == expect
