@@ -3,6 +3,7 @@ doccountvectorizer,dochashcountvectorizer}*.md)."""
 import json
 
 import pandas as pd
+import pytest
 
 from alink_amd import *  # noqa: F401,F403
 from alink_amd.models.nlp.text import JiebaSegmenter, java_split
