@@ -183,3 +183,23 @@ def test_doc_count_vectorizer_mapper_reference(ftype, min_tf, text, expect):
                                       schema_str_to_schema("sentence string"), p)
     m.loadModel(rows)
     assert str(m.map((text,))[-1]) == expect
+
+
+@pytest.mark.parametrize("ftype,expect", [
+    ("TF_IDF", "$20$7:0.0 13:0.06757751801802739 14:-0.25541281188299536 15:-0.047947012075296815"),
+    ("WORD_COUNT", "$20$7:1.0 13:1.0 14:3.0 15:1.0"),
+    ("TF", "$20$7:0.16666666666666666 13:0.16666666666666666 14:0.5 15:0.16666666666666666"),
+    ("BINARY", "$20$7:1.0 13:1.0 14:1.0 15:1.0"),
+    ("IDF", "$20$7:0.0 13:0.4054651081081644 14:-0.5108256237659907 15:-0.2876820724517809")])
+def test_doc_hash_count_vectorizer_mapper_reference(ftype, expect):
+    """DocHashCountVectorizerModelMapperTest: 20 hash buckets, the reference's IDF row, text "a b c d a a "."""
+    from alink_amd.common.params import Params
+    from alink_amd.common.types import schema_str_to_schema
+    from alink_amd.models.nlp.text import DocHashCountVectorizerModelMapper
+    rows = [(0, '{"numFeatures":"20","minTF":"1.0","featureType":"\\"%s\\""}' % ftype),
+            (1048576, '{"16":0.4054651081081644,"7":0.0,"13":0.4054651081081644,"14":-0.5108256237659907,'
+                      '"15":-0.2876820724517809}')]
+    m = DocHashCountVectorizerModelMapper(schema_str_to_schema("model_id bigint, model_info string"),
+                                          schema_str_to_schema("sentence string"), Params().set("selectedCol", "sentence"))
+    m.loadModel(rows)
+    assert str(m.map(("a b c d a a ",))[0]) == expect
