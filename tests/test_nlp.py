@@ -203,3 +203,35 @@ def test_doc_hash_count_vectorizer_mapper_reference(ftype, expect):
                                           schema_str_to_schema("sentence string"), Params().set("selectedCol", "sentence"))
     m.loadModel(rows)
     assert str(m.map(("a b c d a a ",))[0]) == expect
+
+
+def _siso(cls, **params):
+    from alink_amd.common.params import Params
+    from alink_amd.common.types import schema_str_to_schema
+    p = Params().set("selectedCol", "sentence")
+    for k, v in params.items():
+        p.set(k, v)
+    return cls(schema_str_to_schema("sentence string"), p)
+
+
+def test_stop_words_remover_mapper_reference():
+    """StopWordsRemoverMapperTest: the bundled English / Chinese stop words plus "Test", case-insensitive by
+    default, case-sensitive on request."""
+    from alink_amd.models.nlp.text import StopWordsRemoverMapper
+    m = _siso(StopWordsRemoverMapper, stopWords=["Test"])
+    assert m.map(("This is a unit test for filtering stopWords",))[0] == "unit filtering stopWords"
+    assert m.map(("Filter stopWords test",))[0] == "Filter stopWords"
+    assert m.map(("这 是 停用词 过滤 的 单元 测试",))[0] == "停用词 过滤 单元 测试"
+    m = _siso(StopWordsRemoverMapper, caseSensitive=True, stopWords=["Test"])
+    assert m.map(("This is a unit test for filtering stopWords",))[0] == "This unit test filtering stopWords"
+    assert m.map(("Filter stopWords test",))[0] == "Filter stopWords test"
+
+
+@pytest.mark.parametrize("n,expect", [(None, "This_is is_a a_unit unit_test test_for for_mapper"),
+                                      (3, "This_is_a is_a_unit a_unit_test unit_test_for test_for_mapper"),
+                                      (10, "")])
+def test_ngram_mapper_reference(n, expect):
+    """NGramMapperTest."""
+    from alink_amd.models.nlp.text import NGramMapper
+    m = _siso(NGramMapper, **({} if n is None else {"n": n}))
+    assert m.map(("This is a unit test for mapper",))[0] == expect
