@@ -93,8 +93,19 @@ class WindowGroupByStreamOp(StreamOperator):
     def linkFrom(self, *inputs):
         (inp,) = self._connect(*inputs)
         self._in_schema = inp.getSchema()
-        self._schema = self._aggregate(_MTable.empty(self._in_schema)).schema
+        self._schema = self._windowed(_MTable.empty(self._in_schema), 0.0, 0.0).schema
         return self
+
+    def _windowed(self, rows_mt, start: float, end: float):
+        """The aggregate of one window plus its ``window_start`` / ``window_end`` TIMESTAMP columns (the
+        reference's ``CAST(TUMBLE_START(...) AS TIMESTAMP(3))`` pair, WindowGroupByStreamOp.java:80-82)."""
+        import datetime as _dt
+        from ...common.types import Types as _T
+        agg = self._aggregate(rows_mt)
+        n = agg.num_rows
+        ts = [_dt.datetime.fromtimestamp(round(start, 3)), _dt.datetime.fromtimestamp(round(end, 3))]
+        return agg.with_columns(["window_start", "window_end"], [_T.TIMESTAMP, _T.TIMESTAMP],
+                                [_Column.from_values([v] * n, _T.TIMESTAMP) for v in ts])
 
     def _aggregate(self, mt):
         by = self.getGroupByClause()
@@ -132,7 +143,8 @@ class WindowGroupByStreamOp(StreamOperator):
             else:
                 sessions.append(cur)
             for s in sessions:
-                self._emit(self._aggregate(_MTable.from_rows([r for _, r in s], self._in_schema)))
+                self._emit(self._windowed(_MTable.from_rows([r for _, r in s], self._in_schema), s[0][0],
+                                          s[-1][0] + gap))
             self._pending = keep
             return
         buckets = {}
@@ -142,7 +154,7 @@ class WindowGroupByStreamOp(StreamOperator):
         remaining = {}
         for w in sorted(buckets):
             if final or w[1] <= self._watermark:
-                self._emit(self._aggregate(_MTable.from_rows([r for _, r in buckets[w]], self._in_schema)))
+                self._emit(self._windowed(_MTable.from_rows([r for _, r in buckets[w]], self._in_schema), w[0], w[1]))
             else:
                 for item in buckets[w]:
                     remaining[id(item[1])] = item

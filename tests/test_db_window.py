@@ -35,15 +35,22 @@ def _run(op):
 
 
 def test_window_group_by():
-    tumble = _run(WindowGroupByStreamOp().setTimeCol("ts").setWindowLength(1)
-                  .setSelectClause("k, SUM(v) AS s, COUNT(*) AS c").setGroupByClause("k"))
+    """Aggregates per window plus the reference's window_start / window_end TIMESTAMP columns
+    (WindowGroupByStreamOp.java:80-82; WindowGroupByStreamOpTest: 2 selected + 2 window columns)."""
+    def split(rows):
+        return [r[:-2] for r in rows], [(r[-2].timestamp(), r[-1].timestamp()) for r in rows]
+    tumble, win = split(_run(WindowGroupByStreamOp().setTimeCol("ts").setWindowLength(1)
+                             .setSelectClause("k, SUM(v) AS s, COUNT(*) AS c").setGroupByClause("k")))
     assert tumble == [("a", 1.0, 1), ("a", 2.0, 1), ("b", 3.0, 1), ("a", 4.0, 1), ("b", 5.0, 1)]
-    session = _run(WindowGroupByStreamOp().setTimeCol("ts").setWindowType("SESSION").setSessionGap(1)
-                   .setSelectClause("SUM(v) AS s"))
+    assert win == [(0.0, 1.0), (1.0, 2.0), (1.0, 2.0), (2.0, 3.0), (4.0, 5.0)]
+    session, win = split(_run(WindowGroupByStreamOp().setTimeCol("ts").setWindowType("SESSION").setSessionGap(1)
+                              .setSelectClause("SUM(v) AS s")))
     assert session == [(10.0,), (5.0,)]
-    hop = _run(WindowGroupByStreamOp().setTimeCol("ts").setWindowType("HOP").setWindowLength(2)
-               .setSlidingLength(1).setSelectClause("SUM(v) AS s"))
+    assert win == [(0.5, 3.1), (4.0, 5.0)]                   # session end = last event + gap
+    hop, win = split(_run(WindowGroupByStreamOp().setTimeCol("ts").setWindowType("HOP").setWindowLength(2)
+                          .setSlidingLength(1).setSelectClause("SUM(v) AS s")))
     assert hop == [(1.0,), (6.0,), (9.0,), (4.0,), (5.0,), (5.0,)]
+    assert all(e - s == 2.0 for s, e in win)
 
 
 def test_kafka_file_broker_and_hive_local_warehouse(tmp_path):
