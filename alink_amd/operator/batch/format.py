@@ -38,6 +38,19 @@ def _all_format_params():
     return list(seen.values())
 
 
+def format_ctor_args(args):
+    """The reference's format-op constructors take the FormatType(s) first: ``BaseFormatTransBatchOp(from, to,
+    params)``, ``AnyToTripleBatchOp(from, params)``, ``TripleToAnyBatchOp(to, params)``.  -> (format names,
+    params)."""
+    fmts, params = [], None
+    for a in args:
+        if a is None or isinstance(a, Params):
+            params = a
+        else:
+            fmts.append(str(getattr(a, "name", a)).upper())
+    return fmts, params
+
+
 class BaseFormatTransBatchOp(MapBatchOp):
     """Generic ``fromFormat`` -> ``toFormat`` conversion (``BaseFormatTransBatchOp.java``)."""
     MAPPER = F.FormatTransMapper
@@ -46,11 +59,14 @@ class BaseFormatTransBatchOp(MapBatchOp):
     FROM: Optional[str] = None
     TO: Optional[str] = None
 
-    def __init__(self, params: Optional[Params] = None, **kw):
+    def __init__(self, *args, **kw):
+        fmts, params = format_ctor_args(args)
         super().__init__(params, **kw)
         if self.FROM is not None:
             self.getParams().set("fromFormat", self.FROM)
             self.getParams().set("toFormat", self.TO)
+        if len(fmts) == 2:
+            self.getParams().set("fromFormat", fmts[0]).set("toFormat", fmts[1])
 
 
 class AnyToTripleBatchOp(FlatMapBatchOp):
@@ -59,10 +75,13 @@ class AnyToTripleBatchOp(FlatMapBatchOp):
     EXTRA_PARAMS = BaseFormatTransBatchOp.EXTRA_PARAMS
     FROM: Optional[str] = None
 
-    def __init__(self, params: Optional[Params] = None, **kw):
+    def __init__(self, *args, **kw):
+        fmts, params = format_ctor_args(args)
         super().__init__(params, **kw)
         if self.FROM is not None:
             self.getParams().set("fromFormat", self.FROM)
+        if fmts:
+            self.getParams().set("fromFormat", fmts[0])
 
 
 class TripleToAnyBatchOp(BatchOperator):
@@ -70,10 +89,13 @@ class TripleToAnyBatchOp(BatchOperator):
     EXTRA_PARAMS = BaseFormatTransBatchOp.EXTRA_PARAMS
     TO: Optional[str] = None
 
-    def __init__(self, params: Optional[Params] = None, **kw):
+    def __init__(self, *args, **kw):
+        fmts, params = format_ctor_args(args)
         super().__init__(params, **kw)
         if self.TO is not None:
             self.getParams().set("toFormat", self.TO)
+        if fmts:
+            self.getParams().set("toFormat", fmts[0])
 
     def linkFrom(self, *inputs):
         mt = self.checkAndGetFirst(inputs).getOutputTable()

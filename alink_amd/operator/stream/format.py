@@ -17,7 +17,7 @@ from ...common.table import MTable, Row, infer_type
 from ...common.types import TableSchema, Types, type_from_str
 from ...models.dataproc import format as F
 from ...models.dataproc import vector as V
-from ..batch.format import FORMATS, BaseFormatTransBatchOp
+from ..batch.format import FORMATS, BaseFormatTransBatchOp, format_ctor_args
 from ..batch.utils import _UDFMapper
 from .base import FlatMapStreamOp, MapStreamOp, StreamOperator, _register_upstream_sources
 
@@ -31,11 +31,14 @@ class BaseFormatTransStreamOp(MapStreamOp):
     FROM: Optional[str] = None
     TO: Optional[str] = None
 
-    def __init__(self, params: Optional[Params] = None, **kw):
+    def __init__(self, *args, **kw):
+        fmts, params = format_ctor_args(args)
         super().__init__(params, **kw)
         if self.FROM is not None:
             self.getParams().set("fromFormat", self.FROM)
             self.getParams().set("toFormat", self.TO)
+        if len(fmts) == 2:
+            self.getParams().set("fromFormat", fmts[0]).set("toFormat", fmts[1])
 
 
 class AnyToTripleStreamOp(FlatMapStreamOp):
@@ -43,10 +46,13 @@ class AnyToTripleStreamOp(FlatMapStreamOp):
     EXTRA_PARAMS = BaseFormatTransStreamOp.EXTRA_PARAMS
     FROM: Optional[str] = None
 
-    def __init__(self, params: Optional[Params] = None, **kw):
+    def __init__(self, *args, **kw):
+        fmts, params = format_ctor_args(args)
         super().__init__(params, **kw)
         if self.FROM is not None:
             self.getParams().set("fromFormat", self.FROM)
+        if fmts:
+            self.getParams().set("fromFormat", fmts[0])
 
 
 class CsvToColumnsStreamOp(MapStreamOp):

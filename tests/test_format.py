@@ -177,3 +177,21 @@ def test_vector_mappers_reference_values():
     assert run(VectorNormalizeBatchOp().setSelectedCol("vec").setOutputCol("res").setP(1.0),
                DenseVector([2.0, 3.0])) == DenseVector([0.4, 0.6])
     assert run(VectorSliceBatchOp().setSelectedCol("vec").setIndices([0, 1]), DenseVector([3.0, 4.0, 3.0])) == d34
+
+
+def test_triple_to_any_reference_constructor():
+    """TripleToAnyBatchOpTest: the reference's (FormatType, Params) constructor; 8 triples over 4 row ids give 4
+    KV rows and 4 vector rows."""
+    import alink_amd as A
+    from alink_amd.common.params import Params
+    from alink_amd.operator.batch.source import MemSourceBatchOp
+    rows = [(1, 1, 1.0), (1, 2, 1.0), (2, 3, 1.0), (3, 4, 1.0), (4, 2, 1.0), (3, 1, 1.0), (2, 4, 1.0), (4, 1, 1.0)]
+    data = MemSourceBatchOp(rows, ["start", "dest", "weight"])
+    base = Params().set("tripleRowCol", "start").set("tripleColCol", "dest").set("tripleValCol", "weight")
+    kv = A.TripleToAnyBatchOp("KV", base.clone().set("kvCol", "kv")).linkFrom(data).collect()
+    assert sorted(tuple(r) for r in kv) == [(1, "1:1.0,2:1.0"), (2, "3:1.0,4:1.0"), (3, "1:1.0,4:1.0"),
+                                            (4, "1:1.0,2:1.0")]
+    vec = A.TripleToAnyBatchOp("VECTOR", base.clone().set("vectorCol", "vec")).linkFrom(data).collect()
+    assert len(vec) == 4
+    trans = A.BaseFormatTransBatchOp("KV", "COLUMNS", Params().set("kvCol", "kv").set("schemaStr", "1 double"))
+    assert trans.getParams().get("fromFormat") == "KV" and trans.getParams().get("toFormat") == "COLUMNS"
