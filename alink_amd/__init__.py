@@ -12,6 +12,7 @@ from .parallel.launch import launch, launch_script  # noqa: F401
 from .common.linalg import DenseVector, SparseVector, VectorUtil, DenseMatrix, BLAS, MatVecOp, NormalEquation  # noqa: F401,E501
 from .common.table import MTable, Row  # noqa: F401
 from .common.types import TableSchema, Types  # noqa: F401
+from .operator.common.sql.udf import ScalarFunction, TableFunction, udf, udtf  # noqa: F401
 from .operator.common.io.db import BaseDB, SqliteDB, DerbyDB, MySqlDB, JdbcDB  # noqa: F401
 from .operator.base import BatchOperator  # noqa: F401
 from .operator.batch import *  # noqa: F401,F403

@@ -139,7 +139,9 @@ class UDTFBatchOp(BatchOperator):
         outs = p.get("outputCols")
         reserved = p.get("reservedCols") if p.contains("reservedCols") else None
         f = self.getFunc()
-        f = getattr(f, "eval", f)
+        from ..common.sql.udf import TableFunction
+        if not isinstance(f, TableFunction):       # a TableFunction collects its rows; plain callables return them
+            f = getattr(f, "eval", f)
         idx = [mt.schema.names.index(c) for c in sel]
         rts = getattr(self.getFunc(), "result_types", None) or p.get(self._param_infos["resultTypes"])
         rows_out = []

@@ -1,8 +1,44 @@
 """Scalar / table function registry for SQL and ``udf``/``udtf`` ops (reference ``BatchOperator.registerFunction``,
 ``docs/pyalink/pyalink-udf.md``)."""
-from typing import Callable, Dict, Optional
+from typing import Callable, Dict, List, Optional
 
 _FUNCS: Dict[str, Callable] = {}
+
+
+class ScalarFunction:
+    """A scalar UDF in the reference's (Flink) form: subclass with ``eval(*args)`` and optionally
+    ``getResultType(*signature)`` returning the result type (an Alink type or its name)."""
+
+    def getResultType(self, *signature):
+        return None
+
+    @property
+    def result_type(self):
+        return self.getResultType()
+
+
+class TableFunction:
+    """A table UDF in the reference's (Flink) form: ``eval(*args)`` emits any number of rows through
+    ``self.collect(row)``; ``getResultType`` may name the output column types."""
+
+    def __init__(self):
+        self._rows: List = []
+
+    def collect(self, row):
+        self._rows.append(row)
+
+    def getResultType(self, *signature):
+        return None
+
+    @property
+    def result_types(self):
+        return self.getResultType()
+
+    def __call__(self, *args):
+        self._rows = []
+        self.eval(*args)
+        out, self._rows = self._rows, []
+        return out
 
 
 def register_function(name: str, fn: Callable):

@@ -109,7 +109,8 @@ class _UDTFMapper(FlatMapper):
     def __init__(self, dataSchema, params, func, result_types):
         super().__init__(dataSchema, params)
         p = self.params
-        self.func = getattr(func, "eval", func)
+        from ..common.sql.udf import TableFunction
+        self.func = func if isinstance(func, TableFunction) else getattr(func, "eval", func)
         self.idx = [dataSchema.names.index(c) for c in p.get("selectedCols")]
         self.outs = list(p.get("outputCols"))
         reserved = p.get("reservedCols") if p.contains("reservedCols") else None

@@ -321,3 +321,47 @@ def test_map_flatmap_udf_udtf_print(capsys):
         CollectStreamOp(sw))
     StreamOperator.execute()
     assert _rows(sw) == _rows(out)
+
+
+def test_udf_stream_reference_function_classes():
+    """UDFStreamOpTest / UDTFStreamOpTest: Flink-style ScalarFunction (eval + getResultType) over (c1, c2) into c2;
+    default reservedCols keep every input column (c2 replaced), empty reservedCols keep only the output; a
+    TableFunction emits rows through collect()."""
+    import alink_amd as A
+    from alink_amd.operator.stream.source import MemSourceStreamOp
+
+    class LengthPlusValue(A.ScalarFunction):
+        def eval(self, s, v):
+            return len(s) + v
+
+        def getResultType(self, *signature):
+            return A.Types.LONG
+
+    def src():
+        return MemSourceStreamOp([("1", "a", 1), ("2", "b33", 2)], ["c0", "c1", "c2"])
+    op = A.UDFStreamOp().setFunc(LengthPlusValue()).setSelectedCols(["c1", "c2"]).setOutputCol("c2")
+    op.linkFrom(src())
+    assert op.getColNames() == ["c0", "c1", "c2"]
+    out = []
+    op.collect_to(out)
+    A.StreamOperator.execute()
+    assert [tuple(r) for r in out] == [("1", "a", 2), ("2", "b33", 5)]
+    op = A.UDFStreamOp().setFunc(LengthPlusValue()).setSelectedCols(["c1", "c2"]).setReservedCols([]) \
+        .setOutputCol("c2")
+    op.linkFrom(src())
+    assert op.getColNames() == ["c2"]
+
+    class Split(A.TableFunction):
+        def eval(self, s):
+            for ch in s:
+                self.collect((ch, 1))
+    op = A.UDTFStreamOp().setFunc(Split()).setSelectedCols(["c1"]).setOutputCols(["ch", "n"]) \
+        .setResultTypes(["STRING", "LONG"])
+    op.linkFrom(src())
+    out = []
+    op.collect_to(out)
+    A.StreamOperator.execute()
+    assert [tuple(r)[-2:] for r in out] == [("a", 1), ("b", 1), ("3", 1), ("3", 1)]
+    rows = A.UDTFBatchOp().setFunc(Split()).setSelectedCols(["c1"]).setOutputCols(["ch", "n"]) \
+        .linkFrom(A.MemSourceBatchOp([("1", "a", 1), ("2", "b33", 2)], ["c0", "c1", "c2"])).collect()
+    assert [tuple(r)[-2:] for r in rows] == [("a", 1), ("b", 1), ("3", 1), ("3", 1)]
