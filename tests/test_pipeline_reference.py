@@ -538,3 +538,14 @@ def test_gaussian_mixture_univariate_reference():
         assert c["weight"] == pytest.approx(w, abs=1e-2)
         assert c["mean"]["data"][0] == pytest.approx(mean, abs=1e-2)
         assert c["cov"]["data"][0] == pytest.approx(cov, abs=1e-2)
+
+
+def test_split_append_id_union_reference():
+    """SplitBatchOpTest: AppendId, fraction 0.1 of iris -> exactly 15 / 135 rows, union back to 150."""
+    src, _ = _iris()
+    data = A.AppendIdBatchOp().linkFrom(src)
+    splitter = A.SplitBatchOp().setFraction(0.1)
+    left = splitter.linkFrom(data)
+    right = splitter.getSideOutput(0)
+    assert left.count() == 15 and right.count() == 135
+    assert A.UnionBatchOp().linkFrom(left, right).count() == 150
