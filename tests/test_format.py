@@ -195,3 +195,28 @@ def test_triple_to_any_reference_constructor():
     assert len(vec) == 4
     trans = A.BaseFormatTransBatchOp("KV", "COLUMNS", Params().set("kvCol", "kv").set("schemaStr", "1 double"))
     assert trans.getParams().get("fromFormat") == "KV" and trans.getParams().get("toFormat") == "COLUMNS"
+
+
+def test_vector_size_hint_slice_to_columns_mappers_reference():
+    """VectorSizeHintMapperTest / VectorSliceMapperTest / VectorToColumnsMapperTest."""
+    from alink_amd.common.linalg import DenseVector, SparseVector
+    from alink_amd.common.params import Params
+    from alink_amd.common.types import schema_str_to_schema
+    from alink_amd.models.dataproc import vector as V
+    s = schema_str_to_schema("vec string")
+    m = V.VectorSizeHintMapper(s, Params().set("selectedCol", "vec").set("size", 3))
+    assert m.getOutputSchema().getFieldNames() == ["vec"]
+    m = V.VectorSizeHintMapper(s, Params().set("selectedCol", "vec").set("outputCol", "res")
+                               .set("handleInvalid", "SKIP").set("size", 2))
+    assert m.getOutputSchema().getFieldNames() == ["vec", "res"]
+    m = V.VectorSliceMapper(s, Params().set("selectedCol", "vec").set("indices", [0, 1]))
+    assert str(m.map((DenseVector([3.0, 4.0, 3.0]),))[0]) == "3.0 4.0"
+    m = V.VectorSliceMapper(s, Params().set("selectedCol", "vec").set("outputCol", "res").set("reservedCols", [])
+                            .set("indices", [0, 2, 4]))
+    assert str(m.map((SparseVector(5, [0, 2, 4], [3.0, 4.0, 3.0]),))[0]) == "$3$0:3.0 1:4.0 2:3.0"
+    m = V.VectorToColumnsMapper(s, Params().set("selectedCol", "vec").set("outputCols", ["f0", "f1"]))
+    assert tuple(m.map((DenseVector([3.0, 4.0]),)))[1:] == (3.0, 4.0)
+    assert m.getOutputSchema().getFieldNames() == ["vec", "f0", "f1"]
+    m = V.VectorToColumnsMapper(s, Params().set("selectedCol", "vec").set("outputCols", ["f0", "f1", "f2"])
+                                .set("reservedCols", []))
+    assert tuple(m.map((SparseVector(3, [1, 2], [3.0, 4.0]),))) == (0.0, 3.0, 4.0)
