@@ -243,12 +243,15 @@ def binary_summary_block(label_col, blk, label_array: List[str], device=None):
     (positiveBin, negativeBin, logLoss, total) over all ranks — the strings are ``Double.toString`` of these same
     doubles, which parse back exactly.  None when the block's labels are not the two of ``label_array`` or a
     probability is out of range (the caller then takes the string path and its exact errors)."""
-    # the fall-back decision is collective (the string path's all-reduce must run on every rank or on none)
-    valid = float(detail_block_valid(blk, label_array))
+    # the fall-back decision is collective (the string path's all-reduce must run on every rank or on none);
+    # ``blk`` None = this rank's micro-batch is empty (it contributes zero bins)
+    valid = float(blk is None or len(blk) == 0 or detail_block_valid(blk, label_array))
     if comm.is_distributed():
         valid = min(comm.all_gather_object(valid))
     if valid < 1.0:
         return None
+    if blk is None or len(blk) == 0:
+        return _reduce_bins(np.zeros(2 * DETAIL_BIN_NUMBER), 0.0, 0, device or torch.device("cpu"))
     keys = [str(x) for x in blk.labels]
     ustr, inv, lnull = _label_codes(label_col)
     ok = ~lnull if blk.nulls is None else (~lnull & ~blk.nulls)

@@ -275,7 +275,7 @@ def _detail_json(labels: Sequence[Any], probs: np.ndarray) -> List[str]:
                 for row in probs]
     strs = body.split(",") if probs.size else []
     K = len(order)
-    tmpl = "{" + ",".join(gson_dumps(k) + ':"%s"' for k in order) + "}"
+    tmpl = "{" + ",".join(gson_dumps(k).replace("%", "%%") + ':"%s"' for k in order) + "}"
     return [tmpl % tuple(strs[i * K:(i + 1) * K]) for i in range(probs.shape[0])]
 
 

@@ -70,14 +70,21 @@ class _EvalClass(_EvalBase):
         dev = self.env.device
         if detail_col:
             from ...common.detail import DetailBlock
-            dcol = mt.col(detail_col)
-            if self.BINARY and isinstance(dcol.values, DetailBlock):
+            dvals = mt.col(detail_col).values
+            blk = dvals if isinstance(dvals, DetailBlock) else None
+            # the columnar and the string branch issue different collectives: every rank takes the same one (a
+            # rank with no rows abstains)
+            use_block = self.BINARY and (blk is not None or mt.num_rows == 0)
+            if comm.is_distributed():
+                use_block = bool(min(comm.all_gather_object(bool(use_block))))
+            if use_block:
                 # columnar detail (probabilities, not strings): label set and bins without per-row parsing
                 label_set = set()
-                for part in comm.all_gather_object(sorted(M.detail_block_keys(mt.col(label_col), dcol.values))):
+                keys = M.detail_block_keys(mt.col(label_col), blk) if blk is not None else set()
+                for part in comm.all_gather_object(sorted(keys)):
                     label_set.update(part)
                 arr = M.build_label_index(label_set, True, pos)
-                fast = M.binary_summary_block(mt.col(label_col), dcol.values, arr, dev)
+                fast = M.binary_summary_block(mt.col(label_col), blk, arr, dev)
                 if fast is not None:
                     pb, nb, ll, n = fast
                     if n == 0:

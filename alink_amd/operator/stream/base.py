@@ -121,9 +121,9 @@ class StreamEngine:
     def run(self, checkpoint=None):
         """Drive every source to exhaustion, one micro-batch per source per round.
 
-        With a checkpoint conf on a multi-rank job the rounds are a LOCKSTEP protocol: every round ends with one
-        MAX all-reduce of (any source still live, checkpoint due), a rank whose sources ended keeps emitting empty
-        micro-batches until every rank's have, and a checkpoint is written by all ranks at the same round — a
+        On a multi-rank job the rounds are a LOCKSTEP protocol: every round ends with one MAX all-reduce of (any
+        source still live, checkpoint due), a rank whose sources ended keeps emitting empty micro-batches until
+        every rank's have, and with a checkpoint conf a checkpoint is written by all ranks at the same round — a
         consistent cut (the reference's Flink checkpoint barrier, ``StreamOperator.java:216-239``)."""
         import time
         import torch
@@ -131,7 +131,10 @@ class StreamEngine:
         srcs = [s for s in self.sources if s._subscribers]
         its = [(s, s.batches()) for s in srcs]
         consumed = [0] * len(its)
-        lockstep = checkpoint is not None and comm.get_world_size() > 1
+        # under a process group every rank runs the same number of rounds (an ended source emits empty
+        # micro-batches until every rank's sources have ended), so operators whose on_batch issues collectives
+        # (evaluation windows, DB sinks, FTRL) stay in step even when the ranks' streams differ in length
+        lockstep = comm.get_world_size() > 1
         fp = self._fingerprint() if checkpoint is not None else None
         rnd = 0
         if checkpoint is not None:

@@ -43,17 +43,40 @@ class _EvalStream(StreamOperator):
         self._labels = None
         return self
 
+    def _agree_labels(self, keys, p) -> bool:
+        """Fix the label index from this micro-batch's label keys (the union over the ranks under a process
+        group, so every rank indexes the same labels).  False while no rank has seen an effective row yet."""
+        if comm.is_distributed():
+            keys = set().union(*[set(part) for part in comm.all_gather_object(sorted(keys))])
+        if not keys:
+            return False
+        self._labels = M.build_label_index(keys, self.BINARY, _pget(p, "positiveLabelValueString"))
+        return True
+
     def _summary(self, mt):
+        """This micro-batch's summary over all ranks, or None while no label index exists.  Every collective in
+        here runs on every rank, including ranks whose micro-batch is empty (the lockstep runner sends those)."""
         p = self.getParams()
-        labels = mt.column_values(p.get("labelCol"))
         det_col = _pget(p, "predictionDetailCol")
         pred_col = _pget(p, "predictionCol")
+        lcol = mt.col(p.get("labelCol"))
         if det_col:
-            dcol = mt.col(det_col)
-            if self.BINARY and isinstance(dcol.values, DetailBlock) and len(dcol.values.labels) == 2:
-                fast = self._binary_columnar(mt.col(p.get("labelCol")), dcol.values, p)
-                if fast is not None:
-                    return fast
+            dvals = mt.col(det_col).values
+            blk = dvals if isinstance(dvals, DetailBlock) else None
+            # the columnar / string branch issues different collectives: agree on it first (an empty
+            # micro-batch abstains)
+            use_block = self.BINARY and ((blk is not None and len(blk.labels) == 2) or mt.num_rows == 0)
+            if comm.is_distributed():
+                use_block = bool(min(comm.all_gather_object(bool(use_block))))
+            if use_block:
+                if self._labels is None:
+                    keys = M.detail_block_keys(lcol, blk) if blk is not None else set()
+                    if not self._agree_labels(keys, p):
+                        return None
+                res = M.binary_summary_block(lcol, blk, self._labels)
+                if res is not None:
+                    return ("b",) + res
+            labels = mt.column_values(p.get("labelCol"))
             dets = mt.column_values(det_col)
             if self._labels is None:
                 # the label index is fixed by the first window (its labels and detail keys)
@@ -62,23 +85,17 @@ class _EvalStream(StreamOperator):
                     if l is not None and d is not None:
                         keys.update(M.parse_detail(d).keys())
                         keys.add(str(l))
-                self._labels = M.build_label_index(keys, self.BINARY, _pget(p, "positiveLabelValueString"))
+                if not self._agree_labels(keys, p):
+                    return None
             if self.BINARY:
                 return ("b",) + M.binary_summary(labels, dets, self._labels)
             return ("m",) + M.multi_summary_from_detail(labels, dets, self._labels)
+        labels = mt.column_values(p.get("labelCol"))
         preds = mt.column_values(pred_col)
         if self._labels is None:
-            self._labels = M.build_label_index({str(x) for x in labels + preds if x is not None}, self.BINARY,
-                                               _pget(p, "positiveLabelValueString"))
+            if not self._agree_labels({str(x) for x in labels + preds if x is not None}, p):
+                return None
         return ("m",) + M.multi_summary_from_pred(labels, preds, self._labels)
-
-    def _binary_columnar(self, lcol, blk, p):
-        """Binary summary straight from a ``DetailBlock`` (no detail strings; ``metrics.binary_summary_block``)."""
-        if self._labels is None:
-            self._labels = M.build_label_index(M.detail_block_keys(lcol, blk), True,
-                                               _pget(p, "positiveLabelValueString"))
-        res = M.binary_summary_block(lcol, blk, self._labels)
-        return None if res is None else ("b",) + res
 
     @staticmethod
     def _metrics(s, labels):
@@ -117,10 +134,10 @@ class _EvalStream(StreamOperator):
         self._emit(MTable.from_rows(rows, _SCHEMA))
 
     def on_batch(self, port, mt):
-        if mt.num_rows == 0:
+        if mt.num_rows == 0 and not comm.is_distributed():
             return
         s = self._summary(mt)
-        if s[-1] != 0:
+        if s is not None and s[-1] != 0:
             if self._win_t0 is None:
                 self._win_t0 = time.perf_counter()
             self._win = self._merge(self._win, s)

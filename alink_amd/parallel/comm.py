@@ -59,7 +59,19 @@ class CommStats:
 STATS = CommStats()
 
 
-_DEV_TIMING = {"on": False, "events": []}
+_DEV_TIMING = {"on": False, "events": [], "folded": (0, 0.0, {})}
+_DEV_TIMING_MAX_PENDING = 1024       # older event pairs are resolved into running totals beyond this many
+
+
+def _fold_events(evs, acc):
+    n, tot, per = acc
+    per = dict(per)
+    for name, s, e in evs:
+        e.synchronize()
+        dt = s.elapsed_time(e) * 1e-3
+        tot += dt
+        per[name] = per.get(name, 0.0) + dt
+    return n + len(evs), tot, per
 
 
 def device_timing(on: bool = True):
@@ -72,14 +84,9 @@ def device_timing(on: bool = True):
 def device_timing_collect():
     """(count, total seconds, per-name totals) of the collectives timed since the last collect; synchronises the
     recorded events."""
-    evs, _DEV_TIMING["events"] = _DEV_TIMING["events"], []
-    tot, per = 0.0, {}
-    for name, s, e in evs:
-        e.synchronize()
-        dt = s.elapsed_time(e) * 1e-3
-        tot += dt
-        per[name] = per.get(name, 0.0) + dt
-    return len(evs), tot, per
+    evs, acc = _DEV_TIMING["events"], _DEV_TIMING["folded"]
+    _DEV_TIMING["events"], _DEV_TIMING["folded"] = [], (0, 0.0, {})
+    return _fold_events(evs, acc)
 
 
 def _collective(fn):
@@ -111,7 +118,12 @@ def _collective(fn):
         finally:
             if ev is not None:
                 ev[1].record(torch.cuda.current_stream(t.device))
-                _DEV_TIMING["events"].append((name, ev[0], ev[1]))
+                evl = _DEV_TIMING["events"]
+                evl.append((name, ev[0], ev[1]))
+                if len(evl) > _DEV_TIMING_MAX_PENDING:     # bounded: a long timed job holds few live events
+                    half = len(evl) // 2
+                    _DEV_TIMING["folded"] = _fold_events(evl[:half], _DEV_TIMING["folded"])
+                    del evl[:half]
             STATS.time_s += time.perf_counter() - t0
             _NEST.v = False
     return wrapper

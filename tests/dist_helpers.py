@@ -588,5 +588,45 @@ def scenario_trace(out):
     out["steps"] = [r for r in metrics.records("superstep") if r.get("job") == "KMeans"]
 
 
+def scenario_eval_uneven(out):
+    """Binary evaluation where rank 0 holds 200 rows and rank 1 60 (P=1 holds all 260), as a stream (40-row
+    micro-batches, windows after every batch; phase ``ckpt`` adds a stream checkpoint conf) and as a batch op.
+    Phase ``mixed``: rank 0's detail column is a columnar DetailBlock, rank 1's plain strings — the ranks must
+    agree on one summary branch instead of issuing different collectives."""
+    import numpy as np
+    os.environ["ALINK_STREAM_BATCH"] = "40"
+    from alink_amd import useLocalEnv, StreamOperator, EvalBinaryClassStreamOp, EvalBinaryClassBatchOp, \
+        CollectStreamOp
+    from alink_amd.common.detail import DetailBlock
+    from alink_amd.common.table import Column, MTable
+    from alink_amd.common.types import TableSchema, Types
+    from alink_amd.operator.batch.source import TableSourceBatchOp
+    from alink_amd.operator.stream.source import TableSourceStreamOp
+    from alink_amd.parallel import comm
+    import torch
+    phase = os.environ.get("ALINK_TEST_PHASE", "plain")
+    useLocalEnv(1)
+    rng = np.random.default_rng(11)
+    p = rng.random(260)
+    y = (rng.random(260) < p).astype(np.int64)
+    ws, r = comm.get_world_size(), comm.get_rank()
+    sl = slice(0, 260) if ws == 1 else (slice(0, 200) if r == 0 else slice(200, 260))
+    blk = DetailBlock(["1", "0"], np.stack([p[sl], 1.0 - p[sl]], 1))
+    dcol = Column(blk) if (phase == "mixed" and r == 0) or ws == 1 else Column(blk.to_list())
+    mt = MTable(TableSchema(["label", "detail"], [Types.LONG, Types.STRING]),
+                [Column(torch.from_numpy(y[sl].copy())), dcol])
+    if phase == "ckpt":
+        StreamOperator.setCheckPointConf(interval_s=1e9, directory=os.path.join(os.environ["ALINK_TEST_TMP"],
+                                         "ck_eval"), every_batches=2)
+    box = []
+    EvalBinaryClassStreamOp().setLabelCol("label").setPredictionDetailCol("detail").setTimeInterval(0) \
+        .linkFrom(TableSourceStreamOp(mt)).link(CollectStreamOp(box))
+    StreamOperator.execute()
+    out["stream"] = [list(rw) for rw in box]
+    m = EvalBinaryClassBatchOp().setLabelCol("label").setPredictionDetailCol("detail") \
+        .linkFrom(TableSourceBatchOp(mt)).collectMetrics()
+    out["batch"] = {"auc": m.getAuc(), "logloss": m.getLogLoss(), "total": m.getTotalSamples()}
+
+
 if __name__ == "__main__":
     run(int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), sys.argv[4], sys.argv[5])

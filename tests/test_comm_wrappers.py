@@ -75,3 +75,35 @@ def test_comm_wrappers_rccl_one_rank_no_oneshot(tmp_path):
     o = _run(1, tmp_path, "rccl_plain", {"ALINK_ONESHOT_ALLREDUCE": "0"})[0]
     assert o["backend"] == "nccl" and o["is_distributed"]
     assert not o["oneshot_instance"] and o["stats"]["oneshot"] == 0
+
+
+def test_device_timing_event_list_is_bounded():
+    """Device timing folds old event pairs into running totals: a long timed job never holds more than the cap of
+    live events, and collect() still returns every collective's count and time."""
+    from alink_amd.parallel import comm
+
+    class _Ev:
+        def synchronize(self):
+            pass
+
+        def elapsed_time(self, other):
+            return 2.0                                          # ms
+
+    saved = dict(comm._DEV_TIMING)
+    try:
+        comm._DEV_TIMING.update({"events": [], "folded": (0, 0.0, {})})
+        cap = comm._DEV_TIMING_MAX_PENDING
+        for i in range(3 * cap):
+            evl = comm._DEV_TIMING["events"]
+            evl.append(("all_reduce", _Ev(), _Ev()))
+            if len(evl) > cap:
+                half = len(evl) // 2
+                comm._DEV_TIMING["folded"] = comm._fold_events(evl[:half], comm._DEV_TIMING["folded"])
+                del evl[:half]
+            assert len(comm._DEV_TIMING["events"]) <= cap
+        n, tot, per = comm.device_timing_collect()
+        assert n == 3 * cap and abs(tot - 3 * cap * 2e-3) < 1e-9 and set(per) == {"all_reduce"}
+        assert comm.device_timing_collect()[0] == 0
+    finally:
+        comm._DEV_TIMING.clear()
+        comm._DEV_TIMING.update(saved)

@@ -400,3 +400,22 @@ def test_eval_stream_windows_agree_across_ranks(tmp_path):
     assert [r[0] for r in a] == [r[0] for r in b]
     assert len(a) >= 4                                   # rank 1's stalls close at least one window early
     assert json.loads(a[-1][1])["TotalSamples"] == json.loads(b[-1][1])["TotalSamples"]
+
+
+@pytest.mark.parametrize("phase", ["plain", "ckpt", "mixed"])
+def test_eval_uneven_ranks_and_mixed_detail_kinds(tmp_path, monkeypatch, phase):
+    """Binary evaluation on ranks of unequal length (the shorter rank's stream ends first and keeps joining the
+    collectives with empty micro-batches), with and without a stream checkpoint, and with one rank's detail column
+    columnar and the other's strings: no hang, and the final cumulative metrics equal one rank over all rows."""
+    monkeypatch.setenv("ALINK_TEST_PHASE", phase)
+    one = _run("eval_uneven", 1, tmp_path)[0]
+    two = _run("eval_uneven", 2, tmp_path)
+    assert two[0]["stream"] == two[1]["stream"]
+    fin1 = json.loads([r for r in one["stream"] if r[0] == "all"][-1][1])
+    fin2 = json.loads([r for r in two[0]["stream"] if r[0] == "all"][-1][1])
+    assert int(fin2["TotalSamples"]) == int(fin1["TotalSamples"]) == 260
+    assert float(fin2["AUC"]) == float(fin1["AUC"])
+    assert abs(float(fin2["LogLoss"]) - float(fin1["LogLoss"])) < 1e-12
+    assert two[0]["batch"]["total"] == two[1]["batch"]["total"] == one["batch"]["total"] == 260
+    assert two[0]["batch"]["auc"] == one["batch"]["auc"]
+    assert abs(two[0]["batch"]["logloss"] - one["batch"]["logloss"]) < 1e-12

@@ -248,3 +248,10 @@ def test_regression_metrics_reference_values():
     m = M.regression_metrics(np.array([1.6, 0.66, 2.8, 1.599, 1.2, 0.38, 7.08, 5]))
     for name, v in {"R2": -1.56, "Sse": 0.38, "Mape": 141.6, "Rmse": 0.27, "Mae": 0.24, "Ssr": 0.31}.items():
         assert getattr(m, "get" + name)() == pytest.approx(v, abs=0.01), name
+
+
+def test_detail_json_label_with_percent():
+    """Labels containing '%' survive the per-table detail template (it is %-formatted)."""
+    from alink_amd.models.linear.model import _detail_json
+    out = _detail_json(["50%", "a%s"], np.array([[0.25, 0.75], [1.0, 0.0]]))
+    assert [json.loads(s) for s in out] == [{"50%": "0.25", "a%s": "0.75"}, {"50%": "1.0", "a%s": "0.0"}]

@@ -26,9 +26,10 @@ case "$step" in
     cd "$R" && timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 \
       && echo "SMOKE_OK $(tail -1 "$O/smoke.log")" || { tail -30 "$O/smoke.log"; exit 1; } ;;
   bench)
-    cd "$R" && timeout -k 10 ${LIMIT:-600} python bench.py "$@" > "$O/bench.log" 2>&1 \
-      && { tail -1 "$O/bench.log" > "$O/bench.json"; echo BENCH_OK; cat "$O/bench.json"; } \
-      || { tail -30 "$O/bench.log"; exit 1; } ;;
+    tag=${TAG:-bench}
+    cd "$R" && timeout -k 10 ${LIMIT:-600} python bench.py "$@" > "$O/$tag.log" 2>&1 \
+      && { tail -1 "$O/$tag.log" > "$O/$tag.json"; echo BENCH_OK; cat "$O/$tag.json"; } \
+      || { tail -30 "$O/$tag.log"; exit 1; } ;;
   run)
     name=$1; secs=$2; shift 2
     cd "$R" && timeout -k 10 "$secs" "$@" > "$O/$name.log" 2>&1 && { echo "RUN_OK $name"; tail -40 "$O/$name.log"; } \
