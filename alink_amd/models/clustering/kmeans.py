@@ -192,12 +192,16 @@ def _global_count(n_local: int) -> List[int]:
 _M64 = (1 << 64) - 1
 
 
+def _round_key(seed: int, rnd: int) -> int:
+    key = (seed * 0x9E3779B97F4A7C15 + rnd * 0xBF58476D1CE4E5B9 + 0x94D049BB133111EB) & _M64
+    return key - (1 << 64) if key >= (1 << 63) else key
+
+
 def _row_uniform(first_row: int, n: int, seed: int, rnd: int, device) -> torch.Tensor:
     """Counter-based U(0,1) per *global* row index (splitmix64 of (seed, round, row)): the k-means||
     oversampling draws are the same for any world size / partitioning, so a P-rank job picks exactly
     the candidates a 1-rank job picks (the reference's per-subtask Random makes them P-dependent)."""
-    key = (seed * 0x9E3779B97F4A7C15 + rnd * 0xBF58476D1CE4E5B9 + 0x94D049BB133111EB) & _M64
-    key = key - (1 << 64) if key >= (1 << 63) else key
+    key = _round_key(seed, rnd)
     z = torch.arange(first_row, first_row + n, dtype=torch.int64, device=device) * 0x2545F491 + key
 
     def _shr(x, k):  # logical shift right on int64
@@ -224,6 +228,44 @@ def _fetch_global_rows(X: torch.Tensor, global_idx: List[int], counts: List[int]
     return out
 
 
+def _seed_reference_device(D: torch.Tensor, w: torch.Tensor, k: int, rng, idx0: int) -> Optional[torch.Tensor]:
+    """Picks 1..k-1 of the reference seeding rule without a host round trip per pick: the k-1 uniforms are drawn
+    up front (the same values, in the same order, that the per-pick ``rng.random(1)`` calls return) and every
+    pick's cumulative weight x cost, scaled draw, ``searchsorted`` and cost update run as device ops.  Returns the
+    [k] candidate indices, or None (rng untouched) when some pick met an all-zero total — the per-pick host loop
+    then runs instead, since that case consumes the generator differently."""
+    n = D.shape[0]
+    state = rng.bit_generator.state
+    U = torch.as_tensor(rng.random(k - 1), dtype=torch.float64, device=D.device)
+    chosen = torch.empty(k, dtype=torch.int64, device=D.device)
+    mintot = torch.full((1,), float("inf"), dtype=torch.float64, device=D.device)
+    if D.is_cuda and n <= 4096 and _lib.available():
+        # all k-1 picks in one single-workgroup launch (csrc/kmeans_nearest.hip kmeans_seed_ref_kernel)
+        L = _lib.require()
+        Dc, wc = D.contiguous(), w.contiguous()
+        rc = L.alink_kmeans_seed_ref(Dc.data_ptr(), wc.data_ptr(), U.data_ptr(), n, k, int(idx0), chosen.data_ptr(),
+                                     mintot.data_ptr(), _lib.stream_ptr(D.device))
+        if rc != 0:
+            raise RuntimeError(f"alink_kmeans_seed_ref failed: {rc}")
+        if not float(mintot.item()) > 0:
+            rng.bit_generator.state = state
+            return None
+        return chosen
+    chosen[0] = idx0
+    costs = D[idx0].clone()
+    for j in range(1, k):
+        cw = torch.cumsum(w * costs, 0)
+        tot = cw[-1:]
+        torch.minimum(mintot, tot, out=mintot)
+        i = torch.searchsorted(cw, U[j - 1:j] * tot).clamp_(max=n - 1)
+        chosen[j:j + 1] = i
+        costs = torch.minimum(costs, D.index_select(0, i)[0])
+    if not float(mintot.item()) > 0:
+        rng.bit_generator.state = state
+        return None
+    return chosen
+
+
 def _local_kmeans(samples: torch.Tensor, weights: torch.Tensor, k: int, dist_type: str,
                   max_iter: int = 30, seed: int = 0) -> torch.Tensor:
     """Weighted k-means++ seeding + Lloyd on the k-means|| candidate set (LocalKmeansFunc.java:36-141).
@@ -234,7 +276,12 @@ def _local_kmeans(samples: torch.Tensor, weights: torch.Tensor, k: int, dist_typ
 
     ``ALINK_KMEANS_SEEDING=greedy``: every pick takes the candidate that lowers the weighted *squared*-distance
     potential most — over ALL candidates when the set is small (<= 4096, the usual k-means|| output, O(k m^2)
-    on the device), else over 2 + ln k sampled trials."""
+    on the device), else over 2 + ln k sampled trials.
+
+    Device-resident: the reference rule's picks (``_seed_reference_device``) and every Lloyd iteration issue no
+    per-centroid or per-pick host read — one 2-flag read per Lloyd iteration (changed assignment, empty cluster);
+    an empty cluster is refilled from a random candidate in ascending cluster order, as before.  On the GPU the
+    cluster sums are a one-hot fp64 GEMM (run-to-run deterministic)."""
     import os
     rng = np.random.default_rng(seed)
     n = samples.shape[0]
@@ -243,52 +290,60 @@ def _local_kmeans(samples: torch.Tensor, weights: torch.Tensor, k: int, dist_typ
     D = pairwise_distance(samples, samples, dist_type)                                      # [n, n]
     if not reference_rule:
         D = _seed_cost(D, dist_type)
-    if reference_rule:
-        trials = 1
+    trials = 1 if reference_rule else 2 + int(np.log(max(k, 2)))
     exhaustive = n <= 4096 and not reference_rule
-    if not reference_rule:
-        trials = 2 + int(np.log(max(k, 2)))
     cum = torch.cumsum(w, 0).cpu().numpy()
     idx = int(min(np.searchsorted(cum, rng.random() * cum[-1], side="left"), n - 1))
-    chosen = [idx]
-    costs = D[idx].clone()
-    for _ in range(1, k):
-        if exhaustive:
-            pot = (torch.minimum(costs[None, :], D) * w[None, :]).sum(1)
-            pot[chosen] = float("inf")
+    chosen_t = _seed_reference_device(D, w, k, rng, idx) if reference_rule and k > 1 else None
+    if chosen_t is not None:
+        C = samples.index_select(0, chosen_t)
+    else:
+        chosen = [idx]
+        costs = D[idx].clone()
+        for _ in range(1, k):
+            if exhaustive:
+                pot = (torch.minimum(costs[None, :], D) * w[None, :]).sum(1)
+                pot[chosen] = float("inf")
+                b = int(pot.argmin().item())
+                chosen.append(b)
+                costs = torch.minimum(costs, D[b])
+                continue
+            cw = torch.cumsum(w * costs, 0).cpu().numpy()
+            tot = cw[-1]
+            if tot <= 0:
+                cand = rng.integers(n, size=trials)
+            else:
+                cand = np.minimum(np.searchsorted(cw, rng.random(trials) * tot, side="left"), n - 1)
+            cand_t = torch.as_tensor(cand, device=samples.device)
+            newc = torch.minimum(costs[None, :], D[cand_t])  # [trials, n]
+            pot = (newc * w[None, :]).sum(1)
             b = int(pot.argmin().item())
-            chosen.append(b)
-            costs = torch.minimum(costs, D[b])
-            continue
-        cw = torch.cumsum(w * costs, 0).cpu().numpy()
-        tot = cw[-1]
-        if tot <= 0:
-            cand = rng.integers(n, size=trials)
-        else:
-            cand = np.minimum(np.searchsorted(cw, rng.random(trials) * tot, side="left"), n - 1)
-        cand_t = torch.as_tensor(cand, device=samples.device)
-        newc = torch.minimum(costs[None, :], D[cand_t])  # [trials, n]
-        pot = (newc * w[None, :]).sum(1)
-        b = int(pot.argmin().item())
-        chosen.append(int(cand[b]))
-        costs = newc[b]
-    C = samples[chosen].clone()
+            chosen.append(int(cand[b]))
+            costs = newc[b]
+        C = samples[chosen].clone()
     assign = torch.full((n,), -1, dtype=torch.int64, device=samples.device)
     for _ in range(max_iter):
         a = pairwise_distance(samples, C, dist_type).argmin(1)
-        converged = bool(torch.equal(a, assign))
+        if samples.is_cuda:
+            # one-hot fp64 GEMM: a fixed summation order (device index_add_ sums by atomics in any order)
+            oh = (a[None, :] == torch.arange(k, device=a.device)[:, None]).to(torch.float64)
+            S = oh @ (samples * w[:, None])
+            cnt = oh @ w
+        else:
+            S = torch.zeros_like(C)
+            S.index_add_(0, a, samples * w[:, None])
+            cnt = torch.zeros(k, dtype=torch.float64, device=samples.device).index_add_(0, a, w)
+        live = cnt > 0
+        flags = torch.stack([(a != assign).any(), (~live).any()]).cpu()
+        changed, any_empty = bool(flags[0]), bool(flags[1])
         assign = a
-        S = torch.zeros_like(C)
-        S.index_add_(0, a, samples * w[:, None])
-        cnt = torch.zeros(k, dtype=torch.float64, device=samples.device).index_add_(0, a, w)
-        for c in range(k):
-            if cnt[c] > 0:
-                C[c] = S[c] / cnt[c]
-            else:
+        C = torch.where(live[:, None], S / torch.where(live, cnt, torch.ones_like(cnt))[:, None], C)
+        if any_empty:
+            for c in np.flatnonzero(~live.cpu().numpy()).tolist():
                 C[c] = samples[int(rng.integers(n))]
         if dist_type.upper() == "COSINE":
             C = _normalize_rows(C)
-        if converged:
+        if not changed:
             break
     return C
 
@@ -308,17 +363,22 @@ def kmeans_init(X: torch.Tensor, k: int, init_mode: str, init_steps: int, dist_t
     centers = _fetch_global_rows(X, [int(rng.integers(n))], counts)
     cost = _min_dist_to(X, centers, dist_type)
     first_row = int(sum(counts[:comm.get_rank()]))
-    for rnd in range(max(0, init_steps - 1)):
+    rounds = max(0, init_steps - 1)
+    for rnd in range(rounds):
         tot = torch.tensor([float(cost.sum().item())], dtype=torch.float64)
         comm.all_reduce(tot)
         thre = 2.0 * k / max(float(tot.item()), 1e-300)
-        u = _row_uniform(first_row, X.shape[0], seed, rnd, X.device)
-        pick = torch.nonzero(u < cost * thre).reshape(-1)
+        if cost.is_cuda and _lib.available():
+            pick = kops.par_pick_hip(cost, first_row, _round_key(seed, rnd), thre)
+        else:
+            u = _row_uniform(first_row, X.shape[0], seed, rnd, X.device)
+            pick = torch.nonzero(u < cost * thre).reshape(-1)
         new = comm.all_gather_varlen(X[pick].to(torch.float64))   # rank order == global row order
         if new.shape[0] == 0:
             continue
         centers = torch.cat([centers, new])
-        cost = torch.minimum(cost, _min_dist_to(X, new, dist_type))
+        if rnd + 1 < rounds:           # the last round's costs would never be read: no pass over X for them
+            cost = torch.minimum(cost, _min_dist_to(X, new, dist_type))
     if centers.shape[0] <= k:
         return centers
     near = _nearest(X, centers, dist_type)
@@ -353,7 +413,7 @@ class KMeansAssignCluster(ComputeFunction):
         if X is None or X.shape[0] == 0:
             buf = torch.zeros((k, C.shape[1] + 1), dtype=torch.float64, device=C.device)
         else:
-            buf = kops.assign_accumulate(X, C)
+            buf = kops.assign_accumulate(X, C, reverse=kops.serpentine_reverse(ctx.getStepNo()))
         ctx.putObj(CENTROID_ALL_REDUCE, buf)
 
 
@@ -395,7 +455,8 @@ class KMeansUpdateCentroids(ComputeFunction):
                        and X is not None and X.shape[0] > 0 and kops.hip_supported(X, buf.shape[0]))
             C, read = kops.update_centroids_hip(buf, prev, deferred=True)
             if spec_ok:
-                ctx.putObj(SPEC_BUF, ((step + 1, kops._ckey(C)), kops.assign_accumulate_hip(X, C)))
+                ctx.putObj(SPEC_BUF, ((step + 1, kops._ckey(C)),
+                                      kops.assign_accumulate_hip(X, C, reverse=kops.serpentine_reverse(step + 1))))
             shift, has_empty = read()
             if has_empty:
                 ctx.removeObj(SPEC_BUF)

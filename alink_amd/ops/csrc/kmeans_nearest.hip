@@ -159,9 +159,116 @@ int launch(const void* X, int64_t N, const void* C, const float* chalf, int m, i
     return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
+// k-means|| oversampling draw (KMeansInitCentroids.java: every row is a candidate with probability
+// 2k * cost / sum(cost)): row i of this rank is picked when u(first_row + i) < cost[i] * thre, u being the
+// counter-based splitmix64 uniform of the GLOBAL row index (models/clustering/kmeans.py _row_uniform, bit for
+// bit: the same 64-bit wrapping products and the same double rounding), so every partitioning picks the same
+// rows.  Picked local indices go to out[] in arbitrary order (the caller sorts them); *count receives the number
+// of picks (it may exceed cap: then only cap are stored and the caller redoes the draw).
+__global__ __launch_bounds__(256) void kmeans_par_pick_kernel(const double* __restrict__ cost, int64_t n,
+                                                              int64_t first_row, uint64_t key, double thre,
+                                                              int64_t* __restrict__ out, int64_t cap,
+                                                              unsigned long long* __restrict__ count) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        uint64_t z = (uint64_t)(first_row + i) * 0x2545F491ull + key;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        z = z ^ (z >> 31);
+        const double u = ((double)(z >> 11) + 0.5) * (1.0 / 9007199254740992.0);
+        if (u < cost[i] * thre) {
+            const unsigned long long pos = atomicAdd(count, 1ull);
+            if ((int64_t)pos < cap) out[pos] = i;
+        }
+    }
+}
+
+// The reference seeding rule over the k-means|| candidates (LocalKmeansFunc.sampleInitialCentroids,
+// LocalKmeansFunc.java:36-86) in ONE workgroup: picks 1..k-1, each = the first candidate whose cumulative
+// weight x cost reaches U[j-1] x total (numpy/torch searchsorted, side left), then cost = min(cost, D[pick]).
+// costs and the cumulative sums live in LDS (n <= SEED_NMAX); the prefix sum is sequential within each thread's
+// contiguous chunk and a fixed-order scan across threads (deterministic).  *mintot receives the smallest total
+// seen (<= 0 means some pick had nothing left to sample: the caller redoes the picks on the host).
+constexpr int SEED_NMAX = 4096;
+constexpr int SEED_T = 512;
+
+__global__ __launch_bounds__(SEED_T) void kmeans_seed_ref_kernel(const double* __restrict__ D,
+                                                                 const double* __restrict__ w,
+                                                                 const double* __restrict__ U, int n, int k, int idx0,
+                                                                 int64_t* __restrict__ chosen,
+                                                                 double* __restrict__ mintot) {
+    __shared__ double costs[SEED_NMAX];
+    __shared__ double cw[SEED_NMAX];
+    __shared__ double tsum[SEED_T];
+    __shared__ int cnt;
+    const int t = threadIdx.x;
+    const int per = (n + SEED_T - 1) / SEED_T;
+    const int lo = t * per < n ? t * per : n;
+    const int hi = lo + per < n ? lo + per : n;
+    for (int i = t; i < n; i += SEED_T) costs[i] = D[(int64_t)idx0 * n + i];
+    if (t == 0) chosen[0] = idx0;
+    double mt = 1.0 / 0.0;
+    __syncthreads();
+    for (int j = 1; j < k; ++j) {
+        double run = 0.0;
+        for (int i = lo; i < hi; ++i) {
+            run += w[i] * costs[i];
+            cw[i] = run;
+        }
+        tsum[t] = run;
+        if (t == 0) cnt = 0;
+        __syncthreads();
+        // inclusive scan of the thread totals (Hillis-Steele, fixed order)
+        for (int off = 1; off < SEED_T; off <<= 1) {
+            const double v = t >= off ? tsum[t - off] : 0.0;
+            __syncthreads();
+            tsum[t] += v;
+            __syncthreads();
+        }
+        const double base = t > 0 ? tsum[t - 1] : 0.0;
+        const double tot = tsum[SEED_T - 1];
+        const double target = U[j - 1] * tot;
+        mt = tot < mt ? tot : mt;
+        int c = 0;
+        for (int i = lo; i < hi; ++i) c += (base + cw[i]) < target;
+        if (c) atomicAdd(&cnt, c);
+        __syncthreads();
+        const int pick = cnt < n - 1 ? cnt : n - 1;
+        if (t == 0) chosen[j] = pick;
+        for (int i = t; i < n; i += SEED_T) {
+            const double dv = D[(int64_t)pick * n + i];
+            costs[i] = dv < costs[i] ? dv : costs[i];
+        }
+        __syncthreads();
+    }
+    if (t == 0) *mintot = mt;
+}
+
 }  // namespace
 
 extern "C" {
+
+// reference-rule k-means++ picks over n <= 4096 candidates (kmeans_seed_ref_kernel): D [n][n], w [n], U [k-1]
+int alink_kmeans_seed_ref(const double* D, const double* w, const double* U, int n, int k, int idx0, int64_t* chosen,
+                          double* mintot, void* stream) {
+    if (n < 1 || n > SEED_NMAX || k < 1 || idx0 < 0 || idx0 >= n) return 1;
+    hipLaunchKernelGGL(kmeans_seed_ref_kernel, dim3(1), dim3(SEED_T), 0, reinterpret_cast<hipStream_t>(stream), D, w,
+                       U, n, k, idx0, chosen, mintot);
+    return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+// k-means|| oversampling picks of this rank's rows (kmeans_par_pick_kernel); *count must be zero on entry
+int alink_kmeans_par_pick(const double* cost, int64_t n, int64_t first_row, int64_t key, double thre, int64_t* out,
+                          int64_t cap, void* count, void* stream) {
+    if (n < 0 || cap < 0) return 1;
+    if (n == 0) return 0;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    int64_t blocks = (n + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(kmeans_par_pick_kernel, dim3((unsigned)blocks), dim3(256), 0, st, cost, n, first_row,
+                       (uint64_t)key, thre, out, cap, reinterpret_cast<unsigned long long*>(count));
+    return hipGetLastError() == hipSuccess ? 0 : 2;
+}
 
 // one chunk (m <= 256) of nearest-centroid search; grid = persistent workgroups
 int alink_kmeans_nearest_bf16(const void* X, int64_t N, int D, const void* C, const float* chalf, int m, int c0,

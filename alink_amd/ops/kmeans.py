@@ -108,6 +108,8 @@ V7_VAR = int(os.environ.get("ALINK_KMEANS_V7_VAR", "1"))
 # although the load pipeline alone streams faster with nt
 V10_FLAGS = int(os.environ.get("ALINK_KMEANS_V10_FLAGS", "1"))
 V10_KMAX = 112
+# serpentine tile order across Lloyd supersteps (serpentine_reverse)
+SERPENTINE = os.environ.get("ALINK_KMEANS_SERPENTINE", "1") != "0"
 
 
 def kernel_version(k: int = 100) -> str:
@@ -136,11 +138,14 @@ def _num_cus(device) -> int:
 
 
 def assign_accumulate_hip(X: torch.Tensor, C: torch.Tensor, grid: Optional[int] = None,
-                          assign_out: Optional[torch.Tensor] = None, mode: int = 0) -> torch.Tensor:
+                          assign_out: Optional[torch.Tensor] = None, mode: int = 0,
+                          reverse: bool = False) -> torch.Tensor:
     """[k, d+1] fp64 sums|counts of this rank's rows (``csrc/kmeans_v10.hip`` for k <= 112, else
     ``csrc/kmeans_v7.hip``: role-split waves on 16x16x32 MFMA, LDS-DMA tile ring; ``kernel_version``).
     ``assign_out`` (int32 [N]) also receives every row's centroid id; ``mode`` 1/2 are the kernel's load-only /
-    compute-only diagnostics (results meaningless)."""
+    compute-only diagnostics (results meaningless).  ``reverse`` (v10): every workgroup walks its rows backwards —
+    Lloyd alternates it per superstep (serpentine order), so a pass starts on the rows the previous pass read last,
+    which are still in the Infinity Cache.  Same assignments and counts; the fp32 sums differ only in order."""
     global HIP_CALLS
     L = _lib.require()
     HIP_CALLS += 1
@@ -167,6 +172,8 @@ def assign_accumulate_hip(X: torch.Tensor, C: torch.Tensor, grid: Optional[int] 
     st = _lib.stream_ptr(dev)
     if mode < 16:
         mode |= (V7_VAR << 4) if ver == "v7" else (V10_FLAGS << 4)
+    if reverse and ver == "v10":
+        mode |= 32
     rc = getattr(L, f"alink_kmeans_assign_accum_bf16_{ver}")(
         X.data_ptr(), n, cpad.data_ptr(), ninit.data_ptr(), k, slab.data_ptr(), slab_cnt.data_ptr(), grid, st,
         None if assign_out is None else assign_out.data_ptr(), int(mode))
@@ -460,10 +467,18 @@ def assign_accumulate_general_hip(X: torch.Tensor, C: torch.Tensor,
     return accumulate_by_index_hip(X, idx, C.shape[0], weights)
 
 
-def assign_accumulate(X: torch.Tensor, C: torch.Tensor, weights: Optional[torch.Tensor] = None) -> torch.Tensor:
+def serpentine_reverse(step: int) -> bool:
+    """Lloyd's walk direction at superstep ``step`` (1-based): with ``ALINK_KMEANS_SERPENTINE`` on (default),
+    even supersteps walk every workgroup's rows backwards (``assign_accumulate_hip(reverse=...)``).  A function of
+    the step only, so a run is reproducible and a speculative next-step launch uses the direction of its step."""
+    return SERPENTINE and step % 2 == 0
+
+
+def assign_accumulate(X: torch.Tensor, C: torch.Tensor, weights: Optional[torch.Tensor] = None,
+                      reverse: bool = False) -> torch.Tensor:
     hip_ok = _lib.available() or not _lib.torch_fallback_allowed()
     if weights is None and hip_supported(X, C.shape[0]) and hip_ok:
-        return assign_accumulate_hip(X, C)
+        return assign_accumulate_hip(X, C, reverse=reverse)
     if general_supported(X, C.shape[0]) and hip_ok:
         return assign_accumulate_general_hip(X, C, weights)
     if f32_supported(X, C.shape[0]) and hip_ok:
@@ -501,6 +516,29 @@ NEAREST_CHUNK = 256
 def nearest_supported(X: torch.Tensor) -> bool:
     return (X.is_cuda and X.dtype == torch.bfloat16 and X.dim() == 2 and X.shape[1] in NEAREST_DIMS
             and X.shape[0] > 0 and X.is_contiguous() and X.data_ptr() % 16 == 0)
+
+
+def par_pick_hip(cost: torch.Tensor, first_row: int, key: int, thre: float) -> torch.Tensor:
+    """k-means|| oversampling draw in one launch (``csrc/kmeans_nearest.hip`` ``kmeans_par_pick_kernel``): the
+    sorted local indices i with ``u(first_row + i) < cost[i] * thre`` — the same picks, bit for bit, as the torch
+    expression over ``models/clustering/kmeans._row_uniform`` (splitmix64 of the global row index, ``key`` being
+    its signed 64-bit round key), without materialising the [N] uniforms.  One 8-byte read for the pick count."""
+    L = _lib.require()
+    dev = cost.device
+    n = int(cost.shape[0])
+    cost = cost.contiguous()
+    cap = 4096
+    while True:
+        out = torch.empty(cap, dtype=torch.int64, device=dev)
+        cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+        rc = L.alink_kmeans_par_pick(cost.data_ptr(), n, int(first_row), int(key), float(thre), out.data_ptr(),
+                                     cap, cnt.data_ptr(), _lib.stream_ptr(dev))
+        if rc != 0:
+            raise RuntimeError(f"alink_kmeans_par_pick failed: {rc}")
+        c = int(cnt.item())
+        if c <= cap:
+            return torch.sort(out[:c]).values
+        cap = c
 
 
 def nearest_hip(X: torch.Tensor, C: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:

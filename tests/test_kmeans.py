@@ -189,3 +189,70 @@ def test_update_sum_matrix_reference():
     for i in range(10):
         X[i, i % 3] = i * i
     assert assign_accumulate_torch(X, C).flatten().tolist() == [117.0, 65.0, 89.0, 6.0, 9.0, 1.0, 4.0, 4.0]
+
+
+def _host_loop_local_kmeans(samples, weights, k, dist_type, max_iter=30, seed=0):
+    """The per-pick / per-centroid host loop _local_kmeans replaced (reference seeding rule), kept verbatim as the
+    oracle of the device-resident version."""
+    import torch
+    from alink_amd.models.clustering.kmeans import pairwise_distance, _normalize_rows
+    rng = np.random.default_rng(seed)
+    n = samples.shape[0]
+    w = weights.to(torch.float64)
+    D = pairwise_distance(samples, samples, dist_type)
+    cum = torch.cumsum(w, 0).cpu().numpy()
+    idx = int(min(np.searchsorted(cum, rng.random() * cum[-1], side="left"), n - 1))
+    chosen = [idx]
+    costs = D[idx].clone()
+    for _ in range(1, k):
+        cw = torch.cumsum(w * costs, 0).cpu().numpy()
+        tot = cw[-1]
+        if tot <= 0:
+            cand = rng.integers(n, size=1)
+        else:
+            cand = np.minimum(np.searchsorted(cw, rng.random(1) * tot, side="left"), n - 1)
+        cand_t = torch.as_tensor(cand, device=samples.device)
+        newc = torch.minimum(costs[None, :], D[cand_t])
+        b = int((newc * w[None, :]).sum(1).argmin().item())
+        chosen.append(int(cand[b]))
+        costs = newc[b]
+    C = samples[chosen].clone()
+    assign = torch.full((n,), -1, dtype=torch.int64, device=samples.device)
+    for _ in range(max_iter):
+        a = pairwise_distance(samples, C, dist_type).argmin(1)
+        converged = bool(torch.equal(a, assign))
+        assign = a
+        S = torch.zeros_like(C)
+        S.index_add_(0, a, samples * w[:, None])
+        cnt = torch.zeros(k, dtype=torch.float64, device=samples.device).index_add_(0, a, w)
+        for c in range(k):
+            if cnt[c] > 0:
+                C[c] = S[c] / cnt[c]
+            else:
+                C[c] = samples[int(rng.integers(n))]
+        if dist_type.upper() == "COSINE":
+            C = _normalize_rows(C)
+        if converged:
+            break
+    return C
+
+
+@pytest.mark.parametrize("n,k,dist,dup", [(220, 20, "EUCLIDEAN", False), (60, 25, "EUCLIDEAN", True),
+                                          (150, 10, "COSINE", False), (12, 12, "EUCLIDEAN", True)])
+def test_local_kmeans_device_resident_equals_host_loop(n, k, dist, dup, monkeypatch):
+    """The device-resident reference-rule seeding + Lloyd (no per-pick / per-centroid host reads) returns exactly
+    the centroids of the old host loop, including when picks exhaust the distinct candidates (all-zero totals:
+    duplicated rows) and when Lloyd empties clusters (refilled from the same generator draws)."""
+    import torch
+    from alink_amd.models.clustering import kmeans as km
+    monkeypatch.delenv("ALINK_KMEANS_SEEDING", raising=False)
+    g = torch.Generator().manual_seed(n + k)
+    X = torch.randn(n, 6, generator=g, dtype=torch.float64)
+    if dup:
+        X = torch.cat([X[: n // 3]] * 3 + [X[: n - 3 * (n // 3)]])
+    if dist == "COSINE":
+        X = km._normalize_rows(X)
+    w = torch.randint(1, 9, (n,), generator=g).to(torch.float64)
+    got = km._local_kmeans(X, w, k, dist, seed=3)
+    ref = _host_loop_local_kmeans(X, w, k, dist, seed=3)
+    assert torch.equal(got, ref)

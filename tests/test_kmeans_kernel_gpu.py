@@ -274,3 +274,66 @@ def test_speculative_next_step_launch_gives_identical_model():
                              sync_steps=range(100))
         assert len(qa.stats) == len(qb.stats)
         assert [list(r) for r in a] == [list(r) for r in b]
+
+
+@pytest.mark.parametrize("n,k,grid", [(300001, 100, None), (49157, 97, 3), (4097, 16, None), (129, 50, 1),
+                                      (70001, 112, 5)])
+def test_v10_serpentine_reverse_order(n, k, grid):
+    """The serpentine (reverse) walk visits the same rows: identical assignments and counts, sums equal up to the
+    fp32 summation order; and the reverse launch is itself deterministic."""
+    from alink_amd.ops import kmeans as K
+    X, C = _data(n, k, seed=21)
+    fa = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+    ra = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+    f = K.assign_accumulate_hip(X, C, grid=grid, assign_out=fa)
+    r = K.assign_accumulate_hip(X, C, grid=grid, assign_out=ra, reverse=True)
+    r2 = K.assign_accumulate_hip(X, C, grid=grid, reverse=True)
+    assert K.kernel_version(k) == "v10"
+    assert torch.equal(fa, ra)
+    assert torch.equal(f[:, 128], r[:, 128])
+    assert torch.equal(r, r2)
+    _own_assignment_check(X, C, r, ra, k)
+
+
+@pytest.mark.parametrize("n,first_row,rnd", [(1, 0, 0), (1000, 0, 0), (300001, 12345, 1), (2_000_003, 10**9, 3)])
+def test_par_pick_kernel_equals_torch_draw(n, first_row, rnd):
+    """k-means|| oversampling picks of the HIP kernel are bit-for-bit the torch expression's (same splitmix64
+    uniforms of the global row index, same fp64 threshold compare), including more picks than the first cap."""
+    from alink_amd.models.clustering import kmeans as km
+    from alink_amd.ops import kmeans as K
+    g = torch.Generator(device="cpu").manual_seed(n)
+    cost = (torch.rand(n, generator=g, dtype=torch.float64) * 3).cuda()
+    for thre in (200.0 / float(cost.sum()), 9000.0 / float(cost.sum())):
+        got = K.par_pick_hip(cost, first_row, km._round_key(7, rnd), thre)
+        u = km._row_uniform(first_row, n, 7, rnd, cost.device)
+        ref = torch.nonzero(u < cost * thre).reshape(-1)
+        assert torch.equal(got, ref)
+
+
+def test_local_kmeans_device_resident_equals_host_loop_on_gpu():
+    """The device-resident k-means++ seeding + Lloyd on the GPU agrees with the host loop and is deterministic."""
+    import numpy as np  # noqa: F401
+    from alink_amd.models.clustering import kmeans as km
+    from tests.test_kmeans import _host_loop_local_kmeans
+    g = torch.Generator(device="cpu").manual_seed(5)
+    X = torch.randn(230, 128, generator=g, dtype=torch.float64).cuda()
+    w = torch.randint(1, 50, (230,), generator=g).to(torch.float64).cuda()
+    got = km._local_kmeans(X, w, 100, "EUCLIDEAN", seed=1)
+    # the host loop's device index_add_ sums in atomic order: equal up to fp64 rounding
+    assert torch.allclose(got, _host_loop_local_kmeans(X, w, 100, "EUCLIDEAN", seed=1), rtol=1e-12, atol=1e-12)
+    assert torch.equal(got, km._local_kmeans(X, w, 100, "EUCLIDEAN", seed=1))          # deterministic
+
+
+@pytest.mark.parametrize("n,k", [(2, 2), (230, 100), (1000, 300), (4096, 50)])
+def test_seed_ref_kernel_equals_torch_loop(n, k):
+    """The one-workgroup seeding kernel picks the same candidates as the per-pick torch loop (run on the host)."""
+    import numpy as np
+    from alink_amd.models.clustering import kmeans as km
+    g = torch.Generator(device="cpu").manual_seed(n)
+    S = torch.randn(n, 16, generator=g, dtype=torch.float64)
+    D = km.pairwise_distance(S, S, "EUCLIDEAN")
+    w = torch.randint(1, 30, (n,), generator=g).to(torch.float64)
+    a = km._seed_reference_device(D.cuda(), w.cuda(), k, np.random.default_rng(4), 0)
+    b = km._seed_reference_device(D, w, k, np.random.default_rng(4), 0)
+    assert a is not None and b is not None
+    assert torch.equal(a.cpu(), b)

@@ -7,6 +7,8 @@
 #   d16      : -DKM10_ACC_B32=0 (two ds_read_u16_d16_hi + two v_add_f32 per row; the default before round 4)
 #   dot2     : -DKM10_ACC_B32=1 + body "dot2" (ds_read_b32 + 2 v_dot2_f32_bf16 per row; the default now)
 #   dot2pair : dot2 + pair
+#   timing   : -DKM10_TIMING=1 (per-workgroup wall-clock stamps; tools/kmeans_wg_timing.py).  `... timing` builds
+#              only this one
 set -e
 cd "$(dirname "$0")/.."
 mkdir -p variants
@@ -21,9 +23,11 @@ build_var() {
   objs=$(ls build/hip/*.o | grep -v kmeans_v10)
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "variants/libalink_hip_$name.so" $objs "$d/kmeans_v10.o"
 }
+[ "$1" = timing ] && { build_var timing base "-DKM10_TIMING=1"; exit 0; }
 build_var d16 base "-DKM10_ACC_B32=0"
 build_var pk pk "-DKM10_ACC_B32=0"
 build_var pair base "-DKM10_ACC_B32=0 -DKM10_PAIRMAX=1"
 build_var pkpair pk "-DKM10_ACC_B32=0 -DKM10_PAIRMAX=1"
 build_var dot2 dot2 "-DKM10_ACC_B32=1"
 build_var dot2pair dot2 "-DKM10_ACC_B32=1 -DKM10_PAIRMAX=1"
+build_var timing base "-DKM10_TIMING=1"

@@ -51,13 +51,20 @@ def main():
         Xs = X[:rows]
         for cfg in a.configs.split(","):
             ver, flags = cfg.split(":")
+            alt = flags.endswith("a")          # "v10:1a": serpentine, the direction alternates every launch
+            flags = flags.rstrip("a")
             os.environ["ALINK_KMEANS_KERNEL"] = ver
             for m in [int(v) for v in a.modes.split(",")]:
+                calls = [0]
+
                 def run():
-                    return K.assign_accumulate_hip(Xs, C, grid=a.grid, mode=m | (int(flags) << 4))
+                    calls[0] += 1
+                    return K.assign_accumulate_hip(Xs, C, grid=a.grid, mode=m | (int(flags) << 4),
+                                                   reverse=alt and calls[0] % 2 == 1)
                 out = run()
                 torch.cuda.synchronize()
-                res = {"rows": rows, "k": k, "kernel": K.kernel_version(k), "flags": int(flags), "mode": m}
+                res = {"rows": rows, "k": k, "kernel": K.kernel_version(k), "flags": int(flags), "mode": m,
+                       "serpentine": alt}
                 if m == 0 and rows == n:
                     if ref_small is None:
                         ref_small = K.assign_accumulate_torch(X[:2_000_000], C)

@@ -14,6 +14,7 @@ def main():
     ap.add_argument("--top", type=int, default=25)
     ap.add_argument("--match", default=None)
     ap.add_argument("--timeline", default=None)
+    ap.add_argument("--steady", type=int, default=40, help="periods of the --timeline kernel to summarise")
     a = ap.parse_args()
     c = sqlite3.connect(a.db)
     cols = [r[1] for r in c.execute("pragma table_info(kernels)")]
@@ -36,6 +37,15 @@ def main():
             print(f"\ntimeline between the last two '{a.timeline}' launches (offset_us, dur_us, kernel):")
             for k in ks[i0:i1 + 1]:
                 print(f"  {(k[1] - t0) / 1e3:10.1f} {(k[2] - k[1]) / 1e3:9.1f}  {k[0][:100]}")
+            # steady state over the last launches: anchor duration, launch-to-launch period, time outside it
+            last = anchors[-min(len(anchors), a.steady + 1):]
+            if len(last) >= 3:
+                durs = sorted((ks[i][2] - ks[i][1]) / 1e3 for i in last[:-1])
+                pers = sorted((ks[j][1] - ks[i][1]) / 1e3 for i, j in zip(last[:-1], last[1:]))
+                med = lambda v: v[len(v) // 2]  # noqa: E731
+                print(f"\nsteady state over the last {len(last) - 1} '{a.timeline}' periods: kernel median "
+                      f"{med(durs):.1f} us (min {durs[0]:.1f}, max {durs[-1]:.1f}), period median {med(pers):.1f} us "
+                      f"(min {pers[0]:.1f}, max {pers[-1]:.1f}), outside the kernel {med(pers) - med(durs):.1f} us")
 
 
 if __name__ == "__main__":
