@@ -13,7 +13,7 @@ import numpy as np
 
 __all__ = ["lib", "parse_csv_lines", "murmur3_utf16", "murmur3_bytes", "murmur3_utf8", "parse_dense_vectors", "ftrl_update_csr",
            "ftrl_partial_margin", "ftrl_shard_update", "parse_binary_detail", "java_double_join",
-           "java_double_rows", "sample_thresholds"]
+           "java_double_rows", "sample_thresholds", "gbdt_rank_grad"]
 
 # ALINK_NATIVE_LIB points at another build of the same sources (e.g. the AddressSanitizer build of
 # tools/asan_host.py)
@@ -41,6 +41,8 @@ if os.path.exists(_PATH):
             lib.alink_sample_thresholds.restype = ctypes.c_int64
         if hasattr(lib, "alink_binary_bins"):
             lib.alink_binary_bins.restype = None
+        if hasattr(lib, "alink_gbdt_rank_grad_host"):
+            lib.alink_gbdt_rank_grad_host.restype = ctypes.c_int
     except OSError:
         lib = None
 
@@ -185,6 +187,25 @@ def sample_thresholds(thr, step: float, err: float) -> Optional[np.ndarray]:
     m = lib.alink_sample_thresholds(_ptr(a), ctypes.c_int64(a.size), ctypes.c_double(step), ctypes.c_double(err),
                                     _ptr(keep))
     return keep[:m]
+
+
+def gbdt_rank_grad(pred: np.ndarray, gain: np.ndarray, offsets: np.ndarray, disc: np.ndarray, algo: int):
+    """(g, h) float32 of the GBDT learning-to-rank losses (algo 2 LambdaMART-NDCG, 3 LambdaMART-DCG, 4 GBRank)
+    over contiguous queries ``offsets`` (int64 [Q+1]) — the reference's pair loop in C++ (``csrc/gbdt_rank.cpp``,
+    the host twin of ``ops/csrc/gbdt_rank.hip``); None without the library."""
+    if lib is None or getattr(lib, "alink_gbdt_rank_grad_host", None) is None:
+        return None
+    p = np.ascontiguousarray(pred, dtype=np.float32)
+    y = np.ascontiguousarray(gain, dtype=np.float32)
+    off = np.ascontiguousarray(offsets, dtype=np.int64)
+    d = np.ascontiguousarray(disc, dtype=np.float32)
+    g = np.zeros(p.size, dtype=np.float32)
+    h = np.zeros(p.size, dtype=np.float32)
+    rc = lib.alink_gbdt_rank_grad_host(_ptr(p), _ptr(y), _ptr(off), ctypes.c_int64(off.size - 1), _ptr(d),
+                                       ctypes.c_int(algo), _ptr(g), _ptr(h))
+    if rc != 0:
+        raise RuntimeError(f"alink_gbdt_rank_grad_host failed: {rc}")
+    return g, h
 
 
 def binary_bins(probs: np.ndarray, c0: int, c1: int, code: np.ndarray, ok: Optional[np.ndarray], B: int,

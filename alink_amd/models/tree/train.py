@@ -3,7 +3,9 @@
 Reference: ``A/operator/common/tree/BaseGbdtTrainBatchOp.java`` (params, depth from ``maxLeaves``
 ``:255-263``, label handling, model meta ``:265-300``, feature-importance side output ``:230-236``),
 ``parallelcart/ConstructLocalBin.java`` (gradients: least squares ``g = pred - (y - mean)``, ``h = 1``
-``:105-131``; logistic ``g = p - y``, ``h = p(1-p)`` with float32 storage ``:170-205``),
+``:105-131``; logistic ``g = p - y``, ``h = p(1-p)`` with float32 storage ``:170-205``; learning to rank
+``algoType`` 2 LambdaMART-NDCG / 3 LambdaMART-DCG / 4 GBRank over ``groupCol`` queries ``:296-430``, see
+``ops/csrc/gbdt_rank.hip``),
 ``parallelcart/Split.java`` (row / feature subsampling after every tree ``:100-160``) and
 ``BaseRandomForestTrainBatchOp.java`` (per-tree row sampling ``SampleData`` ``:470-503``, gain type per tree
 for ``treeType`` AVG/PARTITION ``:420-460``, model meta = the op params).
@@ -107,7 +109,14 @@ def train_gbdt(mt: MTable, params: Params, env, algo_type: int) -> Tuple[List[tu
     seed = int(_pget(params, "seed", 0))
     label_type = mt.col_type(label_col)
     labels = None
-    if algo_type == 1:
+    offsets = group_sample_idx = None
+    if algo_type >= 2:
+        mt, offsets, group_sample_idx = _rank_groups(mt, params, dev)
+        # InitialTrainningBuffer.java:221-224: the gain 2^min(label, 31) - 1, stored as float; no label centring
+        yd, _ = numeric_column(mt, label_col, dev)
+        y = (torch.pow(2.0, torch.clamp(yd, max=31.0)) - 1.0).to(torch.float32)
+        period = 0.0
+    elif algo_type == 1:
         labels = distinct_labels(mt, label_col)
         if len(labels) != 2:
             raise ValueError(f"Binary classification requires exactly 2 labels, found {len(labels)}")
@@ -139,18 +148,33 @@ def train_gbdt(mt: MTable, params: Params, env, algo_type: int) -> Tuple[List[tu
     roots = []
     fmask = np.ones(F, dtype=bool)
     for t in range(num_trees):
-        sample = (torch.rand(n, generator=row_gen, device=dev) < sub_ratio) if sub_ratio < 1.0 else \
-            torch.ones(n, dtype=torch.bool, device=dev)
+        if sub_ratio < 1.0 and group_sample_idx is not None:
+            # learning to rank samples whole queries (Split.java:142-153)
+            ng = int(offsets.numel()) - 1
+            sample = (torch.rand(ng, generator=row_gen, device=dev) < sub_ratio)[group_sample_idx]
+        else:
+            sample = (torch.rand(n, generator=row_gen, device=dev) < sub_ratio) if sub_ratio < 1.0 else \
+                torch.ones(n, dtype=torch.bool, device=dev)
         if feat_ratio < 1.0:   # InitialTrainningBuffer / Split draw a feature subset for every tree
             fmask = feat_rng.random(F) < feat_ratio
         # K6: {g*g, g, h, 1} row records in one fused pass (logistic g/h in fp64, weights applied in fp32)
-        stats = ew.gbdt_grad_stats(pred, y, w, 1 if algo_type == 1 else 0)
+        if algo_type >= 2:
+            # K6 ranking variant: per-query pair lambdas (ConstructLocalBin.java:296-430)
+            stats = ew.gbdt_rank_stats(pred, y, w, offsets, algo_type)
+        else:
+            stats = ew.gbdt_grad_stats(pred, y, w, 1 if algo_type == 1 else 0)
         root, codes, leaves = builder.build(stats, sample, fmask)
         roots.append(root)
         # Split.java: predBuf = (float) (curPred + leftCounter.sum / leftCounter.weightSum)
         vals = torch.tensor([lf.counter.distributions[0] if lf.counter and lf.counter.distributions else 0.0
                              for lf in leaves] or [0.0], dtype=torch.float64, device=dev)
-        pred = ew.gbdt_leaf_update(pred, codes.to(torch.int32), vals)
+        if algo_type == 4:
+            # GBRank keeps the running MEAN of the trees' outputs (Split.java:128-131, iterCount = t + 1)
+            leaf = (-1 - codes.long()).clamp(min=0, max=vals.numel() - 1)
+            inc = torch.where(codes < 0, vals[leaf], torch.zeros_like(vals[leaf]))
+            pred = ((t * pred.double() + inc) / (t + 1)).to(torch.float32)
+        else:
+            pred = ew.gbdt_leaf_update(pred, codes.to(torch.int32), vals)
     meta = params.clone()
     meta.set("featureCols", feature_cols).set("labelCol", label_col).set("categoricalCols", cat)
     meta.set("numTrees", num_trees).set("maxDepth", depth).set("algoType", algo_type)
@@ -166,6 +190,30 @@ def train_gbdt(mt: MTable, params: Params, env, algo_type: int) -> Tuple[List[tu
     info = {"numTrees": num_trees, "depth": depth, "bins": data.B, "binning_s": t_bin,
             "trees_s": time.perf_counter() - t_trees}
     return rows, conv, imp, info
+
+
+def _rank_groups(mt: MTable, params: Params, dev):
+    """Learning-to-rank layout (BaseGbdtTrainBatchOp.java:245-252, 431-446; InitialTrainningBuffer.java:157-235):
+    the rows of one query (``groupCol``, read as an integer like the reference's ``intValue()``) on one rank
+    (hash exchange), contiguous and in their input order.  Returns (the regrouped table, int64 [Q+1] query row
+    offsets, each row's query index)."""
+    from ...parallel.shuffle import hash_partition
+    gcol = _pget(params, "groupCol")
+    if gcol is None:
+        raise ValueError("learning to rank (algoType 2-4) needs groupCol")
+    mt = hash_partition(mt, [mt.schema.names.index(gcol)])
+    gv, gnull = numeric_column(mt, gcol, dev)
+    if bool(gnull.any()):
+        raise ValueError(f"groupCol {gcol} has null values")
+    gid = gv.to(torch.int64)                       # intValue(): truncation toward zero
+    order = torch.sort(gid, stable=True).indices
+    mt = mt.take(order)
+    gid = gid[order]
+    _, counts = torch.unique_consecutive(gid, return_counts=True)
+    offsets = torch.zeros(counts.numel() + 1, dtype=torch.int64, device=gid.device)
+    torch.cumsum(counts, 0, out=offsets[1:])
+    qidx = torch.repeat_interleave(torch.arange(counts.numel(), device=gid.device), counts)
+    return mt, offsets, qidx
 
 
 # ---------------------------------------------------------------------------------------------------

@@ -31,11 +31,21 @@ class _TreeTrainInfo(WithTrainInfo):
 
 
 class BaseGbdtTrainBatchOp(BatchOperator, _TreeTrainInfo):
+    """``algoType`` (the reference's public field, ``BaseGbdtTrainBatchOp.java:63-66``): 0 regression, 1 binary
+    classification, 2 LambdaMART-NDCG, 3 LambdaMART-DCG, 4 GBRank — the ranking losses need ``groupCol``
+    (query id).  Set it as ``op.algoType = 2`` or ``BaseGbdtTrainBatchOp(algoType=2)``."""
     ALGO_TYPE = 1
+
+    def __init__(self, params=None, algoType=None, **kw):
+        super().__init__(params, **kw)
+        self.algoType = self.ALGO_TYPE if algoType is None else int(algoType)
 
     def linkFrom(self, *inputs):
         mt = self.checkAndGetFirst(inputs).getOutputTable()
-        rows, conv, imp, info = train_gbdt(mt, self.getParams().clone(), self.env, self.ALGO_TYPE)
+        algo = int(getattr(self, "algoType", self.ALGO_TYPE))
+        if algo not in (0, 1, 2, 3, 4):
+            raise ValueError(f"algoType must be 0..4, got {algo}")
+        rows, conv, imp, info = train_gbdt(mt, self.getParams().clone(), self.env, algo)
         self._train_info = info
         self.setOutputTable(MTable.from_rows(rows, conv.getModelSchema(), replicated=True))
         self.setSideOutputTables([MTable.from_rows(imp, IMPORTANCE_SCHEMA, replicated=True)])

@@ -16,6 +16,7 @@ from __future__ import annotations
 
 from typing import Optional
 
+import numpy as np
 import torch
 
 from . import _lib
@@ -63,6 +64,54 @@ def gbdt_grad_stats(pred: torch.Tensor, y: torch.Tensor, w: Optional[torch.Tenso
     _check(L.alink_gbdt_grad_stats(pred.data_ptr(), y.data_ptr(), w.data_ptr() if w is not None else None, n,
                                    int(algo), out.data_ptr(), _lib.stream_ptr(pred.device)), "alink_gbdt_grad_stats")
     return out
+
+
+RANK_MAX_POSITION = 10000       # the reference's kMaxPosition (ConstructLocalBin.java:46): longest query
+_DISC = {}
+
+
+def dcg_discount(device) -> torch.Tensor:
+    """The reference's float discount table (float)(log 2 / log(2 + r)), r < 10000 (ConstructLocalBin.java:46-50)."""
+    key = str(device)
+    if key not in _DISC:
+        r = np.arange(RANK_MAX_POSITION, dtype=np.float64)
+        _DISC[key] = torch.from_numpy((np.log(2.0) / np.log(2.0 + r)).astype(np.float32)).to(device)
+    return _DISC[key]
+
+
+def gbdt_rank_stats(pred: torch.Tensor, gain: torch.Tensor, w: Optional[torch.Tensor], offsets: torch.Tensor,
+                    algo: int) -> torch.Tensor:
+    """K6 ranking variant: {g*g, g, h, 1} float32 row records of LambdaMART-NDCG (algo 2), LambdaMART-DCG (3) or
+    GBRank (4) over contiguous queries (``offsets`` int64 [Q+1], every query <= 10000 rows).  GPU: one workgroup
+    per query (``csrc/gbdt_rank.hip``); CPU: the reference's pair loop in C++ (``_native.gbdt_rank_grad``)."""
+    n = pred.numel()
+    assert pred.dtype == gain.dtype == torch.float32 and gain.numel() == n
+    sizes = offsets[1:] - offsets[:-1]
+    if sizes.numel() and int(sizes.max()) > RANK_MAX_POSITION:
+        raise ValueError(f"a query has more than {RANK_MAX_POSITION} rows (the reference's kMaxPosition)")
+    if _use_kernel(pred):
+        L = _lib.require()
+        pred, gain = pred.contiguous(), gain.contiguous()
+        off = offsets.to(device=pred.device, dtype=torch.int64).contiguous()
+        if w is not None:
+            w = w.to(torch.float32).contiguous()
+        out = torch.empty((n, 4), dtype=torch.float32, device=pred.device)
+        rs = torch.empty(n, dtype=torch.int32, device=pred.device)
+        ss = torch.empty(n, dtype=torch.float32, device=pred.device)
+        _check(L.alink_gbdt_rank_stats(pred.data_ptr(), gain.data_ptr(), None if w is None else w.data_ptr(),
+                                       off.data_ptr(), off.numel() - 1, dcg_discount(pred.device).data_ptr(),
+                                       int(algo), rs.data_ptr(), ss.data_ptr(), out.data_ptr(),
+                                       _lib.stream_ptr(pred.device)), "alink_gbdt_rank_stats")
+        return out
+    from .. import _native
+    res = _native.gbdt_rank_grad(pred.detach().cpu().numpy(), gain.detach().cpu().numpy(),
+                                 offsets.detach().cpu().numpy(), dcg_discount("cpu").numpy(), int(algo))
+    if res is None:
+        raise RuntimeError("GBDT ranking gradients need the host library (python build_native.py)")
+    g, h = (torch.from_numpy(a).to(pred.device) for a in res)
+    if w is not None:
+        g, h = g * w.to(torch.float32), h * w.to(torch.float32)
+    return torch.stack([g * g, g, h, torch.ones_like(g)], dim=1)
 
 
 def gbdt_leaf_update_torch(pred: torch.Tensor, codes: torch.Tensor, vals: torch.Tensor) -> torch.Tensor:

@@ -82,6 +82,22 @@ def scenario_gbdt(out):
     out["model"] = [list(r) for r in m.collect()]
 
 
+def scenario_gbdt_rank(out):
+    """LambdaMART-NDCG over queries spread across ranks: rows are exchanged so each query lives on one rank."""
+    import numpy as np
+    import pandas as pd
+    from alink_amd import useLocalEnv, BatchOperator, GbdtRegTrainBatchOp
+    useLocalEnv(1)
+    rng = np.random.default_rng(4)
+    X = rng.normal(size=(480, 3))
+    rel = np.clip(np.round(1.5 + X[:, 0] - 0.5 * X[:, 1]), 0, 3)
+    df = pd.DataFrame({"f0": X[:, 0], "f1": X[:, 1], "f2": X[:, 2], "qid": (np.arange(480) * 7) % 40, "rel": rel})
+    src = BatchOperator.fromDataframe(df, schemaStr="f0 double, f1 double, f2 double, qid int, rel double")
+    m = GbdtRegTrainBatchOp(algoType=int(os.environ.get("ALINK_TEST_ALGO", "2"))) \
+        .setFeatureCols(["f0", "f1", "f2"]).setLabelCol("rel").setGroupCol("qid").setNumTrees(4) \
+        .setMinSamplesPerLeaf(5).setMaxDepth(3).linkFrom(src)
+    out["model"] = [list(r) for r in m.collect()]
+
 def scenario_gbdt_wide(out):
     """7 continuous features (not a multiple of the world size): feature-sharded histograms with a padded block."""
     import numpy as np

@@ -78,7 +78,7 @@ def _tree_nodes(model_rows):
     return out
 
 
-@pytest.mark.parametrize("scenario", ["gbdt", "gbdt_wide", "rf", "rf_parallel", "rf_sampled"])
+@pytest.mark.parametrize("scenario", ["gbdt", "gbdt_wide", "rf", "rf_parallel", "rf_sampled", "gbdt_rank"])
 def test_trees_two_processes_equal_single(tmp_path, scenario):
     """Histogram all-reduce over 2 ranks (gbdt, rf_parallel) and tree-parallel forests (rf, rf_sampled: each rank
     grows its own trees on the all-gathered bins) give the same trees as one rank."""
