@@ -19,14 +19,18 @@ __all__ = ["DetailBlock"]
 
 class DetailBlock:
     """``n`` detail strings as ``labels`` (K label values, the mapper's order) and ``probs`` ([n, K] float64
-    numpy, ``probs[i, k]`` = probability of ``labels[k]``).  ``nulls`` (optional bool [n]) marks NULL rows."""
+    numpy, ``probs[i, k]`` = probability of ``labels[k]``).  ``nulls`` (optional bool [n]) marks NULL rows.
+    ``quoted``: the map's values are strings (``HashMap<String, String>``, linear / softmax mappers) or, when False,
+    JSON numbers (``HashMap<String, Double>``, the tree mappers) — both ``Double.toString`` of the probability."""
 
-    __slots__ = ("labels", "probs", "nulls", "_list")
+    __slots__ = ("labels", "probs", "nulls", "quoted", "_list")
 
-    def __init__(self, labels: Sequence[Any], probs: np.ndarray, nulls: Optional[np.ndarray] = None):
+    def __init__(self, labels: Sequence[Any], probs: np.ndarray, nulls: Optional[np.ndarray] = None,
+                 quoted: bool = True):
         self.labels = list(labels)
         self.probs = np.asarray(probs, dtype=np.float64).reshape(-1, len(self.labels))
         self.nulls = None if nulls is None or not np.any(nulls) else np.asarray(nulls, dtype=bool)
+        self.quoted = bool(quoted)
         self._list: Optional[List[Optional[str]]] = None
 
     def __len__(self) -> int:
@@ -35,7 +39,7 @@ class DetailBlock:
     def to_list(self) -> List[Optional[str]]:
         if self._list is None:
             from ..models.linear.model import _detail_json
-            out = _detail_json(self.labels, self.probs) if len(self) else []
+            out = _detail_json(self.labels, self.probs, self.quoted) if len(self) else []
             if self.nulls is not None:
                 out = [None if m else s for s, m in zip(out, self.nulls.tolist())]
             self._list = out
@@ -58,17 +62,17 @@ class DetailBlock:
             sel = np.asarray(idx)
             if sel.dtype != bool:
                 sel = sel.astype(np.int64)
-        return DetailBlock(self.labels, self.probs[sel], None if self.nulls is None else self.nulls[sel])
+        return DetailBlock(self.labels, self.probs[sel], None if self.nulls is None else self.nulls[sel], self.quoted)
 
     @staticmethod
     def concat(blocks: Sequence["DetailBlock"]) -> Optional["DetailBlock"]:
         """One block, or None when the blocks' label sets differ (the caller falls back to strings)."""
-        if not blocks or any(b.labels != blocks[0].labels for b in blocks):
+        if not blocks or any(b.labels != blocks[0].labels or b.quoted != blocks[0].quoted for b in blocks):
             return None
         nulls = None
         if any(b.nulls is not None for b in blocks):
             nulls = np.concatenate([b.nulls if b.nulls is not None else np.zeros(len(b), bool) for b in blocks])
-        return DetailBlock(blocks[0].labels, np.concatenate([b.probs for b in blocks]), nulls)
+        return DetailBlock(blocks[0].labels, np.concatenate([b.probs for b in blocks]), nulls, blocks[0].quoted)
 
     def __repr__(self):
         return f"DetailBlock(n={len(self)}, labels={self.labels})"

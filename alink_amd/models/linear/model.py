@@ -260,8 +260,9 @@ def _dev(mt: MTable):
     return torch.device("cpu")
 
 
-def _detail_json(labels: Sequence[Any], probs: np.ndarray) -> List[str]:
-    """HashMap<String,String> of label -> Double.toString(prob), Gson-serialised in Java HashMap order.
+def _detail_json(labels: Sequence[Any], probs: np.ndarray, quoted: bool = True) -> List[str]:
+    """HashMap<String,String> of label -> Double.toString(prob), Gson-serialised in Java HashMap order
+    (``quoted`` False: HashMap<String,Double>, the same digits as JSON numbers — the tree mappers' detail).
     Batched: every probability is formatted by the C++ Double.toString twin in one call and the rows are
     assembled from one per-table template (the keys and their order are the same on every row)."""
     from ... import _native
@@ -271,11 +272,14 @@ def _detail_json(labels: Sequence[Any], probs: np.ndarray) -> List[str]:
     cols = [keys.index(k) for k in order]
     body = _native.java_double_join(np.ascontiguousarray(probs[:, cols]).reshape(-1)) if probs.size else ""
     if body is None:
+        if not quoted:
+            return [gson_dumps({k: float(row[keys.index(k)]) for k in order}, java_map_order=True) for row in probs]
         return [gson_dumps({k: java_double_str(float(row[keys.index(k)])) for k in order}, java_map_order=True)
                 for row in probs]
     strs = body.split(",") if probs.size else []
     K = len(order)
-    tmpl = "{" + ",".join(gson_dumps(k).replace("%", "%%") + ':"%s"' for k in order) + "}"
+    val = ':"%s"' if quoted else ':%s'
+    tmpl = "{" + ",".join(gson_dumps(k).replace("%", "%%") + val for k in order) + "}"
     return [tmpl % tuple(strs[i * K:(i + 1) * K]) for i in range(probs.shape[0])]
 
 

@@ -122,7 +122,8 @@ def _node_from_json(d: dict) -> Node:
 
 
 def deserialize_tree(strings: Sequence[str]) -> Optional[Node]:
-    objs = [json.loads(s) for s in strings]
+    # one JSON document per tree (a list of its node objects) instead of one parse per node
+    objs = json.loads("[" + ",".join(strings) + "]") if strings else []
     size = len(objs)
     nodes: List[Optional[Node]] = [None] * size
     nexts: List[Optional[list]] = [None] * size
@@ -245,6 +246,72 @@ class _FlatForest:
         self.max_steps = len(feats) + 1
 
 
+class _DeviceForest:
+    """``_FlatForest`` as the tables of ``ops/csrc/tree_predict.hip``: every feature the forest splits on gets a
+    code slot; a continuous split stores the rank k of its threshold among that feature's sorted distinct
+    thresholds (x <= thr  <=>  code(x) <= k, code(x) = #thresholds < x), a categorical split -(map row)-1."""
+
+    def __init__(self, flat: "_FlatForest", cat_features: Sequence[int], cat_sizes: Sequence[int], device):
+        internal = flat.feat >= 0
+        used = sorted(set(flat.feat[internal].tolist()))
+        self.slot = {f: i for i, f in enumerate(used)}
+        self.cat_features = set(int(f) for f in cat_features)
+        ynode = np.zeros(len(flat.feat), dtype=np.int64)
+        self.thresholds: Dict[int, np.ndarray] = {}
+        widest = 0
+        for f in used:
+            sel = internal & (flat.feat == f)
+            if f in self.cat_features:
+                ynode[sel] = -flat.catrow[sel] - 1
+                widest = max(widest, int(cat_sizes[f]) if f < len(cat_sizes) else 0, flat.cat.shape[1])
+            else:
+                T = np.unique(flat.thr[sel])
+                self.thresholds[f] = T
+                ynode[sel] = np.searchsorted(T, flat.thr[sel])
+                widest = max(widest, len(T) + 1)
+        # code width: uint8 while every code and the MISS sentinel (255) stay apart
+        self.code_bytes = 1 if widest < 255 else (2 if widest < 65535 else 0)
+        self.supported = self.code_bytes > 0 and len(flat.roots) > 0
+        F = max(1, len(used))
+        self.stride = ((F * max(1, self.code_bytes) + 15) // 16) * 16
+        self.supported = self.supported and self.stride * 64 <= 160 * 1024
+        node_slot = np.where(internal, np.asarray([self.slot.get(int(f), -1) for f in flat.feat.tolist()]), -1)
+        nodes = np.stack([node_slot, ynode, np.where(internal, flat.first, 0), flat.nchild], 1).astype(np.int32)
+        self.dev = device
+        self.nodes = torch.from_numpy(np.ascontiguousarray(nodes)).to(device)
+        self.dist = torch.from_numpy(np.ascontiguousarray(flat.dist)).to(device)
+        self.nd = int(flat.dist.shape[1])
+        self.wsum = torch.from_numpy(np.ascontiguousarray(flat.wsum)).to(device)
+        self.cat = torch.from_numpy(np.ascontiguousarray(flat.cat.astype(np.int32))).to(device)
+        self.roots = torch.tensor(flat.roots, dtype=torch.int32, device=device)
+        # per continuous feature: thresholds padded with +inf into one [Fc, L] table for a batched searchsorted
+        self.cont = [f for f in used if f not in self.cat_features]
+        L = max([len(self.thresholds[f]) for f in self.cont] + [1])
+        Tp = np.full((max(1, len(self.cont)), L), np.inf)
+        for i, f in enumerate(self.cont):
+            Tp[i, :len(self.thresholds[f])] = self.thresholds[f]
+        self.T = torch.from_numpy(Tp).to(device)
+
+    def codes(self, cols: Dict[int, torch.Tensor], cat_codes: Dict[int, torch.Tensor], n: int) -> torch.Tensor:
+        """[n, stride] uint8 code rows (uint16 pairs when code_bytes is 2) from fp64 continuous columns (NaN =
+        missing) and int64 categorical indices (-1 = missing)."""
+        ct = torch.uint8 if self.code_bytes == 1 else torch.int16
+        miss = 255 if self.code_bytes == 1 else -1              # 0xFFFF as int16
+        out = torch.zeros((n, self.stride // self.code_bytes), dtype=ct, device=self.dev)
+        if self.cont:
+            X = torch.stack([cols[f] for f in self.cont])                                   # [Fc, n]
+            c = torch.searchsorted(self.T, X.contiguous())
+            c = torch.where(torch.isnan(X), torch.full_like(c, 65535), c)
+            idx = torch.tensor([self.slot[f] for f in self.cont], device=self.dev)
+            vals = torch.where(c >= 65535, torch.full_like(c, miss), c)
+            out[:, idx] = vals.T.to(ct)
+        for f in self.slot:
+            if f in self.cat_features:
+                v = cat_codes[f]
+                out[:, self.slot[f]] = torch.where(v < 0, torch.full_like(v, miss), v).to(ct)
+        return out
+
+
 class TreeModelMapper(RichModelMapper):
     """Shared tree prediction (``TreeModelMapper.java``): categorical columns through the embedded string
     indexer (unseen -> missing), continuous columns as doubles, weighted descent on missing values."""
@@ -289,18 +356,86 @@ class TreeModelMapper(RichModelMapper):
             return 1
         return len(r0.counter.distributions)
 
-    # -- feature matrix: X [n, F] float64 with NaN for missing; categorical as index (NaN if unseen) --
+    # -- feature columns, columnar: continuous -> fp64 (NaN = NULL), categorical -> indexer code (-1 = NULL/unseen) --
+    def _cont_column(self, mt, c, device) -> torch.Tensor:
+        col = mt.col(c)
+        v = col.values
+        if isinstance(v, torch.Tensor) and v.dim() == 1:
+            x = v.to(device=device, dtype=torch.float64)
+            if col.nulls is not None:
+                x = torch.where(col.nulls.to(device), torch.full_like(x, float("nan")), x)
+            return x
+        vals = mt.column_values(c)
+        return torch.tensor([np.nan if v is None else float(v) for v in vals], dtype=torch.float64, device=device)
+
+    def _cat_column(self, mt, c, device) -> torch.Tensor:
+        m = self.cat_maps.get(c, {})
+        vals = mt.column_values(c)
+        look = {v: m.get(java_str(v), -1) for v in set(vals) if v is not None}   # one indexer lookup per distinct
+        look[None] = -1
+        return torch.tensor([look[v] for v in vals], dtype=torch.int64, device=device)
+
     def _features(self, mt) -> np.ndarray:
+        """X [n, F] float64 with NaN for missing; categorical as index (NaN if unseen) — the host walk's input."""
         n = mt.num_rows
         X = np.empty((n, len(self.feature_cols)), dtype=np.float64)
         for j, c in enumerate(self.feature_cols):
-            vals = mt.column_values(c)
             if c in self.cat_cols:
-                m = self.cat_maps.get(c, {})
-                X[:, j] = [np.nan if v is None else m.get(java_str(v), np.nan) for v in vals]
+                x = self._cat_column(mt, c, "cpu").numpy().astype(np.float64)
+                X[:, j] = np.where(x < 0, np.nan, x)
             else:
-                X[:, j] = [np.nan if v is None else float(v) for v in vals]
+                X[:, j] = self._cont_column(mt, c, "cpu").numpy()
         return X
+
+    def _device(self, mt):
+        for c in self.feature_cols:
+            v = mt.col(c).values
+            if isinstance(v, torch.Tensor) and v.is_cuda:
+                return v.device
+        env = getattr(self, "env", None)
+        if env is None:
+            from ...common.mlenv import MLEnvironmentFactory
+            env = MLEnvironmentFactory.getDefault()
+        env_dev = getattr(env, "device", None)
+        return env_dev if env_dev is not None and torch.device(env_dev).type == "cuda" else None
+
+    def _accumulate_device(self, mt, flat: "_FlatForest", dev):
+        """(acc, wacc) on the GPU (``ops/csrc/tree_predict.hip``), or None when the forest does not fit the kernel
+        (code width / stack) — the caller then takes the host walk."""
+        from ...ops import _lib
+        dfo = getattr(self, "_dforest", None)
+        if dfo is None or dfo.dev != dev:
+            sizes = [len(self.cat_maps.get(c, {})) if c in self.cat_cols else 0 for c in self.feature_cols]
+            cat_idx = [j for j, c in enumerate(self.feature_cols) if c in self.cat_cols]
+            dfo = self._dforest = _DeviceForest(flat, cat_idx, sizes, dev)
+        if not dfo.supported:
+            return None
+        L = _lib.require()
+        n = mt.num_rows
+        cols = {f: self._cont_column(mt, self.feature_cols[f], dev) for f in dfo.cont}
+        cats = {f: self._cat_column(mt, self.feature_cols[f], dev) for f in dfo.slot if f in dfo.cat_features}
+        acc = torch.empty((n, dfo.nd), dtype=torch.float64, device=dev)
+        wacc = torch.empty(n, dtype=torch.float64, device=dev)
+        err = torch.zeros(1, dtype=torch.int32, device=dev)
+        # codes are built per chunk of rows (the batched searchsorted holds [features, rows] int64 temporaries)
+        chunk = max(64, ((1 << 27) // max(1, len(dfo.slot))) // 64 * 64)
+        for lo in range(0, n, chunk):
+            hi = min(n, lo + chunk)
+            codes = dfo.codes({f: v[lo:hi] for f, v in cols.items()}, {f: v[lo:hi] for f, v in cats.items()},
+                              hi - lo)
+            rc = L.alink_tree_predict(codes.data_ptr(), hi - lo, dfo.stride, dfo.code_bytes, dfo.nodes.data_ptr(),
+                                      dfo.dist.data_ptr(), dfo.nd, dfo.wsum.data_ptr(), dfo.cat.data_ptr(),
+                                      int(dfo.cat.shape[1]), dfo.roots.data_ptr(), int(dfo.roots.numel()),
+                                      acc[lo:hi].data_ptr(), wacc[lo:hi].data_ptr(), err.data_ptr(),
+                                      _lib.stream_ptr(dev))
+            if rc != 0:
+                raise RuntimeError(f"alink_tree_predict failed: {rc}")
+        e = int(err.item())
+        if e & 1:
+            raise RuntimeError("Model is broken. Sum weight is zero.")
+        if e & 2:
+            return None
+        return acc.cpu().numpy(), wacc.cpu().numpy()
 
     def _accumulate(self, X: np.ndarray, flat: _FlatForest) -> (np.ndarray, np.ndarray):
         """Sum over trees of leaf distributions (x weight) and of the weights, per row."""
@@ -350,7 +485,7 @@ class TreeModelMapper(RichModelMapper):
                             raise RuntimeError("Model is broken. Sum weight is zero.")
                         fr.extend([r_] * k)
                         fnode.extend(ch.tolist())
-                        fw.extend((w_ * cw / tot).tolist())
+                        fw.extend((w_ * (cw / tot)).tolist())       # ProcessMissing: weight * (w_i / sum)
                     keep = ~miss
                     rows = np.concatenate([rows[keep], np.asarray(fr, dtype=np.int64)])
                     node = np.concatenate([flat.first[node[keep]] + child[keep], np.asarray(fnode, dtype=np.int64)])
@@ -361,16 +496,37 @@ class TreeModelMapper(RichModelMapper):
 
     def _map_columns(self, mt):
         from ...common.table import Column
-        X = self._features(mt)
         flat = getattr(self, "_flat", None)
         if flat is None:
             flat = self._flat = _FlatForest(self.model.roots, self._n_dist())
-        acc, wacc = self._accumulate(X, flat)
-        preds, details = self._finish(acc, wacc)
-        cols = [Column.from_values(preds, self.helper.out_types[0])]
+        res = None
+        dev = self._device(mt) if mt.num_rows and len(flat.roots) else None
+        if dev is not None:
+            from ...ops import _lib
+            if _lib.available() or not _lib.torch_fallback_allowed():
+                res = self._accumulate_device(mt, flat, dev)
+        if res is None:
+            res = self._accumulate(self._features(mt), flat)
+        preds, details = self._finish(*res)
+        cols = [preds if isinstance(preds, Column) else Column.from_values(preds, self.helper.out_types[0])]
         if self.detail_col:
-            cols.append(Column.from_values(details, Types.STRING))
+            cols.append(details if isinstance(details, Column) else Column.from_values(details, Types.STRING))
         return cols
+
+    def _label_column(self, idx: np.ndarray) -> "Column":
+        """Prediction column of label values ``labels[idx]`` (idx -1 -> NULL), built without a per-row loop."""
+        from ...common.table import Column
+        t = self.helper.out_types[0]
+        bad = idx < 0
+        labs = self.labels
+        if labs and all(isinstance(l, (int, float)) and not isinstance(l, bool) for l in labs):
+            arr = np.asarray(labs)[np.where(bad, 0, idx)]
+            col = Column.from_values(arr, t)
+            if bad.any():
+                col = Column(col.values, torch.from_numpy(bad.copy()))
+            return col
+        lab = np.asarray(labs + [None], dtype=object)
+        return Column.from_values(lab[np.where(bad, len(labs), idx)].tolist(), t)
 
     def _map_row_values(self, row):
         from ...common.table import MTable
@@ -401,15 +557,16 @@ class GbdtModelMapper(TreeModelMapper):
         return Types.DOUBLE
 
     def _finish(self, acc, wacc):
+        from ...common.detail import DetailBlock
+        from ...common.table import Column
         s = acc[:, 0]
         if self.algo_type == 1:
-            preds, details = [], []
-            for v in s:
-                p = 1.0 / (1.0 + math.exp(-v))
-                preds.append(self.labels[1] if p >= 0.5 else self.labels[0])
-                details.append(_detail_json({java_str(self.labels[0]): 1.0 - p, java_str(self.labels[1]): p}))
-            return preds, details
-        return [float(v) + self.period for v in s], [None] * len(s)
+            p = 1.0 / (1.0 + np.exp(-s))
+            preds = self._label_column((p >= 0.5).astype(np.int64))
+            det = Column(DetailBlock([java_str(self.labels[0]), java_str(self.labels[1])],
+                                     np.stack([1.0 - p, p], 1), quoted=False))
+            return preds, det
+        return Column(torch.from_numpy(s + self.period)), [None] * len(s)
 
 
 class RandomForestModelMapper(TreeModelMapper):
@@ -425,16 +582,18 @@ class RandomForestModelMapper(TreeModelMapper):
         return Types.DOUBLE
 
     def _finish(self, acc, wacc):
+        from ...common.detail import DetailBlock
+        from ...common.table import Column
+        # LabelCounter.normWithWeight: divide by the weight sum unless it is zero
         norm = np.where(wacc[:, None] != 0, acc / np.where(wacc == 0, 1.0, wacc)[:, None], acc)
         if self.regression:
-            return [float(v) for v in norm[:, 0]], [None] * len(norm)
-        preds, details = [], []
-        for row in norm:
-            d, best, bi = {}, 0.0, -1
-            for i, p in enumerate(row):
-                d[java_str(self.labels[i])] = float(p)
-                if best < p:
-                    best, bi = p, i
-            preds.append(self.labels[bi] if bi >= 0 else None)
-            details.append(_detail_json(d))
-        return preds, details
+            return Column(torch.from_numpy(np.ascontiguousarray(norm[:, 0]))), [None] * len(norm)
+        # argmax with the reference's strict "best < p" from best = 0: first maximum, none when nothing is > 0
+        bi = np.argmax(norm, axis=1) if norm.shape[1] else np.zeros(len(norm), np.int64)
+        bi = np.where(norm[np.arange(len(norm)), bi] > 0.0, bi, -1) if norm.shape[1] else bi - 1
+        keys = [java_str(l) for l in self.labels]
+        if len(set(keys)) == len(keys) and len(keys) == norm.shape[1]:
+            det = Column(DetailBlock(keys, norm, quoted=False))
+        else:
+            det = [_detail_json({java_str(self.labels[i]): float(p) for i, p in enumerate(row)}) for row in norm]
+        return self._label_column(bi.astype(np.int64)), det

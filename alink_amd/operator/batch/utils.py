@@ -63,6 +63,7 @@ class ModelMapBatchOp(BatchOperator):
         model_op, data_op = inputs
         data = data_op.getOutputTable()
         mapper = load_model_mapper(self.MAPPER, model_op.getOutputTable(), data.schema, self.getParams())
+        mapper.env = self.env                           # device-aware mappers (tree predict) read the op's env
         self.setOutputTable(mapper.map_table(data))
         mapper.close()
         return self

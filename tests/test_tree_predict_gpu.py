@@ -1,0 +1,125 @@
+"""Device tree-ensemble prediction (``ops/csrc/tree_predict.hip``) against the host walk of the same mapper: GBDT
+(binary and regression), random forest (multi-class, regression) with categorical splits and missing values."""
+import numpy as np
+import pandas as pd
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _frame(n=3000, seed=0, classes=2):
+    rng = np.random.default_rng(seed)
+    x0 = rng.normal(size=n)
+    x1 = rng.normal(size=n)
+    cat = rng.choice(["a", "b", "c", "d", "e"], n)
+    y_num = x0 - 0.5 * x1 + (cat == "c") * 1.5 + 0.2 * rng.normal(size=n)
+    q = np.quantile(y_num, np.linspace(0, 1, classes + 1)[1:-1])
+    y = np.searchsorted(q, y_num)
+    df = pd.DataFrame({"x0": x0, "x1": x1, "c": cat, "y": y, "t": y_num})
+    return df
+
+
+def _with_missing(df, seed=1):
+    rng = np.random.default_rng(seed)
+    df = df.copy().astype({"x0": object, "c": object})
+    m0 = rng.random(len(df)) < 0.1
+    m1 = rng.random(len(df)) < 0.1
+    df.loc[m0, "x0"] = None
+    df.loc[m1, "c"] = None
+    df.loc[rng.random(len(df)) < 0.03, "c"] = "unseen"
+    return df
+
+
+SCHEMA = "x0 double, x1 double, c string, y int, t double"
+
+
+def _predict_both(train_op, pred_cls, df_train, df_pred, detail=True):
+    from alink_amd import BatchOperator, useLocalEnv
+    from alink_amd.models.tree import model as tm
+    useLocalEnv(1, device="cuda:0")
+    model = train_op.linkFrom(BatchOperator.fromDataframe(df_train, schemaStr=SCHEMA))
+    src = BatchOperator.fromDataframe(df_pred, schemaStr=SCHEMA)
+
+    def run():
+        op = pred_cls().setPredictionCol("p")
+        if detail:
+            op = op.setPredictionDetailCol("d")
+        return op.linkFrom(model, src).collect()
+    calls = {"dev": 0}
+    orig = tm.TreeModelMapper._accumulate_device
+    orig_device = tm.TreeModelMapper._device
+
+    def spy(self, *a):
+        calls["dev"] += 1
+        return orig(self, *a)
+    tm.TreeModelMapper._accumulate_device = spy
+    try:
+        dev = run()
+        tm.TreeModelMapper._device = lambda self, mt: None          # host walk
+        host = run()
+    finally:
+        tm.TreeModelMapper._accumulate_device = orig
+        tm.TreeModelMapper._device = orig_device
+    assert calls["dev"] >= 1
+    return dev, host
+
+
+def _compare(dev, host, detail, exact_pred=True):
+    assert len(dev) == len(host)
+    for a, b in zip(dev, host):
+        if exact_pred:
+            assert a[5] == b[5]
+        else:
+            assert a[5] == pytest.approx(b[5], rel=1e-12, abs=1e-12)
+        if detail:
+            da, db = (None if x is None else __import__("json").loads(x) for x in (a[6], b[6]))
+            assert da.keys() == db.keys()
+            for k in da:
+                assert da[k] == pytest.approx(db[k], rel=1e-12, abs=1e-12)
+
+
+def test_gbdt_binary_device_predict_matches_host():
+    from alink_amd import GbdtTrainBatchOp, GbdtPredictBatchOp
+    df = _frame()
+    tr = GbdtTrainBatchOp().setFeatureCols(["x0", "x1", "c"]).setCategoricalCols(["c"]).setLabelCol("y") \
+        .setNumTrees(20).setMaxDepth(5).setMinSamplesPerLeaf(10)
+    dev, host = _predict_both(tr, GbdtPredictBatchOp, df, _with_missing(df))
+    _compare(dev, host, True)
+
+
+def test_gbdt_regression_device_predict_matches_host():
+    from alink_amd import GbdtRegTrainBatchOp, GbdtRegPredictBatchOp
+    df = _frame(seed=3)
+    tr = GbdtRegTrainBatchOp().setFeatureCols(["x0", "x1", "c"]).setCategoricalCols(["c"]).setLabelCol("t") \
+        .setNumTrees(15).setMaxDepth(6).setMinSamplesPerLeaf(10)
+    dev, host = _predict_both(tr, GbdtRegPredictBatchOp, df, _with_missing(df), detail=False)
+    _compare(dev, host, False, exact_pred=False)
+
+
+@pytest.mark.parametrize("classes", [2, 3, 6])
+def test_random_forest_device_predict_matches_host(classes):
+    from alink_amd import RandomForestTrainBatchOp, RandomForestPredictBatchOp
+    df = _frame(seed=5, classes=classes)
+    tr = RandomForestTrainBatchOp().setFeatureCols(["x0", "x1", "c"]).setCategoricalCols(["c"]).setLabelCol("y") \
+        .setNumTrees(12).setMaxDepth(7)
+    dev, host = _predict_both(tr, RandomForestPredictBatchOp, df, _with_missing(df))
+    _compare(dev, host, True)
+
+
+def test_random_forest_regression_device_predict_matches_host():
+    from alink_amd import RandomForestRegTrainBatchOp, RandomForestRegPredictBatchOp
+    df = _frame(seed=7)
+    tr = RandomForestRegTrainBatchOp().setFeatureCols(["x0", "x1", "c"]).setCategoricalCols(["c"]) \
+        .setLabelCol("t").setNumTrees(8).setMaxDepth(8)
+    dev, host = _predict_both(tr, RandomForestRegPredictBatchOp, df, _with_missing(df), detail=False)
+    _compare(dev, host, False, exact_pred=False)
+
+
+def test_tree_predict_kernel_rows_not_multiple_of_block():
+    from alink_amd import GbdtTrainBatchOp, GbdtPredictBatchOp
+    df = _frame(n=131)
+    tr = GbdtTrainBatchOp().setFeatureCols(["x0", "x1", "c"]).setCategoricalCols(["c"]).setLabelCol("y") \
+        .setNumTrees(5).setMaxDepth(3).setMinSamplesPerLeaf(3)
+    dev, host = _predict_both(tr, GbdtPredictBatchOp, df, df.iloc[:67])
+    _compare(dev, host, True)

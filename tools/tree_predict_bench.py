@@ -1,0 +1,128 @@
+#!/usr/bin/env python3
+"""Tree-ensemble serving throughput (BASELINE config-3 model shape): a random GBDT of ``--trees`` full
+binary trees of depth ``--depth`` over ``--features`` continuous features (binary classification, as a trained
+config-3 model would be), scored by the public ``GbdtPredictBatchOp`` on ``--rows`` device-resident rows, with and
+without the prediction-detail column.  Prints one JSON line per variant with rows/s (median of ``--reps``).
+
+    python tools/tree_predict_bench.py --rows 2000000 --trees 500 --depth 8 --features 1000
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+
+def random_forest(trees, depth, F, seed=0):
+    from alink_amd.models.tree.model import LabelCounter, Node
+    rng = np.random.default_rng(seed)
+    roots = []
+    for _ in range(trees):
+        def build(d):
+            if d == depth:
+                return Node(-1, 0.0, LabelCounter(float(rng.integers(1, 100)), 1, [float(rng.normal() * 0.1)]))
+            nd = Node(int(rng.integers(F)), 1.0, LabelCounter(1.0, 1, [0.0]), None,
+                      float(np.round(rng.normal(), 2)))     # ~a few hundred distinct thresholds per feature
+            nd.nextNodes = [build(d + 1), build(d + 1)]
+            nd.counter.weightSum = nd.nextNodes[0].counter.weightSum + nd.nextNodes[1].counter.weightSum
+            return nd
+        roots.append(build(0))
+    return roots
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", type=int, default=2_000_000)
+    ap.add_argument("--trees", type=int, default=500)
+    ap.add_argument("--depth", type=int, default=8)
+    ap.add_argument("--features", type=int, default=1000)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--missing", type=float, default=0.0, help="fraction of NULL cells")
+    a = ap.parse_args()
+    from alink_amd import useLocalEnv, GbdtPredictBatchOp
+    from alink_amd.common.params import Params
+    from alink_amd.common.table import Column, MTable
+    from alink_amd.common.types import TableSchema, Types
+    from alink_amd.models.tree.model import TreeModel, TreeModelDataConverter
+    from alink_amd.operator.batch.source import TableSourceBatchOp
+    env = useLocalEnv(1)
+    dev = env.device
+    t0 = time.perf_counter()
+    roots = random_forest(a.trees, a.depth, a.features)
+    names = [f"f{i}" for i in range(a.features)]
+    meta = Params().set("featureCols", names).set("labelCol", "label").set("categoricalCols", []) \
+        .set("algoType", 1).set("gbdt.y.period", 0.0).set("numTrees", a.trees).set("maxDepth", a.depth + 1)
+    conv = TreeModelDataConverter(Types.INT)
+    rows = conv.save(TreeModel(meta, roots, [0, 1], None))
+    model = TableSourceBatchOp(MTable.from_rows(rows, conv.getModelSchema(), replicated=True))
+    t_model = time.perf_counter() - t0
+    g = torch.Generator(device=dev).manual_seed(1)
+    cols = []
+    for _ in range(a.features):
+        x = torch.randn(a.rows, generator=g, device=dev, dtype=torch.float64)
+        nulls = (torch.rand(a.rows, generator=g, device=dev) < a.missing) if a.missing > 0 else None
+        cols.append(Column(x, nulls))
+    data = TableSourceBatchOp(MTable(TableSchema(names, [Types.DOUBLE] * a.features), cols))
+    for detail in (False, True):
+        times = []
+        for _ in range(a.reps):
+            op = GbdtPredictBatchOp().setPredictionCol("p").setReservedCols([])
+            if detail:
+                op = op.setPredictionDetailCol("d")
+            if dev.type == "cuda":
+                torch.cuda.synchronize(dev)
+            t = time.perf_counter()
+            out = op.linkFrom(model, data).getOutputTable()
+            p = out.col("p").values
+            if detail:
+                _ = out.col("d").values                     # columnar DetailBlock (strings only when read)
+            if isinstance(p, torch.Tensor) and p.is_cuda:
+                torch.cuda.synchronize(dev)
+            times.append(time.perf_counter() - t)
+        tm = sorted(times)[len(times) // 2]
+        print(json.dumps({"rows": a.rows, "trees": a.trees, "depth": a.depth, "features": a.features,
+                          "missing": a.missing, "detail": detail, "device": str(dev), "s": round(tm, 4),
+                          "rows_per_s": a.rows / tm, "model_build_s": round(t_model, 2)}), flush=True)
+    # serving split: the model loaded once (LocalPredictor-style), then per-phase times of one scoring pass
+    from alink_amd.operator.batch.utils import load_model_mapper
+    from alink_amd.models.tree.model import GbdtModelMapper
+    sync = (lambda: torch.cuda.synchronize(dev)) if dev.type == "cuda" else (lambda: None)
+    t = time.perf_counter()
+    mapper = load_model_mapper(GbdtModelMapper, model.getOutputTable(), data.getOutputTable().schema,
+                               Params().set("predictionCol", "p").set("predictionDetailCol", "d"))
+    mapper.env = env
+    t_load = time.perf_counter() - t
+    mt = data.getOutputTable()
+    ph = {}
+    orig_codes = None
+    from alink_amd.models.tree import model as tmod
+    orig_codes = tmod._DeviceForest.codes
+
+    def timed_codes(self, *x):
+        sync()
+        t1 = time.perf_counter()
+        r = orig_codes(self, *x)
+        sync()
+        ph["codes_s"] = ph.get("codes_s", 0.0) + time.perf_counter() - t1
+        return r
+    tmod._DeviceForest.codes = timed_codes
+    for rep in range(2):
+        ph.clear()
+        sync()
+        t = time.perf_counter()
+        cols = mapper._map_columns(mt)
+        sync()
+        ph["map_columns_s"] = time.perf_counter() - t
+    tmod._DeviceForest.codes = orig_codes
+    print(json.dumps({"serving": True, "rows": a.rows, "load_model_s": round(t_load, 3),
+                      **{k: round(v, 4) for k, v in ph.items()},
+                      "rows_per_s_map_columns": a.rows / ph["map_columns_s"]}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
