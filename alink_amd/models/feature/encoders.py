@@ -419,8 +419,13 @@ def _round(x: float, mode: str) -> int:
 
 
 def train_quantile_discretizer(mt: MTable, params: Params) -> MTable:
-    """Exact distributed quantiles: each column's non-missing values are gathered and sorted once on the
-    device; split j = sorted[round(q * (n-1) * j)] (``QIndex.genIndex``), de-duplicated."""
+    """Exact distributed quantiles (reference ``QuantileDiscretizerTrainBatchOp.java:181``, ``SortUtilsNext.pSort``):
+    each column's non-missing values stay on their rank as a device tensor; the split values are the order
+    statistics at global positions round(q * (n-1) * j) (``QIndex.genIndex``), de-duplicated, found by
+    ``parallel/sort.global_order_statistics`` — a device sort on one rank, the distributed sample sort plus a
+    count prefix on several; no rank ever holds another rank's values."""
+    from ...parallel.sort import global_order_statistics
+    from ..tree.data import numeric_column
     from ...common.model.converter import SimpleModelDataConverter, append_meta_rows, append_data_rows
     cols = list(params.get("selectedCols"))
     nb = _pget(params, "numBuckets")
@@ -429,15 +434,13 @@ def train_quantile_discretizer(mt: MTable, params: Params) -> MTable:
     mode = _ename(_pget(params, "roundMode"), "ROUND")
     left_open = bool(_pget(params, "leftOpen", True))
     borders = {}
+    dev = _device_of(mt)
     for c, q in zip(cols, nums):
-        vals = [float(v) for v in mt.col(c).to_list() if v is not None and not (isinstance(v, float) and v != v)]
-        allv = np.sort(np.concatenate([np.asarray(p, dtype=np.float64) for p in comm.all_gather_object(vals)]))
-        n = len(allv)
-        splits = []
-        if n:
-            for j in range(1, q):
-                splits.append(float(allv[min(n - 1, _round(1.0 / q * (n - 1.0) * j, mode))]))
-        splits = sorted(set(splits))
+        x, null = numeric_column(mt, c, dev)
+        x = x[~(null | torch.isnan(x))]
+        n, vals = global_order_statistics(
+            x, lambda n: [min(n - 1, _round(1.0 / q * (n - 1.0) * j, mode)) for j in range(1, q)] if n else [])
+        splits = sorted(set(float(v) for v in vals)) if n else []
         ctype = "LONG" if mt.col_type(c) in (Types.LONG, Types.INT, Types.SHORT, Types.BYTE) else "DOUBLE"
         borders[c] = {"featureName": c, "splitsArray": splits, "isLeftOpen": left_open, "colType": ctype}
     meta = Params().set("selectedCols", cols).set("leftOpen", left_open)
@@ -445,6 +448,13 @@ def train_quantile_discretizer(mt: MTable, params: Params) -> MTable:
     append_meta_rows(meta, rows, 2)
     append_data_rows([json.dumps(borders[c], separators=(",", ":")) for c in cols], rows, 2)
     return MTable.from_rows(rows, QUANTILE_SCHEMA, replicated=True)
+
+
+def _device_of(mt: MTable):
+    for c in mt.cols:
+        if isinstance(c.values, torch.Tensor) and c.values.is_cuda:
+            return c.values.device
+    return torch.device("cpu")
 
 
 class _Bucketing:

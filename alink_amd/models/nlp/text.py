@@ -396,21 +396,19 @@ def train_doc_count_vectorizer(mt: MTable, params: Params) -> List[tuple]:
         for w, c in words.items():
             df_c[w] += 1
             wc_c[w] += c
-    parts = comm.all_gather_object(({k: (df_c[k], wc_c[k]) for k in df_c}, ndoc))
-    dfs, wcs, docs = Counter(), Counter(), 0
-    for d, n in parts:
-        docs += n
-        for k, (a, b) in d.items():
-            dfs[k] += a
-            wcs[k] += b
+    docs = int(sum(comm.all_gather_object(ndoc))) if comm.get_world_size() > 1 else ndoc
     max_df = float(_pget(params, "maxDF", float(2 ** 63 - 1)))
     min_df = float(_pget(params, "minDF", 1.0))
     max_df = max_df if max_df >= 1.0 else max_df * docs
     min_df = min_df if min_df >= 1.0 else min_df * docs
     if max_df < min_df:
         raise ValueError("MaxDF must be greater than MinDF!")
-    keep = [(w, wcs[w], math.log((1.0 + docs) / (1.0 + dfs[w]))) for w in dfs if min_df <= dfs[w] <= max_df]
-    keep.sort(key=lambda t: (-t[1], t[0]))
+    # (word count, document frequency) reduced on one owner rank per word, filtered by df there, ordered by
+    # count desc / word asc (parallel/sort.merged_vocabulary; DocCountVectorizerTrainBatchOp.java:77 pSort)
+    from ...parallel.sort import merged_vocabulary
+    merged = merged_vocabulary({k: (wc_c[k], df_c[k]) for k in df_c},
+                               keep=lambda w, c: min_df <= c[1] <= max_df)
+    keep = [(w, c[0], math.log((1.0 + docs) / (1.0 + c[1]))) for w, c in merged]
     vocab = int(_pget(params, "vocabSize", 2 ** 18))
     keep = keep[:vocab]
     meta = Params().set("minTF", float(_pget(params, "minTF", 1.0))) \

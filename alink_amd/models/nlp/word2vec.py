@@ -158,12 +158,14 @@ def train_word2vec(mt: MTable, params: Params, env) -> List[tuple]:
     cnt = Counter()
     for d in docs_tok:
         cnt.update(d)
-    total = Counter()
-    for part in comm.all_gather_object(dict(cnt)):
-        total.update(part)
-    vocab = sorted([w for w, c in total.items() if c >= min_count], key=lambda w: (-total[w], w))
-    if not vocab:
+    # global vocabulary: counts reduced on one owner rank per word, ordered count desc / word asc
+    # (parallel/sort.merged_vocabulary; the reference's pSort, Word2VecTrainBatchOp.java:145)
+    from ...parallel.sort import merged_vocabulary
+    merged = merged_vocabulary(dict(cnt), keep=lambda w, c: c >= min_count)
+    if not merged:
         return []
+    total = dict(merged)
+    vocab = [w for w, _ in merged]
     index = {w: i for i, w in enumerate(vocab)}
     V = len(vocab)
     C, P, lens = huffman(np.array([total[w] for w in vocab]))

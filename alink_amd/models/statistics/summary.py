@@ -312,13 +312,11 @@ def _is_spearman(method) -> bool:
 
 
 def _rank_global(v: torch.Tensor) -> torch.Tensor:
-    """Average ranks (1-based, ties averaged) of the GLOBAL column, returned for this rank's rows."""
-    parts = comm.all_gather_object(v.cpu().numpy())
-    full = np.concatenate(parts) if parts else np.zeros(0)
-    from scipy.stats import rankdata
-    ranks = rankdata(full, method="average")
-    off = int(sum(len(p) for p in parts[:comm.get_rank()]))
-    return torch.as_tensor(ranks[off:off + v.shape[0]], dtype=torch.float64, device=v.device)
+    """Average ranks (1-based, ties averaged) of the GLOBAL column, returned for this rank's rows — the
+    distributed sample sort of ``parallel/sort.global_average_ranks`` (reference ``SpearmanCorrelation.java:61``,
+    ``SortUtils.pSort``): no rank gathers the column."""
+    from ...parallel.sort import global_average_ranks
+    return global_average_ranks(v)
 
 
 def _pearson_pairwise(X: torch.Tensor, valid: torch.Tensor) -> np.ndarray:

@@ -108,6 +108,8 @@ class SosBatchOp(BatchOperator):
             partition_bounds(full.num_rows, self.env)
         own = full.slice(lo, hi) if (lo, hi) != (0, full.num_rows) else full
         out = own.with_columns([p.get("predictionCol")], [Types.DOUBLE], [Column(scores[lo:hi].cpu())])
+        # each rank keeps its own row block of the gathered table: a partitioned output (collect gathers it)
+        out.replicated = bool(mt.replicated or comm.get_world_size() == 1)
         self.setOutputTable(out)
         return self
 

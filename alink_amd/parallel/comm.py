@@ -170,6 +170,7 @@ def init_distributed(backend: Optional[str] = None, timeout_s: float = 1800.0) -
         return False
     if dist.is_initialized():
         return is_distributed()
+    timeout_s = float(os.environ.get("ALINK_DIST_TIMEOUT_S", timeout_s))
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     if ws <= 1 and not force_collective():
         return False

@@ -76,6 +76,16 @@ def test_bench_self_launches_n_ranks():
     assert res["effective_config"]["rows_per_rank"] == 10000
 
 
+def test_bench_self_launches_eight_ranks_like_the_driver():
+    """The driver's 8-GPU shape of the headline bench (N=8, strong scaling), rehearsed on the CPU: 8 ranks, a row
+    count that does not divide by 8, the convergence run included; every rank holds its share of the rows."""
+    res = _bench(8, ["--rows", "40003", "--converge-iters", "20"])
+    assert res["n_gpus"] == 8 and res["config"]["parallelism"] == "dp8"
+    assert res["effective_config"]["rows_per_rank"] == 40003 // 8
+    assert res["allreduce_bytes_per_step"] == res["live_k"] * (128 + 1) * 8
+    assert 1 <= res["iters_to_converge"] <= 20 and res["convergence"]["reference"]["sse"] > 0
+
+
 def test_bench_rejects_mismatched_world():
     env = dict(os.environ, ALINK_DEVICE="cpu", WORLD_SIZE="1", RANK="0", MASTER_ADDR="127.0.0.1",
                MASTER_PORT="29999")
