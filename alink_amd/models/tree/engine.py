@@ -19,6 +19,7 @@ node) cross to the host to build the model objects.
 from __future__ import annotations
 
 import collections
+import time
 
 import math
 from dataclasses import dataclass
@@ -50,6 +51,10 @@ class SplitConfig:
     min_sum_hessian_per_leaf: float = 0.0
     learning_rate: float = 1.0
     node_feature_count: Optional[int] = None  # RF bagging: features tried per node (shuffled order)
+    # device bytes the histograms of one pass may take (``maxMemoryInMB``, TreeObj.java:113,263-286): a level's
+    # histogram builds and split searches run in node batches within it, and the level's histograms kept for the
+    # next level's sibling subtraction move to host memory when they exceed it (None: unbounded)
+    max_memory_bytes: Optional[int] = None
 
     @property
     def classification(self) -> bool:
@@ -207,6 +212,7 @@ class TreeBuilder:
     RS_BYTES = collections.deque(maxlen=4096)     # reduce-scatter input bytes (fp32) per histogram piece (latest)
     RS_CALLS = 0                                  # reduce-scattered histogram pieces (all time)
     HIST_BYTES = collections.deque(maxlen=4096)   # full-width fp32 histogram bytes per histogram call (latest)
+    LEVEL_STATS = collections.deque(maxlen=4096)  # (depth, nodes, split candidates, host wall s) per grown level
 
     def _histograms_sharded(self, slot, sub, nslots: int, prep) -> torch.Tensor:
         """Feature-block reduce-scatter overlapped with the histogram build: every rank's
@@ -523,6 +529,16 @@ class TreeBuilder:
             return False
         return p.total[-1] > 0
 
+    def _node_batch(self, nl: int, S: int) -> Tuple[int, bool]:
+        """(nodes per histogram pass / split search, park the level's histograms on the host) under
+        ``cfg.max_memory_bytes`` — the reference's loop buffer (TreeObj.determineLoopNode: as many node
+        histograms as fit maxMemoryInMB, at least one)."""
+        budget = self.cfg.max_memory_bytes
+        if budget is None:
+            return max(1, nl), False
+        per = self.Fb * self.B * S * (4 if self.dev.type == "cuda" else 8)
+        return max(1, int(budget // max(1, per))), nl * per > budget
+
     def build(self, stats: torch.Tensor, sample: torch.Tensor, feature_mask: Optional[np.ndarray] = None,
               rng=None) -> Tuple[Node, torch.Tensor, List[Node]]:
         """Grow one tree.  ``stats`` [n, S] per-row statistics, ``sample`` [n] rows that count.
@@ -547,6 +563,7 @@ class TreeBuilder:
         level_hist = {0: Hroot[0]}
         while level:
             nl = len(level)
+            t_level = time.perf_counter()
             for p in level:
                 p.splittable = self._node_splittable(p)
             # which nodes need a histogram built vs derived from the parent
@@ -568,26 +585,33 @@ class TreeBuilder:
                     else:
                         build_ids.extend(need)
                 build_ids = sorted(set(build_ids))
-                if build_ids:
+                # memory bound: one histogram pass holds at most `mb` nodes; a level whose histograms exceed the
+                # budget parks them in host memory (they feed the next level's sibling subtraction)
+                mbatch, park = self._node_batch(nl, stats.shape[1])
+                for c0 in range(0, len(build_ids), mbatch):
+                    chunk = build_ids[c0:c0 + mbatch]
                     som = torch.full((nl,), -1, dtype=torch.int32)
-                    for s, i in enumerate(build_ids):
+                    for s, i in enumerate(chunk):
                         som[i] = s
-                    H = self._histograms(node_of_row, sample, som.to(dev), len(build_ids), stats)
-                    for s, i in enumerate(build_ids):
-                        level_hist[i] = H[s]
+                    H = self._histograms(node_of_row, sample, som.to(dev), len(chunk), stats)
+                    for s, i in enumerate(chunk):
+                        level_hist[i] = H[s].cpu() if park else H[s]
+                    del H
                 for big, (par, others) in derive.items():
-                    h = self._prev_hist[par].clone()
+                    h = self._prev_hist[par].to(dev).clone()
                     for o in others:
-                        h -= level_hist[o]
-                    level_hist[big] = h
+                        h -= level_hist[o].to(dev)
+                    level_hist[big] = h.cpu() if park else h
             if bagging:
                 # every polled node shuffles its inherited splitter order (DecisionTree.bagging), in BFS order
                 for p in level:
                     p.order = rng.shuffle(list(p.order))
-            cand = [i for i in range(nl) if level[i].splittable]
+            cand_all = [i for i in range(nl) if level[i].splittable]
             splits = {}
-            if cand:
-                Hn = torch.stack([level_hist[i] for i in cand]).to(torch.float32).to(torch.float64)
+            mbatch = self._node_batch(nl, stats.shape[1])[0]
+            for c0 in range(0, len(cand_all), mbatch):
+                cand = cand_all[c0:c0 + mbatch]
+                Hn = torch.stack([level_hist[i].to(dev) for i in cand]).to(torch.float32).to(torch.float64)
                 m = len(cand)
                 order = torch.arange(F, device=dev).expand(m, F).clone()
                 ok = fmask[None, :].expand(m, F).clone()
@@ -661,6 +685,8 @@ class TreeBuilder:
                     q.node.counter = self._counter(tot[c])
             self._prev_hist = level_hist
             level_hist = {}
+            TreeBuilder.LEVEL_STATS.append((level[0].depth if level else 0, nl, len(cand_all),
+                                            time.perf_counter() - t_level))
             level = nxt
         self._prev_hist = {}
         self._hist_sub = None

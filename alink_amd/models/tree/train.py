@@ -328,7 +328,8 @@ def train_forest(mt: MTable, params: Params, env, regression: bool) -> Tuple[Lis
                           min_sample_ratio_per_child=float(_pget(params, "minSampleRatioPerChild", 0.0)),
                           min_info_gain=float(_pget(params, "minInfoGain", 0.0)),
                           max_leaves=int(_pget(params, "maxLeaves", 2 ** 31 - 1)),
-                          node_feature_count=node_feats)
+                          node_feature_count=node_feats,
+                          max_memory_bytes=int(_pget(params, "maxMemoryInMB", 64)) * (1 << 20))
         builder = TreeBuilder(data, cfg, local=series)
         # per-tree row sample drawn on the device from a (seed, tree)-keyed stream: the same tree gets the same
         # sample whichever rank grows it

@@ -123,3 +123,23 @@ def test_tree_predict_kernel_rows_not_multiple_of_block():
         .setNumTrees(5).setMaxDepth(3).setMinSamplesPerLeaf(3)
     dev, host = _predict_both(tr, GbdtPredictBatchOp, df, df.iloc[:67])
     _compare(dev, host, True)
+
+
+def test_random_forest_memory_bound_identical_trees_gpu():
+    """RF with the default unbounded depth on the GPU: maxMemoryInMB 8 (node-batched histogram passes, level
+    histograms parked in host memory) grows exactly the trees of an unbounded budget."""
+    from tests.test_tree import _rf_trees
+    from alink_amd.models.tree.engine import TreeBuilder
+    from alink_amd import useLocalEnv
+    rng = np.random.default_rng(1)
+    n, F = 200_000, 100
+    X = rng.normal(size=(n, F)).astype(np.float32)
+    df = pd.DataFrame({f"f{i}": X[:, i].astype(np.float64) for i in range(F)})
+    df["label"] = ((X[:, 0] + np.sin(3 * X[:, 1]) + X[:, 2] * X[:, 3] + 0.5 * rng.normal(size=n)) > 0).astype(int)
+    TreeBuilder.LEVEL_STATS.clear()
+    small = _rf_trees(df, 8, n_trees=1, dev="cuda:0")
+    widest = max(nodes for _, nodes, _, _ in TreeBuilder.LEVEL_STATS)
+    big = _rf_trees(df, 1 << 20, n_trees=1, dev="cuda:0")
+    useLocalEnv(1)
+    assert widest * F * 128 * 3 * 4 > 8 << 20          # some level really exceeded the budget
+    assert small[1:] == big[1:]
