@@ -110,6 +110,13 @@ V10_FLAGS = int(os.environ.get("ALINK_KMEANS_V10_FLAGS", "1"))
 V10_KMAX = 112
 # serpentine tile order across Lloyd supersteps (serpentine_reverse)
 SERPENTINE = os.environ.get("ALINK_KMEANS_SERPENTINE", "1") != "0"
+# v10 work-stealing tail (csrc/kmeans_v10.hip DYN), opt-in: the last V10_POOL of the tiles are claimed at run time
+# so workgroups on a slower XCD take fewer of them.  Measured (profiles/kmeans_dyn_r5.txt): the workgroups' exits
+# line up (spread 40-190 us -> ~12 us) but the per-tile cost of the dynamic indexing makes the launch ~4 % slower,
+# and which workgroup sums which rows (fp32) then varies run to run — so the deterministic static split (0) stays
+# the default
+V10_POOL = float(os.environ.get("ALINK_KMEANS_V10_POOL", "0"))
+_DYN: Dict[int, list] = {}        # device -> [two int32 counters, launch parity]
 
 
 def kernel_version(k: int = 100) -> str:
@@ -174,9 +181,18 @@ def assign_accumulate_hip(X: torch.Tensor, C: torch.Tensor, grid: Optional[int] 
         mode |= (V7_VAR << 4) if ver == "v7" else (V10_FLAGS << 4)
     if reverse and ver == "v10":
         mode |= 32
-    rc = getattr(L, f"alink_kmeans_assign_accum_bf16_{ver}")(
-        X.data_ptr(), n, cpad.data_ptr(), ninit.data_ptr(), k, slab.data_ptr(), slab_cnt.data_ptr(), grid, st,
-        None if assign_out is None else assign_out.data_ptr(), int(mode))
+    if ver == "v10" and V10_POOL > 0 and (mode & 7) == 0 and hasattr(L, "alink_kmeans_assign_accum_bf16_v10d"):
+        dyn = _DYN.get(dev.index)
+        if dyn is None:
+            dyn = _DYN[dev.index] = [torch.zeros(2, dtype=torch.int32, device=dev), 0]
+        rc = L.alink_kmeans_assign_accum_bf16_v10d(
+            X.data_ptr(), n, cpad.data_ptr(), ninit.data_ptr(), k, slab.data_ptr(), slab_cnt.data_ptr(), grid, st,
+            None if assign_out is None else assign_out.data_ptr(), int(mode), dyn[0].data_ptr(), dyn[1], V10_POOL)
+        dyn[1] ^= 1
+    else:
+        rc = getattr(L, f"alink_kmeans_assign_accum_bf16_{ver}")(
+            X.data_ptr(), n, cpad.data_ptr(), ninit.data_ptr(), k, slab.data_ptr(), slab_cnt.data_ptr(), grid, st,
+            None if assign_out is None else assign_out.data_ptr(), int(mode))
     if rc != 0:
         raise RuntimeError(f"alink_kmeans_assign_accum_bf16_{ver} failed: {rc}")
     rc = L.alink_kmeans_reduce_slabs(slab.data_ptr(), slab_cnt.data_ptr(), grid, k, out.data_ptr(), st)

@@ -337,3 +337,24 @@ def test_seed_ref_kernel_equals_torch_loop(n, k):
     b = km._seed_reference_device(D, w, k, np.random.default_rng(4), 0)
     assert a is not None and b is not None
     assert torch.equal(a.cpu(), b)
+
+
+@pytest.mark.parametrize("pool", [0.0, 0.1, 0.5, 1.0])
+@pytest.mark.parametrize("n,k,grid", [(300001, 100, None), (49157, 97, 3), (4097, 16, None), (129, 50, 1),
+                                      (1000003, 112, 7), (70, 8, 2)])
+def test_v10_work_stealing_tail(n, k, grid, pool, monkeypatch):
+    """DYN: static chunks plus a pool of 16-tile chunks claimed from a device counter — every tile exactly once
+    (identical assignments and counts to the static split, sums to fp32 order), in both walk directions, and the
+    two alternating counters reset themselves across launches."""
+    from alink_amd.ops import kmeans as K
+    X, C = _data(n, k, seed=31)
+    monkeypatch.setattr(K, "V10_POOL", 0.0)
+    sa = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+    ref = K.assign_accumulate_hip(X, C, grid=grid, assign_out=sa)
+    monkeypatch.setattr(K, "V10_POOL", pool)
+    for rev in (False, True, False, True):
+        da = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+        got = K.assign_accumulate_hip(X, C, grid=grid, assign_out=da, reverse=rev)
+        assert torch.equal(da, sa)
+        assert torch.equal(got[:, 128], ref[:, 128])
+        _own_assignment_check(X, C, got, da, k)

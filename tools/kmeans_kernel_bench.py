@@ -51,6 +51,10 @@ def main():
         Xs = X[:rows]
         for cfg in a.configs.split(","):
             ver, flags = cfg.split(":")
+            pool = None
+            if "p" in flags:                   # "v10:1p0.1": work-stealing pool fraction (0 = static split)
+                flags, pool = flags.split("p")
+                K.V10_POOL = float(pool)
             alt = flags.endswith("a")          # "v10:1a": serpentine, the direction alternates every launch
             flags = flags.rstrip("a")
             os.environ["ALINK_KMEANS_KERNEL"] = ver
@@ -64,7 +68,7 @@ def main():
                 out = run()
                 torch.cuda.synchronize()
                 res = {"rows": rows, "k": k, "kernel": K.kernel_version(k), "flags": int(flags), "mode": m,
-                       "serpentine": alt}
+                       "serpentine": alt, "pool": K.V10_POOL}
                 if m == 0 and rows == n:
                     if ref_small is None:
                         ref_small = K.assign_accumulate_torch(X[:2_000_000], C)
