@@ -191,7 +191,9 @@ class TreeBuilder:
         if self._hist_sub is None or self._hist_sub[0] is not stats:
             sub = stats if len(cols) == stats.shape[1] else stats[:, cols].contiguous()
             # the fixed-point kernel's quantised statistics are built once per tree, not once per level
-            prep = tops.FmStats(sub) if tops.fm_eligible(self.d.bins, len(cols), self.B) else None
+            elig = tops.fm_eligible(self.d.bins, len(cols), self.B) or \
+                (len(cols) == 3 and tops.fm_eligible(self.d.bins, 3, self.B, pack=True))
+            prep = tops.FmStats(sub) if elig else None
             self._hist_sub = (stats, sub, prep)
         _, sub, prep = self._hist_sub
         TreeBuilder.HIST_BYTES.append(nslots * self.F * self.B * len(cols) * 4)

@@ -58,7 +58,7 @@ _c_d = ctypes.c_double
 # signatures of further kernels (registered when present in the library)
 _EXTRA_SIGNATURES = {
     "alink_tree_hist_fm": [_c_vp, _c_int, _c_vp, _c_vp, _c_vp, _c_int, _c_vp, _c_int, _c_int, _c_int, _c_vp, _c_int,
-                           _c_int, _c_vp, _c_vp, _c_vp, _c_vp],
+                           _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_int],
     "alink_tree_hist_f32": [_c_vp, _c_i64, _c_int, _c_vp, _c_vp, _c_int, _c_int, _c_int, _c_vp, _c_int, _c_int,
                             _c_vp],
     "alink_tree_node_sums": [_c_vp, _c_vp, _c_vp, _c_i64, _c_int, _c_int, _c_vp, _c_int, _c_vp],

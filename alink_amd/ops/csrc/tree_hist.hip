@@ -235,8 +235,15 @@ __global__ __launch_bounds__(kThreads) void tree_node_sums_global(const int32_t*
 // into an int64 slab (no global atomics, no zeroing); tree_hist_fm_reduce sums a slot's chunks and scales.
 constexpr int kFmThreads = 1024;   // 16 waves: the single LDS-resident workgroup per CU hides HBM latency
 constexpr int kFmPairs = 8;          // row pairs per batch and wave
+// PACK (S == 3 with a unit count column, the GBDT / binary-RF case): the count rides in the low kPackBits of the
+// first statistic's int64 — ((int64) q0 << kPackBits) + 1 per row, |q0| < 2^30 — so a (row, feature) pair costs
+// 2 LDS atomics instead of 3 (the kernel is LDS-atomic-issue bound).  Exact while a chunk has < 2^kPackBits rows
+// (the host caps chunks at kPackMaxRows): the q0 part then stays below 2^46 * 2^17 = 2^63 and the count never
+// carries into it; tree_hist_fm_reduce unpacks every chunk's partial before summing chunks.
+constexpr int kPackBits = 17;
+constexpr int kPackMaxRows = 1 << 16;
 
-template <int S, bool IDX>
+template <int S, bool IDX, bool PACK = false>
 __global__ __launch_bounds__(kFmThreads) void tree_hist_fm(const uint8_t* __restrict__ bins, int F,
                                                            const int32_t* __restrict__ ridx,
                                                            const int32_t* __restrict__ q,
@@ -251,7 +258,8 @@ __global__ __launch_bounds__(kFmThreads) void tree_hist_fm(const uint8_t* __rest
   const int pos = (quad_id - c * nquad) * 4 + ((bid >> 3) & 3);   // entry of the feature-group list
   if (c >= nchunks || pos >= nfg) return;                // whole block, before any barrier
   const int fg = fgl != nullptr ? fgl[pos] : pos;
-  const int n_e = B * S * 32;
+  constexpr int SL = PACK ? 2 : S;                       // int64 statistics per bin in LDS
+  const int n_e = B * SL * 32;
   for (int i = threadIdx.x; i < n_e; i += kFmThreads) lq[i] = 0;
   __syncthreads();
   const int lane = threadIdx.x & 63;
@@ -287,13 +295,25 @@ __global__ __launch_bounds__(kFmThreads) void tree_hist_fm(const uint8_t* __rest
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int u = 0; u < kFmPairs; ++u) {
-      unsigned long long* hp = lb + min(bb[u], bmax) * (S * 32);
+      unsigned long long* hp = lb + min(bb[u], bmax) * (SL * 32);
       if (valid) {
+        if constexpr (PACK) {
+          // both rows' packed words are formed from the scalar statistics first (wave-uniform 64-bit values), and
+          // the lane's half selects between them — selecting the int32 first made the compiler index qs and
+          // spill it to scratch (10x slower)
+          const long long p0 = ((long long)qs[u][0] << kPackBits) + 1, p1 = ((long long)qs[u][4] << kPackBits) + 1;
+          const int h0 = qs[u][1], h1 = qs[u][5];
+          const long long pv = half ? p1 : p0;
+          const int hv = half ? h1 : h0;
+          atomicAdd(hp, (unsigned long long)pv);
+          atomicAdd(hp + 32, (unsigned long long)(long long)hv);
+        } else {
 #pragma unroll
-        for (int k = 0; k < S; ++k) {
-          const int lo = qs[u][k], hi = qs[u][4 + k];       // select by value: an index would go to scratch
-          const int v = half ? hi : lo;
-          atomicAdd(hp + k * 32, (unsigned long long)(long long)v);
+          for (int k = 0; k < S; ++k) {
+            const int lo = qs[u][k], hi = qs[u][4 + k];     // select by value: an index would go to scratch
+            const int v = half ? hi : lo;
+            atomicAdd(hp + k * 32, (unsigned long long)(long long)v);
+          }
         }
       }
     }
@@ -303,11 +323,16 @@ __global__ __launch_bounds__(kFmThreads) void tree_hist_fm(const uint8_t* __rest
     const int64_t r0 = IDX ? (int64_t)ridx[i] : (int64_t)i;
     const int64_t r1 = has1 ? (IDX ? (int64_t)ridx[i + 1] : (int64_t)(i + 1)) : r0;
     const int b = bcol[(half ? r1 : r0) * F];
-    unsigned long long* hp = lb + min(b, bmax) * (S * 32);
+    unsigned long long* hp = lb + min(b, bmax) * (SL * 32);
     if (valid && (half == 0 || has1)) {
+      if constexpr (PACK) {
+        atomicAdd(hp, (unsigned long long)(((long long)q[(int64_t)(i + half) * 4] << kPackBits) + 1));
+        atomicAdd(hp + 32, (unsigned long long)(long long)q[(int64_t)(i + half) * 4 + 1]);
+      } else {
 #pragma unroll
-      for (int k = 0; k < S; ++k)
-        atomicAdd(hp + k * 32, (unsigned long long)(long long)q[(int64_t)(i + half) * 4 + k]);
+        for (int k = 0; k < S; ++k)
+          atomicAdd(hp + k * 32, (unsigned long long)(long long)q[(int64_t)(i + half) * 4 + k]);
+      }
     }
   }
   __syncthreads();
@@ -324,20 +349,47 @@ __global__ __launch_bounds__(256) void tree_hist_fm_reduce(const long long* __re
                                                            const int32_t* __restrict__ slot_chunk,
                                                            const int32_t* __restrict__ fgl, int nfg, int nslots,
                                                            int F, int B, int S, const double* __restrict__ inv_scale,
-                                                           int feat_major, float* __restrict__ H) {
+                                                           int feat_major, float* __restrict__ H, int pack) {
   __shared__ float tile[kRedBins * 4 * 33];
   const int s = blockIdx.x / nfg, pos = blockIdx.x - (blockIdx.x / nfg) * nfg;
   const int fg = fgl != nullptr ? fgl[pos] : pos;
   const int b0 = blockIdx.y * kRedBins;
   const int nb = min(kRedBins, B - b0);
-  const int n_e = B * S * 32;
-  const int m = nb * S * 32;
   const int cs = slot_chunk[s], ce = slot_chunk[s + 1];
-  for (int t = threadIdx.x; t < m; t += 256) {
-    long long acc = 0;
-    for (int j = cs; j < ce; ++j) acc += slab[((int64_t)j * nfg + pos) * n_e + (int64_t)b0 * S * 32 + t];
-    const int k = (t >> 5) % S;
-    tile[(t >> 5) * 33 + (t & 31)] = (float)((double)acc * inv_scale[k]);
+  if (pack) {
+    // slab holds [B][2][32]: (q0 << kPackBits) + count, q1.  Every chunk's packed word is split before the chunks
+    // are summed (the count field is exact per chunk only); output statistics 0, 1 scaled, 2 = the count.
+    const int n_e = B * 2 * 32;
+    const int m = nb * 2 * 32;
+    for (int t = threadIdx.x; t < m; t += 256) {
+      long long acc = 0, cnt = 0;
+      const bool first = ((t >> 5) & 1) == 0;
+      for (int j = cs; j < ce; ++j) {
+        const long long v = slab[((int64_t)j * nfg + pos) * n_e + (int64_t)b0 * 2 * 32 + t];
+        if (first) {
+          acc += v >> kPackBits;
+          cnt += v & ((1ll << kPackBits) - 1);
+        } else {
+          acc += v;
+        }
+      }
+      const int bl = t >> 6, l = t & 31;
+      if (first) {
+        tile[(bl * 3 + 0) * 33 + l] = (float)((double)acc * inv_scale[0]);
+        tile[(bl * 3 + 2) * 33 + l] = (float)cnt;
+      } else {
+        tile[(bl * 3 + 1) * 33 + l] = (float)((double)acc * inv_scale[1]);
+      }
+    }
+  } else {
+    const int n_e = B * S * 32;
+    const int m = nb * S * 32;
+    for (int t = threadIdx.x; t < m; t += 256) {
+      long long acc = 0;
+      for (int j = cs; j < ce; ++j) acc += slab[((int64_t)j * nfg + pos) * n_e + (int64_t)b0 * S * 32 + t];
+      const int k = (t >> 5) % S;
+      tile[(t >> 5) * 33 + (t & 31)] = (float)((double)acc * inv_scale[k]);
+    }
   }
   __syncthreads();
   const int w = nb * S;
@@ -352,19 +404,19 @@ __global__ __launch_bounds__(256) void tree_hist_fm_reduce(const long long* __re
   }
 }
 
-template <int S>
+template <int S, bool PACK = false>
 int launch_fm(bool idx, int64_t grid, size_t lds, hipStream_t stream, const uint8_t* bins, int F, const int32_t* ridx,
               const int32_t* sst, const int32_t* chunk_rows, int nchunks, const int32_t* fgl, int nfg, int B,
               long long* slab) {
-  const void* k = idx ? reinterpret_cast<const void*>(tree_hist_fm<S, true>)
-                      : reinterpret_cast<const void*>(tree_hist_fm<S, false>);
+  const void* k = idx ? reinterpret_cast<const void*>(tree_hist_fm<S, true, PACK>)
+                      : reinterpret_cast<const void*>(tree_hist_fm<S, false, PACK>);
   if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return 3;
   if (idx)
-    hipLaunchKernelGGL((tree_hist_fm<S, true>), dim3((unsigned)grid), dim3(kFmThreads), lds, stream, bins, F, ridx, sst,
-                       chunk_rows, nchunks, fgl, nfg, B, slab);
+    hipLaunchKernelGGL((tree_hist_fm<S, true, PACK>), dim3((unsigned)grid), dim3(kFmThreads), lds, stream, bins, F,
+                       ridx, sst, chunk_rows, nchunks, fgl, nfg, B, slab);
   else
-    hipLaunchKernelGGL((tree_hist_fm<S, false>), dim3((unsigned)grid), dim3(kFmThreads), lds, stream, bins, F, ridx,
-                       sst, chunk_rows, nchunks, fgl, nfg, B, slab);
+    hipLaunchKernelGGL((tree_hist_fm<S, false, PACK>), dim3((unsigned)grid), dim3(kFmThreads), lds, stream, bins, F,
+                       ridx, sst, chunk_rows, nchunks, fgl, nfg, B, slab);
   return 0;
 }
 
@@ -457,12 +509,14 @@ int alink_tree_hist_f32(const uint8_t* bins, int64_t n, int F, const int32_t* sl
 // slot; fgl: [nfl] 32-feature groups to build (nullptr: all, nfl ignored); inv_scale: [S] fp64 (device);
 // slab: [nchunks, nfl, B, S, 32] int64 scratch; H: [nslots, F, B, S] fp32, or with feat_major
 // [nfl * 32, nslots, B, S] (fully written, no zeroing needed).
+// pack = 1 (S == 3, statistic 2 a unit count; every chunk < kPackMaxRows rows): the packed 2-atomic build.
 int alink_tree_hist_fm(const uint8_t* bins, int F, const int32_t* ridx, const int32_t* q, const int32_t* chunk_rows,
                        int nchunks, const int32_t* slot_chunk, int nslots, int S, int B, const int32_t* fgl, int nfl,
-                       int feat_major, const double* inv_scale, long long* slab, float* H, hipStream_t stream) {
+                       int feat_major, const double* inv_scale, long long* slab, float* H, hipStream_t stream,
+                       int pack) {
   if (nslots <= 0) return 0;
-  if (F <= 0 || S < 1 || S > 4 || B <= 0 || B > 256) return 1;
-  const size_t lds = (size_t)B * S * 32 * sizeof(long long);
+  if (F <= 0 || S < 1 || S > 4 || B <= 0 || B > 256 || (pack && S != 3)) return 1;
+  const size_t lds = (size_t)B * (pack ? 2 : S) * 32 * sizeof(long long);
   if (lds > 160 * 1024) return 1;
   const int nfg = fgl != nullptr ? nfl : (F + 31) / 32;
   if (nfg <= 0) return 0;
@@ -470,14 +524,15 @@ int alink_tree_hist_fm(const uint8_t* bins, int F, const int32_t* ridx, const in
     const int64_t quads = (int64_t)nchunks * ((nfg + 3) / 4);
     const int64_t grid = (quads + 7) / 8 * 32;
     if (grid > 0x7fffffff) return 1;
-    const int rc = S == 1 ? launch_fm<1>(ridx != nullptr, grid, lds, stream, bins, F, ridx, q, chunk_rows, nchunks, fgl, nfg, B, slab)
+    const int rc = pack ? launch_fm<3, true>(ridx != nullptr, grid, lds, stream, bins, F, ridx, q, chunk_rows, nchunks, fgl, nfg, B, slab)
+                 : S == 1 ? launch_fm<1>(ridx != nullptr, grid, lds, stream, bins, F, ridx, q, chunk_rows, nchunks, fgl, nfg, B, slab)
                  : S == 2 ? launch_fm<2>(ridx != nullptr, grid, lds, stream, bins, F, ridx, q, chunk_rows, nchunks, fgl, nfg, B, slab)
                  : S == 3 ? launch_fm<3>(ridx != nullptr, grid, lds, stream, bins, F, ridx, q, chunk_rows, nchunks, fgl, nfg, B, slab)
                           : launch_fm<4>(ridx != nullptr, grid, lds, stream, bins, F, ridx, q, chunk_rows, nchunks, fgl, nfg, B, slab);
     if (rc != 0) return rc;
   }
   hipLaunchKernelGGL(tree_hist_fm_reduce, dim3((unsigned)(nslots * nfg), (unsigned)((B + kRedBins - 1) / kRedBins)),
-                     dim3(256), 0, stream, slab, slot_chunk, fgl, nfg, nslots, F, B, S, inv_scale, feat_major, H);
+                     dim3(256), 0, stream, slab, slot_chunk, fgl, nfg, nslots, F, B, S, inv_scale, feat_major, H, pack);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 

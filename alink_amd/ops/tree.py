@@ -61,15 +61,21 @@ import os
 HIST_VARIANT = int(os.environ.get("ALINK_TREE_HIST_VARIANT", "2"))
 FM_TARGET_BLOCKS = 2048       # histogram workgroups per launch (one 32-feature group x one row chunk each)
 FM_MIN_ROWS = 8192            # rows per chunk floor: the LDS clear + slab store amortise over >= 0.5 MB of bins
+FM_PACK_MAX_ROWS = 1 << 16    # packed (g, count) histograms: rows per chunk below 2^16 (csrc/tree_hist.hip PACK)
+# packed statistic + count LDS atomics for S == 3 with a unit count column (ALINK_TREE_HIST_PACK=0 disables)
+FM_PACK = os.environ.get("ALINK_TREE_HIST_PACK", "1") != "0"
 
 
-def fm_plan(counts, nfg: int):
+def fm_plan(counts, nfg: int, max_rows: int = None):
     """Chunking of slot-grouped rows for ``tree_hist_fm``: ``counts[s]`` rows of slot s (consecutive in the
-    sorted order).  Returns (chunk_rows [nchunks+1], slot_chunk [nslots+1]) as int32 numpy arrays."""
+    sorted order); ``max_rows`` caps the rows of a chunk.  Returns (chunk_rows [nchunks+1], slot_chunk
+    [nslots+1]) as int32 numpy arrays."""
     import numpy as np
     counts = np.asarray(counts, dtype=np.int64)
     total = int(counts.sum())
     R = max(FM_MIN_ROWS, -(-total * nfg // FM_TARGET_BLOCKS)) if total else FM_MIN_ROWS
+    if max_rows is not None:
+        R = min(R, int(max_rows))
     nch = -(-counts // R)
     slot_chunk = np.zeros(counts.size + 1, dtype=np.int64)
     np.cumsum(nch, out=slot_chunk[1:])
@@ -122,6 +128,8 @@ class FmStats:
         n, S = stats.shape
         self.S = S
         self.n = n
+        # the packed kernel keeps the count in the low bits of statistic 0 (exact row counts, 2 atomics per pair)
+        self.pack = bool(FM_PACK and S == 3 and n and bool((stats[:, 2] == 1).all()))
         scales = fm_scales(stats)
         dev = stats.device
         self.q = torch.zeros((n, 4), dtype=torch.int32, device=dev)
@@ -164,15 +172,16 @@ def _histogram_fm(L, bins, slot, stats, nslots: int, B: int, prep: "FmStats" = N
         hist = torch.empty((nfg * 32, nslots, B, S), dtype=torch.float32, device=dev)
         if nfg == 0:
             return hist
-    chunk_rows, slot_chunk = fm_plan(counts, nfg)
+    chunk_rows, slot_chunk = fm_plan(counts, nfg, FM_PACK_MAX_ROWS - 1 if prep.pack else None)
     nchunks = chunk_rows.size - 1
     cr = torch.from_numpy(chunk_rows).to(dev)
     scn = torch.from_numpy(slot_chunk).to(dev)
-    slab = torch.empty(max(nchunks, 1) * nfg * B * S * 32, dtype=torch.int64, device=dev)
+    slab = torch.empty(max(nchunks, 1) * nfg * B * (2 if prep.pack else S) * 32, dtype=torch.int64, device=dev)
     rc = L.alink_tree_hist_fm(bins.data_ptr(), F, None if ridx is None else ridx.data_ptr(), q.data_ptr(),
                               cr.data_ptr(), nchunks, scn.data_ptr(), nslots, S, B,
                               None if fgl is None else fgl.data_ptr(), nfg, int(fgl is not None),
-                              prep.inv.data_ptr(), slab.data_ptr(), hist.data_ptr(), _lib.stream_ptr(dev))
+                              prep.inv.data_ptr(), slab.data_ptr(), hist.data_ptr(), _lib.stream_ptr(dev),
+                              int(prep.pack))
     if rc != 0:
         raise RuntimeError(f"alink_tree_hist_fm failed: {rc}")
     return hist
@@ -189,7 +198,9 @@ def histogram_groups(bins: torch.Tensor, slot: torch.Tensor, stats: torch.Tensor
     reference over the selected columns."""
     n, F = bins.shape
     S = stats.shape[1]
-    if fm_eligible(bins, S, B):
+    if prep is None and S == 3 and FM_PACK and fm_eligible(bins, S, B, pack=True):
+        prep = FmStats(stats)
+    if fm_eligible(bins, S, B, pack=prep is not None and prep.pack):
         return _histogram_fm(_lib.require(), bins, slot.to(torch.int32).contiguous(), stats, nslots, B, prep,
                              fgroups=fgroups)
     feats = torch.tensor([g * 32 + l for g in fgroups for l in range(32)], dtype=torch.long)
@@ -204,10 +215,11 @@ def histogram_groups(bins: torch.Tensor, slot: torch.Tensor, stats: torch.Tensor
     return out
 
 
-def fm_eligible(bins: torch.Tensor, S: int, B: int, variant: int = None) -> bool:
+def fm_eligible(bins: torch.Tensor, S: int, B: int, variant: int = None, pack: bool = False) -> bool:
+    """The fixed-point kernel fits: its LDS histogram is [B, S, 32] int64 ([B, 2, 32] when packed)."""
     v = HIST_VARIANT if variant is None else int(variant)
-    return bins.is_cuda and v == 2 and S <= 4 and B * S * 256 <= 160 * 1024 and bins.shape[0] < 2 ** 31 \
-        and _lib.available()
+    return bins.is_cuda and v == 2 and S <= 4 and B * (2 if pack else S) * 256 <= 160 * 1024 \
+        and bins.shape[0] < 2 ** 31 and _lib.available()
 
 
 def histogram(bins: torch.Tensor, slot: torch.Tensor, stats: torch.Tensor, nslots: int, B: int,
@@ -229,7 +241,9 @@ def histogram(bins: torch.Tensor, slot: torch.Tensor, stats: torch.Tensor, nslot
     stats = stats.to(torch.float32).contiguous()
     if slot.shape[0] != n or stats.shape[0] != n:
         raise ValueError("slot/stats row count mismatch")
-    if fm_eligible(bins, S, B, variant) and nslots > 0:
+    if prep is None and S == 3 and FM_PACK and fm_eligible(bins, S, B, variant, pack=True):
+        prep = FmStats(stats)               # decides whether the packed (g, count) build applies
+    if fm_eligible(bins, S, B, variant, pack=prep is not None and prep.pack) and nslots > 0:
         return _histogram_fm(L, bins, slot, stats, nslots, B, prep)
     hist = torch.zeros((nslots, F, B, S), dtype=torch.float32, device=bins.device)
     if n == 0 or nslots == 0:

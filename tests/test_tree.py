@@ -458,3 +458,37 @@ def test_random_forest_memory_bounded_levels_identical_trees():
     assert deep > 100                        # the default unbounded depth grows wide levels
     assert len(small) == len(big) > 100
     assert small[1:] == big[1:]              # every tree row (the meta row records the differing budget)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,F,B,nslots,sampled", [(150000, 130, 129, 1, False), (150000, 130, 129, 1, True),
+                                                  (200000, 64, 129, 9, True), (70001, 33, 17, 3, False),
+                                                  (300000, 32, 255, 1, False)])
+def test_hip_histogram_fm_packed_count_bit_identical(n, F, B, nslots, sampled, monkeypatch):
+    """Packed (g, count) LDS atomics (S == 3, unit count column): two atomics per (row, feature) instead of three,
+    chunks capped below 2^16 rows — the histogram is bitwise the unpacked one (exact fixed point), counts exact."""
+    rng = np.random.default_rng(n + F)
+    bins = torch.as_tensor(rng.integers(0, B, size=(n, F)), dtype=torch.uint8).cuda()
+    slot = torch.zeros(n, dtype=torch.int32) if nslots == 1 else \
+        torch.as_tensor(rng.integers(-1, nslots, size=n), dtype=torch.int32)
+    if sampled and nslots == 1:
+        slot[torch.as_tensor(rng.random(n) < 0.3)] = -1
+    slot = slot.cuda()
+    stats = torch.as_tensor(rng.normal(size=(n, 3)), dtype=torch.float32)
+    stats[:, 1] = stats[:, 1].abs()
+    stats[:, 2] = 1.0
+    stats = stats.cuda()
+    monkeypatch.setattr(tops, "FM_PACK", True)
+    p = tops.FmStats(stats)
+    assert p.pack
+    packed = tops.histogram(bins, slot, stats, nslots, B, variant=2, prep=p)
+    monkeypatch.setattr(tops, "FM_PACK", False)
+    q = tops.FmStats(stats)
+    assert not q.pack
+    plain = tops.histogram(bins, slot, stats, nslots, B, variant=2, prep=q)
+    ref = tops.histogram_torch(bins.cpu(), slot.cpu(), stats.cpu().double(), nslots, B)
+    if B * 3 * 256 <= 160 * 1024:
+        assert torch.equal(packed, plain)
+    else:                                   # only the packed layout fits LDS here (the plain build uses fp32 atomics)
+        np.testing.assert_allclose(packed.cpu().double().numpy(), ref.numpy(), rtol=1e-4, atol=2e-3)
+    assert torch.equal(packed[..., 2].cpu().double(), ref[..., 2])
