@@ -23,18 +23,39 @@ class DetailBlock:
     ``quoted``: the map's values are strings (``HashMap<String, String>``, linear / softmax mappers) or, when False,
     JSON numbers (``HashMap<String, Double>``, the tree mappers) — both ``Double.toString`` of the probability."""
 
-    __slots__ = ("labels", "probs", "nulls", "quoted", "_list")
+    __slots__ = ("labels", "_probs", "_probs_t", "nulls", "quoted", "trusted", "_list")
 
-    def __init__(self, labels: Sequence[Any], probs: np.ndarray, nulls: Optional[np.ndarray] = None,
-                 quoted: bool = True):
+    def __init__(self, labels: Sequence[Any], probs, nulls: Optional[np.ndarray] = None,
+                 quoted: bool = True, trusted: bool = False):
+        """``probs``: numpy [n, K], or a (device) torch tensor — then the block stays on the device until something
+        reads ``probs`` / the strings (a scoring -> evaluation stream never copies it to the host).  ``trusted``:
+        the producer guarantees probabilities in [0, 1] summing to 1 per row (a sigmoid pair), so columnar
+        consumers skip the validity scan."""
         self.labels = list(labels)
-        self.probs = np.asarray(probs, dtype=np.float64).reshape(-1, len(self.labels))
+        if hasattr(probs, "detach"):
+            self._probs_t = probs.detach().to(__import__("torch").float64).reshape(-1, len(self.labels))
+            self._probs = None
+        else:
+            self._probs_t = None
+            self._probs = np.asarray(probs, dtype=np.float64).reshape(-1, len(self.labels))
         self.nulls = None if nulls is None or not np.any(nulls) else np.asarray(nulls, dtype=bool)
         self.quoted = bool(quoted)
+        self.trusted = bool(trusted)
         self._list: Optional[List[Optional[str]]] = None
 
+    @property
+    def probs(self) -> np.ndarray:
+        if self._probs is None:
+            self._probs = self._probs_t.cpu().numpy()
+        return self._probs
+
+    def probs_tensor(self):
+        """The probabilities as a torch tensor (on the producer's device when it was one), no host copy."""
+        import torch
+        return self._probs_t if self._probs_t is not None else torch.from_numpy(self._probs)
+
     def __len__(self) -> int:
-        return int(self.probs.shape[0])
+        return int((self._probs_t if self._probs_t is not None else self._probs).shape[0])
 
     def to_list(self) -> List[Optional[str]]:
         if self._list is None:
@@ -62,7 +83,13 @@ class DetailBlock:
             sel = np.asarray(idx)
             if sel.dtype != bool:
                 sel = sel.astype(np.int64)
-        return DetailBlock(self.labels, self.probs[sel], None if self.nulls is None else self.nulls[sel], self.quoted)
+        if self._probs_t is not None and self.nulls is None:
+            import torch
+            t = self._probs_t[sel] if isinstance(sel, slice) else \
+                self._probs_t[torch.as_tensor(sel, device=self._probs_t.device)]
+            return DetailBlock(self.labels, t, None, self.quoted, self.trusted)
+        return DetailBlock(self.labels, self.probs[sel], None if self.nulls is None else self.nulls[sel], self.quoted,
+                           self.trusted)
 
     @staticmethod
     def concat(blocks: Sequence["DetailBlock"]) -> Optional["DetailBlock"]:
@@ -72,7 +99,8 @@ class DetailBlock:
         nulls = None
         if any(b.nulls is not None for b in blocks):
             nulls = np.concatenate([b.nulls if b.nulls is not None else np.zeros(len(b), bool) for b in blocks])
-        return DetailBlock(blocks[0].labels, np.concatenate([b.probs for b in blocks]), nulls, blocks[0].quoted)
+        return DetailBlock(blocks[0].labels, np.concatenate([b.probs for b in blocks]), nulls, blocks[0].quoted,
+                           all(b.trusted for b in blocks))
 
     def __repr__(self):
         return f"DetailBlock(n={len(self)}, labels={self.labels})"

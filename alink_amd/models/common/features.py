@@ -60,7 +60,9 @@ class FeatureMatrix:
     def row_ids(self) -> torch.Tensor:
         if self._row_ids is None:
             counts = self.crow[1:] - self.crow[:-1]
-            self._row_ids = torch.repeat_interleave(torch.arange(self.nrows, device=self.val.device), counts)
+            # output_size: the entry count is known on the host, so no device->host sync for the result size
+            self._row_ids = torch.repeat_interleave(torch.arange(self.nrows, device=self.val.device), counts,
+                                                    output_size=int(self.col.numel()))
         return self._row_ids
 
     def set_ncols(self, d: int) -> "FeatureMatrix":
@@ -169,20 +171,23 @@ class FeatureMatrix:
         if self.dense is not None:
             ones = torch.ones((self.nrows, 1), dtype=self.dense.dtype, device=self.dense.device)
             return FeatureMatrix(torch.cat([ones, self.dense], 1))
+        # every row gains one leading entry: entry i of row r moves to i + r + 1, the new entry sits at the row's
+        # new start — pure index arithmetic, sizes known on the host (no device->host sync, no boolean mask)
         n = self.nrows
+        m = int(self.col.numel())
         counts = self.crow[1:] - self.crow[:-1] + 1
         crow = torch.zeros(n + 1, dtype=torch.int64, device=self.crow.device)
         crow[1:] = torch.cumsum(counts, 0)
-        nnz = int(crow[-1])
+        nnz = m + n
         col = torch.empty(nnz, dtype=self.col.dtype, device=self.col.device)
         val = torch.empty(nnz, dtype=self.val.dtype, device=self.val.device)
         first = crow[:-1]
         col[first] = 0
         val[first] = 1.0
-        mask = torch.ones(nnz, dtype=torch.bool, device=self.col.device)
-        mask[first] = False
-        col[mask] = self.col + 1
-        val[mask] = self.val
+        if m:
+            pos = torch.arange(m, device=self.col.device) + self.row_ids() + 1
+            col[pos] = self.col + 1
+            val[pos] = self.val
         return FeatureMatrix(crow=crow, col=col, val=val, ncols=self._ncols + 1)
 
     def standardize(self, mean: torch.Tensor, std: torch.Tensor, center: bool) -> "FeatureMatrix":

@@ -245,13 +245,22 @@ def binary_summary_block(label_col, blk, label_array: List[str], device=None):
     probability is out of range (the caller then takes the string path and its exact errors)."""
     # the fall-back decision is collective (the string path's all-reduce must run on every rank or on none);
     # ``blk`` None = this rank's micro-batch is empty (it contributes zero bins)
-    valid = float(blk is None or len(blk) == 0 or detail_block_valid(blk, label_array))
+    dev_res = _binary_block_device(label_col, blk, label_array)
+    if dev_res is not None and not comm.is_distributed():
+        return dev_res
+    valid = float(blk is None or len(blk) == 0 or (dev_res is not None) or detail_block_valid(blk, label_array))
     if comm.is_distributed():
         valid = min(comm.all_gather_object(valid))
     if valid < 1.0:
         return None
     if blk is None or len(blk) == 0:
         return _reduce_bins(np.zeros(2 * DETAIL_BIN_NUMBER), 0.0, 0, device or torch.device("cpu"))
+    if dev_res is not None:
+        pb, nb, ll, keep = dev_res
+        buf = torch.cat([pb.to(torch.float64), nb.to(torch.float64), ll.reshape(1), keep.reshape(1).to(torch.float64)])
+        comm.all_reduce(buf, "sum")
+        B = DETAIL_BIN_NUMBER
+        return buf[:B].to(torch.int64), buf[B:2 * B].to(torch.int64), buf[-2], buf[-1].to(torch.int64)
     keys = [str(x) for x in blk.labels]
     ustr, inv, lnull = _label_codes(label_col)
     ok = ~lnull if blk.nulls is None else (~lnull & ~blk.nulls)
@@ -271,6 +280,59 @@ def binary_summary_block(label_col, blk, label_array: List[str], device=None):
     terms = -np.log(np.clip(pl, LOG_LOSS_EPS, 1 - LOG_LOSS_EPS))
     ll = float(np.cumsum(terms)[-1]) if len(terms) else 0.0       # the loop's left-to-right summation order
     return _binary_bins(p0, is_pos, ll, int(sel.sum()), device or torch.device("cpu"))
+
+
+def host_value(x):
+    """numpy array / python scalar of a (device) tensor summary part; anything else unchanged."""
+    if isinstance(x, torch.Tensor):
+        x = x.detach().cpu()
+        return x.numpy() if x.dim() else x.item()
+    return x
+
+
+def _numeric_label_value(s: str, dtype):
+    """The numeric value whose Alink string form is ``s`` for a label column of torch ``dtype``, or None."""
+    from ...common.javafmt import java_str
+    try:
+        v = float(s)
+    except ValueError:
+        return None
+    if dtype.is_floating_point:
+        return v if java_str(v) == s else None
+    return int(v) if v == int(v) and str(int(v)) == s else None
+
+
+def _binary_block_device(label_col, blk, label_array: List[str]):
+    """The binary summary of a device-resident, trusted ``DetailBlock`` (a GPU scorer's output) with a numeric device
+    label column, computed on the device: (positive bins int64 [B], negative bins int64 [B], log loss fp64 0-dim,
+    kept rows int64 0-dim), all device tensors — a scoring -> evaluation stream never copies the micro-batch to the
+    host.  The log loss is a device sum (fp64, any order) instead of the row-order loop.  None when not applicable."""
+    if blk is None or len(blk) == 0 or not blk.trusted or blk._probs_t is None or not blk._probs_t.is_cuda:
+        return None
+    lab = label_col.values
+    if not (isinstance(lab, torch.Tensor) and lab.dim() == 1 and lab.device == blk._probs_t.device) \
+            or label_col.nulls is not None or blk.nulls is not None:
+        return None
+    keys = [str(x) for x in blk.labels]
+    if len(keys) != 2 or set(keys) != set(label_array):
+        return None
+    v0, v1 = (_numeric_label_value(x, lab.dtype) for x in label_array)
+    if v0 is None or v1 is None:
+        return None
+    pr = blk._probs_t
+    c0, c1 = keys.index(label_array[0]), keys.index(label_array[1])
+    is_pos = lab == v0
+    sel = is_pos | (lab == v1)
+    B = DETAIL_BIN_NUMBER
+    p0 = pr[:, c0]
+    idx = torch.where(p0 == 1.0, torch.full_like(p0, B - 1), torch.floor(p0 * B)).to(torch.int64)
+    ok = sel & (idx >= 0) & (idx < B)
+    slot = torch.where(is_pos, idx, idx + B)
+    bins = torch.bincount(torch.where(ok, slot, torch.full_like(slot, 2 * B)), minlength=2 * B + 1)[:2 * B]
+    pl = torch.where(is_pos, p0, pr[:, c1])
+    terms = -torch.log(torch.clamp(pl, LOG_LOSS_EPS, 1 - LOG_LOSS_EPS))
+    ll = torch.where(sel, terms, torch.zeros_like(terms)).sum()
+    return bins[:B], bins[B:], ll, sel.sum()
 
 
 def _binary_detail_native(labels_col, details, label_array: List[str]):
@@ -570,7 +632,9 @@ def _binary_arrays(TP, FP, FN, TN):
 def binary_metrics(posb: np.ndarray, negb: np.ndarray, labels: List[str], logloss: float, total: int
                    ) -> BinaryClassMetrics:
     """``BinaryMetricsSummary.toMetrics`` :72-...: full curves for AUC/PRC/KS, 0.001-sampled curves and
-    threshold arrays, confusion matrix at the threshold nearest 0.5."""
+    threshold arrays, confusion matrix at the threshold nearest 0.5.  Device-tensor summaries (the GPU columnar
+    path) are read back here, once per emitted window."""
+    posb, negb, logloss, total = (host_value(x) for x in (posb, negb, logloss, total))
     eff = np.nonzero((posb != 0) | (negb != 0))[0]
     mid = DETAIL_BIN_NUMBER // 2
     at = int(np.searchsorted(eff, mid))

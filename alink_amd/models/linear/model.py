@@ -294,6 +294,10 @@ class LinearModelMapper(_LinearMapperBase):
         m = self.model
         fm = self._features(mt)
         coef = self._coef(fm.device)
+        if mt.num_rows and fm.device.type == "cuda":
+            dev_cols = self._map_columns_device(fm.mv(coef))
+            if dev_cols is not None:
+                return dev_cols
         dot = fm.mv(coef).cpu().numpy() if mt.num_rows else np.zeros(0)
         tname = m.linearModelType.name
         out = []
@@ -315,6 +319,29 @@ class LinearModelMapper(_LinearMapperBase):
                 out.append(Column(DetailBlock(m.labelValues, np.stack([prob, 1 - prob], 1))))
             else:
                 out.append(Column([None] * mt.num_rows))
+        return out
+
+
+    def _map_columns_device(self, dot: torch.Tensor):
+        """GPU scoring without a host round trip: margins, labels and the detail block stay device tensors (a
+        scoring -> evaluation stream reads them there).  None when the labels are not numeric (host path)."""
+        m = self.model
+        tname = m.linearModelType.name
+        if tname in ("LinearReg", "SVR"):
+            out = [Column(dot)]
+        else:
+            lv = m.labelValues
+            t = self.helper.out_types[0]
+            if t.torch_dtype is None or not all(isinstance(x, (int, float)) and not isinstance(x, bool) for x in lv):
+                return None
+            out = [Column(torch.where(dot >= 0, torch.tensor(lv[0], dtype=t.torch_dtype, device=dot.device),
+                                      torch.tensor(lv[1], dtype=t.torch_dtype, device=dot.device)))]
+        if self.detail_col:
+            if tname in ("LR", "SVM"):
+                prob = 1.0 - 1.0 / (1.0 + torch.exp(dot))
+                out.append(Column(DetailBlock(m.labelValues, torch.stack([prob, 1 - prob], 1), trusted=True)))
+            else:
+                out.append(Column([None] * int(dot.shape[0])))
         return out
 
 

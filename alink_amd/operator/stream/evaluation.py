@@ -107,6 +107,10 @@ class _EvalStream(StreamOperator):
     def _merge(a, b):
         if a is None:
             return b
+        if any(isinstance(x, torch.Tensor) for x in a[1:]) != any(isinstance(x, torch.Tensor) for x in b[1:]):
+            # a device (GPU columnar) summary meets a host one: merge on the host
+            a = (a[0],) + tuple(M.host_value(x) for x in a[1:])
+            b = (b[0],) + tuple(M.host_value(x) for x in b[1:])
         if a[0] == "b":
             return ("b", a[1] + b[1], a[2] + b[2], a[3] + b[3], a[4] + b[4])
         ll = a[2] + b[2] if a[2] >= 0 and b[2] >= 0 else -1.0
@@ -126,6 +130,8 @@ class _EvalStream(StreamOperator):
 
     def _emit_window(self):
         s, self._win, self._win_t0 = self._win, None, None
+        if s is not None:
+            s = (s[0],) + tuple(M.host_value(x) for x in s[1:])     # device summaries: one read per window
         if s is None or s[-1] == 0:
             return
         self._acc = self._merge(self._acc, s)
@@ -137,7 +143,8 @@ class _EvalStream(StreamOperator):
         if mt.num_rows == 0 and not comm.is_distributed():
             return
         s = self._summary(mt)
-        if s is not None and s[-1] != 0:
+        # a device summary's count is not read back per micro-batch: any non-empty micro-batch opens the window
+        if s is not None and (mt.num_rows > 0 if isinstance(s[-1], torch.Tensor) else s[-1] != 0):
             if self._win_t0 is None:
                 self._win_t0 = time.perf_counter()
             self._win = self._merge(self._win, s)
