@@ -66,6 +66,24 @@ class JavaRandom:
     def nextBoolean(self) -> bool:
         return self._next(1) != 0
 
+    def shuffle_rows(self, rows) -> "np.ndarray":
+        """``shuffle`` applied to every row of an int array [m, n] in row order, in place — one host C++ call
+        (``_native/csrc/jrandom.cpp``) for a whole tree level; the Python loop without the library."""
+        import ctypes
+        import numpy as np
+        from .. import _native
+        a = np.ascontiguousarray(rows, dtype=np.int32)
+        L = _native.lib
+        if L is not None and hasattr(L, "alink_java_shuffle_rows") and a.ndim == 2 and a.size:
+            st = ctypes.c_uint64(self._seed)
+            L.alink_java_shuffle_rows(ctypes.byref(st), a.ctypes.data_as(ctypes.c_void_p), ctypes.c_int64(a.shape[0]),
+                                      ctypes.c_int32(a.shape[1]))
+            self._seed = int(st.value)
+            return a
+        for r in range(a.shape[0]):
+            a[r] = self.shuffle(a[r].tolist())
+        return a
+
     def shuffle(self, arr: list) -> list:
         """In-place shuffle as ``DecisionTree.shuffle`` (Fisher-Yates from the end, ``nextInt(i + 1)``)."""
         for i in range(len(arr) - 1, 0, -1):

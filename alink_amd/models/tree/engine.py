@@ -596,34 +596,40 @@ class TreeBuilder:
                     for s, i in enumerate(chunk):
                         som[i] = s
                     H = self._histograms(node_of_row, sample, som.to(dev), len(chunk), stats)
+                    Hk = H.cpu() if park else H                    # one copy per pass when parking
                     for s, i in enumerate(chunk):
-                        level_hist[i] = H[s].cpu() if park else H[s]
-                    del H
+                        level_hist[i] = Hk[s]
+                    del H, Hk
+                # sibling subtraction where the histograms live (host when parked: fp32 subtraction rounds the same)
+                tgt = torch.device("cpu") if park else dev
                 for big, (par, others) in derive.items():
-                    h = self._prev_hist[par].to(dev).clone()
+                    h = self._prev_hist[par].to(tgt).clone()
                     for o in others:
-                        h -= level_hist[o].to(dev)
-                    level_hist[big] = h.cpu() if park else h
+                        h -= level_hist[o].to(tgt)
+                    level_hist[big] = h
             if bagging:
-                # every polled node shuffles its inherited splitter order (DecisionTree.bagging), in BFS order
-                for p in level:
-                    p.order = rng.shuffle(list(p.order))
+                # every polled node shuffles its inherited splitter order (DecisionTree.bagging), in BFS order:
+                # the whole level in one host C++ call (the same java.util.Random draws, node after node)
+                orders = rng.shuffle_rows(np.asarray([p.order for p in level], dtype=np.int32))
+                for p, o in zip(level, orders):
+                    p.order = o
             cand_all = [i for i in range(nl) if level[i].splittable]
             splits = {}
             mbatch = self._node_batch(nl, stats.shape[1])[0]
             for c0 in range(0, len(cand_all), mbatch):
                 cand = cand_all[c0:c0 + mbatch]
-                Hn = torch.stack([level_hist[i].to(dev) for i in cand]).to(torch.float32).to(torch.float64)
+                Hn = torch.stack([level_hist[i] for i in cand]).to(dev).to(torch.float32).to(torch.float64)
                 m = len(cand)
                 order = torch.arange(F, device=dev).expand(m, F).clone()
                 ok = fmask[None, :].expand(m, F).clone()
                 if bagging:
-                    ok[:] = False
+                    # the batch's scan orders and admitted features in one host->device copy each
                     k = cfg.node_feature_count or F
-                    for r_, i in enumerate(cand):
-                        pf = level[i].order
-                        order[r_] = torch.as_tensor(pf, device=dev)
-                        ok[r_, torch.as_tensor(pf[:k], device=dev)] = True
+                    ord_np = np.stack([np.asarray(level[i].order, dtype=np.int64) for i in cand])
+                    ok_np = np.zeros((m, F), dtype=bool)
+                    np.put_along_axis(ok_np, ord_np[:, :k], True, axis=1)
+                    order = torch.from_numpy(ord_np).to(dev)
+                    ok = torch.from_numpy(ok_np).to(dev)
                 if self.fshard:
                     gbest, fbest, jbest, mbest, accept, rows_t, prow = self._search_sharded(Hn, order, ok)
                     rows_host = rows_t.cpu().numpy()                                     # [m, B, S]

@@ -93,7 +93,65 @@ class _Partitions:
 
 
 def serialize_tree(root: Node) -> List[str]:
-    """BFS numbering exactly as ``TreeModelDataConverter.serializeTree`` (FIFO queue, ids on enqueue)."""
+    """BFS numbering exactly as ``TreeModelDataConverter.serializeTree`` (FIFO queue, ids on enqueue).  Every
+    double of the tree is formatted in ONE host C++ ``Double.toString`` call and the node strings are assembled
+    from them (``_serialize_tree_gson`` — the generic Gson walk — is the reference form and the fallback)."""
+    fast = _serialize_tree_fast(root)
+    return fast if fast is not None else _serialize_tree_gson(root)
+
+
+def _serialize_tree_fast(root: Node) -> Optional[List[str]]:
+    from ... import _native
+    order = [root]
+    head = 0
+    while head < len(order):
+        nd = order[head]
+        head += 1
+        if not nd.isLeaf():
+            order.extend(nd.nextNodes)
+    vals = []
+    for nd in order:
+        c = nd.counter
+        vals.append(nd.gain)
+        if c is not None:
+            vals.append(c.weightSum)
+            if c.distributions is not None:
+                vals.extend(c.distributions)
+        vals.append(nd.continuousSplit)
+    arr = np.asarray(vals, dtype=np.float64)
+    if not np.all(np.isfinite(arr)):
+        return None
+    body = _native.java_double_join(arr)
+    if body is None:
+        return None
+    strs = body.split(",")
+    out, k, nid = [], 0, 1
+    for i, nd in enumerate(order):
+        c = nd.counter
+        parts = ['{"node":{"featureIndex":', str(int(nd.featureIndex)), ',"gain":', strs[k]]
+        k += 1
+        if c is not None:
+            parts += [',"counter":{"weightSum":', strs[k], ',"numInst":', str(int(c.numInst))]
+            k += 1
+            if c.distributions is not None:
+                nd_ = len(c.distributions)
+                parts += [',"distributions":[', ",".join(strs[k:k + nd_]), "]"]
+                k += nd_
+            parts.append("}")
+        if nd.categoricalSplit is not None:
+            parts += [',"categoricalSplit":[', ",".join(str(int(x)) for x in nd.categoricalSplit), "]"]
+        parts += [',"continuousSplit":', strs[k], '},"id":', str(i)]
+        k += 1
+        if not nd.isLeaf():
+            ids = range(nid, nid + len(nd.nextNodes))
+            nid += len(nd.nextNodes)
+            parts += [',"nextIds":[', ",".join(str(x) for x in ids), "]"]
+        parts.append("}")
+        out.append("".join(parts))
+    return out
+
+
+def _serialize_tree_gson(root: Node) -> List[str]:
     out = []
     nid = 0
     queue = [_NodeSerializable(root, nid)]

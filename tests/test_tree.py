@@ -492,3 +492,24 @@ def test_hip_histogram_fm_packed_count_bit_identical(n, F, B, nslots, sampled, m
     else:                                   # only the packed layout fits LDS here (the plain build uses fp32 atomics)
         np.testing.assert_allclose(packed.cpu().double().numpy(), ref.numpy(), rtol=1e-4, atol=2e-3)
     assert torch.equal(packed[..., 2].cpu().double(), ref[..., 2])
+
+
+def test_fast_tree_serializer_equals_gson_walk():
+    """The batched node serializer (one C++ Double.toString call per tree) writes exactly the generic Gson walk's
+    strings: categorical splits, null counters / distributions, tiny and huge doubles, multi-way children."""
+    from alink_amd.models.tree.model import Node, LabelCounter, _serialize_tree_fast, _serialize_tree_gson
+    rng = np.random.default_rng(0)
+
+    def build(d):
+        if d == 0 or rng.random() < 0.2:
+            c = None if rng.random() < 0.1 else LabelCounter(
+                float(rng.random() * 100), int(rng.integers(100)),
+                None if rng.random() < 0.1 else list(rng.normal(size=3) * 10.0 ** rng.integers(-8, 8)))
+            return Node(-1, 0.0, c)
+        nd = Node(int(rng.integers(10)), float(rng.normal()), LabelCounter(float(rng.random()), 3, [float(rng.normal())]),
+                  [0, 1, -1] if rng.random() < 0.3 else None, float(rng.normal() * 1e-7))
+        nd.nextNodes = [build(d - 1) for _ in range(int(rng.integers(2, 4)))]
+        return nd
+    for _ in range(30):
+        r = build(6)
+        assert _serialize_tree_fast(r) == _serialize_tree_gson(r)
