@@ -13,7 +13,8 @@ import numpy as np
 
 __all__ = ["lib", "parse_csv_lines", "murmur3_utf16", "murmur3_bytes", "murmur3_utf8", "parse_dense_vectors", "ftrl_update_csr",
            "ftrl_partial_margin", "ftrl_shard_update", "parse_binary_detail", "java_double_join",
-           "java_double_rows", "sample_thresholds", "gbdt_rank_grad"]
+           "java_double_rows", "java_double_rows_packed", "parse_csv_packed",
+           "parse_dense_vectors_packed", "sample_thresholds", "gbdt_rank_grad"]
 
 # ALINK_NATIVE_LIB points at another build of the same sources (e.g. the AddressSanitizer build of
 # tools/asan_host.py)
@@ -51,6 +52,22 @@ def _ptr(a: np.ndarray):
     return a.ctypes.data_as(ctypes.c_void_p)
 
 
+def _pack_utf8(strings: Sequence[str]):
+    """(bytes, int64 offsets[n+1]) of UTF-8 strings laid back to back: one join + encode when the text is ASCII
+    (offsets from the character lengths), per-string encodes otherwise."""
+    n = len(strings)
+    off = np.zeros(n + 1, dtype=np.int64)
+    text = "".join(strings)
+    if text.isascii():
+        if n:
+            np.cumsum(np.fromiter(map(len, strings), dtype=np.int64, count=n), out=off[1:])
+        return text.encode("ascii"), off
+    enc = [x.encode("utf-8") for x in strings]
+    if n:
+        np.cumsum(np.fromiter(map(len, enc), dtype=np.int64, count=n), out=off[1:])
+    return b"".join(enc), off
+
+
 def parse_csv_lines(lines: Sequence[str], codes: List[int], delim: str, quote: str, skip_blank: bool):
     """Returns per column (values, nulls): numpy arrays for numeric, python lists for strings; or None."""
     if lib is None:
@@ -59,12 +76,27 @@ def parse_csv_lines(lines: Sequence[str], codes: List[int], delim: str, quote: s
         lines = list(lines)
     else:
         lines = [l for l in lines if l]
-    enc = [l.encode("utf-8") for l in lines]
-    n = len(enc)
-    off = np.zeros(n + 1, dtype=np.int64)
-    if n:
-        np.cumsum([len(b) for b in enc], out=off[1:])
-    buf = b"".join(enc)
+    buf, off = _pack_utf8(lines)
+    try:
+        return parse_csv_packed(np.frombuffer(buf, dtype=np.uint8), off, codes, delim, quote)
+    except _CsvLineError as e:
+        raise RuntimeError(f'Fail to parse line "{lines[e.line]}"') from None
+
+
+class _CsvLineError(RuntimeError):
+    def __init__(self, line: int):
+        super().__init__(f"Fail to parse line {line}")
+        self.line = line
+
+
+def parse_csv_packed(data: np.ndarray, off: np.ndarray, codes: List[int], delim: str, quote: str):
+    """``parse_csv_lines`` over lines already packed as UTF-8 bytes (``data`` uint8, ``off`` int64 [n+1], e.g. a
+    host ``StringBlock``); raises ``RuntimeError`` (with ``.line``) on the first line it cannot parse."""
+    if lib is None:
+        return None
+    data = np.ascontiguousarray(data, dtype=np.uint8) if data.size else np.zeros(1, np.uint8)
+    off = np.ascontiguousarray(off, dtype=np.int64)
+    n = off.size - 1
     ncol = len(codes)
     nums, nulls, soffs, sescs = [], [], [], []
     num_ptrs = (ctypes.c_void_p * ncol)()
@@ -83,15 +115,17 @@ def parse_csv_lines(lines: Sequence[str], codes: List[int], delim: str, quote: s
         sesc_ptrs[c] = se.ctypes.data
     ct = np.asarray(codes, dtype=np.int32)
     q = ord(quote) if quote else -1
-    rc = lib.alink_csv_parse(ctypes.c_char_p(buf), _ptr(off), ctypes.c_int64(n), ctypes.c_int(ncol), _ptr(ct),
+    rc = lib.alink_csv_parse(_ptr(data), _ptr(off), ctypes.c_int64(n), ctypes.c_int(ncol), _ptr(ct),
                              ctypes.c_char(delim.encode()), ctypes.c_int(q), num_ptrs, null_ptrs, soff_ptrs,
                              sesc_ptrs)
     if rc != 0:
-        raise RuntimeError(f'Fail to parse line "{lines[-1 - rc]}"')
+        raise _CsvLineError(-1 - rc)
     out = []
+    raw = None
     for c, t in enumerate(codes):
         nl = nulls[c][:n].astype(bool)
         if t == 0:
+            raw = data.tobytes() if raw is None else raw
             so = soffs[c]
             vals = []
             for i in range(n):
@@ -99,7 +133,7 @@ def parse_csv_lines(lines: Sequence[str], codes: List[int], delim: str, quote: s
                 if a < 0:
                     vals.append(None)
                 else:
-                    s = buf[a:b].decode("utf-8")
+                    s = raw[a:b].decode("utf-8")
                     if sescs[c][i]:
                         s = s.replace(quote * 2, quote)
                     vals.append(s)
@@ -159,9 +193,10 @@ def java_double_join(x) -> Optional[str]:
     return buf[:n].tobytes().decode("ascii")
 
 
-def java_double_rows(x, sep: str = " ") -> Optional[List[str]]:
-    """One string per row of a 2-D float array: ``sep.join(java_double_str(v) for v in row)`` (Alink's dense
-    vector string), formatted in C++; None without the library."""
+def java_double_rows_packed(x, sep: str = " "):
+    """(uint8 bytes, int64 offsets [n+1]) of one string per row of a 2-D float array,
+    ``sep.join(java_double_str(v) for v in row)`` formatted in C++ (OpenMP row blocks) and left packed, the layout
+    of a ``StringBlock``; None without the library."""
     if lib is None or getattr(lib, "alink_java_double_rows", None) is None:
         return None
     a = np.ascontiguousarray(np.asarray(x, dtype=np.float64))
@@ -169,12 +204,22 @@ def java_double_rows(x, sep: str = " ") -> Optional[List[str]]:
         raise ValueError("java_double_rows needs a 2-D array")
     n, k = a.shape
     buf = np.empty(26 * max(a.size, 1) + 16, dtype=np.uint8)
-    ends = np.zeros(max(n, 1), dtype=np.int64)
+    off = np.zeros(n + 1, dtype=np.int64)
     total = lib.alink_java_double_rows(_ptr(a), ctypes.c_int64(n), ctypes.c_int64(k), ctypes.c_char(sep.encode()),
-                                       _ptr(buf), _ptr(ends))
-    text = buf[:total].tobytes().decode("ascii")
-    starts = np.concatenate([[0], ends[:n - 1]]) if n else np.zeros(0, np.int64)
-    return [text[s:e] for s, e in zip(starts.tolist(), ends[:n].tolist())]
+                                       _ptr(buf), _ptr(off[1:]))
+    return buf[:total], off
+
+
+def java_double_rows(x, sep: str = " ") -> Optional[List[str]]:
+    """One string per row of a 2-D float array: ``sep.join(java_double_str(v) for v in row)`` (Alink's dense
+    vector string), formatted in C++; None without the library."""
+    r = java_double_rows_packed(x, sep)
+    if r is None:
+        return None
+    data, off = r
+    text = data.tobytes().decode("ascii")
+    o = off.tolist()
+    return [text[o[i]:o[i + 1]] for i in range(len(o) - 1)]
 
 
 def sample_thresholds(thr, step: float, err: float) -> Optional[np.ndarray]:
@@ -231,17 +276,14 @@ def parse_binary_detail(strings: Sequence[str], key0: str, key1: str):
     if lib is None or getattr(lib, "alink_parse_binary_detail", None) is None:
         return None
     try:
-        enc = [s.encode("utf-8") for s in strings]
-    except AttributeError:
+        buf, off = _pack_utf8(strings)
+    except TypeError:
         return None
-    off = np.zeros(len(enc) + 1, dtype=np.int64)
-    if enc:
-        np.cumsum([len(b) for b in enc], out=off[1:])
-    buf = b"".join(enc)
+    n = len(strings)
     k0, k1 = key0.encode("utf-8"), key1.encode("utf-8")
-    p0 = np.zeros(len(enc), dtype=np.float64)
-    p1 = np.zeros(len(enc), dtype=np.float64)
-    bad = lib.alink_parse_binary_detail(ctypes.c_char_p(buf), _ptr(off), ctypes.c_int64(len(enc)), ctypes.c_char_p(k0),
+    p0 = np.zeros(n, dtype=np.float64)
+    p1 = np.zeros(n, dtype=np.float64)
+    bad = lib.alink_parse_binary_detail(ctypes.c_char_p(buf), _ptr(off), ctypes.c_int64(n), ctypes.c_char_p(k0),
                                         ctypes.c_int(len(k0)), ctypes.c_char_p(k1), ctypes.c_int(len(k1)), _ptr(p0),
                                         _ptr(p1))
     return None if bad != 0 else (p0, p1)
@@ -250,14 +292,20 @@ def parse_binary_detail(strings: Sequence[str], key0: str, key1: str):
 def parse_dense_vectors(strings: Sequence[str], d: int) -> Optional[np.ndarray]:
     if lib is None:
         return None
-    enc = [s.encode("ascii") for s in strings]
-    off = np.zeros(len(enc) + 1, dtype=np.int64)
-    if enc:
-        np.cumsum([len(b) for b in enc], out=off[1:])
-    buf = b"".join(enc)
-    out = np.zeros((len(enc), d), dtype=np.float64)
-    rc = lib.alink_parse_dense_vectors(ctypes.c_char_p(buf), _ptr(off), ctypes.c_int64(len(enc)),
-                                       ctypes.c_int64(d), _ptr(out))
+    buf, off = _pack_utf8(strings)
+    return parse_dense_vectors_packed(np.frombuffer(buf, dtype=np.uint8), off, d)
+
+
+def parse_dense_vectors_packed(data: np.ndarray, off: np.ndarray, d: int) -> Optional[np.ndarray]:
+    """[n, d] float64 of packed dense-vector strings (plain decimal tokens split by ' ' / ','; shorter rows are
+    zero-padded), or None (library missing, or a row with another token or more than ``d`` values)."""
+    if lib is None:
+        return None
+    data = np.ascontiguousarray(data, dtype=np.uint8) if data.size else np.zeros(1, np.uint8)
+    off = np.ascontiguousarray(off, dtype=np.int64)
+    n = off.size - 1
+    out = np.zeros((n, d), dtype=np.float64)
+    rc = lib.alink_parse_dense_vectors(_ptr(data), _ptr(off), ctypes.c_int64(n), ctypes.c_int64(d), _ptr(out))
     if rc != 0:
         return None
     return out

@@ -244,14 +244,19 @@ int alink_parse_dense_vectors(const char* buf, const int64_t* off, int64_t n, in
         int64_t j = 0;
         std::string tmp;
         while (p < e) {
-            while (p < e && (*p == ' ' || *p == ',' || *p == '\t')) ++p;
+            while (p < e && (*p == ' ' || *p == ',')) ++p;
             if (p >= e) break;
             const char* q = p;
-            while (q < e && *q != ' ' && *q != ',' && *q != '\t') ++q;
+            while (q < e && *q != ' ' && *q != ',') ++q;
             tmp.assign(p, q - p);
+            // plain decimal tokens only: strtod would also take inf / nan / hex forms Double.parseDouble rejects
+            // (the caller parses anything else on its general path)
+            bool plain = true;
+            for (const char* c = p; c < q; ++c)
+                plain &= (*c >= '0' && *c <= '9') || *c == '.' || *c == 'e' || *c == 'E' || *c == '+' || *c == '-';
             char* ep = nullptr;
             double v = strtod(tmp.c_str(), &ep);
-            if (*ep != 0 || j >= d) {
+            if (!plain || *ep != 0 || j >= d) {
 #pragma omp critical
                 { if (err < 0 || i < err) err = i; }
                 break;
@@ -407,15 +412,44 @@ static int java_double_to(double x, char* out) {
 
 // n rows of k values: row i = java_double(x[i*k]) sep ... sep java_double(x[i*k+k-1]), rows written back to back;
 // row_end[i] = end offset of row i in out (dense-vector strings of a prediction detail column, VectorUtil.toString)
+// Large inputs: OpenMP row blocks format into their own slices of out (capacity 26 per value, the bound each
+// block is given), then the blocks are compacted left in order.
 extern "C" int64_t alink_java_double_rows(const double* x, int64_t n, int64_t k, char sep, char* out,
                                           int64_t* row_end) {
-    int64_t p = 0;
-    for (int64_t i = 0; i < n; ++i) {
-        for (int64_t j = 0; j < k; ++j) {
-            if (j) out[p++] = sep;
-            p += java_double_to(x[i * k + j], out + p);
+    if (n * k < (1 << 16)) {
+        int64_t p = 0;
+        for (int64_t i = 0; i < n; ++i) {
+            for (int64_t j = 0; j < k; ++j) {
+                if (j) out[p++] = sep;
+                p += java_double_to(x[i * k + j], out + p);
+            }
+            row_end[i] = p;
         }
-        row_end[i] = p;
+        return p;
+    }
+    const int64_t rows_per = std::max<int64_t>(1, 8192 / std::max<int64_t>(k, 1));
+    const int64_t nb = (n + rows_per - 1) / rows_per;
+    std::vector<int64_t> blen(nb);
+#pragma omp parallel for schedule(dynamic, 4)
+    for (int64_t b = 0; b < nb; ++b) {
+        const int64_t r0 = b * rows_per, r1 = std::min(n, r0 + rows_per);
+        char* base = out + r0 * k * 26;
+        int64_t p = 0;
+        for (int64_t i = r0; i < r1; ++i) {
+            for (int64_t j = 0; j < k; ++j) {
+                if (j) base[p++] = sep;
+                p += java_double_to(x[i * k + j], base + p);
+            }
+            row_end[i] = p;                     // block-relative for now
+        }
+        blen[b] = p;
+    }
+    int64_t p = 0;
+    for (int64_t b = 0; b < nb; ++b) {
+        const int64_t r0 = b * rows_per, r1 = std::min(n, r0 + rows_per);
+        if (p != r0 * k * 26) std::memmove(out + p, out + r0 * k * 26, (size_t)blen[b]);
+        for (int64_t i = r0; i < r1; ++i) row_end[i] += p;
+        p += blen[b];
     }
     return p;
 }

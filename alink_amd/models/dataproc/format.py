@@ -484,6 +484,193 @@ def _handle_error(params: Params) -> bool:
     return _enum_name(_p(params, "handleInvalid", "ERROR")) == "ERROR"
 
 
+# ---------------------------------------------------------------------------------------------------
+# columnar fast paths: numeric conversions done over whole columns (C++ formatting / parsing) with output
+# identical to the reader -> map -> writer row path; any input outside the exact conditions returns None and
+# the caller takes the row path (which also owns every error / handleInvalid case)
+# ---------------------------------------------------------------------------------------------------
+_SAFE_SEP = set("0123456789.-+eEINaityf")          # separators that could occur inside Double.toString
+
+
+def _native():
+    try:
+        from ... import _native as N
+    except Exception:   # pragma: no cover - library import failure: row path
+        return None
+    return N if N.lib is not None else None
+
+
+def _double_matrix(mt, names: Sequence[str]):
+    """(n, k) float64 numpy of DOUBLE columns without nulls, or None."""
+    import numpy as np
+    import torch
+    cols = []
+    for nm in names:
+        i = find_col_index(mt.schema.names, nm)
+        c = mt.cols[i]
+        if mt.schema.types[i] != Types.DOUBLE or not isinstance(c.values, torch.Tensor) or c.values.dim() != 1:
+            return None
+        if c.nulls is not None and bool(c.nulls.any()):
+            return None
+        cols.append(c.values)
+    if not cols:
+        return None
+    return np.ascontiguousarray(torch.stack(cols, 1).to("cpu", torch.float64).numpy())
+
+
+def _packed_strings(col):
+    """(uint8 bytes, int64 offsets [n+1]) of a string column without nulls — a host view of a ``StringBlock``, or
+    one pack of a list of str — or None."""
+    import numpy as np
+    from ...common.strings import StringBlock
+    v = col.values
+    if isinstance(v, StringBlock):
+        if v.nulls is not None:
+            return None
+        return v.data.cpu().numpy(), v.offsets.cpu().numpy()
+    if not isinstance(v, list) or not all(isinstance(s, str) for s in v):
+        return None
+    N = _native()
+    buf, off = N._pack_utf8(v)
+    return np.frombuffer(buf, dtype=np.uint8), off
+
+
+def _string_block(data, off, prefix: str = ""):
+    """``StringBlock`` over packed ASCII rows, with ``prefix`` prepended to every row."""
+    import numpy as np
+    import torch
+    from ...common.strings import StringBlock
+    if prefix:
+        pb = np.frombuffer(prefix.encode("ascii"), dtype=np.uint8)
+        n, lp = off.size - 1, pb.size
+        lens = np.diff(off)
+        noff = np.zeros(n + 1, dtype=np.int64)
+        np.cumsum(lens + lp, out=noff[1:])
+        out = np.empty(int(noff[-1]), dtype=np.uint8)
+        for j in range(lp):
+            out[noff[:-1] + j] = pb[j]
+        row = np.repeat(np.arange(n, dtype=np.int64), lens)
+        out[np.arange(data.size, dtype=np.int64) + lp * (row + 1)] = data
+        data, off = out, noff
+    return StringBlock(torch.from_numpy(np.array(data, dtype=np.uint8)), torch.from_numpy(off))
+
+
+_CSV_CODES = {Types.DOUBLE: 1, Types.FLOAT: 1, Types.LONG: 2, Types.INT: 2, Types.SHORT: 2, Types.BYTE: 2,
+              Types.BOOLEAN: 3, Types.STRING: 0}
+_INT_RANGE = {Types.INT: 31, Types.SHORT: 15, Types.BYTE: 7}
+
+
+def csv_columns_fast(col, types, delim: str, quote: Optional[str]):
+    """Typed columns of a column of non-empty CSV lines through the C++ parser (the CSV source's bulk path), or
+    None when a line is null / empty / unparsable, a type has no native code or an integer leaves its Java range."""
+    import numpy as np
+    import torch
+    from ...common.table import Column
+    N = _native()
+    if N is None or len(delim) != 1 or (quote is not None and len(quote) > 1):
+        return None
+    if any(t not in _CSV_CODES for t in types):
+        return None
+    packed = _packed_strings(col) if isinstance(col, Column) else _packed_strings(Column(list(col)))
+    if packed is None or (packed[1].size > 1 and not np.diff(packed[1]).all()):
+        return None
+    try:
+        res = N.parse_csv_packed(packed[0], packed[1], [_CSV_CODES[t] for t in types], delim, quote or "")
+    except RuntimeError:
+        return None
+    if res is None:
+        return None
+    out = []
+    for t, (vals, nulls) in zip(types, res):
+        if isinstance(vals, list):
+            out.append(Column(vals))
+            continue
+        if t in _INT_RANGE:
+            b = 1 << _INT_RANGE[t]
+            if vals.size and (int(vals.min()) < -b or int(vals.max()) >= b):
+                return None
+        nm = torch.from_numpy(np.ascontiguousarray(nulls)) if nulls is not None and nulls.any() else None
+        out.append(Column(torch.from_numpy(vals).to(t.torch_dtype), nm))
+    return out
+
+
+def _cols_to_vector(m: "FormatTransMapper", mt):
+    w, names = m.writer, m.reader.names
+    n, prefix = len(w.from_names), ""
+    if w.size > n:
+        prefix = f"${w.size}$"
+    elif 0 < w.size < n:
+        n = w.size
+    X = _double_matrix(mt, w.from_names[:n])
+    N = _native()
+    if X is None or N is None or list(names) != list(w.from_names):
+        return None
+    from ...common.table import Column
+    r = N.java_double_rows_packed(X, " ")
+    return None if r is None else [Column(_string_block(r[0], r[1], prefix))]
+
+
+def _cols_to_csv(m: "FormatTransMapper", mt):
+    w = m.writer
+    if (len(w.delim) != 1 or w.delim in _SAFE_SEP or (w.quote and (len(w.quote) != 1 or w.quote in _SAFE_SEP))
+            or not set(w.cols) <= set(m.reader.names)):
+        return None
+    X = _double_matrix(mt, w.cols)
+    N = _native()
+    if X is None or N is None:
+        return None
+    from ...common.table import Column
+    r = N.java_double_rows_packed(X, w.delim)
+    return None if r is None else [Column(_string_block(r[0], r[1]))]
+
+
+def _vector_to_cols(m: "FormatTransMapper", mt):
+    import numpy as np
+    import torch
+    from ...common.table import Column
+    vn, w = m.reader.names, m.writer
+    if vn is None or len(set(vn)) != len(vn) or any(t != Types.DOUBLE for t in w.types):
+        return None
+    c = mt.cols[m.reader.col]
+    if isinstance(c.values, torch.Tensor) and c.values.dim() == 2:
+        if c.nulls is not None and bool(c.nulls.any()):
+            return None
+        V, d = c.values.to(torch.float64), int(c.values.shape[1])
+    else:
+        N = _native()
+        packed = _packed_strings(c) if N is not None else None
+        if packed is None:
+            return None
+        P = N.parse_dense_vectors_packed(packed[0], packed[1], len(vn))
+        if P is None:
+            return None
+        V, d = torch.from_numpy(P), len(vn)
+    pos = {nm: i for i, nm in enumerate(vn)}
+    out = []
+    for nm in w.names:
+        i = pos.get(nm)
+        if i is None or i >= d:
+            out.append(Column(torch.zeros(V.shape[0], dtype=torch.float64, device=V.device)))
+        else:
+            out.append(Column(V[:, i].contiguous()))
+    return out
+
+
+def _csv_to_cols(m: "FormatTransMapper", mt):
+    r, w = m.reader, m.writer
+    if r.names != w.names or [*r.parser.types] != [*w.types]:
+        return None
+    cols = csv_columns_fast(mt.cols[r.col], w.types, r.parser.delim, r.parser.quote)
+    # an empty typed field is a null map value that ColumnsWriter fails to parse: the row path owns that case
+    if cols is None or any(c.nulls is not None for c in cols):
+        return None
+    return cols
+
+
+_COLUMNAR = {("COLUMNS", "VECTOR"): _cols_to_vector, ("COLUMNS", "CSV"): _cols_to_csv,
+             ("VECTOR", "COLUMNS"): _vector_to_cols, ("CSV", "COLUMNS"): _csv_to_cols}
+
+
 class FormatTransMapper(Mapper):
     """``FormatTransMapper.java`` — ``fromFormat``/``toFormat`` params pick the reader and the writer."""
 
@@ -496,6 +683,15 @@ class FormatTransMapper(Mapper):
                             and _enum_name(self.params.get("toFormat")) == "COLUMNS")
         self.helper = OutputColsHelper(dataSchema, self.writer.names, self.writer.types,
                                        _p(self.params, "reservedCols"))
+        self._fast = _COLUMNAR.get((_enum_name(self.params.get("fromFormat")),
+                                    _enum_name(self.params.get("toFormat"))))
+
+    def _map_columns(self, mt):
+        if self._fast is not None and mt.num_rows > 0:
+            cols = self._fast(self, mt)
+            if cols is not None:
+                return cols
+        return super()._map_columns(mt)
 
     def _map_row_values(self, row):
         ok, m = self.reader.read(row)
@@ -596,6 +792,13 @@ class CsvToColumnsMapper(_StringToColumns):
         super().__init__(dataSchema, params)
         delim = _p(self.params, "csvFieldDelimiter") or _p(self.params, "fieldDelimiter") or ","
         self.parser = CsvParser(self.types, delim, _p(self.params, "quoteChar", '"'))
+
+    def _map_columns(self, mt):
+        if mt.num_rows > 0:
+            cols = csv_columns_fast(mt.cols[self.idx], self.types, self.parser.delim, self.parser.quote)
+            if cols is not None:
+                return cols
+        return super()._map_columns(mt)
 
     def parse(self, text):
         return self.parser.parse(text)

@@ -17,16 +17,25 @@ from ....common.types import AlinkType, Types
 __all__ = ["CsvParser", "CsvFormatter", "parse_token", "parse_timestamp", "format_timestamp"]
 
 
+_INT_BITS = {Types.LONG: 64, Types.INT: 32, Types.SHORT: 16, Types.BYTE: 8}
+
+
 def parse_token(tok: str, t: AlinkType):
     if t == Types.STRING:
         return tok
     if not tok.strip():
         return None
     s = tok.strip()
+    if "_" in s:                                    # Python literal separators: not a Java number
+        raise ValueError(s)
     if t in (Types.DOUBLE, Types.FLOAT, Types.DECIMAL):
         return float(s)
     if t in (Types.LONG, Types.INT, Types.SHORT, Types.BYTE):
-        return int(s)
+        v = int(s)
+        b = _INT_BITS[t]
+        if not -(1 << (b - 1)) <= v < (1 << (b - 1)):   # Long/Integer/Short/Byte.parseX overflow
+            raise ValueError(s)
+        return v
     if t == Types.BOOLEAN:
         ls = s.lower()
         if ls in ("true", "1"):

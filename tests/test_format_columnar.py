@@ -1,0 +1,147 @@
+"""Columnar fast paths of the format conversions (``models/dataproc/format.py``: COLUMNS<->VECTOR, COLUMNS->CSV,
+CSV->COLUMNS, ``CsvToColumnsMapper``): on every input — including the ones outside the fast path's conditions,
+which fall back — the output equals the reader -> map -> writer row path cell for cell (repr, so NaN / -0.0 /
+integer-vs-float differences count)."""
+import numpy as np
+import pytest
+import torch
+
+from alink_amd.common.mapper import Mapper
+from alink_amd.common.params import Params
+from alink_amd.common.table import Column, MTable
+from alink_amd.common.types import TableSchema, Types
+from alink_amd.models.dataproc import format as F
+
+
+def _doubles(n, rng):
+    x = rng.normal(size=n) * 10.0 ** rng.integers(-12, 12, size=n)
+    x[rng.random(n) < 0.05] = 0.0
+    x[rng.random(n) < 0.03] = -0.0
+    x[rng.random(n) < 0.02] = np.nan
+    x[rng.random(n) < 0.02] = np.inf
+    x[rng.random(n) < 0.02] = 1e300
+    x[rng.random(n) < 0.02] = 5e-324
+    return x
+
+
+def _both(m, mt):
+    fast = m.map_table(mt)
+    slow = m.helper.result_table(mt, Mapper._map_columns(m, mt))   # the per-row reader -> writer path
+    rf = [[repr(v) for v in r] for r in fast.rows()]
+    rs = [[repr(v) for v in r] for r in slow.rows()]
+    assert rf == rs
+    return fast
+
+
+def _num_table(k, n, rng, nulls=False):
+    names = [f"c{i}" for i in range(k)]
+    cols = []
+    for _ in range(k):
+        nm = torch.from_numpy(rng.random(n) < 0.1) if nulls else None
+        cols.append(Column(torch.from_numpy(_doubles(n, rng)), nm))
+    return MTable(TableSchema(names, [Types.DOUBLE] * k), cols), names
+
+
+@pytest.mark.parametrize("size", [-1, 3, 9])
+def test_columns_to_vector_fast_equals_rows(size):
+    rng = np.random.default_rng(size + 5)
+    mt, names = _num_table(5, 400, rng)
+    p = Params().set("fromFormat", "COLUMNS").set("toFormat", "VECTOR").set("selectedCols", names) \
+        .set("vectorCol", "vec").set("vectorSize", size)
+    m = F.FormatTransMapper(mt.schema, p)
+    assert m._fast(m, mt) is not None
+    _both(m, mt)
+    mtn, _ = _num_table(5, 200, rng, nulls=True)                 # nulls: row path ("null" cells)
+    assert m._fast(m, mtn) is None
+    _both(m, mtn)
+
+
+@pytest.mark.parametrize("delim", [",", "\t", "|"])
+def test_columns_to_csv_fast_equals_rows(delim):
+    rng = np.random.default_rng(len(delim) + ord(delim))
+    mt, names = _num_table(4, 300, rng)
+    p = Params().set("fromFormat", "COLUMNS").set("toFormat", "CSV").set("selectedCols", names) \
+        .set("csvCol", "csv").set("schemaStr", ", ".join(f"{c} double" for c in names)) \
+        .set("csvFieldDelimiter", delim)
+    m = F.FormatTransMapper(mt.schema, p)
+    assert m._fast(m, mt) is not None
+    _both(m, mt)
+    p2 = p.clone().set("csvFieldDelimiter", ".")                 # separator inside the numbers: row path quotes
+    m2 = F.FormatTransMapper(mt.schema, p2)
+    assert m2._fast(m2, mt) is None
+    _both(m2, mt)
+
+
+def _vec_strings(n, d, rng):
+    out = []
+    for i in range(n):
+        k = int(rng.integers(0, d + 1))
+        v = _doubles(k, rng)
+        v[~np.isfinite(v)] = 1.5
+        sep = ", " if i % 3 == 0 else " "
+        out.append(sep.join(repr(float(x)) for x in v))
+    return out
+
+
+def test_vector_to_columns_fast_equals_rows():
+    rng = np.random.default_rng(11)
+    strs = _vec_strings(300, 6, rng)
+    mt = MTable(TableSchema(["id", "vec"], [Types.LONG, Types.STRING]),
+                [Column(torch.arange(300)), Column(strs)])
+    p = Params().set("fromFormat", "VECTOR").set("toFormat", "COLUMNS").set("vectorCol", "vec") \
+        .set("schemaStr", "f0 double, f1 double, f2 double, f3 double, f4 double, f5 double") \
+        .set("reservedCols", ["id"])
+    m = F.FormatTransMapper(mt.schema, p)
+    assert m._fast(m, mt) is not None
+    _both(m, mt)
+    # NaN / sparse / over-long vectors -> row path
+    for bad in ("NaN 1.0", "$6$0:1.0 3:2.0", "1 2 3 4 5 6 7"):
+        mt2 = MTable(mt.schema, [Column(torch.arange(3)), Column(["1.0 2.0", bad, "3.0"])])
+        assert m._fast(m, mt2) is None
+        _both(m, mt2)
+    # a dense 2-D tensor vector column
+    X = torch.from_numpy(rng.normal(size=(50, 4)))
+    mt3 = MTable(TableSchema(["id", "vec"], [Types.LONG, Types.DENSE_VECTOR]), [Column(torch.arange(50)), Column(X)])
+    m3 = F.FormatTransMapper(mt3.schema, p)
+    assert m3._fast(m3, mt3) is not None
+    _both(m3, mt3)
+
+
+def _csv_lines(n, rng, full=False):
+    out = []
+    for i in range(n):
+        s = ["plain", "", 'with "q"', "a,b", "x"][i % 5]
+        q = '"' + s.replace('"', '""') + '"' if ("," in s or '"' in s) else s
+        d = "" if i % 7 == 0 and not full else repr(float(rng.normal()))
+        li = "" if i % 11 == 0 and not full else str(int(rng.integers(-10 ** 12, 10 ** 12)))
+        b = ["true", "false", "" if not full else "true"][i % 3]
+        out.append(",".join([d, li, q, b, str(int(rng.integers(-100, 100)))]))
+    return out
+
+
+@pytest.mark.parametrize("how", ["ERROR", "SKIP"])
+def test_csv_to_columns_fast_equals_rows(how):
+    rng = np.random.default_rng(3)
+    schema_str = "d double, l long, s string, b boolean, i int"
+    lines = _csv_lines(200, rng)
+    mt = MTable(TableSchema(["csv"], [Types.STRING]), [Column(lines)])
+    p = Params().set("fromFormat", "CSV").set("toFormat", "COLUMNS").set("csvCol", "csv") \
+        .set("schemaStr", schema_str).set("handleInvalid", how)
+    m = F.FormatTransMapper(mt.schema, p)
+    assert m._fast(m, mt) is None                          # empty typed fields: ColumnsWriter's row path
+    if how == "SKIP":
+        _both(m, mt)
+    full = _csv_lines(200, rng, full=True)
+    mtf = MTable(mt.schema, [Column(full)])
+    assert m._fast(m, mtf) is not None
+    _both(m, mtf)
+    m2 = F.CsvToColumnsMapper(mt.schema, Params().set("selectedCol", "csv").set("schemaStr", schema_str)
+                              .set("handleInvalid", how))
+    assert F.csv_columns_fast(lines, m2.types, m2.parser.delim, m2.parser.quote) is not None
+    _both(m2, mt)
+    if how == "SKIP":                                          # an unparsable number / int overflow: row path
+        for extra in ("1.0,notanumber,s,true,1", "1.0,1,s,true,99999999999"):
+            mt2 = MTable(mt.schema, [Column(lines[:5] + [extra])])
+            assert F.csv_columns_fast(lines[:5] + [extra], m2.types, ",", '"') is None
+            _both(m2, mt2)
+            _both(m, mt2)
