@@ -100,6 +100,8 @@ _EXTRA_SIGNATURES = {
     "alink_ftrl_partial_margin_f64": [_c_vp, _c_vp, _c_vp, _c_i64, _c_vp, _c_i64, _c_i64, _c_vp, _c_int, _c_vp],
     "alink_ftrl_coord_update_f64": [_c_vp, _c_i64, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_d, _c_d, _c_d, _c_d,
                                     _c_i64, _c_int, _c_vp],
+    "alink_ftrl_coord_scan_f64": [_c_vp, _c_vp, _c_vp, _c_i64, _c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_d, _c_d, _c_d,
+                                  _c_d, _c_vp],
     "alink_ftrl_coord_long_f64": [_c_vp, _c_vp, _c_vp, _c_i64, _c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_d, _c_d, _c_d,
                                   _c_d, _c_vp],
     "alink_ftrl_prox_f64": [_c_vp, _c_i64, _c_vp, _c_vp, _c_vp, _c_d, _c_d, _c_d, _c_d, _c_int, _c_vp],
@@ -117,6 +119,8 @@ _EXTRA_SIGNATURES = {
     "alink_gbdt_split": [_c_vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_d, _c_d, _c_vp, _c_vp,
                          _c_vp],
     "alink_als_fused_solve": [_c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_int, _c_int, _c_f, _c_vp, _c_vp, _c_vp, _c_vp,
+                              _c_vp, _c_vp],
+    "alink_als_mfma_solve": [_c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_int, _c_int, _c_f, _c_vp, _c_vp, _c_vp, _c_vp,
                               _c_vp, _c_vp],
     "alink_als_heavy_solve": [_c_vp, _c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_f, _c_vp, _c_vp, _c_vp, _c_i64, _c_vp,
                               _c_vp, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp, _c_vp, _c_int, _c_vp],

@@ -10,7 +10,10 @@ projected coordinate-descent NNLS (reference ``NNLSSolver``) for the non-negativ
 
 ``fused_solve(...)``: the GPU default for the unconstrained solve — ``alink_als_fused_solve`` builds each row's
 normal equations in registers (fp64), factors and solves them in LDS, one wave per row; the ``[m, r, r]``
-matrices never touch HBM.  Rows whose matrix is not SPD are re-solved with ``pinv`` on the host side.
+matrices never touch HBM.  Rows whose matrix is not SPD are re-solved with ``pinv`` on the host side.  At rank
+33..64 the light rows run ``alink_als_mfma_solve`` instead: Gram and block LDL^T on the f64 matrix cores
+(``v_mfma_f64_16x16x4``), no LDS; explicit rows with <= 32 ratings take the push-through m x m solve and rows with
+> 16384 ratings the split heavy path.
 """
 from __future__ import annotations
 
@@ -122,6 +125,9 @@ HEAVY_MFMA = int(__import__("os").environ.get("ALINK_ALS_HEAVY_MFMA", "1"))
 # explicit rows with <= 8 / 16 / 32 neighbours (below the padded rank): m x m push-through solve
 # (alink_als_woodbury_solve) instead of the r x r system; 0 disables
 WOODBURY = int(__import__("os").environ.get("ALINK_ALS_WOODBURY", "1"))
+# rank 33..64 light rows: the normal-equation Gram and the block LDL^T solve on the f64 matrix cores
+# (alink_als_mfma_solve); 0 keeps the VALU Gram + Gauss-Jordan kernel (alink_als_fused_solve)
+MFMA_LIGHT = int(__import__("os").environ.get("ALINK_ALS_MFMA_LIGHT", "1"))
 WOODBURY_BUCKETS = tuple(int(x) for x in __import__("os").environ.get("ALINK_ALS_WOODBURY_BUCKETS", "8,16,32")
                          .split(","))
 
@@ -173,12 +179,12 @@ def fused_solve(indptr: torch.Tensor, nbr: torch.Tensor, rating: torch.Tensor, Y
         light = None
     nl = m if light is None else light.numel()
     if nl:
-        rc = L.alink_als_fused_solve(indptr.data_ptr(), nbr.data_ptr(), rating.data_ptr(), Yf.data_ptr(), nl, r,
-                                     int(bool(implicit)), float(alpha), regd.data_ptr(),
-                                     None if yty is None else yty.data_ptr(),
-                                     None if light is None else light.data_ptr(), X.data_ptr(), status.data_ptr(), st)
+        fn = L.alink_als_mfma_solve if (MFMA_LIGHT and RP == 64) else L.alink_als_fused_solve
+        rc = fn(indptr.data_ptr(), nbr.data_ptr(), rating.data_ptr(), Yf.data_ptr(), nl, r, int(bool(implicit)),
+                float(alpha), regd.data_ptr(), None if yty is None else yty.data_ptr(),
+                None if light is None else light.data_ptr(), X.data_ptr(), status.data_ptr(), st)
         if rc != 0:
-            raise RuntimeError(f"alink_als_fused_solve failed: {rc}")
+            raise RuntimeError(f"{fn.__name__} failed: {rc}")
     if heavy.numel():
         # popular items: the neighbour list is split into HEAVY_CHUNK pieces, one wave each (partial Grams
         # summed in fp64), then one wave per row solves

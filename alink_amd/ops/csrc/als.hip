@@ -402,6 +402,224 @@ __global__ __launch_bounds__(64 * GJ_WAVES) void als_fused_solve(const int64_t* 
 }
 
 // ---------------------------------------------------------------------------------------------------------------
+// Light rows on the matrix cores (rank 33..64, RP = 64): the whole normal-equation solve in v_mfma_f64_16x16x4
+// C-layout tiles, fp64 throughout, no LDS.
+//   Basis: the system is formed in the permuted order p = 16 I + m  <->  column j = 4 m + I, so that lane
+//   (k = lane >> 4, m = lane & 15) of a 4-neighbour step loads columns 4m .. 4m+3 of neighbour k with ONE
+//   16-byte load and holds exactly the MFMA operands: A operand of tile row I = c_k y_k[4m + I], B operand of
+//   tile column J = y_k[4m + J].  Gram: 10 upper tiles (I <= J) += A_I x B_J per step (10 MFMAs per 4
+//   neighbours, no cross-lane traffic: the r2 VALU Gram broadcast every neighbour through LDS and was bound by
+//   LDS bandwidth, profiles/als_r3.txt).
+//   Solve: block LDL^T over the 4 x 4 tile grid.  A C-layout tile S (lane: column lane & 15, rows
+//   (lane >> 4) + 4 s in register s) is, register by register, the B operand of S and the A operand of S^T
+//   (checked by tools/micro/mfma_f64_probe.hip), so every product below is "S^T x T" with both tiles straight
+//   from registers:
+//     D_k^-1       sweep operator on the 16 x 16 diagonal tile (cross-lane reads by __shfl; SPD, no pivoting;
+//                  D^-1 is symmetric, so its C-layout also serves as its own A operand; the sweep leaves -D^-1,
+//                  which the products below use as is, so no operand is ever negated);
+//     W_kj = D_k^-1 A_kj;  A_ij -= A_ki^T W_kj  (k < i <= j);  V_kj = A_kj^T D_k^-1 (kept for the back
+//     substitution) -- 88 MFMAs per system;
+//   the vector steps z_k = D_k^-1 b_k, b_i -= A_ki^T z_k, x_k = z_k - sum_j V_kj^T x_j run on the VALU with one
+//   vector entry per lane (tvec: __shfl gathers, 4 FMAs, two xor-shuffle reductions).
+// A non-positive pivot flags the row for the host pinv fallback, as in the other paths.
+// ---------------------------------------------------------------------------------------------------------------
+typedef double d4_t __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ d4_t mf64(double a, double b, d4_t c) {
+  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+// acc + S^T x T (sgn = +1) or acc - S^T x T (sgn = -1)
+template <int SGN>
+__device__ __forceinline__ d4_t mm_tn(const d4_t& S, const d4_t& T, d4_t acc) {
+#pragma unroll
+  for (int s = 0; s < 4; ++s) acc = mf64(SGN > 0 ? S[s] : -S[s], T[s], acc);
+  return acc;
+}
+
+__device__ __forceinline__ d4_t mm_tn0(const d4_t& S, const d4_t& T) {
+  d4_t z = {0.0, 0.0, 0.0, 0.0};
+  return mm_tn<1>(S, T, z);
+}
+
+// vectors: one entry per lane, v[p] at lane p (segment q = entries 16q .. 16q+15).  T^T v_k for a C-layout tile
+// T and segment k: lane (g, m) takes v_k[g + 4s] by __shfl, sums T[g + 4s][m] v_k[g + 4s] over its 4 rows and the
+// partials over g by two xor shuffles -> (T^T v_k)[m] on every lane with column m.
+__device__ __forceinline__ double tvec(const d4_t& T, double v, int k, int g) {
+  double u = 0.0;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) u = fma(T[s], __shfl(v, 16 * k + g + 4 * s), u);
+  u += __shfl_xor(u, 16);
+  u += __shfl_xor(u, 32);
+  return u;
+}
+
+// -D^-1 of an SPD 16 x 16 C-layout tile by 16 sweep steps (after sweeping every index the matrix is -D^-1)
+__device__ __forceinline__ d4_t sweep_neg_inv16(d4_t a, int lane, int& bad) {
+  const int g = lane >> 4, j = lane & 15;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int kr = k >> 2, kg = k & 3;
+    const double d = __shfl(a[kr], 16 * kg + k);                // D[k][k]
+    const double row = __shfl(a[kr], 16 * kg + j);              // D[k][j]
+    double col[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) col[s] = __shfl(a[s], 16 * g + k);   // D[g + 4s][k]
+    bad |= !(d > 0.0);
+    const double rd = rcp_f64(d > 0.0 ? d : 1.0);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int i = g + 4 * s;
+      double v = fma(-col[s] * rd, row, a[s]);
+      v = j == k ? col[s] * rd : v;
+      v = i == k ? row * rd : v;
+      v = (i == k && j == k) ? -rd : v;
+      a[s] = v;
+    }
+  }
+  return a;
+}
+
+constexpr int MF_WAVES = 4;
+
+__host__ __device__ constexpr int ut(int I, int J) { return I * 4 - I * (I - 1) / 2 + (J - I); }   // upper tile id
+
+template <bool VEC4, bool IMPL>
+__global__ __launch_bounds__(64 * MF_WAVES, 3) void als_mfma_solve(const int64_t* __restrict__ indptr,
+                                                                const int32_t* __restrict__ nbr,
+                                                                const float* __restrict__ rating,
+                                                                const float* __restrict__ Y, int r, float alpha,
+                                                                const double* __restrict__ reg,
+                                                                const double* __restrict__ YtY,
+                                                                const int64_t* __restrict__ rows, int64_t nrows,
+                                                                float* __restrict__ X, int32_t* __restrict__ status) {
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int64_t idx = (int64_t)blockIdx.x * MF_WAVES + w;
+  if (idx >= nrows) return;                       // whole wave; no block barrier below
+  const int64_t row = rows != nullptr ? rows[idx] : idx;
+  const int g = lane >> 4, m = lane & 15;
+  const bool colok = VEC4 ? 4 * m < r : true;
+  // tiles start as reg I (+ Y^T Y for implicit feedback); padded dimensions get an identity block
+  d4_t A[10];
+  const double lam = reg[row];
+#pragma unroll
+  for (int I = 0; I < 4; ++I)
+#pragma unroll
+    for (int J = I; J < 4; ++J)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int mi = g + 4 * q;                  // row inside the tile (column: m)
+        const int ji = 4 * mi + I, jj = 4 * m + J; // original indices
+        double add = 0.0;
+        if (IMPL && YtY != nullptr && ji < r && jj < r) add = YtY[ji * r + jj];
+        if (I == J && mi == m) add += ji < r ? lam : 1.0;
+        A[ut(I, J)][q] = add;
+      }
+  double bacc[4] = {0.0, 0.0, 0.0, 0.0};
+  const int64_t s = indptr[row], e = indptr[row + 1];
+  if (e > s) {
+    auto load_y = [&](int64_t nb, float (&y)[4]) {
+      if (VEC4) {
+        if (colok) {
+          const float4 q = *reinterpret_cast<const float4*>(Y + nb * r + 4 * m);
+          y[0] = q.x; y[1] = q.y; y[2] = q.z; y[3] = q.w;
+        } else {
+          y[0] = y[1] = y[2] = y[3] = 0.f;
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) y[q] = 4 * m + q < r ? Y[nb * r + 4 * m + q] : 0.f;
+      }
+    };
+    // one step ahead: factors of the next 4 neighbours and the neighbour ids after them are in flight while this
+    // step's 10 MFMAs run (past-the-end neighbours reload row e - 1 and get weight 0)
+    int64_t tc = s + g < e ? s + g : e - 1;
+    float ycur[4];
+    load_y(nbr[tc], ycur);
+    float rcur = rating[tc];
+    int64_t tn = s + 4 + g < e ? s + 4 + g : e - 1;
+    int32_t nbn = nbr[tn];
+    float rn = rating[tn];
+    for (int64_t t0 = s; t0 < e; t0 += 4) {
+      float ynext[4];
+      load_y(nbn, ynext);
+      const float rnext = rn;
+      const int64_t t2 = t0 + 8 + g < e ? t0 + 8 + g : e - 1;
+      nbn = nbr[t2];
+      rn = rating[t2];
+      const bool live = t0 + g < e;
+      double cw, ww;
+      if (IMPL) {
+        cw = rcur > 0.f ? (double)alpha * rcur : 0.0;
+        ww = rcur > 0.f ? 1.0 + cw : 0.0;
+      } else {
+        cw = 1.0;
+        ww = rcur;
+      }
+      cw = live ? cw : 0.0;
+      ww = live ? ww : 0.0;
+      double yb[4], ya[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        yb[q] = (double)ycur[q];
+        ya[q] = cw * yb[q];
+        bacc[q] = fma(ww, yb[q], bacc[q]);
+      }
+#pragma unroll
+      for (int I = 0; I < 4; ++I)
+#pragma unroll
+        for (int J = I; J < 4; ++J) A[ut(I, J)] = mf64(ya[I], yb[J], A[ut(I, J)]);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) ycur[q] = ynext[q];
+      rcur = rnext;
+    }
+  }
+  // right-hand side b'[p] at lane p: lane (g, m) holds partials of b'[16 q + m] for its neighbour g
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    bacc[q] += __shfl_xor(bacc[q], 16);
+    bacc[q] += __shfl_xor(bacc[q], 32);
+  }
+  double v = g == 0 ? bacc[0] : g == 1 ? bacc[1] : g == 2 ? bacc[2] : bacc[3];
+  // block LDL^T; the vector steps (z_k = D^-1 b_k, b_i -= A_ki^T z_k) run on the VALU between the tile products
+  int bad = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const d4_t Dn = sweep_neg_inv16(A[ut(k, k)], lane, bad);      // -D_k^-1 (symmetric)
+    const double z = -tvec(Dn, v, k, g);
+    v = g == k ? z : v;
+#pragma unroll
+    for (int i = k + 1; i < 4; ++i) {
+      const double u = tvec(A[ut(k, i)], v, k, g);
+      v = g == i ? v - u : v;
+    }
+#pragma unroll
+    for (int j = k + 1; j < 4; ++j) {
+      const d4_t Wn = mm_tn0(Dn, A[ut(k, j)]);                      // -W_kj = -D^-1 A_kj
+#pragma unroll
+      for (int i = k + 1; i <= j; ++i) A[ut(i, j)] = mm_tn<1>(A[ut(k, i)], Wn, A[ut(i, j)]);
+    }
+#pragma unroll
+    for (int j = k + 1; j < 4; ++j) A[ut(k, j)] = mm_tn0(A[ut(k, j)], Dn);   // -V_kj = -A_kj^T D^-1
+  }
+  // back substitution x_k = z_k - sum_{j > k} V_kj^T x_j  (the tiles hold -V_kj)
+#pragma unroll
+  for (int k = 2; k >= 0; --k) {
+    double u = 0.0;
+#pragma unroll
+    for (int j = k + 1; j < 4; ++j) u += tvec(A[ut(k, j)], v, j, g);
+    v = g == k ? v + u : v;
+  }
+  // x'[p] at lane p = 16 q + m -> original index 4 m + q
+  {
+    const int jo = 4 * m + g;
+    if (jo < r) X[row * r + jo] = (float)v;
+  }
+  if (lane == 0) status[row] = bad;
+}
+
+// ---------------------------------------------------------------------------------------------------------------
 // Explicit-feedback rows with few neighbours (m <= P < RP): the push-through identity
 //     (Y_u^T Y_u + reg I_r)^{-1} Y_u^T r_u  =  Y_u^T (Y_u Y_u^T + reg I_m)^{-1} r_u
 // turns the r x r system into an m x m one (padded to P with an identity block).  A user with 10 ratings at rank
@@ -753,6 +971,24 @@ int alink_als_woodbury_solve(const int64_t* indptr, const int32_t* nbr, const fl
                        X, status);
   else
     return 1;
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+// Light rows of rank 33..64 on the matrix cores (als_mfma_solve): same contract as alink_als_fused_solve.
+int alink_als_mfma_solve(const int64_t* indptr, const int32_t* nbr, const float* rating, const float* Y,
+                         int64_t nrows, int r, int implicit, float alpha, const double* reg, const double* YtY,
+                         const int64_t* rows, float* X, int32_t* status, hipStream_t stream) {
+  if (nrows <= 0) return 0;
+  if (r <= 32 || r > 64) return 1;
+  const dim3 grid((unsigned)((nrows + MF_WAVES - 1) / MF_WAVES)), block(64 * MF_WAVES);
+#define ALS_MF(V, I) hipLaunchKernelGGL((als_mfma_solve<V, I>), grid, block, 0, stream, indptr, nbr, rating, Y, r, \
+                                        alpha, reg, YtY, rows, nrows, X, status)
+  const bool v4 = r % 4 == 0;
+  if (v4 && implicit) ALS_MF(true, true);
+  else if (v4) ALS_MF(true, false);
+  else if (implicit) ALS_MF(false, true);
+  else ALS_MF(false, false);
+#undef ALS_MF
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 

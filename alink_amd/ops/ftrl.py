@@ -56,6 +56,9 @@ def ftrl_hogwild(indptr: torch.Tensor, idx: torch.Tensor, val: torch.Tensor, lab
 
 
 LONG_SEGMENT = 256
+# segments with more entries (the intercept: every sample) take the whole-segment speculative block scan
+# (ftrl_coord_scan_kernel) instead of the one-wave chunk walk
+SCAN_SEGMENT = int(__import__("os").environ.get("ALINK_FTRL_SCAN_SEGMENT", "4096"))
 
 
 def _grid(n: int, per: int, cap: int = 4096) -> int:
@@ -133,11 +136,15 @@ def ftrl_shard_update_hip(indptr: torch.Tensor, idx: torch.Tensor, val: torch.Te
         if rc != 0:
             raise RuntimeError(f"alink_ftrl_coord_update_f64 failed: {rc}")
     if nlong:
-        rc = L.alink_ftrl_coord_long_f64(seg.data_ptr(), coord.data_ptr(), lsegs.data_ptr(), nlong, g.data_ptr(),
-                                         w.data_ptr(), n.data_ptr(), z.data_ptr(), int(lo), float(alpha), float(beta),
-                                         float(l1), float(l2), st)
-        if rc != 0:
-            raise RuntimeError(f"alink_ftrl_coord_long_f64 failed: {rc}")
+        huge = counts[lsegs] > SCAN_SEGMENT
+        for fn, ids in ((L.alink_ftrl_coord_long_f64, lsegs[~huge]), (L.alink_ftrl_coord_scan_f64, lsegs[huge])):
+            if ids.numel() == 0:
+                continue
+            ids = ids.contiguous()
+            rc = fn(seg.data_ptr(), coord.data_ptr(), ids.data_ptr(), ids.numel(), g.data_ptr(), w.data_ptr(),
+                    n.data_ptr(), z.data_ptr(), int(lo), float(alpha), float(beta), float(l1), float(l2), st)
+            if rc != 0:
+                raise RuntimeError(f"{fn.__name__} failed: {rc}")
 
 
 def ftrl_dp_gradients(indptr: torch.Tensor, idx: torch.Tensor, val: torch.Tensor, label: torch.Tensor,

@@ -289,3 +289,42 @@ def test_hip_als_woodbury_small_rows_match_rxr(r, monkeypatch):
     A = A + reg[:, None, None] * torch.eye(r, dtype=torch.float64)[None]
     ref = (torch.linalg.pinv(A) @ bb[:, :, None])[:, :, 0].numpy()
     np.testing.assert_allclose(a, ref, rtol=2e-4, atol=2e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("r", [33, 40, 62, 64])
+@pytest.mark.parametrize("implicit", [False, True])
+def test_hip_als_mfma_light_solve_matches_fp64(r, implicit, monkeypatch):
+    """Rank 33..64 light rows on the f64 matrix cores (permuted-basis MFMA Gram + block LDL^T, alink_als_mfma_solve)
+    vs fp64 Cholesky and vs the VALU Gauss-Jordan kernel: rows with 0 .. 300 neighbours (past-the-end steps of the
+    4-neighbour loop), one with 5000, r not a multiple of 4 (scalar loads), repeated neighbours, implicit Y^T Y."""
+    rng = np.random.default_rng(31 + r + implicit)
+    n = 2000
+    counts = np.concatenate([[0, 1, 3, 4, 5, 33, 34, 35, 36, 37, 5000], rng.integers(33, 300, size=600)])
+    m = counts.size
+    indptr = torch.zeros(m + 1, dtype=torch.int64)
+    indptr[1:] = torch.as_tensor(np.cumsum(counts))
+    nnz = int(indptr[-1])
+    nbr = rng.integers(0, n, size=nnz)
+    nbr[int(indptr[6]):int(indptr[7])] = nbr[int(indptr[6])]
+    nbr = torch.as_tensor(nbr, dtype=torch.int32)
+    rt = torch.as_tensor(rng.integers(1, 6, size=nnz).astype(np.float32))
+    if implicit:
+        rt[torch.as_tensor(rng.random(nnz) < 0.2)] = 0.0
+    Y = torch.as_tensor(rng.normal(size=(n, r)) * 0.3, dtype=torch.float32)
+    reg = torch.as_tensor(np.maximum(counts, 1) * 0.05, dtype=torch.float64)
+    YtY = (Y.double().T @ Y.double()) if implicit else None
+    args = (indptr.cuda(), nbr.cuda(), rt.cuda(), Y.cuda(), reg.cuda(), implicit, 2.0,
+            None if YtY is None else YtY.cuda())
+    monkeypatch.setattr(aops, "WOODBURY", 0)           # every row through the r x r kernels
+    monkeypatch.setattr(aops, "MFMA_LIGHT", 1)
+    a = aops.fused_solve(*args).cpu().double().numpy()
+    monkeypatch.setattr(aops, "MFMA_LIGHT", 0)
+    b = aops.fused_solve(*args).cpu().double().numpy()
+    A, bb = aops.normal_equations_torch(indptr, nbr, rt, Y, implicit, 2.0)
+    if implicit:
+        A = A + YtY[None]
+    A = A + reg[:, None, None] * torch.eye(r, dtype=torch.float64)[None]
+    ref = torch.cholesky_solve(bb[:, :, None], torch.linalg.cholesky(A))[:, :, 0].float().double().numpy()
+    np.testing.assert_allclose(a, ref, rtol=2e-5, atol=2e-6)
+    np.testing.assert_allclose(a, b, rtol=2e-5, atol=2e-6)

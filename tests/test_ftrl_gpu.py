@@ -245,3 +245,33 @@ def test_gpu_scoring_to_evaluation_stays_on_device_and_matches_host():
     assert abs(a[2] - b[2]) < 1e-9 * abs(a[2])
     assert abs(float(a[4]["AUC"]) - float(b[4]["AUC"])) < 1e-6
     assert int(a[4]["TotalSamples"]) == int(b[4]["TotalSamples"]) == 20000
+
+
+@pytest.mark.parametrize("l1", [0.01, 3.0])
+@pytest.mark.parametrize("drift", [0.0, 0.3])
+def test_ftrl_shard_update_block_scan_matches_native(l1, drift, monkeypatch):
+    """Segments above SCAN_SEGMENT run the whole-segment speculative block scan (ftrl_coord_scan_kernel): equal
+    to the native sequential replay, both when z stays in one prox regime (drift 0.3: one-signed errors) and when
+    it crosses |z| = l1 inside the segment (the scan falls back to the chunk walk from the first failing entry)."""
+    from alink_amd import _native
+    from alink_amd.ops import ftrl as F
+    monkeypatch.setattr(F, "SCAN_SEGMENT", 600)
+    rng = np.random.default_rng(21)
+    nrows, dim = 20000, 30
+    lens = {0: nrows, 1: 5000, 2: 601, 3: 600, 4: 1500}
+    rows = []
+    for r in range(nrows):
+        cols = {c for c, L in lens.items() if r < L} | set(rng.choice(np.arange(5, dim), 2, replace=False).tolist())
+        rows.append([(c, float(rng.normal()) if c else 1.0) for c in sorted(cols)])
+    indptr, idx, val = _csr(rows)
+    err = rng.normal(size=nrows) * 0.5 + drift
+    prm = (0.1, 1.0, l1, 0.02)
+    w0 = rng.normal(size=dim) * 0.1
+    ref = [w0.copy(), np.zeros(dim), np.zeros(dim)]
+    _native.ftrl_shard_update(indptr, idx, val, err, *ref, 0, dim, *prm)
+    dev = [torch.as_tensor(a).cuda() for a in (indptr, idx, val)]
+    st = [torch.tensor(a, dtype=torch.float64, device="cuda") for a in (w0, np.zeros(dim), np.zeros(dim))]
+    F.ftrl_shard_update_hip(*dev, torch.as_tensor(err).cuda(), *st, 0, dim, *prm)
+    torch.cuda.synchronize()
+    for g, r in zip(st, ref):
+        np.testing.assert_allclose(g.cpu().numpy(), r, rtol=1e-10, atol=1e-12)
