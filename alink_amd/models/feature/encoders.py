@@ -619,9 +619,18 @@ class FeatureHasherMapper(Mapper):
         hash("col=val"), 1.0), hashed and assembled into a row-sorted CSR ``SparseBlock`` on the env's device
         (``ops/csrc/feature.hip`` on a GPU) — no per-row Python objects."""
         from ...ops.feature import csr_assemble, murmur3_index
+        from ...common.strings import StringBlock
         dev = feature_device()
         n = mt.num_rows
         m = len(self.num) + len(self.cat)
+        if dev.type == "cuda" and not self.num and n:
+            blocks = [mt.col(c).values for c in self.cat]
+            if all(isinstance(b, StringBlock) and b.device == dev for b in blocks):
+                # every field hashed in one launch straight into the [m, n] entry matrix
+                from ...ops.strings import murmur3_multi_index
+                r = murmur3_multi_index(blocks, [c + "=" for c in self.cat], self.nf)
+                if r is not None:
+                    return [Column(csr_assemble(r[0], None, r[1], self.nf))]
         idx = torch.zeros((m, n), dtype=torch.int64, device=dev)
         val = torch.ones((m, n), dtype=torch.float64, device=dev)
         valid = torch.zeros((m, n), dtype=torch.bool, device=dev)
@@ -630,7 +639,6 @@ class FeatureHasherMapper(Mapper):
             idx[j] = int(self.num_index[j])
             val[j] = torch.from_numpy(v).to(dev)
             valid[j] = torch.from_numpy(~null).to(dev)
-        from ...common.strings import StringBlock
         for j, c in enumerate(self.cat, start=len(self.num)):
             colv = mt.col(c).values
             if isinstance(colv, StringBlock):

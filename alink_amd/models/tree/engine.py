@@ -541,6 +541,101 @@ class TreeBuilder:
         per = self.Fb * self.B * S * (4 if self.dev.type == "cuda" else 8)
         return max(1, int(budget // max(1, per))), nl * per > budget
 
+    def _search_batch(self, level, cand, Hn, fmask, bagging) -> dict:
+        """Best splits of the candidate nodes ``cand`` (level indices) from their histograms ``Hn`` [m, F, B, S]
+        (device): {level index: _Split} for the accepted ones."""
+        cfg, F, B, dev = self.cfg, self.F, self.B, self.dev
+        Hn = Hn.to(torch.float32).to(torch.float64)
+        m = len(cand)
+        order = torch.arange(F, device=dev).expand(m, F).clone()
+        ok = fmask[None, :].expand(m, F).clone()
+        if bagging:
+            # the batch's scan orders and admitted features in one host->device copy each
+            k = cfg.node_feature_count or F
+            ord_np = np.stack([np.asarray(level[i].order, dtype=np.int64) for i in cand])
+            ok_np = np.zeros((m, F), dtype=bool)
+            np.put_along_axis(ok_np, ord_np[:, :k], True, axis=1)
+            order = torch.from_numpy(ord_np).to(dev)
+            ok = torch.from_numpy(ok_np).to(dev)
+        if self.fshard:
+            gbest, fbest, jbest, mbest, accept, rows_t, prow = self._search_sharded(Hn, order, ok)
+            rows_host = rows_t.cpu().numpy()                                     # [m, B, S]
+            perm = None if prow is None else prow[:, None, :].expand(m, F, B - 1)
+        else:
+            gbest, fbest, jbest, mbest, accept, perm = self._search(Hn, order, ok)
+            rows_host = Hn[torch.arange(m, device=dev), fbest].cpu().numpy()      # [m, B, S]
+        if perm is None:                     # GPU / sharded search: rebuild the chosen features' order
+            fb_np = fbest.cpu().numpy()
+            perm_host = np.stack([tops.split_order_key(rows_host[r_], cfg.kind, cfg.n_classes,
+                                                       bool(self.d.is_cat[int(fb_np[r_])]))
+                                  for r_ in range(m)]) if m else np.zeros((0, B - 1), np.int64)
+        else:
+            perm_host = perm[torch.arange(m, device=dev), fbest].cpu().numpy()    # [m, B-1]
+        acc = accept.cpu().numpy()
+        fb, jb, mb, gb = (fbest.cpu().numpy(), jbest.cpu().numpy(), mbest.cpu().numpy(), gbest.cpu().numpy())
+        out = {}
+        for r_, i in enumerate(cand):
+            if acc[r_]:
+                out[i] = self._materialise(rows_host[r_], int(fb[r_]), int(jb[r_]), bool(mb[r_]), perm_host[r_],
+                                           float(gb[r_]))
+        return out
+
+    def _level_parked(self, level, node_of_row, sample, stats, build_ids, derive, mbatch, fmask, bagging):
+        """A level whose histograms exceed the memory budget, one node batch at a time: the batch's built
+        histograms, its derived ones (parent parked on the host from the previous level, minus the siblings
+        built in the same batch: batches are whole sibling groups), the split search, and the park of the
+        accepted nodes' histograms (the next level's parents) to the host in ONE copy.  Returns (splits, parked
+        histograms {level index: host tensor})."""
+        dev, nl = self.dev, len(level)
+        built = set(build_ids)
+        # whole sibling groups (contiguous in BFS order), packed up to mbatch histograms per batch
+        groups, cur = [], []
+        for i in range(nl):
+            if cur and level[i].parent != level[cur[-1]].parent:
+                groups.append(cur)
+                cur = []
+            cur.append(i)
+        if cur:
+            groups.append(cur)
+        batches, cur, cnt = [], [], 0
+        for gr in groups:
+            k = sum(1 for i in gr if i in built or i in derive)
+            if cur and cnt + k > mbatch:
+                batches.append(cur)
+                cur, cnt = [], 0
+            cur.extend(gr)
+            cnt += k
+        if cur:
+            batches.append(cur)
+        splits, parked = {}, {}
+        for batch in batches:
+            bids = [i for i in batch if i in built]
+            hb = {}
+            if bids:
+                som = torch.full((nl,), -1, dtype=torch.int32)
+                for s_, i in enumerate(bids):
+                    som[i] = s_
+                H = self._histograms(node_of_row, sample, som.to(dev), len(bids), stats)
+                for s_, i in enumerate(bids):
+                    hb[i] = H[s_]
+            for big in (i for i in batch if i in derive):
+                par, others = derive[big]
+                h = self._prev_hist[par].to(dev).clone()
+                for o in others:
+                    h -= hb[o]
+                hb[big] = h
+            cand = [i for i in batch if level[i].splittable]
+            if cand:
+                got = self._search_batch(level, cand, torch.stack([hb[i] for i in cand]), fmask, bagging)
+                splits.update(got)
+                keep = [i for i in cand if i in got]
+                if keep:
+                    Hk = torch.stack([hb[i] for i in keep]).cpu()
+                    for s_, i in enumerate(keep):
+                        parked[i] = Hk[s_]
+            del hb
+        return splits, parked
+
     def build(self, stats: torch.Tensor, sample: torch.Tensor, feature_mask: Optional[np.ndarray] = None,
               rng=None) -> Tuple[Node, torch.Tensor, List[Node]]:
         """Grow one tree.  ``stats`` [n, S] per-row statistics, ``sample`` [n] rows that count.
@@ -568,8 +663,15 @@ class TreeBuilder:
             t_level = time.perf_counter()
             for p in level:
                 p.splittable = self._node_splittable(p)
+            if bagging:
+                # every polled node shuffles its inherited splitter order (DecisionTree.bagging), in BFS order:
+                # the whole level in one host C++ call (the same java.util.Random draws, node after node)
+                orders = rng.shuffle_rows(np.asarray([p.order for p in level], dtype=np.int32))
+                for p, o in zip(level, orders):
+                    p.order = o
             # which nodes need a histogram built vs derived from the parent
             build_ids, derive = [], {}
+            parked = None
             if all(k in level_hist for k in range(nl)):
                 pass
             else:
@@ -587,70 +689,38 @@ class TreeBuilder:
                     else:
                         build_ids.extend(need)
                 build_ids = sorted(set(build_ids))
-                # memory bound: one histogram pass holds at most `mb` nodes; a level whose histograms exceed the
-                # budget parks them in host memory (they feed the next level's sibling subtraction)
+                # memory bound: one histogram pass holds at most `mbatch` nodes; a level whose histograms exceed
+                # the budget runs batch by batch (build, derive, search) and parks only its accepted nodes'
+                # histograms (the next level's parents) in host memory
                 mbatch, park = self._node_batch(nl, stats.shape[1])
-                for c0 in range(0, len(build_ids), mbatch):
-                    chunk = build_ids[c0:c0 + mbatch]
-                    som = torch.full((nl,), -1, dtype=torch.int32)
-                    for s, i in enumerate(chunk):
-                        som[i] = s
-                    H = self._histograms(node_of_row, sample, som.to(dev), len(chunk), stats)
-                    Hk = H.cpu() if park else H                    # one copy per pass when parking
-                    for s, i in enumerate(chunk):
-                        level_hist[i] = Hk[s]
-                    del H, Hk
-                # sibling subtraction where the histograms live (host when parked: fp32 subtraction rounds the same)
-                tgt = torch.device("cpu") if park else dev
-                for big, (par, others) in derive.items():
-                    h = self._prev_hist[par].to(tgt).clone()
-                    for o in others:
-                        h -= level_hist[o].to(tgt)
-                    level_hist[big] = h
-            if bagging:
-                # every polled node shuffles its inherited splitter order (DecisionTree.bagging), in BFS order:
-                # the whole level in one host C++ call (the same java.util.Random draws, node after node)
-                orders = rng.shuffle_rows(np.asarray([p.order for p in level], dtype=np.int32))
-                for p, o in zip(level, orders):
-                    p.order = o
+                if park:
+                    parked, level_hist = self._level_parked(level, node_of_row, sample, stats, build_ids, derive,
+                                                            mbatch, fmask, bagging)
+                else:
+                    for c0 in range(0, len(build_ids), mbatch):
+                        chunk = build_ids[c0:c0 + mbatch]
+                        som = torch.full((nl,), -1, dtype=torch.int32)
+                        for s, i in enumerate(chunk):
+                            som[i] = s
+                        H = self._histograms(node_of_row, sample, som.to(dev), len(chunk), stats)
+                        for s, i in enumerate(chunk):
+                            level_hist[i] = H[s]
+                        del H
+                    for big, (par, others) in derive.items():
+                        h = self._prev_hist[par].to(dev).clone()
+                        for o in others:
+                            h -= level_hist[o]
+                        level_hist[big] = h
             cand_all = [i for i in range(nl) if level[i].splittable]
-            splits = {}
-            mbatch = self._node_batch(nl, stats.shape[1])[0]
-            for c0 in range(0, len(cand_all), mbatch):
-                cand = cand_all[c0:c0 + mbatch]
-                Hn = torch.stack([level_hist[i] for i in cand]).to(dev).to(torch.float32).to(torch.float64)
-                m = len(cand)
-                order = torch.arange(F, device=dev).expand(m, F).clone()
-                ok = fmask[None, :].expand(m, F).clone()
-                if bagging:
-                    # the batch's scan orders and admitted features in one host->device copy each
-                    k = cfg.node_feature_count or F
-                    ord_np = np.stack([np.asarray(level[i].order, dtype=np.int64) for i in cand])
-                    ok_np = np.zeros((m, F), dtype=bool)
-                    np.put_along_axis(ok_np, ord_np[:, :k], True, axis=1)
-                    order = torch.from_numpy(ord_np).to(dev)
-                    ok = torch.from_numpy(ok_np).to(dev)
-                if self.fshard:
-                    gbest, fbest, jbest, mbest, accept, rows_t, prow = self._search_sharded(Hn, order, ok)
-                    rows_host = rows_t.cpu().numpy()                                     # [m, B, S]
-                    perm = None if prow is None else prow[:, None, :].expand(m, F, B - 1)
-                else:
-                    gbest, fbest, jbest, mbest, accept, perm = self._search(Hn, order, ok)
-                    rows_host = Hn[torch.arange(m, device=dev), fbest].cpu().numpy()      # [m, B, S]
-                if perm is None:                     # GPU / sharded search: rebuild the chosen features' order
-                    fb_np = fbest.cpu().numpy()
-                    perm_host = np.stack([tops.split_order_key(rows_host[r_], cfg.kind, cfg.n_classes,
-                                                               bool(self.d.is_cat[int(fb_np[r_])]))
-                                          for r_ in range(m)]) if m else np.zeros((0, B - 1), np.int64)
-                else:
-                    perm_host = perm[torch.arange(m, device=dev), fbest].cpu().numpy()    # [m, B-1]
-                acc = accept.cpu().numpy()
-                fb, jb, mb, gb = (fbest.cpu().numpy(), jbest.cpu().numpy(), mbest.cpu().numpy(),
-                                  gbest.cpu().numpy())
-                for r_, i in enumerate(cand):
-                    if acc[r_]:
-                        splits[i] = self._materialise(rows_host[r_], int(fb[r_]), int(jb[r_]), bool(mb[r_]),
-                                                      perm_host[r_], float(gb[r_]))
+            if parked is not None:
+                splits = parked
+            else:
+                splits = {}
+                mbatch = self._node_batch(nl, stats.shape[1])[0]
+                for c0 in range(0, len(cand_all), mbatch):
+                    cand = cand_all[c0:c0 + mbatch]
+                    Hn = torch.stack([level_hist[i] for i in cand]).to(dev)
+                    splits.update(self._search_batch(level, cand, Hn, fmask, bagging))
             # finalize nodes in BFS order; children form the next level
             nxt: List[_Pending] = []
             feat = np.full(nl, -1, dtype=np.int32)

@@ -98,14 +98,15 @@ _EXTRA_SIGNATURES = {
     "alink_ftrl_hogwild_f64": [_c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_vp, _c_vp, _c_vp, _c_d, _c_d, _c_d, _c_d, _c_int,
                                _c_vp],
     "alink_ftrl_partial_margin_f64": [_c_vp, _c_vp, _c_vp, _c_i64, _c_vp, _c_i64, _c_i64, _c_vp, _c_int, _c_vp],
-    "alink_ftrl_coord_update_f64": [_c_vp, _c_i64, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_d, _c_d, _c_d, _c_d,
-                                    _c_i64, _c_int, _c_vp],
-    "alink_ftrl_coord_scan_f64": [_c_vp, _c_vp, _c_vp, _c_i64, _c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_d, _c_d, _c_d,
-                                  _c_d, _c_vp],
-    "alink_ftrl_coord_long_f64": [_c_vp, _c_vp, _c_vp, _c_i64, _c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_d, _c_d, _c_d,
-                                  _c_d, _c_vp],
+    "alink_ftrl_coord_update_f64": [_c_vp, _c_i64, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_i64, _c_d, _c_d,
+                                    _c_d, _c_d, _c_i64, _c_int, _c_vp],
+    "alink_ftrl_coord_scan_f64": [_c_vp, _c_vp, _c_vp, _c_i64, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_d, _c_d,
+                                  _c_d, _c_d, _c_int, _c_vp],
+    "alink_ftrl_coord_long_f64": [_c_vp, _c_vp, _c_vp, _c_i64, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_d, _c_d,
+                                  _c_d, _c_d, _c_int, _c_vp],
     "alink_ftrl_prox_f64": [_c_vp, _c_i64, _c_vp, _c_vp, _c_vp, _c_d, _c_d, _c_d, _c_d, _c_int, _c_vp],
     "alink_murmur3_utf8_index": [_c_vp, _c_vp, _c_i64, _c_vp, _c_int, ctypes.c_uint32, _c_i64, _c_vp, _c_vp, _c_vp],
+    "alink_murmur3_multi_index": [_c_vp, _c_int, _c_i64, ctypes.c_uint32, _c_i64, _c_vp, _c_vp, _c_vp],
     "alink_murmur3_bytes": [_c_vp, _c_vp, _c_i64, ctypes.c_uint32, _c_vp, _c_vp],
     "alink_vector_assemble": [_c_i64, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_int, _c_vp],
     "alink_murmur3_index": [_c_vp, _c_vp, _c_i64, _c_vp, _c_int, ctypes.c_uint32, _c_i64, _c_vp, _c_vp, _c_vp],

@@ -94,14 +94,17 @@ __global__ __launch_bounds__(THREADS) void ftrl_partial_margin_kernel(const int6
 // a walk over a contiguous g run: the n / sqrt / denominator chain does not depend on z, so unrolled steps
 // overlap it with the z recurrence.  State arrays are the owned shard (index - lo).
 __global__ __launch_bounds__(256) void ftrl_coord_update_kernel(const int64_t* __restrict__ seg, int64_t nseg,
+                                                               const int64_t* __restrict__ nseg_dev,
                                                                const int64_t* __restrict__ coord,
                                                                const double* __restrict__ g, double* w, double* n,
-                                                               double* z, int64_t lo, double alpha, double beta,
-                                                               double l1, double l2, int64_t maxlen) {
+                                                               double* z, int64_t lo, int64_t hi, double alpha,
+                                                               double beta, double l1, double l2, int64_t maxlen) {
     const double ia = 1.0 / alpha;
-    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nseg; q += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t ns = nseg_dev != nullptr ? *nseg_dev : nseg;   // device-side count: no host sync to size it
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < ns; q += (int64_t)gridDim.x * blockDim.x) {
         const int64_t s = seg[q], e = seg[q + 1];
         if (e - s > maxlen) continue;                 // ftrl_coord_long_kernel's segment
+        if (coord[q] >= hi) continue;                 // entries of coordinates this shard does not own
         const int64_t i = coord[q] - lo;
         double wi = w[i], ni = n[i], zi = z[i], sq = sqrt(ni);
         // The only serial dependence is z -> w -> z: sigma_t and the prox denominator depend on n alone (a prefix
@@ -209,19 +212,23 @@ __device__ void long_chain(const double* __restrict__ g, int64_t s, int64_t e, i
 
 __global__ __launch_bounds__(64) void ftrl_coord_long_kernel(const int64_t* __restrict__ seg,
                                                             const int64_t* __restrict__ coord,
-                                                            const int64_t* __restrict__ lsegs,
+                                                            const int64_t* __restrict__ lsegs, int64_t nlong,
+                                                            const int64_t* __restrict__ nlong_dev,
                                                             const double* __restrict__ g, double* w, double* n,
                                                             double* z, int64_t lo, double alpha, double beta,
                                                             double l1, double l2) {
     const int lane = threadIdx.x;
-    const int64_t q = lsegs[blockIdx.x];
-    const int64_t i = coord[q] - lo;
-    double wi = w[i], ni = n[i], zi = z[i];
-    long_chain(g, seg[q], seg[q + 1], lane, 1.0 / alpha, beta, l1, l2, wi, ni, zi);
-    if (lane == 0) {
-        w[i] = wi;
-        n[i] = ni;
-        z[i] = zi;
+    const int64_t cnt = nlong_dev != nullptr ? *nlong_dev : nlong;
+    for (int64_t li = blockIdx.x; li < cnt; li += gridDim.x) {
+        const int64_t q = lsegs[li];
+        const int64_t i = coord[q] - lo;
+        double wi = w[i], ni = n[i], zi = z[i];
+        long_chain(g, seg[q], seg[q + 1], lane, 1.0 / alpha, beta, l1, l2, wi, ni, zi);
+        if (lane == 0) {
+            w[i] = wi;
+            n[i] = ni;
+            z[i] = zi;
+        }
     }
 }
 
@@ -284,17 +291,21 @@ __device__ Aff block_excl_aff(Aff v, double* sa, double* sb) {
     return lane == 0 ? off : aff_then(off, ex);
 }
 
-__global__ __launch_bounds__(SCAN_NT) void ftrl_coord_scan_kernel(const int64_t* __restrict__ seg,
-                                                                const int64_t* __restrict__ coord,
-                                                                const int64_t* __restrict__ lsegs,
-                                                                const double* __restrict__ g, double* w, double* n,
-                                                                double* z, int64_t lo, double alpha, double beta,
-                                                                double l1, double l2) {
-    __shared__ double sh_a[SCAN_NT / 64], sh_b[SCAN_NT / 64];
-    __shared__ long long sh_bad;
-    __shared__ double sh_z, sh_n;
+struct ScanShared {
+    double a[SCAN_NT / 64], b[SCAN_NT / 64];
+    long long bad;
+    double z, n;
+};
+
+__device__ void scan_segment(ScanShared& sm, int64_t q, const int64_t* __restrict__ seg,
+                             const int64_t* __restrict__ coord, const double* __restrict__ g, double* w, double* n,
+                             double* z, int64_t lo, double alpha, double beta, double l1, double l2) {
+    double* sh_a = sm.a;
+    double* sh_b = sm.b;
+    long long& sh_bad = sm.bad;
+    double& sh_z = sm.z;
+    double& sh_n = sm.n;
     const int tid = threadIdx.x;
-    const int64_t q = lsegs[blockIdx.x];
     const int64_t s = seg[q], e = seg[q + 1];
     const int64_t i = coord[q] - lo;
     const double ia = 1.0 / alpha;
@@ -409,6 +420,21 @@ __global__ __launch_bounds__(SCAN_NT) void ftrl_coord_scan_kernel(const int64_t*
     }
 }
 
+__global__ __launch_bounds__(SCAN_NT) void ftrl_coord_scan_kernel(const int64_t* __restrict__ seg,
+                                                                const int64_t* __restrict__ coord,
+                                                                const int64_t* __restrict__ lsegs, int64_t nlong,
+                                                                const int64_t* __restrict__ nlong_dev,
+                                                                const double* __restrict__ g, double* w, double* n,
+                                                                double* z, int64_t lo, double alpha, double beta,
+                                                                double l1, double l2) {
+    __shared__ ScanShared sm;
+    const int64_t cnt = nlong_dev != nullptr ? *nlong_dev : nlong;
+    for (int64_t li = blockIdx.x; li < cnt; li += gridDim.x) {
+        scan_segment(sm, lsegs[li], seg, coord, g, w, n, z, lo, alpha, beta, l1, l2);
+        __syncthreads();                              // the shared state is reused by the next segment
+    }
+}
+
 // w_i = prox(z_i, n_i) for the listed coordinates (all when coords == nullptr): makes the Hogwild weights
 // consistent with the exact n/z sums after a contended micro-batch (the racing w stores are last-writer-wins).
 __global__ __launch_bounds__(256) void ftrl_prox_kernel(const int32_t* __restrict__ coords, int64_t m, double* w,
@@ -458,34 +484,40 @@ int alink_ftrl_partial_margin_f64(const int64_t* indptr, const int32_t* idx, con
     return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
-int alink_ftrl_coord_update_f64(const int64_t* seg, int64_t nseg, const int64_t* coord, const double* g, double* w,
-                                double* n, double* z, int64_t lo, double alpha, double beta, double l1, double l2,
-                                int64_t maxlen, int grid, void* stream) {
+// nseg_dev (nullable): the segment count read on the device (nseg is then only the launch's upper bound);
+// coordinates >= hi are skipped (entries the shard does not own, sorted to the end)
+int alink_ftrl_coord_update_f64(const int64_t* seg, int64_t nseg, const int64_t* nseg_dev, const int64_t* coord,
+                                const double* g, double* w, double* n, double* z, int64_t lo, int64_t hi,
+                                double alpha, double beta, double l1, double l2, int64_t maxlen, int grid,
+                                void* stream) {
     if (nseg <= 0) return 0;
     if (grid <= 0 || alpha <= 0.0) return 1;
     hipLaunchKernelGGL(ftrl_coord_update_kernel, dim3(grid), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), seg,
-                       nseg, coord, g, w, n, z, lo, alpha, beta, l1, l2, maxlen);
+                       nseg, nseg_dev, coord, g, w, n, z, lo, hi, alpha, beta, l1, l2, maxlen);
     return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
 // segments of SCAN_MIN entries or more: one 512-thread speculative scan each (ftrl_coord_scan_kernel)
+// nlong_dev (nullable): the list length read on the device; the launch then has `grid` blocks striding over it
 int alink_ftrl_coord_scan_f64(const int64_t* seg, const int64_t* coord, const int64_t* lsegs, int64_t nlong,
-                              const double* g, double* w, double* n, double* z, int64_t lo, double alpha,
-                              double beta, double l1, double l2, void* stream) {
+                              const int64_t* nlong_dev, const double* g, double* w, double* n, double* z, int64_t lo,
+                              double alpha, double beta, double l1, double l2, int grid, void* stream) {
     if (nlong <= 0) return 0;
-    hipLaunchKernelGGL(ftrl_coord_scan_kernel, dim3((unsigned)nlong), dim3(SCAN_NT), 0,
-                       reinterpret_cast<hipStream_t>(stream), seg, coord, lsegs, g, w, n, z, lo, alpha, beta, l1, l2);
+    const unsigned gb = nlong_dev != nullptr ? (unsigned)(grid > 0 ? grid : 1) : (unsigned)nlong;
+    hipLaunchKernelGGL(ftrl_coord_scan_kernel, dim3(gb), dim3(SCAN_NT), 0, reinterpret_cast<hipStream_t>(stream), seg,
+                       coord, lsegs, nlong, nlong_dev, g, w, n, z, lo, alpha, beta, l1, l2);
     return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
 // long segments (lsegs: nlong segment ids), one wave each
 int alink_ftrl_coord_long_f64(const int64_t* seg, const int64_t* coord, const int64_t* lsegs, int64_t nlong,
-                              const double* g, double* w, double* n, double* z, int64_t lo, double alpha, double beta,
-                              double l1, double l2, void* stream) {
+                              const int64_t* nlong_dev, const double* g, double* w, double* n, double* z, int64_t lo,
+                              double alpha, double beta, double l1, double l2, int grid, void* stream) {
     if (nlong <= 0) return 0;
     if (alpha <= 0.0) return 1;
-    hipLaunchKernelGGL(ftrl_coord_long_kernel, dim3((unsigned)nlong), dim3(64), 0,
-                       reinterpret_cast<hipStream_t>(stream), seg, coord, lsegs, g, w, n, z, lo, alpha, beta, l1, l2);
+    const unsigned gb = nlong_dev != nullptr ? (unsigned)(grid > 0 ? grid : 1) : (unsigned)nlong;
+    hipLaunchKernelGGL(ftrl_coord_long_kernel, dim3(gb), dim3(64), 0, reinterpret_cast<hipStream_t>(stream), seg,
+                       coord, lsegs, nlong, nlong_dev, g, w, n, z, lo, alpha, beta, l1, l2);
     return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 

@@ -58,6 +58,7 @@ def ftrl_hogwild(indptr: torch.Tensor, idx: torch.Tensor, val: torch.Tensor, lab
 LONG_SEGMENT = 256
 # segments with more entries (the intercept: every sample) take the whole-segment speculative block scan
 # (ftrl_coord_scan_kernel) instead of the one-wave chunk walk
+_FOREIGN = 1 << 62          # sort key of entries another shard owns (after every coordinate)
 SCAN_SEGMENT = int(__import__("os").environ.get("ALINK_FTRL_SCAN_SEGMENT", "4096"))
 
 
@@ -99,52 +100,53 @@ def ftrl_shard_update_hip(indptr: torch.Tensor, idx: torch.Tensor, val: torch.Te
                           w: torch.Tensor, n: torch.Tensor, z: torch.Tensor, lo: int, hi: int, alpha: float,
                           beta: float, l1: float, l2: float) -> None:
     """Owned coordinates [lo, hi) replay their entries in sample order with ``err = p - y`` fixed for the
-    micro-batch: entries filtered to the shard, stably sorted by coordinate on the device, one lane per
-    coordinate segment (``ftrl_coord_update_kernel``), one wave per segment longer than ``LONG_SEGMENT``
-    (``ftrl_coord_long_kernel``)."""
+    micro-batch: entries stably sorted by coordinate on the device (entries of other shards keyed past every
+    coordinate), one lane per coordinate segment (``ftrl_coord_update_kernel``), one wave per segment longer than
+    ``LONG_SEGMENT`` (``ftrl_coord_long_kernel``), one 512-thread speculative scan per segment longer than
+    ``SCAN_SEGMENT`` (``ftrl_coord_scan_kernel``).  Segment boundaries, the long-segment lists and their lengths
+    stay on the device (the kernels read the counts there): no host synchronisation in the whole update."""
     L = _lib.require()
     dev = w.device
     nrows = indptr.shape[0] - 1
-    if nrows <= 0 or idx.numel() == 0:
+    nnz = idx.numel()
+    if nrows <= 0 or nnz == 0:
         return
-    lens = indptr[1:] - indptr[:-1]
-    erow = torch.repeat_interleave(torch.arange(nrows, device=dev, dtype=torch.int64), lens)
-    ii = idx.to(torch.int64)
-    if lo == 0 and int(ii.max()) < hi:           # every entry is owned: no filtering pass
-        keys, ent = torch.sort(ii, stable=True)
-    else:
-        ent = torch.nonzero((ii >= lo) & (ii < hi), as_tuple=False).reshape(-1)
-        if ent.numel() == 0:
-            return
-        keys, perm = torch.sort(ii[ent], stable=True)
-        ent = ent[perm]
-    g = (err[erow[ent]] * val[ent]).contiguous()          # per-entry gradient, in coordinate-sorted order
-    coord, counts = torch.unique_consecutive(keys, return_counts=True)
-    seg = torch.zeros(counts.numel() + 1, dtype=torch.int64, device=dev)
-    torch.cumsum(counts, 0, out=seg[1:])
-    nseg = counts.numel()
-    coord = coord.contiguous()
     st = _lib.stream_ptr(dev)
-    # segments longer than LONG_SEGMENT (the intercept, hot categorical values) replay on one wave each with
-    # their off-chain terms computed lane-parallel; the rest one lane per segment
-    lsegs = torch.nonzero(counts > LONG_SEGMENT, as_tuple=False).reshape(-1).contiguous()
-    nlong = lsegs.numel()
-    if nlong < nseg:
-        rc = L.alink_ftrl_coord_update_f64(seg.data_ptr(), nseg, coord.data_ptr(), g.data_ptr(), w.data_ptr(),
-                                           n.data_ptr(), z.data_ptr(), int(lo), float(alpha), float(beta), float(l1),
-                                           float(l2), LONG_SEGMENT, _grid(nseg, 256), st)
+    lens = indptr[1:] - indptr[:-1]
+    erow = torch.repeat_interleave(torch.arange(nrows, device=dev, dtype=torch.int64), lens, output_size=nnz)
+    ii = idx.to(torch.int64)
+    keys = torch.where((ii >= lo) & (ii < hi), ii, torch.full_like(ii, _FOREIGN))
+    keys, ent = torch.sort(keys, stable=True)
+    g = (err[erow[ent]] * val[ent]).contiguous()          # per-entry gradient, in coordinate-sorted order
+    ar = torch.arange(nnz, device=dev, dtype=torch.int64)
+    head = torch.ones(nnz, dtype=torch.bool, device=dev)
+    torch.ne(keys[1:], keys[:-1], out=head[1:])
+    sid = torch.cumsum(head, 0) - 1
+    nseg = sid[-1:] + 1                                    # device scalar
+    seg = torch.empty(nnz + 2, dtype=torch.int64, device=dev)
+    seg.index_put_((torch.where(head, sid, nnz + 1),), ar)     # seg[q] = first entry of segment q (nnz + 1: dummy)
+    seg.index_put_((nseg,), torch.full((1,), nnz, dtype=torch.int64, device=dev))
+    first = seg[:nnz].clamp(0, nnz - 1)                    # slots past nseg hold garbage: never read as segments
+    coord = keys[first].contiguous()
+    cnt = seg[1:nnz + 1] - seg[:nnz]
+    live = (ar < nseg) & (coord < hi)
+    rc = L.alink_ftrl_coord_update_f64(seg.data_ptr(), nnz, nseg.data_ptr(), coord.data_ptr(), g.data_ptr(),
+                                       w.data_ptr(), n.data_ptr(), z.data_ptr(), int(lo), int(hi), float(alpha),
+                                       float(beta), float(l1), float(l2), LONG_SEGMENT, _grid(nnz, 256), st)
+    if rc != 0:
+        raise RuntimeError(f"alink_ftrl_coord_update_f64 failed: {rc}")
+    # segments longer than LONG_SEGMENT (the intercept, hot categorical values): compacted id lists + counts on
+    # the device; the kernels stride over them from a fixed grid
+    for fn, sel, grid in ((L.alink_ftrl_coord_long_f64, live & (cnt > LONG_SEGMENT) & (cnt <= SCAN_SEGMENT), 256),
+                          (L.alink_ftrl_coord_scan_f64, live & (cnt > SCAN_SEGMENT), 16)):
+        pos = torch.cumsum(sel, 0) - 1
+        lst = torch.empty(nnz + 1, dtype=torch.int64, device=dev)
+        lst.index_put_((torch.where(sel, pos, nnz),), ar)
+        num = pos[-1:] + 1
+        rc = fn(seg.data_ptr(), coord.data_ptr(), lst.data_ptr(), nnz, num.data_ptr(), g.data_ptr(), w.data_ptr(),
+                n.data_ptr(), z.data_ptr(), int(lo), float(alpha), float(beta), float(l1), float(l2), grid, st)
         if rc != 0:
-            raise RuntimeError(f"alink_ftrl_coord_update_f64 failed: {rc}")
-    if nlong:
-        huge = counts[lsegs] > SCAN_SEGMENT
-        for fn, ids in ((L.alink_ftrl_coord_long_f64, lsegs[~huge]), (L.alink_ftrl_coord_scan_f64, lsegs[huge])):
-            if ids.numel() == 0:
-                continue
-            ids = ids.contiguous()
-            rc = fn(seg.data_ptr(), coord.data_ptr(), ids.data_ptr(), ids.numel(), g.data_ptr(), w.data_ptr(),
-                    n.data_ptr(), z.data_ptr(), int(lo), float(alpha), float(beta), float(l1), float(l2), st)
-            if rc != 0:
-                raise RuntimeError(f"{fn.__name__} failed: {rc}")
+            raise RuntimeError(f"{fn.__name__} failed: {rc}")
 
 
 def ftrl_dp_gradients(indptr: torch.Tensor, idx: torch.Tensor, val: torch.Tensor, label: torch.Tensor,

@@ -10,6 +10,8 @@ whichever side hashed).
 """
 from __future__ import annotations
 
+import ctypes
+
 import numpy as np
 import torch
 
@@ -90,6 +92,55 @@ def _device_prefix(pu: np.ndarray, prefix: str, dev) -> torch.Tensor:
             _PREFIX_CACHE.clear()
         t = _PREFIX_CACHE[key] = torch.from_numpy(pu).to(dev)
     return t
+
+
+MH_MAX_COLS, MH_MAX_PREFIX = 32, 1024
+
+
+class _MultiHashArgs(ctypes.Structure):
+    """Mirror of ``MultiHashArgs`` (ops/csrc/feature.hip)."""
+    _fields_ = [("data", ctypes.c_void_p * MH_MAX_COLS), ("off", ctypes.c_void_p * MH_MAX_COLS),
+                ("nulls", ctypes.c_void_p * MH_MAX_COLS), ("pstart", ctypes.c_int32 * (MH_MAX_COLS + 1)),
+                ("prefix", ctypes.c_uint16 * MH_MAX_PREFIX)]
+
+
+def murmur3_multi_index(blocks, prefixes, nf: int, seed: int = 0):
+    """(idx int32 [m, n], valid uint8 [m, n]) of ``murmur3_utf8_index(blocks[j], nf, prefixes[j])`` for m device
+    ``StringBlock`` columns of equal length in ONE kernel launch (valid = not NULL; idx 0 there), or None when the
+    columns do not fit the launch table (more than 32, prefixes over 1024 UTF-16 units, not on a GPU)."""
+    m = len(blocks)
+    if m == 0 or m > MH_MAX_COLS or any(b.device.type != "cuda" for b in blocks):
+        return None
+    units = [np.frombuffer(p.encode("utf-16-le"), dtype=np.uint16) for p in prefixes]
+    if sum(u.size for u in units) > MH_MAX_PREFIX:
+        return None
+    n = len(blocks[0])
+    dev = blocks[0].device
+    L = _lib.require()
+    a = _MultiHashArgs()
+    keep = []
+    pos = 0
+    for j, (b, u) in enumerate(zip(blocks, units)):
+        data = b.data if b.nbytes else torch.zeros(1, dtype=torch.uint8, device=dev)
+        off = b.offsets.contiguous()
+        keep += [data, off]
+        a.data[j], a.off[j] = data.data_ptr(), off.data_ptr()
+        if b.nulls is not None:
+            nl = b.nulls.to(dev, torch.bool).contiguous()
+            keep.append(nl)
+            a.nulls[j] = nl.data_ptr()
+        a.pstart[j] = pos
+        for q, c in enumerate(u.tolist()):
+            a.prefix[pos + q] = c
+        pos += u.size
+    a.pstart[m] = pos
+    idx = torch.empty((m, n), dtype=torch.int32, device=dev)
+    valid = torch.empty((m, n), dtype=torch.uint8, device=dev)
+    rc = L.alink_murmur3_multi_index(ctypes.addressof(a), m, n, seed & 0xFFFFFFFF, int(nf), idx.data_ptr(),
+                                     valid.data_ptr(), _lib.stream_ptr(dev))
+    if rc != 0:
+        raise RuntimeError(f"alink_murmur3_multi_index failed: {rc}")
+    return idx, valid
 
 
 def murmur3_utf8_index(block: StringBlock, nf: int, prefix: str = "", seed: int = 0) -> torch.Tensor:

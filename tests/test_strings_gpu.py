@@ -61,3 +61,39 @@ def test_feature_hasher_on_device_string_block_equals_list_column():
     b = FeatureHasherBatchOp().setSelectedCols(["c", "x"]).setCategoricalCols(["c"]).setOutputCol("f") \
         .setNumFeatures(1 << 16).linkFrom(TableSourceBatchOp(mt2)).collect()
     assert [str(r[-1]) for r in a] == [str(r[-1]) for r in b]
+
+
+def test_hip_multi_column_feature_hash_equals_per_column():
+    """murmur3_multi_index: m string columns (different prefixes, NULLs, empty strings, non-ASCII) in one launch ==
+    murmur3_utf8_index per column; and an all-categorical FeatureHasher over device StringBlocks (the one-launch
+    path) == the same strings as Python lists (the per-column path)."""
+    cols = [_words(4000, 10 + j) for j in range(5)]
+    nulls = [None, torch.as_tensor(np.random.default_rng(1).random(4000) < 0.1), None, None, None]
+    blocks = []
+    for w, nl in zip(cols, nulls):
+        b = StringBlock.from_list([None if (nl is not None and bool(nl[i])) else s for i, s in enumerate(w)])
+        blocks.append(b.to("cuda"))
+    prefixes = [f"C{j}=" for j in range(4)] + ["中="]
+    idx, valid = S.murmur3_multi_index(blocks, prefixes, 1 << 20)
+    for j, b in enumerate(blocks):
+        ref = S.murmur3_utf8_index(b, 1 << 20, prefix=prefixes[j])
+        ok = ~b.null_mask()
+        assert torch.equal(valid[j].bool(), ok)
+        assert torch.equal(idx[j].long()[ok], ref[ok])
+    import pandas as pd
+    from alink_amd import useLocalEnv, BatchOperator, FeatureHasherBatchOp
+    from alink_amd.common.mlenv import resetEnv
+    from alink_amd.common.table import Column, MTable
+    from alink_amd.common.types import TableSchema, Types
+    from alink_amd.operator.batch.source import TableSourceBatchOp
+    resetEnv()
+    useLocalEnv(1, device="cuda:0")
+    names = [f"c{j}" for j in range(5)]
+    lists = [[None if (nl is not None and bool(nl[i])) else s for i, s in enumerate(w)] for w, nl in zip(cols, nulls)]
+    df = pd.DataFrame({nm: col for nm, col in zip(names, lists)})
+    op = lambda: FeatureHasherBatchOp().setSelectedCols(names).setCategoricalCols(names).setOutputCol("f") \
+        .setNumFeatures(1 << 18)
+    a = op().linkFrom(BatchOperator.fromDataframe(df, schemaStr=", ".join(f"{c} string" for c in names))).collect()
+    mt = MTable(TableSchema(names, [Types.STRING] * 5), [Column(b) for b in blocks])
+    b = op().linkFrom(TableSourceBatchOp(mt)).collect()
+    assert [str(r[-1]) for r in a] == [str(r[-1]) for r in b]
