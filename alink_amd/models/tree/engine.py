@@ -143,6 +143,11 @@ class _Split:
     threshold: float
 
 
+# GPU fixed-point histograms read the tree's node-grouped row order (tops.RowOrder) below the root; 0: a stable
+# sort of the slot keys and a statistics gather per histogram call
+ROW_ORDER = int(__import__("os").environ.get("ALINK_TREE_ROW_ORDER", "1"))
+
+
 class TreeBuilder:
     """Grows trees over one ``BinnedData`` (rows stay on the device between trees)."""
 
@@ -182,7 +187,10 @@ class TreeBuilder:
         counters, which come from per-node row sums instead — so the kernel moves 3 floats, not 4."""
         return [1, 2, 3] if self.cfg.kind == "gbdt" else list(range(S))
 
-    def _histograms(self, node_of_row, sample, slot_of_node: torch.Tensor, nslots: int, stats) -> torch.Tensor:
+    def _histograms(self, node_of_row, sample, slot_of_node: torch.Tensor, nslots: int, stats,
+                    slot_nodes=None) -> torch.Tensor:
+        """[nslots, F, B, S] histograms of the level nodes ``slot_nodes`` (slot s = node slot_nodes[s]; also
+        given as the device map ``slot_of_node``)."""
         nn = slot_of_node.numel()
         act = sample & (node_of_row >= 0) & (node_of_row < nn)
         slot = torch.where(act, slot_of_node[node_of_row.clamp(0, max(nn - 1, 0)).long()].to(node_of_row.dtype),
@@ -197,10 +205,17 @@ class TreeBuilder:
             self._hist_sub = (stats, sub, prep)
         _, sub, prep = self._hist_sub
         TreeBuilder.HIST_BYTES.append(nslots * self.F * self.B * len(cols) * 4)
+        tro = None
+        if prep is not None and slot_nodes is not None and self._level_no > 0 and ROW_ORDER:
+            # below the root: the tree's node-grouped row order, regrouped once per level (RowOrder)
+            if self._tro is None:
+                self._tro = tops.RowOrder(prep, sample & (node_of_row >= 0))
+            self._tro.regroup(node_of_row, nn, self._level_no)
+            tro = self._tro
         if self.fshard:
-            H = self._histograms_sharded(slot, sub, nslots, prep)
+            H = self._histograms_sharded(slot, sub, nslots, prep, tro, slot_nodes)
         else:
-            H = tops.histogram(self.d.bins, slot, sub, nslots, self.B, prep=prep)
+            H = tops.histogram(self.d.bins, slot, sub, nslots, self.B, prep=prep, tro=tro, slot_nodes=slot_nodes)
             if not self.local:
                 comm.all_reduce(H, "sum")
         if len(cols) != stats.shape[1]:
@@ -216,7 +231,7 @@ class TreeBuilder:
     HIST_BYTES = collections.deque(maxlen=4096)   # full-width fp32 histogram bytes per histogram call (latest)
     LEVEL_STATS = collections.deque(maxlen=4096)  # (depth, nodes, split candidates, host wall s) per grown level
 
-    def _histograms_sharded(self, slot, sub, nslots: int, prep) -> torch.Tensor:
+    def _histograms_sharded(self, slot, sub, nslots: int, prep, tro=None, slot_nodes=None) -> torch.Tensor:
         """Feature-block reduce-scatter overlapped with the histogram build: every rank's
         block of Fb features is cut into G pieces; piece c of ALL ranks' blocks is built as one feature-major
         histogram ([P * piece, slots, B, S]) and its reduce-scatter is issued asynchronously (RCCL comm stream)
@@ -232,7 +247,7 @@ class TreeBuilder:
             if lo >= gpr:
                 break
             fgs = [j * gpr + lo + t if lo + t < gpr else pad for j in range(ws) for t in range(ps)]
-            Hc = tops.histogram_groups(self.d.bins, slot, sub, nslots, self.B, fgs, prep)
+            Hc = tops.histogram_groups(self.d.bins, slot, sub, nslots, self.B, fgs, prep, tro, slot_nodes)
             TreeBuilder.RS_BYTES.append(int(Hc.numel() * 4))            # fp32-equivalent, as HIST_BYTES
             TreeBuilder.RS_CALLS += 1
             pend.append(comm.reduce_scatter_async(Hc, "sum"))
@@ -574,11 +589,61 @@ class TreeBuilder:
         acc = accept.cpu().numpy()
         fb, jb, mb, gb = (fbest.cpu().numpy(), jbest.cpu().numpy(), mbest.cpu().numpy(), gbest.cpu().numpy())
         out = {}
+        if cfg.kind == "gbdt":
+            # binary threshold splits of continuous features: every accepted node of the batch at once
+            vec = acc.astype(bool) & ~mb.astype(bool) & ~np.asarray(self.d.is_cat, dtype=bool)[fb]
+            out.update(self._materialise_gbdt(rows_host, fb, jb, gb, [i for r_, i in enumerate(cand) if vec[r_]],
+                                              np.nonzero(vec)[0]))
+        else:
+            vec = np.zeros(m, dtype=bool)
         for r_, i in enumerate(cand):
-            if acc[r_]:
+            if acc[r_] and not vec[r_]:
                 out[i] = self._materialise(rows_host[r_], int(fb[r_]), int(jb[r_]), bool(mb[r_]), perm_host[r_],
                                            float(gb[r_]))
         return out
+
+    def _materialise_gbdt(self, rows_host, fb, jb, gb, ids, rsel) -> dict:
+        """``_materialise`` of GBDT binary splits on continuous features for many nodes in numpy: left = bins
+        <= j, the missing bin (and unused ones) right; child totals as sequential row sums (the same order as
+        one node at a time)."""
+        if len(ids) == 0:
+            return {}
+        B = self.B
+        h = rows_host[rsel]                                   # [m, B, S]
+        j = jb[rsel].astype(np.int64)
+        b = np.arange(B - 1)
+        inl = b[None, :] <= j[:, None]                        # [m, B-1]
+        hv = h[:, :B - 1]
+        lt = np.cumsum(np.where(inl[..., None], hv, 0.0), axis=1)[:, -1]
+        rt = np.cumsum(np.where(inl[..., None], 0.0, hv), axis=1)[:, -1] + h[:, B - 1]   # + missing (right child)
+        route = np.ones((len(ids), 256), dtype=np.int64)
+        route[:, :B - 1] = np.where(inl, 0, 1)
+        out = {}
+        thr = self.d.thresholds
+        for k, i in enumerate(ids):
+            f, jj = int(fb[rsel[k]]), int(j[k])
+            t = float(thr[f][jj]) if jj < len(thr[f]) else float("inf")
+            out[i] = _Split(f, float(gb[rsel[k]]), route[k], 2, np.stack([lt[k], rt[k]]), None, t)
+        return out
+
+    def _derive_batched(self, derive: dict, hist: dict, dev) -> None:
+        """Sibling subtraction for every derived node of a level in a few launches: the parents' histograms
+        stacked, minus the k-th built sibling of every node in round k (the same fp32 subtraction order as one
+        node at a time, so bitwise the same histograms)."""
+        if not derive:
+            return
+        bigs = list(derive)
+        H = torch.stack([self._prev_hist[derive[b][0]].to(dev) for b in bigs])
+        for k in range(max(len(derive[b][1]) for b in bigs)):
+            rows = [r for r, b in enumerate(bigs) if len(derive[b][1]) > k]
+            sib = torch.stack([hist[derive[bigs[r]][1][k]] for r in rows])
+            if len(rows) == len(bigs):
+                H -= sib
+            else:
+                ri = torch.as_tensor(rows, dtype=torch.long, device=dev)
+                H[ri] = H[ri] - sib
+        for r, b in enumerate(bigs):
+            hist[b] = H[r]
 
     def _level_parked(self, level, node_of_row, sample, stats, build_ids, derive, mbatch, fmask, bagging):
         """A level whose histograms exceed the memory budget, one node batch at a time: the batch's built
@@ -615,15 +680,10 @@ class TreeBuilder:
                 som = torch.full((nl,), -1, dtype=torch.int32)
                 for s_, i in enumerate(bids):
                     som[i] = s_
-                H = self._histograms(node_of_row, sample, som.to(dev), len(bids), stats)
+                H = self._histograms(node_of_row, sample, som.to(dev), len(bids), stats, bids)
                 for s_, i in enumerate(bids):
                     hb[i] = H[s_]
-            for big in (i for i in batch if i in derive):
-                par, others = derive[big]
-                h = self._prev_hist[par].to(dev).clone()
-                for o in others:
-                    h -= hb[o]
-                hb[big] = h
+            self._derive_batched({b: derive[b] for b in batch if b in derive}, hb, dev)
             cand = [i for i in batch if level[i].splittable]
             if cand:
                 got = self._search_batch(level, cand, torch.stack([hb[i] for i in cand]), fmask, bagging)
@@ -652,7 +712,8 @@ class TreeBuilder:
             torch.as_tensor(feature_mask, dtype=torch.bool, device=dev)
         leaves: List[Node] = []
         # root statistics from a 1-slot histogram
-        Hroot = self._histograms(node_of_row, sample, torch.zeros(1, dtype=torch.int32, device=dev), 1, stats)
+        self._tro, self._level_no = None, 0
+        Hroot = self._histograms(node_of_row, sample, torch.zeros(1, dtype=torch.int32, device=dev), 1, stats, [0])
         root_total = self._node_totals(node_of_row, sample, 1, stats)[0]
         root = Node(counter=self._counter(root_total))
         bagging = cfg.kind != "gbdt" and rng is not None
@@ -661,6 +722,7 @@ class TreeBuilder:
         while level:
             nl = len(level)
             t_level = time.perf_counter()
+            self._level_no += 1
             for p in level:
                 p.splittable = self._node_splittable(p)
             if bagging:
@@ -702,15 +764,11 @@ class TreeBuilder:
                         som = torch.full((nl,), -1, dtype=torch.int32)
                         for s, i in enumerate(chunk):
                             som[i] = s
-                        H = self._histograms(node_of_row, sample, som.to(dev), len(chunk), stats)
+                        H = self._histograms(node_of_row, sample, som.to(dev), len(chunk), stats, chunk)
                         for s, i in enumerate(chunk):
                             level_hist[i] = H[s]
                         del H
-                    for big, (par, others) in derive.items():
-                        h = self._prev_hist[par].to(dev).clone()
-                        for o in others:
-                            h -= level_hist[o]
-                        level_hist[big] = h
+                    self._derive_batched(derive, level_hist, dev)
             cand_all = [i for i in range(nl) if level[i].splittable]
             if parked is not None:
                 splits = parked
@@ -768,6 +826,7 @@ class TreeBuilder:
             level = nxt
         self._prev_hist = {}
         self._hist_sub = None
+        self._tro = None
         # leaf probabilities (split nodes keep raw counters)
         for lf in leaves:
             lf.make_leaf_prob()
@@ -776,3 +835,5 @@ class TreeBuilder:
         return root, node_of_row, leaves
 
     _prev_hist: dict = {}
+    _tro = None
+    _level_no = 0

@@ -57,6 +57,7 @@ _c_i64, _c_int, _c_vp, _c_f = ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, cty
 _c_d = ctypes.c_double
 # signatures of further kernels (registered when present in the library)
 _EXTRA_SIGNATURES = {
+    "alink_tree_gather_rows": [_c_vp, _c_vp, _c_vp, _c_i64, _c_vp, _c_vp, _c_vp],
     "alink_tree_hist_fm": [_c_vp, _c_int, _c_vp, _c_vp, _c_vp, _c_int, _c_vp, _c_int, _c_int, _c_int, _c_vp, _c_int,
                            _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_int],
     "alink_tree_hist_f32": [_c_vp, _c_i64, _c_int, _c_vp, _c_vp, _c_int, _c_int, _c_int, _c_vp, _c_int, _c_int,

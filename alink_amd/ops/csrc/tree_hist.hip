@@ -268,7 +268,7 @@ __global__ __launch_bounds__(kFmThreads) void tree_hist_fm(const uint8_t* __rest
   const int64_t f = (int64_t)fg * 32 + (lane & 31);      // fg may be a padding group far past F
   const bool valid = fg >= 0 && f < F;
   const uint8_t* bcol = bins + (valid ? f : 0);
-  const int rb = chunk_rows[c], re = chunk_rows[c + 1];
+  const int rb = chunk_rows[2 * c], re = chunk_rows[2 * c + 1];   // (start, end) pair: chunks may skip rows
   constexpr int nw = kFmThreads / 64;
   const int len = re - rb;
   const int per = ((len + nw - 1) / nw + 1) & ~1;        // even rows per wave
@@ -404,6 +404,20 @@ __global__ __launch_bounds__(256) void tree_hist_fm_reduce(const long long* __re
   }
 }
 
+// Row gather of the tree's node-grouped order (RowOrder.regroup / the per-call sort path): dst_q[i] = src_q[p[i]]
+// (16-byte rows of four int32 statistics, one int4 load + store per thread) and dst_o[i] = src_o[p[i]] when src_o
+// is given.  torch's generic index kernel moved these 16-byte rows at ~0.2 TB/s.
+__global__ __launch_bounds__(256) void tree_gather_rows_kernel(const int4* __restrict__ src_q,
+                                                              const int32_t* __restrict__ src_o,
+                                                              const int64_t* __restrict__ p, int64_t n,
+                                                              int4* __restrict__ dst_q, int32_t* __restrict__ dst_o) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t j = p[i];
+    dst_q[i] = src_q[j];
+    if (src_o != nullptr) dst_o[i] = src_o[j];
+  }
+}
+
 template <int S, bool PACK = false>
 int launch_fm(bool idx, int64_t grid, size_t lds, hipStream_t stream, const uint8_t* bins, int F, const int32_t* ridx,
               const int32_t* sst, const int32_t* chunk_rows, int nchunks, const int32_t* fgl, int nfg, int B,
@@ -503,9 +517,21 @@ int alink_tree_hist_f32(const uint8_t* bins, int64_t n, int F, const int32_t* sl
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
+// dst_q[i] = src_q[p[i]] (int32 [., 4] rows), dst_o[i] = src_o[p[i]] (src_o / dst_o nullable), i < n.
+int alink_tree_gather_rows(const int32_t* src_q, const int32_t* src_o, const int64_t* p, int64_t n, int32_t* dst_q,
+                           int32_t* dst_o, hipStream_t stream) {
+  if (n <= 0) return 0;
+  const int64_t blocks = (n + 255) / 256;
+  hipLaunchKernelGGL(tree_gather_rows_kernel, dim3((unsigned)(blocks < 65536 ? blocks : 65536)), dim3(256), 0, stream,
+                     reinterpret_cast<const int4*>(src_q), src_o, p, n, reinterpret_cast<int4*>(dst_q), dst_o);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
 // Fixed-point histogram (tree_hist_fm): rows grouped by slot.  ridx: [total] row ids sorted by slot (nullptr =
 // identity: rows 0..total-1 all in slot 0); q: [total, 4] int32 quantised statistics in that order;
-// chunk_rows: [nchunks+1] row offsets (each chunk inside one slot); slot_chunk: [nslots+1] chunk ranges per
+// chunk_rows: [nchunks][2] (start, end) row offsets (each chunk inside one slot; rows between chunks are
+// skipped: the tree's node-grouped row order holds the rows of derived / finished nodes too); slot_chunk:
+// [nslots+1] chunk ranges per
 // slot; fgl: [nfl] 32-feature groups to build (nullptr: all, nfl ignored); inv_scale: [S] fp64 (device);
 // slab: [nchunks, nfl, B, S, 32] int64 scratch; H: [nslots, F, B, S] fp32, or with feat_major
 // [nfl * 32, nslots, B, S] (fully written, no zeroing needed).

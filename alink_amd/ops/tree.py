@@ -66,10 +66,10 @@ FM_PACK_MAX_ROWS = 1 << 16    # packed (g, count) histograms: rows per chunk bel
 FM_PACK = os.environ.get("ALINK_TREE_HIST_PACK", "1") != "0"
 
 
-def fm_plan(counts, nfg: int, max_rows: int = None):
-    """Chunking of slot-grouped rows for ``tree_hist_fm``: ``counts[s]`` rows of slot s (consecutive in the
-    sorted order); ``max_rows`` caps the rows of a chunk.  Returns (chunk_rows [nchunks+1], slot_chunk
-    [nslots+1]) as int32 numpy arrays."""
+def fm_plan(counts, nfg: int, max_rows: int = None, starts=None):
+    """Chunking of slot-grouped rows for ``tree_hist_fm``: ``counts[s]`` rows of slot s, starting at row offset
+    ``starts[s]`` (default: consecutive, slot after slot); ``max_rows`` caps the rows of a chunk.  Returns
+    (chunk bounds [nchunks, 2] (start, end) row offsets, slot_chunk [nslots+1]) as int32 numpy arrays."""
     import numpy as np
     counts = np.asarray(counts, dtype=np.int64)
     total = int(counts.sum())
@@ -79,16 +79,64 @@ def fm_plan(counts, nfg: int, max_rows: int = None):
     nch = -(-counts // R)
     slot_chunk = np.zeros(counts.size + 1, dtype=np.int64)
     np.cumsum(nch, out=slot_chunk[1:])
-    starts = np.zeros(counts.size + 1, dtype=np.int64)
-    np.cumsum(counts, out=starts[1:])
-    bounds = [0]
+    if starts is None:
+        starts = np.zeros(counts.size, dtype=np.int64)
+        np.cumsum(counts[:-1], out=starts[1:])
+    starts = np.asarray(starts, dtype=np.int64)
+    pairs = []
     for s_, c in enumerate(counts):
         if c == 0:
             continue
         k = int(nch[s_])
-        edges = starts[s_] + (np.arange(1, k + 1, dtype=np.int64) * c) // k
-        bounds.extend(edges.tolist())
-    return np.asarray(bounds, dtype=np.int32), slot_chunk.astype(np.int32)
+        edges = starts[s_] + (np.arange(0, k + 1, dtype=np.int64) * c) // k
+        pairs.append(np.stack([edges[:-1], edges[1:]], 1))
+    bounds = np.concatenate(pairs) if pairs else np.zeros((0, 2), dtype=np.int64)
+    return bounds.astype(np.int32), slot_chunk.astype(np.int32)
+
+
+def gather_rows(q: torch.Tensor, p: torch.Tensor, order: torch.Tensor = None):
+    """(q[p], order[p]) for the int32 [n, 4] statistics rows (and the int32 row ids) in one HIP gather; p int64."""
+    n = p.numel()
+    dev = q.device
+    qo = torch.empty((n, 4), dtype=torch.int32, device=dev)
+    oo = torch.empty(n, dtype=torch.int32, device=dev) if order is not None else None
+    if n:
+        L = _lib.require()
+        rc = L.alink_tree_gather_rows(q.data_ptr(), None if order is None else order.data_ptr(), p.data_ptr(), n,
+                                      qo.data_ptr(), None if oo is None else oo.data_ptr(), _lib.stream_ptr(dev))
+        if rc != 0:
+            raise RuntimeError(f"alink_tree_gather_rows failed: {rc}")
+    return qo, oo
+
+
+class RowOrder:
+    """The rows of the tree being grown, grouped by their node of the current level (stable: ascending row id
+    inside a node), and their quantised statistics in that order.  Re-grouped once per level from the previous
+    grouping (rows only move inside their parent's segment, so the gathers walk memory almost in order) instead
+    of a full sort + random gather of the statistics for every histogram call; the histogram kernel then reads
+    the build nodes' segments in place (chunks skip the derived / finished nodes' rows)."""
+
+    def __init__(self, prep: "FmStats", active: torch.Tensor):
+        idx = torch.nonzero(active, as_tuple=False).reshape(-1)
+        self.order = idx.to(torch.int32)
+        self.q = gather_rows(prep.q, idx)[0]
+        self.seg = np.asarray([0, int(self.order.numel())], dtype=np.int64)    # node segments
+        self.tag = None
+
+    def regroup(self, node_of_row: torch.Tensor, nn: int, tag) -> None:
+        """Group by ``node_of_row`` (level node ids 0..nn-1; anything else leaves the order)."""
+        if self.tag == tag:
+            return
+        dev = self.order.device
+        key = node_of_row[self.order.long()]
+        kt = torch.uint8 if nn < 255 else (torch.int16 if nn < 32767 else torch.int32)
+        k = torch.where((key >= 0) & (key < nn), key, torch.full_like(key, nn)).to(kt)
+        sk, p = torch.sort(k, stable=True)
+        bnd = torch.searchsorted(sk, torch.arange(nn + 1, device=dev, dtype=kt)).cpu().numpy().astype(np.int64)
+        keep = int(bnd[nn])
+        self.q, self.order = gather_rows(self.q, p[:keep].contiguous(), self.order)
+        self.seg = bnd
+        self.tag = tag
 
 
 def _col_absmax(stats: torch.Tensor, blk: int = 4096) -> torch.Tensor:
@@ -138,7 +186,8 @@ class FmStats:
         self.inv = torch.tensor([1.0 / x for x in scales], dtype=torch.float64, device=dev)
 
 
-def _histogram_fm(L, bins, slot, stats, nslots: int, B: int, prep: "FmStats" = None, fgroups=None) -> torch.Tensor:
+def _histogram_fm(L, bins, slot, stats, nslots: int, B: int, prep: "FmStats" = None, fgroups=None,
+                  tro: "RowOrder" = None, slot_nodes=None) -> torch.Tensor:
     """``tree_hist_fm`` path: rows grouped by slot (stable sort of the slot keys, or the identity when every row
     is in slot 0), statistics quantised to int64 fixed point (``prep``, or here) and gathered into that order,
     chunk plan, kernel + exact fixed-order reduce.  ``fgroups`` (int sequence of 32-feature groups): build only
@@ -148,19 +197,28 @@ def _histogram_fm(L, bins, slot, stats, nslots: int, B: int, prep: "FmStats" = N
     S = stats.shape[1] if stats is not None else prep.S
     if prep is None:
         prep = FmStats(stats)
-    act = (slot >= 0) & (slot < nslots)
-    if nslots == 1 and bool(act.all()):
+    starts = None
+    if tro is not None:
+        # the tree's node-grouped order: slot s = node slot_nodes[s]'s segment, read in place
+        ridx, q = tro.order, tro.q
+        starts = [int(tro.seg[i]) for i in slot_nodes]
+        counts = [int(tro.seg[i + 1] - tro.seg[i]) for i in slot_nodes]
+    elif nslots == 1 and bool(((slot >= 0) & (slot < nslots)).all()):
         ridx = None
         counts = [n]
         q = prep.q
     else:
-        key = torch.where(act, slot, torch.full_like(slot, nslots))
-        counts_t = torch.bincount(key.to(torch.int64), minlength=nslots + 1)[:nslots]
-        _, order = torch.sort(key, stable=True)
-        counts = counts_t.cpu().numpy()
+        act = (slot >= 0) & (slot < nslots)
+        # the narrowest key type: the radix sort makes one pass per key byte (uint8 for < 255 slots)
+        kt = torch.uint8 if nslots < 255 else (torch.int16 if nslots < 32767 else torch.int32)
+        key = torch.where(act, slot, torch.full_like(slot, nslots)).to(kt)
+        skey, order = torch.sort(key, stable=True)
+        # per-slot counts from the sorted keys (slot boundaries by binary search, no separate histogram pass)
+        bnd = torch.searchsorted(skey, torch.arange(nslots + 1, device=dev, dtype=kt))
+        counts = (bnd[1:] - bnd[:-1]).cpu().numpy()
         total = int(counts.sum())
         ridx = order[:total].to(torch.int32).contiguous()
-        q = prep.q[order[:total]]
+        q = gather_rows(prep.q, order[:total].contiguous())[0]
     if fgroups is None:
         nfg, fgl = (F + 31) // 32, None
         hist = torch.empty((nslots, F, B, S), dtype=torch.float32, device=dev)
@@ -172,8 +230,8 @@ def _histogram_fm(L, bins, slot, stats, nslots: int, B: int, prep: "FmStats" = N
         hist = torch.empty((nfg * 32, nslots, B, S), dtype=torch.float32, device=dev)
         if nfg == 0:
             return hist
-    chunk_rows, slot_chunk = fm_plan(counts, nfg, FM_PACK_MAX_ROWS - 1 if prep.pack else None)
-    nchunks = chunk_rows.size - 1
+    chunk_rows, slot_chunk = fm_plan(counts, nfg, FM_PACK_MAX_ROWS - 1 if prep.pack else None, starts)
+    nchunks = chunk_rows.shape[0]
     cr = torch.from_numpy(chunk_rows).to(dev)
     scn = torch.from_numpy(slot_chunk).to(dev)
     slab = torch.empty(max(nchunks, 1) * nfg * B * (2 if prep.pack else S) * 32, dtype=torch.int64, device=dev)
@@ -191,7 +249,7 @@ PAD_GROUP = 1 << 24       # a 32-feature group index past every feature (zero ro
 
 
 def histogram_groups(bins: torch.Tensor, slot: torch.Tensor, stats: torch.Tensor, nslots: int, B: int,
-                     fgroups, prep: "FmStats" = None) -> torch.Tensor:
+                     fgroups, prep: "FmStats" = None, tro: "RowOrder" = None, slot_nodes=None) -> torch.Tensor:
     """Feature-major histogram of the 32-feature groups ``fgroups`` only: ``[len(fgroups) * 32, nslots, B, S]``
     (features >= F, e.g. padding groups of the last rank's block, are zero rows) — the unit a per-rank
     feature-block reduce-scatter sends.  GPU: the fixed-point kernel over the listed groups; CPU: the fp64
@@ -202,7 +260,7 @@ def histogram_groups(bins: torch.Tensor, slot: torch.Tensor, stats: torch.Tensor
         prep = FmStats(stats)
     if fm_eligible(bins, S, B, pack=prep is not None and prep.pack):
         return _histogram_fm(_lib.require(), bins, slot.to(torch.int32).contiguous(), stats, nslots, B, prep,
-                             fgroups=fgroups)
+                             fgroups=fgroups, tro=tro, slot_nodes=slot_nodes)
     feats = torch.tensor([g * 32 + l for g in fgroups for l in range(32)], dtype=torch.long)
     out = torch.zeros((feats.numel(), nslots, B, S), dtype=torch.float32 if bins.is_cuda else torch.float64,
                       device=bins.device)
@@ -223,7 +281,7 @@ def fm_eligible(bins: torch.Tensor, S: int, B: int, variant: int = None, pack: b
 
 
 def histogram(bins: torch.Tensor, slot: torch.Tensor, stats: torch.Tensor, nslots: int, B: int,
-              variant: int = None, prep: FmStats = None) -> torch.Tensor:
+              variant: int = None, prep: FmStats = None, tro: "RowOrder" = None, slot_nodes=None) -> torch.Tensor:
     """[nslots, F, B, S] histogram (fp32 on GPU via HIP, fp64 on CPU).  ``prep``: the statistics already
     quantised for the fixed-point kernel (``FmStats(stats)``, reused across the levels of a tree)."""
     if not bins.is_cuda:
@@ -244,7 +302,7 @@ def histogram(bins: torch.Tensor, slot: torch.Tensor, stats: torch.Tensor, nslot
     if prep is None and S == 3 and FM_PACK and fm_eligible(bins, S, B, variant, pack=True):
         prep = FmStats(stats)               # decides whether the packed (g, count) build applies
     if fm_eligible(bins, S, B, variant, pack=prep is not None and prep.pack) and nslots > 0:
-        return _histogram_fm(L, bins, slot, stats, nslots, B, prep)
+        return _histogram_fm(L, bins, slot, stats, nslots, B, prep, tro=tro, slot_nodes=slot_nodes)
     hist = torch.zeros((nslots, F, B, S), dtype=torch.float32, device=bins.device)
     if n == 0 or nslots == 0:
         return hist

@@ -223,14 +223,53 @@ def test_hip_histogram_and_route_match_torch():
 
 
 def test_fm_plan_chunks_cover_slots_in_order():
-    plan_rows, slot_chunk = tops.fm_plan([0, 5, 100000, 0, 3], nfg=16)
-    assert plan_rows[0] == 0 and plan_rows[-1] == 100008
+    plan, slot_chunk = tops.fm_plan([0, 5, 100000, 0, 3], nfg=16)
+    assert plan[0, 0] == 0 and plan[-1, 1] == 100008
     assert list(np.diff(slot_chunk)) == [0, 1, -(-100000 // max(tops.FM_MIN_ROWS, -(-100008 * 16 // tops.FM_TARGET_BLOCKS))), 0, 1]
-    # every chunk lies inside one slot's row range
+    # every chunk lies inside one slot's row range, chunks tile the slots
     starts = np.cumsum([0, 0, 5, 100000, 0, 3])
     for s_ in range(5):
-        for c in range(slot_chunk[s_], slot_chunk[s_ + 1]):
-            assert starts[s_] <= plan_rows[c] < plan_rows[c + 1] <= starts[s_ + 1]
+        cs = range(slot_chunk[s_], slot_chunk[s_ + 1])
+        for c in cs:
+            assert starts[s_] <= plan[c, 0] < plan[c, 1] <= starts[s_ + 1]
+        if len(cs):
+            assert plan[cs[0], 0] == starts[s_] and plan[cs[-1], 1] == starts[s_ + 1]
+    # slots at explicit offsets (node segments of the tree's row order, with gaps between them)
+    plan2, sc2 = tops.fm_plan([5, 7], nfg=16, starts=[100, 10])
+    assert [tuple(x) for x in plan2] == [(100, 105), (10, 17)] and list(sc2) == [0, 1, 2]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["gbdt", "rf"])
+def test_tree_row_order_histograms_identical_trees(kind, monkeypatch):
+    """Below the root the GPU histograms read the tree's node-grouped row order (RowOrder: regrouped once per
+    level, build-node segments read in place); the trees equal the per-call sort + gather path exactly."""
+    from alink_amd.models.tree import engine as E
+    rng = np.random.default_rng(5)
+    n, F = 60000, 40
+    X = rng.normal(size=(n, F))
+    X[rng.random((n, F)) < 0.05] = np.nan
+    y = ((X[:, 0] > 0) ^ (np.nan_to_num(X[:, 1]) > 0.5)).astype(int)
+    import pandas as pd
+    from alink_amd import useLocalEnv, BatchOperator, GbdtTrainBatchOp, RandomForestTrainBatchOp
+    from alink_amd.common.mlenv import resetEnv
+    cols = [f"f{i}" for i in range(F)]
+    df = pd.DataFrame(X, columns=cols)
+    df["label"] = y
+    schema = ", ".join(f"{c} double" for c in cols) + ", label int"
+    out = []
+    for flag in (1, 0):
+        monkeypatch.setattr(E, "ROW_ORDER", flag)
+        resetEnv()
+        useLocalEnv(1, device="cuda:0")
+        src = BatchOperator.fromDataframe(df, schemaStr=schema)
+        if kind == "gbdt":
+            op = GbdtTrainBatchOp().setFeatureCols(cols).setLabelCol("label").setNumTrees(4).setMaxDepth(7)
+        else:
+            op = RandomForestTrainBatchOp().setFeatureCols(cols).setLabelCol("label").setNumTrees(3) \
+                .setMaxDepth(12)
+        out.append(op.linkFrom(src).collect())
+    assert out[0] == out[1]
 
 
 @pytest.mark.gpu
