@@ -373,6 +373,9 @@ def _split_and(e: Expr) -> List[Expr]:
     return [e]
 
 
+_BLOCKED_JOIN_MAX_PAIRS = 1 << 34      # columnar nested-loop joins up to this many pairs (then the hash / row path)
+
+
 def sql_join(left: MTable, right: MTable, predicate: str, select: str = "*", how: str = "inner") -> MTable:
     ln, rn = left.schema.names, right.schema.names
     qual = {"a": (0, ln), "b": (len(ln), rn)}
@@ -393,6 +396,10 @@ def sql_join(left: MTable, right: MTable, predicate: str, select: str = "*", how
                 eq_r.append(i - len(ln))
     if eq_l:
         res = _join_columnar(left, right, pred, eq_l, eq_r, how, select, schema, qual, resolve)
+        if res is not None:
+            return res
+    if left.num_rows * right.num_rows <= _BLOCKED_JOIN_MAX_PAIRS:
+        res = _join_blocked(left, right, pred, how, select, schema, qual, resolve)
         if res is not None:
             return res
     pf = compile_expr(pred, resolve)
@@ -541,7 +548,7 @@ def _join_columnar(left, right, pred, eq_l, eq_r, how, select, schema, qual, res
                 continue
         rest.append(c)
     if rest and li.numel():
-        cand = MTable(schema, [c.take(li) for c in left.cols] + [c.take(ri) for c in right.cols])
+        cand = _pair_table(left, right, li, ri, schema, _need(rest, resolve), lambda c, i, n: c.take(i))
         keep = None
         for c in rest:
             r = try_evaluate(c, cand, resolve)
@@ -552,6 +559,36 @@ def _join_columnar(left, right, pred, eq_l, eq_r, how, select, schema, qual, res
                 m = (r[0] if r[1] is None else r[0] & ~r[1]).to(dev)
             keep = m if keep is None else keep & m
         li, ri = li[keep], ri[keep]
+    return _finish_join(left, right, li, ri, how, select, schema, qual, dev)
+
+
+def _pair_table(left, right, li, ri, schema, need, take) -> MTable:
+    """The (li, ri) pairs as a table of the joined schema; only the columns in ``need`` are gathered (the
+    others are inert placeholders nothing reads)."""
+    import torch
+    from ....common.table import Column
+    n = int(li.numel())
+    cols = list(left.cols) + list(right.cols)
+    nl_cols = len(left.cols)
+    out = []
+    for i, c in enumerate(cols):
+        if i not in need:
+            out.append(Column(torch.zeros(n, dtype=torch.bool)))
+        elif i < nl_cols:
+            out.append(take(c, li, left.num_rows))
+        else:
+            out.append(take(c, ri, right.num_rows))
+    return MTable(schema, out)
+
+
+def _need(exprs, resolve) -> set:
+    return {resolve(nm) for e in exprs for nm in e.columns()}
+
+
+def _finish_join(left, right, li, ri, how, select, schema, qual, dev) -> MTable:
+    """Matched pairs (li, ri) in the row path's order -> outer padding (index -1 = NULL row) -> select."""
+    import torch
+    nl, nr = left.num_rows, right.num_rows
     if how in ("left", "full"):
         hit = torch.zeros(nl, dtype=torch.bool, device=dev)
         hit[li] = True
@@ -567,9 +604,40 @@ def _join_columnar(left, right, pred, eq_l, eq_r, how, select, schema, qual, res
         ur = torch.nonzero(~hit).reshape(-1)
         li = torch.cat([li, torch.full_like(ur, -1)])
         ri = torch.cat([ri, ur])
-    joined = MTable(schema, [_take_or_null(c, li, nl) for c in left.cols] +
-                    [_take_or_null(c, ri, nr) for c in right.cols])
+    items = _expand_star(parse_select_list(select), schema)
+    need = _need([it.expr for it in items], _resolver(schema.names, qual))
+    joined = _pair_table(left, right, li, ri, schema, need, _take_or_null)
     return sql_select(joined, select, qual)
+
+
+def _join_blocked(left, right, pred, how, select, schema, qual, resolve, pairs: int = 1 << 21) -> Optional[MTable]:
+    """Joins without usable equality keys (theta joins such as ``a.x < b.y``, or key columns that do not
+    factorise): the left x right pairs in blocks of whole left rows, the predicate evaluated columnar (``vexpr``)
+    on each block -- the same O(nl * nr) comparisons as the nested loop, without per-pair Python.  Pair order is
+    the nested loop's.  None when the predicate has no columnar form (the row path then runs it)."""
+    import torch
+    from .vexpr import try_evaluate
+    nl, nr = left.num_rows, right.num_rows
+    dev = next((c.values.device for c in list(left.cols) + list(right.cols) if isinstance(c.values, torch.Tensor)),
+               torch.device("cpu"))
+    lis, ris = [], []
+    if nl and nr:
+        step = max(1, pairs // nr)
+        rr = torch.arange(nr, device=dev)
+        for a in range(0, nl, step):
+            b = min(nl, a + step)
+            li = torch.arange(a, b, device=dev).repeat_interleave(nr)
+            ri = rr.repeat(b - a)
+            cand = _pair_table(left, right, li, ri, schema, _need([pred], resolve), lambda c, i, n: c.take(i))
+            r = try_evaluate(pred, cand, resolve)
+            if r is None or r[0].dtype != torch.bool:
+                return None
+            m = (r[0] if r[1] is None else r[0] & ~r[1]).to(dev)
+            lis.append(li[m])
+            ris.append(ri[m])
+    li = torch.cat(lis) if lis else torch.zeros(0, dtype=torch.int64, device=dev)
+    ri = torch.cat(ris) if ris else torch.zeros(0, dtype=torch.int64, device=dev)
+    return _finish_join(left, right, li, ri, how, select, schema, qual, dev)
 
 
 def _set_codes(a: MTable, b: MTable):

@@ -126,6 +126,7 @@ _EXTRA_SIGNATURES = {
                               _c_vp, _c_vp],
     "alink_als_heavy_solve": [_c_vp, _c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_f, _c_vp, _c_vp, _c_vp, _c_i64, _c_vp,
                               _c_vp, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp, _c_vp, _c_int, _c_vp],
+    "alink_als_woodbury16_mfma": [_c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp],
     "alink_als_woodbury_solve": [_c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_int, _c_vp, _c_vp, _c_int, _c_vp, _c_vp,
                                  _c_vp],
     "alink_als_padded_rank": [_c_int],

@@ -128,6 +128,9 @@ WOODBURY = int(__import__("os").environ.get("ALINK_ALS_WOODBURY", "1"))
 # rank 33..64 light rows: the normal-equation Gram and the block LDL^T solve on the f64 matrix cores
 # (alink_als_mfma_solve); 0 keeps the VALU Gram + Gauss-Jordan kernel (alink_als_fused_solve)
 MFMA_LIGHT = int(__import__("os").environ.get("ALINK_ALS_MFMA_LIGHT", "1"))
+# explicit rows with 9..16 ratings: Gram / solve / Y^T a of the push-through identity on the f64 matrix cores
+# (alink_als_woodbury16_mfma); 0 keeps the LDS-staged kernel
+WOODBURY_MFMA = int(__import__("os").environ.get("ALINK_ALS_WOODBURY_MFMA", "1"))
 WOODBURY_BUCKETS = tuple(int(x) for x in __import__("os").environ.get("ALINK_ALS_WOODBURY_BUCKETS", "8,16,32")
                          .split(","))
 
@@ -168,9 +171,14 @@ def fused_solve(indptr: torch.Tensor, nbr: torch.Tensor, rating: torch.Tensor, Y
         ids = torch.nonzero(sel, as_tuple=False).reshape(-1)
         lo = P
         if ids.numel():
-            rc = L.alink_als_woodbury_solve(indptr.data_ptr(), nbr.data_ptr(), rating.data_ptr(), Yf.data_ptr(),
-                                            ids.numel(), r, regd.data_ptr(), ids.data_ptr(), P, X.data_ptr(),
-                                            status.data_ptr(), st)
+            if P == 16 and WOODBURY_MFMA:
+                rc = L.alink_als_woodbury16_mfma(indptr.data_ptr(), nbr.data_ptr(), rating.data_ptr(), Yf.data_ptr(),
+                                                 ids.numel(), r, regd.data_ptr(), ids.data_ptr(), X.data_ptr(),
+                                                 status.data_ptr(), st)
+            else:
+                rc = L.alink_als_woodbury_solve(indptr.data_ptr(), nbr.data_ptr(), rating.data_ptr(), Yf.data_ptr(),
+                                                ids.numel(), r, regd.data_ptr(), ids.data_ptr(), P, X.data_ptr(),
+                                                status.data_ptr(), st)
             if rc != 0:
                 raise RuntimeError(f"alink_als_woodbury_solve failed: {rc}")
     if heavy.numel() or buckets:

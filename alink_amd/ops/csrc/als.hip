@@ -711,6 +711,86 @@ __global__ __launch_bounds__(64 * WB_WAVES) void als_woodbury_solve(const int64_
   if (lane == 0) status[row] = bad | (deg > P);
 }
 
+// Push-through solve for explicit rows with 9..16 ratings on the f64 matrix cores (the bulk of the user sweep:
+// the LDS-staged version above reads 128 KB of LDS per user for the Gram alone and is LDS-bandwidth bound).
+// One wave per row, no LDS:
+//   lane (g = lane >> 4, t = lane & 15) loads columns 16g .. 16g+15 of neighbour t (four 16-byte loads);
+//   K = Y_u Y_u^T (16 x 16, padded rows identity) = 16 v_mfma_f64_16x16x4 whose A and B operands are the SAME
+//   register (A[m][k] = y_m[k], B[k][n] = y_n[k], with the k order permuted per step: the sum is over all k);
+//   -K^-1 by the 16-step sweep (sweep_neg_inv16, shared with als_mfma_solve), a = K^-1 r by tvec;
+//   x = Y_u^T a as a 16-lane reduce-scatter (4 xor stages, 8 + 4 + 2 + 1 shuffles) that leaves x[lane] on lane.
+// fp64 throughout; results equal the LDS version to fp64 rounding.
+__global__ __launch_bounds__(64 * MF_WAVES, 3) void als_woodbury16_mfma(const int64_t* __restrict__ indptr,
+                                                                      const int32_t* __restrict__ nbr,
+                                                                      const float* __restrict__ rating,
+                                                                      const float* __restrict__ Y, int r,
+                                                                      const double* __restrict__ reg,
+                                                                      const int64_t* __restrict__ rows,
+                                                                      int64_t nrows, float* __restrict__ X,
+                                                                      int32_t* __restrict__ status) {
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int64_t idx = (int64_t)blockIdx.x * MF_WAVES + w;
+  if (idx >= nrows) return;
+  const int64_t row = rows[idx];
+  const int64_t s = indptr[row];
+  const int64_t deg = indptr[row + 1] - s;
+  const int m = __builtin_amdgcn_readfirstlane(deg > 16 ? 0 : (int)deg);
+  const int g = lane >> 4, t = lane & 15;
+  float y[16];
+  if (t < m) {
+    const float* yr = Y + (int64_t)nbr[s + t] * r;
+    if ((r & 3) == 0) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int col = 16 * g + 4 * c;
+        float4 q4 = col < r ? *reinterpret_cast<const float4*>(yr + col) : float4{0.f, 0.f, 0.f, 0.f};
+        y[4 * c] = q4.x;
+        y[4 * c + 1] = q4.y;
+        y[4 * c + 2] = q4.z;
+        y[4 * c + 3] = q4.w;
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < 16; ++c) y[c] = 16 * g + c < r ? yr[16 * g + c] : 0.f;
+    }
+  } else {
+#pragma unroll
+    for (int c = 0; c < 16; ++c) y[c] = 0.f;
+  }
+  d4_t K = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int c = 0; c < 16; ++c) {
+    const double yc = (double)y[c];
+    K = mf64(yc, yc, K);
+  }
+  // + reg on the diagonal (padded rows: identity); C-layout: lane holds K[g + 4q][t]
+  const double lam = reg[row];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    if (g + 4 * q == t) K[q] += t < m ? lam : 1.0;
+  const double v = lane < m ? (double)rating[s + lane] : 0.0;      // r_u, entry t on lane t
+  int bad = 0;
+  const d4_t Kn = sweep_neg_inv16(K, lane, bad);
+  const double a = -tvec(Kn, v, 0, g);                              // a[t] on every lane with column t
+  // x[16 g + c] = sum_t a_t y_t[16 g + c]: reduce-scatter over the 16 lanes of group g
+  double p[16];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) p[c] = a * (double)y[c];
+#pragma unroll
+  for (int hb = 8; hb >= 1; hb >>= 1) {
+    const bool up = (t & hb) != 0;                                  // this lane keeps the upper half
+#pragma unroll
+    for (int c = 0; c < hb; ++c) {
+      const double send = up ? p[c] : p[c + hb];
+      const double recv = __shfl_xor(send, hb);
+      p[c] = (up ? p[c + hb] : p[c]) + recv;
+    }
+  }
+  if (lane < r) X[row * r + lane] = (float)p[0];
+  if (lane == 0) status[row] = bad | (deg > 16);
+}
+
 // heavy rows, pass 1: one wave per (row, chunk of `chunk` neighbours) adds its partial Gram / rhs into fp64
 // global accumulators G [nh][RP][RP], B [nh][RP] (device-scope atomics; a 1e6-neighbour item is 1e6/chunk waves
 // instead of one serial wave)
@@ -989,6 +1069,18 @@ int alink_als_mfma_solve(const int64_t* indptr, const int32_t* nbr, const float*
   else if (implicit) ALS_MF(false, true);
   else ALS_MF(false, false);
 #undef ALS_MF
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+// Explicit rows with <= 16 ratings on the matrix cores (als_woodbury16_mfma); same contract as
+// alink_als_woodbury_solve with P = 16.
+int alink_als_woodbury16_mfma(const int64_t* indptr, const int32_t* nbr, const float* rating, const float* Y,
+                              int64_t nrows, int r, const double* reg, const int64_t* rows, float* X, int32_t* status,
+                              hipStream_t stream) {
+  if (nrows <= 0) return 0;
+  if (r <= 0 || r > 64 || rows == nullptr) return 1;
+  hipLaunchKernelGGL(als_woodbury16_mfma, dim3((unsigned)((nrows + MF_WAVES - 1) / MF_WAVES)), dim3(64 * MF_WAVES), 0,
+                     stream, indptr, nbr, rating, Y, r, reg, rows, nrows, X, status);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 

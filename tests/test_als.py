@@ -328,3 +328,36 @@ def test_hip_als_mfma_light_solve_matches_fp64(r, implicit, monkeypatch):
     ref = torch.cholesky_solve(bb[:, :, None], torch.linalg.cholesky(A))[:, :, 0].float().double().numpy()
     np.testing.assert_allclose(a, ref, rtol=2e-5, atol=2e-6)
     np.testing.assert_allclose(a, b, rtol=2e-5, atol=2e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("r", [10, 24, 62, 64])
+def test_hip_als_woodbury16_mfma_matches_lds_kernel(r, monkeypatch):
+    """Explicit rows with 9..16 ratings on the f64 matrix cores (alink_als_woodbury16_mfma: MFMA Gram, sweep
+    inverse, reduce-scatter Y^T a) == the LDS-staged push-through kernel and fp64 Cholesky; r % 4 != 0 takes the
+    scalar loads; repeated neighbours; a lambda = 0 row."""
+    rng = np.random.default_rng(70 + r)
+    n = 700
+    counts = np.concatenate([[9, 16, 12, 16, 10], rng.integers(9, 17, size=3000)])
+    m = counts.size
+    indptr = torch.zeros(m + 1, dtype=torch.int64)
+    indptr[1:] = torch.as_tensor(np.cumsum(counts))
+    nnz = int(indptr[-1])
+    nbr = rng.integers(0, n, size=nnz)
+    nbr[int(indptr[2]):int(indptr[3])] = nbr[int(indptr[2])]
+    nbr = torch.as_tensor(nbr, dtype=torch.int32)
+    rt = torch.as_tensor(rng.integers(1, 6, size=nnz).astype(np.float32))
+    Y = torch.as_tensor(rng.normal(size=(n, r)) * 0.3, dtype=torch.float32)
+    reg = torch.as_tensor(counts * 0.05, dtype=torch.float64)
+    reg[4] = 0.0
+    args = (indptr.cuda(), nbr.cuda(), rt.cuda(), Y.cuda(), reg.cuda(), False, 0.0, None)
+    monkeypatch.setattr(aops, "WOODBURY", 1)
+    monkeypatch.setattr(aops, "WOODBURY_MFMA", 1)
+    a = aops.fused_solve(*args).cpu().double().numpy()
+    monkeypatch.setattr(aops, "WOODBURY_MFMA", 0)
+    b = aops.fused_solve(*args).cpu().double().numpy()
+    np.testing.assert_allclose(a, b, rtol=2e-5, atol=2e-6)
+    A, bb = aops.normal_equations_torch(indptr, nbr, rt, Y, False, 0.0)
+    A = A + reg[:, None, None] * torch.eye(r, dtype=torch.float64)[None]
+    ref = (torch.linalg.pinv(A) @ bb[:, :, None])[:, :, 0].numpy()
+    np.testing.assert_allclose(a, ref, rtol=2e-4, atol=2e-5)

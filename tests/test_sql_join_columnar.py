@@ -53,10 +53,35 @@ def test_join_columnar_equals_row_path(monkeypatch, how, pred, select):
     A, B = _tables()
     got = E.sql_join(A, B, pred, select, how)
     monkeypatch.setattr(E, "_join_columnar", lambda *a, **k: None)
+    monkeypatch.setattr(E, "_join_blocked", lambda *a, **k: None)
     ref = E.sql_join(A, B, pred, select, how)
     assert got.schema.names == ref.schema.names
     assert _rows(got) == _rows(ref)
     assert len(_rows(ref)) > 0
+
+
+THETA = [
+    ("a.v < b.w", "a.id, a.v, b.w"),
+    ("a.v < b.w AND a.g = 1", "*"),
+    ("a.id > b.key AND b.g = 2 OR a.v > 1.5", "a.id, b.key, a.g, b.g"),
+    ("a.s = b.t OR a.v > b.w", "a.s, b.t, a.v"),
+]
+
+
+@pytest.mark.parametrize("how", ["inner", "left", "right", "full"])
+@pytest.mark.parametrize("pred,select", THETA)
+def test_theta_join_blocked_equals_row_path(monkeypatch, how, pred, select):
+    """Joins without equality keys run the left x right pairs in blocks with the predicate evaluated columnar
+    (``_join_blocked``): the same rows in the same order as the nested loop, NULLs (three-valued logic) and outer
+    padding included; small blocks exercise the block boundaries."""
+    A, B = _tables(n=120, m=90)
+    real = E._join_blocked
+    monkeypatch.setattr(E, "_join_blocked", lambda *a, **k: real(*a, **{**k, "pairs": 1000}))
+    got = E.sql_join(A, B, pred, select, how)
+    monkeypatch.setattr(E, "_join_blocked", lambda *a, **k: None)
+    ref = E.sql_join(A, B, pred, select, how)
+    assert got.schema.names == ref.schema.names
+    assert _rows(got) == _rows(ref)
 
 
 def test_join_columnar_keeps_tensor_columns():

@@ -1,0 +1,10 @@
+#!/bin/bash
+# round-5 GPU call: ALS user sweep (Woodbury 9..16 ratings) on the f64 matrix cores; RF levels after RowOrder
+set -o pipefail
+R=$PWD
+LIMIT=400 tools/gpu.sh tests tests/test_als.py || exit 1
+tools/gpu.sh prof als 400 python $R/tools/als_bench.py --iters 2 || exit 1
+python tools/rocpd_stats.py gpurun_out/prof_als/als_results.db --top 20 > gpurun_out/prof_als_stats.txt 2>&1 || true
+tools/gpu.sh run rflevels 600 python tools/rf_level_bench.py --rows 1000000 --features 100 || exit 1
+find gpurun_out -type f -size +1M ! -name '*.gz' -exec gzip -9 {} \;
+tools/gpu.sh run initprof 300 python tools/kmeans_init_profile.py --reps 2 || exit 1
