@@ -130,7 +130,7 @@ WOODBURY = int(__import__("os").environ.get("ALINK_ALS_WOODBURY", "1"))
 MFMA_LIGHT = int(__import__("os").environ.get("ALINK_ALS_MFMA_LIGHT", "1"))
 # explicit rows with 9..16 ratings: Gram / solve / Y^T a of the push-through identity on the f64 matrix cores
 # (alink_als_woodbury16_mfma); 0 keeps the LDS-staged kernel
-WOODBURY_MFMA = int(__import__("os").environ.get("ALINK_ALS_WOODBURY_MFMA", "1"))
+WOODBURY_MFMA = int(__import__("os").environ.get("ALINK_ALS_WOODBURY_MFMA", "0"))
 WOODBURY_BUCKETS = tuple(int(x) for x in __import__("os").environ.get("ALINK_ALS_WOODBURY_BUCKETS", "8,16,32")
                          .split(","))
 

@@ -3,7 +3,7 @@
 set -o pipefail
 R=$PWD
 LIMIT=400 tools/gpu.sh tests tests/test_als.py || exit 1
-tools/gpu.sh prof als 400 python $R/tools/als_bench.py --iters 2 || exit 1
+ALINK_ALS_WOODBURY_MFMA=1 tools/gpu.sh prof als 400 python $R/tools/als_bench.py --iters 2 || exit 1
 python tools/rocpd_stats.py gpurun_out/prof_als/als_results.db --top 20 > gpurun_out/prof_als_stats.txt 2>&1 || true
 tools/gpu.sh run rflevels 600 python tools/rf_level_bench.py --rows 1000000 --features 100 || exit 1
 find gpurun_out -type f -size +1M ! -name '*.gz' -exec gzip -9 {} \;
