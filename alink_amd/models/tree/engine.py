@@ -589,40 +589,56 @@ class TreeBuilder:
         acc = accept.cpu().numpy()
         fb, jb, mb, gb = (fbest.cpu().numpy(), jbest.cpu().numpy(), mbest.cpu().numpy(), gbest.cpu().numpy())
         out = {}
-        if cfg.kind == "gbdt":
-            # binary threshold splits of continuous features: every accepted node of the batch at once
-            vec = acc.astype(bool) & ~mb.astype(bool) & ~np.asarray(self.d.is_cat, dtype=bool)[fb]
-            out.update(self._materialise_gbdt(rows_host, fb, jb, gb, [i for r_, i in enumerate(cand) if vec[r_]],
-                                              np.nonzero(vec)[0]))
-        else:
-            vec = np.zeros(m, dtype=bool)
+        # binary threshold splits of continuous features: every accepted node of the batch at once
+        vec = acc.astype(bool) & ~mb.astype(bool) & ~np.asarray(self.d.is_cat, dtype=bool)[fb]
+        out.update(self._materialise_cont(rows_host, fb, jb, gb, [i for r_, i in enumerate(cand) if vec[r_]],
+                                          np.nonzero(vec)[0]))
         for r_, i in enumerate(cand):
             if acc[r_] and not vec[r_]:
                 out[i] = self._materialise(rows_host[r_], int(fb[r_]), int(jb[r_]), bool(mb[r_]), perm_host[r_],
                                            float(gb[r_]))
         return out
 
-    def _materialise_gbdt(self, rows_host, fb, jb, gb, ids, rsel) -> dict:
-        """``_materialise`` of GBDT binary splits on continuous features for many nodes in numpy: left = bins
-        <= j, the missing bin (and unused ones) right; child totals as sequential row sums (the same order as
-        one node at a time)."""
+    def _materialise_cont(self, rows_host, fb, jb, gb, ids, rsel) -> dict:
+        """``_materialise`` of binary threshold splits on continuous features for many nodes in numpy: left =
+        bins <= j; the missing bin goes right (GBDT) or to the heavier child; the threshold is the training
+        threshold (GBDT) or the midpoint to the next used bin value (the other criteria); child totals as
+        sequential row sums (the same order as one node at a time)."""
         if len(ids) == 0:
             return {}
-        B = self.B
+        cfg, B = self.cfg, self.B
         h = rows_host[rsel]                                   # [m, B, S]
         j = jb[rsel].astype(np.int64)
         b = np.arange(B - 1)
         inl = b[None, :] <= j[:, None]                        # [m, B-1]
         hv = h[:, :B - 1]
         lt = np.cumsum(np.where(inl[..., None], hv, 0.0), axis=1)[:, -1]
-        rt = np.cumsum(np.where(inl[..., None], 0.0, hv), axis=1)[:, -1] + h[:, B - 1]   # + missing (right child)
+        rt = np.cumsum(np.where(inl[..., None], 0.0, hv), axis=1)[:, -1]
+        miss = h[:, B - 1]
+        if cfg.kind == "gbdt":
+            mchild = np.ones(len(ids), dtype=np.int64)
+        else:
+            mchild = (rt[:, -1] > lt[:, -1]).astype(np.int64)     # np.argmax of the two counts (ties -> 0)
+        lt = lt + np.where(mchild[:, None] == 0, miss, 0.0)
+        rt = rt + np.where(mchild[:, None] == 1, miss, 0.0)
         route = np.ones((len(ids), 256), dtype=np.int64)
         route[:, :B - 1] = np.where(inl, 0, 1)
+        route[:, B - 1] = mchild
+        vals_all = self.d.bin_values if (cfg.kind != "gbdt" and self.d.bin_values) else None
+        if vals_all is not None:
+            used = (hv[:, :, -1] > 0) & ~inl                  # used bins right of the split
+            has = used.any(1)
+            nxt = np.argmax(used, 1)
         out = {}
         thr = self.d.thresholds
         for k, i in enumerate(ids):
             f, jj = int(fb[rsel[k]]), int(j[k])
-            t = float(thr[f][jj]) if jj < len(thr[f]) else float("inf")
+            vals = vals_all[f] if vals_all is not None else None
+            if vals is not None:
+                hi = vals[nxt[k]] if has[k] else vals[min(jj + 1, len(vals) - 1)]
+                t = float((vals[jj] + hi) / 2.0)
+            else:
+                t = float(thr[f][jj]) if jj < len(thr[f]) else float("inf")
             out[i] = _Split(f, float(gb[rsel[k]]), route[k], 2, np.stack([lt[k], rt[k]]), None, t)
         return out
 
