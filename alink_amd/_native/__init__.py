@@ -14,7 +14,7 @@ import numpy as np
 __all__ = ["lib", "parse_csv_lines", "murmur3_utf16", "murmur3_bytes", "murmur3_utf8", "parse_dense_vectors", "ftrl_update_csr",
            "ftrl_partial_margin", "ftrl_shard_update", "parse_binary_detail", "java_double_join",
            "java_double_rows", "java_double_rows_packed", "parse_csv_packed",
-           "parse_dense_vectors_packed", "sample_thresholds", "gbdt_rank_grad"]
+           "parse_dense_vectors_packed", "parse_kv_packed", "sample_thresholds", "gbdt_rank_grad"]
 
 # ALINK_NATIVE_LIB points at another build of the same sources (e.g. the AddressSanitizer build of
 # tools/asan_host.py)
@@ -42,6 +42,8 @@ if os.path.exists(_PATH):
             lib.alink_sample_thresholds.restype = ctypes.c_int64
         if hasattr(lib, "alink_binary_bins"):
             lib.alink_binary_bins.restype = None
+        if hasattr(lib, "alink_kv_parse"):
+            lib.alink_kv_parse.restype = ctypes.c_int64
         if hasattr(lib, "alink_gbdt_rank_grad_host"):
             lib.alink_gbdt_rank_grad_host.restype = ctypes.c_int
     except OSError:
@@ -309,6 +311,28 @@ def parse_dense_vectors_packed(data: np.ndarray, off: np.ndarray, d: int) -> Opt
     if rc != 0:
         return None
     return out
+
+
+def parse_kv_packed(data: np.ndarray, off: np.ndarray, keys: Sequence[str], cd: str, vd: str):
+    """(values float64 [n, k], found bool [n, k], dup bool [n]) of packed KV lines for the schema ``keys``
+    (single-character delimiters), or None: library missing, or a line outside the plain form (the caller parses
+    the batch on its general path)."""
+    if lib is None or getattr(lib, "alink_kv_parse", None) is None or len(cd) != 1 or len(vd) != 1:
+        return None
+    data = np.ascontiguousarray(data, dtype=np.uint8) if data.size else np.zeros(1, np.uint8)
+    off = np.ascontiguousarray(off, dtype=np.int64)
+    n, k = off.size - 1, len(keys)
+    kb, koff = _pack_utf8(list(keys))
+    kb = np.frombuffer(kb, dtype=np.uint8) if kb else np.zeros(1, np.uint8)
+    out = np.empty((n, max(k, 1)), dtype=np.float64)
+    found = np.empty((n, max(k, 1)), dtype=np.uint8)
+    flags = np.empty(max(n, 1), dtype=np.uint8)
+    bad = lib.alink_kv_parse(_ptr(data), _ptr(off), ctypes.c_int64(n), ctypes.c_char(cd.encode()),
+                             ctypes.c_char(vd.encode()), _ptr(kb), _ptr(koff), ctypes.c_int64(k), _ptr(out),
+                             _ptr(found), _ptr(flags))
+    if bad:
+        return None
+    return out[:, :k], found[:, :k].astype(bool), (flags[:n] & 2).astype(bool)
 
 
 def ftrl_update_csr(indptr, indices, values, label, w, n, z, alpha, beta, l1, l2, scale=1.0) -> bool:

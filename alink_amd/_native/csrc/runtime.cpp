@@ -501,3 +501,80 @@ extern "C" int64_t alink_java_double_join(const double* x, int64_t n, char* out)
     }
     return p;
 }
+
+// ---------------------------------------------------------------------------------------------------------------
+// KV strings ("k1:v1,k2:v2,...": KvToColumns / FormatTrans KV -> COLUMNS with DOUBLE columns) parsed into an
+// [n, k] double matrix for the k schema keys.  A line takes the fast path only in its plain form: every field
+// non-empty with exactly one value delimiter, and every value of a schema key a plain decimal token (digits, sign,
+// '.', exponent; strtod consumes it whole).  flags[i]: bit 0 = the line is not plain (the caller re-parses the
+// batch on its general path), bit 1 = a schema key occurs twice (later value kept).  found[i*k + j] = key j seen.
+// ---------------------------------------------------------------------------------------------------------------
+#include <string_view>
+#include <unordered_map>
+
+extern "C" int64_t alink_kv_parse(const char* buf, const int64_t* off, int64_t n, char cd, char vd,
+                                  const char* keys, const int64_t* koff, int64_t k, double* out, uint8_t* found,
+                                  uint8_t* flags) {
+    std::unordered_map<std::string_view, int64_t> pos;
+    pos.reserve((size_t)k * 2 + 1);
+    for (int64_t j = 0; j < k; ++j) pos.emplace(std::string_view(keys + koff[j], (size_t)(koff[j + 1] - koff[j])), j);
+    int64_t nbad = 0;
+#pragma omp parallel for schedule(static) reduction(+ : nbad)
+    for (int64_t i = 0; i < n; ++i) {
+        const char* p = buf + off[i];
+        const char* e = buf + off[i + 1];
+        double* row = out + i * k;
+        uint8_t* fr = found + i * k;
+        for (int64_t j = 0; j < k; ++j) {
+            row[j] = 0.0;
+            fr[j] = 0;
+        }
+        uint8_t fl = 0;
+        char tmp[64];
+        if (p == e) fl |= 1;
+        while (p < e && !(fl & 1)) {
+            const char* q = p;
+            while (q < e && *q != cd) ++q;                 // field [p, q)
+            const char* d = nullptr;
+            int nvd = 0;
+            for (const char* c = p; c < q; ++c)
+                if (*c == vd) {
+                    if (!d) d = c;
+                    ++nvd;
+                }
+            if (q == p || nvd != 1) {
+                fl |= 1;
+                break;
+            }
+            auto it = pos.find(std::string_view(p, (size_t)(d - p)));
+            if (it != pos.end()) {
+                const char* vs = d + 1;
+                const int64_t len = q - vs;
+                bool plain = len > 0 && len < 63;
+                for (const char* c = vs; plain && c < q; ++c)
+                    plain = (*c >= '0' && *c <= '9') || *c == '.' || *c == 'e' || *c == 'E' || *c == '+' || *c == '-';
+                if (!plain) {
+                    fl |= 1;
+                    break;
+                }
+                std::memcpy(tmp, vs, (size_t)len);
+                tmp[len] = 0;
+                char* ep = nullptr;
+                const double v = strtod(tmp, &ep);
+                if (*ep != 0) {
+                    fl |= 1;
+                    break;
+                }
+                const int64_t j = it->second;
+                if (fr[j]) fl |= 2;
+                fr[j] = 1;
+                row[j] = v;
+            }
+            p = q < e ? q + 1 : q;
+            if (q < e && p == e) fl |= 1;                   // trailing delimiter: an empty last field
+        }
+        flags[i] = fl;
+        nbad += (fl & 1) ? 1 : 0;
+    }
+    return nbad;
+}

@@ -667,8 +667,40 @@ def _csv_to_cols(m: "FormatTransMapper", mt):
     return cols
 
 
+def kv_columns_fast(col, names, types, cd: str, vd: str, need_all: bool, allow_dup: bool):
+    """DOUBLE columns of a column of plain KV lines through the C++ parser: (columns with NULL where a key is
+    absent) or None -- another column type, a multi-character delimiter (the row path splits on a regex then),
+    a line outside the plain form, a key given twice (unless ``allow_dup``: the last one wins, as a HashMap put),
+    or a line missing a key when ``need_all``."""
+    import torch
+    from ...common.table import Column
+    N = _native()
+    if N is None or len(cd) != 1 or len(vd) != 1 or any(t != Types.DOUBLE for t in types):
+        return None
+    packed = _packed_strings(col)
+    if packed is None:
+        return None
+    r = N.parse_kv_packed(packed[0], packed[1], names, cd, vd)
+    if r is None:
+        return None
+    vals, found, dup = r
+    if (not allow_dup and dup.any()) or (need_all and not found.all()):
+        return None
+    out = []
+    for j in range(len(names)):
+        miss = ~found[:, j]
+        out.append(Column(torch.from_numpy(vals[:, j].copy()), torch.from_numpy(miss) if miss.any() else None))
+    return out
+
+
+def _kv_to_cols(m: "FormatTransMapper", mt):
+    r, w = m.reader, m.writer
+    return kv_columns_fast(mt.cols[r.col], w.names, w.types, r.cd, r.vd, need_all=False, allow_dup=True)
+
+
 _COLUMNAR = {("COLUMNS", "VECTOR"): _cols_to_vector, ("COLUMNS", "CSV"): _cols_to_csv,
-             ("VECTOR", "COLUMNS"): _vector_to_cols, ("CSV", "COLUMNS"): _csv_to_cols}
+             ("VECTOR", "COLUMNS"): _vector_to_cols, ("CSV", "COLUMNS"): _csv_to_cols,
+             ("KV", "COLUMNS"): _kv_to_cols}
 
 
 class FormatTransMapper(Mapper):
@@ -837,6 +869,15 @@ class KvToColumnsMapper(_StringToColumns):
         self.cd = _p(self.params, "kvColDelimiter") or _p(self.params, "colDelimiter") or ","
         self.vd = _p(self.params, "kvValDelimiter") or _p(self.params, "valDelimiter") or ":"
         self.pos = {n: i for i, n in enumerate(self.names)}
+
+    def _map_columns(self, mt):
+        if mt.num_rows > 0:
+            # lines missing a key fail this parser (ERROR mode raises: the row path owns that), else NULL cells
+            cols = kv_columns_fast(mt.cols[self.idx], self.names, self.types, self.cd, self.vd, need_all=self.err,
+                                   allow_dup=False)
+            if cols is not None:
+                return cols
+        return super()._map_columns(mt)
 
     def parse(self, text):
         out = [None] * len(self.names)

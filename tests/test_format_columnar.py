@@ -145,3 +145,42 @@ def test_csv_to_columns_fast_equals_rows(how):
             assert F.csv_columns_fast(lines[:5] + [extra], m2.types, ",", '"') is None
             _both(m2, mt2)
             _both(m, mt2)
+
+
+def _kv_lines(n, rng, keys, holes=False, dup=False):
+    out = []
+    for i in range(n):
+        ks = list(keys) + ["extra"]
+        rng.shuffle(ks)
+        if holes and i % 5 == 0:
+            ks = ks[1:]
+        if dup and i == n // 2:
+            ks.append(ks[0])
+        out.append(",".join(f"{k}:{repr(float(rng.normal() * 10.0 ** int(rng.integers(-5, 5))))}" for k in ks))
+    return out
+
+
+@pytest.mark.parametrize("holes", [False, True])
+@pytest.mark.parametrize("how", ["ERROR", "SKIP"])
+def test_kv_to_columns_fast_equals_rows(holes, how):
+    rng = np.random.default_rng(13)
+    keys = ["k0", "k1", "k2", "k3"]
+    schema_str = ", ".join(f"{k} double" for k in keys)
+    lines = _kv_lines(300, rng, keys, holes=holes)
+    mt = MTable(TableSchema(["kv"], [Types.STRING]), [Column(lines)])
+    m = F.FormatTransMapper(mt.schema, Params().set("fromFormat", "KV").set("toFormat", "COLUMNS")
+                            .set("kvCol", "kv").set("schemaStr", schema_str).set("handleInvalid", how))
+    assert m._fast(m, mt) is not None                      # missing keys are NULL cells for FormatTrans
+    _both(m, mt)
+    m2 = F.KvToColumnsMapper(mt.schema, Params().set("selectedCol", "kv").set("schemaStr", schema_str)
+                             .set("handleInvalid", how))
+    fast = F.kv_columns_fast(mt.cols[0], m2.names, m2.types, ",", ":", need_all=m2.err, allow_dup=False)
+    assert (fast is None) == (holes and how == "ERROR")
+    if not (holes and how == "ERROR"):
+        _both(m2, mt)
+    # outside the plain form -> row path (whitespace, empty field, duplicate key for KvToColumns)
+    for bad in ("k0: 1.0,k1:2,k2:3,k3:4", "k0:1,,k1:2,k2:3,k3:4", "k0:1,k0:2,k1:2,k2:3,k3:4"):
+        mt2 = MTable(mt.schema, [Column(lines[:3] + [bad])])
+        assert F.kv_columns_fast(mt2.cols[0], m2.names, m2.types, ",", ":", need_all=False, allow_dup=False) is None
+        if how == "SKIP":
+            _both(m2, mt2)
