@@ -14,7 +14,7 @@ import numpy as np
 __all__ = ["lib", "parse_csv_lines", "murmur3_utf16", "murmur3_bytes", "murmur3_utf8", "parse_dense_vectors", "ftrl_update_csr",
            "ftrl_partial_margin", "ftrl_shard_update", "parse_binary_detail", "java_double_join",
            "java_double_rows", "java_double_rows_packed", "parse_csv_packed",
-           "parse_dense_vectors_packed", "parse_kv_packed", "sample_thresholds", "gbdt_rank_grad"]
+           "parse_dense_vectors_packed", "parse_kv_packed", "parse_json_flat_packed", "sample_thresholds", "gbdt_rank_grad"]
 
 # ALINK_NATIVE_LIB points at another build of the same sources (e.g. the AddressSanitizer build of
 # tools/asan_host.py)
@@ -44,6 +44,8 @@ if os.path.exists(_PATH):
             lib.alink_binary_bins.restype = None
         if hasattr(lib, "alink_kv_parse"):
             lib.alink_kv_parse.restype = ctypes.c_int64
+        if hasattr(lib, "alink_json_flat_parse"):
+            lib.alink_json_flat_parse.restype = ctypes.c_int64
         if hasattr(lib, "alink_gbdt_rank_grad_host"):
             lib.alink_gbdt_rank_grad_host.restype = ctypes.c_int
     except OSError:
@@ -333,6 +335,26 @@ def parse_kv_packed(data: np.ndarray, off: np.ndarray, keys: Sequence[str], cd: 
     if bad:
         return None
     return out[:, :k], found[:, :k].astype(bool), (flags[:n] & 2).astype(bool)
+
+
+def parse_json_flat_packed(data: np.ndarray, off: np.ndarray, keys: Sequence[str]):
+    """(values float64 [n, k], found bool [n, k]) of packed flat JSON objects with numeric members for the schema
+    ``keys``, or None (library missing, or a line outside that form: the caller parses with the JSON reader)."""
+    if lib is None or getattr(lib, "alink_json_flat_parse", None) is None:
+        return None
+    data = np.ascontiguousarray(data, dtype=np.uint8) if data.size else np.zeros(1, np.uint8)
+    off = np.ascontiguousarray(off, dtype=np.int64)
+    n, k = off.size - 1, len(keys)
+    kb, koff = _pack_utf8(list(keys))
+    kb = np.frombuffer(kb, dtype=np.uint8) if kb else np.zeros(1, np.uint8)
+    out = np.empty((n, max(k, 1)), dtype=np.float64)
+    found = np.empty((n, max(k, 1)), dtype=np.uint8)
+    flags = np.empty(max(n, 1), dtype=np.uint8)
+    bad = lib.alink_json_flat_parse(_ptr(data), _ptr(off), ctypes.c_int64(n), _ptr(kb), _ptr(koff),
+                                    ctypes.c_int64(k), _ptr(out), _ptr(found), _ptr(flags))
+    if bad:
+        return None
+    return out[:, :k], found[:, :k].astype(bool)
 
 
 def ftrl_update_csr(indptr, indices, values, label, w, n, z, alpha, beta, l1, l2, scale=1.0) -> bool:

@@ -578,3 +578,91 @@ extern "C" int64_t alink_kv_parse(const char* buf, const int64_t* off, int64_t n
     }
     return nbad;
 }
+
+// Flat JSON objects ({"k": number, ...}: JsonToColumns / FormatTrans JSON -> COLUMNS with DOUBLE columns) into an
+// [n, k] double matrix for the k schema keys.  Plain form only: one object per line, keys plain strings (no
+// escapes), every member value a JSON number (members whose key is not in the schema may also be strings without
+// escapes); anything else sets flags bit 0 (the caller parses the batch with the general JSON reader).  Integer
+// tokens give +0.0 for -0 (the reader turns them into integers first).  A key given twice keeps the later value.
+static inline const char* json_ws(const char* p, const char* e) {
+    while (p < e && (*p == ' ' || *p == '\t' || *p == '\n' || *p == '\r')) ++p;
+    return p;
+}
+
+extern "C" int64_t alink_json_flat_parse(const char* buf, const int64_t* off, int64_t n, const char* keys,
+                                         const int64_t* koff, int64_t k, double* out, uint8_t* found,
+                                         uint8_t* flags) {
+    std::unordered_map<std::string_view, int64_t> pos;
+    pos.reserve((size_t)k * 2 + 1);
+    for (int64_t j = 0; j < k; ++j) pos.emplace(std::string_view(keys + koff[j], (size_t)(koff[j + 1] - koff[j])), j);
+    int64_t nbad = 0;
+#pragma omp parallel for schedule(static) reduction(+ : nbad)
+    for (int64_t i = 0; i < n; ++i) {
+        const char* p = buf + off[i];
+        const char* e = buf + off[i + 1];
+        double* row = out + i * k;
+        uint8_t* fr = found + i * k;
+        for (int64_t j = 0; j < k; ++j) {
+            row[j] = 0.0;
+            fr[j] = 0;
+        }
+        bool bad = false;
+        char tmp[80];
+        p = json_ws(p, e);
+        if (p >= e || *p != '{') bad = true;
+        else ++p;
+        p = json_ws(p, e);
+        if (!bad && p < e && *p == '}') {
+            ++p;
+        } else {
+            while (!bad) {
+                p = json_ws(p, e);
+                if (p >= e || *p != '"') { bad = true; break; }
+                const char* ks = ++p;
+                while (p < e && *p != '"' && *p != '\\') ++p;
+                if (p >= e || *p != '"') { bad = true; break; }
+                const std::string_view key(ks, (size_t)(p - ks));
+                ++p;
+                p = json_ws(p, e);
+                if (p >= e || *p != ':') { bad = true; break; }
+                p = json_ws(p + 1, e);
+                auto it = pos.find(key);
+                if (p < e && *p == '"') {                   // a string value: only for keys outside the schema
+                    if (it != pos.end()) { bad = true; break; }
+                    ++p;
+                    while (p < e && *p != '"' && *p != '\\') ++p;
+                    if (p >= e || *p != '"') { bad = true; break; }
+                    ++p;
+                } else {
+                    const char* vs = p;
+                    bool intlike = true;
+                    while (p < e && ((*p >= '0' && *p <= '9') || *p == '-' || *p == '+' || *p == '.' || *p == 'e' ||
+                                     *p == 'E')) {
+                        if (*p == '.' || *p == 'e' || *p == 'E') intlike = false;
+                        ++p;
+                    }
+                    const int64_t len = p - vs;
+                    if (len <= 0 || len >= 79) { bad = true; break; }
+                    std::memcpy(tmp, vs, (size_t)len);
+                    tmp[len] = 0;
+                    char* ep = nullptr;
+                    double v = strtod(tmp, &ep);
+                    if (*ep != 0 || std::isinf(v) || std::isnan(v)) { bad = true; break; }
+                    if (intlike && v == 0.0) v = 0.0;           // "-0" is the integer 0
+                    if (it != pos.end()) {
+                        row[it->second] = v;
+                        fr[it->second] = 1;
+                    }
+                }
+                p = json_ws(p, e);
+                if (p < e && *p == ',') { ++p; continue; }
+                if (p < e && *p == '}') { ++p; break; }
+                bad = true;
+            }
+        }
+        if (!bad && json_ws(p, e) != e) bad = true;
+        flags[i] = bad ? 1 : 0;
+        nbad += bad ? 1 : 0;
+    }
+    return nbad;
+}

@@ -693,6 +693,38 @@ def kv_columns_fast(col, names, types, cd: str, vd: str, need_all: bool, allow_d
     return out
 
 
+_PLAIN_KEY = re.compile(r"[A-Za-z_][A-Za-z0-9_]*")
+
+
+def json_columns_fast(col, names, types, need_all: bool):
+    """DOUBLE columns of a column of flat JSON objects with numeric members through the C++ reader (NULL where a
+    key is absent), or None: another column type, a key that is a JSON path rather than a plain name, a line
+    outside that form, or a line missing a key when ``need_all``."""
+    import torch
+    from ...common.table import Column
+    N = _native()
+    if N is None or any(t != Types.DOUBLE for t in types) or not all(_PLAIN_KEY.fullmatch(n) for n in names):
+        return None
+    packed = _packed_strings(col)
+    if packed is None:
+        return None
+    r = N.parse_json_flat_packed(packed[0], packed[1], names)
+    if r is None:
+        return None
+    vals, found = r
+    if need_all and not found.all():
+        return None
+    out = []
+    for j in range(len(names)):
+        miss = ~found[:, j]
+        out.append(Column(torch.from_numpy(vals[:, j].copy()), torch.from_numpy(miss) if miss.any() else None))
+    return out
+
+
+def _json_to_cols(m: "FormatTransMapper", mt):
+    return json_columns_fast(mt.cols[m.reader.col], m.writer.names, m.writer.types, need_all=False)
+
+
 def _kv_to_cols(m: "FormatTransMapper", mt):
     r, w = m.reader, m.writer
     return kv_columns_fast(mt.cols[r.col], w.names, w.types, r.cd, r.vd, need_all=False, allow_dup=True)
@@ -700,7 +732,7 @@ def _kv_to_cols(m: "FormatTransMapper", mt):
 
 _COLUMNAR = {("COLUMNS", "VECTOR"): _cols_to_vector, ("COLUMNS", "CSV"): _cols_to_csv,
              ("VECTOR", "COLUMNS"): _vector_to_cols, ("CSV", "COLUMNS"): _csv_to_cols,
-             ("KV", "COLUMNS"): _kv_to_cols}
+             ("KV", "COLUMNS"): _kv_to_cols, ("JSON", "COLUMNS"): _json_to_cols}
 
 
 class FormatTransMapper(Mapper):
@@ -838,6 +870,13 @@ class CsvToColumnsMapper(_StringToColumns):
 
 class JsonToColumnsMapper(_StringToColumns):
     COL_PARAMS = ("jsonCol",)
+
+    def _map_columns(self, mt):
+        if mt.num_rows > 0:
+            cols = json_columns_fast(mt.cols[self.idx], self.names, self.types, need_all=self.err)
+            if cols is not None:
+                return cols
+        return super()._map_columns(mt)
 
     def parse(self, text):
         try:

@@ -184,3 +184,49 @@ def test_kv_to_columns_fast_equals_rows(holes, how):
         assert F.kv_columns_fast(mt2.cols[0], m2.names, m2.types, ",", ":", need_all=False, allow_dup=False) is None
         if how == "SKIP":
             _both(m2, mt2)
+
+
+def _json_lines(n, rng, keys, holes=False):
+    import json as _json
+    out = []
+    for i in range(n):
+        d = {}
+        for k in keys + ["note"]:
+            if holes and i % 4 == 0 and k == keys[0]:
+                continue
+            if k == "note":
+                d[k] = "x"
+            elif i % 7 == 0:
+                d[k] = int(rng.integers(-5, 5))                # integers, -0 written by hand below
+            else:
+                d[k] = float(rng.normal() * 10.0 ** int(rng.integers(-8, 8)))
+        s = _json.dumps(d, separators=(",", ":") if i % 2 else (", ", ": "))
+        out.append(s.replace('": 0,', '": -0,') if i % 9 == 0 else s)
+    return out
+
+
+@pytest.mark.parametrize("holes", [False, True])
+@pytest.mark.parametrize("how", ["ERROR", "SKIP"])
+def test_json_to_columns_fast_equals_rows(holes, how):
+    rng = np.random.default_rng(17)
+    keys = ["a", "b_2", "c"]
+    schema_str = ", ".join(f"{k} double" for k in keys)
+    lines = _json_lines(300, rng, keys, holes=holes)
+    mt = MTable(TableSchema(["js"], [Types.STRING]), [Column(lines)])
+    m = F.FormatTransMapper(mt.schema, Params().set("fromFormat", "JSON").set("toFormat", "COLUMNS")
+                            .set("jsonCol", "js").set("schemaStr", schema_str).set("handleInvalid", how))
+    assert m._fast(m, mt) is not None
+    _both(m, mt)
+    m2 = F.JsonToColumnsMapper(mt.schema, Params().set("selectedCol", "js").set("schemaStr", schema_str)
+                               .set("handleInvalid", how))
+    fast = F.json_columns_fast(mt.cols[0], m2.names, m2.types, need_all=m2.err)
+    assert (fast is None) == (holes and how == "ERROR")
+    if not (holes and how == "ERROR"):
+        _both(m2, mt)
+    # outside the plain form -> the JSON reader (null / string / nested values, lenient syntax, escapes)
+    for bad in ('{"a":null,"b_2":1,"c":2}', '{"a":"1.5","b_2":1,"c":2}', "{a:1,b_2:2,c:3}",
+                '{"a":[1],"b_2":1,"c":2}', '{"a\\u0041":1,"a":1,"b_2":1,"c":2}'):
+        mt2 = MTable(mt.schema, [Column(lines[:3] + [bad])])
+        assert F.json_columns_fast(mt2.cols[0], m2.names, m2.types, need_all=False) is None
+        if how == "SKIP":
+            _both(m2, mt2)
