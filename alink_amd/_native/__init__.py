@@ -14,7 +14,7 @@ import numpy as np
 __all__ = ["lib", "parse_csv_lines", "murmur3_utf16", "murmur3_bytes", "murmur3_utf8", "parse_dense_vectors", "ftrl_update_csr",
            "ftrl_partial_margin", "ftrl_shard_update", "parse_binary_detail", "java_double_join",
            "java_double_rows", "java_double_rows_packed", "parse_csv_packed",
-           "parse_dense_vectors_packed", "parse_kv_packed", "parse_json_flat_packed", "sample_thresholds", "gbdt_rank_grad"]
+           "parse_dense_vectors_packed", "parse_kv_packed", "parse_json_flat_packed", "java_double_rows_fmt", "sample_thresholds", "gbdt_rank_grad"]
 
 # ALINK_NATIVE_LIB points at another build of the same sources (e.g. the AddressSanitizer build of
 # tools/asan_host.py)
@@ -38,6 +38,8 @@ if os.path.exists(_PATH):
             lib.alink_java_double_join.restype = ctypes.c_int64
         if hasattr(lib, "alink_java_double_rows"):
             lib.alink_java_double_rows.restype = ctypes.c_int64
+        if hasattr(lib, "alink_java_double_rows_fmt"):
+            lib.alink_java_double_rows_fmt.restype = ctypes.c_int64
         if hasattr(lib, "alink_sample_thresholds"):
             lib.alink_sample_thresholds.restype = ctypes.c_int64
         if hasattr(lib, "alink_binary_bins"):
@@ -211,6 +213,28 @@ def java_double_rows_packed(x, sep: str = " "):
     off = np.zeros(n + 1, dtype=np.int64)
     total = lib.alink_java_double_rows(_ptr(a), ctypes.c_int64(n), ctypes.c_int64(k), ctypes.c_char(sep.encode()),
                                        _ptr(buf), _ptr(off[1:]))
+    return buf[:total], off
+
+
+def java_double_rows_fmt(x, pre: Sequence[str], post: Sequence[str], sep: str, ropen: str = "", rclose: str = ""):
+    """(uint8 bytes, int64 offsets [n+1]) of rows ``ropen + sep.join(pre[j] + Double.toString(x[i, j]) + post[j])
+    + rclose`` (ASCII decorations), formatted in C++; None without the library."""
+    if lib is None or getattr(lib, "alink_java_double_rows_fmt", None) is None:
+        return None
+    a = np.ascontiguousarray(np.asarray(x, dtype=np.float64))
+    n, k = a.shape
+    pb, poff = _pack_utf8(list(pre))
+    qb, qoff = _pack_utf8(list(post))
+    pa = np.frombuffer(pb, dtype=np.uint8) if pb else np.zeros(1, np.uint8)
+    qa = np.frombuffer(qb, dtype=np.uint8) if qb else np.zeros(1, np.uint8)
+    ro, rc = ropen.encode("ascii"), rclose.encode("ascii")
+    per_row = len(ro) + len(rc) + max(k - 1, 0) + int(poff[-1]) + int(qoff[-1]) + 26 * k
+    buf = np.empty(per_row * max(n, 1) + 16, dtype=np.uint8)
+    off = np.zeros(n + 1, dtype=np.int64)
+    total = lib.alink_java_double_rows_fmt(_ptr(a), ctypes.c_int64(n), ctypes.c_int64(k), _ptr(pa), _ptr(poff),
+                                           _ptr(qa), _ptr(qoff), ctypes.c_char(sep.encode()), ctypes.c_char_p(ro),
+                                           ctypes.c_int64(len(ro)), ctypes.c_char_p(rc), ctypes.c_int64(len(rc)),
+                                           _ptr(buf), _ptr(off[1:]))
     return buf[:total], off
 
 

@@ -666,3 +666,49 @@ extern "C" int64_t alink_json_flat_parse(const char* buf, const int64_t* off, in
     }
     return nbad;
 }
+
+// Rows of k doubles with per-column decoration: row i = ropen + [pre_0 v_0 post_0] sep [pre_1 v_1 post_1] ... + rclose,
+// v = Double.toString (COLUMNS -> KV "k:v,..." / JSON {"k":"v",...} writers).  out capacity: the caller's bound;
+// row_end[i] = end offset of row i.  OpenMP row blocks formatted into per-block slices, then compacted.
+extern "C" int64_t alink_java_double_rows_fmt(const double* x, int64_t n, int64_t k, const char* pre,
+                                              const int64_t* pre_off, const char* post, const int64_t* post_off,
+                                              char sep, const char* ropen, int64_t lo, const char* rclose, int64_t lc,
+                                              char* out, int64_t* row_end) {
+    int64_t deco = lo + lc + (k > 0 ? k - 1 : 0) + pre_off[k] + post_off[k];
+    const int64_t per_row = deco + 26 * k;
+    const int64_t rows_per = std::max<int64_t>(1, 8192 / std::max<int64_t>(k, 1));
+    const int64_t nb = (n + rows_per - 1) / rows_per;
+    std::vector<int64_t> blen(nb);
+#pragma omp parallel for schedule(dynamic, 4)
+    for (int64_t b = 0; b < nb; ++b) {
+        const int64_t r0 = b * rows_per, r1 = std::min(n, r0 + rows_per);
+        char* base = out + r0 * per_row;
+        int64_t p = 0;
+        for (int64_t i = r0; i < r1; ++i) {
+            std::memcpy(base + p, ropen, (size_t)lo);
+            p += lo;
+            for (int64_t j = 0; j < k; ++j) {
+                if (j) base[p++] = sep;
+                const int64_t a = pre_off[j + 1] - pre_off[j];
+                std::memcpy(base + p, pre + pre_off[j], (size_t)a);
+                p += a;
+                p += java_double_to(x[i * k + j], base + p);
+                const int64_t c = post_off[j + 1] - post_off[j];
+                std::memcpy(base + p, post + post_off[j], (size_t)c);
+                p += c;
+            }
+            std::memcpy(base + p, rclose, (size_t)lc);
+            p += lc;
+            row_end[i] = p;
+        }
+        blen[b] = p;
+    }
+    int64_t p = 0;
+    for (int64_t b = 0; b < nb; ++b) {
+        const int64_t r0 = b * rows_per, r1 = std::min(n, r0 + rows_per);
+        if (p != r0 * per_row) std::memmove(out + p, out + r0 * per_row, (size_t)blen[b]);
+        for (int64_t i = r0; i < r1; ++i) row_end[i] += p;
+        p += blen[b];
+    }
+    return p;
+}

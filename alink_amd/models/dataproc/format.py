@@ -725,6 +725,40 @@ def _json_to_cols(m: "FormatTransMapper", mt):
     return json_columns_fast(mt.cols[m.reader.col], m.writer.names, m.writer.types, need_all=False)
 
 
+def _cols_to_kv(m: "FormatTransMapper", mt):
+    """COLUMNS -> KV over DOUBLE columns without nulls: the HashMap key order of the row path (the same for every
+    row when no value is null), one C++ formatting pass into a StringBlock."""
+    w, names = m.writer, list(m.reader.names)
+    if (len(w.cd) != 1 or w.cd in _SAFE_SEP or any(w.cd in k or w.vd in k for k in names)
+            or len(set(names)) != len(names)):
+        return None
+    order = [k for k, _ in _hash_items({k: "" for k in names})]
+    X = _double_matrix(mt, order)
+    N = _native()
+    if X is None or N is None or not all(k.isascii() for k in order) or not w.vd.isascii():
+        return None
+    from ...common.table import Column
+    r = N.java_double_rows_fmt(X, [k + w.vd for k in order], [""] * len(order), w.cd)
+    return None if r is None else [Column(_string_block(r[0], r[1]))]
+
+
+def _cols_to_json(m: "FormatTransMapper", mt):
+    """COLUMNS -> JSON over DOUBLE columns without nulls with plain key names: {"k":"v",...} (the map holds the
+    values' strings) in the row path's HashMap order."""
+    import json as _json
+    names = list(m.reader.names)
+    if not all(_PLAIN_KEY.fullmatch(k) for k in names) or len(set(names)) != len(names):
+        return None
+    order = list(_json.loads(gson_dumps({k: "0" for k in names}, java_map_order=True)).keys())
+    X = _double_matrix(mt, order)
+    N = _native()
+    if X is None or N is None:
+        return None
+    from ...common.table import Column
+    r = N.java_double_rows_fmt(X, ['"' + k + '":"' for k in order], ['"'] * len(order), ",", "{", "}")
+    return None if r is None else [Column(_string_block(r[0], r[1]))]
+
+
 def _kv_to_cols(m: "FormatTransMapper", mt):
     r, w = m.reader, m.writer
     return kv_columns_fast(mt.cols[r.col], w.names, w.types, r.cd, r.vd, need_all=False, allow_dup=True)
@@ -732,7 +766,8 @@ def _kv_to_cols(m: "FormatTransMapper", mt):
 
 _COLUMNAR = {("COLUMNS", "VECTOR"): _cols_to_vector, ("COLUMNS", "CSV"): _cols_to_csv,
              ("VECTOR", "COLUMNS"): _vector_to_cols, ("CSV", "COLUMNS"): _csv_to_cols,
-             ("KV", "COLUMNS"): _kv_to_cols, ("JSON", "COLUMNS"): _json_to_cols}
+             ("KV", "COLUMNS"): _kv_to_cols, ("JSON", "COLUMNS"): _json_to_cols,
+             ("COLUMNS", "KV"): _cols_to_kv, ("COLUMNS", "JSON"): _cols_to_json}
 
 
 class FormatTransMapper(Mapper):

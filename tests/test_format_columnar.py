@@ -230,3 +230,17 @@ def test_json_to_columns_fast_equals_rows(holes, how):
         assert F.json_columns_fast(mt2.cols[0], m2.names, m2.types, need_all=False) is None
         if how == "SKIP":
             _both(m2, mt2)
+
+
+@pytest.mark.parametrize("to", ["KV", "JSON"])
+def test_columns_to_kv_json_fast_equals_rows(to):
+    rng = np.random.default_rng(23)
+    mt, names = _num_table(6, 300, rng)
+    p = Params().set("fromFormat", "COLUMNS").set("toFormat", to).set("selectedCols", names) \
+        .set("kvCol", "out").set("jsonCol", "out")
+    m = F.FormatTransMapper(mt.schema, p)
+    assert m._fast(m, mt) is not None
+    _both(m, mt)
+    mtn, _ = _num_table(6, 100, rng, nulls=True)            # nulls drop keys row by row: row path
+    assert m._fast(m, mtn) is None
+    _both(m, mtn)
