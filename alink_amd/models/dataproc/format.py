@@ -594,34 +594,48 @@ def csv_columns_fast(col, types, delim: str, quote: Optional[str]):
     return out
 
 
-def _cols_to_vector(m: "FormatTransMapper", mt):
-    w, names = m.writer, m.reader.names
+def _w_vector(m: "FormatTransMapper", get, names):
+    w = m.writer
     n, prefix = len(w.from_names), ""
     if w.size > n:
         prefix = f"${w.size}$"
     elif 0 < w.size < n:
         n = w.size
-    X = _double_matrix(mt, w.from_names[:n])
+    if list(names) != list(w.from_names):
+        return None
+    X = get(w.from_names[:n])
     N = _native()
-    if X is None or N is None or list(names) != list(w.from_names):
+    if X is None or N is None:
         return None
     from ...common.table import Column
     r = N.java_double_rows_packed(X, " ")
     return None if r is None else [Column(_string_block(r[0], r[1], prefix))]
 
 
-def _cols_to_csv(m: "FormatTransMapper", mt):
+def _w_csv(m: "FormatTransMapper", get, names):
     w = m.writer
     if (len(w.delim) != 1 or w.delim in _SAFE_SEP or (w.quote and (len(w.quote) != 1 or w.quote in _SAFE_SEP))
-            or not set(w.cols) <= set(m.reader.names)):
+            or not set(w.cols) <= set(names)):
         return None
-    X = _double_matrix(mt, w.cols)
+    X = get(w.cols)
     N = _native()
     if X is None or N is None:
         return None
     from ...common.table import Column
     r = N.java_double_rows_packed(X, w.delim)
     return None if r is None else [Column(_string_block(r[0], r[1]))]
+
+
+def _cols_getter(mt):
+    return lambda names: _double_matrix(mt, names)
+
+
+def _cols_to_vector(m: "FormatTransMapper", mt):
+    return _w_vector(m, _cols_getter(mt), m.reader.names)
+
+
+def _cols_to_csv(m: "FormatTransMapper", mt):
+    return _w_csv(m, _cols_getter(mt), m.reader.names)
 
 
 def _vector_to_cols(m: "FormatTransMapper", mt):
@@ -725,38 +739,67 @@ def _json_to_cols(m: "FormatTransMapper", mt):
     return json_columns_fast(mt.cols[m.reader.col], m.writer.names, m.writer.types, need_all=False)
 
 
-def _cols_to_kv(m: "FormatTransMapper", mt):
-    """COLUMNS -> KV over DOUBLE columns without nulls: the HashMap key order of the row path (the same for every
-    row when no value is null), one C++ formatting pass into a StringBlock."""
-    w, names = m.writer, list(m.reader.names)
+def _w_kv(m: "FormatTransMapper", get, names):
+    """KV over DOUBLE values without nulls: the HashMap key order of the row path (the same for every row when
+    no value is null), one C++ formatting pass into a StringBlock."""
+    w, names = m.writer, list(names)
     if (len(w.cd) != 1 or w.cd in _SAFE_SEP or any(w.cd in k or w.vd in k for k in names)
-            or len(set(names)) != len(names)):
+            or len(set(names)) != len(names) or not all(k.isascii() for k in names) or not w.vd.isascii()):
         return None
     order = [k for k, _ in _hash_items({k: "" for k in names})]
-    X = _double_matrix(mt, order)
+    X = get(order)
     N = _native()
-    if X is None or N is None or not all(k.isascii() for k in order) or not w.vd.isascii():
+    if X is None or N is None:
         return None
     from ...common.table import Column
     r = N.java_double_rows_fmt(X, [k + w.vd for k in order], [""] * len(order), w.cd)
     return None if r is None else [Column(_string_block(r[0], r[1]))]
 
 
-def _cols_to_json(m: "FormatTransMapper", mt):
-    """COLUMNS -> JSON over DOUBLE columns without nulls with plain key names: {"k":"v",...} (the map holds the
-    values' strings) in the row path's HashMap order."""
+def _w_json(m: "FormatTransMapper", get, names):
+    """JSON over DOUBLE values without nulls with plain key names: {"k":"v",...} (the map holds the values'
+    strings) in the row path's HashMap order."""
     import json as _json
-    names = list(m.reader.names)
+    names = list(names)
     if not all(_PLAIN_KEY.fullmatch(k) for k in names) or len(set(names)) != len(names):
         return None
     order = list(_json.loads(gson_dumps({k: "0" for k in names}, java_map_order=True)).keys())
-    X = _double_matrix(mt, order)
+    X = get(order)
     N = _native()
     if X is None or N is None:
         return None
     from ...common.table import Column
     r = N.java_double_rows_fmt(X, ['"' + k + '":"' for k in order], ['"'] * len(order), ",", "{", "}")
     return None if r is None else [Column(_string_block(r[0], r[1]))]
+
+
+def _cols_to_kv(m: "FormatTransMapper", mt):
+    return _w_kv(m, _cols_getter(mt), m.reader.names)
+
+
+def _cols_to_json(m: "FormatTransMapper", mt):
+    return _w_json(m, _cols_getter(mt), m.reader.names)
+
+
+def _csv_getter(m: "FormatTransMapper", mt):
+    """The CSV reader's DOUBLE fields parsed once (C++), as a getter of [n, k] matrices; None unless every field
+    is DOUBLE and present (an empty field is a null map value: the row path)."""
+    import numpy as np
+    r = m.reader
+    if any(t != Types.DOUBLE for t in r.parser.types):
+        return None
+    cols = csv_columns_fast(mt.cols[r.col], r.parser.types, r.parser.delim, r.parser.quote)
+    if cols is None or any(c.nulls is not None for c in cols):
+        return None
+    arr = {nm: c.values.numpy() for nm, c in zip(r.names, cols)}
+    return lambda names: np.ascontiguousarray(np.stack([arr[nm] for nm in names], 1)) if names else None
+
+
+def _csv_to(writer):
+    def fn(m: "FormatTransMapper", mt):
+        get = _csv_getter(m, mt)
+        return None if get is None else writer(m, get, m.reader.names)
+    return fn
 
 
 def _kv_to_cols(m: "FormatTransMapper", mt):
@@ -767,7 +810,9 @@ def _kv_to_cols(m: "FormatTransMapper", mt):
 _COLUMNAR = {("COLUMNS", "VECTOR"): _cols_to_vector, ("COLUMNS", "CSV"): _cols_to_csv,
              ("VECTOR", "COLUMNS"): _vector_to_cols, ("CSV", "COLUMNS"): _csv_to_cols,
              ("KV", "COLUMNS"): _kv_to_cols, ("JSON", "COLUMNS"): _json_to_cols,
-             ("COLUMNS", "KV"): _cols_to_kv, ("COLUMNS", "JSON"): _cols_to_json}
+             ("COLUMNS", "KV"): _cols_to_kv, ("COLUMNS", "JSON"): _cols_to_json,
+             ("CSV", "VECTOR"): _csv_to(_w_vector), ("CSV", "CSV"): _csv_to(_w_csv), ("CSV", "KV"): _csv_to(_w_kv),
+             ("CSV", "JSON"): _csv_to(_w_json)}
 
 
 class FormatTransMapper(Mapper):

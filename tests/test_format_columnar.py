@@ -244,3 +244,24 @@ def test_columns_to_kv_json_fast_equals_rows(to):
     mtn, _ = _num_table(6, 100, rng, nulls=True)            # nulls drop keys row by row: row path
     assert m._fast(m, mtn) is None
     _both(m, mtn)
+
+
+@pytest.mark.parametrize("to", ["VECTOR", "CSV", "KV", "JSON"])
+def test_csv_to_writers_fast_equals_rows(to):
+    """CSV (all-DOUBLE schema) into the VECTOR / CSV / KV / JSON writers: one C++ parse, one C++ format pass."""
+    rng = np.random.default_rng(29)
+    names = ["x0", "x1", "x2", "x3"]
+    X = _doubles(4 * 200, rng).reshape(200, 4)
+    X[~np.isfinite(X)] = 2.5
+    lines = [",".join(repr(float(v)) for v in row) for row in X]
+    mt = MTable(TableSchema(["csv"], [Types.STRING]), [Column(lines)])
+    p = Params().set("fromFormat", "CSV").set("toFormat", to).set("csvCol", "csv") \
+        .set("schemaStr", ", ".join(f"{c} double" for c in names)).set("vectorCol", "o").set("kvCol", "o") \
+        .set("jsonCol", "o")
+    if to == "CSV":
+        p = p.set("csvFieldDelimiter", ",")
+    m = F.FormatTransMapper(mt.schema, p)
+    assert m._fast(m, mt) is not None
+    _both(m, mt)
+    mt2 = MTable(mt.schema, [Column(lines[:5] + ["1.0,,2.0,3.0"])])   # an empty field: the row path
+    assert m._fast(m, mt2) is None
