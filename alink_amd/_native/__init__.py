@@ -324,19 +324,22 @@ def parse_dense_vectors(strings: Sequence[str], d: int) -> Optional[np.ndarray]:
     return parse_dense_vectors_packed(np.frombuffer(buf, dtype=np.uint8), off, d)
 
 
-def parse_dense_vectors_packed(data: np.ndarray, off: np.ndarray, d: int) -> Optional[np.ndarray]:
+def parse_dense_vectors_packed(data: np.ndarray, off: np.ndarray, d: int, with_counts: bool = False):
     """[n, d] float64 of packed dense-vector strings (plain decimal tokens split by ' ' / ','; shorter rows are
-    zero-padded), or None (library missing, or a row with another token or more than ``d`` values)."""
+    zero-padded), or None (library missing, or a row with another token or more than ``d`` values).
+    ``with_counts``: also the int64 [n] number of values of every row."""
     if lib is None:
         return None
     data = np.ascontiguousarray(data, dtype=np.uint8) if data.size else np.zeros(1, np.uint8)
     off = np.ascontiguousarray(off, dtype=np.int64)
     n = off.size - 1
     out = np.zeros((n, d), dtype=np.float64)
-    rc = lib.alink_parse_dense_vectors(_ptr(data), _ptr(off), ctypes.c_int64(n), ctypes.c_int64(d), _ptr(out))
+    cnt = np.zeros(max(n, 1), dtype=np.int64) if with_counts else None
+    rc = lib.alink_parse_dense_vectors(_ptr(data), _ptr(off), ctypes.c_int64(n), ctypes.c_int64(d), _ptr(out),
+                                       None if cnt is None else _ptr(cnt))
     if rc != 0:
         return None
-    return out
+    return (out, cnt[:n]) if with_counts else out
 
 
 def parse_kv_packed(data: np.ndarray, off: np.ndarray, keys: Sequence[str], cd: str, vd: str):

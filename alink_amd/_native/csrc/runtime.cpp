@@ -233,7 +233,8 @@ void alink_murmur3_utf8_batch(const uint8_t* bytes, const int64_t* off, int64_t 
 }
 
 // dense vector strings -> row-major [n][d] doubles (missing tail = 0); returns -1 - row on error
-int alink_parse_dense_vectors(const char* buf, const int64_t* off, int64_t n, int64_t d, double* out) {
+int alink_parse_dense_vectors(const char* buf, const int64_t* off, int64_t n, int64_t d, double* out,
+                              int64_t* counts) {
     int64_t err = -1;
 #pragma omp parallel for schedule(static)
     for (int64_t i = 0; i < n; ++i) {
@@ -264,6 +265,7 @@ int alink_parse_dense_vectors(const char* buf, const int64_t* off, int64_t n, in
             row[j++] = v;
             p = q;
         }
+        if (counts != nullptr) counts[i] = j;
     }
     return err >= 0 ? (int)(-1 - err) : 0;
 }

@@ -795,6 +795,48 @@ def _csv_getter(m: "FormatTransMapper", mt):
     return lambda names: np.ascontiguousarray(np.stack([arr[nm] for nm in names], 1)) if names else None
 
 
+def _vector_getter(m: "FormatTransMapper", mt):
+    """(names, getter) of the VECTOR reader over dense vectors that all have exactly the reader's width (the map
+    then holds every name: the schema names, or "0" .. "d-1" without a schema), or None."""
+    import numpy as np
+    import torch
+    r = m.reader
+    c = mt.cols[r.col]
+    if isinstance(c.values, torch.Tensor) and c.values.dim() == 2:
+        if c.nulls is not None and bool(c.nulls.any()):
+            return None
+        V = c.values.to("cpu", torch.float64).numpy()
+        d = V.shape[1]
+    else:
+        N = _native()
+        packed = _packed_strings(c) if N is not None else None
+        if packed is None or packed[1].size < 2:
+            return None
+        d = len(r.names) if r.names is not None else None
+        if d is None:
+            # width from the first row, then every row must match it
+            first = bytes(packed[0][packed[1][0]:packed[1][1]]).decode("ascii", "replace")
+            d = len([t for t in first.replace(",", " ").split(" ") if t])
+        res = N.parse_dense_vectors_packed(packed[0], packed[1], d, with_counts=True) if d else None
+        if res is None:
+            return None
+        V, cnt = res
+        if not (cnt == d).all():
+            return None
+    names = list(r.names) if r.names is not None else [str(i) for i in range(d)]
+    if len(names) != d or len(set(names)) != d:
+        return None
+    pos = {nm: i for i, nm in enumerate(names)}
+    return names, (lambda ns: np.ascontiguousarray(V[:, [pos[nm] for nm in ns]]) if ns else None)
+
+
+def _vector_to(writer):
+    def fn(m: "FormatTransMapper", mt):
+        g = _vector_getter(m, mt)
+        return None if g is None else writer(m, g[1], g[0])
+    return fn
+
+
 def _csv_to(writer):
     def fn(m: "FormatTransMapper", mt):
         get = _csv_getter(m, mt)
@@ -812,7 +854,9 @@ _COLUMNAR = {("COLUMNS", "VECTOR"): _cols_to_vector, ("COLUMNS", "CSV"): _cols_t
              ("KV", "COLUMNS"): _kv_to_cols, ("JSON", "COLUMNS"): _json_to_cols,
              ("COLUMNS", "KV"): _cols_to_kv, ("COLUMNS", "JSON"): _cols_to_json,
              ("CSV", "VECTOR"): _csv_to(_w_vector), ("CSV", "CSV"): _csv_to(_w_csv), ("CSV", "KV"): _csv_to(_w_kv),
-             ("CSV", "JSON"): _csv_to(_w_json)}
+             ("CSV", "JSON"): _csv_to(_w_json),
+             ("VECTOR", "CSV"): _vector_to(_w_csv), ("VECTOR", "KV"): _vector_to(_w_kv),
+             ("VECTOR", "JSON"): _vector_to(_w_json)}
 
 
 class FormatTransMapper(Mapper):

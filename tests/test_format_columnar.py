@@ -265,3 +265,25 @@ def test_csv_to_writers_fast_equals_rows(to):
     _both(m, mt)
     mt2 = MTable(mt.schema, [Column(lines[:5] + ["1.0,,2.0,3.0"])])   # an empty field: the row path
     assert m._fast(m, mt2) is None
+
+
+@pytest.mark.parametrize("to", ["CSV", "KV", "JSON"])
+@pytest.mark.parametrize("named", [False, True])
+def test_vector_to_writers_fast_equals_rows(to, named):
+    """Dense VECTOR (all rows of the reader's width; with or without a schema) into the CSV / KV / JSON writers."""
+    rng = np.random.default_rng(31)
+    X = _doubles(5 * 150, rng).reshape(150, 5)
+    X[~np.isfinite(X)] = -3.25
+    strs = [" ".join(repr(float(v)) for v in row) for row in X]
+    mt = MTable(TableSchema(["vec"], [Types.STRING]), [Column(strs)])
+    p = Params().set("fromFormat", "VECTOR").set("toFormat", to).set("vectorCol", "vec").set("kvCol", "o") \
+        .set("jsonCol", "o").set("csvCol", "o")
+    if named or to == "CSV":
+        p = p.set("schemaStr", "a double, b double, c double, d double, e double")
+    m = F.FormatTransMapper(mt.schema, p)
+    fast_ok = not (to == "JSON" and not (named or to == "CSV"))   # digit keys are not plain JSON names
+    assert (m._fast(m, mt) is not None) == fast_ok
+    _both(m, mt)
+    mt2 = MTable(mt.schema, [Column(strs[:4] + ["1.0 2.0"])])       # a shorter row: the row path
+    assert m._fast(m, mt2) is None
+    _both(m, mt2)
