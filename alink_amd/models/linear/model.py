@@ -334,8 +334,9 @@ class LinearModelMapper(_LinearMapperBase):
             t = self.helper.out_types[0]
             if t.torch_dtype is None or not all(isinstance(x, (int, float)) and not isinstance(x, bool) for x in lv):
                 return None
-            out = [Column(torch.where(dot >= 0, torch.tensor(lv[0], dtype=t.torch_dtype, device=dot.device),
-                                      torch.tensor(lv[1], dtype=t.torch_dtype, device=dot.device)))]
+            # filled on the device from Python scalars: no per-batch host -> device copies of the label values
+            out = [Column(torch.full(dot.shape, lv[1], dtype=t.torch_dtype, device=dot.device)
+                          .masked_fill_(dot >= 0, lv[0]))]
         if self.detail_col:
             if tname in ("LR", "SVM"):
                 prob = 1.0 - 1.0 / (1.0 + torch.exp(dot))
