@@ -89,14 +89,23 @@ __global__ __launch_bounds__(TB) void oneshot_kernel(const T* in, T* out, int64_
             uint64_t spins = 0;
             // wrap-safe: a peer may already have finished call seq and signalled seq + 1 before this wave's
             // first poll (a preempted wave, ranks time-sharing a GPU); any flag at or past seq means "arrived"
+            // back-off: ~4096 short polls (~0.4 ms) at full rate, then s_sleep 64 (32x as long, counted as 32
+            // spins so the deadline stays in time units) -- a late peer (ranks time-sharing one GPU, a rank still
+            // in its compute kernel) no longer has the waiting waves take issue slots from its work
             while ((int32_t)(__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - seq) < 0) {
-                if (++spins > deadline_spins) {
+                if (spins > deadline_spins) {
                     atomicOr(err, 1);
                     if (host_err != nullptr)          // mapped host word: the host sees the failure without a copy
                         __hip_atomic_store(host_err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     break;
                 }
-                __builtin_amdgcn_s_sleep(2);
+                if (spins < 4096) {
+                    __builtin_amdgcn_s_sleep(2);
+                    spins += 1;
+                } else {
+                    __builtin_amdgcn_s_sleep(64);
+                    spins += 32;
+                }
             }
         }
         __syncthreads();
