@@ -121,6 +121,21 @@ class _Side:
         self.n_pos = (cs[self.indptr[1:]] - cs[self.indptr[:-1]]).to(torch.float64)
         self.n_all = counts.to(torch.float64)
 
+    def subset_cached(self, key, mask_fn):
+        """``subset(mask_fn())`` computed once per key: the row blocks of a side are the same every iteration,
+        so the CSR sub-matrices (and the solver's row plan keyed by their identity) are built on the first sweep
+        only.  The whole side is the side's own CSR (no copy)."""
+        sub = getattr(self, "_subs", None)
+        if sub is None:
+            sub = self._subs = {}
+        if key not in sub:
+            mask = mask_fn()
+            if bool(mask.all()):
+                sub[key] = (torch.arange(mask.numel(), device=mask.device), self.indptr, self.nbr, self.rating)
+            else:
+                sub[key] = self.subset(mask)
+        return sub[key]
+
     def subset(self, mask: torch.Tensor):
         sel = mask.nonzero().view(-1)
         starts, ends = self.indptr[:-1][sel], self.indptr[1:][sel]
@@ -138,7 +153,7 @@ GATHER_BLOCKS = int(os.environ.get("ALINK_ALS_GATHER_BLOCKS", "4"))
 
 
 def _update(side: _Side, mask: torch.Tensor, Y: torch.Tensor, X: torch.Tensor, lam: float, implicit: bool,
-            alpha: float, nonneg: bool, YtY: Optional[torch.Tensor]):
+            alpha: float, nonneg: bool, YtY: Optional[torch.Tensor], key=None):
     """Solve this rank's rows of ``side`` against ``Y`` and replicate them into ``X``.  Over P ranks the rows are
     solved in GATHER_BLOCKS pieces: the all-gather of piece b runs on the comm stream (asynchronous) while piece
     b+1 solves (SURVEY §7.1 compute / communication overlap; the reference's AlsTrain exchanges factor blocks
@@ -149,22 +164,26 @@ def _update(side: _Side, mask: torch.Tensor, Y: torch.Tensor, X: torch.Tensor, l
         bounds = [(len(sel_all) * b) // GATHER_BLOCKS for b in range(GATHER_BLOCKS + 1)]
         pend = []
         for b in range(GATHER_BLOCKS):
-            m = torch.zeros_like(mask)
-            m[sel_all[bounds[b]:bounds[b + 1]]] = True
-            rows, x = _solve(side, m, Y, X, lam, implicit, alpha, nonneg, YtY)
+            def piece(b=b):
+                m = torch.zeros_like(mask)
+                m[sel_all[bounds[b]:bounds[b + 1]]] = True
+                return m
+            rows, x = _solve(side, piece, Y, X, lam, implicit, alpha, nonneg, YtY,
+                             key=None if key is None else (key, b, GATHER_BLOCKS))
             pend.append((comm.all_gather_varlen_async(rows), comm.all_gather_varlen_async(x)))
         for pr, px in pend:
             X[pr.wait()] = px.wait().to(X.dtype)
         return
-    rows, x = _solve(side, mask, Y, X, lam, implicit, alpha, nonneg, YtY)
+    rows, x = _solve(side, lambda: mask, Y, X, lam, implicit, alpha, nonneg, YtY,
+                     key=None if key is None else (key, 0, 1))
     rows_all = comm.all_gather_varlen(rows)
     x_all = comm.all_gather_varlen(x)
     X[rows_all] = x_all.to(X.dtype)
 
 
-def _solve(side: _Side, mask: torch.Tensor, Y: torch.Tensor, X: torch.Tensor, lam: float, implicit: bool,
-           alpha: float, nonneg: bool, YtY: Optional[torch.Tensor]):
-    sel, indptr, nbr, rating = side.subset(mask)
+def _solve(side: _Side, mask_fn, Y: torch.Tensor, X: torch.Tensor, lam: float, implicit: bool,
+           alpha: float, nonneg: bool, YtY: Optional[torch.Tensor], key=None):
+    sel, indptr, nbr, rating = side.subset_cached(key, mask_fn) if key is not None else side.subset(mask_fn())
     if sel.numel() and not nonneg and aops.fused_supported(Y):
         # GPU: normal equations + Cholesky fused per row (ops/csrc/als.hip), no [m, r, r] tensor in HBM
         reg = (side.n_pos[sel] if implicit else side.n_all[sel]) * lam
@@ -257,7 +276,7 @@ def train_als(mt: MTable, params: Params, env) -> AlsModelData:
             YtY = tn_matmul(Y.to(torch.float64), Y.to(torch.float64)) if implicit else None
             for bb in range(nblocks):
                 mask = (side.raw.abs() % nblocks) == bb
-                _update(side, mask, Y, X, lam, implicit, alpha, nonneg, YtY)
+                _update(side, mask, Y, X, lam, implicit, alpha, nonneg, YtY, key=("block", bb, nblocks))
             mark(f"update {name}")
         if timed:
             if dev.type == "cuda":

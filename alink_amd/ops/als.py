@@ -61,8 +61,6 @@ def normal_equations(indptr: torch.Tensor, nbr: torch.Tensor, rating: torch.Tens
     nbr = nbr.to(torch.int32).contiguous()
     rating = rating.to(torch.float32).contiguous()
     Yf = Y.to(torch.float32).contiguous()
-    if nbr.numel() and int(nbr.max()) >= Yf.shape[0]:
-        raise ValueError("neighbour index out of range")
     A = torch.empty((m, r, r), dtype=torch.float32, device=Y.device)
     b = torch.empty((m, r), dtype=torch.float32, device=Y.device)
     if m == 0:
@@ -139,6 +137,49 @@ def fused_supported(Y: torch.Tensor) -> bool:
     return Y.is_cuda and Y.shape[1] <= 64 and (_lib.available() or not _lib.torch_fallback_allowed())
 
 
+_PLANS = {}
+
+
+def _row_plan(indptr: torch.Tensor, nbr: torch.Tensor, n_factors: int, buckets: tuple) -> dict:
+    """The row partition of a CSR rating matrix for ``fused_solve`` -- heavy rows and their chunking, the
+    Woodbury buckets, the light rows -- and the neighbour-range check, computed once per (CSR, bucket set):
+    ALS re-solves the same two CSR matrices every iteration, so the per-sweep deg / nonzero / max passes (and
+    their host synchronisations) are paid on the first sweep only.  Keyed by the tensors' identity and version."""
+    import weakref
+    key = (indptr.data_ptr(), indptr.numel(), indptr._version, nbr.data_ptr(), nbr.numel(), nbr._version, n_factors,
+           buckets, HEAVY_DEGREE, HEAVY_CHUNK)
+    hit = _PLANS.get(key)
+    if hit is not None and hit[0]() is indptr and hit[1]() is nbr:
+        return hit[2]
+    if nbr.numel() and int(nbr.max()) >= n_factors:
+        raise ValueError("neighbour index out of range")
+    dev = indptr.device
+    deg = indptr[1:] - indptr[:-1]
+    heavy = torch.nonzero(deg > HEAVY_DEGREE, as_tuple=False).reshape(-1)
+    small = torch.zeros_like(deg, dtype=torch.bool)
+    lo, ids_list = -1, []
+    for P in buckets:
+        sel = (deg > lo) & (deg <= P)
+        small |= sel
+        ids_list.append(torch.nonzero(sel, as_tuple=False).reshape(-1))
+        lo = P
+    light = torch.nonzero((deg <= HEAVY_DEGREE) & ~small, as_tuple=False).reshape(-1) \
+        if (heavy.numel() or buckets) else None
+    plan = {"heavy": heavy, "buckets": ids_list, "light": light, "chunk_row": None, "chunk_start": None}
+    if heavy.numel():
+        hd = deg[heavy]
+        nck = (hd + HEAVY_CHUNK - 1) // HEAVY_CHUNK
+        chunk_row = torch.repeat_interleave(torch.arange(heavy.numel(), device=dev), nck)
+        first = torch.cumsum(nck, 0) - nck
+        chunk_start = indptr[:-1][heavy][chunk_row] + (torch.arange(int(nck.sum()), device=dev) - first[chunk_row]) \
+            * HEAVY_CHUNK
+        plan["chunk_row"], plan["chunk_start"] = chunk_row.contiguous(), chunk_start.contiguous()
+    if len(_PLANS) >= 8:
+        _PLANS.clear()
+    _PLANS[key] = (weakref.ref(indptr), weakref.ref(nbr), plan)
+    return plan
+
+
 def fused_solve(indptr: torch.Tensor, nbr: torch.Tensor, rating: torch.Tensor, Y: torch.Tensor, reg: torch.Tensor,
                 implicit: bool = False, alpha: float = 0.0, YtY: torch.Tensor = None) -> torch.Tensor:
     """x_u (float32 [m, r]) of ``(sum c y y^T + reg_u I [+ YtY]) x = sum w y`` for every CSR row u (GPU)."""
@@ -153,23 +194,15 @@ def fused_solve(indptr: torch.Tensor, nbr: torch.Tensor, rating: torch.Tensor, Y
     nbr = nbr.to(device=dev, dtype=torch.int32).contiguous()
     rating = rating.to(device=dev, dtype=torch.float32).contiguous()
     Yf = Y.to(torch.float32).contiguous()
-    if nbr.numel() and int(nbr.max()) >= Yf.shape[0]:
-        raise ValueError("neighbour index out of range")
     regd = reg.to(device=dev, dtype=torch.float64).contiguous()
     yty = None if YtY is None else YtY.to(device=dev, dtype=torch.float64).contiguous()
     status = torch.zeros(m, dtype=torch.int32, device=dev)
     st = _lib.stream_ptr(dev)
-    deg = indptr[1:] - indptr[:-1]
-    heavy = torch.nonzero(deg > HEAVY_DEGREE, as_tuple=False).reshape(-1)
     RP = int(L.alink_als_padded_rank(r))
     buckets = [P for P in WOODBURY_BUCKETS if WOODBURY and not implicit and yty is None and P < RP]
-    small = torch.zeros_like(deg, dtype=torch.bool)
-    lo = -1
-    for P in buckets:
-        sel = (deg > lo) & (deg <= P)
-        small |= sel
-        ids = torch.nonzero(sel, as_tuple=False).reshape(-1)
-        lo = P
+    plan = _row_plan(indptr, nbr, Yf.shape[0], tuple(buckets))
+    heavy, light = plan["heavy"], plan["light"]
+    for P, ids in zip(buckets, plan["buckets"]):
         if ids.numel():
             if P == 16 and WOODBURY_MFMA:
                 rc = L.alink_als_woodbury16_mfma(indptr.data_ptr(), nbr.data_ptr(), rating.data_ptr(), Yf.data_ptr(),
@@ -181,10 +214,6 @@ def fused_solve(indptr: torch.Tensor, nbr: torch.Tensor, rating: torch.Tensor, Y
                                                 status.data_ptr(), st)
             if rc != 0:
                 raise RuntimeError(f"alink_als_woodbury_solve failed: {rc}")
-    if heavy.numel() or buckets:
-        light = torch.nonzero((deg <= HEAVY_DEGREE) & ~small, as_tuple=False).reshape(-1)
-    else:
-        light = None
     nl = m if light is None else light.numel()
     if nl:
         fn = L.alink_als_mfma_solve if (MFMA_LIGHT and RP == 64) else L.alink_als_fused_solve
@@ -196,12 +225,7 @@ def fused_solve(indptr: torch.Tensor, nbr: torch.Tensor, rating: torch.Tensor, Y
     if heavy.numel():
         # popular items: the neighbour list is split into HEAVY_CHUNK pieces, one wave each (partial Grams
         # summed in fp64), then one wave per row solves
-        hd = deg[heavy]
-        nck = (hd + HEAVY_CHUNK - 1) // HEAVY_CHUNK
-        chunk_row = torch.repeat_interleave(torch.arange(heavy.numel(), device=dev), nck)
-        first = torch.cumsum(nck, 0) - nck
-        chunk_start = indptr[:-1][heavy][chunk_row] + (torch.arange(int(nck.sum()), device=dev) - first[chunk_row]) \
-            * HEAVY_CHUNK
+        chunk_row, chunk_start = plan["chunk_row"], plan["chunk_start"]
         G = torch.zeros((heavy.numel(), RP, RP), dtype=torch.float64, device=dev)
         B = torch.zeros((heavy.numel(), RP), dtype=torch.float64, device=dev)
         rc = L.alink_als_heavy_solve(indptr.data_ptr(), nbr.data_ptr(), rating.data_ptr(), Yf.data_ptr(), r,
