@@ -14,7 +14,9 @@
 // * one workgroup = 4 waves; a wave owns 32 rows whose bf16 B fragments stay in 4*KS VGPRs while it
 //   sweeps every centroid block of the chunk (C chunk staged once per workgroup in LDS, XOR-swizzled so
 //   the 32 rows a fragment read touches fall in distinct 16-byte bank groups);
-// * the next 32-row group's fragments are loaded while the current group runs its MFMAs;
+// * RG = 2 (default for D <= 128): a wave takes two 32-row groups per iteration, so each centroid fragment and
+//   bias read from LDS feeds two independent MFMA chains;
+// * the next iteration's row fragments are loaded while the current ones run their MFMAs;
 // * chunks of > 256 candidates are processed by successive launches that merge into (idx, d2) in place
 //   (``merge`` = 1), so X is read once per 256 candidates.
 //
@@ -39,7 +41,7 @@ __device__ __forceinline__ int cswz(int row, int ch) {
     return row * (NCH * 16) + 16 * (ch ^ (row & MASK));
 }
 
-template <int KS>
+template <int KS, int RG>
 __global__ __launch_bounds__(256, 2) void kmeans_nearest_kernel(
     const __bf16* __restrict__ X, int64_t N, const __bf16* __restrict__ C, const float* __restrict__ chalf,
     int m, int c0, int* __restrict__ out_idx, float* __restrict__ out_d2, int merge) {
@@ -63,97 +65,122 @@ __global__ __launch_bounds__(256, 2) void kmeans_nearest_kernel(
     for (int e = tid; e < nb * 32; e += 256) lneg[e] = e < m ? -chalf[e] : -3.0e38f;
     __syncthreads();
 
+    // a wave owns RG consecutive 32-row groups per iteration: every centroid fragment read from LDS (and every
+    // bias read) feeds RG independent MFMA chains
     const int64_t ngroups = (N + 31) >> 5;
+    const int64_t nsuper = (ngroups + RG - 1) / RG;
     const int64_t gstride = (int64_t)gridDim.x * WAVES;
     int64_t g = (int64_t)blockIdx.x * WAVES + wave;
 
-    auto load_frags = [&](int64_t grp, bf16x8* xf) {
-        int64_t r = grp * 32 + l32;
-        r = r < N ? r : N - 1;
-        const bf16x8* p = reinterpret_cast<const bf16x8*>(X + r * D + 8 * h);
+    auto load_frags = [&](int64_t sg, bf16x8 (*xf)[KS]) {
 #pragma unroll
-        for (int s = 0; s < KS; ++s) xf[s] = p[2 * s];
+        for (int q = 0; q < RG; ++q) {
+            int64_t r = (sg * RG + q) * 32 + l32;
+            r = r < N ? r : N - 1;
+            const bf16x8* p = reinterpret_cast<const bf16x8*>(X + r * D + 8 * h);
+#pragma unroll
+            for (int s = 0; s < KS; ++s) xf[q][s] = p[2 * s];
+        }
     };
 
-    bf16x8 xf[KS], xn[KS];
-    if (g < ngroups) load_frags(g, xf);
-    for (; g < ngroups; g += gstride) {
+    bf16x8 xf[RG][KS], xn[RG][KS];
+    if (g < nsuper) load_frags(g, xf);
+    for (; g < nsuper; g += gstride) {
         const int64_t gn = g + gstride;
-        if (gn < ngroups) load_frags(gn, xn);
+        if (gn < nsuper) load_frags(gn, xn);
 
-        float xx = 0.f;
+        float xx[RG], best[RG];
+        int bidx[RG];
 #pragma unroll
-        for (int s = 0; s < KS; ++s)
+        for (int q = 0; q < RG; ++q) {
+            float a = 0.f;
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const float v = (float)xf[s][j];
-                xx = fmaf(v, v, xx);
-            }
-        xx += __shfl_xor(xx, 32);
+            for (int s = 0; s < KS; ++s)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const float v = (float)xf[q][s][j];
+                    a = fmaf(v, v, a);
+                }
+            xx[q] = a + __shfl_xor(a, 32);
+            best[q] = -3.4e38f;
+            bidx[q] = 0x7fffffff;
+        }
 
-        float best = -3.4e38f;
-        int bidx = 0x7fffffff;
         for (int b = 0; b < nb; ++b) {
-            f32x16 acc;
+            f32x16 acc[RG];
 #pragma unroll
-            for (int r = 0; r < 16; ++r) acc[r] = lneg[32 * b + (r & 3) + 8 * (r >> 2) + 4 * h];
+            for (int r = 0; r < 16; ++r) {
+                const float bias = lneg[32 * b + (r & 3) + 8 * (r >> 2) + 4 * h];
+#pragma unroll
+                for (int q = 0; q < RG; ++q) acc[q][r] = bias;
+            }
             const int crow = 32 * b + l32;
 #pragma unroll
             for (int s = 0; s < KS; ++s) {
                 const bf16x8 cf = *reinterpret_cast<const bf16x8*>(lds + cswz<KS>(crow, 2 * s + h));
-                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cf, xf[s], acc, 0, 0, 0);
+#pragma unroll
+                for (int q = 0; q < RG; ++q) acc[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cf, xf[q][s], acc[q], 0, 0, 0);
             }
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int c = 32 * b + (r & 3) + 8 * (r >> 2) + 4 * h;
-                if (acc[r] > best) {   // c increases with r inside a lane -> strict > keeps the lowest index
-                    best = acc[r];
-                    bidx = c;
+            for (int q = 0; q < RG; ++q)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int c = 32 * b + (r & 3) + 8 * (r >> 2) + 4 * h;
+                    if (acc[q][r] > best[q]) {   // c increases with r inside a lane -> strict > keeps the lowest index
+                        best[q] = acc[q][r];
+                        bidx[q] = c;
+                    }
                 }
+        }
+#pragma unroll
+        for (int q = 0; q < RG; ++q) {
+            float bq = best[q];
+            int iq = bidx[q];
+            const float ob = __shfl_xor(bq, 32);
+            const int oi = __shfl_xor(iq, 32);
+            if (ob > bq || (ob == bq && oi < iq)) {
+                bq = ob;
+                iq = oi;
             }
-        }
-        const float ob = __shfl_xor(best, 32);
-        const int oi = __shfl_xor(bidx, 32);
-        if (ob > best || (ob == best && oi < bidx)) {
-            best = ob;
-            bidx = oi;
-        }
-        const int64_t row = g * 32 + l32;
-        if (h == 0 && row < N) {
-            const float d2 = fmaxf(xx - 2.f * best, 0.f);
-            const int gi = bidx + c0;
-            if (merge) {
-                const float prev = out_d2[row];
-                if (d2 < prev) {
+            const int64_t row = (g * RG + q) * 32 + l32;
+            if (h == 0 && row < N) {
+                const float d2 = fmaxf(xx[q] - 2.f * bq, 0.f);
+                const int gi = iq + c0;
+                if (merge) {
+                    const float prev = out_d2[row];
+                    if (d2 < prev) {
+                        out_d2[row] = d2;
+                        out_idx[row] = gi;
+                    }
+                } else {
                     out_d2[row] = d2;
                     out_idx[row] = gi;
                 }
-            } else {
-                out_d2[row] = d2;
-                out_idx[row] = gi;
             }
         }
-        if (gn < ngroups) {
+        if (gn < nsuper) {
 #pragma unroll
-            for (int s = 0; s < KS; ++s) xf[s] = xn[s];
+            for (int q = 0; q < RG; ++q)
+#pragma unroll
+                for (int s = 0; s < KS; ++s) xf[q][s] = xn[q][s];
         }
     }
 }
 
-template <int KS>
+template <int KS, int RG>
 int launch(const void* X, int64_t N, const void* C, const float* chalf, int m, int c0, int* idx, float* d2,
            int merge, int grid, hipStream_t st) {
     const int nb = (m + 31) / 32;
     const size_t lds = (size_t)nb * 32 * (16 * KS) * 2 + (size_t)nb * 32 * 4;
     static bool attr_set = false;  // > 64 KiB of dynamic LDS must be opted into once per kernel
     if (!attr_set) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void*>(kmeans_nearest_kernel<KS>),
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(kmeans_nearest_kernel<KS, RG>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize,
                                 NB_MAX * 32 * 16 * KS * 2 + NB_MAX * 32 * 4) != hipSuccess)
             return 3;
         attr_set = true;
     }
-    hipLaunchKernelGGL(kmeans_nearest_kernel<KS>, dim3(grid), dim3(256), lds, st,
+    hipLaunchKernelGGL((kmeans_nearest_kernel<KS, RG>), dim3(grid), dim3(256), lds, st,
                        reinterpret_cast<const __bf16*>(X), N, reinterpret_cast<const __bf16*>(C), chalf, m, c0,
                        idx, d2, merge);
     return hipGetLastError() == hipSuccess ? 0 : 2;
@@ -270,17 +297,30 @@ int alink_kmeans_par_pick(const double* cost, int64_t n, int64_t first_row, int6
     return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
-// one chunk (m <= 256) of nearest-centroid search; grid = persistent workgroups
-int alink_kmeans_nearest_bf16(const void* X, int64_t N, int D, const void* C, const float* chalf, int m, int c0,
-                              int* out_idx, float* out_d2, int merge, int grid, void* stream) {
-    if (N <= 0 || m <= 0 || m > NB_MAX * 32 || grid <= 0) return 1;
+// one chunk (m <= 256) of nearest-centroid search; grid = persistent workgroups; rg = 32-row groups per wave
+// iteration (1 or 2; 2 needs D <= 128)
+int alink_kmeans_nearest_bf16_rg(const void* X, int64_t N, int D, const void* C, const float* chalf, int m, int c0,
+                                 int* out_idx, float* out_d2, int merge, int grid, int rg, void* stream) {
+    if (N <= 0 || m <= 0 || m > NB_MAX * 32 || grid <= 0 || (rg != 1 && rg != 2) || (rg == 2 && D > 128)) return 1;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (rg == 2) {
+        switch (D) {
+            case 64: return launch<4, 2>(X, N, C, chalf, m, c0, out_idx, out_d2, merge, grid, st);
+            case 128: return launch<8, 2>(X, N, C, chalf, m, c0, out_idx, out_d2, merge, grid, st);
+            default: return 1;
+        }
+    }
     switch (D) {
-        case 64: return launch<4>(X, N, C, chalf, m, c0, out_idx, out_d2, merge, grid, st);
-        case 128: return launch<8>(X, N, C, chalf, m, c0, out_idx, out_d2, merge, grid, st);
-        case 256: return launch<16>(X, N, C, chalf, m, c0, out_idx, out_d2, merge, grid, st);
+        case 64: return launch<4, 1>(X, N, C, chalf, m, c0, out_idx, out_d2, merge, grid, st);
+        case 128: return launch<8, 1>(X, N, C, chalf, m, c0, out_idx, out_d2, merge, grid, st);
+        case 256: return launch<16, 1>(X, N, C, chalf, m, c0, out_idx, out_d2, merge, grid, st);
         default: return 1;
     }
+}
+
+int alink_kmeans_nearest_bf16(const void* X, int64_t N, int D, const void* C, const float* chalf, int m, int c0,
+                              int* out_idx, float* out_d2, int merge, int grid, void* stream) {
+    return alink_kmeans_nearest_bf16_rg(X, N, D, C, chalf, m, c0, out_idx, out_d2, merge, grid, 1, stream);
 }
 
 }  // extern "C"

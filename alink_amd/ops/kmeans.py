@@ -527,6 +527,10 @@ def assign(X: torch.Tensor, C: torch.Tensor, chunk: int = 1 << 20) -> Tuple[torc
 
 NEAREST_DIMS = (64, 128, 256)
 NEAREST_CHUNK = 256
+# 32-row groups per wave iteration of the nearest kernel (2: each LDS centroid fragment feeds two MFMA chains;
+# D = 256 always runs 1)
+NEAREST_RG = int(os.environ.get("ALINK_KMEANS_NEAREST_RG", "2"))
+NEAREST_GRID = int(os.environ.get("ALINK_KMEANS_NEAREST_GRID", "2"))     # persistent workgroups per CU
 
 
 def nearest_supported(X: torch.Tensor) -> bool:
@@ -571,12 +575,14 @@ def nearest_hip(X: torch.Tensor, C: torch.Tensor) -> Tuple[torch.Tensor, torch.T
     chalf = (0.5 * (Cb.float() ** 2).sum(1)).contiguous()
     idx = torch.empty(n, dtype=torch.int32, device=X.device)
     d2 = torch.empty(n, dtype=torch.float32, device=X.device)
-    grid = 2 * _num_cus(X.device)
+    grid = NEAREST_GRID * _num_cus(X.device)
     st = _lib.stream_ptr(X.device)
     for c0 in range(0, Cb.shape[0], NEAREST_CHUNK):
         m = min(NEAREST_CHUNK, Cb.shape[0] - c0)
-        rc = L.alink_kmeans_nearest_bf16(X.data_ptr(), n, d, Cb[c0].data_ptr(), chalf[c0].data_ptr(), m, c0,
-                                         idx.data_ptr(), d2.data_ptr(), int(c0 > 0), grid, st)
+        # one centroid block (the first k-means|| cost pass): load-bound, RG = 1 measured 2 % ahead
+        rg = 2 if NEAREST_RG == 2 and d <= 128 and m > 32 else 1
+        rc = L.alink_kmeans_nearest_bf16_rg(X.data_ptr(), n, d, Cb[c0].data_ptr(), chalf[c0].data_ptr(), m, c0,
+                                            idx.data_ptr(), d2.data_ptr(), int(c0 > 0), grid, rg, st)
         if rc != 0:
             raise RuntimeError(f"alink_kmeans_nearest_bf16 failed: {rc}")
     return idx, d2

@@ -144,6 +144,22 @@ def test_nearest_kernel_matches_fp32_reference(n, m, d):
     assert (idx.long() != ridx).float().mean().item() < 0.01
 
 
+@pytest.mark.parametrize("d", [64, 128])
+@pytest.mark.parametrize("n,m", [(1, 3), (33, 40), (65, 1), (20001, 201), (70001, 401)])
+def test_nearest_kernel_two_row_groups_identical(n, m, d, monkeypatch):
+    """RG = 2 (two 32-row groups per wave iteration) returns exactly the RG = 1 indices and distances, including
+    row counts that leave the last wave iteration half or wholly past N."""
+    from alink_amd.ops import kmeans as K
+    g = torch.Generator(device="cpu").manual_seed(n * 7 + m + d)
+    X = (torch.randn(n, d, generator=g) * 2).to("cuda", torch.bfloat16)
+    C = (torch.randn(m, d, generator=g) * 2).to("cuda", torch.float64)
+    monkeypatch.setattr(K, "NEAREST_RG", 1)
+    i1, d1 = K.nearest_hip(X, C)
+    monkeypatch.setattr(K, "NEAREST_RG", 2)
+    i2, d2 = K.nearest_hip(X, C)
+    assert torch.equal(i1, i2) and torch.equal(d1, d2)
+
+
 def test_nearest_kernel_exact_candidates():
     """k-means|| candidates are rows of X: distance to itself must come out 0 and the index its own."""
     from alink_amd.ops import kmeans as K

@@ -1,0 +1,57 @@
+#!/usr/bin/env python3
+"""A/B of the k-means|| nearest-centroid kernel (csrc/kmeans_nearest.hip): rows per wave iteration (RG 1 / 2) and
+persistent workgroups per CU, at the headline shape (1e8 x 128 bf16) for candidate counts 1 (the first cost pass),
+~201 (initSteps = 2: the weights pass) and 401.  Every variant must give the same (idx, d2) as RG = 1.
+
+    python tools/kmeans_nearest_bench.py [--rows 100000000] [--reps 5]"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from alink_amd.ops import kmeans as K  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", type=int, default=100_000_000)
+    ap.add_argument("--reps", type=int, default=5)
+    a = ap.parse_args()
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev).manual_seed(0)
+    X = (torch.randn(a.rows, 128, device=dev, generator=g) * 3).to(torch.bfloat16)
+    floor_ms = X.numel() * 2 / 8e12 * 1e3
+    print(json.dumps({"rows": a.rows, "bytes": X.numel() * 2, "hbm_floor_ms_at_8TBs": round(floor_ms, 3)}), flush=True)
+    for m in (1, 201, 256, 401):
+        C = X[torch.randint(0, a.rows, (m,), device=dev, generator=g)].double()
+        ref = None
+        for rg, gm in ((1, 2), (2, 2), (1, 4), (2, 1)):
+            K.NEAREST_RG, K.NEAREST_GRID = rg, gm
+            out = K.nearest_hip(X, C)
+            torch.cuda.synchronize()
+            ts = []
+            for _ in range(a.reps):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                K.nearest_hip(X, C)
+                e1.record()
+                e1.synchronize()
+                ts.append(e0.elapsed_time(e1))
+            ts.sort()
+            if ref is None:
+                ref = out
+                same = True
+            else:
+                same = bool(torch.equal(out[0], ref[0]) and torch.equal(out[1], ref[1]))
+            flops = 2.0 * a.rows * 128 * m
+            print(json.dumps({"m": m, "rg": rg, "wg_per_cu": gm, "ms_median": round(ts[len(ts) // 2], 3),
+                              "ms_min": round(ts[0], 3), "tflops": round(flops / (ts[0] * 1e-3) / 1e12, 1),
+                              "identical_to_rg1": same}), flush=True)
+            del out
+
+
+if __name__ == "__main__":
+    main()
