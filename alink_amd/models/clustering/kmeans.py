@@ -430,13 +430,18 @@ class KMeansUpdateCentroids(ComputeFunction):
     straight through the host's criterion / engine bookkeeping.  The queued result is used only if that next
     superstep runs with exactly these centroids (no empty-cluster compaction, not converged, not the last
     step); otherwise it is dropped — results are identical either way.  ``sync_steps``: supersteps after which
-    nothing may be queued ahead (a caller that times supersteps, e.g. bench.py, synchronises there)."""
+    nothing may be queued ahead (a caller that times supersteps, e.g. bench.py, synchronises there).
+    ``tol`` (the termination epsilon): the update kernel also leaves a device word "converged" (max shift < tol, no
+    empty cluster) that the queued kernel reads first, returning at once — so the run's last superstep does not pay
+    for a pass over X nobody reads.  Its result is then dropped on the host by the same test."""
 
-    def __init__(self, dist_type: str, max_iter: int = 2 ** 31 - 1, sync_steps=(), speculate: bool = True):
+    def __init__(self, dist_type: str, max_iter: int = 2 ** 31 - 1, sync_steps=(), speculate: bool = True,
+                 tol: Optional[float] = None):
         self.dist_type = dist_type
         self.max_iter = int(max_iter)
         self.sync_steps = set(sync_steps or ())
         self.speculate = speculate
+        self.tol = None if tol is None else float(tol)
 
     def calc(self, ctx):
         tgt = ctx.getObj(CENTROID2) if ctx.getStepNo() % 2 == 0 else ctx.getObj(CENTROID1)
@@ -453,13 +458,15 @@ class KMeansUpdateCentroids(ComputeFunction):
             X = ctx.getObj(TRAIN_DATA)
             spec_ok = (self.speculate and step >= 2 and step < self.max_iter and step not in self.sync_steps
                        and X is not None and X.shape[0] > 0 and kops.hip_supported(X, buf.shape[0]))
-            C, read = kops.update_centroids_hip(buf, prev, deferred=True)
+            C, read = kops.update_centroids_hip(buf, prev, deferred=True,
+                                                skip_tol=self.tol if spec_ok and self.tol is not None else None)
             if spec_ok:
                 ctx.putObj(SPEC_BUF, ((step + 1, kops._ckey(C)),
-                                      kops.assign_accumulate_hip(X, C, reverse=kops.serpentine_reverse(step + 1))))
+                                      kops.assign_accumulate_hip(X, C, reverse=kops.serpentine_reverse(step + 1),
+                                                                 skip=read.skip)))
             shift, has_empty = read()
-            if has_empty:
-                ctx.removeObj(SPEC_BUF)
+            if has_empty or (read.skip is not None and shift is not None and shift < self.tol):
+                ctx.removeObj(SPEC_BUF)     # not used (compaction) / possibly skipped on the device (converged)
             if not has_empty:
                 ctx.putObj("maxShift", shift)
                 tgt[0] = ctx.getStepNo()
@@ -574,7 +581,7 @@ def train_kmeans(X: torch.Tensor, k: int, max_iter: int, tol: float, dist_type: 
          .add(KMeansPreallocateCentroid())
          .add(KMeansAssignCluster())
          .add(AllReduce(CENTROID_ALL_REDUCE))
-         .add(KMeansUpdateCentroids(dist_type, max_iter, sync_steps))
+         .add(KMeansUpdateCentroids(dist_type, max_iter, sync_steps, tol=tol))
          .setCompareCriterionOfNode0(KMeansIterTermination(dist_type, tol), replicated=True)
          .closeWith(KMeansOutputModel(dist_type, vector_col, lat_col, lon_col))
          .setMaxIter(max_iter))

@@ -69,6 +69,8 @@ _EXTRA_SIGNATURES = {
     "alink_kmeans_v7_grid": [_c_i64, _c_int],
     "alink_kmeans_assign_accum_bf16_v10": [_c_vp, _c_i64, _c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_int, _c_vp, _c_vp,
                                            _c_int],
+    "alink_kmeans_assign_accum_bf16_v10s": [_c_vp, _c_i64, _c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_int, _c_vp, _c_vp,
+                                            _c_int, _c_vp],
     "alink_kmeans_assign_accum_bf16_v10d": [_c_vp, _c_i64, _c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_int, _c_vp, _c_vp,
                                             _c_int, _c_vp, _c_int, _c_d],
     "alink_kmeans_v10_grid": [_c_i64, _c_int],
@@ -87,6 +89,7 @@ _EXTRA_SIGNATURES = {
     "alink_linear_search_f64": [_c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_int, _c_int, _c_d, _c_d, _c_int, _c_vp,
                                 _c_int, _c_vp, _c_vp],
     "alink_kmeans_update": [_c_vp, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_int, _c_vp, _c_vp],
+    "alink_kmeans_update2": [_c_vp, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_int, _c_vp, _c_d, _c_vp, _c_vp],
     "alink_kmeans_host_stat_alloc": [ctypes.POINTER(_c_vp), ctypes.POINTER(_c_vp)],
     "alink_kmeans_host_stat_free": [_c_vp],
     "alink_kmeans_accum_bf16": [_c_vp, _c_i64, _c_int, _c_vp, _c_vp, _c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp],

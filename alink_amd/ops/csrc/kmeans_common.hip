@@ -90,7 +90,8 @@ __global__ __launch_bounds__(128) void kmeans_update_kernel(const double* __rest
                                                             double* __restrict__ C, __bf16* __restrict__ cpad,
                                                             float* __restrict__ ninit,
                                                             unsigned long long* __restrict__ stat, int hyst,
-                                                            unsigned long long* __restrict__ host_out) {
+                                                            unsigned long long* __restrict__ host_out, double tol,
+                                                            unsigned* __restrict__ skip) {
     __shared__ float red[128];
     __shared__ double redd[128];
     const int c = blockIdx.x, d = threadIdx.x;
@@ -152,6 +153,14 @@ __global__ __launch_bounds__(128) void kmeans_update_kernel(const double* __rest
                 const unsigned long long s0 = atomicAdd(stat, 0ull), s1 = atomicAdd(stat + 1, 0ull);
                 __hip_atomic_store(host_out, s0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 __hip_atomic_store(host_out + 1, s1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                if (skip != nullptr) {
+                    // the next superstep will not run on these centroids: an empty cluster (the host compacts and
+                    // relaunches) or converged by the host's own test (max shift < tol on the same double) — a
+                    // speculative next-superstep assign launched with this word returns at once
+                    const unsigned drop =
+                        s1 != 0ull || (prev != nullptr && __longlong_as_double((long long)s0) < tol);
+                    __hip_atomic_store(skip, drop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
                 __threadfence_system();
                 atomicExch(stat, 0ull);
                 atomicExch(stat + 1, 0ull);
@@ -172,14 +181,22 @@ extern "C" {
 // before the FIRST launch; the kernel's last block writes host_out[0..1] and re-zeroes stat itself.
 // hyst != 0: bf16 operand hysteresis (keep cpad[c][d] while |C[c][d] - cpad[c][d]| < one bf16 ulp of max_d |C[c][d]|;
 // cpad should hold the operands of the step just run, but any contents are safe: a kept value is that close to C)
-int alink_kmeans_update(const double* buf, int k, const double* prev, double* C, void* cpad, float* ninit,
-                        unsigned long long* stat, int hyst, unsigned long long* host_out, void* stream) {
-    if (k < 1 || k > 128) return -1;
+// skip != nullptr (needs host_out): the last block also writes *skip = 1 when some cluster is empty or (prev given)
+// the max shift is < tol (the termination test), else 0 — read by a speculative next-superstep assign launch
+int alink_kmeans_update2(const double* buf, int k, const double* prev, double* C, void* cpad, float* ninit,
+                         unsigned long long* stat, int hyst, unsigned long long* host_out, double tol, unsigned* skip,
+                         void* stream) {
+    if (k < 1 || k > 128 || (skip != nullptr && host_out == nullptr)) return -1;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     if (host_out == nullptr && hipMemsetAsync(stat, 0, 2 * sizeof(unsigned long long), st) != hipSuccess) return -2;
     hipLaunchKernelGGL(kmeans_update_kernel, dim3(128), dim3(128), 0, st, buf, k, prev, C, (__bf16*)cpad, ninit,
-                       stat, hyst, host_out);
+                       stat, hyst, host_out, tol, skip);
     return (int)hipGetLastError();
+}
+
+int alink_kmeans_update(const double* buf, int k, const double* prev, double* C, void* cpad, float* ninit,
+                        unsigned long long* stat, int hyst, unsigned long long* host_out, void* stream) {
+    return alink_kmeans_update2(buf, k, prev, C, cpad, ninit, stat, hyst, host_out, 0.0, nullptr, stream);
 }
 
 // 32 bytes of mapped, coherent pinned host memory for the update's stats: *host = host address, *dev = the

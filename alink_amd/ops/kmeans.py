@@ -146,13 +146,15 @@ def _num_cus(device) -> int:
 
 def assign_accumulate_hip(X: torch.Tensor, C: torch.Tensor, grid: Optional[int] = None,
                           assign_out: Optional[torch.Tensor] = None, mode: int = 0,
-                          reverse: bool = False) -> torch.Tensor:
+                          reverse: bool = False, skip: Optional[torch.Tensor] = None) -> torch.Tensor:
     """[k, d+1] fp64 sums|counts of this rank's rows (``csrc/kmeans_v10.hip`` for k <= 112, else
     ``csrc/kmeans_v7.hip``: role-split waves on 16x16x32 MFMA, LDS-DMA tile ring; ``kernel_version``).
     ``assign_out`` (int32 [N]) also receives every row's centroid id; ``mode`` 1/2 are the kernel's load-only /
     compute-only diagnostics (results meaningless).  ``reverse`` (v10): every workgroup walks its rows backwards —
     Lloyd alternates it per superstep (serpentine order), so a pass starts on the rows the previous pass read last,
-    which are still in the Infinity Cache.  Same assignments and counts; the fp32 sums differ only in order."""
+    which are still in the Infinity Cache.  Same assignments and counts; the fp32 sums differ only in order.
+    ``skip`` (v10, static split): a device word written by ``update_centroids_hip(..., skip_tol=)``; when it is
+    nonzero at run time the launch returns at once and the result is garbage (the caller drops it)."""
     global HIP_CALLS
     L = _lib.require()
     HIP_CALLS += 1
@@ -181,7 +183,11 @@ def assign_accumulate_hip(X: torch.Tensor, C: torch.Tensor, grid: Optional[int] 
         mode |= (V7_VAR << 4) if ver == "v7" else (V10_FLAGS << 4)
     if reverse and ver == "v10":
         mode |= 32
-    if ver == "v10" and V10_POOL > 0 and (mode & 7) == 0 and hasattr(L, "alink_kmeans_assign_accum_bf16_v10d"):
+    if skip is not None and ver == "v10" and V10_POOL <= 0:
+        rc = L.alink_kmeans_assign_accum_bf16_v10s(
+            X.data_ptr(), n, cpad.data_ptr(), ninit.data_ptr(), k, slab.data_ptr(), slab_cnt.data_ptr(), grid, st,
+            None if assign_out is None else assign_out.data_ptr(), int(mode), skip.data_ptr())
+    elif ver == "v10" and V10_POOL > 0 and (mode & 7) == 0 and hasattr(L, "alink_kmeans_assign_accum_bf16_v10d"):
         dyn = _DYN.get(dev.index)
         if dyn is None:
             dyn = _DYN[dev.index] = [torch.zeros(2, dtype=torch.int32, device=dev), 0]
@@ -202,6 +208,7 @@ def assign_accumulate_hip(X: torch.Tensor, C: torch.Tensor, grid: Optional[int] 
 
 
 _STAT = {}
+_SKIP = {}      # device -> int32 [1] convergence word of the last update (speculative assign launches read it)
 
 
 class _HostStat:
@@ -248,12 +255,15 @@ def operand_hysteresis() -> bool:
 
 
 def update_centroids_hip(buf: torch.Tensor, prev: Optional[torch.Tensor], deferred: bool = False,
-                         hysteresis: Optional[bool] = None):
+                         hysteresis: Optional[bool] = None, skip_tol: Optional[float] = None):
     """Fused Lloyd update on the all-reduced ``[k, 129]`` buffer (``csrc/kmeans_common.hip``): returns
     ``(C [k,128] fp64, max_shift vs prev or None, any_empty)`` with ONE 16-byte device->host read, and leaves
     the next superstep's bf16 operands prepared (``prepare_centroids`` of the returned C launches nothing).
     ``deferred=True`` returns ``(C, read)`` instead: ``read()`` waits for the stats later, so the caller can queue
-    more GPU work (the next superstep's assign kernel) first."""
+    more GPU work (the next superstep's assign kernel) first.  ``skip_tol`` (with ``deferred``): the kernel also
+    writes a device word = (some cluster empty, or prev given and max shift < skip_tol) — ``read.skip`` is that word (None
+    when unavailable), for a speculative ``assign_accumulate_hip(..., skip=read.skip)`` to return at once on
+    convergence; the caller must drop such a result whenever ``shift < skip_tol`` or a cluster is empty."""
     L = _lib.require()
     dev = buf.device
     k = buf.shape[0]
@@ -270,9 +280,15 @@ def update_centroids_hip(buf: torch.Tensor, prev: Optional[torch.Tensor], deferr
     C = torch.empty((k, HIP_D), dtype=torch.float64, device=dev)
     if hysteresis is None:
         hysteresis = operand_hysteresis()
-    rc = L.alink_kmeans_update(buf.data_ptr(), k, None if pv is None else pv.data_ptr(), C.data_ptr(),
-                               cpad.data_ptr(), ninit.data_ptr(), stat.data_ptr(), int(bool(hysteresis)),
-                               hs.dev_ptr, _lib.stream_ptr(dev))
+    skip = None
+    if skip_tol is not None and hs.dev_ptr is not None:
+        skip = _SKIP.get(dev.index)
+        if skip is None:
+            skip = _SKIP[dev.index] = torch.zeros(1, dtype=torch.int32, device=dev)
+    rc = L.alink_kmeans_update2(buf.data_ptr(), k, None if pv is None else pv.data_ptr(), C.data_ptr(),
+                                cpad.data_ptr(), ninit.data_ptr(), stat.data_ptr(), int(bool(hysteresis)),
+                                hs.dev_ptr, float(skip_tol) if skip is not None else 0.0,
+                                None if skip is None else skip.data_ptr(), _lib.stream_ptr(dev))
     if rc != 0:
         raise RuntimeError(f"alink_kmeans_update failed: {rc}")
     if hs.dev_ptr is None:
@@ -288,6 +304,7 @@ def update_centroids_hip(buf: torch.Tensor, prev: Optional[torch.Tensor], deferr
         shift_bits, empty = hs.values()
         shift = float(np.frombuffer(np.int64(shift_bits).tobytes(), dtype=np.float64)[0]) if use_prev else None
         return shift, bool(empty)
+    read.skip = skip
     if deferred:
         return C, read
     shift, empty = read()

@@ -271,6 +271,40 @@ def test_update_operand_hysteresis():
     torch.testing.assert_close(ninit[:k], -0.5 * (f * f).sum(1), rtol=1e-6, atol=1e-3)
 
 
+def test_update_convergence_word_and_skipped_assign():
+    """kmeans_update's skip word (an empty cluster, or max shift < tol with prev given) is exactly the host's drop
+    test on the returned stats; an assign launch reading a set word leaves the slabs untouched, one reading a
+    cleared word equals a plain launch."""
+    from alink_amd.ops import kmeans as K
+    X, C = _data(100_003, 60, seed=9)
+    buf = K.assign_accumulate_hip(X, C)
+    prev = (buf[:, :128] / buf[:, 128:]) + 1e-3
+    for tol, want in ((1.0, 1), (1e-9, 0)):
+        Cn, read = K.update_centroids_hip(buf, prev, deferred=True, hysteresis=False, skip_tol=tol)
+        assert read.skip is not None
+        shift, empty = read()
+        assert not empty and (shift < tol) == bool(want)
+        assert int(read.skip.item()) == want
+    Cn, read = K.update_centroids_hip(buf, prev, deferred=True, hysteresis=False, skip_tol=1e-9)
+    read()
+    plain = K.assign_accumulate_hip(X, Cn)
+    assert torch.equal(K.assign_accumulate_hip(X, Cn, skip=read.skip), plain)
+    bad = buf.clone()
+    bad[3, 128] = 0.0
+    _, read = K.update_centroids_hip(bad, prev, deferred=True, hysteresis=False, skip_tol=-1.0)
+    _, empty = read()
+    assert empty and int(read.skip.item()) == 1
+    _, read = K.update_centroids_hip(bad, None, deferred=True, hysteresis=False, skip_tol=-1.0)
+    _, empty = read()
+    assert empty and int(read.skip.item()) == 1
+    _, read = K.update_centroids_hip(buf, prev, deferred=True, hysteresis=False, skip_tol=1e9)
+    read()
+    slab = [t.clone() for pair in K._BUF.values() for t in pair]
+    K.assign_accumulate_hip(X, Cn, skip=read.skip)
+    torch.cuda.synchronize()
+    assert all(torch.equal(a, b) for a, b in zip(slab, [t for pair in K._BUF.values() for t in pair]))
+
+
 def test_speculative_next_step_launch_gives_identical_model():
     """KMeansUpdateCentroids queues the next superstep's assign kernel before reading the update stats; the
     trained model must be bit-identical to a run without speculation (sync after every step), incl. a run that
