@@ -75,7 +75,11 @@ class FtrlTrainStreamOp(StreamOperator):
 
     ``updateMode``:
 
-    * ``SEQUENTIAL`` (default): sample-by-sample rule in stream order (native host loop).  With P ranks every
+    * ``AUTO`` (default): ``SHARDED`` when the environment's device is a GPU, else ``SEQUENTIAL``.  SHARDED's
+      step-start margins are the reference's own staleness: there a sample's margin is computed on arrival
+      (``FtrlTrainStreamOp.java:396-420``) and the coefficients are updated when the reduced margin comes back
+      through the feedback edge (``:424-480``), with other samples' updates in between.
+    * ``SEQUENTIAL``: sample-by-sample rule in stream order (native host loop), every margin on the latest weights.  With P ranks every
       step all-gathers the ranks' micro-batches (rank order) and every rank applies the identical update to a
       replicated coefficient vector, so the model equals the 1-rank model on the same global batch sequence.
     * ``SHARDED``: the reference's distributed design (``FtrlTrainStreamOp.java:72-85`` split info,
@@ -98,9 +102,10 @@ class FtrlTrainStreamOp(StreamOperator):
     micro-batches stay in lockstep: a rank whose stream ended keeps joining steps with an empty batch until all
     ranks are done.  Snapshots: at the first step, whenever any rank's ``timeInterval`` elapsed, and at the end.
     """
-    EXTRA_PARAMS = [ParamInfo("updateMode", str, "SEQUENTIAL, SHARDED (feature-sharded micro-batch), DATA_PARALLEL "
-                                                 "(replicated, all-reduced mini-batch gradients) or HOGWILD (GPU, "
-                                                 "one wave per sample)", default="SEQUENTIAL"),
+    EXTRA_PARAMS = [ParamInfo("updateMode", str, "AUTO (SHARDED on a GPU, else SEQUENTIAL), SEQUENTIAL, SHARDED "
+                                                 "(feature-sharded micro-batch), DATA_PARALLEL (replicated, "
+                                                 "all-reduced mini-batch gradients) or HOGWILD (GPU, one wave per "
+                                                 "sample)", default="AUTO"),
                     ParamInfo("asyncGradReduce", bool, "DATA_PARALLEL: overlap the gradient all-reduce of a step "
                                                        "with scoring the next (one-step-stale gradients)",
                               default=False)]
@@ -138,7 +143,9 @@ class FtrlTrainStreamOp(StreamOperator):
         self._vec_col = _pget(p, "vectorCol")
         self._feat_cols = _pget(p, "featureCols")
         self._vsize = _pget(p, "vectorSize")
-        self._mode = str(_pget(p, "updateMode", "SEQUENTIAL")).upper()
+        self._mode = str(_pget(p, "updateMode", "AUTO")).upper()
+        if self._mode == "AUTO":
+            self._mode = "SHARDED" if self.env.device.type == "cuda" else "SEQUENTIAL"
         self._async_reduce = bool(_pget(p, "asyncGradReduce", False))
         self._pending = None
         if self._mode not in ("SEQUENTIAL", "SHARDED", "DATA_PARALLEL", "HOGWILD"):
