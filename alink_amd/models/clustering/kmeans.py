@@ -381,8 +381,10 @@ def kmeans_init(X: torch.Tensor, k: int, init_mode: str, init_steps: int, dist_t
             cost = torch.minimum(cost, _min_dist_to(X, new, dist_type))
     if centers.shape[0] <= k:
         return centers
-    near = _nearest(X, centers, dist_type)
-    w = torch.bincount(near, minlength=centers.shape[0]).to(torch.float64)
+    if _hip_nearest_ok(X, dist_type):
+        w = kops.nearest_counts_hip(X, centers).to(torch.float64)      # one pass, no per-row output
+    else:
+        w = torch.bincount(_nearest(X, centers, dist_type), minlength=centers.shape[0]).to(torch.float64)
     comm.all_reduce(w)
     return _local_kmeans(centers, w, k, dist_type, seed=seed)
 

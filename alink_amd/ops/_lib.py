@@ -82,7 +82,7 @@ _EXTRA_SIGNATURES = {
     "alink_kmeans_nearest_bf16": [_c_vp, _c_i64, _c_int, _c_vp, _c_vp, _c_int, _c_int, _c_vp, _c_vp, _c_int,
                                   _c_int, _c_vp],
     "alink_kmeans_nearest_bf16_rg": [_c_vp, _c_i64, _c_int, _c_vp, _c_vp, _c_int, _c_int, _c_vp, _c_vp, _c_int,
-                                     _c_int, _c_int, _c_vp],
+                                     _c_int, _c_int, _c_vp, _c_vp],
     "alink_linear_grad_f64": [_c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_int, _c_int, _c_d, _c_vp, _c_int, _c_vp,
                               _c_vp],
     "alink_linear_grad_pad": [_c_int],

@@ -44,11 +44,13 @@ __device__ __forceinline__ int cswz(int row, int ch) {
 template <int KS, int RG>
 __global__ __launch_bounds__(256, 2) void kmeans_nearest_kernel(
     const __bf16* __restrict__ X, int64_t N, const __bf16* __restrict__ C, const float* __restrict__ chalf,
-    int m, int c0, int* __restrict__ out_idx, float* __restrict__ out_d2, int merge) {
+    int m, int c0, int* __restrict__ out_idx, float* __restrict__ out_d2, int merge,
+    unsigned long long* __restrict__ counts) {
     constexpr int D = 16 * KS;
     extern __shared__ __attribute__((aligned(16))) char lds[];
     const int nb = (m + 31) >> 5;
     float* lneg = reinterpret_cast<float*>(lds + nb * 32 * D * 2);  // after the staged chunk
+    unsigned* lcnt = reinterpret_cast<unsigned*>(lneg + nb * 32);    // counts mode: rows per candidate
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
@@ -62,7 +64,10 @@ __global__ __launch_bounds__(256, 2) void kmeans_nearest_kernel(
         if (row < m) v = *reinterpret_cast<const uint4*>(C + (int64_t)row * D + 8 * ch);
         *reinterpret_cast<uint4*>(lds + cswz<KS>(row, ch)) = v;
     }
-    for (int e = tid; e < nb * 32; e += 256) lneg[e] = e < m ? -chalf[e] : -3.0e38f;
+    for (int e = tid; e < nb * 32; e += 256) {
+        lneg[e] = e < m ? -chalf[e] : -3.0e38f;
+        lcnt[e] = 0u;
+    }
     __syncthreads();
 
     // a wave owns RG consecutive 32-row groups per iteration: every centroid fragment read from LDS (and every
@@ -143,7 +148,10 @@ __global__ __launch_bounds__(256, 2) void kmeans_nearest_kernel(
                 iq = oi;
             }
             const int64_t row = (g * RG + q) * 32 + l32;
-            if (h == 0 && row < N) {
+            if (counts != nullptr) {
+                // counts mode (one launch holds every candidate): the k-means|| candidate weights, no per-row output
+                if (h == 0 && row < N && (unsigned)iq < (unsigned)m) atomicAdd(lcnt + iq, 1u);   // NaN rows: none
+            } else if (h == 0 && row < N) {
                 const float d2 = fmaxf(xx[q] - 2.f * bq, 0.f);
                 const int gi = iq + c0;
                 if (merge) {
@@ -165,24 +173,29 @@ __global__ __launch_bounds__(256, 2) void kmeans_nearest_kernel(
                 for (int s = 0; s < KS; ++s) xf[q][s] = xn[q][s];
         }
     }
+    if (counts != nullptr) {      // integer sums: the same totals in any order
+        __syncthreads();
+        for (int e = tid; e < m; e += 256)
+            if (lcnt[e] != 0u) atomicAdd(counts + e, (unsigned long long)lcnt[e]);
+    }
 }
 
 template <int KS, int RG>
 int launch(const void* X, int64_t N, const void* C, const float* chalf, int m, int c0, int* idx, float* d2,
-           int merge, int grid, hipStream_t st) {
+           int merge, int grid, hipStream_t st, unsigned long long* counts) {
     const int nb = (m + 31) / 32;
-    const size_t lds = (size_t)nb * 32 * (16 * KS) * 2 + (size_t)nb * 32 * 4;
+    const size_t lds = (size_t)nb * 32 * (16 * KS) * 2 + (size_t)nb * 32 * 8;
     static bool attr_set = false;  // > 64 KiB of dynamic LDS must be opted into once per kernel
     if (!attr_set) {
         if (hipFuncSetAttribute(reinterpret_cast<const void*>(kmeans_nearest_kernel<KS, RG>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize,
-                                NB_MAX * 32 * 16 * KS * 2 + NB_MAX * 32 * 4) != hipSuccess)
+                                NB_MAX * 32 * 16 * KS * 2 + NB_MAX * 32 * 8) != hipSuccess)
             return 3;
         attr_set = true;
     }
     hipLaunchKernelGGL((kmeans_nearest_kernel<KS, RG>), dim3(grid), dim3(256), lds, st,
                        reinterpret_cast<const __bf16*>(X), N, reinterpret_cast<const __bf16*>(C), chalf, m, c0,
-                       idx, d2, merge);
+                       idx, d2, merge, counts);
     return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
@@ -299,28 +312,33 @@ int alink_kmeans_par_pick(const double* cost, int64_t n, int64_t first_row, int6
 
 // one chunk (m <= 256) of nearest-centroid search; grid = persistent workgroups; rg = 32-row groups per wave
 // iteration (1 or 2; 2 needs D <= 128)
+// counts != nullptr: no per-row output (out_idx / out_d2 unused, merge must be 0); counts[j] (uint64, zeroed by the
+// caller) += rows whose nearest candidate is j — the k-means|| candidate weights of a single-launch candidate set
 int alink_kmeans_nearest_bf16_rg(const void* X, int64_t N, int D, const void* C, const float* chalf, int m, int c0,
-                                 int* out_idx, float* out_d2, int merge, int grid, int rg, void* stream) {
+                                 int* out_idx, float* out_d2, int merge, int grid, int rg, void* counts_v,
+                                 void* stream) {
     if (N <= 0 || m <= 0 || m > NB_MAX * 32 || grid <= 0 || (rg != 1 && rg != 2) || (rg == 2 && D > 128)) return 1;
+    unsigned long long* counts = reinterpret_cast<unsigned long long*>(counts_v);
+    if (counts != nullptr && (merge || c0 != 0)) return 1;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     if (rg == 2) {
         switch (D) {
-            case 64: return launch<4, 2>(X, N, C, chalf, m, c0, out_idx, out_d2, merge, grid, st);
-            case 128: return launch<8, 2>(X, N, C, chalf, m, c0, out_idx, out_d2, merge, grid, st);
+            case 64: return launch<4, 2>(X, N, C, chalf, m, c0, out_idx, out_d2, merge, grid, st, counts);
+            case 128: return launch<8, 2>(X, N, C, chalf, m, c0, out_idx, out_d2, merge, grid, st, counts);
             default: return 1;
         }
     }
     switch (D) {
-        case 64: return launch<4, 1>(X, N, C, chalf, m, c0, out_idx, out_d2, merge, grid, st);
-        case 128: return launch<8, 1>(X, N, C, chalf, m, c0, out_idx, out_d2, merge, grid, st);
-        case 256: return launch<16, 1>(X, N, C, chalf, m, c0, out_idx, out_d2, merge, grid, st);
+        case 64: return launch<4, 1>(X, N, C, chalf, m, c0, out_idx, out_d2, merge, grid, st, counts);
+        case 128: return launch<8, 1>(X, N, C, chalf, m, c0, out_idx, out_d2, merge, grid, st, counts);
+        case 256: return launch<16, 1>(X, N, C, chalf, m, c0, out_idx, out_d2, merge, grid, st, counts);
         default: return 1;
     }
 }
 
 int alink_kmeans_nearest_bf16(const void* X, int64_t N, int D, const void* C, const float* chalf, int m, int c0,
                               int* out_idx, float* out_d2, int merge, int grid, void* stream) {
-    return alink_kmeans_nearest_bf16_rg(X, N, D, C, chalf, m, c0, out_idx, out_d2, merge, grid, 1, stream);
+    return alink_kmeans_nearest_bf16_rg(X, N, D, C, chalf, m, c0, out_idx, out_d2, merge, grid, 1, nullptr, stream);
 }
 
 }  // extern "C"

@@ -311,6 +311,31 @@ def update_centroids_hip(buf: torch.Tensor, prev: Optional[torch.Tensor], deferr
     return C, shift, empty
 
 
+def nearest_counts_hip(X: torch.Tensor, C: torch.Tensor) -> torch.Tensor:
+    """int64 [m]: how many rows of X have each centroid as their nearest — ``nearest_hip`` + ``bincount`` in ONE
+    pass with no per-row output (per-workgroup LDS counts, integer global adds) when the m <= 256 centroids fit one
+    launch; otherwise the two-step form.  Ties and rounding exactly as ``nearest_hip``."""
+    L = _lib.require()
+    if not nearest_supported(X):
+        raise ValueError("nearest_counts_hip needs contiguous bf16 [N, D] on GPU with D in (64, 128, 256)")
+    n, d = X.shape
+    m = C.shape[0]
+    if m > NEAREST_CHUNK:
+        return torch.bincount(nearest_hip(X, C)[0].to(torch.int64), minlength=m)
+    Cb = C.to(device=X.device, dtype=torch.bfloat16).contiguous()
+    if Cb.shape[1] != d or m == 0:
+        raise ValueError("centroid shape mismatch")
+    chalf = (0.5 * (Cb.float() ** 2).sum(1)).contiguous()
+    counts = torch.zeros(m, dtype=torch.int64, device=X.device)
+    rg = 2 if NEAREST_RG == 2 and d <= 128 and m > 32 else 1
+    rc = L.alink_kmeans_nearest_bf16_rg(X.data_ptr(), n, d, Cb.data_ptr(), chalf.data_ptr(), m, 0, None, None, 0,
+                                        NEAREST_GRID * _num_cus(X.device), rg, counts.data_ptr(),
+                                        _lib.stream_ptr(X.device))
+    if rc != 0:
+        raise RuntimeError(f"alink_kmeans_nearest_bf16 (counts) failed: {rc}")
+    return counts
+
+
 def _scores(Xc: torch.Tensor, C: torch.Tensor, emulate_bf16: bool) -> torch.Tensor:
     """x.c - |c|^2/2 (argmax == argmin of squared euclidean distance)."""
     if emulate_bf16:
@@ -599,7 +624,7 @@ def nearest_hip(X: torch.Tensor, C: torch.Tensor) -> Tuple[torch.Tensor, torch.T
         # one centroid block (the first k-means|| cost pass): load-bound, RG = 1 measured 2 % ahead
         rg = 2 if NEAREST_RG == 2 and d <= 128 and m > 32 else 1
         rc = L.alink_kmeans_nearest_bf16_rg(X.data_ptr(), n, d, Cb[c0].data_ptr(), chalf[c0].data_ptr(), m, c0,
-                                            idx.data_ptr(), d2.data_ptr(), int(c0 > 0), grid, rg, st)
+                                            idx.data_ptr(), d2.data_ptr(), int(c0 > 0), grid, rg, None, st)
         if rc != 0:
             raise RuntimeError(f"alink_kmeans_nearest_bf16 failed: {rc}")
     return idx, d2

@@ -160,6 +160,24 @@ def test_nearest_kernel_two_row_groups_identical(n, m, d, monkeypatch):
     assert torch.equal(i1, i2) and torch.equal(d1, d2)
 
 
+@pytest.mark.parametrize("d", [64, 128, 256])
+@pytest.mark.parametrize("n,m", [(1, 1), (33, 40), (4097, 256), (70001, 201), (20001, 300)])
+def test_nearest_counts_equal_bincount_of_nearest(n, m, d):
+    """Counts mode of the nearest kernel (k-means|| candidate weights in one pass) == bincount of nearest_hip's
+    indices, including a NaN row (counted nowhere by the kernel) and m > 256 (two-step fallback)."""
+    from alink_amd.ops import kmeans as K
+    g = torch.Generator(device="cpu").manual_seed(n + 3 * m + d)
+    X = (torch.randn(n, d, generator=g) * 2).to("cuda", torch.bfloat16)
+    C = (torch.randn(m, d, generator=g) * 2).to("cuda", torch.float64)
+    want = torch.bincount(K.nearest_hip(X, C)[0].long(), minlength=m)
+    got = K.nearest_counts_hip(X, C)
+    assert got.dtype == torch.int64 and torch.equal(got, want)
+    if n > 1 and m <= 256:
+        X[n // 2] = float("nan")
+        got = K.nearest_counts_hip(X, C)
+        assert int(got.sum()) == n - 1
+
+
 def test_nearest_kernel_exact_candidates():
     """k-means|| candidates are rows of X: distance to itself must come out 0 and the index its own."""
     from alink_amd.ops import kmeans as K

@@ -50,6 +50,8 @@ def main():
                                         "_global_count")}
     for n, f in orig.items():
         setattr(km, n, wrap(n, f))
+    counts_orig = km.kops.nearest_counts_hip          # the candidate weights pass (one kernel, counts mode)
+    km.kops.nearest_counts_hip = wrap("nearest_counts", counts_orig)
     res = {"rows": a.rows, "k": a.k, "initSteps": a.init_steps, "device": str(dev), "reps": []}
     for _ in range(a.reps):
         acc.clear()
@@ -65,6 +67,7 @@ def main():
         res["reps"].append(rep)
     for n, f in orig.items():
         setattr(km, n, f)
+    km.kops.nearest_counts_hip = counts_orig
     # split of one full training run (the bench's convergence.reference run)
     marks = {}
     init_orig = km.kmeans_init
