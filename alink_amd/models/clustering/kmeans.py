@@ -164,6 +164,8 @@ def _hip_nearest_ok(X: torch.Tensor, dist_type: str) -> bool:
 
 def _min_dist_to(X: torch.Tensor, C: torch.Tensor, dist_type: str, chunk=1 << 20) -> torch.Tensor:
     if _hip_nearest_ok(X, dist_type):
+        if C.shape[0] == 1:      # the first k-means|| cost: one streaming pass, fp64 distances straight out
+            return kops.cost1_hip(X, C[0])
         return kops.nearest_hip(X, C)[1].to(torch.float64).sqrt_()
     out = []
     Cf = C.to(torch.float32 if X.dtype in (torch.bfloat16, torch.float16) else X.dtype)

@@ -29,6 +29,7 @@ namespace {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int NB_MAX = 8;    // centroid blocks of 32 per chunk -> 256 candidates
 constexpr int WAVES = 4;
@@ -199,6 +200,59 @@ int launch(const void* X, int64_t N, const void* C, const float* chalf, int m, i
     return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
+// k-means|| first cost pass (KMeansInitCentroids.java: every row's distance to the first, randomly drawn center):
+// a pure streaming pass, so no MFMA tile — lane l of a wave owns 8 dims (16 bytes) of row (l / LPR), LPR = D / 8
+// lanes per row, so every load instruction reads 64 x 16 B = 1 KiB of consecutive rows; the center's 8 dims stay in
+// the lane's registers.  cost[r] = sqrt(sum_d (x_rd - c_d)^2) in fp64 (the fp32 sum of squared differences:
+// no cancellation, unlike the expanded |x|^2 - 2 x.c + |c|^2 form of the nearest kernel).
+template <int D, int U, bool NT>
+__global__ __launch_bounds__(256) void kmeans_cost1_kernel(const __bf16* __restrict__ X, int64_t N,
+                                                           const __bf16* __restrict__ c, double* __restrict__ cost) {
+    constexpr int LPR = D / 8;              // lanes per row
+    constexpr int RPW = 64 / LPR;           // rows per wave-instruction (U row groups in flight per lane)
+    const int lane = threadIdx.x & 63;
+    const int piece = lane % LPR;
+    const int sub = lane / LPR;
+    float cv[8];
+    {
+        const uint4 cw = *reinterpret_cast<const uint4*>(c + 8 * piece);
+        const __bf16* cb = reinterpret_cast<const __bf16*>(&cw);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) cv[j] = (float)cb[j];
+    }
+    const int64_t ngroups = (N + RPW - 1) / RPW;
+    const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
+    const int64_t w0 = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    for (int64_t g0 = w0 * U; g0 < ngroups; g0 += nwaves * U) {
+        u32x4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            int64_t r = (g0 + u) * RPW + sub;
+            r = r < N ? r : N - 1;
+            const u32x4* src = reinterpret_cast<const u32x4*>(X + r * D + 8 * piece);
+            if constexpr (NT) v[u] = __builtin_nontemporal_load(src);
+            else v[u] = *src;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const __bf16* xb = reinterpret_cast<const __bf16*>(&v[u]);
+            float s = 0.f;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float dlt = (float)xb[j] - cv[j];
+                s = fmaf(dlt, dlt, s);
+            }
+#pragma unroll
+            for (int off = LPR / 2; off > 0; off >>= 1) s += __shfl_xor(s, off);
+            const int64_t r = (g0 + u) * RPW + sub;
+            if (piece == 0 && r < N) {
+                if constexpr (NT) __builtin_nontemporal_store(sqrt((double)s), cost + r);
+                else cost[r] = sqrt((double)s);
+            }
+        }
+    }
+}
+
 // k-means|| oversampling draw (KMeansInitCentroids.java: every row is a candidate with probability
 // 2k * cost / sum(cost)): row i of this rank is picked when u(first_row + i) < cost[i] * thre, u being the
 // counter-based splitmix64 uniform of the GLOBAL row index (models/clustering/kmeans.py _row_uniform, bit for
@@ -284,9 +338,38 @@ __global__ __launch_bounds__(SEED_T) void kmeans_seed_ref_kernel(const double* _
     if (t == 0) *mintot = mt;
 }
 
+template <int U, bool NT>
+int launch_cost1(const __bf16* Xb, int64_t N, int D, const __bf16* cb, double* cost, int grid, hipStream_t st) {
+    switch (D) {
+        case 64: hipLaunchKernelGGL((kmeans_cost1_kernel<64, U, NT>), dim3(grid), dim3(256), 0, st, Xb, N, cb, cost); break;
+        case 128: hipLaunchKernelGGL((kmeans_cost1_kernel<128, U, NT>), dim3(grid), dim3(256), 0, st, Xb, N, cb, cost); break;
+        case 256: hipLaunchKernelGGL((kmeans_cost1_kernel<256, U, NT>), dim3(grid), dim3(256), 0, st, Xb, N, cb, cost); break;
+        default: return 1;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
 }  // namespace
 
 extern "C" {
+
+// k-means|| first cost pass: cost[r] = |x_r - c| (fp64) for one bf16 center c [D]; D in {64, 128, 256}.
+// variant (rows in flight per lane / load policy; profiles/kmeans_init_r5.txt): 0 = 8, non-temporal loads and
+// stores; 1 = 8, cached (the default: 4.77 ms at 1e8 x 128, 5.5 TB/s); 2 = 16, non-temporal; 3 = 4, non-temporal
+int alink_kmeans_cost1_bf16(const void* X, int64_t N, int D, const void* c, double* cost, int grid, int variant,
+                            void* stream) {
+    if (N <= 0 || grid <= 0) return 1;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const __bf16* Xb = reinterpret_cast<const __bf16*>(X);
+    const __bf16* cb = reinterpret_cast<const __bf16*>(c);
+    switch (variant) {
+        case 0: return launch_cost1<8, true>(Xb, N, D, cb, cost, grid, st);
+        case 1: return launch_cost1<8, false>(Xb, N, D, cb, cost, grid, st);
+        case 2: return launch_cost1<16, true>(Xb, N, D, cb, cost, grid, st);
+        case 3: return launch_cost1<4, true>(Xb, N, D, cb, cost, grid, st);
+        default: return 1;
+    }
+}
 
 // reference-rule k-means++ picks over n <= 4096 candidates (kmeans_seed_ref_kernel): D [n][n], w [n], U [k-1]
 int alink_kmeans_seed_ref(const double* D, const double* w, const double* U, int n, int k, int idx0, int64_t* chosen,

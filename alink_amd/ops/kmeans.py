@@ -311,6 +311,28 @@ def update_centroids_hip(buf: torch.Tensor, prev: Optional[torch.Tensor], deferr
     return C, shift, empty
 
 
+COST1_GRID = int(os.environ.get("ALINK_KMEANS_COST1_GRID", "4"))    # streaming workgroups per CU (all resident)
+COST1_VARIANT = int(os.environ.get("ALINK_KMEANS_COST1_VARIANT", "1"))  # csrc: rows in flight / load policy
+
+
+def cost1_hip(X: torch.Tensor, c: torch.Tensor) -> torch.Tensor:
+    """fp64 [N] Euclidean distance of every row of X to ONE center (rounded to bf16: k-means|| centers are rows of
+    X) -- ``csrc/kmeans_nearest.hip`` kmeans_cost1_kernel, one coalesced streaming pass (the first k-means|| cost)."""
+    L = _lib.require()
+    if not nearest_supported(X):
+        raise ValueError("cost1_hip needs contiguous bf16 [N, D] on GPU with D in (64, 128, 256)")
+    n, d = X.shape
+    cb = c.reshape(-1).to(device=X.device, dtype=torch.bfloat16).contiguous()
+    if cb.numel() != d:
+        raise ValueError("center shape mismatch")
+    cost = torch.empty(n, dtype=torch.float64, device=X.device)
+    rc = L.alink_kmeans_cost1_bf16(X.data_ptr(), n, d, cb.data_ptr(), cost.data_ptr(),
+                                   COST1_GRID * _num_cus(X.device), COST1_VARIANT, _lib.stream_ptr(X.device))
+    if rc != 0:
+        raise RuntimeError(f"alink_kmeans_cost1_bf16 failed: {rc}")
+    return cost
+
+
 def nearest_counts_hip(X: torch.Tensor, C: torch.Tensor) -> torch.Tensor:
     """int64 [m]: how many rows of X have each centroid as their nearest — ``nearest_hip`` + ``bincount`` in ONE
     pass with no per-row output (per-workgroup LDS counts, integer global adds) when the m <= 256 centroids fit one

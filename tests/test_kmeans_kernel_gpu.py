@@ -178,6 +178,22 @@ def test_nearest_counts_equal_bincount_of_nearest(n, m, d):
         assert int(got.sum()) == n - 1
 
 
+@pytest.mark.parametrize("d", [64, 128, 256])
+@pytest.mark.parametrize("n", [1, 3, 17, 4099, 300_001])
+def test_first_cost_kernel_matches_fp64(n, d):
+    """kmeans_cost1_kernel (the first k-means|| cost pass) vs the fp64 distance to the bf16 center; a row equal to
+    the center costs exactly 0."""
+    from alink_amd.ops import kmeans as K
+    g = torch.Generator(device="cpu").manual_seed(n + d)
+    X = (torch.randn(n, d, generator=g) * 3).to("cuda", torch.bfloat16)
+    c = X[n // 2].double() + 0.0
+    got = K.cost1_hip(X, c)
+    ref = ((X.double() - c.to(torch.bfloat16).double()[None, :]) ** 2).sum(1).sqrt()
+    assert got.dtype == torch.float64 and got.shape == (n,)
+    torch.testing.assert_close(got, ref, rtol=2e-6, atol=1e-6)
+    assert float(got[n // 2]) == 0.0
+
+
 def test_nearest_kernel_exact_candidates():
     """k-means|| candidates are rows of X: distance to itself must come out 0 and the index its own."""
     from alink_amd.ops import kmeans as K

@@ -25,6 +25,25 @@ def main():
     X = (torch.randn(a.rows, 128, device=dev, generator=g) * 3).to(torch.bfloat16)
     floor_ms = X.numel() * 2 / 8e12 * 1e3
     print(json.dumps({"rows": a.rows, "bytes": X.numel() * 2, "hbm_floor_ms_at_8TBs": round(floor_ms, 3)}), flush=True)
+    c = X[12345].double()
+    for gm, var in ((4, 0), (4, 1), (4, 2), (4, 3), (2, 2), (6, 0), (8, 3)):
+        K.COST1_GRID, K.COST1_VARIANT = gm, var
+        K.cost1_hip(X, c)
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(a.reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            K.cost1_hip(X, c)
+            e1.record()
+            e1.synchronize()
+            ts.append(e0.elapsed_time(e1))
+        ts.sort()
+        print(json.dumps({"cost1_wg_per_cu": gm, "variant": var, "ms_median": round(ts[len(ts) // 2], 3), "ms_min": round(ts[0], 3),
+                          "TBps": round((X.numel() * 2 + X.shape[0] * 8) / (ts[0] * 1e-3) / 1e12, 2)}), flush=True)
+    K.COST1_GRID, K.COST1_VARIANT = 4, 1
+    if os.environ.get("COST1_ONLY"):
+        return
     for m in (1, 201, 256, 401):
         C = X[torch.randint(0, a.rows, (m,), device=dev, generator=g)].double()
         ref = None
