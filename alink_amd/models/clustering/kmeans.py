@@ -471,6 +471,26 @@ class KMeansUpdateCentroids(ComputeFunction):
             shift, has_empty = read()
             if has_empty or (read.skip is not None and shift is not None and shift < self.tol):
                 ctx.removeObj(SPEC_BUF)     # not used (compaction) / possibly skipped on the device (converged)
+            if has_empty:
+                # drop the empty clusters on the host (k x 129 values): the fused update's C rows are the same
+                # fp64 quotients the generic path computes, and the rare path issues no torch kernel that the
+                # supersteps do not already use (a first use of e.g. norm / nonzero costs a lazy code-object load,
+                # ~100 ms, inside the first job's supersteps)
+                cnt_h = cnt.cpu().numpy()
+                keep = np.flatnonzero(cnt_h > 0)
+                C_h = C.cpu().numpy()[keep]
+                C = torch.from_numpy(C_h).to(C.device)
+                # the criterion's shift (first k rows of the previous centroids vs the new ones), on the host too
+                shift_h = None
+                if prev is not None and prev.shape[0] >= len(keep) and prev.shape[1] == C_h.shape[1]:
+                    dlt = prev[:len(keep)].cpu().numpy() - C_h
+                    shift_h = float(np.sqrt((dlt * dlt).sum(1)).max()) if len(keep) else None
+                ctx.putObj("maxShift", shift_h)
+                tgt[0] = ctx.getStepNo()
+                tgt[1] = C
+                ctx.putObj("lastWeights", torch.from_numpy(cnt_h[keep]).to(cnt.device))
+                ctx.putObj(K, int(C.shape[0]))
+                return
             if not has_empty:
                 ctx.putObj("maxShift", shift)
                 tgt[0] = ctx.getStepNo()
