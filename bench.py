@@ -71,6 +71,8 @@ def main():
     ap.add_argument("--dims", type=int, default=128)
     ap.add_argument("--converge-iters", type=int, default=100, help="maxIter of the convergence run (0 = skip)")
     ap.add_argument("--timeout", type=float, default=1500.0, help="self-launched job time limit (s)")
+    ap.add_argument("--convergence-first", type=int, default=0,
+                    help="1: the untimed convergence runs before the timed run (0: after it)")
     a = ap.parse_args()
 
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -99,6 +101,39 @@ def main():
         torch.cuda.synchronize(dev)
     t_gen = time.perf_counter() - t_gen
 
+    from alink_amd.operator.batch.source import TableSourceBatchOp
+
+    def convergence_runs():
+        iters, conv = None, {}
+        # ---- convergence runs (epsilon 1e-4): the reference defaults (k-means|| initSteps=2, the reference's sampled
+        # k-means++ seeding over the candidates), the opt-in greedy seeding, and initSteps=5 ----
+        if a.converge_iters > 0:
+            for tag, steps, seeding in (("reference", 2, "reference"), ("greedy", 2, "greedy"),
+                                        ("initSteps5", 5, "reference")):
+                old = os.environ.get("ALINK_KMEANS_SEEDING")
+                os.environ["ALINK_KMEANS_SEEDING"] = seeding
+                t_c = time.perf_counter()
+                op2 = KMeansTrainBatchOp().setVectorCol("vec").setK(a.k).setMaxIter(a.converge_iters) \
+                    .setInitSteps(steps)
+                op2.linkFrom(TableSourceBatchOp(data))
+                wall = time.perf_counter() - t_c
+                info = op2.getTrainInfo()
+                if old is None:
+                    os.environ.pop("ALINK_KMEANS_SEEDING", None)
+                else:
+                    os.environ["ALINK_KMEANS_SEEDING"] = old
+                shift = (info["max_shift"] or [None])[-1]
+                conv[tag] = {"iters": info["iterations"], "wall_s": wall, "initSteps": steps,
+                             "final_max_shift": shift, "converged": shift is not None and shift < 1e-4,
+                             "seeding": seeding, "live_k": int(op2._queue.final_contexts[0].getObj("k")),
+                             "sse": _sse(data, op2, dev)}
+            iters = conv["reference"]["iters"]
+
+        return iters, conv
+
+    if a.convergence_first:
+        iters, conv = convergence_runs()
+
     # ---- timed run: W warmup supersteps + exactly K timed supersteps (no early convergence) ----
     marks = {}
 
@@ -120,7 +155,6 @@ def main():
     op = KMeansTrainBatchOp().setVectorCol("vec").setK(a.k).setMaxIter(a.warmup + a.steps).setEpsilon(-1.0)
     op._on_step = on_step
     op._sync_steps = (a.warmup, a.warmup + a.steps)   # nothing queued across the timing marks
-    from alink_amd.operator.batch.source import TableSourceBatchOp
     t_tot = time.perf_counter()
     hip0 = kops.HIP_CALLS
     op.linkFrom(TableSourceBatchOp(data))
@@ -144,30 +178,8 @@ def main():
     comm_bytes = sum(s["comm_bytes"] for s in stats) / max(1, len(stats))
     timed_sse = _sse(data, op, dev)
 
-    # ---- convergence runs (epsilon 1e-4): the reference defaults (k-means|| initSteps=2, the reference's sampled
-    # k-means++ seeding over the candidates), the opt-in greedy seeding, and initSteps=5 ----
-    iters, conv = None, {}
-    if a.converge_iters > 0:
-        for tag, steps, seeding in (("reference", 2, "reference"), ("greedy", 2, "greedy"),
-                                    ("initSteps5", 5, "reference")):
-            old = os.environ.get("ALINK_KMEANS_SEEDING")
-            os.environ["ALINK_KMEANS_SEEDING"] = seeding
-            t_c = time.perf_counter()
-            op2 = KMeansTrainBatchOp().setVectorCol("vec").setK(a.k).setMaxIter(a.converge_iters) \
-                .setInitSteps(steps)
-            op2.linkFrom(TableSourceBatchOp(data))
-            wall = time.perf_counter() - t_c
-            info = op2.getTrainInfo()
-            if old is None:
-                os.environ.pop("ALINK_KMEANS_SEEDING", None)
-            else:
-                os.environ["ALINK_KMEANS_SEEDING"] = old
-            shift = (info["max_shift"] or [None])[-1]
-            conv[tag] = {"iters": info["iterations"], "wall_s": wall, "initSteps": steps,
-                         "final_max_shift": shift, "converged": shift is not None and shift < 1e-4,
-                         "seeding": seeding, "live_k": int(op2._queue.final_contexts[0].getObj("k")),
-                         "sse": _sse(data, op2, dev)}
-        iters = conv["reference"]["iters"]
+    if not a.convergence_first:
+        iters, conv = convergence_runs()
 
     rows_per_s = a.rows * a.steps / elapsed
     res = {
