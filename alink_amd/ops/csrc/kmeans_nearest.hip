@@ -246,8 +246,10 @@ __global__ __launch_bounds__(256) void kmeans_cost1_kernel(const __bf16* __restr
             for (int off = LPR / 2; off > 0; off >>= 1) s += __shfl_xor(s, off);
             const int64_t r = (g0 + u) * RPW + sub;
             if (piece == 0 && r < N) {
-                if constexpr (NT) __builtin_nontemporal_store(sqrt((double)s), cost + r);
-                else cost[r] = sqrt((double)s);
+                // a row with a NaN / inf value costs 0 (never sampled), as in the nearest kernel's clamped form
+                const double dv = __builtin_isfinite(s) ? sqrt((double)s) : 0.0;
+                if constexpr (NT) __builtin_nontemporal_store(dv, cost + r);
+                else cost[r] = dv;
             }
         }
     }

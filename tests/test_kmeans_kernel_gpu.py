@@ -192,6 +192,11 @@ def test_first_cost_kernel_matches_fp64(n, d):
     assert got.dtype == torch.float64 and got.shape == (n,)
     torch.testing.assert_close(got, ref, rtol=2e-6, atol=1e-6)
     assert float(got[n // 2]) == 0.0
+    if n > 2:
+        X[0, d - 1] = float("nan")
+        X[1, 0] = float("inf")
+        got = K.cost1_hip(X, c)
+        assert float(got[0]) == 0.0 and float(got[1]) == 0.0
 
 
 def test_nearest_kernel_exact_candidates():
