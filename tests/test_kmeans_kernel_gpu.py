@@ -344,6 +344,29 @@ def test_update_convergence_word_and_skipped_assign():
     assert all(torch.equal(a, b) for a, b in zip(slab, [t for pair in K._BUF.values() for t in pair]))
 
 
+def test_fused_update_host_compaction_equals_generic_path(monkeypatch):
+    """An empty cluster (a far-away initial centroid) is compacted by the fused update path on the host; the model
+    and the superstep count equal the generic torch update path's on the same assign kernels."""
+    from alink_amd import useLocalEnv
+    from alink_amd.models.clustering.kmeans import train_kmeans
+    from alink_amd.ops import kmeans as K
+    env = useLocalEnv(1, device="cuda:0")
+    g = torch.Generator(device="cuda").manual_seed(11)
+    k = 24
+    centers = torch.randn(k, 128, device="cuda", generator=g) * 4
+    lab = torch.randint(0, k, (200_000,), device="cuda", generator=g)
+    X = (centers[lab] + torch.randn(lab.numel(), 128, device="cuda", generator=g)).to(torch.bfloat16)
+    init = (centers + 0.5 * torch.randn(k, 128, device="cuda", generator=g)).double()
+    init[5] = 1e4                       # attracts no row: emptied at the first update
+    monkeypatch.setenv("ALINK_KMEANS_HYSTERESIS", "0")     # the generic path re-quantises every step
+    a, qa = train_kmeans(X, k, 15, 1e-4, "EUCLIDEAN", "RANDOM", 2, "v", env, init_centroids=init)
+    monkeypatch.setattr(K, "update_supported", lambda buf: False)
+    b, qb = train_kmeans(X, k, 15, 1e-4, "EUCLIDEAN", "RANDOM", 2, "v", env, init_centroids=init)
+    assert len(qa.stats) == len(qb.stats)
+    assert [list(r) for r in a] == [list(r) for r in b]
+    assert int(qa.final_contexts[0].getObj("k")) == k - 1
+
+
 def test_speculative_next_step_launch_gives_identical_model():
     """KMeansUpdateCentroids queues the next superstep's assign kernel before reading the update stats; the
     trained model must be bit-identical to a run without speculation (sync after every step), incl. a run that
