@@ -25,6 +25,14 @@ def main():
     X = (torch.randn(a.rows, 128, device=dev, generator=g) * 3).to(torch.bfloat16)
     floor_ms = X.numel() * 2 / 8e12 * 1e3
     print(json.dumps({"rows": a.rows, "bytes": X.numel() * 2, "hbm_floor_ms_at_8TBs": round(floor_ms, 3)}), flush=True)
+    only_m = int(os.environ.get("NEAREST_ONLY_M", "0"))
+    if only_m:        # one candidate count, default variant (profiler passes)
+        C = X[torch.randint(0, a.rows, (only_m,), device=dev, generator=g)].double()
+        for _ in range(a.reps):
+            K.nearest_counts_hip(X, C)
+        torch.cuda.synchronize()
+        print(json.dumps({"m": only_m, "reps": a.reps}), flush=True)
+        return
     c = X[12345].double()
     for gm, var in ((4, 0), (4, 1), (4, 2), (4, 3), (2, 2), (6, 0), (8, 3)):
         K.COST1_GRID, K.COST1_VARIANT = gm, var
