@@ -90,7 +90,8 @@ _EXTRA_SIGNATURES = {
     "alink_linear_search_f64": [_c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_int, _c_int, _c_d, _c_d, _c_int, _c_vp,
                                 _c_int, _c_vp, _c_vp],
     "alink_kmeans_update": [_c_vp, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_int, _c_vp, _c_vp],
-    "alink_kmeans_update2": [_c_vp, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_int, _c_vp, _c_d, _c_vp, _c_vp],
+    "alink_kmeans_update2": [_c_vp, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_int, _c_vp, _c_d, _c_vp,
+                             ctypes.c_uint64, _c_vp],
     "alink_kmeans_host_stat_alloc": [ctypes.POINTER(_c_vp), ctypes.POINTER(_c_vp)],
     "alink_kmeans_host_stat_free": [_c_vp],
     "alink_kmeans_accum_bf16": [_c_vp, _c_i64, _c_int, _c_vp, _c_vp, _c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp],

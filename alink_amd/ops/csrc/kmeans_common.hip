@@ -91,7 +91,7 @@ __global__ __launch_bounds__(128) void kmeans_update_kernel(const double* __rest
                                                             float* __restrict__ ninit,
                                                             unsigned long long* __restrict__ stat, int hyst,
                                                             unsigned long long* __restrict__ host_out, double tol,
-                                                            unsigned* __restrict__ skip) {
+                                                            unsigned* __restrict__ skip, unsigned long long seq) {
     __shared__ float red[128];
     __shared__ double redd[128];
     const int c = blockIdx.x, d = threadIdx.x;
@@ -153,6 +153,12 @@ __global__ __launch_bounds__(128) void kmeans_update_kernel(const double* __rest
                 const unsigned long long s0 = atomicAdd(stat, 0ull), s1 = atomicAdd(stat + 1, 0ull);
                 __hip_atomic_store(host_out, s0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 __hip_atomic_store(host_out + 1, s1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                if (seq != 0ull) {
+                    // launch sequence number after the stats: a host polling host_out[2] == seq reads host_out[0..1]
+                    // without an event between this kernel and the work queued after it
+                    __threadfence_system();
+                    __hip_atomic_store(host_out + 2, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                }
                 if (skip != nullptr) {
                     // the next superstep will not run on these centroids: an empty cluster (the host compacts and
                     // relaunches) or converged by the host's own test (max shift < tol on the same double) — a
@@ -183,20 +189,21 @@ extern "C" {
 // cpad should hold the operands of the step just run, but any contents are safe: a kept value is that close to C)
 // skip != nullptr (needs host_out): the last block also writes *skip = 1 when some cluster is empty or (prev given)
 // the max shift is < tol (the termination test), else 0 — read by a speculative next-superstep assign launch
+// seq != 0 (needs host_out): host_out[2] = seq is written after the two stats (host completion poll)
 int alink_kmeans_update2(const double* buf, int k, const double* prev, double* C, void* cpad, float* ninit,
                          unsigned long long* stat, int hyst, unsigned long long* host_out, double tol, unsigned* skip,
-                         void* stream) {
-    if (k < 1 || k > 128 || (skip != nullptr && host_out == nullptr)) return -1;
+                         unsigned long long seq, void* stream) {
+    if (k < 1 || k > 128 || ((skip != nullptr || seq != 0ull) && host_out == nullptr)) return -1;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     if (host_out == nullptr && hipMemsetAsync(stat, 0, 2 * sizeof(unsigned long long), st) != hipSuccess) return -2;
     hipLaunchKernelGGL(kmeans_update_kernel, dim3(128), dim3(128), 0, st, buf, k, prev, C, (__bf16*)cpad, ninit,
-                       stat, hyst, host_out, tol, skip);
+                       stat, hyst, host_out, tol, skip, seq);
     return (int)hipGetLastError();
 }
 
 int alink_kmeans_update(const double* buf, int k, const double* prev, double* C, void* cpad, float* ninit,
                         unsigned long long* stat, int hyst, unsigned long long* host_out, void* stream) {
-    return alink_kmeans_update2(buf, k, prev, C, cpad, ninit, stat, hyst, host_out, 0.0, nullptr, stream);
+    return alink_kmeans_update2(buf, k, prev, C, cpad, ninit, stat, hyst, host_out, 0.0, nullptr, 0ull, stream);
 }
 
 // 32 bytes of mapped, coherent pinned host memory for the update's stats: *host = host address, *dev = the

@@ -208,6 +208,11 @@ def assign_accumulate_hip(X: torch.Tensor, C: torch.Tensor, grid: Optional[int] 
 
 
 _STAT = {}
+# wait for the update's stats by polling a sequence word in the mapped memory instead of a stream event: no event
+# marker between the update and the speculative next-superstep launch (a ~6 us launch gap per superstep,
+# profiles/gpu_tests_r5.txt); ALINK_KMEANS_HOST_POLL=0 waits on an event
+HOST_POLL = os.environ.get("ALINK_KMEANS_HOST_POLL", "1") != "0"
+HOST_POLL_TIMEOUT_S = 120.0
 _SKIP = {}      # device -> int32 [1] convergence word of the last update (speculative assign launches read it)
 
 
@@ -225,10 +230,35 @@ class _HostStat:
         if os.environ.get("ALINK_KMEANS_HOST_STAT", "1") != "0" and \
                 L.alink_kmeans_host_stat_alloc(ctypes.byref(h), ctypes.byref(d)) == 0 and d.value:
             self._hptr, self.dev_ptr = h.value, d.value
-            self._view = np.ctypeslib.as_array((ctypes.c_uint64 * 2).from_address(h.value))
+            self._view = np.ctypeslib.as_array((ctypes.c_uint64 * 3).from_address(h.value))
             self._L = L
         else:
             self.host = torch.empty(2, dtype=torch.int64, pin_memory=True)
+        self.seq = 0
+
+    def next_seq(self) -> int:
+        """Sequence number of the next update launch (0: no host poll -- the caller waits on an event)."""
+        if self._view is None or not HOST_POLL:
+            return 0
+        self.seq += 1
+        return self.seq
+
+    def wait(self, seq: int, dev) -> None:
+        """Until the update launched with ``seq`` has published its stats (a tight poll of the mapped word, then
+        20 us sleeps); past ``HOST_POLL_TIMEOUT_S`` the stream is synchronised and the word must be there."""
+        view = self._view
+        for _ in range(4000):
+            if int(view[2]) == seq:
+                return
+        import time
+        t_end = time.perf_counter() + HOST_POLL_TIMEOUT_S
+        while time.perf_counter() < t_end:
+            if int(view[2]) == seq:
+                return
+            time.sleep(20e-6)
+        torch.cuda.current_stream(dev).synchronize()
+        if int(view[2]) != seq:
+            raise RuntimeError(f"kmeans_update completed without publishing sequence {seq}")
 
     def values(self):
         if self._view is not None:
@@ -285,22 +315,28 @@ def update_centroids_hip(buf: torch.Tensor, prev: Optional[torch.Tensor], deferr
         skip = _SKIP.get(dev.index)
         if skip is None:
             skip = _SKIP[dev.index] = torch.zeros(1, dtype=torch.int32, device=dev)
+    seq = hs.next_seq()
     rc = L.alink_kmeans_update2(buf.data_ptr(), k, None if pv is None else pv.data_ptr(), C.data_ptr(),
                                 cpad.data_ptr(), ninit.data_ptr(), stat.data_ptr(), int(bool(hysteresis)),
                                 hs.dev_ptr, float(skip_tol) if skip is not None else 0.0,
-                                None if skip is None else skip.data_ptr(), _lib.stream_ptr(dev))
+                                None if skip is None else skip.data_ptr(), seq, _lib.stream_ptr(dev))
     if rc != 0:
         raise RuntimeError(f"alink_kmeans_update failed: {rc}")
     if hs.dev_ptr is None:
         hs.host.copy_(stat[:2], non_blocking=True)
-    ev = torch.cuda.Event()
-    ev.record(torch.cuda.current_stream(dev))
+    ev = None
+    if not seq:
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(dev))
     _PREPARED[dev.index] = _ckey(C)
 
     def read():
         """Wait for THIS update's 16-byte stats only (work queued after it, e.g. a speculative next-step
         kernel, keeps running) and return (max_shift or None, any_empty)."""
-        ev.synchronize()
+        if seq:
+            hs.wait(seq, dev)
+        else:
+            ev.synchronize()
         shift_bits, empty = hs.values()
         shift = float(np.frombuffer(np.int64(shift_bits).tobytes(), dtype=np.float64)[0]) if use_prev else None
         return shift, bool(empty)
