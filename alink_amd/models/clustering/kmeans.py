@@ -435,9 +435,10 @@ class KMeansUpdateCentroids(ComputeFunction):
     superstep runs with exactly these centroids (no empty-cluster compaction, not converged, not the last
     step); otherwise it is dropped — results are identical either way.  ``sync_steps``: supersteps after which
     nothing may be queued ahead (a caller that times supersteps, e.g. bench.py, synchronises there).
-    ``tol`` (the termination epsilon): the update kernel also leaves a device word "converged" (max shift < tol, no
-    empty cluster) that the queued kernel reads first, returning at once — so the run's last superstep does not pay
-    for a pass over X nobody reads.  Its result is then dropped on the host by the same test."""
+    ``tol`` (the termination epsilon): the update kernel also leaves a device word "the next superstep will not
+    use this launch" (an empty cluster, or max shift < tol) that the queued kernel reads first, returning at once —
+    so neither the compaction superstep nor the run's last one pays for a pass over X nobody reads.  Its result is
+    then dropped on the host by the same test.  An empty cluster is compacted on the host (k x 129 values)."""
 
     def __init__(self, dist_type: str, max_iter: int = 2 ** 31 - 1, sync_steps=(), speculate: bool = True,
                  tol: Optional[float] = None):
