@@ -213,7 +213,7 @@ _STAT = {}
 # profiles/gpu_tests_r5.txt); ALINK_KMEANS_HOST_POLL=0 waits on an event
 HOST_POLL = os.environ.get("ALINK_KMEANS_HOST_POLL", "1") != "0"
 HOST_POLL_TIMEOUT_S = 120.0
-_SKIP = {}      # device -> int32 [1] convergence word of the last update (speculative assign launches read it)
+_SKIP = {}      # device -> int32 [1] skip word of the last update (empty cluster or converged; speculative launches read it)
 
 
 class _HostStat:
