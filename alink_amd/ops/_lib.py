@@ -74,6 +74,7 @@ _EXTRA_SIGNATURES = {
     "alink_kmeans_assign_accum_bf16_v10d": [_c_vp, _c_i64, _c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_int, _c_vp, _c_vp,
                                             _c_int, _c_vp, _c_int, _c_d],
     "alink_kmeans_v10_grid": [_c_i64, _c_int],
+    "alink_kmeans_reduce_slabs2": [_c_vp, _c_vp, _c_int, _c_int, _c_vp, _c_vp, _c_vp],
     "alink_tree_predict": [_c_vp, _c_i64, _c_int, _c_int, _c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_int, _c_vp, _c_int,
                            _c_vp, _c_vp, _c_vp, _c_vp],
     "alink_gbdt_rank_stats": [_c_vp, _c_vp, _c_vp, _c_vp, _c_int, _c_vp, _c_int, _c_vp, _c_vp, _c_vp, _c_vp],

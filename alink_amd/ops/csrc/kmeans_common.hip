@@ -23,7 +23,11 @@ constexpr int D = 128;
 // 128-B rows), then group partials are added in group order, so the result is run-to-run deterministic.
 __global__ __launch_bounds__(256) void kmeans_reduce_slabs_kernel(const float* __restrict__ slab,
                                                                   const float* __restrict__ slab_cnt, int nslab,
-                                                                  int k, double* __restrict__ out) {
+                                                                  int k, double* __restrict__ out,
+                                                                  const unsigned* __restrict__ skip) {
+    // a skipped speculative assign launch left the slabs stale: its reduction is dropped by the host too, so it
+    // returns at once on the same word (uniform early return, before any barrier)
+    if (skip != nullptr && __hip_atomic_load(skip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return;
     __shared__ double part[8][32];
     const int c = blockIdx.x, y = blockIdx.y;
     const int d = threadIdx.x & 31, g = threadIdx.x >> 5;
@@ -217,12 +221,18 @@ int alink_kmeans_host_stat_alloc(void** host, void** dev) {
 
 int alink_kmeans_host_stat_free(void* host) { return (int)hipHostFree(host); }
 
-int alink_kmeans_reduce_slabs(const float* slab, const float* slab_cnt, int nslab, int k, double* out,
-                              void* stream) {
+// skip (nullable): the update's skip word; when nonzero at run time the reduction returns at once (out untouched)
+int alink_kmeans_reduce_slabs2(const float* slab, const float* slab_cnt, int nslab, int k, double* out,
+                               const void* skip, void* stream) {
     if (k < 1 || k > 128 || nslab < 1) return -1;
     hipLaunchKernelGGL(kmeans_reduce_slabs_kernel, dim3(k, 5), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
-                       slab, slab_cnt, nslab, k, out);
+                       slab, slab_cnt, nslab, k, out, (const unsigned*)skip);
     return (int)hipGetLastError();
+}
+
+int alink_kmeans_reduce_slabs(const float* slab, const float* slab_cnt, int nslab, int k, double* out,
+                              void* stream) {
+    return alink_kmeans_reduce_slabs2(slab, slab_cnt, nslab, k, out, nullptr, stream);
 }
 
 int alink_kmeans_prep_centroids(const double* C, int k, void* cpad, float* ninit, void* stream) {

@@ -174,8 +174,10 @@ def assign_accumulate_hip(X: torch.Tensor, C: torch.Tensor, grid: Optional[int] 
     grid = _GRID[gkey]
     key = (dev.index, grid)
     if key not in _BUF:
-        _BUF[key] = (torch.empty((grid, HIP_KMAX, HIP_D), dtype=torch.float32, device=dev),
-                     torch.empty((grid, HIP_KMAX), dtype=torch.float32, device=dev))
+        # zeroed once: the kernels write only the first 16*ceil(k/16) rows of a slab, so the tail would otherwise
+        # hold whatever the allocator recycled (NaN bit patterns included)
+        _BUF[key] = (torch.zeros((grid, HIP_KMAX, HIP_D), dtype=torch.float32, device=dev),
+                     torch.zeros((grid, HIP_KMAX), dtype=torch.float32, device=dev))
     slab, slab_cnt = _BUF[key]
     out = torch.empty((k, HIP_D + 1), dtype=torch.float64, device=dev)
     st = _lib.stream_ptr(dev)
@@ -183,7 +185,8 @@ def assign_accumulate_hip(X: torch.Tensor, C: torch.Tensor, grid: Optional[int] 
         mode |= (V7_VAR << 4) if ver == "v7" else (V10_FLAGS << 4)
     if reverse and ver == "v10":
         mode |= 32
-    if skip is not None and ver == "v10" and V10_POOL <= 0:
+    skipped = skip is not None and ver == "v10" and V10_POOL <= 0
+    if skipped:
         rc = L.alink_kmeans_assign_accum_bf16_v10s(
             X.data_ptr(), n, cpad.data_ptr(), ninit.data_ptr(), k, slab.data_ptr(), slab_cnt.data_ptr(), grid, st,
             None if assign_out is None else assign_out.data_ptr(), int(mode), skip.data_ptr())
@@ -201,7 +204,12 @@ def assign_accumulate_hip(X: torch.Tensor, C: torch.Tensor, grid: Optional[int] 
             None if assign_out is None else assign_out.data_ptr(), int(mode))
     if rc != 0:
         raise RuntimeError(f"alink_kmeans_assign_accum_bf16_{ver} failed: {rc}")
-    rc = L.alink_kmeans_reduce_slabs(slab.data_ptr(), slab_cnt.data_ptr(), grid, k, out.data_ptr(), st)
+    if skipped and hasattr(L, "alink_kmeans_reduce_slabs2"):
+        # the reduction reads the same skip word: a skipped launch costs two empty kernels, not a slab pass
+        rc = L.alink_kmeans_reduce_slabs2(slab.data_ptr(), slab_cnt.data_ptr(), grid, k, out.data_ptr(),
+                                          skip.data_ptr(), st)
+    else:
+        rc = L.alink_kmeans_reduce_slabs(slab.data_ptr(), slab_cnt.data_ptr(), grid, k, out.data_ptr(), st)
     if rc != 0:
         raise RuntimeError(f"alink_kmeans_reduce_slabs failed: {rc}")
     return out

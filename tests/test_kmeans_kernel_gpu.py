@@ -338,10 +338,42 @@ def test_update_convergence_word_and_skipped_assign():
     assert empty and int(read.skip.item()) == 1
     _, read = K.update_centroids_hip(buf, prev, deferred=True, hysteresis=False, skip_tol=1e9)
     read()
-    slab = [t.clone() for pair in K._BUF.values() for t in pair]
-    K.assign_accumulate_hip(X, Cn, skip=read.skip)
+    # bitwise comparison (int32 views): a slab row the kernel never writes (rows >= 16*ceil(k/16)) may hold a NaN
+    # pattern, and torch.equal(NaN, NaN) is False even when nothing changed -- the round-5 driver failure
+    # (profiles/kmeans_skip_r6.txt).  The slabs are zeroed at allocation now, but the check must not rest on that.
+    slab = [t.view(torch.int32).clone() for pair in K._BUF.values() for t in pair]
+    out = K.assign_accumulate_hip(X, Cn, skip=read.skip)
     torch.cuda.synchronize()
-    assert all(torch.equal(a, b) for a, b in zip(slab, [t for pair in K._BUF.values() for t in pair]))
+    after = [t.view(torch.int32) for pair in K._BUF.values() for t in pair]
+    for a, b in zip(slab, after):
+        diff = (a != b).nonzero()
+        assert diff.numel() == 0, f"skipped launch wrote {diff.shape[0]} slab words, first at {diff[0].tolist()}"
+    # the reduction reads the same word: a poisoned output buffer stays poisoned
+    poison = torch.full((60, 129), 7.0, dtype=torch.float64, device="cuda")
+    L = K._lib.require()
+    key = next(iter(K._BUF))
+    s, sc = K._BUF[key]
+    assert L.alink_kmeans_reduce_slabs2(s.data_ptr(), sc.data_ptr(), key[1], 60, poison.data_ptr(),
+                                        read.skip.data_ptr(), K._lib.stream_ptr(poison.device)) == 0
+    torch.cuda.synchronize()
+    assert bool((poison == 7.0).all()) and out.shape == (60, 129)
+
+
+def test_slab_tail_nan_garbage_is_not_a_write():
+    """The round-5 failure mode, reproduced deliberately: NaN bits in the never-written tail of a slab make
+    torch.equal report a change although no word changed; the bitwise view does not."""
+    from alink_amd.ops import kmeans as K
+    X, C = _data(20_011, 60, seed=4)
+    K.assign_accumulate_hip(X, C)
+    grid = K._GRID[(K.kernel_version(60), X.shape[0], None, X.device.index)]
+    s, _ = K._BUF[(X.device.index, grid)]
+    s[:, 64:].fill_(float("nan"))           # rows >= 16*ceil(60/16) = 64 are never written by v10 for k = 60
+    before = s.clone()
+    K.assign_accumulate_hip(X, C)
+    torch.cuda.synchronize()
+    assert not torch.equal(before, s)        # NaN != NaN
+    assert torch.equal(before[:, 64:].view(torch.int32), s[:, 64:].view(torch.int32))
+    s[:, 64:].zero_()
 
 
 def test_fused_update_host_compaction_equals_generic_path(monkeypatch):

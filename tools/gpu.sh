@@ -3,7 +3,7 @@
 # under its own time limit, logs under gpurun_out/, prints a one-line verdict, and exits non-zero on failure
 # so steps chain with &&:
 #
-#   tools/gpu.sh tests [PYTEST_PATHS_OR_ARGS...]       pytest -m gpu (default: tests/)
+#   tools/gpu.sh tests [PYTEST_PATHS_OR_ARGS...]       pytest -m gpu (default: tests/; XOPT= runs past failures)
 #   tools/gpu.sh smoke                                 __graft_entry__.smoke()
 #   tools/gpu.sh bench [BENCH_ARGS...]                 bench.py, JSON line -> gpurun_out/bench.json
 #   tools/gpu.sh run NAME SECONDS CMD...               any python command, log gpurun_out/NAME.log
@@ -19,7 +19,7 @@ case "$step" in
   tests)
     tag=${TAG:-gpu}
     [ $# -eq 0 ] && set -- tests/
-    cd "$R" && timeout -k 10 ${LIMIT:-900} python -u -m pytest "$@" -x -q -m gpu --timeout 120 --timeout-method thread \
+    cd "$R" && timeout -k 10 ${LIMIT:-900} python -u -m pytest "$@" ${XOPT--x} -q -m gpu --timeout 120 --timeout-method thread \
       > "$O/pytest_$tag.log" 2>&1 && { echo "TESTS_OK $(tail -1 "$O/pytest_$tag.log")"; } \
       || { tail -40 "$O/pytest_$tag.log"; exit 1; } ;;
   smoke)
