@@ -8,7 +8,7 @@ from .modelinfo import FmModelInfoBatchOp, WithModelInfoBatchOp
 from ..base import BatchOperator
 from .utils import ModelMapBatchOp
 
-__all__ = ["FmClassifierTrainBatchOp", "FmClassifierPredictBatchOp", "FmRegressorTrainBatchOp",
+__all__ = ["FmTrainBatchOp", "FmPredictBatchOp", "FmClassifierTrainBatchOp", "FmClassifierPredictBatchOp", "FmRegressorTrainBatchOp",
            "FmRegressorPredictBatchOp", "NaiveBayesTextTrainBatchOp", "NaiveBayesTextPredictBatchOp", "MultilayerPerceptronTrainBatchOp",
            "MultilayerPerceptronPredictBatchOp"]
 
@@ -84,4 +84,44 @@ class FmClassifierPredictBatchOp(ModelMapBatchOp):
 
 
 class FmRegressorPredictBatchOp(ModelMapBatchOp):
+    MAPPER = _FM.FmModelMapper
+
+
+_FM_TASKS = {"BINARY_CLASSIFICATION": "BINARY_CLASSIFICATION", "CLASSIFICATION": "BINARY_CLASSIFICATION",
+             "REGRESSION": "REGRESSION"}
+
+
+class FmTrainBatchOp(_FmTrainBatchOp):
+    """The public generic FM trainer (``A/operator/common/fm/FmTrainBatchOp.java:17``): the task is a constructor
+    argument / the ``task`` param (``ModelParamName.TASK``; "binary_classification" or "regression", case-insensitive
+    as ``Task.valueOf(...toUpperCase())`` at ``BaseFmTrainBatchOp.java:99``).  Same trainer as the classifier /
+    regressor ops, so the models are identical to theirs for the same task."""
+    _NO_AUTO_PARAMS = True
+    from ...params import op_params as _op_params
+    from ...common.params import ParamInfo as _ParamInfo
+    PARAMS = _op_params("FmRegressorTrainBatchOp") + [
+        _ParamInfo("task", str, "FM task: binary_classification or regression (ModelParamName.TASK).", default=None)]
+    del _op_params, _ParamInfo
+
+    def __init__(self, params=None, task=None, **kwargs):
+        if isinstance(params, str) and task is None:       # FmTrainBatchOp("regression")
+            params, task = None, params
+        super().__init__(params, **kwargs)
+        if task is not None:
+            self.getParams().set("task", task)
+
+    @property
+    def TASK(self):
+        t = self.getParams().get("task") if self.getParams().contains("task") else None
+        if t is None:
+            raise ValueError("FmTrainBatchOp needs a task: binary_classification or regression")
+        key = str(t).upper()
+        if key not in _FM_TASKS:
+            raise ValueError(f"unknown FM task {t!r}")
+        return _FM_TASKS[key]
+
+
+class FmPredictBatchOp(ModelMapBatchOp):
+    """``A/operator/common/fm/FmPredictBatchOp.java:12``: a ModelMapBatchOp over ``FmModelMapper`` (the task comes
+    from the model's meta, so one op serves both tasks)."""
     MAPPER = _FM.FmModelMapper

@@ -44,3 +44,31 @@ def test_fm_classifier_detail_and_model_format():
     m = FmModelDataConverter(Types.STRING).load(model.collect())
     assert m.task == "BINARY_CLASSIFICATION" and m.labelValues[0] == "b" and m.dim == [1, 1, 4]
     assert len(m.fmModel.factors) == 3 and len(m.fmModel.factors[0]) == 4
+
+
+def test_generic_fm_ops_equal_task_specific_ops():
+    """FmTrainBatchOp(task) / FmPredictBatchOp (A/operator/common/fm/FmTrainBatchOp.java:17, FmPredictBatchOp.java:12)
+    train the same model as the classifier / regressor ops and predict the same rows."""
+    import pytest
+    X = _data(400, seed=3)
+    y = np.where(X[:, 0] * X[:, 1] > 0, "p", "n")
+    yr = X[:, 0] * X[:, 1] + 0.5 * X[:, 2]
+    src = MemSourceBatchOp([(" ".join(map(str, x)), str(a), float(b)) for x, a, b in zip(X.tolist(), y, yr)],
+                           "vec string, label string, y double")
+    for task, spec_cls, label in (("binary_classification", FmClassifierTrainBatchOp, "label"),
+                                  ("REGRESSION", FmRegressorTrainBatchOp, "y")):
+        def conf(op):
+            return op.setVectorCol("vec").setLabelCol(label).setNumEpochs(5).setNumFactor(3).setLearnRate(0.05)
+        a = src.link(conf(FmTrainBatchOp(task)))
+        b = src.link(conf(spec_cls()))
+        assert a.collect() == b.collect()
+        pa = FmPredictBatchOp().setPredictionCol("p").linkFrom(a, src).collect()
+        pb = (FmClassifierPredictBatchOp() if label == "label" else FmRegressorPredictBatchOp()) \
+            .setPredictionCol("p").linkFrom(b, src).collect()
+        assert pa == pb
+    c = src.link(FmTrainBatchOp().setTask("regression").setVectorCol("vec").setLabelCol("y").setNumEpochs(5)
+                 .setNumFactor(3).setLearnRate(0.05))
+    assert c.collect() == src.link(FmRegressorTrainBatchOp().setVectorCol("vec").setLabelCol("y").setNumEpochs(5)
+                                   .setNumFactor(3).setLearnRate(0.05)).collect()
+    with pytest.raises(ValueError):
+        src.link(FmTrainBatchOp().setVectorCol("vec").setLabelCol("y"))
