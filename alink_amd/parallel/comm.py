@@ -368,25 +368,48 @@ def all_reduce_coalesced(ts: List[torch.Tensor], op: str = "sum") -> List[torch.
     return ts
 
 
+def scatter_block(n: int, ws: int, r: int):
+    """Rows ``[lo, hi)`` of dim 0 that rank ``r`` owns after a reduce-scatter of ``n`` rows over ``ws`` ranks:
+    blocks of ``ceil(n / ws)`` rows in rank order, the last ones shorter (possibly empty) when ``ws`` does not
+    divide ``n``."""
+    b = -(-n // ws)
+    lo = min(n, r * b)
+    return lo, min(n, lo + b)
+
+
+def _rs_padded(t: torch.Tensor, ws: int) -> torch.Tensor:
+    """``t`` zero-padded along dim 0 to a multiple of ``ws`` (the padding only ever lands in rows no rank keeps)."""
+    n = t.shape[0]
+    b = -(-n // ws)
+    if b * ws == n:
+        return t.contiguous()
+    pad = torch.zeros((b * ws - n,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+    return torch.cat([t, pad], 0)
+
+
 @_collective
 def reduce_scatter(t: torch.Tensor, op: str = "sum") -> torch.Tensor:
-    """Reduce-scatter along dim 0 (t.shape[0] must divide world size); returns this rank's block."""
+    """Reduce-scatter along dim 0; returns this rank's block ``scatter_block(t.shape[0], ws, rank)`` — any row
+    count works: a non-divisible buffer is zero-padded to a multiple of the world size and the padding is cut
+    off again, never silently dropping the remainder rows."""
     ws = get_world_size()
     if not is_distributed():
         return t
     rop = getattr(dist.ReduceOp, _OPS[op.lower()])
-    out = torch.empty((t.shape[0] // ws,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+    n = t.shape[0]
+    lo, hi = scatter_block(n, ws, get_rank())
+    b = -(-n // ws)
     STATS.calls += 1
     STATS.bytes += t.numel() * t.element_size()
     if _backend() == "nccl":
-        d = (t if t.is_cuda else t.to(device_for_rank())).contiguous()
-        o = out if t.is_cuda else torch.empty(out.shape, dtype=t.dtype, device=d.device)
+        d = _rs_padded(t if t.is_cuda else t.to(device_for_rank()), ws)
+        o = torch.empty((b,) + tuple(t.shape[1:]), dtype=t.dtype, device=d.device)
         _on_comm_stream(d.device, [d, o], lambda: dist.reduce_scatter_tensor(o, d, op=rop))
-        return out if t.is_cuda else o.cpu()
+        o = o[:hi - lo]
+        return o if t.is_cuda else o.cpu()
     full = t.clone()
     all_reduce(full, op)
-    r = get_rank()
-    return full[r * out.shape[0]:(r + 1) * out.shape[0]].clone()
+    return full[lo:hi].clone()
 
 
 def _wait_event(dev, ev, x):
@@ -421,31 +444,33 @@ class Pending:
 
 
 def reduce_scatter_async(t: torch.Tensor, op: str = "sum") -> Pending:
-    """Asynchronous ``reduce_scatter`` (dim 0 split over ranks): returns a ``Pending`` whose ``wait()`` yields
-    this rank's block.  Used to overlap per-block histogram reductions with building the next block."""
+    """Asynchronous ``reduce_scatter`` (dim 0 split over ranks as ``scatter_block``; any row count): returns a
+    ``Pending`` whose ``wait()`` yields this rank's block.  Used to overlap per-block histogram reductions with building the next block."""
     ws = get_world_size()
     if not is_distributed():
         return Pending(t)
     rop = getattr(dist.ReduceOp, _OPS[op.lower()])
     STATS.calls += 1
     STATS.bytes += t.numel() * t.element_size()
-    rows = t.shape[0] // ws
+    n = t.shape[0]
+    lo, hi = scatter_block(n, ws, get_rank())
+    rows = -(-n // ws)
     if _backend() == "nccl":
-        d = (t if t.is_cuda else t.to(device_for_rank())).contiguous()
-        o = torch.empty((rows,) + tuple(t.shape[1:]), dtype=t.dtype, device=d.device)
+        d = _rs_padded(t if t.is_cuda else t.to(device_for_rank()), ws)
+        o_full = torch.empty((rows,) + tuple(t.shape[1:]), dtype=t.dtype, device=d.device)
+        o = o_full[:hi - lo]
 
         def issue():
-            w = dist.reduce_scatter_tensor(o, d, op=rop, async_op=True)
+            w = dist.reduce_scatter_tensor(o_full, d, op=rop, async_op=True)
             w.wait()                         # comm stream waits on RCCL's stream (no host block)
-        _, done = _on_comm_stream(d.device, [d, o], issue, wait_now=False)
+        _, done = _on_comm_stream(d.device, [d, o_full], issue, wait_now=False)
         dev = d.device
         return Pending(o, None, (lambda x: _wait_event(dev, done, x)) if t.is_cuda else
                        (lambda x: _wait_event(dev, done, x).cpu()), keep=(d,))
     full = t.detach().cpu().clone()
     work = dist.all_reduce(full, op=rop, async_op=True)
-    r = get_rank()
     dev = t.device
-    return Pending(full, work, lambda x: x[r * rows:(r + 1) * rows].clone().to(dev))
+    return Pending(full, work, lambda x: x[lo:hi].clone().to(dev))
 
 
 def all_reduce_async(t: torch.Tensor, op: str = "sum") -> Pending:

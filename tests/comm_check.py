@@ -83,6 +83,20 @@ def checks(out):
         ok(f"reduce_scatter.{where}", close(got, want) and got.device.type == src.device.type)
         got = comm.reduce_scatter_async(src.clone()).wait()
         ok(f"reduce_scatter_async.{where}", close(got, want) and got.device.type == src.device.type)
+    # non-divisible dim 0: blocks of ceil(n / ws) rows, the last ones shorter or empty, no row dropped
+    for n in (ws * 5 + 2, ws + 1):
+        full = [_x(r, n * 3, torch.float64, 6).view(n, 3) for r in range(ws)]
+        lo, hi = comm.scatter_block(n, ws, me)
+        want = _fold(full, "sum")[lo:hi]
+        for where in ("dev", "host"):
+            src = full[me].clone() if where == "host" else full[me].to(dev)
+            got = comm.reduce_scatter(src)
+            ok(f"reduce_scatter.uneven{n}.{where}", got.shape == want.shape and close(got, want))
+            got = comm.reduce_scatter_async(src.clone()).wait()
+            ok(f"reduce_scatter_async.uneven{n}.{where}", got.shape == want.shape and close(got, want))
+        blocks = comm.all_gather_object((lo, hi))
+        ok(f"reduce_scatter.uneven{n}.cover", [b for blk in blocks for b in blk][0] == 0 and blocks[-1][1] == n
+           and all(blocks[i][1] == blocks[i + 1][0] for i in range(ws - 1)))
     mx = [_x(r, ws * 4, torch.float32, 3).view(ws * 4, 1) for r in range(ws)]
     got = comm.reduce_scatter(mx[me].to(dev), "max")
     ok("reduce_scatter.max", close(got, _fold(mx, "max")[me * 4:(me + 1) * 4], 1e-6))
