@@ -136,6 +136,55 @@ def kernel_version(k: int = 100) -> str:
 _CUS: Dict[int, int] = {}
 _GRID: Dict[Tuple, int] = {}
 
+# per-rank assign time (bench.py's straggler split): while on, every assign+accumulate call is bracketed by HIP
+# events on the caller's stream (GPU) or timed on the host (CPU paths)
+_KT = {"on": False, "ev": [], "host_s": 0.0, "n": 0}
+
+
+def kernel_timing(on: bool) -> None:
+    """Start / stop recording the device time of every assign+accumulate call (events are collected later)."""
+    _KT["on"] = bool(on)
+
+
+def kernel_timing_collect() -> Tuple[int, float]:
+    """(calls, seconds) of the assign+accumulate work recorded since the last collect (synchronises the events)."""
+    n, sec = _KT["n"], _KT["host_s"]
+    for a, b in _KT["ev"]:
+        b.synchronize()
+        sec += a.elapsed_time(b) * 1e-3
+    _KT.update(ev=[], host_s=0.0, n=0)
+    return n, sec
+
+
+class _timed:
+    """Bracket one assign+accumulate call when ``kernel_timing`` is on (no-op otherwise)."""
+    __slots__ = ("dev", "e0", "t0")
+
+    def __init__(self, dev):
+        self.dev = dev if _KT["on"] else None
+
+    def __enter__(self):
+        if self.dev is not None:
+            if self.dev.type == "cuda":
+                self.e0 = torch.cuda.Event(enable_timing=True)
+                self.e0.record(torch.cuda.current_stream(self.dev))
+            else:
+                import time
+                self.t0 = time.perf_counter()
+        return self
+
+    def __exit__(self, *exc):
+        if self.dev is not None:
+            _KT["n"] += 1
+            if self.dev.type == "cuda":
+                e1 = torch.cuda.Event(enable_timing=True)
+                e1.record(torch.cuda.current_stream(self.dev))
+                _KT["ev"].append((self.e0, e1))
+            else:
+                import time
+                _KT["host_s"] += time.perf_counter() - self.t0
+        return False
+
 
 def _num_cus(device) -> int:
     idx = torch.device(device).index or 0
@@ -147,6 +196,13 @@ def _num_cus(device) -> int:
 def assign_accumulate_hip(X: torch.Tensor, C: torch.Tensor, grid: Optional[int] = None,
                           assign_out: Optional[torch.Tensor] = None, mode: int = 0,
                           reverse: bool = False, skip: Optional[torch.Tensor] = None) -> torch.Tensor:
+    with _timed(X.device):
+        return _assign_accumulate_hip(X, C, grid, assign_out, mode, reverse, skip)
+
+
+def _assign_accumulate_hip(X: torch.Tensor, C: torch.Tensor, grid: Optional[int] = None,
+                           assign_out: Optional[torch.Tensor] = None, mode: int = 0,
+                           reverse: bool = False, skip: Optional[torch.Tensor] = None) -> torch.Tensor:
     """[k, d+1] fp64 sums|counts of this rank's rows (``csrc/kmeans_v10.hip`` for k <= 112, else
     ``csrc/kmeans_v7.hip``: role-split waves on 16x16x32 MFMA, LDS-DMA tile ring; ``kernel_version``).
     ``assign_out`` (int32 [N]) also receives every row's centroid id; ``mode`` 1/2 are the kernel's load-only /
@@ -603,11 +659,12 @@ def assign_accumulate(X: torch.Tensor, C: torch.Tensor, weights: Optional[torch.
     hip_ok = _lib.available() or not _lib.torch_fallback_allowed()
     if weights is None and hip_supported(X, C.shape[0]) and hip_ok:
         return assign_accumulate_hip(X, C, reverse=reverse)
-    if general_supported(X, C.shape[0]) and hip_ok:
-        return assign_accumulate_general_hip(X, C, weights)
-    if f32_supported(X, C.shape[0]) and hip_ok:
-        return assign_accumulate_f32_hip(X, C, weights)
-    return assign_accumulate_torch(X, C, weights)
+    with _timed(X.device):
+        if general_supported(X, C.shape[0]) and hip_ok:
+            return assign_accumulate_general_hip(X, C, weights)
+        if f32_supported(X, C.shape[0]) and hip_ok:
+            return assign_accumulate_f32_hip(X, C, weights)
+        return assign_accumulate_torch(X, C, weights)
 
 
 def assign(X: torch.Tensor, C: torch.Tensor, chunk: int = 1 << 20) -> Tuple[torch.Tensor, torch.Tensor]:

@@ -26,6 +26,16 @@ Communication fields: ``comm_backend`` (nccl = RCCL, gloo, or none for a 1-rank 
 superstep's collectives, event-timed on the compute stream, i.e. including the wait for the slowest rank) and
 ``allreduce_calls_per_step``.  ``ALINK_COMM_FORCE_COLLECTIVE=1`` makes a 1-rank job run its collectives for
 real (the RCCL path of a multi-GPU job, on one GPU).
+
+Straggler split: ``assign_ms_per_step_{max,min}`` are the max / min over ranks of the assign+accumulate device time
+per timed superstep (HIP events around the fused kernel and its slab reduction), ``assign_ms_per_step_by_rank`` the
+per-rank values and ``straggler_ms_per_step`` their spread — so a multi-GPU step time splits into the slowest
+rank's kernel, the wait for it (inside ``allreduce_us_per_step``) and the collective itself.
+
+Telemetry (``--telemetry 1``, default on a GPU): an ``amdsmi`` sampling thread (``alink_amd/utils/telemetry.py``)
+records gfx / memory clocks, socket power and temperatures every 5 ms; ``telemetry`` holds per-phase min / median /
+max (data generation, warm-up, timed window, convergence runs) and the throttle-residency deltas of rank 0, plus
+every rank's timed-window medians.  ``ALINK_TELEMETRY_OUT=path`` also writes rank 0's raw series there.
 """
 from __future__ import annotations
 
@@ -73,6 +83,7 @@ def main():
     ap.add_argument("--timeout", type=float, default=1500.0, help="self-launched job time limit (s)")
     ap.add_argument("--convergence-first", type=int, default=0,
                     help="1: the untimed convergence runs before the timed run (0: after it)")
+    ap.add_argument("--telemetry", type=int, default=1, help="1: sample GPU clocks / power (amdsmi) during the run")
     a = ap.parse_args()
 
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -93,6 +104,15 @@ def main():
     if dev.type == "cuda":
         _lib.require()
 
+    tel = None
+    if dev.type == "cuda" and a.telemetry:
+        from alink_amd.utils.telemetry import GpuTelemetry
+        tel = GpuTelemetry(dev).start()
+
+    def mark(name):
+        if tel is not None:
+            tel.mark(name)
+
     src = RandomVectorSourceBatchOp().setNumRows(a.rows).setSize(a.dims).setNumClusters(a.k) \
         .setClusterStd(1.0).setCenterScale(4.0).setDtype("bf16").setSeed(2024).setOutputCol("vec")
     t_gen = time.perf_counter()
@@ -100,6 +120,7 @@ def main():
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
     t_gen = time.perf_counter() - t_gen
+    mark("datagen_end")
 
     from alink_amd.operator.batch.source import TableSourceBatchOp
 
@@ -146,11 +167,16 @@ def main():
                 torch.cuda.synchronize(dev)
             marks[step] = time.perf_counter()
             if step == a.warmup:
+                mark("window_start")
                 comm.device_timing_collect()                  # drop warmup events
+                kops.kernel_timing_collect()
                 marks["oneshot0"] = comm.STATS.oneshot
                 comm.device_timing(dev.type == "cuda")
+                kops.kernel_timing(True)
             else:
+                mark("window_end")
                 comm.device_timing(False)
+                kops.kernel_timing(False)
 
     op = KMeansTrainBatchOp().setVectorCol("vec").setK(a.k).setMaxIter(a.warmup + a.steps).setEpsilon(-1.0)
     op._on_step = on_step
@@ -165,6 +191,9 @@ def main():
     elapsed = marks[a.warmup + a.steps] - marks[a.warmup]
     el = torch.tensor([elapsed], dtype=torch.float64)
     n_ev, dev_comm_s, _ = comm.device_timing_collect()
+    n_kt, kern_s = kops.kernel_timing_collect()
+    mark("timed_run_end")
+    kern_by_rank = [float(v) for v in comm.all_gather_object(kern_s / a.steps * 1e3)]
     oneshot_calls = comm.STATS.oneshot - marks.get("oneshot0", comm.STATS.oneshot)
     comm_backend = comm._backend() if comm.is_distributed() else "none"
     el_max = el.clone()
@@ -180,6 +209,21 @@ def main():
 
     if not a.convergence_first:
         iters, conv = convergence_runs()
+    mark("convergence_end")
+    telemetry = None
+    if tel is not None:
+        tel.stop()
+        telemetry = tel.summary()
+        out_path = os.environ.get("ALINK_TELEMETRY_OUT")
+        if out_path and env.rank == 0:
+            with open(out_path, "w") as f:
+                json.dump({"summary": telemetry, "series": tel.series(),
+                           "columns": ["t_s", "gfxclk_min_mhz", "gfxclk_max_mhz", "uclk_mhz", "socket_power_w",
+                                       "hotspot_c", "hbm_c"]}, f)
+    win = (telemetry or {}).get("phases", {}).get("window_start->window_end", {})
+    per_rank_win = comm.all_gather_object({k: v.get("median") for k, v in win.items() if isinstance(v, dict)})
+    if telemetry is not None:
+        telemetry["window_median_by_rank"] = per_rank_win
 
     rows_per_s = a.rows * a.steps / elapsed
     res = {
@@ -216,9 +260,16 @@ def main():
         "allreduce_us_per_step": dev_comm_s / a.steps * 1e6,
         "allreduce_calls_per_step": n_ev / a.steps,
         "allreduce_bytes_per_step": comm_bytes,
+        "assign_ms_per_step_max": max(kern_by_rank),
+        "assign_ms_per_step_min": min(kern_by_rank),
+        "assign_ms_per_step_by_rank": kern_by_rank,
+        "straggler_ms_per_step": max(kern_by_rank) - min(kern_by_rank),
+        "assign_calls_timed": n_kt,
         "hip_kernels": bool(hip_used),
         "datagen_s": t_gen,
         "train_wall_s": t_tot,
+        "telemetry": telemetry if telemetry is not None else {"available": False,
+                                                              "error": "disabled" if dev.type == "cuda" else "cpu"},
     }
     if env.rank == 0:
         print(json.dumps(res), flush=True)

@@ -82,6 +82,13 @@ def test_bench_self_launches_eight_ranks_like_the_driver():
     res = _bench(8, ["--rows", "40003", "--converge-iters", "20"])
     assert res["n_gpus"] == 8 and res["config"]["parallelism"] == "dp8"
     assert res["effective_config"]["rows_per_rank"] == 40003 // 8
+    # straggler split: every rank's timed assign time, max / min / spread consistent with them
+    by = res["assign_ms_per_step_by_rank"]
+    assert len(by) == 8 and all(v > 0 for v in by)
+    assert res["assign_ms_per_step_max"] == max(by) and res["assign_ms_per_step_min"] == min(by)
+    assert abs(res["straggler_ms_per_step"] - (max(by) - min(by))) < 1e-9
+    assert res["assign_calls_timed"] == res["steps"]
+    assert res["telemetry"]["available"] is False
     assert res["allreduce_bytes_per_step"] == res["live_k"] * (128 + 1) * 8
     assert 1 <= res["iters_to_converge"] <= 20 and res["convergence"]["reference"]["sse"] > 0
 
