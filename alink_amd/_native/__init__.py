@@ -14,7 +14,8 @@ import numpy as np
 __all__ = ["lib", "parse_csv_lines", "murmur3_utf16", "murmur3_bytes", "murmur3_utf8", "parse_dense_vectors", "ftrl_update_csr",
            "ftrl_partial_margin", "ftrl_shard_update", "parse_binary_detail", "java_double_join",
            "java_double_rows", "java_double_rows_packed", "parse_csv_packed",
-           "parse_dense_vectors_packed", "parse_kv_packed", "parse_json_flat_packed", "java_double_rows_fmt", "sample_thresholds", "gbdt_rank_grad"]
+           "parse_dense_vectors_packed", "parse_kv_packed", "parse_json_flat_packed", "java_double_rows_fmt", "sample_thresholds", "gbdt_rank_grad",
+           "tree_flatten"]
 
 # ALINK_NATIVE_LIB points at another build of the same sources (e.g. the AddressSanitizer build of
 # tools/asan_host.py)
@@ -50,6 +51,9 @@ if os.path.exists(_PATH):
             lib.alink_json_flat_parse.restype = ctypes.c_int64
         if hasattr(lib, "alink_gbdt_rank_grad_host"):
             lib.alink_gbdt_rank_grad_host.restype = ctypes.c_int
+        if hasattr(lib, "alink_tree_flatten"):
+            lib.alink_tree_scan.restype = ctypes.c_int64
+            lib.alink_tree_flatten.restype = ctypes.c_int64
     except OSError:
         lib = None
 
@@ -449,3 +453,36 @@ def ftrl_shard_update(indptr, indices, values, err, w, n, z, lo, hi, alpha, beta
                                 ctypes.c_int64(len(indptr) - 1), _ptr(w), _ptr(n), _ptr(z), ctypes.c_int64(lo),
                                 ctypes.c_int64(hi), ctypes.c_double(alpha), ctypes.c_double(beta),
                                 ctypes.c_double(l1), ctypes.c_double(l2))
+
+
+def tree_flatten(strings: Sequence[str], tree_lo: Sequence[int]):
+    """Tree-model node strings (``TreeModelDataConverter`` rows; tree t = strings[tree_lo[t]:tree_lo[t+1]]) parsed
+    straight into flat arrays by ``csrc/tree_model.cpp``: dict of feat / thr / first / nchild / wsum / dist
+    [n, max_dist] / dist_len / cat_len / cat_off / cat (int32 values), or None (library missing, or a row outside
+    the serializer's form -- the caller takes the generic JSON path)."""
+    if lib is None or getattr(lib, "alink_tree_flatten", None) is None:
+        return None
+    data, off = _pack_utf8(strings)
+    buf = np.frombuffer(data, dtype=np.uint8) if data else np.zeros(1, np.uint8)
+    n = len(strings)
+    lo = np.ascontiguousarray(tree_lo, dtype=np.int64)
+    nd, ncat = 4, 1024          # first guess (GBDT leaves hold 1 value, classifiers one per label)
+    md, ct = ctypes.c_int64(0), ctypes.c_int64(0)
+    for _ in range(2):
+        out = {"feat": np.empty(n, np.int32), "thr": np.empty(n, np.float64), "first": np.empty(n, np.int32),
+               "nchild": np.empty(n, np.int32), "wsum": np.empty(n, np.float64),
+               "dist": np.empty((n, nd), np.float64), "dist_len": np.empty(n, np.int32),
+               "cat_len": np.empty(n, np.int32), "cat_off": np.empty(n, np.int64), "cat": np.empty(ncat, np.int32)}
+        rc = lib.alink_tree_flatten(_ptr(buf), _ptr(off), ctypes.c_int64(n), _ptr(lo), ctypes.c_int64(len(lo) - 1),
+                                    ctypes.c_int64(nd), _ptr(out["feat"]), _ptr(out["thr"]), _ptr(out["first"]),
+                                    _ptr(out["nchild"]), _ptr(out["wsum"]), _ptr(out["dist"]),
+                                    _ptr(out["dist_len"]), _ptr(out["cat_len"]), _ptr(out["cat_off"]),
+                                    _ptr(out["cat"]), ctypes.c_int64(ncat), ctypes.byref(md), ctypes.byref(ct))
+        if rc != -2:
+            break
+        nd, ncat = max(1, int(md.value)), max(1, int(ct.value))
+    if rc != 0:
+        return None
+    out["dist"] = out["dist"][:, :max(1, int(md.value))]
+    out["max_dist"] = int(md.value)
+    return out

@@ -245,7 +245,7 @@ class BroadcastModelSource(ModelSource):
         return self._full
 
     def getModelRows(self):
-        return self._get().rows()
+        return self._get().lazy_rows()
 
     def getSchema(self):
         return self._mt.schema

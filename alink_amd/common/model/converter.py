@@ -16,7 +16,9 @@ from __future__ import annotations
 from typing import Any, Iterable, List, Optional, Sequence, Tuple
 
 from ..params import Params
-from ..table import MTable, Row
+import numpy as np
+
+from ..table import LazyRows, MTable, Row
 from ..types import AlinkType, TableSchema, Types
 
 __all__ = ["SEGMENT_SIZE", "MAX_NUM_SLICES", "get_model_id", "get_string_index", "append_meta_rows",
@@ -83,7 +85,43 @@ def _ordered(rows: Sequence[Sequence[Any]]):
     return sorted(rows, key=lambda r: int(r[0]))
 
 
+def _lazy_order(rows: LazyRows):
+    """(stable sort order by model_id, string index per sorted row) of a columnar model table, or None."""
+    ids = rows.int_column(0) if rows.width >= 2 else None
+    if ids is None:
+        return None
+    order = np.argsort(ids, kind="stable")
+    return order, ids[order] // MAX_NUM_SLICES
+
+
+def _extract_meta_and_data_lazy(rows: LazyRows):
+    got = _lazy_order(rows)
+    if got is None:
+        return None
+    order, sid = got
+    info = rows.column(1)
+    meta_idx = order[sid == 0]
+    sel = (sid != 0) & (sid != AUX_STRING_INDEX)
+    idx, ks = order[sel], sid[sel]
+    keep = [k for k, i in enumerate(idx.tolist()) if info[i] is not None]
+    if len(keep) != idx.size:
+        idx, ks = idx[keep], ks[keep]
+    il = idx.tolist()
+    if ks.size <= 1 or bool(np.all(ks[1:] != ks[:-1])):
+        data = [info[i] for i in il]                         # one slice per string: no joins
+    else:
+        cut = [0] + (np.flatnonzero(ks[1:] != ks[:-1]) + 1).tolist() + [ks.size]
+        data = ["".join(info[i] for i in il[a:b]) for a, b in zip(cut[:-1], cut[1:])]
+    meta_segs = [info[i] for i in meta_idx.tolist() if info[i] is not None]
+    meta = Params.fromJson("".join(meta_segs)) if meta_segs else Params()
+    return meta, data
+
+
 def extract_meta_and_data(rows: Sequence[Sequence[Any]]) -> Tuple[Params, List[str]]:
+    if isinstance(rows, LazyRows):
+        got = _extract_meta_and_data_lazy(rows)
+        if got is not None:
+            return got
     rows = _ordered(rows)
     meta_segs: List[str] = []
     data: List[str] = []
@@ -107,6 +145,16 @@ def extract_meta_and_data(rows: Sequence[Sequence[Any]]) -> Tuple[Params, List[s
 
 
 def extract_aux_data(rows: Sequence[Sequence[Any]], is_label: bool) -> List[Any]:
+    if isinstance(rows, LazyRows):
+        got = _lazy_order(rows)
+        if got is not None:
+            order, sid = got
+            idx = order[sid == AUX_STRING_INDEX].tolist()
+            if is_label:
+                col = rows.column(2)
+                return [col[i] for i in idx]
+            cols = [rows.column(j) for j in range(2, rows.width)]
+            return [Row(tuple(c[i] for c in cols)) for i in idx]
     out = []
     for r in _ordered(rows):
         if get_string_index(int(r[0])) == AUX_STRING_INDEX:

@@ -198,12 +198,46 @@ def deserialize_tree(strings: Sequence[str]) -> Optional[Node]:
 
 
 class TreeModel:
-    def __init__(self, meta: Params, roots: List[Node], labels: Optional[List[Any]],
-                 indexer_rows: Optional[List[Any]]):
+    """A tree ensemble.  A model read from a table keeps its trees as the node strings (``tree_strings``) and
+    builds ``Node`` objects only when ``roots`` is first read; serving takes ``native_flat()`` instead — the flat
+    arrays parsed in one C++ pass (``_native/csrc/tree_model.cpp``), no per-node Python objects."""
+
+    def __init__(self, meta: Params, roots: Optional[List[Node]], labels: Optional[List[Any]],
+                 indexer_rows: Optional[List[Any]], tree_strings: Optional[List[Sequence[str]]] = None):
         self.meta = meta
-        self.roots = roots
+        self._roots = roots
         self.labels = labels
         self.indexer_rows = indexer_rows
+        self._tree_strings = tree_strings
+        self._native = None
+
+    @property
+    def roots(self) -> List[Optional[Node]]:
+        if self._roots is None:
+            self._roots = [deserialize_tree(s) for s in (self._tree_strings or [])]
+        return self._roots
+
+    @roots.setter
+    def roots(self, v):
+        self._roots = v
+        self._tree_strings = None
+        self._native = None
+
+    def native_flat(self):
+        """``(arrays, tree_lo)`` of ``_native.tree_flatten`` over the model's node strings, or None (model built in
+        memory, library missing, or rows outside the serializer's form)."""
+        if self._native is None:
+            self._native = False
+            if self._tree_strings is not None:
+                from ... import _native
+                sizes = [len(s) for s in self._tree_strings]
+                lo = np.zeros(len(sizes) + 1, dtype=np.int64)
+                np.cumsum(sizes, out=lo[1:])
+                strings = [x for s in self._tree_strings for x in s]
+                res = _native.tree_flatten(strings, lo)
+                if res is not None:
+                    self._native = (res, lo)
+        return self._native or None
 
 
 class TreeModelDataConverter(LabeledModelDataConverter):
@@ -231,8 +265,8 @@ class TreeModelDataConverter(LabeledModelDataConverter):
             for i in range(f0, f1):
                 o = json.loads(data[i])
                 indexer_rows.append((int(o[0]), o[1], o[2]))
-        roots = [deserialize_tree(data[p["f0"]:p["f1"]]) for p in meta.get("treePartition")["partitions"]]
-        return TreeModel(meta, roots, list(labels) if labels else [], indexer_rows)
+        trees = [data[p["f0"]:p["f1"]] for p in meta.get("treePartition")["partitions"]]
+        return TreeModel(meta, None, list(labels) if labels else [], indexer_rows, tree_strings=trees)
 
 
 def feature_importance(roots: Sequence[Node], feature_cols: Sequence[str]) -> List[tuple]:
@@ -303,6 +337,41 @@ class _FlatForest:
             self.cat[i, :len(m)] = m
         self.max_steps = len(feats) + 1
 
+    @classmethod
+    def from_native(cls, nat: dict, tree_lo: np.ndarray, n_dist: int) -> "_FlatForest":
+        """The same arrays from ``_native.tree_flatten`` (node i of tree t at tree_lo[t] + its BFS id — the order
+        the constructor's BFS produces for a serialized tree)."""
+        self = cls.__new__(cls)
+        n = int(nat["feat"].shape[0])
+        self.feat = nat["feat"].astype(np.int64)
+        self.thr = nat["thr"]
+        leaf = self.feat == -1
+        self.first = np.where(leaf, -1, nat["first"]).astype(np.int64)
+        self.nchild = np.where(leaf, 0, nat["nchild"]).astype(np.int64)
+        d = nat["dist"]
+        if d.shape[1] >= n_dist:
+            self.dist = np.ascontiguousarray(d[:, :n_dist])
+        else:
+            self.dist = np.zeros((n, n_dist), dtype=np.float64)
+            self.dist[:, :d.shape[1]] = d
+        self.wsum = nat["wsum"]
+        self.roots = [int(tree_lo[t]) for t in range(len(tree_lo) - 1) if tree_lo[t + 1] > tree_lo[t]]
+        cl = nat["cat_len"].astype(np.int64)
+        has = (~leaf) & (cl >= 0)
+        self.catrow = np.full(n, -1, dtype=np.int64)
+        idx = np.flatnonzero(has)
+        self.catrow[idx] = np.arange(idx.size)
+        lens = cl[idx]
+        width = int(max(lens.max() if lens.size else 1, 1))
+        self.cat = np.full((max(1, idx.size), width), -1, dtype=np.int64)
+        if lens.sum():
+            rows = np.repeat(np.arange(idx.size), lens)
+            starts = nat["cat_off"][idx]
+            pos = np.arange(int(lens.sum())) - np.repeat(np.cumsum(lens) - lens, lens)
+            self.cat[rows, pos] = nat["cat"][np.repeat(starts, lens) + pos]
+        self.max_steps = n + 1
+        return self
+
 
 class _DeviceForest:
     """``_FlatForest`` as the tables of ``ops/csrc/tree_predict.hip``: every feature the forest splits on gets a
@@ -349,12 +418,48 @@ class _DeviceForest:
         for i, f in enumerate(self.cont):
             Tp[i, :len(self.thresholds[f])] = self.thresholds[f]
         self.T = torch.from_numpy(Tp).to(device)
+        # the device code kernel's table: rows padded with +inf to a power of two W > every threshold count
+        W = 1
+        while W < L + 1:
+            W *= 2
+        Tw = np.full((max(1, len(self.cont)), W), np.inf)
+        Tw[:, :L] = Tp
+        self.TW, self.W = torch.from_numpy(Tw).to(device), W
+        self.cont_slots = torch.tensor([self.slot[f] for f in self.cont] or [0], dtype=torch.int32, device=device)
 
-    def codes(self, cols: Dict[int, torch.Tensor], cat_codes: Dict[int, torch.Tensor], n: int) -> torch.Tensor:
-        """[n, stride] uint8 code rows (uint16 pairs when code_bytes is 2) from fp64 continuous columns (NaN =
-        missing) and int64 categorical indices (-1 = missing)."""
+    def codes(self, cols: Dict[int, torch.Tensor], cat_codes: Dict[int, torch.Tensor], n: int,
+              row0: int = 0, use_kernel: Optional[bool] = None) -> torch.Tensor:
+        """[n, stride] uint8 code rows (uint16 pairs when code_bytes is 2) of rows ``row0 .. row0+n-1`` from fp64
+        continuous columns (NaN = missing) and int64 categorical indices (-1 = missing).  On the GPU the continuous
+        codes come from ``alink_tree_codes`` (one pass, ops/csrc/tree_predict.hip); ``use_kernel=False`` is the
+        torch searchsorted form (the tests' reference)."""
+        from ...ops import _lib
         ct = torch.uint8 if self.code_bytes == 1 else torch.int16
         miss = 255 if self.code_bytes == 1 else -1              # 0xFFFF as int16
+        if use_kernel is None:
+            use_kernel = torch.device(self.dev).type == "cuda" and _lib.available() and \
+                hasattr(_lib.require(), "alink_tree_codes")
+        if use_kernel:
+            L = _lib.require()
+            out = torch.empty((n, self.stride // self.code_bytes), dtype=ct, device=self.dev)
+            ptrs = torch.tensor([cols[f].data_ptr() for f in self.cont] or [0], dtype=torch.int64, device=self.dev)
+            for f in self.cont:
+                v = cols[f]
+                if v.dtype != torch.float64 or not v.is_contiguous() or v.device != torch.device(self.dev) or \
+                        v.numel() < row0 + n:
+                    raise ValueError("tree codes need contiguous fp64 device columns covering the rows")
+            rc = L.alink_tree_codes(ptrs.data_ptr(), len(self.cont), self.cont_slots.data_ptr(), self.TW.data_ptr(),
+                                    self.W, int(row0), int(n), self.stride, self.code_bytes, out.data_ptr(),
+                                    _lib.stream_ptr(self.dev))
+            if rc != 0:
+                raise RuntimeError(f"alink_tree_codes failed: {rc}")
+            for f in self.slot:
+                if f in self.cat_features:
+                    v = cat_codes[f][row0:row0 + n]
+                    out[:, self.slot[f]] = torch.where(v < 0, torch.full_like(v, miss), v).to(ct)
+            return out
+        cols = {f: v[row0:row0 + n] for f, v in cols.items()}
+        cat_codes = {f: v[row0:row0 + n] for f, v in cat_codes.items()}
         out = torch.zeros((n, self.stride // self.code_bytes), dtype=ct, device=self.dev)
         if self.cont:
             X = torch.stack([cols[f] for f in self.cont])                                   # [Fc, n]
@@ -409,6 +514,12 @@ class TreeModelMapper(RichModelMapper):
         pass
 
     def _n_dist(self) -> int:
+        nat = self.model.native_flat() if self.model._roots is None else None
+        if nat is not None:
+            res, lo = nat
+            if len(lo) < 2 or lo[1] == lo[0] or res["dist_len"][0] < 0:
+                return 1
+            return int(res["dist_len"][0])
         r0 = self.model.roots[0] if self.model.roots else None
         if r0 is None or r0.counter is None or r0.counter.distributions is None:
             return 1
@@ -476,11 +587,13 @@ class TreeModelMapper(RichModelMapper):
         wacc = torch.empty(n, dtype=torch.float64, device=dev)
         err = torch.zeros(1, dtype=torch.int32, device=dev)
         # codes are built per chunk of rows (the batched searchsorted holds [features, rows] int64 temporaries)
-        chunk = max(64, ((1 << 27) // max(1, len(dfo.slot))) // 64 * 64)
+        # the device code kernel needs only the [chunk, stride] code block (1 GiB of rows at a time); the torch form
+        # holds [features, rows] int64 temporaries
+        chunk = max(64, ((1 << 30) // dfo.stride) // 64 * 64) if hasattr(L, "alink_tree_codes") else \
+            max(64, ((1 << 27) // max(1, len(dfo.slot))) // 64 * 64)
         for lo in range(0, n, chunk):
             hi = min(n, lo + chunk)
-            codes = dfo.codes({f: v[lo:hi] for f, v in cols.items()}, {f: v[lo:hi] for f, v in cats.items()},
-                              hi - lo)
+            codes = dfo.codes(cols, cats, hi - lo, row0=lo)
             rc = L.alink_tree_predict(codes.data_ptr(), hi - lo, dfo.stride, dfo.code_bytes, dfo.nodes.data_ptr(),
                                       dfo.dist.data_ptr(), dfo.nd, dfo.wsum.data_ptr(), dfo.cat.data_ptr(),
                                       int(dfo.cat.shape[1]), dfo.roots.data_ptr(), int(dfo.roots.numel()),
@@ -556,7 +669,9 @@ class TreeModelMapper(RichModelMapper):
         from ...common.table import Column
         flat = getattr(self, "_flat", None)
         if flat is None:
-            flat = self._flat = _FlatForest(self.model.roots, self._n_dist())
+            nat = self.model.native_flat() if self.model._roots is None else None
+            flat = self._flat = (_FlatForest.from_native(nat[0], nat[1], self._n_dist()) if nat is not None else
+                                 _FlatForest(self.model.roots, self._n_dist()))
         res = None
         dev = self._device(mt) if mt.num_rows and len(flat.roots) else None
         if dev is not None:

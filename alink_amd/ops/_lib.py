@@ -77,6 +77,7 @@ _EXTRA_SIGNATURES = {
     "alink_kmeans_reduce_slabs2": [_c_vp, _c_vp, _c_int, _c_int, _c_vp, _c_vp, _c_vp],
     "alink_tree_predict": [_c_vp, _c_i64, _c_int, _c_int, _c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_int, _c_vp, _c_int,
                            _c_vp, _c_vp, _c_vp, _c_vp],
+    "alink_tree_codes": [_c_vp, _c_int, _c_vp, _c_vp, _c_int, _c_i64, _c_i64, _c_int, _c_int, _c_vp, _c_vp],
     "alink_gbdt_rank_stats": [_c_vp, _c_vp, _c_vp, _c_vp, _c_int, _c_vp, _c_int, _c_vp, _c_vp, _c_vp, _c_vp],
     "alink_kmeans_seed_ref": [_c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_int, _c_vp, _c_vp, _c_vp],
     "alink_kmeans_par_pick": [_c_vp, _c_i64, _c_i64, _c_i64, _c_d, _c_vp, _c_i64, _c_vp, _c_vp],

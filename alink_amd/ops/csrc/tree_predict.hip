@@ -4,7 +4,7 @@
 // GbdtModelMapper.java:40-85 (sum of leaf values), RandomForestModelMapper.java (average of leaf distributions),
 // LabelCounter.add (weightSum += w; dist[i] += leaf.dist[i] * w).
 //
-// Rows arrive as CODES, not raw values (built on the host side by models/tree/model.py): for every continuous
+// Rows arrive as CODES, not raw values (built by tree_codes_kernel below, models/tree/model.py): for every continuous
 // feature the forest splits on, code = #{forest thresholds of that feature < x}, so "x <= threshold_k" is exactly
 // "code <= k" (k = the threshold's rank); a categorical feature's code is its string-indexer index; MISS (the
 // type's maximum) is a NULL / unseen value.  Codes are uint8 when every feature has < 255 thresholds / categories
@@ -138,9 +138,78 @@ int launch_tp(const void* codes, int64_t n, int stride, const void* nodes, const
     return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
+// Row codes for the walk above, on the device (replaces a batched searchsorted + scatter): block = TC_ROWS rows; the
+// 256 threads take (row = t % TC_ROWS, feature phase = t / TC_ROWS), read their column value (coalesced over rows),
+// count the feature's thresholds below it by a branchless binary search over a power-of-two row of the threshold
+// table (+inf padded; W >= #thresholds + 1, so the count is exact: x <= thr_k <=> code <= k), and write the code
+// into an LDS tile of the rows' code vectors, which then goes out in 16-byte stores.  NaN -> MISS.  Slots the
+// kernel does not own (categorical features) are left 0 for the caller to fill.
+constexpr int TC_ROWS = 64;
+
+template <typename CT>
+__global__ __launch_bounds__(256) void tree_codes_kernel(const double* const* __restrict__ cols, int fc,
+                                                         const int* __restrict__ slots,
+                                                         const double* __restrict__ T, int W, int64_t row0,
+                                                         int64_t n, int stride, CT* __restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    constexpr CT MISS = (CT)~(CT)0;
+    const int tid = threadIdx.x;
+    const int64_t r0 = (int64_t)blockIdx.x * TC_ROWS;
+    const int nrows = n - r0 < TC_ROWS ? (int)(n - r0) : TC_ROWS;
+    const int nvec = TC_ROWS * stride / 16;
+    uint4* tile = reinterpret_cast<uint4*>(lds);
+    for (int e = tid; e < nvec; e += 256) tile[e] = make_uint4(0u, 0u, 0u, 0u);
+    __syncthreads();
+    const int r = tid % TC_ROWS;
+    if (r < nrows) {
+        CT* rc = reinterpret_cast<CT*>(lds + r * stride);
+        for (int f = tid / TC_ROWS; f < fc; f += 256 / TC_ROWS) {
+            const double x = cols[f][row0 + r0 + r];
+            const double* t = T + (int64_t)f * W;
+            int lo = 0;
+            for (int s = W >> 1; s >= 1; s >>= 1)
+                if (t[lo + s - 1] < x) lo += s;
+            rc[slots[f]] = x != x ? MISS : (CT)lo;
+        }
+    }
+    __syncthreads();
+    uint4* dst = reinterpret_cast<uint4*>(reinterpret_cast<char*>(out) + r0 * stride);
+    const int nv = nrows * stride / 16;
+    for (int e = tid; e < nv; e += 256) dst[e] = tile[e];
+}
+
 }  // namespace
 
 extern "C" {
+
+// out [n][stride bytes] codes of rows row0 .. row0+n-1: for cont feature f (device pointer cols[f] to an fp64 column,
+// NaN = NULL) the count of T[f][0..W) below the value at byte/short slot slots[f]; T rows are ascending, +inf padded,
+// W a power of two > every feature's threshold count.  Other slots are zeroed.
+int alink_tree_codes(const void* cols, int fc, const int* slots, const double* T, int W, int64_t row0, int64_t n,
+                     int stride, int code_bytes, void* out, void* stream) {
+    if (n <= 0) return 0;
+    if (fc < 0 || W < 1 || (W & (W - 1)) != 0 || stride <= 0 || stride % 16 != 0 ||
+        (int64_t)stride * TC_ROWS > 160 * 1024 || (code_bytes != 1 && code_bytes != 2))
+        return 1;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const size_t lds = (size_t)TC_ROWS * stride;
+    const unsigned blocks = (unsigned)((n + TC_ROWS - 1) / TC_ROWS);
+    const double* const* c = reinterpret_cast<const double* const*>(cols);
+    if (code_bytes == 1) {
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(tree_codes_kernel<uint8_t>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+            return 3;
+        hipLaunchKernelGGL(tree_codes_kernel<uint8_t>, dim3(blocks), dim3(256), lds, st, c, fc, slots, T, W, row0, n,
+                           stride, reinterpret_cast<uint8_t*>(out));
+    } else {
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(tree_codes_kernel<uint16_t>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+            return 3;
+        hipLaunchKernelGGL(tree_codes_kernel<uint16_t>, dim3(blocks), dim3(256), lds, st, c, fc, slots, T, W, row0, n,
+                           stride, reinterpret_cast<uint16_t*>(out));
+    }
+    return hipGetLastError() == hipSuccess ? 0 : 2;
+}
 
 // acc [n][nd] / wacc [n] (fp64) = the reference's LabelCounter of every row over the forest.  codes: [n] rows of
 // `stride` bytes (multiple of 16, <= 160 KiB / 64), code_bytes 1 or 2.  *err |= 1 (a zero-weight fan-out: "Model is

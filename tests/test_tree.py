@@ -552,3 +552,46 @@ def test_fast_tree_serializer_equals_gson_walk():
     for _ in range(30):
         r = build(6)
         assert _serialize_tree_fast(r) == _serialize_tree_gson(r)
+
+
+def test_native_tree_flatten_equals_node_walk():
+    """Model load for serving (_native/csrc/tree_model.cpp): the flat arrays parsed straight from the node strings
+    equal _FlatForest's walk over deserialized Node objects -- categorical maps, null counters / distributions,
+    multi-way children, empty trees -- and a row outside the serializer's form falls back (None)."""
+    from alink_amd import _native
+    from alink_amd.common.params import Params
+    from alink_amd.common.types import Types
+    from alink_amd.models.tree.model import LabelCounter, Node, TreeModel, _FlatForest
+    if _native.lib is None or not hasattr(_native.lib, "alink_tree_flatten"):
+        pytest.skip("native library not built")
+    rng = np.random.default_rng(1)
+
+    def build(d):
+        if d == 0 or rng.random() < 0.2:
+            c = None if rng.random() < 0.1 else LabelCounter(
+                float(rng.random() * 100), int(rng.integers(100)),
+                None if rng.random() < 0.1 else list(rng.normal(size=3)))
+            return Node(-1, 0.0, c)
+        cat = rng.random() < 0.3
+        nd = Node(int(rng.integers(10)), float(rng.normal()), LabelCounter(float(rng.random()), 3, [0.5, 0.25, 0.25]),
+                  [int(v) for v in rng.integers(-1, 3, size=int(rng.integers(1, 6)))] if cat else None,
+                  float(rng.normal()))
+        nd.nextNodes = [build(d - 1) for _ in range(3 if cat else 2)]
+        return nd
+    roots = [build(5) for _ in range(12)]
+    meta = Params().set("featureCols", [f"f{i}" for i in range(10)]).set("labelCol", "y")
+    conv = TreeModelDataConverter(Types.DOUBLE)
+    rows = conv.save(TreeModel(meta, roots, [0.0, 1.0, 2.0], None))
+    tm = conv.load(rows)
+    nat = tm.native_flat()
+    assert nat is not None and tm._roots is None            # no Node objects were built for it
+    for n_dist in (3, 1, 5):
+        a = _FlatForest.from_native(nat[0], nat[1], n_dist)
+        b = _FlatForest(tm.roots, n_dist)
+        for f in ("feat", "thr", "catrow", "first", "nchild", "dist", "wsum", "cat"):
+            assert np.array_equal(getattr(a, f), getattr(b, f)), f
+        assert a.roots == b.roots and a.max_steps == b.max_steps
+    assert _native.tree_flatten(['{"node":{"featureIndex":1},"id":0,"nextIds":[1,3]}', '{"id":1}', '{"id":2}',
+                                 '{"id":3}'], [0, 4]) is None        # non-consecutive children
+    assert _native.tree_flatten(['{"node":{"featureIndex":1},"id":0,"nextIds":[1,2]}', '{"id":1}', "{oops"],
+                                [0, 3]) is None

@@ -143,3 +143,45 @@ def test_random_forest_memory_bound_identical_trees_gpu():
     useLocalEnv(1)
     assert widest * F * 128 * 3 * 4 > 8 << 20          # some level really exceeded the budget
     assert small[1:] == big[1:]
+
+
+def _forest(trees, depth, F, seed, decimals):
+    from alink_amd.models.tree.model import LabelCounter, Node
+    rng = np.random.default_rng(seed)
+
+    def build(d):
+        if d == depth:
+            return Node(-1, 0.0, LabelCounter(1.0, 1, [float(rng.normal())]))
+        nd = Node(int(rng.integers(F)), 1.0, LabelCounter(2.0, 1, [0.0]), None,
+                  float(np.round(rng.normal(), decimals)))
+        nd.nextNodes = [build(d + 1), build(d + 1)]
+        return nd
+    return [build(0) for _ in range(trees)]
+
+
+@pytest.mark.parametrize("decimals,F,n,row0", [(2, 40, 1000, 0), (2, 40, 4099, 131), (4, 3, 777, 64)])
+def test_device_row_codes_equal_searchsorted(decimals, F, n, row0):
+    """alink_tree_codes (ops/csrc/tree_predict.hip) == the torch searchsorted + scatter form, bit for bit: values
+    exactly on thresholds, NaN (MISS), +-inf, uint8 codes and uint16 codes (> 254 thresholds on a feature),
+    row offsets and row counts off the 64-row block."""
+    from alink_amd.models.tree.model import _DeviceForest, _FlatForest
+    flat = _FlatForest(_forest(60 if decimals == 4 else 30, 6, F, seed=decimals + F, decimals=decimals), 1)
+    dfo = _DeviceForest(flat, [], [0] * F, "cuda:0")
+    assert dfo.code_bytes == (2 if decimals == 4 else 1)
+    g = torch.Generator(device="cpu").manual_seed(n)
+    cols = {}
+    for f in dfo.cont:
+        x = torch.randn(row0 + n, generator=g, dtype=torch.float64)
+        T = torch.from_numpy(dfo.thresholds[f])
+        k = torch.randint(0, len(T), (row0 + n,), generator=g)
+        on = torch.rand(row0 + n, generator=g) < 0.2
+        x = torch.where(on, T[k], x)                            # exactly on a threshold
+        x[torch.rand(row0 + n, generator=g) < 0.05] = float("nan")
+        x[3] = float("inf")
+        x[5] = -float("inf")
+        cols[f] = x.cuda()
+    a = dfo.codes(cols, {}, n, row0=row0, use_kernel=True)
+    b = dfo.codes(cols, {}, n, row0=row0, use_kernel=False)
+    torch.cuda.synchronize()
+    assert a.dtype == b.dtype and a.shape == b.shape
+    assert torch.equal(a, b)

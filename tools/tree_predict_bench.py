@@ -103,10 +103,10 @@ def main():
     from alink_amd.models.tree import model as tmod
     orig_codes = tmod._DeviceForest.codes
 
-    def timed_codes(self, *x):
+    def timed_codes(self, *x, **kw):
         sync()
         t1 = time.perf_counter()
-        r = orig_codes(self, *x)
+        r = orig_codes(self, *x, **kw)
         sync()
         ph["codes_s"] = ph.get("codes_s", 0.0) + time.perf_counter() - t1
         return r
