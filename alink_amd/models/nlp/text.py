@@ -20,6 +20,7 @@ from collections import Counter
 from typing import Dict, List, Optional, Sequence
 
 import numpy as np
+import torch
 
 from ...common.javafmt import gson_dumps
 from ...common.linalg import SparseVector
@@ -368,13 +369,6 @@ class DocWordSplitCount:
         return [(w, int(c)) for w, c in counts.items()]
 
 
-def _merge_counters(local: Counter) -> Counter:
-    tot = Counter()
-    for part in comm.all_gather_object(dict(local)):
-        tot.update(part)
-    return tot
-
-
 class _Tuple3:
     __gson_fields__ = ("f0", "f1", "f2")
 
@@ -382,20 +376,48 @@ class _Tuple3:
         self.f0, self.f1, self.f2 = a, b, c
 
 
+def _doc_word_stats(mt: MTable, col: str):
+    """(words, word count int64, document frequency int64) of this rank's documents, built as tensors: the device
+    split (``ops/strings.split_tokens``), an exact dictionary encoding of the non-empty tokens (``unique_ids``),
+    ``bincount`` of the word ids for the counts and of the distinct (document, word) pairs for the document
+    frequency.  Only the distinct words become Python strings.  None when the encoding meets a hash collision."""
+    from ...ops.strings import split_tokens, unique_ids
+    from ..feature.encoders import feature_device
+    dev = feature_device()
+    tok, doc = split_tokens(_string_block(mt, col, dev))
+    ne = tok.lengths() > 0
+    tok, doc = tok.take(torch.nonzero(ne).reshape(-1)), doc[ne]
+    enc = unique_ids(tok)
+    if enc is None:
+        return None
+    ids, rep = enc
+    u = int(rep.numel())
+    wc = torch.bincount(ids, minlength=u)
+    pair = torch.unique(doc * max(u, 1) + ids)
+    dfv = torch.bincount(pair % max(u, 1), minlength=u)
+    words = tok.take(rep).to_list()
+    return words, wc.cpu().numpy(), dfv.cpu().numpy()
+
+
 def train_doc_count_vectorizer(mt: MTable, params: Params) -> List[tuple]:
     """Vocabulary by total word count (ties: ascending word), document-frequency filter, idf
     ``log((1 + N) / (1 + df))`` (``DocCountVectorizerTrainBatchOp.CalcIdf``)."""
     col = params.get("selectedCol")
-    df_c, wc_c = Counter(), Counter()
-    ndoc = 0
-    for v in mt.column_values(col):
-        ndoc += 1   # COUNT(1) counts null documents too
-        if v is None or str(v) == "":
-            continue
-        words = Counter(w for w in java_split(str(v), WORD_DELIMITER) if w)
-        for w, c in words.items():
-            df_c[w] += 1
-            wc_c[w] += c
+    ndoc = mt.num_rows    # COUNT(1) counts null documents too
+    stats = _doc_word_stats(mt, col)
+    if stats is not None:
+        words, wc, dfv = stats
+        wc_c = dict(zip(words, wc.tolist()))
+        df_c = dict(zip(words, dfv.tolist()))
+    else:
+        df_c, wc_c = Counter(), Counter()
+        for v in mt.column_values(col):
+            if v is None or str(v) == "":
+                continue
+            cnt = Counter(w for w in java_split(str(v), WORD_DELIMITER) if w)
+            for w, c in cnt.items():
+                df_c[w] += 1
+                wc_c[w] += c
     docs = int(sum(comm.all_gather_object(ndoc))) if comm.get_world_size() > 1 else ndoc
     max_df = float(_pget(params, "maxDF", float(2 ** 63 - 1)))
     min_df = float(_pget(params, "minDF", 1.0))
@@ -417,30 +439,58 @@ def train_doc_count_vectorizer(mt: MTable, params: Params) -> List[tuple]:
     return SimpleModelDataConverter.rows_from(meta, data)
 
 
+def _string_block(mt: MTable, col: str, dev):
+    """The column as a packed ``StringBlock`` on ``dev`` (a packed column moves as bytes; a list is packed once)."""
+    from ...common.strings import StringBlock
+    v = mt.col(col).values
+    blk = v if isinstance(v, StringBlock) else StringBlock.from_list(mt.column_values(col))
+    return blk.to(dev)
+
+
 def train_doc_hash_count_vectorizer(mt: MTable, params: Params) -> List[tuple]:
     """Hashed word counts over all documents (the reference counts word occurrences, not document
-    frequency, in ``HashingTF``), idf ``log((N + 1) / (count + 1))`` for indices with count >= minDF."""
-    from ..feature.encoders import murmur3_index
+    frequency, in ``HashingTF``), idf ``log((N + 1) / (count + 1))`` for indices with count >= minDF.
+
+    Tensor form (``DocHashCountVectorizerTrainBatchOp.java:40-60`` reduces per-task HashMaps): the documents are
+    split on the device (``ops/strings.split_tokens``), every token hashed by the device murmur3
+    (``csrc/feature.hip``), counted by ``bincount`` and the ``[numFeatures + 1]`` int64 vector (counts | #docs)
+    summed over ranks in ONE all-reduce."""
+    from ...ops.strings import murmur3_utf8_index, split_tokens
+    from ..feature.encoders import feature_device
     col = params.get("selectedCol")
     nf = int(_pget(params, "numFeatures", 1 << 18))
-    cnt = Counter()
-    ndoc = 0
-    for v in mt.column_values(col):
-        ndoc += 1
-        words = java_split(str(v), WORD_DELIMITER) if v is not None else []
-        if words:
-            cnt.update(murmur3_index(words, nf).tolist())
-    parts = comm.all_gather_object((dict(cnt), ndoc))
-    tot, docs = Counter(), 0
-    for d, n in parts:
-        tot.update(d)
-        docs += n
+    dev = feature_device()
+    tok, _ = split_tokens(_string_block(mt, col, dev))
+    acc = torch.zeros(nf + 1, dtype=torch.int64, device=dev)
+    if len(tok):
+        acc[:nf] = torch.bincount(murmur3_utf8_index(tok, nf).to(dev), minlength=nf)
+    acc[nf] = mt.num_rows                       # COUNT(1): null documents count too
+    comm.all_reduce(acc, "sum")
+    acc = acc.cpu().numpy()
+    cnt, docs = acc[:nf], int(acc[nf])
     min_df = float(_pget(params, "minDF", 1.0))
     min_df = min_df if min_df >= 1.0 else min_df * docs
-    idf = {int(k): math.log((docs + 1.0) / (c + 1.0)) for k, c in tot.items() if c >= min_df}
+    keys = np.flatnonzero((cnt > 0) & (cnt >= min_df))
+    vals = cnt[keys]
+    # Math.log per distinct count (libm, as the per-key form), broadcast to the keys
+    uniq, inv = np.unique(vals, return_inverse=True)
+    logs = np.asarray([math.log((docs + 1.0) / (float(c) + 1.0)) for c in uniq.tolist()], dtype=np.float64)
     meta = Params().set("numFeatures", nf).set("minTF", float(_pget(params, "minTF", 1.0))) \
         .set("featureType", _ename(_pget(params, "featureType"), "WORD_COUNT"))
-    return SimpleModelDataConverter.rows_from(meta, [gson_dumps({str(k): v for k, v in idf.items()})])
+    return SimpleModelDataConverter.rows_from(meta, [_int_double_map_json(keys, logs[inv.reshape(-1)])])
+
+
+def _int_double_map_json(keys: np.ndarray, vals: np.ndarray) -> str:
+    """Gson of a ``HashMap<Integer, Double>`` whose keys are below its capacity (the reference's
+    ``new HashMap<>(numFeatures)`` over indices < numFeatures): iteration is by bucket = ``k ^ (k >>> 16)``,
+    one key per bucket, so the order is ascending in that value whatever the insertion order."""
+    from ...common.javafmt import java_double_str
+    from ... import _native
+    order = np.argsort(keys ^ (keys >> 16), kind="stable")
+    k, v = keys[order].tolist(), vals[order]
+    body = _native.java_double_join(v) if len(k) else ""
+    strs = body.split(",") if body else [java_double_str(float(x)) for x in v.tolist()]
+    return "{" + ",".join('"%d":%s' % (a, b) for a, b in zip(k, strs)) + "}"
 
 
 class _VectorizerMapper(ModelMapper):

@@ -7,10 +7,13 @@ whichever side hashed).
 * ``murmur3_utf8_index(block, nf, prefix)``: Guava ``hashUnencodedChars(prefix + s)`` (UTF-16 code units,
   decoded from the UTF-8 bytes inside the kernel) -> ``floorMod(abs(h), nf)``: the FeatureHasher / one-hot
   path of ``FeatureHasherMapper.java:104-106`` without any host string handling.
+* ``split_tokens(block)``: Java ``String.split(" ")`` of every document into one token block (NLP counting).
+* ``unique_ids(block)``: exact dictionary encoding (two-hash 64-bit key + byte comparison with a representative).
 """
 from __future__ import annotations
 
 import ctypes
+from typing import Optional, Tuple
 
 import numpy as np
 import torch
@@ -18,7 +21,7 @@ import torch
 from ..common.strings import StringBlock
 from . import _lib
 
-__all__ = ["hash_bytes", "murmur3_utf8_index", "murmur3_bytes_py"]
+__all__ = ["hash_bytes", "murmur3_utf8_index", "murmur3_bytes_py", "split_tokens", "unique_ids"]
 
 
 def murmur3_bytes_py(b: bytes, seed: int = 0) -> int:
@@ -170,3 +173,83 @@ def murmur3_utf8_index(block: StringBlock, nf: int, prefix: str = "", seed: int 
     a = np.abs(h.astype(np.int64))
     a = np.where(h == np.iinfo(np.int32).min, np.int64(np.iinfo(np.int32).min), a)   # Java abs(MIN_VALUE)
     return torch.from_numpy(np.mod(a, int(nf)))
+
+
+def split_tokens(block: StringBlock, delim: int = 0x20):
+    """Java ``String.split(" ")`` of every string of a packed block, on the block's device with no per-string
+    Python work: returns ``(tokens, doc)`` — a ``StringBlock`` of the tokens back to back (document order) and the
+    int64 document index of each token.  Semantics as ``models/nlp/text.java_split``: leading empty tokens are
+    kept, trailing ones dropped, the empty string gives one empty token, a NULL gives none.  UTF-8 never carries
+    the delimiter byte inside a multi-byte character, so splitting the bytes is splitting the characters."""
+    dev = block.device
+    n = len(block)
+    data, off = block.data, block.offsets.to(torch.int64)
+    nb = int(data.numel())
+    is_d = data == delim
+    # spaces per document (prefix sum of the delimiter mask at the document boundaries)
+    cum = torch.zeros(nb + 1, dtype=torch.int64, device=dev)
+    if nb:
+        torch.cumsum(is_d.to(torch.int64), 0, out=cum[1:])
+    nsp = cum[off[1:]] - cum[off[:-1]]
+    ntok = nsp + 1                                            # tokens before the trailing-empty rule
+    tok_doc = torch.repeat_interleave(torch.arange(n, device=dev), ntok)
+    T = int(tok_doc.numel())
+    # token t of document d ends at its k-th delimiter (k = t - first token of d) or at the document end
+    first_tok = torch.cumsum(ntok, 0) - ntok
+    k = torch.arange(T, device=dev) - first_tok[tok_doc]
+    dpos = torch.nonzero(is_d).reshape(-1)                    # delimiter byte positions, ascending
+    gk = cum[off[:-1]][tok_doc] + k                           # global index of that delimiter
+    is_last = k == nsp[tok_doc]
+    end = torch.where(is_last, off[1:][tok_doc], dpos[gk.clamp(max=max(dpos.numel() - 1, 0))] if dpos.numel()
+                      else off[1:][tok_doc])
+    start = torch.where(k == 0, off[:-1][tok_doc],
+                        (dpos[(gk - 1).clamp(min=0)] + 1) if dpos.numel() else off[:-1][tok_doc])
+    tlen = end - start
+    # trailing empty tokens dropped; "" keeps its single empty token; a NULL document has none
+    tid = torch.arange(T, device=dev)
+    last_ne = torch.full((n,), -1, dtype=torch.int64, device=dev)
+    ne = tlen > 0
+    if T:
+        last_ne.scatter_reduce_(0, tok_doc[ne], tid[ne], reduce="amax")
+    dlen = off[1:] - off[:-1]
+    keep = (tid <= last_ne[tok_doc]) | (dlen[tok_doc] == 0)
+    if block.nulls is not None:
+        keep &= ~block.nulls.to(dev)[tok_doc]
+    start, tlen, tok_doc = start[keep], tlen[keep], tok_doc[keep]
+    toff = torch.zeros(int(tlen.numel()) + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(tlen, 0, out=toff[1:])
+    # token bytes back to back: every non-delimiter byte of a kept token, in order
+    src = torch.repeat_interleave(start - toff[:-1], tlen) + torch.arange(int(toff[-1]), device=dev)
+    tdata = data[src] if src.numel() else torch.zeros(0, dtype=torch.uint8, device=dev)
+    return StringBlock(tdata, toff), tok_doc
+
+
+def unique_ids(block: StringBlock) -> Optional[Tuple[torch.Tensor, torch.Tensor]]:
+    """Exact dictionary encoding of a packed block on its device: ``(ids int64 [n], rep int64 [u])`` — equal
+    strings get equal ids (0..u-1, in order of the 64-bit key), ``rep[i]`` is the first string with id i.  Keys are
+    two 32-bit murmur3 hashes of the bytes; every string is then compared byte for byte with its representative, so
+    the result is exact or None (a 64-bit collision: the caller takes its host path)."""
+    n = len(block)
+    dev = block.device
+    if n == 0:
+        z = torch.zeros(0, dtype=torch.int64, device=dev)
+        return z, z
+    h0 = hash_bytes(block, 0).to(torch.int64) & 0xFFFFFFFF
+    h1 = hash_bytes(block, 0x5BD1E995).to(torch.int64) & 0xFFFFFFFF
+    key = (h0 << 32) | h1
+    uk, ids = torch.unique(key, return_inverse=True)
+    pos = torch.arange(n, device=dev)
+    rep = torch.full((uk.numel(),), n, dtype=torch.int64, device=dev)
+    rep.scatter_reduce_(0, ids, pos, reduce="amin")
+    off = block.offsets
+    lens = off[1:] - off[:-1]
+    r = rep[ids]
+    if not bool(torch.equal(lens, lens[r])):
+        return None
+    tot = int(lens.sum())
+    if tot:
+        seg = torch.repeat_interleave(pos, lens)
+        j = torch.arange(tot, device=dev) - torch.repeat_interleave(torch.cumsum(lens, 0) - lens, lens)
+        if not bool(torch.equal(block.data[off[:-1][seg] + j], block.data[off[:-1][r][seg] + j])):
+            return None
+    return ids, rep

@@ -167,6 +167,9 @@ def s_doccount(out):
     from alink_amd import BatchOperator, DocCountVectorizerTrainBatchOp
     src = BatchOperator.fromDataframe(_docs(), schemaStr="id long, doc string")
     out["model"] = _rows(DocCountVectorizerTrainBatchOp().setSelectedCol("doc").setMinDF(2.0).linkFrom(src))
+    from alink_amd import DocHashCountVectorizerTrainBatchOp
+    out["hash"] = _rows(DocHashCountVectorizerTrainBatchOp().setSelectedCol("doc").setNumFeatures(64)
+                        .setMinDF(2.0).linkFrom(src))
 
 
 def s_word2vec(out):

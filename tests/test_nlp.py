@@ -235,3 +235,83 @@ def test_ngram_mapper_reference(n, expect):
     from alink_amd.models.nlp.text import NGramMapper
     m = _siso(NGramMapper, **({} if n is None else {"n": n}))
     assert m.map(("This is a unit test for mapper",))[0] == expect
+
+
+def test_doc_hash_count_vectorizer_tensor_counts_equal_per_document_counter():
+    """The tensor trainer (device split + murmur3 + bincount + one int64 all-reduce) writes exactly the model of the
+    per-document form it replaced: Java split semantics (leading / doubled / trailing spaces, empty and NULL
+    documents), non-ASCII words, fractional minDF."""
+    import math
+    import random
+    from collections import Counter
+    from alink_amd.common.javafmt import gson_dumps
+    from alink_amd.models.feature.encoders import murmur3_index
+    from alink_amd.models.nlp.text import java_split
+    random.seed(3)
+    docs = ["", " ", "a b", " a  b ", "héllo wörld  x", None, "   ", "中文 分词 中文"]
+    for _ in range(400):
+        docs.append(" ".join(random.choice(["a", "b", "", "c", "dé", "ß", "w%d" % random.randint(0, 50)])
+                             for _ in range(random.randint(0, 9))) if random.random() > 0.05 else None)
+    src = BatchOperator.fromDataframe(pd.DataFrame({"t": docs}), schemaStr="t string")
+    for nf, min_df in ((32, 1.0), (1 << 10, 3.0), (1 << 10, 0.01)):
+        got = DocHashCountVectorizerTrainBatchOp().setSelectedCol("t").setNumFeatures(nf).setMinDF(min_df) \
+            .linkFrom(src).collect()
+        cnt = Counter()
+        for v in docs:
+            words = java_split(str(v), " ") if v is not None else []
+            if words:
+                cnt.update(murmur3_index(words, nf).tolist())
+        md = min_df if min_df >= 1.0 else min_df * len(docs)
+        idf = {int(k): math.log((len(docs) + 1.0) / (c + 1.0)) for k, c in cnt.items() if c >= md}
+        # HashMap<Integer, Double> iteration (keys < capacity): ascending k ^ (k >>> 16)
+        want = "{" + ",".join('"%d":%s' % (k, gson_dumps(idf[k])) for k in sorted(idf, key=lambda k: k ^ (k >> 16))) \
+            + "}"
+        data = [r[1] for r in got if r[0] != 0 and r[1] is not None]
+        assert data == [want]
+
+
+def _random_docs(n, seed):
+    import random
+    random.seed(seed)
+    docs = ["", " ", "a b", " a  b ", "héllo wörld  x", None, "   ", "中文 分词 中文"]
+    for _ in range(n):
+        docs.append(" ".join(random.choice(["a", "b", "", "c", "dé", "ß", "w%d" % random.randint(0, 50)])
+                             for _ in range(random.randint(0, 9))) if random.random() > 0.05 else None)
+    return docs
+
+
+def test_doc_count_vectorizer_tensor_stats_equal_counter_path(monkeypatch):
+    """DocCountVectorizer's tensor word statistics (device split, exact dictionary encoding, bincounts) train the
+    same model as the per-document Counter path, which stays as the fallback of a hash collision."""
+    from alink_amd.ops import strings as S
+    docs = _random_docs(500, 5)
+    src = BatchOperator.fromDataframe(pd.DataFrame({"t": docs}), schemaStr="t string")
+
+    def train():
+        return DocCountVectorizerTrainBatchOp().setSelectedCol("t").setMinDF(2.0).setFeatureType("TF_IDF") \
+            .linkFrom(src).collect()
+    a = train()
+    monkeypatch.setattr(S, "unique_ids", lambda blk: None)
+    b = train()
+    assert a == b and len(a) > 10
+
+
+def test_split_tokens_and_unique_ids_host():
+    """ops/strings.split_tokens == java_split per document; unique_ids is an exact dictionary encoding."""
+    from alink_amd.common.strings import StringBlock
+    from alink_amd.ops.strings import split_tokens, unique_ids
+    docs = _random_docs(300, 9)
+    tok, doc = split_tokens(StringBlock.from_list(docs))
+    got = {}
+    for t, d in zip(tok.to_list(), doc.tolist()):
+        got.setdefault(d, []).append(t)
+    for i, s in enumerate(docs):
+        assert got.get(i, []) == ([] if s is None else java_split(s, " "))
+    ids, rep = unique_ids(tok)
+    toks = tok.to_list()
+    first = {}
+    for i, t in enumerate(toks):
+        first.setdefault(t, i)
+    assert sorted(first.values()) == sorted(rep.tolist())
+    for i, t in enumerate(toks):
+        assert toks[int(rep[ids[i]])] == t

@@ -97,3 +97,41 @@ def test_hip_multi_column_feature_hash_equals_per_column():
     mt = MTable(TableSchema(names, [Types.STRING] * 5), [Column(b) for b in blocks])
     b = op().linkFrom(TableSourceBatchOp(mt)).collect()
     assert [str(r[-1]) for r in a] == [str(r[-1]) for r in b]
+
+
+def test_split_tokens_unique_ids_device_equal_host():
+    """ops/strings.split_tokens / unique_ids on the GPU return exactly the host results (the NLP count trainers)."""
+    import random
+    from alink_amd.common.strings import StringBlock
+    from alink_amd.ops.strings import split_tokens, unique_ids
+    random.seed(11)
+    docs = ["", " ", " a  b ", "中文 分词", None] + [
+        " ".join(random.choice(["a", "", "é", "w%d" % random.randint(0, 300)]) for _ in range(random.randint(0, 12)))
+        for _ in range(20000)]
+    h = StringBlock.from_list(docs)
+    th, dh = split_tokens(h)
+    td, dd = split_tokens(h.to("cuda"))
+    assert torch.equal(td.data.cpu(), th.data) and torch.equal(td.offsets.cpu(), th.offsets)
+    assert torch.equal(dd.cpu(), dh)
+    ih, rh = unique_ids(th)
+    idd, rd = unique_ids(td)
+    assert torch.equal(idd.cpu(), ih) and torch.equal(rd.cpu(), rh)
+
+
+def test_doc_count_and_hash_vectorizers_gpu_equal_cpu():
+    import pandas as pd
+    from alink_amd import BatchOperator, DocCountVectorizerTrainBatchOp, DocHashCountVectorizerTrainBatchOp, \
+        useLocalEnv
+    import random
+    random.seed(12)
+    docs = [" ".join(random.choice(["a", "b", "", "dé", "w%d" % random.randint(0, 80)])
+                     for _ in range(random.randint(0, 9))) for _ in range(3000)] + [None, ""]
+    out = {}
+    for dev in ("cpu", "cuda:0"):
+        useLocalEnv(1, device=dev)
+        src = BatchOperator.fromDataframe(pd.DataFrame({"t": docs}), schemaStr="t string")
+        out[dev] = (DocCountVectorizerTrainBatchOp().setSelectedCol("t").setMinDF(2.0).linkFrom(src).collect(),
+                    DocHashCountVectorizerTrainBatchOp().setSelectedCol("t").setNumFeatures(512).linkFrom(src)
+                    .collect())
+    useLocalEnv(1)
+    assert out["cpu"] == out["cuda:0"]
