@@ -75,11 +75,8 @@ class FtrlTrainStreamOp(StreamOperator):
 
     ``updateMode``:
 
-    * ``AUTO`` (default): ``SHARDED`` when the environment's device is a GPU, else ``SEQUENTIAL``.  SHARDED's
-      step-start margins are the reference's own staleness: there a sample's margin is computed on arrival
-      (``FtrlTrainStreamOp.java:396-420``) and the coefficients are updated when the reduced margin comes back
-      through the feedback edge (``:424-480``), with other samples' updates in between.
-    * ``SEQUENTIAL``: sample-by-sample rule in stream order (native host loop), every margin on the latest weights.  With P ranks every
+    * ``SEQUENTIAL`` (default): sample-by-sample rule in stream order (native host loop), every margin on the
+      latest weights — the same model on every device, so a job trains identically on CPU and GPU.  With P ranks every
       step all-gathers the ranks' micro-batches (rank order) and every rank applies the identical update to a
       replicated coefficient vector, so the model equals the 1-rank model on the same global batch sequence.
     * ``SHARDED``: the reference's distributed design (``FtrlTrainStreamOp.java:72-85`` split info,
@@ -89,7 +86,13 @@ class FtrlTrainStreamOp(StreamOperator):
       ~1/P of the global batch's nonzeros); each shard computes partial margins of the global batch on its range
       (HIP kernel on GPU), the margins are summed per sample (all-reduce), and each shard replays its
       coordinates in global sample order with the margins of the step start — the reference's feedback
-      staleness bounded to one micro-batch.  Deterministic and independent of the number of ranks.
+      staleness bounded to one micro-batch.  Deterministic and independent of the number of ranks.  Its
+      step-start margins are the reference's own kind of staleness (a sample's margin is computed on arrival,
+      ``FtrlTrainStreamOp.java:396-420``, and the coefficients updated when the reduced margin comes back through
+      the feedback edge, ``:424-480``), so its model differs from SEQUENTIAL's (by ~0.2 in a coefficient on the
+      6-feature stream of tests/test_ftrl_gpu.py).
+    * ``AUTO`` (opt-in): ``SHARDED`` when the environment's device is a GPU, else ``SEQUENTIAL`` — the GPU
+      throughput path (profiles/ftrl_r5.txt), whose model then depends on the device.
     * ``DATA_PARALLEL``: replicated coefficients, the ranks' micro-batches form one global step: every rank
       scores its own samples, the per-coordinate gradient sums (g, g^2) are all-reduced as one dense buffer
       (RCCL), and every rank applies the same mini-batch FTRL-proximal update (n += sum g^2, z += sum g - sigma w).
@@ -102,10 +105,10 @@ class FtrlTrainStreamOp(StreamOperator):
     micro-batches stay in lockstep: a rank whose stream ended keeps joining steps with an empty batch until all
     ranks are done.  Snapshots: at the first step, whenever any rank's ``timeInterval`` elapsed, and at the end.
     """
-    EXTRA_PARAMS = [ParamInfo("updateMode", str, "AUTO (SHARDED on a GPU, else SEQUENTIAL), SEQUENTIAL, SHARDED "
-                                                 "(feature-sharded micro-batch), DATA_PARALLEL (replicated, "
-                                                 "all-reduced mini-batch gradients) or HOGWILD (GPU, one wave per "
-                                                 "sample)", default="AUTO"),
+    EXTRA_PARAMS = [ParamInfo("updateMode", str, "SEQUENTIAL (default), AUTO (SHARDED on a GPU, else "
+                                                 "SEQUENTIAL), SHARDED (feature-sharded micro-batch), "
+                                                 "DATA_PARALLEL (replicated, all-reduced mini-batch gradients) or "
+                                                 "HOGWILD (GPU, one wave per sample)", default="SEQUENTIAL"),
                     ParamInfo("asyncGradReduce", bool, "DATA_PARALLEL: overlap the gradient all-reduce of a step "
                                                        "with scoring the next (one-step-stale gradients)",
                               default=False)]
@@ -143,7 +146,7 @@ class FtrlTrainStreamOp(StreamOperator):
         self._vec_col = _pget(p, "vectorCol")
         self._feat_cols = _pget(p, "featureCols")
         self._vsize = _pget(p, "vectorSize")
-        self._mode = str(_pget(p, "updateMode", "AUTO")).upper()
+        self._mode = str(_pget(p, "updateMode", "SEQUENTIAL")).upper()
         if self._mode == "AUTO":
             self._mode = "SHARDED" if self.env.device.type == "cuda" else "SEQUENTIAL"
         self._async_reduce = bool(_pget(p, "asyncGradReduce", False))

@@ -275,3 +275,42 @@ def test_ftrl_shard_update_block_scan_matches_native(l1, drift, monkeypatch):
     torch.cuda.synchronize()
     for g, r in zip(st, ref):
         np.testing.assert_allclose(g.cpu().numpy(), r, rtol=1e-10, atol=1e-12)
+
+
+def test_ftrl_default_mode_is_device_independent_and_auto_is_sharded():
+    """The default updateMode (SEQUENTIAL) trains the bit-identical model on a CPU and a GPU environment; AUTO is
+    the opt-in GPU throughput path (SHARDED there), whose step-start margins change the model (~0.2 in a
+    coefficient here) -- the difference this pins."""
+    import json
+    import pandas as pd
+    from alink_amd import (useLocalEnv, BatchOperator, StreamOperator, LogisticRegressionTrainBatchOp,
+                           FtrlTrainStreamOp, CollectStreamOp)
+    from alink_amd.common.mlenv import resetEnv
+    rng = np.random.default_rng(4)
+    X = rng.normal(size=(3000, 6))
+    df = pd.DataFrame({f"f{i}": X[:, i] for i in range(6)})
+    df["label"] = (X @ rng.normal(size=6) > 0).astype(int)
+    schema = ", ".join(f"f{i} double" for i in range(6)) + ", label int"
+    cols = [f"f{i}" for i in range(6)]
+
+    def run(dev, mode):
+        resetEnv()
+        useLocalEnv(1, device=dev)
+        model = LogisticRegressionTrainBatchOp().setFeatureCols(cols).setLabelCol("label").setMaxIter(3) \
+            .linkFrom(BatchOperator.fromDataframe(df.iloc[:100], schemaStr=schema))
+        snaps = []
+        op = FtrlTrainStreamOp(model).setFeatureCols(cols).setLabelCol("label").setTimeInterval(1e9) \
+            .setAlpha(0.1).setBeta(1.0).setL1(0.01).setL2(0.01)
+        if mode is not None:
+            op = op.setUpdateMode(mode)
+        op.linkFrom(StreamOperator.fromDataframe(df, schemaStr=schema)).link(CollectStreamOp(snaps))
+        StreamOperator.execute()
+        last = max(r[0] for r in snaps)
+        row = [r for r in snaps if r[0] == last and r[2] == 1048576][0][3]
+        return np.asarray(json.loads(row)["coefVector"]["data"])
+    cpu, gpu = run("cpu", None), run("cuda:0", None)
+    assert np.array_equal(cpu, gpu)
+    auto, sharded = run("cuda:0", "AUTO"), run("cuda:0", "SHARDED")
+    assert np.array_equal(auto, sharded)
+    assert not np.array_equal(auto, cpu)
+    assert np.abs(auto - cpu).max() < 0.5 and np.array_equal(np.sign(auto[1:]), np.sign(cpu[1:]))
