@@ -59,6 +59,7 @@ __global__ __launch_bounds__(RK_T) void gbdt_rank_stats_kernel(const float* __re
     const int tid = threadIdx.x;
     const int64_t b = off[gi];
     const int n = (int)(off[gi + 1] - b);
+    if (n <= 0) return;          // an empty query has no pairs (uniform over the block: before any barrier)
     const float* P = pred + b;
     const float* Y = lab + b;
     int* R = rank_scratch + b;

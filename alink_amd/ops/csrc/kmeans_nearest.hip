@@ -282,8 +282,8 @@ __global__ __launch_bounds__(256) void kmeans_par_pick_kernel(const double* __re
 // The reference seeding rule over the k-means|| candidates (LocalKmeansFunc.sampleInitialCentroids,
 // LocalKmeansFunc.java:36-86) in ONE workgroup: picks 1..k-1, each = the first candidate whose cumulative
 // weight x cost reaches U[j-1] x total (numpy/torch searchsorted, side left), then cost = min(cost, D[pick]).
-// costs and the cumulative sums live in LDS (n <= SEED_NMAX); the prefix sum is sequential within each thread's
-// contiguous chunk and a fixed-order scan across threads (deterministic).  *mintot receives the smallest total
+// costs and the cumulative sums live in LDS (n <= SEED_NMAX); the prefix sum is ONE sequential fp64 pass in index
+// order, as torch.cumsum on the host, so GPU and CPU pick the same candidates.  *mintot receives the smallest total
 // seen (<= 0 means some pick had nothing left to sample: the caller redoes the picks on the host).
 constexpr int SEED_NMAX = 4096;
 constexpr int SEED_T = 512;
@@ -295,38 +295,46 @@ __global__ __launch_bounds__(SEED_T) void kmeans_seed_ref_kernel(const double* _
                                                                  double* __restrict__ mintot) {
     __shared__ double costs[SEED_NMAX];
     __shared__ double cw[SEED_NMAX];
-    __shared__ double tsum[SEED_T];
+    __shared__ double tot_sh;
     __shared__ int cnt;
     const int t = threadIdx.x;
-    const int per = (n + SEED_T - 1) / SEED_T;
-    const int lo = t * per < n ? t * per : n;
-    const int hi = lo + per < n ? lo + per : n;
     for (int i = t; i < n; i += SEED_T) costs[i] = D[(int64_t)idx0 * n + i];
     if (t == 0) chosen[0] = idx0;
     double mt = 1.0 / 0.0;
     __syncthreads();
     for (int j = 1; j < k; ++j) {
-        double run = 0.0;
-        for (int i = lo; i < hi; ++i) {
-            run += w[i] * costs[i];
-            cw[i] = run;
-        }
-        tsum[t] = run;
+        // cumulative weight x cost in exactly the host order (torch.cumsum on the CPU: products rounded first, then
+        // one sequential fp64 sum), so the picks equal the host path's bit for bit, ties and near-ties included:
+        // the products in parallel, the prefix by one lane (n <= 4096; ~12 cycles per candidate)
+        for (int i = t; i < n; i += SEED_T) cw[i] = w[i] * costs[i];
         if (t == 0) cnt = 0;
         __syncthreads();
-        // inclusive scan of the thread totals (Hillis-Steele, fixed order)
-        for (int off = 1; off < SEED_T; off <<= 1) {
-            const double v = t >= off ? tsum[t - off] : 0.0;
-            __syncthreads();
-            tsum[t] += v;
-            __syncthreads();
+        if (t == 0) {
+            double run = 0.0;
+            int i = 0;
+            for (; i + 8 <= n; i += 8) {
+                double v[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) v[u] = cw[i + u];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    run += v[u];
+                    cw[i + u] = run;
+                }
+            }
+            for (; i < n; ++i) {
+                run += cw[i];
+                cw[i] = run;
+            }
+            tot_sh = run;
         }
-        const double base = t > 0 ? tsum[t - 1] : 0.0;
-        const double tot = tsum[SEED_T - 1];
+        __syncthreads();
+        const double tot = tot_sh;
         const double target = U[j - 1] * tot;
         mt = tot < mt ? tot : mt;
+        // searchsorted(cw, target, left) = #{cw < target} (cw is non-decreasing)
         int c = 0;
-        for (int i = lo; i < hi; ++i) c += (base + cw[i]) < target;
+        for (int i = t; i < n; i += SEED_T) c += cw[i] < target;
         if (c) atomicAdd(&cnt, c);
         __syncthreads();
         const int pick = cnt < n - 1 ? cnt : n - 1;

@@ -483,6 +483,25 @@ def test_seed_ref_kernel_equals_torch_loop(n, k):
     assert torch.equal(a.cpu(), b)
 
 
+@pytest.mark.parametrize("n,k", [(64, 30), (700, 120), (4096, 40)])
+def test_seed_ref_kernel_equals_host_on_ties_and_wide_weights(n, k):
+    """Tied distances (integer grid points), zero weights (flat cumulative runs) and weights over 18 decades (sums
+    whose rounding depends on the order): the kernel's sequential prefix picks exactly the host torch.cumsum's."""
+    import numpy as np
+    from alink_amd.models.clustering import kmeans as km
+    g = torch.Generator(device="cpu").manual_seed(n + k)
+    S = torch.randint(0, 3, (n, 4), generator=g).to(torch.float64)
+    D = km.pairwise_distance(S, S, "EUCLIDEAN")
+    w = torch.pow(10.0, torch.randint(-3, 16, (n,), generator=g).to(torch.float64))
+    w[torch.rand(n, generator=g) < 0.3] = 0.0
+    for seed in range(3):
+        a = km._seed_reference_device(D.cuda(), w.cuda(), k, np.random.default_rng(seed), 0)
+        b = km._seed_reference_device(D, w, k, np.random.default_rng(seed), 0)
+        assert (a is None) == (b is None)
+        if a is not None:
+            assert torch.equal(a.cpu(), b)
+
+
 @pytest.mark.parametrize("pool", [0.0, 0.1, 0.5, 1.0])
 @pytest.mark.parametrize("n,k,grid", [(300001, 100, None), (49157, 97, 3), (4097, 16, None), (129, 50, 1),
                                       (1000003, 112, 7), (70, 8, 2)])
