@@ -74,7 +74,9 @@ class VectorAssemblerMapper(MISOMapper):
         fast = all(isinstance(c.values, torch.Tensor) and c.nulls is None for c in cols)
         if fast and cols:
             dev = cols[0].values.device
-            parts = [(c.values.to(dev).reshape(c.values.shape[0], -1)) for c in cols]
+            # a 1-D column is one value per row (explicit width: reshape(0, -1) of an empty column is ambiguous)
+            parts = [c.values.to(dev).reshape(c.values.shape[0], int(np.prod(c.values.shape[1:], dtype=np.int64)))
+                     for c in cols]
             dt = torch.float64
             if all(p.dtype in (torch.bfloat16,) for p in parts):
                 dt = torch.bfloat16

@@ -242,9 +242,18 @@ class StreamOperator(AlgoOperator):
         raise RuntimeError("stream operators have no materialised output table; use print/collect sinks")
 
     # ---- data flow ----
+    # row-local operators (mappers, predictors, SQL select / where) map an empty micro-batch to an empty one of their
+    # output schema without running: the lockstep rounds of a multi-rank job feed every operator empty batches
+    # after its rank's stream ended, and a mapper need not handle zero rows.  Operators that issue collectives per
+    # batch (evaluation windows, FTRL, DB sinks) keep receiving them.
+    EMPTY_PASSTHROUGH = False
+
     def _emit(self, mt: MTable):
         for op, port in self._subscribers:
-            op.on_batch(port, mt)
+            if op.EMPTY_PASSTHROUGH and mt.num_rows == 0 and op._schema is not None:
+                op._emit(MTable.empty(op._schema))
+            else:
+                op.on_batch(port, mt)
 
     def on_batch(self, port: int, mt: MTable):
         raise NotImplementedError
@@ -368,6 +377,7 @@ class StreamSourceOp(StreamOperator):
 
 class MapStreamOp(StreamOperator):
     MAPPER: Callable[..., Mapper] = None
+    EMPTY_PASSTHROUGH = True
 
     def __init__(self, params: Optional[Params] = None, mapper=None, **kw):
         super().__init__(params, **kw)
@@ -389,6 +399,7 @@ class MapStreamOp(StreamOperator):
 class ModelMapStreamOp(StreamOperator):
     """Stream predict with a static model (reference ``ModelMapStreamOp.java:39-56``)."""
     MAPPER: Callable[..., ModelMapper] = None
+    EMPTY_PASSTHROUGH = True
 
     def __init__(self, model=None, params: Optional[Params] = None, mapper=None, **kw):
         if isinstance(model, Params):
@@ -417,6 +428,7 @@ class ModelMapStreamOp(StreamOperator):
 
 class FlatMapStreamOp(StreamOperator):
     MAPPER: Callable[..., FlatMapper] = None
+    EMPTY_PASSTHROUGH = True
 
     def __init__(self, params: Optional[Params] = None, mapper=None, **kw):
         super().__init__(params, **kw)

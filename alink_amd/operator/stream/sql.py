@@ -13,6 +13,7 @@ __all__ = ["SelectStreamOp", "AsStreamOp", "WhereStreamOp", "FilterStreamOp", "U
 
 class _RowLocal(StreamOperator):
     FN = None
+    EMPTY_PASSTHROUGH = True
 
     def __init__(self, clause=None, params: Optional[Params] = None, **kw):
         if isinstance(clause, Params):

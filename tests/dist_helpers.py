@@ -644,5 +644,85 @@ def scenario_eval_uneven(out):
     out["batch"] = {"auc": m.getAuc(), "logloss": m.getLogLoss(), "total": m.getTotalSamples()}
 
 
+def scenario_stream_ops_uneven(out):
+    """Lockstep micro-batches through the common stream operators when the ranks' streams differ in length (rank 0:
+    150 rows, rank 1: 20 rows, or none with ALINK_TEST_PHASE=empty; 40-row micro-batches): rank 1 feeds empty
+    batches for most rounds.  Every branch's rows on a rank must equal the batch ops over that rank's rows."""
+    import numpy as np
+    import pandas as pd
+    os.environ["ALINK_STREAM_BATCH"] = "40"
+    from alink_amd import (useLocalEnv, BatchOperator, StreamOperator, CollectStreamOp, CsvSinkStreamOp,
+                           VectorAssemblerStreamOp, VectorAssemblerBatchOp, LogisticRegressionTrainBatchOp,
+                           LogisticRegressionPredictStreamOp, LogisticRegressionPredictBatchOp,
+                           StandardScalerTrainBatchOp, StandardScalerPredictStreamOp, StandardScalerPredictBatchOp,
+                           StringIndexerTrainBatchOp, StringIndexerPredictStreamOp, StringIndexerPredictBatchOp,
+                           KMeansTrainBatchOp, KMeansPredictStreamOp, KMeansPredictBatchOp, GbdtTrainBatchOp,
+                           GbdtPredictStreamOp, GbdtPredictBatchOp, TokenizerStreamOp, TokenizerBatchOp,
+                           EvalBinaryClassStreamOp)
+    from alink_amd.common.table import MTable
+    from alink_amd.operator.batch.source import TableSourceBatchOp
+    from alink_amd.operator.stream.source import TableSourceStreamOp
+    from alink_amd.parallel import comm
+    useLocalEnv(1)
+    rng = np.random.default_rng(3)
+    n = 170
+    X = rng.normal(size=(n, 3))
+    df = pd.DataFrame({"x0": X[:, 0], "x1": X[:, 1], "x2": X[:, 2],
+                       "y": (X @ np.array([1.0, -1.0, 0.5]) > 0).astype(int),
+                       "s": [["Alpha Beta", "beta", "GAMMA x"][i % 3] for i in range(n)]})
+    schema = "x0 double, x1 double, x2 double, y int, s string"
+    feats = ["x0", "x1", "x2"]
+    train = BatchOperator.fromDataframe(df, schemaStr=schema)
+    lr = LogisticRegressionTrainBatchOp().setFeatureCols(feats).setLabelCol("y").setMaxIter(5).linkFrom(train)
+    sc = StandardScalerTrainBatchOp().setSelectedCols(feats).linkFrom(train)
+    si = StringIndexerTrainBatchOp().setSelectedCol("s").linkFrom(train)
+    km = KMeansTrainBatchOp().setVectorCol("v").setK(3).setMaxIter(5).linkFrom(
+        VectorAssemblerBatchOp().setSelectedCols(feats).setOutputCol("v").linkFrom(train))
+    gb = GbdtTrainBatchOp().setFeatureCols(feats).setLabelCol("y").setNumTrees(3).setMinSamplesPerLeaf(5) \
+        .linkFrom(train)
+    ws, r = comm.get_world_size(), comm.get_rank()
+    phase = os.environ.get("ALINK_TEST_PHASE", "short")
+    local = df.iloc[:150] if r == 0 else (df.iloc[150:] if phase == "short" else df.iloc[:0])
+    mt = MTable.from_rows([tuple(x) for x in local.itertuples(index=False)], schema)
+    mt.replicated = False
+    branches = {
+        "lr": (lambda s: LogisticRegressionPredictStreamOp(lr).setPredictionCol("p").setPredictionDetailCol("d")
+               .linkFrom(s),
+               lambda b: LogisticRegressionPredictBatchOp().setPredictionCol("p").setPredictionDetailCol("d")
+               .linkFrom(lr, b)),
+        "scaler": (lambda s: StandardScalerPredictStreamOp(sc).linkFrom(s),
+                   lambda b: StandardScalerPredictBatchOp().linkFrom(sc, b)),
+        "indexer": (lambda s: StringIndexerPredictStreamOp(si).setSelectedCol("s").setOutputCol("si").linkFrom(s),
+                    lambda b: StringIndexerPredictBatchOp().setSelectedCol("s").setOutputCol("si").linkFrom(si, b)),
+        "kmeans": (lambda s: KMeansPredictStreamOp(km).setPredictionCol("c").linkFrom(
+                       VectorAssemblerStreamOp().setSelectedCols(feats).setOutputCol("v").linkFrom(s)),
+                   lambda b: KMeansPredictBatchOp().setPredictionCol("c").linkFrom(
+                       km, VectorAssemblerBatchOp().setSelectedCols(feats).setOutputCol("v").linkFrom(b))),
+        "gbdt": (lambda s: GbdtPredictStreamOp(gb).setPredictionCol("g").linkFrom(s),
+                 lambda b: GbdtPredictBatchOp().setPredictionCol("g").linkFrom(gb, b)),
+        "sql_tok": (lambda s: TokenizerStreamOp().setSelectedCol("s").setOutputCol("t").linkFrom(
+                        s.where("x0 > -0.5").select("x0, y, s")),
+                    lambda b: TokenizerBatchOp().setSelectedCol("s").setOutputCol("t").linkFrom(
+                        b.where("x0 > -0.5").select("x0, y, s"))),
+    }
+    src = TableSourceStreamOp(mt)
+    boxes = {k: [] for k in branches}
+    for k, (sf, _) in branches.items():
+        sf(src).link(CollectStreamOp(boxes[k]))
+    ev_box = []
+    EvalBinaryClassStreamOp().setLabelCol("y").setPredictionDetailCol("d").setTimeInterval(0).linkFrom(
+        branches["lr"][0](src)).link(CollectStreamOp(ev_box))
+    CsvSinkStreamOp().setFilePath(os.path.join(os.environ["ALINK_TEST_TMP"], f"uneven_{phase}_{ws}.csv")) \
+        .setOverwriteSink(True).linkFrom(branches["indexer"][0](src))
+    StreamOperator.execute()
+    out["ok"] = {}
+    for k, (_, bf) in branches.items():
+        want = [list(x) for x in bf(TableSourceBatchOp(mt)).getOutputTable().rows()]
+        got = [list(x) for x in boxes[k]]
+        out["ok"][k] = got == want
+        out.setdefault("rows", {})[k] = len(got)
+    out["eval_windows"] = len(ev_box)
+
+
 if __name__ == "__main__":
     run(int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), sys.argv[4], sys.argv[5])

@@ -419,3 +419,17 @@ def test_eval_uneven_ranks_and_mixed_detail_kinds(tmp_path, monkeypatch, phase):
     assert two[0]["batch"]["total"] == two[1]["batch"]["total"] == one["batch"]["total"] == 260
     assert two[0]["batch"]["auc"] == one["batch"]["auc"]
     assert abs(two[0]["batch"]["logloss"] - one["batch"]["logloss"]) < 1e-12
+
+
+@pytest.mark.parametrize("phase", ["short", "empty"])
+def test_stream_ops_uneven_rank_streams_lockstep(tmp_path, monkeypatch, phase):
+    """Two ranks whose streams differ in length (rank 1 ends early, or holds no rows at all) run common stream
+    operators -- predictors, scaler, indexer, SQL where/select, tokenizer, KMeans over a vector assembler, the
+    binary evaluation (a collective per window) and a CSV sink -- through the lockstep rounds' empty micro-batches:
+    every branch equals the batch ops on the rank's own rows."""
+    monkeypatch.setenv("ALINK_TEST_PHASE", phase)
+    outs = _run("stream_ops_uneven", 2, tmp_path)
+    for r, o in enumerate(outs):
+        assert all(o["ok"].values()), (r, o["ok"])
+    assert outs[0]["rows"]["lr"] == 150 and outs[1]["rows"]["lr"] == (20 if phase == "short" else 0)
+    assert outs[0]["eval_windows"] == outs[1]["eval_windows"] > 0
