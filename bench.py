@@ -158,7 +158,11 @@ def main():
     # ---- timed run: W warmup supersteps + exactly K timed supersteps (no early convergence) ----
     marks = {}
 
+    step_t = []
+
     def on_step(step, q):
+        if a.warmup < step < a.warmup + a.steps:
+            step_t.append(time.perf_counter())         # host superstep boundaries inside the window
         if step == a.warmup or step == a.warmup + a.steps:
             if dev.type == "cuda":
                 torch.cuda.synchronize(dev)
@@ -220,6 +224,14 @@ def main():
                 json.dump({"summary": telemetry, "series": tel.series(),
                            "columns": ["t_s", "gfxclk_min_mhz", "gfxclk_max_mhz", "uclk_mhz", "socket_power_w",
                                        "hotspot_c", "hbm_c"]}, f)
+    if telemetry is not None and len(step_t) >= 2:
+        # host-side superstep periods through the window (speculation keeps the GPU one step ahead, so these
+        # follow the device within a step): the first and last fifth, to set against the clock series
+        ts = [marks[a.warmup]] + step_t + [marks[a.warmup + a.steps]]
+        per = [1e3 * (b - x) for x, b in zip(ts[:-1], ts[1:])]
+        q5 = max(1, len(per) // 5)
+        telemetry["step_ms_first_fifth"] = sum(per[:q5]) / q5
+        telemetry["step_ms_last_fifth"] = sum(per[-q5:]) / q5
     win = (telemetry or {}).get("phases", {}).get("window_start->window_end", {})
     per_rank_win = comm.all_gather_object({k: v.get("median") for k, v in win.items() if isinstance(v, dict)})
     if telemetry is not None:
