@@ -18,6 +18,7 @@
 //   * node: {feature slot (-1 leaf), threshold rank k >= 0 or -(categorical map row)-1, first child, #children}.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 namespace {
 
@@ -111,14 +112,182 @@ __global__ __launch_bounds__(TP_ROWS) void tree_predict_kernel(const CT* __restr
     wacc[row] = ws;
 }
 
+// Tree-split walk (the default when the LDS fits): the one-wave kernel above is latency-bound at 2 waves per CU —
+// a 1000-feature code row block takes 64 KiB of LDS, so only two 64-row blocks fit a CU.  Here a 256-thread
+// block shares ONE staged code block between 4 waves: wave w walks trees w, w+4, ... of a group of TP2_G trees for
+// the same 64 rows (4x the waves per CU for the same LDS) and records each (tree, row)'s leaf — or -1 when the walk
+// meets a missing value / unmapped category — in an LDS table; then wave 0 adds the group's leaves in tree order
+// (weight 1: a[i] + dv[i] * 1 == a[i] + dv[i]) and redoes a -1 tree with the reference's weighted fan-out in
+// place.  The sums therefore run in exactly the one-wave kernel's order: bit-identical results.
+constexpr int TP2_G = 64;
+constexpr int TP2_WAVES = 4;
+
+template <typename CT, int NDR>
+__global__ __launch_bounds__(64 * TP2_WAVES) void tree_predict2_kernel(
+    const CT* __restrict__ codes, int64_t n, int stride, const int4* __restrict__ nodes,
+    const double* __restrict__ dist, int nd, const double* __restrict__ wsum, const int* __restrict__ cat, int catw,
+    const int* __restrict__ roots, int ntrees, double* __restrict__ acc, double* __restrict__ wacc,
+    int* __restrict__ err) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    constexpr uint32_t MISS = (uint32_t)(CT)~(CT)0;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int64_t row0 = (int64_t)blockIdx.x * TP_ROWS;
+    const int nrows = n - row0 < TP_ROWS ? (int)(n - row0) : TP_ROWS;
+    {
+        const uint4* src = reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(codes) + row0 * stride);
+        uint4* dst = reinterpret_cast<uint4*>(lds);
+        const int nvec = nrows * stride / 16;
+        for (int e = tid; e < nvec; e += 64 * TP2_WAVES) dst[e] = src[e];
+    }
+    int* leafbuf = reinterpret_cast<int*>(lds + TP_ROWS * stride);
+    __syncthreads();
+    const bool live = lane < nrows;
+    const CT* rc = reinterpret_cast<const CT*>(lds + lane * stride);
+    const int64_t row = row0 + lane;
+    double a[NDR > 0 ? NDR : 1];
+    for (int i = 0; i < (NDR > 0 ? NDR : 1); ++i) a[i] = 0.0;
+    double* ga = acc + row * nd;
+    if (NDR == 0 && wave == 0 && live)
+        for (int i = 0; i < nd; ++i) ga[i] = 0.0;
+    double ws = 0.0;
+    bool dead = false;
+    for (int g0 = 0; g0 < ntrees; g0 += TP2_G) {
+        const int gn = ntrees - g0 < TP2_G ? ntrees - g0 : TP2_G;
+        if (live) {
+            for (int j = wave; j < gn; j += TP2_WAVES) {
+                int node = roots[g0 + j];
+                int res;
+                while (true) {
+                    const int4 nv = nodes[node];
+                    if (nv.x < 0) {
+                        res = node;
+                        break;
+                    }
+                    const uint32_t c = (uint32_t)rc[nv.x];
+                    int child = -1;
+                    if (c != MISS) {
+                        if (nv.y >= 0) child = (int)c <= nv.y ? 0 : 1;
+                        else if ((int)c < catw) child = cat[(int64_t)(-nv.y - 1) * catw + c];
+                    }
+                    if (child < 0) {
+                        res = -1;
+                        break;
+                    }
+                    node = nv.z + child;
+                }
+                leafbuf[j * TP_ROWS + lane] = res;
+            }
+        }
+        __syncthreads();
+        if (wave == 0 && live && !dead) {
+            for (int j = 0; j < gn; ++j) {
+                const int leaf = leafbuf[j * TP_ROWS + lane];
+                if (leaf >= 0) {
+                    ws += 1.0;
+                    const double* dv = dist + (int64_t)leaf * nd;
+                    if (NDR > 0) {
+#pragma unroll
+                        for (int i = 0; i < NDR; ++i) a[i] += dv[i];
+                    } else {
+                        for (int i = 0; i < nd; ++i) ga[i] += dv[i];
+                    }
+                    continue;
+                }
+                // the reference's weighted fan-out for this tree, depth first, added in place (one-wave kernel)
+                int st_node[TP_STACK];
+                double st_w[TP_STACK];
+                int sp = 0, node = roots[g0 + j];
+                double w = 1.0;
+                while (true) {
+                    const int4 nv = nodes[node];
+                    if (nv.x < 0) {
+                        ws += w;
+                        const double* dv = dist + (int64_t)node * nd;
+                        if (NDR > 0) {
+#pragma unroll
+                            for (int i = 0; i < NDR; ++i) a[i] += dv[i] * w;
+                        } else {
+                            for (int i = 0; i < nd; ++i) ga[i] += dv[i] * w;
+                        }
+                        if (sp == 0) break;
+                        --sp;
+                        node = st_node[sp];
+                        w = st_w[sp];
+                        continue;
+                    }
+                    const uint32_t c = (uint32_t)rc[nv.x];
+                    int child = -1;
+                    if (c != MISS) {
+                        if (nv.y >= 0) child = (int)c <= nv.y ? 0 : 1;
+                        else if ((int)c < catw) child = cat[(int64_t)(-nv.y - 1) * catw + c];
+                    }
+                    if (child >= 0) {
+                        node = nv.z + child;
+                        continue;
+                    }
+                    double tot = 0.0;
+                    for (int i = 0; i < nv.w; ++i) tot += wsum[nv.z + i];
+                    if (tot == 0.0 || sp + nv.w - 1 > TP_STACK) {
+                        atomicOr(err, tot == 0.0 ? 1 : 2);
+                        dead = true;
+                        break;
+                    }
+                    for (int i = nv.w - 1; i >= 1; --i) {
+                        st_node[sp] = nv.z + i;
+                        st_w[sp] = w * (wsum[nv.z + i] / tot);
+                        ++sp;
+                    }
+                    w = w * (wsum[nv.z] / tot);
+                    node = nv.z;
+                }
+                if (dead) break;
+            }
+        }
+        __syncthreads();          // the leaf table is rewritten by the next group
+    }
+    if (wave == 0 && live && !dead) {
+        if (NDR > 0)
+#pragma unroll
+            for (int i = 0; i < NDR; ++i) ga[i] = a[i];
+        wacc[row] = ws;
+    }
+}
+
+// ALINK_TREE_PREDICT_KERNEL=1 forces the one-wave kernel (A/B); default 2 = tree-split when its LDS fits
+int tp_variant() {
+    const char* e = getenv("ALINK_TREE_PREDICT_KERNEL");      // read per launch: tests A/B both in one process
+    return (e != nullptr && e[0] == '1') ? 1 : 2;
+}
+
 template <typename CT>
 int launch_tp(const void* codes, int64_t n, int stride, const void* nodes, const double* dist, int nd,
               const double* wsum, const int* cat, int catw, const int* roots, int ntrees, double* acc, double* wacc,
               int* err, hipStream_t st) {
     const int64_t blocks = (n + TP_ROWS - 1) / TP_ROWS;
-    const size_t lds = (size_t)TP_ROWS * stride;
     const CT* c = reinterpret_cast<const CT*>(codes);
     const int4* nv = reinterpret_cast<const int4*>(nodes);
+    const size_t lds2 = (size_t)TP_ROWS * stride + (size_t)TP2_G * TP_ROWS * sizeof(int);
+    if (lds2 <= 160 * 1024 && tp_variant() == 2) {
+#define TP2_LAUNCH(NDR)                                                                                            \
+    do {                                                                                                           \
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(tree_predict2_kernel<CT, NDR>),                    \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2) != hipSuccess)              \
+            return 3;                                                                                              \
+        hipLaunchKernelGGL((tree_predict2_kernel<CT, NDR>), dim3((unsigned)blocks), dim3(64 * TP2_WAVES), lds2,   \
+                           st, c, n, stride, nv, dist, nd, wsum, cat, catw, roots, ntrees, acc, wacc, err);        \
+    } while (0)
+        switch (nd) {
+            case 1: TP2_LAUNCH(1); break;
+            case 2: TP2_LAUNCH(2); break;
+            case 3: TP2_LAUNCH(3); break;
+            case 4: TP2_LAUNCH(4); break;
+            default: TP2_LAUNCH(0); break;
+        }
+#undef TP2_LAUNCH
+        return hipGetLastError() == hipSuccess ? 0 : 2;
+    }
+    const size_t lds = (size_t)TP_ROWS * stride;
 #define TP_LAUNCH(NDR)                                                                                             \
     do {                                                                                                           \
         if (hipFuncSetAttribute(reinterpret_cast<const void*>(tree_predict_kernel<CT, NDR>),                     \

@@ -293,11 +293,18 @@ def test_ftrl_default_mode_is_device_independent_and_auto_is_sharded():
     schema = ", ".join(f"f{i} double" for i in range(6)) + ", label int"
     cols = [f"f{i}" for i in range(6)]
 
+    from alink_amd.common.table import MTable
+    from alink_amd.operator.batch.source import TableSourceBatchOp
+    resetEnv()
+    useLocalEnv(1, device="cpu")
+    init = LogisticRegressionTrainBatchOp().setFeatureCols(cols).setLabelCol("label").setMaxIter(3) \
+        .linkFrom(BatchOperator.fromDataframe(df.iloc[:100], schemaStr=schema))
+    init_rows, init_schema = init.collect(), init.getOutputTable().schema       # one initial model for every run
+
     def run(dev, mode):
         resetEnv()
         useLocalEnv(1, device=dev)
-        model = LogisticRegressionTrainBatchOp().setFeatureCols(cols).setLabelCol("label").setMaxIter(3) \
-            .linkFrom(BatchOperator.fromDataframe(df.iloc[:100], schemaStr=schema))
+        model = TableSourceBatchOp(MTable.from_rows(init_rows, init_schema, replicated=True))
         snaps = []
         op = FtrlTrainStreamOp(model).setFeatureCols(cols).setLabelCol("label").setTimeInterval(1e9) \
             .setAlpha(0.1).setBeta(1.0).setL1(0.01).setL2(0.01)

@@ -185,3 +185,51 @@ def test_device_row_codes_equal_searchsorted(decimals, F, n, row0):
     torch.cuda.synchronize()
     assert a.dtype == b.dtype and a.shape == b.shape
     assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("missing", [0.0, 0.05])
+@pytest.mark.parametrize("nd_classes", [1, 3, 6])
+def test_tree_split_predict_kernel_bit_identical_to_one_wave(missing, nd_classes, monkeypatch):
+    """tree_predict2_kernel (4 waves walk different trees of the same staged rows, wave 0 adds the leaves in tree
+    order and redoes fan-out trees in place) == the one-wave kernel bit for bit: GBDT-like 1-value leaves and
+    multi-class distributions, with and without missing values, more trees than one 64-tree group."""
+    from alink_amd.models.tree.model import LabelCounter, Node, _DeviceForest, _FlatForest
+    from alink_amd.ops import _lib
+    rng = np.random.default_rng(nd_classes)
+    F = 50
+
+    def build(d):
+        if d == 5:
+            return Node(-1, 0.0, LabelCounter(float(rng.integers(1, 50)), 1, list(rng.normal(size=nd_classes))))
+        nd = Node(int(rng.integers(F)), 1.0, LabelCounter(1.0, 1, [0.0] * nd_classes), None,
+                  float(np.round(rng.normal(), 2)))
+        nd.nextNodes = [build(d + 1), build(d + 1)]
+        nd.counter.weightSum = nd.nextNodes[0].counter.weightSum + nd.nextNodes[1].counter.weightSum
+        return nd
+    flat = _FlatForest([build(0) for _ in range(150)], nd_classes)
+    dfo = _DeviceForest(flat, [], [0] * F, "cuda:0")
+    n = 3001
+    cols = {}
+    for f in dfo.cont:
+        x = torch.randn(n, dtype=torch.float64)
+        x[torch.rand(n) < missing] = float("nan")
+        cols[f] = x.cuda()
+    codes = dfo.codes(cols, {}, n)
+    L = _lib.require()
+    out = {}
+    for v in ("1", "2"):
+        monkeypatch.setenv("ALINK_TREE_PREDICT_KERNEL", v)
+        acc = torch.full((n, dfo.nd), 7.0, dtype=torch.float64, device="cuda")
+        wacc = torch.full((n,), 7.0, dtype=torch.float64, device="cuda")
+        err = torch.zeros(1, dtype=torch.int32, device="cuda")
+        assert L.alink_tree_predict(codes.data_ptr(), n, dfo.stride, dfo.code_bytes, dfo.nodes.data_ptr(),
+                                    dfo.dist.data_ptr(), dfo.nd, dfo.wsum.data_ptr(), dfo.cat.data_ptr(),
+                                    int(dfo.cat.shape[1]), dfo.roots.data_ptr(), int(dfo.roots.numel()),
+                                    acc.data_ptr(), wacc.data_ptr(), err.data_ptr(), _lib.stream_ptr("cuda:0")) == 0
+        torch.cuda.synchronize()
+        assert int(err.item()) == 0
+        out[v] = (acc.cpu(), wacc.cpu())
+    assert torch.equal(out["1"][0].view(torch.int64), out["2"][0].view(torch.int64))
+    assert torch.equal(out["1"][1].view(torch.int64), out["2"][1].view(torch.int64))
+    if missing == 0.0:
+        assert bool((out["2"][1] == 150.0).all())
