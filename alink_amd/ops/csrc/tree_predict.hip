@@ -307,13 +307,17 @@ int launch_tp(const void* codes, int64_t n, int stride, const void* nodes, const
     return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
-// Row codes for the walk above, on the device (replaces a batched searchsorted + scatter): block = TC_ROWS rows; the
-// 256 threads take (row = t % TC_ROWS, feature phase = t / TC_ROWS), read their column value (coalesced over rows),
-// count the feature's thresholds below it by a branchless binary search over a power-of-two row of the threshold
-// table (+inf padded; W >= #thresholds + 1, so the count is exact: x <= thr_k <=> code <= k), and write the code
-// into an LDS tile of the rows' code vectors, which then goes out in 16-byte stores.  NaN -> MISS.  Slots the
-// kernel does not own (categorical features) are left 0 for the caller to fill.
-constexpr int TC_ROWS = 64;
+// Row codes for the walk above, on the device (replaces a batched searchsorted + scatter): block = TC_ROWS = 16 rows
+// x 16 feature phases (256 threads).  A thread reads its column value (a wave covers 4 features x 16 consecutive
+// rows: 128-byte segments), counts the feature's thresholds below it by a branchless binary search over a
+// power-of-two row of the threshold table (+inf padded; W >= #thresholds + 1, so the count is exact:
+// x <= thr_k <=> code <= k) and writes the code into an LDS tile of the rows' code vectors, which then goes out in
+// 16-byte stores.  Two features per thread at a time (independent searches interleave), and only 16 rows of LDS
+// per block (16 KiB at 1000 features) so ~8 blocks share a CU: the dependent threshold loads are latency-bound,
+// occupancy is what hides them (round 6: a 64-row tile left 2 blocks per CU, 10.8 ms per 5e5 x 1000 rows).
+// NaN -> MISS.  Slots the kernel does not own (categorical features) are left 0 for the caller to fill.
+constexpr int TC_ROWS = 16;
+constexpr int TC_PH = 256 / TC_ROWS;
 
 template <typename CT>
 __global__ __launch_bounds__(256) void tree_codes_kernel(const double* const* __restrict__ cols, int fc,
@@ -332,12 +336,27 @@ __global__ __launch_bounds__(256) void tree_codes_kernel(const double* const* __
     const int r = tid % TC_ROWS;
     if (r < nrows) {
         CT* rc = reinterpret_cast<CT*>(lds + r * stride);
-        for (int f = tid / TC_ROWS; f < fc; f += 256 / TC_ROWS) {
-            const double x = cols[f][row0 + r0 + r];
+        const int64_t row = row0 + r0 + r;
+        int f = tid / TC_ROWS;
+        for (; f + TC_PH < fc; f += 2 * TC_PH) {
+            const int g = f + TC_PH;
+            const double x0 = cols[f][row], x1 = cols[g][row];
+            const double* t0 = T + (int64_t)f * W;
+            const double* t1 = T + (int64_t)g * W;
+            int lo0 = 0, lo1 = 0;
+            for (int s = W >> 1; s >= 1; s >>= 1) {
+                const double a0 = t0[lo0 + s - 1], a1 = t1[lo1 + s - 1];
+                lo0 += a0 < x0 ? s : 0;
+                lo1 += a1 < x1 ? s : 0;
+            }
+            rc[slots[f]] = x0 != x0 ? MISS : (CT)lo0;
+            rc[slots[g]] = x1 != x1 ? MISS : (CT)lo1;
+        }
+        if (f < fc) {
+            const double x = cols[f][row];
             const double* t = T + (int64_t)f * W;
             int lo = 0;
-            for (int s = W >> 1; s >= 1; s >>= 1)
-                if (t[lo + s - 1] < x) lo += s;
+            for (int s = W >> 1; s >= 1; s >>= 1) lo += t[lo + s - 1] < x ? s : 0;
             rc[slots[f]] = x != x ? MISS : (CT)lo;
         }
     }
@@ -358,7 +377,7 @@ int alink_tree_codes(const void* cols, int fc, const int* slots, const double* T
                      int stride, int code_bytes, void* out, void* stream) {
     if (n <= 0) return 0;
     if (fc < 0 || W < 1 || (W & (W - 1)) != 0 || stride <= 0 || stride % 16 != 0 ||
-        (int64_t)stride * TC_ROWS > 160 * 1024 || (code_bytes != 1 && code_bytes != 2))
+        (int64_t)stride * TC_ROWS > 64 * 1024 || (code_bytes != 1 && code_bytes != 2))
         return 1;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     const size_t lds = (size_t)TC_ROWS * stride;
