@@ -24,6 +24,7 @@
 // [N][D] 16-byte aligned, C row-major bf16 [m][D], cnorm_half[m] = |c|^2/2 in fp32, 1 <= m.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 namespace {
 
@@ -32,6 +33,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int NB_MAX = 8;    // centroid blocks of 32 per chunk -> 256 candidates
+constexpr float kPkNone = -3.4e38f;   // packed-mode initial best (a real or padding score always exceeds it)
 constexpr int WAVES = 4;
 
 template <int KS>
@@ -42,7 +44,20 @@ __device__ __forceinline__ int cswz(int row, int ch) {
     return row * (NCH * 16) + 16 * (ch ^ (row & MASK));
 }
 
-template <int KS, int RG>
+// packed score for the counts-mode argmax: the lane-local candidate index li (16 * block + r, < 128) replaces the
+// low 7 mantissa bits, as 127 - li so equal truncated scores prefer the lower index; one v_max3 then reduces
+// three scores at once (the Lloyd kernel's trick, kmeans_v10.hip pack)
+__device__ __forceinline__ float pack_li(float v, uint32_t li) {
+    return __uint_as_float((__float_as_uint(v) & 0xFFFFFF80u) | (127u - li));
+}
+
+__device__ __forceinline__ float max3f(float a, float b, float c) {
+    float r;
+    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
+template <int KS, int RG, bool PK = false>
 __global__ __launch_bounds__(256, 2) void kmeans_nearest_kernel(
     const __bf16* __restrict__ X, int64_t N, const __bf16* __restrict__ C, const float* __restrict__ chalf,
     int m, int c0, int* __restrict__ out_idx, float* __restrict__ out_d2, int merge,
@@ -108,7 +123,7 @@ __global__ __launch_bounds__(256, 2) void kmeans_nearest_kernel(
                     a = fmaf(v, v, a);
                 }
             xx[q] = a + __shfl_xor(a, 32);
-            best[q] = -3.4e38f;
+            best[q] = PK ? kPkNone : -3.4e38f;
             bidx[q] = 0x7fffffff;
         }
 
@@ -127,6 +142,21 @@ __global__ __launch_bounds__(256, 2) void kmeans_nearest_kernel(
 #pragma unroll
                 for (int q = 0; q < RG; ++q) acc[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cf, xf[q][s], acc[q], 0, 0, 0);
             }
+            if constexpr (PK) {
+                // counts mode: 16 packed scores folded by v_max3 (6 instructions incl. the running best) instead of
+                // a compare and two selects per score.  Exact except for scores equal in their top 25 bits
+                // (relative 2^-16): such near-ties resolve by index, which only shifts k-means|| candidate weights
+#pragma unroll
+                for (int q = 0; q < RG; ++q) {
+                    float p[16];
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) p[r] = pack_li(acc[q][r], (uint32_t)(16 * b + r));
+                    const float m0 = max3f(p[0], p[1], p[2]), m1 = max3f(p[3], p[4], p[5]);
+                    const float m2 = max3f(p[6], p[7], p[8]), m3 = max3f(p[9], p[10], p[11]);
+                    const float m4 = max3f(p[12], p[13], p[14]);
+                    best[q] = max3f(max3f(m0, m1, m2), max3f(m3, m4, p[15]), best[q]);
+                }
+            } else {
 #pragma unroll
             for (int q = 0; q < RG; ++q)
 #pragma unroll
@@ -137,9 +167,18 @@ __global__ __launch_bounds__(256, 2) void kmeans_nearest_kernel(
                         bidx[q] = c;
                     }
                 }
+            }
         }
 #pragma unroll
         for (int q = 0; q < RG; ++q) {
+            if constexpr (PK) {
+                // decode the lane's winner (the sentinel = every score NaN: counted nowhere), then merge the halves
+                const uint32_t bits = __float_as_uint(best[q]);
+                if (bits != __float_as_uint(kPkNone)) {
+                    const int li = 127 - (int)(bits & 127u), bb = li >> 4, r = li & 15;
+                    bidx[q] = 32 * bb + (r & 3) + 8 * (r >> 2) + 4 * h;
+                }
+            }
             float bq = best[q];
             int iq = bidx[q];
             const float ob = __shfl_xor(bq, 32);
@@ -181,23 +220,37 @@ __global__ __launch_bounds__(256, 2) void kmeans_nearest_kernel(
     }
 }
 
-template <int KS, int RG>
-int launch(const void* X, int64_t N, const void* C, const float* chalf, int m, int c0, int* idx, float* d2,
-           int merge, int grid, hipStream_t st, unsigned long long* counts) {
+template <int KS, int RG, bool PK>
+int launch_k(const void* X, int64_t N, const void* C, const float* chalf, int m, int c0, int* idx, float* d2,
+             int merge, int grid, hipStream_t st, unsigned long long* counts) {
     const int nb = (m + 31) / 32;
     const size_t lds = (size_t)nb * 32 * (16 * KS) * 2 + (size_t)nb * 32 * 8;
     static bool attr_set = false;  // > 64 KiB of dynamic LDS must be opted into once per kernel
     if (!attr_set) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void*>(kmeans_nearest_kernel<KS, RG>),
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(kmeans_nearest_kernel<KS, RG, PK>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize,
                                 NB_MAX * 32 * 16 * KS * 2 + NB_MAX * 32 * 8) != hipSuccess)
             return 3;
         attr_set = true;
     }
-    hipLaunchKernelGGL((kmeans_nearest_kernel<KS, RG>), dim3(grid), dim3(256), lds, st,
+    hipLaunchKernelGGL((kmeans_nearest_kernel<KS, RG, PK>), dim3(grid), dim3(256), lds, st,
                        reinterpret_cast<const __bf16*>(X), N, reinterpret_cast<const __bf16*>(C), chalf, m, c0,
                        idx, d2, merge, counts);
     return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+// packed argmax only in counts mode, where no per-row index leaves the kernel (ALINK_KMEANS_COUNTS_PACKED=0: exact)
+inline bool counts_packed() {
+    const char* e = getenv("ALINK_KMEANS_COUNTS_PACKED");
+    return !(e != nullptr && e[0] == '0');
+}
+
+template <int KS, int RG>
+int launch(const void* X, int64_t N, const void* C, const float* chalf, int m, int c0, int* idx, float* d2,
+           int merge, int grid, hipStream_t st, unsigned long long* counts) {
+    if (counts != nullptr && counts_packed())
+        return launch_k<KS, RG, true>(X, N, C, chalf, m, c0, idx, d2, merge, grid, st, counts);
+    return launch_k<KS, RG, false>(X, N, C, chalf, m, c0, idx, d2, merge, grid, st, counts);
 }
 
 // k-means|| first cost pass (KMeansInitCentroids.java: every row's distance to the first, randomly drawn center):

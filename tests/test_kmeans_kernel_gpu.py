@@ -162,20 +162,29 @@ def test_nearest_kernel_two_row_groups_identical(n, m, d, monkeypatch):
 
 @pytest.mark.parametrize("d", [64, 128, 256])
 @pytest.mark.parametrize("n,m", [(1, 1), (33, 40), (4097, 256), (70001, 201), (20001, 300)])
-def test_nearest_counts_equal_bincount_of_nearest(n, m, d):
+def test_nearest_counts_equal_bincount_of_nearest(n, m, d, monkeypatch):
     """Counts mode of the nearest kernel (k-means|| candidate weights in one pass) == bincount of nearest_hip's
-    indices, including a NaN row (counted nowhere by the kernel) and m > 256 (two-step fallback)."""
+    indices, including a NaN row (counted nowhere by the kernel) and m > 256 (two-step fallback): exactly with the
+    exact argmax (ALINK_KMEANS_COUNTS_PACKED=0); with the default packed v_max3 argmax every row is still counted
+    once and only near-ties (scores equal in their top 25 bits) may move between candidates."""
     from alink_amd.ops import kmeans as K
     g = torch.Generator(device="cpu").manual_seed(n + 3 * m + d)
     X = (torch.randn(n, d, generator=g) * 2).to("cuda", torch.bfloat16)
     C = (torch.randn(m, d, generator=g) * 2).to("cuda", torch.float64)
     want = torch.bincount(K.nearest_hip(X, C)[0].long(), minlength=m)
+    monkeypatch.setenv("ALINK_KMEANS_COUNTS_PACKED", "0")
     got = K.nearest_counts_hip(X, C)
     assert got.dtype == torch.int64 and torch.equal(got, want)
-    if n > 1 and m <= 256:
-        X[n // 2] = float("nan")
-        got = K.nearest_counts_hip(X, C)
-        assert int(got.sum()) == n - 1
+    monkeypatch.setenv("ALINK_KMEANS_COUNTS_PACKED", "1")
+    pk = K.nearest_counts_hip(X, C)
+    assert int(pk.sum()) == n and int((pk - want).abs().sum()) <= max(2, n // 5000)
+    for flag in ("0", "1"):
+        monkeypatch.setenv("ALINK_KMEANS_COUNTS_PACKED", flag)
+        if n > 1 and m <= 256:
+            Xn = X.clone()
+            Xn[n // 2] = float("nan")
+            got = K.nearest_counts_hip(Xn, C)
+            assert int(got.sum()) == n - 1
 
 
 @pytest.mark.parametrize("d", [64, 128, 256])
