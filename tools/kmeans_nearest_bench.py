@@ -33,6 +33,29 @@ def main():
         torch.cuda.synchronize()
         print(json.dumps({"m": only_m, "reps": a.reps}), flush=True)
         return
+    if os.environ.get("COUNTS_AB"):    # the k-means|| weights pass: exact vs packed (v_max3) argmax
+        for m in (201, 256):
+            C = X[torch.randint(0, a.rows, (m,), device=dev, generator=g)].double()
+            res = {}
+            for flag in ("0", "1", "0", "1"):
+                os.environ["ALINK_KMEANS_COUNTS_PACKED"] = flag
+                cnt = K.nearest_counts_hip(X, C)
+                torch.cuda.synchronize()
+                ts = []
+                for _ in range(a.reps):
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    K.nearest_counts_hip(X, C)
+                    e1.record()
+                    e1.synchronize()
+                    ts.append(e0.elapsed_time(e1))
+                ts.sort()
+                res[flag] = cnt
+                print(json.dumps({"m": m, "counts_packed": flag, "ms_median": round(ts[len(ts) // 2], 3),
+                                  "ms_min": round(ts[0], 3)}), flush=True)
+            moved = int((res["0"] - res["1"]).abs().sum()) // 2
+            print(json.dumps({"m": m, "rows_moved_by_packing": moved, "rows": a.rows}), flush=True)
+        return
     c = X[12345].double()
     for gm, var in ((4, 0), (4, 1), (4, 2), (4, 3), (2, 2), (6, 0), (8, 3)):
         K.COST1_GRID, K.COST1_VARIANT = gm, var
