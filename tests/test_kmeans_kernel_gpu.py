@@ -165,8 +165,8 @@ def test_nearest_kernel_two_row_groups_identical(n, m, d, monkeypatch):
 def test_nearest_counts_equal_bincount_of_nearest(n, m, d, monkeypatch):
     """Counts mode of the nearest kernel (k-means|| candidate weights in one pass) == bincount of nearest_hip's
     indices, including a NaN row (counted nowhere by the kernel) and m > 256 (two-step fallback): exactly with the
-    exact argmax (ALINK_KMEANS_COUNTS_PACKED=0); with the default packed v_max3 argmax every row is still counted
-    once and only near-ties (scores equal in their top 25 bits) may move between candidates."""
+    default exact argmax; with the packed v_max3 argmax (A/B, ALINK_KMEANS_COUNTS_PACKED=1) every row is still
+    counted once and only near-ties (scores equal in their top 25 bits) may move between candidates."""
     from alink_amd.ops import kmeans as K
     g = torch.Generator(device="cpu").manual_seed(n + 3 * m + d)
     X = (torch.randn(n, d, generator=g) * 2).to("cuda", torch.bfloat16)
