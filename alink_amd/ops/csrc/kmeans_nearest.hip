@@ -104,11 +104,18 @@ __global__ __launch_bounds__(256, 2) void kmeans_nearest_kernel(
         }
     };
 
-    bf16x8 xf[RG][KS], xn[RG][KS];
-    if (g < nsuper) load_frags(g, xf);
+    // RG <= 2: the next iteration's fragments load while this one computes (double buffer); RG 3 / 4 have no
+    // registers for a second set (256 per lane at 2 waves per SIMD) and rely on the other wave of the SIMD instead
+    constexpr bool PF = RG <= 2;
+    bf16x8 xf[RG][KS], xn[PF ? RG : 1][KS];
+    if (PF && g < nsuper) load_frags(g, xf);
     for (; g < nsuper; g += gstride) {
         const int64_t gn = g + gstride;
-        if (gn < nsuper) load_frags(gn, xn);
+        if constexpr (PF) {
+            if (gn < nsuper) load_frags(gn, xn);
+        } else {
+            load_frags(g, xf);
+        }
 
         float xx[RG], best[RG];
         int bidx[RG];
@@ -206,11 +213,13 @@ __global__ __launch_bounds__(256, 2) void kmeans_nearest_kernel(
                 }
             }
         }
-        if (gn < nsuper) {
+        if constexpr (PF) {
+            if (gn < nsuper) {
 #pragma unroll
-            for (int q = 0; q < RG; ++q)
+                for (int q = 0; q < RG; ++q)
 #pragma unroll
-                for (int s = 0; s < KS; ++s) xf[q][s] = xn[q][s];
+                    for (int s = 0; s < KS; ++s) xf[q][s] = xn[q][s];
+            }
         }
     }
     if (counts != nullptr) {      // integer sums: the same totals in any order
@@ -465,7 +474,7 @@ int alink_kmeans_par_pick(const double* cost, int64_t n, int64_t first_row, int6
 int alink_kmeans_nearest_bf16_rg(const void* X, int64_t N, int D, const void* C, const float* chalf, int m, int c0,
                                  int* out_idx, float* out_d2, int merge, int grid, int rg, void* counts_v,
                                  void* stream) {
-    if (N <= 0 || m <= 0 || m > NB_MAX * 32 || grid <= 0 || (rg != 1 && rg != 2) || (rg == 2 && D > 128)) return 1;
+    if (N <= 0 || m <= 0 || m > NB_MAX * 32 || grid <= 0 || rg < 1 || rg > 4 || (rg > 1 && D > 128)) return 1;
     unsigned long long* counts = reinterpret_cast<unsigned long long*>(counts_v);
     if (counts != nullptr && (merge || c0 != 0)) return 1;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
@@ -476,6 +485,9 @@ int alink_kmeans_nearest_bf16_rg(const void* X, int64_t N, int D, const void* C,
             default: return 1;
         }
     }
+    // RG 3 / 4 (D = 128, A/B): each LDS centroid fragment feeds 3 / 4 MFMA chains
+    if (rg == 3) return D == 128 ? launch<8, 3>(X, N, C, chalf, m, c0, out_idx, out_d2, merge, grid, st, counts) : 1;
+    if (rg == 4) return D == 128 ? launch<8, 4>(X, N, C, chalf, m, c0, out_idx, out_d2, merge, grid, st, counts) : 1;
     switch (D) {
         case 64: return launch<4, 1>(X, N, C, chalf, m, c0, out_idx, out_d2, merge, grid, st, counts);
         case 128: return launch<8, 1>(X, N, C, chalf, m, c0, out_idx, out_d2, merge, grid, st, counts);

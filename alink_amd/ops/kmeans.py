@@ -449,7 +449,7 @@ def nearest_counts_hip(X: torch.Tensor, C: torch.Tensor) -> torch.Tensor:
         raise ValueError("centroid shape mismatch")
     chalf = (0.5 * (Cb.float() ** 2).sum(1)).contiguous()
     counts = torch.zeros(m, dtype=torch.int64, device=X.device)
-    rg = 2 if NEAREST_RG == 2 and d <= 128 and m > 32 else 1
+    rg = _rg(d, m)
     rc = L.alink_kmeans_nearest_bf16_rg(X.data_ptr(), n, d, Cb.data_ptr(), chalf.data_ptr(), m, 0, None, None, 0,
                                         NEAREST_GRID * _num_cus(X.device), rg, counts.data_ptr(),
                                         _lib.stream_ptr(X.device))
@@ -693,9 +693,17 @@ def assign(X: torch.Tensor, C: torch.Tensor, chunk: int = 1 << 20) -> Tuple[torc
 NEAREST_DIMS = (64, 128, 256)
 NEAREST_CHUNK = 256
 # 32-row groups per wave iteration of the nearest kernel (2: each LDS centroid fragment feeds two MFMA chains;
-# D = 256 always runs 1)
+# 3 / 4 at D = 128 only, see _rg; D = 256 always runs 1)
 NEAREST_RG = int(os.environ.get("ALINK_KMEANS_NEAREST_RG", "2"))
 NEAREST_GRID = int(os.environ.get("ALINK_KMEANS_NEAREST_GRID", "2"))     # persistent workgroups per CU
+
+
+def _rg(d: int, m: int) -> int:
+    """32-row groups per wave iteration of the nearest kernel: NEAREST_RG (1..4; 3 and 4 only at D = 128, without
+    the fragment prefetch) when more than one centroid block is scanned, else 1."""
+    if m <= 32 or d > 128 or NEAREST_RG <= 1:
+        return 1
+    return NEAREST_RG if d == 128 else 2
 
 
 def nearest_supported(X: torch.Tensor) -> bool:
@@ -745,7 +753,7 @@ def nearest_hip(X: torch.Tensor, C: torch.Tensor) -> Tuple[torch.Tensor, torch.T
     for c0 in range(0, Cb.shape[0], NEAREST_CHUNK):
         m = min(NEAREST_CHUNK, Cb.shape[0] - c0)
         # one centroid block (the first k-means|| cost pass): load-bound, RG = 1 measured 2 % ahead
-        rg = 2 if NEAREST_RG == 2 and d <= 128 and m > 32 else 1
+        rg = _rg(d, m)
         rc = L.alink_kmeans_nearest_bf16_rg(X.data_ptr(), n, d, Cb[c0].data_ptr(), chalf[c0].data_ptr(), m, c0,
                                             idx.data_ptr(), d2.data_ptr(), int(c0 > 0), grid, rg, None, st)
         if rc != 0:

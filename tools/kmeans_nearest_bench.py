@@ -33,6 +33,31 @@ def main():
         torch.cuda.synchronize()
         print(json.dumps({"m": only_m, "reps": a.reps}), flush=True)
         return
+    if os.environ.get("RG_AB"):        # nearest kernel row groups per wave iteration at D = 128
+        for m in (201, 256):
+            C = X[torch.randint(0, a.rows, (m,), device=dev, generator=g)].double()
+            ref = None
+            for rg, gm in ((2, 2), (3, 2), (4, 2), (2, 2), (3, 2), (4, 2)):
+                K.NEAREST_RG, K.NEAREST_GRID = rg, gm
+                cnt = K.nearest_counts_hip(X, C)
+                idx = K.nearest_hip(X[:4_000_000], C)[0]
+                torch.cuda.synchronize()
+                ts = []
+                for _ in range(a.reps):
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    K.nearest_counts_hip(X, C)
+                    e1.record()
+                    e1.synchronize()
+                    ts.append(e0.elapsed_time(e1))
+                ts.sort()
+                if ref is None:
+                    ref = (cnt, idx)
+                same = bool(torch.equal(cnt, ref[0]) and torch.equal(idx, ref[1]))
+                print(json.dumps({"m": m, "rg": rg, "wg_per_cu": gm, "counts_ms_median": round(ts[len(ts) // 2], 3),
+                                  "ms_min": round(ts[0], 3), "identical_to_rg2": same}), flush=True)
+        K.NEAREST_RG, K.NEAREST_GRID = 2, 2
+        return
     if os.environ.get("COUNTS_AB"):    # the k-means|| weights pass: exact vs packed (v_max3) argmax
         for m in (201, 256):
             C = X[torch.randint(0, a.rows, (m,), device=dev, generator=g)].double()
