@@ -57,8 +57,8 @@ __device__ __forceinline__ float max3f(float a, float b, float c) {
     return r;
 }
 
-template <int KS, int RG, bool PK = false>
-__global__ __launch_bounds__(256, 2) void kmeans_nearest_kernel(
+template <int KS, int RG, bool PK = false, bool LAG = false>
+__global__ __launch_bounds__(256, LAG ? 1 : 2) void kmeans_nearest_kernel(
     const __bf16* __restrict__ X, int64_t N, const __bf16* __restrict__ C, const float* __restrict__ chalf,
     int m, int c0, int* __restrict__ out_idx, float* __restrict__ out_d2, int merge,
     unsigned long long* __restrict__ counts) {
@@ -134,8 +134,8 @@ __global__ __launch_bounds__(256, 2) void kmeans_nearest_kernel(
             bidx[q] = 0x7fffffff;
         }
 
-        for (int b = 0; b < nb; ++b) {
-            f32x16 acc[RG];
+        // block b's scores: bias init + KS MFMA k-steps per row group
+        auto issue = [&](int b, f32x16 (&acc)[RG]) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const float bias = lneg[32 * b + (r & 3) + 8 * (r >> 2) + 4 * h];
@@ -149,6 +149,9 @@ __global__ __launch_bounds__(256, 2) void kmeans_nearest_kernel(
 #pragma unroll
                 for (int q = 0; q < RG; ++q) acc[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cf, xf[q][s], acc[q], 0, 0, 0);
             }
+        };
+        // fold block b's scores into the running argmax (blocks in ascending order: ties keep the lowest index)
+        auto reduce = [&](int b, const f32x16 (&acc)[RG]) {
             if constexpr (PK) {
                 // counts mode: 16 packed scores folded by v_max3 (6 instructions incl. the running best) instead of
                 // a compare and two selects per score.  Exact except for scores equal in their top 25 bits
@@ -165,15 +168,33 @@ __global__ __launch_bounds__(256, 2) void kmeans_nearest_kernel(
                 }
             } else {
 #pragma unroll
-            for (int q = 0; q < RG; ++q)
+                for (int q = 0; q < RG; ++q)
 #pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int c = 32 * b + (r & 3) + 8 * (r >> 2) + 4 * h;
-                    if (acc[q][r] > best[q]) {   // c increases with r inside a lane -> strict > keeps the lowest index
-                        best[q] = acc[q][r];
-                        bidx[q] = c;
+                    for (int r = 0; r < 16; ++r) {
+                        const int c = 32 * b + (r & 3) + 8 * (r >> 2) + 4 * h;
+                        if (acc[q][r] > best[q]) {   // c increases with r inside a lane: strict > keeps the lowest
+                            best[q] = acc[q][r];
+                            bidx[q] = c;
+                        }
                     }
-                }
+            }
+        };
+        if constexpr (LAG) {
+            // lag-1 software pipeline: block b+1's MFMAs are issued before block b's scores are read, so the
+            // argmax VALU work never waits on the matrix pipe's result latency (the v10 kernel's interleave)
+            f32x16 accA[RG], accB[RG];
+            issue(0, accA);
+            for (int b = 0; b < nb; b += 2) {
+                if (b + 1 < nb) issue(b + 1, accB);
+                reduce(b, accA);
+                if (b + 2 < nb) issue(b + 2, accA);
+                if (b + 1 < nb) reduce(b + 1, accB);
+            }
+        } else {
+            for (int b = 0; b < nb; ++b) {
+                f32x16 acc[RG];
+                issue(b, acc);
+                reduce(b, acc);
             }
         }
 #pragma unroll
@@ -229,20 +250,20 @@ __global__ __launch_bounds__(256, 2) void kmeans_nearest_kernel(
     }
 }
 
-template <int KS, int RG, bool PK>
+template <int KS, int RG, bool PK, bool LAG>
 int launch_k(const void* X, int64_t N, const void* C, const float* chalf, int m, int c0, int* idx, float* d2,
              int merge, int grid, hipStream_t st, unsigned long long* counts) {
     const int nb = (m + 31) / 32;
     const size_t lds = (size_t)nb * 32 * (16 * KS) * 2 + (size_t)nb * 32 * 8;
     static bool attr_set = false;  // > 64 KiB of dynamic LDS must be opted into once per kernel
     if (!attr_set) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void*>(kmeans_nearest_kernel<KS, RG, PK>),
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(kmeans_nearest_kernel<KS, RG, PK, LAG>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize,
                                 NB_MAX * 32 * 16 * KS * 2 + NB_MAX * 32 * 8) != hipSuccess)
             return 3;
         attr_set = true;
     }
-    hipLaunchKernelGGL((kmeans_nearest_kernel<KS, RG, PK>), dim3(grid), dim3(256), lds, st,
+    hipLaunchKernelGGL((kmeans_nearest_kernel<KS, RG, PK, LAG>), dim3(grid), dim3(256), lds, st,
                        reinterpret_cast<const __bf16*>(X), N, reinterpret_cast<const __bf16*>(C), chalf, m, c0,
                        idx, d2, merge, counts);
     return hipGetLastError() == hipSuccess ? 0 : 2;
@@ -256,12 +277,21 @@ inline bool counts_packed() {
     return e != nullptr && e[0] == '1';
 }
 
+// A/B: ALINK_KMEANS_NEAREST_LAG=1 runs the lag-1 MFMA / argmax software pipeline
+inline bool nearest_lag() {
+    const char* e = getenv("ALINK_KMEANS_NEAREST_LAG");
+    return e != nullptr && e[0] == '1';
+}
+
 template <int KS, int RG>
 int launch(const void* X, int64_t N, const void* C, const float* chalf, int m, int c0, int* idx, float* d2,
            int merge, int grid, hipStream_t st, unsigned long long* counts) {
-    if (counts != nullptr && counts_packed())
-        return launch_k<KS, RG, true>(X, N, C, chalf, m, c0, idx, d2, merge, grid, st, counts);
-    return launch_k<KS, RG, false>(X, N, C, chalf, m, c0, idx, d2, merge, grid, st, counts);
+    const bool pk = counts != nullptr && counts_packed();
+    if (nearest_lag())
+        return pk ? launch_k<KS, RG, true, true>(X, N, C, chalf, m, c0, idx, d2, merge, grid, st, counts)
+                  : launch_k<KS, RG, false, true>(X, N, C, chalf, m, c0, idx, d2, merge, grid, st, counts);
+    return pk ? launch_k<KS, RG, true, false>(X, N, C, chalf, m, c0, idx, d2, merge, grid, st, counts)
+              : launch_k<KS, RG, false, false>(X, N, C, chalf, m, c0, idx, d2, merge, grid, st, counts);
 }
 
 // k-means|| first cost pass (KMeansInitCentroids.java: every row's distance to the first, randomly drawn center):

@@ -158,9 +158,10 @@ def test_nearest_kernel_two_row_groups_identical(n, m, d, monkeypatch):
     monkeypatch.setattr(K, "NEAREST_RG", 2)
     i2, d2 = K.nearest_hip(X, C)
     assert torch.equal(i1, i2) and torch.equal(d1, d2)
-    if d == 128:                  # RG 3 / 4 (no fragment prefetch), counts mode included
-        c1 = K.nearest_counts_hip(X, C)
-        for rg in (3, 4):
+    c1 = K.nearest_counts_hip(X, C)
+    for lag in ("0", "1"):        # the lag-1 MFMA / argmax pipeline (A/B) too
+        monkeypatch.setenv("ALINK_KMEANS_NEAREST_LAG", lag)
+        for rg in ((1, 2, 3, 4) if d == 128 else (1, 2)):     # RG 3 / 4 (no fragment prefetch) at D = 128
             monkeypatch.setattr(K, "NEAREST_RG", rg)
             i3, d3 = K.nearest_hip(X, C)
             assert torch.equal(i1, i3) and torch.equal(d1, d3)

@@ -37,8 +37,10 @@ def main():
         for m in (201, 256):
             C = X[torch.randint(0, a.rows, (m,), device=dev, generator=g)].double()
             ref = None
-            for rg, gm in ((2, 2), (3, 2), (4, 2), (2, 2), (3, 2), (4, 2)):
+            for rg, gm, lag in ((2, 2, "0"), (3, 2, "0"), (2, 2, "1"), (3, 2, "1"), (4, 2, "1"), (2, 1, "1"),
+                                (2, 2, "0"), (3, 2, "0"), (2, 2, "1"), (3, 2, "1"), (4, 2, "1"), (2, 1, "1")):
                 K.NEAREST_RG, K.NEAREST_GRID = rg, gm
+                os.environ["ALINK_KMEANS_NEAREST_LAG"] = lag
                 cnt = K.nearest_counts_hip(X, C)
                 idx = K.nearest_hip(X[:4_000_000], C)[0]
                 torch.cuda.synchronize()
@@ -54,9 +56,11 @@ def main():
                 if ref is None:
                     ref = (cnt, idx)
                 same = bool(torch.equal(cnt, ref[0]) and torch.equal(idx, ref[1]))
-                print(json.dumps({"m": m, "rg": rg, "wg_per_cu": gm, "counts_ms_median": round(ts[len(ts) // 2], 3),
+                print(json.dumps({"m": m, "rg": rg, "wg_per_cu": gm, "lag": lag,
+                                  "counts_ms_median": round(ts[len(ts) // 2], 3),
                                   "ms_min": round(ts[0], 3), "identical_to_rg2": same}), flush=True)
         K.NEAREST_RG, K.NEAREST_GRID = 2, 2
+        os.environ.pop("ALINK_KMEANS_NEAREST_LAG", None)
         return
     if os.environ.get("COUNTS_AB"):    # the k-means|| weights pass: exact vs packed (v_max3) argmax
         for m in (201, 256):
