@@ -694,7 +694,9 @@ NEAREST_DIMS = (64, 128, 256)
 NEAREST_CHUNK = 256
 # 32-row groups per wave iteration of the nearest kernel (2: each LDS centroid fragment feeds two MFMA chains;
 # 3 / 4 at D = 128 only, see _rg; D = 256 always runs 1)
-NEAREST_RG = int(os.environ.get("ALINK_KMEANS_NEAREST_RG", "2"))
+# default 3 (D = 128; D = 64 runs 2): tools/kmeans_nearest_bench.py RG_AB, 1e8 rows x 201 candidates, counts mode
+# 7.03-7.20 ms (RG 2) -> 6.86-6.88 (RG 3), identical results (profiles/kmeans_init_r6.txt)
+NEAREST_RG = int(os.environ.get("ALINK_KMEANS_NEAREST_RG", "3"))
 NEAREST_GRID = int(os.environ.get("ALINK_KMEANS_NEAREST_GRID", "2"))     # persistent workgroups per CU
 
 
