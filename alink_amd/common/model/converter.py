@@ -15,9 +15,9 @@ from __future__ import annotations
 
 from typing import Any, Iterable, List, Optional, Sequence, Tuple
 
-from ..params import Params
 import numpy as np
 
+from ..params import Params
 from ..table import LazyRows, MTable, Row
 from ..types import AlinkType, TableSchema, Types
 
