@@ -47,6 +47,7 @@ def main():
     C = (centers + 0.5 * torch.randn(k, d, device=dev, generator=g)).double()
     row_list = [n] + [int(r) for r in a.sub_rows.split(",") if r]
     ref_small = None
+    ref_out = {}
     for rows in row_list:
         Xs = X[:rows]
         for cfg in a.configs.split(","):
@@ -57,6 +58,10 @@ def main():
                 K.V10_POOL = float(pool)
             alt = flags.endswith("a")          # "v10:1a": serpentine, the direction alternates every launch
             flags = flags.rstrip("a")
+            pfd = "0"
+            if "f" in flags:                   # "v10:1f4": L2 prefetch 4 tiles ahead (ALINK_KMEANS_V10_PFD)
+                flags, pfd = flags.split("f")
+            os.environ["ALINK_KMEANS_V10_PFD"] = pfd
             os.environ["ALINK_KMEANS_KERNEL"] = ver
             for m in [int(v) for v in a.modes.split(",")]:
                 calls = [0]
@@ -68,7 +73,12 @@ def main():
                 out = run()
                 torch.cuda.synchronize()
                 res = {"rows": rows, "k": k, "kernel": K.kernel_version(k), "flags": int(flags), "mode": m,
-                       "serpentine": alt, "pool": K.V10_POOL}
+                       "serpentine": alt, "pool": K.V10_POOL, "pfd": int(pfd)}
+                if m == 0:
+                    key = (rows, alt)
+                    ref_out.setdefault(key, out.clone())
+                    res["identical_to_first_config"] = bool(torch.equal(out.view(torch.int64),
+                                                                        ref_out[key].view(torch.int64)))
                 if m == 0 and rows == n:
                     if ref_small is None:
                         ref_small = K.assign_accumulate_torch(X[:2_000_000], C)
@@ -86,6 +96,7 @@ def main():
                             "min_ms": round(min(times) * 1e3, 4)})
                 print(json.dumps(res), flush=True)
     os.environ.pop("ALINK_KMEANS_KERNEL", None)
+    os.environ.pop("ALINK_KMEANS_V10_PFD", None)
     if a.torch:
         ref = K.assign_accumulate_torch(X, C)
         torch.cuda.synchronize()
