@@ -538,3 +538,22 @@ def test_v10_work_stealing_tail(n, k, grid, pool, monkeypatch):
         assert torch.equal(da, sa)
         assert torch.equal(got[:, 128], ref[:, 128])
         _own_assignment_check(X, C, got, da, k)
+
+
+@pytest.mark.parametrize("pfd", [1, 4, 12])
+@pytest.mark.parametrize("n,k,grid", [(300001, 100, None), (49157, 97, 3), (4097, 16, None), (129, 50, 1),
+                                      (70001, 112, 5)])
+def test_v10_l2_prefetch_identical(n, k, grid, pfd, monkeypatch):
+    """ALINK_KMEANS_V10_PFD: the L2 prefetch loads (LDS-DMA into a sink, 5 loads per staged tile in the vmcnt
+    arithmetic) change no result -- forward and serpentine walks, ids included, and a skipped launch stays skipped."""
+    from alink_amd.ops import kmeans as K
+    X, C = _data(n, k, seed=31)
+    out = {}
+    for v in ("0", str(pfd)):
+        monkeypatch.setenv("ALINK_KMEANS_V10_PFD", v)
+        ids = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+        f = K.assign_accumulate_hip(X, C, grid=grid, assign_out=ids)
+        r = K.assign_accumulate_hip(X, C, grid=grid, reverse=True)
+        torch.cuda.synchronize()
+        out[v] = (f.view(torch.int64).clone(), r.view(torch.int64).clone(), ids.clone())
+    assert all(torch.equal(a, b) for a, b in zip(out["0"], out[str(pfd)]))

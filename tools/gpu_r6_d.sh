@@ -3,5 +3,5 @@
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 cd "$R"
-tools/gpu.sh run pfd_small 120 env ALINK_KMEANS_V10_PFD=4 python -m pytest -x -q tests/test_kmeans_kernel_gpu.py -k "v10 or skipped or serpentine" --timeout 100 || exit 1
+LIMIT=200 tools/gpu.sh tests tests/test_kmeans_kernel_gpu.py -k "prefetch" || exit 1
 tools/gpu.sh run pfd_ab 400 python tools/kmeans_kernel_bench.py --rows 100000000 --k 100 --iters 20 --sub-rows 12500000 --configs v10:1,v10:1f2,v10:1f4,v10:1f8,v10:1f12,v10:1,v10:1f4,v10:1f8 --modes 0 || exit 1
