@@ -268,6 +268,38 @@ def _seed_reference_device(D: torch.Tensor, w: torch.Tensor, k: int, rng, idx0: 
     return chosen
 
 
+def _local_kmeans_kernels(samples: torch.Tensor, w: torch.Tensor, D: torch.Tensor, k: int, max_iter: int,
+                          rng) -> Optional[torch.Tensor]:
+    """``_local_kmeans`` (reference rule, EUCLIDEAN) as two one-workgroup launches and ONE device -> host read:
+    the seeding kernel makes all k picks, the first one included (from the same ``rng.random()`` draw over the
+    sequential cumulative weights), and the Lloyd kernel runs the iterations on the chip
+    (``ops/kmeans.py`` ``seed_ref_hip`` / ``local_lloyd_hip``).  Only an empty cluster brings the host back in,
+    to refill it from the same generator draws in ascending cluster order, as the torch loop does.  Returns None
+    with ``rng`` restored when a pick met an all-zero total or an input is not finite: the caller then runs the
+    torch path, which handles both."""
+    state = rng.bit_generator.state
+    r0 = float(rng.random())
+    U = torch.as_tensor(rng.random(k - 1), dtype=torch.float64, device=samples.device)
+    chosen, mintot = kops.seed_ref_hip(D, w, U, k, idx0=-1, r0=r0)
+    C, assign, status, live = kops.local_lloyd_hip(samples, w, k, chosen=chosen, max_iter=max_iter, mintot=mintot)
+    st = status.cpu().tolist()
+    if st[3] != 0 or not st[4] > 0:
+        rng.bit_generator.state = state
+        return None
+    n = samples.shape[0]
+    it = int(st[0])
+    while True:
+        changed, empty = st[1] != 0, st[2] != 0
+        if empty:
+            for c in np.flatnonzero(live.cpu().numpy() == 0).tolist():
+                C[c] = samples[int(rng.integers(n))]
+        if not changed or it >= max_iter:
+            return C
+        C, assign, status, live = kops.local_lloyd_hip(samples, w, k, C=C, assign=assign, max_iter=max_iter - it)
+        st = status.cpu().tolist()
+        it += int(st[0])
+
+
 def _local_kmeans(samples: torch.Tensor, weights: torch.Tensor, k: int, dist_type: str,
                   max_iter: int = 30, seed: int = 0) -> torch.Tensor:
     """Weighted k-means++ seeding + Lloyd on the k-means|| candidate set (LocalKmeansFunc.java:36-141).
@@ -290,6 +322,11 @@ def _local_kmeans(samples: torch.Tensor, weights: torch.Tensor, k: int, dist_typ
     w = weights.to(torch.float64)
     reference_rule = os.environ.get("ALINK_KMEANS_SEEDING", "reference").lower() != "greedy"
     D = pairwise_distance(samples, samples, dist_type)                                      # [n, n]
+    if (reference_rule and k > 1 and dist_type.upper() == "EUCLIDEAN" and kops.local_lloyd_ok(samples, k)
+            and os.environ.get("ALINK_KMEANS_LOCAL_KERNEL", "1") != "0"):
+        C = _local_kmeans_kernels(samples, w, D, k, max_iter, rng)
+        if C is not None:
+            return C
     if not reference_rule:
         D = _seed_cost(D, dist_type)
     trials = 1 if reference_rule else 2 + int(np.log(max(k, 2)))
@@ -363,11 +400,18 @@ def kmeans_init(X: torch.Tensor, k: int, init_mode: str, init_steps: int, dist_t
         return _fetch_global_rows(X, gidx, counts)
     # k-means||
     centers = _fetch_global_rows(X, [int(rng.integers(n))], counts)
-    cost = _min_dist_to(X, centers, dist_type)
+    psum = None
+    if _hip_nearest_ok(X, dist_type):
+        # the first cost pass also leaves per-wave sums: the threshold's total without a second pass over cost
+        cost, psum = kops.cost1_hip(X, centers[0], with_sum=True)
+    else:
+        cost = _min_dist_to(X, centers, dist_type)
     first_row = int(sum(counts[:comm.get_rank()]))
     rounds = max(0, init_steps - 1)
     for rnd in range(rounds):
-        tot = torch.tensor([float(cost.sum().item())], dtype=torch.float64)
+        local = psum.sum() if psum is not None else cost.sum()
+        psum = None
+        tot = torch.tensor([float(local.item())], dtype=torch.float64)
         comm.all_reduce(tot)
         thre = 2.0 * k / max(float(tot.item()), 1e-300)
         if cost.is_cuda and _lib.available():

@@ -80,10 +80,14 @@ _EXTRA_SIGNATURES = {
     "alink_tree_codes": [_c_vp, _c_int, _c_vp, _c_vp, _c_int, _c_i64, _c_i64, _c_int, _c_int, _c_vp, _c_vp],
     "alink_gbdt_rank_stats": [_c_vp, _c_vp, _c_vp, _c_vp, _c_int, _c_vp, _c_int, _c_vp, _c_vp, _c_vp, _c_vp],
     "alink_kmeans_seed_ref": [_c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_int, _c_vp, _c_vp, _c_vp],
+    "alink_kmeans_seed_ref2": [_c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_int, _c_d, _c_vp, _c_vp, _c_vp, _c_vp],
+    "alink_kmeans_local_lloyd": [_c_vp, _c_vp, _c_int, _c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_int, _c_vp,
+                                 _c_vp, _c_vp, _c_vp, _c_vp],
     "alink_kmeans_par_pick": [_c_vp, _c_i64, _c_i64, _c_i64, _c_d, _c_vp, _c_i64, _c_vp, _c_vp],
     "alink_kmeans_nearest_bf16": [_c_vp, _c_i64, _c_int, _c_vp, _c_vp, _c_int, _c_int, _c_vp, _c_vp, _c_int,
                                   _c_int, _c_vp],
     "alink_kmeans_cost1_bf16": [_c_vp, _c_i64, _c_int, _c_vp, _c_vp, _c_int, _c_int, _c_vp],
+    "alink_kmeans_cost1_bf16_sum": [_c_vp, _c_i64, _c_int, _c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_vp],
     "alink_kmeans_nearest_bf16_rg": [_c_vp, _c_i64, _c_int, _c_vp, _c_vp, _c_int, _c_int, _c_vp, _c_vp, _c_int,
                                      _c_int, _c_int, _c_vp, _c_vp],
     "alink_linear_grad_f64": [_c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_int, _c_int, _c_d, _c_vp, _c_int, _c_vp,

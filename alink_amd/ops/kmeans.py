@@ -415,9 +415,11 @@ COST1_GRID = int(os.environ.get("ALINK_KMEANS_COST1_GRID", "4"))    # streaming 
 COST1_VARIANT = int(os.environ.get("ALINK_KMEANS_COST1_VARIANT", "1"))  # csrc: rows in flight / load policy
 
 
-def cost1_hip(X: torch.Tensor, c: torch.Tensor) -> torch.Tensor:
+def cost1_hip(X: torch.Tensor, c: torch.Tensor, with_sum: bool = False):
     """fp64 [N] Euclidean distance of every row of X to ONE center (rounded to bf16: k-means|| centers are rows of
-    X) -- ``csrc/kmeans_nearest.hip`` kmeans_cost1_kernel, one coalesced streaming pass (the first k-means|| cost)."""
+    X) -- ``csrc/kmeans_nearest.hip`` kmeans_cost1_kernel, one coalesced streaming pass (the first k-means|| cost).
+    ``with_sum``: also the per-wave sums of the costs (fp64 [waves], a fixed order for a given grid), so the
+    oversampling threshold's total needs no second pass over the [N] costs: returns (cost, partial sums)."""
     L = _lib.require()
     if not nearest_supported(X):
         raise ValueError("cost1_hip needs contiguous bf16 [N, D] on GPU with D in (64, 128, 256)")
@@ -426,11 +428,14 @@ def cost1_hip(X: torch.Tensor, c: torch.Tensor) -> torch.Tensor:
     if cb.numel() != d:
         raise ValueError("center shape mismatch")
     cost = torch.empty(n, dtype=torch.float64, device=X.device)
-    rc = L.alink_kmeans_cost1_bf16(X.data_ptr(), n, d, cb.data_ptr(), cost.data_ptr(),
-                                   COST1_GRID * _num_cus(X.device), COST1_VARIANT, _lib.stream_ptr(X.device))
+    grid = COST1_GRID * _num_cus(X.device)
+    wsum = torch.empty(grid * 4, dtype=torch.float64, device=X.device) if with_sum else None
+    rc = L.alink_kmeans_cost1_bf16_sum(X.data_ptr(), n, d, cb.data_ptr(), cost.data_ptr(),
+                                       None if wsum is None else wsum.data_ptr(), grid, COST1_VARIANT,
+                                       _lib.stream_ptr(X.device))
     if rc != 0:
         raise RuntimeError(f"alink_kmeans_cost1_bf16 failed: {rc}")
-    return cost
+    return (cost, wsum) if with_sum else cost
 
 
 def nearest_counts_hip(X: torch.Tensor, C: torch.Tensor) -> torch.Tensor:
@@ -734,6 +739,79 @@ def par_pick_hip(cost: torch.Tensor, first_row: int, key: int, thre: float) -> t
         if c <= cap:
             return torch.sort(out[:c]).values
         cap = c
+
+
+def seed_ref_hip(D: torch.Tensor, w: torch.Tensor, U: torch.Tensor, k: int, idx0: int = -1,
+                 r0: float = 0.0, prof: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """The reference seeding rule's k picks over n <= 4096 k-means|| candidates in one launch
+    (``csrc/kmeans_nearest.hip`` ``kmeans_seed_ref_kernel``): D [n, n] fp64 plain distances, w [n] weights,
+    U [k-1] the picks' uniforms.  ``idx0 < 0``: the first pick too, from the uniform ``r0`` over the sequential
+    cumulative weights.  Returns (chosen int64 [k], mintot fp64 [1]) on the device, nothing read back."""
+    L = _lib.require()
+    n = int(D.shape[0])
+    chosen = torch.empty(k, dtype=torch.int64, device=D.device)
+    mintot = torch.full((1,), float("inf"), dtype=torch.float64, device=D.device)
+    Dc, wc, Uc = D.contiguous(), w.contiguous(), U.contiguous()
+    rc = L.alink_kmeans_seed_ref2(Dc.data_ptr(), wc.data_ptr(), Uc.data_ptr(), n, int(k), int(idx0), float(r0),
+                                  chosen.data_ptr(), mintot.data_ptr(), None if prof is None else prof.data_ptr(),
+                                  _lib.stream_ptr(D.device))
+    if rc != 0:
+        raise RuntimeError(f"alink_kmeans_seed_ref2 failed: {rc}")
+    return chosen, mintot
+
+
+LOCAL_LLOYD_NMAX = 4096
+
+
+def local_lloyd_lds(n: int, d: int, k: int) -> int:
+    """LDS bytes of ``kmeans_local_lloyd_kernel`` (csrc/kmeans_nearest.hip local_lloyd_lds)."""
+    return (k * (d + 1) + 2 * k + 2 * n) * 8 + (2 * n + k + 1) * 4
+
+
+def local_lloyd_ok(samples: torch.Tensor, k: int) -> bool:
+    """The one-workgroup weighted Lloyd applies: fp64 [n, d] candidates on the GPU, n <= 4096, and the
+    centroids (rows padded to d + 1) plus the per-sample state fit the 160 KiB LDS."""
+    if not (samples.is_cuda and samples.dtype == torch.float64 and samples.dim() == 2):
+        return False
+    n, d = samples.shape
+    return (1 <= n <= LOCAL_LLOYD_NMAX and d >= 1 and 1 <= k <= n and local_lloyd_lds(n, d, k) <= 160 * 1024
+            and _lib.available())
+
+
+def local_lloyd_hip(X: torch.Tensor, w: torch.Tensor, k: int, C: Optional[torch.Tensor] = None,
+                    chosen: Optional[torch.Tensor] = None, assign: Optional[torch.Tensor] = None,
+                    max_iter: int = 30, mintot: Optional[torch.Tensor] = None, prof: Optional[torch.Tensor] = None):
+    """Weighted Lloyd (EUCLIDEAN) on the k-means|| candidates in ONE workgroup, every iteration on the chip
+    (``csrc/kmeans_nearest.hip`` ``kmeans_local_lloyd_kernel``): runs until the assignment is unchanged, a cluster
+    is empty (the caller refills it and calls again with ``C`` / ``assign``) or ``max_iter`` iterations.  The
+    start centroids are ``C`` (updated in place) or the rows ``X[chosen]``.  Returns (C [k, d], assign int64 [n],
+    status fp64 [6] = iterations, changed, empty, non-finite input, mintot, chosen[0], live uint8 [k]), all on the
+    device: the caller reads ``status`` once.  ``prof``: int64 [50] receives 100 MHz wall-clock stamps (setup, then
+    six phases per iteration for the first 8; tools/kmeans_local_bench.py)."""
+    L = _lib.require()
+    n, d = X.shape
+    dev = X.device
+    Xc = X.contiguous()
+    wc = w.to(torch.float64).contiguous()
+    if C is None:
+        if chosen is None:
+            raise ValueError("local_lloyd_hip needs C or chosen")
+        C = torch.empty((k, d), dtype=torch.float64, device=dev)
+    if assign is None:
+        assign = torch.full((n,), -1, dtype=torch.int64, device=dev)
+    ct = (k + 63) // 64
+    bd = torch.empty(n * ct, dtype=torch.float64, device=dev)
+    bi = torch.empty(n * ct, dtype=torch.int32, device=dev)
+    status = torch.zeros(6, dtype=torch.float64, device=dev)
+    live = torch.empty(k, dtype=torch.uint8, device=dev)
+    ch = chosen.contiguous() if chosen is not None else None
+    rc = L.alink_kmeans_local_lloyd(Xc.data_ptr(), wc.data_ptr(), n, d, int(k), None if ch is None else ch.data_ptr(),
+                                    C.data_ptr(), assign.data_ptr(), bd.data_ptr(), bi.data_ptr(), int(max_iter),
+                                    None if mintot is None else mintot.data_ptr(), status.data_ptr(), live.data_ptr(),
+                                    None if prof is None else prof.data_ptr(), _lib.stream_ptr(dev))
+    if rc != 0:
+        raise RuntimeError(f"alink_kmeans_local_lloyd failed: {rc}")
+    return C, assign, status, live
 
 
 def nearest_hip(X: torch.Tensor, C: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:

@@ -209,6 +209,10 @@ def test_first_cost_kernel_matches_fp64(n, d):
     assert got.dtype == torch.float64 and got.shape == (n,)
     torch.testing.assert_close(got, ref, rtol=2e-6, atol=1e-6)
     assert float(got[n // 2]) == 0.0
+    got2, ws = K.cost1_hip(X, c, with_sum=True)        # per-wave sums: the same costs, their total, deterministic
+    assert torch.equal(got2, got)
+    torch.testing.assert_close(ws.sum(), got.sum(), rtol=1e-12, atol=0.0)
+    assert torch.equal(ws, K.cost1_hip(X, c, with_sum=True)[1])
     if n > 2:
         X[0, d - 1] = float("nan")
         X[1, 0] = float("inf")
@@ -517,6 +521,97 @@ def test_seed_ref_kernel_equals_host_on_ties_and_wide_weights(n, k):
         assert (a is None) == (b is None)
         if a is not None:
             assert torch.equal(a.cpu(), b)
+
+
+@pytest.mark.parametrize("n,k", [(1, 1), (201, 100), (700, 120), (4096, 40)])
+def test_seed_ref_kernel_first_pick(n, k):
+    """idx0 < 0: the kernel also makes the first pick, as the host does (searchsorted over the SEQUENTIAL cumulative
+    weights, side left), then the same picks as with that index given."""
+    import numpy as np
+    from alink_amd.models.clustering import kmeans as km
+    from alink_amd.ops import kmeans as K
+    g = torch.Generator(device="cpu").manual_seed(n + 7)
+    S = torch.randint(0, 4, (n, 5), generator=g).to(torch.float64)
+    D = km.pairwise_distance(S, S, "EUCLIDEAN").cuda()
+    w = torch.pow(10.0, torch.randint(-3, 16, (n,), generator=g).to(torch.float64))
+    w[torch.rand(n, generator=g) < 0.2] = 0.0
+    w[0] = 1.0
+    for seed in range(4):
+        rng = np.random.default_rng(seed)
+        r0 = float(rng.random())
+        U = torch.as_tensor(rng.random(max(k - 1, 0)), dtype=torch.float64)
+        cum = np.cumsum(w.numpy())
+        idx = int(min(np.searchsorted(cum, r0 * cum[-1], side="left"), n - 1))
+        a, ma = K.seed_ref_hip(D, w.cuda(), U.cuda(), k, idx0=-1, r0=r0)
+        b, mb = K.seed_ref_hip(D, w.cuda(), U.cuda(), k, idx0=idx)
+        assert int(a[0]) == idx
+        assert torch.equal(a, b) and torch.equal(ma, mb)
+
+
+def _lloyd_case(n, d, k, seed, dup=False):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    X = torch.randn(n, d, generator=g, dtype=torch.float64) * 3
+    if dup:
+        X = torch.cat([X[: n // 2]] * 2 + [X[: n - 2 * (n // 2)]])
+    # weights >= 1 (k-means|| candidate counts): zero weights plus refills make exact-copy centroids whose
+    # distances tie at the rounding level, which two summation orders may break differently
+    w = torch.randint(1, 40, (n,), generator=g).to(torch.float64)
+    return X.cuda(), w.cuda()
+
+
+@pytest.mark.parametrize("n,d,k,dup", [(201, 128, 100, False), (230, 128, 100, True), (600, 16, 150, False),
+                                       (4096, 8, 64, False), (65, 3, 64, False), (129, 256, 20, True)])
+def test_local_kmeans_kernels_equal_torch_path(n, d, k, dup, monkeypatch):
+    """The one-workgroup seeding + Lloyd kernels (ALINK_KMEANS_LOCAL_KERNEL, default on) return the torch device
+    path's centroids: the same picks (fallback to the torch path when a pick meets an all-zero total), the same
+    assignments each iteration, sums equal up to fp64 summation order; empty clusters (zero weights, duplicated
+    rows) refilled from the same generator draws; run-to-run deterministic."""
+    from alink_amd.models.clustering import kmeans as km
+    from alink_amd.ops import kmeans as K
+    monkeypatch.delenv("ALINK_KMEANS_SEEDING", raising=False)
+    X, w = _lloyd_case(n, d, k, seed=n + k, dup=dup)
+    assert K.local_lloyd_ok(X, k)
+    monkeypatch.setenv("ALINK_KMEANS_LOCAL_KERNEL", "0")
+    ref = km._local_kmeans(X, w, k, "EUCLIDEAN", seed=2)
+    monkeypatch.setenv("ALINK_KMEANS_LOCAL_KERNEL", "1")
+    got = km._local_kmeans(X, w, k, "EUCLIDEAN", seed=2)
+    assert torch.allclose(got, ref, rtol=1e-11, atol=1e-11)
+    assert torch.equal(got, km._local_kmeans(X, w, k, "EUCLIDEAN", seed=2))
+
+
+def test_local_lloyd_kernel_iterations_and_empty_exit():
+    """The Lloyd kernel stops at the first empty cluster (live flags mark it, centroid kept), and max_iter = 1
+    runs exactly one iteration whose assignment is the torch argmin of the start centroids."""
+    from alink_amd.models.clustering import kmeans as km
+    from alink_amd.ops import kmeans as K
+    X, w = _lloyd_case(300, 32, 40, seed=5)
+    C0 = X[:40].clone()
+    C0[7] = 1e3                                   # far away: nobody's nearest -> empty in iteration 1
+    C, a, st, live = K.local_lloyd_hip(X, w, 40, C=C0.clone(), max_iter=30)
+    st = st.cpu().tolist()
+    assert st[0] == 1 and st[1] == 1 and st[2] == 1 and st[3] == 0
+    assert int(live[7]) == 0 and int(live.sum()) == 39
+    assert torch.equal(C[7], C0[7])
+    assert torch.equal(a, km.pairwise_distance(X, C0, "EUCLIDEAN").argmin(1))
+    C1, a1, st1, _ = K.local_lloyd_hip(X, w, 40, C=X[:40].clone(), max_iter=1)
+    assert st1.cpu().tolist()[0] == 1
+    assert torch.equal(a1, km.pairwise_distance(X, X[:40], "EUCLIDEAN").argmin(1))
+
+
+def test_local_lloyd_kernel_non_finite_falls_back(monkeypatch):
+    """A non-finite candidate: the kernel writes nothing and flags it; _local_kmeans takes the torch path with the
+    generator untouched (same result as the kernel switched off)."""
+    from alink_amd.models.clustering import kmeans as km
+    from alink_amd.ops import kmeans as K
+    X, w = _lloyd_case(120, 16, 10, seed=9)
+    X[17, 3] = float("nan")
+    _, _, st, _ = K.local_lloyd_hip(X, w, 10, C=X[20:30].clone(), max_iter=5)
+    assert st.cpu().tolist()[3] == 1
+    monkeypatch.setenv("ALINK_KMEANS_LOCAL_KERNEL", "0")
+    ref = km._local_kmeans(X, w, 10, "EUCLIDEAN", seed=1)
+    monkeypatch.setenv("ALINK_KMEANS_LOCAL_KERNEL", "1")
+    got = km._local_kmeans(X, w, 10, "EUCLIDEAN", seed=1)
+    assert torch.equal(torch.nan_to_num(got, nan=7.0), torch.nan_to_num(ref, nan=7.0))
 
 
 @pytest.mark.parametrize("pool", [0.0, 0.1, 0.5, 1.0])
