@@ -521,19 +521,39 @@ class KMeansUpdateCentroids(ComputeFunction):
                 # fp64 quotients the generic path computes, and the rare path issues no torch kernel that the
                 # supersteps do not already use (a first use of e.g. norm / nonzero costs a lazy code-object load,
                 # ~100 ms, inside the first job's supersteps)
-                cnt_h = cnt.cpu().numpy()
+                # one stream sync for all three reads (async copies into pinned buffers), one H2D copy back
+                kk, dd = C.shape
+                use_prev = prev is not None and prev.shape[1] == dd and prev.dtype == C.dtype
+                pin = C.is_cuda
+                h_cnt = torch.empty(cnt.shape, dtype=cnt.dtype, pin_memory=pin)
+                h_C = torch.empty(C.shape, dtype=C.dtype, pin_memory=pin)
+                h_prev = torch.empty((min(prev.shape[0], kk) if use_prev else 0, dd), dtype=C.dtype, pin_memory=pin)
+                h_cnt.copy_(cnt, non_blocking=pin)
+                h_C.copy_(C, non_blocking=pin)
+                if use_prev:
+                    h_prev.copy_(prev[:h_prev.shape[0]], non_blocking=pin)
+                if pin:
+                    torch.cuda.current_stream(C.device).synchronize()
+                cnt_h = h_cnt.numpy()
                 keep = np.flatnonzero(cnt_h > 0)
-                C_h = C.cpu().numpy()[keep]
-                C = torch.from_numpy(C_h).to(C.device)
+                C_h = h_C.numpy()[keep]
                 # the criterion's shift (first k rows of the previous centroids vs the new ones), on the host too
                 shift_h = None
-                if prev is not None and prev.shape[0] >= len(keep) and prev.shape[1] == C_h.shape[1]:
-                    dlt = prev[:len(keep)].cpu().numpy() - C_h
+                if use_prev and h_prev.shape[0] >= len(keep):
+                    dlt = h_prev.numpy()[:len(keep)] - C_h
                     shift_h = float(np.sqrt((dlt * dlt).sum(1)).max()) if len(keep) else None
+                # the kept centroids and their weights in one pinned block -> one copy; C / weights are views of it
+                kk2 = len(keep)
+                h_pack = torch.empty(kk2 * dd + kk2, dtype=C.dtype, pin_memory=pin)
+                hp = h_pack.numpy()
+                hp[:kk2 * dd] = C_h.reshape(-1)
+                hp[kk2 * dd:] = cnt_h[keep]
+                pack = h_pack.to(C.device, non_blocking=pin)
+                C = pack[:kk2 * dd].view(kk2, dd)
                 ctx.putObj("maxShift", shift_h)
                 tgt[0] = ctx.getStepNo()
                 tgt[1] = C
-                ctx.putObj("lastWeights", torch.from_numpy(cnt_h[keep]).to(cnt.device))
+                ctx.putObj("lastWeights", pack[kk2 * dd:].to(cnt.dtype))
                 ctx.putObj(K, int(C.shape[0]))
                 return
             if not has_empty:
