@@ -84,6 +84,8 @@ def main():
     ap.add_argument("--convergence-first", type=int, default=0,
                     help="1: the untimed convergence runs before the timed run (0: after it)")
     ap.add_argument("--telemetry", type=int, default=1, help="1: sample GPU clocks / power (amdsmi) during the run")
+    ap.add_argument("--kernel-timing", type=int, default=1,
+                    help="1: HIP events around every assign launch in the window (per-rank kernel time fields)")
     a = ap.parse_args()
 
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -176,7 +178,7 @@ def main():
                 kops.kernel_timing_collect()
                 marks["oneshot0"] = comm.STATS.oneshot
                 comm.device_timing(dev.type == "cuda")
-                kops.kernel_timing(True)
+                kops.kernel_timing(bool(a.kernel_timing))
             else:
                 mark("window_end")
                 comm.device_timing(False)

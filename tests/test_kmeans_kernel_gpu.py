@@ -1,4 +1,6 @@
 """Numerics of the fused HIP KMeans assign+accumulate kernel vs a PyTorch fp32/fp64 reference."""
+import os
+
 import pytest
 import torch
 
@@ -635,20 +637,40 @@ def test_v10_work_stealing_tail(n, k, grid, pool, monkeypatch):
         _own_assignment_check(X, C, got, da, k)
 
 
-@pytest.mark.parametrize("pfd", [1, 4, 12])
-@pytest.mark.parametrize("n,k,grid", [(300001, 100, None), (49157, 97, 3), (4097, 16, None), (129, 50, 1),
-                                      (70001, 112, 5)])
-def test_v10_l2_prefetch_identical(n, k, grid, pfd, monkeypatch):
-    """ALINK_KMEANS_V10_PFD: the L2 prefetch loads (LDS-DMA into a sink, 5 loads per staged tile in the vmcnt
-    arithmetic) change no result -- forward and serpentine walks, ids included, and a skipped launch stays skipped."""
+_PFD_CASES = [(300001, 100, None), (49157, 97, 3), (4097, 16, None), (129, 50, 1), (70001, 112, 5)]
+
+
+def _pfd_identity_check():
+    """Runs in a child process on the KM10_PFD=1 variant library (ALINK_HIP_LIB): every prefetch distance returns
+    bit-identical sums, counts and ids to distance 0, forward and serpentine."""
     from alink_amd.ops import kmeans as K
-    X, C = _data(n, k, seed=31)
-    out = {}
-    for v in ("0", str(pfd)):
-        monkeypatch.setenv("ALINK_KMEANS_V10_PFD", v)
-        ids = torch.full((n,), -1, dtype=torch.int32, device="cuda")
-        f = K.assign_accumulate_hip(X, C, grid=grid, assign_out=ids)
-        r = K.assign_accumulate_hip(X, C, grid=grid, reverse=True)
-        torch.cuda.synchronize()
-        out[v] = (f.view(torch.int64).clone(), r.view(torch.int64).clone(), ids.clone())
-    assert all(torch.equal(a, b) for a, b in zip(out["0"], out[str(pfd)]))
+    for n, k, grid in _PFD_CASES:
+        X, C = _data(n, k, seed=31)
+        out = {}
+        for v in ("0", "1", "4", "12"):
+            os.environ["ALINK_KMEANS_V10_PFD"] = v
+            ids = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+            f = K.assign_accumulate_hip(X, C, grid=grid, assign_out=ids)
+            r = K.assign_accumulate_hip(X, C, grid=grid, reverse=True)
+            torch.cuda.synchronize()
+            out[v] = (f.view(torch.int64).clone(), r.view(torch.int64).clone(), ids.clone())
+        for v in ("1", "4", "12"):
+            assert all(torch.equal(a, b) for a, b in zip(out["0"], out[v])), (n, k, grid, v)
+    print("PFD_IDENTICAL_OK")
+
+
+def test_v10_l2_prefetch_identical():
+    """ALINK_KMEANS_V10_PFD (the L2 prefetch A/B, compiled only into variants/libalink_hip_pfd.so by
+    tools/build_kmeans_variants.sh pfd -- the default build compiles it out): the prefetch loads (LDS-DMA into a
+    sink, 5 loads per staged tile in the vmcnt arithmetic) change no result.  Run in a child process because the
+    kernel library is loaded once per process."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    lib = os.path.join(root, "variants", "libalink_hip_pfd.so")
+    if not os.path.exists(lib):
+        pytest.skip("variants/libalink_hip_pfd.so not built (tools/build_kmeans_variants.sh pfd)")
+    env = dict(os.environ, ALINK_HIP_LIB=lib, PYTHONPATH=root)
+    r = subprocess.run([sys.executable, "-c", "import tests.test_kmeans_kernel_gpu as t; t._pfd_identity_check()"],
+                       cwd=root, env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0 and "PFD_IDENTICAL_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]

@@ -9,6 +9,7 @@
 #   dot2pair : dot2 + pair
 #   timing   : -DKM10_TIMING=1 (per-workgroup wall-clock stamps; tools/kmeans_wg_timing.py).  `... timing` builds
 #              only this one
+#   pfd      : -DKM10_PFD=1 (the ALINK_KMEANS_V10_PFD L2 prefetch A/B; `... pfd` builds only this one)
 set -e
 cd "$(dirname "$0")/.."
 mkdir -p variants
@@ -24,6 +25,7 @@ build_var() {
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "variants/libalink_hip_$name.so" $objs "$d/kmeans_v10.o"
 }
 [ "$1" = timing ] && { build_var timing base "-DKM10_TIMING=1"; exit 0; }
+[ "$1" = pfd ] && { build_var pfd base "-DKM10_PFD=1"; exit 0; }
 build_var d16 base "-DKM10_ACC_B32=0"
 build_var pk pk "-DKM10_ACC_B32=0"
 build_var pair base "-DKM10_ACC_B32=0 -DKM10_PAIRMAX=1"
@@ -31,3 +33,4 @@ build_var pkpair pk "-DKM10_ACC_B32=0 -DKM10_PAIRMAX=1"
 build_var dot2 dot2 "-DKM10_ACC_B32=1"
 build_var dot2pair dot2 "-DKM10_ACC_B32=1 -DKM10_PAIRMAX=1"
 build_var timing base "-DKM10_TIMING=1"
+build_var pfd base "-DKM10_PFD=1"
