@@ -1,9 +1,11 @@
 """GPU clock / power / temperature telemetry sampled next to a benchmark (``amdsmi`` gpu_metrics).
 
 ``GpuTelemetry(device)`` finds the amdsmi handle of a torch device (by PCI bus id), ``start()`` runs a daemon
-thread that reads the SMU's gpu_metrics table every ``interval_s`` (one ioctl-backed read; the ctypes call
-releases the GIL), ``mark(name)`` time-stamps a phase boundary (e.g. the timed window of bench.py) and ``stop()``
-returns a JSON-ready summary:
+thread that reads the SMU's gpu_metrics table every ``interval_s``, ``mark(name)`` time-stamps a phase boundary
+(e.g. the timed window of bench.py) and ``stop()`` returns a JSON-ready summary.  ``process=True`` (bench.py) runs
+the sampler as a child process instead (``telemetry_child.py``): decoding a gpu_metrics table is Python work that
+holds the GIL, and a thread doing it every 5 ms cost the host-heavy KMeans convergence run ~0.9 ms of 43
+(profiles/kmeans_telemetry_r6.txt); the child shares only the monotonic clock.  The summary holds:
 
 * per phase: min / median / max of the gfx clock (over XCDs: ``current_gfxclks``), memory clock (``current_uclk``),
   socket power, hotspot and HBM temperature;
@@ -17,7 +19,11 @@ job (SURVEY §5.5 metrics).
 """
 from __future__ import annotations
 
+import json
+import os
 import statistics
+import subprocess
+import sys
 import threading
 import time
 from typing import Dict, List, Optional
@@ -56,8 +62,11 @@ def _sum_list(v) -> Optional[float]:
 
 
 class GpuTelemetry:
-    def __init__(self, device=None, interval_s: float = 0.005):
+    def __init__(self, device=None, interval_s: float = 0.005, process: bool = False):
         self.interval_s = float(interval_s)
+        self.process = bool(process)
+        self._child: Optional[subprocess.Popen] = None
+        self._bdf = "-"
         self.error: Optional[str] = None
         self._h = None
         self._smi = None
@@ -75,6 +84,8 @@ class GpuTelemetry:
             self._h = self._match(amdsmi, handles, device)
             if self._h is None:
                 self.error = f"no amdsmi handle matches {device}"
+            elif len(handles) > 1:
+                self._bdf = amdsmi.amdsmi_get_gpu_device_bdf(self._h)
         except Exception as e:      # not installed / no driver access on this host
             self.error = f"amdsmi unavailable: {type(e).__name__}: {e}"
 
@@ -135,15 +146,38 @@ class GpuTelemetry:
 
     def start(self) -> "GpuTelemetry":
         self._t0 = time.perf_counter()
-        if self.available and self._thr is None:
+        if self.available and self.process and self._child is None:
+            child = os.path.join(os.path.dirname(os.path.abspath(__file__)), "telemetry_child.py")
+            self._child = subprocess.Popen([sys.executable, child, str(self._bdf), str(self.interval_s)]
+                                           + list(_RESIDENCY + _XCP + ("throttle_status",)),
+                                           stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True)
+            self._child.stdout.readline()          # "ready": the first sample is taken
+        elif self.available and self._thr is None:
             self._thr = threading.Thread(target=self._loop, name="alink-gpu-telemetry", daemon=True)
             self._thr.start()
         return self
+
+    def _stop_child(self):
+        c, self._child = self._child, None
+        try:
+            out, _ = c.communicate("stop\n", timeout=10.0)
+            res = json.loads(out.strip().splitlines()[-1])
+        except Exception as e:                     # keep the bench alive; say why the series is missing
+            c.kill()
+            c.wait()
+            self.error = f"telemetry child failed: {type(e).__name__}: {e}"
+            return
+        self._rows = [tuple([r[0] - self._t0] + r[1:]) for r in res.get("rows", [])]
+        self._first, self._last = res.get("first"), res.get("last")
+        if res.get("error"):
+            self.error = res["error"]
 
     def mark(self, name: str) -> None:
         self._marks[name] = time.perf_counter() - self._t0
 
     def stop(self) -> dict:
+        if self._child is not None:
+            self._stop_child()
         if self._thr is not None:
             self._stop.set()
             self._thr.join(timeout=2.0)

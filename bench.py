@@ -32,7 +32,7 @@ per timed superstep (HIP events around the fused kernel and its slab reduction),
 per-rank values and ``straggler_ms_per_step`` their spread — so a multi-GPU step time splits into the slowest
 rank's kernel, the wait for it (inside ``allreduce_us_per_step``) and the collective itself.
 
-Telemetry (``--telemetry 1``, default on a GPU): an ``amdsmi`` sampling thread (``alink_amd/utils/telemetry.py``)
+Telemetry (``--telemetry 1``, default on a GPU): an ``amdsmi`` sampling process (``alink_amd/utils/telemetry.py``)
 records gfx / memory clocks, socket power and temperatures every 5 ms; ``telemetry`` holds per-phase min / median /
 max (data generation, warm-up, timed window, convergence runs) and the throttle-residency deltas of rank 0, plus
 every rank's timed-window medians.  ``ALINK_TELEMETRY_OUT=path`` also writes rank 0's raw series there.
@@ -109,7 +109,7 @@ def main():
     tel = None
     if dev.type == "cuda" and a.telemetry:
         from alink_amd.utils.telemetry import GpuTelemetry
-        tel = GpuTelemetry(dev).start()
+        tel = GpuTelemetry(dev, process=True).start()
 
     def mark(name):
         if tel is not None:

@@ -53,3 +53,47 @@ def test_telemetry_without_amdsmi(monkeypatch):
     t.mark("x")
     s = t.stop()
     assert s["available"] is False and "no driver" in s["error"]
+
+
+_FAKE_SRC = """
+state = {"n": 0}
+
+
+def amdsmi_init():
+    pass
+
+
+def amdsmi_get_processor_handles():
+    return ["h0"]
+
+
+def amdsmi_get_gpu_metrics_info(h):
+    state["n"] += 1
+    n = state["n"]
+    return {"current_gfxclks": [2400, 2300 - n % 2, "N/A", 0], "current_uclk": 1900,
+            "current_socket_power": 900 + n, "temperature_hotspot": 70, "temperature_mem": "N/A",
+            "ppt_residency_acc": 10 * n, "xcp_stats.gfx_below_host_limit_ppt_acc": [n, n, "N/A"]}
+"""
+
+
+def test_telemetry_child_process(monkeypatch, tmp_path):
+    """process=True: the sampler runs as a child process (no GIL shared with the caller) with the same summary --
+    rows on the parent's clock, phase split by the parent's marks, residency deltas from the child's first / last
+    tables."""
+    (tmp_path / "fake_amdsmi_child.py").write_text(_FAKE_SRC)
+    monkeypatch.setitem(sys.modules, "amdsmi", _fake_amdsmi())
+    monkeypatch.setenv("ALINK_AMDSMI_MODULE", "fake_amdsmi_child")
+    monkeypatch.setenv("PYTHONPATH", str(tmp_path))
+    t = GpuTelemetry("cpu", interval_s=0.002, process=True).start()
+    time.sleep(0.05)
+    t.mark("window_start")
+    time.sleep(0.05)
+    t.mark("window_end")
+    s = t.stop()
+    assert s["available"] and s["samples"] >= 10, s
+    w = s["phases"]["window_start->window_end"]
+    assert w["samples"] >= 5 and w["gfxclk_max_mhz"]["max"] == 2400 and w["uclk_mhz"]["median"] == 1900
+    d = s["residency_delta"]
+    assert d["ppt_residency_acc"] == 10 * (s["samples"] - 1)
+    assert d["xcp_stats.gfx_below_host_limit_ppt_acc"] == 2 * (s["samples"] - 1)
+    assert all(0.0 <= r[0] < 1.0 for r in t.series())
