@@ -109,7 +109,9 @@ def main():
     tel = None
     if dev.type == "cuda" and a.telemetry:
         from alink_amd.utils.telemetry import GpuTelemetry
-        tel = GpuTelemetry(dev, process=True).start()
+        # a sampler process per rank keeps the amdsmi decoding off the rank's GIL; above 4 ranks a thread, so a node
+        # never carries more than 8 extra processes next to the ranks
+        tel = GpuTelemetry(dev, process=comm.get_world_size() <= 4).start()
 
     def mark(name):
         if tel is not None:
