@@ -279,7 +279,9 @@ def _local_kmeans_kernels(samples: torch.Tensor, w: torch.Tensor, D: torch.Tenso
     torch path, which handles both."""
     state = rng.bit_generator.state
     r0 = float(rng.random())
-    U = torch.as_tensor(rng.random(k - 1), dtype=torch.float64, device=samples.device)
+    # the uniforms go up from pinned memory without blocking: the host queues the seeding and Lloyd kernels while
+    # the weights pass is still running (a pageable copy would wait for it)
+    U = torch.as_tensor(rng.random(k - 1), dtype=torch.float64).pin_memory().to(samples.device, non_blocking=True)
     chosen, mintot = kops.seed_ref_hip(D, w, U, k, idx0=-1, r0=r0)
     C, assign, status, live = kops.local_lloyd_hip(samples, w, k, chosen=chosen, max_iter=max_iter, mintot=mintot)
     st = status.cpu().tolist()
