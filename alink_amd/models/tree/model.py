@@ -386,23 +386,46 @@ class _DeviceForest:
         ynode = np.zeros(len(flat.feat), dtype=np.int64)
         self.thresholds: Dict[int, np.ndarray] = {}
         widest = 0
-        for f in used:
-            sel = internal & (flat.feat == f)
-            if f in self.cat_features:
-                ynode[sel] = -flat.catrow[sel] - 1
-                widest = max(widest, int(cat_sizes[f]) if f < len(cat_sizes) else 0, flat.cat.shape[1])
-            else:
-                T = np.unique(flat.thr[sel])
-                self.thresholds[f] = T
-                ynode[sel] = np.searchsorted(T, flat.thr[sel])
-                widest = max(widest, len(T) + 1)
+        # every internal node at once (255k nodes x 1000 features took 0.11 s as a per-feature mask loop): continuous
+        # nodes sorted by (feature, threshold); a threshold's rank is its dense index within its feature's distinct
+        # values -- np.searchsorted(np.unique(thr of f), thr) -- NaN thresholds equal to each other, last
+        is_cat = np.zeros(len(flat.feat), dtype=bool)
+        if self.cat_features:
+            is_cat = internal & np.isin(flat.feat, np.fromiter(self.cat_features, dtype=np.int64))
+            ynode[is_cat] = -flat.catrow[is_cat] - 1
+            for f in used:
+                if f in self.cat_features:
+                    widest = max(widest, int(cat_sizes[f]) if f < len(cat_sizes) else 0, flat.cat.shape[1])
+        cidx = np.flatnonzero(internal & ~is_cat)
+        if cidx.size:
+            fz, tz = flat.feat[cidx], flat.thr[cidx]
+            order = np.lexsort((tz, fz))
+            fs, ts = fz[order], tz[order]
+            new_f = np.ones(fs.size, dtype=bool)
+            new_f[1:] = fs[1:] != fs[:-1]
+            same_t = np.zeros(ts.size, dtype=bool)
+            same_t[1:] = (ts[1:] == ts[:-1]) | (np.isnan(ts[1:]) & np.isnan(ts[:-1]))
+            new_v = new_f | ~same_t
+            dense = np.cumsum(new_v) - 1                       # global index of a distinct (feature, threshold)
+            gstart = np.flatnonzero(new_f)                     # first sorted position of each feature
+            glen = np.diff(np.append(gstart, fs.size))
+            base = np.repeat(dense[gstart], glen)
+            ynode[cidx[order]] = dense - base
+            vals = ts[new_v]                                   # distinct thresholds, feature-major
+            vstart = dense[gstart]
+            vend = np.append(vstart[1:], vals.size)
+            for f, a, b in zip(fs[gstart].tolist(), vstart.tolist(), vend.tolist()):
+                self.thresholds[f] = vals[a:b]
+                widest = max(widest, b - a + 1)
         # code width: uint8 while every code and the MISS sentinel (255) stay apart
         self.code_bytes = 1 if widest < 255 else (2 if widest < 65535 else 0)
         self.supported = self.code_bytes > 0 and len(flat.roots) > 0
         F = max(1, len(used))
         self.stride = ((F * max(1, self.code_bytes) + 15) // 16) * 16
         self.supported = self.supported and self.stride * 64 <= 160 * 1024
-        node_slot = np.where(internal, np.asarray([self.slot.get(int(f), -1) for f in flat.feat.tolist()]), -1)
+        lut = np.full(max(used) + 2 if used else 1, -1, dtype=np.int64)
+        lut[np.asarray(used, dtype=np.int64)] = np.arange(len(used))
+        node_slot = np.where(internal, lut[np.maximum(flat.feat, 0)], -1)
         nodes = np.stack([node_slot, ynode, np.where(internal, flat.first, 0), flat.nchild], 1).astype(np.int32)
         self.dev = device
         self.nodes = torch.from_numpy(np.ascontiguousarray(nodes)).to(device)

@@ -595,3 +595,32 @@ def test_native_tree_flatten_equals_node_walk():
                                  '{"id":3}'], [0, 4]) is None        # non-consecutive children
     assert _native.tree_flatten(['{"node":{"featureIndex":1},"id":0,"nextIds":[1,2]}', '{"id":1}', "{oops"],
                                 [0, 3]) is None
+
+
+def test_device_forest_threshold_ranks_vectorized():
+    """_DeviceForest ranks every continuous split's threshold among its feature's distinct thresholds in one
+    sorted pass; equal to the per-feature np.unique + np.searchsorted definition, NaN and signed-zero thresholds
+    included, and the node slots to the sorted used-feature order."""
+    import os
+    import sys
+    import numpy as np
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    from tree_predict_bench import random_forest
+    from alink_amd.models.tree import model as M
+    for seed, (T, D, F) in enumerate([(20, 5, 30), (40, 6, 500), (3, 3, 2)]):
+        flat = M._FlatForest(random_forest(T, D, F, seed=seed), 2)
+        flat.thr = flat.thr.copy()
+        idx = np.flatnonzero(flat.feat >= 0)
+        flat.thr[idx[::7]] = np.nan
+        flat.thr[idx[1::11]] = -0.0
+        flat.thr[idx[2::11]] = 0.0
+        df = M._DeviceForest(flat, [], [], "cpu")
+        nodes = df.nodes.numpy()
+        used = sorted(set(flat.feat[idx].tolist()))
+        for f in used:
+            sel = np.flatnonzero(flat.feat == f)
+            T_f = np.unique(flat.thr[sel])
+            assert np.array_equal(df.thresholds[f], T_f, equal_nan=True)
+            assert np.array_equal(nodes[sel, 1], np.searchsorted(T_f, flat.thr[sel]))
+            assert (nodes[sel, 0] == used.index(f)).all()
+        assert (nodes[flat.feat < 0, 0] == -1).all()

@@ -43,6 +43,7 @@ def main():
     ap.add_argument("--features", type=int, default=1000)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--missing", type=float, default=0.0, help="fraction of NULL cells")
+    ap.add_argument("--profile", type=int, default=0, help="1: cProfile one end-to-end run (top 40 by cumulative)")
     a = ap.parse_args()
     from alink_amd import useLocalEnv, GbdtPredictBatchOp
     from alink_amd.common.params import Params
@@ -88,6 +89,24 @@ def main():
         print(json.dumps({"rows": a.rows, "trees": a.trees, "depth": a.depth, "features": a.features,
                           "missing": a.missing, "detail": detail, "device": str(dev), "s": round(tm, 4),
                           "rows_per_s": a.rows / tm, "model_build_s": round(t_model, 2)}), flush=True)
+    if a.profile:
+        import cProfile
+        import io
+        import pstats
+        pr = cProfile.Profile()
+        op = GbdtPredictBatchOp().setPredictionCol("p").setReservedCols([])
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        pr.enable()
+        out = op.linkFrom(model, data).getOutputTable()
+        _ = out.col("p").values
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        pr.disable()
+        for key in ("cumulative", "tottime"):
+            sio = io.StringIO()
+            pstats.Stats(pr, stream=sio).sort_stats(key).print_stats(40)
+            print(sio.getvalue(), flush=True)
     # serving split: the model loaded once (LocalPredictor-style), then per-phase times of one scoring pass
     from alink_amd.operator.batch.utils import load_model_mapper
     from alink_amd.models.tree.model import GbdtModelMapper
