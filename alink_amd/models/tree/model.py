@@ -380,7 +380,7 @@ class _DeviceForest:
 
     def __init__(self, flat: "_FlatForest", cat_features: Sequence[int], cat_sizes: Sequence[int], device):
         internal = flat.feat >= 0
-        used = sorted(set(flat.feat[internal].tolist()))
+        used = np.unique(flat.feat[internal]).tolist()
         self.slot = {f: i for i, f in enumerate(used)}
         self.cat_features = set(int(f) for f in cat_features)
         ynode = np.zeros(len(flat.feat), dtype=np.int64)
@@ -465,7 +465,11 @@ class _DeviceForest:
         if use_kernel:
             L = _lib.require()
             out = torch.empty((n, self.stride // self.code_bytes), dtype=ct, device=self.dev)
-            ptrs = torch.tensor([cols[f].data_ptr() for f in self.cont] or [0], dtype=torch.int64, device=self.dev)
+            # column pointers go up from pinned memory without a host wait (a pageable copy would block until the
+            # previous chunk's kernels finish)
+            ptrs = torch.tensor([cols[f].data_ptr() for f in self.cont] or [0], dtype=torch.int64)
+            if torch.device(self.dev).type == "cuda":
+                ptrs = ptrs.pin_memory().to(self.dev, non_blocking=True)
             for f in self.cont:
                 v = cols[f]
                 if v.dtype != torch.float64 or not v.is_contiguous() or v.device != torch.device(self.dev) or \
