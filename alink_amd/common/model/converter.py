@@ -61,7 +61,11 @@ def append_meta_rows(meta: Optional[Params], out: List[Row], n_fields: int):
 def append_data_rows(data: Optional[Iterable[str]], out: List[Row], n_fields: int):
     if data is None:
         return
+    pad = (None,) * (n_fields - 2)
     for idx, s in enumerate(data):
+        if s and len(s) <= SEGMENT_SIZE:         # the common case: one segment, no slicing / helper calls
+            out.append(Row((MAX_NUM_SLICES * (idx + 1), s) + pad))
+            continue
         for i, seg in enumerate(_slices(s)):
             out.append(_row(n_fields, get_model_id(idx + 1, i), seg))
 

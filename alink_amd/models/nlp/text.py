@@ -22,7 +22,7 @@ from typing import Dict, List, Optional, Sequence
 import numpy as np
 import torch
 
-from ...common.javafmt import gson_dumps
+from ...common.javafmt import _gson_escape, gson_dumps
 from ...common.linalg import SparseVector
 from ...common.mapper import SISOMapper, ModelMapper, OutputColsHelper, find_col_index
 from ...common.model.converter import SimpleModelDataConverter
@@ -435,8 +435,20 @@ def train_doc_count_vectorizer(mt: MTable, params: Params) -> List[tuple]:
     keep = keep[:vocab]
     meta = Params().set("minTF", float(_pget(params, "minTF", 1.0))) \
         .set("featureType", _ename(_pget(params, "featureType"), "WORD_COUNT"))
-    data = [gson_dumps(_Tuple3(w, float(idf), i), java_map_order=False) for i, (w, _, idf) in enumerate(keep)]
-    return SimpleModelDataConverter.rows_from(meta, data)
+    return SimpleModelDataConverter.rows_from(meta, _tuple3_rows(keep))
+
+
+def _tuple3_rows(keep) -> List[str]:
+    """``gson_dumps(_Tuple3(word, idf, index))`` for every vocabulary entry, with the idf digits from the C++ Java
+    double formatter in one call (the generic serializer took ~1 s per 1e5 words)."""
+    from ... import _native
+    idfs = np.asarray([float(idf) for _, _, idf in keep], dtype=np.float64)
+    joined = _native.java_double_join(idfs) if len(keep) else ""
+    if joined is None:
+        return [gson_dumps(_Tuple3(w, float(idf), i), java_map_order=False) for i, (w, _, idf) in enumerate(keep)]
+    ds = joined.split(",") if len(keep) else []
+    return ['{"f0":' + _gson_escape(w) + ',"f1":' + d + ',"f2":' + str(i) + '}'
+            for i, ((w, _, _), d) in enumerate(zip(keep, ds))]
 
 
 def _string_block(mt: MTable, col: str, dev):

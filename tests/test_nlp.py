@@ -315,3 +315,17 @@ def test_split_tokens_and_unique_ids_host():
     assert sorted(first.values()) == sorted(rep.tolist())
     for i, t in enumerate(toks):
         assert toks[int(rep[ids[i]])] == t
+
+
+def test_doc_count_model_rows_fast_format_equals_gson():
+    """The DocCountVectorizer model strings from the C++ double formatter equal the generic Gson serializer's,
+    escaped words, long vocabularies and Java double edge values included."""
+    import math
+    from alink_amd.common.javafmt import gson_dumps
+    from alink_amd.models.nlp.text import _Tuple3, _tuple3_rows
+    words = [f"w{i}" for i in range(300)] + ['q"uote', "back\\slash", "tab\there", "é", "", " x"]
+    keep = [(w, 1, v) for w, v in zip(words, [math.log((1.0 + 1e7) / (1.0 + i)) for i in range(len(words))])]
+    keep += [("a", 1, 0.0), ("b", 1, 1e-3), ("c", 1, 1e7), ("d", 1, 123456789.125), ("e", 1, 5e-324)]
+    ref = [gson_dumps(_Tuple3(w, float(idf), i), java_map_order=False) for i, (w, _, idf) in enumerate(keep)]
+    assert _tuple3_rows(keep) == ref
+    assert _tuple3_rows([]) == []
