@@ -346,6 +346,38 @@ def parse_dense_vectors_packed(data: np.ndarray, off: np.ndarray, d: int, with_c
     return (out, cnt[:n]) if with_counts else out
 
 
+def parse_double_csv(text: str) -> Optional[np.ndarray]:
+    """float64 [n] of a comma-separated list of plain decimal numbers (the inside of a JSON number array, e.g. a
+    serialized coefficient vector), parsed in C++ over up to 64 comma-aligned chunks in parallel; None when the
+    library is missing or a token is not a plain decimal (NaN / Infinity / anything else: the caller's JSON path)."""
+    if lib is None:
+        return None
+    try:
+        b = text.encode("ascii")
+    except UnicodeEncodeError:
+        return None
+    n = len(b)
+    if n == 0 or not b.strip():
+        return np.zeros(0, dtype=np.float64)
+    nch = min(64, max(1, n // 65536))
+    cuts = [0]
+    for c in range(1, nch):
+        p = b.find(b",", c * n // nch)
+        if p >= 0 and p + 1 > cuts[-1]:
+            cuts.append(p + 1)
+    cuts.append(n)
+    per = [b.count(b",", cuts[i], cuts[i + 1]) + 1 for i in range(len(cuts) - 1)]
+    res = parse_dense_vectors_packed(np.frombuffer(b, dtype=np.uint8), np.asarray(cuts, dtype=np.int64), max(per),
+                                     with_counts=True)
+    if res is None:
+        return None
+    out, cnt = res
+    total = b.count(b",") + 1
+    if int(cnt.sum()) != total:                 # an empty token (",,") or a stray separator: not a plain list
+        return None
+    return np.concatenate([out[i, :int(cnt[i])] for i in range(out.shape[0])])
+
+
 def parse_kv_packed(data: np.ndarray, off: np.ndarray, keys: Sequence[str], cd: str, vd: str):
     """(values float64 [n, k], found bool [n, k], dup bool [n]) of packed KV lines for the schema ``keys``
     (single-character delimiters), or None: library missing, or a line outside the plain form (the caller parses

@@ -292,3 +292,27 @@ def test_linear_model_mapper_reference_rows():
     m.loadModel(rows)
     assert tuple(m.map((1.0, 1.0, 0.0, 1.0)))[4] == 1
     assert m.getOutputSchema().getFieldNames() == ["f0", "f1", "f2", "f3", "pred"]
+
+
+def test_linear_model_large_coefficients_native_parse():
+    """A large coefficient vector is read by the C++ number parser (cut out of the model JSON), a vector with NaN
+    by json.loads: both round-trip exactly through the model rows."""
+    import numpy as np
+    from alink_amd.common.linalg import DenseVector
+    from alink_amd.common.types import Types
+    from alink_amd.models.linear.model import LinearModelData, LinearModelDataConverter
+    rng = np.random.default_rng(3)
+    for special in (False, True):
+        m = LinearModelData()
+        m.modelName, m.linearModelType, m.hasInterceptItem = "Logistic Regression", "LR", True
+        m.vectorColName, m.vectorSize, m.labelName = "vec", 150_000, "label"
+        m.featureNames = m.featureTypes = m.coefVectors = None
+        w = rng.normal(size=150_001) * 10.0 ** rng.integers(-20, 20, size=150_001)
+        if special:
+            w[7] = np.nan
+        m.coefVector = DenseVector(w)
+        m.labelValues = [0, 1]
+        conv = LinearModelDataConverter(Types.INT)
+        got = conv.load(conv.save(m))
+        assert np.array_equal(got.coefVector.data, w, equal_nan=True)
+        assert got.featureNames is None and got.vectorSize == 150_000
