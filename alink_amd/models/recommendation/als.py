@@ -42,8 +42,20 @@ class AlsModelData:
         self.user_factors = np.asarray(user_factors, dtype=np.float32)
         self.item_ids = np.asarray(item_ids, dtype=np.int64)
         self.item_factors = np.asarray(item_factors, dtype=np.float32)
-        self.user_map = {int(u): i for i, u in enumerate(self.user_ids)}
-        self.item_map = {int(u): i for i, u in enumerate(self.item_ids)}
+        self._user_map = self._item_map = None
+
+    # id -> row maps, built on first use (a Python dict over 1e7 user ids costs ~1 s; training never reads them)
+    @property
+    def user_map(self):
+        if self._user_map is None:
+            self._user_map = dict(zip(self.user_ids.tolist(), range(len(self.user_ids))))
+        return self._user_map
+
+    @property
+    def item_map(self):
+        if self._item_map is None:
+            self._item_map = dict(zip(self.item_ids.tolist(), range(len(self.item_ids))))
+        return self._item_map
 
     # the reference's field names (AlsModelData.java: userIds, userFactors, itemIds, itemFactors)
     userIds = property(lambda self: self.user_ids)
