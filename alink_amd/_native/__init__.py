@@ -15,7 +15,7 @@ __all__ = ["lib", "parse_csv_lines", "murmur3_utf16", "murmur3_bytes", "murmur3_
            "ftrl_partial_margin", "ftrl_shard_update", "parse_binary_detail", "java_double_join",
            "java_double_rows", "java_double_rows_packed", "parse_csv_packed",
            "parse_dense_vectors_packed", "parse_kv_packed", "parse_json_flat_packed", "java_double_rows_fmt", "sample_thresholds", "gbdt_rank_grad",
-           "tree_flatten"]
+           "tree_flatten", "java_float_rows", "java_float_rows_packed", "parse_double_csv"]
 
 # ALINK_NATIVE_LIB points at another build of the same sources (e.g. the AddressSanitizer build of
 # tools/asan_host.py)
@@ -39,6 +39,8 @@ if os.path.exists(_PATH):
             lib.alink_java_double_join.restype = ctypes.c_int64
         if hasattr(lib, "alink_java_double_rows"):
             lib.alink_java_double_rows.restype = ctypes.c_int64
+        if hasattr(lib, "alink_java_float_rows"):
+            lib.alink_java_float_rows.restype = ctypes.c_int64
         if hasattr(lib, "alink_java_double_rows_fmt"):
             lib.alink_java_double_rows_fmt.restype = ctypes.c_int64
         if hasattr(lib, "alink_sample_thresholds"):
@@ -218,6 +220,34 @@ def java_double_rows_packed(x, sep: str = " "):
     total = lib.alink_java_double_rows(_ptr(a), ctypes.c_int64(n), ctypes.c_int64(k), ctypes.c_char(sep.encode()),
                                        _ptr(buf), _ptr(off[1:]))
     return buf[:total], off
+
+
+def java_float_rows_packed(x, sep: str = " "):
+    """``java_double_rows_packed`` for a float32 array in ``java.lang.Float.toString`` form
+    (``common/javafmt.java_float_str`` per value); None without the library."""
+    if lib is None or getattr(lib, "alink_java_float_rows", None) is None:
+        return None
+    a = np.ascontiguousarray(np.asarray(x, dtype=np.float32))
+    if a.ndim != 2:
+        raise ValueError("java_float_rows needs a 2-D array")
+    n, k = a.shape
+    buf = np.empty(26 * max(a.size, 1) + 16, dtype=np.uint8)
+    off = np.zeros(n + 1, dtype=np.int64)
+    total = lib.alink_java_float_rows(_ptr(a), ctypes.c_int64(n), ctypes.c_int64(k), ctypes.c_char(sep.encode()),
+                                      _ptr(buf), _ptr(off[1:]))
+    return buf[:total], off
+
+
+def java_float_rows(x, sep: str = " ") -> Optional[List[str]]:
+    """One string per row of a float32 2-D array, values in ``Float.toString`` form joined by ``sep``; None without
+    the library."""
+    r = java_float_rows_packed(x, sep)
+    if r is None:
+        return None
+    data, off = r
+    text = data.tobytes().decode("ascii")
+    o = off.tolist()
+    return [text[o[i]:o[i + 1]] for i in range(len(o) - 1)]
 
 
 def java_double_rows_fmt(x, pre: Sequence[str], post: Sequence[str], sep: str, ropen: str = "", rclose: str = ""):

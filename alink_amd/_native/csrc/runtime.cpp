@@ -356,7 +356,9 @@ int alink_native_version() { return 1; }
 #include <cmath>
 #include <cstring>
 
-static int java_double_to(double x, char* out) {
+// T = float: java.lang.Float.toString -- the same layout over the shortest float32 round-trip digits
+template <typename T>
+static int java_num_to(T x, char* out) {
     if (std::isnan(x)) { std::memcpy(out, "NaN", 3); return 3; }
     if (std::isinf(x)) {
         if (x > 0) { std::memcpy(out, "Infinity", 8); return 8; }
@@ -369,7 +371,7 @@ static int java_double_to(double x, char* out) {
         return p + 3;
     }
     if (x < 0) out[p++] = '-';
-    const double ax = std::fabs(x);
+    const T ax = std::fabs(x);
     char buf[40];
     const auto res = std::to_chars(buf, buf + sizeof(buf), ax, std::chars_format::scientific);
     const char* e = static_cast<const char*>(std::memchr(buf, 'e', (size_t)(res.ptr - buf)));
@@ -412,18 +414,20 @@ static int java_double_to(double x, char* out) {
     return (int)(r2.ptr - out);
 }
 
+static int java_double_to(double x, char* out) { return java_num_to<double>(x, out); }
+
 // n rows of k values: row i = java_double(x[i*k]) sep ... sep java_double(x[i*k+k-1]), rows written back to back;
 // row_end[i] = end offset of row i in out (dense-vector strings of a prediction detail column, VectorUtil.toString)
 // Large inputs: OpenMP row blocks format into their own slices of out (capacity 26 per value, the bound each
 // block is given), then the blocks are compacted left in order.
-extern "C" int64_t alink_java_double_rows(const double* x, int64_t n, int64_t k, char sep, char* out,
-                                          int64_t* row_end) {
+template <typename T>
+static int64_t java_rows(const T* x, int64_t n, int64_t k, char sep, char* out, int64_t* row_end) {
     if (n * k < (1 << 16)) {
         int64_t p = 0;
         for (int64_t i = 0; i < n; ++i) {
             for (int64_t j = 0; j < k; ++j) {
                 if (j) out[p++] = sep;
-                p += java_double_to(x[i * k + j], out + p);
+                p += java_num_to<T>(x[i * k + j], out + p);
             }
             row_end[i] = p;
         }
@@ -440,7 +444,7 @@ extern "C" int64_t alink_java_double_rows(const double* x, int64_t n, int64_t k,
         for (int64_t i = r0; i < r1; ++i) {
             for (int64_t j = 0; j < k; ++j) {
                 if (j) base[p++] = sep;
-                p += java_double_to(x[i * k + j], base + p);
+                p += java_num_to<T>(x[i * k + j], base + p);
             }
             row_end[i] = p;                     // block-relative for now
         }
@@ -454,6 +458,17 @@ extern "C" int64_t alink_java_double_rows(const double* x, int64_t n, int64_t k,
         p += blen[b];
     }
     return p;
+}
+
+extern "C" int64_t alink_java_double_rows(const double* x, int64_t n, int64_t k, char sep, char* out,
+                                          int64_t* row_end) {
+    return java_rows<double>(x, n, k, sep, out, row_end);
+}
+
+// the same rows of float32 values in java.lang.Float.toString form (ALS factor strings)
+extern "C" int64_t alink_java_float_rows(const float* x, int64_t n, int64_t k, char sep, char* out,
+                                         int64_t* row_end) {
+    return java_rows<float>(x, n, k, sep, out, row_end);
 }
 
 // Threshold sampling of a binary-classification curve over descending thresholds: index 0, then every index

@@ -76,12 +76,24 @@ class AlsModelDataConverter:
         return TableSchema([self.user_col, self.item_col, "factors"], [Types.LONG, Types.LONG, Types.STRING])
 
     def save(self, m: AlsModelData) -> List[tuple]:
-        rows = [(int(u), None, _factor_str(f)) for u, f in zip(m.user_ids, m.user_factors)]
-        rows += [(None, int(i), _factor_str(f)) for i, f in zip(m.item_ids, m.item_factors)]
+        # factor strings in Float.toString form from the C++ formatter (OpenMP row blocks): 1e7 users x rank 64
+        # are 6.4e8 values, hours through the per-value Python formatter
+        from ... import _native
+        us = _native.java_float_rows(m.user_factors.reshape(len(m.user_ids), -1))
+        its = _native.java_float_rows(m.item_factors.reshape(len(m.item_ids), -1))
+        if us is None or its is None:
+            us = [_factor_str(f) for f in m.user_factors]
+            its = [_factor_str(f) for f in m.item_factors]
+        rows = [(u, None, f) for u, f in zip(m.user_ids.tolist(), us)]
+        rows += [(None, i, f) for i, f in zip(m.item_ids.tolist(), its)]
         return rows
 
     @staticmethod
     def load(rows) -> AlsModelData:
+        rows = list(rows)
+        fast = AlsModelDataConverter._load_native(rows)
+        if fast is not None:
+            return fast
         us, uf, its, itf = [], [], [], []
         for r in rows:
             f = np.asarray([float(x) for x in str(r[2]).split(" ")], dtype=np.float32)
@@ -94,6 +106,28 @@ class AlsModelDataConverter:
         rk = len(uf[0]) if uf else (len(itf[0]) if itf else 0)
         return AlsModelData(us, np.stack(uf) if uf else np.zeros((0, rk)), its,
                             np.stack(itf) if itf else np.zeros((0, rk)))
+
+    @staticmethod
+    def _load_native(rows) -> Optional[AlsModelData]:
+        """The factor strings parsed by the C++ number reader (all rows one rank wide, plain decimal tokens);
+        None sends the rows through the per-row path (NaN / Infinity tokens, ragged rows, no library)."""
+        from ... import _native
+        if not rows or _native.lib is None:
+            return None
+        user = [r[0] is not None for r in rows]
+        strs = [str(r[2]) for r in rows]
+        rk = len(strs[0].split(" "))
+        res = _native.parse_dense_vectors(strs, rk)
+        if res is None:
+            return None
+        # parse_dense_vectors zero-pads short rows: every row must hold exactly rk values
+        if any(s.count(" ") != rk - 1 for s in strs):
+            return None
+        F = res.astype(np.float32)
+        um = np.asarray(user, dtype=bool)
+        uid = [int(r[0]) for r in rows if r[0] is not None]
+        iid = [int(r[1]) for r in rows if r[0] is None]
+        return AlsModelData(uid, F[um], iid, F[~um])
 
 
 # ---------------------------------------------------------------------------------------------------

@@ -361,3 +361,27 @@ def test_hip_als_woodbury16_mfma_matches_lds_kernel(r, monkeypatch):
     A = A + reg[:, None, None] * torch.eye(r, dtype=torch.float64)[None]
     ref = (torch.linalg.pinv(A) @ bb[:, :, None])[:, :, 0].numpy()
     np.testing.assert_allclose(a, ref, rtol=2e-4, atol=2e-5)
+
+
+def test_als_model_rows_native_format_and_parse():
+    """ALS model rows: factor strings from the C++ Float.toString formatter equal the per-value formatter's, and
+    the C++ reader loads them back bit-exactly (NaN tokens fall back to the per-row path)."""
+    import numpy as np
+    from alink_amd.common.javafmt import java_float_str
+    from alink_amd.models.recommendation.als import AlsModelData, AlsModelDataConverter
+    rng = np.random.default_rng(1)
+    uf = (rng.normal(size=(300, 16)) * 10.0 ** rng.integers(-9, 9, size=(300, 16))).astype(np.float32)
+    itf = rng.normal(size=(50, 16)).astype(np.float32)
+    m = AlsModelData(np.arange(300) * 7, uf, np.arange(50) + 1000, itf)
+    conv = AlsModelDataConverter("u", "i")
+    rows = conv.save(m)
+    assert rows[5][2] == " ".join(java_float_str(float(v)) for v in uf[5]) and rows[5][:2] == (35, None)
+    assert rows[300 + 3][:2] == (None, 1003)
+    got = conv.load(rows)
+    assert np.array_equal(got.user_factors, uf) and np.array_equal(got.item_factors, itf)
+    assert got.user_ids.tolist() == (np.arange(300) * 7).tolist() and got.user_map[14] == 2
+    uf[3, 2] = np.nan
+    rows = conv.save(AlsModelData(np.arange(300), uf, np.arange(50), itf))
+    assert "NaN" in rows[3][2]
+    got = conv.load(rows)
+    assert np.array_equal(got.user_factors, uf, equal_nan=True)
