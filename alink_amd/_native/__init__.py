@@ -15,7 +15,8 @@ __all__ = ["lib", "parse_csv_lines", "murmur3_utf16", "murmur3_bytes", "murmur3_
            "ftrl_partial_margin", "ftrl_shard_update", "parse_binary_detail", "java_double_join",
            "java_double_rows", "java_double_rows_packed", "parse_csv_packed",
            "parse_dense_vectors_packed", "parse_kv_packed", "parse_json_flat_packed", "java_double_rows_fmt", "sample_thresholds", "gbdt_rank_grad",
-           "tree_flatten", "java_float_rows", "java_float_rows_packed", "parse_double_csv"]
+           "tree_flatten", "java_float_rows", "java_float_rows_packed", "parse_double_csv",
+           "java_float_kv_rows"]
 
 # ALINK_NATIVE_LIB points at another build of the same sources (e.g. the AddressSanitizer build of
 # tools/asan_host.py)
@@ -41,6 +42,8 @@ if os.path.exists(_PATH):
             lib.alink_java_double_rows.restype = ctypes.c_int64
         if hasattr(lib, "alink_java_float_rows"):
             lib.alink_java_float_rows.restype = ctypes.c_int64
+        if hasattr(lib, "alink_java_float_kv_rows"):
+            lib.alink_java_float_kv_rows.restype = ctypes.c_int64
         if hasattr(lib, "alink_java_double_rows_fmt"):
             lib.alink_java_double_rows_fmt.restype = ctypes.c_int64
         if hasattr(lib, "alink_sample_thresholds"):
@@ -248,6 +251,26 @@ def java_float_rows(x, sep: str = " ") -> Optional[List[str]]:
     text = data.tobytes().decode("ascii")
     o = off.tolist()
     return [text[o[i]:o[i + 1]] for i in range(len(o) - 1)]
+
+
+def java_float_kv_rows(keys, vals, kvsep: str = ":", sep: str = ",") -> Optional[List[str]]:
+    """One string per row of ``key kvsep Float.toString(value)`` pairs joined by ``sep`` (int64 keys [n, k], float32
+    values [n, k]), formatted in C++; None without the library."""
+    if lib is None or getattr(lib, "alink_java_float_kv_rows", None) is None:
+        return None
+    ka = np.ascontiguousarray(np.asarray(keys, dtype=np.int64))
+    va = np.ascontiguousarray(np.asarray(vals, dtype=np.float32))
+    if ka.shape != va.shape or ka.ndim != 2:
+        raise ValueError("java_float_kv_rows needs two 2-D arrays of one shape")
+    n, k = ka.shape
+    buf = np.empty(48 * max(ka.size, 1) + 16, dtype=np.uint8)
+    off = np.zeros(n + 1, dtype=np.int64)
+    total = lib.alink_java_float_kv_rows(_ptr(ka), _ptr(va), ctypes.c_int64(n), ctypes.c_int64(k),
+                                         ctypes.c_char(kvsep.encode()), ctypes.c_char(sep.encode()), _ptr(buf),
+                                         _ptr(off[1:]))
+    text = buf[:total].tobytes().decode("ascii")
+    o = off.tolist()
+    return [text[o[i]:o[i + 1]] for i in range(n)]
 
 
 def java_double_rows_fmt(x, pre: Sequence[str], post: Sequence[str], sep: str, ropen: str = "", rclose: str = ""):

@@ -465,6 +465,42 @@ extern "C" int64_t alink_java_double_rows(const double* x, int64_t n, int64_t k,
     return java_rows<double>(x, n, k, sep, out, row_end);
 }
 
+// n rows of k (int64 key, float32 value) pairs: row i = "key:Float.toString(v),key:v,..." (kvsep ':' and sep ','
+// as given) -- the "item:score,..." lists of ALS recommendations.  OpenMP row blocks write into their own
+// 48-bytes-per-pair slices of out, then the blocks are compacted in order; row_end[i] = end offset of row i.
+extern "C" int64_t alink_java_float_kv_rows(const int64_t* keys, const float* vals, int64_t n, int64_t k,
+                                            char kvsep, char sep, char* out, int64_t* row_end) {
+    const int64_t W = 48;
+    const int64_t rows_per = std::max<int64_t>(1, 8192 / std::max<int64_t>(k, 1));
+    const int64_t nb = (n + rows_per - 1) / rows_per;
+    std::vector<int64_t> blen(nb);
+#pragma omp parallel for schedule(dynamic, 4) if (n * k >= (1 << 16))
+    for (int64_t b = 0; b < nb; ++b) {
+        const int64_t r0 = b * rows_per, r1 = std::min(n, r0 + rows_per);
+        char* base = out + r0 * k * W;
+        int64_t p = 0;
+        for (int64_t i = r0; i < r1; ++i) {
+            for (int64_t j = 0; j < k; ++j) {
+                if (j) base[p++] = sep;
+                const auto r = std::to_chars(base + p, base + p + 21, keys[i * k + j]);
+                p = r.ptr - base;
+                base[p++] = kvsep;
+                p += java_num_to<float>(vals[i * k + j], base + p);
+            }
+            row_end[i] = p;
+        }
+        blen[b] = p;
+    }
+    int64_t p = 0;
+    for (int64_t b = 0; b < nb; ++b) {
+        const int64_t r0 = b * rows_per, r1 = std::min(n, r0 + rows_per);
+        if (p != r0 * k * W) std::memmove(out + p, out + r0 * k * W, (size_t)blen[b]);
+        for (int64_t i = r0; i < r1; ++i) row_end[i] += p;
+        p += blen[b];
+    }
+    return p;
+}
+
 // the same rows of float32 values in java.lang.Float.toString form (ALS factor strings)
 extern "C" int64_t alink_java_float_rows(const float* x, int64_t n, int64_t k, char sep, char* out,
                                          int64_t* row_end) {

@@ -393,8 +393,9 @@ def als_topk(model: AlsModelData, users: Sequence[int], k: int, device) -> List[
         return []
     val, idx = blockwise_topk(U, V, kk)            # collective: every rank takes part, even with no users
     val, idx = val.cpu().numpy(), idx.cpu().numpy()
-    out = []
-    for j, uid in enumerate(uniq):
-        items = model.item_ids[idx[j]]
-        out.append((uid, ",".join(f"{int(a)}:{java_float_str(float(b))}" for a, b in zip(items, val[j]))))
-    return out
+    from ... import _native
+    strs = _native.java_float_kv_rows(model.item_ids[idx], val) if len(uniq) else []
+    if strs is None:
+        strs = [",".join(f"{int(a)}:{java_float_str(float(b))}" for a, b in zip(model.item_ids[idx[j]], val[j]))
+                for j in range(len(uniq))]
+    return list(zip(uniq, strs))
