@@ -58,6 +58,10 @@ def _column_token_counts(col) -> Dict[str, int]:
     go through ``collections.Counter`` (C) over the values."""
     from collections import Counter
     v = col.values
+    enc = _block_codes(col)
+    if enc is not None:        # packed strings: counts of the distinct tokens from one device encoding
+        _, words, _, cnt = enc
+        return {w: int(c) for w, c in zip(words, cnt.tolist()) if c > 0}
     if isinstance(v, torch.Tensor) and v.dim() == 1:
         x = v if col.nulls is None else v[~col.nulls.to(v.device)]
         if x.numel() == 0:
@@ -83,6 +87,32 @@ def _column_token_counts(col) -> Dict[str, int]:
         return dict(cnt)
     cnt = Counter(java_str(x) for x in vals if x is not None)
     return dict(cnt)
+
+
+def _block_codes(col):
+    """Device dictionary encoding of a packed string column (``ops/strings.unique_ids``): (ids int64 [n] on the
+    column's device, distinct strings [u] -- "" for an id shared only by empty strings and nulls, None for an id of
+    nulls only --, null mask bool [n] or None, per-id count of non-null rows int64 [u]), or None for another column
+    type or a hash collision (the caller's per-value path)."""
+    from ...common.strings import StringBlock
+    v = col.values
+    if not isinstance(v, StringBlock) or len(v) == 0:
+        return None
+    from ...ops.strings import unique_ids
+    enc = unique_ids(v)
+    if enc is None:
+        return None
+    ids, rep = enc
+    nm = v.nulls
+    if col.nulls is not None:
+        cn = col.nulls.to(ids.device)
+        nm = cn if nm is None else (nm.to(ids.device) | cn)
+    u = int(rep.numel())
+    live = ids if nm is None else ids[~nm]
+    cnt = torch.bincount(live, minlength=u).cpu().numpy()
+    words = v.take(rep).to_list()
+    words = [("" if (w is None and cnt[i] > 0) else w) for i, w in enumerate(words)]
+    return ids, words, nm, cnt
 
 
 def _global_token_counts(mt: MTable, cols: Sequence[str]) -> List[Dict[str, int]]:
@@ -171,6 +201,34 @@ class StringIndexerModelMapper(_SISOModelMapper):
         if self.invalid == "SKIP":
             return None
         raise RuntimeError(f"Unseen token: {key}")
+
+    def _map_columns(self, mt):
+        """A packed string column maps through its device dictionary encoding: every DISTINCT token is looked up
+        once (mapColumn's rules, nulls included) and the rows gather their id's result on the device."""
+        col = mt.col(self.selected)
+        enc = _block_codes(col)
+        if enc is None:
+            return super()._map_columns(mt)
+        ids, words, nm, cnt = enc
+        u = len(words)
+        lut = np.zeros(u + 1, dtype=np.int64)
+        lut_null = np.zeros(u + 1, dtype=bool)
+        for i, w in enumerate(words + [None]):          # slot u: the null rows
+            if i < u and cnt[i] == 0:
+                continue                                # an id of null rows only: they use slot u
+            r = self.mapColumn(w)
+            if r is None:
+                lut_null[i] = True
+            else:
+                lut[i] = r
+        dev = ids.device
+        if nm is not None:
+            if bool(nm.any()):
+                self.mapColumn(None)                    # ERROR on a null raises as the row path does
+            ids = torch.where(nm, torch.full_like(ids, u), ids)
+        out = torch.from_numpy(lut).to(dev)[ids]
+        null = torch.from_numpy(lut_null).to(dev)[ids]
+        return [Column(out.cpu(), null.cpu() if bool(null.any()) else None)]
 
 
 class IndexToStringModelMapper(_SISOModelMapper):
@@ -284,8 +342,13 @@ class _EncodeSpec:
         """idx [n, cols] int64 bucket indices; valid False -> null (SKIP)."""
         n, k = idx.shape
         if self.encode == "INDEX":
-            return [Column.from_values([int(idx[r, j]) if valid[r, j] else None for r in range(n)], Types.LONG)
-                    for j in range(k)]
+            # columnar: int64 values (0 under a null, as Column.from_values fills) + a null mask when any is null
+            out = []
+            for j in range(k):
+                ok = valid[:, j]
+                v = np.where(ok, idx[:, j], 0).astype(np.int64)
+                out.append(Column(torch.from_numpy(v), None if ok.all() else torch.from_numpy(~ok)))
+            return out
         if self.encode == "VECTOR":
             out = []
             for j in range(k):
@@ -378,9 +441,16 @@ class OneHotModelMapper(ModelMapper):
         inv, ee = self.spec.invalid, self.enable_else
         for j, (c, m) in enumerate(zip(self.cols, self.maps)):
             vs = self.spec.vector_size[j]
-            vals = mt.col(c).to_list()
-            codes, uniq = pd.factorize(pd.Series(vals, dtype=object), use_na_sentinel=True)
-            look = np.asarray([m.get(java_str(u), -1) for u in uniq], dtype=np.int64)
+            enc = _block_codes(mt.col(c))
+            if enc is not None:         # packed strings: the device dictionary encoding, no Python list of rows
+                ids, uniq, nm, _ = enc
+                codes = ids.cpu().numpy()
+                if nm is not None:
+                    codes = np.where(nm.cpu().numpy(), -1, codes)
+            else:
+                vals = mt.col(c).to_list()
+                codes, uniq = pd.factorize(pd.Series(vals, dtype=object), use_na_sentinel=True)
+            look = np.asarray([m.get(java_str(u), -1) if u is not None else -1 for u in uniq], dtype=np.int64)
             got = np.where(codes >= 0, look[np.maximum(codes, 0)] if look.size else -1, -1)
             is_null = codes < 0
             unseen = (got < 0) & ~is_null
@@ -399,7 +469,8 @@ class OneHotModelMapper(ModelMapper):
             elif inv == "SKIP":
                 valid[is_null | unseen, j] = False
             elif (is_null | unseen).any():
-                bad = vals[int(np.nonzero(is_null | unseen)[0][0])]
+                i0 = int(np.nonzero(is_null | unseen)[0][0])
+                bad = None if codes[i0] < 0 else uniq[int(codes[i0])]
                 raise RuntimeError(f"Unseen token: {bad}")
         return self.spec.columns(idx, valid)
 
@@ -495,6 +566,9 @@ class _BucketMapperMixin:
 
     def _map_columns(self, mt):
         n, k = mt.num_rows, len(self.spec.cols)
+        if self.spec.encode == "INDEX" and all(isinstance(mt.col(c).values, torch.Tensor) and
+                                               mt.col(c).values.dim() == 1 for c in self.spec.cols):
+            return self._index_columns_device(mt)
         idx = np.zeros((n, k), dtype=np.int64)
         valid = np.ones((n, k), dtype=bool)
         for j, c in enumerate(self.spec.cols):
@@ -506,6 +580,30 @@ class _BucketMapperMixin:
                 elif self.spec.invalid == "ERROR":
                     raise RuntimeError("Unseen token: null")
         return self.spec.columns(idx, valid)
+
+
+    def _index_columns_device(self, mt):
+        """INDEX output of tensor columns where they live: ``torch.searchsorted`` over the bucket bounds (the
+        side ``_Bucketing.find`` uses), nulls / NaN to the null bucket or, under SKIP, to a null cell."""
+        out = []
+        for j, c in enumerate(self.spec.cols):
+            col = mt.col(c)
+            v = col.values.to(torch.float64)
+            null = torch.isnan(v)
+            if col.nulls is not None:
+                null = null | col.nulls.to(v.device)
+            b = self.buckets[j]
+            bt = torch.as_tensor(b.bounds, dtype=torch.float64, device=v.device)
+            hit = (torch.searchsorted(bt, v, right=not b.left_open) - 1).clamp_(0, b.nbins - 1)
+            hit = torch.where(null, torch.full_like(hit, b.null_index), hit)
+            any_null = bool(null.any())
+            if any_null and self.spec.invalid == "ERROR":
+                raise RuntimeError("Unseen token: null")
+            if any_null and self.spec.invalid == "SKIP":
+                out.append(Column(torch.where(null, torch.zeros_like(hit), hit), null))
+            else:
+                out.append(Column(hit))
+        return out
 
 
 class QuantileDiscretizerModelMapper(_BucketMapperMixin, ModelMapper):

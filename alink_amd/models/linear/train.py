@@ -52,14 +52,33 @@ def java_compare(a, b) -> int:
     return (sa > sb) - (sa < sb)
 
 
+def _int_label_tensor(col):
+    """The label column as an integer / bool tensor (no nulls), or None (other types take the per-value path)."""
+    v = col.values
+    if isinstance(v, torch.Tensor) and v.dim() == 1 and not v.is_floating_point() and not v.is_complex() and \
+            (col.nulls is None or not bool(col.nulls.any())):
+        return v
+    return None
+
+
 def distinct_labels(mt: MTable, label_col: str) -> List[Any]:
     """Global distinct label values (first-seen order across ranks)."""
-    local = []
-    seen = set()
-    for v in mt.col(label_col).to_list():
-        if v is not None and v not in seen:
-            seen.add(v)
-            local.append(v)
+    col = mt.col(label_col)
+    t = _int_label_tensor(col)
+    if t is not None and t.numel():
+        # first-seen order of the distinct values from one unique + first-index pass (what the loop below yields)
+        uq, inv = torch.unique(t, return_inverse=True)
+        first = torch.full((uq.numel(),), t.numel(), dtype=torch.int64, device=t.device)
+        first.scatter_reduce_(0, inv, torch.arange(t.numel(), device=t.device), reduce="amin")
+        vals = uq[torch.argsort(first)].tolist()
+        local = [bool(x) for x in vals] if t.dtype == torch.bool else [int(x) for x in vals]
+    else:
+        local = []
+        seen = set()
+        for v in col.to_list():
+            if v is not None and v not in seen:
+                seen.add(v)
+                local.append(v)
     out, seen = [], set()
     for part in comm.all_gather_object(local):
         for v in part:
@@ -158,13 +177,22 @@ def train_linear(mt: MTable, params: Params, model_type: str, model_name: str, e
     standardization = bool(_pget(params, "standardization", True))
     label_type = Types.DOUBLE if is_reg else mt.col_type(label_col)
     labels = None
-    lab = mt.col(label_col).to_list()
+    lcol = mt.col(label_col)
+    lt = lcol.values if isinstance(lcol.values, torch.Tensor) and lcol.values.dim() == 1 and \
+        (lcol.nulls is None or not bool(lcol.nulls.any())) else None
     if is_reg:
-        y = torch.tensor([float(v) for v in lab], dtype=torch.float64, device=dev)
+        y = lt.to(device=dev, dtype=torch.float64) if lt is not None and not lt.is_complex() else \
+            torch.tensor([float(v) for v in lcol.to_list()], dtype=torch.float64, device=dev)
     else:
         labels = order_binary_labels(distinct_labels(mt, label_col))
-        pos = str(labels[0])
-        y = torch.tensor([1.0 if str(v) == pos else -1.0 for v in lab], dtype=torch.float64, device=dev)
+        it = _int_label_tensor(lcol)
+        if it is not None and isinstance(labels[0], (int, bool)):
+            # integer labels: str(v) == str(labels[0]) <=> v == labels[0]
+            y = torch.where(it.to(dev) == int(labels[0]), 1.0, -1.0).to(torch.float64)
+        else:
+            pos = str(labels[0])
+            y = torch.tensor([1.0 if str(v) == pos else -1.0 for v in lcol.to_list()], dtype=torch.float64,
+                             device=dev)
     X = extract_features(mt, fc, vc, dev)
     d = global_vector_size(X) if vc else len(fc)
     X.set_ncols(d)

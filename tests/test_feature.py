@@ -246,3 +246,85 @@ def test_dense_vector_summary_reference():
               "normL2": [7.416198, 7.416198, 6.7082]}
     for name, e in expect.items():
         assert _dense(getattr(s, name)()) == pytest.approx(e, abs=1e-3), name
+
+
+@pytest.mark.parametrize("invalid", ["KEEP", "SKIP", "ERROR"])
+def test_string_indexer_packed_column_paths_equal_row_path(invalid):
+    """StringIndexer train / predict on a packed string column (device dictionary encoding, one lookup per
+    distinct token) equal the per-value paths: nulls, empty strings, unseen tokens under KEEP / SKIP / ERROR,
+    and the INDEX bucket output of the quantile discretizer stays int64 with its null mask."""
+    import torch
+    from alink_amd.common.params import Params
+    from alink_amd.common.strings import StringBlock
+    from alink_amd.common.table import Column, MTable
+    from alink_amd.common.types import TableSchema, Types
+    from alink_amd.models.feature import encoders as E
+    vals = ["b", "a", None, "", "c", "a", "b", "", None, "zz"] * 7
+    blk = StringBlock.from_list(vals)
+    mt_blk = MTable(TableSchema(["c"], [Types.STRING]), [Column(blk)])
+    mt_lst = MTable(TableSchema(["c"], [Types.STRING]), [Column(list(vals))])
+    assert E._column_token_counts(mt_blk.col("c")) == E._column_token_counts(mt_lst.col("c"))
+    model = E.train_string_indexer(MTable(TableSchema(["c"], [Types.STRING]),
+                                          [Column([v for v in vals if v != "zz"])]),
+                                   Params().set("selectedCol", "c").set("stringOrderType", "ALPHABET_ASC"))
+    p = Params().set("selectedCol", "c").set("outputCol", "i").set("handleInvalid", invalid)
+    m = E.StringIndexerModelMapper(model.schema, mt_blk.schema, p)
+    m.loadModel(list(model.rows()))
+    if invalid == "ERROR":
+        with pytest.raises(RuntimeError):
+            m._map_columns(mt_blk)
+        return
+    got = m._map_columns(mt_blk)[0].to_list()
+    ref = [m.mapColumn(v) for v in vals]
+    assert got == ref
+
+
+@pytest.mark.parametrize("invalid", ["KEEP", "SKIP"])
+@pytest.mark.parametrize("left_open", [True, False])
+def test_bucket_index_tensor_path_equals_numpy_path(invalid, left_open):
+    """INDEX bucketing of tensor columns (torch.searchsorted where the column lives) equals the numpy path:
+    values on the split points (both interval sides), NaN / null cells, +-inf."""
+    import numpy as np
+    import torch
+    from alink_amd.common.params import Params
+    from alink_amd.common.table import Column, MTable
+    from alink_amd.common.types import TableSchema, Types
+    from alink_amd.models.feature.encoders import BucketizerMapper
+    x = torch.tensor([-5.0, 0.0, 1.0, 1.5, 2.0, 3.0, float("nan"), float("inf"), -float("inf"), 2.0, 0.5],
+                     dtype=torch.float64)
+    nulls = torch.zeros(11, dtype=torch.bool)
+    nulls[9] = True
+    mt = MTable(TableSchema(["a"], [Types.DOUBLE]), [Column(x, nulls)])
+    p = Params().set("selectedCols", ["a"]).set("cutsArray", [[0.0, 1.0, 2.0]]).set("leftOpen", left_open) \
+        .set("handleInvalid", invalid).set("encode", "INDEX")
+    m = BucketizerMapper(mt.schema, p)
+    got = m._map_columns(mt)[0]
+    vals = [None if (nulls[i] or np.isnan(x[i].item())) else x[i].item() for i in range(11)]
+    mt2 = MTable(TableSchema(["a"], [Types.DOUBLE]), [Column(vals)])
+    ref = m._map_columns(mt2)[0]
+    assert got.to_list() == ref.to_list()
+
+
+@pytest.mark.parametrize("invalid,enable_else", [("KEEP", False), ("SKIP", False), ("KEEP", True), ("SKIP", True)])
+def test_onehot_packed_column_equals_list_column(invalid, enable_else):
+    """OneHot predict on a packed string column (device dictionary encoding) equals the list-column path:
+    nulls, empty strings, unseen tokens, every invalid / else strategy."""
+    from alink_amd.common.strings import StringBlock
+    from alink_amd.common.table import Column, MTable
+    from alink_amd.common.types import TableSchema, Types
+    from alink_amd.operator.batch.source import TableSourceBatchOp
+    import alink_amd as A
+    train_vals = ["b", "a", "", "c", "a", "b"] * 5
+    vals = ["b", "a", None, "", "c", "zz", "a", None] * 4
+    tr = MTable(TableSchema(["c"], [Types.STRING]), [Column(list(train_vals))])
+    op = A.OneHotTrainBatchOp().setSelectedCols(["c"])
+    if enable_else:
+        op = op.setDiscreteThresholds(6)              # rare tokens go to the 'else' slot
+    model = op.linkFrom(TableSourceBatchOp(tr))
+    outs = []
+    for col in (Column(StringBlock.from_list(vals)), Column(list(vals))):
+        mt = MTable(TableSchema(["c"], [Types.STRING]), [col])
+        op = A.OneHotPredictBatchOp().setSelectedCols(["c"]).setOutputCols(["oh"]).setHandleInvalid(invalid) \
+            .setReservedCols([]).linkFrom(model, TableSourceBatchOp(mt))
+        outs.append([str(v) for v in op.getOutputTable().col("oh").to_list()])
+    assert outs[0] == outs[1]
