@@ -319,3 +319,18 @@ class VectorToColumnsMapper(Mapper):
             return [None] * len(self.outs)
         vec = VectorUtil.getVector(v)
         return [vec.get(i) for i in range(len(self.outs))]
+
+    def _map_columns(self, mt):
+        """Whole columns: the format flavour through the format mapper's columnar paths (it was reached only row
+        by row -- a Double.toString and a parse per value); the ``outputCols`` flavour slices a dense [n, d] tensor
+        column (more output columns than components, or null cells: the row path, which raises as ``Vector.get``
+        on the former)."""
+        if self._delegate is not None:
+            return self._delegate._map_columns(mt)
+        c = mt.cols[self.idx]
+        v = c.values
+        if isinstance(v, torch.Tensor) and v.dim() == 2 and len(self.outs) <= v.shape[1] and \
+                (c.nulls is None or not bool(c.nulls.any())):
+            V = v.to(torch.float64)
+            return [Column(V[:, i].contiguous()) for i in range(len(self.outs))]
+        return super()._map_columns(mt)

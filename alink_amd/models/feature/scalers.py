@@ -205,7 +205,6 @@ class ImputerModelMapper(_ColumnScalerMapper):
         fill = self.model.meta.get("fillValue") if self.model.meta.contains("fillValue") else None
         for j, c in enumerate(self.cols):
             t = self.col_types[j]
-            lst = mt.col(c).to_list()
             if vals is not None:
                 f = float(vals[j])
                 rep = int(f) if t in (Types.LONG, Types.INT, Types.SHORT, Types.BYTE) else f
@@ -222,8 +221,20 @@ class ImputerModelMapper(_ColumnScalerMapper):
                 rep = int(fill)
             else:
                 rep = float(fill)
+            col = mt.col(c)
+            v = col.values
+            if isinstance(v, torch.Tensor) and v.dim() == 1 and t != Types.STRING and \
+                    getattr(t, "torch_dtype", None) is not None:
+                # a tensor column stays a tensor: nulls (and NaN in a float column) take the statistic
+                bad = col.nulls.to(v.device) if col.nulls is not None else torch.zeros(v.shape, dtype=torch.bool,
+                                                                                         device=v.device)
+                if v.is_floating_point():
+                    bad = bad | torch.isnan(v)
+                r = torch.where(bad, torch.tensor(rep, dtype=v.dtype, device=v.device), v)
+                out.append(Column(r.to(t.torch_dtype)))
+                continue
             out.append(Column.from_values([rep if (x is None or (isinstance(x, float) and x != x)) else x
-                                           for x in lst], t))
+                                           for x in col.to_list()], t))
         return out
 
 

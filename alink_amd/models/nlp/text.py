@@ -75,6 +75,18 @@ class TokenizerMapper(SISOMapper):
             return None
         return " ".join(java_split(str(v).lower(), r"\s+")).strip()
 
+    def _map_columns(self, mt):
+        """A packed string column is tokenized byte-parallel where it lives (``ops/strings.tokenize_ws_lower``);
+        anything else (or non-ASCII text) row by row."""
+        from ...common.strings import StringBlock
+        from ...ops.strings import tokenize_ws_lower
+        col = mt.col(self.selected)
+        if isinstance(col.values, StringBlock) and col.nulls is None:
+            blk = tokenize_ws_lower(col.values)
+            if blk is not None:
+                return [Column(blk)]
+        return super()._map_columns(mt)
+
 
 class RegexTokenizerMapper(SISOMapper):
     def __init__(self, dataSchema, params=None):

@@ -220,6 +220,22 @@ def _factorize(c) -> Tuple[Any, int]:
             inv = torch.where(c.nulls.to(inv.device), torch.full_like(inv, k), inv)
             k += 1
         return inv.to(torch.int64), k
+    from ....common.strings import StringBlock
+    if isinstance(v, StringBlock) and len(v):
+        # packed strings: the device dictionary encoding (exact, or None on a hash collision -> the list path)
+        from ....ops.strings import unique_ids
+        enc = unique_ids(v)
+        if enc is not None:
+            ids, rep = enc
+            k = int(rep.numel())
+            nm = v.nulls
+            if c.nulls is not None:
+                cn = c.nulls.to(ids.device)
+                nm = cn if nm is None else (nm.to(ids.device) | cn)
+            if nm is not None:
+                ids = torch.where(nm.to(ids.device), torch.full_like(ids, k), ids)
+                k += 1
+            return ids, k
     vals = c.to_list()
     if not all(x is None or isinstance(x, (str, int, float, bool)) for x in vals):
         return None, 0

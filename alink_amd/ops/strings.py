@@ -21,7 +21,7 @@ import torch
 from ..common.strings import StringBlock
 from . import _lib
 
-__all__ = ["hash_bytes", "murmur3_utf8_index", "murmur3_bytes_py", "split_tokens", "unique_ids"]
+__all__ = ["tokenize_ws_lower", "hash_bytes", "murmur3_utf8_index", "murmur3_bytes_py", "split_tokens", "unique_ids"]
 
 
 def murmur3_bytes_py(b: bytes, seed: int = 0) -> int:
@@ -253,3 +253,34 @@ def unique_ids(block: StringBlock) -> Optional[Tuple[torch.Tensor, torch.Tensor]
         if not bool(torch.equal(block.data[off[:-1][seg] + j], block.data[off[:-1][r][seg] + j])):
             return None
     return ids, rep
+
+
+def tokenize_ws_lower(block: StringBlock) -> Optional[StringBlock]:
+    """TokenizerMapper on a packed block, byte-parallel on its device: ASCII lower case, every run of ``\\s``
+    (space, \\t \\n \\v \\f \\r) between tokens becomes one space, leading / trailing runs go -- what
+    ``" ".join(java_split(s.lower(), "\\s+")).strip()`` gives.  None when a byte is non-ASCII (Unicode lower case)
+    or an ASCII separator 0x1c-0x1f (which Python's strip() also treats as whitespace): the caller's row path."""
+    d, off = block.data, block.offsets
+    n, T = len(block), int(d.numel())
+    if T == 0:
+        return block
+    if bool(((d >= 128) | ((d >= 0x1C) & (d <= 0x1F))).any()):
+        return None
+    dev = d.device
+    ws = (d == 32) | ((d >= 9) & (d <= 13))
+    lens = off[1:] - off[:-1]
+    seg = torch.repeat_interleave(torch.arange(n, device=dev), lens)
+    pos = torch.arange(T, device=dev)
+    start, end = off[:-1][seg], off[1:][seg]
+    prev_ws = torch.zeros_like(ws)
+    prev_ws[1:] = ws[:-1]
+    prev_ws &= pos != start
+    last_nw = torch.cummax(torch.where(~ws, pos, torch.full_like(pos, -1)), 0).values
+    next_nw = torch.flip(torch.cummin(torch.flip(torch.where(~ws, pos, torch.full_like(pos, T)), [0]), 0).values, [0])
+    keep = ~ws | (~prev_ws & (last_nw >= start) & (next_nw < end))
+    low = torch.where((d >= 65) & (d <= 90), d + 32, d)
+    out = torch.where(ws, torch.full_like(d, 32), low)[keep]
+    nl = torch.bincount(seg[keep], minlength=n)
+    noff = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(nl, 0, out=noff[1:])
+    return StringBlock(out, noff, block.nulls)

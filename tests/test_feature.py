@@ -328,3 +328,26 @@ def test_onehot_packed_column_equals_list_column(invalid, enable_else):
             .setReservedCols([]).linkFrom(model, TableSourceBatchOp(mt))
         outs.append([str(v) for v in op.getOutputTable().col("oh").to_list()])
     assert outs[0] == outs[1]
+
+
+def test_imputer_tensor_columns_equal_list_columns():
+    """Imputer on tensor columns (nulls and NaN replaced on the tensor) equals the list path, int and double."""
+    import torch
+    from alink_amd.common.table import Column, MTable
+    from alink_amd.common.types import TableSchema, Types
+    from alink_amd.operator.batch.source import TableSourceBatchOp
+    import alink_amd as A
+    x = torch.tensor([1.0, float("nan"), 3.0, 4.0, 0.5], dtype=torch.float64)
+    xn = torch.tensor([False, False, False, True, False])
+    k = torch.tensor([1, 2, 3, 4, 5], dtype=torch.int64)
+    kn = torch.tensor([False, True, False, False, False])
+    schema = TableSchema(["x", "k"], [Types.DOUBLE, Types.LONG])
+    t_mt = MTable(schema, [Column(x, xn), Column(k, kn)])
+    l_mt = MTable(schema, [Column([1.0, float("nan"), 3.0, None, 0.5]), Column([1, None, 3, 4, 5])])
+    for strategy in ("MEAN", "MIN", "VALUE"):
+        op = A.ImputerTrainBatchOp().setSelectedCols(["x", "k"]).setStrategy(strategy)
+        if strategy == "VALUE":
+            op = op.setFillValue("7")
+        model = op.linkFrom(TableSourceBatchOp(l_mt))
+        outs = [A.ImputerPredictBatchOp().linkFrom(model, TableSourceBatchOp(m)).collect() for m in (t_mt, l_mt)]
+        assert [tuple(r) for r in outs[0]] == [tuple(r) for r in outs[1]], strategy

@@ -287,3 +287,24 @@ def test_vector_to_writers_fast_equals_rows(to, named):
     mt2 = MTable(mt.schema, [Column(strs[:4] + ["1.0 2.0"])])       # a shorter row: the row path
     assert m._fast(m, mt2) is None
     _both(m, mt2)
+
+
+@pytest.mark.parametrize("flavour", ["outputCols", "schemaStr"])
+def test_vector_to_columns_columnar_equals_rows(flavour):
+    """VectorToColumns on a dense tensor vector column (both flavours) equals the per-row mapping (schema columns
+    past the vector's width: 0.0)."""
+    import torch
+    from alink_amd.common.params import Params
+    from alink_amd.common.table import Column, MTable
+    from alink_amd.common.types import TableSchema, Types
+    from alink_amd.models.dataproc.vector import VectorToColumnsMapper
+    V = torch.randn(9, 3, dtype=torch.float64)
+    mt = MTable(TableSchema(["v"], [Types.DENSE_VECTOR]), [Column(V)])
+    p = Params().set("selectedCol", "v").set("reservedCols", [])
+    p = p.set("outputCols", ["a", "b", "c"]) if flavour == "outputCols" else \
+        p.set("schemaStr", "a double, b double, c double, d double")
+    m = VectorToColumnsMapper(mt.schema, p)
+    got = [c.to_list() for c in m._map_columns(mt)]
+    rows = [m._map_row_values(r) for r in mt.rows()]
+    ref = [[r[j] for r in rows] for j in range(len(got))]
+    assert got == ref

@@ -329,3 +329,21 @@ def test_doc_count_model_rows_fast_format_equals_gson():
     ref = [gson_dumps(_Tuple3(w, float(idf), i), java_map_order=False) for i, (w, _, idf) in enumerate(keep)]
     assert _tuple3_rows(keep) == ref
     assert _tuple3_rows([]) == []
+
+
+def test_tokenizer_packed_block_equals_row_path():
+    """Tokenizer on a packed block (byte-parallel lower case + whitespace runs) equals the per-row mapper: leading /
+    trailing / mixed whitespace runs, all-whitespace and empty strings, nulls; non-ASCII text takes the row path."""
+    from alink_amd.common.params import Params
+    from alink_amd.common.strings import StringBlock
+    from alink_amd.common.table import Column, MTable
+    from alink_amd.common.types import TableSchema, Types
+    from alink_amd.models.nlp.text import TokenizerMapper
+    vals = ["Hello  World", "  Lead and TRAIL \\t\\n", "", "   ", None, "a\\tb\\x0bc\\x0cd\\re", "MiXeD 123 !@#",
+            "x", " y", "z ", "A  B   C    D"] * 3
+    for extra in ([], ["Ünïcode Tëxt"]):
+        v = vals + extra
+        mt = MTable(TableSchema(["s"], [Types.STRING]), [Column(StringBlock.from_list(v))])
+        m = TokenizerMapper(mt.schema, Params().set("selectedCol", "s").set("outputCol", "t"))
+        got = m._map_columns(mt)[0].to_list()
+        assert got == [m.mapColumn(x) for x in v]

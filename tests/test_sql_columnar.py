@@ -113,3 +113,25 @@ def test_columnar_distinct_equals_row_path(monkeypatch):
     monkeypatch.setattr(E, "_row_codes", lambda *a: None)
     ref = E.sql_distinct(mt).rows()
     assert [tuple(r) for r in got] == [tuple(r) for r in ref]
+
+
+def test_groupby_distinct_packed_string_keys_equal_list_keys():
+    """GROUP BY / DISTINCT on a packed string key (device dictionary codes) give the rows and order of the list
+    key (first appearance), nulls and empty strings as their own groups."""
+    import torch
+    from alink_amd.common.strings import StringBlock
+    from alink_amd.common.table import Column, MTable
+    from alink_amd.common.types import TableSchema, Types
+    from alink_amd.operator.common.sql.engine import sql_distinct
+    import alink_amd as A
+    from alink_amd.operator.batch.source import TableSourceBatchOp
+    keys = ["b", "a", None, "", "b", "c", None, "a", "", "b"] * 3
+    x = torch.arange(len(keys), dtype=torch.float64)
+    outs = []
+    for kc in (Column(StringBlock.from_list(keys)), Column(list(keys))):
+        mt = MTable(TableSchema(["k", "x"], [Types.STRING, Types.DOUBLE]), [kc, Column(x)])
+        g = A.GroupByBatchOp().setGroupByPredicate("k").setSelectClause("k, COUNT(*) AS n, SUM(x) AS s") \
+            .linkFrom(TableSourceBatchOp(mt)).collect()
+        d = sql_distinct(MTable(TableSchema(["k"], [Types.STRING]), [kc])).col("k").to_list()
+        outs.append(([tuple(r) for r in g], d))
+    assert outs[0] == outs[1]

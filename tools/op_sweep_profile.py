@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--rows", type=int, default=10_000_000)
     ap.add_argument("--only", default="")
     ap.add_argument("--top", type=int, default=8)
+    ap.add_argument("--set", type=int, default=1, help="1: model ops; 2: data processing / SQL / scalers")
     a = ap.parse_args()
     import alink_amd as A
     from alink_amd.common.table import Column, MTable
@@ -89,6 +90,38 @@ def main():
         "standard_scaler_train": lambda: A.StandardScalerTrainBatchOp().setSelectedCols(names)
         .linkFrom(TableSourceBatchOp(dense)).getOutputTable(),
     }
+    if a.set == 2:
+        ss = A.StandardScalerTrainBatchOp().setSelectedCols(names).linkFrom(TableSourceBatchOp(dense))
+        mm = A.MinMaxScalerTrainBatchOp().setSelectedCols(names).linkFrom(TableSourceBatchOp(dense))
+        imp = A.ImputerTrainBatchOp().setSelectedCols(names).setStrategy("MEAN").linkFrom(TableSourceBatchOp(dense))
+        src = TableSourceBatchOp(dense)
+        catsrc = TableSourceBatchOp(MTable(TableSchema(["c", "x0", "label"], [Types.STRING, Types.DOUBLE, Types.INT]),
+                                           [catcol.col("c"), cols[0], Column(y)]))
+        jobs = {
+            "standard_scaler_predict": lambda: A.StandardScalerPredictBatchOp().linkFrom(ss, src).getOutputTable(),
+            "minmax_scaler_predict": lambda: A.MinMaxScalerPredictBatchOp().linkFrom(mm, src).getOutputTable(),
+            "imputer_predict": lambda: A.ImputerPredictBatchOp().linkFrom(imp, src).getOutputTable(),
+            "feature_hasher": lambda: A.FeatureHasherBatchOp().setSelectedCols(["c", "x0"]).setOutputCol("h")
+            .setReservedCols([]).linkFrom(catsrc).getOutputTable().col("h").values,
+            "columns_to_vector": lambda: A.ColumnsToVectorBatchOp().setSelectedCols(names).setVectorCol("v")
+            .setReservedCols([]).linkFrom(src).getOutputTable().col("v").values,
+            "vector_to_columns": lambda: A.VectorToColumnsBatchOp().setSelectedCol("v")
+            .setSchemaStr(", ".join(f"y{i} double" for i in range(F))).setReservedCols([])
+            .linkFrom(A.VectorAssemblerBatchOp().setSelectedCols(names).setOutputCol("v").setReservedCols([])
+                      .linkFrom(src)).getOutputTable(),
+            "where": lambda: A.WhereBatchOp().setClause("x0 > 0.5 AND x1 < 0").linkFrom(src).getOutputTable(),
+            "select": lambda: A.SelectBatchOp().setClause("x0 + x1 AS s, x2 * 2 AS t, label")
+            .linkFrom(src).getOutputTable(),
+            "groupby": lambda: A.GroupByBatchOp().setGroupByPredicate("c")
+            .setSelectClause("c, COUNT(*) AS n, AVG(x0) AS m").linkFrom(catsrc).getOutputTable(),
+            "split": lambda: A.SplitBatchOp().setFraction(0.8).linkFrom(src).getOutputTable(),
+            "sample": lambda: A.SampleBatchOp().setRatio(0.1).linkFrom(src).getOutputTable(),
+            "numerical_type_cast": lambda: A.NumericalTypeCastBatchOp().setSelectedCols(names[:5])
+            .setTargetType("INT").linkFrom(src).getOutputTable(),
+            "summarizer": lambda: A.SummarizerBatchOp().setSelectedCols(names).linkFrom(src).collectSummary(),
+            "tokenizer": lambda: A.TokenizerBatchOp().setSelectedCol("c").setOutputCol("t")
+            .linkFrom(catsrc).getOutputTable(),
+        }
     only = [s for s in a.only.split(",") if s]
     for name, fn in jobs.items():
         if only and name not in only:
