@@ -175,6 +175,33 @@ class AppendIdBatchOp(BatchOperator):
         return self
 
 
+def _cast_tensor_column(col, t):
+    """``float(v)`` / ``int(float(v))`` over a numeric tensor column at once (through float64, as the row path
+    rounds), nulls kept; None (the row path) for other columns, a NaN / infinite value under an integer target
+    (the row path raises) or a value outside the integer target's range."""
+    import torch
+    v = col.values
+    dt = getattr(t, "torch_dtype", None)
+    if not (isinstance(v, torch.Tensor) and v.dim() == 1 and dt is not None and not v.is_complex()):
+        return None
+    nm = col.nulls.to(v.device) if col.nulls is not None else None
+    x = v.to(torch.float64)
+    if t.py is float:
+        r = x.to(dt)
+    else:
+        live = x if nm is None else x[~nm]
+        if live.numel() and not bool(torch.isfinite(live).all()):
+            return None
+        x = torch.trunc(torch.where(nm, torch.zeros_like(x), x) if nm is not None else x)
+        info = torch.iinfo(dt)
+        if x.numel() and (float(x.min()) < info.min or float(x.max()) > info.max):
+            return None
+        r = x.to(dt)
+    if nm is not None:
+        r = torch.where(nm, torch.zeros_like(r), r)
+    return Column(r, nm)
+
+
 class NumericalTypeCastBatchOp(BatchOperator):
     def linkFrom(self, *inputs):
         mt = self.checkAndGetFirst(inputs).getOutputTable()
@@ -183,10 +210,14 @@ class NumericalTypeCastBatchOp(BatchOperator):
         sel = self.getSelectedCols()
         names, types, cols = [], [], []
         for n in sel:
-            vals = mt.column_values(n)
-            conv = [None if v is None else (float(v) if t.py is float else int(float(v))) for v in vals]
             names.append(n)
             types.append(t)
+            fast = _cast_tensor_column(mt.col(n), t)
+            if fast is not None:
+                cols.append(fast)
+                continue
+            vals = mt.column_values(n)
+            conv = [None if v is None else (float(v) if t.py is float else int(float(v))) for v in vals]
             cols.append(Column.from_values(conv, t))
         self.setOutputTable(mt.with_columns(names, types, cols))
         return self

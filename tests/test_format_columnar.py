@@ -308,3 +308,23 @@ def test_vector_to_columns_columnar_equals_rows(flavour):
     rows = [m._map_row_values(r) for r in mt.rows()]
     ref = [[r[j] for r in rows] for j in range(len(got))]
     assert got == ref
+
+
+@pytest.mark.parametrize("target", ["DOUBLE", "INT", "BIGINT"])
+def test_numerical_type_cast_tensor_equals_list(target):
+    """NumericalTypeCast over tensor columns equals the per-value path: truncation toward zero, nulls kept."""
+    import torch
+    from alink_amd.common.table import Column, MTable
+    from alink_amd.common.types import TableSchema, Types
+    from alink_amd.operator.batch.source import TableSourceBatchOp
+    import alink_amd as A
+    x = torch.tensor([1.7, -1.7, 0.0, -0.0, 2.5, 1e9, -3.999], dtype=torch.float64)
+    xn = torch.tensor([False, False, True, False, False, False, False])
+    k = torch.tensor([3, -4, 5, 2 ** 40, 0, 7, 9], dtype=torch.int64)
+    schema = TableSchema(["x", "k"], [Types.DOUBLE, Types.LONG])
+    tm = MTable(schema, [Column(x, xn), Column(k)])
+    lm = MTable(schema, [Column([None if xn[i] else float(x[i]) for i in range(7)]), Column(k.tolist())])
+    cols = ["x"] if target == "INT" else ["x", "k"]
+    outs = [A.NumericalTypeCastBatchOp().setSelectedCols(cols).setTargetType(target)
+            .linkFrom(TableSourceBatchOp(m)).collect() for m in (tm, lm)]
+    assert [tuple(r) for r in outs[0]] == [tuple(r) for r in outs[1]]
