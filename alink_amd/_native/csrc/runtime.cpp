@@ -164,7 +164,7 @@ static int32_t murmur3_utf16(const uint16_t* chars, int64_t len, uint32_t seed) 
 // batch: strings given as UTF-16 code units concatenated, offsets (in code units) n+1
 void alink_murmur3_utf16_batch(const uint16_t* chars, const int64_t* off, int64_t n, uint32_t seed,
                                int32_t* out) {
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) if (n > 4096)
     for (int64_t i = 0; i < n; ++i) out[i] = murmur3_utf16(chars + off[i], off[i + 1] - off[i], seed);
 }
 
@@ -236,7 +236,7 @@ void alink_murmur3_utf8_batch(const uint8_t* bytes, const int64_t* off, int64_t 
 int alink_parse_dense_vectors(const char* buf, const int64_t* off, int64_t n, int64_t d, double* out,
                               int64_t* counts) {
     int64_t err = -1;
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) if (n > 64)
     for (int64_t i = 0; i < n; ++i) {
         const char* p = buf + off[i];
         const char* e = buf + off[i + 1];

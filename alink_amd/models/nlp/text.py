@@ -533,6 +533,64 @@ class _VectorizerMapper(ModelMapper):
         v = row[self.col_idx]
         return [None if v is None else self._vec(str(v))]
 
+    # ---- columnar path: a packed document column, every document's vector from whole-token-array ops
+    def _token_features(self, tok):
+        """(feature index int64 [T], token counts toward the vector bool [T], idf / value table fp64 [F]) of the
+        tokens, or None (the row path)."""
+        raise NotImplementedError
+
+    def _map_columns(self, mt):
+        from ...common.strings import StringBlock
+        col = mt.col(self.col)
+        if isinstance(col.values, StringBlock) and col.nulls is None and len(col.values):
+            out = self._columnar(col.values)
+            if out is not None:
+                return [out]
+        return super()._map_columns(mt)
+
+    def _columnar(self, blk):
+        from ...common.linalg.block import SparseBlock
+        from ...ops.strings import split_tokens
+        n = len(blk)
+        tok, doc = split_tokens(blk)
+        dev = doc.device
+        ntok = torch.bincount(doc, minlength=n)
+        nulls = blk.nulls.to(dev) if blk.nulls is not None else None
+        live = ntok if nulls is None else ntok[~nulls]
+        if bool((live == 0).any()):
+            return None                  # an all-space document: 1 / len(tokens) fails on the row path too
+        feats = self._token_features(tok)
+        if feats is None:
+            return None
+        fidx, ok, table = feats
+        F = int(self.feature_size)
+        key = doc[ok] * F + fidx[ok]
+        uk, cnt = torch.unique(key, return_counts=True)          # sorted: by document, then feature index
+        d, i = uk // F, uk % F
+        nt = ntok.to(torch.float64)[d]
+        c = cnt.to(torch.float64)
+        min_count = torch.full_like(nt, self.min_tf) if self.min_tf >= 1.0 else self.min_tf * nt
+        keep = c >= min_count
+        ratio = 1.0 / nt
+        idf = table.to(dev)[i]
+        ft = self.ftype
+        if ft == "IDF":
+            val = idf
+        elif ft == "WORD_COUNT":
+            val = c
+        elif ft == "TF_IDF":
+            val = idf * c * ratio
+        elif ft == "BINARY":
+            val = torch.ones_like(c)
+        elif ft == "TF":
+            val = c * ratio
+        else:
+            return None
+        per = torch.bincount(d[keep], minlength=n)
+        crow = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+        torch.cumsum(per, 0, out=crow[1:])
+        return Column(SparseBlock(crow, i[keep], val[keep], F), nulls)
+
 
 class DocCountVectorizerModelMapper(_VectorizerMapper):
     def loadModel(self, rows):
@@ -545,6 +603,22 @@ class DocCountVectorizerModelMapper(_VectorizerMapper):
             d = json.loads(s)
             self.vocab[d["f0"]] = (int(d["f2"]), float(d["f1"]))
         self.n = len(data)
+        self.feature_size = self.n
+
+    def _token_features(self, tok):
+        """Vocabulary ids through the device dictionary encoding of the tokens: one dict probe per distinct token."""
+        from ...ops.strings import unique_ids
+        enc = unique_ids(tok)
+        if enc is None:
+            return None
+        ids, rep = enc
+        words = tok.take(rep).to_list()
+        lut = torch.tensor([self.vocab[w][0] if w in self.vocab else -1 for w in words] or [0], dtype=torch.int64)
+        table = torch.zeros(max(self.n, 1), dtype=torch.float64)
+        for w, (j, idf) in self.vocab.items():
+            table[j] = idf
+        fidx = lut.to(ids.device)[ids] if len(words) else ids
+        return fidx.clamp(min=0), fidx >= 0, table
 
     def _vec(self, content):
         toks = java_split(content, WORD_DELIMITER)
@@ -565,6 +639,20 @@ class DocHashCountVectorizerModelMapper(_VectorizerMapper):
         self.min_tf = float(meta.get("minTF"))
         self.ftype = _ename(meta.get("featureType"), "WORD_COUNT")
         self.idf = {int(k): float(v) for k, v in json.loads(data[0]).items()} if data else {}
+        self.feature_size = self.nf
+
+    def _token_features(self, tok):
+        """Guava murmur3 bucket of every token on the device (empty tokens included, as the row path hashes them);
+        the model's idf map as a dense [numFeatures] table and membership mask."""
+        from ...ops.strings import murmur3_utf8_index
+        idx = murmur3_utf8_index(tok, self.nf)
+        table = torch.zeros(max(self.nf, 1), dtype=torch.float64)
+        mask = torch.zeros(max(self.nf, 1), dtype=torch.bool)
+        if self.idf:
+            k = torch.tensor(list(self.idf.keys()), dtype=torch.int64)
+            table[k] = torch.tensor(list(self.idf.values()), dtype=torch.float64)
+            mask[k] = True
+        return idx, mask.to(idx.device)[idx], table
 
     def _vec(self, content):
         from ..feature.encoders import murmur3_index

@@ -347,3 +347,33 @@ def test_tokenizer_packed_block_equals_row_path():
         m = TokenizerMapper(mt.schema, Params().set("selectedCol", "s").set("outputCol", "t"))
         got = m._map_columns(mt)[0].to_list()
         assert got == [m.mapColumn(x) for x in v]
+
+
+@pytest.mark.parametrize("ftype", ["WORD_COUNT", "TF_IDF", "TF", "BINARY", "IDF"])
+@pytest.mark.parametrize("min_tf", [1.0, 2.0, 0.3])
+def test_doc_vectorizer_predict_packed_equals_row_path(ftype, min_tf):
+    """DocCount / DocHashCount predict on a packed document column (token arrays on the device) equal the per-row
+    mapper: repeated words, double spaces (empty tokens), unseen words, nulls, every feature type, absolute and
+    relative minTF."""
+    from alink_amd.common.params import Params
+    from alink_amd.common.strings import StringBlock
+    from alink_amd.common.table import Column, MTable
+    from alink_amd.common.types import TableSchema, Types
+    from alink_amd.models.nlp import text as T
+    train = ["a b c a", "b b d", "c a e", "e e e b", "f"] * 4
+    docs = ["a b c a a", "b  b d", None, "zz a", "e", "", "a a a b b c d e f"] * 3
+    mtr = MTable(TableSchema(["doc"], [Types.STRING]), [Column(list(train))])
+    for kind in ("count", "hash"):
+        p = Params().set("selectedCol", "doc").set("minTF", min_tf).set("featureType", ftype)
+        if kind == "count":
+            rows = T.train_doc_count_vectorizer(mtr, p)
+            mapper_cls = T.DocCountVectorizerModelMapper
+        else:
+            rows = T.train_doc_hash_count_vectorizer(mtr, p.clone().set("numFeatures", 64))
+            mapper_cls = T.DocHashCountVectorizerModelMapper
+        mt = MTable(TableSchema(["doc"], [Types.STRING]), [Column(StringBlock.from_list(docs))])
+        m = mapper_cls(None, mt.schema, Params().set("selectedCol", "doc").set("outputCol", "v"))
+        m.loadModel(rows)
+        got = m._map_columns(mt)[0].to_list()
+        ref = [m._map_row_values([d])[0] for d in docs]
+        assert [str(x) for x in got] == [str(x) for x in ref], kind

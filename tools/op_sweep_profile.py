@@ -24,7 +24,8 @@ def main():
     ap.add_argument("--rows", type=int, default=10_000_000)
     ap.add_argument("--only", default="")
     ap.add_argument("--top", type=int, default=8)
-    ap.add_argument("--set", type=int, default=1, help="1: model ops; 2: data processing / SQL / scalers")
+    ap.add_argument("--set", type=int, default=1,
+                    help="1: model ops; 2: data processing / SQL / scalers; 3: evaluation / NLP / trees / formats")
     a = ap.parse_args()
     import alink_amd as A
     from alink_amd.common.table import Column, MTable
@@ -121,6 +122,53 @@ def main():
             "summarizer": lambda: A.SummarizerBatchOp().setSelectedCols(names).linkFrom(src).collectSummary(),
             "tokenizer": lambda: A.TokenizerBatchOp().setSelectedCol("c").setOutputCol("t")
             .linkFrom(catsrc).getOutputTable(),
+        }
+    if a.set == 3:
+        src = TableSourceBatchOp(dense)
+        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+        from nlp_count_bench import make_docs
+        docsrc = TableSourceBatchOp(MTable(TableSchema(["doc"], [Types.STRING]),
+                                           [Column(make_docs(n, 6, 1000, dev))]))
+        yreg = cols[0].values * 2 + cols[1].values
+        reg = MTable(TableSchema(["label", "p"], [Types.DOUBLE, Types.DOUBLE]),
+                     [Column(yreg), Column(yreg + 0.1 * torch.randn(n, generator=g, device=dev, dtype=torch.float64))])
+        ml = MTable(TableSchema(["label", "pred"], [Types.INT, Types.INT]),
+                    [Column(torch.randint(0, 5, (n,), generator=g, device=dev).to(torch.int32)),
+                     Column(torch.randint(0, 5, (n,), generator=g, device=dev).to(torch.int32))])
+        small = MTable(TableSchema(names + ["label"], [Types.DOUBLE] * F + [Types.INT]),
+                       [Column(c.values[:200000]) for c in cols] + [Column(y[:200000])])
+        dt_model = A.DecisionTreeTrainBatchOp().setFeatureCols(names).setLabelCol("label").setMaxDepth(6) \
+            .linkFrom(TableSourceBatchOp(small))
+        rf_model = A.RandomForestTrainBatchOp().setFeatureCols(names).setLabelCol("label").setMaxDepth(6) \
+            .setNumTrees(10).linkFrom(TableSourceBatchOp(small))
+        dhc = A.DocHashCountVectorizerTrainBatchOp().setSelectedCol("doc").linkFrom(docsrc)
+        dcc = A.DocCountVectorizerTrainBatchOp().setSelectedCol("doc").linkFrom(docsrc)
+        jobs = {
+            "eval_regression": lambda: A.EvalRegressionBatchOp().setLabelCol("label").setPredictionCol("p")
+            .linkFrom(TableSourceBatchOp(reg)).collect(),
+            "eval_multiclass": lambda: A.EvalMultiClassBatchOp().setLabelCol("label").setPredictionCol("pred")
+            .linkFrom(TableSourceBatchOp(ml)).collect(),
+            "binarizer": lambda: A.BinarizerBatchOp().setSelectedCol("x0").setOutputCol("b").setThreshold(0.1)
+            .linkFrom(src).getOutputTable(),
+            "bucketizer": lambda: A.BucketizerBatchOp().setSelectedCols(["x0", "x1"])
+            .setCutsArray([[-1.0, 0.0, 1.0], [0.0]]).linkFrom(src).getOutputTable(),
+            "dt_predict": lambda: A.DecisionTreePredictBatchOp().setPredictionCol("p").setReservedCols([])
+            .linkFrom(dt_model, src).getOutputTable().col("p").values,
+            "rf_predict": lambda: A.RandomForestPredictBatchOp().setPredictionCol("p").setReservedCols([])
+            .linkFrom(rf_model, src).getOutputTable().col("p").values,
+            "stopwords": lambda: A.StopWordsRemoverBatchOp().setSelectedCol("doc").setOutputCol("o")
+            .linkFrom(docsrc).getOutputTable(),
+            "ngram": lambda: A.NGramBatchOp().setSelectedCol("doc").setOutputCol("o").linkFrom(docsrc)
+            .getOutputTable(),
+            "dochash_predict": lambda: A.DocHashCountVectorizerPredictBatchOp().setSelectedCol("doc")
+            .setOutputCol("v").linkFrom(dhc, docsrc).getOutputTable().col("v").values,
+            "doccount_predict": lambda: A.DocCountVectorizerPredictBatchOp().setSelectedCol("doc")
+            .setOutputCol("v").linkFrom(dcc, docsrc).getOutputTable().col("v").values,
+            "append_id": lambda: A.AppendIdBatchOp().linkFrom(src).getOutputTable(),
+            "columns_to_kv": lambda: A.ColumnsToKvBatchOp().setSelectedCols(names[:5]).setKvCol("kv")
+            .setReservedCols([]).linkFrom(src).getOutputTable(),
+            "columns_to_json": lambda: A.ColumnsToJsonBatchOp().setSelectedCols(names[:5]).setJsonCol("j")
+            .setReservedCols([]).linkFrom(src).getOutputTable(),
         }
     only = [s for s in a.only.split(",") if s]
     for name, fn in jobs.items():
