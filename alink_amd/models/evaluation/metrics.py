@@ -427,9 +427,38 @@ def multi_summary_from_pred(labels_col, preds, label_array: List[str], device=No
     return _confusion(pi, li, len(label_array), -1.0, len(pi), dev)
 
 
+def multi_summary_pred_tensors(lc, pc, binary: bool, pos, device=None):
+    """(confusion matrix, -1, rows, label array) of integer / bool label and prediction tensor columns with no
+    per-row Python: the label set from the distinct values of each column (as ``str`` of the value, every rank's
+    union), the codes by ``searchsorted`` over the distinct values.  None for other column types."""
+    a, b = lc.values, pc.values
+    ok_t = lambda v: isinstance(v, torch.Tensor) and v.dim() == 1 and not v.is_floating_point() and \
+        not v.is_complex()
+    if not (ok_t(a) and ok_t(b)) or a.dtype != b.dtype:
+        return None
+    dev = device or torch.device("cpu")
+    a, b = a.to(dev), b.to(dev)
+    nl = lc.nulls.to(dev) if lc.nulls is not None else torch.zeros(a.shape, dtype=torch.bool, device=dev)
+    npd = pc.nulls.to(dev) if pc.nulls is not None else torch.zeros(b.shape, dtype=torch.bool, device=dev)
+    uniq = torch.unique(torch.cat([a[~nl], b[~npd]]))
+    strs = [str(v) for v in uniq.tolist()]
+    label_set = set()
+    for part in comm.all_gather_object(sorted(set(strs))):
+        label_set.update(part)
+    arr = build_label_index(label_set, binary, pos)
+    index = {l: i for i, l in enumerate(arr)}
+    lut = torch.tensor([index[x] for x in strs] or [0], dtype=torch.long, device=dev)
+    ok = ~(nl | npd)
+    la, pa = a[ok], b[ok]
+    li = lut[torch.searchsorted(uniq, la)] if la.numel() else la.long()
+    pi = lut[torch.searchsorted(uniq, pa)] if pa.numel() else pa.long()
+    mat, ll, n = _confusion(pi, li, len(arr), -1.0, int(la.numel()), dev)
+    return mat, ll, n, arr
+
+
 def _confusion(pi, li, K, ll, n, dev):
-    p = torch.tensor(pi, dtype=torch.long, device=dev)
-    l = torch.tensor(li, dtype=torch.long, device=dev)
+    p = torch.as_tensor(pi, dtype=torch.long, device=dev)
+    l = torch.as_tensor(li, dtype=torch.long, device=dev)
     mat = torch.bincount(p * K + l, minlength=K * K).double()
     buf = torch.cat([mat, torch.tensor([max(ll, 0.0), float(n)], dtype=torch.float64, device=dev)])
     comm.all_reduce(buf, "sum")
@@ -439,8 +468,10 @@ def _confusion(pi, li, K, ll, n, dev):
 
 def regression_summary(y, pred, device=None):
     dev = device or torch.device("cpu")
-    yv = torch.as_tensor(np.asarray(y, dtype=np.float64), device=dev)
-    pv = torch.as_tensor(np.asarray(pred, dtype=np.float64), device=dev)
+    yv = y.to(dev, torch.float64) if isinstance(y, torch.Tensor) else \
+        torch.as_tensor(np.asarray(y, dtype=np.float64), device=dev)
+    pv = pred.to(dev, torch.float64) if isinstance(pred, torch.Tensor) else \
+        torch.as_tensor(np.asarray(pred, dtype=np.float64), device=dev)
     diff = (yv - pv).abs()
     buf = torch.stack([yv.sum(), (yv * yv).sum(), pv.sum(), (pv * pv).sum(), diff.sum(), (diff * diff).sum(),
                        (diff / yv).abs().sum(), torch.tensor(float(yv.shape[0]), dtype=torch.float64, device=dev)])

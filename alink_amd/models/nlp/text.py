@@ -131,6 +131,26 @@ class StopWordsRemoverMapper(SISOMapper):
                if t and (t if self.case else t.lower()) not in self.stop]
         return WORD_DELIMITER.join(out)
 
+    def _map_columns(self, mt):
+        """Packed documents: split on the device, one stop-word test per DISTINCT token, the kept tokens joined
+        back byte-parallel (``ops/strings.join_tokens``)."""
+        from ...common.strings import StringBlock
+        from ...ops.strings import join_tokens, split_tokens, unique_ids
+        col = mt.col(self.selected)
+        blk = col.values
+        if isinstance(blk, StringBlock) and col.nulls is None and len(blk):
+            tok, doc = split_tokens(blk)
+            enc = unique_ids(tok)
+            if enc is not None:
+                ids, rep = enc
+                words = tok.take(rep).to_list()
+                ok = torch.tensor([bool(w) and (w if self.case else w.lower()) not in self.stop for w in words]
+                                  or [False], dtype=torch.bool)
+                keep = ok.to(ids.device)[ids] if len(words) else torch.zeros(0, dtype=torch.bool,
+                                                                             device=ids.device)
+                return [Column(join_tokens(tok, doc, keep, len(blk), blk.nulls))]
+        return super()._map_columns(mt)
+
 
 class NGramMapper(SISOMapper):
     def __init__(self, dataSchema, params=None):
@@ -145,6 +165,21 @@ class NGramMapper(SISOMapper):
         toks = java_split(str(v), WORD_DELIMITER)
         grams = ["_".join(toks[i:i + self.n]) for i in range(0, 1 + len(toks) - self.n)]
         return WORD_DELIMITER.join(grams).strip()
+
+    def _map_columns(self, mt):
+        """Packed ASCII documents with n >= 2: split on the device and the grams assembled byte-parallel
+        (``ops/strings.ngram_join``); other input (non-ASCII or \\t.. \\r / 0x1c-0x1f bytes, which strip()
+        treats as whitespace) row by row."""
+        from ...common.strings import StringBlock
+        from ...ops.strings import ngram_join, split_tokens
+        col = mt.col(self.selected)
+        blk = col.values
+        if isinstance(blk, StringBlock) and col.nulls is None and len(blk) and self.n >= 2:
+            d = blk.data
+            if not bool(((d >= 128) | ((d >= 9) & (d <= 13)) | ((d >= 0x1C) & (d <= 0x1F))).any()):
+                tok, doc = split_tokens(blk)
+                return [Column(ngram_join(tok, doc, len(blk), self.n, blk.nulls))]
+        return super()._map_columns(mt)
 
 
 # ---------------------------------------------------------------------------------------------------

@@ -3,10 +3,12 @@ each outputs ONE row ``Data`` = the metrics ``Params`` JSON; ``collectMetrics()`
 from __future__ import annotations
 
 import numpy as np
+import torch
 
 from ...common.table import MTable
 from ...common.types import TableSchema, Types
 from ...models.evaluation import metrics as M
+
 from ...parallel import comm
 from ..base import BatchOperator
 
@@ -66,9 +68,9 @@ class _EvalClass(_EvalBase):
         detail_col = _pget(p, "predictionDetailCol")
         pred_col = _pget(p, "predictionCol")
         pos = _pget(p, "positiveLabelValueString")
-        labels = mt.column_values(label_col)
         dev = self.env.device
         if detail_col:
+            labels = mt.column_values(label_col)
             from ...common.detail import DetailBlock
             dvals = mt.col(detail_col).values
             blk = dvals if isinstance(dvals, DetailBlock) else None
@@ -107,9 +109,24 @@ class _EvalClass(_EvalBase):
                 return self._out(M.binary_metrics(pb, nb, arr, ll, n))
             mat, ll, n = M.multi_summary_from_detail(labels, details, arr, dev)
         elif pred_col:
-            preds = mt.column_values(pred_col)
-            arr = M.build_label_index(_global_labels(labels) | _global_labels(preds), self.BINARY, pos)
-            mat, ll, n = M.multi_summary_from_pred(labels, preds, arr, dev)
+            # integer / bool tensor columns: codes without a Python pass over the rows (every rank must take the
+            # same branch: the label-set gather differs)
+            fast_ok = M.multi_summary_pred_tensors if mt.num_rows else None
+            use_fast = fast_ok is not None and all(
+                isinstance(mt.col(c).values, torch.Tensor) and mt.col(c).values.dim() == 1 and
+                not mt.col(c).values.is_floating_point() for c in (label_col, pred_col)) and \
+                mt.col(label_col).values.dtype == mt.col(pred_col).values.dtype
+            if comm.is_distributed():
+                use_fast = bool(min(comm.all_gather_object(bool(use_fast))))
+            fast = M.multi_summary_pred_tensors(mt.col(label_col), mt.col(pred_col), self.BINARY, pos, dev) \
+                if use_fast else None
+            if fast is not None:
+                mat, ll, n, arr = fast
+            else:
+                labels = mt.column_values(label_col)
+                preds = mt.column_values(pred_col)
+                arr = M.build_label_index(_global_labels(labels) | _global_labels(preds), self.BINARY, pos)
+                mat, ll, n = M.multi_summary_from_pred(labels, preds, arr, dev)
         else:
             raise ValueError("Error Input, must give either predictionCol or predictionDetailCol!")
         if n == 0:
@@ -131,10 +148,20 @@ class EvalRegressionBatchOp(_EvalBase):
 
     def linkFrom(self, *inputs):
         mt = self.checkAndGetFirst(inputs).getOutputTable()
-        y = mt.column_values(self.getLabelCol())
-        pr = mt.column_values(self.getPredictionCol())
-        keep = [(a, b) for a, b in zip(y, pr) if a is not None and b is not None]
-        s = M.regression_summary([a for a, _ in keep], [b for _, b in keep], self.env.device)
+        yc, pc = mt.col(self.getLabelCol()), mt.col(self.getPredictionCol())
+        if all(isinstance(c.values, torch.Tensor) and c.values.dim() == 1 and not c.values.is_complex()
+               for c in (yc, pc)):
+            # tensor columns: the non-null pairs masked on the device, no Python pass over the rows
+            ok = torch.ones(yc.values.shape, dtype=torch.bool, device=yc.values.device)
+            for c in (yc, pc):
+                if c.nulls is not None:
+                    ok &= ~c.nulls.to(ok.device)
+            s = M.regression_summary(yc.values[ok], pc.values.to(ok.device)[ok], self.env.device)
+        else:
+            y = mt.column_values(self.getLabelCol())
+            pr = mt.column_values(self.getPredictionCol())
+            keep = [(a, b) for a, b in zip(y, pr) if a is not None and b is not None]
+            s = M.regression_summary([a for a, _ in keep], [b for _, b in keep], self.env.device)
         if s[-1] == 0:
             raise ValueError("Please check the evaluation input! there is no effective row!")
         return self._out(M.regression_metrics(s))

@@ -21,7 +21,7 @@ import torch
 from ..common.strings import StringBlock
 from . import _lib
 
-__all__ = ["tokenize_ws_lower", "hash_bytes", "murmur3_utf8_index", "murmur3_bytes_py", "split_tokens", "unique_ids"]
+__all__ = ["tokenize_ws_lower", "join_tokens", "ngram_join", "hash_bytes", "murmur3_utf8_index", "murmur3_bytes_py", "split_tokens", "unique_ids"]
 
 
 def murmur3_bytes_py(b: bytes, seed: int = 0) -> int:
@@ -284,3 +284,82 @@ def tokenize_ws_lower(block: StringBlock) -> Optional[StringBlock]:
     noff = torch.zeros(n + 1, dtype=torch.int64, device=dev)
     torch.cumsum(nl, 0, out=noff[1:])
     return StringBlock(out, noff, block.nulls)
+
+
+def _gather_bytes(tok: StringBlock, tids: torch.Tensor, starts: torch.Tensor, total: int, fill: int,
+                  seps: Optional[torch.Tensor] = None, sep_pos: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """An output byte buffer of ``total`` bytes (pre-filled with ``fill``) holding token ``tids[k]`` at ``starts[k]``
+    (and the bytes ``seps`` at ``sep_pos``)."""
+    dev = tok.data.device
+    out = torch.full((total,), fill, dtype=torch.uint8, device=dev)
+    toff = tok.offsets.to(dev)
+    tl = (toff[1:] - toff[:-1])[tids]
+    nb = int(tl.sum()) if tl.numel() else 0
+    if nb:
+        piece = torch.repeat_interleave(torch.arange(tids.numel(), device=dev), tl)
+        local = torch.arange(nb, device=dev) - torch.repeat_interleave(torch.cumsum(tl, 0) - tl, tl)
+        out[starts[piece] + local] = tok.data[toff[:-1][tids][piece] + local]
+    if seps is not None and sep_pos is not None and sep_pos.numel():
+        out[sep_pos] = seps
+    return out
+
+
+def join_tokens(tok: StringBlock, doc: torch.Tensor, keep: torch.Tensor, n: int, nulls=None,
+                sep: int = 0x20) -> StringBlock:
+    """Per document, its kept tokens (document order) joined by ``sep``: the rebuild half of a token filter
+    (``sep.join(t for t in tokens if keep)``), byte-parallel.  ``n`` documents; ``nulls`` carried over."""
+    dev = doc.device
+    kid = torch.nonzero(keep).reshape(-1)
+    kd = doc[kid]
+    toff = tok.offsets.to(dev)
+    tl = (toff[1:] - toff[:-1])[kid]
+    cnt = torch.bincount(kd, minlength=n)
+    blen = torch.zeros(n, dtype=torch.int64, device=dev)
+    if kid.numel():
+        blen.index_add_(0, kd, tl)
+    dlen = blen + (cnt - 1).clamp(min=0)
+    off = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(dlen, 0, out=off[1:])
+    # start of kept token k = its document's offset + the bytes and separators of the kept tokens before it
+    cb = torch.cumsum(tl, 0) - tl                              # global exclusive prefix of kept bytes
+    first = torch.cumsum(cnt, 0) - cnt                         # first kept token of each document
+    rank = torch.arange(kid.numel(), device=dev) - first[kd]
+    starts = off[:-1][kd] + (cb - cb[first[kd]]) + rank
+    data = _gather_bytes(tok, kid, starts, int(off[-1]), sep)
+    return StringBlock(data, off, nulls)
+
+
+def ngram_join(tok: StringBlock, doc: torch.Tensor, n: int, ngram: int, nulls=None) -> StringBlock:
+    """NGramMapper on split tokens: per document with m tokens, the m - ngram + 1 grams (``"_"``-joined runs of
+    ``ngram`` consecutive tokens) joined by spaces; fewer than ``ngram`` tokens give "".  ngram >= 2 (a gram always
+    holds a "_", so no gram is empty and the row path's strip() has nothing to remove)."""
+    dev = doc.device
+    m = torch.bincount(doc, minlength=n)
+    G = (m - ngram + 1).clamp(min=0)
+    Gt = int(G.sum())
+    if Gt == 0:
+        return StringBlock(torch.zeros(0, dtype=torch.uint8, device=dev),
+                           torch.zeros(n + 1, dtype=torch.int64, device=dev), nulls)
+    gdoc = torch.repeat_interleave(torch.arange(n, device=dev), G)
+    tfirst = torch.cumsum(m, 0) - m                            # first token of each document
+    gfirst = torch.cumsum(G, 0) - G                            # first gram of each document
+    grank = torch.arange(Gt, device=dev) - gfirst[gdoc]
+    pt = (tfirst[gdoc] + grank)[:, None] + torch.arange(ngram, device=dev)[None, :]   # [Gt, ngram] token ids
+    toff = tok.offsets.to(dev)
+    tl = (toff[1:] - toff[:-1])[pt]                            # [Gt, ngram]
+    last_gram = grank == (G[gdoc] - 1)
+    sep_len = torch.ones_like(tl)
+    sep_len[:, -1] = (~last_gram).to(sep_len.dtype)            # " " after a gram but the document's last
+    plen = (tl + sep_len).reshape(-1)
+    pstart = torch.cumsum(plen, 0) - plen
+    dlen = torch.zeros(n, dtype=torch.int64, device=dev)
+    dlen.index_add_(0, gdoc, (tl + sep_len).sum(1))
+    off = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(dlen, 0, out=off[1:])
+    flat_t = pt.reshape(-1)
+    has_sep = sep_len.reshape(-1) > 0
+    sep_char = torch.full((Gt, ngram), 0x5F, dtype=torch.uint8, device=dev)     # "_"
+    sep_char[:, -1] = 0x20                                                      # " "
+    sp = (pstart + tl.reshape(-1))[has_sep]
+    data = _gather_bytes(tok, flat_t, pstart, int(off[-1]), 0x20, sep_char.reshape(-1)[has_sep], sp)
+    return StringBlock(data, off, nulls)

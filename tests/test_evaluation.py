@@ -255,3 +255,36 @@ def test_detail_json_label_with_percent():
     from alink_amd.models.linear.model import _detail_json
     out = _detail_json(["50%", "a%s"], np.array([[0.25, 0.75], [1.0, 0.0]]))
     assert [json.loads(s) for s in out] == [{"50%": "0.25", "a%s": "0.75"}, {"50%": "1.0", "a%s": "0.0"}]
+
+
+def test_multiclass_and_regression_eval_tensor_columns_equal_lists():
+    """EvalMultiClass (prediction column) and EvalRegression on tensor columns (no per-row Python) give the
+    metrics of the list columns: nulls in either column, labels seen only in predictions."""
+    import torch
+    from alink_amd.common.table import Column, MTable
+    from alink_amd.common.types import TableSchema, Types
+    from alink_amd.operator.batch.source import TableSourceBatchOp
+    import alink_amd as A
+    g = torch.Generator().manual_seed(0)
+    n = 500
+    lab = torch.randint(0, 4, (n,), generator=g)
+    pred = torch.randint(0, 5, (n,), generator=g)
+    ln = torch.rand(n, generator=g) < 0.05
+    pn = torch.rand(n, generator=g) < 0.05
+    to_list = lambda v, m: [None if m[i] else int(v[i]) for i in range(n)]  # noqa: E731
+    s = TableSchema(["l", "p"], [Types.LONG, Types.LONG])
+    outs = []
+    for mt in (MTable(s, [Column(lab, ln), Column(pred, pn)]),
+               MTable(s, [Column(to_list(lab, ln)), Column(to_list(pred, pn))])):
+        outs.append(A.EvalMultiClassBatchOp().setLabelCol("l").setPredictionCol("p")
+                    .linkFrom(TableSourceBatchOp(mt)).collect()[0][0])
+    assert outs[0] == outs[1]
+    y = torch.randn(n, generator=g, dtype=torch.float64)
+    yp = y + 0.1 * torch.randn(n, generator=g, dtype=torch.float64)
+    s = TableSchema(["l", "p"], [Types.DOUBLE, Types.DOUBLE])
+    outs = []
+    for mt in (MTable(s, [Column(y, ln), Column(yp)]),
+               MTable(s, [Column([None if ln[i] else float(y[i]) for i in range(n)]), Column(yp.tolist())])):
+        outs.append(A.EvalRegressionBatchOp().setLabelCol("l").setPredictionCol("p")
+                    .linkFrom(TableSourceBatchOp(mt)).collect()[0][0])
+    assert outs[0] == outs[1]

@@ -377,3 +377,23 @@ def test_doc_vectorizer_predict_packed_equals_row_path(ftype, min_tf):
         got = m._map_columns(mt)[0].to_list()
         ref = [m._map_row_values([d])[0] for d in docs]
         assert [str(x) for x in got] == [str(x) for x in ref], kind
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_stopwords_and_ngram_packed_equal_row_path(n):
+    """StopWordsRemover and NGram on packed documents (device split + byte-parallel rebuild) equal the row
+    mappers: double spaces (empty tokens), leading / trailing spaces, case, documents shorter than n, nulls."""
+    from alink_amd.common.params import Params
+    from alink_amd.common.strings import StringBlock
+    from alink_amd.common.table import Column, MTable
+    from alink_amd.common.types import TableSchema, Types
+    from alink_amd.models.nlp.text import NGramMapper, StopWordsRemoverMapper
+    docs = ["the quick brown fox", "A  The an apple", " leading and", "trailing the ", "", None, "one",
+            "x y", "THE The the", "a b c d e f g", "  "] * 3
+    mt = MTable(TableSchema(["d"], [Types.STRING]), [Column(StringBlock.from_list(docs))])
+    for case in (False, True):
+        m = StopWordsRemoverMapper(mt.schema, Params().set("selectedCol", "d").set("outputCol", "o")
+                                   .set("caseSensitive", case))
+        assert m._map_columns(mt)[0].to_list() == [m.mapColumn(x) for x in docs]
+    g = NGramMapper(mt.schema, Params().set("selectedCol", "d").set("outputCol", "o").set("n", n))
+    assert g._map_columns(mt)[0].to_list() == [g.mapColumn(x) for x in docs]
