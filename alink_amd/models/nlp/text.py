@@ -167,16 +167,15 @@ class NGramMapper(SISOMapper):
         return WORD_DELIMITER.join(grams).strip()
 
     def _map_columns(self, mt):
-        """Packed ASCII documents with n >= 2: split on the device and the grams assembled byte-parallel
-        (``ops/strings.ngram_join``); other input (non-ASCII or \\t.. \\r / 0x1c-0x1f bytes, which strip()
-        treats as whitespace) row by row."""
+        """Packed documents with n >= 2: split on the device and the grams assembled byte-parallel
+        (``ops/strings.ngram_join``); text holding a character strip() removes (other than the space, which never
+        ends a gram) row by row."""
         from ...common.strings import StringBlock
-        from ...ops.strings import ngram_join, split_tokens
+        from ...ops.strings import has_strip_space, ngram_join, split_tokens
         col = mt.col(self.selected)
         blk = col.values
         if isinstance(blk, StringBlock) and col.nulls is None and len(blk) and self.n >= 2:
-            d = blk.data
-            if not bool(((d >= 128) | ((d >= 9) & (d <= 13)) | ((d >= 0x1C) & (d <= 0x1F))).any()):
+            if not has_strip_space(blk.data):
                 tok, doc = split_tokens(blk)
                 return [Column(ngram_join(tok, doc, len(blk), self.n, blk.nulls))]
         return super()._map_columns(mt)

@@ -21,7 +21,7 @@ import torch
 from ..common.strings import StringBlock
 from . import _lib
 
-__all__ = ["tokenize_ws_lower", "join_tokens", "ngram_join", "hash_bytes", "murmur3_utf8_index", "murmur3_bytes_py", "split_tokens", "unique_ids"]
+__all__ = ["tokenize_ws_lower", "has_strip_space", "join_tokens", "ngram_join", "hash_bytes", "murmur3_utf8_index", "murmur3_bytes_py", "split_tokens", "unique_ids"]
 
 
 def murmur3_bytes_py(b: bytes, seed: int = 0) -> int:
@@ -363,3 +363,24 @@ def ngram_join(tok: StringBlock, doc: torch.Tensor, n: int, ngram: int, nulls=No
     sp = (pstart + tl.reshape(-1))[has_sep]
     data = _gather_bytes(tok, flat_t, pstart, int(off[-1]), 0x20, sep_char.reshape(-1)[has_sep], sp)
     return StringBlock(data, off, nulls)
+
+
+def has_strip_space(data: torch.Tensor) -> bool:
+    """Whether UTF-8 bytes hold a character Python's ``str.strip()`` removes other than the plain space: \\t..\\r,
+    0x1c-0x1f, U+0085, U+00A0, U+1680, U+2000-U+200A, U+2028, U+2029, U+202F, U+205F, U+3000."""
+    d = data
+    if d.numel() == 0:
+        return False
+    if bool((((d >= 9) & (d <= 13)) | ((d >= 0x1C) & (d <= 0x1F))).any()):
+        return True
+    if d.numel() >= 2 and bool(((d[:-1] == 0xC2) & ((d[1:] == 0x85) | (d[1:] == 0xA0))).any()):
+        return True
+    if d.numel() >= 3:
+        a, b, c = d[:-2], d[1:-1], d[2:]
+        hit = (a == 0xE1) & (b == 0x9A) & (c == 0x80)
+        hit |= (a == 0xE2) & (b == 0x80) & (((c >= 0x80) & (c <= 0x8A)) | (c == 0xA8) | (c == 0xA9) | (c == 0xAF))
+        hit |= (a == 0xE2) & (b == 0x81) & (c == 0x9F)
+        hit |= (a == 0xE3) & (b == 0x80) & (c == 0x80)
+        if bool(hit.any()):
+            return True
+    return False

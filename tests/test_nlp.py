@@ -389,7 +389,7 @@ def test_stopwords_and_ngram_packed_equal_row_path(n):
     from alink_amd.common.types import TableSchema, Types
     from alink_amd.models.nlp.text import NGramMapper, StopWordsRemoverMapper
     docs = ["the quick brown fox", "A  The an apple", " leading and", "trailing the ", "", None, "one",
-            "x y", "THE The the", "a b c d e f g", "  "] * 3
+            "x y", "THE The the", "a b c d e f g", "  ", "é à ü", "日本 語 テキスト"] * 3
     mt = MTable(TableSchema(["d"], [Types.STRING]), [Column(StringBlock.from_list(docs))])
     for case in (False, True):
         m = StopWordsRemoverMapper(mt.schema, Params().set("selectedCol", "d").set("outputCol", "o")
@@ -397,3 +397,15 @@ def test_stopwords_and_ngram_packed_equal_row_path(n):
         assert m._map_columns(mt)[0].to_list() == [m.mapColumn(x) for x in docs]
     g = NGramMapper(mt.schema, Params().set("selectedCol", "d").set("outputCol", "o").set("n", n))
     assert g._map_columns(mt)[0].to_list() == [g.mapColumn(x) for x in docs]
+
+
+def test_has_strip_space_matches_python_strip():
+    """has_strip_space flags exactly the texts in which Python's strip() could remove more than spaces."""
+    import torch
+    from alink_amd.ops.strings import has_strip_space
+    for ch in ["\t", "\n", "\x0b", "\x0c", "\r", "\x1c", "\x1f", "\x85", "\xa0", "\u1680", "\u2000", "\u200a",
+               "\u2028", "\u2029", "\u202f", "\u205f", "\u3000"]:
+        assert ch.strip() == ""
+        assert has_strip_space(torch.frombuffer(bytearray(("a" + ch + "b").encode()), dtype=torch.uint8))
+    for txt in ["plain text", "é à ü", "日本語", "\u200b zero width", "\u180e"]:
+        assert has_strip_space(torch.frombuffer(bytearray(txt.encode()), dtype=torch.uint8)) is False
