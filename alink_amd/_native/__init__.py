@@ -16,7 +16,7 @@ __all__ = ["lib", "parse_csv_lines", "murmur3_utf16", "murmur3_bytes", "murmur3_
            "java_double_rows", "java_double_rows_packed", "parse_csv_packed",
            "parse_dense_vectors_packed", "parse_kv_packed", "parse_json_flat_packed", "java_double_rows_fmt", "sample_thresholds", "gbdt_rank_grad",
            "tree_flatten", "java_float_rows", "java_float_rows_packed", "parse_double_csv",
-           "java_float_kv_rows"]
+           "java_float_kv_rows", "join_packed_columns"]
 
 # ALINK_NATIVE_LIB points at another build of the same sources (e.g. the AddressSanitizer build of
 # tools/asan_host.py)
@@ -44,6 +44,8 @@ if os.path.exists(_PATH):
             lib.alink_java_float_rows.restype = ctypes.c_int64
         if hasattr(lib, "alink_java_float_kv_rows"):
             lib.alink_java_float_kv_rows.restype = ctypes.c_int64
+        if hasattr(lib, "alink_join_packed_columns"):
+            lib.alink_join_packed_columns.restype = None
         if hasattr(lib, "alink_java_double_rows_fmt"):
             lib.alink_java_double_rows_fmt.restype = ctypes.c_int64
         if hasattr(lib, "alink_sample_thresholds"):
@@ -271,6 +273,27 @@ def java_float_kv_rows(keys, vals, kvsep: str = ":", sep: str = ",") -> Optional
     text = buf[:total].tobytes().decode("ascii")
     o = off.tolist()
     return [text[o[i]:o[i + 1]] for i in range(n)]
+
+
+def join_packed_columns(cols, delim: str, rowdelim: str) -> Optional[np.ndarray]:
+    """uint8 bytes of the lines ``col0 + delim + ... + col{k-1} + rowdelim`` over k packed columns, each a
+    (uint8 bytes, int64 offsets [n+1]) pair, assembled in C++; None without the library."""
+    if lib is None or getattr(lib, "alink_join_packed_columns", None) is None or not cols:
+        return None
+    n = int(cols[0][1].size) - 1
+    datas = [np.ascontiguousarray(c[0], dtype=np.uint8) if c[0].size else np.zeros(1, np.uint8) for c in cols]
+    offs = [np.ascontiguousarray(c[1], dtype=np.int64) for c in cols]
+    d, rd = delim.encode("utf-8"), rowdelim.encode("utf-8")
+    lens = sum(o[1:] - o[:-1] for o in offs) + (len(cols) - 1) * len(d) + len(rd)
+    row_off = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(lens, out=row_off[1:])
+    out = np.empty(max(int(row_off[-1]), 1), dtype=np.uint8)
+    dp = (ctypes.c_void_p * len(cols))(*[a.ctypes.data for a in datas])
+    op = (ctypes.c_void_p * len(cols))(*[o.ctypes.data for o in offs])
+    lib.alink_join_packed_columns(ctypes.c_int64(len(cols)), dp, op, ctypes.c_int64(n), ctypes.c_char_p(d),
+                                  ctypes.c_int64(len(d)), ctypes.c_char_p(rd), ctypes.c_int64(len(rd)),
+                                  _ptr(row_off), _ptr(out))
+    return out[:int(row_off[-1])]
 
 
 def java_double_rows_fmt(x, pre: Sequence[str], post: Sequence[str], sep: str, ropen: str = "", rclose: str = ""):

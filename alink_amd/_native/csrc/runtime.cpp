@@ -792,3 +792,22 @@ extern "C" int64_t alink_java_double_rows_fmt(const double* x, int64_t n, int64_
     }
     return p;
 }
+
+// CSV / text lines from k packed string columns: row r = col0[r] + delim + col1[r] + ... + col{k-1}[r] + rowdelim,
+// written at out + row_off[r] (row_off from the caller's length prefix sum, so rows are independent: OpenMP over
+// row blocks).  data[j] / off[j] are column j's bytes and its int64 [n+1] offsets.
+extern "C" void alink_join_packed_columns(int64_t k, const uint8_t* const* data, const int64_t* const* off, int64_t n,
+                                          const char* delim, int64_t dlen, const char* rowdelim, int64_t rlen,
+                                          const int64_t* row_off, uint8_t* out) {
+#pragma omp parallel for schedule(static) if (n > 4096)
+    for (int64_t r = 0; r < n; ++r) {
+        uint8_t* p = out + row_off[r];
+        for (int64_t j = 0; j < k; ++j) {
+            if (j) { std::memcpy(p, delim, (size_t)dlen); p += dlen; }
+            const int64_t a = off[j][r], b = off[j][r + 1];
+            std::memcpy(p, data[j] + a, (size_t)(b - a));
+            p += b - a;
+        }
+        std::memcpy(p, rowdelim, (size_t)rlen);
+    }
+}

@@ -25,7 +25,8 @@ def main():
     ap.add_argument("--only", default="")
     ap.add_argument("--top", type=int, default=8)
     ap.add_argument("--set", type=int, default=1,
-                    help="1: model ops; 2: data processing / SQL / scalers; 3: evaluation / NLP / trees / formats")
+                    help="1: model ops; 2: data processing / SQL / scalers; 3: evaluation / NLP / trees / formats; "
+                         "4: IO, more model predicts")
     a = ap.parse_args()
     import alink_amd as A
     from alink_amd.common.table import Column, MTable
@@ -169,6 +170,44 @@ def main():
             .setReservedCols([]).linkFrom(src).getOutputTable(),
             "columns_to_json": lambda: A.ColumnsToJsonBatchOp().setSelectedCols(names[:5]).setJsonCol("j")
             .setReservedCols([]).linkFrom(src).getOutputTable(),
+        }
+    if a.set == 4:
+        import tempfile
+        src = TableSourceBatchOp(dense)
+        tmp = tempfile.mkdtemp()
+        csv_path = os.path.join(tmp, "d.csv")
+        A.CsvSinkBatchOp().setFilePath(csv_path).setOverwriteSink(True).linkFrom(src)
+        schema_str = ", ".join(f"{c} double" for c in names) + ", label int"
+        sm = MTable(TableSchema(names + ["label"], [Types.DOUBLE] * F + [Types.INT]),
+                    [Column(c.values[:200000]) for c in cols] + [Column(y[:200000])])
+        nb_docs = TableSourceBatchOp(MTable(TableSchema(["doc", "label"], [Types.STRING, Types.INT]),
+                                            [Column(vocab.take(cats)), Column(y)]))
+        sm_src = TableSourceBatchOp(sm)
+        softmax_model = A.SoftmaxTrainBatchOp().setFeatureCols(names).setLabelCol("label").setMaxIter(3) \
+            .linkFrom(sm_src)
+        gmm_model = A.GmmTrainBatchOp().setVectorCol("vec").setK(10).setMaxIter(3) \
+            .linkFrom(TableSourceBatchOp(MTable(TableSchema(["vec"], [Types.DENSE_VECTOR]),
+                                                [Column(vec.col("vec").values[:200000].float())])))
+        nb_model = A.NaiveBayesTextTrainBatchOp().setVectorCol("v").setLabelCol("label") \
+            .linkFrom(A.DocHashCountVectorizerPredictBatchOp().setSelectedCol("doc").setOutputCol("v")
+                      .linkFrom(A.DocHashCountVectorizerTrainBatchOp().setSelectedCol("doc").setNumFeatures(1000)
+                                .linkFrom(nb_docs), nb_docs))
+        jobs = {
+            "csv_sink": lambda: A.CsvSinkBatchOp().setFilePath(csv_path + ".2").setOverwriteSink(True)
+            .linkFrom(src),
+            "csv_source": lambda: A.CsvSourceBatchOp().setFilePath(csv_path).setSchemaStr(schema_str)
+            .getOutputTable(),
+            "collect_rows": lambda: TableSourceBatchOp(sm).collect(),
+            "softmax_predict": lambda: A.SoftmaxPredictBatchOp().setPredictionCol("p").setReservedCols([])
+            .linkFrom(softmax_model, src).getOutputTable().col("p").values,
+            "gmm_predict": lambda: A.GmmPredictBatchOp().setPredictionCol("p").setReservedCols([])
+            .linkFrom(gmm_model, TableSourceBatchOp(vec)).getOutputTable().col("p").values,
+            "naive_bayes_text_predict": lambda: A.NaiveBayesTextPredictBatchOp().setPredictionCol("p")
+            .setReservedCols([]).linkFrom(nb_model, A.DocHashCountVectorizerPredictBatchOp().setSelectedCol("doc")
+                                          .setOutputCol("v").linkFrom(
+                                              A.DocHashCountVectorizerTrainBatchOp().setSelectedCol("doc")
+                                              .setNumFeatures(1000).linkFrom(nb_docs), nb_docs))
+            .getOutputTable().col("p").values,
         }
     only = [s for s in a.only.split(",") if s]
     for name, fn in jobs.items():
