@@ -26,8 +26,16 @@ from ...common.params import Params
 from ...common.table import Column, MTable
 from ...common.types import Types
 from ...parallel import comm
-from ..common.features import extract_features, global_vector_size
-from ..linear.model import _recover_label
+from ...common.strings import StringBlock
+from ..common.features import FeatureMatrix, extract_features, global_vector_size
+from ..linear.model import _dev, _recover_label
+
+
+def _recount_crow(crow: torch.Tensor, keep: torch.Tensor) -> torch.Tensor:
+    """CSR row pointers after dropping the entries where ``keep`` is False."""
+    c = torch.zeros(keep.numel() + 1, dtype=torch.int64, device=keep.device)
+    torch.cumsum(keep.to(torch.int64), 0, out=c[1:])
+    return c[crow.to(torch.int64)]
 
 __all__ = ["train_naive_bayes_text", "NaiveBayesTextModelDataConverter", "NaiveBayesTextModelMapper"]
 
@@ -134,12 +142,23 @@ class NaiveBayesTextModelMapper(RichModelMapper):
 
     def _scores(self, mt):
         vec_col = self.params.get("vectorCol") if self.params.contains("vectorCol") else self.model["vectorCol"]
-        fm = extract_features(mt, None, vec_col, torch.device("cpu"))
+        dev = _dev(mt)
+        fm = extract_features(mt, None, vec_col, dev)
         th = self.model["theta"]
         d = th.shape[1]
+        if fm.is_sparse and self.model["modelType"] != "Bernoulli":
+            # X @ theta^T straight from the CSR rows (indices >= d dropped, as the dense path truncates)
+            fm.set_ncols(d)
+            if fm.val.numel() and int(fm.col.max()) >= d:
+                keep = fm.col < d
+                fm = FeatureMatrix(crow=_recount_crow(fm.crow, keep), col=fm.col[keep], val=fm.val[keep], ncols=d)
+            T = torch.as_tensor(th.T, dtype=torch.float64, device=dev)
+            S = fm.to(dev).mm(T) if fm.val.dtype == torch.float64 else \
+                FeatureMatrix(crow=fm.crow, col=fm.col, val=fm.val.double(), ncols=d).mm(T)
+            return (S + torch.as_tensor(self.model["pi"], dtype=torch.float64, device=dev)[None, :]).cpu().numpy()
         if fm.is_sparse:
             fm.set_ncols(d)
-        X = fm.to_dense().double().numpy()
+        X = fm.to_dense().double().cpu().numpy()
         if X.shape[1] < d:
             X = np.pad(X, ((0, 0), (0, d - X.shape[1])))
         X = X[:, :d]
@@ -156,6 +175,23 @@ class NaiveBayesTextModelMapper(RichModelMapper):
     def _map_columns(self, mt):
         S = self._scores(mt)
         labels = self.model["labels"]
+        if not self.detail_col and len(S):
+            # first strict maximum over the classes (NaN never wins; a row of -inf / NaN predicts null)
+            Sf = np.where(np.isnan(S), -np.inf, S)
+            idx = Sf.argmax(1)
+            ok = Sf[np.arange(len(Sf)), idx] > -np.inf
+            t = self.helper.out_types[0]
+            if ok.all() and all(v is not None for v in labels):
+                if t == Types.STRING and all(isinstance(v, str) for v in labels):
+                    return [Column(StringBlock.from_list(labels).take(torch.from_numpy(idx)))]
+                if t.torch_dtype is not None and t.py in (int, float) and \
+                        all(isinstance(v, (int, float)) and not isinstance(v, bool) for v in labels):
+                    return [Column(torch.tensor(labels, dtype=t.torch_dtype)[torch.from_numpy(idx)])]
+            lab = np.empty(len(labels), dtype=object)
+            lab[:] = labels
+            preds = lab[idx]
+            preds[~ok] = None
+            return [Column.from_values(preds.tolist(), t)]
         preds, details = [], []
         for s in S:
             best, res = float("-inf"), None

@@ -29,6 +29,7 @@ from ...common.linalg import DenseVector, VectorUtil
 from ...common.mapper import OutputColsHelper, RichModelMapper
 from ...common.model.converter import SimpleModelDataConverter
 from ...common.params import Params
+from ...common.strings import StringBlock
 from ...common.table import Column, MTable
 from ...common.types import Types
 from ...ops import gmm as gmm_ops
@@ -73,7 +74,11 @@ def _root_inv(cov: torch.Tensor):
 
 def gaussian_logpdf(X: torch.Tensor, mean: torch.Tensor, cov: torch.Tensor) -> torch.Tensor:
     """[n, k] log densities (``MultivariateGaussian.logpdf``)."""
-    W, logdet, rank = _root_inv(cov)
+    return _logpdf_root(X, mean, *_root_inv(cov))
+
+
+def _logpdf_root(X, mean, W, logdet, rank):
+    """``gaussian_logpdf`` from the ``_root_inv`` factors (all on X's device)."""
     out = torch.empty((X.shape[0], mean.shape[0]), dtype=X.dtype, device=X.device)
     for j in range(mean.shape[0]):
         z = (X - mean[j]) @ W[j]
@@ -213,17 +218,29 @@ class GmmModelMapper(RichModelMapper):
         return [c.to_list()[0] for c in self._map_columns(mt)]
 
     def _map_columns(self, mt):
-        fm = extract_features(mt, None, self.vcol, torch.device("cpu"))
+        from ..linear.model import _dev
+        dev = _dev(mt)
+        fm = extract_features(mt, None, self.vcol, dev)
         if fm.is_sparse:
             fm.set_ncols(self.d)
         X = fm.to_dense().double()
-        lp = gaussian_logpdf(X, torch.as_tensor(self.mu), torch.as_tensor(self.S)).numpy()
+        f = getattr(self, "_factors", None)
+        if f is None or f[0].device != X.device:
+            # pseudo-inverse roots once per mapper, on the host (small k x d x d eigh), then kept on X's device
+            W, logdet, rank = _root_inv(torch.as_tensor(self.S))
+            f = self._factors = tuple(t.to(X.device) for t in (torch.as_tensor(self.mu), W, logdet, rank))
+        lp = _logpdf_root(X, *f).cpu().numpy()
         lw = lp + np.log(self.w)[None, :]
         m = lw.max(1, keepdims=True)
         prob = np.exp(lw - m)
         prob = prob / prob.sum(1, keepdims=True)
         pred = prob.argmax(1)
-        cols = [Column.from_values([int(p) for p in pred], Types.LONG)]
+        cols = [Column(torch.from_numpy(pred.astype(np.int64)))]
         if self.detail_col:
-            cols.append(Column.from_values([VectorUtil.toString(DenseVector(p)) for p in prob], Types.STRING))
+            from ... import _native
+            r = _native.java_double_rows_packed(prob, " ") if len(prob) else None
+            if r is not None:
+                cols.append(Column(StringBlock(torch.from_numpy(np.ascontiguousarray(r[0])), torch.from_numpy(r[1]))))
+            else:
+                cols.append(Column.from_values([VectorUtil.toString(DenseVector(p)) for p in prob], Types.STRING))
         return cols

@@ -130,3 +130,26 @@ def test_multivariate_gaussian_reference_values():
     deg = MultivariateGaussian(mu, DenseMatrix(2, 2, [1.0, 1.0, 1.0, 1.0]))
     assert deg.pdf(DenseVector.zeros(2)) == pytest.approx(0.11254, abs=tol)
     assert deg.pdf(DenseVector.ones(2)) == pytest.approx(0.068259, abs=tol)
+
+
+def test_gmm_predict_detail_packed():
+    """GMM prediction detail strings (Double.toString of the posteriors, space separated) formatted in C++ equal
+    VectorUtil.toString of the same DenseVector; predictions are an int64 column."""
+    import numpy as np
+    import pandas as pd
+    from alink_amd import BatchOperator, GmmPredictBatchOp, GmmTrainBatchOp
+    from alink_amd.common.linalg import DenseVector, VectorUtil
+    rng = np.random.default_rng(0)
+    X = np.concatenate([rng.standard_normal((100, 3)), rng.standard_normal((100, 3)) + 5])
+    df = pd.DataFrame({"v": [" ".join(map(str, r)) for r in X]})
+    b = BatchOperator.fromDataframe(df, schemaStr="v string")
+    m = GmmTrainBatchOp().setVectorCol("v").setK(2).setMaxIter(20).linkFrom(b)
+    out = GmmPredictBatchOp().setPredictionCol("p").setPredictionDetailCol("d").linkFrom(m, b)
+    mt = out.getOutputTable()
+    rows = out.collect()
+    assert {r[1] for r in rows} == {0, 1}
+    for r in rows[:20]:
+        probs = [float(x) for x in r[2].split(" ")]
+        assert r[2] == VectorUtil.toString(DenseVector(np.array(probs)))
+        assert abs(sum(probs) - 1) < 1e-12
+    assert mt.col("p").values.dtype.is_floating_point is False

@@ -49,3 +49,26 @@ def test_reference_model_fixture():
     mapper.loadModel(rows)
     assert mapper.map(("1.0, 1.0, 0.0, 1.0",))[1] == 1
     assert mapper.getOutputSchema().names == ["vec", "pred"] and mapper.getOutputSchema().types[1] == Types.INT
+
+
+@pytest.mark.parametrize("mtype", ["Multinomial", "Bernoulli"])
+def test_vectorized_prediction_matches_detail_path(mtype):
+    """Columnar prediction (CSR scores, argmax over the classes at once) gives the labels the per-row detail
+    path picks; sparse indices beyond the model width are dropped as the dense path truncates."""
+    rng = np.random.default_rng(1)
+    rows = []
+    for i in range(300):
+        idx = sorted(rng.choice(12, 4, replace=False))
+        vals = [1.0 if mtype == "Bernoulli" else float(rng.integers(1, 4)) for _ in idx]
+        rows.append(["$12$" + " ".join(f"{a}:{b}" for a, b in zip(idx, vals)), ["a", "b", "c"][i % 3]])
+    df = pd.DataFrame(rows, columns=["sv", "label"])
+    b = BatchOperator.fromDataframe(df, schemaStr="sv string, label string")
+    model = b.link(NaiveBayesTextTrainBatchOp().setVectorCol("sv").setLabelCol("label").setModelType(mtype))
+    test = [[r[0].replace("$12$", "$20$") + (" 15:1.0" if mtype != "Bernoulli" else "")] for r in rows[:50]] + \
+        [[r[0]] for r in rows[50:]]
+    t = BatchOperator.fromDataframe(pd.DataFrame(test, columns=["sv"]), schemaStr="sv string")
+    fast = NaiveBayesTextPredictBatchOp().setVectorCol("sv").setPredictionCol("p").linkFrom(model, t).collect()
+    slow = NaiveBayesTextPredictBatchOp().setVectorCol("sv").setPredictionCol("p").setPredictionDetailCol("d") \
+        .linkFrom(model, t).collect()
+    assert [r[1] for r in fast] == [r[1] for r in slow]
+    assert len({r[1] for r in fast}) > 1
