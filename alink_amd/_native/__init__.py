@@ -16,7 +16,7 @@ __all__ = ["lib", "parse_csv_lines", "murmur3_utf16", "murmur3_bytes", "murmur3_
            "java_double_rows", "java_double_rows_packed", "parse_csv_packed",
            "parse_dense_vectors_packed", "parse_kv_packed", "parse_json_flat_packed", "java_double_rows_fmt", "sample_thresholds", "gbdt_rank_grad",
            "tree_flatten", "java_float_rows", "java_float_rows_packed", "parse_double_csv",
-           "java_float_kv_rows", "join_packed_columns"]
+           "java_float_kv_rows", "join_packed_columns", "parse_csv_spans"]
 
 # ALINK_NATIVE_LIB points at another build of the same sources (e.g. the AddressSanitizer build of
 # tools/asan_host.py)
@@ -27,6 +27,7 @@ if os.path.exists(_PATH):
     try:
         lib = ctypes.CDLL(_PATH)
         lib.alink_csv_parse.restype = ctypes.c_int
+        lib.alink_csv_parse_spans.restype = ctypes.c_int
         lib.alink_murmur3_utf16_batch.restype = None
         if hasattr(lib, "alink_murmur3_bytes_batch"):
             lib.alink_murmur3_bytes_batch.restype = None
@@ -109,11 +110,22 @@ class _CsvLineError(RuntimeError):
 def parse_csv_packed(data: np.ndarray, off: np.ndarray, codes: List[int], delim: str, quote: str):
     """``parse_csv_lines`` over lines already packed as UTF-8 bytes (``data`` uint8, ``off`` int64 [n+1], e.g. a
     host ``StringBlock``); raises ``RuntimeError`` (with ``.line``) on the first line it cannot parse."""
+    off = np.ascontiguousarray(off, dtype=np.int64)
+    return parse_csv_spans(data, off[:-1], off[1:], codes, delim, quote)
+
+
+def parse_csv_spans(data: np.ndarray, starts: np.ndarray, ends: np.ndarray, codes: List[int], delim: str,
+                    quote: str, blocks: bool = False):
+    """Lines ``data[starts[i]:ends[i]]`` of one buffer (a file read whole, row delimiters left between the spans)
+    parsed in C++.  Per column (values, nulls): numpy arrays for numeric columns; for string columns a python
+    list, or with ``blocks`` a (bytes, offsets [n+1], nulls) triple -- the ``StringBlock`` layout -- when no
+    field of the column holds an escaped quote."""
     if lib is None:
         return None
     data = np.ascontiguousarray(data, dtype=np.uint8) if data.size else np.zeros(1, np.uint8)
-    off = np.ascontiguousarray(off, dtype=np.int64)
-    n = off.size - 1
+    starts = np.ascontiguousarray(starts, dtype=np.int64)
+    ends = np.ascontiguousarray(ends, dtype=np.int64)
+    n = starts.size
     ncol = len(codes)
     nums, nulls, soffs, sescs = [], [], [], []
     num_ptrs = (ctypes.c_void_p * ncol)()
@@ -121,10 +133,12 @@ def parse_csv_packed(data: np.ndarray, off: np.ndarray, codes: List[int], delim:
     soff_ptrs = (ctypes.c_void_p * ncol)()
     sesc_ptrs = (ctypes.c_void_p * ncol)()
     for c, t in enumerate(codes):
-        a = np.zeros(n, dtype=np.float64 if t == 1 else np.int64) if t != 0 else np.zeros(1, dtype=np.int64)
-        nl = np.ones(max(n, 1), dtype=np.uint8)
-        so = np.full(2 * max(n, 1), -1, dtype=np.int64)
-        se = np.zeros(max(n, 1), dtype=np.uint8)
+        a = np.empty(n, dtype=np.float64 if t == 1 else np.int64) if t != 0 else np.zeros(1, dtype=np.int64)
+        if t != 0:
+            a.fill(0)
+        nl = np.empty(max(n, 1), dtype=np.uint8)
+        so = np.empty(2 * max(n, 1), dtype=np.int64) if t == 0 else np.zeros(2, dtype=np.int64)
+        se = np.empty(max(n, 1), dtype=np.uint8) if t == 0 else np.zeros(1, dtype=np.uint8)
         nums.append(a), nulls.append(nl), soffs.append(so), sescs.append(se)
         num_ptrs[c] = a.ctypes.data
         null_ptrs[c] = nl.ctypes.data
@@ -132,9 +146,9 @@ def parse_csv_packed(data: np.ndarray, off: np.ndarray, codes: List[int], delim:
         sesc_ptrs[c] = se.ctypes.data
     ct = np.asarray(codes, dtype=np.int32)
     q = ord(quote) if quote else -1
-    rc = lib.alink_csv_parse(_ptr(data), _ptr(off), ctypes.c_int64(n), ctypes.c_int(ncol), _ptr(ct),
-                             ctypes.c_char(delim.encode()), ctypes.c_int(q), num_ptrs, null_ptrs, soff_ptrs,
-                             sesc_ptrs)
+    rc = lib.alink_csv_parse_spans(_ptr(data), _ptr(starts), _ptr(ends), ctypes.c_int64(n), ctypes.c_int(ncol),
+                                   _ptr(ct), ctypes.c_char(delim.encode()), ctypes.c_int(q), num_ptrs, null_ptrs,
+                                   soff_ptrs, sesc_ptrs)
     if rc != 0:
         raise _CsvLineError(-1 - rc)
     out = []
@@ -142,11 +156,18 @@ def parse_csv_packed(data: np.ndarray, off: np.ndarray, codes: List[int], delim:
     for c, t in enumerate(codes):
         nl = nulls[c][:n].astype(bool)
         if t == 0:
+            so = soffs[c][:2 * n].reshape(n, 2)
+            if blocks and not sescs[c][:n].any():
+                lens = np.where(so[:, 0] < 0, 0, so[:, 1] - so[:, 0])
+                o = np.zeros(n + 1, dtype=np.int64)
+                np.cumsum(lens, out=o[1:])
+                src = np.repeat(so[:, 0] - o[:-1], lens) + np.arange(int(o[-1]), dtype=np.int64)
+                out.append(((data[src], o, so[:, 0] < 0), None))
+                continue
             raw = data.tobytes() if raw is None else raw
-            so = soffs[c]
             vals = []
             for i in range(n):
-                a, b = so[2 * i], so[2 * i + 1]
+                a, b = so[i, 0], so[i, 1]
                 if a < 0:
                     vals.append(None)
                 else:

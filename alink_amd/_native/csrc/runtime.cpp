@@ -20,14 +20,16 @@ extern "C" {
 // out_soff[c]: int64_t* 2*nlines (start, end byte offsets into buf; -1 = NULL), for string columns
 // out_sesc[c]: uint8_t* nlines (1 = contains escaped quotes to collapse)
 // returns -1 - line on parse error, else 0
-int alink_csv_parse(const char* buf, const int64_t* line_off, int64_t nlines, int ncols, const int* types,
-                    char delim, int quote, void** out_num, uint8_t** out_null, int64_t** out_soff,
-                    uint8_t** out_sesc) {
+// alink_csv_parse_spans: the same over lines [line_start[i], line_end[i]) of one buffer (a file read whole, the
+// row delimiters left in place between the spans).
+int alink_csv_parse_spans(const char* buf, const int64_t* line_off, const int64_t* line_end, int64_t nlines,
+                          int ncols, const int* types, char delim, int quote, void** out_num, uint8_t** out_null,
+                          int64_t** out_soff, uint8_t** out_sesc) {
     int64_t err = -1;
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) if (nlines > 256)
     for (int64_t li = 0; li < nlines; ++li) {
         const char* s = buf + line_off[li];
-        const int64_t n = line_off[li + 1] - line_off[li];
+        const int64_t n = line_end[li] - line_off[li];
         int64_t pos = 0;
         bool ok = true;
         for (int c = 0; c < ncols; ++c) {
@@ -38,7 +40,7 @@ int alink_csv_parse(const char* buf, const int64_t* line_off, int64_t nlines, in
                 out_sesc[c][li] = 0;
             }
             if (pos > n) {
-                ok = false;
+                if (n != 0) ok = false;  // an empty line (skipBlankLine off) is a row of nulls
                 continue;
             }
             // find the end of this field
@@ -116,6 +118,13 @@ int alink_csv_parse(const char* buf, const int64_t* line_off, int64_t nlines, in
         }
     }
     return err >= 0 ? (int)(-1 - err) : 0;
+}
+
+int alink_csv_parse(const char* buf, const int64_t* line_off, int64_t nlines, int ncols, const int* types,
+                    char delim, int quote, void** out_num, uint8_t** out_null, int64_t** out_soff,
+                    uint8_t** out_sesc) {
+    return alink_csv_parse_spans(buf, line_off, line_off + 1, nlines, ncols, types, delim, quote, out_num, out_null,
+                                 out_soff, out_sesc);
 }
 
 static inline uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }

@@ -43,7 +43,7 @@ def read_text(path: str) -> str:
         return f.read()
 
 
-def read_text_range(path: str, row_delim: str, rank: int, world: int):
+def read_text_range(path: str, row_delim: str, rank: int, world: int, raw: bool = False):
     """(text of the lines whose first byte lies in this rank's byte range, whether the range holds the file's
     first line) for a local file on a multi-rank job; None when a whole-file read applies (one rank, URLs)."""
     if world <= 1 or path.startswith(("http://", "https://")):
@@ -76,7 +76,7 @@ def read_text_range(path: str, row_delim: str, rank: int, world: int):
                         break
             lo = start
         if lo >= hi:
-            return "", rank == 0
+            return (b"" if raw else ""), rank == 0
         f.seek(lo)
         data = f.read(hi - lo)
         if not data.endswith(d):
@@ -91,7 +91,7 @@ def read_text_range(path: str, row_delim: str, rank: int, world: int):
                     break
                 rest += chunk
             data += rest
-    return data.decode("utf-8"), lo == 0
+    return (data if raw else data.decode("utf-8")), lo == 0
 
 
 class BaseSourceBatchOp(BatchOperator):
@@ -205,6 +205,13 @@ class CsvSourceBatchOp(BaseSourceBatchOp):
         schema = schema_str_to_schema(self.getSchemaStr())
         row_delim = self.getRowDelimiter() or "\n"
         path = self.getFilePath()
+        quote = self.getParams().get(self._param_infos["quoteChar"])
+        delim = self.getFieldDelimiter()
+        skip_blank = self.getSkipBlankLine()
+        mt = _csv_bytes_table(path, schema, row_delim, delim, quote, skip_blank, self.getIgnoreFirstLine()) \
+            if self.env.world_size == comm.get_world_size() else None
+        if mt is not None:
+            return mt
         ranged = read_text_range(path, row_delim, comm.get_rank(), comm.get_world_size())
         if ranged is not None:
             # byte-range split (CsvSourceBatchOp.java:76-116 / Flink input splits): this rank reads only the
@@ -220,9 +227,6 @@ class CsvSourceBatchOp(BaseSourceBatchOp):
             lines = lines[1:]
         if ranged is None:
             lines = partition_rows(lines, self.env)
-        quote = self.getParams().get(self._param_infos["quoteChar"])
-        delim = self.getFieldDelimiter()
-        skip_blank = self.getSkipBlankLine()
         mt = _native_parse_csv(lines, schema, delim, quote, skip_blank)
         if mt is not None:
             return mt
@@ -240,14 +244,7 @@ class CsvSourceBatchOp(BaseSourceBatchOp):
         return MTable.from_rows(rows, schema)
 
 
-def _native_parse_csv(lines, schema, delim, quote, skip_blank) -> Optional[MTable]:
-    """Bulk path through the native C++ parser (numeric columns straight into arrays)."""
-    try:
-        from ... import _native
-    except Exception:
-        return None
-    if _native.lib is None or len(delim) != 1 or (quote is not None and len(quote) != 1):
-        return None
+def _csv_codes(schema):
     codes = []
     for t in schema.types:
         if t in (Types.DOUBLE, Types.FLOAT, Types.DECIMAL):
@@ -260,18 +257,92 @@ def _native_parse_csv(lines, schema, delim, quote, skip_blank) -> Optional[MTabl
             codes.append(0)
         else:
             return None
-    res = _native.parse_csv_lines(lines, codes, delim, quote or "", skip_blank)
-    if res is None:
-        return None
+    return codes
+
+
+def _csv_table(schema, res) -> MTable:
+    from ...common.strings import StringBlock
     cols = []
     for t, (vals, nulls) in zip(schema.types, res):
-        if isinstance(vals, list):
+        if isinstance(vals, tuple):
+            b, o, nm = vals
+            cols.append(Column(StringBlock(torch.from_numpy(b), torch.from_numpy(o),
+                                           torch.from_numpy(nm) if nm.any() else None)))
+        elif isinstance(vals, list):
             cols.append(Column(vals))
         else:
             tt = torch.from_numpy(vals).to(t.torch_dtype)
             nm = torch.from_numpy(nulls) if nulls is not None and nulls.any() else None
             cols.append(Column(tt, nm))
     return MTable(schema, cols)
+
+
+def _csv_bytes_table(path, schema, row_delim, delim, quote, skip_blank, ignore_first) -> Optional[MTable]:
+    """The CSV source without Python strings: the file (or this rank's byte range) read as bytes, lines found
+    with numpy on a one-byte row delimiter, fields parsed in C++ straight from the file buffer
+    (``alink_csv_parse_spans``), string columns left packed as ``StringBlock``s.  None (the line path) for
+    URLs, multi-byte delimiters, or a single rank of a multi-rank job reading a non-file."""
+    from ... import _native
+    if _native.lib is None or getattr(_native.lib, "alink_csv_parse_spans", None) is None:
+        return None
+    d = row_delim.encode("utf-8")
+    if len(d) != 1 or len(delim) != 1 or (quote is not None and len(quote) != 1) or \
+            path.startswith(("http://", "https://")):
+        return None
+    codes = _csv_codes(schema)
+    if codes is None:
+        return None
+    fpath = path[len("file://"):] if path.startswith("file://") else path
+    if not os.path.isfile(fpath):
+        return None
+    ws = comm.get_world_size()
+    if ws > 1:
+        ranged = read_text_range(path, row_delim, comm.get_rank(), ws, raw=True)
+        if ranged is None:
+            return None
+        raw, first = ranged
+    else:
+        with open(fpath, "rb") as f:
+            raw = f.read()
+        first = True
+    buf = np.frombuffer(raw, dtype=np.uint8)
+    ends = np.flatnonzero(buf == d[0])
+    starts = np.empty(ends.size + 1, dtype=np.int64)
+    starts[0] = 0
+    starts[1:] = ends + 1
+    ends = np.append(ends, buf.size).astype(np.int64)
+    if starts[-1] == buf.size:           # text ending in the delimiter: no trailing empty line
+        starts, ends = starts[:-1], ends[:-1]
+    if row_delim == "\n" and ends.size:
+        cr = (ends > starts) & (buf[np.maximum(ends - 1, 0)] == 13)
+        ends = ends - cr
+    if ignore_first and first and starts.size:
+        starts, ends = starts[1:], ends[1:]
+    if skip_blank:
+        keep = ends > starts
+        if not keep.all():
+            starts, ends = starts[keep], ends[keep]
+    try:
+        res = _native.parse_csv_spans(buf, starts, ends, codes, delim, quote or "", blocks=True)
+    except _native._CsvLineError as e:
+        line = buf[starts[e.line]:ends[e.line]].tobytes().decode("utf-8", "replace")
+        raise RuntimeError(f'Fail to parse line "{line}"') from None
+    return None if res is None else _csv_table(schema, res)
+
+
+def _native_parse_csv(lines, schema, delim, quote, skip_blank) -> Optional[MTable]:
+    """Bulk path through the native C++ parser (numeric columns straight into arrays)."""
+    try:
+        from ... import _native
+    except Exception:
+        return None
+    if _native.lib is None or len(delim) != 1 or (quote is not None and len(quote) != 1):
+        return None
+    codes = _csv_codes(schema)
+    if codes is None:
+        return None
+    res = _native.parse_csv_lines(lines, codes, delim, quote or "", skip_blank)
+    return None if res is None else _csv_table(schema, res)
 
 
 class TextSourceBatchOp(BaseSourceBatchOp):

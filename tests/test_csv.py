@@ -1,6 +1,8 @@
 """CSV parser / formatter against the reference's unit tests (``core/src/test/java/com/alibaba/alink/operator/
 common/io/csv/{CsvParserTest,CsvFormatterTest}.java``)."""
 import datetime
+
+import pytest
 import math
 import random
 import sys
@@ -96,3 +98,39 @@ def test_csv_sink_columnar_matches_row_path(tmp_path, monkeypatch):
     fast = _sink_text(tmp_path, mt2, "e.csv", True, monkeypatch)
     slow = _sink_text(tmp_path, mt2, "f.csv", False, monkeypatch)
     assert fast == slow
+
+
+@pytest.mark.parametrize("crlf", [False, True])
+@pytest.mark.parametrize("skip_blank", [False, True])
+def test_csv_source_bytes_path_matches_line_path(tmp_path, monkeypatch, crlf, skip_blank):
+    """The byte-level CSV source (lines found with numpy, fields parsed in C++ from the file buffer, strings left
+    packed) reads the same rows as the line-by-line path: header skip, CRLF, blank lines, quoted fields with
+    delimiters and escaped quotes, nulls, non-ASCII text, a last line without its delimiter."""
+    from alink_amd.operator.batch import source as S
+    nl = "\r\n" if crlf else "\n"
+    lines = ["h1,h2,h3,h4", "1.5,7,abc,true", "", ',,"",', '-2e-3,-9,"x,y",false', '3,0,"say ""hi""",True',
+             "4,5,héllo wörld,0", "  6.25 , 12 ,  sp , 1 "]
+    text = nl.join(lines)
+    p = tmp_path / "in.csv"
+    p.write_bytes(text.encode("utf-8"))
+
+    def read(fast):
+        if not fast:
+            monkeypatch.setattr(S, "_csv_bytes_table", lambda *a, **k: None)
+        op = S.CsvSourceBatchOp().setFilePath(str(p)).setSchemaStr("a double, b long, s string, f boolean") \
+            .setIgnoreFirstLine(True).setSkipBlankLine(skip_blank)
+        rows = [tuple(r) for r in op.collect()]
+        monkeypatch.undo()
+        return rows
+
+    fast, slow = read(True), read(False)
+    assert fast == slow and len(fast) == (6 if skip_blank else 7)
+    assert any(r[2] == 'say "hi"' for r in fast)
+
+
+def test_csv_source_bytes_path_error_names_line(tmp_path):
+    from alink_amd.operator.batch.source import CsvSourceBatchOp
+    p = tmp_path / "bad.csv"
+    p.write_bytes(b"1,2\n3,x\n")
+    with pytest.raises(RuntimeError, match='"3,x"'):
+        CsvSourceBatchOp().setFilePath(str(p)).setSchemaStr("a double, b double").collect()
