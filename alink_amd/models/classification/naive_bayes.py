@@ -26,9 +26,8 @@ from ...common.params import Params
 from ...common.table import Column, MTable
 from ...common.types import Types
 from ...parallel import comm
-from ...common.strings import StringBlock
 from ..common.features import FeatureMatrix, extract_features, global_vector_size
-from ..linear.model import _dev, _recover_label
+from ..linear.model import _dev, _recover_label, label_column
 
 
 def _recount_crow(crow: torch.Tensor, keep: torch.Tensor) -> torch.Tensor:
@@ -181,12 +180,8 @@ class NaiveBayesTextModelMapper(RichModelMapper):
             idx = Sf.argmax(1)
             ok = Sf[np.arange(len(Sf)), idx] > -np.inf
             t = self.helper.out_types[0]
-            if ok.all() and all(v is not None for v in labels):
-                if t == Types.STRING and all(isinstance(v, str) for v in labels):
-                    return [Column(StringBlock.from_list(labels).take(torch.from_numpy(idx)))]
-                if t.torch_dtype is not None and t.py in (int, float) and \
-                        all(isinstance(v, (int, float)) and not isinstance(v, bool) for v in labels):
-                    return [Column(torch.tensor(labels, dtype=t.torch_dtype)[torch.from_numpy(idx)])]
+            if ok.all():
+                return [label_column(labels, idx, t)]
             lab = np.empty(len(labels), dtype=object)
             lab[:] = labels
             preds = lab[idx]

@@ -282,6 +282,22 @@ def _dev(mt: MTable):
     return torch.device("cpu")
 
 
+def label_column(labels: Sequence[Any], idx, t) -> Column:
+    """``[labels[i] for i in idx]`` as a column of type ``t`` without a per-row list: a tensor gather for numeric
+    labels, a ``StringBlock`` take for string labels (a list of python values otherwise)."""
+    idx = np.asarray(idx, dtype=np.int64)
+    it = torch.from_numpy(idx)
+    if t.torch_dtype is not None and t.py in (int, float) and labels and \
+            all(isinstance(v, (int, float)) and not isinstance(v, bool) for v in labels):
+        return Column(torch.tensor(list(labels), dtype=t.torch_dtype)[it])
+    if t == Types.STRING and labels and all(isinstance(v, str) for v in labels):
+        from ...common.strings import StringBlock
+        return Column(StringBlock.from_list(list(labels)).take(it))
+    lab = np.empty(len(labels), dtype=object)
+    lab[:] = list(labels)
+    return Column.from_values(lab[idx].tolist(), t)
+
+
 def _detail_json(labels: Sequence[Any], probs: np.ndarray, quoted: bool = True) -> List[str]:
     """HashMap<String,String> of label -> Double.toString(prob), Gson-serialised in Java HashMap order
     (``quoted`` False: HashMap<String,Double>, the same digits as JSON numbers — the tree mappers' detail).
@@ -333,7 +349,7 @@ class LinearModelMapper(_LinearMapperBase):
                                     torch.tensor(lv[1], dtype=t.torch_dtype))
                 out.append(Column(preds))
             else:
-                out.append(Column.from_values([lv[0] if v >= 0 else lv[1] for v in dot], t))
+                out.append(label_column(lv, np.where(dot >= 0, 0, 1), t))
         if self.detail_col:
             if tname in ("LR", "SVM"):
                 prob = 1.0 - 1.0 / (1.0 + np.exp(dot))
@@ -381,7 +397,7 @@ class SoftmaxModelMapper(_LinearMapperBase):
             s = 1.0 + e.sum(1, keepdims=True)
             probs = np.concatenate([e, np.ones((e.shape[0], 1))], 1) / s
             idx = probs.argmax(1)
-            out.append(Column.from_values([m.labelValues[i] for i in idx], self.helper.out_types[0]))
+            out.append(label_column(m.labelValues, idx, self.helper.out_types[0]))
             out.append(Column(_detail_json(m.labelValues, probs)))
         else:
             # predictResult: argmax over k < K-1 of eta with a 0.0 floor -> pivot class K-1
@@ -391,7 +407,7 @@ class SoftmaxModelMapper(_LinearMapperBase):
                 better = eta[:, k] > bval
                 best[better] = k
                 bval[better] = eta[better, k]
-            out.append(Column.from_values([m.labelValues[i] for i in best], self.helper.out_types[0]))
+            out.append(label_column(m.labelValues, best, self.helper.out_types[0]))
         return out
 
 
