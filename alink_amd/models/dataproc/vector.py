@@ -141,6 +141,33 @@ class VectorNormalizeMapper(SISOMapper):
         vec.normalizeEqual(float(self.params.get("p")) if self.params.contains("p") else 2.0)
         return vec
 
+    def _map_columns(self, mt):
+        """A dense 2-D tensor column normalised at once, with ``np.linalg.norm``'s per-order reductions along each
+        row (the row path's numbers to rounding: its 2-norm is a BLAS dot); other columns row by row."""
+        v = mt.cols[self.col_idx].values
+        if not (isinstance(v, torch.Tensor) and v.dim() == 2 and not v.is_complex()):
+            return super()._map_columns(mt)
+        p = float(self.params.get("p")) if self.params.contains("p") else 2.0
+        X = v.detach().to("cpu", torch.float64).numpy().copy()
+        if X.shape[1] == 0:
+            return [Column(torch.from_numpy(X))]
+        ax = np.abs(X)
+        if p == np.inf:
+            nrm = ax.max(1)
+        elif p == -np.inf:
+            nrm = ax.min(1)
+        elif p == 0:
+            nrm = (X != 0).sum(1).astype(np.float64)
+        elif p == 1:
+            nrm = np.add.reduce(ax, axis=1)
+        elif p == 2:
+            nrm = np.sqrt(np.add.reduce(X * X, axis=1))
+        else:
+            nrm = np.add.reduce(ax ** p, axis=1) ** (1.0 / p)
+        nz = nrm != 0
+        X[nz] /= nrm[nz, None]
+        return [Column(torch.from_numpy(X))]
+
 
 class VectorSliceMapper(SISOMapper):
     def outputType(self):

@@ -148,4 +148,9 @@ class PcaModelMapper(ModelMapper):
         Z = np.where(ok[None, :], (Z - self.mean[None, :]) / np.where(ok, self.std, 1.0)[None, :],
                      np.where(len(self.idx) != self.nx, 0.0, Z))
         P = Z @ self.coef.T / self.score_std[None, :]
-        return [Column.from_values([VectorUtil.toString(DenseVector(r)) for r in P], Types.STRING)]
+        from ... import _native
+        r = _native.java_double_rows_packed(P, " ") if P.size else None
+        if r is None:
+            return [Column.from_values([VectorUtil.toString(DenseVector(r)) for r in P], Types.STRING)]
+        from ...common.strings import StringBlock
+        return [Column(StringBlock(torch.from_numpy(np.ascontiguousarray(r[0])), torch.from_numpy(r[1])))]

@@ -193,7 +193,17 @@ def sql_order_by(mt: MTable, clause: str, order: str = "asc", limit=None, offset
         if len(toks) > 1 and toks[-1].lower() in ("asc", "desc"):
             asc = toks[-1].lower() == "asc"
             part = " ".join(toks[:-1])
-        keys.append((compile_expr(parse_expr(part), _resolver(mt.schema.names)), asc))
+        keys.append((parse_expr(part), asc))
+    idx = _order_columnar(mt, keys)
+    if idx is not None:
+        lo = offset if offset is not None and offset > 0 else 0
+        idx = idx[lo:]
+        if fetch is not None and fetch >= 0:
+            idx = idx[:fetch]
+        if limit is not None and limit >= 0:
+            idx = idx[:limit]
+        return mt.take(idx)
+    keys = [(compile_expr(e, _resolver(mt.schema.names)), asc) for e, asc in keys]
     rows = mt.rows()
     idx = list(range(len(rows)))
     for f, asc in reversed(keys):
@@ -207,6 +217,44 @@ def sql_order_by(mt: MTable, clause: str, order: str = "asc", limit=None, offset
     if limit is not None and limit >= 0:
         idx = idx[:limit]
     return mt.take(idx)
+
+
+def _order_columnar(mt: MTable, keys):
+    """Row order of ``ORDER BY`` over numeric key expressions evaluated on tensors: stable sorts from the last
+    key to the first, NULLs first ascending / last descending (the row path's key), equal keys in input order.
+    None (the row path) for a non-columnar key or a NaN key."""
+    import torch
+    from .vexpr import try_evaluate
+    n = mt.num_rows
+    if n == 0:
+        return None
+    res = _resolver(mt.schema.names)
+    ev = []
+    for e, asc in keys:
+        r = try_evaluate(e, mt, res)
+        if r is None:
+            return None
+        v, nm = r
+        if not isinstance(v, torch.Tensor) or v.dim() != 1 or v.numel() != n or v.is_complex():
+            return None
+        if v.dtype == torch.bool:
+            v = v.to(torch.int8)
+        elif v.is_floating_point():
+            if bool(torch.isnan(v if nm is None else v[~nm.to(v.device)]).any()):
+                return None
+            v = v + 0.0                               # -0.0 == 0.0 for the sort, as for python's compare
+        ev.append((v, None if nm is None else nm.to(v.device), asc))
+    idx = torch.arange(n, device=ev[0][0].device)
+    for v, nm, asc in reversed(ev):
+        idx = idx.to(v.device)
+        if nm is None:
+            idx = idx[torch.sort(v[idx], stable=True, descending=not asc).indices]
+            continue
+        knm = nm[idx]
+        nl, nn = idx[knm], idx[~knm]
+        nn = nn[torch.sort(v[nn], stable=True, descending=not asc).indices]
+        idx = torch.cat([nl, nn]) if asc else torch.cat([nn, nl])
+    return idx.cpu()
 
 
 def _factorize(c) -> Tuple[Any, int]:

@@ -135,3 +135,29 @@ def test_groupby_distinct_packed_string_keys_equal_list_keys():
         d = sql_distinct(MTable(TableSchema(["k"], [Types.STRING]), [kc])).col("k").to_list()
         outs.append(([tuple(r) for r in g], d))
     assert outs[0] == outs[1]
+
+
+@pytest.mark.parametrize("clause,order", [("a", "asc"), ("a", "desc"), ("a desc, b", "asc"), ("b, a asc", "desc"),
+                                          ("a + b", "asc")])
+def test_order_by_columnar_matches_row_path(monkeypatch, clause, order):
+    """ORDER BY on tensor keys (stable device sorts) gives the row path's order: ties in input order, NULLs
+    first ascending / last descending, -0.0 equal to 0.0, offset/limit applied after."""
+    import torch
+    from alink_amd.common.table import Column, MTable
+    from alink_amd.common.types import TableSchema, Types
+    from alink_amd.operator.common.sql import engine as E
+    g = torch.Generator().manual_seed(5)
+    n = 300
+    a = torch.randint(0, 7, (n,), generator=g).to(torch.float64)
+    a[::17] = -0.0
+    b = torch.randint(0, 4, (n,), generator=g)
+    an = torch.zeros(n, dtype=torch.bool)
+    an[5::23] = True
+    mt = MTable(TableSchema(["a", "b", "i"], [Types.DOUBLE, Types.LONG, Types.LONG]),
+                [Column(a, an), Column(b), Column(torch.arange(n))])
+    for off, lim in [(None, None), (3, 50)]:
+        fast = E.sql_order_by(mt, clause, order, limit=lim, offset=off)
+        with monkeypatch.context() as m:
+            m.setattr(E, "_order_columnar", lambda *x: None)
+            slow = E.sql_order_by(mt, clause, order, limit=lim, offset=off)
+        assert fast.col("i").values.tolist() == slow.col("i").values.tolist()

@@ -26,7 +26,7 @@ def main():
     ap.add_argument("--top", type=int, default=8)
     ap.add_argument("--set", type=int, default=1,
                     help="1: model ops; 2: data processing / SQL / scalers; 3: evaluation / NLP / trees / formats; "
-                         "4: IO, more model predicts")
+                         "4: IO, more model predicts; 5: SQL joins / sets / order, PCA, normalize, correlation, JSON")
     a = ap.parse_args()
     import alink_amd as A
     from alink_amd.common.table import Column, MTable
@@ -208,6 +208,34 @@ def main():
                                               A.DocHashCountVectorizerTrainBatchOp().setSelectedCol("doc")
                                               .setNumFeatures(1000).linkFrom(nb_docs), nb_docs))
             .getOutputTable().col("p").values,
+        }
+    if a.set == 5:
+        src = TableSourceBatchOp(dense)
+        keyed = MTable(TableSchema(["k", "x0", "c"], [Types.LONG, Types.DOUBLE, Types.STRING]),
+                       [Column(cats.to(torch.int64)), cols[0], Column(vocab.take(cats))])
+        dim = MTable(TableSchema(["k2", "name"], [Types.LONG, Types.STRING]),
+                     [Column(torch.arange(1000, device=dev)), Column(vocab)])
+        ksrc, dsrc = TableSourceBatchOp(keyed), TableSourceBatchOp(dim)
+        pca_model = A.PcaTrainBatchOp().setSelectedCols(names).setK(5).linkFrom(src)
+        js = A.ColumnsToJsonBatchOp().setSelectedCols(names[:3]).setJsonCol("j").setReservedCols([]) \
+            .linkFrom(src).getOutputTable()
+        jsrc = TableSourceBatchOp(js)
+        vsrc = TableSourceBatchOp(vec)
+        jobs = {
+            "join": lambda: A.JoinBatchOp().setJoinPredicate("k = k2").setSelectClause("k, x0, name")
+            .linkFrom(ksrc, dsrc).getOutputTable(),
+            "union_all": lambda: A.UnionAllBatchOp().linkFrom(ksrc, ksrc).getOutputTable(),
+            "distinct": lambda: A.DistinctBatchOp().linkFrom(
+                TableSourceBatchOp(MTable(TableSchema(["k", "c"], [Types.LONG, Types.STRING]),
+                                          [keyed.cols[0], keyed.cols[2]]))).getOutputTable(),
+            "order_by": lambda: A.OrderByBatchOp().setClause("x0").setLimit(1000).linkFrom(ksrc).getOutputTable(),
+            "pca_predict": lambda: A.PcaPredictBatchOp().setPredictionCol("p").setReservedCols([])
+            .linkFrom(pca_model, src).getOutputTable().col("p").values,
+            "vector_normalize": lambda: A.VectorNormalizeBatchOp().setSelectedCol("vec").linkFrom(vsrc)
+            .getOutputTable().col("vec").values,
+            "correlation": lambda: A.CorrelationBatchOp().setSelectedCols(names).linkFrom(src).collect(),
+            "json_value": lambda: A.JsonValueBatchOp().setSelectedCol("j").setJsonPath(["$.x0", "$.x1"])
+            .setOutputCols(["a", "b"]).linkFrom(jsrc).getOutputTable(),
         }
     only = [s for s in a.only.split(",") if s]
     for name, fn in jobs.items():
