@@ -19,6 +19,7 @@ per micro-batch on the CPU side of the DAG, columnar where the input allows it.
 """
 from __future__ import annotations
 
+import functools
 import json
 import re
 from typing import Any, Dict, List, Optional, Sequence, Tuple
@@ -27,7 +28,7 @@ from ...common.javafmt import gson_dumps, java_double_str, java_hashmap_order, j
 from ...common.linalg import DenseVector, SparseVector, VectorUtil
 from ...common.mapper import FlatMapper, Mapper, OutputColsHelper, find_col_index, find_col_indices
 from ...common.params import Params
-from ...common.table import Row
+from ...common.table import Column, Row
 from ...common.types import TableSchema, Types, schema_str_to_schema
 from ...operator.common.io.csv import CsvParser, parse_token
 
@@ -168,14 +169,13 @@ def lenient_json_loads(s: str):
 _PATH_TOK = re.compile(r"\.\.|\.\*|\.([^.\[\]]+)|\[\s*\*\s*\]|\[\s*(-?\d+)\s*\]|\[\s*['\"]([^'\"]+)['\"]\s*\]")
 
 
-def json_path_read(doc, path: str):
-    """Subset of Jayway JsonPath used by Alink docs: ``$``, ``.name``, ``['name']``, ``[i]``, ``[*]``, ``.*``.
-    A wildcard makes the result a list.  Missing keys raise ``KeyError`` (``PathNotFoundException``)."""
+@functools.lru_cache(maxsize=256)
+def _json_path_tokens(path: str):
+    """A json path split once into (kind, arg) steps: ("*", None) wildcard, ("i", int) index, ("k", str) key."""
     path = path.strip()
     if not path.startswith("$"):
         path = "$." + path
-    cur = [doc]
-    multi = False
+    toks = []
     pos = 1
     while pos < len(path):
         m = _PATH_TOK.match(path, pos)
@@ -183,27 +183,41 @@ def json_path_read(doc, path: str):
             raise ValueError(f"bad json path {path}")
         tok = m.group(0)
         pos = m.end()
-        nxt = []
         if tok == "..":
             raise ValueError("deep scan '..' is not supported")
         if tok in (".*",) or tok.replace(" ", "") == "[*]":
+            toks.append(("*", None))
+        elif m.group(2) is not None:
+            toks.append(("i", int(m.group(2))))
+        else:
+            toks.append(("k", m.group(1) if m.group(1) is not None else m.group(3)))
+    return path, tuple(toks)
+
+
+def json_path_read(doc, path: str):
+    """Subset of Jayway JsonPath used by Alink docs: ``$``, ``.name``, ``['name']``, ``[i]``, ``[*]``, ``.*``.
+    A wildcard makes the result a list.  Missing keys raise ``KeyError`` (``PathNotFoundException``)."""
+    path, toks = _json_path_tokens(path)
+    cur = [doc]
+    multi = False
+    for kind, arg in toks:
+        nxt = []
+        if kind == "*":
             multi = True
             for c in cur:
                 if isinstance(c, dict):
                     nxt.extend(c.values())
                 elif isinstance(c, list):
                     nxt.extend(c)
-        elif m.group(2) is not None:
-            i = int(m.group(2))
+        elif kind == "i":
             for c in cur:
                 if not isinstance(c, list):
                     raise KeyError(path)
-                nxt.append(c[i])
+                nxt.append(c[arg])
         else:
-            key = m.group(1) if m.group(1) is not None else m.group(3)
             for c in cur:
-                if isinstance(c, dict) and key in c:
-                    nxt.append(c[key])
+                if isinstance(c, dict) and arg in c:
+                    nxt.append(c[arg])
                 elif not multi:
                     raise KeyError(f"No results for path: {path}")
         cur = nxt
@@ -1101,3 +1115,43 @@ class JsonPathMapper(Mapper):
                     raise RuntimeError(f"Fail to getVector json path: {e}")
                 res.append(None)
         return res
+
+    def _map_columns(self, mt):
+        """Plain key paths (``$.a.b``) read over the whole column in one loop: no row tuples, no per-row path
+        walk set-up; the row path's values, NULLs and errors."""
+        try:
+            keys = [_json_path_tokens(p)[1] for p in self.paths]
+        except ValueError:
+            return super()._map_columns(mt)
+        if not all(toks and all(k == "k" for k, _ in toks) for toks in keys):
+            return super()._map_columns(mt)
+        keys = [tuple(a for _, a in toks) for toks in keys]
+        texts = mt.cols[self.idx].to_list()
+        n = len(texts)
+        outs = [[None] * n for _ in keys]
+        skip = self.skip
+        for i, text in enumerate(texts):
+            if text is None or not str(text).strip():
+                if skip:
+                    continue
+                raise RuntimeError("empty json string")
+            try:
+                doc = lenient_json_loads(text)
+            except ValueError as e:
+                if not skip:
+                    raise RuntimeError(f"Fail to getVector json path: {e}")
+                continue
+            for j, ks in enumerate(keys):
+                o = doc
+                for k in ks:
+                    if isinstance(o, dict) and k in o:
+                        o = o[k]
+                    else:
+                        if not skip:
+                            raise RuntimeError(f"Fail to getVector json path: 'No results for path: "
+                                               f"{_json_path_tokens(self.paths[j])[0]}'")
+                        o = None
+                        break
+                else:
+                    outs[j][i] = o if isinstance(o, str) else _gson_of(o)
+        return [Column(o) for o in outs]

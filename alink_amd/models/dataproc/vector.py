@@ -148,6 +148,11 @@ class VectorNormalizeMapper(SISOMapper):
         if not (isinstance(v, torch.Tensor) and v.dim() == 2 and not v.is_complex()):
             return super()._map_columns(mt)
         p = float(self.params.get("p")) if self.params.contains("p") else 2.0
+        if v.is_cuda and v.shape[1] and p in (1.0, 2.0, float("inf")):
+            # on the device: the same orders through torch's row norms (to rounding), float64 like the row path
+            X = v.detach().to(torch.float64)
+            nrm = torch.linalg.vector_norm(X, ord=p, dim=1, keepdim=True)
+            return [Column(torch.where(nrm != 0, X / torch.where(nrm != 0, nrm, torch.ones_like(nrm)), X))]
         X = v.detach().to("cpu", torch.float64).numpy().copy()
         if X.shape[1] == 0:
             return [Column(torch.from_numpy(X))]

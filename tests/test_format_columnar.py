@@ -364,3 +364,56 @@ def test_pca_predict_packed_strings():
         s = r[-1]
         assert s == VectorUtil.toString(DenseVector(np.array([float(x) for x in s.split(" ")])))
         assert len(s.split(" ")) == 2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("p", [1.0, 2.0, float("inf")])
+def test_vector_normalize_device(p):
+    """VectorNormalize on a cuda 2-D column stays on the device and equals the host path to rounding."""
+    import torch
+    from alink_amd.common.params import Params
+    from alink_amd.common.table import Column, MTable
+    from alink_amd.common.types import TableSchema, Types
+    from alink_amd.models.dataproc.vector import VectorNormalizeMapper
+    X = torch.randn(1000, 33, dtype=torch.float64)
+    X[7] = 0
+    schema = TableSchema(["v"], [Types.DENSE_VECTOR])
+    m = VectorNormalizeMapper(schema, Params().set("selectedCol", "v").set("p", p))
+    host = m._map_columns(MTable(schema, [Column(X)]))[0].values
+    dev = m._map_columns(MTable(schema, [Column(X.cuda())]))[0].values
+    assert dev.is_cuda and dev.dtype == torch.float64
+    torch.testing.assert_close(dev.cpu(), host, rtol=1e-14, atol=0)
+
+
+@pytest.mark.parametrize("skip", [True, False])
+def test_json_value_columnar_matches_row_path(skip):
+    from alink_amd.common.params import Params
+    from alink_amd.common.table import MTable
+    from alink_amd.common.types import TableSchema, Types
+    from alink_amd.models.dataproc.format import JsonPathMapper
+    docs = ['{"a": 1, "b": {"c": "x", "d": [1, 2.5]}}', '{"a": 1.5e3, "b": {"c": {"z": true}}}',
+            '{"a": "s", "b": {}}', None, "  ", "{bad", '{"a": null, "b": {"c": null}}']
+    if not skip:
+        docs = [docs[0], docs[1], docs[6]]
+    schema = TableSchema(["j"], [Types.STRING])
+    mt = MTable.from_rows([(d,) for d in docs], schema)
+    paths = ["$.a", "$.b.c", "b.d"] if skip else ["$.a", "$.b.c"]
+    m = JsonPathMapper(schema, Params().set("selectedCol", "j").set("jsonPath", paths)
+                       .set("outputCols", [f"o{i}" for i in range(len(paths))]).set("skipFailed", skip))
+    cols = m._map_columns(mt)
+    fast = [tuple(c.to_list()[i] for c in cols) for i in range(len(docs))]
+    slow = [tuple(m._map_row_values((d,))) for d in docs]
+    assert fast == slow
+
+
+def test_json_value_columnar_raises_like_row_path():
+    from alink_amd.common.params import Params
+    from alink_amd.common.table import MTable
+    from alink_amd.common.types import TableSchema, Types
+    from alink_amd.models.dataproc.format import JsonPathMapper
+    schema = TableSchema(["j"], [Types.STRING])
+    m = JsonPathMapper(schema, Params().set("selectedCol", "j").set("jsonPath", ["$.q"]).set("outputCols", ["o"]))
+    with pytest.raises(RuntimeError, match="No results for path"):
+        m._map_columns(MTable.from_rows([('{"a": 1}',)], schema))
+    with pytest.raises(RuntimeError, match="No results for path"):
+        m._map_row_values(('{"a": 1}',))
