@@ -16,7 +16,8 @@ __all__ = ["lib", "parse_csv_lines", "murmur3_utf16", "murmur3_bytes", "murmur3_
            "java_double_rows", "java_double_rows_packed", "parse_csv_packed",
            "parse_dense_vectors_packed", "parse_kv_packed", "parse_json_flat_packed", "java_double_rows_fmt", "sample_thresholds", "gbdt_rank_grad",
            "tree_flatten", "java_float_rows", "java_float_rows_packed", "parse_double_csv",
-           "java_float_kv_rows", "join_packed_columns", "parse_csv_spans"]
+           "java_float_kv_rows", "join_packed_columns", "parse_csv_spans",
+           "json_top_values"]
 
 # ALINK_NATIVE_LIB points at another build of the same sources (e.g. the AddressSanitizer build of
 # tools/asan_host.py)
@@ -45,6 +46,8 @@ if os.path.exists(_PATH):
             lib.alink_java_float_rows.restype = ctypes.c_int64
         if hasattr(lib, "alink_java_float_kv_rows"):
             lib.alink_java_float_kv_rows.restype = ctypes.c_int64
+        if hasattr(lib, "alink_json_top_values"):
+            lib.alink_json_top_values.restype = None
         if hasattr(lib, "alink_join_packed_columns"):
             lib.alink_join_packed_columns.restype = None
         if hasattr(lib, "alink_java_double_rows_fmt"):
@@ -615,3 +618,23 @@ def tree_flatten(strings: Sequence[str], tree_lo: Sequence[int]):
     out["dist"] = out["dist"][:, :max(1, int(md.value))]
     out["max_dist"] = int(md.value)
     return out
+
+
+def json_top_values(data: np.ndarray, off: np.ndarray, keys: Sequence[str]):
+    """Top-level members ``keys`` of packed JSON objects scanned in C++: (span int64 [n, k, 2] absolute byte
+    offsets, kind uint8 [n, k], num float64 [n, k], row_ok bool [n]) -- kinds as ``alink_json_top_values``
+    documents; None without the library."""
+    if lib is None or getattr(lib, "alink_json_top_values", None) is None:
+        return None
+    data = np.ascontiguousarray(data, dtype=np.uint8) if data.size else np.zeros(1, np.uint8)
+    off = np.ascontiguousarray(off, dtype=np.int64)
+    n, k = off.size - 1, len(keys)
+    kb, koff = _pack_utf8(list(keys))
+    kb = np.frombuffer(kb, dtype=np.uint8) if kb else np.zeros(1, np.uint8)
+    span = np.zeros((max(n, 1), k, 2), dtype=np.int64)
+    kind = np.zeros((max(n, 1), k), dtype=np.uint8)
+    num = np.zeros((max(n, 1), k), dtype=np.float64)
+    ok = np.zeros(max(n, 1), dtype=np.uint8)
+    lib.alink_json_top_values(_ptr(data), _ptr(off), ctypes.c_int64(n), _ptr(kb), _ptr(koff), ctypes.c_int64(k),
+                              _ptr(span), _ptr(kind), _ptr(num), _ptr(ok))
+    return span[:n], kind[:n], num[:n], ok[:n].astype(bool)

@@ -820,3 +820,140 @@ extern "C" void alink_join_packed_columns(int64_t k, const uint8_t* const* data,
         std::memcpy(p, rowdelim, (size_t)rlen);
     }
 }
+
+// ---------------------------------------------------------------------------------------------------------------
+// Top-level member values of JSON objects (JsonValueBatchOp with plain "$.key" paths).  Per document i and key j:
+//   kind 0 missing, 1 string without escapes / control bytes (span = its contents), 3 canonical integer literal
+//   (span = its text), 4 other number (num = strtod value), 5 true / false (span = its text), 2 anything else
+//   (object, array, null, escaped string, "-0": the caller's JSON reader formats it).
+// row_ok[i] = 0 when the document is not one well-formed JSON object as this scanner reads it (the caller parses
+// it with its lenient reader).  Duplicate members: the last one wins, as a dict-building parser.
+namespace {
+struct JsonScan {
+    const uint8_t* s;
+    int64_t n, p;
+    bool ws() {
+        while (p < n && (s[p] == ' ' || s[p] == '\t' || s[p] == '\n' || s[p] == '\r')) ++p;
+        return p < n;
+    }
+    // string at s[p] == '"': end = index of the closing quote; esc = backslash or control byte inside
+    bool str(int64_t& a, int64_t& b, bool& esc) {
+        a = ++p;
+        esc = false;
+        while (p < n && s[p] != '"') {
+            if (s[p] == '\\') { esc = true; p += 2; continue; }
+            if (s[p] < 0x20) esc = true;
+            ++p;
+        }
+        if (p >= n) return false;
+        b = p++;
+        return true;
+    }
+    bool skip_nested() {  // s[p] is '{' or '['
+        int depth = 0;
+        while (p < n) {
+            uint8_t c = s[p];
+            if (c == '"') { int64_t a, b; bool e; if (!str(a, b, e)) return false; continue; }
+            if (c == '{' || c == '[') ++depth;
+            else if (c == '}' || c == ']') { if (--depth == 0) { ++p; return true; } }
+            ++p;
+        }
+        return false;
+    }
+};
+}  // namespace
+
+extern "C" void alink_json_top_values(const uint8_t* buf, const int64_t* off, int64_t n, const uint8_t* kbuf,
+                                      const int64_t* koff, int64_t k, int64_t* span, uint8_t* kind, double* num,
+                                      uint8_t* row_ok) {
+#pragma omp parallel for schedule(dynamic, 4096) if (n > 4096)
+    for (int64_t i = 0; i < n; ++i) {
+        uint8_t* kd = kind + i * k;
+        for (int64_t j = 0; j < k; ++j) kd[j] = 0;
+        JsonScan t{buf + off[i], off[i + 1] - off[i], 0};
+        bool ok = t.ws() && t.s[t.p] == '{';
+        if (ok) {
+            ++t.p;
+            ok = t.ws();
+            if (ok && t.s[t.p] == '}') ++t.p;
+            else {
+                while (ok) {
+                    int64_t ka, kb;
+                    bool kesc;
+                    if (!(t.s[t.p] == '"' && t.str(ka, kb, kesc)) || kesc) { ok = false; break; }
+                    if (!t.ws() || t.s[t.p] != ':') { ok = false; break; }
+                    ++t.p;
+                    if (!t.ws()) { ok = false; break; }
+                    int64_t va = t.p, vb;
+                    uint8_t vk;
+                    double v = 0;
+                    uint8_t c = t.s[t.p];
+                    if (c == '"') {
+                        int64_t a, b;
+                        bool e;
+                        if (!t.str(a, b, e)) { ok = false; break; }
+                        va = a, vb = b, vk = e ? 2 : 1;
+                    } else if (c == '{' || c == '[') {
+                        if (!t.skip_nested()) { ok = false; break; }
+                        vb = t.p, vk = 2;
+                    } else if (c == 't' || c == 'f' || c == 'n') {
+                        const char* lit = c == 't' ? "true" : (c == 'f' ? "false" : "null");
+                        int64_t L = (int64_t)std::strlen(lit);
+                        if (t.p + L > t.n || std::memcmp(t.s + t.p, lit, (size_t)L) != 0) { ok = false; break; }
+                        t.p += L;
+                        vb = t.p, vk = c == 'n' ? 2 : 5;
+                    } else if (c == '-' || (c >= '0' && c <= '9')) {
+                        int64_t q = t.p + (c == '-');
+                        int64_t d0 = q;
+                        while (q < t.n && t.s[q] >= '0' && t.s[q] <= '9') ++q;
+                        int64_t nd = q - d0;
+                        if (nd == 0 || (nd > 1 && t.s[d0] == '0')) { ok = false; break; }
+                        bool isint = true;
+                        if (q < t.n && t.s[q] == '.') {
+                            isint = false;
+                            int64_t f0 = ++q;
+                            while (q < t.n && t.s[q] >= '0' && t.s[q] <= '9') ++q;
+                            if (q == f0) { ok = false; break; }
+                        }
+                        if (q < t.n && (t.s[q] == 'e' || t.s[q] == 'E')) {
+                            isint = false;
+                            ++q;
+                            if (q < t.n && (t.s[q] == '+' || t.s[q] == '-')) ++q;
+                            int64_t e0 = q;
+                            while (q < t.n && t.s[q] >= '0' && t.s[q] <= '9') ++q;
+                            if (q == e0) { ok = false; break; }
+                        }
+                        vb = q;
+                        t.p = q;
+                        if (isint) {
+                            vk = (c == '-' && nd == 1 && t.s[d0] == '0') ? 2 : 3;
+                        } else {
+                            std::string tmp((const char*)t.s + va, (size_t)(vb - va));
+                            v = std::strtod(tmp.c_str(), nullptr);
+                            vk = 4;
+                        }
+                    } else { ok = false; break; }
+                    for (int64_t j = 0; j < k; ++j) {
+                        int64_t L = koff[j + 1] - koff[j];
+                        if (L == kb - ka && std::memcmp(t.s + ka, kbuf + koff[j], (size_t)L) == 0) {
+                            kd[j] = vk;
+                            span[2 * (i * k + j)] = off[i] + va;
+                            span[2 * (i * k + j) + 1] = off[i] + vb;
+                            num[i * k + j] = v;
+                        }
+                    }
+                    if (!t.ws()) { ok = false; break; }
+                    if (t.s[t.p] == ',') {
+                        ++t.p;
+                        if (!t.ws()) { ok = false; break; }
+                        continue;
+                    }
+                    if (t.s[t.p] == '}') { ++t.p; break; }
+                    ok = false;
+                }
+            }
+            if (ok && t.ws()) ok = false;  // trailing bytes after the object
+        }
+        row_ok[i] = ok ? 1 : 0;
+    }
+}

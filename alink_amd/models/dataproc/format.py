@@ -1126,6 +1126,10 @@ class JsonPathMapper(Mapper):
         if not all(toks and all(k == "k" for k, _ in toks) for toks in keys):
             return super()._map_columns(mt)
         keys = [tuple(a for _, a in toks) for toks in keys]
+        if mt.num_rows and all(len(ks) == 1 for ks in keys):
+            out = self._top_members_native(mt, [ks[0] for ks in keys])
+            if out is not None:
+                return out
         texts = mt.cols[self.idx].to_list()
         n = len(texts)
         outs = [[None] * n for _ in keys]
@@ -1155,3 +1159,68 @@ class JsonPathMapper(Mapper):
                 else:
                     outs[j][i] = o if isinstance(o, str) else _gson_of(o)
         return [Column(o) for o in outs]
+
+    def _top_members_native(self, mt, keys):
+        """Top-level members through the C++ scanner (``_native.json_top_values``): plain strings, integer
+        literals and booleans are copied as bytes, other numbers formatted by the C++ Double.toString, and only
+        documents holding something else (objects, arrays, null, escapes, a missing member without skipFailed,
+        a malformed document) go through ``_map_row_values``; the columns come back as ``StringBlock``s."""
+        import numpy as np
+        import torch
+        from ... import _native as N
+        from ...common.strings import StringBlock
+        v = mt.cols[self.idx].values
+        n = mt.num_rows
+        if isinstance(v, StringBlock):
+            data, off = v.data.cpu().numpy(), v.offsets.cpu().numpy()
+            nm = v.nulls.cpu().numpy() if v.nulls is not None else np.zeros(n, dtype=bool)
+        elif isinstance(v, list) and all(x is None or isinstance(x, str) for x in v):
+            b, off = N._pack_utf8(["" if x is None else x for x in v])
+            data = np.frombuffer(b, dtype=np.uint8)
+            nm = np.fromiter((x is None for x in v), dtype=bool, count=n)
+        else:
+            return None
+        r = N.json_top_values(data, off, keys)
+        if r is None:
+            return None
+        span, kind, num, ok = r
+        py = ~ok | nm | (kind == 2).any(1)
+        if not self.skip:
+            py |= (kind == 0).any(1)
+        py_rows = np.flatnonzero(py)
+        py_vals = []
+        for i in py_rows.tolist():
+            text = None if nm[i] else bytes(data[off[i]:off[i + 1]]).decode("utf-8")
+            row = [None] * (self.idx + 1)
+            row[self.idx] = text
+            py_vals.append(self._map_row_values(row))
+        fast = ~py
+        cols = []
+        for j in range(len(keys)):
+            kj = kind[:, j]
+            lens = np.where(fast & ((kj == 1) | (kj == 3) | (kj == 5)), span[:, j, 1] - span[:, j, 0], 0)
+            src = span[:, j, 0].copy()
+            nulls = fast & (kj == 0)
+            parts = [data]
+            base = data.size
+            f = np.flatnonzero(fast & (kj == 4))
+            if f.size:
+                fb, fo = N.java_double_rows_packed(num[f, j].reshape(-1, 1), " ")
+                lens[f] = fo[1:] - fo[:-1]
+                src[f] = base + fo[:-1]
+                parts.append(np.asarray(fb, dtype=np.uint8))
+                base += int(fo[-1])
+            if py_rows.size:
+                strs = [pv[j] for pv in py_vals]
+                pb, po = N._pack_utf8(["" if x is None else x for x in strs])
+                lens[py_rows] = po[1:] - po[:-1]
+                src[py_rows] = base + po[:-1]
+                nulls[py_rows] = np.fromiter((x is None for x in strs), dtype=bool, count=len(strs))
+                parts.append(np.frombuffer(pb, dtype=np.uint8))
+            allb = np.concatenate(parts) if len(parts) > 1 else data
+            o = np.zeros(n + 1, dtype=np.int64)
+            np.cumsum(lens, out=o[1:])
+            idx = np.repeat(src - o[:-1], lens) + np.arange(int(o[-1]), dtype=np.int64)
+            cols.append(Column(StringBlock(torch.from_numpy(allb[idx]), torch.from_numpy(o),
+                                           torch.from_numpy(nulls) if nulls.any() else None)))
+        return cols

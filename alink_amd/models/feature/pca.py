@@ -137,20 +137,40 @@ class PcaModelMapper(ModelMapper):
         self.nx = nx
 
     def _map_columns(self, mt):
-        fm = extract_features(mt, self.fcols if not self.vcol else None, self.vcol, torch.device("cpu"))
+        from ..linear.model import _dev
+        dev = _dev(mt)
+        fm = extract_features(mt, self.fcols if not self.vcol else None, self.vcol, dev)
         if fm.is_sparse:
             fm.set_ncols(self.nx)
-        X = fm.to_dense().double().numpy()
-        if X.shape[1] < self.nx:
-            X = np.pad(X, ((0, 0), (0, self.nx - X.shape[1])))
-        Z = X[:, self.idx]
-        ok = np.abs(self.std) > 1e-12
-        Z = np.where(ok[None, :], (Z - self.mean[None, :]) / np.where(ok, self.std, 1.0)[None, :],
-                     np.where(len(self.idx) != self.nx, 0.0, Z))
-        P = Z @ self.coef.T / self.score_std[None, :]
+        if dev.type == "cuda" and mt.num_rows:
+            P = self._project_device(fm.to_dense().double())
+        else:
+            P = self._project(fm.to_dense().double().numpy())
         from ... import _native
         r = _native.java_double_rows_packed(P, " ") if P.size else None
         if r is None:
             return [Column.from_values([VectorUtil.toString(DenseVector(r)) for r in P], Types.STRING)]
         from ...common.strings import StringBlock
         return [Column(StringBlock(torch.from_numpy(np.ascontiguousarray(r[0])), torch.from_numpy(r[1])))]
+
+    def _project_device(self, X: torch.Tensor) -> np.ndarray:
+        """``_project`` in float64 on the input's device (the same operations; matmul rounding may differ)."""
+        dev = X.device
+        if X.shape[1] < self.nx:
+            X = torch.nn.functional.pad(X, (0, self.nx - X.shape[1]))
+        t = lambda a: torch.as_tensor(a, dtype=torch.float64, device=dev)  # noqa: E731
+        Z = X[:, torch.as_tensor(self.idx, dtype=torch.int64, device=dev)]
+        ok = np.abs(self.std) > 1e-12
+        std = t(np.where(ok, self.std, 1.0))
+        Zs = (Z - t(self.mean)[None, :]) / std[None, :]
+        Z = torch.where(torch.as_tensor(ok, device=dev)[None, :], Zs, Z if len(self.idx) == self.nx else torch.zeros_like(Z))
+        return (Z @ t(self.coef).T / t(self.score_std)[None, :]).cpu().numpy()
+
+    def _project(self, X: np.ndarray) -> np.ndarray:
+        if X.shape[1] < self.nx:
+            X = np.pad(X, ((0, 0), (0, self.nx - X.shape[1])))
+        Z = X[:, self.idx]
+        ok = np.abs(self.std) > 1e-12
+        Z = np.where(ok[None, :], (Z - self.mean[None, :]) / np.where(ok, self.std, 1.0)[None, :],
+                     np.where(len(self.idx) != self.nx, 0.0, Z))
+        return Z @ self.coef.T / self.score_std[None, :]

@@ -85,6 +85,26 @@ m = N.ftrl_partial_margin(indptr, idx, val, w[10:30].copy(), 10, 30)
 assert m.shape == (nrows,)
 ws, ns, zs = w[10:30].copy(), n[10:30].copy(), z[10:30].copy()
 N.ftrl_shard_update(indptr, idx, val, rng.normal(size=nrows), ws, ns, zs, 10, 30, 0.1, 1.0, 0.01, 0.01)
+# round-6 entry points: CSV over spans, JSON top-level members, packed column join, Java float rows
+data = np.frombuffer(b'1,"a""b",2\n\n3,,x\n4,"unterminated', dtype=np.uint8)
+st = np.array([0, 11, 12, 18], dtype=np.int64)
+en = np.array([10, 11, 17, 31], dtype=np.int64)
+for blocks in (False, True):
+    try:
+        N.parse_csv_spans(data, st, en, [2, 0, 0], ",", '"', blocks=blocks)
+    except RuntimeError:
+        pass
+docs = [b'{"a": 1, "b": "x"}', b'{"a": [1, {"q": "]"}], "b": "\\"}', b'{"a":', b'{"a": "unterminated',
+        b'', b'{"a": -0, "b": 1e400}', b'{"a"', b'{' * 3000]
+jd = np.frombuffer(b"".join(docs), dtype=np.uint8)
+jo = np.zeros(len(docs) + 1, dtype=np.int64)
+jo[1:] = np.cumsum([len(d) for d in docs])
+N.json_top_values(jd, jo, ["a", "b", ""])
+N.json_top_values(jd, jo, [])
+c1 = (np.frombuffer(b"abcde", dtype=np.uint8), np.array([0, 2, 2, 5], dtype=np.int64))
+c2 = (np.zeros(0, dtype=np.uint8), np.zeros(4, dtype=np.int64))
+assert bytes(N.join_packed_columns([c1, c2], ",", "\r\n")) == b"ab,\r\n,\r\ncde,\r\n"
+N.java_float_rows(np.array([[1.5, -0.0, 3e38], [1e-45, np.nan, np.inf]], dtype=np.float32), " ")
 print("ASAN_EXERCISE_OK")
 '''
 
