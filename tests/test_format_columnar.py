@@ -420,7 +420,8 @@ def test_json_value_columnar_raises_like_row_path():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("calc,transform", [("COV", "SIMPLE"), ("CORR", "NORMALIZATION"), ("COV", "SUBMEAN")])
+@pytest.mark.parametrize("calc,transform", [("COV_SAMPLE", "SIMPLE"), ("CORR", "NORMALIZATION"),
+                                            ("COVAR_POP", "SUBMEAN")])
 def test_pca_predict_device_matches_host(calc, transform):
     """PCA projection on a cuda table equals the host projection to rounding."""
     import numpy as np
