@@ -174,6 +174,14 @@ class VectorNormalizeMapper(SISOMapper):
         return [Column(torch.from_numpy(X))]
 
 
+def _dense_col(mt, i):
+    """The 2-D float tensor of a dense vector column (None for any other layout)."""
+    v = mt.cols[i].values
+    if isinstance(v, torch.Tensor) and v.dim() == 2 and v.is_floating_point():
+        return v
+    return None
+
+
 class VectorSliceMapper(SISOMapper):
     def outputType(self):
         return Types.VECTOR
@@ -182,6 +190,13 @@ class VectorSliceMapper(SISOMapper):
         if v is None:
             return None
         return VectorUtil.getVector(v).slice(self.params.get("indices"))
+
+    def _map_columns(self, mt):
+        X = _dense_col(mt, self.col_idx)
+        idx = [int(i) for i in self.params.get("indices")]
+        if X is None or any(i < -X.shape[1] or i >= X.shape[1] for i in idx):
+            return super()._map_columns(mt)
+        return [Column(X.to(torch.float64)[:, torch.as_tensor(idx, dtype=torch.int64, device=X.device)])]
 
 
 class VectorElementwiseProductMapper(SISOMapper):
@@ -200,6 +215,14 @@ class VectorElementwiseProductMapper(SISOMapper):
         if isinstance(vec, SparseVector):
             return SparseVector(vec.n, vec.indices.copy(), vec.values * s[vec.indices])
         return DenseVector(vec.data * s[:vec.size()])
+
+    def _map_columns(self, mt):
+        X = _dense_col(mt, self.col_idx)
+        s = self.scale.toDense().data
+        if X is None or s.size < X.shape[1]:
+            return super()._map_columns(mt)
+        return [Column(X.to(torch.float64) * torch.as_tensor(s[:X.shape[1]], dtype=torch.float64,
+                                                             device=X.device)[None, :])]
 
 
 class VectorInteractionMapper(MISOMapper):
@@ -222,6 +245,15 @@ class VectorInteractionMapper(MISOMapper):
             return SparseVector(a.size() * b.size(), idx, val)
         return DenseVector(np.outer(a.data, b.data).reshape(-1))
 
+    def _map_columns(self, mt):
+        if len(self.col_idx) != 2:
+            return super()._map_columns(mt)
+        A, B = _dense_col(mt, self.col_idx[0]), _dense_col(mt, self.col_idx[1])
+        if A is None or B is None or A.device != B.device:
+            return super()._map_columns(mt)
+        A, B = A.to(torch.float64), B.to(torch.float64)
+        return [Column((A[:, :, None] * B[:, None, :]).reshape(A.shape[0], -1))]
+
 
 def poly_size(num_features: int, degree: int) -> int:
     """Number of monomials of total degree <= ``degree`` in ``num_features`` variables, constant included
@@ -243,6 +275,26 @@ def _expand_dense(vals, last, degree, mult, out, cur):
             i += 1
             alpha *= v
     return cur + poly_size(last + 1, degree)
+
+
+def _poly_terms(d: int, degree: int):
+    """(output position, exponent per feature) of every monomial ``_expand_dense`` writes, in its order."""
+    terms = []
+
+    def rec(last, deg, exps, cur):
+        if deg == 0 or last < 0:
+            if cur >= 0:
+                terms.append((cur, tuple(exps)))
+        else:
+            start = cur
+            for i in range(deg + 1):
+                e = list(exps)
+                e[last] = i
+                start = rec(last - 1, deg - i, e, start)
+        return cur + poly_size(last + 1, deg)
+
+    rec(d - 1, degree, [0] * d, -1)
+    return terms
 
 
 def _expand_sparse(idx, vals, last, last_feature, degree, mult, out_i, out_v, cur):
@@ -284,6 +336,27 @@ class VectorPolynomialExpandMapper(SISOMapper):
         _expand_dense(x, len(x) - 1, degree, 1.0, out, -1)
         return DenseVector(out)
 
+    def _map_columns(self, mt):
+        """Dense tensor columns at once: each output position's monomial multiplied up in the row path's order
+        (last feature first, one factor at a time from 1.0), a product that reached zero on the way kept at
+        +0.0 as the recursion stops there -- the row path's values bit for bit."""
+        X = _dense_col(mt, self.col_idx)
+        degree = int(self.params.get("degree")) if self.params.contains("degree") else 2
+        if X is None or poly_size(X.shape[1], degree) > 1 << 16:
+            return super()._map_columns(mt)
+        X = X.to(torch.float64)
+        n, d = X.shape
+        out = torch.zeros((n, poly_size(d, degree) - 1), dtype=torch.float64, device=X.device)
+        for pos, exps in _poly_terms(d, degree):
+            acc = torch.ones(n, dtype=torch.float64, device=X.device)
+            dead = torch.zeros(n, dtype=torch.bool, device=X.device)
+            for k in range(d - 1, -1, -1):
+                for _ in range(exps[k]):
+                    acc = acc * X[:, k]
+                    dead |= acc == 0
+            out[:, pos] = torch.where(dead, torch.zeros_like(acc), acc)
+        return [Column(out)]
+
 
 class VectorSizeHintMapper(SISOMapper):
     def outputType(self):
@@ -303,6 +376,12 @@ class VectorSizeHintMapper(SISOMapper):
                 raise ValueError(f"VectorSizeHint: expect size {size}, got {vec.size()}")
             return None
         return vec
+
+    def _map_columns(self, mt):
+        X = _dense_col(mt, self.col_idx)
+        if X is None or X.shape[1] != self.params.get("size"):
+            return super()._map_columns(mt)
+        return [Column(X)]                   # every row already has the hinted size: passed through
 
 
 class VectorSerializeMapper(Mapper):

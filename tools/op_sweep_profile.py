@@ -26,7 +26,8 @@ def main():
     ap.add_argument("--top", type=int, default=8)
     ap.add_argument("--set", type=int, default=1,
                     help="1: model ops; 2: data processing / SQL / scalers; 3: evaluation / NLP / trees / formats; "
-                         "4: IO, more model predicts; 5: SQL joins / sets / order, PCA, normalize, correlation, JSON")
+                         "4: IO, more model predicts; 5: SQL joins / sets / order, PCA, normalize, correlation, JSON; "
+                         "6: vector mappers, more scalers")
     a = ap.parse_args()
     import alink_amd as A
     from alink_amd.common.table import Column, MTable
@@ -236,6 +237,31 @@ def main():
             "correlation": lambda: A.CorrelationBatchOp().setSelectedCols(names).linkFrom(src).collect(),
             "json_value": lambda: A.JsonValueBatchOp().setSelectedCol("j").setJsonPath(["$.x0", "$.x1"])
             .setOutputCols(["a", "b"]).linkFrom(jsrc).getOutputTable(),
+        }
+    if a.set == 6:
+        vsrc = TableSourceBatchOp(vec)
+        src = TableSourceBatchOp(dense)
+        two = MTable(TableSchema(["v1", "v2"], [Types.DENSE_VECTOR, Types.DENSE_VECTOR]),
+                     [Column(vec.col("vec").values[:, :8].double()), Column(vec.col("vec").values[:, 8:12].double())])
+        mas = A.MaxAbsScalerTrainBatchOp().setSelectedCols(names).linkFrom(src)
+        vss = A.VectorStandardScalerTrainBatchOp().setSelectedCol("vec").linkFrom(vsrc)
+        jobs = {
+            "vector_slice": lambda: A.VectorSliceBatchOp().setSelectedCol("vec").setOutputCol("s")
+            .setIndices([0, 3, 5]).setReservedCols([]).linkFrom(vsrc).getOutputTable().col("s").values,
+            "vector_elementwise_product": lambda: A.VectorElementwiseProductBatchOp().setSelectedCol("vec")
+            .setOutputCol("e").setScalingVector(" ".join(["2.0"] * 128)).setReservedCols([]).linkFrom(vsrc)
+            .getOutputTable().col("e").values,
+            "vector_interaction": lambda: A.VectorInteractionBatchOp().setSelectedCols(["v1", "v2"])
+            .setOutputCol("i").setReservedCols([]).linkFrom(TableSourceBatchOp(two)).getOutputTable()
+            .col("i").values,
+            "vector_polynomial_expand": lambda: A.VectorPolynomialExpandBatchOp().setSelectedCol("v2")
+            .setOutputCol("p").setDegree(2).setReservedCols([]).linkFrom(TableSourceBatchOp(two))
+            .getOutputTable().col("p").values,
+            "vector_size_hint": lambda: A.VectorSizeHintBatchOp().setSelectedCol("vec").setSize(128)
+            .linkFrom(vsrc).getOutputTable(),
+            "maxabs_scaler_predict": lambda: A.MaxAbsScalerPredictBatchOp().linkFrom(mas, src).getOutputTable(),
+            "vector_standard_scaler_predict": lambda: A.VectorStandardScalerPredictBatchOp().linkFrom(vss, vsrc)
+            .getOutputTable().col("vec").values,
         }
     only = [s for s in a.only.split(",") if s]
     for name, fn in jobs.items():
