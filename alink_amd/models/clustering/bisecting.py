@@ -214,6 +214,29 @@ class BisectingKMeansModelMapper(RichModelMapper):
             c = 2 * c if left else 2 * c + 1
         return c
 
+    def _leaves_of(self, X: np.ndarray) -> np.ndarray:
+        """``_leaf_of`` for every row at once: rows descend level by level, each internal node's rows split by
+        one matrix-vector product (the row path's per-row dot to rounding)."""
+        c = np.ones(X.shape[0], dtype=np.int64)
+        while True:
+            moved = False
+            for node in np.unique(c).tolist():
+                if not (2 * node in self.centers and 2 * node + 1 in self.centers):
+                    continue
+                rows = np.flatnonzero(c == node)
+                x = X[rows]
+                l, r = self.centers[2 * node], self.centers[2 * node + 1]
+                if self.cosine:
+                    xn = x / np.sqrt(np.einsum("ij,ij->i", x, x))[:, None]
+                    left = (1 - xn @ (l / np.sqrt(l @ l))) < (1 - xn @ (r / np.sqrt(r @ r)))
+                else:
+                    v, m = r - l, 0.5 * (r + l)
+                    left = x @ v < m @ v
+                c[rows] = np.where(left, 2 * node, 2 * node + 1)
+                moved = True
+            if not moved:
+                return c
+
     def _map_row_values(self, row):
         mt = MTable.from_rows([tuple(row)], self.dataSchema)
         return [c.to_list()[0] for c in self._map_columns(mt)]
@@ -228,6 +251,11 @@ class BisectingKMeansModelMapper(RichModelMapper):
         X = fm.to_dense().double().numpy()
         if X.shape[1] != self.d:
             raise RuntimeError(f"Dim of predict data not equal to vectorSize of training data: {self.d}")
+        if not self.detail_col:
+            leaves = self._leaves_of(X)
+            ids = np.unique(leaves)
+            idx = np.array([self.leaf_index[int(i)] for i in ids], dtype=np.int64)
+            return [Column(torch.from_numpy(idx[np.searchsorted(ids, leaves)]))]
         preds, details = [], []
         nl = len(self.leaf_ids)
         for x in X:

@@ -784,12 +784,25 @@ class KMeansModelMapper(ModelMapper):
             full = np.zeros_like(probs)
             full[:, self.model.ids] = probs          # cluster-id order, as the per-row DenseVector was
             from ... import _native
-            det = _native.java_double_rows(full, " ")
-            if det is None:
+            r = _native.java_double_rows_packed(full, " ") if len(full) else None
+            if r is not None:
+                # left packed as a StringBlock; null rows emptied
+                from ...common.strings import StringBlock
+                b, o = np.asarray(r[0], dtype=np.uint8), r[1]
+                nm = None
+                if nulls is not None and any(nulls):
+                    nm = np.asarray(nulls, dtype=bool)
+                    lens = o[1:] - o[:-1]
+                    b = b[np.repeat(~nm, lens)]
+                    o = np.zeros_like(o)
+                    np.cumsum(np.where(nm, 0, lens), out=o[1:])
+                    nm = torch.from_numpy(nm)
+                outs.append(Column(StringBlock(torch.from_numpy(np.ascontiguousarray(b)), torch.from_numpy(o), nm)))
+            else:
                 det = [VectorUtil.toString(DenseVector(r)) for r in full]
-            if nulls is not None and any(nulls):
-                det = [None if nl else s_ for s_, nl in zip(det, nulls)]
-            outs.append(Column(det))
+                if nulls is not None and any(nulls):
+                    det = [None if nl else s_ for s_, nl in zip(det, nulls)]
+                outs.append(Column(det))
         if self.dist_col:
             bd = best.to(torch.float64).cpu()
             if nulls is not None and any(nulls):

@@ -296,6 +296,44 @@ class MultiStringIndexerModelMapper(ModelMapper):
                 raise RuntimeError(f"Unseen token: {key}")
         return out
 
+    def _index_one(self, m, v):
+        key = None if v is None else java_str(v)
+        if key in m:
+            return m[key]
+        if self.invalid == "KEEP":
+            return len(m)
+        if self.invalid == "SKIP":
+            return None
+        raise RuntimeError(f"Unseen token: {key}")
+
+    def _map_columns(self, mt):
+        """Packed string columns through their device dictionary encodings: each DISTINCT token (and NULL, when
+        present) looked up once with the row path's rules, the rows gather their id's index."""
+        encs = [_block_codes(mt.col(c)) for c in self.cols]
+        if any(e is None for e in encs):
+            return super()._map_columns(mt)
+        out = []
+        for m, (ids, words, nm, cnt) in zip(self.maps, encs):
+            u = len(words)
+            lut = np.zeros(u + 1, dtype=np.int64)
+            lut_null = np.zeros(u + 1, dtype=bool)
+            has_null = nm is not None and bool(nm.any())
+            for i, w in enumerate(words + [None]):
+                if (i < u and cnt[i] == 0) or (i == u and not has_null):
+                    continue
+                r = self._index_one(m, w)
+                if r is None:
+                    lut_null[i] = True
+                else:
+                    lut[i] = r
+            if has_null:
+                ids = torch.where(nm, torch.full_like(ids, u), ids)
+            dev = ids.device
+            o = torch.from_numpy(lut).to(dev)[ids]
+            null = torch.from_numpy(lut_null).to(dev)[ids]
+            out.append(Column(o.cpu(), null.cpu() if bool(null.any()) else None))
+        return out
+
 
 # ---------------------------------------------------------------------------------------------------
 # discretizer output encoding (QuantileDiscretizerModelMapper.setResultRow)

@@ -158,7 +158,23 @@ class IsotonicRegressionModelMapper(ModelMapper):
 
     def _map_columns(self, mt: MTable):
         col = self.vector_col or self.feature_col
-        vals = mt.col(col).to_list()
+        c = mt.col(col)
+        if not self.vector_col and isinstance(c.values, torch.Tensor) and c.values.dim() == 1 and len(self.b):
+            # the whole column through searchsorted (bisect_left's index; NaN goes left as bisect sends it)
+            x = c.values.detach().to("cpu", torch.float64).numpy()
+            b, v = self.b, self.v
+            i = np.searchsorted(b, x, side="left")
+            i[np.isnan(x)] = 0
+            ic = np.minimum(i, len(b) - 1)
+            lo = np.maximum(i - 1, 0)
+            with np.errstate(all="ignore"):
+                mid = (x - b[lo]) / (b[ic] - b[lo]) * (v[ic] - v[lo]) + v[lo]
+            out = np.where(i == 0, v[0], np.where(i == len(b), v[-1], mid))
+            out = np.where((i < len(b)) & (b[ic] == x), v[ic], out)
+            if c.nulls is not None:
+                out[c.nulls.cpu().numpy()] = 0.0
+            return [Column(torch.from_numpy(out), c.nulls.cpu() if c.nulls is not None else None)]
+        vals = c.to_list()
         out = []
         for x in vals:
             if x is None:

@@ -351,3 +351,34 @@ def test_imputer_tensor_columns_equal_list_columns():
         model = op.linkFrom(TableSourceBatchOp(l_mt))
         outs = [A.ImputerPredictBatchOp().linkFrom(model, TableSourceBatchOp(m)).collect() for m in (t_mt, l_mt)]
         assert [tuple(r) for r in outs[0]] == [tuple(r) for r in outs[1]], strategy
+
+
+@pytest.mark.parametrize("invalid", ["KEEP", "SKIP", "ERROR"])
+def test_multi_string_indexer_columnar(invalid):
+    """MultiStringIndexer predict over packed string columns (device dictionary codes, one lookup per distinct
+    token) equals the row path: unseen tokens, nulls and the handleInvalid rules."""
+    from alink_amd import MultiStringIndexerPredictBatchOp, MultiStringIndexerTrainBatchOp
+    from alink_amd.common.strings import StringBlock
+    from alink_amd.common.table import Column, MTable
+    from alink_amd.common.types import TableSchema, Types
+    from alink_amd.models.feature.encoders import MultiStringIndexerModelMapper
+    from alink_amd.operator.batch.source import TableSourceBatchOp
+    schema = TableSchema(["c", "d"], [Types.STRING, Types.STRING])
+    train = MTable(schema, [Column(StringBlock.from_list(["a", "b", "a", "c"])),
+                            Column(StringBlock.from_list(["x", "y", "y", "z"]))])
+    model = MultiStringIndexerTrainBatchOp().setSelectedCols(["c", "d"]).linkFrom(TableSourceBatchOp(train))
+    cs = ["a", "b", "c", "a"] * 5 if invalid == "ERROR" else ["a", "q", None, "b", "", "c"] * 4
+    ds = ["y", "x", "z", "y"] * 5 if invalid == "ERROR" else ["z", None, "w", "x", "y", "y"] * 4
+    test = MTable(schema, [Column(StringBlock.from_list(cs)), Column(StringBlock.from_list(ds))])
+    op = MultiStringIndexerPredictBatchOp().setSelectedCols(["c", "d"]).setOutputCols(["ci", "di"]) \
+        .setHandleInvalid(invalid).setReservedCols([])
+    fast = op.linkFrom(model, TableSourceBatchOp(test)).collect()
+    mapper = MultiStringIndexerModelMapper(model.getOutputTable().schema, schema,
+                                           op.getParams().set("handleInvalid", invalid))
+    mapper.loadModel(model.getOutputTable().rows())
+    slow = [tuple(mapper._map_row_values(r)) for r in test.rows()]
+    assert [tuple(r) for r in fast] == slow
+    if invalid == "ERROR":
+        bad = MTable(schema, [Column(StringBlock.from_list(["a", "zz"])), Column(StringBlock.from_list(["x", "y"]))])
+        with pytest.raises(RuntimeError, match="Unseen token"):
+            op.linkFrom(model, TableSourceBatchOp(bad)).collect()

@@ -153,3 +153,20 @@ def test_gmm_predict_detail_packed():
         assert r[2] == VectorUtil.toString(DenseVector(np.array(probs)))
         assert abs(sum(probs) - 1) < 1e-12
     assert mt.col("p").values.dtype.is_floating_point is False
+
+
+@pytest.mark.parametrize("distance", ["EUCLIDEAN", "COSINE"])
+def test_bisecting_predict_columnar_matches_rows(distance):
+    """Level-by-level leaf descent over the whole matrix gives the per-row descent's clusters."""
+    import numpy as np
+    import pandas as pd
+    from alink_amd import BatchOperator, BisectingKMeansPredictBatchOp, BisectingKMeansTrainBatchOp
+    rng = np.random.default_rng(4)
+    X = np.concatenate([rng.standard_normal((60, 3)) + c for c in ([0, 0, 0], [6, 0, 0], [0, 6, 0], [0, 0, 6])])
+    df = pd.DataFrame({"v": [" ".join(map(str, r)) for r in X]})
+    b = BatchOperator.fromDataframe(df, schemaStr="v string")
+    m = BisectingKMeansTrainBatchOp().setVectorCol("v").setK(4).setDistanceType(distance).linkFrom(b)
+    fast = [r[-1] for r in BisectingKMeansPredictBatchOp().setPredictionCol("p").linkFrom(m, b).collect()]
+    slow = [r[-2] for r in BisectingKMeansPredictBatchOp().setPredictionCol("p").setPredictionDetailCol("d")
+            .linkFrom(m, b).collect()]
+    assert fast == slow and len(set(fast)) == 4

@@ -256,3 +256,22 @@ def test_local_kmeans_device_resident_equals_host_loop(n, k, dist, dup, monkeypa
     got = km._local_kmeans(X, w, k, dist, seed=3)
     ref = _host_loop_local_kmeans(X, w, k, dist, seed=3)
     assert torch.equal(got, ref)
+
+
+def test_kmeans_predict_detail_packed_with_nulls():
+    """Prediction detail strings come back packed (C++ Double.toString rows); a null vector row reads None."""
+    import numpy as np
+    import pandas as pd
+    from alink_amd import BatchOperator, KMeansPredictBatchOp, KMeansTrainBatchOp
+    from alink_amd.common.linalg import DenseVector, VectorUtil
+    rng = np.random.default_rng(1)
+    X = np.concatenate([rng.standard_normal((30, 2)), rng.standard_normal((30, 2)) + 8])
+    vs = [" ".join(map(str, r)) for r in X]
+    b = BatchOperator.fromDataframe(pd.DataFrame({"v": vs}), schemaStr="v string")
+    m = KMeansTrainBatchOp().setVectorCol("v").setK(2).linkFrom(b)
+    t = BatchOperator.fromDataframe(pd.DataFrame({"v": vs[:5] + [None]}), schemaStr="v string")
+    rows = KMeansPredictBatchOp().setPredictionCol("p").setPredictionDetailCol("d").linkFrom(m, t).collect()
+    assert rows[-1][1] is None and rows[-1][2] is None
+    for r in rows[:-1]:
+        p = np.array([float(x) for x in r[2].split(" ")])
+        assert r[2] == VectorUtil.toString(DenseVector(p)) and abs(p.sum() - 1) < 1e-12

@@ -27,7 +27,7 @@ def main():
     ap.add_argument("--set", type=int, default=1,
                     help="1: model ops; 2: data processing / SQL / scalers; 3: evaluation / NLP / trees / formats; "
                          "4: IO, more model predicts; 5: SQL joins / sets / order, PCA, normalize, correlation, JSON; "
-                         "6: vector mappers, more scalers")
+                         "6: vector mappers, more scalers; 7: more predicts, SQL expressions, regex tokenizer")
     a = ap.parse_args()
     import alink_amd as A
     from alink_amd.common.table import Column, MTable
@@ -262,6 +262,33 @@ def main():
             "maxabs_scaler_predict": lambda: A.MaxAbsScalerPredictBatchOp().linkFrom(mas, src).getOutputTable(),
             "vector_standard_scaler_predict": lambda: A.VectorStandardScalerPredictBatchOp().linkFrom(vss, vsrc)
             .getOutputTable().col("vec").values,
+        }
+    if a.set == 7:
+        src = TableSourceBatchOp(dense)
+        vsrc = TableSourceBatchOp(vec)
+        catsrc = TableSourceBatchOp(MTable(TableSchema(["c", "d"], [Types.STRING, Types.STRING]),
+                                           [Column(vocab.take(cats)), Column(vocab.take(cats.flip(0)))]))
+        iso = A.IsotonicRegTrainBatchOp().setFeatureCol("x0").setLabelCol("label").linkFrom(src)
+        msi = A.MultiStringIndexerTrainBatchOp().setSelectedCols(["c", "d"]).linkFrom(catsrc)
+        bkm = A.BisectingKMeansTrainBatchOp().setVectorCol("vec").setK(8).setMaxIter(3).linkFrom(
+            TableSourceBatchOp(MTable(vec.schema, [Column(vec.col("vec").values[:100000])])))
+        docs = TableSourceBatchOp(MTable(TableSchema(["doc"], [Types.STRING]), [Column(vocab.take(cats))]))
+        jobs = {
+            "isotonic_predict": lambda: A.IsotonicRegPredictBatchOp().setPredictionCol("p").linkFrom(iso, src)
+            .getOutputTable().col("p").values,
+            "multi_string_indexer_predict": lambda: A.MultiStringIndexerPredictBatchOp().setSelectedCols(["c", "d"])
+            .setOutputCols(["ci", "di"]).linkFrom(msi, catsrc).getOutputTable(),
+            "kmeans_predict_detail": lambda: A.KMeansPredictBatchOp().setPredictionCol("p")
+            .setPredictionDetailCol("d").setReservedCols([]).linkFrom(km_model, vsrc).getOutputTable()
+            .col("p").values,
+            "bisecting_kmeans_predict": lambda: A.BisectingKMeansPredictBatchOp().setPredictionCol("p")
+            .setReservedCols([]).linkFrom(bkm, vsrc).getOutputTable().col("p").values,
+            "select_expr": lambda: A.SelectBatchOp().setClause("x0 * 2 + x1 AS a, label").linkFrom(src)
+            .getOutputTable(),
+            "select_string_fn": lambda: A.SelectBatchOp().setClause("UPPER(c) AS u, CONCAT(c, '_', d) AS cd")
+            .linkFrom(catsrc).getOutputTable(),
+            "regex_tokenizer": lambda: A.RegexTokenizerBatchOp().setSelectedCol("doc").setPattern("_")
+            .linkFrom(docs).getOutputTable(),
         }
     only = [s for s in a.only.split(",") if s]
     for name, fn in jobs.items():
