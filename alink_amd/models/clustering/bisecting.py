@@ -237,6 +237,29 @@ class BisectingKMeansModelMapper(RichModelMapper):
             if not moved:
                 return c
 
+    def _leaves_of_device(self, X: torch.Tensor) -> torch.Tensor:
+        """``_leaves_of`` on the device (float64; the split products to rounding)."""
+        c = torch.ones(X.shape[0], dtype=torch.int64, device=X.device)
+        t = lambda a: torch.as_tensor(a, dtype=torch.float64, device=X.device)  # noqa: E731
+        while True:
+            moved = False
+            for node in torch.unique(c).tolist():
+                if not (2 * node in self.centers and 2 * node + 1 in self.centers):
+                    continue
+                rows = torch.nonzero(c == node).reshape(-1)
+                x = X[rows]
+                l, r = self.centers[2 * node], self.centers[2 * node + 1]
+                if self.cosine:
+                    xn = x / torch.sqrt((x * x).sum(1, keepdim=True))
+                    left = (1 - xn @ t(l / np.sqrt(l @ l))) < (1 - xn @ t(r / np.sqrt(r @ r)))
+                else:
+                    v, m = r - l, 0.5 * (r + l)
+                    left = x @ t(v) < float(m @ v)
+                c[rows] = torch.where(left, 2 * node, 2 * node + 1)
+                moved = True
+            if not moved:
+                return c
+
     def _map_row_values(self, row):
         mt = MTable.from_rows([tuple(row)], self.dataSchema)
         return [c.to_list()[0] for c in self._map_columns(mt)]
@@ -245,10 +268,20 @@ class BisectingKMeansModelMapper(RichModelMapper):
         from ...common.linalg import VectorUtil
         vcol = self.params.get("vectorCol") if self.params.contains("vectorCol") and \
             self.params.get("vectorCol") else self.vcol
-        fm = extract_features(mt, None, vcol, torch.device("cpu"))
+        from ..linear.model import _dev
+        dev = _dev(mt) if not self.detail_col else torch.device("cpu")
+        fm = extract_features(mt, None, vcol, dev)
         if fm.is_sparse:
             fm.set_ncols(self.d)
-        X = fm.to_dense().double().numpy()
+        X = fm.to_dense().double()
+        if dev.type == "cuda":
+            if X.shape[1] != self.d:
+                raise RuntimeError(f"Dim of predict data not equal to vectorSize of training data: {self.d}")
+            leaves = self._leaves_of_device(X)
+            ids = torch.unique(leaves)
+            idx = torch.tensor([self.leaf_index[int(i)] for i in ids.tolist()], dtype=torch.int64, device=dev)
+            return [Column(idx[torch.searchsorted(ids, leaves)].cpu())]
+        X = X.numpy()
         if X.shape[1] != self.d:
             raise RuntimeError(f"Dim of predict data not equal to vectorSize of training data: {self.d}")
         if not self.detail_col:

@@ -105,6 +105,34 @@ class RegexTokenizerMapper(SISOMapper):
         toks = java_split(s, self.pattern) if self.gaps else [m.group() for m in self._re.finditer(s)]
         return WORD_DELIMITER.join(t for t in toks if len(t) >= self.min_len)
 
+    def _literal_byte(self):
+        """The delimiter byte when ``pattern`` (gaps mode) matches exactly one fixed ASCII character."""
+        pat = self.pattern
+        if len(pat) == 2 and pat[0] == "\\" and not pat[1].isalnum() and pat[1].isascii():
+            pat = pat[1]
+        if len(pat) == 1 and pat.isascii() and pat not in ".^$*+?{}[]|()\\" and ord(pat) >= 0x20:
+            return ord(pat)
+        return None
+
+    def _map_columns(self, mt):
+        """A one-character delimiter over packed documents: lower-casing (ASCII bytes), Java split and the
+        minimum-length filter on the device, tokens joined back byte-parallel -- the row path's text."""
+        from ...common.strings import StringBlock
+        from ...ops.strings import join_tokens, split_tokens
+        col = mt.col(self.selected)
+        blk = col.values
+        d = self._literal_byte() if self.gaps else None
+        if d is None or not isinstance(blk, StringBlock) or col.nulls is not None or not len(blk) or \
+                (blk.data.numel() and bool((blk.data >= 0x80).any())):
+            return super()._map_columns(mt)
+        if self.lower:
+            up = (blk.data >= 0x41) & (blk.data <= 0x5A)
+            blk = StringBlock(torch.where(up, blk.data + 32, blk.data), blk.offsets, blk.nulls)
+        tok, doc = split_tokens(blk, d)
+        toff = tok.offsets.to(doc.device)
+        keep = (toff[1:] - toff[:-1]) >= self.min_len
+        return [Column(join_tokens(tok, doc, keep, len(blk), blk.nulls))]
+
 
 _STOP_CACHE: Optional[List[str]] = None
 

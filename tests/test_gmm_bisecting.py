@@ -170,3 +170,25 @@ def test_bisecting_predict_columnar_matches_rows(distance):
     slow = [r[-2] for r in BisectingKMeansPredictBatchOp().setPredictionCol("p").setPredictionDetailCol("d")
             .linkFrom(m, b).collect()]
     assert fast == slow and len(set(fast)) == 4
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("distance", ["EUCLIDEAN", "COSINE"])
+def test_bisecting_predict_device(distance):
+    """Bisecting k-means predict on a cuda vector column descends on the device to the host's clusters."""
+    import numpy as np
+    import torch
+    from alink_amd import BisectingKMeansPredictBatchOp, BisectingKMeansTrainBatchOp
+    from alink_amd.common.table import Column, MTable
+    from alink_amd.common.types import TableSchema, Types
+    from alink_amd.operator.batch.source import TableSourceBatchOp
+    rng = np.random.default_rng(4)
+    X = np.concatenate([rng.standard_normal((200, 3)) + c for c in ([0, 0, 0], [6, 0, 0], [0, 6, 0], [0, 0, 6])])
+    schema = TableSchema(["v"], [Types.DENSE_VECTOR])
+    host = TableSourceBatchOp(MTable(schema, [Column(torch.from_numpy(X))]))
+    dev = TableSourceBatchOp(MTable(schema, [Column(torch.from_numpy(X).cuda())]))
+    m = BisectingKMeansTrainBatchOp().setVectorCol("v").setK(4).setDistanceType(distance).linkFrom(host)
+    op = lambda: BisectingKMeansPredictBatchOp().setPredictionCol("p").setReservedCols([])  # noqa: E731
+    a = op().linkFrom(m, host).getOutputTable().col("p").values
+    b = op().linkFrom(m, dev).getOutputTable().col("p").values
+    assert torch.equal(a.cpu(), b.cpu())

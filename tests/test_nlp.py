@@ -409,3 +409,23 @@ def test_has_strip_space_matches_python_strip():
         assert has_strip_space(torch.frombuffer(bytearray(("a" + ch + "b").encode()), dtype=torch.uint8))
     for txt in ["plain text", "é à ü", "日本語", "\u200b zero width", "\u180e"]:
         assert has_strip_space(torch.frombuffer(bytearray(txt.encode()), dtype=torch.uint8)) is False
+
+
+@pytest.mark.parametrize("pattern,lower,min_len", [("_", True, 1), ("\\|", False, 2), (",", True, 0),
+                                                   ("\\s+", True, 1)])
+def test_regex_tokenizer_literal_delimiter_columnar(pattern, lower, min_len):
+    """RegexTokenizer on a one-character delimiter runs on packed bytes and equals the regex row path (leading
+    empties kept, trailing dropped, minimum length, ASCII lower-casing, nulls); other patterns use the row path."""
+    from alink_amd.common.params import Params
+    from alink_amd.common.strings import StringBlock
+    from alink_amd.common.table import Column, MTable
+    from alink_amd.common.types import TableSchema, Types
+    from alink_amd.models.nlp.text import RegexTokenizerMapper
+    docs = ["Ab_cD_e", "_x__Y_", "", None, "a|B||c|", "no delim", ",,a,b,,", "Q_r,s|T"]
+    schema = TableSchema(["s"], [Types.STRING])
+    mt = MTable(schema, [Column(StringBlock.from_list(docs))])
+    m = RegexTokenizerMapper(schema, Params().set("selectedCol", "s").set("pattern", pattern)
+                             .set("toLowerCase", lower).set("minTokenLength", min_len))
+    fast = m._map_columns(mt)[0].to_list()
+    slow = [m.mapColumn(d) for d in docs]
+    assert fast == slow
