@@ -128,6 +128,12 @@ def _select_columnar(mt: MTable, items, resolve=None) -> Optional[MTable]:
             cols.append(mt.cols[i])
             types.append(mt.schema.types[i])
             continue
+        if it.expr.kind == "fn" and it.expr.args[0] in _STRING_FNS:
+            sb = _string_columnar(it.expr, mt, resolve)
+            if sb is not None:
+                cols.append(Column(sb))
+                types.append(Types.STRING)
+                continue
         r = try_evaluate(it.expr, mt, resolve)
         if r is None:
             return None
@@ -139,6 +145,77 @@ def _select_columnar(mt: MTable, items, resolve=None) -> Optional[MTable]:
         cols.append(Column(vals, nulls if nulls is not None and bool(nulls.any()) else None))
         types.append(t)
     return MTable(TableSchema(_names_for(items), types), cols, mt.replicated)
+
+
+_STRING_FNS = ("UPPER", "LOWER", "CONCAT")
+
+
+def _string_columnar(e, mt: MTable, resolve):
+    """UPPER / LOWER / CONCAT over packed string columns and string literals as byte operations on the device
+    (``StringBlock`` in, ``StringBlock`` out, NULL in -> NULL out as the row functions); None -> the row path
+    (other argument kinds, or non-ASCII text under UPPER / LOWER, whose Unicode case rules the bytes lack)."""
+    import torch
+    from ....common.strings import StringBlock
+    n = mt.num_rows
+    if e.kind == "lit":
+        return e.args[0].encode("utf-8") if isinstance(e.args[0], str) else None
+    if e.kind == "col":
+        i = resolve(e.args[0])
+        v = mt.cols[i].values
+        if not isinstance(v, StringBlock) or mt.schema.types[i] != Types.STRING:
+            return None
+        return v
+    if e.kind != "fn" or e.args[0] not in _STRING_FNS:
+        return None
+    name, args = e.args[0], [_string_columnar(a, mt, resolve) for a in e.args[1]]
+    if any(a is None for a in args):
+        return None
+    if name in ("UPPER", "LOWER"):
+        if len(args) != 1 or not isinstance(args[0], StringBlock):
+            return None
+        b = args[0]
+        if b.data.numel() and bool((b.data >= 0x80).any()):
+            return None
+        lo, hi = (0x61, 0x7A) if name == "UPPER" else (0x41, 0x5A)
+        hit = (b.data >= lo) & (b.data <= hi)
+        return StringBlock(torch.where(hit, b.data - 32 if name == "UPPER" else b.data + 32, b.data), b.offsets,
+                           b.nulls)
+    blocks = [a for a in args if isinstance(a, StringBlock)]
+    if not blocks:
+        return None
+    dev = blocks[0].device
+    nulls = None
+    lens = []
+    for a in args:
+        if isinstance(a, StringBlock):
+            if a.nulls is not None:
+                nm = a.nulls.to(dev)
+                nulls = nm if nulls is None else (nulls | nm)
+            o = a.offsets.to(dev, torch.int64)
+            lens.append(o[1:] - o[:-1])
+        else:
+            lens.append(torch.full((n,), len(a), dtype=torch.int64, device=dev))
+    if nulls is not None:
+        lens = [torch.where(nulls, torch.zeros_like(L), L) for L in lens]
+    tot = torch.stack(lens).sum(0)
+    out_off = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(tot, 0, out=out_off[1:])
+    out = torch.empty(int(out_off[-1]), dtype=torch.uint8, device=dev)
+    start = out_off[:-1].clone()
+    rows = torch.arange(n, device=dev)
+    for a, L in zip(args, lens):
+        m = int(L.sum())
+        if m:
+            row = torch.repeat_interleave(rows, L)
+            first = torch.cumsum(L, 0) - L
+            k = torch.arange(m, device=dev) - first[row]
+            if isinstance(a, StringBlock):
+                src = a.data.to(dev)[a.offsets.to(dev, torch.int64)[:-1][row] + k]
+            else:
+                src = torch.tensor(list(a), dtype=torch.uint8, device=dev)[k]
+            out[start[row] + k] = src
+        start += L
+    return StringBlock(out, out_off, nulls if nulls is not None and bool(nulls.any()) else None)
 
 
 def sql_as(mt: MTable, clause: str) -> MTable:

@@ -161,3 +161,37 @@ def test_order_by_columnar_matches_row_path(monkeypatch, clause, order):
             m.setattr(E, "_order_columnar", lambda *x: None)
             slow = E.sql_order_by(mt, clause, order, limit=lim, offset=off)
         assert fast.col("i").values.tolist() == slow.col("i").values.tolist()
+
+
+@pytest.mark.parametrize("clause", ["UPPER(c) AS u, CONCAT(c, '_', d) AS cd", "LOWER(CONCAT(d, c)) AS x",
+                                    "CONCAT('[', UPPER(d), ']') AS b, c", "UPPER(c) AS u, LOWER(e) AS l"])
+def test_select_string_functions_columnar(monkeypatch, clause):
+    """UPPER / LOWER / CONCAT on packed strings (byte operations on the device) select the row path's values:
+    NULLs propagate, empty strings, literals; non-ASCII text goes back to the row path."""
+    from alink_amd.common.strings import StringBlock
+    cs = ["aB", None, "", "xyz", "Q r"] * 3
+    ds = ["d1", "E", None, "", "zz"] * 3
+    es = ["Ünï", "b", "c", None, "É"] * 3
+    schema = TableSchema(["c", "d", "e"], [Types.STRING] * 3)
+    mt = MTable(schema, [Column(StringBlock.from_list(cs)), Column(StringBlock.from_list(ds)),
+                         Column(StringBlock.from_list(es))])
+    fast = E.sql_select(mt, clause)
+    with monkeypatch.context() as m:
+        m.setattr(E, "_select_columnar", lambda *a, **k: None)
+        slow = E.sql_select(mt, clause)
+    assert fast.schema.names == slow.schema.names and fast.schema.types == slow.schema.types
+    assert [tuple(r) for r in fast.rows()] == [tuple(r) for r in slow.rows()]
+
+
+@pytest.mark.gpu
+def test_select_string_functions_device():
+    from alink_amd.common.strings import StringBlock
+    cs = ["aB", None, "", "xyz", "Q r"] * 50
+    ds = ["d1", "E", None, "", "zz"] * 50
+    schema = TableSchema(["c", "d"], [Types.STRING] * 2)
+    host = MTable(schema, [Column(StringBlock.from_list(cs)), Column(StringBlock.from_list(ds))])
+    dev = MTable(schema, [Column(StringBlock.from_list(cs).to("cuda")), Column(StringBlock.from_list(ds).to("cuda"))])
+    clause = "UPPER(c) AS u, CONCAT(c, '_', LOWER(d)) AS cd"
+    a, b = E.sql_select(host, clause), E.sql_select(dev, clause)
+    assert b.cols[0].values.device.type == "cuda"
+    assert [tuple(r) for r in a.rows()] == [tuple(r) for r in b.rows()]
