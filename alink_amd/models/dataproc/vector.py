@@ -398,6 +398,24 @@ class VectorSerializeMapper(Mapper):
         return [None if row[i] is None else (VectorUtil.toString(row[i]) if isinstance(row[i], Vector)
                                              else str(row[i])) for i in self.vidx]
 
+    def _map_columns(self, mt):
+        """Dense 2-D tensor vector columns formatted by the C++ Double.toString rows (packed); other vector
+        columns value by value."""
+        from ... import _native
+        from ...common.strings import StringBlock
+        out = []
+        for i in self.vidx:
+            X = _dense_col(mt, i)
+            r = _native.java_double_rows_packed(X.detach().to("cpu", torch.float64).numpy(), " ") \
+                if X is not None and mt.num_rows and X.shape[1] else None
+            if r is not None:
+                out.append(Column(StringBlock(torch.from_numpy(np.ascontiguousarray(r[0])), torch.from_numpy(r[1]))))
+                continue
+            vals = mt.cols[i].to_list()
+            out.append(Column([None if v is None else (VectorUtil.toString(v) if isinstance(v, Vector) else str(v))
+                               for v in vals]))
+        return out
+
 
 class VectorToColumnsMapper(Mapper):
     """``VectorToColumnsMapper`` (``outputCols``) or, when ``schemaStr`` is given instead, the format

@@ -241,6 +241,33 @@ class IndexToStringModelMapper(_SISOModelMapper):
     def mapColumn(self, v):
         return None if v is None else self.map_.get(int(v))
 
+    def _map_columns(self, mt):
+        """An integer tensor column: each DISTINCT index looked up once, the rows take their string from a
+        packed block of the results (unknown index -> NULL, as ``map_.get``)."""
+        from ...common.strings import StringBlock
+        col = mt.cols[self.col_idx]
+        v = col.values
+        if not (isinstance(v, torch.Tensor) and v.dim() == 1 and not v.is_floating_point() and v.dtype != torch.bool
+                and mt.num_rows):
+            return super()._map_columns(mt)
+        uniq, inv = torch.unique(v.cpu(), return_inverse=True)
+        words = [self.map_.get(int(u)) for u in uniq.tolist()]
+        if not all(w is None or isinstance(w, str) for w in words):
+            return super()._map_columns(mt)
+        blk = StringBlock.from_list(words).take(inv)
+        nm = blk.nulls
+        if col.nulls is not None:
+            cn = col.nulls.cpu()
+            nm = cn if nm is None else (nm.cpu() | cn)
+        if nm is not None and bool(nm.any()):
+            keep = ~nm
+            lens = (blk.offsets[1:] - blk.offsets[:-1]) * keep
+            data = blk.data[torch.repeat_interleave(keep, blk.offsets[1:] - blk.offsets[:-1])]
+            off = torch.zeros(len(lens) + 1, dtype=torch.int64)
+            torch.cumsum(lens, 0, out=off[1:])
+            blk = StringBlock(data, off, nm)
+        return [Column(blk)]
+
 
 def train_multi_string_indexer(mt: MTable, params: Params, meta_extra: Optional[Params] = None) -> MTable:
     cols = list(params.get("selectedCols"))

@@ -511,3 +511,27 @@ def test_vector_mappers_columnar_bitwise():
         _row_vs_columnar(V.VectorPolynomialExpandMapper(schema, P().set("degree", deg)), mt)
     m = V.VectorSizeHintMapper(schema, P().set("size", 4))
     assert m._map_columns(mt)[0].values is X
+
+
+def test_vector_serialize_and_index_to_string_columnar():
+    """VectorSerialize of a dense tensor column (C++ Double.toString rows) and IndexToString over an integer
+    tensor column (one lookup per distinct index) equal their row paths, NULLs and unknown indices included."""
+    import torch
+    from alink_amd.common.params import Params
+    from alink_amd.common.table import Column, MTable
+    from alink_amd.common.types import TableSchema, Types
+    from alink_amd.models.dataproc.vector import VectorSerializeMapper
+    from alink_amd.models.feature.encoders import IndexToStringModelMapper
+    X = torch.tensor([[1.0, -0.0, 1e-7], [float("nan"), 3.5, 1e21]], dtype=torch.float64)
+    schema = TableSchema(["v", "i"], [Types.DENSE_VECTOR, Types.LONG])
+    mt = MTable(schema, [Column(X), Column(torch.tensor([0, 5]))])
+    m = VectorSerializeMapper(schema, Params())
+    assert m._map_columns(mt)[0].to_list() == [m._map_row_values(r)[0] for r in mt.rows()]
+    ischema = TableSchema(["i"], [Types.LONG])
+    idx = torch.tensor([2, 0, 7, 2, 1, 0])
+    nm = torch.tensor([False, False, False, True, False, False])
+    imt = MTable(ischema, [Column(idx, nm)])
+    mm = IndexToStringModelMapper(TableSchema(["token", "token_index"], [Types.STRING, Types.LONG]), ischema,
+                                  Params().set("selectedCol", "i").set("outputCol", "s"))
+    mm.loadModel([("a", 0), ("bé", 1), ("c", 2)])
+    assert mm._map_columns(imt)[0].to_list() == [mm.mapColumn(v) for v in imt.col("i").to_list()]
