@@ -243,3 +243,72 @@ class Word2VecModelMapper(ModelMapper):
         if self.method == "AVG":
             d = d * (1.0 / len(vecs))
         return [VectorUtil.toString(DenseVector(d))]
+
+    def _map_columns(self, mt):
+        """Packed documents with a one-byte delimiter: split on the device, each DISTINCT token looked up once,
+        then the fold runs position by position over all documents at once (document d's k-th known word
+        joins its vector at step k), so every vector is combined in the row path's order; the results are
+        formatted by the C++ Double.toString rows."""
+        from ... import _native
+        from ...common.strings import StringBlock
+        from ...common.table import Column
+        from ...ops.strings import split_tokens, unique_ids
+        col = mt.cols[self.col_idx]
+        blk = col.values
+        db = self.delim.encode("utf-8")
+        if not (isinstance(blk, StringBlock) and col.nulls is None and len(blk) and len(db) == 1 and db[0] < 0x80
+                and self.embed and self.method in ("AVG", "SUM", "MIN", "MAX")):
+            return super()._map_columns(mt)
+        tok, doc = split_tokens(blk, db[0])
+        n = len(blk)
+        dev = doc.device
+        if len(tok):
+            enc = unique_ids(tok)
+            if enc is None:
+                return super()._map_columns(mt)
+            ids, rep = enc
+            words = tok.take(rep).to_list()
+            dim = len(next(iter(self.embed.values())))
+            rows = [self.embed.get(w) for w in words]
+            known_w = torch.tensor([r is not None for r in rows], dtype=torch.bool)
+            E = torch.as_tensor(np.stack([r if r is not None else np.zeros(dim) for r in rows]), dtype=torch.float64,
+                                device=dev)
+            keep = known_w.to(dev)[ids]
+            kid, kdoc = ids[keep], doc[keep]
+        else:
+            dim = len(next(iter(self.embed.values())))
+            E = torch.zeros((1, dim), dtype=torch.float64, device=dev)
+            kid = kdoc = torch.zeros(0, dtype=torch.int64, device=dev)
+        cnt = torch.bincount(kdoc, minlength=n)
+        first = torch.cumsum(cnt, 0) - cnt
+        pos = torch.arange(kid.numel(), device=dev) - first[kdoc]
+        D = torch.zeros((n, dim), dtype=torch.float64, device=dev)
+        kmax = int(cnt.max()) if n else 0
+        for k in range(kmax):
+            sel = pos == k
+            dk, vk = kdoc[sel], E[kid[sel]]
+            if k == 0:
+                D[dk] = vk
+            elif self.method == "MIN":
+                D[dk] = torch.minimum(D[dk], vk)
+            elif self.method == "MAX":
+                D[dk] = torch.maximum(D[dk], vk)
+            else:
+                D[dk] = D[dk] + vk
+        if self.method == "AVG":
+            D = D * (1.0 / cnt.clamp(min=1).to(torch.float64))[:, None]
+        nulls = (cnt == 0).cpu()
+        if blk.nulls is not None:
+            nulls |= blk.nulls.cpu()
+        r = _native.java_double_rows_packed(D.cpu().numpy(), " ")
+        if r is None:
+            return super()._map_columns(mt)
+        b, o = np.asarray(r[0], dtype=np.uint8), r[1]
+        nm = nulls.numpy()
+        if nm.any():
+            lens = o[1:] - o[:-1]
+            b = b[np.repeat(~nm, lens)]
+            o = np.zeros_like(o)
+            np.cumsum(np.where(nm, 0, lens), out=o[1:])
+        return [Column(StringBlock(torch.from_numpy(np.ascontiguousarray(b)), torch.from_numpy(o),
+                                   torch.from_numpy(nm) if nm.any() else None))]

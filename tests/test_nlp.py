@@ -429,3 +429,27 @@ def test_regex_tokenizer_literal_delimiter_columnar(pattern, lower, min_len):
     fast = m._map_columns(mt)[0].to_list()
     slow = [m.mapColumn(d) for d in docs]
     assert fast == slow
+
+
+@pytest.mark.parametrize("method", ["AVG", "SUM", "MIN", "MAX"])
+def test_word2vec_predict_columnar(method):
+    """Word2Vec document vectors over packed documents (position-by-position fold) equal the per-document row
+    path bit for bit: unknown words, repeats, empty and null documents, all-unknown documents."""
+    import numpy as np
+    from alink_amd.common.params import Params
+    from alink_amd.common.strings import StringBlock
+    from alink_amd.common.table import Column, MTable
+    from alink_amd.common.types import TableSchema, Types
+    from alink_amd.models.nlp.word2vec import Word2VecModelMapper
+    rng = np.random.default_rng(0)
+    vocab = ["a", "bb", "c", "dé"]
+    schema = TableSchema(["s"], [Types.STRING])
+    m = Word2VecModelMapper(TableSchema(["word", "vec"], [Types.STRING, Types.STRING]), schema,
+                            Params().set("selectedCol", "s").set("outputCol", "o").set("predMethod", method))
+    m.embed = {w: rng.standard_normal(5) for w in vocab}
+    docs = ["a bb c", "zz a a", "", None, "q r", "dé  c bb a bb", " a", "c"] * 3
+    mt = MTable(schema, [Column(StringBlock.from_list(docs))])
+    fast = m._map_columns(mt)[0]
+    assert isinstance(fast.values, StringBlock)
+    slow = [m._map_row_values((d,))[0] for d in docs]
+    assert fast.to_list() == slow
