@@ -273,6 +273,10 @@ def main():
         bkm = A.BisectingKMeansTrainBatchOp().setVectorCol("vec").setK(8).setMaxIter(3).linkFrom(
             TableSourceBatchOp(MTable(vec.schema, [Column(vec.col("vec").values[:100000])])))
         docs = TableSourceBatchOp(MTable(TableSchema(["doc"], [Types.STRING]), [Column(vocab.take(cats))]))
+        svocab = StringBlock.from_list([f"w{i % 97} w{i % 89} w{i % 83} w{i % 79} w{i % 7}" for i in range(1000)])
+        sents = TableSourceBatchOp(MTable(TableSchema(["doc"], [Types.STRING]), [Column(svocab.to(dev).take(cats))]))
+        w2v = A.Word2VecTrainBatchOp().setSelectedCol("doc").setVectorSize(64).setMinCount(1).setNumIter(1) \
+            .linkFrom(TableSourceBatchOp(MTable(TableSchema(["doc"], [Types.STRING]), [Column(svocab)])))
         jobs = {
             "isotonic_predict": lambda: A.IsotonicRegPredictBatchOp().setPredictionCol("p").linkFrom(iso, src)
             .getOutputTable().col("p").values,
@@ -289,6 +293,8 @@ def main():
             .linkFrom(catsrc).getOutputTable(),
             "regex_tokenizer": lambda: A.RegexTokenizerBatchOp().setSelectedCol("doc").setPattern("_")
             .linkFrom(docs).getOutputTable(),
+            "word2vec_predict": lambda: A.Word2VecPredictBatchOp().setSelectedCol("doc").setOutputCol("v")
+            .linkFrom(w2v, sents).getOutputTable().col("v").values,
         }
     only = [s for s in a.only.split(",") if s]
     for name, fn in jobs.items():
