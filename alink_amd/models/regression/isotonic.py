@@ -161,19 +161,21 @@ class IsotonicRegressionModelMapper(ModelMapper):
         c = mt.col(col)
         if not self.vector_col and isinstance(c.values, torch.Tensor) and c.values.dim() == 1 and len(self.b):
             # the whole column through searchsorted (bisect_left's index; NaN goes left as bisect sends it)
-            x = c.values.detach().to("cpu", torch.float64).numpy()
-            b, v = self.b, self.v
-            i = np.searchsorted(b, x, side="left")
-            i[np.isnan(x)] = 0
-            ic = np.minimum(i, len(b) - 1)
-            lo = np.maximum(i - 1, 0)
-            with np.errstate(all="ignore"):
-                mid = (x - b[lo]) / (b[ic] - b[lo]) * (v[ic] - v[lo]) + v[lo]
-            out = np.where(i == 0, v[0], np.where(i == len(b), v[-1], mid))
-            out = np.where((i < len(b)) & (b[ic] == x), v[ic], out)
-            if c.nulls is not None:
-                out[c.nulls.cpu().numpy()] = 0.0
-            return [Column(torch.from_numpy(out), c.nulls.cpu() if c.nulls is not None else None)]
+            # separate elementwise tensor ops (no fused multiply-add): the scalar formula's rounding
+            x = c.values.detach().to(torch.float64)
+            b = torch.as_tensor(self.b, device=x.device)
+            v = torch.as_tensor(self.v, device=x.device)
+            i = torch.searchsorted(b, x, side="left")
+            i = torch.where(torch.isnan(x), torch.zeros_like(i), i)
+            ic = i.clamp(max=len(b) - 1)
+            lo = (i - 1).clamp(min=0)
+            mid = (x - b[lo]) / (b[ic] - b[lo]) * (v[ic] - v[lo]) + v[lo]
+            out = torch.where(i == 0, v[0], torch.where(i == len(b), v[-1], mid))
+            out = torch.where((i < len(b)) & (b[ic] == x), v[ic], out)
+            nm = c.nulls.to(x.device) if c.nulls is not None else None
+            if nm is not None:
+                out = torch.where(nm, torch.zeros_like(out), out)
+            return [Column(out, nm)]
         vals = c.to_list()
         out = []
         for x in vals:
