@@ -844,3 +844,16 @@ class DCTMapper(SISOMapper):
         x = x.toDenseVector().data if isinstance(x, SparseVector) else x.data
         inv = bool(_pget(self.params, "inverse", False))
         return DenseVector((idct if inv else dct)(x, type=2, norm="ortho"))
+
+    def _map_columns(self, mt):
+        """A dense 2-D tensor column transformed as one batch along its rows (the same scipy transform per
+        row); other columns vector by vector."""
+        v = mt.cols[self.col_idx].values
+        if not (isinstance(v, torch.Tensor) and v.dim() == 2 and v.is_floating_point() and v.shape[1]
+                and mt.num_rows):
+            return super()._map_columns(mt)
+        from scipy.fft import dct, idct
+        inv = bool(_pget(self.params, "inverse", False))
+        X = v.detach().to("cpu", torch.float64).numpy()
+        return [Column(torch.from_numpy(np.ascontiguousarray((idct if inv else dct)(X, type=2, norm="ortho",
+                                                                                   axis=1))))]

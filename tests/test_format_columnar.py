@@ -535,3 +535,21 @@ def test_vector_serialize_and_index_to_string_columnar():
                                   Params().set("selectedCol", "i").set("outputCol", "s"))
     mm.loadModel([("a", 0), ("bé", 1), ("c", 2)])
     assert mm._map_columns(imt)[0].to_list() == [mm.mapColumn(v) for v in imt.col("i").to_list()]
+
+
+@pytest.mark.parametrize("inverse", [False, True])
+def test_dct_columnar(inverse):
+    import numpy as np
+    import torch
+    from alink_amd.common.linalg import DenseVector
+    from alink_amd.common.params import Params
+    from alink_amd.common.table import Column, MTable
+    from alink_amd.common.types import TableSchema, Types
+    from alink_amd.models.feature.encoders import DCTMapper
+    X = torch.randn(64, 17, dtype=torch.float64)
+    schema = TableSchema(["v"], [Types.DENSE_VECTOR])
+    m = DCTMapper(schema, Params().set("selectedCol", "v").set("inverse", inverse))
+    out = m._map_columns(MTable(schema, [Column(X)]))[0].values.numpy()
+    for i in range(64):
+        ref = m.mapColumn(DenseVector(X[i].numpy().copy())).getData()
+        np.testing.assert_allclose(out[i], ref, rtol=1e-13, atol=1e-15)
